@@ -1,0 +1,35 @@
+# Top-level build.  Product: fabric_amd/libfgv.so (HIP for gfx950 + C++ host, C ABI in
+# include/fgv.h).  Test infrastructure: oracle/liboracle.so.  Workload generator:
+# fabric_amd/synth/libfgv_synth.so.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
+CSRC := fabric_amd/csrc
+OBJDIR := build
+KOBJS := $(OBJDIR)/sha256.o $(OBJDIR)/p256_kernels.o $(OBJDIR)/fgv_host.o
+HDRS := $(CSRC)/p256_field.h $(CSRC)/fgv_kernels.h $(CSRC)/fgv_der.h include/fgv.h
+
+all: fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so
+
+$(OBJDIR):
+	mkdir -p $(OBJDIR)
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/fgv_host.o: $(CSRC)/fgv_host.cpp $(HDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+fabric_amd/libfgv.so: $(KOBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(KOBJS)
+
+oracle/liboracle.so: oracle/fgv_oracle.c oracle/fgv_oracle.h
+	$(MAKE) -C oracle
+
+fabric_amd/synth/libfgv_synth.so: fabric_amd/synth/fgv_synth.c
+	gcc -O2 -fPIC -shared -Wall -o $@ $< -lcrypto -lpthread
+
+clean:
+	rm -rf $(OBJDIR) fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so
+
+.PHONY: all clean

@@ -1,0 +1,133 @@
+"""ctypes binding of libfgv.so (include/fgv.h).
+
+The product path: every call goes to the HIP engine.  There is no CPU fallback here --
+if the shared library or a GPU is missing, FgvError is raised (a Go shim would then use
+its own sw BCCSP, which is the reference's behaviour, not ours).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfgv.so")
+
+# status bytes (include/fgv.h)
+SIG_VALID, SIG_FALSE, SIG_DER, SIG_HIGH_S, SIG_RANGE, SIG_BADKEY, SIG_EMPTY = range(7)
+
+EXPORTED = [
+    "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_sha256_batch",
+    "fgv_p256_verify_batch", "fgv_p256_verify_msgs",
+]
+
+
+class FgvError(RuntimeError):
+    pass
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("key_slots", ctypes.c_uint32),
+                ("host_threads", ctypes.c_uint32)]
+
+
+_L = None
+
+
+def load():
+    """Load libfgv.so (no GPU needed just to load and resolve symbols)."""
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB_PATH):
+            raise FgvError(f"{LIB_PATH} not built -- run `make` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.fgv_init.argtypes = [ctypes.POINTER(_Config), ctypes.POINTER(vp)]
+        L.fgv_destroy.argtypes = [vp]
+        L.fgv_destroy.restype = None
+        L.fgv_strerror.argtypes = [ctypes.c_int]
+        L.fgv_strerror.restype = ctypes.c_char_p
+        L.fgv_last_timing.argtypes = [vp] + [ctypes.POINTER(ctypes.c_double)] * 4
+        L.fgv_sha256_batch.argtypes = [vp, vp, sz, vp, vp, sz, vp]
+        L.fgv_p256_verify_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp]
+        L.fgv_p256_verify_msgs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
+        _L = L
+    return _L
+
+
+def _check(rc):
+    if rc != 0:
+        raise FgvError(f"libfgv error {rc}: {load().fgv_strerror(rc).decode()}")
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None and a.size else None
+
+
+def pack(blobs):
+    """List of bytes -> (arena uint8, offsets uint64, lengths uint32)."""
+    lens = np.fromiter((len(b) for b in blobs), dtype=np.uint32, count=len(blobs))
+    offs = np.zeros(len(blobs), dtype=np.uint64)
+    if len(blobs) > 1:
+        np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
+    arena = np.frombuffer(b"".join(blobs), dtype=np.uint8) if blobs else np.zeros(0, np.uint8)
+    return np.ascontiguousarray(arena), offs, lens
+
+
+class Engine:
+    """One libfgv context = one GPU (one process per GPU)."""
+
+    def __init__(self, device: int = 0, key_slots: int = 4096):
+        self._L = load()
+        cfg = _Config(device, key_slots, 0)
+        h = ctypes.c_void_p()
+        _check(self._L.fgv_init(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.fgv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def timing(self):
+        v = [ctypes.c_double() for _ in range(4)]
+        _check(self._L.fgv_last_timing(self._h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("sha_ms", "prep_ms", "point_ms", "keytab_ms"), (x.value for x in v)))
+
+    # --- BCCSP Hash
+    def sha256_batch(self, msgs):
+        arena, offs, lens = pack(msgs) if isinstance(msgs, list) else msgs
+        n = len(offs)
+        out = np.zeros((n, 32), dtype=np.uint8)
+        _check(self._L.fgv_sha256_batch(self._h, _ptr(arena), arena.size, _ptr(offs), _ptr(lens), n,
+                                        _ptr(out)))
+        return out
+
+    # --- BCCSP Verify (digest given)
+    def verify_batch(self, keys, sigs, digests):
+        """keys: (n,64) uint8 X||Y; sigs: list of DER bytes or packed triple; digests (n,32)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        digests = np.ascontiguousarray(digests, dtype=np.uint8)
+        sarena, soffs, slens = pack(sigs) if isinstance(sigs, list) else sigs
+        n = len(soffs)
+        st = np.zeros(n, dtype=np.uint8)
+        _check(self._L.fgv_p256_verify_batch(self._h, _ptr(keys), _ptr(sarena), sarena.size, _ptr(soffs),
+                                             _ptr(slens), _ptr(digests), n, _ptr(st)))
+        return st
+
+    # --- identity.Verify(msg, sig), fused hash + verify
+    def verify_msgs(self, keys, msgs, sigs):
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        marena, moffs, mlens = pack(msgs) if isinstance(msgs, list) else msgs
+        sarena, soffs, slens = pack(sigs) if isinstance(sigs, list) else sigs
+        n = len(soffs)
+        st = np.zeros(n, dtype=np.uint8)
+        _check(self._L.fgv_p256_verify_msgs(self._h, _ptr(keys), _ptr(marena), marena.size, _ptr(moffs),
+                                            _ptr(mlens), _ptr(sarena), sarena.size, _ptr(soffs), _ptr(slens),
+                                            n, _ptr(st)))
+        return st

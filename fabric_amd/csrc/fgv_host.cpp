@@ -1,0 +1,428 @@
+// fgv_host.cpp -- host side of libfgv.so: context, device buffers, key-table cache and
+// the BCCSP-shaped batch entry points of include/fgv.h.
+//
+// Data flow for one verify batch (all device work on ctx->stream):
+//   host: Go-rule DER decode + low-S (fgv_der.h), key -> table slot (cache), SoA packing
+//   H2D:  status/slot (5 B/item), r,s limbs (64 B/item) [+ digests or message arena]
+//   dev:  [k_keytab for keys not yet cached] -> [k_sha256] -> k_prep -> k_point
+//   D2H:  status (1 B/item)
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/fgv.h"
+#include "fgv_der.h"
+#include "fgv_kernels.h"
+
+namespace {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    if (hipMalloc(&p, want) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct HostBuf {  // pinned staging
+  void *p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+  void release() {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct KeyHash {
+  size_t operator()(const std::array<uint8_t, 64> &k) const {
+    uint64_t h = 1469598103934665603ull;
+    for (int i = 0; i < 64; i += 8) {
+      uint64_t w;
+      memcpy(&w, k.data() + i, 8);
+      h = (h ^ w) * 1099511628211ull;
+    }
+    return (size_t)h;
+  }
+};
+
+// big-endian 32 bytes -> 8 little-endian limbs
+inline void be32_to_limbs(const uint8_t *b, uint32_t *l) {
+  for (int i = 0; i < 8; i++) {
+    const uint8_t *p = b + 4 * (7 - i);
+    l[i] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+  }
+}
+
+}  // namespace
+
+struct fgv_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8] = {};
+  std::mutex mu;
+  // generator table (88 KB) and the public-key table cache
+  DevBuf gtab, g_ok;
+  DevBuf ktab, key_ok;
+  uint32_t key_slots = 0;
+  std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_map;
+  // per-batch device buffers
+  DevBuf kt_q, kt_slot, kt_scratch;
+  DevBuf status, slot, r, s, dig, d1, d2, wscr, msg, moff, mlen;
+  // pinned staging
+  HostBuf h_status, h_slot, h_r, h_s, h_dig, h_kq, h_kslot, h_moff, h_mlen;
+  double t_sha = 0, t_prep = 0, t_point = 0, t_keytab = 0;
+};
+
+#define HIP_TRY(x)                                     \
+  do {                                                 \
+    if ((x) != hipSuccess) return FGV_EDEVICE;         \
+  } while (0)
+
+static const uint8_t GX[32] = {0x6b, 0x17, 0xd1, 0xf2, 0xe1, 0x2c, 0x42, 0x47, 0xf8, 0xbc, 0xe6,
+                               0xe5, 0x63, 0xa4, 0x40, 0xf2, 0x77, 0x03, 0x7d, 0x81, 0x2d, 0xeb,
+                               0x33, 0xa0, 0xf4, 0xa1, 0x39, 0x45, 0xd8, 0x98, 0xc2, 0x96};
+static const uint8_t GY[32] = {0x4f, 0xe3, 0x42, 0xe2, 0xfe, 0x1a, 0x7f, 0x9b, 0x8e, 0xe7, 0xeb,
+                               0x4a, 0x7c, 0x0f, 0x9e, 0x16, 0x2b, 0xce, 0x33, 0x57, 0x6b, 0x31,
+                               0x5e, 0xce, 0xcb, 0xb6, 0x40, 0x68, 0x37, 0xbf, 0x51, 0xf5};
+
+// Build tables for `nk` keys (qxy: nk*16 limbs) into `tables` at `slots`.
+static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slots, uint32_t nk,
+                        apoint_raw *tables, uint8_t *ok) {
+  if (!c->kt_q.ensure((size_t)nk * 64) || !c->kt_slot.ensure((size_t)nk * 4) ||
+      !c->kt_scratch.ensure((size_t)nk * KT_ENTRIES * sizeof(jpoint_raw)))
+    return FGV_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(c->kt_q.p, h_qxy, (size_t)nk * 64, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->kt_slot.p, h_slots, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[6], c->stream));
+  hipLaunchKernelGGL(k_keytab, dim3(nk), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
+                     c->kt_slot.as<uint32_t>(), tables, c->kt_scratch.as<jpoint_raw>(), ok, nk);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[7], c->stream));
+  return FGV_OK;
+}
+
+extern "C" {
+
+const char *fgv_strerror(int code) {
+  switch (code) {
+    case FGV_OK: return "ok";
+    case FGV_EINVAL: return "invalid argument";
+    case FGV_EDEVICE: return "HIP device error";
+    case FGV_ENOMEM: return "out of memory";
+    case FGV_ECOMM: return "communication error";
+    case FGV_ESTATE: return "invalid state";
+    default: return "unknown error";
+  }
+}
+
+int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
+  if (!out) return FGV_EINVAL;
+  *out = nullptr;
+  fgv_ctx *c = new (std::nothrow) fgv_ctx();
+  if (!c) return FGV_ENOMEM;
+  c->device = cfg ? cfg->device : 0;
+  c->key_slots = (cfg && cfg->key_slots) ? cfg->key_slots : 4096;
+  auto fail = [&](int e) {
+    fgv_destroy(c);
+    return e;
+  };
+  if (hipSetDevice(c->device) != hipSuccess) return fail(FGV_EDEVICE);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
+  for (auto &e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
+  if (hipFuncSetAttribute((const void *)k_point, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)KT_BYTES) != hipSuccess)
+    return fail(FGV_EDEVICE);
+  if (!c->gtab.ensure(KT_BYTES) || !c->g_ok.ensure(16) ||
+      !c->ktab.ensure((size_t)c->key_slots * KT_BYTES) || !c->key_ok.ensure(c->key_slots))
+    return fail(FGV_ENOMEM);
+  // generator table = key table of G (same kernel)
+  uint32_t q[16], slot0 = 0;
+  be32_to_limbs(GX, q);
+  be32_to_limbs(GY, q + 8);
+  int rc = build_tables(c, q, &slot0, 1, c->gtab.as<apoint_raw>(), c->g_ok.as<uint8_t>());
+  if (rc) return fail(rc);
+  uint8_t gok = 0;
+  if (hipMemcpyAsync(&gok, c->g_ok.p, 1, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess || gok != 1)
+    return fail(FGV_EDEVICE);
+  *out = c;
+  return FGV_OK;
+}
+
+void fgv_destroy(fgv_ctx *c) {
+  if (!c) return;
+  if (c->stream) hipStreamSynchronize(c->stream);
+  DevBuf *d[] = {&c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->kt_q, &c->kt_slot, &c->kt_scratch,
+                 &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->d2, &c->wscr, &c->msg,
+                 &c->moff, &c->mlen};
+  for (auto *b : d) b->release();
+  HostBuf *h[] = {&c->h_status, &c->h_slot, &c->h_r, &c->h_s, &c->h_dig, &c->h_kq, &c->h_kslot,
+                  &c->h_moff, &c->h_mlen};
+  for (auto *b : h) b->release();
+  for (auto &e : c->ev)
+    if (e) hipEventDestroy(e);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int fgv_last_timing(fgv_ctx *c, double *sha_ms, double *prep_ms, double *point_ms,
+                    double *keytab_ms) {
+  if (!c) return FGV_EINVAL;
+  if (sha_ms) *sha_ms = c->t_sha;
+  if (prep_ms) *prep_ms = c->t_prep;
+  if (point_ms) *point_ms = c->t_point;
+  if (keytab_ms) *keytab_ms = c->t_keytab;
+  return FGV_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ verify core
+// digests: host pointer (n*32) or nullptr when ctx->dig already holds device digests.
+static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, size_t sig_buf_len,
+                       const uint64_t *sig_off, const uint32_t *sig_len, const uint8_t *h_digests,
+                       size_t n, uint8_t *status_out, bool dev_digests) {
+  if (n == 0) return FGV_OK;
+  if (n > 0x7fffffffu) return FGV_EINVAL;
+  const uint32_t N = (uint32_t)n;
+  if (!c->h_status.ensure(n) || !c->h_slot.ensure(n * 4) || !c->h_r.ensure(n * 32) ||
+      !c->h_s.ensure(n * 32))
+    return FGV_ENOMEM;
+  uint8_t *st = c->h_status.as<uint8_t>();
+  uint32_t *slot = c->h_slot.as<uint32_t>(), *R = c->h_r.as<uint32_t>(), *S = c->h_s.as<uint32_t>();
+
+  // 1) host: Go-rule DER + low-S; key -> slot
+  std::vector<uint32_t> new_keys;  // item index of first occurrence
+  size_t pending = 0;
+  for (size_t i = 0; i < n; i++) {
+    uint32_t r[8], s[8];
+    uint8_t code = ST_PENDING;
+    const size_t so = sig_off[i], sl = sig_len[i];
+    if (sl == 0) {
+      code = FGV_SIG_EMPTY;
+    } else if (so > sig_buf_len || sl > sig_buf_len - so) {
+      return FGV_EINVAL;
+    } else {
+      bool rb, sb;
+      if (fgv::der_decode_sig(sig_buf + so, sl, r, s, rb, sb)) {
+        code = FGV_SIG_DER;
+      } else if (sb || !fgv::is_low_s(s)) {
+        code = FGV_SIG_HIGH_S;
+      } else if (rb) {
+        // r >= 2^256: force an out-of-range value (n) so the device reports RANGE after
+        // the key check, matching ecdsa.Verify's order
+        static const uint32_t NL[8] = {0xFC632551u, 0xF3B9CAC2u, 0xA7179E84u, 0xBCE6FAADu,
+                                       0xFFFFFFFFu, 0xFFFFFFFFu, 0x00000000u, 0xFFFFFFFFu};
+        memcpy(r, NL, 32);
+      }
+    }
+    st[i] = code;
+    if (code != ST_PENDING) {
+      memset(r, 0, 32);
+      memset(s, 0, 32);
+      slot[i] = 0;
+    } else {
+      pending++;
+      std::array<uint8_t, 64> k;
+      memcpy(k.data(), keys + 64 * i, 64);
+      auto it = c->key_map.find(k);
+      if (it == c->key_map.end()) {
+        slot[i] = 0xFFFFFFFFu;  // assigned below
+        new_keys.push_back((uint32_t)i);
+      } else {
+        slot[i] = it->second;
+      }
+    }
+    for (int k = 0; k < 8; k++) {
+      R[(size_t)k * n + i] = r[k];
+      S[(size_t)k * n + i] = s[k];
+    }
+  }
+  // 2) assign slots to new keys (dedup), evicting the whole cache if it would overflow
+  c->t_keytab = 0;
+  if (!new_keys.empty()) {
+    std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> fresh;
+    for (uint32_t i : new_keys) {
+      std::array<uint8_t, 64> k;
+      memcpy(k.data(), keys + 64 * (size_t)i, 64);
+      fresh.emplace(k, 0);
+    }
+    if (c->key_map.size() + fresh.size() > c->key_slots) {
+      // count distinct keys this batch needs; evict everything else
+      std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> needed;
+      for (size_t i = 0; i < n; i++)
+        if (st[i] == ST_PENDING) {
+          std::array<uint8_t, 64> k;
+          memcpy(k.data(), keys + 64 * i, 64);
+          needed.emplace(k, 0);
+        }
+      if (needed.size() > c->key_slots) return FGV_ENOMEM;
+      c->key_map.clear();
+      fresh = std::move(needed);
+    }
+    uint32_t nk = (uint32_t)fresh.size();
+    if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kslot.ensure((size_t)nk * 4)) return FGV_ENOMEM;
+    uint32_t *kq = c->h_kq.as<uint32_t>(), *ks = c->h_kslot.as<uint32_t>();
+    uint32_t j = 0, next = (uint32_t)c->key_map.size();
+    for (auto &kv : fresh) {
+      be32_to_limbs(kv.first.data(), kq + 16 * j);
+      be32_to_limbs(kv.first.data() + 32, kq + 16 * j + 8);
+      ks[j] = next;
+      c->key_map.emplace(kv.first, next);
+      next++;
+      j++;
+    }
+    int rc = build_tables(c, kq, ks, nk, c->ktab.as<apoint_raw>(), c->key_ok.as<uint8_t>());
+    if (rc) return rc;
+    // re-resolve every pending slot (the cache may have been flushed)
+    for (size_t i = 0; i < n; i++)
+      if (st[i] == ST_PENDING) {
+        std::array<uint8_t, 64> k;
+        memcpy(k.data(), keys + 64 * i, 64);
+        slot[i] = c->key_map[k];
+      }
+  }
+  // 3) upload + kernels
+  if (!c->status.ensure(n) || !c->slot.ensure(n * 4) || !c->r.ensure(n * 32) ||
+      !c->s.ensure(n * 32) || !c->dig.ensure(n * 32) || !c->d1.ensure((size_t)NWIN * n) ||
+      !c->d2.ensure((size_t)NWIN * n))
+    return FGV_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(c->status.p, st, n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->slot.p, slot, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->r.p, R, n * 32, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->s.p, S, n * 32, hipMemcpyHostToDevice, c->stream));
+  if (!dev_digests) {
+    if (!c->h_dig.ensure(n * 32)) return FGV_ENOMEM;
+    memcpy(c->h_dig.p, h_digests, n * 32);
+    HIP_TRY(hipMemcpyAsync(c->dig.p, c->h_dig.p, n * 32, hipMemcpyHostToDevice, c->stream));
+  }
+  if (pending) {
+    uint32_t nl = (N + PREP_B - 1) / PREP_B;
+    nl = (nl + 255) / 256 * 256;
+    if (!c->wscr.ensure((size_t)PREP_B * 8 * nl * 4)) return FGV_ENOMEM;
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    hipLaunchKernelGGL(k_prep, dim3(nl / 256), dim3(256), 0, c->stream, N, c->status.as<uint8_t>(),
+                       c->slot.as<uint32_t>(), c->key_ok.as<uint8_t>(), c->r.as<uint32_t>(),
+                       c->s.as<uint32_t>(), c->dig.as<uint8_t>(), c->d1.as<int8_t>(),
+                       c->d2.as<int8_t>(), c->wscr.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    uint32_t grid = (N + POINT_THREADS - 1) / POINT_THREADS;
+    if (grid > 1024) grid = 1024;
+    hipLaunchKernelGGL(k_point, dim3(grid), dim3(POINT_THREADS), KT_BYTES, c->stream, N,
+                       c->status.as<uint8_t>(), c->slot.as<uint32_t>(), c->gtab.as<apoint_raw>(),
+                       c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(), c->d2.as<int8_t>(),
+                       c->r.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+  }
+  HIP_TRY(hipMemcpyAsync(st, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  memcpy(status_out, st, n);
+  float ms = 0;
+  c->t_prep = c->t_point = 0;
+  if (pending) {
+    if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->t_prep = ms;
+    if (hipEventElapsedTime(&ms, c->ev[3], c->ev[4]) == hipSuccess) c->t_point = ms;
+  }
+  if (!new_keys.empty() && hipEventElapsedTime(&ms, c->ev[6], c->ev[7]) == hipSuccess)
+    c->t_keytab = ms;
+  return FGV_OK;
+}
+
+static int sha_core(fgv_ctx *c, const uint8_t *buf, size_t buf_len, const uint64_t *off,
+                    const uint32_t *len, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (off[i] > buf_len || len[i] > buf_len - off[i]) return FGV_EINVAL;
+  if (!c->msg.ensure(buf_len + 64) || !c->moff.ensure(n * 8) || !c->mlen.ensure(n * 4) ||
+      !c->dig.ensure(n * 32))
+    return FGV_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(c->msg.p, buf, buf_len, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemsetAsync(c->msg.as<uint8_t>() + buf_len, 0, 64, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->moff.p, off, n * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->mlen.p, len, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  hipLaunchKernelGGL(k_sha256, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, c->stream,
+                     c->msg.as<uint8_t>(), c->moff.as<uint64_t>(), c->mlen.as<uint32_t>(),
+                     (uint32_t)n, c->dig.as<uint8_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  return FGV_OK;
+}
+
+extern "C" {
+
+int fgv_sha256_batch(fgv_ctx *c, const uint8_t *buf, size_t buf_len, const uint64_t *off,
+                     const uint32_t *len, size_t n, uint8_t *out) {
+  if (!c || (n && (!off || !len || !out)) || (buf_len && !buf)) return FGV_EINVAL;
+  if (n == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  int rc = sha_core(c, buf, buf_len, off, len, n);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out, c->dig.p, n * 32, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->t_sha = ms;
+  return FGV_OK;
+}
+
+int fgv_p256_verify_batch(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf,
+                          size_t sig_buf_len, const uint64_t *sig_off, const uint32_t *sig_len,
+                          const uint8_t *digests, size_t n, uint8_t *status) {
+  if (!c || (n && (!keys || !sig_off || !sig_len || !digests || !status))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  c->t_sha = 0;
+  return verify_core(c, keys, sig_buf, sig_buf_len, sig_off, sig_len, digests, n, status, false);
+}
+
+int fgv_p256_verify_msgs(fgv_ctx *c, const uint8_t *keys, const uint8_t *msg_buf,
+                         size_t msg_buf_len, const uint64_t *msg_off, const uint32_t *msg_len,
+                         const uint8_t *sig_buf, size_t sig_buf_len, const uint64_t *sig_off,
+                         const uint32_t *sig_len, size_t n, uint8_t *status) {
+  if (!c || (n && (!keys || !msg_off || !msg_len || !sig_off || !sig_len || !status)))
+    return FGV_EINVAL;
+  if (n == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  int rc = sha_core(c, msg_buf, msg_buf_len, msg_off, msg_len, n);
+  if (rc) return rc;
+  rc = verify_core(c, keys, sig_buf, sig_buf_len, sig_off, sig_len, nullptr, n, status, true);
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->t_sha = ms;
+  return rc;
+}
+
+}  // extern "C"

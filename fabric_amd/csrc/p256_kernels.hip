@@ -1,0 +1,341 @@
+// p256_kernels.hip -- ECDSA-P256 batch verification for gfx950.
+//
+// Pipeline per batch (one HIP stream, three launches):
+//   k_keytab  (per NEW public key, cached across batches) -- fixed-base comb table
+//             T_Q[w][k-1] = k * 2^(6w) * Q, w < 43, k = 1..32, affine Montgomery (88 KB/key).
+//             The generator table T_G is the same kernel run once on G at init.
+//   k_prep    (per item, PREP_B items per lane) -- range checks, w = s^-1 mod n with a
+//             per-lane batched (Montgomery-trick) inversion, u1 = e*w, u2 = r*w,
+//             signed 6-bit recoding of u1/u2 into 43 digits each.
+//   k_point   (per item) -- R = sum_w T_G[w][d1_w] + T_Q[w][d2_w]: 86 complete mixed
+//             additions and NO doublings; T_G staged in LDS (88 KB), T_Q gathered from
+//             HBM/L2; then x_R mod n == r checked projectively (X == r*Z^2 or (r+n)*Z^2).
+//
+// Semantics restated: Go 1.21.9 crypto/ecdsa verifyNISTEC (SEC 1 v2 s4.1.4) behind
+// fabric-lib-go bccsp/sw/ecdsa.go:41-57.  Exceptional additions (P == Q, P == -Q, inf)
+// are handled exactly, so results are bit-exact for adversarial inputs as well.
+#include "p256_field.h"
+#include "fgv_kernels.h"
+
+// R^2 mod p (to Montgomery), little-endian limbs
+__constant__ static const uint32_t R2P[8] = {0x00000003u, 0x00000000u, 0xFFFFFFFFu, 0xFFFFFFFBu,
+                                              0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFDu, 0x00000004u};
+// R^2 mod n
+__constant__ static const uint32_t R2N[8] = {0xBE79EEA2u, 0x83244C95u, 0x49BD6FA6u, 0x4699799Cu,
+                                              0x2B6BEC59u, 0x2845B239u, 0xF3D95620u, 0x66E12D94u};
+// R mod n = 2^256 - n
+__constant__ static const uint32_t ONEN[8] = {0x039CDAAFu, 0x0C46353Du, 0x58E8617Bu, 0x43190552u,
+                                              0x00000000u, 0x00000000u, 0xFFFFFFFFu, 0x00000000u};
+// b (curve coefficient), plain little-endian
+__constant__ static const uint32_t B_PLAIN[8] = {0x27D2604Bu, 0x3BCE3C3Eu, 0xCC53B0F6u, 0x651D06B0u,
+                                                 0x769886BCu, 0xB3EBBD55u, 0xAA3A93E7u, 0x5AC635D8u};
+
+FGV_DEV void fe_load_c(fe &r, const uint32_t *c) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = c[i];
+}
+FGV_DEV void fe_to_mont(fe &r, const fe &a) {
+  fe r2;
+  fe_load_c(r2, R2P);
+  fe_mul(r, a, r2);
+}
+FGV_DEV bool lt_p(const uint32_t a[8]) {
+  const uint32_t p[8] = {P_0, P_1, P_2, P_3, P_4, P_5, P_6, P_7};
+  return lt_256(a, p);
+}
+FGV_DEV bool lt_n(const uint32_t a[8]) {
+  uint32_t n[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) n[i] = N_LIMBS[i];
+  return lt_256(a, n);
+}
+FGV_DEV bool is_zero8(const uint32_t a[8]) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x |= a[i];
+  return x == 0u;
+}
+
+// y^2 == x^3 - 3x + b, coordinates < p (Go nistec pointFromAffine)
+FGV_DEV bool on_curve(const fe &x, const fe &y, fe &xm, fe &ym) {
+  if (!lt_p(x.v) || !lt_p(y.v)) return false;
+  fe_to_mont(xm, x);
+  fe_to_mont(ym, y);
+  fe lhs, rhs, t, b;
+  fe_sqr(lhs, ym);
+  fe_sqr(rhs, xm);
+  fe_mul(rhs, rhs, xm);
+  fe_add(t, xm, xm);
+  fe_add(t, t, xm);
+  fe_sub(rhs, rhs, t);
+  fe_load_c(t, B_PLAIN);
+  fe_to_mont(b, t);
+  fe_add(rhs, rhs, b);
+  return fe_eq(lhs, rhs);
+}
+
+FGV_DEV void store_fe(uint32_t *dst, const fe &a) {
+  uint4 *d = reinterpret_cast<uint4 *>(dst);
+  d[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  d[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+FGV_DEV void load_fe(fe &a, const uint32_t *src) {
+  const uint4 *s = reinterpret_cast<const uint4 *>(src);
+  uint4 p = s[0], q = s[1];
+  a.v[0] = p.x; a.v[1] = p.y; a.v[2] = p.z; a.v[3] = p.w;
+  a.v[4] = q.x; a.v[5] = q.y; a.v[6] = q.z; a.v[7] = q.w;
+}
+
+// ---------------------------------------------------------------- k_keytab
+// grid.x = number of keys, block = 64 (one wave per key, lane w < NWIN owns window w).
+// qxy: [nkeys][16] plain little-endian limbs (x then y).
+// scratch: [nkeys][KT_ENTRIES] Jacobian points + prefix products (jpoint_raw = X,Y,Z,pref).
+__global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
+                                               const uint32_t *__restrict__ slots,
+                                               apoint_raw *__restrict__ tables,
+                                               jpoint_raw *__restrict__ scratch,
+                                               uint8_t *__restrict__ key_ok, uint32_t nkeys) {
+  const uint32_t kid = blockIdx.x;
+  const int w = threadIdx.x;
+  if (kid >= nkeys) return;
+  fe x, y, xm, ym;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    x.v[i] = qxy[kid * 16 + i];
+    y.v[i] = qxy[kid * 16 + 8 + i];
+  }
+  const bool ok = on_curve(x, y, xm, ym);
+  const uint32_t slot = slots[kid];
+  if (w == 0) key_ok[slot] = ok ? 1 : 0;
+  if (!ok || w >= NWIN) return;
+
+  jpoint b;
+  b.x = xm;
+  b.y = ym;
+  fe_set_one(b.z);
+  for (int i = 0; i < WBITS * w; i++) pt_dbl(b, b);
+
+  jpoint_raw *scr = scratch + (size_t)kid * KT_ENTRIES + (size_t)w * TAB_K;
+  apoint_raw *tab = tables + (size_t)slot * KT_ENTRIES + (size_t)w * TAB_K;
+  // P_1 = B, P_2 = 2B, P_k = P_{k-1} + B  (k*B != +-B for 3 <= k <= 32 < n)
+  jpoint pk = b;
+  fe pref;
+  fe_set_one(pref);
+  for (int k = 1; k <= TAB_K; k++) {
+    if (k == 2) {
+      pt_dbl(pk, b);
+    } else if (k > 2) {
+      jpoint t = pk;
+      pt_add(pk, t, b);
+    }
+    fe_mul(pref, pref, pk.z);
+    jpoint_raw *e = scr + (k - 1);
+    store_fe(e->x, pk.x);
+    store_fe(e->y, pk.y);
+    store_fe(e->z, pk.z);
+    store_fe(e->pref, pref);
+  }
+  // Montgomery trick: one Fermat inversion for the 32 Z's of this window
+  fe inv;
+  fe_inv(inv, pref);
+  for (int k = TAB_K; k >= 1; k--) {
+    jpoint_raw *e = scr + (k - 1);
+    fe X, Y, Z, prev, zinv, z2, z3, ax, ay;
+    load_fe(X, e->x);
+    load_fe(Y, e->y);
+    load_fe(Z, e->z);
+    if (k > 1) load_fe(prev, (e - 1)->pref);
+    else fe_set_one(prev);
+    fe_mul(zinv, inv, prev);  // Z_k^-1 = (Z_1..Z_k)^-1 * (Z_1..Z_{k-1})
+    fe_mul(inv, inv, Z);      // (Z_1..Z_{k-1})^-1
+    fe_sqr(z2, zinv);
+    fe_mul(z3, z2, zinv);
+    fe_mul(ax, X, z2);
+    fe_mul(ay, Y, z3);
+    store_fe(tab[k - 1].x, ax);
+    store_fe(tab[k - 1].y, ay);
+  }
+}
+
+// ---------------------------------------------------------------- k_prep
+// Items are processed in PREP_B strided rounds per lane: item = lane + b * nlanes.
+// in:  status (0xFF = pending; host pre-decided otherwise), key slot, r/s as plain
+//      little-endian limbs [8][n] (limb-major), digests [n][32] big-endian bytes.
+// out: status (4/5 decided here), digits d1/d2 [NWIN][n] int8.
+__global__ __launch_bounds__(256) void k_prep(uint32_t n, uint8_t *__restrict__ status,
+                                              const uint32_t *__restrict__ key_slot,
+                                              const uint8_t *__restrict__ key_ok,
+                                              const uint32_t *__restrict__ r_limbs,
+                                              const uint32_t *__restrict__ s_limbs,
+                                              const uint8_t *__restrict__ digests,
+                                              int8_t *__restrict__ d1, int8_t *__restrict__ d2,
+                                              uint32_t *__restrict__ w_scratch) {
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nl = gridDim.x * blockDim.x;
+  uint32_t one[8], r2n[8], acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    one[i] = ONEN[i];
+    r2n[i] = R2N[i];
+    acc[i] = one[i];
+  }
+  // pass 1: validate, s -> Montgomery, prefix products (kept in w_scratch [b][8][nl])
+  uint32_t live = 0;
+#pragma unroll 1
+  for (int b = 0; b < PREP_B; b++) {
+    const uint32_t i = lane + (uint32_t)b * nl;
+    uint32_t sm[8];
+    bool use = false;
+    if (i < n && status[i] == ST_PENDING) {
+      uint32_t r[8], s[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        r[k] = r_limbs[(size_t)k * n + i];
+        s[k] = s_limbs[(size_t)k * n + i];
+      }
+      if (!key_ok[key_slot[i]]) {
+        status[i] = 5;
+      } else if (is_zero8(r) || is_zero8(s) || !lt_n(r) || !lt_n(s)) {
+        status[i] = 4;
+      } else {
+        sn_mul(sm, s, r2n);
+        use = true;
+      }
+    }
+    if (use) {
+      live |= 1u << b;
+      sn_mul(acc, acc, sm);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) w_scratch[((size_t)b * 8 + k) * nl + lane] = acc[k];
+  }
+  if (live == 0) return;
+  uint32_t inv[8];
+  sn_inv(inv, acc, one);  // (prod s_m)^-1 in Montgomery form
+  // pass 2: walk back, w_b = inv * prefix_{b-1}; inv *= s_m[b]
+#pragma unroll 1
+  for (int b = PREP_B - 1; b >= 0; b--) {
+    if (!((live >> b) & 1u)) continue;
+    const uint32_t i = lane + (uint32_t)b * nl;
+    uint32_t prev[8], w[8], r[8], s[8], sm[8], e[8], u1[8], u2[8];
+    // prefix_{b-1}: scan down to the previous slot (prefix unchanged over dead slots)
+    if (b > 0) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) prev[k] = w_scratch[((size_t)(b - 1) * 8 + k) * nl + lane];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) prev[k] = one[k];
+    }
+    sn_mul(w, inv, prev);  // s^-1 * R (Montgomery)
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      r[k] = r_limbs[(size_t)k * n + i];
+      s[k] = s_limbs[(size_t)k * n + i];
+    }
+    sn_mul(sm, s, r2n);
+    sn_mul(inv, inv, sm);
+    // e = leftmost 256 bits of the digest, mod n (digest is exactly 32 bytes)
+    const uint32_t *dg = reinterpret_cast<const uint32_t *>(digests + (size_t)i * 32);
+#pragma unroll
+    for (int k = 0; k < 8; k++) e[k] = __builtin_bswap32(dg[7 - k]);
+    if (!lt_n(e)) {
+      uint32_t bo = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) e[k] = subb(e[k], N_LIMBS[k], bo, &bo);
+    }
+    sn_mul(u1, e, w);  // e * s^-1 (plain)
+    sn_mul(u2, r, w);  // r * s^-1 (plain)
+    // signed base-64 recoding: digits in [-31, 32], 43 windows (top window <= 16)
+    int c1 = 0, c2 = 0;
+#pragma unroll
+    for (int win = 0; win < NWIN; win++) {
+      const int bit = WBITS * win, li = bit >> 5, sh = bit & 31;
+      uint32_t v1 = u1[li] >> sh, v2 = u2[li] >> sh;
+      if (sh > 32 - WBITS && li < 7) {
+        v1 |= u1[li + 1] << (32 - sh);
+        v2 |= u2[li + 1] << (32 - sh);
+      }
+      int a1 = (int)(v1 & 63u) + c1, a2 = (int)(v2 & 63u) + c2;
+      c1 = a1 > 32;
+      c2 = a2 > 32;
+      a1 -= c1 << 6;
+      a2 -= c2 << 6;
+      d1[(size_t)win * n + i] = (int8_t)a1;
+      d2[(size_t)win * n + i] = (int8_t)a2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- k_point
+// grid-stride over items; every workgroup stages T_G (KT_ENTRIES * 64 B = 88 KB) in LDS.
+FGV_DEV void lds_load_apoint(apoint &p, const uint4 *lds, uint32_t idx) {
+  uint4 a = lds[idx * 4 + 0], b = lds[idx * 4 + 1], c = lds[idx * 4 + 2], d = lds[idx * 4 + 3];
+  p.x.v[0] = a.x; p.x.v[1] = a.y; p.x.v[2] = a.z; p.x.v[3] = a.w;
+  p.x.v[4] = b.x; p.x.v[5] = b.y; p.x.v[6] = b.z; p.x.v[7] = b.w;
+  p.y.v[0] = c.x; p.y.v[1] = c.y; p.y.v[2] = c.z; p.y.v[3] = c.w;
+  p.y.v[4] = d.x; p.y.v[5] = d.y; p.y.v[6] = d.z; p.y.v[7] = d.w;
+}
+
+__global__ __launch_bounds__(POINT_THREADS) void k_point(
+    uint32_t n, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
+    const apoint_raw *__restrict__ gtab, const apoint_raw *__restrict__ ktab,
+    const int8_t *__restrict__ d1, const int8_t *__restrict__ d2,
+    const uint32_t *__restrict__ r_limbs) {
+  extern __shared__ uint4 lds_g[];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(gtab);
+    for (uint32_t j = threadIdx.x; j < KT_ENTRIES * 4; j += blockDim.x) lds_g[j] = src[j];
+  }
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (status[i] != ST_PENDING) continue;
+    const apoint_raw *qt = ktab + (size_t)key_slot[i] * KT_ENTRIES;
+    jpoint acc;
+    fe_set_zero(acc.x);
+    fe_set_zero(acc.y);
+    fe_set_zero(acc.z);
+#pragma unroll 1
+    for (int w = 0; w < NWIN; w++) {
+      const int a = d1[(size_t)w * n + i];
+      const int b = d2[(size_t)w * n + i];
+      if (a != 0) {
+        apoint p;
+        lds_load_apoint(p, lds_g, (uint32_t)(w * TAB_K + (a < 0 ? -a : a) - 1));
+        if (a < 0) fe_neg(p.y, p.y);
+        pt_madd(acc, acc, p);
+      }
+      if (b != 0) {
+        apoint p;
+        const apoint_raw *e = qt + w * TAB_K + (b < 0 ? -b : b) - 1;
+        load_fe(p.x, e->x);
+        load_fe(p.y, e->y);
+        if (b < 0) fe_neg(p.y, p.y);
+        pt_madd(acc, acc, p);
+      }
+    }
+    uint8_t st = 1;
+    if (!fe_is_zero(acc.z)) {
+      fe r, rm, z2, lhs;
+#pragma unroll
+      for (int k = 0; k < 8; k++) r.v[k] = r_limbs[(size_t)k * n + i];
+      fe_sqr(z2, acc.z);
+      fe_to_mont(rm, r);
+      fe_mul(lhs, rm, z2);
+      if (fe_eq(lhs, acc.x)) {
+        st = 0;
+      } else {
+        // x_R in [n, p): x_R mod n == r  <=>  x_R == r + n  (only if r + n < p)
+        uint32_t c = 0;
+        fe rn;
+#pragma unroll
+        for (int k = 0; k < 8; k++) rn.v[k] = addc(r.v[k], N_LIMBS[k], c, &c);
+        if (c == 0u && lt_p(rn.v)) {
+          fe_to_mont(rm, rn);
+          fe_mul(lhs, rm, z2);
+          if (fe_eq(lhs, acc.x)) st = 0;
+        }
+      }
+    }
+    status[i] = st;
+  }
+}

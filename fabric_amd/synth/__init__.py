@@ -1,0 +1,85 @@
+"""Synthetic Fabric workloads (keys, certificates, signed blocks) for tests and bench.
+
+Signing uses OpenSSL through fgv_synth.c -- an implementation independent of both the
+GPU engine and the oracle.  This package is input generation, not the product path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "libfgv_synth.so")
+        if not os.path.exists(path):
+            raise RuntimeError("fabric_amd/synth/libfgv_synth.so not built (run `make`)")
+        L = ctypes.CDLL(path)
+        L.synth_keygen.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p,
+                                   ctypes.c_char_p]
+        L.synth_sign_rs.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p,
+                                    ctypes.c_char_p]
+        L.synth_der_encode.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+        L.synth_der_encode.restype = ctypes.c_size_t
+        L.synth_sign_batch.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+        L.synth_make_cert.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                      ctypes.c_char_p, ctypes.c_int, ctypes.c_long, ctypes.c_char_p,
+                                      ctypes.c_size_t]
+        _LIB = L
+    return _LIB
+
+
+class Key:
+    """A P-256 key pair derived deterministically from (seed, idx)."""
+
+    def __init__(self, seed: int, idx: int):
+        priv = ctypes.create_string_buffer(32)
+        qx = ctypes.create_string_buffer(32)
+        qy = ctypes.create_string_buffer(32)
+        lib().synth_keygen(seed, idx, priv, qx, qy)
+        self.priv, self.qx, self.qy = priv.raw, qx.raw, qy.raw
+
+    @property
+    def pub(self) -> bytes:
+        return self.qx + self.qy
+
+
+def der_encode(r: int, s: int) -> bytes:
+    out = ctypes.create_string_buffer(80)
+    n = lib().synth_der_encode(r.to_bytes(32, "big"), s.to_bytes(32, "big"), out)
+    return out.raw[:n]
+
+
+def sign_rs(key: Key, digest: bytes, high_s: bool = False):
+    r = ctypes.create_string_buffer(32)
+    s = ctypes.create_string_buffer(32)
+    lib().synth_sign_rs(key.priv, digest, 1 if high_s else 0, r, s)
+    return int.from_bytes(r.raw, "big"), int.from_bytes(s.raw, "big")
+
+
+def sign(key: Key, digest: bytes, high_s: bool = False) -> bytes:
+    r, s = sign_rs(key, digest, high_s)
+    return der_encode(r, s)
+
+
+def sign_batch(privs: bytes, digests: bytes, n: int, threads: int = 8, high_s: bool = False):
+    """Sign n digests; privs/digests are n*32 concatenated bytes.  Returns list of DER sigs."""
+    stride = 80
+    buf = ctypes.create_string_buffer(stride * n)
+    lens = (ctypes.c_uint32 * n)()
+    lib().synth_sign_batch(privs, digests, n, buf, lens, stride, 1 if high_s else 0, threads)
+    raw = buf.raw
+    return [raw[stride * i: stride * i + lens[i]] for i in range(n)]
+
+
+def make_cert(subject: Key, issuer: Key, cn: str, org: str, issuer_cn: str, is_ca: bool,
+              serial: int) -> bytes:
+    out = ctypes.create_string_buffer(4096)
+    n = lib().synth_make_cert(subject.priv, issuer.priv, cn.encode(), org.encode(), issuer_cn.encode(),
+                              1 if is_ca else 0, serial, out, 4096)
+    if n < 0:
+        raise RuntimeError("certificate generation failed")
+    return out.raw[:n]

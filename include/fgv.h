@@ -1,0 +1,82 @@
+/*
+ * fgv.h -- C ABI of the MI355X block-validation engine for Hyperledger Fabric's
+ * committer hot path (libfgv.so).  Plain pointers and sizes only; no exceptions or
+ * aborts cross this boundary.  Every entry point returns 0 on success or a negative
+ * FGV_E* code; on a negative return the caller (the Go shim) falls back
+ * to its own CPU path for that batch -- it never halts the channel.
+ *
+ * Each entry point names the reference interface it replaces (paths under the
+ * PM-Master/fabric tree; fabric-lib-go is vendored at vendor/github.com/hyperledger/).
+ */
+#ifndef FGV_H
+#define FGV_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ errors */
+#define FGV_OK 0
+#define FGV_EINVAL (-1)   /* bad argument (null pointer, size overflow)        */
+#define FGV_EDEVICE (-2)  /* HIP runtime / kernel failure                      */
+#define FGV_ENOMEM (-3)   /* device or host allocation failed                  */
+#define FGV_ECOMM (-4)    /* RCCL / torch.distributed exchange failed          */
+#define FGV_ESTATE (-5)   /* call out of order (e.g. not initialised)         */
+
+/* ------------------------------------------------- per-signature status bytes
+ * Only FGV_SIG_VALID means "valid"; the reference maps every other outcome to an
+ * error (msp/identities.go:190-196), so the shim maps 0 -> (true,nil), else invalid. */
+#define FGV_SIG_VALID 0     /* ecdsa.Verify returned true                          */
+#define FGV_SIG_FALSE 1     /* equation false or R at infinity                     */
+#define FGV_SIG_DER 2       /* Go encoding/asn1 decode error, or r<=0 / s<=0       */
+#define FGV_SIG_HIGH_S 3    /* s > n>>1 (bccsp/utils/ecdsa.go:82-89)              */
+#define FGV_SIG_RANGE 4     /* r >= n or s >= n                                    */
+#define FGV_SIG_BADKEY 5    /* public key is not a P-256 point                     */
+#define FGV_SIG_EMPTY 6     /* empty signature or digest (bccsp/sw/impl.go:253-259) */
+
+typedef struct fgv_ctx fgv_ctx;
+
+typedef struct fgv_config {
+  int device;            /* HIP device ordinal (one process per GPU)                 */
+  uint32_t key_slots;    /* capacity of the device public-key table cache (0 = 4096) */
+  uint32_t host_threads; /* host worker threads for parsing / policy fold (0 = 16)    */
+} fgv_config;
+
+/* Replaces factory.GetDefault() / sw.NewDefaultSecurityLevel* for the verify + hash
+ * capabilities (fabric-lib-go bccsp/factory/factory.go:42, bccsp/sw/new.go:29-80).
+ * Builds the fixed-base generator table on the device. */
+int fgv_init(const fgv_config *cfg, fgv_ctx **out);
+void fgv_destroy(fgv_ctx *ctx);
+const char *fgv_strerror(int code);
+/* kernel-time accounting of the last call (ms, HIP events around each kernel) */
+int fgv_last_timing(fgv_ctx *ctx, double *sha_ms, double *prep_ms, double *point_ms,
+                    double *keytab_ms);
+
+/* ---------------------------------------------------------- BCCSP Hash / Verify */
+
+/* SHA-256 over n messages (msg i = buf[off[i] .. off[i]+len[i])), out = n*32 bytes.
+ * Replaces CSP.Hash(msg, &SHA256Opts{}) -- bccsp/sw/impl.go:177-194, sw/hash.go:29-33. */
+int fgv_sha256_batch(fgv_ctx *ctx, const uint8_t *buf, size_t buf_len, const uint64_t *off,
+                     const uint32_t *len, size_t n, uint8_t *out);
+
+/* ECDSA-P256 verify of n (key, DER signature, digest) triples; status = n bytes.
+ * keys: n*64 bytes (X||Y big-endian affine); digests: n*32 bytes.
+ * Replaces CSP.Verify(k, sig, digest, nil) for *ecdsaPublicKey keys:
+ * bccsp/sw/impl.go:247-270 -> sw/ecdsa.go:71-75 -> verifyECDSA sw/ecdsa.go:41-57
+ * (utils.UnmarshalECDSASignature utils/ecdsa.go:41-65, IsLowS :82-89, ecdsa.Verify). */
+int fgv_p256_verify_batch(fgv_ctx *ctx, const uint8_t *keys, const uint8_t *sig_buf,
+                          size_t sig_buf_len, const uint64_t *sig_off, const uint32_t *sig_len,
+                          const uint8_t *digests, size_t n, uint8_t *status);
+
+/* Fused identity.Verify(msg, sig): digest = SHA-256(msg) on the device, then verify.
+ * Replaces msp/identities.go:170-199 (getHashOpt SHA2 + bccsp.Hash + bccsp.Verify). */
+int fgv_p256_verify_msgs(fgv_ctx *ctx, const uint8_t *keys, const uint8_t *msg_buf,
+                         size_t msg_buf_len, const uint64_t *msg_off, const uint32_t *msg_len,
+                         const uint8_t *sig_buf, size_t sig_buf_len, const uint64_t *sig_off,
+                         const uint32_t *sig_len, size_t n, uint8_t *status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FGV_H */
