@@ -17,7 +17,8 @@ SIG_VALID, SIG_FALSE, SIG_DER, SIG_HIGH_S, SIG_RANGE, SIG_BADKEY, SIG_EMPTY = ra
 
 EXPORTED = [
     "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_sha256_batch",
-    "fgv_p256_verify_batch", "fgv_p256_verify_msgs",
+    "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset",
+    "fgv_p256_verify_msgs_dev",
 ]
 
 
@@ -50,6 +51,9 @@ def load():
         L.fgv_sha256_batch.argtypes = [vp, vp, sz, vp, vp, sz, vp]
         L.fgv_p256_verify_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp]
         L.fgv_p256_verify_msgs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
+        L.fgv_keys_register.argtypes = [vp, vp, sz, vp]
+        L.fgv_keys_reset.argtypes = [vp]
+        L.fgv_p256_verify_msgs_dev.argtypes = [vp] * 8 + [sz, vp]
         _L = L
     return _L
 
@@ -131,3 +135,18 @@ class Engine:
                                             _ptr(mlens), _ptr(sarena), sarena.size, _ptr(soffs), _ptr(slens),
                                             n, _ptr(st)))
         return st
+
+    # --- key registry (MSP identity cache analogue)
+    def keys_register(self, keys):
+        keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 64)
+        slots = np.zeros(len(keys), dtype=np.uint32)
+        _check(self._L.fgv_keys_register(self._h, _ptr(keys), len(keys), _ptr(slots)))
+        return slots
+
+    def keys_reset(self):
+        _check(self._L.fgv_keys_reset(self._h))
+
+    # --- HBM-resident batch: arguments are device pointers (ints), e.g. tensor.data_ptr()
+    def verify_msgs_dev(self, msg_buf, msg_off, msg_len, sig_buf, sig_off, sig_len, key_slot, n, status):
+        _check(self._L.fgv_p256_verify_msgs_dev(self._h, msg_buf, msg_off, msg_len, sig_buf, sig_off, sig_len,
+                                                key_slot, n, status))

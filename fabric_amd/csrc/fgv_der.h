@@ -7,8 +7,10 @@
 //     (Go's struct decoding tolerates trailing elements);
 //   * lengths definite and minimal; INTEGER contents non-empty and minimal;
 //   * R.Sign() != 1 or S.Sign() != 1 (zero or negative) is an error.
-// Host-side by design: the device only ever sees fixed-width (r, s).
+// Compiled for host (buffers handed over by the BCCSP-shaped calls) and for the device
+// (k_der, for batches already resident in HBM); one definition, so both agree.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
@@ -22,7 +24,7 @@ struct DerTL {
 };
 
 // parseTagAndLength; returns false on any error
-inline bool der_read_tl(const uint8_t *b, size_t n, size_t &o, DerTL &t) {
+__host__ __device__ inline bool der_read_tl(const uint8_t *b, size_t n, size_t &o, DerTL &t) {
   if (o >= n) return false;
   const uint8_t first = b[o++];
   t.cls = first >> 6;
@@ -61,7 +63,7 @@ inline bool der_read_tl(const uint8_t *b, size_t n, size_t &o, DerTL &t) {
 }
 
 // One INTEGER.  Writes the magnitude as 8 little-endian u32 limbs; big=true if >= 2^256.
-inline bool der_read_int(const uint8_t *b, size_t n, size_t &o, uint32_t limbs[8], bool &big,
+__host__ __device__ inline bool der_read_int(const uint8_t *b, size_t n, size_t &o, uint32_t limbs[8], bool &big,
                          bool &positive) {
   if (o == n) return false;  // "sequence truncated"
   DerTL t;
@@ -80,7 +82,7 @@ inline bool der_read_int(const uint8_t *b, size_t n, size_t &o, uint32_t limbs[8
   }
   positive = !neg && len > 0;
   big = len > 32;
-  memset(limbs, 0, 32);
+  for (int k = 0; k < 8; k++) limbs[k] = 0;
   if (!big) {
     for (size_t i = 0; i < len; i++) {
       const size_t bytepos = len - 1 - i;  // little-endian byte index
@@ -91,7 +93,7 @@ inline bool der_read_int(const uint8_t *b, size_t n, size_t &o, uint32_t limbs[8
 }
 
 // Returns 0 on success (r, s written), 2 (FGV_SIG_DER) on any error.
-inline int der_decode_sig(const uint8_t *sig, size_t n, uint32_t r[8], uint32_t s[8], bool &r_big,
+__host__ __device__ inline int der_decode_sig(const uint8_t *sig, size_t n, uint32_t r[8], uint32_t s[8], bool &r_big,
                           bool &s_big) {
   size_t o = 0;
   DerTL t;
@@ -109,8 +111,8 @@ inline int der_decode_sig(const uint8_t *sig, size_t n, uint32_t r[8], uint32_t 
 }
 
 // s <= n >> 1 (bccsp/utils/ecdsa.go:82-89); limbs little-endian
-inline bool is_low_s(const uint32_t s[8]) {
-  static const uint32_t HALF_N[8] = {0x7E3192A8u, 0x79DCE561u, 0xD38BCF42u, 0xDE737D56u,
+__host__ __device__ inline bool is_low_s(const uint32_t s[8]) {
+  const uint32_t HALF_N[8] = {0x7E3192A8u, 0x79DCE561u, 0xD38BCF42u, 0xDE737D56u,
                                      0xFFFFFFFFu, 0x7FFFFFFFu, 0x80000000u, 0x7FFFFFFFu};
   for (int i = 7; i >= 0; i--) {
     if (s[i] < HALF_N[i]) return true;

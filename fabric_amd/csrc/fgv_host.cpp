@@ -208,6 +208,37 @@ int fgv_last_timing(fgv_ctx *c, double *sha_ms, double *prep_ms, double *point_m
 
 }  // extern "C"
 
+// k_prep + k_point on device-resident SoA inputs (events ev[2..4] bracket them)
+static int launch_verify_stages(fgv_ctx *c, uint32_t N, uint8_t *d_status, const uint32_t *d_slot,
+                                const uint32_t *d_r, const uint32_t *d_s, const uint8_t *d_dig) {
+  if (!c->d1.ensure((size_t)NWIN * N) || !c->d2.ensure((size_t)NWIN * N)) return FGV_ENOMEM;
+  uint32_t nl = (N + PREP_B - 1) / PREP_B;
+  nl = (nl + 255) / 256 * 256;
+  if (!c->wscr.ensure((size_t)PREP_B * 8 * nl * 4)) return FGV_ENOMEM;
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  hipLaunchKernelGGL(k_prep, dim3(nl / 256), dim3(256), 0, c->stream, N, d_status, d_slot,
+                     c->key_ok.as<uint8_t>(), d_r, d_s, d_dig, c->d1.as<int8_t>(), c->d2.as<int8_t>(),
+                     c->wscr.as<uint32_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+  uint32_t grid = (N + POINT_THREADS - 1) / POINT_THREADS;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(k_point, dim3(grid), dim3(POINT_THREADS), KT_BYTES, c->stream, N, d_status,
+                     d_slot, c->gtab.as<apoint_raw>(), c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(),
+                     c->d2.as<int8_t>(), d_r);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+  return FGV_OK;
+}
+
+static void read_stage_times(fgv_ctx *c, bool ran) {
+  float ms = 0;
+  c->t_prep = c->t_point = 0;
+  if (!ran) return;
+  if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->t_prep = ms;
+  if (hipEventElapsedTime(&ms, c->ev[3], c->ev[4]) == hipSuccess) c->t_point = ms;
+}
+
 // ------------------------------------------------------------------ verify core
 // digests: host pointer (n*32) or nullptr when ctx->dig already holds device digests.
 static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, size_t sig_buf_len,
@@ -315,8 +346,7 @@ static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, 
   }
   // 3) upload + kernels
   if (!c->status.ensure(n) || !c->slot.ensure(n * 4) || !c->r.ensure(n * 32) ||
-      !c->s.ensure(n * 32) || !c->dig.ensure(n * 32) || !c->d1.ensure((size_t)NWIN * n) ||
-      !c->d2.ensure((size_t)NWIN * n))
+      !c->s.ensure(n * 32) || !c->dig.ensure(n * 32))
     return FGV_ENOMEM;
   HIP_TRY(hipMemcpyAsync(c->status.p, st, n, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->slot.p, slot, n * 4, hipMemcpyHostToDevice, c->stream));
@@ -328,36 +358,28 @@ static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, 
     HIP_TRY(hipMemcpyAsync(c->dig.p, c->h_dig.p, n * 32, hipMemcpyHostToDevice, c->stream));
   }
   if (pending) {
-    uint32_t nl = (N + PREP_B - 1) / PREP_B;
-    nl = (nl + 255) / 256 * 256;
-    if (!c->wscr.ensure((size_t)PREP_B * 8 * nl * 4)) return FGV_ENOMEM;
-    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    hipLaunchKernelGGL(k_prep, dim3(nl / 256), dim3(256), 0, c->stream, N, c->status.as<uint8_t>(),
-                       c->slot.as<uint32_t>(), c->key_ok.as<uint8_t>(), c->r.as<uint32_t>(),
-                       c->s.as<uint32_t>(), c->dig.as<uint8_t>(), c->d1.as<int8_t>(),
-                       c->d2.as<int8_t>(), c->wscr.as<uint32_t>());
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-    uint32_t grid = (N + POINT_THREADS - 1) / POINT_THREADS;
-    if (grid > 1024) grid = 1024;
-    hipLaunchKernelGGL(k_point, dim3(grid), dim3(POINT_THREADS), KT_BYTES, c->stream, N,
-                       c->status.as<uint8_t>(), c->slot.as<uint32_t>(), c->gtab.as<apoint_raw>(),
-                       c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(), c->d2.as<int8_t>(),
-                       c->r.as<uint32_t>());
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    int rc = launch_verify_stages(c, N, c->status.as<uint8_t>(), c->slot.as<uint32_t>(),
+                                  c->r.as<uint32_t>(), c->s.as<uint32_t>(), c->dig.as<uint8_t>());
+    if (rc) return rc;
   }
   HIP_TRY(hipMemcpyAsync(st, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   memcpy(status_out, st, n);
+  read_stage_times(c, pending != 0);
   float ms = 0;
-  c->t_prep = c->t_point = 0;
-  if (pending) {
-    if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->t_prep = ms;
-    if (hipEventElapsedTime(&ms, c->ev[3], c->ev[4]) == hipSuccess) c->t_point = ms;
-  }
   if (!new_keys.empty() && hipEventElapsedTime(&ms, c->ev[6], c->ev[7]) == hipSuccess)
     c->t_keytab = ms;
+  return FGV_OK;
+}
+
+static int launch_sha(fgv_ctx *c, const uint8_t *d_buf, const uint64_t *d_off,
+                      const uint32_t *d_len, size_t n) {
+  if (!c->dig.ensure(n * 32)) return FGV_ENOMEM;
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  hipLaunchKernelGGL(k_sha256, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, c->stream, d_buf,
+                     d_off, d_len, (uint32_t)n, c->dig.as<uint8_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   return FGV_OK;
 }
 
@@ -372,13 +394,7 @@ static int sha_core(fgv_ctx *c, const uint8_t *buf, size_t buf_len, const uint64
   HIP_TRY(hipMemsetAsync(c->msg.as<uint8_t>() + buf_len, 0, 64, c->stream));
   HIP_TRY(hipMemcpyAsync(c->moff.p, off, n * 8, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->mlen.p, len, n * 4, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  hipLaunchKernelGGL(k_sha256, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, c->stream,
-                     c->msg.as<uint8_t>(), c->moff.as<uint64_t>(), c->mlen.as<uint32_t>(),
-                     (uint32_t)n, c->dig.as<uint8_t>());
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-  return FGV_OK;
+  return launch_sha(c, c->msg.as<uint8_t>(), c->moff.as<uint64_t>(), c->mlen.as<uint32_t>(), n);
 }
 
 extern "C" {
@@ -423,6 +439,82 @@ int fgv_p256_verify_msgs(fgv_ctx *c, const uint8_t *keys, const uint8_t *msg_buf
   float ms = 0;
   if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->t_sha = ms;
   return rc;
+}
+
+int fgv_keys_reset(fgv_ctx *c) {
+  if (!c) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->key_map.clear();
+  return FGV_OK;
+}
+
+int fgv_keys_register(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots) {
+  if (!c || (n && (!keys || !slots))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  std::vector<std::array<uint8_t, 64>> fresh;
+  std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> seen;
+  for (size_t i = 0; i < n; i++) {
+    std::array<uint8_t, 64> k;
+    memcpy(k.data(), keys + 64 * i, 64);
+    if (c->key_map.count(k) || seen.count(k)) continue;
+    seen.emplace(k, 0);
+    fresh.push_back(k);
+  }
+  if (c->key_map.size() + fresh.size() > c->key_slots) return FGV_ENOMEM;
+  c->t_keytab = 0;
+  if (!fresh.empty()) {
+    const uint32_t nk = (uint32_t)fresh.size();
+    if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kslot.ensure((size_t)nk * 4)) return FGV_ENOMEM;
+    uint32_t *kq = c->h_kq.as<uint32_t>(), *ks = c->h_kslot.as<uint32_t>();
+    uint32_t next = (uint32_t)c->key_map.size();
+    for (uint32_t j = 0; j < nk; j++) {
+      be32_to_limbs(fresh[j].data(), kq + 16 * j);
+      be32_to_limbs(fresh[j].data() + 32, kq + 16 * j + 8);
+      ks[j] = next + j;
+    }
+    int rc = build_tables(c, kq, ks, nk, c->ktab.as<apoint_raw>(), c->key_ok.as<uint8_t>());
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (uint32_t j = 0; j < nk; j++) c->key_map.emplace(fresh[j], next + j);
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev[6], c->ev[7]) == hipSuccess) c->t_keytab = ms;
+  }
+  for (size_t i = 0; i < n; i++) {
+    std::array<uint8_t, 64> k;
+    memcpy(k.data(), keys + 64 * i, 64);
+    slots[i] = c->key_map[k];
+  }
+  return FGV_OK;
+}
+
+int fgv_p256_verify_msgs_dev(fgv_ctx *c, const uint8_t *d_msg_buf, const uint64_t *d_msg_off,
+                             const uint32_t *d_msg_len, const uint8_t *d_sig_buf,
+                             const uint64_t *d_sig_off, const uint32_t *d_sig_len,
+                             const uint32_t *d_key_slot, size_t n, uint8_t *d_status) {
+  if (!c || (n && (!d_msg_buf || !d_msg_off || !d_msg_len || !d_sig_buf || !d_sig_off ||
+                   !d_sig_len || !d_key_slot || !d_status)))
+    return FGV_EINVAL;
+  if (n == 0) return FGV_OK;
+  if (n > 0x7fffffffu) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  const uint32_t N = (uint32_t)n;
+  if (!c->r.ensure(n * 32) || !c->s.ensure(n * 32)) return FGV_ENOMEM;
+  int rc = launch_sha(c, d_msg_buf, d_msg_off, d_msg_len, n);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, d_sig_buf, d_sig_off,
+                     d_sig_len, N, d_status, c->r.as<uint32_t>(), c->s.as<uint32_t>());
+  HIP_TRY(hipGetLastError());
+  rc = launch_verify_stages(c, N, d_status, d_key_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>(),
+                            c->dig.as<uint8_t>());
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->t_sha = ms;
+  read_stage_times(c, true);
+  c->t_keytab = 0;
+  return FGV_OK;
 }
 
 }  // extern "C"

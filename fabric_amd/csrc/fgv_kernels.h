@@ -34,3 +34,5 @@ __global__ void k_point(uint32_t n, uint8_t *status, const uint32_t *key_slot, c
                         const uint32_t *r_limbs);
 __global__ void k_sha256(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint32_t n,
                          uint8_t *out);
+__global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_t *len, uint32_t n,
+                      uint8_t *status, uint32_t *r_limbs, uint32_t *s_limbs);

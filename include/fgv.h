@@ -76,6 +76,24 @@ int fgv_p256_verify_msgs(fgv_ctx *ctx, const uint8_t *keys, const uint8_t *msg_b
                          const uint8_t *sig_buf, size_t sig_buf_len, const uint64_t *sig_off,
                          const uint32_t *sig_len, size_t n, uint8_t *status);
 
+/* ------------------------------------------- key registry + HBM-resident batches */
+
+/* Register public keys (n*64 bytes X||Y) in the device key-table cache and return their
+ * slots.  The analogue of the MSP identity cache (msp/cache/cache.go:65-83): identities are
+ * deserialized once, their key tables built once, and every later verify is a slot lookup.
+ * Returns FGV_ENOMEM when the cache is full (call fgv_keys_reset and re-register). */
+int fgv_keys_register(fgv_ctx *ctx, const uint8_t *keys, size_t n, uint32_t *slots);
+int fgv_keys_reset(fgv_ctx *ctx);
+
+/* identity.Verify over a batch already resident in device memory: every pointer below is a
+ * DEVICE pointer (e.g. hipMalloc or a torch tensor's data_ptr on this device).  Message and
+ * signature arenas must be readable 64 bytes past their last byte.  Runs k_sha256, k_der,
+ * k_prep, k_point on the context's stream and returns when d_status is final. */
+int fgv_p256_verify_msgs_dev(fgv_ctx *ctx, const uint8_t *d_msg_buf, const uint64_t *d_msg_off,
+                             const uint32_t *d_msg_len, const uint8_t *d_sig_buf,
+                             const uint64_t *d_sig_off, const uint32_t *d_sig_len,
+                             const uint32_t *d_key_slot, size_t n, uint8_t *d_status);
+
 #ifdef __cplusplus
 }
 #endif
