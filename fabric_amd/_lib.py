@@ -18,12 +18,20 @@ SIG_VALID, SIG_FALSE, SIG_DER, SIG_HIGH_S, SIG_RANGE, SIG_BADKEY, SIG_EMPTY = ra
 EXPORTED = [
     "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_sha256_batch",
     "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset",
-    "fgv_p256_verify_msgs_dev",
+    "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
+    "fgv_ledger_add_txids", "fgv_validate_blocks",
 ]
+FGV_EUNSUPPORTED = -6
 
 
 class FgvError(RuntimeError):
-    pass
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
+
+
+class Unsupported(FgvError):
+    """FGV_EUNSUPPORTED: the batch needs logic outside the engine's model."""
 
 
 class _Config(ctypes.Structure):
@@ -54,13 +62,20 @@ def load():
         L.fgv_keys_register.argtypes = [vp, vp, sz, vp]
         L.fgv_keys_reset.argtypes = [vp]
         L.fgv_p256_verify_msgs_dev.argtypes = [vp] * 8 + [sz, vp]
+        L.fgv_channel_init.argtypes = [vp, ctypes.c_char_p]
+        L.fgv_msp_add_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
+        L.fgv_chaincode_define.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
+        L.fgv_ledger_add_txids.argtypes = [vp, vp, vp, vp, sz]
+        L.fgv_validate_blocks.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp]
         _L = L
     return _L
 
 
 def _check(rc):
+    if rc == FGV_EUNSUPPORTED:
+        raise Unsupported("libfgv: block outside the engine's model", rc)
     if rc != 0:
-        raise FgvError(f"libfgv error {rc}: {load().fgv_strerror(rc).decode()}")
+        raise FgvError(f"libfgv error {rc}: {load().fgv_strerror(rc).decode()}", rc)
 
 
 def _ptr(a):
@@ -150,3 +165,36 @@ class Engine:
     def verify_msgs_dev(self, msg_buf, msg_off, msg_len, sig_buf, sig_off, sig_len, key_slot, n, status):
         _check(self._L.fgv_p256_verify_msgs_dev(self._h, msg_buf, msg_off, msg_len, sig_buf, sig_off, sig_len,
                                                 key_slot, n, status))
+
+    # --- committer: channel model + whole blocks
+    def channel_init(self, name: str):
+        _check(self._L.fgv_channel_init(self._h, name.encode()))
+
+    def msp_add_identity(self, serialized: bytes, pubkey64, valid: bool, id_digest: bytes):
+        _check(self._L.fgv_msp_add_identity(self._h, serialized, len(serialized), pubkey64, 1 if valid else 0,
+                                            id_digest))
+
+    def chaincode_define(self, ns: str, policy: bytes):
+        _check(self._L.fgv_chaincode_define(self._h, ns.encode(), policy, len(policy)))
+
+    def ledger_add_txids(self, txids):
+        arena, offs, lens = pack([t.encode() for t in txids])
+        _check(self._L.fgv_ledger_add_txids(self._h, _ptr(arena), _ptr(offs), _ptr(lens), len(txids)))
+
+    def validate_blocks(self, blocks, d_blocks=None):
+        """blocks: list of bytes (host).  d_blocks: optional list of device addresses (ints).
+        Returns a list of numpy uint8 flag arrays (TxValidationFlags), one per block."""
+        nb = len(blocks)
+        bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+        ptrs = (ctypes.c_void_p * nb)(*[b.ctypes.data for b in bufs])
+        lens = (ctypes.c_size_t * nb)(*[len(b) for b in blocks])
+        dptr = (ctypes.c_void_p * nb)(*d_blocks) if d_blocks is not None else None
+        cap = sum(len(b) for b in blocks) // 16 + 1024  # >= one byte per envelope
+        flags = np.zeros(cap, dtype=np.uint8)
+        ntx = (ctypes.c_size_t * nb)()
+        _check(self._L.fgv_validate_blocks(self._h, nb, ptrs, lens, dptr, _ptr(flags), cap, ntx))
+        out, o = [], 0
+        for i in range(nb):
+            out.append(flags[o:o + ntx[i]].copy())
+            o += ntx[i]
+        return out

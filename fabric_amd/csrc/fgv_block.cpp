@@ -1,0 +1,1094 @@
+// fgv_block.cpp -- TxValidator.Validate for blocks of endorser transactions (libfgv.so).
+//
+// One call validates a batch of blocks (signatures of several blocks are verified in one GPU
+// pass -- verify bits are pure functions of their inputs, so speculative batching is exact):
+//   A. host, parallel over txs: single-pass protobuf parse of every envelope (pbwire.h, Go
+//      protobuf-go rules) into a TxRec: every check of the reference that needs no crypto is
+//      decided here, and hash / verify jobs are emitted for the rest;
+//   B. device: k_sha256_jobs (creator payload, nonce||creator, chdr||shdr||ccpp,
+//      prp||endorser -- spans read in place from the block bytes in HBM), k_der, k_prep,
+//      k_point over every creator + endorsement signature;
+//   C. host, parallel over txs: the reference's code precedence, cauthdsl policy folding over
+//      the verify bits, then (serial) markTXIdDuplicates and the txid index across blocks.
+//
+// Reference (behaviour restated; citations under /root/reference):
+//   core/committer/txvalidator/v20/validator.go:180-481, core/common/validation/msgvalidation.go
+//   :26-320, plugindispatcher/dispatcher.go:102-302, builtin/v20/validation_logic.go:109-217,
+//   statebased/validator_keylevel.go:38-282 + v20.go:105-167, core/policy/application.go:148-163,
+//   common/cauthdsl/cauthdsl.go:24-92 + policy.go:86-108, common/policies/policy.go:363-395,
+//   msp/identities.go:170-199, protoutil/{proputils.go:198-223,351-370, txutils.go:21-58,449-466,
+//   503-534}.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/fgv.h"
+#include "fgv_internal.h"
+#include "pbwire.h"
+
+using pbw::Span;
+
+namespace fgvb {
+
+// ------------------------------------------------------------------ small helpers
+static uint64_t hash_bytes(const uint8_t *p, size_t n, uint64_t h = 0x9E3779B97F4A7C15ull) {
+  for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001B3ull;
+  return h ^ (h >> 29);
+}
+
+// ------------------------------------------------------------------ message visitors
+struct VEnvelope {
+  Span payload, signature;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? payload : signature) = s; return true; }
+};
+struct VHeader {
+  Span channel_header, signature_header;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? channel_header : signature_header) = s; return true; }
+};
+struct VPayload {
+  pbw::MsgField header;
+  Span data;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_MSG : n == 2 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) header.add(s); else data = s;
+    return true;
+  }
+};
+struct VTimestamp {  // google.protobuf.Timestamp {seconds int64 = 1, nanos int32 = 2}
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_VARINT : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VChannelHeader {
+  int32_t type = 0;
+  uint64_t epoch = 0;
+  Span channel_id, tx_id, extension;
+  pbw::Kind kind(uint32_t n) {
+    switch (n) {
+      case 1: case 2: case 6: return pbw::K_VARINT;
+      case 3: return pbw::K_MSG;
+      case 4: case 5: return pbw::K_STRING;
+      case 7: case 8: return pbw::K_BYTES;
+      default: return pbw::K_NONE;
+    }
+  }
+  void on_varint(uint32_t n, uint64_t v) {
+    if (n == 1) type = pbw::as_int32(v);
+    else if (n == 6) epoch = v;
+  }
+  bool on_len(uint32_t n, Span s) {
+    if (n == 3) { VTimestamp t; return pbw::decode(s.p, s.n, t); }
+    if (n == 4) channel_id = s;
+    else if (n == 5) tx_id = s;
+    else if (n == 7) extension = s;
+    return true;
+  }
+};
+struct VSignatureHeader {
+  Span creator, nonce;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? creator : nonce) = s; return true; }
+};
+struct VTransactionAction {
+  Span header, payload;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? header : payload) = s; return true; }
+};
+struct VTransaction {
+  std::vector<VTransactionAction> actions;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    VTransactionAction a;
+    if (!pbw::decode(s.p, s.n, a)) return false;
+    actions.push_back(a);
+    return true;
+  }
+};
+struct VEndorsement {
+  Span endorser, signature;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? endorser : signature) = s; return true; }
+};
+struct VEndorsedAction {
+  Span prp;
+  std::vector<VEndorsement> ends;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { prp = s; return true; }
+    VEndorsement e;
+    if (!pbw::decode(s.p, s.n, e)) return false;
+    ends.push_back(e);
+    return true;
+  }
+};
+struct VCcActionPayload {
+  Span ccpp;
+  bool has_action = false;
+  VEndorsedAction action;  // all occurrences merged in order
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { ccpp = s; return true; }
+    has_action = true;
+    return pbw::decode(s.p, s.n, action);
+  }
+};
+struct VPrp {
+  Span proposal_hash, extension;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? proposal_hash : extension) = s; return true; }
+};
+struct VChaincodeID {
+  Span path, name, version;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_STRING : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? path : n == 2 ? name : version) = s; return true; }
+};
+struct VResponse {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_VARINT : n == 2 ? pbw::K_STRING : n == 3 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VCcAction {
+  Span results, events;
+  bool has_ccid = false;
+  VChaincodeID ccid;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : (n == 3 || n == 4) ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { results = s; return true; }
+    if (n == 2) { events = s; return true; }
+    if (n == 3) { VResponse r; return pbw::decode(s.p, s.n, r); }
+    has_ccid = true;
+    return pbw::decode(s.p, s.n, ccid);
+  }
+};
+struct VHdrExt {  // ChaincodeHeaderExtension {chaincode_id = 2}
+  bool has_ccid = false;
+  VChaincodeID ccid;
+  pbw::Kind kind(uint32_t n) { return n == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) { has_ccid = true; return pbw::decode(s.p, s.n, ccid); }
+};
+struct VCcEvent {
+  Span chaincode_id;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_STRING : n == 4 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { if (n == 1) chaincode_id = s; return true; }
+};
+// --- rwset (validated in full; the committer only needs namespaces + write presence)
+struct VVersion {
+  uint64_t block = 0, tx = 0;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_VARINT : pbw::K_NONE; }
+  void on_varint(uint32_t n, uint64_t v) { (n == 1 ? block : tx) = v; }
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VKVRead {
+  Span key;
+  bool has_ver = false;
+  VVersion ver;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { key = s; return true; }
+    has_ver = true;
+    return pbw::decode(s.p, s.n, ver);
+  }
+};
+struct VQueryReads {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) { VKVRead r; return pbw::decode(s.p, s.n, r); }
+};
+struct VMerkle {
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_VARINT : n == 3 ? pbw::K_REP_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VRangeQuery {
+  pbw::Kind kind(uint32_t n) {
+    return (n == 1 || n == 2) ? pbw::K_STRING : n == 3 ? pbw::K_VARINT : (n == 4 || n == 5) ? pbw::K_MSG : pbw::K_NONE;
+  }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 4) { VQueryReads q; return pbw::decode(s.p, s.n, q); }
+    if (n == 5) { VMerkle m; return pbw::decode(s.p, s.n, m); }
+    return true;
+  }
+};
+struct VKVWrite {
+  Span key, value;
+  bool is_delete = false;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_VARINT : n == 3 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { is_delete = v != 0; }
+  bool on_len(uint32_t n, Span s) { (n == 1 ? key : value) = s; return true; }
+};
+struct VMetaEntry {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VMetaWrite {  // KVMetadataWrite {key string=1, entries=2}
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) return true;
+    VMetaEntry e;
+    return pbw::decode(s.p, s.n, e);
+  }
+};
+struct VKVRWSet {
+  uint32_t nreads = 0, nrq = 0, nwrites = 0, nmeta = 0;
+  std::vector<VKVRead> *reads = nullptr;     // optional capture (MVCC)
+  std::vector<VKVWrite> *writes = nullptr;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 4) ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) {
+      VKVRead r;
+      if (!pbw::decode(s.p, s.n, r)) return false;
+      nreads++;
+      if (reads) reads->push_back(r);
+      return true;
+    }
+    if (n == 2) { nrq++; VRangeQuery q; return pbw::decode(s.p, s.n, q); }
+    if (n == 3) {
+      VKVWrite w;
+      if (!pbw::decode(s.p, s.n, w)) return false;
+      nwrites++;
+      if (writes) writes->push_back(w);
+      return true;
+    }
+    nmeta++;
+    VMetaWrite m;
+    return pbw::decode(s.p, s.n, m);
+  }
+};
+struct VHashRead {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) return true;
+    VVersion v;
+    return pbw::decode(s.p, s.n, v);
+  }
+};
+struct VHashWrite {
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 3) ? pbw::K_BYTES : (n == 2 || n == 4) ? pbw::K_VARINT : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VHashMeta {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) return true;
+    VMetaEntry e;
+    return pbw::decode(s.p, s.n, e);
+  }
+};
+struct VHashedRWSet {
+  uint32_t nreads = 0, nwrites = 0, nmeta = 0;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { nreads++; VHashRead r; return pbw::decode(s.p, s.n, r); }
+    if (n == 2) { nwrites++; VHashWrite w; return pbw::decode(s.p, s.n, w); }
+    nmeta++;
+    VHashMeta m;
+    return pbw::decode(s.p, s.n, m);
+  }
+};
+struct VCollHashed {
+  Span name, hashed;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : (n == 2 || n == 3) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) name = s;
+    else if (n == 2) hashed = s;
+    return true;
+  }
+};
+struct VNsRwSet {
+  Span ns, rwset;
+  std::vector<VCollHashed> coll;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_BYTES : n == 3 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { ns = s; return true; }
+    if (n == 2) { rwset = s; return true; }
+    VCollHashed c;
+    if (!pbw::decode(s.p, s.n, c)) return false;
+    coll.push_back(c);
+    return true;
+  }
+};
+struct VTxRwSet {
+  std::vector<VNsRwSet> ns;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_VARINT : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    VNsRwSet r;
+    if (!pbw::decode(s.p, s.n, r)) return false;
+    ns.push_back(std::move(r));
+    return true;
+  }
+};
+struct VSerializedIdentity {
+  Span mspid, id_bytes;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? mspid : id_bytes) = s; return true; }
+};
+struct VBlockData {
+  std::vector<Span> data;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_REP_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) { data.push_back(s); return true; }
+};
+struct VSkipMsg {  // BlockHeader / BlockMetadata: validated, contents unused
+  uint32_t rep_bytes_field = 0;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? (rep_bytes_field ? pbw::K_REP_BYTES : pbw::K_VARINT) : (n == 2 || n == 3) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VBlock {
+  VBlockData data;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 2) return pbw::decode(s.p, s.n, data);
+    VSkipMsg m;
+    m.rep_bytes_field = (n == 3);
+    return pbw::decode(s.p, s.n, m);
+  }
+};
+
+// --- policies
+struct VMSPRole {
+  Span mspid;
+  int32_t role = 0;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_VARINT : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { role = pbw::as_int32(v); }
+  bool on_len(uint32_t, Span s) { mspid = s; return true; }
+};
+struct VPrincipal {
+  int32_t cls = 0;
+  Span principal;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_VARINT : n == 2 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { cls = pbw::as_int32(v); }
+  bool on_len(uint32_t, Span s) { principal = s; return true; }
+};
+
+}  // namespace fgvb
+
+// ======================================================================= channel model
+namespace fgvb {
+
+struct Ident {
+  std::string mspid;
+  std::string id_bytes;
+  int32_t key_slot = -1;  // -1: not a P-256 key (Verify errors)
+  bool valid = false;     // msp Validate() result
+  uint32_t canon = 0;     // dedup identity id: Mspid + Id (Id = hex SHA-256(cert))
+};
+
+struct PNode {
+  int type = 0;  // 1 NOutOf, 2 SignedBy
+  int32_t n = 0;
+  int principal = -1;
+  std::vector<int> kids;
+};
+struct Policy {
+  bool decode_ok = false, compile_ok = false, unsupported = false;
+  std::vector<PNode> nodes;
+  int root = -1;
+  std::vector<std::string> principal_msp;  // "" + bad flag for undecodable principal
+  std::vector<bool> principal_bad;
+};
+
+// SignaturePolicy decoding into the node list (recursive, oneof: last member wins)
+struct VSigPolicy;
+struct VNOutOf {
+  int32_t n = 0;
+  std::vector<Span> rules;
+  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_VARINT : f == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { n = pbw::as_int32(v); }
+  bool on_len(uint32_t, Span s) { rules.push_back(s); return true; }
+};
+struct VSigPolicyRaw {
+  int which = 0;  // 0 none, 1 signed_by, 2 n_out_of
+  int32_t signed_by = 0;
+  std::vector<Span> noutof;  // merged occurrences
+  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_VARINT : f == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { which = 1; signed_by = pbw::as_int32(v); noutof.clear(); }
+  bool on_len(uint32_t, Span s) {
+    if (which != 2) noutof.clear();
+    which = 2;
+    noutof.push_back(s);
+    return true;
+  }
+};
+struct VSPE {
+  int32_t version = 0;
+  bool has_rule = false;
+  std::vector<Span> rule;
+  std::vector<Span> identities;
+  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_VARINT : f == 2 ? pbw::K_MSG : f == 3 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { version = pbw::as_int32(v); }
+  bool on_len(uint32_t f, Span s) {
+    if (f == 2) { has_rule = true; rule.push_back(s); }
+    else identities.push_back(s);
+    return true;
+  }
+};
+struct VAppPolicy {
+  int which = 0;  // 1 signature_policy, 2 channel ref
+  std::vector<Span> spe;
+  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_MSG : f == 2 ? pbw::K_STRING : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t f, Span s) {
+    if (f == 1) {
+      if (which != 1) spe.clear();
+      which = 1;
+      spe.push_back(s);
+    } else {
+      which = 2;
+      spe.clear();
+    }
+    return true;
+  }
+};
+
+// decode a (merged) SignaturePolicy fully; returns false on wire error
+static bool decode_sigpolicy(const std::vector<Span> &occ, VSigPolicyRaw &out) {
+  for (const Span &s : occ)
+    if (!pbw::decode(s.p, s.n, out)) return false;
+  return true;
+}
+
+// Build nodes (cauthdsl.compile shape).  Returns node index or -1 on compile error.
+static int build_node(Policy &P, const std::vector<Span> &occ, bool &wire_ok, int depth) {
+  if (depth > 1000) { wire_ok = false; return -1; }
+  VSigPolicyRaw raw;
+  if (!decode_sigpolicy(occ, raw)) { wire_ok = false; return -1; }
+  PNode node;
+  if (raw.which == 1) {
+    node.type = 2;
+    if (raw.signed_by < 0 || raw.signed_by >= (int32_t)P.principal_msp.size()) return -1;
+    node.principal = raw.signed_by;
+  } else if (raw.which == 2) {
+    node.type = 1;
+    VNOutOf no;
+    for (const Span &s : raw.noutof)
+      if (!pbw::decode(s.p, s.n, no)) { wire_ok = false; return -1; }
+    node.n = no.n;
+    // sub-rules must all decode (eager protobuf) before compile errors matter
+    std::vector<int> kids;
+    bool compile_fail = false;
+    for (const Span &r : no.rules) {
+      std::vector<Span> one{r};
+      int k = build_node(P, one, wire_ok, depth + 1);
+      if (!wire_ok) return -1;
+      if (k < 0) compile_fail = true;
+      kids.push_back(k);
+    }
+    if (compile_fail) return -1;
+    node.kids = kids;
+  } else {
+    return -1;  // "Unknown type" (nil rule handled by caller)
+  }
+  P.nodes.push_back(node);
+  return (int)P.nodes.size() - 1;
+}
+
+static Policy compile_policy(const uint8_t *b, size_t n) {
+  Policy P;
+  VAppPolicy ap;
+  if (!pbw::decode(b, n, ap)) return P;  // unmarshal error -> evaluation error
+  if (ap.which == 2) { P.decode_ok = true; P.unsupported = true; return P; }
+  if (ap.which != 1) { P.decode_ok = true; return P; }  // unsupported policy type -> error
+  VSPE spe;
+  for (const Span &s : ap.spe)
+    if (!pbw::decode(s.p, s.n, spe)) return P;
+  // 1) wire: every MSPPrincipal and the whole rule tree decode eagerly (proto.Unmarshal)
+  std::vector<VPrincipal> prs(spe.identities.size());
+  for (size_t i = 0; i < spe.identities.size(); i++)
+    if (!pbw::decode(spe.identities[i].p, spe.identities[i].n, prs[i])) return P;
+  for (const VPrincipal &pr : prs) {
+    VMSPRole role;
+    bool ok = pbw::decode(pr.principal.p, pr.principal.n, role);
+    P.principal_msp.push_back(ok ? role.mspid.str() : std::string());
+    P.principal_bad.push_back(!ok);
+  }
+  bool wire_ok = true;
+  int root = -1;
+  if (spe.has_rule) root = build_node(P, spe.rule, wire_ok, 0);
+  if (!wire_ok) return Policy();
+  // 2) principals outside ROLE/MEMBER need MSP data the engine does not model
+  for (size_t i = 0; i < prs.size(); i++) {
+    if (prs[i].cls != 0) { P.decode_ok = true; P.unsupported = true; return P; }
+    if (!P.principal_bad[i]) {
+      VMSPRole role;
+      pbw::decode(prs[i].principal.p, prs[i].principal.n, role);
+      if (role.role != 0) { P.decode_ok = true; P.unsupported = true; return P; }
+    }
+  }
+  P.decode_ok = true;
+  P.root = root;
+  P.compile_ok = root >= 0;
+  return P;
+}
+
+struct Channel {
+  std::string name;
+  std::vector<Ident> idents;
+  std::unordered_multimap<uint64_t, uint32_t> ident_index;
+  std::unordered_map<std::string, uint32_t> canon_ids;
+  std::vector<Policy> policies;
+  std::unordered_map<std::string, int> chaincodes;  // namespace -> policies index
+  std::unordered_set<std::string> committed;
+
+  int lookup(const Span &ser) const {
+    VSerializedIdentity sid;
+    if (!pbw::decode(ser.p, ser.n, sid)) return -1;
+    uint64_t h = hash_bytes(sid.mspid.p, sid.mspid.n);
+    h = hash_bytes(sid.id_bytes.p, sid.id_bytes.n, h ^ 0xA5);
+    auto range = ident_index.equal_range(h);
+    for (auto it = range.first; it != range.second; ++it) {
+      const Ident &I = idents[it->second];
+      if (sid.mspid.eq(I.mspid.data(), I.mspid.size()) && sid.id_bytes.eq(I.id_bytes.data(), I.id_bytes.size()))
+        return (int)it->second;
+    }
+    return -1;
+  }
+};
+
+// ======================================================================= per-tx records
+enum : uint8_t { C_VALID = 0, C_BAD_PAYLOAD = 2, C_BAD_HDR = 3, C_BAD_CREATOR = 4, C_BAD_ETX = 5,
+                 C_UNSUP_PAYLOAD = 7, C_BAD_TXID = 8, C_DUP_TXID = 9, C_POLICY = 10,
+                 C_BAD_HDR_EXT = 19, C_BAD_RESP = 21, C_BAD_RWSET = 22, C_ILLEGAL_WS = 23,
+                 C_INVALID_CC = 25, C_OTHER = 255, C_PENDING = 0xFE, C_UNSUPPORTED = 0xFD };
+
+struct EndRec {
+  int ident = -1;
+  uint32_t vjob = UINT32_MAX;  // verify job (UINT32_MAX: no verification possible)
+  Span endorser, sig;
+};
+
+struct TxRec {
+  uint8_t pre = C_PENDING;   // decided without crypto (final) or C_PENDING
+  int32_t type = 0;
+  Span payload, env_sig, nonce, creator, chdr, act_hdr, ccpp, prop_hash, prp, txid;
+  int creator_ident = -1;
+  uint8_t etx = C_PENDING;   // validateEndorserTransaction structural result (0 ok, 5, unsupported)
+  uint8_t disp = C_PENDING;  // Dispatch structural result (0 ok -> policies)
+  std::vector<int> policies;  // chaincode policy per written namespace (-1 unknown chaincode)
+  std::vector<EndRec> ends;
+  uint32_t cjob = UINT32_MAX, txid_job = UINT32_MAX, prop_job = UINT32_MAX, cvjob = UINT32_MAX;
+  std::string index_txid;  // GetOrComputeTxIDFromEnvelope (txid index), "" on error
+  bool index_ok = false;
+  Span idx_nonce, idx_creator;  // for the computed txid when chdr.TxId is empty
+  uint32_t index_job = UINT32_MAX;
+};
+
+}  // namespace fgvb
+
+// ======================================================================= context glue
+using namespace fgvb;
+
+struct ThreadPool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  std::function<void(size_t)> job;
+  size_t njobs = 0;
+  std::atomic<size_t> next{0};
+  size_t active = 0;
+  uint64_t gen = 0;
+  bool stop = false;
+  explicit ThreadPool(unsigned n) {
+    for (unsigned i = 0; i < n; i++)
+      th.emplace_back([this] {
+        uint64_t seen = 0;
+        for (;;) {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return stop || gen != seen; });
+          if (stop) return;
+          seen = gen;
+          lk.unlock();
+          for (size_t i; (i = next.fetch_add(1)) < njobs;) job(i);
+          lk.lock();
+          if (--active == 0) done_cv.notify_all();
+        }
+      });
+  }
+  ~ThreadPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+  // run f(i) for i in [0, n) in chunks
+  void parallel_for(size_t n, const std::function<void(size_t)> &f) {
+    if (n == 0) return;
+    if (th.empty() || n < 64) {
+      for (size_t i = 0; i < n; i++) f(i);
+      return;
+    }
+    const size_t chunk = std::max<size_t>(16, n / (th.size() * 8));
+    const size_t nchunks = (n + chunk - 1) / chunk;
+    std::unique_lock<std::mutex> lk(mu);
+    job = [&](size_t c) {
+      size_t lo = c * chunk, hi = std::min(n, lo + chunk);
+      for (size_t i = lo; i < hi; i++) f(i);
+    };
+    njobs = nchunks;
+    next = 0;
+    active = th.size();
+    gen++;
+    cv.notify_all();
+    done_cv.wait(lk, [&] { return active == 0; });
+  }
+};
+
+struct fgv_block_state {
+  Channel ch;
+  ThreadPool pool;
+  // per-call scratch
+  std::vector<TxRec> recs;
+  explicit fgv_block_state(unsigned threads) : pool(threads) {}
+};
+
+fgv_block_state *fgv_block_state_new(unsigned threads) { return new fgv_block_state(threads); }
+void fgv_block_state_free(fgv_block_state *s) { delete s; }
+
+// ======================================================================= parsing
+static void parse_tx(const Channel &ch, Span d, TxRec &R) {
+  R = TxRec();
+  VEnvelope env;
+  if (!pbw::decode(d.p, d.n, env)) { R.pre = C_OTHER; return; }
+  VPayload pl;
+  VHeader hdr;
+  if (!pbw::decode(env.payload.p, env.payload.n, pl) || !pl.header.decode_into(hdr)) {
+    R.pre = C_BAD_PAYLOAD;
+    return;
+  }
+  // txid index value (protoutil.GetOrComputeTxIDFromEnvelope, txutils.go:503-534)
+  if (pl.header.present) {
+    VChannelHeader c0;
+    if (pbw::decode(hdr.channel_header.p, hdr.channel_header.n, c0)) {
+      if (c0.tx_id.n) {
+        R.index_txid = c0.tx_id.str();
+        R.index_ok = true;
+      } else {
+        VSignatureHeader s0;
+        if (pbw::decode(hdr.signature_header.p, hdr.signature_header.n, s0)) {
+          R.index_ok = true;  // computed on the device (ComputeTxID)
+          R.idx_nonce = s0.nonce;
+          R.idx_creator = s0.creator;
+        }
+      }
+    }
+  }
+  if (!pl.header.present) { R.pre = C_BAD_HDR; return; }
+  VChannelHeader chdr;
+  VSignatureHeader shdr;
+  if (!pbw::decode(hdr.channel_header.p, hdr.channel_header.n, chdr) ||
+      !pbw::decode(hdr.signature_header.p, hdr.signature_header.n, shdr)) {
+    R.pre = C_BAD_HDR;
+    return;
+  }
+  if (chdr.type != 3 && chdr.type != 2 && chdr.type != 1) { R.pre = C_BAD_HDR; return; }
+  if (chdr.epoch != 0 || shdr.nonce.nil() || shdr.creator.nil()) { R.pre = C_BAD_HDR; return; }
+  R.type = chdr.type;
+  R.payload = env.payload;
+  R.env_sig = env.signature;
+  R.nonce = shdr.nonce;
+  R.creator = shdr.creator;
+  R.chdr = hdr.channel_header;
+  R.txid = chdr.tx_id;
+  // checkSignatureFromCreator (msgvalidation.go:26-64)
+  if (env.signature.nil()) { R.pre = C_BAD_CREATOR; return; }
+  if (chdr.channel_id.n == 0) { R.pre = C_UNSUPPORTED; return; }  // peer-local MSP
+  if (!chdr.channel_id.eq(ch.name.data(), ch.name.size())) { R.pre = C_BAD_CREATOR; return; }
+  R.creator_ident = ch.lookup(shdr.creator);
+  if (R.creator_ident < 0) { R.pre = C_BAD_CREATOR; return; }
+  const Ident &ci = ch.idents[R.creator_ident];
+  if (!ci.valid || ci.key_slot < 0) { R.pre = C_BAD_CREATOR; return; }
+  if (chdr.type != 3) return;  // CONFIG (unsupported) / CONFIG_UPDATE (7) decided in the fold
+
+  // validateEndorserTransaction (msgvalidation.go:165-245)
+  R.etx = C_BAD_ETX;
+  if (pl.data.nil()) return;
+  VTransaction tx;
+  if (!pbw::decode(pl.data.p, pl.data.n, tx) || tx.actions.size() != 1) return;
+  const VTransactionAction &act = tx.actions[0];
+  VSignatureHeader ash;
+  if (!pbw::decode(act.header.p, act.header.n, ash) || ash.nonce.nil() || ash.creator.nil()) return;
+  VCcActionPayload cap;
+  if (!pbw::decode(act.payload.p, act.payload.n, cap)) return;
+  if (!cap.has_action) { R.etx = C_UNSUPPORTED; return; }  // reference dereferences nil (panic)
+  VPrp prp;
+  if (!pbw::decode(cap.action.prp.p, cap.action.prp.n, prp)) return;
+  if (cap.ccpp.nil() || act.header.nil()) return;  // GetProposalHash2 nil arguments
+  R.etx = C_VALID;
+  R.act_hdr = act.header;
+  R.ccpp = cap.ccpp;
+  R.prop_hash = prp.proposal_hash;
+  R.prp = cap.action.prp;
+
+  // Dispatch (dispatcher.go:102-221)
+  VHdrExt ext;
+  if (!pbw::decode(chdr.extension.p, chdr.extension.n, ext)) { R.disp = C_BAD_HDR_EXT; return; }
+  // GetActionFromEnvelope: same bytes as above; failure points re-checked in order
+  if (cap.action.prp.nil()) { R.disp = C_BAD_RESP; return; }
+  if (prp.extension.nil()) { R.disp = C_BAD_RESP; return; }
+  VCcAction cca;
+  if (!pbw::decode(prp.extension.p, prp.extension.n, cca)) { R.disp = C_BAD_RESP; return; }
+  VTxRwSet rw;
+  if (!pbw::decode(cca.results.p, cca.results.n, rw)) { R.disp = C_BAD_RWSET; return; }
+  std::vector<VKVRWSet> kvs(rw.ns.size());
+  std::vector<bool> coll_writes(rw.ns.size(), false);
+  for (size_t k = 0; k < rw.ns.size(); k++) {
+    if (!pbw::decode(rw.ns[k].rwset.p, rw.ns[k].rwset.n, kvs[k])) { R.disp = C_BAD_RWSET; return; }
+    for (const VCollHashed &c : rw.ns[k].coll) {
+      VHashedRWSet h;
+      if (!pbw::decode(c.hashed.p, c.hashed.n, h)) { R.disp = C_BAD_RWSET; return; }
+      if (h.nwrites || h.nmeta) coll_writes[k] = true;
+    }
+  }
+  if (!ext.has_ccid || !cca.has_ccid) { R.disp = C_OTHER; return; }
+  const Span ccid = ext.ccid.name;
+  if (ccid.n == 0 || !ccid.eq(reinterpret_cast<const char *>(cca.ccid.name.p), cca.ccid.name.n) ||
+      cca.ccid.version.n == 0) {
+    R.disp = C_INVALID_CC;
+    return;
+  }
+  if (!cca.events.nil()) {
+    VCcEvent ev;
+    if (!pbw::decode(cca.events.p, cca.events.n, ev) ||
+        !ev.chaincode_id.eq(reinterpret_cast<const char *>(ccid.p), ccid.n)) {
+      R.disp = C_OTHER;
+      return;
+    }
+  }
+  std::vector<std::string> wr{ccid.str()};
+  std::unordered_set<std::string> seen;
+  for (size_t k = 0; k < rw.ns.size(); k++) {
+    std::string ns = rw.ns[k].ns.str();
+    if (!seen.insert(ns).second) { R.disp = C_ILLEGAL_WS; return; }
+    bool writes = kvs[k].nwrites || kvs[k].nmeta || coll_writes[k];
+    if (writes && std::find(wr.begin(), wr.end(), ns) == wr.end()) wr.push_back(ns);
+  }
+  // key-level / collection endorsement policies are outside the modelled state
+  for (size_t k = 0; k < rw.ns.size(); k++) {
+    std::string ns = rw.ns[k].ns.str();
+    if (std::find(wr.begin(), wr.end(), ns) != wr.end() && (kvs[k].nmeta || coll_writes[k])) {
+      R.disp = C_UNSUPPORTED;
+      return;
+    }
+  }
+  std::sort(wr.begin(), wr.end());
+  R.disp = C_VALID;
+  for (const std::string &ns : wr) {
+    auto it = ch.chaincodes.find(ns);
+    R.policies.push_back(it == ch.chaincodes.end() ? -1 : it->second);
+  }
+  // endorsement signature set (validator_keylevel.go:246-260)
+  R.ends.resize(cap.action.ends.size());
+  for (size_t k = 0; k < cap.action.ends.size(); k++) {
+    EndRec &e = R.ends[k];
+    e.endorser = cap.action.ends[k].endorser;
+    e.sig = cap.action.ends[k].signature;
+    e.ident = ch.lookup(e.endorser);
+  }
+}
+
+// ======================================================================= policy fold
+static bool eval_node(const Policy &P, int node, const std::vector<int> &ids, const Channel &ch,
+                      std::vector<uint8_t> &used) {
+  const PNode &N = P.nodes[node];
+  if (N.type == 2) {
+    const bool bad = P.principal_bad[N.principal];
+    const std::string &msp = P.principal_msp[N.principal];
+    for (size_t i = 0; i < ids.size(); i++) {
+      if (used[i]) continue;
+      const Ident &I = ch.idents[ids[i]];
+      if (!bad && I.mspid == msp && I.valid) {
+        used[i] = 1;
+        return true;
+      }
+    }
+    return false;
+  }
+  int32_t verified = 0;
+  std::vector<uint8_t> tmp(used.size());
+  for (int k : N.kids) {
+    tmp = used;
+    if (eval_node(P, k, ids, ch, tmp)) {
+      verified++;
+      used = tmp;
+    }
+  }
+  return verified >= N.n;
+}
+
+// ======================================================================= API
+int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
+                            const size_t *lens, const uint8_t *const *d_blocks, uint8_t *flags_out,
+                            size_t flags_cap, size_t *ntx_out) {
+  Channel &ch = S->ch;
+  // --- block envelopes
+  std::vector<std::vector<Span>> envs(nblocks);
+  size_t total = 0;
+  for (size_t b = 0; b < nblocks; b++) {
+    VBlock blk;
+    if (!pbw::decode(h_blocks[b], lens[b], blk)) return FGV_EINVAL;  // unparsable block
+    envs[b] = std::move(blk.data.data);
+    ntx_out[b] = envs[b].size();
+    total += envs[b].size();
+  }
+  if (total > flags_cap) return FGV_EINVAL;
+  std::vector<TxRec> &recs = S->recs;
+  recs.resize(total);
+  std::vector<size_t> base(nblocks + 1, 0);
+  for (size_t b = 0; b < nblocks; b++) base[b + 1] = base[b] + envs[b].size();
+  std::vector<std::pair<uint32_t, uint32_t>> where(total);
+  for (size_t b = 0; b < nblocks; b++)
+    for (size_t i = 0; i < envs[b].size(); i++) where[base[b] + i] = {(uint32_t)b, (uint32_t)i};
+
+  // --- A. parse
+  S->pool.parallel_for(total, [&](size_t t) {
+    parse_tx(ch, envs[where[t].first][where[t].second], recs[t]);
+  });
+
+  // --- assign GPU jobs (grouped by kind: lanes of a wave hash similar lengths)
+  auto dev_addr = [&](size_t b, const Span &s) -> uint64_t {
+    return (uint64_t)(uintptr_t)d_blocks[b] + (uint64_t)(s.p - h_blocks[b]);
+  };
+  std::vector<ShaJob> jobs;
+  std::vector<uint64_t> sig_ptr;
+  std::vector<uint32_t> sig_len, key_slot, dig_idx;
+  jobs.reserve(total * 5);
+  auto add_job = [&](size_t b, std::initializer_list<Span> spans) {
+    ShaJob j{};
+    int k = 0;
+    for (const Span &s : spans) {
+      j.p[k] = s.n ? dev_addr(b, s) : 0;
+      j.n[k] = s.n;
+      k++;
+    }
+    jobs.push_back(j);
+    return (uint32_t)(jobs.size() - 1);
+  };
+  for (size_t t = 0; t < total; t++) {  // creator payload hashes + creator verifies
+    TxRec &R = recs[t];
+    if (R.pre != C_PENDING) continue;
+    const size_t b = where[t].first;
+    R.cjob = add_job(b, {R.payload});
+    R.cvjob = (uint32_t)sig_ptr.size();
+    sig_ptr.push_back(dev_addr(b, R.env_sig));
+    sig_len.push_back(R.env_sig.n);
+    key_slot.push_back((uint32_t)ch.idents[R.creator_ident].key_slot);
+    dig_idx.push_back(R.cjob);
+  }
+  for (size_t t = 0; t < total; t++) {
+    TxRec &R = recs[t];
+    if (R.pre != C_PENDING || R.type != 3) continue;
+    R.txid_job = add_job(where[t].first, {R.nonce, R.creator});
+  }
+  for (size_t t = 0; t < total; t++) {
+    TxRec &R = recs[t];
+    if (R.pre != C_PENDING || R.type != 3 || R.etx != C_VALID) continue;
+    R.prop_job = add_job(where[t].first, {R.chdr, R.act_hdr, R.ccpp});
+  }
+  for (size_t t = 0; t < total; t++) {
+    TxRec &R = recs[t];
+    if (R.pre != C_PENDING || R.type != 3 || R.etx != C_VALID || R.disp != C_VALID) continue;
+    const size_t b = where[t].first;
+    for (EndRec &e : R.ends) {
+      if (e.ident < 0 || ch.idents[e.ident].key_slot < 0) continue;
+      uint32_t hj = add_job(b, {R.prp, e.endorser});
+      e.vjob = (uint32_t)sig_ptr.size();
+      sig_ptr.push_back(e.sig.n ? dev_addr(b, e.sig) : 0);
+      sig_len.push_back(e.sig.n);
+      key_slot.push_back((uint32_t)ch.idents[e.ident].key_slot);
+      dig_idx.push_back(hj);
+    }
+  }
+  for (size_t t = 0; t < total; t++) {  // computed txids for the index (rare)
+    TxRec &R = recs[t];
+    if (R.index_ok && R.index_txid.empty()) R.index_job = add_job(where[t].first, {R.idx_nonce, R.idx_creator});
+  }
+  // --- B. device
+  std::vector<uint8_t> digests, vstatus;
+  int rc = fgv_run_block_jobs(c, jobs, sig_ptr, sig_len, key_slot, dig_idx, digests, vstatus);
+  if (rc) return rc;
+
+  // --- C. fold (code precedence, validator.go:297-453)
+  static const char HEX[] = "0123456789abcdef";
+  std::atomic<bool> unsupported{false};
+  std::vector<uint8_t> codes(total, C_PENDING);
+  std::vector<std::string> fold_txid(total);
+  S->pool.parallel_for(total, [&](size_t t) {
+    TxRec &R = recs[t];
+    uint8_t code;
+    if (R.pre != C_PENDING) {
+      code = R.pre;
+    } else if (vstatus[R.cvjob] != 0) {
+      code = C_BAD_CREATOR;
+    } else if (R.type == 1) {
+      code = C_UNSUPPORTED;  // CONFIG transaction
+    } else if (R.type == 2) {
+      code = C_UNSUP_PAYLOAD;
+    } else {
+      // CheckTxID: hex(SHA-256(nonce||creator)) == chdr.TxId
+      const uint8_t *d = &digests[(size_t)R.txid_job * 32];
+      bool ok = R.txid.n == 64;
+      for (int k = 0; ok && k < 32; k++)
+        ok = R.txid.p[2 * k] == (uint8_t)HEX[d[k] >> 4] && R.txid.p[2 * k + 1] == (uint8_t)HEX[d[k] & 15];
+      if (!ok) {
+        code = C_BAD_TXID;
+      } else if (R.etx != C_VALID) {
+        code = R.etx;
+      } else if (R.prop_hash.n != 32 || memcmp(&digests[(size_t)R.prop_job * 32], R.prop_hash.p, 32) != 0) {
+        code = C_BAD_ETX;
+      } else if (ch.committed.count(R.txid.str())) {
+        code = C_DUP_TXID;  // checkTxIdDupsLedger (initial ledger; batch-earlier blocks below)
+      } else if (R.disp != C_VALID) {
+        code = R.disp;
+      } else {
+        // SignatureSetToValidIdentities (policy.go:363-395): dedup before verify
+        std::vector<int> ids;
+        std::vector<uint32_t> seen;
+        for (const EndRec &e : R.ends) {
+          if (e.ident < 0) continue;
+          const uint32_t canon = ch.idents[e.ident].canon;
+          if (std::find(seen.begin(), seen.end(), canon) != seen.end()) continue;
+          if (e.vjob == UINT32_MAX || vstatus[e.vjob] != 0) continue;
+          seen.push_back(canon);
+          ids.push_back(e.ident);
+        }
+        bool has25 = false, has10 = false;
+        for (int pi : R.policies) {
+          if (pi < 0) { has25 = true; continue; }
+          const Policy &P = ch.policies[pi];
+          if (P.unsupported) { code = C_UNSUPPORTED; goto done; }
+          bool ok2 = false;
+          if (P.decode_ok && P.compile_ok) {
+            std::vector<uint8_t> used(ids.size(), 0);
+            ok2 = eval_node(P, P.root, ids, ch, used);
+          }
+          if (!ok2) has10 = true;
+        }
+        if (has25 && has10) code = C_UNSUPPORTED;  // Go map order decides the reported code
+        else if (has25) code = C_INVALID_CC;
+        else if (has10) code = C_POLICY;
+        else code = C_VALID;
+      }
+    }
+  done:
+    if (code == C_UNSUPPORTED) unsupported = true;
+    codes[t] = code;
+    if (code == C_VALID) fold_txid[t] = R.txid.str();
+    // txid index entry for later blocks of this batch: chdr.TxId, or when empty
+    // ComputeTxID(nonce, creator) (protoutil/txutils.go:503-534)
+    if (R.index_ok && R.index_txid.empty() && R.index_job != UINT32_MAX) {
+      const uint8_t *d = &digests[(size_t)R.index_job * 32];
+      std::string h(64, '0');
+      for (int k = 0; k < 32; k++) {
+        h[2 * k] = HEX[d[k] >> 4];
+        h[2 * k + 1] = HEX[d[k] & 15];
+      }
+      R.index_txid = h;
+    }
+  });
+  if (unsupported) return FGV_EUNSUPPORTED;
+  // serial: ledger index across blocks of the batch + markTXIdDuplicates per block
+  std::unordered_set<std::string> batch_index;
+  for (size_t b = 0; b < nblocks; b++) {
+    std::unordered_set<std::string> seen;
+    for (size_t i = 0; i < envs[b].size(); i++) {
+      const size_t t = base[b] + i;
+      if (codes[t] == C_VALID && batch_index.count(fold_txid[t])) codes[t] = C_DUP_TXID;
+    }
+    for (size_t i = 0; i < envs[b].size(); i++) {
+      const size_t t = base[b] + i;
+      if (codes[t] != C_VALID) continue;
+      if (!seen.insert(fold_txid[t]).second) codes[t] = C_DUP_TXID;
+    }
+    for (size_t i = 0; i < envs[b].size(); i++) {
+      const TxRec &R = recs[base[b] + i];
+      if (R.index_ok && !R.index_txid.empty()) batch_index.insert(R.index_txid);
+    }
+  }
+  memcpy(flags_out, codes.data(), total);
+  return FGV_OK;
+}
+
+// ---- configuration entry points (called from fgv_host.cpp wrappers)
+int fgv_block_set_channel(fgv_block_state *S, const char *name) {
+  S->ch.name = name ? name : "";
+  return FGV_OK;
+}
+
+int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, int32_t key_slot, int valid,
+                           const uint8_t id_digest[32]) {
+  VSerializedIdentity sid;
+  if (!pbw::decode(ser, len, sid)) return FGV_EINVAL;
+  Ident I;
+  I.mspid = sid.mspid.str();
+  I.id_bytes = sid.id_bytes.str();
+  I.key_slot = key_slot;
+  I.valid = valid != 0;
+  std::string canon = I.mspid + std::string(reinterpret_cast<const char *>(id_digest), 32);
+  auto it = S->ch.canon_ids.find(canon);
+  if (it == S->ch.canon_ids.end()) it = S->ch.canon_ids.emplace(canon, (uint32_t)S->ch.canon_ids.size()).first;
+  I.canon = it->second;
+  uint64_t h = hash_bytes(sid.mspid.p, sid.mspid.n);
+  h = hash_bytes(sid.id_bytes.p, sid.id_bytes.n, h ^ 0xA5);
+  if (S->ch.lookup(Span{ser, (uint32_t)len}) >= 0) return FGV_OK;  // already registered
+  S->ch.idents.push_back(I);
+  S->ch.ident_index.emplace(h, (uint32_t)S->ch.idents.size() - 1);
+  return FGV_OK;
+}
+
+int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const uint8_t *policy, size_t len) {
+  auto it = S->ch.chaincodes.find(ns);
+  if (it == S->ch.chaincodes.end()) {
+    S->ch.policies.push_back(compile_policy(policy, len));
+    S->ch.chaincodes.emplace(ns, (int)S->ch.policies.size() - 1);
+  } else {
+    S->ch.policies[it->second] = compile_policy(policy, len);
+  }
+  return FGV_OK;
+}
+
+int fgv_block_add_txids(fgv_block_state *S, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
+                        size_t n) {
+  for (size_t i = 0; i < n; i++) S->ch.committed.insert(std::string(reinterpret_cast<const char *>(buf + off[i]), len[i]));
+  return FGV_OK;
+}

@@ -17,6 +17,7 @@
 
 #include "../../include/fgv.h"
 #include "fgv_der.h"
+#include "fgv_internal.h"
 #include "fgv_kernels.h"
 
 namespace {
@@ -94,7 +95,11 @@ struct fgv_ctx {
   DevBuf gtab, g_ok;
   DevBuf ktab, key_ok;
   uint32_t key_slots = 0;
+  uint32_t pinned = 0;  // slots [0, pinned) hold registered keys and are never evicted
   std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_map;
+  fgv_block_state *blk = nullptr;
+  DevBuf bj_jobs, bj_sigp, bj_sigl, bj_slot, bj_didx, bj_dig, bj_vst, blk_arena;
+  HostBuf hb_dig, hb_vst;
   // per-batch device buffers
   DevBuf kt_q, kt_slot, kt_scratch;
   DevBuf status, slot, r, s, dig, d1, d2, wscr, msg, moff, mlen;
@@ -152,6 +157,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   if (!c) return FGV_ENOMEM;
   c->device = cfg ? cfg->device : 0;
   c->key_slots = (cfg && cfg->key_slots) ? cfg->key_slots : 4096;
+  c->blk = fgv_block_state_new((cfg && cfg->host_threads) ? cfg->host_threads : 16);
   auto fail = [&](int e) {
     fgv_destroy(c);
     return e;
@@ -185,7 +191,11 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   DevBuf *d[] = {&c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->kt_q, &c->kt_slot, &c->kt_scratch,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->d2, &c->wscr, &c->msg,
-                 &c->moff, &c->mlen};
+                 &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
+                 &c->bj_dig, &c->bj_vst, &c->blk_arena};
+  if (c->blk) fgv_block_state_free(c->blk);
+  c->hb_dig.release();
+  c->hb_vst.release();
   for (auto *b : d) b->release();
   HostBuf *h[] = {&c->h_status, &c->h_slot, &c->h_r, &c->h_s, &c->h_dig, &c->h_kq, &c->h_kslot,
                   &c->h_moff, &c->h_mlen};
@@ -210,14 +220,15 @@ int fgv_last_timing(fgv_ctx *c, double *sha_ms, double *prep_ms, double *point_m
 
 // k_prep + k_point on device-resident SoA inputs (events ev[2..4] bracket them)
 static int launch_verify_stages(fgv_ctx *c, uint32_t N, uint8_t *d_status, const uint32_t *d_slot,
-                                const uint32_t *d_r, const uint32_t *d_s, const uint8_t *d_dig) {
+                                const uint32_t *d_r, const uint32_t *d_s, const uint8_t *d_dig,
+                                const uint32_t *d_dig_idx = nullptr) {
   if (!c->d1.ensure((size_t)NWIN * N) || !c->d2.ensure((size_t)NWIN * N)) return FGV_ENOMEM;
   uint32_t nl = (N + PREP_B - 1) / PREP_B;
   nl = (nl + 255) / 256 * 256;
   if (!c->wscr.ensure((size_t)PREP_B * 8 * nl * 4)) return FGV_ENOMEM;
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   hipLaunchKernelGGL(k_prep, dim3(nl / 256), dim3(256), 0, c->stream, N, d_status, d_slot,
-                     c->key_ok.as<uint8_t>(), d_r, d_s, d_dig, c->d1.as<int8_t>(), c->d2.as<int8_t>(),
+                     c->key_ok.as<uint8_t>(), d_r, d_s, d_dig, d_dig_idx, c->d1.as<int8_t>(), c->d2.as<int8_t>(),
                      c->wscr.as<uint32_t>());
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));
@@ -318,14 +329,17 @@ static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, 
           memcpy(k.data(), keys + 64 * i, 64);
           needed.emplace(k, 0);
         }
-      if (needed.size() > c->key_slots) return FGV_ENOMEM;
-      c->key_map.clear();
+      if (needed.size() + c->pinned > c->key_slots) return FGV_ENOMEM;
+      for (auto it = c->key_map.begin(); it != c->key_map.end();)
+        it = (it->second >= c->pinned) ? c->key_map.erase(it) : std::next(it);
+      for (auto it = needed.begin(); it != needed.end();)
+        it = c->key_map.count(it->first) ? needed.erase(it) : std::next(it);
       fresh = std::move(needed);
     }
     uint32_t nk = (uint32_t)fresh.size();
     if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kslot.ensure((size_t)nk * 4)) return FGV_ENOMEM;
     uint32_t *kq = c->h_kq.as<uint32_t>(), *ks = c->h_kslot.as<uint32_t>();
-    uint32_t j = 0, next = (uint32_t)c->key_map.size();
+    uint32_t j = 0, next = (uint32_t)c->key_map.size();  // == pinned + live ad-hoc keys
     for (auto &kv : fresh) {
       be32_to_limbs(kv.first.data(), kq + 16 * j);
       be32_to_limbs(kv.first.data() + 32, kq + 16 * j + 8);
@@ -444,13 +458,22 @@ int fgv_p256_verify_msgs(fgv_ctx *c, const uint8_t *keys, const uint8_t *msg_buf
 int fgv_keys_reset(fgv_ctx *c) {
   if (!c) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->pinned) return FGV_ESTATE;  // identities of the channel model hold slots
   c->key_map.clear();
   return FGV_OK;
 }
 
+static int keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots);
+
 int fgv_keys_register(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots) {
   if (!c || (n && (!keys || !slots))) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  return keys_register_locked(c, keys, n, slots);
+}
+
+// registered keys are pinned: ad-hoc (BCCSP-path) keys are dropped first so the pinned range
+// stays contiguous
+static int keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots) {
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
   std::vector<std::array<uint8_t, 64>> fresh;
   std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> seen;
@@ -461,13 +484,15 @@ int fgv_keys_register(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots
     seen.emplace(k, 0);
     fresh.push_back(k);
   }
-  if (c->key_map.size() + fresh.size() > c->key_slots) return FGV_ENOMEM;
+  if (c->pinned + fresh.size() > c->key_slots) return FGV_ENOMEM;
   c->t_keytab = 0;
   if (!fresh.empty()) {
+    for (auto it = c->key_map.begin(); it != c->key_map.end();)
+      it = (it->second >= c->pinned) ? c->key_map.erase(it) : std::next(it);
     const uint32_t nk = (uint32_t)fresh.size();
     if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kslot.ensure((size_t)nk * 4)) return FGV_ENOMEM;
     uint32_t *kq = c->h_kq.as<uint32_t>(), *ks = c->h_kslot.as<uint32_t>();
-    uint32_t next = (uint32_t)c->key_map.size();
+    uint32_t next = c->pinned;
     for (uint32_t j = 0; j < nk; j++) {
       be32_to_limbs(fresh[j].data(), kq + 16 * j);
       be32_to_limbs(fresh[j].data() + 32, kq + 16 * j + 8);
@@ -477,6 +502,7 @@ int fgv_keys_register(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (uint32_t j = 0; j < nk; j++) c->key_map.emplace(fresh[j], next + j);
+    c->pinned += nk;
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->ev[6], c->ev[7]) == hipSuccess) c->t_keytab = ms;
   }
@@ -515,6 +541,115 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *c, const uint8_t *d_msg_buf, const uint64_
   read_stage_times(c, true);
   c->t_keytab = 0;
   return FGV_OK;
+}
+
+}  // extern "C"
+
+// ======================================================================= block engine glue
+int fgv_run_block_jobs(fgv_ctx *c, const std::vector<ShaJob> &jobs, const std::vector<uint64_t> &sig_ptr,
+                       const std::vector<uint32_t> &sig_len, const std::vector<uint32_t> &key_slot,
+                       const std::vector<uint32_t> &dig_idx, std::vector<uint8_t> &digests,
+                       std::vector<uint8_t> &vstatus) {
+  const size_t nj = jobs.size(), nv = sig_ptr.size();
+  digests.assign(nj * 32, 0);
+  vstatus.assign(nv, 0);
+  if (nj == 0) return FGV_OK;
+  if (!c->bj_jobs.ensure(nj * sizeof(ShaJob)) || !c->bj_dig.ensure(nj * 32) || !c->hb_dig.ensure(nj * 32))
+    return FGV_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(c->bj_jobs.p, jobs.data(), nj * sizeof(ShaJob), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  hipLaunchKernelGGL(k_sha256_jobs, dim3((uint32_t)((nj + 255) / 256)), dim3(256), 0, c->stream,
+                     c->bj_jobs.as<ShaJob>(), (uint32_t)nj, c->bj_dig.as<uint8_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  bool ran = false;
+  if (nv) {
+    const uint32_t N = (uint32_t)nv;
+    if (!c->bj_sigp.ensure(nv * 8) || !c->bj_sigl.ensure(nv * 4) || !c->bj_slot.ensure(nv * 4) ||
+        !c->bj_didx.ensure(nv * 4) || !c->bj_vst.ensure(nv) || !c->r.ensure(nv * 32) || !c->s.ensure(nv * 32) ||
+        !c->hb_vst.ensure(nv))
+      return FGV_ENOMEM;
+    HIP_TRY(hipMemcpyAsync(c->bj_sigp.p, sig_ptr.data(), nv * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->bj_sigl.p, sig_len.data(), nv * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->bj_slot.p, key_slot.data(), nv * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->bj_didx.p, dig_idx.data(), nv * 4, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr,
+                       c->bj_sigp.as<uint64_t>(), c->bj_sigl.as<uint32_t>(), N, c->bj_vst.as<uint8_t>(),
+                       c->r.as<uint32_t>(), c->s.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    int rc = launch_verify_stages(c, N, c->bj_vst.as<uint8_t>(), c->bj_slot.as<uint32_t>(), c->r.as<uint32_t>(),
+                                  c->s.as<uint32_t>(), c->bj_dig.as<uint8_t>(), c->bj_didx.as<uint32_t>());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->hb_vst.p, c->bj_vst.p, nv, hipMemcpyDeviceToHost, c->stream));
+    ran = true;
+  }
+  HIP_TRY(hipMemcpyAsync(c->hb_dig.p, c->bj_dig.p, nj * 32, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  memcpy(digests.data(), c->hb_dig.p, nj * 32);
+  if (nv) memcpy(vstatus.data(), c->hb_vst.p, nv);
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->t_sha = ms;
+  read_stage_times(c, ran);
+  return FGV_OK;
+}
+
+extern "C" {
+
+int fgv_channel_init(fgv_ctx *c, const char *name) {
+  if (!c || !name) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_set_channel(c->blk, name);
+}
+
+int fgv_msp_add_identity(fgv_ctx *c, const uint8_t *serialized, size_t len, const uint8_t *pubkey, int valid,
+                         const uint8_t *id_digest) {
+  if (!c || !serialized || !id_digest) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  int32_t slot = -1;
+  if (pubkey) {
+    uint32_t s;
+    int rc = keys_register_locked(c, pubkey, 1, &s);
+    if (rc) return rc;
+    slot = (int32_t)s;
+  }
+  return fgv_block_add_identity(c->blk, serialized, len, slot, valid, id_digest);
+}
+
+int fgv_chaincode_define(fgv_ctx *c, const char *ns, const uint8_t *policy, size_t len) {
+  if (!c || !ns || (len && !policy)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_define_chaincode(c->blk, ns, policy, len);
+}
+
+int fgv_ledger_add_txids(fgv_ctx *c, const uint8_t *buf, const uint64_t *off, const uint32_t *len, size_t n) {
+  if (!c || (n && (!buf || !off || !len))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_add_txids(c->blk, buf, off, len, n);
+}
+
+int fgv_validate_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                        const uint8_t *const *d_blocks, uint8_t *flags, size_t flags_cap, size_t *ntx) {
+  if (!c || (nblocks && (!blocks || !lens || !flags || !ntx))) return FGV_EINVAL;
+  if (nblocks == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  std::vector<const uint8_t *> dev(nblocks);
+  if (d_blocks) {
+    for (size_t b = 0; b < nblocks; b++) dev[b] = d_blocks[b];
+  } else {
+    // stage the blocks into one device arena (64 B padding after each block)
+    size_t total = 0;
+    for (size_t b = 0; b < nblocks; b++) total += (lens[b] + 64 + 255) & ~(size_t)255;
+    if (!c->blk_arena.ensure(total)) return FGV_ENOMEM;
+    size_t o = 0;
+    for (size_t b = 0; b < nblocks; b++) {
+      HIP_TRY(hipMemcpyAsync(c->blk_arena.as<uint8_t>() + o, blocks[b], lens[b], hipMemcpyHostToDevice, c->stream));
+      dev[b] = c->blk_arena.as<uint8_t>() + o;
+      o += (lens[b] + 64 + 255) & ~(size_t)255;
+    }
+  }
+  return fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), flags, flags_cap, ntx);
 }
 
 }  // extern "C"

@@ -28,10 +28,16 @@ __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw 
                          jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys);
 __global__ void k_prep(uint32_t n, uint8_t *status, const uint32_t *key_slot, const uint8_t *key_ok,
                        const uint32_t *r_limbs, const uint32_t *s_limbs, const uint8_t *digests,
-                       int8_t *d1, int8_t *d2, uint32_t *w_scratch);
+                       const uint32_t *dig_idx, int8_t *d1, int8_t *d2, uint32_t *w_scratch);
 __global__ void k_point(uint32_t n, uint8_t *status, const uint32_t *key_slot, const apoint_raw *gtab,
                         const apoint_raw *ktab, const int8_t *d1, const int8_t *d2,
                         const uint32_t *r_limbs);
+struct ShaJob {  // message = span0 || span1 || span2 (absolute device addresses)
+  uint64_t p[3];
+  uint32_t n[3];
+  uint32_t pad;
+};
+__global__ void k_sha256_jobs(const ShaJob *jobs, uint32_t n, uint8_t *out);
 __global__ void k_sha256(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint32_t n,
                          uint8_t *out);
 __global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_t *len, uint32_t n,

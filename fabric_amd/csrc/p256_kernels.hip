@@ -160,7 +160,8 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
 // ---------------------------------------------------------------- k_prep
 // Items are processed in PREP_B strided rounds per lane: item = lane + b * nlanes.
 // in:  status (0xFF = pending; host pre-decided otherwise), key slot, r/s as plain
-//      little-endian limbs [8][n] (limb-major), digests [n][32] big-endian bytes.
+//      little-endian limbs [8][n] (limb-major), digests [*][32] big-endian bytes, item i
+//      using digest dig_idx[i] (or i when dig_idx is null).
 // out: status (4/5 decided here), digits d1/d2 [NWIN][n] int8.
 __global__ __launch_bounds__(256) void k_prep(uint32_t n, uint8_t *__restrict__ status,
                                               const uint32_t *__restrict__ key_slot,
@@ -168,6 +169,7 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, uint8_t *__restrict__ 
                                               const uint32_t *__restrict__ r_limbs,
                                               const uint32_t *__restrict__ s_limbs,
                                               const uint8_t *__restrict__ digests,
+                                              const uint32_t *__restrict__ dig_idx,
                                               int8_t *__restrict__ d1, int8_t *__restrict__ d2,
                                               uint32_t *__restrict__ w_scratch) {
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
@@ -235,7 +237,8 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, uint8_t *__restrict__ 
     sn_mul(sm, s, r2n);
     sn_mul(inv, inv, sm);
     // e = leftmost 256 bits of the digest, mod n (digest is exactly 32 bytes)
-    const uint32_t *dg = reinterpret_cast<const uint32_t *>(digests + (size_t)i * 32);
+    const uint32_t di = dig_idx ? dig_idx[i] : i;
+    const uint32_t *dg = reinterpret_cast<const uint32_t *>(digests + (size_t)di * 32);
 #pragma unroll
     for (int k = 0; k < 8; k++) e[k] = __builtin_bswap32(dg[7 - k]);
     if (!lt_n(e)) {

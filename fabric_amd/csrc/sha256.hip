@@ -101,3 +101,76 @@ __global__ __launch_bounds__(256) void k_sha256(const uint8_t *__restrict__ buf,
 #pragma unroll
   for (int j = 0; j < 8; j++) o[j] = __builtin_bswap32(h[j]);
 }
+
+// ---------------------------------------------------------------------------------
+// k_sha256_jobs: messages that are the concatenation of up to 3 spans, each given by an
+// absolute device address (spans point straight into block bytes resident in HBM):
+//   creator payload (1 span), nonce||creator (TxID, protoutil/proputils.go:351-360),
+//   chdr||shdr||ccpp (proposal hash, protoutil/txutils.go:449-466),
+//   prp||endorser (endorsement message, statebased/validator_keylevel.go:246-260).
+// 64-byte blocks lying inside one span use the aligned dword path; blocks that straddle a
+// span boundary or hold the padding are assembled byte by byte.
+__device__ __forceinline__ uint32_t job_byte(const ShaJob &j, uint32_t q) {
+  if (q < j.n[0]) return reinterpret_cast<const uint8_t *>(j.p[0])[q];
+  q -= j.n[0];
+  if (q < j.n[1]) return reinterpret_cast<const uint8_t *>(j.p[1])[q];
+  q -= j.n[1];
+  return reinterpret_cast<const uint8_t *>(j.p[2])[q];
+}
+
+__global__ __launch_bounds__(256) void k_sha256_jobs(const ShaJob *__restrict__ jobs, uint32_t n,
+                                                     uint8_t *__restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ShaJob j = jobs[i];
+  const uint32_t L = j.n[0] + j.n[1] + j.n[2];
+  const uint32_t nblk = (L + 8) / 64 + 1;
+  const uint64_t bits = (uint64_t)L * 8;
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint32_t w[16];
+  uint32_t cum0 = j.n[0], cum1 = j.n[0] + j.n[1];
+#pragma unroll 1
+  for (uint32_t blk = 0; blk < nblk; blk++) {
+    const uint32_t s = blk * 64, e = s + 64;
+    int span = -1;
+    uint32_t base = 0;
+    if (e <= cum0) { span = 0; base = 0; }
+    else if (s >= cum0 && e <= cum1) { span = 1; base = cum0; }
+    else if (s >= cum1 && e <= L) { span = 2; base = cum1; }
+    if (span >= 0) {
+      const uint8_t *msg = reinterpret_cast<const uint8_t *>(j.p[span]) + (s - base);
+      const uintptr_t a = reinterpret_cast<uintptr_t>(msg);
+      const uint32_t *al = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(a & 3);
+      uint32_t cur = al[0];
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        uint32_t nxt = (sh || k < 15) ? al[k + 1] : 0u;  // aligned & last word: no over-read
+        uint32_t v = sh ? __builtin_amdgcn_alignbyte(nxt, cur, sh) : cur;
+        w[k] = __builtin_bswap32(v);
+        cur = nxt;
+      }
+    } else {
+#pragma unroll 1
+      for (int k = 0; k < 16; k++) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t pos = s + k * 4 + q;
+          const uint32_t byte = pos < L ? job_byte(j, pos) : (pos == L ? 0x80u : 0u);
+          word = (word << 8) | byte;
+        }
+        w[k] = word;
+      }
+      if (blk == nblk - 1) {
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+      }
+    }
+    sha_compress(h, w);
+  }
+  uint32_t *o = reinterpret_cast<uint32_t *>(out + (size_t)i * 32);
+#pragma unroll
+  for (int k = 0; k < 8; k++) o[k] = __builtin_bswap32(h[k]);
+}

@@ -1,0 +1,315 @@
+"""Synthetic Fabric blocks (BASELINE configs C2 / C5 shapes).
+
+A Network holds the MSPs (one CA per org, one endorsing peer per org, a pool of client
+identities), the channel name and the chaincode definitions (ValidationInfo: plugin "vscc"
++ ApplicationPolicy bytes).  make_block() builds a common.Block of endorser transactions
+exactly as a Fabric client/peer would (protoutil CreateSignedTx shape): every signature is an
+OpenSSL ECDSA-P256 low-S signature over SHA-256 of the bytes Fabric signs.
+
+Each transaction carries the generator's LABEL -- the validation code the injected fault must
+produce in the reference (a generation-time fact, independent of the oracle):
+  clean -> 0, bad creator sig -> 4, one bad endorsement of 3 -> 0, policy unsatisfied -> 10,
+  duplicate txid -> 9, bad txid -> 8, bad proposal hash -> 5, epoch != 0 -> 3,
+  unknown chaincode -> 25, two actions -> 5, unknown creator MSP -> 4, high-S creator -> 4,
+  events with other chaincode id -> 255, corrupt envelope bytes -> None (oracle decides).
+
+Wire encoding is hand-rolled proto3 (field numbers: SURVEY.md Appendix B, checked against
+vendor/github.com/hyperledger/fabric-protos-go).
+"""
+import hashlib
+import random
+
+from . import Key, make_cert, sign_batch
+
+# ------------------------------------------------------------------ proto3 encoding
+
+
+def _varint(v: int) -> bytes:
+    v &= (1 << 64) - 1
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def f_bytes(num: int, b: bytes) -> bytes:
+    """length-delimited field; proto3 omits empty bytes/strings/messages-by-bytes"""
+    if not b:
+        return b""
+    return _varint(num << 3 | 2) + _varint(len(b)) + b
+
+
+def f_msg(num: int, b: bytes) -> bytes:
+    """embedded message: present even when empty"""
+    return _varint(num << 3 | 2) + _varint(len(b)) + b
+
+
+def f_str(num: int, s: str) -> bytes:
+    return f_bytes(num, s.encode())
+
+
+def f_varint(num: int, v: int) -> bytes:
+    if v == 0:
+        return b""
+    return _varint(num << 3) + _varint(v)
+
+
+# ------------------------------------------------------------------ messages
+
+def serialized_identity(mspid: str, pem: bytes) -> bytes:
+    return f_str(1, mspid) + f_bytes(2, pem)
+
+
+def msp_role_principal(mspid: str, role: int = 0) -> bytes:
+    role_bytes = f_str(1, mspid) + f_varint(2, role)
+    return f_varint(1, 0) + f_bytes(2, role_bytes)  # classification ROLE = 0
+
+
+def signed_by(i: int) -> bytes:
+    return _varint(1 << 3) + _varint(i)  # oneof: encoded even when 0
+
+
+def n_out_of(n: int, rules) -> bytes:
+    return f_msg(2, f_varint(1, n) + b"".join(f_msg(2, r) for r in rules))
+
+
+def out_of_policy(n: int, mspids) -> bytes:
+    """ApplicationPolicy{signature_policy: OutOf(n, [m.member for m in mspids])}
+    (common/policydsl/policydsl_builder.go SignedByNOutOfGivenRole shape)."""
+    spe = f_varint(1, 0) + f_msg(2, n_out_of(n, [signed_by(i) for i in range(len(mspids))])) + \
+        b"".join(f_msg(3, msp_role_principal(m)) for m in mspids)
+    return f_msg(1, spe)
+
+
+def kv_rwset(reads, writes) -> bytes:
+    out = b""
+    for k, ver in reads:
+        v = b"" if ver is None else f_msg(2, f_varint(1, ver[0]) + f_varint(2, ver[1]))
+        out += f_msg(1, f_str(1, k) + v)
+    for k, val, is_del in writes:
+        out += f_msg(3, f_str(1, k) + f_varint(2, 1 if is_del else 0) + f_bytes(3, val))
+    return out
+
+
+def tx_rwset(ns_sets) -> bytes:
+    """TxReadWriteSet{data_model KV, ns_rwset: [(ns, kvrwset_bytes)]}"""
+    return b"".join(f_msg(2, f_str(1, ns) + f_bytes(2, rw)) for ns, rw in ns_sets)
+
+
+def chaincode_id(name: str, version: str = "") -> bytes:
+    return f_str(2, name) + f_str(3, version)
+
+
+# ------------------------------------------------------------------ network
+
+class Identity:
+    def __init__(self, key: Key, mspid: str, pem: bytes, role: str):
+        self.key, self.mspid, self.pem, self.role = key, mspid, pem, role
+        self.serialized = serialized_identity(mspid, pem)
+        der = _pem_to_der(pem)
+        self.id_digest = hashlib.sha256(der).digest()  # identity Id = hex(SHA-256(cert.Raw))
+
+
+def _pem_to_der(pem: bytes) -> bytes:
+    import base64
+    body = pem.split(b"-----BEGIN CERTIFICATE-----")[1].split(b"-----END CERTIFICATE-----")[0]
+    return base64.b64decode(b"".join(body.split()))
+
+
+class Network:
+    """orgs: number of MSPs; clients: client identities (spread over the orgs)."""
+
+    def __init__(self, seed=3, orgs=3, clients=100, channel="testchannel", policy_n=2):
+        self.seed, self.channel = seed, channel
+        self.mspids = [f"Org{i + 1}MSP" for i in range(orgs)]
+        self.cas, self.peers, self.clients = [], [], []
+        for o, m in enumerate(self.mspids):
+            ca = Key(seed, 10_000 + o)
+            self.cas.append(ca)
+            pk = Key(seed, 20_000 + o)
+            pem = make_cert(pk, ca, f"peer0.org{o + 1}", m, f"ca.org{o + 1}", False, 100 + o)
+            self.peers.append(Identity(pk, m, pem, "peer"))
+        for c in range(clients):
+            o = c % orgs
+            ck = Key(seed, 30_000 + c)
+            pem = make_cert(ck, self.cas[o], f"user{c}.org{o + 1}", self.mspids[o], f"ca.org{o + 1}", False,
+                            1000 + c)
+            self.clients.append(Identity(ck, self.mspids[o], pem, "client"))
+        # an identity from an MSP the channel does not know (deserialization fails)
+        rk = Key(seed, 40_000)
+        rogue_ca = Key(seed, 40_001)
+        self.rogue = Identity(rk, "RogueMSP", make_cert(rk, rogue_ca, "rogue", "RogueMSP", "ca.rogue", False, 7),
+                              "client")
+        # an identity claiming Org1MSP but with a cert from a foreign CA: deserializes (known
+        # MSP) but fails Validate (not issued by Org1's CA)
+        fk = Key(seed, 40_002)
+        self.forged = Identity(fk, self.mspids[0], make_cert(fk, rogue_ca, "forged", self.mspids[0], "ca.rogue",
+                                                             False, 8), "peer")
+        self.chaincodes = {"mycc": out_of_policy(policy_n, self.mspids)}
+
+    def identities(self):
+        """What the MSP layer knows: (serialized, mspid, pubkey64, valid, id_digest).
+        RogueMSP is unknown to the channel, so it is NOT listed (deserialize error)."""
+        out = []
+        for ident in self.peers + self.clients:
+            out.append((ident.serialized, ident.mspid, ident.key.pub, True, ident.id_digest))
+        out.append((self.forged.serialized, self.forged.mspid, self.forged.key.pub, False, self.forged.id_digest))
+        return out
+
+
+# ------------------------------------------------------------------ blocks
+
+FAULTS_C2 = (("bad_creator_sig", 0.02), ("one_bad_endorsement", 0.02), ("policy_unsatisfied", 0.02),
+             ("dup_txid", 0.005))
+EXPECTED = {"clean": 0, "bad_creator_sig": 4, "one_bad_endorsement": 0, "policy_unsatisfied": 10,
+            "dup_txid": 9, "bad_txid": 8, "bad_proposal_hash": 5, "bad_epoch": 3, "unknown_cc": 25,
+            "two_actions": 5, "rogue_creator": 4, "high_s_creator": 4, "dup_endorser": 10,
+            "forged_endorser": 10, "event_other_cc": 255, "bad_payload": 2, "no_sig": 4,
+            "corrupt": None}
+
+
+class _Tx:
+    pass
+
+
+def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FAULTS_C2, endorse_dist=((2, 0.6), (3, 0.4)),
+               reads=4, writes=4, value_len=200, threads=8, prev_hash=b"\x00" * 32, force=None, ns="mycc",
+               key_space=1_000_000):
+    """Returns (block_bytes, labels list, envelopes list)."""
+    rng = random.Random((net.seed << 20) ^ (number << 4) ^ seed)
+    txs = []
+    fault_names = [f for f, _ in faults]
+    cum = []
+    acc = 0.0
+    for _, p in faults:
+        acc += p
+        cum.append(acc)
+    for i in range(ntx):
+        t = _Tx()
+        u = rng.random()
+        t.label = "clean"
+        for name, c in zip(fault_names, cum):
+            if u < c:
+                t.label = name
+                break
+        if force is not None and force[i] is not None:
+            t.label = force[i]
+        t.creator = net.rogue if t.label == "rogue_creator" else rng.choice(net.clients)
+        t.nonce = bytes(rng.getrandbits(8) for _ in range(24))
+        if t.label == "dup_txid" and i > 0:
+            clean = [x for x in txs if x.label == "clean"]
+            if clean:
+                src = clean[rng.randrange(len(clean))]
+                t.creator, t.nonce = src.creator, src.nonce
+            else:
+                t.label = "clean"
+        r = rng.random()
+        ne, accp = endorse_dist[-1][0], 0.0
+        for e, p in endorse_dist:
+            accp += p
+            if r < accp:
+                ne = e
+                break
+        orgs = rng.sample(range(len(net.peers)), min(ne, len(net.peers)))
+        t.endorsers = [net.peers[o] for o in orgs]
+        if t.label == "policy_unsatisfied":
+            t.endorsers = t.endorsers[:1]
+        if t.label == "dup_endorser":
+            t.endorsers = [t.endorsers[0], t.endorsers[0]]
+        if t.label == "forged_endorser":
+            t.endorsers = [t.endorsers[0], net.forged]
+        if t.label == "one_bad_endorsement" and len(t.endorsers) < 3:
+            orgs = rng.sample(range(len(net.peers)), 3)
+            t.endorsers = [net.peers[o] for o in orgs]
+        t.bad_endorsement = rng.randrange(len(t.endorsers)) if t.label == "one_bad_endorsement" else -1
+        t.reads = [(f"k{rng.randrange(key_space):07d}", (rng.randrange(1, 1000), rng.randrange(500)))
+                   for _ in range(reads)]
+        t.writes = [(f"k{rng.randrange(key_space):07d}", bytes(rng.getrandbits(8) for _ in range(value_len)), False)
+                    for _ in range(writes)]
+        t.ccpp = f_bytes(1, bytes(rng.getrandbits(8) for _ in range(128)))  # ChaincodeProposalPayload{input}
+        t.ts = (1_700_000_000 + number * 1000 + i, rng.randrange(10 ** 9))
+        txs.append(t)
+
+    # pass 1: headers, proposal response payloads, endorsement digests
+    e_privs, e_digests, e_refs = [], [], []
+    for t in txs:
+        txid = hashlib.sha256(t.nonce + t.creator.serialized).hexdigest()
+        if t.label == "bad_txid":
+            txid = txid[:-1] + ("0" if txid[-1] != "0" else "1")
+        ccname = "othercc" if t.label == "unknown_cc" else ns
+        ext = f_msg(2, chaincode_id(ccname))  # ChaincodeHeaderExtension{chaincode_id}
+        ts = f_msg(3, f_varint(1, t.ts[0]) + f_varint(2, t.ts[1]))
+        t.chdr = f_varint(1, 3) + ts + f_str(4, net.channel) + f_str(5, txid) + \
+            f_varint(6, 1 if t.label == "bad_epoch" else 0) + f_bytes(7, ext)
+        t.shdr = f_bytes(1, t.creator.serialized) + f_bytes(2, t.nonce)
+        ph = hashlib.sha256(t.chdr + t.shdr + t.ccpp).digest()
+        if t.label == "bad_proposal_hash":
+            ph = bytes([ph[0] ^ 1]) + ph[1:]
+        rw = tx_rwset([(ccname, kv_rwset(t.reads, t.writes))])
+        events = b""
+        if t.label == "event_other_cc":
+            events = f_str(1, "someothercc") + f_str(3, "ev")
+        cca = f_bytes(1, rw) + f_bytes(2, events) + f_msg(3, f_varint(1, 200)) + f_msg(4, chaincode_id(ccname, "1.0"))
+        t.prp = f_bytes(1, ph) + f_bytes(2, cca)
+        for j, e in enumerate(t.endorsers):
+            e_privs.append(e.key.priv)
+            e_digests.append(hashlib.sha256(t.prp + e.serialized).digest())
+            e_refs.append((t, j))
+    esigs = sign_batch(b"".join(e_privs), b"".join(e_digests), len(e_privs), threads=threads) if e_privs else []
+    for t in txs:
+        t.esigs = [None] * len(t.endorsers)
+    for (t, j), s in zip(e_refs, esigs):
+        if j == t.bad_endorsement:
+            s = s[:10] + bytes([s[10] ^ 0x55]) + s[11:]
+        t.esigs[j] = s
+
+    # pass 2: assemble payloads; creator signatures
+    c_privs, c_digests = [], []
+    for t in txs:
+        ends = b"".join(f_msg(2, f_bytes(1, e.serialized) + f_bytes(2, s)) for e, s in zip(t.endorsers, t.esigs))
+        cea = f_bytes(1, t.prp) + ends
+        cap = f_bytes(1, t.ccpp) + f_msg(2, cea)
+        action = f_msg(1, f_bytes(1, t.shdr) + f_bytes(2, cap))
+        if t.label == "two_actions":
+            action = action + action
+        hdr = f_bytes(1, t.chdr) + f_bytes(2, t.shdr)
+        t.payload = f_msg(1, hdr) + f_bytes(2, action)
+        if t.label == "bad_payload":
+            t.payload = t.payload[:-3]  # truncated -> Payload unmarshal error
+        c_privs.append(t.creator.key.priv)
+        c_digests.append(hashlib.sha256(t.payload).digest())
+    csigs = sign_batch(b"".join(c_privs), b"".join(c_digests), len(c_privs), threads=threads,
+                       high_s=False) if c_privs else []
+    envs = []
+    for t, s in zip(txs, csigs):
+        if t.label == "bad_creator_sig":
+            s = s[:12] + bytes([s[12] ^ 0x21]) + s[13:]
+        if t.label == "high_s_creator":
+            from .workloads import _der_int, _der_rs, N
+            r_, s_ = _der_rs(s)
+            body = _der_int(r_) + _der_int(N - s_)
+            s = b"\x30" + bytes([len(body)]) + body
+        if t.label == "no_sig":
+            s = b""
+        env = f_bytes(1, t.payload) + f_bytes(2, s)
+        if t.label == "corrupt":
+            b = bytearray(env)
+            for _ in range(3):
+                b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+            env = bytes(b)
+        envs.append(env)
+    labels = [t.label for t in txs]
+    data_hash = hashlib.sha256(b"".join(envs)).digest()
+    header = f_varint(1, number) + f_bytes(2, prev_hash) + f_bytes(3, data_hash)
+    data = b"".join(f_msg(1, e) for e in envs) if envs else b""
+    metadata = b"".join(f_msg(1, b"") for _ in range(5))
+    block = f_msg(1, header) + f_msg(2, data) + f_msg(3, metadata)
+    return block, labels, envs
+
+
+def expected_codes(labels):
+    """Generator-side expectation (None where the fault's effect is left to the oracle).
+    dup_txid: the later VALID duplicate gets 9 (validator.go:279-295)."""
+    return [EXPECTED[l] for l in labels]

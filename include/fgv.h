@@ -23,6 +23,10 @@ extern "C" {
 #define FGV_ENOMEM (-3)   /* device or host allocation failed                  */
 #define FGV_ECOMM (-4)    /* RCCL / torch.distributed exchange failed          */
 #define FGV_ESTATE (-5)   /* call out of order (e.g. not initialised)         */
+#define FGV_EUNSUPPORTED (-6) /* block holds something outside the engine's model
+                                 (config tx, key-level/collection endorsement policy,
+                                 channel-reference policy, NodeOU roles, ...): validate it
+                                 with the reference code instead                         */
 
 /* ------------------------------------------------- per-signature status bytes
  * Only FGV_SIG_VALID means "valid"; the reference maps every other outcome to an
@@ -93,6 +97,38 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *ctx, const uint8_t *d_msg_buf, const uint6
                              const uint32_t *d_msg_len, const uint8_t *d_sig_buf,
                              const uint64_t *d_sig_off, const uint32_t *d_sig_len,
                              const uint32_t *d_key_slot, size_t n, uint8_t *d_status);
+
+/* ------------------------------------------------------------ committer: whole blocks */
+
+/* Channel model the block validator runs against (what the peer's channel resources give
+ * the reference validator):
+ *   fgv_channel_init      -- channel name (chdr.ChannelId of valid txs; validator.go:155-158)
+ *   fgv_msp_add_identity  -- one MSP identity, keyed by its exact SerializedIdentity
+ *                            (mspid, id_bytes) pair (msp/mspmgrimpl.go:75-100): P-256 public
+ *                            key X||Y (NULL if the key is not P-256 -> Verify always fails),
+ *                            Validate() result, and SHA-256 of the certificate (identity Id,
+ *                            used for de-duplication, common/policies/policy.go:375).
+ *                            The Go shim adds identities as its MSP cache deserializes them.
+ *   fgv_chaincode_define  -- ValidationInfo of a namespace: ApplicationPolicy bytes
+ *                            (plugin "vscc"; dispatcher.go:237-275)
+ *   fgv_ledger_add_txids  -- txids already in the block store (TxIDExists, kv_ledger.go:496) */
+int fgv_channel_init(fgv_ctx *ctx, const char *channel_name);
+int fgv_msp_add_identity(fgv_ctx *ctx, const uint8_t *serialized, size_t len, const uint8_t *pubkey64,
+                         int valid, const uint8_t *id_digest32);
+int fgv_chaincode_define(fgv_ctx *ctx, const char *ns, const uint8_t *policy, size_t len);
+int fgv_ledger_add_txids(fgv_ctx *ctx, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
+                         size_t n);
+
+/* TxValidator.Validate (core/committer/txvalidator/v20/validator.go:180-265) for `nblocks`
+ * consecutive blocks (marshalled common.Block).  Writes one TxValidationCode byte per
+ * transaction (blocks concatenated) into `flags` -- the TRANSACTIONS_FILTER metadata -- and
+ * the transaction count of each block into ntx[b].  Block b sees the txids of blocks < b as
+ * committed.  d_blocks: optional device copies of the same bytes (each readable 64 bytes
+ * past its end); NULL -> the library uploads them.  Returns FGV_EUNSUPPORTED when a block
+ * needs logic outside the engine's model (the caller validates that batch itself). */
+int fgv_validate_blocks(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
+                        const size_t *lens, const uint8_t *const *d_blocks, uint8_t *flags,
+                        size_t flags_cap, size_t *ntx);
 
 #ifdef __cplusplus
 }
