@@ -43,9 +43,17 @@ _L = None
 
 
 def load():
-    """Load libfgv.so (no GPU needed just to load and resolve symbols)."""
+    """Load libfgv.so (no GPU needed just to load and resolve symbols).
+
+    torch (when installed) ships its own libamdhip64.so.7; libfgv.so links the same soname.
+    Import torch first so the process holds ONE HIP runtime whichever module a caller
+    touches first (a second copy makes torch report "No HIP GPUs are available")."""
     global _L
     if _L is None:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise FgvError(f"{LIB_PATH} not built -- run `make` (or __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)

@@ -167,7 +167,7 @@ EXPECTED = {"clean": 0, "bad_creator_sig": 4, "one_bad_endorsement": 0, "policy_
             "dup_txid": 9, "bad_txid": 8, "bad_proposal_hash": 5, "bad_epoch": 3, "unknown_cc": 25,
             "two_actions": 5, "rogue_creator": 4, "high_s_creator": 4, "dup_endorser": 10,
             "forged_endorser": 10, "event_other_cc": 255, "bad_payload": 2, "no_sig": 4,
-            "corrupt": None}
+            "corrupt": None, "dup_txid_prev": 9}
 
 
 class _Tx:
@@ -176,8 +176,10 @@ class _Tx:
 
 def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FAULTS_C2, endorse_dist=((2, 0.6), (3, 0.4)),
                reads=4, writes=4, value_len=200, threads=8, prev_hash=b"\x00" * 32, force=None, ns="mycc",
-               key_space=1_000_000):
-    """Returns (block_bytes, labels list, envelopes list)."""
+               key_space=1_000_000, reuse=None, out_txs=None):
+    """Returns (block_bytes, labels list, envelopes list).
+    reuse: {tx index: (creator Identity, nonce)} -> that tx re-uses an earlier txid (label
+    'dup_txid_prev'); out_txs: list that receives the generated tx objects."""
     rng = random.Random((net.seed << 20) ^ (number << 4) ^ seed)
     txs = []
     fault_names = [f for f, _ in faults]
@@ -198,6 +200,9 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
             t.label = force[i]
         t.creator = net.rogue if t.label == "rogue_creator" else rng.choice(net.clients)
         t.nonce = bytes(rng.getrandbits(8) for _ in range(24))
+        if reuse and i in reuse:
+            t.creator, t.nonce = reuse[i]
+            t.label = "dup_txid_prev"
         if t.label == "dup_txid" and i > 0:
             clean = [x for x in txs if x.label == "clean"]
             if clean:
@@ -301,6 +306,8 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
             env = bytes(b)
         envs.append(env)
     labels = [t.label for t in txs]
+    if out_txs is not None:
+        out_txs.extend(txs)
     data_hash = hashlib.sha256(b"".join(envs)).digest()
     header = f_varint(1, number) + f_bytes(2, prev_hash) + f_bytes(3, data_hash)
     data = b"".join(f_msg(1, e) for e in envs) if envs else b""

@@ -1,0 +1,112 @@
+"""GPU parity of whole-block validation: TxValidationFlags from libfgv (HIP engine) must be
+bit-identical to the oracle's restated v20 committer on the same blocks."""
+import numpy as np
+import pytest
+
+from fabric_amd import _lib, txvalidator
+from fabric_amd.synth import blocks
+from oracle import v20
+from tests.blockfix import SPECIAL, block_from_envs, corrupt_envelopes, network
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine_for(net, committed=()):
+    eng = _lib.Engine(0)
+    txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes, committed)
+    return eng
+
+
+def _oracle(net, blks, committed=()):
+    m = v20.ChannelModel(net.channel, net.identities(), net.chaincodes, committed)
+    return v20.validate_blocks(m, blks)
+
+
+def _check(eng, net, blks, committed=()):
+    got = eng.validate_blocks(blks)
+    exp = _oracle(net, blks, committed)
+    for b, (g, e) in enumerate(zip(got, exp)):
+        mism = [(i, int(g[i]), e[i]) for i in range(len(e)) if g[i] != e[i]]
+        assert len(g) == len(e) and not mism, (b, mism[:10])
+    return exp
+
+
+def test_c2_blocks_and_fault_classes():
+    net = network()
+    eng = _engine_for(net)
+    blks = [blocks.make_block(net, 500, number=1 + i, seed=i)[0] for i in range(2)]
+    blks.append(blocks.make_block(net, len(SPECIAL), number=3, seed=3, faults=(), force=SPECIAL)[0])
+    exp = _check(eng, net, blks)
+    assert exp[2] == blocks.expected_codes(blocks.make_block(net, len(SPECIAL), number=3, seed=3, faults=(),
+                                                              force=SPECIAL)[1])
+    eng.close()
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_corruption_fuzz(seed):
+    """Mutated envelopes exercise every protobuf rule and code-precedence branch."""
+    net = network()
+    eng = _engine_for(net)
+    _, _, envs = blocks.make_block(net, 60, number=1, seed=seed)
+    bad = corrupt_envelopes(envs, seed, 300)
+    _check(eng, net, [block_from_envs(envs + bad, number=2)])
+    eng.close()
+
+
+def test_multi_block_txid_index_and_ledger():
+    net = network()
+    txs = []
+    b1, _, envs1 = blocks.make_block(net, 20, number=1, seed=21, faults=(), out_txs=txs)
+    b2, _, _ = blocks.make_block(net, 20, number=2, seed=22, faults=(), reuse={5: (txs[7].creator, txs[7].nonce),
+                                                                                 9: (txs[7].creator, txs[7].nonce)})
+    committed = [v20.index_txid(envs1[0])]
+    b3, _, _ = blocks.make_block(net, 5, number=3, seed=23, faults=(), reuse={1: (txs[0].creator, txs[0].nonce)})
+    eng = _engine_for(net, committed)
+    exp = _check(eng, net, [b1, b2, b3], committed)
+    assert exp[0][0] == 9 and exp[1][5] == 9 and exp[1][9] == 9 and exp[2][1] == 9
+    eng.close()
+
+
+def test_empty_and_degenerate_blocks():
+    net = network()
+    eng = _engine_for(net)
+    _, _, envs = blocks.make_block(net, 3, number=1, seed=31, faults=())
+    blks = [block_from_envs([]), block_from_envs([b"", b"\x0a\x00", envs[0], b"\x12\x00"]),
+            block_from_envs([envs[1]] * 3)]
+    exp = _check(eng, net, blks)
+    assert len(exp[0]) == 0 and exp[2] == [0, 9, 9]
+    eng.close()
+
+
+def test_policy_variants():
+    for n in (1, 3):
+        net = network(policy_n=n)
+        eng = _engine_for(net)
+        blk, _, _ = blocks.make_block(net, 50, number=1, seed=40 + n)
+        _check(eng, net, [blk])
+        eng.close()
+
+
+def test_unsupported_is_reported_not_guessed():
+    net = network()
+    eng = _lib.Engine(0)
+    txvalidator.setup_channel(eng, net.channel, net.identities(), {"mycc": blocks.f_str(2, "/Channel/Application/E")})
+    blk, _, _ = blocks.make_block(net, 4, number=1, seed=50, faults=())
+    with pytest.raises(_lib.Unsupported):
+        eng.validate_blocks([blk])
+    eng.close()
+
+
+def test_device_resident_blocks_match_host_upload():
+    import torch
+    net = network()
+    eng = _engine_for(net)
+    blks = [blocks.make_block(net, 100, number=1 + i, seed=60 + i)[0] for i in range(3)]
+    dev = [torch.zeros(len(b) + 64, dtype=torch.uint8, device="cuda:0") for b in blks]
+    for d, b in zip(dev, blks):
+        d[:len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+    torch.cuda.synchronize()
+    a = eng.validate_blocks(blks)
+    b = eng.validate_blocks(blks, [d.data_ptr() for d in dev])
+    assert all(np.array_equal(x, y) for x, y in zip(a, b))
+    eng.close()

@@ -1,0 +1,84 @@
+"""CPU: the restated committer (oracle/v20.py) against the generator's labels (independent
+expectations) and the protobuf decoding rules it restates."""
+import pytest
+
+from fabric_amd.synth import blocks
+from oracle import v20
+from oracle.protowire import DecodeError, decode
+from tests.blockfix import SPECIAL, network
+
+
+def _model(net):
+    return v20.ChannelModel(net.channel, net.identities(), net.chaincodes)
+
+
+def test_c2_block_matches_generator_labels():
+    net = network()
+    blk, labels, _ = blocks.make_block(net, 200, number=1, seed=1)
+    flags = v20.validate_block(_model(net), blk)
+    exp = blocks.expected_codes(labels)
+    assert [f for f, e in zip(flags, exp) if e is not None] == [e for e in exp if e is not None]
+    assert 0 in flags
+
+
+def test_every_special_fault_class():
+    net = network()
+    blk, labels, _ = blocks.make_block(net, len(SPECIAL), number=2, seed=2, faults=(), force=SPECIAL)
+    flags = v20.validate_block(_model(net), blk)
+    assert flags == blocks.expected_codes(labels)
+
+
+def test_txid_index_across_blocks():
+    """Block k sees txids of blocks < k (TxIDExists) -> DUPLICATE_TXID(9)."""
+    net = network()
+    txs = []
+    b1, _, _ = blocks.make_block(net, 10, number=1, seed=5, faults=(), out_txs=txs)
+    reuse = {3: (txs[4].creator, txs[4].nonce)}
+    b2, labels2, _ = blocks.make_block(net, 10, number=2, seed=6, faults=(), reuse=reuse)
+    f1, f2 = v20.validate_blocks(_model(net), [b1, b2])
+    assert f1 == [0] * 10
+    assert f2[3] == 9 and sum(f2) == 9
+
+
+def test_committed_ledger_txid():
+    net = network()
+    blk, _, envs = blocks.make_block(net, 4, number=1, seed=8, faults=())
+    m = _model(net)
+    tid = v20.index_txid(envs[2])
+    m.committed.add(tid)
+    assert v20.validate_block(m, blk) == [0, 0, 9, 0]
+
+
+def test_policy_3_of_3_and_1_of_3():
+    for n, exp in [(3, 10), (1, 0)]:
+        net = network(policy_n=n)
+        blk, labels, _ = blocks.make_block(net, 6, number=1, seed=3, faults=(), endorse_dist=((2, 1.0),))
+        assert v20.validate_block(_model(net), blk) == [exp] * 6
+
+
+def test_unsupported_config_tx():
+    net = network()
+    blk, _, envs = blocks.make_block(net, 2, number=1, seed=3, faults=())
+    # turn tx 0 into a CONFIG (type 1) envelope is not constructible without re-signing; use
+    # a channel-reference policy instead
+    m = v20.ChannelModel(net.channel, net.identities(), {"mycc": blocks.f_str(2, "/Channel/Application/Endorsement")})
+    with pytest.raises(v20.Unsupported):
+        v20.validate_block(m, blk)
+
+
+# ---- protobuf-go decoding rules (oracle/protowire.py)
+def test_wire_rules():
+    assert decode("Envelope", b"\x0a\x00") == {}                 # empty bytes -> nil
+    assert decode("Envelope", b"\x0a\x01x\x0a\x01y")["payload"] == b"y"   # last wins
+    assert decode("Envelope", b"\x08\x05") == {}                 # wrong wire type -> unknown
+    assert decode("Envelope", b"\x1b\x08\x01\x1c") == {}         # unknown group skipped
+    for bad in [b"\x0a\x05ab", b"\x00\x01", b"\x0c", b"\x0f", b"\x08" + b"\xff" * 10, b"\x1b\x08\x01"]:
+        with pytest.raises(DecodeError):
+            decode("Envelope", bad)
+    with pytest.raises(DecodeError):
+        decode("ChannelHeader", b"\x22\x02\xc3\x28")             # invalid UTF-8 in channel_id
+    m = decode("Payload", b"\x0a\x03\x0a\x01a" + b"\x0a\x03\x12\x01b")   # Header merged
+    assert m["header"] == {"channel_header": b"a", "signature_header": b"b"}
+    sp = decode("SignaturePolicy", b"\x12\x00\x08\x00")          # oneof: last member (signed_by 0)
+    assert sp == {"signed_by": 0}
+    assert decode("ChannelHeader", b"\x08\xff\xff\xff\xff\x0f")["type"] == -1
