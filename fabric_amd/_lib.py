@@ -19,8 +19,9 @@ EXPORTED = [
     "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_sha256_batch",
     "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
-    "fgv_ledger_add_txids", "fgv_validate_blocks",
+    "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
 ]
+TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
 
 
@@ -75,6 +76,8 @@ def load():
         L.fgv_chaincode_define.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
         L.fgv_ledger_add_txids.argtypes = [vp, vp, vp, vp, sz]
         L.fgv_validate_blocks.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp]
+        L.fgv_validate_shard.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
+        L.fgv_finalize_flags.argtypes = [sz, vp, vp, vp]
         _L = L
     return _L
 
@@ -206,3 +209,29 @@ class Engine:
             out.append(flags[o:o + ntx[i]].copy())
             o += ntx[i]
         return out
+
+    def validate_shard(self, blocks, tx_lo, tx_hi, d_blocks=None):
+        """Validate transactions [tx_lo[b], tx_hi[b]) of each block.  Returns (results uint8
+        array of shape (n, 68) = fgv_tx_result records, ntx per block)."""
+        nb = len(blocks)
+        bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+        ptrs = (ctypes.c_void_p * nb)(*[b.ctypes.data for b in bufs])
+        lens = (ctypes.c_size_t * nb)(*[len(b) for b in blocks])
+        dptr = (ctypes.c_void_p * nb)(*d_blocks) if d_blocks is not None else None
+        lo = np.ascontiguousarray(tx_lo, dtype=np.uint32)
+        hi = np.ascontiguousarray(tx_hi, dtype=np.uint32)
+        cap = int(np.maximum(hi.astype(np.int64) - lo, 0).sum())
+        res = np.zeros((max(cap, 1), TX_RESULT_BYTES), dtype=np.uint8)
+        ntx = (ctypes.c_size_t * nb)()
+        _check(self._L.fgv_validate_shard(self._h, nb, ptrs, lens, dptr, _ptr(lo), _ptr(hi), _ptr(res), cap, ntx))
+        return res[:cap], np.array(list(ntx), dtype=np.uint64)
+
+
+def finalize_flags(ntx, results):
+    """fgv_finalize_flags over the results of ALL transactions (blocks concatenated)."""
+    L = load()
+    ntx = np.ascontiguousarray(ntx, dtype=np.uint64)
+    results = np.ascontiguousarray(results, dtype=np.uint8)
+    flags = np.zeros(int(ntx.sum()), dtype=np.uint8)
+    _check(L.fgv_finalize_flags(len(ntx), _ptr(ntx), _ptr(results), _ptr(flags)))
+    return flags

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -857,28 +858,46 @@ static bool eval_node(const Policy &P, int node, const std::vector<int> &ids, co
 }
 
 // ======================================================================= API
+static bool hex32(const std::string &s, uint8_t out[32]) {
+  if (s.size() != 64) return false;
+  for (int k = 0; k < 64; k++) {
+    const char ch = s[k];
+    int v;
+    if (ch >= '0' && ch <= '9') v = ch - '0';
+    else if (ch >= 'a' && ch <= 'f') v = ch - 'a' + 10;
+    else return false;  // only lowercase hex can equal a VALID txid (ComputeTxID output)
+    if (k & 1) out[k >> 1] |= (uint8_t)v;
+    else out[k >> 1] = (uint8_t)(v << 4);
+  }
+  return true;
+}
+
 int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
-                            const size_t *lens, const uint8_t *const *d_blocks, uint8_t *flags_out,
-                            size_t flags_cap, size_t *ntx_out) {
+                            const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                            const uint32_t *tx_hi, fgv_tx_result *res_out, size_t res_cap, size_t *ntx_out) {
   Channel &ch = S->ch;
-  // --- block envelopes
+  // --- block envelopes (shard: transactions [tx_lo[b], tx_hi[b]) of block b)
   std::vector<std::vector<Span>> envs(nblocks);
+  std::vector<uint32_t> lo(nblocks), hi(nblocks);
   size_t total = 0;
   for (size_t b = 0; b < nblocks; b++) {
     VBlock blk;
     if (!pbw::decode(h_blocks[b], lens[b], blk)) return FGV_EINVAL;  // unparsable block
     envs[b] = std::move(blk.data.data);
     ntx_out[b] = envs[b].size();
-    total += envs[b].size();
+    lo[b] = tx_lo ? std::min<uint32_t>(tx_lo[b], (uint32_t)envs[b].size()) : 0;
+    hi[b] = tx_hi ? std::min<uint32_t>(tx_hi[b], (uint32_t)envs[b].size()) : (uint32_t)envs[b].size();
+    if (hi[b] < lo[b]) hi[b] = lo[b];
+    total += hi[b] - lo[b];
   }
-  if (total > flags_cap) return FGV_EINVAL;
+  if (total > res_cap) return FGV_EINVAL;
   std::vector<TxRec> &recs = S->recs;
   recs.resize(total);
   std::vector<size_t> base(nblocks + 1, 0);
-  for (size_t b = 0; b < nblocks; b++) base[b + 1] = base[b] + envs[b].size();
+  for (size_t b = 0; b < nblocks; b++) base[b + 1] = base[b] + (hi[b] - lo[b]);
   std::vector<std::pair<uint32_t, uint32_t>> where(total);
   for (size_t b = 0; b < nblocks; b++)
-    for (size_t i = 0; i < envs[b].size(); i++) where[base[b] + i] = {(uint32_t)b, (uint32_t)i};
+    for (size_t i = lo[b]; i < hi[b]; i++) where[base[b] + i - lo[b]] = {(uint32_t)b, (uint32_t)i};
 
   // --- A. parse
   S->pool.parallel_for(total, [&](size_t t) {
@@ -952,7 +971,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   static const char HEX[] = "0123456789abcdef";
   std::atomic<bool> unsupported{false};
   std::vector<uint8_t> codes(total, C_PENDING);
-  std::vector<std::string> fold_txid(total);
+  std::vector<uint8_t> reached(total, 0);
   S->pool.parallel_for(total, [&](size_t t) {
     TxRec &R = recs[t];
     uint8_t code;
@@ -976,8 +995,8 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         code = R.etx;
       } else if (R.prop_hash.n != 32 || memcmp(&digests[(size_t)R.prop_job * 32], R.prop_hash.p, 32) != 0) {
         code = C_BAD_ETX;
-      } else if (ch.committed.count(R.txid.str())) {
-        code = C_DUP_TXID;  // checkTxIdDupsLedger (initial ledger; batch-earlier blocks below)
+      } else if ((reached[t] = 1, ch.committed.count(R.txid.str()))) {
+        code = C_DUP_TXID;  // checkTxIdDupsLedger (initial ledger; batch-earlier blocks: finalize)
       } else if (R.disp != C_VALID) {
         code = R.disp;
       } else {
@@ -1013,7 +1032,6 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   done:
     if (code == C_UNSUPPORTED) unsupported = true;
     codes[t] = code;
-    if (code == C_VALID) fold_txid[t] = R.txid.str();
     // txid index entry for later blocks of this batch: chdr.TxId, or when empty
     // ComputeTxID(nonce, creator) (protoutil/txutils.go:503-534)
     if (R.index_ok && R.index_txid.empty() && R.index_job != UINT32_MAX) {
@@ -1027,25 +1045,60 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     }
   });
   if (unsupported) return FGV_EUNSUPPORTED;
-  // serial: ledger index across blocks of the batch + markTXIdDuplicates per block
-  std::unordered_set<std::string> batch_index;
-  for (size_t b = 0; b < nblocks; b++) {
-    std::unordered_set<std::string> seen;
-    for (size_t i = 0; i < envs[b].size(); i++) {
-      const size_t t = base[b] + i;
-      if (codes[t] == C_VALID && batch_index.count(fold_txid[t])) codes[t] = C_DUP_TXID;
-    }
-    for (size_t i = 0; i < envs[b].size(); i++) {
-      const size_t t = base[b] + i;
-      if (codes[t] != C_VALID) continue;
-      if (!seen.insert(fold_txid[t]).second) codes[t] = C_DUP_TXID;
-    }
-    for (size_t i = 0; i < envs[b].size(); i++) {
-      const TxRec &R = recs[base[b] + i];
-      if (R.index_ok && !R.index_txid.empty()) batch_index.insert(R.index_txid);
-    }
+  S->pool.parallel_for(total, [&](size_t t) {
+    const TxRec &R = recs[t];
+    fgv_tx_result &o = res_out[t];
+    memset(&o, 0, sizeof o);
+    o.code = codes[t];
+    if (reached[t] && hex32(R.txid.str(), o.txid)) o.flags |= FGV_TXR_REACHED;
+    if (R.index_ok && hex32(R.index_txid, o.index_txid)) o.flags |= FGV_TXR_INDEXED;
+  });
+  return FGV_OK;
+}
+
+// number of transactions of a block (-1 if the block does not decode)
+long fgv_block_count_txs(const uint8_t *b, size_t n) {
+  VBlock blk;
+  if (!pbw::decode(b, n, blk)) return -1;
+  return (long)blk.data.data.size();
+}
+
+// markTXIdDuplicates + the txid index of earlier blocks of the batch (see fgv.h)
+struct Key32Hash {
+  size_t operator()(const std::array<uint8_t, 32> &k) const {
+    uint64_t h;
+    memcpy(&h, k.data(), 8);
+    return (size_t)h;
   }
-  memcpy(flags_out, codes.data(), total);
+};
+int fgv_finalize_impl(size_t nblocks, const size_t *ntx, const fgv_tx_result *res, uint8_t *flags) {
+  std::unordered_set<std::array<uint8_t, 32>, Key32Hash> index;
+  size_t o = 0;
+  for (size_t b = 0; b < nblocks; b++) {
+    const size_t n = ntx[b];
+    std::array<uint8_t, 32> k;
+    for (size_t i = 0; i < n; i++) {
+      const fgv_tx_result &r = res[o + i];
+      uint8_t code = r.code;
+      if (r.flags & FGV_TXR_REACHED) {
+        memcpy(k.data(), r.txid, 32);
+        if (index.count(k)) code = C_DUP_TXID;  // checkTxIdDupsLedger precedes Dispatch
+      }
+      flags[o + i] = code;
+    }
+    std::unordered_set<std::array<uint8_t, 32>, Key32Hash> seen;
+    for (size_t i = 0; i < n; i++) {
+      if (flags[o + i] != C_VALID) continue;
+      memcpy(k.data(), res[o + i].txid, 32);
+      if (!seen.insert(k).second) flags[o + i] = C_DUP_TXID;
+    }
+    for (size_t i = 0; i < n; i++) {
+      if (!(res[o + i].flags & FGV_TXR_INDEXED)) continue;
+      memcpy(k.data(), res[o + i].index_txid, 32);
+      index.insert(k);
+    }
+    o += n;
+  }
   return FGV_OK;
 }
 

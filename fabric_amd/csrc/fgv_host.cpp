@@ -628,28 +628,60 @@ int fgv_ledger_add_txids(fgv_ctx *c, const uint8_t *buf, const uint64_t *off, co
   return fgv_block_add_txids(c->blk, buf, off, len, n);
 }
 
+static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                        const uint8_t *const *d_blocks, std::vector<const uint8_t *> &dev) {
+  dev.resize(nblocks);
+  if (d_blocks) {
+    for (size_t b = 0; b < nblocks; b++) dev[b] = d_blocks[b];
+    return FGV_OK;
+  }
+  // stage the blocks into one device arena (64 B padding after each block)
+  size_t total = 0;
+  for (size_t b = 0; b < nblocks; b++) total += (lens[b] + 64 + 255) & ~(size_t)255;
+  if (!c->blk_arena.ensure(total)) return FGV_ENOMEM;
+  size_t o = 0;
+  for (size_t b = 0; b < nblocks; b++) {
+    HIP_TRY(hipMemcpyAsync(c->blk_arena.as<uint8_t>() + o, blocks[b], lens[b], hipMemcpyHostToDevice, c->stream));
+    dev[b] = c->blk_arena.as<uint8_t>() + o;
+    o += (lens[b] + 64 + 255) & ~(size_t)255;
+  }
+  return FGV_OK;
+}
+
+int fgv_validate_shard(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                       const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                       fgv_tx_result *results, size_t results_cap, size_t *ntx) {
+  if (!c || (nblocks && (!blocks || !lens || !ntx || (results_cap && !results)))) return FGV_EINVAL;
+  if (nblocks == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  std::vector<const uint8_t *> dev;
+  int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
+  if (rc) return rc;
+  return fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi, results,
+                                 results_cap, ntx);
+}
+
+int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *results, uint8_t *flags) {
+  if (nblocks && (!ntx || !flags)) return FGV_EINVAL;
+  return fgv_finalize_impl(nblocks, ntx, results, flags);
+}
+
 int fgv_validate_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                         const uint8_t *const *d_blocks, uint8_t *flags, size_t flags_cap, size_t *ntx) {
   if (!c || (nblocks && (!blocks || !lens || !flags || !ntx))) return FGV_EINVAL;
   if (nblocks == 0) return FGV_OK;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
-  std::vector<const uint8_t *> dev(nblocks);
-  if (d_blocks) {
-    for (size_t b = 0; b < nblocks; b++) dev[b] = d_blocks[b];
-  } else {
-    // stage the blocks into one device arena (64 B padding after each block)
-    size_t total = 0;
-    for (size_t b = 0; b < nblocks; b++) total += (lens[b] + 64 + 255) & ~(size_t)255;
-    if (!c->blk_arena.ensure(total)) return FGV_ENOMEM;
-    size_t o = 0;
-    for (size_t b = 0; b < nblocks; b++) {
-      HIP_TRY(hipMemcpyAsync(c->blk_arena.as<uint8_t>() + o, blocks[b], lens[b], hipMemcpyHostToDevice, c->stream));
-      dev[b] = c->blk_arena.as<uint8_t>() + o;
-      o += (lens[b] + 64 + 255) & ~(size_t)255;
-    }
+  size_t total = 0;
+  for (size_t b = 0; b < nblocks; b++) {
+    long k = fgv_block_count_txs(blocks[b], lens[b]);
+    if (k < 0) return FGV_EINVAL;
+    total += (size_t)k;
   }
-  return fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), flags, flags_cap, ntx);
+  if (total > flags_cap) return FGV_EINVAL;
+  std::vector<fgv_tx_result> res(total);
+  int rc = fgv_validate_shard(c, nblocks, blocks, lens, d_blocks, nullptr, nullptr, res.data(), total, ntx);
+  if (rc) return rc;
+  return fgv_finalize_impl(nblocks, ntx, res.data(), flags);
 }
 
 }  // extern "C"

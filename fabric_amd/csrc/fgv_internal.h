@@ -20,8 +20,10 @@ int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const uint8_t
 int fgv_block_add_txids(fgv_block_state *S, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
                         size_t n);
 int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
-                            const size_t *lens, const uint8_t *const *d_blocks, uint8_t *flags_out,
-                            size_t flags_cap, size_t *ntx_out);
+                            const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                            const uint32_t *tx_hi, fgv_tx_result *res_out, size_t res_cap, size_t *ntx_out);
+long fgv_block_count_txs(const uint8_t *b, size_t n);
+int fgv_finalize_impl(size_t nblocks, const size_t *ntx, const fgv_tx_result *res, uint8_t *flags);
 
 // Device pass for one block batch: SHA-256 jobs -> digests (all), then ECDSA verify jobs whose
 // digest is digests[dig_idx[i]] -> vstatus.  Implemented in fgv_host.cpp.

@@ -130,6 +130,31 @@ int fgv_validate_blocks(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *bloc
                         const size_t *lens, const uint8_t *const *d_blocks, uint8_t *flags,
                         size_t flags_cap, size_t *ntx);
 
+/* ----------------------------------------------- multi-GPU committer (one process per GPU)
+ * fgv_validate_blocks = fgv_validate_shard over every transaction + fgv_finalize_flags.
+ * With G GPUs each rank validates transactions [tx_lo[b], tx_hi[b]) of every block b (the
+ * north-star sharding by transaction index), the ranks all-gather their fgv_tx_result
+ * records (RCCL over xGMI), and fgv_finalize_flags applies the two cross-transaction steps
+ * of the reference: the block-store txid index of earlier blocks of the batch
+ * (checkTxIdDupsLedger, validator.go:460-481, which precedes Dispatch) and
+ * markTXIdDuplicates (validator.go:279-295). */
+#define FGV_TXR_REACHED 1u  /* tx reached the ledger duplicate check; txid = hex-decoded TxId */
+#define FGV_TXR_INDEXED 2u  /* index_txid = the 64-hex txid this tx adds to the block index  */
+typedef struct fgv_tx_result {
+  uint8_t code;  /* code decided by the tx alone (initial ledger txids applied)           */
+  uint8_t flags;
+  uint8_t pad[2];
+  uint8_t txid[32];
+  uint8_t index_txid[32];
+} fgv_tx_result; /* 68 bytes */
+
+int fgv_validate_shard(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                       const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                       fgv_tx_result *results, size_t results_cap, size_t *ntx);
+/* pure host function: results of ALL transactions, blocks concatenated in order */
+int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *results,
+                       uint8_t *flags);
+
 #ifdef __cplusplus
 }
 #endif

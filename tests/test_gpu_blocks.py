@@ -110,3 +110,50 @@ def test_device_resident_blocks_match_host_upload():
     b = eng.validate_blocks(blks, [d.data_ptr() for d in dev])
     assert all(np.array_equal(x, y) for x, y in zip(a, b))
     eng.close()
+
+
+def test_batch_duplicate_precedes_dispatch_failure():
+    """A later block's tx re-using an earlier txid gets 9 even when its endorsements would
+    fail the policy (checkTxIdDupsLedger runs before Dispatch, validator.go:365-373)."""
+    net = network()
+    txs = []
+    b1, _, _ = blocks.make_block(net, 6, number=1, seed=71, faults=(), out_txs=txs)
+    force = [None, "policy_unsatisfied", None, "unknown_cc", None]
+    b2, labels, _ = blocks.make_block(net, 5, number=2, seed=72, faults=(), force=force,
+                                      reuse={1: (txs[2].creator, txs[2].nonce), 3: (txs[3].creator, txs[3].nonce)})
+    eng = _engine_for(net)
+    exp = _check(eng, net, [b1, b2])
+    assert exp[1][1] == 9 and exp[1][3] == 9
+    eng.close()
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+def test_sharded_validation_matches_single(shards):
+    """Multi-GPU protocol on one device: per-shard results + finalize == whole-batch flags."""
+    net = network()
+    txs = []
+    b1, _, _ = blocks.make_block(net, 40, number=1, seed=81, out_txs=txs)
+    b2, _, _ = blocks.make_block(net, 37, number=2, seed=82, reuse={2: (txs[5].creator, txs[5].nonce),
+                                                                     30: (txs[9].creator, txs[9].nonce)})
+    blks = [b1, b2]
+    eng = _engine_for(net)
+    whole = eng.validate_blocks(blks)
+    ntx = [40, 37]
+    parts = []
+    for r in range(shards):
+        lo = [n * r // shards for n in ntx]
+        hi = [n * (r + 1) // shards for n in ntx]
+        res, nt = eng.validate_shard(blks, lo, hi)
+        assert list(nt) == ntx
+        parts.append((lo, hi, res))
+    # reorder to block-major, tx order (what the all-gather + reshuffle produces)
+    rows = []
+    for b in range(2):
+        for lo, hi, res in parts:
+            off = sum(hi[k] - lo[k] for k in range(b))
+            rows.append(res[off: off + hi[b] - lo[b]])
+    flags = _lib.finalize_flags(ntx, np.concatenate(rows))
+    assert np.array_equal(flags, np.concatenate(whole))
+    exp = _oracle(net, blks)
+    assert list(flags) == exp[0] + exp[1]
+    eng.close()
