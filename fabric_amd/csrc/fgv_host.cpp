@@ -106,6 +106,7 @@ struct fgv_ctx {
   // pinned staging
   HostBuf h_status, h_slot, h_r, h_s, h_dig, h_kq, h_kslot, h_moff, h_mlen;
   double t_sha = 0, t_prep = 0, t_point = 0, t_keytab = 0;
+  uint64_t n_sha_jobs = 0, n_sha_blocks = 0, n_verifies = 0;  // last call
 };
 
 #define HIP_TRY(x)                                     \
@@ -204,6 +205,14 @@ void fgv_destroy(fgv_ctx *c) {
     if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
+}
+
+int fgv_last_counts(fgv_ctx *c, uint64_t *sha_jobs, uint64_t *sha_blocks, uint64_t *verifies) {
+  if (!c) return FGV_EINVAL;
+  if (sha_jobs) *sha_jobs = c->n_sha_jobs;
+  if (sha_blocks) *sha_blocks = c->n_sha_blocks;
+  if (verifies) *verifies = c->n_verifies;
+  return FGV_OK;
 }
 
 int fgv_last_timing(fgv_ctx *c, double *sha_ms, double *prep_ms, double *point_ms,
@@ -553,6 +562,10 @@ int fgv_run_block_jobs(fgv_ctx *c, const std::vector<ShaJob> &jobs, const std::v
   const size_t nj = jobs.size(), nv = sig_ptr.size();
   digests.assign(nj * 32, 0);
   vstatus.assign(nv, 0);
+  c->n_sha_jobs = nj;
+  c->n_verifies = nv;
+  c->n_sha_blocks = 0;
+  for (const ShaJob &j : jobs) c->n_sha_blocks += (j.n[0] + j.n[1] + j.n[2] + 8) / 64 + 1;
   if (nj == 0) return FGV_OK;
   if (!c->bj_jobs.ensure(nj * sizeof(ShaJob)) || !c->bj_dig.ensure(nj * 32) || !c->hb_dig.ensure(nj * 32))
     return FGV_ENOMEM;

@@ -121,33 +121,42 @@ def _pem_to_der(pem: bytes) -> bytes:
 class Network:
     """orgs: number of MSPs; clients: client identities (spread over the orgs)."""
 
-    def __init__(self, seed=3, orgs=3, clients=100, channel="testchannel", policy_n=2):
+    def __init__(self, seed=3, orgs=3, clients=100, channel="testchannel", policy_n=2, pems=None):
+        """pems: certificates exported by another process (Network.export_pems()) -- X.509
+        signatures are randomised, so multi-process users share one set of certificates."""
         self.seed, self.channel = seed, channel
+        _pem_iter = iter(pems) if pems is not None else None
+
+        def cert(*a):  # reuse exported certificates in order
+            return next(_pem_iter) if _pem_iter is not None else make_cert(*a)
         self.mspids = [f"Org{i + 1}MSP" for i in range(orgs)]
         self.cas, self.peers, self.clients = [], [], []
         for o, m in enumerate(self.mspids):
             ca = Key(seed, 10_000 + o)
             self.cas.append(ca)
             pk = Key(seed, 20_000 + o)
-            pem = make_cert(pk, ca, f"peer0.org{o + 1}", m, f"ca.org{o + 1}", False, 100 + o)
+            pem = cert(pk, ca, f"peer0.org{o + 1}", m, f"ca.org{o + 1}", False, 100 + o)
             self.peers.append(Identity(pk, m, pem, "peer"))
         for c in range(clients):
             o = c % orgs
             ck = Key(seed, 30_000 + c)
-            pem = make_cert(ck, self.cas[o], f"user{c}.org{o + 1}", self.mspids[o], f"ca.org{o + 1}", False,
+            pem = cert(ck, self.cas[o], f"user{c}.org{o + 1}", self.mspids[o], f"ca.org{o + 1}", False,
                             1000 + c)
             self.clients.append(Identity(ck, self.mspids[o], pem, "client"))
         # an identity from an MSP the channel does not know (deserialization fails)
         rk = Key(seed, 40_000)
         rogue_ca = Key(seed, 40_001)
-        self.rogue = Identity(rk, "RogueMSP", make_cert(rk, rogue_ca, "rogue", "RogueMSP", "ca.rogue", False, 7),
+        self.rogue = Identity(rk, "RogueMSP", cert(rk, rogue_ca, "rogue", "RogueMSP", "ca.rogue", False, 7),
                               "client")
         # an identity claiming Org1MSP but with a cert from a foreign CA: deserializes (known
         # MSP) but fails Validate (not issued by Org1's CA)
         fk = Key(seed, 40_002)
-        self.forged = Identity(fk, self.mspids[0], make_cert(fk, rogue_ca, "forged", self.mspids[0], "ca.rogue",
+        self.forged = Identity(fk, self.mspids[0], cert(fk, rogue_ca, "forged", self.mspids[0], "ca.rogue",
                                                              False, 8), "peer")
         self.chaincodes = {"mycc": out_of_policy(policy_n, self.mspids)}
+
+    def export_pems(self):
+        return [i.pem for i in self.peers + self.clients] + [self.rogue.pem, self.forged.pem]
 
     def identities(self):
         """What the MSP layer knows: (serialized, mspid, pubkey64, valid, id_digest).

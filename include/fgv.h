@@ -56,6 +56,8 @@ const char *fgv_strerror(int code);
 /* kernel-time accounting of the last call (ms, HIP events around each kernel) */
 int fgv_last_timing(fgv_ctx *ctx, double *sha_ms, double *prep_ms, double *point_ms,
                     double *keytab_ms);
+/* work of the last block call: SHA-256 messages, 64-byte compressions, ECDSA verifies */
+int fgv_last_counts(fgv_ctx *ctx, uint64_t *sha_jobs, uint64_t *sha_blocks, uint64_t *verifies);
 
 /* ---------------------------------------------------------- BCCSP Hash / Verify */
 
