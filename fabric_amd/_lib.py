@@ -20,6 +20,7 @@ EXPORTED = [
     "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
+    "fgv_statedb_init", "fgv_statedb_load", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -79,6 +80,12 @@ def load():
         L.fgv_validate_blocks.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp]
         L.fgv_validate_shard.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
         L.fgv_finalize_flags.argtypes = [sz, vp, vp, vp]
+        L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
+        L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
+        L.fgv_mvcc_validate_block.argtypes = [vp, vp, sz, vp, ctypes.c_uint64, vp, sz, ctypes.c_int]
+        L.fgv_mvcc_last_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.POINTER(ctypes.c_uint32)]
         _L = L
     return _L
 
@@ -231,6 +238,34 @@ class Engine:
         ntx = (ctypes.c_size_t * nb)()
         _check(self._L.fgv_validate_shard(self._h, nb, ptrs, lens, dptr, _ptr(lo), _ptr(hi), _ptr(res), cap, ntx))
         return res[:cap], np.array(list(ntx), dtype=np.uint64)
+
+
+    # --- MVCC
+    def statedb_init(self, slots=1 << 22, arena_bytes=64 << 20):
+        _check(self._L.fgv_statedb_init(self._h, slots, arena_bytes))
+
+    def statedb_load(self, ns, keys, blk, txn):
+        arena, offs, lens = pack([k.encode() if isinstance(k, str) else k for k in keys])
+        blk = np.ascontiguousarray(blk, dtype=np.uint64)
+        txn = np.ascontiguousarray(txn, dtype=np.uint64)
+        _check(self._L.fgv_statedb_load(self._h, ns.encode(), _ptr(arena), _ptr(offs), _ptr(lens), _ptr(blk),
+                                        _ptr(txn), len(keys)))
+
+    def mvcc_validate(self, block: bytes, block_num: int, flags, commit=True, d_block=None):
+        """flags: committer TxValidationFlags (updated copy returned)."""
+        f = np.array(flags, dtype=np.uint8)
+        buf = np.frombuffer(block, dtype=np.uint8)
+        _check(self._L.fgv_mvcc_validate_block(self._h, buf.ctypes.data, len(block), d_block, block_num, _ptr(f),
+                                               len(f), 1 if commit else 0))
+        return f
+
+    def mvcc_stats(self):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        r, w = ctypes.c_uint64(), ctypes.c_uint64()
+        rounds = ctypes.c_uint32()
+        _check(self._L.fgv_mvcc_last_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(r), ctypes.byref(w),
+                                           ctypes.byref(rounds)))
+        return dict(lookup_ms=a.value, total_ms=b.value, reads=r.value, writes=w.value, rounds=rounds.value)
 
 
 def finalize_flags(ntx, results):

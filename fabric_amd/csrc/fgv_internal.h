@@ -4,14 +4,126 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/fgv.h"
 #include "fgv_kernels.h"
 
 struct fgv_block_state;
+struct fgv_mvcc_state;
+
+namespace fgvh {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    if (hipMalloc(&p, want) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct HostBuf {  // pinned staging
+  void *p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+  void release() {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct KeyHash {
+  size_t operator()(const std::array<uint8_t, 64> &k) const {
+    uint64_t h = 1469598103934665603ull;
+    for (int i = 0; i < 64; i += 8) {
+      uint64_t w;
+      memcpy(&w, k.data() + i, 8);
+      h = (h ^ w) * 1099511628211ull;
+    }
+    return (size_t)h;
+  }
+};
+
+// big-endian 32 bytes -> 8 little-endian limbs
+inline void be32_to_limbs(const uint8_t *b, uint32_t *l) {
+  for (int i = 0; i < 8; i++) {
+    const uint8_t *p = b + 4 * (7 - i);
+    l[i] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+  }
+}
+
+}  // namespace fgvh
+using namespace fgvh;
+
+struct fgv_ctx {
+  fgv_mvcc_state *mv = nullptr;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8] = {};
+  std::mutex mu;
+  // generator table (88 KB) and the public-key table cache
+  DevBuf gtab, g_ok;
+  DevBuf ktab, key_ok;
+  uint32_t key_slots = 0;
+  uint32_t pinned = 0;  // slots [0, pinned) hold registered keys and are never evicted
+  std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_map;
+  fgv_block_state *blk = nullptr;
+  DevBuf bj_jobs, bj_sigp, bj_sigl, bj_slot, bj_didx, bj_dig, bj_vst, blk_arena;
+  HostBuf hb_dig, hb_vst;
+  // per-batch device buffers
+  DevBuf kt_q, kt_slot, kt_scratch;
+  DevBuf status, slot, r, s, dig, d1, d2, wscr, msg, moff, mlen;
+  // pinned staging
+  HostBuf h_status, h_slot, h_r, h_s, h_dig, h_kq, h_kslot, h_moff, h_mlen;
+  double t_sha = 0, t_prep = 0, t_point = 0, t_keytab = 0;
+  uint64_t n_sha_jobs = 0, n_sha_blocks = 0, n_verifies = 0;  // last call
+  double t_mvcc_lookup = 0, t_mvcc_total = 0;
+  uint64_t n_mvcc_reads = 0, n_mvcc_writes = 0;
+};
+
+#define HIP_TRY(x)                                     \
+  do {                                                 \
+    if ((x) != hipSuccess) return FGV_EDEVICE;         \
+  } while (0)
+
+
 fgv_block_state *fgv_block_state_new(unsigned threads);
 void fgv_block_state_free(fgv_block_state *s);
+
+#include <functional>
+void fgv_parallel_for(fgv_block_state *S, size_t n, const std::function<void(size_t)> &f);
+void fgv_mvcc_free(fgv_mvcc_state *M);
 
 int fgv_block_set_channel(fgv_block_state *S, const char *name);
 int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, int32_t key_slot, int valid,

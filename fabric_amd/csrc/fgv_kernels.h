@@ -42,3 +42,47 @@ __global__ void k_sha256(const uint8_t *buf, const uint64_t *off, const uint32_t
                          uint8_t *out);
 __global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_t *len, uint32_t n,
                       uint8_t *status, uint32_t *r_limbs, uint32_t *s_limbs);
+
+// ---- MVCC (mvcc.hip)
+struct MvKey {  // one read or write of a transaction; key bytes live in the block (device)
+  uint64_t ptr;
+  uint32_t len;
+  uint32_t ns;     // namespace id (< 32768)
+  uint32_t tx;     // transaction index in the block
+  uint32_t flags;  // reads: bit0 = has version; writes: bit0 = is_delete
+  uint64_t blk, txn;
+};
+struct StateSlot {  // committed state: open addressing, key bytes in the arena
+  uint64_t tag;     // 0 = empty
+  uint64_t blk, txn;
+  uint32_t key_off;
+  uint16_t key_len;
+  uint16_t nsf;     // ns id | 0x8000 when the key is present (not deleted)
+};
+struct BlkSlot {    // keys written in the block
+  uint32_t owner;   // write index + 1 (0 = empty)
+  uint32_t fw_cand, fw_valid, pad;
+  uint64_t last;    // (tx << 32) | (write index + 1) of the last VALID writer
+};
+__global__ void k_mv_tags(const MvKey *keys, uint32_t n, uint64_t *tags);
+__global__ void k_mv_lookup(const MvKey *reads, const uint64_t *tags, uint32_t n, const StateSlot *tbl, uint64_t mask,
+                            const uint8_t *arena, uint8_t *bad_tx);
+__global__ void k_mv_blk_insert(const MvKey *writes, const uint64_t *tags, uint32_t n, BlkSlot *tbl, uint32_t mask,
+                                uint32_t *wslot);
+__global__ void k_mv_blk_find(const MvKey *reads, const uint64_t *rtags, uint32_t n, const BlkSlot *tbl, uint32_t mask,
+                              const MvKey *writes, const uint64_t *wtags, uint32_t *rslot);
+__global__ void k_mv_init(uint32_t ntx, const uint8_t *part, const uint8_t *bad_tx, uint8_t *st);
+__global__ void k_mv_reset(BlkSlot *tbl, uint32_t cap);
+__global__ void k_mv_min(const MvKey *writes, const uint32_t *wslot, uint32_t n, const uint8_t *st, BlkSlot *tbl);
+__global__ void k_mv_decide(uint32_t ntx, const uint32_t *rbeg, const uint32_t *rslot, const BlkSlot *tbl, uint8_t *st,
+                            uint32_t *undecided);
+__global__ void k_mv_lastwriter(const MvKey *writes, const uint32_t *wslot, uint32_t n, const uint8_t *st, BlkSlot *tbl);
+__global__ void k_mv_apply_find(const BlkSlot *btbl, uint32_t bcap, const MvKey *writes, const uint64_t *wtags,
+                                StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint64_t block_num, uint32_t *pend,
+                                uint32_t *npend);
+__global__ void k_mv_apply_insert(const BlkSlot *btbl, const uint32_t *pend, uint32_t np, const MvKey *writes,
+                                  const uint64_t *wtags, StateSlot *tbl, uint64_t mask, uint8_t *arena,
+                                  unsigned long long *arena_top, uint64_t block_num);
+__global__ void k_mv_load(const MvKey *keys, const uint64_t *tags, uint32_t n, StateSlot *tbl, uint64_t mask,
+                          uint8_t *arena, unsigned long long *arena_top);
+__global__ void k_mv_flags(uint32_t ntx, const uint8_t *part, const uint8_t *st, uint8_t *out);

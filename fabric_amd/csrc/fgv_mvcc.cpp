@@ -1,0 +1,339 @@
+// fgv_mvcc.cpp -- host side of MVCC validation (libfgv.so): the committed-state table on the
+// GPU (a cache of the state DB, rebuilt from it at start -- never authoritative), per-block
+// rwset extraction, kernel orchestration (mvcc.hip).
+//
+// Reference (core/ledger/kvledger/txmgmt): validation/batch_preparer.go:192-286
+// (preprocessProtoBlock: skip committer-invalid txs, NIL_TXACTION(16) / INVALID_OTHER_REASON
+// (255) on extraction errors), validation/validator.go:81-200 (sequential MVCC, code 11),
+// validation/types.go:81-112 + tx_ops.go:17-51 (puts/deletes applied at Height{blk, tx}; a
+// later write of the same key wins), statedb/stateleveldb/stateleveldb.go:128-137 (GetVersion),
+// internal/version/version.go:82-90 (AreSame: nil == nil).
+#include <hip/hip_runtime.h>
+
+#include <functional>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/fgv.h"
+#include "fgv_internal.h"
+#include "fgv_visitors.h"
+
+using namespace fgvb;
+
+namespace {
+
+struct MvRead {
+  Span ns, key;
+  bool has_ver;
+  uint64_t blk, txn;
+};
+struct MvWrite {
+  Span ns, key;
+  bool del;
+};
+struct MvTx {
+  uint8_t code = 0;  // 0 participates; 16 / 255 decided here; 0xFD unsupported; 0xFF skipped
+  std::vector<MvRead> reads;
+  std::vector<MvWrite> writes;
+};
+
+constexpr uint8_t MV_UNSUP = 0xFD, MV_SKIP = 0xFF;
+
+// GetActionFromEnvelope + TxRwSet.FromProtoBytes for one committer-valid transaction
+void mv_parse(Span d, MvTx &T) {
+  T = MvTx();
+  VEnvelope env;
+  VPayload pl;
+  VHeader hdr;
+  VChannelHeader chdr;
+  if (!pbw::decode(d.p, d.n, env) || !pbw::decode(env.payload.p, env.payload.n, pl) || !pl.header.present ||
+      !pl.header.decode_into(hdr) || !pbw::decode(hdr.channel_header.p, hdr.channel_header.n, chdr)) {
+    T.code = MV_UNSUP;  // the reference returns an error (channel halt) -- not ours to decide
+    return;
+  }
+  if (chdr.type != 3) {
+    T.code = MV_UNSUP;  // CONFIG etc. go through custom tx processors
+    return;
+  }
+  VTransaction tx;
+  if (!pbw::decode(pl.data.p, pl.data.n, tx) || tx.actions.empty()) { T.code = 16; return; }
+  VCcActionPayload cap;
+  if (!pbw::decode(tx.actions[0].payload.p, tx.actions[0].payload.n, cap)) { T.code = 16; return; }
+  if (!cap.has_action || cap.action.prp.nil()) { T.code = 16; return; }
+  VPrp prp;
+  if (!pbw::decode(cap.action.prp.p, cap.action.prp.n, prp) || prp.extension.nil()) { T.code = 16; return; }
+  VCcAction cca;
+  if (!pbw::decode(prp.extension.p, prp.extension.n, cca)) { T.code = 16; return; }
+  VTxRwSet rw;
+  if (!pbw::decode(cca.results.p, cca.results.n, rw)) { T.code = 255; return; }
+  bool unsup = false;
+  for (VNsRwSet &ns : rw.ns) {
+    std::vector<VKVRead> reads;
+    std::vector<VKVWrite> writes;
+    VKVRWSet kv;
+    kv.reads = &reads;
+    kv.writes = &writes;
+    if (!pbw::decode(ns.rwset.p, ns.rwset.n, kv)) { T.code = 255; return; }
+    for (const VCollHashed &c : ns.coll) {
+      VHashedRWSet h;
+      if (!pbw::decode(c.hashed.p, c.hashed.n, h)) { T.code = 255; return; }
+      if (h.nreads || h.nwrites || h.nmeta) unsup = true;  // private data: not modelled
+    }
+    if (kv.nrq || kv.nmeta) unsup = true;  // phantom checks / metadata writes: not modelled
+    for (const VKVRead &r : reads) T.reads.push_back(MvRead{ns.ns, r.key, r.has_ver, r.ver.block, r.ver.tx});
+    for (const VKVWrite &w : writes) T.writes.push_back(MvWrite{ns.ns, w.key, w.is_delete});
+  }
+  if (unsup) T.code = MV_UNSUP;
+}
+
+}  // namespace
+
+struct fgv_mvcc_state {
+  std::unordered_map<std::string, uint32_t> ns_ids;
+  uint64_t cap = 0, mask = 0, nkeys = 0, arena_cap = 0, arena_used = 0;
+  DevBuf tbl, arena, top;
+  DevBuf reads, writes, rtags, wtags, btbl, wslot, rslot, rbeg, part, bad, st, undec, pend, npend, flags, lbytes, lkeys;
+  std::vector<MvTx> txs;
+  uint32_t last_rounds = 0;
+};
+
+void fgv_mvcc_free(fgv_mvcc_state *M) {
+  if (!M) return;
+  DevBuf *d[] = {&M->tbl, &M->arena, &M->top, &M->reads, &M->writes, &M->rtags, &M->wtags, &M->btbl, &M->wslot,
+                 &M->rslot, &M->rbeg, &M->part, &M->bad, &M->st, &M->undec, &M->pend, &M->npend, &M->flags,
+                 &M->lbytes, &M->lkeys};
+  for (auto *b : d) b->release();
+  delete M;
+}
+
+static bool ns_lookup(fgv_mvcc_state *M, const Span &s, bool create, uint32_t &id) {
+  const std::string k = s.str();
+  auto it = M->ns_ids.find(k);
+  if (it != M->ns_ids.end()) {
+    id = it->second;
+    return true;
+  }
+  if (!create || M->ns_ids.size() >= 0x7fff) return false;
+  id = (uint32_t)M->ns_ids.size();
+  M->ns_ids.emplace(k, id);
+  return true;
+}
+
+static inline dim3 grid_for(size_t n) { return dim3((uint32_t)((n + 255) / 256)); }
+
+extern "C" {
+
+int fgv_statedb_init(fgv_ctx *c, uint64_t slots, uint64_t arena_bytes) {
+  if (!c) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  if (!c->mv) c->mv = new fgv_mvcc_state();
+  fgv_mvcc_state *M = c->mv;
+  uint64_t cap = 1024;
+  while (cap < (slots ? slots : (1ull << 22))) cap <<= 1;
+  const uint64_t arena = arena_bytes ? arena_bytes : (64ull << 20);
+  if (!M->tbl.ensure(cap * sizeof(StateSlot)) || !M->arena.ensure(arena) || !M->top.ensure(8)) return FGV_ENOMEM;
+  M->cap = cap;
+  M->mask = cap - 1;
+  M->arena_cap = arena;
+  M->arena_used = 0;
+  M->nkeys = 0;
+  M->ns_ids.clear();
+  HIP_TRY(hipMemsetAsync(M->tbl.p, 0, cap * sizeof(StateSlot), c->stream));
+  HIP_TRY(hipMemsetAsync(M->top.p, 0, 8, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return FGV_OK;
+}
+
+int fgv_statedb_load(fgv_ctx *c, const char *ns, const uint8_t *key_buf, const uint64_t *key_off,
+                     const uint32_t *key_len, const uint64_t *blk, const uint64_t *txn, size_t n) {
+  if (!c || !ns || (n && (!key_buf || !key_off || !key_len || !blk || !txn))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  fgv_mvcc_state *M = c->mv;
+  if (!M) return FGV_ESTATE;
+  if (n == 0) return FGV_OK;
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  uint32_t nsid;
+  if (!ns_lookup(M, Span{reinterpret_cast<const uint8_t *>(ns), (uint32_t)strlen(ns)}, true, nsid))
+    return FGV_EUNSUPPORTED;
+  if ((M->nkeys + n) * 10 > M->cap * 7) return FGV_ENOMEM;  // keep the load factor <= 0.7
+  size_t bytes = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (key_len[i] > 0xffff) return FGV_EUNSUPPORTED;
+    bytes = std::max<size_t>(bytes, key_off[i] + key_len[i]);
+  }
+  if (M->arena_used + bytes > M->arena_cap) return FGV_ENOMEM;
+  if (!M->lbytes.ensure(bytes + 64) || !M->lkeys.ensure(n * sizeof(MvKey)) || !M->wtags.ensure(n * 8))
+    return FGV_ENOMEM;
+  std::vector<MvKey> keys(n);
+  const uint64_t base = (uint64_t)(uintptr_t)M->lbytes.p;
+  for (size_t i = 0; i < n; i++) keys[i] = MvKey{base + key_off[i], key_len[i], nsid, 0, 0, blk[i], txn[i]};
+  HIP_TRY(hipMemcpyAsync(M->lbytes.p, key_buf, bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(M->lkeys.p, keys.data(), n * sizeof(MvKey), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_mv_tags, grid_for(n), dim3(256), 0, c->stream, M->lkeys.as<MvKey>(), (uint32_t)n,
+                     M->wtags.as<uint64_t>());
+  hipLaunchKernelGGL(k_mv_load, grid_for(n), dim3(256), 0, c->stream, M->lkeys.as<MvKey>(), M->wtags.as<uint64_t>(),
+                     (uint32_t)n, M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
+                     M->top.as<unsigned long long>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  M->nkeys += n;
+  M->arena_used += bytes;
+  return FGV_OK;
+}
+
+int fgv_mvcc_validate_block(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block,
+                            uint64_t block_num, uint8_t *flags, size_t ntx, int commit) {
+  if (!c || !block || (ntx && !flags)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  fgv_mvcc_state *M = c->mv;
+  if (!M) return FGV_ESTATE;
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  VBlock blk;
+  if (!pbw::decode(block, len, blk)) return FGV_EINVAL;
+  const std::vector<Span> &envs = blk.data.data;
+  if (envs.size() != ntx) return FGV_EINVAL;
+  const uint8_t *dblk = d_block;
+  if (!dblk) {
+    if (!c->blk_arena.ensure(len + 64)) return FGV_ENOMEM;
+    HIP_TRY(hipMemcpyAsync(c->blk_arena.p, block, len, hipMemcpyHostToDevice, c->stream));
+    dblk = c->blk_arena.as<uint8_t>();
+  }
+  // --- host: rwsets of committer-valid txs (parallel)
+  M->txs.resize(ntx);
+  fgv_parallel_for(c->blk, ntx, [&](size_t i) {
+    if (flags[i] != 0) {
+      M->txs[i] = MvTx();
+      M->txs[i].code = MV_SKIP;
+      return;
+    }
+    mv_parse(envs[i], M->txs[i]);
+  });
+  auto dev = [&](const Span &s) { return (uint64_t)(uintptr_t)dblk + (uint64_t)(s.p - block); };
+  std::vector<MvKey> reads, writes;
+  std::vector<uint32_t> rbeg(ntx + 1, 0);
+  std::vector<uint8_t> part(ntx, 0);
+  for (size_t i = 0; i < ntx; i++) {
+    MvTx &T = M->txs[i];
+    rbeg[i] = (uint32_t)reads.size();
+    if (T.code == MV_UNSUP) return FGV_EUNSUPPORTED;
+    if (T.code != 0) continue;
+    part[i] = 1;
+    for (const MvRead &r : T.reads) {
+      uint32_t ns;
+      if (!ns_lookup(M, r.ns, true, ns) || r.key.n > 0xffff) return FGV_EUNSUPPORTED;
+      reads.push_back(MvKey{dev(r.key), r.key.n, ns, (uint32_t)i, r.has_ver ? 1u : 0u, r.blk, r.txn});
+    }
+    for (const MvWrite &w : T.writes) {
+      uint32_t ns;
+      if (!ns_lookup(M, w.ns, true, ns) || w.key.n > 0xffff) return FGV_EUNSUPPORTED;
+      writes.push_back(MvKey{dev(w.key), w.key.n, ns, (uint32_t)i, w.del ? 1u : 0u, 0, 0});
+    }
+  }
+  rbeg[ntx] = (uint32_t)reads.size();
+  const size_t nr = reads.size(), nw = writes.size();
+  uint32_t bcap = 1024;
+  while (bcap < 2 * nw) bcap <<= 1;
+  size_t wbytes = 0;
+  for (const MvKey &w : writes) wbytes += w.len;
+  if (commit && ((M->nkeys + nw) * 10 > M->cap * 7 || M->arena_used + wbytes > M->arena_cap)) return FGV_ENOMEM;
+  if (!M->reads.ensure(std::max<size_t>(nr, 1) * sizeof(MvKey)) || !M->writes.ensure(std::max<size_t>(nw, 1) * sizeof(MvKey)) ||
+      !M->rtags.ensure(std::max<size_t>(nr, 1) * 8) || !M->wtags.ensure(std::max<size_t>(nw, 1) * 8) ||
+      !M->btbl.ensure(bcap * sizeof(BlkSlot)) || !M->wslot.ensure(std::max<size_t>(nw, 1) * 4) ||
+      !M->rslot.ensure(std::max<size_t>(nr, 1) * 4) || !M->rbeg.ensure((ntx + 1) * 4) || !M->part.ensure(ntx + 1) ||
+      !M->bad.ensure(ntx + 1) || !M->st.ensure(ntx + 1) || !M->undec.ensure(4) || !M->pend.ensure(bcap * 4) ||
+      !M->npend.ensure(4) || !M->flags.ensure(ntx + 1))
+    return FGV_ENOMEM;
+  hipStream_t s = c->stream;
+  if (nr) HIP_TRY(hipMemcpyAsync(M->reads.p, reads.data(), nr * sizeof(MvKey), hipMemcpyHostToDevice, s));
+  if (nw) HIP_TRY(hipMemcpyAsync(M->writes.p, writes.data(), nw * sizeof(MvKey), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(M->rbeg.p, rbeg.data(), (ntx + 1) * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(M->part.p, part.data(), ntx, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(M->bad.p, 0, ntx + 1, s));
+  HIP_TRY(hipMemsetAsync(M->btbl.p, 0, bcap * sizeof(BlkSlot), s));
+  HIP_TRY(hipEventRecord(c->ev[0], s));
+  if (nr) hipLaunchKernelGGL(k_mv_tags, grid_for(nr), dim3(256), 0, s, M->reads.as<MvKey>(), (uint32_t)nr, M->rtags.as<uint64_t>());
+  if (nw) hipLaunchKernelGGL(k_mv_tags, grid_for(nw), dim3(256), 0, s, M->writes.as<MvKey>(), (uint32_t)nw, M->wtags.as<uint64_t>());
+  if (nr)
+    hipLaunchKernelGGL(k_mv_lookup, grid_for(nr), dim3(256), 0, s, M->reads.as<MvKey>(), M->rtags.as<uint64_t>(),
+                       (uint32_t)nr, M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(), M->bad.as<uint8_t>());
+  HIP_TRY(hipEventRecord(c->ev[1], s));
+  if (nw)
+    hipLaunchKernelGGL(k_mv_blk_insert, grid_for(nw), dim3(256), 0, s, M->writes.as<MvKey>(), M->wtags.as<uint64_t>(),
+                       (uint32_t)nw, M->btbl.as<BlkSlot>(), bcap - 1, M->wslot.as<uint32_t>());
+  if (nr)
+    hipLaunchKernelGGL(k_mv_blk_find, grid_for(nr), dim3(256), 0, s, M->reads.as<MvKey>(), M->rtags.as<uint64_t>(),
+                       (uint32_t)nr, M->btbl.as<BlkSlot>(), bcap - 1, M->writes.as<MvKey>(), M->wtags.as<uint64_t>(),
+                       M->rslot.as<uint32_t>());
+  hipLaunchKernelGGL(k_mv_init, grid_for(ntx), dim3(256), 0, s, (uint32_t)ntx, M->part.as<uint8_t>(),
+                     M->bad.as<uint8_t>(), M->st.as<uint8_t>());
+  HIP_TRY(hipGetLastError());
+  // fixpoint: two rounds per host check
+  uint32_t undec = 1, rounds = 0;
+  while (undec) {
+    for (int k = 0; k < 2; k++) {
+      hipLaunchKernelGGL(k_mv_reset, grid_for(bcap), dim3(256), 0, s, M->btbl.as<BlkSlot>(), bcap);
+      if (nw)
+        hipLaunchKernelGGL(k_mv_min, grid_for(nw), dim3(256), 0, s, M->writes.as<MvKey>(), M->wslot.as<uint32_t>(),
+                           (uint32_t)nw, M->st.as<uint8_t>(), M->btbl.as<BlkSlot>());
+      HIP_TRY(hipMemsetAsync(M->undec.p, 0, 4, s));
+      hipLaunchKernelGGL(k_mv_decide, grid_for(ntx), dim3(256), 0, s, (uint32_t)ntx, M->rbeg.as<uint32_t>(),
+                         M->rslot.as<uint32_t>(), M->btbl.as<BlkSlot>(), M->st.as<uint8_t>(), M->undec.as<uint32_t>());
+      rounds++;
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&undec, M->undec.p, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (rounds > 2 * ntx + 4) return FGV_EDEVICE;  // cannot happen: one decision per round at least
+  }
+  M->last_rounds = rounds;
+  hipLaunchKernelGGL(k_mv_flags, grid_for(ntx), dim3(256), 0, s, (uint32_t)ntx, M->part.as<uint8_t>(),
+                     M->st.as<uint8_t>(), M->flags.as<uint8_t>());
+  std::vector<uint8_t> mv(ntx);
+  HIP_TRY(hipMemcpyAsync(mv.data(), M->flags.p, ntx, hipMemcpyDeviceToHost, s));
+  if (commit && nw) {
+    HIP_TRY(hipMemsetAsync(M->npend.p, 0, 4, s));
+    hipLaunchKernelGGL(k_mv_lastwriter, grid_for(nw), dim3(256), 0, s, M->writes.as<MvKey>(), M->wslot.as<uint32_t>(),
+                       (uint32_t)nw, M->st.as<uint8_t>(), M->btbl.as<BlkSlot>());
+    hipLaunchKernelGGL(k_mv_apply_find, grid_for(bcap), dim3(256), 0, s, M->btbl.as<BlkSlot>(), bcap,
+                       M->writes.as<MvKey>(), M->wtags.as<uint64_t>(), M->tbl.as<StateSlot>(), M->mask,
+                       M->arena.as<uint8_t>(), block_num, M->pend.as<uint32_t>(), M->npend.as<uint32_t>());
+    uint32_t np = 0;
+    HIP_TRY(hipMemcpyAsync(&np, M->npend.p, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (np)
+      hipLaunchKernelGGL(k_mv_apply_insert, grid_for(np), dim3(256), 0, s, M->btbl.as<BlkSlot>(), M->pend.as<uint32_t>(),
+                         np, M->writes.as<MvKey>(), M->wtags.as<uint64_t>(), M->tbl.as<StateSlot>(), M->mask,
+                         M->arena.as<uint8_t>(), M->top.as<unsigned long long>(), block_num);
+    HIP_TRY(hipGetLastError());
+    M->nkeys += np;
+    M->arena_used += wbytes;  // upper bound of the bytes appended
+  }
+  HIP_TRY(hipEventRecord(c->ev[2], s));
+  HIP_TRY(hipStreamSynchronize(s));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->t_mvcc_lookup = ms;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[2]) == hipSuccess) c->t_mvcc_total = ms;
+  c->n_mvcc_reads = nr;
+  c->n_mvcc_writes = nw;
+  for (size_t i = 0; i < ntx; i++) {
+    const MvTx &T = M->txs[i];
+    if (T.code == MV_SKIP) continue;
+    flags[i] = T.code ? T.code : mv[i];
+  }
+  return FGV_OK;
+}
+
+int fgv_mvcc_last_stats(fgv_ctx *c, double *lookup_ms, double *total_ms, uint64_t *reads, uint64_t *writes,
+                        uint32_t *rounds) {
+  if (!c) return FGV_EINVAL;
+  if (lookup_ms) *lookup_ms = c->t_mvcc_lookup;
+  if (total_ms) *total_ms = c->t_mvcc_total;
+  if (reads) *reads = c->n_mvcc_reads;
+  if (writes) *writes = c->n_mvcc_writes;
+  if (rounds) *rounds = c->mv ? c->mv->last_rounds : 0;
+  return FGV_OK;
+}
+
+}  // extern "C"

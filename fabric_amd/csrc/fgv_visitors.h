@@ -1,0 +1,377 @@
+// fgv_visitors.h -- pbwire visitors for the Fabric messages on the committer path (one
+// struct per message; field numbers from vendor/github.com/hyperledger/fabric-protos-go,
+// SURVEY.md Appendix B).  Shared by the committer (fgv_block.cpp) and MVCC (fgv_mvcc.cpp).
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "pbwire.h"
+
+using pbw::Span;
+
+namespace fgvb {
+
+// ------------------------------------------------------------------ small helpers
+inline uint64_t hash_bytes(const uint8_t *p, size_t n, uint64_t h = 0x9E3779B97F4A7C15ull) {
+  for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001B3ull;
+  return h ^ (h >> 29);
+}
+
+// ------------------------------------------------------------------ message visitors
+struct VEnvelope {
+  Span payload, signature;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? payload : signature) = s; return true; }
+};
+struct VHeader {
+  Span channel_header, signature_header;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? channel_header : signature_header) = s; return true; }
+};
+struct VPayload {
+  pbw::MsgField header;
+  Span data;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_MSG : n == 2 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) header.add(s); else data = s;
+    return true;
+  }
+};
+struct VTimestamp {  // google.protobuf.Timestamp {seconds int64 = 1, nanos int32 = 2}
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_VARINT : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VChannelHeader {
+  int32_t type = 0;
+  uint64_t epoch = 0;
+  Span channel_id, tx_id, extension;
+  pbw::Kind kind(uint32_t n) {
+    switch (n) {
+      case 1: case 2: case 6: return pbw::K_VARINT;
+      case 3: return pbw::K_MSG;
+      case 4: case 5: return pbw::K_STRING;
+      case 7: case 8: return pbw::K_BYTES;
+      default: return pbw::K_NONE;
+    }
+  }
+  void on_varint(uint32_t n, uint64_t v) {
+    if (n == 1) type = pbw::as_int32(v);
+    else if (n == 6) epoch = v;
+  }
+  bool on_len(uint32_t n, Span s) {
+    if (n == 3) { VTimestamp t; return pbw::decode(s.p, s.n, t); }
+    if (n == 4) channel_id = s;
+    else if (n == 5) tx_id = s;
+    else if (n == 7) extension = s;
+    return true;
+  }
+};
+struct VSignatureHeader {
+  Span creator, nonce;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? creator : nonce) = s; return true; }
+};
+struct VTransactionAction {
+  Span header, payload;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? header : payload) = s; return true; }
+};
+struct VTransaction {
+  std::vector<VTransactionAction> actions;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    VTransactionAction a;
+    if (!pbw::decode(s.p, s.n, a)) return false;
+    actions.push_back(a);
+    return true;
+  }
+};
+struct VEndorsement {
+  Span endorser, signature;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? endorser : signature) = s; return true; }
+};
+struct VEndorsedAction {
+  Span prp;
+  std::vector<VEndorsement> ends;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { prp = s; return true; }
+    VEndorsement e;
+    if (!pbw::decode(s.p, s.n, e)) return false;
+    ends.push_back(e);
+    return true;
+  }
+};
+struct VCcActionPayload {
+  Span ccpp;
+  bool has_action = false;
+  VEndorsedAction action;  // all occurrences merged in order
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { ccpp = s; return true; }
+    has_action = true;
+    return pbw::decode(s.p, s.n, action);
+  }
+};
+struct VPrp {
+  Span proposal_hash, extension;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? proposal_hash : extension) = s; return true; }
+};
+struct VChaincodeID {
+  Span path, name, version;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_STRING : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? path : n == 2 ? name : version) = s; return true; }
+};
+struct VResponse {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_VARINT : n == 2 ? pbw::K_STRING : n == 3 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VCcAction {
+  Span results, events;
+  bool has_ccid = false;
+  VChaincodeID ccid;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_BYTES : (n == 3 || n == 4) ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { results = s; return true; }
+    if (n == 2) { events = s; return true; }
+    if (n == 3) { VResponse r; return pbw::decode(s.p, s.n, r); }
+    has_ccid = true;
+    return pbw::decode(s.p, s.n, ccid);
+  }
+};
+struct VHdrExt {  // ChaincodeHeaderExtension {chaincode_id = 2}
+  bool has_ccid = false;
+  VChaincodeID ccid;
+  pbw::Kind kind(uint32_t n) { return n == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) { has_ccid = true; return pbw::decode(s.p, s.n, ccid); }
+};
+struct VCcEvent {
+  Span chaincode_id;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_STRING : n == 4 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { if (n == 1) chaincode_id = s; return true; }
+};
+// --- rwset (validated in full; the committer only needs namespaces + write presence)
+struct VVersion {
+  uint64_t block = 0, tx = 0;
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_VARINT : pbw::K_NONE; }
+  void on_varint(uint32_t n, uint64_t v) { (n == 1 ? block : tx) = v; }
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VKVRead {
+  Span key;
+  bool has_ver = false;
+  VVersion ver;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { key = s; return true; }
+    has_ver = true;
+    return pbw::decode(s.p, s.n, ver);
+  }
+};
+struct VQueryReads {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) { VKVRead r; return pbw::decode(s.p, s.n, r); }
+};
+struct VMerkle {
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 2) ? pbw::K_VARINT : n == 3 ? pbw::K_REP_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VRangeQuery {
+  pbw::Kind kind(uint32_t n) {
+    return (n == 1 || n == 2) ? pbw::K_STRING : n == 3 ? pbw::K_VARINT : (n == 4 || n == 5) ? pbw::K_MSG : pbw::K_NONE;
+  }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 4) { VQueryReads q; return pbw::decode(s.p, s.n, q); }
+    if (n == 5) { VMerkle m; return pbw::decode(s.p, s.n, m); }
+    return true;
+  }
+};
+struct VKVWrite {
+  Span key, value;
+  bool is_delete = false;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_VARINT : n == 3 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { is_delete = v != 0; }
+  bool on_len(uint32_t n, Span s) { (n == 1 ? key : value) = s; return true; }
+};
+struct VMetaEntry {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VMetaWrite {  // KVMetadataWrite {key string=1, entries=2}
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) return true;
+    VMetaEntry e;
+    return pbw::decode(s.p, s.n, e);
+  }
+};
+struct VKVRWSet {
+  uint32_t nreads = 0, nrq = 0, nwrites = 0, nmeta = 0;
+  std::vector<VKVRead> *reads = nullptr;     // optional capture (MVCC)
+  std::vector<VKVWrite> *writes = nullptr;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 4) ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) {
+      VKVRead r;
+      if (!pbw::decode(s.p, s.n, r)) return false;
+      nreads++;
+      if (reads) reads->push_back(r);
+      return true;
+    }
+    if (n == 2) { nrq++; VRangeQuery q; return pbw::decode(s.p, s.n, q); }
+    if (n == 3) {
+      VKVWrite w;
+      if (!pbw::decode(s.p, s.n, w)) return false;
+      nwrites++;
+      if (writes) writes->push_back(w);
+      return true;
+    }
+    nmeta++;
+    VMetaWrite m;
+    return pbw::decode(s.p, s.n, m);
+  }
+};
+struct VHashRead {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) return true;
+    VVersion v;
+    return pbw::decode(s.p, s.n, v);
+  }
+};
+struct VHashWrite {
+  pbw::Kind kind(uint32_t n) { return (n == 1 || n == 3) ? pbw::K_BYTES : (n == 2 || n == 4) ? pbw::K_VARINT : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VHashMeta {
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) return true;
+    VMetaEntry e;
+    return pbw::decode(s.p, s.n, e);
+  }
+};
+struct VHashedRWSet {
+  uint32_t nreads = 0, nwrites = 0, nmeta = 0;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { nreads++; VHashRead r; return pbw::decode(s.p, s.n, r); }
+    if (n == 2) { nwrites++; VHashWrite w; return pbw::decode(s.p, s.n, w); }
+    nmeta++;
+    VHashMeta m;
+    return pbw::decode(s.p, s.n, m);
+  }
+};
+struct VCollHashed {
+  Span name, hashed;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : (n == 2 || n == 3) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) name = s;
+    else if (n == 2) hashed = s;
+    return true;
+  }
+};
+struct VNsRwSet {
+  Span ns, rwset;
+  std::vector<VCollHashed> coll;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_BYTES : n == 3 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { ns = s; return true; }
+    if (n == 2) { rwset = s; return true; }
+    VCollHashed c;
+    if (!pbw::decode(s.p, s.n, c)) return false;
+    coll.push_back(c);
+    return true;
+  }
+};
+struct VTxRwSet {
+  std::vector<VNsRwSet> ns;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_VARINT : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    VNsRwSet r;
+    if (!pbw::decode(s.p, s.n, r)) return false;
+    ns.push_back(std::move(r));
+    return true;
+  }
+};
+struct VSerializedIdentity {
+  Span mspid, id_bytes;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? mspid : id_bytes) = s; return true; }
+};
+struct VBlockData {
+  std::vector<Span> data;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_REP_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) { data.push_back(s); return true; }
+};
+struct VSkipMsg {  // BlockHeader / BlockMetadata: validated, contents unused
+  uint32_t rep_bytes_field = 0;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? (rep_bytes_field ? pbw::K_REP_BYTES : pbw::K_VARINT) : (n == 2 || n == 3) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VBlock {
+  VBlockData data;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 2) return pbw::decode(s.p, s.n, data);
+    VSkipMsg m;
+    m.rep_bytes_field = (n == 3);
+    return pbw::decode(s.p, s.n, m);
+  }
+};
+
+// --- policies
+struct VMSPRole {
+  Span mspid;
+  int32_t role = 0;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_VARINT : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { role = pbw::as_int32(v); }
+  bool on_len(uint32_t, Span s) { mspid = s; return true; }
+};
+struct VPrincipal {
+  int32_t cls = 0;
+  Span principal;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_VARINT : n == 2 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { cls = pbw::as_int32(v); }
+  bool on_len(uint32_t, Span s) { principal = s; return true; }
+};
+
+}  // namespace fgvb
+

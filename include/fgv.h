@@ -157,6 +157,30 @@ int fgv_validate_shard(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *block
 int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *results,
                        uint8_t *flags);
 
+/* ------------------------------------------------------------------------------ MVCC */
+
+/* Committed-state cache on the GPU (statedb GetVersion, stateleveldb.go:128-137): an
+ * open-addressing table of (namespace, key) -> version Height{blockNum, txNum}, exact key
+ * compare.  It is a cache of the state DB, loaded from it at start (fgv_statedb_load) and
+ * kept current by fgv_mvcc_validate_block(..., commit=1); the DB stays authoritative.
+ *   slots: table capacity (rounded up to a power of two, load factor kept <= 0.7)
+ *   arena_bytes: capacity for key bytes */
+int fgv_statedb_init(fgv_ctx *ctx, uint64_t slots, uint64_t arena_bytes);
+int fgv_statedb_load(fgv_ctx *ctx, const char *ns, const uint8_t *key_buf, const uint64_t *key_off,
+                     const uint32_t *key_len, const uint64_t *blk, const uint64_t *txn, size_t n);
+
+/* MVCC validation of one block (txmgmt/validation/batch_preparer.go:72-119 +
+ * validator.go:81-200): `flags` holds the committer's TxValidationFlags (ntx bytes) and is
+ * updated in place -- committer-invalid txs are skipped, others become NIL_TXACTION(16),
+ * INVALID_OTHER_REASON(255), MVCC_READ_CONFLICT(11) or stay VALID.  commit != 0 then applies
+ * the valid write sets to the state cache at Height{block_num, txIdx}.  d_block: optional
+ * device copy of the block bytes.  Range queries, private data and metadata writes return
+ * FGV_EUNSUPPORTED. */
+int fgv_mvcc_validate_block(fgv_ctx *ctx, const uint8_t *block, size_t len, const uint8_t *d_block,
+                            uint64_t block_num, uint8_t *flags, size_t ntx, int commit);
+int fgv_mvcc_last_stats(fgv_ctx *ctx, double *lookup_ms, double *total_ms, uint64_t *reads,
+                        uint64_t *writes, uint32_t *rounds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,76 @@
+"""GPU parity of MVCC: flags and the committed state after each block match the oracle."""
+import numpy as np
+import pytest
+
+from fabric_amd import _lib
+from fabric_amd.synth import mvcc as M
+from oracle import mvcc as OM
+from tests.test_oracle_mvcc import _blk, _db, _tx
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(st, slots=1 << 20):
+    eng = _lib.Engine(0)
+    eng.statedb_init(slots, 32 << 20)
+    keys, blk, txn = st.items()
+    eng.statedb_load("mycc", keys, blk, txn)
+    return eng
+
+
+def test_blocks_match_oracle_and_labels():
+    st = M.MvccState(100_000, seed=4)
+    db = _db(st)
+    eng = _engine(st)
+    for b in range(4):
+        blk, labels, flags = M.make_block(st, 3000, number=1001 + b, seed=10 + b)
+        exp = OM.validate_block(db, blk, flags, 1001 + b, commit=True)
+        got = eng.mvcc_validate(blk, 1001 + b, flags, commit=True)
+        assert list(got) == list(exp) == list(labels)
+    eng.close()
+
+
+def test_known_answers_and_chains():
+    db = OM.StateDB({("ns1", "key%d" % i): (1, i - 1) for i in range(1, 6)})
+    eng = _lib.Engine(0)
+    eng.statedb_init(1 << 12, 1 << 20)
+    eng.statedb_load("ns1", ["key%d" % i for i in range(1, 6)], [1] * 5, list(range(5)))
+    envs = [
+        _tx([("key1", (1, 0)), ("key2", (1, 1))], [("key2", b"v", False)]),
+        _tx([("key2", (1, 1))], []),
+        _tx([("key3", (1, 0))], []),
+        _tx([("key9", None)], [("key4", b"v", False)]),
+        _tx([("key4", (1, 3))], []),
+        _tx([("key5", None)], []),
+        # chain: tx7 writes k, tx8 (invalid: stale) writes m, tx9 reads m -> valid, tx10 reads k -> 11
+        _tx([("key1", (1, 0))], [("kk", b"v", False)]),
+        _tx([("key3", (9, 9))], [("mm", b"v", False)]),
+        _tx([("mm", None)], [("nn", b"v", True)]),
+        _tx([("kk", None)], []),
+        _tx([("nn", None)], []),   # nn deleted by tx 8 (valid) -> in updates -> 11
+    ]
+    blk = _blk(envs)
+    exp = OM.validate_block(db, blk, [0] * len(envs), 2, commit=True)
+    got = eng.mvcc_validate(blk, 2, [0] * len(envs), commit=True)
+    assert list(got) == exp
+    # second block reads the committed heights written by block 2
+    envs2 = [_tx([("key2", (2, 0)), ("key4", (2, 3)), ("kk", (2, 6))], []), _tx([("key2", (1, 1))], []),
+             _tx([("nn", None)], [])]
+    blk2 = _blk(envs2)
+    assert list(eng.mvcc_validate(blk2, 3, [0] * 3)) == OM.validate_block(db, blk2, [0] * 3, 3, commit=True)
+    eng.close()
+
+
+def test_long_dependency_chain():
+    """tx i reads the key written by tx i-1: alternating validity -> many fixpoint rounds."""
+    db = OM.StateDB({("ns1", "c0"): (1, 0)})
+    eng = _lib.Engine(0)
+    eng.statedb_init(1 << 12, 1 << 20)
+    eng.statedb_load("ns1", ["c0"], [1], [0])
+    envs = [_tx([("c%d" % i, (1, 0) if i == 0 else None)], [("c%d" % (i + 1), b"v", False)]) for i in range(40)]
+    blk = _blk(envs)
+    exp = OM.validate_block(db, blk, [0] * 40, 2, commit=False)
+    got = eng.mvcc_validate(blk, 2, [0] * 40, commit=False)
+    assert list(got) == exp
+    assert eng.mvcc_stats()["rounds"] >= 10
+    eng.close()

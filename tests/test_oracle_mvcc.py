@@ -1,0 +1,60 @@
+"""CPU: restated MVCC (oracle/mvcc.py) against the generator's labels over consecutive
+committed blocks, plus the known-answer cases of the reference's own test
+(core/ledger/kvledger/txmgmt/validation/validator_test.go:197-238 TestValidator)."""
+import numpy as np
+
+from fabric_amd.synth import blocks as B
+from fabric_amd.synth import mvcc as M
+from oracle import mvcc as OM
+
+
+def _db(st):
+    keys, blk, txn = st.items()
+    return OM.StateDB({("mycc", k): (int(b), int(x)) for k, b, x in zip(keys, blk, txn)})
+
+
+def test_labels_over_consecutive_blocks():
+    st = M.MvccState(50_000, seed=4)
+    db = _db(st)
+    for b in range(3):
+        blk, labels, flags = M.make_block(st, 1500, number=1001 + b, seed=b)
+        out = OM.validate_block(db, blk, flags, 1001 + b, commit=True)
+        assert list(out) == list(labels)
+        assert 11 in out
+
+
+def _tx(reads, writes):
+    return M._envelope(B.tx_rwset([("ns1", B.kv_rwset(reads, writes))]), 0, 1)
+
+
+def _blk(envs):
+    from tests.blockfix import block_from_envs
+    return block_from_envs(envs)
+
+
+def test_reference_known_answers():
+    """TestValidator shape: key1..key5 committed at Height{1,0..4}; reads at wrong / nil
+    versions and an intra-block write->read conflict."""
+    db = OM.StateDB({("ns1", "key%d" % i): (1, i - 1) for i in range(1, 6)})
+    envs = [
+        _tx([("key1", (1, 0)), ("key2", (1, 1))], [("key2", b"v", False)]),   # valid
+        _tx([("key2", (1, 1))], []),                                           # reads key2 written above -> 11
+        _tx([("key3", (1, 0))], []),                                           # wrong version -> 11
+        _tx([("key9", None)], [("key4", b"v", False)]),                        # absent key read as nil -> valid
+        _tx([("key4", (1, 3))], []),                                           # key4 written by tx 3 -> 11
+        _tx([("key5", None)], []),                                             # nil but committed -> 11
+    ]
+    out = OM.validate_block(db, _blk(envs), [0] * 6, 2, commit=True)
+    assert out == [0, 11, 11, 0, 11, 11]
+    assert db.get_version("ns1", "key2") == (2, 0) and db.get_version("ns1", "key4") == (2, 3)
+
+
+def test_skips_committer_invalid_and_nil_action():
+    import pytest
+    from oracle.v20 import Unsupported
+    db = OM.StateDB({("ns1", "a"): (1, 0)})
+    envs = [_tx([("a", (1, 0))], [("a", b"x", False)]), _tx([("a", (1, 0))], []), b"\x0a\x00"]
+    out = OM.validate_block(db, _blk(envs), [10, 0, 3], 2)
+    assert out == [10, 0, 3]  # the invalid tx's write is not in updates
+    with pytest.raises(Unsupported):  # a committer-VALID tx without header: the reference panics
+        OM.validate_block(db, _blk(envs), [10, 0, 0], 2)
