@@ -1,0 +1,105 @@
+"""Summarise rocprofv3 CSVs (tools/profile_round.sh output) into profiles/<round>_*.
+
+usage: python tools/summarize_profiles.py gpurun_out/prof round1
+Writes profiles/<round>_{block,sig,mvcc}_kernel_stats.csv (copies) and
+profiles/<round>_profile_summary.md (per-kernel durations, VALU counters, HBM bytes).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+SIMDS = 256 * 4          # MI355X: 256 CUs x 4 SIMDs
+XCDS = 8
+PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 78.6 T full-rate 32-bit lane-ops/s
+HBM_PEAK = 8.0e12
+
+
+def kernel_stats(path):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        out[r["Name"].split("(")[0]] = dict(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3,
+                                            pct=float(r["Percentage"]))
+    return out
+
+
+def pmc(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    n = collections.Counter()
+    dur = collections.defaultdict(float)
+    grid = {}
+    seen = set()
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0]
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        n[(k, r["Counter_Name"])] += 1
+        if (k, r["Dispatch_Id"]) not in seen:
+            seen.add((k, r["Dispatch_Id"]))
+            dur[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e9
+            grid[k] = int(r["Grid_Size"])
+    res = {}
+    for k, v in agg.items():
+        d = len([1 for kk, _ in seen if kk == k])
+        res[k] = dict(dispatches=d, avg_s=dur[k] / max(d, 1), grid=grid[k],
+                      **{c: x / max(d, 1) for c, x in v.items()})
+    return res
+
+
+def main(src, rnd):
+    os.makedirs("profiles", exist_ok=True)
+    lines = [f"# rocprofv3 summary — {rnd}", "",
+             "Collected by `tools/profile_round.sh` (kernel-trace/stats runs and separate `--pmc` runs, "
+             "as MI355X_MICROARCH.md prescribes).  Profiled runs clock lower than un-profiled ones "
+             "(DVFS), so durations here read a few % above the bench's live HIP-event numbers.", ""]
+    for wl in ("block", "sig", "mvcc"):
+        p = os.path.join(src, wl, "run_kernel_stats.csv")
+        if not os.path.exists(p):
+            continue
+        shutil.copy(p, f"profiles/{rnd}_{wl}_kernel_stats.csv")
+        js = os.path.join(src, wl + ".json")
+        bench = json.load(open(js)) if os.path.exists(js) and os.path.getsize(js) else {}
+        lines += [f"## {wl} workload", "", f"bench line (profiled run): value={bench.get('value')} {bench.get('unit')}, "
+                  f"stage_ms={bench.get('stage_ms')}", "", "| kernel | calls | avg µs | % of GPU time |", "|---|---|---|---|"]
+        for k, v in sorted(kernel_stats(p).items(), key=lambda kv: -kv[1]["pct"]):
+            lines.append(f"| {k[:60]} | {v['calls']} | {v['avg_us']:.1f} | {v['pct']:.1f} |")
+        lines.append("")
+    p = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
+    if os.path.exists(p):
+        lines += ["## VALU counters (sig workload: 131,072 verifies per dispatch)", "",
+                  "| kernel | avg µs | VALU wave-insts | INT32 | INT64 | lane-ops/s | % of 78.6 T full-rate peak | VALU busy % |",
+                  "|---|---|---|---|---|---|---|---|"]
+        for k, v in pmc(p).items():
+            if not k.startswith("k_"):
+                continue
+            lane = v.get("SQ_INSTS_VALU", 0) * 64 / v["avg_s"] if v["avg_s"] else 0
+            gui = v.get("GRBM_GUI_ACTIVE", 0) / XCDS
+            busy = 100 * v.get("SQ_ACTIVE_INST_VALU", 0) * 4 / SIMDS / gui if gui else 0
+            lines.append(f"| {k} | {v['avg_s'] * 1e6:.1f} | {v.get('SQ_INSTS_VALU', 0):.4g} | "
+                         f"{v.get('SQ_INSTS_VALU_INT32', 0):.3g} | {v.get('SQ_INSTS_VALU_INT64', 0):.3g} | {lane:.3g} | "
+                         f"{100 * lane / PEAK_LANE_OPS:.1f} | {busy:.0f} |")
+        kp = pmc(p).get("k_point")
+        if kp:
+            lines += ["", f"k_point: {kp.get('SQ_INSTS_VALU', 0) / (131072 / 64):,.0f} VALU instructions per verify "
+                          f"(one lane = one verify).", ""]
+        lines += ["VALU busy % = 100·SQ_ACTIVE_INST_VALU·4 / SIMDs / (GRBM_GUI_ACTIVE/8) (gfx94x formula; "
+                  "ROCm 7.2 ships no gfx950 derived-counter section).", ""]
+    for name, ctr in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+        p = os.path.join(src, name, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        lines += [f"## {ctr} (mvcc workload, per dispatch)", "", "| kernel | avg µs | KB | GB/s |", "|---|---|---|---|"]
+        for k, v in pmc(p).items():
+            if not k.startswith("k_mv"):
+                continue
+            kb = v.get(ctr, 0) * (2 if ctr == "FETCH_SIZE" else 1)  # gfx950: FETCH_SIZE reads 1/2
+            lines.append(f"| {k} | {v['avg_s'] * 1e6:.1f} | {kb:.1f} | {kb * 1024 / v['avg_s'] / 1e9 if v['avg_s'] else 0:.1f} |")
+        lines += ["", "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 reports ½ of wide streaming reads); "
+                  "small MVCC gathers are uncalibrated, and a 1M-key table (32 MB) is Infinity-Cache resident.", ""]
+    open(f"profiles/{rnd}_profile_summary.md", "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
