@@ -110,14 +110,18 @@ def run_block(args, world, rank, local, dev):
     ntx = np.array([T] * len(blks), dtype=np.int64)
     lo, hi = shard.shard_ranges(ntx, rank, world)
     rows = shard.padded_rows(ntx, world)
-    recv = torch.empty((world * rows, shard.REC), dtype=torch.uint8, device=dev) if world > 1 else None
+    # records stay in HBM: shard validation -> all-gather (RCCL) -> device finalize
+    send = torch.zeros((rows, shard.REC), dtype=torch.uint8, device=dev)
+    recv = torch.zeros((world * rows, shard.REC), dtype=torch.uint8, device=dev) if world > 1 else send
+    batch = eng.block_batch(blks, dptr)
+    flags_out = np.empty(int(ntx.sum()), dtype=np.uint8)
     torch.cuda.synchronize()
 
     def step():
-        res, nt = eng.validate_shard(blks, lo, hi, dptr)
-        full = shard.allgather_results(res, nt, world, device=dev, out=recv) if world > 1 else res
-        flags = _lib.finalize_flags(nt, full)
-        return flags
+        nt = eng.validate_shard_dev(batch, lo, hi, send.data_ptr(), rows)
+        if world > 1:
+            shard.allgather_device(send, recv)
+        return eng.finalize_flags_dev(nt, world, rows, recv.data_ptr(), out=flags_out)
 
     flags = None
     for _ in range(args.warmup):
@@ -132,10 +136,13 @@ def run_block(args, world, rank, local, dev):
         dist.barrier()
     torch.cuda.synchronize()
     acc = dict(point=0.0, prep=0.0, sha=0.0, verifies=0, sha_blocks=0)
+    host = dict(parse_ms=0.0, assemble_ms=0.0, device_ms=0.0, fold_ms=0.0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         tm, cn = eng.timing(), eng.counts()
+        for k, v in eng.host_timing().items():
+            host[k] += v
         acc["point"] += tm["point_ms"]
         acc["prep"] += tm["prep_ms"]
         acc["sha"] += tm["sha_ms"]
@@ -168,6 +175,7 @@ def run_block(args, world, rank, local, dev):
                stage_ms=dict(sha=round(acc["sha"] / args.steps, 4), prep=round(acc["prep"] / args.steps, 4),
                              point=round(acc["point"] / args.steps, 4)),
                sha256_compressions_per_step=int(acc["sha_blocks"] / args.steps),
+               host_ms={k: round(v / args.steps, 3) for k, v in host.items()},
                roofline=roofline(acc["verifies"] / args.steps, acc["point"] / args.steps), cpu_baseline=None)
     if rank == 0 and world == 1 and args.cpu_threads > 0:
         # crypto-bound upper bound of the reference's CPU committer on this host: every

@@ -16,10 +16,12 @@ LIB_PATH = os.path.join(_HERE, "libfgv.so")
 SIG_VALID, SIG_FALSE, SIG_DER, SIG_HIGH_S, SIG_RANGE, SIG_BADKEY, SIG_EMPTY = range(7)
 
 EXPORTED = [
-    "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_last_counts", "fgv_sha256_batch",
+    "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_last_counts", "fgv_last_host_timing",
+    "fgv_sha256_batch",
     "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
+    "fgv_validate_shard_dev", "fgv_finalize_flags_dev",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
 ]
 TX_RESULT_BYTES = 68
@@ -67,6 +69,7 @@ def load():
         L.fgv_strerror.restype = ctypes.c_char_p
         L.fgv_last_timing.argtypes = [vp] + [ctypes.POINTER(ctypes.c_double)] * 4
         L.fgv_last_counts.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 3
+        L.fgv_last_host_timing.argtypes = [vp] + [ctypes.POINTER(ctypes.c_double)] * 4
         L.fgv_sha256_batch.argtypes = [vp, vp, sz, vp, vp, sz, vp]
         L.fgv_p256_verify_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp]
         L.fgv_p256_verify_msgs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
@@ -80,6 +83,8 @@ def load():
         L.fgv_validate_blocks.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp]
         L.fgv_validate_shard.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
         L.fgv_finalize_flags.argtypes = [sz, vp, vp, vp]
+        L.fgv_validate_shard_dev.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
+        L.fgv_finalize_flags_dev.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
         L.fgv_mvcc_validate_block.argtypes = [vp, vp, sz, vp, ctypes.c_uint64, vp, sz, ctypes.c_int]
@@ -111,6 +116,16 @@ def pack(blobs):
     return np.ascontiguousarray(arena), offs, lens
 
 
+class _BlockBatch:
+    def __init__(self, blocks, d_blocks):
+        self.nb = len(blocks)
+        self._bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+        self.ptrs = (ctypes.c_void_p * self.nb)(*[b.ctypes.data for b in self._bufs])
+        self.lens = (ctypes.c_size_t * self.nb)(*[len(b) for b in blocks])
+        self.dptr = (ctypes.c_void_p * self.nb)(*d_blocks) if d_blocks is not None else None
+        self.ntx = (ctypes.c_size_t * self.nb)()
+
+
 class Engine:
     """One libfgv context = one GPU (one process per GPU)."""
 
@@ -136,6 +151,11 @@ class Engine:
         v = [ctypes.c_double() for _ in range(4)]
         _check(self._L.fgv_last_timing(self._h, *[ctypes.byref(x) for x in v]))
         return dict(zip(("sha_ms", "prep_ms", "point_ms", "keytab_ms"), (x.value for x in v)))
+
+    def host_timing(self):
+        v = [ctypes.c_double() for _ in range(4)]
+        _check(self._L.fgv_last_host_timing(self._h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("parse_ms", "assemble_ms", "device_ms", "fold_ms"), (x.value for x in v)))
 
     def counts(self):
         v = [ctypes.c_uint64() for _ in range(3)]
@@ -239,6 +259,29 @@ class Engine:
         _check(self._L.fgv_validate_shard(self._h, nb, ptrs, lens, dptr, _ptr(lo), _ptr(hi), _ptr(res), cap, ntx))
         return res[:cap], np.array(list(ntx), dtype=np.uint64)
 
+
+    def block_batch(self, blocks, d_blocks=None):
+        """Pre-packed ctypes arguments for a batch validated repeatedly (bench loop)."""
+        return _BlockBatch(blocks, d_blocks)
+
+    def validate_shard_dev(self, batch, tx_lo, tx_hi, d_results, cap):
+        """fgv_validate_shard_dev: records (68 B each) written to device address d_results.
+        batch: block_batch(...) or a list of blocks.  Returns ntx per block (uint64)."""
+        if not isinstance(batch, _BlockBatch):
+            batch = _BlockBatch(batch, None)
+        lo = np.ascontiguousarray(tx_lo, dtype=np.uint32)
+        hi = np.ascontiguousarray(tx_hi, dtype=np.uint32)
+        _check(self._L.fgv_validate_shard_dev(self._h, batch.nb, batch.ptrs, batch.lens, batch.dptr, _ptr(lo),
+                                              _ptr(hi), ctypes.c_void_p(d_results), cap, batch.ntx))
+        return np.ctypeslib.as_array(batch.ntx).astype(np.uint64)
+
+    def finalize_flags_dev(self, ntx, world, rows_per_rank, d_gathered, out=None):
+        """fgv_finalize_flags_dev over world x rows_per_rank gathered records at d_gathered."""
+        ntx = np.ascontiguousarray(ntx, dtype=np.uint64)
+        flags = out if out is not None else np.empty(int(ntx.sum()), dtype=np.uint8)
+        _check(self._L.fgv_finalize_flags_dev(self._h, len(ntx), _ptr(ntx), world, rows_per_rank,
+                                              ctypes.c_void_p(d_gathered), _ptr(flags)))
+        return flags
 
     # --- MVCC
     def statedb_init(self, slots=1 << 22, arena_bytes=64 << 20):

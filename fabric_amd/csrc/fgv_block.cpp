@@ -23,10 +23,13 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -47,6 +50,7 @@ struct Ident {
   int32_t key_slot = -1;  // -1: not a P-256 key (Verify errors)
   bool valid = false;     // msp Validate() result
   uint32_t canon = 0;     // dedup identity id: Mspid + Id (Id = hex SHA-256(cert))
+  int32_t msp = -1;       // interned Mspid (Channel::intern)
 };
 
 struct PNode {
@@ -61,6 +65,7 @@ struct Policy {
   int root = -1;
   std::vector<std::string> principal_msp;  // "" + bad flag for undecodable principal
   std::vector<bool> principal_bad;
+  std::vector<int32_t> principal_mspi;     // interned principal_msp, -1 for a bad principal
 };
 
 // SignaturePolicy decoding into the node list (recursive, oneof: last member wins)
@@ -201,9 +206,20 @@ struct Channel {
   std::vector<Ident> idents;
   std::unordered_multimap<uint64_t, uint32_t> ident_index;
   std::unordered_map<std::string, uint32_t> canon_ids;
+  std::unordered_map<std::string, int32_t> msp_ids;  // Mspid interning (policy principals, idents)
   std::vector<Policy> policies;
   std::unordered_map<std::string, int> chaincodes;  // namespace -> policies index
-  std::unordered_set<std::string> committed;
+  std::deque<std::string> committed_store;          // ledger txids (stable storage)
+  std::unordered_set<std::string_view> committed;
+
+  int32_t intern(const std::string &msp) {
+    auto it = msp_ids.find(msp);
+    if (it == msp_ids.end()) it = msp_ids.emplace(msp, (int32_t)msp_ids.size()).first;
+    return it->second;
+  }
+  bool is_committed(const Span &txid) const {
+    return committed.count(std::string_view(reinterpret_cast<const char *>(txid.p), txid.n)) != 0;
+  }
 
   int lookup(const Span &ser) const {
     VSerializedIdentity sid;
@@ -242,10 +258,23 @@ struct TxRec {
   std::vector<int> policies;  // chaincode policy per written namespace (-1 unknown chaincode)
   std::vector<EndRec> ends;
   uint32_t cjob = UINT32_MAX, txid_job = UINT32_MAX, prop_job = UINT32_MAX, cvjob = UINT32_MAX;
-  std::string index_txid;  // GetOrComputeTxIDFromEnvelope (txid index), "" on error
-  bool index_ok = false;
+  Span index_txid;         // GetOrComputeTxIDFromEnvelope (txid index): chdr.TxId when non-empty
+  bool index_ok = false;   // index entry exists (chdr.TxId, or computed on the device)
   Span idx_nonce, idx_creator;  // for the computed txid when chdr.TxId is empty
   uint32_t index_job = UINT32_MAX;
+  // device job counts of this tx, by kind (filled after parsing; see the assembly stage)
+  uint8_t n_cj = 0, n_tj = 0, n_pj = 0, n_ij = 0;
+  uint16_t n_ej = 0;
+
+  void reset() {  // keep the vectors' capacity across calls
+    std::vector<int> p = std::move(policies);
+    std::vector<EndRec> e = std::move(ends);
+    *this = TxRec();
+    p.clear();
+    e.clear();
+    policies = std::move(p);
+    ends = std::move(e);
+  }
 };
 
 }  // namespace fgvb
@@ -287,6 +316,22 @@ struct ThreadPool {
     cv.notify_all();
     for (auto &t : th) t.join();
   }
+  // run f(j) for every job j in [0, njobs) on the pool (dynamic assignment)
+  void run(size_t nj, const std::function<void(size_t)> &f) {
+    if (nj == 0) return;
+    if (th.empty() || nj == 1) {
+      for (size_t i = 0; i < nj; i++) f(i);
+      return;
+    }
+    std::unique_lock<std::mutex> lk(mu);
+    job = f;
+    njobs = nj;
+    next = 0;
+    active = th.size();
+    gen++;
+    cv.notify_all();
+    done_cv.wait(lk, [&] { return active == 0; });
+  }
   // run f(i) for i in [0, n) in chunks
   void parallel_for(size_t n, const std::function<void(size_t)> &f) {
     if (n == 0) return;
@@ -295,18 +340,10 @@ struct ThreadPool {
       return;
     }
     const size_t chunk = std::max<size_t>(16, n / (th.size() * 8));
-    const size_t nchunks = (n + chunk - 1) / chunk;
-    std::unique_lock<std::mutex> lk(mu);
-    job = [&](size_t c) {
+    run((n + chunk - 1) / chunk, [&](size_t c) {
       size_t lo = c * chunk, hi = std::min(n, lo + chunk);
       for (size_t i = lo; i < hi; i++) f(i);
-    };
-    njobs = nchunks;
-    next = 0;
-    active = th.size();
-    gen++;
-    cv.notify_all();
-    done_cv.wait(lk, [&] { return active == 0; });
+    });
   }
 };
 
@@ -326,7 +363,7 @@ void fgv_block_state_free(fgv_block_state *s) { delete s; }
 
 // ======================================================================= parsing
 static void parse_tx(const Channel &ch, Span d, TxRec &R) {
-  R = TxRec();
+  R.reset();
   VEnvelope env;
   if (!pbw::decode(d.p, d.n, env)) { R.pre = C_OTHER; return; }
   VPayload pl;
@@ -340,7 +377,7 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
     VChannelHeader c0;
     if (pbw::decode(hdr.channel_header.p, hdr.channel_header.n, c0)) {
       if (c0.tx_id.n) {
-        R.index_txid = c0.tx_id.str();
+        R.index_txid = c0.tx_id;
         R.index_ok = true;
       } else {
         VSignatureHeader s0;
@@ -409,15 +446,18 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
   if (!pbw::decode(prp.extension.p, prp.extension.n, cca)) { R.disp = C_BAD_RESP; return; }
   VTxRwSet rw;
   if (!pbw::decode(cca.results.p, cca.results.n, rw)) { R.disp = C_BAD_RWSET; return; }
-  std::vector<VKVRWSet> kvs(rw.ns.size());
-  std::vector<bool> coll_writes(rw.ns.size(), false);
+  // per namespace: 1 = writes (kv / metadata / collection), 2 = metadata or collection writes
+  pbw::SmallVec<uint8_t, 8> wflags;
   for (size_t k = 0; k < rw.ns.size(); k++) {
-    if (!pbw::decode(rw.ns[k].rwset.p, rw.ns[k].rwset.n, kvs[k])) { R.disp = C_BAD_RWSET; return; }
+    VKVRWSet kv;
+    if (!pbw::decode(rw.ns[k].rwset.p, rw.ns[k].rwset.n, kv)) { R.disp = C_BAD_RWSET; return; }
+    bool coll_writes = false;
     for (const VCollHashed &c : rw.ns[k].coll) {
       VHashedRWSet h;
       if (!pbw::decode(c.hashed.p, c.hashed.n, h)) { R.disp = C_BAD_RWSET; return; }
-      if (h.nwrites || h.nmeta) coll_writes[k] = true;
+      if (h.nwrites || h.nmeta) coll_writes = true;
     }
+    wflags.push_back((uint8_t)(((kv.nwrites || kv.nmeta || coll_writes) ? 1 : 0) | ((kv.nmeta || coll_writes) ? 2 : 0)));
   }
   if (!ext.has_ccid || !cca.has_ccid) { R.disp = C_OTHER; return; }
   const Span ccid = ext.ccid.name;
@@ -434,26 +474,25 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
       return;
     }
   }
-  std::vector<std::string> wr{ccid.str()};
-  std::unordered_set<std::string> seen;
+  // duplicate namespace -> ILLEGAL_WRITESET (any duplicate: the reference stops at the first)
+  pbw::SmallVec<Span, 8> nss;
+  for (size_t k = 0; k < rw.ns.size(); k++) nss.push_back(rw.ns[k].ns);
+  std::sort(nss.begin(), nss.end());
+  for (size_t k = 1; k < nss.size(); k++)
+    if (nss[k].eq(nss[k - 1])) { R.disp = C_ILLEGAL_WS; return; }
+  // written namespaces + the invoked chaincode; key-level / collection endorsement policies
+  // are outside the modelled state
+  pbw::SmallVec<Span, 8> wr;
+  wr.push_back(ccid);
   for (size_t k = 0; k < rw.ns.size(); k++) {
-    std::string ns = rw.ns[k].ns.str();
-    if (!seen.insert(ns).second) { R.disp = C_ILLEGAL_WS; return; }
-    bool writes = kvs[k].nwrites || kvs[k].nmeta || coll_writes[k];
-    if (writes && std::find(wr.begin(), wr.end(), ns) == wr.end()) wr.push_back(ns);
-  }
-  // key-level / collection endorsement policies are outside the modelled state
-  for (size_t k = 0; k < rw.ns.size(); k++) {
-    std::string ns = rw.ns[k].ns.str();
-    if (std::find(wr.begin(), wr.end(), ns) != wr.end() && (kvs[k].nmeta || coll_writes[k])) {
-      R.disp = C_UNSUPPORTED;
-      return;
-    }
+    if (!(wflags[k] & 1)) continue;
+    if (wflags[k] & 2) { R.disp = C_UNSUPPORTED; return; }  // (every such namespace is in wr)
+    if (!rw.ns[k].ns.eq(ccid)) wr.push_back(rw.ns[k].ns);
   }
   std::sort(wr.begin(), wr.end());
   R.disp = C_VALID;
-  for (const std::string &ns : wr) {
-    auto it = ch.chaincodes.find(ns);
+  for (const Span &ns : wr) {
+    auto it = ch.chaincodes.find(ns.str());
     R.policies.push_back(it == ch.chaincodes.end() ? -1 : it->second);
   }
   // endorsement signature set (validator_keylevel.go:246-260)
@@ -467,39 +506,60 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
 }
 
 // ======================================================================= policy fold
-static bool eval_node(const Policy &P, int node, const std::vector<int> &ids, const Channel &ch,
-                      std::vector<uint8_t> &used) {
+// cauthdsl greedy evaluation (common/cauthdsl/cauthdsl.go:24-92) over the deduplicated,
+// verified signers `ids`: SignedBy takes the first unused signer satisfying the principal;
+// NOutOf evaluates every sub-rule on a copy of `used` and keeps the copy when it succeeds.
+struct UsedBits {  // <= 64 signers
+  uint64_t w = 0;
+  bool get(size_t i) const { return (w >> i) & 1; }
+  void set(size_t i) { w |= 1ull << i; }
+};
+struct UsedVec {
+  std::vector<uint8_t> v;
+  bool get(size_t i) const { return v[i] != 0; }
+  void set(size_t i) { v[i] = 1; }
+};
+template <class U>
+static bool eval_node(const Policy &P, int node, const int *ids, size_t nids, const Channel &ch, U &used) {
   const PNode &N = P.nodes[node];
   if (N.type == 2) {
-    const bool bad = P.principal_bad[N.principal];
-    const std::string &msp = P.principal_msp[N.principal];
-    for (size_t i = 0; i < ids.size(); i++) {
-      if (used[i]) continue;
+    const int32_t msp = P.principal_mspi[N.principal];  // -1: undecodable principal
+    if (msp < 0) return false;
+    for (size_t i = 0; i < nids; i++) {
+      if (used.get(i)) continue;
       const Ident &I = ch.idents[ids[i]];
-      if (!bad && I.mspid == msp && I.valid) {
-        used[i] = 1;
+      if (I.msp == msp && I.valid) {
+        used.set(i);
         return true;
       }
     }
     return false;
   }
   int32_t verified = 0;
-  std::vector<uint8_t> tmp(used.size());
   for (int k : N.kids) {
-    tmp = used;
-    if (eval_node(P, k, ids, ch, tmp)) {
+    U tmp = used;
+    if (eval_node(P, k, ids, nids, ch, tmp)) {
       verified++;
-      used = tmp;
+      used = std::move(tmp);
     }
   }
   return verified >= N.n;
 }
+static bool eval_policy(const Policy &P, const int *ids, size_t nids, const Channel &ch) {
+  if (nids <= 64) {
+    UsedBits u;
+    return eval_node(P, P.root, ids, nids, ch, u);
+  }
+  UsedVec u;
+  u.v.assign(nids, 0);
+  return eval_node(P, P.root, ids, nids, ch, u);
+}
 
 // ======================================================================= API
-static bool hex32(const std::string &s, uint8_t out[32]) {
-  if (s.size() != 64) return false;
+static bool hex32(const Span &s, uint8_t out[32]) {
+  if (s.n != 64) return false;
   for (int k = 0; k < 64; k++) {
-    const char ch = s[k];
+    const uint8_t ch = s.p[k];
     int v;
     if (ch >= '0' && ch <= '9') v = ch - '0';
     else if (ch >= 'a' && ch <= 'f') v = ch - 'a' + 10;
@@ -510,10 +570,31 @@ static bool hex32(const std::string &s, uint8_t out[32]) {
   return true;
 }
 
+// device jobs of one parsed tx, by kind (see the assembly stage)
+static void count_jobs(const Channel &ch, TxRec &R) {
+  if (R.index_ok && R.index_txid.n == 0) R.n_ij = 1;
+  if (R.pre != C_PENDING) return;
+  R.n_cj = 1;
+  if (R.type != 3) return;
+  R.n_tj = 1;
+  if (R.etx != C_VALID) return;
+  R.n_pj = 1;
+  if (R.disp != C_VALID) return;
+  uint32_t ne = 0;
+  for (const EndRec &e : R.ends)
+    if (e.ident >= 0 && ch.idents[e.ident].key_slot >= 0) ne++;
+  R.n_ej = (uint16_t)std::min<uint32_t>(ne, 0xFFFF);
+}
+
+static inline uint32_t sha_blocks(const ShaJob &j) { return (j.n[0] + j.n[1] + j.n[2] + 8) / 64 + 1; }
+
 int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
                             const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                             const uint32_t *tx_hi, fgv_tx_result *res_out, size_t res_cap, size_t *ntx_out) {
   Channel &ch = S->ch;
+  using clk = std::chrono::steady_clock;
+  auto t_start = clk::now();
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   // --- block envelopes (shard: transactions [tx_lo[b], tx_hi[b]) of block b)
   std::vector<std::vector<Span>> envs(nblocks);
   std::vector<uint32_t> lo(nblocks), hi(nblocks);
@@ -530,89 +611,114 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   }
   if (total > res_cap) return FGV_EINVAL;
   std::vector<TxRec> &recs = S->recs;
-  recs.resize(total);
-  std::vector<size_t> base(nblocks + 1, 0);
-  for (size_t b = 0; b < nblocks; b++) base[b + 1] = base[b] + (hi[b] - lo[b]);
+  if (recs.size() < total) recs.resize(total);
   std::vector<std::pair<uint32_t, uint32_t>> where(total);
-  for (size_t b = 0; b < nblocks; b++)
-    for (size_t i = lo[b]; i < hi[b]; i++) where[base[b] + i - lo[b]] = {(uint32_t)b, (uint32_t)i};
+  for (size_t b = 0, t = 0; b < nblocks; b++)
+    for (size_t i = lo[b]; i < hi[b]; i++) where[t++] = {(uint32_t)b, (uint32_t)i};
 
-  // --- A. parse
+  // --- A. parse (every check that needs no crypto) + per-tx device job counts
   S->pool.parallel_for(total, [&](size_t t) {
-    parse_tx(ch, envs[where[t].first][where[t].second], recs[t]);
+    TxRec &R = recs[t];
+    parse_tx(ch, envs[where[t].first][where[t].second], R);
+    count_jobs(ch, R);
   });
+  c->t_host_parse = ms_since(t_start);
+  auto t_asm = clk::now();
 
-  // --- assign GPU jobs (grouped by kind: lanes of a wave hash similar lengths)
-  auto dev_addr = [&](size_t b, const Span &s) -> uint64_t {
-    return (uint64_t)(uintptr_t)d_blocks[b] + (uint64_t)(s.p - h_blocks[b]);
-  };
-  std::vector<ShaJob> jobs;
-  std::vector<uint64_t> sig_ptr;
-  std::vector<uint32_t> sig_len, key_slot, dig_idx;
-  jobs.reserve(total * 5);
-  auto add_job = [&](size_t b, std::initializer_list<Span> spans) {
-    ShaJob j{};
-    int k = 0;
-    for (const Span &s : spans) {
-      j.p[k] = s.n ? dev_addr(b, s) : 0;
-      j.n[k] = s.n;
-      k++;
+  // --- assemble device jobs, grouped by kind so the lanes of a wave hash similar lengths:
+  //     sha  [creator payload | nonce||creator | chdr||shdr||ccpp | prp||endorser | index txid]
+  //     ecdsa [creator signatures | endorsement signatures]
+  // chunked exclusive scan over the per-tx counts, then a parallel fill of pinned buffers
+  constexpr size_t CH = 256;
+  const size_t nch = (total + CH - 1) / CH;
+  std::vector<std::array<uint32_t, 5>> cbase(nch + 1);
+  S->pool.run(nch, [&](size_t k) {
+    std::array<uint32_t, 5> a{};
+    for (size_t t = k * CH, e = std::min(total, t + CH); t < e; t++) {
+      const TxRec &R = recs[t];
+      a[0] += R.n_cj; a[1] += R.n_tj; a[2] += R.n_pj; a[3] += R.n_ej; a[4] += R.n_ij;
     }
-    jobs.push_back(j);
-    return (uint32_t)(jobs.size() - 1);
-  };
-  for (size_t t = 0; t < total; t++) {  // creator payload hashes + creator verifies
-    TxRec &R = recs[t];
-    if (R.pre != C_PENDING) continue;
-    const size_t b = where[t].first;
-    R.cjob = add_job(b, {R.payload});
-    R.cvjob = (uint32_t)sig_ptr.size();
-    sig_ptr.push_back(dev_addr(b, R.env_sig));
-    sig_len.push_back(R.env_sig.n);
-    key_slot.push_back((uint32_t)ch.idents[R.creator_ident].key_slot);
-    dig_idx.push_back(R.cjob);
-  }
-  for (size_t t = 0; t < total; t++) {
-    TxRec &R = recs[t];
-    if (R.pre != C_PENDING || R.type != 3) continue;
-    R.txid_job = add_job(where[t].first, {R.nonce, R.creator});
-  }
-  for (size_t t = 0; t < total; t++) {
-    TxRec &R = recs[t];
-    if (R.pre != C_PENDING || R.type != 3 || R.etx != C_VALID) continue;
-    R.prop_job = add_job(where[t].first, {R.chdr, R.act_hdr, R.ccpp});
-  }
-  for (size_t t = 0; t < total; t++) {
-    TxRec &R = recs[t];
-    if (R.pre != C_PENDING || R.type != 3 || R.etx != C_VALID || R.disp != C_VALID) continue;
-    const size_t b = where[t].first;
-    for (EndRec &e : R.ends) {
-      if (e.ident < 0 || ch.idents[e.ident].key_slot < 0) continue;
-      uint32_t hj = add_job(b, {R.prp, e.endorser});
-      e.vjob = (uint32_t)sig_ptr.size();
-      sig_ptr.push_back(e.sig.n ? dev_addr(b, e.sig) : 0);
-      sig_len.push_back(e.sig.n);
-      key_slot.push_back((uint32_t)ch.idents[e.ident].key_slot);
-      dig_idx.push_back(hj);
-    }
-  }
-  for (size_t t = 0; t < total; t++) {  // computed txids for the index (rare)
-    TxRec &R = recs[t];
-    if (R.index_ok && R.index_txid.empty()) R.index_job = add_job(where[t].first, {R.idx_nonce, R.idx_creator});
-  }
-  // --- B. device
-  std::vector<uint8_t> digests, vstatus;
-  int rc = fgv_run_block_jobs(c, jobs, sig_ptr, sig_len, key_slot, dig_idx, digests, vstatus);
+    cbase[k + 1] = a;
+  });
+  cbase[0] = {};
+  for (size_t k = 0; k < nch; k++)
+    for (int q = 0; q < 5; q++) cbase[k + 1][q] += cbase[k][q];
+  const std::array<uint32_t, 5> cnt = cbase[nch];
+  const uint32_t kbase[5] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2],
+                             cnt[0] + cnt[1] + cnt[2] + cnt[3]};
+  const size_t nj = (size_t)kbase[4] + cnt[4], nv = (size_t)cnt[0] + cnt[3];
+  BlockJobs J;
+  int rc = fgv_block_jobs_reserve(c, nj, nv, &J);
   if (rc) return rc;
+  auto dev_addr = [&](size_t b, const Span &s) -> uint64_t {
+    return s.n ? (uint64_t)(uintptr_t)d_blocks[b] + (uint64_t)(s.p - h_blocks[b]) : 0;
+  };
+  std::vector<uint64_t> chunk_blocks(nch, 0);
+  S->pool.run(nch, [&](size_t k) {
+    uint32_t o[5];
+    for (int q = 0; q < 5; q++) o[q] = kbase[q] + cbase[k][q];
+    uint32_t ov0 = cbase[k][0], ov3 = cnt[0] + cbase[k][3];
+    uint64_t nb = 0;
+    auto job = [&](uint32_t idx, size_t b, Span s0, Span s1 = Span(), Span s2 = Span()) {
+      ShaJob &j = J.jobs[idx];
+      j.p[0] = dev_addr(b, s0); j.n[0] = s0.n;
+      j.p[1] = dev_addr(b, s1); j.n[1] = s1.n;
+      j.p[2] = dev_addr(b, s2); j.n[2] = s2.n;
+      j.pad = 0;
+      nb += sha_blocks(j);
+    };
+    auto verify = [&](uint32_t vi, size_t b, Span sig, int32_t slot, uint32_t dig) {
+      J.sig_ptr[vi] = dev_addr(b, sig);
+      J.sig_len[vi] = sig.n;
+      J.key_slot[vi] = (uint32_t)slot;
+      J.dig_idx[vi] = dig;
+    };
+    for (size_t t = k * CH, e = std::min(total, t + CH); t < e; t++) {
+      TxRec &R = recs[t];
+      const size_t b = where[t].first;
+      if (R.n_cj) {
+        R.cjob = o[0]++;
+        job(R.cjob, b, R.payload);
+        R.cvjob = ov0++;
+        verify(R.cvjob, b, R.env_sig, ch.idents[R.creator_ident].key_slot, R.cjob);
+      }
+      if (R.n_tj) job(R.txid_job = o[1]++, b, R.nonce, R.creator);
+      if (R.n_pj) job(R.prop_job = o[2]++, b, R.chdr, R.act_hdr, R.ccpp);
+      if (R.n_ej) {
+        uint32_t left = R.n_ej;
+        for (EndRec &e2 : R.ends) {
+          if (!left) break;
+          if (e2.ident < 0 || ch.idents[e2.ident].key_slot < 0) continue;
+          const uint32_t hj = o[3]++;
+          job(hj, b, R.prp, e2.endorser);
+          e2.vjob = ov3++;
+          verify(e2.vjob, b, e2.sig, ch.idents[e2.ident].key_slot, hj);
+          left--;
+        }
+      }
+      if (R.n_ij) job(R.index_job = o[4]++, b, R.idx_nonce, R.idx_creator);
+    }
+    chunk_blocks[k] = nb;
+  });
+  uint64_t nblk = 0;
+  for (uint64_t x : chunk_blocks) nblk += x;
+  c->t_host_assemble = ms_since(t_asm);
 
-  // --- C. fold (code precedence, validator.go:297-453)
+  // --- B. device
+  auto t_dev = clk::now();
+  const uint8_t *digests = nullptr, *vstatus = nullptr;
+  rc = fgv_run_block_jobs(c, nj, nv, nblk, &digests, &vstatus);
+  if (rc) return rc;
+  c->t_host_device = ms_since(t_dev);
+  auto t_fold = clk::now();
+
+  // --- C. fold (code precedence, validator.go:297-453) + result records
   static const char HEX[] = "0123456789abcdef";
   std::atomic<bool> unsupported{false};
-  std::vector<uint8_t> codes(total, C_PENDING);
-  std::vector<uint8_t> reached(total, 0);
   S->pool.parallel_for(total, [&](size_t t) {
-    TxRec &R = recs[t];
+    const TxRec &R = recs[t];
     uint8_t code;
+    bool reached = false;
     if (R.pre != C_PENDING) {
       code = R.pre;
     } else if (vstatus[R.cvjob] != 0) {
@@ -633,14 +739,14 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         code = R.etx;
       } else if (R.prop_hash.n != 32 || memcmp(&digests[(size_t)R.prop_job * 32], R.prop_hash.p, 32) != 0) {
         code = C_BAD_ETX;
-      } else if ((reached[t] = 1, ch.committed.count(R.txid.str()))) {
+      } else if ((reached = true, ch.is_committed(R.txid))) {
         code = C_DUP_TXID;  // checkTxIdDupsLedger (initial ledger; batch-earlier blocks: finalize)
       } else if (R.disp != C_VALID) {
         code = R.disp;
       } else {
         // SignatureSetToValidIdentities (policy.go:363-395): dedup before verify
-        std::vector<int> ids;
-        std::vector<uint32_t> seen;
+        pbw::SmallVec<int, 16> ids;
+        pbw::SmallVec<uint32_t, 16> seen;
         for (const EndRec &e : R.ends) {
           if (e.ident < 0) continue;
           const uint32_t canon = ch.idents[e.ident].canon;
@@ -650,47 +756,42 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
           ids.push_back(e.ident);
         }
         bool has25 = false, has10 = false;
+        code = C_VALID;
         for (int pi : R.policies) {
           if (pi < 0) { has25 = true; continue; }
           const Policy &P = ch.policies[pi];
-          if (P.unsupported) { code = C_UNSUPPORTED; goto done; }
-          bool ok2 = false;
-          if (P.decode_ok && P.compile_ok) {
-            std::vector<uint8_t> used(ids.size(), 0);
-            ok2 = eval_node(P, P.root, ids, ch, used);
-          }
+          if (P.unsupported) { code = C_UNSUPPORTED; break; }
+          const bool ok2 = P.decode_ok && P.compile_ok && eval_policy(P, ids.data(), ids.size(), ch);
           if (!ok2) has10 = true;
         }
-        if (has25 && has10) code = C_UNSUPPORTED;  // Go map order decides the reported code
-        else if (has25) code = C_INVALID_CC;
-        else if (has10) code = C_POLICY;
-        else code = C_VALID;
+        if (code != C_UNSUPPORTED) {
+          if (has25 && has10) code = C_UNSUPPORTED;  // Go map order decides the reported code
+          else if (has25) code = C_INVALID_CC;
+          else if (has10) code = C_POLICY;
+        }
       }
     }
-  done:
     if (code == C_UNSUPPORTED) unsupported = true;
-    codes[t] = code;
-    // txid index entry for later blocks of this batch: chdr.TxId, or when empty
-    // ComputeTxID(nonce, creator) (protoutil/txutils.go:503-534)
-    if (R.index_ok && R.index_txid.empty() && R.index_job != UINT32_MAX) {
-      const uint8_t *d = &digests[(size_t)R.index_job * 32];
-      std::string h(64, '0');
-      for (int k = 0; k < 32; k++) {
-        h[2 * k] = HEX[d[k] >> 4];
-        h[2 * k + 1] = HEX[d[k] & 15];
-      }
-      R.index_txid = h;
-    }
-  });
-  if (unsupported) return FGV_EUNSUPPORTED;
-  S->pool.parallel_for(total, [&](size_t t) {
-    const TxRec &R = recs[t];
     fgv_tx_result &o = res_out[t];
     memset(&o, 0, sizeof o);
-    o.code = codes[t];
-    if (reached[t] && hex32(R.txid.str(), o.txid)) o.flags |= FGV_TXR_REACHED;
-    if (R.index_ok && hex32(R.index_txid, o.index_txid)) o.flags |= FGV_TXR_INDEXED;
+    o.code = code;
+    if (reached) {  // chdr.TxId == hex(digest): the record carries the digest bytes
+      memcpy(o.txid, &digests[(size_t)R.txid_job * 32], 32);
+      o.flags |= FGV_TXR_REACHED;
+    }
+    // txid index entry for later blocks of this batch: chdr.TxId, or when empty
+    // ComputeTxID(nonce, creator) (protoutil/txutils.go:503-534)
+    if (R.index_ok) {
+      if (R.index_txid.n == 0) {
+        memcpy(o.index_txid, &digests[(size_t)R.index_job * 32], 32);
+        o.flags |= FGV_TXR_INDEXED;
+      } else if (hex32(R.index_txid, o.index_txid)) {
+        o.flags |= FGV_TXR_INDEXED;
+      }
+    }
   });
+  c->t_host_fold = ms_since(t_fold);
+  if (unsupported) return FGV_EUNSUPPORTED;
   return FGV_OK;
 }
 
@@ -759,6 +860,7 @@ int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, i
   auto it = S->ch.canon_ids.find(canon);
   if (it == S->ch.canon_ids.end()) it = S->ch.canon_ids.emplace(canon, (uint32_t)S->ch.canon_ids.size()).first;
   I.canon = it->second;
+  I.msp = S->ch.intern(I.mspid);
   uint64_t h = hash_bytes(sid.mspid.p, sid.mspid.n);
   h = hash_bytes(sid.id_bytes.p, sid.id_bytes.n, h ^ 0xA5);
   if (S->ch.lookup(Span{ser, (uint32_t)len}) >= 0) return FGV_OK;  // already registered
@@ -768,18 +870,26 @@ int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, i
 }
 
 int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const uint8_t *policy, size_t len) {
+  Policy P = compile_policy(policy, len);
+  for (size_t i = 0; i < P.principal_msp.size(); i++)
+    P.principal_mspi.push_back(P.principal_bad[i] ? -1 : S->ch.intern(P.principal_msp[i]));
   auto it = S->ch.chaincodes.find(ns);
   if (it == S->ch.chaincodes.end()) {
-    S->ch.policies.push_back(compile_policy(policy, len));
+    S->ch.policies.push_back(std::move(P));
     S->ch.chaincodes.emplace(ns, (int)S->ch.policies.size() - 1);
   } else {
-    S->ch.policies[it->second] = compile_policy(policy, len);
+    S->ch.policies[it->second] = std::move(P);
   }
   return FGV_OK;
 }
 
 int fgv_block_add_txids(fgv_block_state *S, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
                         size_t n) {
-  for (size_t i = 0; i < n; i++) S->ch.committed.insert(std::string(reinterpret_cast<const char *>(buf + off[i]), len[i]));
+  for (size_t i = 0; i < n; i++) {
+    std::string_view v(reinterpret_cast<const char *>(buf + off[i]), len[i]);
+    if (S->ch.committed.count(v)) continue;
+    S->ch.committed_store.emplace_back(v);
+    S->ch.committed.insert(std::string_view(S->ch.committed_store.back()));
+  }
   return FGV_OK;
 }

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <random>
 #include <unordered_map>
 #include <vector>
 
@@ -71,6 +72,10 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   };
   if (hipSetDevice(c->device) != hipSuccess) return fail(FGV_EDEVICE);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
+  {
+    std::random_device rd;  // per-context hash seed of the finalize txid table
+    c->fin_seed = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)(uintptr_t)c;
+  }
   for (auto &e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
   if (hipFuncSetAttribute((const void *)k_point, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -99,19 +104,28 @@ void fgv_destroy(fgv_ctx *c) {
   DevBuf *d[] = {&c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->kt_q, &c->kt_slot, &c->kt_scratch,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->d2, &c->wscr, &c->msg,
                  &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
-                 &c->bj_dig, &c->bj_vst, &c->blk_arena};
+                 &c->bj_dig, &c->bj_vst, &c->blk_arena, &c->fz_meta, &c->fz_rowmap, &c->fz_blkof,
+                 &c->fz_owner, &c->fz_minblk, &c->fz_minvalid, &c->fz_flags, &c->fz_pslot, &c->fz_res};
   if (c->blk) fgv_block_state_free(c->blk);
   if (c->mv) fgv_mvcc_free(c->mv);
-  c->hb_dig.release();
-  c->hb_vst.release();
   for (auto *b : d) b->release();
   HostBuf *h[] = {&c->h_status, &c->h_slot, &c->h_r, &c->h_s, &c->h_dig, &c->h_kq, &c->h_kslot,
-                  &c->h_moff, &c->h_mlen};
+                  &c->h_moff, &c->h_mlen, &c->hb_dig, &c->hb_vst, &c->hb_jobs, &c->hb_sigp,
+                  &c->hb_sigl, &c->hb_slot, &c->hb_didx, &c->hb_fz, &c->hb_fflags, &c->hb_res};
   for (auto *b : h) b->release();
   for (auto &e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
+}
+
+int fgv_last_host_timing(fgv_ctx *c, double *parse_ms, double *assemble_ms, double *device_ms, double *fold_ms) {
+  if (!c) return FGV_EINVAL;
+  if (parse_ms) *parse_ms = c->t_host_parse;
+  if (assemble_ms) *assemble_ms = c->t_host_assemble;
+  if (device_ms) *device_ms = c->t_host_device;
+  if (fold_ms) *fold_ms = c->t_host_fold;
+  return FGV_OK;
 }
 
 int fgv_last_counts(fgv_ctx *c, uint64_t *sha_jobs, uint64_t *sha_blocks, uint64_t *verifies) {
@@ -462,21 +476,29 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *c, const uint8_t *d_msg_buf, const uint64_
 }  // extern "C"
 
 // ======================================================================= block engine glue
-int fgv_run_block_jobs(fgv_ctx *c, const std::vector<ShaJob> &jobs, const std::vector<uint64_t> &sig_ptr,
-                       const std::vector<uint32_t> &sig_len, const std::vector<uint32_t> &key_slot,
-                       const std::vector<uint32_t> &dig_idx, std::vector<uint8_t> &digests,
-                       std::vector<uint8_t> &vstatus) {
-  const size_t nj = jobs.size(), nv = sig_ptr.size();
-  digests.assign(nj * 32, 0);
-  vstatus.assign(nv, 0);
+int fgv_block_jobs_reserve(fgv_ctx *c, size_t nj, size_t nv, BlockJobs *out) {
+  if (!c->hb_jobs.ensure(nj * sizeof(ShaJob) + 64) || !c->hb_sigp.ensure(nv * 8 + 64) ||
+      !c->hb_sigl.ensure(nv * 4 + 64) || !c->hb_slot.ensure(nv * 4 + 64) || !c->hb_didx.ensure(nv * 4 + 64))
+    return FGV_ENOMEM;
+  out->jobs = c->hb_jobs.as<ShaJob>();
+  out->sig_ptr = c->hb_sigp.as<uint64_t>();
+  out->sig_len = c->hb_sigl.as<uint32_t>();
+  out->key_slot = c->hb_slot.as<uint32_t>();
+  out->dig_idx = c->hb_didx.as<uint32_t>();
+  return FGV_OK;
+}
+
+int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, const uint8_t **digests,
+                       const uint8_t **vstatus) {
   c->n_sha_jobs = nj;
   c->n_verifies = nv;
-  c->n_sha_blocks = 0;
-  for (const ShaJob &j : jobs) c->n_sha_blocks += (j.n[0] + j.n[1] + j.n[2] + 8) / 64 + 1;
+  c->n_sha_blocks = sha_blocks;
+  if (!c->hb_dig.ensure(nj * 32 + 64) || !c->hb_vst.ensure(nv + 64)) return FGV_ENOMEM;
+  *digests = c->hb_dig.as<uint8_t>();
+  *vstatus = c->hb_vst.as<uint8_t>();
   if (nj == 0) return FGV_OK;
-  if (!c->bj_jobs.ensure(nj * sizeof(ShaJob)) || !c->bj_dig.ensure(nj * 32) || !c->hb_dig.ensure(nj * 32))
-    return FGV_ENOMEM;
-  HIP_TRY(hipMemcpyAsync(c->bj_jobs.p, jobs.data(), nj * sizeof(ShaJob), hipMemcpyHostToDevice, c->stream));
+  if (!c->bj_jobs.ensure(nj * sizeof(ShaJob)) || !c->bj_dig.ensure(nj * 32)) return FGV_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(c->bj_jobs.p, c->hb_jobs.p, nj * sizeof(ShaJob), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   hipLaunchKernelGGL(k_sha256_jobs, dim3((uint32_t)((nj + 255) / 256)), dim3(256), 0, c->stream,
                      c->bj_jobs.as<ShaJob>(), (uint32_t)nj, c->bj_dig.as<uint8_t>());
@@ -486,13 +508,12 @@ int fgv_run_block_jobs(fgv_ctx *c, const std::vector<ShaJob> &jobs, const std::v
   if (nv) {
     const uint32_t N = (uint32_t)nv;
     if (!c->bj_sigp.ensure(nv * 8) || !c->bj_sigl.ensure(nv * 4) || !c->bj_slot.ensure(nv * 4) ||
-        !c->bj_didx.ensure(nv * 4) || !c->bj_vst.ensure(nv) || !c->r.ensure(nv * 32) || !c->s.ensure(nv * 32) ||
-        !c->hb_vst.ensure(nv))
+        !c->bj_didx.ensure(nv * 4) || !c->bj_vst.ensure(nv) || !c->r.ensure(nv * 32) || !c->s.ensure(nv * 32))
       return FGV_ENOMEM;
-    HIP_TRY(hipMemcpyAsync(c->bj_sigp.p, sig_ptr.data(), nv * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->bj_sigl.p, sig_len.data(), nv * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->bj_slot.p, key_slot.data(), nv * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->bj_didx.p, dig_idx.data(), nv * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->bj_sigp.p, c->hb_sigp.p, nv * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->bj_sigl.p, c->hb_sigl.p, nv * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->bj_slot.p, c->hb_slot.p, nv * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->bj_didx.p, c->hb_didx.p, nv * 4, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr,
                        c->bj_sigp.as<uint64_t>(), c->bj_sigl.as<uint32_t>(), N, c->bj_vst.as<uint8_t>(),
                        c->r.as<uint32_t>(), c->s.as<uint32_t>());
@@ -505,8 +526,6 @@ int fgv_run_block_jobs(fgv_ctx *c, const std::vector<ShaJob> &jobs, const std::v
   }
   HIP_TRY(hipMemcpyAsync(c->hb_dig.p, c->bj_dig.p, nj * 32, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  memcpy(digests.data(), c->hb_dig.p, nj * 32);
-  if (nv) memcpy(vstatus.data(), c->hb_vst.p, nv);
   float ms = 0;
   if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->t_sha = ms;
   read_stage_times(c, ran);
@@ -548,6 +567,65 @@ int fgv_ledger_add_txids(fgv_ctx *c, const uint8_t *buf, const uint64_t *off, co
   return fgv_block_add_txids(c->blk, buf, off, len, n);
 }
 
+
+// Device finalize over W x rows gathered records (finalize.hip).  Caller holds c->mu and has
+// set the device.
+static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t W, size_t rows,
+                             const uint8_t *d_recs, uint8_t *flags) {
+  if (W == 0 || ((uintptr_t)d_recs & 3)) return FGV_EINVAL;
+  uint64_t P = 0;
+  for (size_t b = 0; b < nblocks; b++) P += ntx[b];
+  if (P == 0) return FGV_OK;
+  if (P >= 0x7FFFFFFFull || nblocks >= 0x7FFFFFFFull || rows * W >= 0xFFFFFFFFull) return FGV_EINVAL;
+  // host metadata: blk_start (nb+1 u64) | roff (W x nb u32)
+  const size_t meta = (nblocks + 1) * 8 + (size_t)W * nblocks * 4;
+  if (!c->hb_fz.ensure(meta) || !c->fz_meta.ensure(meta)) return FGV_ENOMEM;
+  uint64_t *bstart = c->hb_fz.as<uint64_t>();
+  uint32_t *roff = reinterpret_cast<uint32_t *>(bstart + nblocks + 1);
+  bstart[0] = 0;
+  for (size_t b = 0; b < nblocks; b++) bstart[b + 1] = bstart[b] + ntx[b];
+  for (uint32_t r = 0; r < W; r++) {
+    uint64_t o = 0;
+    for (size_t b = 0; b < nblocks; b++) {
+      roff[(size_t)r * nblocks + b] = (uint32_t)o;
+      const uint64_t n = ntx[b];
+      o += (n * (r + 1)) / W - (n * r) / W;
+    }
+    if (o > rows) return FGV_EINVAL;  // gathered rows cannot hold rank r's shard
+  }
+  size_t cap = 1024;
+  while (cap < 2 * P) cap <<= 1;
+  if (!c->fz_rowmap.ensure(P * 4) || !c->fz_blkof.ensure(P * 4) || !c->fz_owner.ensure(cap * 4) ||
+      !c->fz_minblk.ensure(cap * 4) || !c->fz_minvalid.ensure(cap * 4) || !c->fz_flags.ensure(P) ||
+      !c->fz_pslot.ensure(P * 4) || !c->hb_fflags.ensure(P))
+    return FGV_ENOMEM;
+  hipStream_t st = c->stream;
+  HIP_TRY(hipMemcpyAsync(c->fz_meta.p, c->hb_fz.p, meta, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(c->fz_owner.p, 0, cap * 4, st));
+  HIP_TRY(hipMemsetAsync(c->fz_minblk.p, 0x7F, cap * 4, st));
+  HIP_TRY(hipMemsetAsync(c->fz_minvalid.p, 0xFF, cap * 4, st));
+  const uint32_t n32 = (uint32_t)P, mask = (uint32_t)(cap - 1);
+  const dim3 grid((n32 + 255) / 256), blk(256);
+  const uint64_t *d_bstart = c->fz_meta.as<uint64_t>();
+  const uint32_t *d_roff = reinterpret_cast<const uint32_t *>(d_bstart + nblocks + 1);
+  hipLaunchKernelGGL(k_fin_rows, grid, blk, 0, st, n32, d_bstart, (uint32_t)nblocks, W, (uint32_t)rows, d_roff,
+                     c->fz_rowmap.as<uint32_t>(), c->fz_blkof.as<uint32_t>());
+  hipLaunchKernelGGL(k_fin_index, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
+                     c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask,
+                     c->fin_seed);
+  hipLaunchKernelGGL(k_fin_codes, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
+                     c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(),
+                     c->fz_minvalid.as<uint32_t>(), mask, c->fin_seed, c->fz_flags.as<uint8_t>(),
+                     c->fz_pslot.as<uint32_t>());
+  hipLaunchKernelGGL(k_fin_dups, grid, blk, 0, st, n32, c->fz_pslot.as<uint32_t>(), c->fz_minvalid.as<uint32_t>(),
+                     c->fz_flags.as<uint8_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(c->hb_fflags.p, c->fz_flags.p, P, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  memcpy(flags, c->hb_fflags.p, P);
+  return FGV_OK;
+}
+
 static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                         const uint8_t *const *d_blocks, std::vector<const uint8_t *> &dev) {
   dev.resize(nblocks);
@@ -582,6 +660,42 @@ int fgv_validate_shard(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks,
                                  results_cap, ntx);
 }
 
+int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                           const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                           void *d_results, size_t results_cap, size_t *ntx) {
+  if (!c || (nblocks && (!blocks || !lens || !ntx || (results_cap && !d_results)))) return FGV_EINVAL;
+  if (nblocks == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  std::vector<const uint8_t *> dev;
+  int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
+  if (rc) return rc;
+  if (!c->hb_res.ensure(results_cap * sizeof(fgv_tx_result) + 64)) return FGV_ENOMEM;
+  fgv_tx_result *res = c->hb_res.as<fgv_tx_result>();
+  rc = fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi, res, results_cap, ntx);
+  if (rc) return rc;
+  size_t n = 0;
+  for (size_t b = 0; b < nblocks; b++) {
+    const size_t lo = tx_lo ? std::min<size_t>(tx_lo[b], ntx[b]) : 0;
+    const size_t hi = tx_hi ? std::min<size_t>(tx_hi[b], ntx[b]) : ntx[b];
+    if (hi > lo) n += hi - lo;
+  }
+  if (n) {
+    HIP_TRY(hipMemcpyAsync(d_results, res, n * sizeof(fgv_tx_result), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  return FGV_OK;
+}
+
+int fgv_finalize_flags_dev(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t world, size_t rows_per_rank,
+                           const void *d_gathered, uint8_t *flags) {
+  if (!c || (nblocks && (!ntx || !flags || !d_gathered))) return FGV_EINVAL;
+  if (nblocks == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  return finalize_dev_core(c, nblocks, ntx, world, rows_per_rank, static_cast<const uint8_t *>(d_gathered), flags);
+}
+
 int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *results, uint8_t *flags) {
   if (nblocks && (!ntx || !flags)) return FGV_EINVAL;
   return fgv_finalize_impl(nblocks, ntx, results, flags);
@@ -598,10 +712,22 @@ int fgv_validate_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks
     total += (size_t)k;
   }
   if (total > flags_cap) return FGV_EINVAL;
-  std::vector<fgv_tx_result> res(total);
-  int rc = fgv_validate_shard(c, nblocks, blocks, lens, d_blocks, nullptr, nullptr, res.data(), total, ntx);
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  std::vector<const uint8_t *> dev;
+  int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
   if (rc) return rc;
-  return fgv_finalize_impl(nblocks, ntx, res.data(), flags);
+  if (total == 0) {
+    for (size_t b = 0; b < nblocks; b++) ntx[b] = 0;
+    return FGV_OK;
+  }
+  if (!c->hb_res.ensure(total * sizeof(fgv_tx_result) + 64) || !c->fz_res.ensure(total * sizeof(fgv_tx_result)))
+    return FGV_ENOMEM;
+  fgv_tx_result *res = c->hb_res.as<fgv_tx_result>();
+  rc = fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), nullptr, nullptr, res, total, ntx);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->fz_res.p, res, total * sizeof(fgv_tx_result), hipMemcpyHostToDevice, c->stream));
+  return finalize_dev_core(c, nblocks, ntx, 1, total, c->fz_res.as<uint8_t>(), flags);
 }
 
 }  // extern "C"

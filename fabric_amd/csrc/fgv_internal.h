@@ -101,6 +101,11 @@ struct fgv_ctx {
   fgv_block_state *blk = nullptr;
   DevBuf bj_jobs, bj_sigp, bj_sigl, bj_slot, bj_didx, bj_dig, bj_vst, blk_arena;
   HostBuf hb_dig, hb_vst;
+  HostBuf hb_jobs, hb_sigp, hb_sigl, hb_slot, hb_didx;  // block-job staging (filled in place)
+  // device finalize (finalize.hip)
+  DevBuf fz_meta, fz_rowmap, fz_blkof, fz_owner, fz_minblk, fz_minvalid, fz_flags, fz_pslot, fz_res;
+  HostBuf hb_fz, hb_fflags, hb_res;
+  uint64_t fin_seed = 0;
   // per-batch device buffers
   DevBuf kt_q, kt_slot, kt_scratch;
   DevBuf status, slot, r, s, dig, d1, d2, wscr, msg, moff, mlen;
@@ -109,6 +114,7 @@ struct fgv_ctx {
   double t_sha = 0, t_prep = 0, t_point = 0, t_keytab = 0;
   uint64_t n_sha_jobs = 0, n_sha_blocks = 0, n_verifies = 0;  // last call
   double t_mvcc_lookup = 0, t_mvcc_total = 0;
+  double t_host_parse = 0, t_host_assemble = 0, t_host_device = 0, t_host_fold = 0;
   uint64_t n_mvcc_reads = 0, n_mvcc_writes = 0;
 };
 
@@ -137,9 +143,15 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
 long fgv_block_count_txs(const uint8_t *b, size_t n);
 int fgv_finalize_impl(size_t nblocks, const size_t *ntx, const fgv_tx_result *res, uint8_t *flags);
 
-// Device pass for one block batch: SHA-256 jobs -> digests (all), then ECDSA verify jobs whose
-// digest is digests[dig_idx[i]] -> vstatus.  Implemented in fgv_host.cpp.
-int fgv_run_block_jobs(fgv_ctx *c, const std::vector<ShaJob> &jobs, const std::vector<uint64_t> &sig_ptr,
-                       const std::vector<uint32_t> &sig_len, const std::vector<uint32_t> &key_slot,
-                       const std::vector<uint32_t> &dig_idx, std::vector<uint8_t> &digests,
-                       std::vector<uint8_t> &vstatus);
+// Pinned host staging for one block batch's device jobs (valid until the next reserve).
+struct BlockJobs {
+  ShaJob *jobs;
+  uint64_t *sig_ptr;  // device address of each DER signature (0: empty)
+  uint32_t *sig_len, *key_slot, *dig_idx;
+};
+int fgv_block_jobs_reserve(fgv_ctx *c, size_t nj, size_t nv, BlockJobs *out);
+// Device pass: SHA-256 jobs -> digests (all nj), then ECDSA verify jobs whose digest is
+// digests[dig_idx[i]] -> vstatus (nv).  Outputs point into pinned host buffers owned by the
+// context.  sha_blocks: compressions of the batch (statistics).  Implemented in fgv_host.cpp.
+int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, const uint8_t **digests,
+                       const uint8_t **vstatus);

@@ -13,9 +13,30 @@ using pbw::Span;
 namespace fgvb {
 
 // ------------------------------------------------------------------ small helpers
+// Word-wise 64-bit hash (four independent multiply-rotate lanes over 32-byte strides) -- used
+// for the identity index, where serialized identities are ~800 B PEM certificates.  Not
+// cryptographic: every hit is confirmed by an exact byte compare.
 inline uint64_t hash_bytes(const uint8_t *p, size_t n, uint64_t h = 0x9E3779B97F4A7C15ull) {
-  for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001B3ull;
-  return h ^ (h >> 29);
+  constexpr uint64_t M1 = 0x9E3779B97F4A7C15ull, M2 = 0xC2B2AE3D27D4EB4Full, M3 = 0x165667B19E3779F9ull;
+  auto rotl = [](uint64_t x, int r) { return (x << r) | (x >> (64 - r)); };
+  auto ld = [](const uint8_t *q) { uint64_t w; memcpy(&w, q, 8); return w; };
+  uint64_t a = h ^ n, b = h + M1, c = h ^ M2, d = h - M3;
+  size_t i = 0;
+  for (; i + 32 <= n; i += 32) {
+    a = rotl(a + ld(p + i) * M2, 31) * M1;
+    b = rotl(b + ld(p + i + 8) * M2, 31) * M1;
+    c = rotl(c + ld(p + i + 16) * M2, 31) * M1;
+    d = rotl(d + ld(p + i + 24) * M2, 31) * M1;
+  }
+  uint64_t x = rotl(a, 1) + rotl(b, 7) + rotl(c, 12) + rotl(d, 18);
+  for (; i + 8 <= n; i += 8) x = rotl(x ^ (ld(p + i) * M2), 27) * M1 + M3;
+  uint64_t t = 0;
+  for (int k = 0; i < n; i++, k += 8) t |= (uint64_t)p[i] << k;
+  x = (x ^ (t * M2)) * M1;
+  x ^= x >> 33;
+  x *= M2;
+  x ^= x >> 29;
+  return x;
 }
 
 // ------------------------------------------------------------------ message visitors
@@ -84,7 +105,7 @@ struct VTransactionAction {
   bool on_len(uint32_t n, Span s) { (n == 1 ? header : payload) = s; return true; }
 };
 struct VTransaction {
-  std::vector<VTransactionAction> actions;
+  pbw::SmallVec<VTransactionAction, 2> actions;
   pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_REP_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t, Span s) {
@@ -102,7 +123,7 @@ struct VEndorsement {
 };
 struct VEndorsedAction {
   Span prp;
-  std::vector<VEndorsement> ends;
+  pbw::SmallVec<VEndorsement, 8> ends;
   pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
@@ -304,7 +325,7 @@ struct VCollHashed {
 };
 struct VNsRwSet {
   Span ns, rwset;
-  std::vector<VCollHashed> coll;
+  pbw::SmallVec<VCollHashed, 2> coll;
   pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_BYTES : n == 3 ? pbw::K_REP_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
@@ -317,13 +338,13 @@ struct VNsRwSet {
   }
 };
 struct VTxRwSet {
-  std::vector<VNsRwSet> ns;
+  pbw::SmallVec<VNsRwSet, 4> ns;
   pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_VARINT : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t, Span s) {
     VNsRwSet r;
     if (!pbw::decode(s.p, s.n, r)) return false;
-    ns.push_back(std::move(r));
+    ns.push_back(r);
     return true;
   }
 };

@@ -1,0 +1,149 @@
+// finalize.hip -- the cross-transaction steps of TxValidator.Validate on the device, over the
+// all-gathered fgv_tx_result records of a block batch (libfgv.so):
+//   * checkTxIdDupsLedger against the txid index of EARLIER blocks of the batch
+//     (core/committer/txvalidator/v20/validator.go:460-481; it precedes Dispatch, so it
+//     applies to every tx that reached it -- FGV_TXR_REACHED);
+//   * markTXIdDuplicates (validator.go:279-295): among the VALID txs of a block, every
+//     occurrence of a txid after the first becomes DUPLICATE_TXID (9).
+// Layout: `recs` holds W ranks x `rows` padded records, rank r's rows = its shard
+// [lo_rb, hi_rb) of every block b in block order, lo_rb = floor(ntx_b * r / W)
+// (fabric_amd/shard.py).  Global position p enumerates transactions block-major.
+//
+// One open-addressing table keyed by the 32-byte txid (key bytes are never copied: a slot
+// names its owner position, whose record holds the key).  Per slot: min block that indexes
+// the txid, min position of a VALID tx carrying it.  Hash seeded per context.
+//   k_fin_rows   p -> gathered row, block
+//   k_fin_index  INDEXED txs: insert index_txid, atomicMin(min block)
+//   k_fin_codes  REACHED txs: ledger-dup if min block < own block; VALID: atomicMin(position)
+//   k_fin_dups   VALID txs whose txid has an earlier VALID position -> 9
+// Every kernel is one lane per transaction, HBM/L2-latency bound (~70 B read per tx).
+// Precondition (guaranteed by fgv_validate_shard[_dev], whose records these are): a VALID
+// record is REACHED, and a REACHED record is INDEXED with index_txid == txid (its chdr.TxId
+// equals hex(SHA-256(nonce||creator)), and that string is the index entry).
+#include <hip/hip_runtime.h>
+
+#include "../../include/fgv.h"
+#include "fgv_kernels.h"
+
+namespace {
+
+constexpr uint32_t REC = 68;
+constexpr uint32_t OFF_TXID = 4, OFF_INDEX = 36;
+
+__device__ inline uint64_t fin_hash(const uint32_t *k, uint64_t seed) {
+  uint64_t h = seed;
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    const uint64_t w = (uint64_t)k[i] | ((uint64_t)k[i + 1] << 32);
+    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+  }
+  h *= 0xBF58476D1CE4E5B9ull;
+  return h ^ (h >> 31);
+}
+
+__device__ inline void load_key(const uint8_t *recs, uint32_t row, uint32_t off, uint32_t k[8]) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(recs + (size_t)row * REC + off);
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = q[i];
+}
+
+__device__ inline bool key_eq(const uint32_t a[8], const uint8_t *recs, uint32_t row) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(recs + (size_t)row * REC + OFF_INDEX);
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; i++) eq &= q[i] == a[i];
+  return eq;
+}
+
+// slot of key k, or -1 (owners' keys are their index_txid)
+__device__ inline int64_t tab_find(const uint32_t k[8], uint64_t h, const uint32_t *owner, const uint32_t *rowmap,
+                                   const uint8_t *recs, uint32_t mask) {
+  for (uint32_t probe = 0; probe <= mask; probe++) {
+    const uint32_t s = (uint32_t)(h + probe) & mask;
+    const uint32_t o = owner[s];
+    if (o == 0) return -1;
+    if (key_eq(k, recs, rowmap[o - 1])) return s;
+  }
+  return -1;
+}
+
+}  // namespace
+
+__global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, uint32_t W, uint32_t rows,
+                           const uint32_t *roff, uint32_t *rowmap, uint32_t *blkof) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  uint32_t lo = 0, hi = nb;  // last b with blk_start[b] <= p
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (blk_start[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t b = lo;
+  const uint64_t n = blk_start[b + 1] - blk_start[b], i = p - blk_start[b];
+  uint32_t r = (uint32_t)((i * W) / n);
+  if (r >= W) r = W - 1;
+  while (r > 0 && (n * r) / W > i) r--;
+  while (r + 1 < W && (n * (r + 1)) / W <= i) r++;
+  const uint64_t lo_r = (n * r) / W;
+  rowmap[p] = r * rows + roff[(size_t)r * nb + b] + (uint32_t)(i - lo_r);
+  blkof[p] = b;
+}
+
+__global__ void k_fin_index(uint32_t P, const uint8_t *recs, const uint32_t *rowmap, const uint32_t *blkof,
+                            uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const uint32_t row = rowmap[p];
+  if (!(recs[(size_t)row * REC + 1] & FGV_TXR_INDEXED)) return;
+  uint32_t k[8];
+  load_key(recs, row, OFF_INDEX, k);
+  const uint64_t h = fin_hash(k, seed);
+  const int32_t b = (int32_t)blkof[p];
+  for (uint32_t probe = 0; probe <= mask; probe++) {
+    const uint32_t s = (uint32_t)(h + probe) & mask;
+    uint32_t o = owner[s];
+    if (o == 0) {
+      o = atomicCAS(&owner[s], 0u, p + 1);
+      if (o == 0) {
+        atomicMin(&minblk[s], b);
+        return;
+      }
+    }
+    if (key_eq(k, recs, rowmap[o - 1])) {
+      atomicMin(&minblk[s], b);
+      return;
+    }
+  }
+}
+
+__global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *rowmap, const uint32_t *blkof,
+                            const uint32_t *owner, const int32_t *minblk, uint32_t *minvalid, uint32_t mask,
+                            uint64_t seed, uint8_t *flags, uint32_t *pslot) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const uint32_t row = rowmap[p];
+  const uint8_t *r = recs + (size_t)row * REC;
+  uint8_t code = r[0];
+  uint32_t slot = 0xFFFFFFFFu;
+  if (r[1] & FGV_TXR_REACHED) {
+    uint32_t k[8];
+    load_key(recs, row, OFF_TXID, k);
+    const int64_t s = tab_find(k, fin_hash(k, seed), owner, rowmap, recs, mask);
+    if (s >= 0) {
+      if (minblk[s] < (int32_t)blkof[p]) code = 9;  // txid indexed by an earlier block of the batch
+      slot = (uint32_t)s;
+    }
+  }
+  if (code == 0 && slot != 0xFFFFFFFFu) atomicMin(&minvalid[slot], p);
+  flags[p] = code;
+  pslot[p] = slot;
+}
+
+__global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  if (flags[p] != 0 || pslot[p] == 0xFFFFFFFFu) return;
+  if (minvalid[pslot[p]] < p) flags[p] = 9;  // markTXIdDuplicates: an earlier VALID tx of this block
+}

@@ -25,6 +25,12 @@ struct Span {
   bool nil() const { return n == 0; }  // proto3 bytes: present <=> non-empty
   std::string str() const { return std::string(reinterpret_cast<const char *>(p), n); }
   bool eq(const char *s, size_t l) const { return n == l && (l == 0 || memcmp(p, s, l) == 0); }
+  bool eq(const Span &o) const { return n == o.n && (n == 0 || memcmp(p, o.p, n) == 0); }
+  // byte-lexicographic order (Go string comparison)
+  bool operator<(const Span &o) const {
+    const int c = memcmp(p, o.p, n < o.n ? n : o.n);
+    return c < 0 || (c == 0 && n < o.n);
+  }
 };
 
 inline bool rd_varint(const uint8_t *&p, const uint8_t *e, uint64_t &v) {
@@ -67,6 +73,12 @@ inline bool skip_value(const uint8_t *&p, const uint8_t *e, uint32_t num, int wt
 // Go utf8.Valid
 inline bool utf8_valid(const uint8_t *s, size_t n) {
   size_t i = 0;
+  while (i + 8 <= n) {  // ASCII fast path
+    uint64_t w;
+    memcpy(&w, s + i, 8);
+    if (w & 0x8080808080808080ull) break;
+    i += 8;
+  }
   while (i < n) {
     const uint8_t c = s[i];
     if (c < 0x80) { i++; continue; }
@@ -144,5 +156,35 @@ struct MsgField {
 };
 
 inline int32_t as_int32(uint64_t v) { return (int32_t)(uint32_t)v; }
+
+// Repeated field storage with N inline elements: the per-transaction decode allocates nothing
+// in the common shapes (1 action, a handful of endorsements / namespaces).
+template <class T, size_t N>
+struct SmallVec {
+  T inl[N];
+  std::vector<T> heap;
+  uint32_t cnt = 0;
+  bool spilled = false;
+  void push_back(const T &x) {
+    if (!spilled) {
+      if (cnt < N) { inl[cnt++] = x; return; }
+      heap.assign(inl, inl + N);
+      spilled = true;
+    }
+    heap.push_back(x);
+    cnt++;
+  }
+  void clear() { cnt = 0; spilled = false; heap.clear(); }
+  size_t size() const { return cnt; }
+  bool empty() const { return cnt == 0; }
+  T *data() { return spilled ? heap.data() : inl; }
+  const T *data() const { return spilled ? heap.data() : inl; }
+  T &operator[](size_t i) { return data()[i]; }
+  const T &operator[](size_t i) const { return data()[i]; }
+  T *begin() { return data(); }
+  T *end() { return data() + cnt; }
+  const T *begin() const { return data(); }
+  const T *end() const { return data() + cnt; }
+};
 
 }  // namespace pbw

@@ -42,6 +42,20 @@ def allgather_results(local, ntx, world, device=None, group=None, out=None):
     return reorder(g, ntx, world, rows)
 
 
+def allgather_device(send, recv, group=None):
+    """All-gather the per-rank device record buffers (rows x 68 each) into `recv`
+    (world*rows x 68, rank-major -- the layout fgv_finalize_flags_dev reads), and wait for it
+    so the engine's own stream may read `recv`.  gloo (CPU rehearsal) gathers through host
+    memory."""
+    if dist.get_backend(group) == "gloo":
+        tmp = torch.empty(recv.shape, dtype=recv.dtype)
+        dist.all_gather_into_tensor(tmp, send.cpu(), group=group)
+        recv.copy_(tmp)
+    else:
+        dist.all_gather_into_tensor(recv, send, group=group)
+    torch.cuda.current_stream(recv.device).synchronize()
+
+
 def reorder(gathered, ntx, world, rows):
     """rank-major padded rows -> block-major transaction order"""
     ntx = np.asarray(ntx, dtype=np.int64)

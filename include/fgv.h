@@ -56,6 +56,10 @@ const char *fgv_strerror(int code);
 /* kernel-time accounting of the last call (ms, HIP events around each kernel) */
 int fgv_last_timing(fgv_ctx *ctx, double *sha_ms, double *prep_ms, double *point_ms,
                     double *keytab_ms);
+/* host-side wall time of the last block call: parse, job assembly, device pass (incl.
+ * transfers), fold (ms) */
+int fgv_last_host_timing(fgv_ctx *ctx, double *parse_ms, double *assemble_ms, double *device_ms,
+                         double *fold_ms);
 /* work of the last block call: SHA-256 messages, 64-byte compressions, ECDSA verifies */
 int fgv_last_counts(fgv_ctx *ctx, uint64_t *sha_jobs, uint64_t *sha_blocks, uint64_t *verifies);
 
@@ -156,6 +160,22 @@ int fgv_validate_shard(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *block
 /* pure host function: results of ALL transactions, blocks concatenated in order */
 int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *results,
                        uint8_t *flags);
+
+/* Device-resident variants for the multi-GPU protocol (records stay in HBM between the
+ * shard validation, the RCCL all-gather and the finalize):
+ *   fgv_validate_shard_dev -- as fgv_validate_shard, records written to device memory
+ *     `d_results` (4-byte aligned, results_cap records) in shard order;
+ *   fgv_finalize_flags_dev -- fgv_finalize_flags over the all-gathered device buffer
+ *     `d_gathered` = world x rows_per_rank records, rank r's rows holding its shard
+ *     [floor(ntx_b*r/world), floor(ntx_b*(r+1)/world)) of every block b in block order
+ *     (the layout all_gather produces from the per-rank fgv_validate_shard_dev buffers).
+ *     Runs as device kernels (open-addressing txid table in HBM); flags -> host memory.
+ * Same results as fgv_validate_shard + fgv_finalize_flags (validator.go:279-295, 460-481). */
+int fgv_validate_shard_dev(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
+                           const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                           const uint32_t *tx_hi, void *d_results, size_t results_cap, size_t *ntx);
+int fgv_finalize_flags_dev(fgv_ctx *ctx, size_t nblocks, const size_t *ntx, uint32_t world,
+                           size_t rows_per_rank, const void *d_gathered, uint8_t *flags);
 
 /* ------------------------------------------------------------------------------ MVCC */
 

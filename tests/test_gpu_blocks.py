@@ -157,3 +157,77 @@ def test_sharded_validation_matches_single(shards):
     exp = _oracle(net, blks)
     assert list(flags) == exp[0] + exp[1]
     eng.close()
+
+
+@pytest.mark.parametrize("shards", [1, 2, 3, 8])
+def test_device_sharded_protocol(shards):
+    """fgv_validate_shard_dev per rank into the rank-major gathered buffer (what
+    all_gather_into_tensor produces) + fgv_finalize_flags_dev == whole-batch flags == oracle."""
+    import torch
+    from fabric_amd import shard
+    net = network()
+    txs = []
+    b1, _, _ = blocks.make_block(net, 40, number=1, seed=91, out_txs=txs)
+    b2, _, _ = blocks.make_block(net, 3, number=2, seed=92, reuse={1: (txs[5].creator, txs[5].nonce)})
+    b3, _, _ = blocks.make_block(net, 29, number=3, seed=93, reuse={4: (txs[7].creator, txs[7].nonce),
+                                                                    20: (txs[7].creator, txs[7].nonce)})
+    blks = [b1, b2, b3]
+    ntx = np.array([40, 3, 29], dtype=np.int64)
+    eng = _engine_for(net)
+    rows = shard.padded_rows(ntx, shards)
+    recv = torch.zeros((shards * rows, shard.REC), dtype=torch.uint8, device="cuda")
+    batch = eng.block_batch(blks)
+    for r in range(shards):
+        lo, hi = shard.shard_ranges(ntx, r, shards)
+        nt = eng.validate_shard_dev(batch, lo, hi, recv[r * rows:].data_ptr(), rows)
+        assert list(nt) == list(ntx)
+    flags = eng.finalize_flags_dev(ntx, shards, rows, recv.data_ptr())
+    exp = _oracle(net, blks)
+    assert list(flags) == exp[0] + exp[1] + exp[2]
+    assert np.array_equal(flags, np.concatenate(eng.validate_blocks(blks)))
+    eng.close()
+
+
+def _random_records(rng, ntx, pool):
+    """fgv_tx_result records honouring the engine's invariants: VALID => REACHED;
+    REACHED => INDEXED with index_txid == txid."""
+    n = int(sum(ntx))
+    rec = np.zeros((n, 68), np.uint8)
+    keys = rng.integers(0, 256, size=(pool, 32), dtype=np.uint8)
+    code = rng.choice(np.array([0, 0, 0, 0, 9, 10, 8, 4, 255], np.uint8), size=n)
+    reached = (code == 0) | (rng.random(n) < 0.3)
+    indexed = reached | (rng.random(n) < 0.5)
+    tid = rng.integers(0, pool, size=n)
+    iid = np.where(reached, tid, rng.integers(0, pool, size=n))
+    rec[:, 0] = code
+    rec[:, 1] = reached.astype(np.uint8) | (indexed.astype(np.uint8) << 1)
+    rec[:, 4:36] = keys[tid]
+    rec[:, 36:68] = keys[iid]
+    return rec
+
+
+@pytest.mark.parametrize("seed,pool,world", [(1, 7, 1), (2, 50, 3), (3, 3000, 8), (4, 2, 2)])
+def test_device_finalize_matches_host_finalize(seed, pool, world):
+    """Device finalize (hash table in HBM) == host finalize on adversarially colliding txids,
+    with the rank-major gathered layout built by hand."""
+    import torch
+    from fabric_amd import shard
+    rng = np.random.default_rng(seed)
+    ntx = np.array([int(x) for x in rng.integers(0, 400, size=12)] + [0, 1], dtype=np.int64)
+    rec = _random_records(rng, ntx, pool)
+    host = _lib.finalize_flags(ntx, rec)
+    rows = shard.padded_rows(ntx, world)
+    g = np.zeros((world * rows, 68), np.uint8)
+    starts = np.concatenate([[0], np.cumsum(ntx)])
+    for r in range(world):
+        lo, hi = shard.shard_ranges(ntx, r, world)
+        o = r * rows
+        for b in range(len(ntx)):
+            k = int(hi[b]) - int(lo[b])
+            g[o:o + k] = rec[starts[b] + int(lo[b]): starts[b] + int(hi[b])]
+            o += k
+    eng = _lib.Engine(0)
+    d = torch.from_numpy(g).to("cuda")
+    dev = eng.finalize_flags_dev(ntx, world, rows, d.data_ptr())
+    assert np.array_equal(dev, host)
+    eng.close()
