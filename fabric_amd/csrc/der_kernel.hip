@@ -5,21 +5,50 @@
 #include "fgv_der.h"
 #include "fgv_kernels.h"
 
+// Signatures up to DER_STAGE_MAX bytes are first copied into LDS with independent aligned
+// dword loads (one memory latency instead of one per parsed byte: the parse is a chain of
+// dependent byte reads), then decoded from LDS.  Longer ones are decoded in place.
+#define DER_STAGE_MAX 124
+#define DER_STAGE_DW 33  // dwords per lane: (3 + DER_STAGE_MAX + 3) / 4 + pad
+
 __global__ __launch_bounds__(256) void k_der(const uint8_t *__restrict__ sig_buf,
                                              const uint64_t *__restrict__ off,
                                              const uint32_t *__restrict__ len, uint32_t n,
                                              uint8_t *__restrict__ status,
                                              uint32_t *__restrict__ r_limbs,
                                              uint32_t *__restrict__ s_limbs) {
+  __shared__ uint32_t stage[256 * DER_STAGE_DW];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t r[8], s[8];
   uint8_t code = ST_PENDING;
   const uint32_t L = len[i];
+  const uint8_t *src = sig_buf ? sig_buf + off[i] : reinterpret_cast<const uint8_t *>((uintptr_t)off[i]);
+  if (L > 0 && L <= DER_STAGE_MAX) {
+    // aligned dwords covering [src, src + L); device allocations are >= 4-byte aligned, so
+    // the dword holding src starts inside the allocation; the last partial dword is read by
+    // bytes (never past src + L)
+    const uintptr_t a = (uintptr_t)src, a0 = a & ~(uintptr_t)3, end = a + L;
+    const uint32_t nd = (uint32_t)((end - a0 + 3) >> 2);
+    uint32_t *dst = stage + threadIdx.x * DER_STAGE_DW;
+#pragma unroll
+    for (uint32_t d = 0; d < DER_STAGE_DW; d++) {
+      const uintptr_t p = a0 + 4 * d;
+      if (d >= nd) {
+      } else if (p + 4 <= end) {
+        dst[d] = *reinterpret_cast<const uint32_t *>(p);
+      } else {
+        uint32_t w = 0;
+        for (uintptr_t q = p; q < end; q++) w |= (uint32_t)(*reinterpret_cast<const uint8_t *>(q)) << (8 * (q - p));
+        dst[d] = w;
+      }
+    }
+    src = reinterpret_cast<const uint8_t *>(dst) + (a - a0);
+  }
   bool rb = false, sb = false;
   if (L == 0) {
     code = 6;
-  } else if (fgv::der_decode_sig(sig_buf + off[i], L, r, s, rb, sb)) {
+  } else if (fgv::der_decode_sig(src, L, r, s, rb, sb)) {
     code = 2;
   } else if (sb || !fgv::is_low_s(s)) {
     code = 3;

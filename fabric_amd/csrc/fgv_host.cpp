@@ -8,8 +8,10 @@
 //   D2H:  status (1 B/item)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <random>
@@ -72,15 +74,22 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   };
   if (hipSetDevice(c->device) != hipSuccess) return fail(FGV_EDEVICE);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
   {
     std::random_device rd;  // per-context hash seed of the finalize txid table
     c->fin_seed = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)(uintptr_t)c;
   }
   for (auto &e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
-  if (hipFuncSetAttribute((const void *)k_point, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)KT_BYTES) != hipSuccess)
+  if (hipFuncSetAttribute((const void *)k_point, hipFuncAttributeMaxDynamicSharedMemorySize, (int)KT_BYTES) !=
+      hipSuccess)
     return fail(FGV_EDEVICE);
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0)
+      return fail(FGV_EDEVICE);
+    c->n_cu = (uint32_t)ncu;
+  }
   if (!c->gtab.ensure(KT_BYTES) || !c->g_ok.ensure(16) ||
       !c->ktab.ensure((size_t)c->key_slots * KT_BYTES) || !c->key_ok.ensure(c->key_slots))
     return fail(FGV_ENOMEM);
@@ -102,7 +111,7 @@ void fgv_destroy(fgv_ctx *c) {
   if (!c) return;
   if (c->stream) hipStreamSynchronize(c->stream);
   DevBuf *d[] = {&c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->kt_q, &c->kt_slot, &c->kt_scratch,
-                 &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->d2, &c->wscr, &c->msg,
+                 &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
                  &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
                  &c->bj_dig, &c->bj_vst, &c->blk_arena, &c->fz_meta, &c->fz_rowmap, &c->fz_blkof,
                  &c->fz_owner, &c->fz_minblk, &c->fz_minvalid, &c->fz_flags, &c->fz_pslot, &c->fz_res};
@@ -116,6 +125,7 @@ void fgv_destroy(fgv_ctx *c) {
   for (auto &e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
+  if (c->stream2) hipStreamDestroy(c->stream2);
   delete c;
 }
 
@@ -149,27 +159,58 @@ int fgv_last_timing(fgv_ctx *c, double *sha_ms, double *prep_ms, double *point_m
 }  // extern "C"
 
 // k_prep + k_point on device-resident SoA inputs (events ev[2..4] bracket them)
+// k_inv on stream `st` (events ev[2]/ev[3]); the caller orders it after k_der.
+static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, uint8_t *d_status, const uint32_t *d_slot,
+                      const uint32_t *d_r, const uint32_t *d_s) {
+  uint32_t nl = (N + PREP_B - 1) / PREP_B;
+  nl = (nl + INV_THREADS - 1) / INV_THREADS * INV_THREADS;
+  if (!c->wscr.ensure((size_t)PREP_B * 8 * nl * 4) || !c->wv.ensure((size_t)N * 32)) return FGV_ENOMEM;
+  HIP_TRY(hipEventRecord(c->ev[2], st));
+  hipLaunchKernelGGL(k_inv, dim3(nl / INV_THREADS), dim3(INV_THREADS), 0, st, N, d_status, d_slot,
+                     c->key_ok.as<uint8_t>(), d_r, d_s, c->wv.as<uint32_t>(), c->wscr.as<uint32_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[3], st));
+  return FGV_OK;
+}
+
+// k_prep + k_point on the main stream, after k_inv (ev[3]) and the digests.
+static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const uint32_t *d_slot,
+                             const uint32_t *d_r, const uint8_t *d_dig, const uint32_t *d_dig_idx) {
+  if (!c->d1.ensure((size_t)DIG_STRIDE * N)) return FGV_ENOMEM;
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->ev[3], 0));
+  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+  hipLaunchKernelGGL(k_prep, dim3((N + 255) / 256), dim3(256), 0, c->stream, N, d_status, d_r,
+                     c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+  // Persistent grid (one 1024-lane workgroup per CU: the 88 KB LDS table and ~118 VGPRs
+  // allow one per CU).  Lanes per verify L: the largest L <= 8 whose groups
+  // (n_cu * 16 waves * floor(64/L)) still cover the batch in one pass -- the per-item
+  // latency falls ~L-fold while the work grows only by the L-1 tree additions.
+  // FGV_POINT_LANES forces L (measurement knob).
+  static const int forced = [] {
+    const char *e = getenv("FGV_POINT_LANES");
+    return e ? atoi(e) : 0;
+  }();
+  const uint64_t waves = (uint64_t)c->n_cu * (POINT_THREADS / 64);
+  uint32_t L = 1;
+  for (uint32_t l = POINT_LANES_MAX; l >= 1; l--)
+    if (waves * (64 / l) >= N) { L = l; break; }
+  if (forced >= 1 && forced <= POINT_LANES_MAX) L = (uint32_t)forced;
+  hipLaunchKernelGGL(k_point, dim3(c->n_cu), dim3(POINT_THREADS), KT_BYTES, c->stream, N, L, d_status, d_slot,
+                     c->gtab.as<apoint_raw>(), c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(), d_r);
+  c->last_lanes = L;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[6], c->stream));
+  return FGV_OK;
+}
+
 static int launch_verify_stages(fgv_ctx *c, uint32_t N, uint8_t *d_status, const uint32_t *d_slot,
                                 const uint32_t *d_r, const uint32_t *d_s, const uint8_t *d_dig,
                                 const uint32_t *d_dig_idx = nullptr) {
-  if (!c->d1.ensure((size_t)NWIN * N) || !c->d2.ensure((size_t)NWIN * N)) return FGV_ENOMEM;
-  uint32_t nl = (N + PREP_B - 1) / PREP_B;
-  nl = (nl + 255) / 256 * 256;
-  if (!c->wscr.ensure((size_t)PREP_B * 8 * nl * 4)) return FGV_ENOMEM;
-  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  hipLaunchKernelGGL(k_prep, dim3(nl / 256), dim3(256), 0, c->stream, N, d_status, d_slot,
-                     c->key_ok.as<uint8_t>(), d_r, d_s, d_dig, d_dig_idx, c->d1.as<int8_t>(), c->d2.as<int8_t>(),
-                     c->wscr.as<uint32_t>());
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-  uint32_t grid = (N + POINT_THREADS - 1) / POINT_THREADS;
-  if (grid > 1024) grid = 1024;
-  hipLaunchKernelGGL(k_point, dim3(grid), dim3(POINT_THREADS), KT_BYTES, c->stream, N, d_status,
-                     d_slot, c->gtab.as<apoint_raw>(), c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(),
-                     c->d2.as<int8_t>(), d_r);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
-  return FGV_OK;
+  int rc = launch_inv(c, c->stream, N, d_status, d_slot, d_r, d_s);
+  if (rc) return rc;
+  return launch_prep_point(c, N, d_status, d_slot, d_r, d_dig, d_dig_idx);
 }
 
 static void read_stage_times(fgv_ctx *c, bool ran) {
@@ -177,7 +218,8 @@ static void read_stage_times(fgv_ctx *c, bool ran) {
   c->t_prep = c->t_point = 0;
   if (!ran) return;
   if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->t_prep = ms;
-  if (hipEventElapsedTime(&ms, c->ev[3], c->ev[4]) == hipSuccess) c->t_point = ms;
+  if (hipEventElapsedTime(&ms, c->ev[4], c->ev[5]) == hipSuccess) c->t_prep += ms;
+  if (hipEventElapsedTime(&ms, c->ev[5], c->ev[6]) == hipSuccess) c->t_point = ms;
 }
 
 // ------------------------------------------------------------------ verify core
@@ -476,15 +518,19 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *c, const uint8_t *d_msg_buf, const uint64_
 }  // extern "C"
 
 // ======================================================================= block engine glue
+// verify-job arrays share one staging block (one H2D copy): [sig_ptr u64 | sig_len | key_slot
+// | dig_idx u32], each of nv entries
+static size_t sig_block_bytes(size_t nv) { return nv * 20; }
+
 int fgv_block_jobs_reserve(fgv_ctx *c, size_t nj, size_t nv, BlockJobs *out) {
-  if (!c->hb_jobs.ensure(nj * sizeof(ShaJob) + 64) || !c->hb_sigp.ensure(nv * 8 + 64) ||
-      !c->hb_sigl.ensure(nv * 4 + 64) || !c->hb_slot.ensure(nv * 4 + 64) || !c->hb_didx.ensure(nv * 4 + 64))
+  if (!c->hb_jobs.ensure(nj * sizeof(ShaJob) + 64) || !c->hb_sigp.ensure(sig_block_bytes(nv) + 64))
     return FGV_ENOMEM;
   out->jobs = c->hb_jobs.as<ShaJob>();
-  out->sig_ptr = c->hb_sigp.as<uint64_t>();
-  out->sig_len = c->hb_sigl.as<uint32_t>();
-  out->key_slot = c->hb_slot.as<uint32_t>();
-  out->dig_idx = c->hb_didx.as<uint32_t>();
+  uint8_t *b = c->hb_sigp.as<uint8_t>();
+  out->sig_ptr = reinterpret_cast<uint64_t *>(b);
+  out->sig_len = reinterpret_cast<uint32_t *>(b + nv * 8);
+  out->key_slot = reinterpret_cast<uint32_t *>(b + nv * 12);
+  out->dig_idx = reinterpret_cast<uint32_t *>(b + nv * 16);
   return FGV_OK;
 }
 
@@ -499,27 +545,38 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
   if (nj == 0) return FGV_OK;
   if (!c->bj_jobs.ensure(nj * sizeof(ShaJob)) || !c->bj_dig.ensure(nj * 32)) return FGV_ENOMEM;
   HIP_TRY(hipMemcpyAsync(c->bj_jobs.p, c->hb_jobs.p, nj * sizeof(ShaJob), hipMemcpyHostToDevice, c->stream));
+  bool ran = false;
+  if (nv) {
+    const uint32_t N = (uint32_t)nv;
+    if (!c->bj_sigp.ensure(sig_block_bytes(nv)) || !c->bj_vst.ensure(nv) || !c->r.ensure(nv * 32) ||
+        !c->s.ensure(nv * 32))
+      return FGV_ENOMEM;
+    HIP_TRY(hipMemcpyAsync(c->bj_sigp.p, c->hb_sigp.p, sig_block_bytes(nv), hipMemcpyHostToDevice, c->stream));
+    uint8_t *dsig = c->bj_sigp.as<uint8_t>();
+    const uint64_t *d_sigp = reinterpret_cast<const uint64_t *>(dsig);
+    const uint32_t *d_sigl = reinterpret_cast<const uint32_t *>(dsig + nv * 8);
+    const uint32_t *d_slot = reinterpret_cast<const uint32_t *>(dsig + nv * 12);
+    // DER decode first (short), then fork: s^-1 on stream2 while the SHA-256 jobs run on the
+    // main stream (launched together, the SHA workgroups would occupy the CUs first)
+    hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr, d_sigp,
+                       d_sigl, N, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(), c->s.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[7], c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev[7], 0));
+    int rc = launch_inv(c, c->stream2, N, c->bj_vst.as<uint8_t>(), d_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>());
+    if (rc) return rc;
+  }
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   hipLaunchKernelGGL(k_sha256_jobs, dim3((uint32_t)((nj + 255) / 256)), dim3(256), 0, c->stream,
                      c->bj_jobs.as<ShaJob>(), (uint32_t)nj, c->bj_dig.as<uint8_t>());
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-  bool ran = false;
   if (nv) {
     const uint32_t N = (uint32_t)nv;
-    if (!c->bj_sigp.ensure(nv * 8) || !c->bj_sigl.ensure(nv * 4) || !c->bj_slot.ensure(nv * 4) ||
-        !c->bj_didx.ensure(nv * 4) || !c->bj_vst.ensure(nv) || !c->r.ensure(nv * 32) || !c->s.ensure(nv * 32))
-      return FGV_ENOMEM;
-    HIP_TRY(hipMemcpyAsync(c->bj_sigp.p, c->hb_sigp.p, nv * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->bj_sigl.p, c->hb_sigl.p, nv * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->bj_slot.p, c->hb_slot.p, nv * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->bj_didx.p, c->hb_didx.p, nv * 4, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr,
-                       c->bj_sigp.as<uint64_t>(), c->bj_sigl.as<uint32_t>(), N, c->bj_vst.as<uint8_t>(),
-                       c->r.as<uint32_t>(), c->s.as<uint32_t>());
-    HIP_TRY(hipGetLastError());
-    int rc = launch_verify_stages(c, N, c->bj_vst.as<uint8_t>(), c->bj_slot.as<uint32_t>(), c->r.as<uint32_t>(),
-                                  c->s.as<uint32_t>(), c->bj_dig.as<uint8_t>(), c->bj_didx.as<uint32_t>());
+    const uint8_t *dsig = c->bj_sigp.as<uint8_t>();
+    int rc = launch_prep_point(c, N, c->bj_vst.as<uint8_t>(), reinterpret_cast<const uint32_t *>(dsig + nv * 12),
+                               c->r.as<uint32_t>(), c->bj_dig.as<uint8_t>(),
+                               reinterpret_cast<const uint32_t *>(dsig + nv * 16));
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->hb_vst.p, c->bj_vst.p, nv, hipMemcpyDeviceToHost, c->stream));
     ran = true;

@@ -90,7 +90,8 @@ struct fgv_ctx {
   fgv_mvcc_state *mv = nullptr;
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[8] = {};
+  hipStream_t stream2 = nullptr;  // k_der + k_inv of a block batch, concurrent with SHA-256
+  hipEvent_t ev[8] = {};          // 0/1 sha, 2/3 inv, 4/5 prep, 6 point end, 7 fork
   std::mutex mu;
   // generator table (88 KB) and the public-key table cache
   DevBuf gtab, g_ok;
@@ -106,9 +107,11 @@ struct fgv_ctx {
   DevBuf fz_meta, fz_rowmap, fz_blkof, fz_owner, fz_minblk, fz_minvalid, fz_flags, fz_pslot, fz_res;
   HostBuf hb_fz, hb_fflags, hb_res;
   uint64_t fin_seed = 0;
+  uint32_t n_cu = 0;        // compute units (persistent k_point grid)
+  uint32_t last_lanes = 0;  // lanes per verify of the last k_point launch
   // per-batch device buffers
   DevBuf kt_q, kt_slot, kt_scratch;
-  DevBuf status, slot, r, s, dig, d1, d2, wscr, msg, moff, mlen;
+  DevBuf status, slot, r, s, dig, d1, wv, wscr, msg, moff, mlen;
   // pinned staging
   HostBuf h_status, h_slot, h_r, h_s, h_dig, h_kq, h_kslot, h_moff, h_mlen;
   double t_sha = 0, t_prep = 0, t_point = 0, t_keytab = 0;

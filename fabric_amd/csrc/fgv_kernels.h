@@ -9,8 +9,10 @@
 #define TAB_K 32
 #define KT_ENTRIES (NWIN * TAB_K)           // 1376 affine points per table
 #define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 88,064 bytes per table
-#define PREP_B 8                            // items per lane in the batched inversion
-#define POINT_THREADS 512
+#define PREP_B 2                            // items per lane in the batched inversion
+#define POINT_THREADS 1024
+#define POINT_LANES_MAX 8    // lanes cooperating on one verify in k_point (partial sums + tree)
+#define DIG_STRIDE 96        // bytes per item of the digit array: (d1, d2) pairs for 43 windows
 #define ST_PENDING 0xFF
 
 struct apoint_raw {  // affine point, Montgomery limbs (64 B, 16-B aligned)
@@ -26,12 +28,13 @@ struct jpoint_raw {  // key-table build scratch: Jacobian point + prefix product
 
 __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw *tables,
                          jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys);
-__global__ void k_prep(uint32_t n, uint8_t *status, const uint32_t *key_slot, const uint8_t *key_ok,
-                       const uint32_t *r_limbs, const uint32_t *s_limbs, const uint8_t *digests,
-                       const uint32_t *dig_idx, int8_t *d1, int8_t *d2, uint32_t *w_scratch);
-__global__ void k_point(uint32_t n, uint8_t *status, const uint32_t *key_slot, const apoint_raw *gtab,
-                        const apoint_raw *ktab, const int8_t *d1, const int8_t *d2,
-                        const uint32_t *r_limbs);
+__global__ void k_inv(uint32_t n, uint8_t *status, const uint32_t *key_slot, const uint8_t *key_ok,
+                      const uint32_t *r_limbs, const uint32_t *s_limbs, uint32_t *w_out, uint32_t *w_scratch);
+__global__ void k_prep(uint32_t n, const uint8_t *status, const uint32_t *r_limbs, const uint32_t *w_in,
+                       const uint8_t *digests, const uint32_t *dig_idx, int8_t *digits);
+__global__ void k_point(uint32_t n, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot, const apoint_raw *gtab,
+                        const apoint_raw *ktab, const int8_t *digits, const uint32_t *r_limbs);
+#define INV_THREADS 128
 struct ShaJob {  // message = span0 || span1 || span2 (absolute device addresses)
   uint64_t p[3];
   uint32_t n[3];

@@ -5,7 +5,7 @@
 //     Because p == -1 mod 2^32, the Montgomery factor is m = t[i] and m*p only touches
 //     limbs i, i+3, i+6, i+7, i+8 -- the reduction is 9 VALU adds per limb, no multiplies.
 //   * Scalar field Z_n (group order): generic CIOS Montgomery, used only in the per-item
-//     scalar preparation (w = s^-1, u1 = e*w, u2 = r*w).
+//     scalar preparation (u1 = e*w, u2 = r*w; the inversion itself is p256_modinv.h).
 // All integer VALU work (v_mad_u64_u32 + add-with-carry chains); no MFMA, no FP.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -241,20 +241,29 @@ FGV_DEV void sn_mul(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
   sn_final_sub(r, t, t[8]);
 }
 
-// a^(n-2) mod n (Montgomery domain in and out)
-__device__ __noinline__ void sn_inv(uint32_t r[8], const uint32_t a[8], const uint32_t one[8]) {
-  // n - 2 little-endian
-  const uint32_t e[8] = {0xFC63254Fu, 0xF3B9CAC2u, 0xA7179E84u, 0xBCE6FAADu,
-                         0xFFFFFFFFu, 0xFFFFFFFFu, 0x00000000u, 0xFFFFFFFFu};
-  uint32_t acc[8];
+// Montgomery reduction mod n of a 512-bit t (generic REDC, 8 rounds)
+FGV_DEV void sn_redc(uint32_t r[8], uint32_t t[16]) {
+  uint32_t pend = 0u;
 #pragma unroll
-  for (int i = 0; i < 8; i++) acc[i] = one[i];
-  for (int i = 255; i >= 0; i--) {
-    sn_mul(acc, acc, acc);
-    if ((e[i >> 5] >> (i & 31)) & 1u) sn_mul(acc, acc, a);
+  for (int i = 0; i < 8; i++) {
+    const uint32_t m = t[i] * N_0INV;
+    uint64_t c = (uint64_t)m * N_LIMBS[0] + t[i];
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      c = (uint64_t)m * N_LIMBS[j] + t[i + j] + (c >> 32);
+      t[i + j] = (uint32_t)c;
+    }
+    uint64_t s = (uint64_t)t[i + 8] + (c >> 32) + pend;
+    t[i + 8] = (uint32_t)s;
+    pend = (uint32_t)(s >> 32);
   }
-#pragma unroll
-  for (int i = 0; i < 8; i++) r[i] = acc[i];
+  sn_final_sub(r, t + 8, pend);
+}
+// Montgomery squaring mod n (off-diagonal products once)
+FGV_DEV void sn_sqr(uint32_t r[8], const uint32_t a[8]) {
+  uint32_t t[16];
+  sqr_256(t, a);
+  sn_redc(r, t);
 }
 
 // compare 256-bit little-endian: a < b
@@ -308,7 +317,8 @@ FGV_DEV void pt_dbl(jpoint &r, const jpoint &p) {
 
 // Complete mixed addition r = p + q (q affine, never infinity), madd-2004-hmv (8M + 3S)
 // with the exceptional cases routed: p = inf -> q; p = q -> dbl; p = -q -> inf.
-__device__ __noinline__ void pt_madd(jpoint &r, const jpoint &p, const apoint &q) {
+// Inlined: callers keep exactly one call site in their loop (no scratch traffic).
+FGV_DEV void pt_madd(jpoint &r, const jpoint &p, const apoint &q) {
   if (fe_is_zero(p.z)) {
     r.x = q.x; r.y = q.y; fe_set_one(r.z);
     return;
@@ -347,8 +357,8 @@ __device__ __noinline__ void pt_madd(jpoint &r, const jpoint &p, const apoint &q
   r.y = y3;
 }
 
-// Complete Jacobian addition (key-table build only)
-__device__ __noinline__ void pt_add(jpoint &r, const jpoint &p, const jpoint &q) {
+// Complete Jacobian addition (inlined form: one call site per loop)
+FGV_DEV void pt_add_inl(jpoint &r, const jpoint &p, const jpoint &q) {
   if (fe_is_zero(p.z)) { r = q; return; }
   if (fe_is_zero(q.z)) { r = p; return; }
   fe z1z1, z2z2, u1, u2, s1, s2, h, rr, t;
@@ -387,3 +397,6 @@ __device__ __noinline__ void pt_add(jpoint &r, const jpoint &p, const jpoint &q)
   fe_mul(z3, z3, h);
   r.x = x3; r.y = y3; r.z = z3;
 }
+
+// out-of-line form (key-table build)
+__device__ __noinline__ void pt_add(jpoint &r, const jpoint &p, const jpoint &q) { pt_add_inl(r, p, q); }

@@ -4,18 +4,24 @@
 //   k_keytab  (per NEW public key, cached across batches) -- fixed-base comb table
 //             T_Q[w][k-1] = k * 2^(6w) * Q, w < 43, k = 1..32, affine Montgomery (88 KB/key).
 //             The generator table T_G is the same kernel run once on G at init.
-//   k_prep    (per item, PREP_B items per lane) -- range checks, w = s^-1 mod n with a
-//             per-lane batched (Montgomery-trick) inversion, u1 = e*w, u2 = r*w,
-//             signed 6-bit recoding of u1/u2 into 43 digits each.
-//   k_point   (per item) -- R = sum_w T_G[w][d1_w] + T_Q[w][d2_w]: 86 complete mixed
-//             additions and NO doublings; T_G staged in LDS (88 KB), T_Q gathered from
-//             HBM/L2; then x_R mod n == r checked projectively (X == r*Z^2 or (r+n)*Z^2).
+//   k_inv     (PREP_B items per lane) -- range checks, w = s^-1 mod n with a per-lane
+//             batched (Montgomery-trick) inversion; independent of the digests, so it runs
+//             concurrently with the SHA-256 jobs of a block batch (second stream).
+//   k_prep    (per item) -- u1 = e*w, u2 = r*w, signed 6-bit recoding into 43 digits each.
+//   k_point   (L lanes per item, L chosen per batch) -- R = sum_w T_G[w][d1_w] + T_Q[w][d2_w]: 86
+//             complete mixed additions and NO doublings, split over the lanes of a group
+//             (lane j sums windows j, j+L, ...), then a log2(L)-level butterfly of complete
+//             Jacobian additions across the group (cross-lane shuffles); T_G staged in LDS
+//             (88 KB), T_Q gathered from HBM/L2; x_R mod n == r checked projectively
+//             (X == r*Z^2 or (r+n)*Z^2).  The split cuts the per-item latency ~L-fold, which
+//             is what bounds block-sized batches (tens of thousands of verifies).
 //
 // Semantics restated: Go 1.21.9 crypto/ecdsa verifyNISTEC (SEC 1 v2 s4.1.4) behind
 // fabric-lib-go bccsp/sw/ecdsa.go:41-57.  Exceptional additions (P == Q, P == -Q, inf)
 // are handled exactly, so results are bit-exact for adversarial inputs as well.
 #include "p256_field.h"
 #include "fgv_kernels.h"
+#include "p256_modinv.h"
 
 // R^2 mod p (to Montgomery), little-endian limbs
 __constant__ static const uint32_t R2P[8] = {0x00000003u, 0x00000000u, 0xFFFFFFFFu, 0xFFFFFFFBu,
@@ -157,21 +163,29 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
   }
 }
 
-// ---------------------------------------------------------------- k_prep
-// Items are processed in PREP_B strided rounds per lane: item = lane + b * nlanes.
-// in:  status (0xFF = pending; host pre-decided otherwise), key slot, r/s as plain
-//      little-endian limbs [8][n] (limb-major), digests [*][32] big-endian bytes, item i
-//      using digest dig_idx[i] (or i when dig_idx is null).
-// out: status (4/5 decided here), digits d1/d2 [NWIN][n] int8.
-__global__ __launch_bounds__(256) void k_prep(uint32_t n, uint8_t *__restrict__ status,
-                                              const uint32_t *__restrict__ key_slot,
-                                              const uint8_t *__restrict__ key_ok,
-                                              const uint32_t *__restrict__ r_limbs,
-                                              const uint32_t *__restrict__ s_limbs,
-                                              const uint8_t *__restrict__ digests,
-                                              const uint32_t *__restrict__ dig_idx,
-                                              int8_t *__restrict__ d1, int8_t *__restrict__ d2,
-                                              uint32_t *__restrict__ w_scratch) {
+// ---------------------------------------------------------------- k_inv / k_prep
+// Scalar preparation is split so the long part (s^-1, which needs only s) can run
+// concurrently with the SHA-256 jobs that produce the digests:
+//   k_inv   items in PREP_B strided rounds per lane (item = lane + b * nlanes): range checks
+//           (status 4/5), s -> Montgomery, prefix products, ONE inversion per lane by
+//           Bernstein-Yang divsteps (p256_modinv.h; ~6x shorter critical path than the Fermat
+//           chain), walk back -> w = s^-1 (Montgomery form) [8][n].
+//   k_prep  one item per lane: e = digest mod n, u1 = e*w, u2 = r*w, signed 6-bit recoding
+//           into (d1, d2) digit pairs [n][DIG_STRIDE].
+// R^3 mod n: maps the plain inverse of a Montgomery representative back to Montgomery form
+// (sn_mul(X^-1, R^3) = (A*R)^-1 * R^2 = A^-1 * R)
+__constant__ static const uint32_t R3N[8] = {0x0b65a624u, 0xac8ebec9u, 0x0c0555c9u, 0x111f28aeu,
+                                              0x6ba5e93fu, 0x2543b924u, 0x6407be65u, 0x503a54e7u};
+
+__global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, uint8_t *__restrict__ status,
+                                                     const uint32_t *__restrict__ key_slot,
+                                                     const uint8_t *__restrict__ key_ok,
+                                                     const uint32_t *__restrict__ r_limbs,
+                                                     const uint32_t *__restrict__ s_limbs,
+                                                     uint32_t *__restrict__ w_out,
+                                                     uint32_t *__restrict__ w_scratch) {
+  // latency-critical: it runs beside the SHA-256 jobs (second stream); win VALU arbitration
+  __builtin_amdgcn_s_setprio(2);
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nl = gridDim.x * blockDim.x;
   uint32_t one[8], r2n[8], acc[8];
@@ -212,15 +226,17 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, uint8_t *__restrict__ 
     for (int k = 0; k < 8; k++) w_scratch[((size_t)b * 8 + k) * nl + lane] = acc[k];
   }
   if (live == 0) return;
-  uint32_t inv[8];
-  sn_inv(inv, acc, one);  // (prod s_m)^-1 in Montgomery form
+  uint32_t inv[8], r3n[8];
+  fgv_modinv::modinv_n(inv, acc);  // plain inverse of the Montgomery representative
+#pragma unroll
+  for (int i = 0; i < 8; i++) r3n[i] = R3N[i];
+  sn_mul(inv, inv, r3n);  // (prod s_m)^-1 in Montgomery form
   // pass 2: walk back, w_b = inv * prefix_{b-1}; inv *= s_m[b]
 #pragma unroll 1
   for (int b = PREP_B - 1; b >= 0; b--) {
     if (!((live >> b) & 1u)) continue;
     const uint32_t i = lane + (uint32_t)b * nl;
-    uint32_t prev[8], w[8], r[8], s[8], sm[8], e[8], u1[8], u2[8];
-    // prefix_{b-1}: scan down to the previous slot (prefix unchanged over dead slots)
+    uint32_t prev[8], w[8], s[8], sm[8];
     if (b > 0) {
 #pragma unroll
       for (int k = 0; k < 8; k++) prev[k] = w_scratch[((size_t)(b - 1) * 8 + k) * nl + lane];
@@ -231,41 +247,60 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, uint8_t *__restrict__ 
     sn_mul(w, inv, prev);  // s^-1 * R (Montgomery)
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      r[k] = r_limbs[(size_t)k * n + i];
       s[k] = s_limbs[(size_t)k * n + i];
+      w_out[(size_t)k * n + i] = w[k];
     }
     sn_mul(sm, s, r2n);
     sn_mul(inv, inv, sm);
-    // e = leftmost 256 bits of the digest, mod n (digest is exactly 32 bytes)
-    const uint32_t di = dig_idx ? dig_idx[i] : i;
-    const uint32_t *dg = reinterpret_cast<const uint32_t *>(digests + (size_t)di * 32);
+  }
+}
+
+// in:  status, r limbs, w = s^-1 (Montgomery) from k_inv, digests [*][32] big-endian, item i
+//      using digest dig_idx[i] (or i when dig_idx is null).
+// out: digits [n][DIG_STRIDE] int8: (d1_w, d2_w) pairs.
+__global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restrict__ status,
+                                              const uint32_t *__restrict__ r_limbs,
+                                              const uint32_t *__restrict__ w_in,
+                                              const uint8_t *__restrict__ digests,
+                                              const uint32_t *__restrict__ dig_idx,
+                                              int8_t *__restrict__ digits) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != ST_PENDING) return;
+  uint32_t w[8], r[8], e[8], u1[8], u2[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) e[k] = __builtin_bswap32(dg[7 - k]);
-    if (!lt_n(e)) {
-      uint32_t bo = 0;
+  for (int k = 0; k < 8; k++) {
+    w[k] = w_in[(size_t)k * n + i];
+    r[k] = r_limbs[(size_t)k * n + i];
+  }
+  // e = leftmost 256 bits of the digest, mod n (digest is exactly 32 bytes)
+  const uint32_t di = dig_idx ? dig_idx[i] : i;
+  const uint32_t *dg = reinterpret_cast<const uint32_t *>(digests + (size_t)di * 32);
 #pragma unroll
-      for (int k = 0; k < 8; k++) e[k] = subb(e[k], N_LIMBS[k], bo, &bo);
+  for (int k = 0; k < 8; k++) e[k] = __builtin_bswap32(dg[7 - k]);
+  if (!lt_n(e)) {
+    uint32_t bo = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) e[k] = subb(e[k], N_LIMBS[k], bo, &bo);
+  }
+  sn_mul(u1, e, w);  // e * s^-1 (plain)
+  sn_mul(u2, r, w);  // r * s^-1 (plain)
+  // signed base-64 recoding: digits in [-31, 32], 43 windows (top window <= 16)
+  int c1 = 0, c2 = 0;
+  uint16_t *dp = reinterpret_cast<uint16_t *>(digits + (size_t)i * DIG_STRIDE);
+#pragma unroll
+  for (int win = 0; win < NWIN; win++) {
+    const int bit = WBITS * win, li = bit >> 5, sh = bit & 31;
+    uint32_t v1 = u1[li] >> sh, v2 = u2[li] >> sh;
+    if (sh > 32 - WBITS && li < 7) {
+      v1 |= u1[li + 1] << (32 - sh);
+      v2 |= u2[li + 1] << (32 - sh);
     }
-    sn_mul(u1, e, w);  // e * s^-1 (plain)
-    sn_mul(u2, r, w);  // r * s^-1 (plain)
-    // signed base-64 recoding: digits in [-31, 32], 43 windows (top window <= 16)
-    int c1 = 0, c2 = 0;
-#pragma unroll
-    for (int win = 0; win < NWIN; win++) {
-      const int bit = WBITS * win, li = bit >> 5, sh = bit & 31;
-      uint32_t v1 = u1[li] >> sh, v2 = u2[li] >> sh;
-      if (sh > 32 - WBITS && li < 7) {
-        v1 |= u1[li + 1] << (32 - sh);
-        v2 |= u2[li + 1] << (32 - sh);
-      }
-      int a1 = (int)(v1 & 63u) + c1, a2 = (int)(v2 & 63u) + c2;
-      c1 = a1 > 32;
-      c2 = a2 > 32;
-      a1 -= c1 << 6;
-      a2 -= c2 << 6;
-      d1[(size_t)win * n + i] = (int8_t)a1;
-      d2[(size_t)win * n + i] = (int8_t)a2;
-    }
+    int a1 = (int)(v1 & 63u) + c1, a2 = (int)(v2 & 63u) + c2;
+    c1 = a1 > 32;
+    c2 = a2 > 32;
+    a1 -= c1 << 6;
+    a2 -= c2 << 6;
+    dp[win] = (uint16_t)((uint8_t)(int8_t)a1 | ((uint16_t)(uint8_t)(int8_t)a2 << 8));
   }
 }
 
@@ -279,43 +314,75 @@ FGV_DEV void lds_load_apoint(apoint &p, const uint4 *lds, uint32_t idx) {
   p.y.v[4] = d.x; p.y.v[5] = d.y; p.y.v[6] = d.z; p.y.v[7] = d.w;
 }
 
+FGV_DEV void shfl_fe(fe &r, const fe &a, int src_lane) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) r.v[k] = (uint32_t)__shfl((int)a.v[k], src_lane);
+}
+
+// L lanes per item (1..8, any value): a wave holds floor(64/L) groups (the remaining lanes
+// idle); lane `sub` of a group sums windows sub, sub+L, ...; then a binary tree over the
+// group's lanes (level m: lane sub takes lane sub^m's sum when that lane exists), leaving the
+// total in lane 0.  Persistent grid: one workgroup per CU, groups stride over the items.
 __global__ __launch_bounds__(POINT_THREADS) void k_point(
-    uint32_t n, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
+    uint32_t n, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
     const apoint_raw *__restrict__ gtab, const apoint_raw *__restrict__ ktab,
-    const int8_t *__restrict__ d1, const int8_t *__restrict__ d2,
-    const uint32_t *__restrict__ r_limbs) {
+    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs) {
   extern __shared__ uint4 lds_g[];
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(gtab);
     for (uint32_t j = threadIdx.x; j < KT_ENTRIES * 4; j += blockDim.x) lds_g[j] = src[j];
   }
   __syncthreads();
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t gpw = 64u / L;  // groups per wave
+  const uint32_t g = lane / L, sub = lane % L;
+  if (g >= gpw) return;  // idle tail lanes of the wave (no barrier follows)
+  const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t groups = waves * gpw;
+  const uint32_t base = lane - sub;  // lane of sub 0 in this group
+  // every lane of a group runs the same iterations (item-uniform control flow), so the
+  // cross-lane reads below always find their partners active
+  for (uint32_t i = (blockIdx.x * (blockDim.x >> 6) + wave) * gpw + g; i < n; i += groups) {
     if (status[i] != ST_PENDING) continue;
     const apoint_raw *qt = ktab + (size_t)key_slot[i] * KT_ENTRIES;
+    const int8_t *dg = digits + (size_t)i * DIG_STRIDE;
     jpoint acc;
     fe_set_zero(acc.x);
     fe_set_zero(acc.y);
     fe_set_zero(acc.z);
+    // terms t = 2*k + {0: G, 1: Q} of windows w = sub + k*L (one madd call site)
+    const int nterms = 2 * ((NWIN - (int)sub + (int)L - 1) / (int)L);
 #pragma unroll 1
-    for (int w = 0; w < NWIN; w++) {
-      const int a = d1[(size_t)w * n + i];
-      const int b = d2[(size_t)w * n + i];
-      if (a != 0) {
-        apoint p;
-        lds_load_apoint(p, lds_g, (uint32_t)(w * TAB_K + (a < 0 ? -a : a) - 1));
-        if (a < 0) fe_neg(p.y, p.y);
-        pt_madd(acc, acc, p);
-      }
-      if (b != 0) {
-        apoint p;
-        const apoint_raw *e = qt + w * TAB_K + (b < 0 ? -b : b) - 1;
+    for (int t = 0; t < nterms; t++) {
+      const int w = (int)sub + (t >> 1) * (int)L;
+      const bool isq = t & 1;
+      const int d = dg[2 * w + (isq ? 1 : 0)];
+      if (d == 0) continue;
+      const int k = (d < 0 ? -d : d) - 1;
+      apoint p;
+      if (!isq) {
+        lds_load_apoint(p, lds_g, (uint32_t)(w * TAB_K + k));
+      } else {
+        const apoint_raw *e = qt + w * TAB_K + k;
         load_fe(p.x, e->x);
         load_fe(p.y, e->y);
-        if (b < 0) fe_neg(p.y, p.y);
-        pt_madd(acc, acc, p);
       }
+      if (d < 0) fe_neg(p.y, p.y);
+      pt_madd(acc, acc, p);
     }
+    // tree: at level m lane sub adds lane (sub ^ m)'s partial sum when that lane exists;
+    // lane 0 ends with the sum over all L lanes
+#pragma unroll 1
+    for (uint32_t m = 1; m < L; m <<= 1) {
+      const uint32_t peer = sub ^ m;
+      const int src = (int)(base + (peer < L ? peer : sub));
+      jpoint o;
+      shfl_fe(o.x, acc.x, src);
+      shfl_fe(o.y, acc.y, src);
+      shfl_fe(o.z, acc.z, src);
+      if (peer < L) pt_add_inl(acc, acc, o);
+    }
+    if (sub != 0) continue;
     uint8_t st = 1;
     if (!fe_is_zero(acc.z)) {
       fe r, rm, z2, lhs;
