@@ -7,7 +7,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-functi
 CSRC := fabric_amd/csrc
 OBJDIR := build
 KOBJS := $(OBJDIR)/sha256.o $(OBJDIR)/p256_kernels.o $(OBJDIR)/der_kernel.o $(OBJDIR)/fgv_host.o $(OBJDIR)/fgv_block.o $(OBJDIR)/mvcc.o $(OBJDIR)/fgv_mvcc.o \
-	$(OBJDIR)/finalize.o
+	$(OBJDIR)/finalize.o $(OBJDIR)/fgv_integrity.o
 HDRS := $(CSRC)/p256_field.h $(CSRC)/fgv_kernels.h $(CSRC)/fgv_der.h $(CSRC)/fgv_internal.h include/fgv.h
 
 all: fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so
@@ -25,6 +25,9 @@ $(OBJDIR)/fgv_block.o: $(CSRC)/fgv_block.cpp $(HDRS) $(CSRC)/pbwire.h $(CSRC)/fg
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/fgv_mvcc.o: $(CSRC)/fgv_mvcc.cpp $(HDRS) $(CSRC)/pbwire.h $(CSRC)/fgv_visitors.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/fgv_integrity.o: $(CSRC)/fgv_integrity.cpp $(HDRS) $(CSRC)/pbwire.h $(CSRC)/fgv_visitors.h $(CSRC)/sha256_host.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 fabric_amd/libfgv.so: $(KOBJS)

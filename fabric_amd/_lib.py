@@ -23,6 +23,7 @@ EXPORTED = [
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
+    "fgv_blocks_verify", "fgv_sha256_host",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -36,6 +37,22 @@ class FgvError(RuntimeError):
 
 class Unsupported(FgvError):
     """FGV_EUNSUPPORTED: the batch needs logic outside the engine's model."""
+
+
+class ChainState(ctypes.Structure):
+    """fgv_chain_state: the last verified block header (number + BlockHeaderHash)."""
+    _fields_ = [("number", ctypes.c_uint64), ("header_hash", ctypes.c_uint8 * 32), ("valid", ctypes.c_uint8),
+                ("has_hash", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 6)]
+
+
+class BlockCheck(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("bad_tx", ctypes.c_uint32), ("number", ctypes.c_uint64),
+                ("data_hash", ctypes.c_uint8 * 32), ("header_hash", ctypes.c_uint8 * 32)]
+
+
+# fgv_block_check.status (include/fgv.h)
+BLK_OK, BLK_UNPARSABLE, BLK_NO_HEADER, BLK_NUMBER, BLK_PREV_HASH, BLK_METADATA, BLK_EMPTY, BLK_TX_MALFORMED, \
+    BLK_DATA_HASH = range(9)
 
 
 class _Config(ctypes.Structure):
@@ -91,6 +108,8 @@ def load():
         L.fgv_mvcc_last_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.POINTER(ctypes.c_uint32)]
+        L.fgv_blocks_verify.argtypes = [vp, sz, vp, vp, vp, vp]
+        L.fgv_sha256_host.argtypes = [vp, sz, vp]
         _L = L
     return _L
 
@@ -283,6 +302,10 @@ class Engine:
                                               ctypes.c_void_p(d_gathered), _ptr(flags)))
         return flags
 
+    # --- deliver-side block integrity (VerifyBlock minus orderer signatures)
+    def blocks_verify(self, blocks, chain=None):
+        return blocks_verify(blocks, chain, ctx=self._h)
+
     # --- MVCC
     def statedb_init(self, slots=1 << 22, arena_bytes=64 << 20):
         _check(self._L.fgv_statedb_init(self._h, slots, arena_bytes))
@@ -319,3 +342,25 @@ def finalize_flags(ntx, results):
     flags = np.zeros(int(ntx.sum()), dtype=np.uint8)
     _check(L.fgv_finalize_flags(len(ntx), _ptr(ntx), _ptr(results), _ptr(flags)))
     return flags
+
+
+def blocks_verify(blocks, chain=None, ctx=None):
+    """fgv_blocks_verify: per-block (status, bad_tx, number, data_hash, header_hash); `chain`
+    (ChainState) is advanced past every verified block.  ctx None -> one host thread."""
+    L = load()
+    nb = len(blocks)
+    bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+    ptrs = (ctypes.c_void_p * nb)(*[b.ctypes.data for b in bufs])
+    lens = (ctypes.c_size_t * nb)(*[len(b) for b in blocks])
+    out = (BlockCheck * nb)()
+    _check(L.fgv_blocks_verify(ctx, nb, ptrs, lens, ctypes.byref(chain) if chain is not None else None, out))
+    return [(o.status, o.bad_tx, o.number, bytes(o.data_hash), bytes(o.header_hash)) for o in out]
+
+
+def sha256_host(buf: bytes):
+    """Host SHA-256 (the data-hash primitive).  Returns (digest, used_sha_extensions)."""
+    L = load()
+    out = ctypes.create_string_buffer(32)
+    b = np.frombuffer(buf, dtype=np.uint8) if len(buf) else np.zeros(1, np.uint8)
+    ni = L.fgv_sha256_host(b.ctypes.data, len(buf), out)
+    return out.raw, bool(ni)

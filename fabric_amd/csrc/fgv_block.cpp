@@ -37,6 +37,7 @@
 
 #include "../../include/fgv.h"
 #include "fgv_internal.h"
+#include "thread_pool.h"
 #include "pbwire.h"
 
 #include "fgv_visitors.h"
@@ -281,71 +282,6 @@ struct TxRec {
 
 // ======================================================================= context glue
 using namespace fgvb;
-
-struct ThreadPool {
-  std::vector<std::thread> th;
-  std::mutex mu;
-  std::condition_variable cv, done_cv;
-  std::function<void(size_t)> job;
-  size_t njobs = 0;
-  std::atomic<size_t> next{0};
-  size_t active = 0;
-  uint64_t gen = 0;
-  bool stop = false;
-  explicit ThreadPool(unsigned n) {
-    for (unsigned i = 0; i < n; i++)
-      th.emplace_back([this] {
-        uint64_t seen = 0;
-        for (;;) {
-          std::unique_lock<std::mutex> lk(mu);
-          cv.wait(lk, [&] { return stop || gen != seen; });
-          if (stop) return;
-          seen = gen;
-          lk.unlock();
-          for (size_t i; (i = next.fetch_add(1)) < njobs;) job(i);
-          lk.lock();
-          if (--active == 0) done_cv.notify_all();
-        }
-      });
-  }
-  ~ThreadPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      stop = true;
-    }
-    cv.notify_all();
-    for (auto &t : th) t.join();
-  }
-  // run f(j) for every job j in [0, njobs) on the pool (dynamic assignment)
-  void run(size_t nj, const std::function<void(size_t)> &f) {
-    if (nj == 0) return;
-    if (th.empty() || nj == 1) {
-      for (size_t i = 0; i < nj; i++) f(i);
-      return;
-    }
-    std::unique_lock<std::mutex> lk(mu);
-    job = f;
-    njobs = nj;
-    next = 0;
-    active = th.size();
-    gen++;
-    cv.notify_all();
-    done_cv.wait(lk, [&] { return active == 0; });
-  }
-  // run f(i) for i in [0, n) in chunks
-  void parallel_for(size_t n, const std::function<void(size_t)> &f) {
-    if (n == 0) return;
-    if (th.empty() || n < 64) {
-      for (size_t i = 0; i < n; i++) f(i);
-      return;
-    }
-    const size_t chunk = std::max<size_t>(16, n / (th.size() * 8));
-    run((n + chunk - 1) / chunk, [&](size_t c) {
-      size_t lo = c * chunk, hi = std::min(n, lo + chunk);
-      for (size_t i = lo; i < hi; i++) f(i);
-    });
-  }
-};
 
 struct fgv_block_state {
   Channel ch;

@@ -117,6 +117,7 @@ void fgv_destroy(fgv_ctx *c) {
                  &c->fz_owner, &c->fz_minblk, &c->fz_minvalid, &c->fz_flags, &c->fz_pslot, &c->fz_res};
   if (c->blk) fgv_block_state_free(c->blk);
   if (c->mv) fgv_mvcc_free(c->mv);
+  fgv_integrity_free(c);
   for (auto *b : d) b->release();
   HostBuf *h[] = {&c->h_status, &c->h_slot, &c->h_r, &c->h_s, &c->h_dig, &c->h_kq, &c->h_kslot,
                   &c->h_moff, &c->h_mlen, &c->hb_dig, &c->hb_vst, &c->hb_jobs, &c->hb_sigp,

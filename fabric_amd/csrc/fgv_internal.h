@@ -18,6 +18,7 @@
 
 struct fgv_block_state;
 struct fgv_mvcc_state;
+struct ThreadPool;
 
 namespace fgvh {
 
@@ -119,7 +120,12 @@ struct fgv_ctx {
   double t_mvcc_lookup = 0, t_mvcc_total = 0;
   double t_host_parse = 0, t_host_assemble = 0, t_host_device = 0, t_host_fold = 0;
   uint64_t n_mvcc_reads = 0, n_mvcc_writes = 0;
+  // deliver-side integrity (fgv_integrity.cpp): own host pool, own lock -- runs concurrently
+  // with committer calls on the same context
+  ThreadPool *integ_pool = nullptr;
+  std::mutex integ_mu;
 };
+void fgv_integrity_free(fgv_ctx *c);
 
 #define HIP_TRY(x)                                     \
   do {                                                 \

@@ -28,6 +28,11 @@ def lib():
         L.synth_make_cert.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                       ctypes.c_char_p, ctypes.c_int, ctypes.c_long, ctypes.c_char_p,
                                       ctypes.c_size_t]
+        L.synth_ed25519_keygen.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p]
+        L.synth_ed25519_sign_batch.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_size_t, ctypes.c_void_p]
+        L.synth_make_cert_ed25519.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                              ctypes.c_char_p, ctypes.c_long, ctypes.c_char_p, ctypes.c_size_t]
         _LIB = L
     return _LIB
 
@@ -80,6 +85,45 @@ def make_cert(subject: Key, issuer: Key, cn: str, org: str, issuer_cn: str, is_c
     out = ctypes.create_string_buffer(4096)
     n = lib().synth_make_cert(subject.priv, issuer.priv, cn.encode(), org.encode(), issuer_cn.encode(),
                               1 if is_ca else 0, serial, out, 4096)
+    if n < 0:
+        raise RuntimeError("certificate generation failed")
+    return out.raw[:n]
+
+
+class EdKey:
+    """An Ed25519 key pair derived deterministically from (seed, idx) (config C5)."""
+
+    kind = "ed25519"
+
+    def __init__(self, seed: int, idx: int):
+        priv = ctypes.create_string_buffer(32)
+        pub = ctypes.create_string_buffer(32)
+        if lib().synth_ed25519_keygen(seed, idx, priv, pub) != 0:
+            raise RuntimeError("ed25519 keygen failed")
+        self.priv, self.pub = priv.raw, pub.raw
+
+
+def ed25519_sign_batch(privs: bytes, msgs):
+    """RFC 8032 signatures (64 B) of msgs[i] under privs[32*i:32*i+32]."""
+    import numpy as np
+    n = len(msgs)
+    if n == 0:
+        return []
+    off = np.zeros(n, np.uint64)
+    ln = np.array([len(m) for m in msgs], np.uint32)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    buf = b"".join(msgs)
+    out = ctypes.create_string_buffer(64 * n)
+    if lib().synth_ed25519_sign_batch(privs, buf, off.ctypes.data, ln.ctypes.data, n, out) != 0:
+        raise RuntimeError("ed25519 signing failed")
+    raw = out.raw
+    return [raw[64 * i: 64 * i + 64] for i in range(n)]
+
+
+def make_cert_ed25519(subject: EdKey, issuer: Key, cn: str, org: str, issuer_cn: str, serial: int) -> bytes:
+    out = ctypes.create_string_buffer(4096)
+    n = lib().synth_make_cert_ed25519(subject.priv, issuer.priv, cn.encode(), org.encode(), issuer_cn.encode(),
+                                      serial, out, 4096)
     if n < 0:
         raise RuntimeError("certificate generation failed")
     return out.raw[:n]

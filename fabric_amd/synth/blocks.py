@@ -19,7 +19,7 @@ vendor/github.com/hyperledger/fabric-protos-go).
 import hashlib
 import random
 
-from . import Key, make_cert, sign_batch
+from . import EdKey, Key, ed25519_sign_batch, make_cert, make_cert_ed25519, sign_batch
 
 # ------------------------------------------------------------------ proto3 encoding
 
@@ -105,8 +105,11 @@ def chaincode_id(name: str, version: str = "") -> bytes:
 # ------------------------------------------------------------------ network
 
 class Identity:
-    def __init__(self, key: Key, mspid: str, pem: bytes, role: str):
+    """key: synth.Key (P-256) or synth.EdKey (Ed25519, config C5)."""
+
+    def __init__(self, key, mspid: str, pem: bytes, role: str):
         self.key, self.mspid, self.pem, self.role = key, mspid, pem, role
+        self.kind = getattr(key, "kind", "p256")
         self.serialized = serialized_identity(mspid, pem)
         der = _pem_to_der(pem)
         self.id_digest = hashlib.sha256(der).digest()  # identity Id = hex(SHA-256(cert.Raw))
@@ -119,29 +122,56 @@ def _pem_to_der(pem: bytes) -> bytes:
 
 
 class Network:
-    """orgs: number of MSPs; clients: client identities (spread over the orgs)."""
+    """orgs: number of MSPs; clients: client identities (spread over the orgs);
+    peers_per_org: endorsing peers per org; ed25519_frac / ed25519_peers: share of the clients
+    and number of the peers that hold Ed25519 keys (config C5, "Fabric v3" identities)."""
 
-    def __init__(self, seed=3, orgs=3, clients=100, channel="testchannel", policy_n=2, pems=None):
+    def __init__(self, seed=3, orgs=3, clients=100, channel="testchannel", policy_n=2, pems=None,
+                 peers_per_org=1, ed25519_frac=0.0, ed25519_peers=0):
         """pems: certificates exported by another process (Network.export_pems()) -- X.509
         signatures are randomised, so multi-process users share one set of certificates."""
-        self.seed, self.channel = seed, channel
+        self.seed, self.channel, self.policy_n = seed, channel, policy_n
         _pem_iter = iter(pems) if pems is not None else None
+        sel = random.Random(seed * 7919 + 17)
+
+        # which identities hold Ed25519 keys: ed25519_frac of the clients, ed25519_peers peers
+        npeer = orgs * peers_per_org
+        kc = int(round(ed25519_frac * clients))
+        ed_clients = set(sel.sample(range(clients), kc)) if kc else set()
+        ed_peers = set(sel.sample(range(npeer), min(ed25519_peers, npeer))) if ed25519_peers else set()
 
         def cert(*a):  # reuse exported certificates in order
             return next(_pem_iter) if _pem_iter is not None else make_cert(*a)
+
+        def ed_cert(*a):
+            return next(_pem_iter) if _pem_iter is not None else make_cert_ed25519(*a)
         self.mspids = [f"Org{i + 1}MSP" for i in range(orgs)]
         self.cas, self.peers, self.clients = [], [], []
+        self.org_peers = [[] for _ in range(orgs)]
         for o, m in enumerate(self.mspids):
-            ca = Key(seed, 10_000 + o)
-            self.cas.append(ca)
-            pk = Key(seed, 20_000 + o)
-            pem = cert(pk, ca, f"peer0.org{o + 1}", m, f"ca.org{o + 1}", False, 100 + o)
-            self.peers.append(Identity(pk, m, pem, "peer"))
+            self.cas.append(Key(seed, 10_000 + o))
+        for o, m in enumerate(self.mspids):
+            for q in range(peers_per_org):
+                idx = o * peers_per_org + q
+                name = f"peer{q}.org{o + 1}"
+                if idx in ed_peers:
+                    pk = EdKey(seed, 20_000 + idx)
+                    pem = ed_cert(pk, self.cas[o], name, m, f"ca.org{o + 1}", 100 + idx)
+                else:
+                    pk = Key(seed, 20_000 + idx)
+                    pem = cert(pk, self.cas[o], name, m, f"ca.org{o + 1}", False, 100 + idx)
+                ident = Identity(pk, m, pem, "peer")
+                self.peers.append(ident)
+                self.org_peers[o].append(ident)
         for c in range(clients):
             o = c % orgs
-            ck = Key(seed, 30_000 + c)
-            pem = cert(ck, self.cas[o], f"user{c}.org{o + 1}", self.mspids[o], f"ca.org{o + 1}", False,
-                            1000 + c)
+            name = f"user{c}.org{o + 1}"
+            if c in ed_clients:
+                ck = EdKey(seed, 30_000 + c)
+                pem = ed_cert(ck, self.cas[o], name, self.mspids[o], f"ca.org{o + 1}", 1000 + c)
+            else:
+                ck = Key(seed, 30_000 + c)
+                pem = cert(ck, self.cas[o], name, self.mspids[o], f"ca.org{o + 1}", False, 1000 + c)
             self.clients.append(Identity(ck, self.mspids[o], pem, "client"))
         # an identity from an MSP the channel does not know (deserialization fails)
         rk = Key(seed, 40_000)
@@ -160,9 +190,15 @@ class Network:
 
     def identities(self):
         """What the MSP layer knows: (serialized, mspid, pubkey64, valid, id_digest).
-        RogueMSP is unknown to the channel, so it is NOT listed (deserialize error)."""
+        RogueMSP is unknown to the channel, so it is NOT listed (deserialize error).  Neither
+        are Ed25519 identities: the reference's BCCSP x509 key importer accepts only ECDSA/RSA
+        keys (vendor/github.com/hyperledger/fabric-lib-go/bccsp/sw/keyimport.go:130-150, SURVEY
+        F4), so DeserializeIdentity fails for them -- creator -> BAD_CREATOR_SIGNATURE,
+        endorser -> skipped by SignatureSetToValidIdentities (common/policies/policy.go:363-395)."""
         out = []
         for ident in self.peers + self.clients:
+            if ident.kind != "p256":
+                continue
             out.append((ident.serialized, ident.mspid, ident.key.pub, True, ident.id_digest))
         out.append((self.forged.serialized, self.forged.mspid, self.forged.key.pub, False, self.forged.id_digest))
         return out
@@ -176,7 +212,9 @@ EXPECTED = {"clean": 0, "bad_creator_sig": 4, "one_bad_endorsement": 0, "policy_
             "dup_txid": 9, "bad_txid": 8, "bad_proposal_hash": 5, "bad_epoch": 3, "unknown_cc": 25,
             "two_actions": 5, "rogue_creator": 4, "high_s_creator": 4, "dup_endorser": 10,
             "forged_endorser": 10, "event_other_cc": 255, "bad_payload": 2, "no_sig": 4,
-            "corrupt": None, "dup_txid_prev": 9}
+            "corrupt": None, "dup_txid_prev": 9, "ed25519_creator": 4, "endorse_short": 10}
+# labels whose code depends on the endorsement set (re-derived for C5-style networks)
+_ENDORSE_LABELS = ("clean", "one_bad_endorsement", "dup_txid")
 
 
 class _Tx:
@@ -208,6 +246,9 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         if force is not None and force[i] is not None:
             t.label = force[i]
         t.creator = net.rogue if t.label == "rogue_creator" else rng.choice(net.clients)
+        if t.creator.kind != "p256" and t.label in ("clean", "one_bad_endorsement", "policy_unsatisfied",
+                                                     "bad_creator_sig", "high_s_creator"):
+            t.label = "ed25519_creator"  # DeserializeIdentity fails
         t.nonce = bytes(rng.getrandbits(8) for _ in range(24))
         if reuse and i in reuse:
             t.creator, t.nonce = reuse[i]
@@ -226,18 +267,30 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
             if r < accp:
                 ne = e
                 break
-        orgs = rng.sample(range(len(net.peers)), min(ne, len(net.peers)))
-        t.endorsers = [net.peers[o] for o in orgs]
+        norg = len(net.org_peers)
+
+        def peer_of(o):
+            ps = net.org_peers[o]
+            return ps[0] if len(ps) == 1 else rng.choice(ps)
+        orgs = rng.sample(range(norg), min(ne, norg))
+        t.endorsers = [peer_of(o) for o in orgs]
         if t.label == "policy_unsatisfied":
             t.endorsers = t.endorsers[:1]
         if t.label == "dup_endorser":
             t.endorsers = [t.endorsers[0], t.endorsers[0]]
         if t.label == "forged_endorser":
             t.endorsers = [t.endorsers[0], net.forged]
-        if t.label == "one_bad_endorsement" and len(t.endorsers) < 3:
-            orgs = rng.sample(range(len(net.peers)), 3)
-            t.endorsers = [net.peers[o] for o in orgs]
+        need = getattr(net, "policy_n", 2) + 1
+        if t.label == "one_bad_endorsement" and len(t.endorsers) < need:
+            orgs = rng.sample(range(norg), min(need, norg))
+            t.endorsers = [peer_of(o) for o in orgs]
         t.bad_endorsement = rng.randrange(len(t.endorsers)) if t.label == "one_bad_endorsement" else -1
+        if t.label in _ENDORSE_LABELS:
+            # distinct orgs among the P-256 endorsers with a good signature (Ed25519 endorsers
+            # fail DeserializeIdentity and are skipped) must satisfy OutOf(policy_n, orgs)
+            good = {e.mspid for j, e in enumerate(t.endorsers) if e.kind == "p256" and j != t.bad_endorsement}
+            if len(good) < getattr(net, "policy_n", 2):
+                t.label = "endorse_short"
         t.reads = [(f"k{rng.randrange(key_space):07d}", (rng.randrange(1, 1000), rng.randrange(500)))
                    for _ in range(reads)]
         t.writes = [(f"k{rng.randrange(key_space):07d}", bytes(rng.getrandbits(8) for _ in range(value_len)), False)
@@ -248,6 +301,7 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
 
     # pass 1: headers, proposal response payloads, endorsement digests
     e_privs, e_digests, e_refs = [], [], []
+    ed_privs, ed_msgs, ed_refs = [], [], []
     for t in txs:
         txid = hashlib.sha256(t.nonce + t.creator.serialized).hexdigest()
         if t.label == "bad_txid":
@@ -268,13 +322,18 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         cca = f_bytes(1, rw) + f_bytes(2, events) + f_msg(3, f_varint(1, 200)) + f_msg(4, chaincode_id(ccname, "1.0"))
         t.prp = f_bytes(1, ph) + f_bytes(2, cca)
         for j, e in enumerate(t.endorsers):
+            if e.kind != "p256":
+                ed_privs.append(e.key.priv)
+                ed_msgs.append(t.prp + e.serialized)
+                ed_refs.append((t, j))
+                continue
             e_privs.append(e.key.priv)
             e_digests.append(hashlib.sha256(t.prp + e.serialized).digest())
             e_refs.append((t, j))
     esigs = sign_batch(b"".join(e_privs), b"".join(e_digests), len(e_privs), threads=threads) if e_privs else []
     for t in txs:
         t.esigs = [None] * len(t.endorsers)
-    for (t, j), s in zip(e_refs, esigs):
+    for (t, j), s in list(zip(e_refs, esigs)) + list(zip(ed_refs, ed25519_sign_batch(b"".join(ed_privs), ed_msgs))):
         if j == t.bad_endorsement:
             s = s[:10] + bytes([s[10] ^ 0x55]) + s[11:]
         t.esigs[j] = s
@@ -292,10 +351,15 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         t.payload = f_msg(1, hdr) + f_bytes(2, action)
         if t.label == "bad_payload":
             t.payload = t.payload[:-3]  # truncated -> Payload unmarshal error
-        c_privs.append(t.creator.key.priv)
-        c_digests.append(hashlib.sha256(t.payload).digest())
+        if t.creator.kind == "p256":
+            c_privs.append(t.creator.key.priv)
+            c_digests.append(hashlib.sha256(t.payload).digest())
     csigs = sign_batch(b"".join(c_privs), b"".join(c_digests), len(c_privs), threads=threads,
                        high_s=False) if c_privs else []
+    ed_tx = [t for t in txs if t.creator.kind != "p256"]
+    ed_sigs = iter(ed25519_sign_batch(b"".join(t.creator.key.priv for t in ed_tx), [t.payload for t in ed_tx]))
+    p_sigs = iter(csigs)
+    csigs = [next(p_sigs) if t.creator.kind == "p256" else next(ed_sigs) for t in txs]
     envs = []
     for t, s in zip(txs, csigs):
         if t.label == "bad_creator_sig":

@@ -196,3 +196,81 @@ int synth_make_cert(const uint8_t subj_priv[32], const uint8_t issuer_priv[32], 
   EVP_PKEY_free(ipk);
   return ret;
 }
+
+/* ---------------------------------------------------------------- Ed25519 (config C5)
+ * Fabric v3-style Ed25519 identities.  The reference snapshot's BCCSP x509 key importer
+ * accepts only ECDSA/RSA keys, so these identities fail DeserializeIdentity;
+ * the generator still produces real RFC 8032 signatures so the blocks are well formed. */
+static EVP_PKEY *ed_from_priv(const uint8_t priv[32]) {
+  return EVP_PKEY_new_raw_private_key(EVP_PKEY_ED25519, NULL, priv, 32);
+}
+
+/* priv = SHA-256("fgv-ed25519" || seed || idx); pub = the RFC 8032 public key */
+int synth_ed25519_keygen(uint64_t seed, uint32_t idx, uint8_t priv[32], uint8_t pub[32]) {
+  uint8_t buf[11 + 8 + 4];
+  memcpy(buf, "fgv-ed25519", 11);
+  memcpy(buf + 11, &seed, 8);
+  memcpy(buf + 19, &idx, 4);
+  SHA256(buf, sizeof buf, priv);
+  EVP_PKEY *k = ed_from_priv(priv);
+  if (!k) return -1;
+  size_t n = 32;
+  int ok = EVP_PKEY_get_raw_public_key(k, pub, &n) == 1 && n == 32;
+  EVP_PKEY_free(k);
+  return ok ? 0 : -1;
+}
+
+/* n messages (concatenated, offsets/lengths) signed with privs[i] (32 B each); 64-byte
+ * signatures into sig_out[i*64] */
+int synth_ed25519_sign_batch(const uint8_t *privs, const uint8_t *msgs, const uint64_t *off,
+                             const uint32_t *len, size_t n, uint8_t *sig_out) {
+  for (size_t i = 0; i < n; i++) {
+    EVP_PKEY *k = ed_from_priv(privs + 32 * i);
+    EVP_MD_CTX *c = EVP_MD_CTX_new();
+    size_t sl = 64;
+    int ok = k && c && EVP_DigestSignInit(c, NULL, NULL, NULL, k) == 1 &&
+             EVP_DigestSign(c, sig_out + 64 * i, &sl, msgs + off[i], len[i]) == 1 && sl == 64;
+    EVP_MD_CTX_free(c);
+    EVP_PKEY_free(k);
+    if (!ok) return -1;
+  }
+  return 0;
+}
+
+/* X.509 certificate for an Ed25519 subject key, issued (ecdsa-with-SHA256) by a P-256 CA */
+int synth_make_cert_ed25519(const uint8_t subj_ed_priv[32], const uint8_t issuer_priv[32], const char *cn,
+                            const char *org, const char *issuer_cn, long serial, char *pem_out, size_t cap) {
+  EVP_PKEY *spk = ed_from_priv(subj_ed_priv), *ipk = EVP_PKEY_new();
+  EVP_PKEY_assign_EC_KEY(ipk, key_from_priv(issuer_priv));
+  X509 *x = X509_new();
+  X509_set_version(x, 2);
+  ASN1_INTEGER_set(X509_get_serialNumber(x), serial);
+  ASN1_TIME_set_string(X509_getm_notBefore(x), "20240101000000Z");
+  ASN1_TIME_set_string(X509_getm_notAfter(x), "20340101000000Z");
+  X509_NAME *sn = X509_NAME_new(), *in = X509_NAME_new();
+  X509_NAME_add_entry_by_txt(sn, "O", MBSTRING_ASC, (const unsigned char *)org, -1, -1, 0);
+  X509_NAME_add_entry_by_txt(sn, "CN", MBSTRING_ASC, (const unsigned char *)cn, -1, -1, 0);
+  X509_NAME_add_entry_by_txt(in, "O", MBSTRING_ASC, (const unsigned char *)org, -1, -1, 0);
+  X509_NAME_add_entry_by_txt(in, "CN", MBSTRING_ASC, (const unsigned char *)issuer_cn, -1, -1, 0);
+  X509_set_subject_name(x, sn);
+  X509_set_issuer_name(x, in);
+  X509_set_pubkey(x, spk);
+  X509_sign(x, ipk, EVP_sha256());
+  BIO *b = BIO_new(BIO_s_mem());
+  PEM_write_bio_X509(b, x);
+  char *data;
+  long len = BIO_get_mem_data(b, &data);
+  int ret = -1;
+  if (len >= 0 && (size_t)len < cap) {
+    memcpy(pem_out, data, len);
+    pem_out[len] = 0;
+    ret = (int)len;
+  }
+  BIO_free(b);
+  X509_NAME_free(sn);
+  X509_NAME_free(in);
+  X509_free(x);
+  EVP_PKEY_free(spk);
+  EVP_PKEY_free(ipk);
+  return ret;
+}

@@ -201,6 +201,43 @@ int fgv_mvcc_validate_block(fgv_ctx *ctx, const uint8_t *block, size_t len, cons
 int fgv_mvcc_last_stats(fgv_ctx *ctx, double *lookup_ms, double *total_ms, uint64_t *reads,
                         uint64_t *writes, uint32_t *rounds);
 
+/* ------------------------------------------------- deliver-side block integrity (a20)
+ * BlockVerificationAssistant.VerifyBlock (common/deliverclient/block_verification.go:243-273)
+ * without the orderer-signature policy: verifyHeader (:311-331), verifyMetadata (:303-309),
+ * VerifyTransactionsAreWellFormed (protoutil/blockutils.go:310-350), Header.DataHash ==
+ * ComputeBlockDataHash (blockutils.go:76-79).  The chain state is the last verified header
+ * (number + BlockHeaderHash, blockutils.go:48-67); only a verified block advances it, as in
+ * the reference.  The data hash is one sequential SHA-256 chain per block: blocks hash in
+ * parallel on the context's host threads (SHA extensions when the CPU has them). */
+#define FGV_BLK_OK 0
+#define FGV_BLK_UNPARSABLE 1   /* proto.Unmarshal of the common.Block failed              */
+#define FGV_BLK_NO_HEADER 2    /* "header must be different from nil"                     */
+#define FGV_BLK_NUMBER 3       /* number != last verified + 1                              */
+#define FGV_BLK_PREV_HASH 4    /* PreviousHash != hash of the last verified header         */
+#define FGV_BLK_METADATA 5     /* fewer than 5 metadata entries                            */
+#define FGV_BLK_EMPTY 6        /* no transactions ("empty block")                         */
+#define FGV_BLK_TX_MALFORMED 7 /* envelope bad_tx is not well formed                      */
+#define FGV_BLK_DATA_HASH 8    /* Header.DataHash != SHA-256(concat(Data.Data))            */
+typedef struct fgv_chain_state {
+  uint64_t number;          /* last verified block number                     */
+  uint8_t header_hash[32];  /* its BlockHeaderHash                             */
+  uint8_t valid;            /* 0: no previous block (number/prev-hash unchecked) */
+  uint8_t has_hash;         /* 0: previous hash unknown (not compared)         */
+  uint8_t pad[6];
+} fgv_chain_state;
+typedef struct fgv_block_check {
+  int32_t status;           /* FGV_BLK_*                                       */
+  uint32_t bad_tx;          /* FGV_BLK_TX_MALFORMED: index of the envelope     */
+  uint64_t number;          /* Header.Number                                   */
+  uint8_t data_hash[32];    /* ComputeBlockDataHash(block.Data)                */
+  uint8_t header_hash[32];  /* BlockHeaderHash(block.Header)                   */
+} fgv_block_check;
+int fgv_blocks_verify(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                      fgv_chain_state *chain, fgv_block_check *out);
+/* host SHA-256 of one buffer (the data-hash primitive); returns 1 when the SHA extensions
+ * were used, 0 for the portable path */
+int fgv_sha256_host(const uint8_t *buf, size_t n, uint8_t out[32]);
+
 #ifdef __cplusplus
 }
 #endif
