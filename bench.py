@@ -71,21 +71,47 @@ def cpu_verify_rate(keymat, msgs, sigs, threads, target_s=12.0):
 
 
 # ------------------------------------------------------------------ block workload
+# C2 (configs[1], the headline) and C5 (configs[4]) share the block pipeline; C5 adds the
+# deliver-side integrity pass (header chain + well-formedness + SHA-256 block data hash).
+BLOCK_SPECS = {
+    "block": dict(net=dict(seed=3, orgs=3, clients=100), endorse=((2, 0.6), (3, 0.4)), integrity=False,
+                  desc="C2: {T}-tx endorser blocks, OutOf(2,[Org1..3.member]), 2-3 endorsements, "
+                       "4R/4W x 200B, 100 clients, faults 2%/2%/2%/0.5%"),
+    "c5": dict(net=dict(seed=5, orgs=8, clients=200, policy_n=5, peers_per_org=2, ed25519_frac=0.1,
+                        ed25519_peers=1), endorse=((5, 0.5), (6, 0.5)), integrity=True,
+               desc="C5: {T}-tx blocks, OutOf(5,[Org1..8.member]), 5-6 endorsements from 16 peers, 10% of "
+                    "clients + 1 peer Ed25519 (rejected at DeserializeIdentity, SURVEY F4), faults "
+                    "2%/2%/2%/0.5%, VerifyBlock integrity + SHA-256 block data hash"),
+}
+
+
 def run_block(args, world, rank, local, dev):
+    import threading
+
     from fabric_amd import _lib, shard, txvalidator
     from fabric_amd.synth import blocks
 
+    spec = BLOCK_SPECS[args.workload]
     t0 = time.time()
     pems = None
     if world > 1:
         obj = [None]
         if rank == 0:
-            obj[0] = blocks.Network(seed=3, orgs=3, clients=100).export_pems()
+            obj[0] = blocks.Network(**spec["net"]).export_pems()
         dist.broadcast_object_list(obj, src=0)
         pems = obj[0]
-    net = blocks.Network(seed=3, orgs=3, clients=100, pems=pems)
+    net = blocks.Network(pems=pems, **spec["net"])
     B, T = args.blocks_per_gpu, args.tx_per_block
-    mine = [blocks.make_block(net, T, number=1 + rank * B + i, seed=7919 * rank + i, threads=8) for i in range(B)]
+    if args.workload == "c5":
+        B = args.c5_blocks_per_gpu
+        T = args.c5_tx_per_block
+    mine, prev = [], b"\x00" * 32
+    for i in range(B):  # each rank's blocks form a hash chain (numbers 1 + rank*B + i)
+        num = 1 + rank * B + i
+        blk, lab, envs = blocks.make_block(net, T, number=num, seed=7919 * rank + i, threads=8,
+                                           endorse_dist=spec["endorse"], prev_hash=prev)
+        mine.append((blk, lab))
+        prev = blocks.header_hash(num, prev, envs)
     my_blocks = [m[0] for m in mine]
     my_labels = [m[1] for m in mine]
     if world > 1:
@@ -117,11 +143,27 @@ def run_block(args, world, rank, local, dev):
     flags_out = np.empty(int(ntx.sum()), dtype=np.uint8)
     torch.cuda.synchronize()
 
+    integ = dict(ms=0.0, ok=True)
+
+    def verify_mine():  # deliver-side VerifyBlock of this rank's blocks (own host pool)
+        chain = _lib.ChainState(number=rank * B, valid=1, has_hash=0)
+        t = time.perf_counter()
+        res = eng.blocks_verify(my_blocks, chain)
+        integ["ms"] += (time.perf_counter() - t) * 1e3
+        integ["ok"] &= all(r[0] == _lib.BLK_OK for r in res) and chain.number == rank * B + B
+
     def step():
+        th = None
+        if spec["integrity"]:  # concurrent with the committer pass, as in a pipelined peer
+            th = threading.Thread(target=verify_mine)
+            th.start()
         nt = eng.validate_shard_dev(batch, lo, hi, send.data_ptr(), rows)
         if world > 1:
             shard.allgather_device(send, recv)
-        return eng.finalize_flags_dev(nt, world, rows, recv.data_ptr(), out=flags_out)
+        f = eng.finalize_flags_dev(nt, world, rows, recv.data_ptr(), out=flags_out)
+        if th is not None:
+            th.join()
+        return f
 
     flags = None
     for _ in range(args.warmup):
@@ -129,6 +171,10 @@ def run_block(args, world, rank, local, dev):
     exp = np.array([e if e is not None else 255 for bl in labels for e in blocks.expected_codes(bl)], np.int64)
     known = np.array([e is not None for bl in labels for e in blocks.expected_codes(bl)])
     mism = int(((flags.astype(np.int64) != exp) & known).sum()) if flags is not None else -1
+    if not integ["ok"]:
+        mism = max(mism, 1)
+        log(f"[bench] rank {rank}: block integrity check failed")
+    integ["ms"] = 0.0
     if mism:
         log(f"[bench] rank {rank}: {mism} flags differ from generator labels")
 
@@ -167,15 +213,15 @@ def run_block(args, world, rank, local, dev):
     out = dict(metric=METRIC, value=round(total_tx / el, 1), unit="validated tx/s", n_gpus=world, steps=args.steps,
                warmup=args.warmup, ms_per_step=round(el / args.steps * 1e3, 3), higher_is_better=True, scaling="weak",
                vs_baseline=None, dtype="u32", data="synthetic",
-               config=dict(workload=f"C2: {T}-tx endorser blocks, OutOf(2,[Org1..3.member]), 2-3 endorsements, "
-                                    f"4R/4W x 200B, 100 clients, faults 2%/2%/2%/0.5%",
+               config=dict(workload=spec["desc"].format(T=T),
                            blocks_per_step=len(blks), tx_per_block=T, global_batch=len(blks) * T,
                            parallelism=f"tx-shard{world}+allgather(68B/tx)"),
                verifies_per_s=round(all_verifies / el, 1), parity_vs_labels=ok,
                stage_ms=dict(sha=round(acc["sha"] / args.steps, 4), prep=round(acc["prep"] / args.steps, 4),
                              point=round(acc["point"] / args.steps, 4)),
                sha256_compressions_per_step=int(acc["sha_blocks"] / args.steps),
-               host_ms={k: round(v / args.steps, 3) for k, v in host.items()},
+               host_ms=dict({k: round(v / args.steps, 3) for k, v in host.items()},
+                            **({"integrity_ms": round(integ["ms"] / args.steps, 3)} if spec["integrity"] else {})),
                roofline=roofline(acc["verifies"] / args.steps, acc["point"] / args.steps), cpu_baseline=None)
     if rank == 0 and world == 1 and args.cpu_threads > 0:
         # crypto-bound upper bound of the reference's CPU committer on this host: every
@@ -360,7 +406,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="block", choices=["block", "sig", "mvcc"])
+    ap.add_argument("--workload", default="block", choices=["block", "c5", "sig", "mvcc"])
+    ap.add_argument("--c5-blocks-per-gpu", type=int, default=2)
+    ap.add_argument("--c5-tx-per-block", type=int, default=20000)
     ap.add_argument("--tx-per-mvcc-block", type=int, default=10000)
     ap.add_argument("--state-keys", type=int, default=1_000_000)
     ap.add_argument("--blocks-per-gpu", type=int, default=32)
@@ -383,7 +431,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    out = dict(block=run_block, sig=run_sig, mvcc=run_mvcc)[args.workload](args, world, rank, local, dev)
+    out = dict(block=run_block, c5=run_block, sig=run_sig, mvcc=run_mvcc)[args.workload](args, world, rank, local, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -389,6 +389,23 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
     return block, labels, envs
 
 
+def header_hash(number: int, prev_hash: bytes, envs) -> bytes:
+    """BlockHeaderHash of a generated block (protoutil/blockutils.go:48-67: SHA-256 of the DER
+    SEQUENCE{INTEGER number, OCTET STRING previous_hash, OCTET STRING data_hash}), used to
+    chain generated blocks through Header.PreviousHash."""
+    def dlen(n):
+        if n < 128:
+            return bytes([n])
+        b = n.to_bytes((n.bit_length() + 7) // 8, "big")
+        return bytes([0x80 | len(b)]) + b
+    nb = number.to_bytes(max(1, (number.bit_length() + 7) // 8), "big")
+    if nb[0] & 0x80:
+        nb = b"\x00" + nb
+    dh = hashlib.sha256(b"".join(envs)).digest()
+    body = b"\x02" + dlen(len(nb)) + nb + b"\x04" + dlen(len(prev_hash)) + prev_hash + b"\x04" + dlen(32) + dh
+    return hashlib.sha256(b"\x30" + dlen(len(body)) + body).digest()
+
+
 def expected_codes(labels):
     """Generator-side expectation (None where the fault's effect is left to the oracle).
     dup_txid: the later VALID duplicate gets 9 (validator.go:279-295)."""

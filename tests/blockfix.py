@@ -45,3 +45,16 @@ def block_from_envs(envs, number=1):
     header = f.f_varint(1, number) + f.f_bytes(2, b"\x00" * 32) + f.f_bytes(3, hashlib.sha256(b"".join(envs)).digest())
     data = b"".join(f.f_msg(1, e) for e in envs)
     return f.f_msg(1, header) + f.f_msg(2, data) + f.f_msg(3, b"".join(f.f_msg(1, b"") for _ in range(5)))
+
+
+C5_NET = dict(seed=5, orgs=8, clients=60, policy_n=5, peers_per_org=2, ed25519_frac=0.1, ed25519_peers=1)
+C5_ENDORSE = ((5, 0.5), (6, 0.5))
+
+
+def network_c5():
+    """C5-shaped network: 8 orgs x 2 peers, OutOf(5, 8 orgs), Ed25519 clients and one Ed25519
+    peer (the reference rejects Ed25519 identities at DeserializeIdentity)."""
+    k = tuple(sorted(C5_NET.items()))
+    if k not in _NET:
+        _NET[k] = blocks.Network(**C5_NET)
+    return _NET[k]

@@ -6,7 +6,7 @@ import pytest
 from fabric_amd import _lib, txvalidator
 from fabric_amd.synth import blocks
 from oracle import v20
-from tests.blockfix import SPECIAL, block_from_envs, corrupt_envelopes, network
+from tests.blockfix import C5_ENDORSE, SPECIAL, block_from_envs, corrupt_envelopes, network, network_c5
 
 pytestmark = pytest.mark.gpu
 
@@ -230,4 +230,31 @@ def test_device_finalize_matches_host_finalize(seed, pool, world):
     d = torch.from_numpy(g).to("cuda")
     dev = eng.finalize_flags_dev(ntx, world, rows, d.data_ptr())
     assert np.array_equal(dev, host)
+    eng.close()
+
+
+def test_c5_mixed_ed25519_blocks_match_oracle():
+    """C5 shape at oracle-sized blocks: 8 orgs, 5-of-8, 5-6 endorsements, Ed25519 identities."""
+    net = network_c5()
+    eng = _engine_for(net)
+    blks = [blocks.make_block(net, 300, number=1 + i, seed=100 + i, endorse_dist=C5_ENDORSE)[0] for i in range(2)]
+    _check(eng, net, blks)
+    eng.close()
+
+
+def test_c5_full_size_block_and_integrity():
+    """A 20k-tx C5 block at full size: flags equal the generator's labels (size-independent
+    property), and the deliver-side integrity pass (data hash over ~110 MB) verifies it."""
+    net = network_c5()
+    eng = _engine_for(net)
+    blk, labels, envs = blocks.make_block(net, 20000, number=1, seed=7, endorse_dist=C5_ENDORSE)
+    got = eng.validate_blocks([blk])[0]
+    exp = blocks.expected_codes(labels)
+    known = [i for i, e in enumerate(exp) if e is not None]
+    assert len(got) == 20000 and all(int(got[i]) == exp[i] for i in known)
+    chk = eng.blocks_verify([blk, blk])
+    assert chk[0][0] == _lib.BLK_OK and chk[0][3] == blocks.hashlib.sha256(b"".join(envs)).digest()
+    chain = _lib.ChainState(number=0, valid=1, has_hash=0)
+    chk = eng.blocks_verify([blk, blk], chain)
+    assert [c[0] for c in chk] == [_lib.BLK_OK, _lib.BLK_NUMBER] and chain.number == 1
     eng.close()

@@ -5,7 +5,7 @@ import pytest
 from fabric_amd.synth import blocks
 from oracle import v20
 from oracle.protowire import DecodeError, decode
-from tests.blockfix import SPECIAL, network
+from tests.blockfix import C5_ENDORSE, SPECIAL, network, network_c5
 
 
 def _model(net):
@@ -82,3 +82,15 @@ def test_wire_rules():
     sp = decode("SignaturePolicy", b"\x12\x00\x08\x00")          # oneof: last member (signed_by 0)
     assert sp == {"signed_by": 0}
     assert decode("ChannelHeader", b"\x08\xff\xff\xff\xff\x0f")["type"] == -1
+
+
+def test_c5_ed25519_block_matches_generator_labels():
+    """C5: Ed25519 creators -> BAD_CREATOR_SIGNATURE, Ed25519 endorsers skipped -> policy
+    failure when fewer than 5 distinct P-256 orgs remain."""
+    net = network_c5()
+    assert any(p.kind == "ed25519" for p in net.peers) and any(c.kind == "ed25519" for c in net.clients)
+    blk, labels, _ = blocks.make_block(net, 160, number=1, seed=3, endorse_dist=C5_ENDORSE)
+    flags = v20.validate_block(_model(net), blk)
+    exp = blocks.expected_codes(labels)
+    assert [f for f, e in zip(flags, exp) if e is not None] == [e for e in exp if e is not None]
+    assert {"ed25519_creator", "endorse_short", "clean"} <= set(labels)
