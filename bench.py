@@ -124,6 +124,8 @@ def run_block(args, world, rank, local, dev):
     log(f"[bench] rank {rank}: {len(blks)} blocks x {T} tx ready in {time.time() - t0:.1f}s")
 
     eng = _lib.Engine(local)
+    if args.host_parse:
+        eng.set_parse_mode(1)
     txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes)
     # the batch resident in HBM (64 B tail padding per block)
     sizes = [(len(b) + 64 + 255) // 256 * 256 for b in blks]
@@ -215,7 +217,8 @@ def run_block(args, world, rank, local, dev):
                vs_baseline=None, dtype="u32", data="synthetic",
                config=dict(workload=spec["desc"].format(T=T),
                            blocks_per_step=len(blks), tx_per_block=T, global_batch=len(blks) * T,
-                           parallelism=f"tx-shard{world}+allgather(68B/tx)"),
+                           parallelism=f"tx-shard{world}+allgather(68B/tx)",
+                           parse="host" if args.host_parse else "device"),
                verifies_per_s=round(all_verifies / el, 1), parity_vs_labels=ok,
                stage_ms=dict(sha=round(acc["sha"] / args.steps, 4), prep=round(acc["prep"] / args.steps, 4),
                              point=round(acc["point"] / args.steps, 4)),
@@ -415,6 +418,7 @@ def main():
     ap.add_argument("--tx-per-block", type=int, default=500)
     ap.add_argument("--per-gpu", type=int, default=131072)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--host-parse", action="store_true", help="parse transactions on host threads (A/B)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

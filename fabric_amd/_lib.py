@@ -23,7 +23,7 @@ EXPORTED = [
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
-    "fgv_blocks_verify", "fgv_sha256_host",
+    "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -109,6 +109,7 @@ def load():
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.POINTER(ctypes.c_uint32)]
         L.fgv_blocks_verify.argtypes = [vp, sz, vp, vp, vp, vp]
+        L.fgv_set_parse_mode.argtypes = [vp, ctypes.c_int]
         L.fgv_sha256_host.argtypes = [vp, sz, vp]
         _L = L
     return _L
@@ -230,6 +231,10 @@ class Engine:
                                                 key_slot, n, status))
 
     # --- committer: channel model + whole blocks
+    def set_parse_mode(self, mode: int):
+        """0: transactions parsed on the GPU (default); 1: host parser (same results)."""
+        _check(self._L.fgv_set_parse_mode(self._h, mode))
+
     def channel_init(self, name: str):
         _check(self._L.fgv_channel_init(self._h, name.encode()))
 

@@ -1,0 +1,125 @@
+// blockdev.h -- device-resident committer pipeline (blockdev.hip): layouts shared by the
+// kernels and the host driver in fgv_block.cpp.  Not part of the C ABI.
+//
+// The block batch lives in HBM; the host only splits blocks into envelope spans (a tag/length
+// walk) and launches.  Per transaction, on the device:
+//   k_bd_parse  single-pass protobuf parse of the envelope (the rules of pbwire.h, restated for
+//               device code with fixed capacities) -> DevTx: spans + structural codes
+//   k_bd_ident  MSP identity resolution of the creator and every endorser: decode the
+//               SerializedIdentity, hash, probe the HBM identity table, exact byte compare
+//   k_bd_count  creator checks + device job counts; k_bd_scan exclusive scan; k_bd_emit writes
+//               the SHA-256 jobs and the ECDSA verify jobs straight into the job arrays
+//   (k_sha256_jobs, k_der, k_inv, k_prep, k_point as for host-assembled batches)
+//   k_bd_fold   code precedence, SignatureSetToValidIdentities, cauthdsl NOutOf fold, txid
+//               index entries -> fgv_tx_result records in HBM (input of the device finalize)
+// A transaction whose shape exceeds a fixed capacity below sets the overflow flag and the
+// batch is redone by the host parser (same rules, unbounded containers).
+#pragma once
+#include <stdint.h>
+
+#define BD_MAX_END 16      // endorsements per transaction
+#define BD_MAX_NS 8        // namespaces per rwset
+#define BD_MAX_POL 8       // policies to evaluate (written namespaces + invoked chaincode)
+#define BD_MAX_MERGE 4     // occurrences of one singular message field (protobuf merge)
+#define BD_MAX_GROUP 32    // nesting of unknown START_GROUP fields
+#define BD_MAX_PNODE 64    // policy tree nodes evaluated per policy (stack depth 16)
+#define BD_OCC (1 + BD_MAX_END)  // identity occurrences per tx: creator + endorsers
+
+struct DSpan {  // bytes [off, off+len) of block `DevTx::blk`; len 0 == nil
+  uint32_t off, len;
+};
+
+enum : uint8_t { BDF_INDEX_OK = 1, BDF_INDEX_FROM_TXID = 2, BDF_IDX_SHDR = 4 };
+
+struct DevTx {
+  uint32_t blk;
+  uint8_t pre, etx, disp, flags;
+  int32_t type;
+  DSpan payload, env_sig, nonce, creator, chdr, act_hdr, ccpp, prop_hash, prp, txid;
+  DSpan idx_nonce, idx_creator, index_txid;
+  uint8_t npol, nend, pad[2];
+  int16_t pol[BD_MAX_POL];
+  DSpan end_ser[BD_MAX_END], end_sig[BD_MAX_END];
+};
+
+// per-tx job bookkeeping written by k_bd_count / k_bd_emit
+enum { BJ_C = 0, BJ_T, BJ_P, BJ_E, BJ_I, BJ_KINDS };
+struct DevJobIdx {
+  uint32_t cnt[BJ_KINDS];  // jobs of each kind (creator-payload, txid, proposal, endorsement, index)
+  uint32_t base[BJ_KINDS]; // first job of each kind (exclusive scan)
+};
+
+// identity registry in HBM (built on the host from the channel model)
+struct DevIdent {
+  uint32_t msp_off, msp_len, idb_off, idb_len;  // into the identity byte arena
+  int32_t key_slot;   // -1: not a P-256 key
+  int32_t msp;        // interned Mspid
+  uint32_t canon;     // dedup id (Mspid + Id)
+  uint32_t valid;
+};
+
+struct DevPNode {
+  int32_t type;       // 1 NOutOf, 2 SignedBy
+  int32_t n;          // NOutOf threshold
+  int32_t msp;        // SignedBy: interned principal Mspid (-1: undecodable principal)
+  uint32_t kid0, nkids;  // NOutOf: kids[kid0 .. kid0+nkids) in the kid array
+};
+struct DevPolicy {
+  uint32_t decode_ok, compile_ok, unsupported;
+  int32_t root;       // node index
+};
+
+struct DevChannel {  // device pointers + sizes (passed by value to the kernels)
+  const uint8_t *name;
+  uint32_t name_len;
+  uint32_t nident;
+  const DevIdent *idents;
+  const uint8_t *ident_bytes;
+  const uint32_t *ident_table;  // open addressing: ident index + 1 (0 empty)
+  const uint64_t *ident_hash;   // hash of each ident (same order as idents)
+  uint32_t ident_mask;
+  uint32_t ncc;
+  const uint32_t *cc;           // ncc x (ns_off, ns_len, policy)
+  const uint8_t *cc_bytes;
+  const DevPolicy *policies;
+  const DevPNode *nodes;
+  const uint32_t *kids;
+  const uint8_t *committed;     // committed ledger txids: open-addressing table of 32-byte keys
+  uint32_t committed_mask;      // (all-zero key == empty; a zero txid is kept in committed_zero)
+  uint32_t committed_zero;
+};
+
+// identity-index hash (host builds the table with it, device probes with it): Mspid bytes,
+// id_bytes length, and the first 64 / last 192 bytes of id_bytes (a PEM certificate: serial
+// number near the front, signature at the end).  Not cryptographic: every hit is confirmed
+// by an exact compare of both fields.
+#if defined(__HIPCC__)
+#define BD_HD __host__ __device__
+#else
+#define BD_HD
+#endif
+BD_HD inline uint64_t bd_mix(uint64_t h, uint64_t v) {
+  h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+  h *= 0xC2B2AE3D27D4EB4Full;
+  return h ^ (h >> 29);
+}
+BD_HD inline uint64_t bd_ident_hash(const uint8_t *msp, uint32_t ml, const uint8_t *idb, uint32_t il) {
+  uint64_t h = bd_mix(0x243F6A8885A308D3ull, ((uint64_t)ml << 32) | il);
+  uint64_t w = 0;
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < ml; i++) {
+    w |= (uint64_t)msp[i] << (8 * (k++));
+    if (k == 8) { h = bd_mix(h, w); w = 0; k = 0; }
+  }
+  h = bd_mix(h, w ^ 0xA5);
+  w = 0;
+  k = 0;
+  const uint32_t head = il < 64 ? il : 64;
+  const uint32_t tail0 = il > 192 ? il - 192 : 0;
+  for (uint32_t i = 0; i < il; i++) {
+    if (i == head && i < tail0) i = tail0;  // skip the middle
+    w |= (uint64_t)idb[i] << (8 * (k++));
+    if (k == 8) { h = bd_mix(h, w); w = 0; k = 0; }
+  }
+  return bd_mix(h, w ^ 0x5A);
+}

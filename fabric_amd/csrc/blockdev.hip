@@ -1,0 +1,999 @@
+// blockdev.hip -- the committer's per-transaction work on the GPU (see blockdev.h).
+//
+// Restates, for device code, the host parser of fgv_block.cpp (parse_tx / count_jobs / the
+// assembly loop / the fold) rule for rule; the protobuf rules are those of pbwire.h
+// (google.golang.org/protobuf v1.33.0 as vendored by the reference).  Reference behaviour:
+//   core/committer/txvalidator/v20/validator.go:297-453 (validateTx precedence),
+//   core/common/validation/msgvalidation.go:26-320, plugindispatcher/dispatcher.go:102-302,
+//   builtin/v20/validation_logic.go:109-217, statebased/validator_keylevel.go:246-260,
+//   common/policies/policy.go:363-395, common/cauthdsl/cauthdsl.go:24-92,
+//   protoutil/txutils.go:503-534 (GetOrComputeTxIDFromEnvelope for the txid index).
+//
+// One thread per transaction (k_bd_parse, k_bd_count, k_bd_emit, k_bd_fold) or per identity
+// occurrence (k_bd_ident).  These are byte-walking kernels: latency-bound on dependent loads,
+// with every transaction of the batch in flight at once.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fgv.h"
+#include "blockdev.h"
+#include "fgv_kernels.h"
+
+namespace {
+
+enum : uint8_t { C_VALID = 0, C_BAD_PAYLOAD = 2, C_BAD_HDR = 3, C_BAD_CREATOR = 4, C_BAD_ETX = 5,
+                 C_UNSUP_PAYLOAD = 7, C_BAD_TXID = 8, C_DUP_TXID = 9, C_POLICY = 10,
+                 C_BAD_HDR_EXT = 19, C_BAD_RESP = 21, C_BAD_RWSET = 22, C_ILLEGAL_WS = 23,
+                 C_INVALID_CC = 25, C_OTHER = 255, C_PENDING = 0xFE, C_UNSUPPORTED = 0xFD };
+
+#define DEV __device__ __forceinline__
+
+// ------------------------------------------------------------------ protobuf wire (device)
+struct S {  // absolute device span
+  const uint8_t *p;
+  uint32_t n;
+};
+DEV bool s_eq(S a, S b) {
+  if (a.n != b.n) return false;
+  for (uint32_t i = 0; i < a.n; i++)
+    if (a.p[i] != b.p[i]) return false;
+  return true;
+}
+DEV bool s_lt(S a, S b) {  // byte-lexicographic (Go string order)
+  const uint32_t m = a.n < b.n ? a.n : b.n;
+  for (uint32_t i = 0; i < m; i++)
+    if (a.p[i] != b.p[i]) return a.p[i] < b.p[i];
+  return a.n < b.n;
+}
+
+enum Kind : uint8_t { K_NONE = 0, K_VARINT, K_BYTES, K_STRING, K_MSG, K_REP_MSG, K_REP_BYTES };
+
+DEV bool rd_varint(const uint8_t *&p, const uint8_t *e, uint64_t &v) {
+  v = 0;
+  for (int i = 0; i < 10; i++) {
+    if (p >= e) return false;
+    const uint8_t c = *p++;
+    if (i == 9 && c > 1) return false;
+    v |= (uint64_t)(c & 0x7f) << (7 * i);
+    if (c < 0x80) return true;
+  }
+  return false;
+}
+
+// skip one field value (wire type wt of field num); START_GROUP nesting tracked on a small
+// explicit stack (pbwire.h recurses; deeper than BD_MAX_GROUP -> overflow)
+DEV bool skip_value(const uint8_t *&p, const uint8_t *e, uint32_t num, int wt, bool &ovf) {
+  uint64_t v;
+  switch (wt) {
+    case 0: return rd_varint(p, e, v);
+    case 1: if (e - p < 8) return false; p += 8; return true;
+    case 5: if (e - p < 4) return false; p += 4; return true;
+    case 2:
+      if (!rd_varint(p, e, v) || v > (uint64_t)(e - p)) return false;
+      p += v;
+      return true;
+    case 3: {
+      uint32_t stack[BD_MAX_GROUP];
+      int sp = 0;
+      stack[sp++] = num;
+      while (sp > 0) {
+        uint64_t tag;
+        if (!rd_varint(p, e, tag)) return false;
+        const uint64_t n2 = tag >> 3;
+        const int w2 = (int)(tag & 7);
+        if (n2 < 1 || n2 > (1u << 29) - 1) return false;
+        if (w2 == 4) {
+          if (n2 != stack[sp - 1]) return false;
+          sp--;
+          continue;
+        }
+        if (w2 == 3) {
+          if (sp == BD_MAX_GROUP) { ovf = true; return false; }
+          stack[sp++] = (uint32_t)n2;
+          continue;
+        }
+        if (w2 == 0) { if (!rd_varint(p, e, v)) return false; }
+        else if (w2 == 1) { if (e - p < 8) return false; p += 8; }
+        else if (w2 == 5) { if (e - p < 4) return false; p += 4; }
+        else if (w2 == 2) { if (!rd_varint(p, e, v) || v > (uint64_t)(e - p)) return false; p += v; }
+        else return false;
+      }
+      return true;
+    }
+    default: return false;
+  }
+}
+
+DEV bool utf8_valid(const uint8_t *s, uint32_t n) {  // Go utf8.Valid
+  uint32_t i = 0;
+  while (i < n) {
+    const uint8_t c = s[i];
+    if (c < 0x80) { i++; continue; }
+    uint32_t len, cp;
+    if ((c & 0xE0) == 0xC0) { len = 2; cp = c & 0x1F; }
+    else if ((c & 0xF0) == 0xE0) { len = 3; cp = c & 0x0F; }
+    else if ((c & 0xF8) == 0xF0) { len = 4; cp = c & 0x07; }
+    else return false;
+    if (i + len > n) return false;
+    for (uint32_t k = 1; k < len; k++) {
+      const uint8_t d = s[i + k];
+      if ((d & 0xC0) != 0x80) return false;
+      cp = (cp << 6) | (d & 0x3F);
+    }
+    if ((len == 2 && cp < 0x80) || (len == 3 && cp < 0x800) || (len == 4 && cp < 0x10000)) return false;
+    if (cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return false;
+    i += len;
+  }
+  return true;
+}
+
+// decode (pbwire.h decode): visitor kind / on_varint / on_len; ovf = a device capacity was hit
+template <class V>
+DEV bool decode(const uint8_t *p, uint32_t n, V &vis, bool &ovf) {
+  const uint8_t *e = p + n;
+  while (p < e) {
+    uint64_t tag;
+    if (!rd_varint(p, e, tag)) return false;
+    const uint64_t num = tag >> 3;
+    const int wt = (int)(tag & 7);
+    if (num < 1 || num > (1u << 29) - 1) return false;
+    if (wt == 4) return false;
+    const Kind k = vis.kind((uint32_t)num);
+    const int want = (k == K_VARINT) ? 0 : 2;
+    if (k == K_NONE || wt != want) {
+      if (!skip_value(p, e, (uint32_t)num, wt, ovf)) return false;
+      continue;
+    }
+    if (k == K_VARINT) {
+      uint64_t v;
+      if (!rd_varint(p, e, v)) return false;
+      vis.on_varint((uint32_t)num, v);
+      continue;
+    }
+    uint64_t l;
+    if (!rd_varint(p, e, l) || l > (uint64_t)(e - p)) return false;
+    S s{p, (uint32_t)l};
+    p += l;
+    if (k == K_STRING && !utf8_valid(s.p, s.n)) return false;
+    if (!vis.on_len((uint32_t)num, s, ovf)) return false;
+  }
+  return true;
+}
+template <class V>
+DEV bool decode(S s, V &vis, bool &ovf) { return decode(s.p, s.n, vis, ovf); }
+
+DEV int32_t as_int32(uint64_t v) { return (int32_t)(uint32_t)v; }
+
+// ------------------------------------------------------------------ visitors (device)
+// Same field maps as fgv_visitors.h.  A singular embedded message field decodes every
+// occurrence in order into one value (protobuf merge): visitors decode at on_len time.
+struct VTwoBytes {  // Envelope / Header / SignatureHeader / TransactionAction / Endorsement / Prp
+  S a{nullptr, 0}, b{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &) { (n == 1 ? a : b) = s; return true; }
+};
+struct VTimestamp {
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_VARINT : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VPayload {
+  bool has_header = false;
+  VTwoBytes hdr;  // channel_header, signature_header (all occurrences merged)
+  S data{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_MSG : n == 2 ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 2) { data = s; return true; }
+    has_header = true;
+    return decode(s, hdr, ovf);
+  }
+};
+struct VChannelHeader {
+  int32_t type = 0;
+  uint64_t epoch = 0;
+  S channel_id{nullptr, 0}, tx_id{nullptr, 0}, extension{nullptr, 0};
+  DEV Kind kind(uint32_t n) {
+    switch (n) {
+      case 1: case 2: case 6: return K_VARINT;
+      case 3: return K_MSG;
+      case 4: case 5: return K_STRING;
+      case 7: case 8: return K_BYTES;
+      default: return K_NONE;
+    }
+  }
+  DEV void on_varint(uint32_t n, uint64_t v) {
+    if (n == 1) type = as_int32(v);
+    else if (n == 6) epoch = v;
+  }
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 3) { VTimestamp t; return decode(s, t, ovf); }
+    if (n == 4) channel_id = s;
+    else if (n == 5) tx_id = s;
+    else if (n == 7) extension = s;
+    return true;
+  }
+};
+struct VTransaction {  // repeated TransactionAction: count + the first
+  uint32_t nact = 0;
+  VTwoBytes first;
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) {
+    VTwoBytes a;
+    if (!decode(s, a, ovf)) return false;
+    if (nact == 0) first = a;
+    nact++;
+    return true;
+  }
+};
+struct VEndorsedAction {
+  S prp{nullptr, 0};
+  uint32_t nend = 0;
+  S ser[BD_MAX_END], sig[BD_MAX_END];
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { prp = s; return true; }
+    VTwoBytes e;
+    if (!decode(s, e, ovf)) return false;
+    if (nend == BD_MAX_END) { ovf = true; return false; }
+    ser[nend] = e.a;
+    sig[nend] = e.b;
+    nend++;
+    return true;
+  }
+};
+struct VCcActionPayload {
+  S ccpp{nullptr, 0};
+  bool has_action = false;
+  VEndorsedAction action;
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { ccpp = s; return true; }
+    has_action = true;
+    return decode(s, action, ovf);
+  }
+};
+struct VChaincodeID {
+  S path{nullptr, 0}, name{nullptr, 0}, version{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? K_STRING : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &) { (n == 1 ? path : n == 2 ? name : version) = s; return true; }
+};
+struct VResponse {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_VARINT : n == 2 ? K_STRING : n == 3 ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VCcAction {
+  S results{nullptr, 0}, events{nullptr, 0};
+  bool has_ccid = false;
+  VChaincodeID ccid;
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_BYTES : (n == 3 || n == 4) ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { results = s; return true; }
+    if (n == 2) { events = s; return true; }
+    if (n == 3) { VResponse r; return decode(s, r, ovf); }
+    has_ccid = true;
+    return decode(s, ccid, ovf);
+  }
+};
+struct VHdrExt {
+  bool has_ccid = false;
+  VChaincodeID ccid;
+  DEV Kind kind(uint32_t n) { return n == 2 ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) { has_ccid = true; return decode(s, ccid, ovf); }
+};
+struct VCcEvent {
+  S chaincode_id{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? K_STRING : n == 4 ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &) { if (n == 1) chaincode_id = s; return true; }
+};
+// rwset: validated in full; the committer needs namespaces and write presence
+struct VVersion {
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_VARINT : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VKVRead {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) return true;
+    VVersion v;
+    return decode(s, v, ovf);
+  }
+};
+struct VQueryReads {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) { VKVRead r; return decode(s, r, ovf); }
+};
+struct VMerkle {
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_VARINT : n == 3 ? K_REP_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VRangeQuery {
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_STRING : n == 3 ? K_VARINT : (n == 4 || n == 5) ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 4) { VQueryReads q; return decode(s, q, ovf); }
+    if (n == 5) { VMerkle m; return decode(s, m, ovf); }
+    return true;
+  }
+};
+struct VKVWrite {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_VARINT : n == 3 ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VMetaEntry {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VMetaWrite {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) return true;
+    VMetaEntry e;
+    return decode(s, e, ovf);
+  }
+};
+struct VKVRWSet {
+  uint32_t nwrites = 0, nmeta = 0;
+  DEV Kind kind(uint32_t n) { return (n >= 1 && n <= 4) ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { VKVRead r; return decode(s, r, ovf); }
+    if (n == 2) { VRangeQuery q; return decode(s, q, ovf); }
+    if (n == 3) { nwrites++; VKVWrite w; return decode(s, w, ovf); }
+    nmeta++;
+    VMetaWrite m;
+    return decode(s, m, ovf);
+  }
+};
+struct VHashRead {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) return true;
+    VVersion v;
+    return decode(s, v, ovf);
+  }
+};
+struct VHashWrite {
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 3) ? K_BYTES : (n == 2 || n == 4) ? K_VARINT : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VHashMeta {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) return true;
+    VMetaEntry e;
+    return decode(s, e, ovf);
+  }
+};
+struct VHashedRWSet {
+  uint32_t nwrites = 0, nmeta = 0;
+  DEV Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { VHashRead r; return decode(s, r, ovf); }
+    if (n == 2) { nwrites++; VHashWrite w; return decode(s, w, ovf); }
+    nmeta++;
+    VHashMeta m;
+    return decode(s, m, ovf);
+  }
+};
+struct VCollHashed {
+  S name{nullptr, 0}, hashed{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : (n == 2 || n == 3) ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &) {
+    if (n == 1) name = s;
+    else if (n == 2) hashed = s;
+    return true;
+  }
+};
+// NsReadWriteSet: namespace, rwset bytes, collection hashed rwsets (kept for the second pass)
+#define BD_MAX_COLL 8
+struct VNsRwSet {
+  S ns{nullptr, 0}, rwset{nullptr, 0};
+  uint32_t ncoll = 0;
+  S coll_hashed[BD_MAX_COLL];
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : n == 3 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { ns = s; return true; }
+    if (n == 2) { rwset = s; return true; }
+    VCollHashed c;
+    if (!decode(s, c, ovf)) return false;
+    if (ncoll == BD_MAX_COLL) { ovf = true; return false; }
+    coll_hashed[ncoll++] = c.hashed;
+    return true;
+  }
+};
+struct VTxRwSet {
+  uint32_t nns = 0;
+  S ns[BD_MAX_NS], rwset[BD_MAX_NS];
+  uint8_t coll_writes[BD_MAX_NS];  // bit0: a collection has writes/metadata; bit1: a collection failed to decode
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_VARINT : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) {
+    VNsRwSet r;
+    if (!decode(s, r, ovf)) return false;
+    if (nns == BD_MAX_NS) { ovf = true; return false; }
+    ns[nns] = r.ns;
+    rwset[nns] = r.rwset;
+    uint8_t cw = 0;
+    for (uint32_t k = 0; k < r.ncoll; k++) {
+      VHashedRWSet h;
+      if (!decode(r.coll_hashed[k], h, ovf)) { cw |= 2; break; }
+      if (h.nwrites || h.nmeta) cw |= 1;
+    }
+    coll_writes[nns] = cw;
+    nns++;
+    return true;
+  }
+};
+struct VSerializedIdentity {
+  S mspid{nullptr, 0}, id_bytes{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &) { (n == 1 ? mspid : id_bytes) = s; return true; }
+};
+
+DEV DSpan rel(const uint8_t *base, S s) { return DSpan{s.n ? (uint32_t)(s.p - base) : 0u, s.n}; }
+DEV S absl(const uint8_t *base, DSpan d) { return S{base + d.off, d.len}; }
+
+// chaincode definition lookup (lifecycle ValidationInfo): policy index or -1
+DEV int cc_lookup(const DevChannel &ch, S ns) {
+  for (uint32_t i = 0; i < ch.ncc; i++) {
+    const uint32_t *e = ch.cc + 3 * i;
+    if (e[1] == ns.n && s_eq(S{ch.cc_bytes + e[0], e[1]}, ns)) return (int)e[2];
+  }
+  return -1;
+}
+
+}  // namespace
+
+// ============================================================ k_bd_parse
+// fgv_block.cpp parse_tx, speculatively past the creator lookup (resolved by k_bd_ident;
+// k_bd_count applies the creator decision before anything downstream reads the rest).
+__global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
+                                                 const uint64_t *__restrict__ bases, DevChannel ch,
+                                                 DevTx *__restrict__ out, uint32_t *__restrict__ flags) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  const uint32_t blk = envtab[3 * t];
+  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
+  const S d{base + envtab[3 * t + 1], envtab[3 * t + 2]};
+  DevTx R;
+  R.blk = blk;
+  R.pre = C_PENDING;
+  R.etx = C_PENDING;
+  R.disp = C_PENDING;
+  R.flags = 0;
+  R.type = 0;
+  const DSpan z{0, 0};
+  R.payload = R.env_sig = R.nonce = R.creator = R.chdr = R.act_hdr = R.ccpp = R.prop_hash = R.prp = R.txid = z;
+  R.idx_nonce = R.idx_creator = R.index_txid = z;
+  R.npol = 0;
+  R.nend = 0;
+  bool ovf = false;
+  do {
+    VTwoBytes env;
+    if (!decode(d, env, ovf)) { R.pre = C_OTHER; break; }
+    VPayload pl;
+    if (!decode(env.a, pl, ovf)) { R.pre = C_BAD_PAYLOAD; break; }
+    const VTwoBytes &hdr = pl.hdr;
+    // txid index value (GetOrComputeTxIDFromEnvelope)
+    if (pl.has_header) {
+      VChannelHeader c0;
+      if (decode(hdr.a, c0, ovf)) {
+        if (c0.tx_id.n) {
+          R.index_txid = rel(base, c0.tx_id);
+          R.flags |= BDF_INDEX_OK | BDF_INDEX_FROM_TXID;
+        } else {
+          VTwoBytes s0;
+          if (decode(hdr.b, s0, ovf)) {
+            R.flags |= BDF_INDEX_OK;
+            R.idx_nonce = rel(base, s0.b);
+            R.idx_creator = rel(base, s0.a);
+          }
+        }
+      }
+    }
+    if (!pl.has_header) { R.pre = C_BAD_HDR; break; }
+    VChannelHeader chdr;
+    VTwoBytes shdr;  // creator, nonce
+    if (!decode(hdr.a, chdr, ovf) || !decode(hdr.b, shdr, ovf)) { R.pre = C_BAD_HDR; break; }
+    if (chdr.type != 3 && chdr.type != 2 && chdr.type != 1) { R.pre = C_BAD_HDR; break; }
+    if (chdr.epoch != 0 || shdr.b.n == 0 || shdr.a.n == 0) { R.pre = C_BAD_HDR; break; }
+    R.type = chdr.type;
+    R.payload = rel(base, env.a);
+    R.env_sig = rel(base, env.b);
+    R.nonce = rel(base, shdr.b);
+    R.creator = rel(base, shdr.a);
+    R.chdr = rel(base, hdr.a);
+    R.txid = rel(base, chdr.tx_id);
+    if (env.b.n == 0) { R.pre = C_BAD_CREATOR; break; }
+    if (chdr.channel_id.n == 0) { R.pre = C_UNSUPPORTED; break; }
+    if (!s_eq(chdr.channel_id, S{ch.name, ch.name_len})) { R.pre = C_BAD_CREATOR; break; }
+    // creator identity: k_bd_ident / k_bd_count
+    if (chdr.type != 3) break;
+
+    // validateEndorserTransaction
+    R.etx = C_BAD_ETX;
+    if (pl.data.n == 0) break;
+    VTransaction tx;
+    if (!decode(pl.data, tx, ovf) || tx.nact != 1) break;
+    VTwoBytes ash;
+    if (!decode(tx.first.a, ash, ovf) || ash.b.n == 0 || ash.a.n == 0) break;
+    VCcActionPayload cap;
+    if (!decode(tx.first.b, cap, ovf)) break;
+    if (!cap.has_action) { R.etx = C_UNSUPPORTED; break; }
+    VTwoBytes prp;  // proposal_hash, extension
+    if (!decode(cap.action.prp, prp, ovf)) break;
+    if (cap.ccpp.n == 0 || tx.first.a.n == 0) break;
+    R.etx = C_VALID;
+    R.act_hdr = rel(base, tx.first.a);
+    R.ccpp = rel(base, cap.ccpp);
+    R.prop_hash = rel(base, prp.a);
+    R.prp = rel(base, cap.action.prp);
+
+    // Dispatch
+    VHdrExt ext;
+    if (!decode(chdr.extension, ext, ovf)) { R.disp = C_BAD_HDR_EXT; break; }
+    if (cap.action.prp.n == 0) { R.disp = C_BAD_RESP; break; }
+    if (prp.b.n == 0) { R.disp = C_BAD_RESP; break; }
+    VCcAction cca;
+    if (!decode(prp.b, cca, ovf)) { R.disp = C_BAD_RESP; break; }
+    VTxRwSet rw;
+    if (!decode(cca.results, rw, ovf)) { R.disp = C_BAD_RWSET; break; }
+    uint8_t wflags[BD_MAX_NS];
+    bool bad_rw = false;
+    for (uint32_t k = 0; k < rw.nns && !bad_rw; k++) {
+      VKVRWSet kv;
+      if (!decode(rw.rwset[k], kv, ovf) || (rw.coll_writes[k] & 2)) { bad_rw = true; break; }
+      const bool cw = rw.coll_writes[k] & 1;
+      wflags[k] = (uint8_t)(((kv.nwrites || kv.nmeta || cw) ? 1 : 0) | ((kv.nmeta || cw) ? 2 : 0));
+    }
+    if (bad_rw) { R.disp = C_BAD_RWSET; break; }
+    if (!ext.has_ccid || !cca.has_ccid) { R.disp = C_OTHER; break; }
+    const S ccid = ext.ccid.name;
+    if (ccid.n == 0 || !s_eq(ccid, cca.ccid.name) || cca.ccid.version.n == 0) { R.disp = C_INVALID_CC; break; }
+    if (cca.events.n != 0) {
+      VCcEvent ev;
+      if (!decode(cca.events, ev, ovf) || !s_eq(ev.chaincode_id, ccid)) { R.disp = C_OTHER; break; }
+    }
+    bool dup = false;
+    for (uint32_t a = 0; a < rw.nns && !dup; a++)
+      for (uint32_t b = a + 1; b < rw.nns; b++)
+        if (s_eq(rw.ns[a], rw.ns[b])) { dup = true; break; }
+    if (dup) { R.disp = C_ILLEGAL_WS; break; }
+    // written namespaces + the invoked chaincode, sorted (Go string order), one policy each
+    S wr[BD_MAX_POL];
+    uint32_t nwr = 0;
+    wr[nwr++] = ccid;
+    bool unsup = false;
+    for (uint32_t k = 0; k < rw.nns; k++) {
+      if (!(wflags[k] & 1)) continue;
+      if (wflags[k] & 2) { unsup = true; break; }
+      if (!s_eq(rw.ns[k], ccid)) {
+        if (nwr == BD_MAX_POL) { ovf = true; break; }
+        wr[nwr++] = rw.ns[k];
+      }
+    }
+    if (ovf) break;
+    if (unsup) { R.disp = C_UNSUPPORTED; break; }
+    for (uint32_t i = 1; i < nwr; i++)  // insertion sort
+      for (uint32_t j = i; j > 0 && s_lt(wr[j], wr[j - 1]); j--) {
+        const S tmp = wr[j];
+        wr[j] = wr[j - 1];
+        wr[j - 1] = tmp;
+      }
+    R.disp = C_VALID;
+    for (uint32_t i = 0; i < nwr; i++) R.pol[i] = (int16_t)cc_lookup(ch, wr[i]);
+    R.npol = (uint8_t)nwr;
+    R.nend = (uint8_t)cap.action.nend;
+    for (uint32_t k = 0; k < cap.action.nend; k++) {
+      R.end_ser[k] = rel(base, cap.action.ser[k]);
+      R.end_sig[k] = rel(base, cap.action.sig[k]);
+    }
+  } while (0);
+  if (ovf) atomicOr(flags, 1u);
+  out[t] = R;
+}
+
+// ============================================================ k_bd_ident
+// One thread per (tx, occurrence): occurrence 0 = creator, 1..nend = endorsers.
+// Channel::lookup restated: decode SerializedIdentity (mspid UTF-8), hash, probe, exact compare.
+__global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__restrict__ txs,
+                                                  const uint64_t *__restrict__ bases, DevChannel ch,
+                                                  int32_t *__restrict__ ident) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = g / BD_OCC, k = g % BD_OCC;
+  if (t >= ntx) return;
+  const DevTx &R = txs[t];
+  int32_t res = -1;
+  DSpan sp{0, 0};
+  bool want;
+  if (k == 0) {
+    // needed when the parse got past the channel check (pre still pending)
+    want = R.pre == C_PENDING && R.creator.len;
+    sp = R.creator;
+  } else {
+    want = k <= R.nend;
+    if (want) sp = R.end_ser[k - 1];
+  }
+  if (want && ch.nident) {
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
+    VSerializedIdentity sid;
+    bool ovf = false;
+    if (decode(absl(base, sp), sid, ovf)) {
+      const uint64_t h = bd_ident_hash(sid.mspid.p, sid.mspid.n, sid.id_bytes.p, sid.id_bytes.n);
+      for (uint32_t pos = (uint32_t)h & ch.ident_mask;; pos = (pos + 1) & ch.ident_mask) {
+        const uint32_t e = ch.ident_table[pos];
+        if (e == 0) break;
+        const uint32_t i = e - 1;
+        if (ch.ident_hash[i] != h) continue;
+        const DevIdent &I = ch.idents[i];
+        if (s_eq(sid.mspid, S{ch.ident_bytes + I.msp_off, I.msp_len}) &&
+            s_eq(sid.id_bytes, S{ch.ident_bytes + I.idb_off, I.idb_len})) {
+          res = (int32_t)i;
+          break;
+        }
+      }
+    }
+  }
+  if (k == 0 || k <= R.nend) ident[(size_t)t * BD_OCC + k] = res;
+}
+
+// ============================================================ k_bd_count
+// creator decision (msgvalidation.go:26-64: deserialize, Validate, then Verify) + count_jobs
+__global__ __launch_bounds__(256) void k_bd_count(uint32_t ntx, DevTx *__restrict__ txs, DevChannel ch,
+                                                  const int32_t *__restrict__ ident, DevJobIdx *__restrict__ jobs) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  DevTx &R = txs[t];
+  const int32_t *id = ident + (size_t)t * BD_OCC;
+  DevJobIdx J;
+  for (int q = 0; q < BJ_KINDS; q++) J.cnt[q] = J.base[q] = 0;
+  if (R.pre == C_PENDING) {
+    const int32_t ci = id[0];
+    if (ci < 0 || !ch.idents[ci].valid || ch.idents[ci].key_slot < 0) R.pre = C_BAD_CREATOR;
+  }
+  if ((R.flags & BDF_INDEX_OK) && !(R.flags & BDF_INDEX_FROM_TXID)) J.cnt[BJ_I] = 1;
+  if (R.pre == C_PENDING) {
+    J.cnt[BJ_C] = 1;
+    if (R.type == 3) {
+      J.cnt[BJ_T] = 1;
+      if (R.etx == C_VALID) {
+        J.cnt[BJ_P] = 1;
+        if (R.disp == C_VALID) {
+          uint32_t ne = 0;
+          for (uint32_t k = 0; k < R.nend; k++) {
+            const int32_t e = id[1 + k];
+            if (e >= 0 && ch.idents[e].key_slot >= 0) ne++;
+          }
+          J.cnt[BJ_E] = ne;
+        }
+      }
+    }
+  }
+  jobs[t] = J;
+}
+
+// ============================================================ k_bd_scan
+// single workgroup exclusive scan of the five job counts over all transactions
+#define SCAN_T 1024
+__global__ __launch_bounds__(SCAN_T) void k_bd_scan(uint32_t ntx, DevJobIdx *__restrict__ jobs,
+                                                    uint32_t *__restrict__ totals) {
+  __shared__ uint32_t part[BJ_KINDS][SCAN_T];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t chunk = (ntx + SCAN_T - 1) / SCAN_T;
+  const uint32_t lo = tid * chunk, hi = min(ntx, lo + chunk);
+  uint32_t sum[BJ_KINDS] = {0, 0, 0, 0, 0};
+  for (uint32_t i = lo; i < hi; i++)
+    for (int q = 0; q < BJ_KINDS; q++) sum[q] += jobs[i].cnt[q];
+  for (int q = 0; q < BJ_KINDS; q++) part[q][tid] = sum[q];
+  __syncthreads();
+  for (uint32_t off = 1; off < SCAN_T; off <<= 1) {  // Hillis-Steele inclusive scan
+    uint32_t v[BJ_KINDS];
+    for (int q = 0; q < BJ_KINDS; q++) v[q] = tid >= off ? part[q][tid - off] : 0u;
+    __syncthreads();
+    for (int q = 0; q < BJ_KINDS; q++) part[q][tid] += v[q];
+    __syncthreads();
+  }
+  uint32_t run[BJ_KINDS];
+  for (int q = 0; q < BJ_KINDS; q++) run[q] = part[q][tid] - sum[q];
+  for (uint32_t i = lo; i < hi; i++) {
+    DevJobIdx &J = jobs[i];
+    for (int q = 0; q < BJ_KINDS; q++) {
+      J.base[q] = run[q];
+      run[q] += J.cnt[q];
+    }
+  }
+  if (tid == SCAN_T - 1)
+    for (int q = 0; q < BJ_KINDS; q++) totals[q] = part[q][tid];
+}
+
+// ============================================================ k_bd_emit
+// the assembly loop: SHA-256 jobs grouped by kind [creator payload | nonce||creator |
+// chdr||shdr||ccpp | prp||endorser | index txid], verify jobs [creators | endorsements]
+__global__ __launch_bounds__(256) void k_bd_emit(uint32_t ntx, const DevTx *__restrict__ txs,
+                                                 const uint64_t *__restrict__ bases, DevChannel ch,
+                                                 const int32_t *__restrict__ ident,
+                                                 const DevJobIdx *__restrict__ jobs,
+                                                 const uint32_t *__restrict__ totals, ShaJob *__restrict__ sha,
+                                                 uint64_t *__restrict__ sig_ptr, uint32_t *__restrict__ sig_len,
+                                                 uint32_t *__restrict__ key_slot, uint32_t *__restrict__ dig_idx,
+                                                 unsigned long long *__restrict__ nblk) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t blocks = 0;
+  if (t < ntx) {
+    const DevTx &R = txs[t];
+    const DevJobIdx &J = jobs[t];
+    const int32_t *id = ident + (size_t)t * BD_OCC;
+    const uint64_t base = bases[R.blk];
+    const uint32_t k0 = 0, k1 = totals[0], k2 = k1 + totals[1], k3 = k2 + totals[2], k4 = k3 + totals[3];
+    auto addr = [&](DSpan s) -> uint64_t { return s.len ? base + s.off : 0ull; };
+    auto job = [&](uint32_t idx, DSpan a, DSpan b, DSpan c) {
+      ShaJob j;
+      j.p[0] = addr(a); j.n[0] = a.len;
+      j.p[1] = addr(b); j.n[1] = b.len;
+      j.p[2] = addr(c); j.n[2] = c.len;
+      j.pad = 0;
+      sha[idx] = j;
+      blocks += (a.len + b.len + c.len + 8) / 64 + 1;
+    };
+    auto verify = [&](uint32_t vi, DSpan sig, int32_t slot, uint32_t dig) {
+      sig_ptr[vi] = addr(sig);
+      sig_len[vi] = sig.len;
+      key_slot[vi] = (uint32_t)slot;
+      dig_idx[vi] = dig;
+    };
+    const DSpan z{0, 0};
+    if (J.cnt[BJ_C]) {
+      const uint32_t cj = k0 + J.base[BJ_C];
+      job(cj, R.payload, z, z);
+      verify(J.base[BJ_C], R.env_sig, ch.idents[id[0]].key_slot, cj);
+    }
+    if (J.cnt[BJ_T]) job(k1 + J.base[BJ_T], R.nonce, R.creator, z);
+    if (J.cnt[BJ_P]) job(k2 + J.base[BJ_P], R.chdr, R.act_hdr, R.ccpp);
+    if (J.cnt[BJ_E]) {
+      uint32_t r = 0;
+      for (uint32_t k = 0; k < R.nend && r < J.cnt[BJ_E]; k++) {
+        const int32_t e = id[1 + k];
+        if (e < 0 || ch.idents[e].key_slot < 0) continue;
+        const uint32_t hj = k3 + J.base[BJ_E] + r;
+        job(hj, R.prp, R.end_ser[k], z);
+        verify(totals[0] + J.base[BJ_E] + r, R.end_sig[k], ch.idents[e].key_slot, hj);
+        r++;
+      }
+    }
+    if (J.cnt[BJ_I]) job(k4 + J.base[BJ_I], R.idx_nonce, R.idx_creator, z);
+  }
+  // one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
+  if ((threadIdx.x & 63) == 0 && blocks) atomicAdd(nblk, (unsigned long long)blocks);
+}
+
+// ============================================================ k_bd_fold
+namespace {
+
+// cauthdsl greedy evaluation (common/cauthdsl/cauthdsl.go:24-92): SignedBy takes the first
+// unused signer satisfying the principal; NOutOf tries each sub-rule on a copy of `used`
+// and keeps the copy when it succeeds.  Iterative DFS; returns -1 on stack overflow.
+DEV int eval_policy(const DevChannel &ch, const DevPolicy &P, const int32_t *ids, uint32_t nids) {
+  struct F {
+    uint32_t node, k;
+    int32_t verified;
+    uint32_t saved;
+  };
+  F st[16];
+  int sp = 0;
+  uint32_t used = 0;
+  // evaluate `node`; for NOutOf push a frame and iterate its kids
+  uint32_t node = (uint32_t)P.root;
+  int ret = -2;  // -2: descend into `node`; else result of the last finished node (0/1)
+  for (;;) {
+    if (ret == -2) {
+      const DevPNode &N = ch.nodes[node];
+      if (N.type == 2) {
+        ret = 0;
+        if (N.msp >= 0)
+          for (uint32_t i = 0; i < nids; i++) {
+            if ((used >> i) & 1u) continue;
+            const DevIdent &I = ch.idents[ids[i]];
+            if (I.msp == N.msp && I.valid) {
+              used |= 1u << i;
+              ret = 1;
+              break;
+            }
+          }
+      } else {
+        if (sp == 16) return -1;
+        st[sp++] = F{node, 0, 0, 0};
+        ret = -3;  // start iterating kids
+      }
+    }
+    // ret in {0,1}: a child finished; -3: frame freshly pushed
+    if (sp == 0) return ret;
+    F &f = st[sp - 1];
+    const DevPNode &N = ch.nodes[f.node];
+    if (ret >= 0 && f.k > 0) {  // a kid returned
+      if (ret == 1) f.verified++;
+      else used = f.saved;
+    }
+    if (f.k < N.nkids) {
+      f.saved = used;
+      node = ch.kids[N.kid0 + f.k];
+      f.k++;
+      ret = -2;
+      continue;
+    }
+    ret = f.verified >= N.n ? 1 : 0;
+    sp--;
+    if (sp == 0) return ret;
+  }
+}
+
+DEV bool hex32(S s, uint8_t out[32]) {
+  if (s.n != 64) return false;
+  for (int k = 0; k < 64; k++) {
+    const uint8_t c = s.p[k];
+    int v;
+    if (c >= '0' && c <= '9') v = c - '0';
+    else if (c >= 'a' && c <= 'f') v = c - 'a' + 10;
+    else return false;
+    if (k & 1) out[k >> 1] |= (uint8_t)v;
+    else out[k >> 1] = (uint8_t)(v << 4);
+  }
+  return true;
+}
+
+DEV bool committed(const DevChannel &ch, const uint8_t *d) {
+  bool zero = true;
+  for (int i = 0; i < 32; i++) zero &= d[i] == 0;
+  if (zero) return ch.committed_zero != 0;
+  if (!ch.committed) return false;
+  uint32_t h;
+  memcpy(&h, d, 4);  // SHA-256 output: uniform
+  for (uint32_t pos = h & ch.committed_mask;; pos = (pos + 1) & ch.committed_mask) {
+    const uint8_t *e = ch.committed + (size_t)pos * 32;
+    bool empty = true, eq = true;
+    for (int i = 0; i < 32; i++) {
+      empty &= e[i] == 0;
+      eq &= e[i] == d[i];
+    }
+    if (eq) return true;
+    if (empty) return false;
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__restrict__ txs,
+                                                 const uint64_t *__restrict__ bases, DevChannel ch,
+                                                 const int32_t *__restrict__ ident,
+                                                 const DevJobIdx *__restrict__ jobs,
+                                                 const uint32_t *__restrict__ totals,
+                                                 const uint8_t *__restrict__ digests,
+                                                 const uint8_t *__restrict__ vstatus,
+                                                 fgv_tx_result *__restrict__ res, uint32_t *__restrict__ flags) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  const DevTx &R = txs[t];
+  const DevJobIdx &J = jobs[t];
+  const int32_t *id = ident + (size_t)t * BD_OCC;
+  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
+  const uint32_t k1 = totals[0], k2 = k1 + totals[1], k3 = k2 + totals[2], k4 = k3 + totals[3];
+  auto hexd = [](uint32_t v) -> uint8_t { return (uint8_t)(v < 10 ? '0' + v : 'a' + v - 10); };
+  uint8_t code;
+  bool reached = false;
+  const uint8_t *txd = nullptr;
+  if (R.pre != C_PENDING) {
+    code = R.pre;
+  } else if (vstatus[J.base[BJ_C]] != 0) {
+    code = C_BAD_CREATOR;
+  } else if (R.type == 1) {
+    code = C_UNSUPPORTED;
+  } else if (R.type == 2) {
+    code = C_UNSUP_PAYLOAD;
+  } else {
+    txd = digests + (size_t)(k1 + J.base[BJ_T]) * 32;
+    const S txid = absl(base, R.txid);
+    bool ok = txid.n == 64;
+    for (int k = 0; ok && k < 32; k++)
+      ok = txid.p[2 * k] == hexd(txd[k] >> 4) && txid.p[2 * k + 1] == hexd(txd[k] & 15);
+    if (!ok) {
+      code = C_BAD_TXID;
+    } else if (R.etx != C_VALID) {
+      code = R.etx;
+    } else {
+      const S ph = absl(base, R.prop_hash);
+      const uint8_t *pd = digests + (size_t)(k2 + J.base[BJ_P]) * 32;
+      bool same = ph.n == 32;
+      for (int k = 0; same && k < 32; k++) same = ph.p[k] == pd[k];
+      if (!same) {
+        code = C_BAD_ETX;
+      } else if ((reached = true, committed(ch, txd))) {
+        code = C_DUP_TXID;
+      } else if (R.disp != C_VALID) {
+        code = R.disp;
+      } else {
+        // SignatureSetToValidIdentities: dedup before verify, insert after success
+        int32_t ids[BD_MAX_END];
+        uint32_t seen[BD_MAX_END];
+        uint32_t nids = 0, r = 0;
+        for (uint32_t k = 0; k < R.nend; k++) {
+          const int32_t e = id[1 + k];
+          if (e < 0) continue;
+          const bool has_job = ch.idents[e].key_slot >= 0;
+          const uint32_t vj = has_job ? totals[0] + J.base[BJ_E] + r : 0u;
+          if (has_job) r++;
+          const uint32_t canon = ch.idents[e].canon;
+          bool dup = false;
+          for (uint32_t q = 0; q < nids; q++) dup |= seen[q] == canon;
+          if (dup) continue;
+          if (!has_job || vstatus[vj] != 0) continue;
+          seen[nids] = canon;
+          ids[nids++] = e;
+        }
+        bool has25 = false, has10 = false;
+        code = C_VALID;
+        for (uint32_t i = 0; i < R.npol; i++) {
+          const int pi = R.pol[i];
+          if (pi < 0) { has25 = true; continue; }
+          const DevPolicy &P = ch.policies[pi];
+          if (P.unsupported) { code = C_UNSUPPORTED; break; }
+          bool ok2 = false;
+          if (P.decode_ok && P.compile_ok) {
+            const int v = eval_policy(ch, P, ids, nids);
+            if (v < 0) atomicOr(flags, 1u);  // deeper than the device stack: host redo
+            ok2 = v == 1;
+          }
+          if (!ok2) has10 = true;
+        }
+        if (code != C_UNSUPPORTED) {
+          if (has25 && has10) code = C_UNSUPPORTED;
+          else if (has25) code = C_INVALID_CC;
+          else if (has10) code = C_POLICY;
+        }
+      }
+    }
+  }
+  if (code == C_UNSUPPORTED) atomicOr(flags, 2u);
+  fgv_tx_result o;
+  o.code = code;
+  o.flags = 0;
+  o.pad[0] = o.pad[1] = 0;
+  for (int k = 0; k < 32; k++) o.txid[k] = o.index_txid[k] = 0;
+  if (reached) {
+    for (int k = 0; k < 32; k++) o.txid[k] = txd[k];
+    o.flags |= FGV_TXR_REACHED;
+  }
+  if (R.flags & BDF_INDEX_OK) {
+    if (!(R.flags & BDF_INDEX_FROM_TXID)) {
+      const uint8_t *d = digests + (size_t)(k4 + J.base[BJ_I]) * 32;
+      for (int k = 0; k < 32; k++) o.index_txid[k] = d[k];
+      o.flags |= FGV_TXR_INDEXED;
+    } else if (hex32(absl(base, R.index_txid), o.index_txid)) {
+      o.flags |= FGV_TXR_INDEXED;
+    }
+  }
+  res[t] = o;
+}

@@ -41,6 +41,7 @@
 #include "pbwire.h"
 
 #include "fgv_visitors.h"
+#include "blockdev.h"
 
 // ======================================================================= channel model
 namespace fgvb {
@@ -283,12 +284,27 @@ struct TxRec {
 // ======================================================================= context glue
 using namespace fgvb;
 
+// channel model image in HBM for the device-resident path (blockdev.h DevChannel)
+struct DevImage {
+  DevBuf name, idents, ibytes, itable, ihash, cc, ccb, pol, nodes, kids, committed;
+  DevChannel ch{};
+  void release() {
+    for (DevBuf *b : {&name, &idents, &ibytes, &itable, &ihash, &cc, &ccb, &pol, &nodes, &kids, &committed})
+      b->release();
+  }
+};
+
 struct fgv_block_state {
   Channel ch;
   ThreadPool pool;
   // per-call scratch
   std::vector<TxRec> recs;
+  // device image of `ch`, rebuilt when the channel model changes
+  DevImage dimg;
+  bool dev_dirty = true;
+  int parse_mode = 0;  // 0: device parse (host parser for capacity overflows), 1: host parse
   explicit fgv_block_state(unsigned threads) : pool(threads) {}
+  ~fgv_block_state() { dimg.release(); }
 };
 
 fgv_block_state *fgv_block_state_new(unsigned threads) { return new fgv_block_state(threads); }
@@ -779,12 +795,14 @@ int fgv_finalize_impl(size_t nblocks, const size_t *ntx, const fgv_tx_result *re
 
 // ---- configuration entry points (called from fgv_host.cpp wrappers)
 int fgv_block_set_channel(fgv_block_state *S, const char *name) {
+  S->dev_dirty = true;
   S->ch.name = name ? name : "";
   return FGV_OK;
 }
 
 int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, int32_t key_slot, int valid,
                            const uint8_t id_digest[32]) {
+  S->dev_dirty = true;
   VSerializedIdentity sid;
   if (!pbw::decode(ser, len, sid)) return FGV_EINVAL;
   Ident I;
@@ -806,6 +824,7 @@ int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, i
 }
 
 int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const uint8_t *policy, size_t len) {
+  S->dev_dirty = true;
   Policy P = compile_policy(policy, len);
   for (size_t i = 0; i < P.principal_msp.size(); i++)
     P.principal_mspi.push_back(P.principal_bad[i] ? -1 : S->ch.intern(P.principal_msp[i]));
@@ -821,11 +840,271 @@ int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const uint8_t
 
 int fgv_block_add_txids(fgv_block_state *S, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
                         size_t n) {
+  S->dev_dirty = true;
   for (size_t i = 0; i < n; i++) {
     std::string_view v(reinterpret_cast<const char *>(buf + off[i]), len[i]);
     if (S->ch.committed.count(v)) continue;
     S->ch.committed_store.emplace_back(v);
     S->ch.committed.insert(std::string_view(S->ch.committed_store.back()));
   }
+  return FGV_OK;
+}
+
+
+// ======================================================================= device-resident path
+int fgv_block_set_parse_mode(fgv_block_state *S, int mode) {
+  if (mode != 0 && mode != 1) return FGV_EINVAL;
+  S->parse_mode = mode;
+  return FGV_OK;
+}
+int fgv_block_parse_mode(fgv_block_state *S) { return S->parse_mode; }
+
+template <class T>
+static int upload(DevBuf &b, const std::vector<T> &v) {
+  const size_t n = v.size() * sizeof(T);
+  if (!b.ensure(n ? n : 16)) return FGV_ENOMEM;
+  if (n) HIP_TRY(hipMemcpy(b.p, v.data(), n, hipMemcpyHostToDevice));
+  return FGV_OK;
+}
+
+// Flatten the channel model into the HBM image the kernels read (blockdev.h).
+static int build_dev_image(fgv_block_state *S) {
+  const Channel &ch = S->ch;
+  DevImage &D = S->dimg;
+  int rc;
+  std::vector<uint8_t> name(ch.name.begin(), ch.name.end());
+  if ((rc = upload(D.name, name))) return rc;
+  // identities
+  std::vector<DevIdent> idents(ch.idents.size());
+  std::vector<uint8_t> ib;
+  std::vector<uint64_t> ih(ch.idents.size());
+  for (size_t i = 0; i < ch.idents.size(); i++) {
+    const Ident &I = ch.idents[i];
+    DevIdent &d = idents[i];
+    d.msp_off = (uint32_t)ib.size();
+    d.msp_len = (uint32_t)I.mspid.size();
+    ib.insert(ib.end(), I.mspid.begin(), I.mspid.end());
+    d.idb_off = (uint32_t)ib.size();
+    d.idb_len = (uint32_t)I.id_bytes.size();
+    ib.insert(ib.end(), I.id_bytes.begin(), I.id_bytes.end());
+    d.key_slot = I.key_slot;
+    d.msp = I.msp;
+    d.canon = I.canon;
+    d.valid = I.valid ? 1u : 0u;
+    ih[i] = bd_ident_hash(reinterpret_cast<const uint8_t *>(I.mspid.data()), d.msp_len,
+                          reinterpret_cast<const uint8_t *>(I.id_bytes.data()), d.idb_len);
+  }
+  size_t icap = 16;
+  while (icap < 2 * ch.idents.size()) icap <<= 1;
+  std::vector<uint32_t> itable(icap, 0);
+  for (size_t i = 0; i < ch.idents.size(); i++) {
+    uint32_t pos = (uint32_t)ih[i] & (uint32_t)(icap - 1);
+    while (itable[pos]) pos = (pos + 1) & (uint32_t)(icap - 1);
+    itable[pos] = (uint32_t)i + 1;
+  }
+  if ((rc = upload(D.idents, idents)) || (rc = upload(D.ibytes, ib)) || (rc = upload(D.itable, itable)) ||
+      (rc = upload(D.ihash, ih)))
+    return rc;
+  // chaincodes -> policies; policies -> flat node / kid arrays
+  std::vector<uint32_t> cc;
+  std::vector<uint8_t> ccb;
+  for (const auto &kv : ch.chaincodes) {
+    cc.push_back((uint32_t)ccb.size());
+    cc.push_back((uint32_t)kv.first.size());
+    cc.push_back((uint32_t)kv.second);
+    ccb.insert(ccb.end(), kv.first.begin(), kv.first.end());
+  }
+  std::vector<DevPolicy> pol(ch.policies.size());
+  std::vector<DevPNode> nodes;
+  std::vector<uint32_t> kids;
+  for (size_t p = 0; p < ch.policies.size(); p++) {
+    const Policy &P = ch.policies[p];
+    const uint32_t nbase = (uint32_t)nodes.size();
+    pol[p].decode_ok = P.decode_ok;
+    pol[p].compile_ok = P.compile_ok;
+    pol[p].unsupported = P.unsupported;
+    pol[p].root = P.root >= 0 ? (int32_t)(nbase + P.root) : -1;
+    for (const PNode &N : P.nodes) {
+      DevPNode d;
+      d.type = N.type;
+      d.n = N.n;
+      d.msp = (N.type == 2) ? P.principal_mspi[N.principal] : -1;
+      d.kid0 = (uint32_t)kids.size();
+      d.nkids = (uint32_t)N.kids.size();
+      for (int k : N.kids) kids.push_back(nbase + (uint32_t)k);
+      nodes.push_back(d);
+    }
+  }
+  if ((rc = upload(D.cc, cc)) || (rc = upload(D.ccb, ccb)) || (rc = upload(D.pol, pol)) ||
+      (rc = upload(D.nodes, nodes)) || (rc = upload(D.kids, kids)))
+    return rc;
+  // committed ledger txids: only 64-char lowercase hex can equal a txid that passed CheckTxID
+  std::vector<std::array<uint8_t, 32>> keys;
+  uint32_t zero = 0;
+  for (const std::string_view &v : ch.committed) {
+    std::array<uint8_t, 32> k;
+    if (!hex32(Span{reinterpret_cast<const uint8_t *>(v.data()), (uint32_t)v.size()}, k.data())) continue;
+    bool z = true;
+    for (uint8_t x : k) z &= x == 0;
+    if (z) zero = 1;
+    else keys.push_back(k);
+  }
+  size_t ccap = 0;
+  std::vector<uint8_t> ctab;
+  if (!keys.empty()) {
+    ccap = 16;
+    while (ccap < 2 * keys.size()) ccap <<= 1;
+    ctab.assign(ccap * 32, 0);
+    for (const auto &k : keys) {
+      uint32_t h;
+      memcpy(&h, k.data(), 4);
+      uint32_t pos = h & (uint32_t)(ccap - 1);
+      while (true) {
+        uint8_t *e = &ctab[(size_t)pos * 32];
+        bool empty = true;
+        for (int i = 0; i < 32; i++) empty &= e[i] == 0;
+        if (empty) { memcpy(e, k.data(), 32); break; }
+        if (memcmp(e, k.data(), 32) == 0) break;
+        pos = (pos + 1) & (uint32_t)(ccap - 1);
+      }
+    }
+  }
+  if ((rc = upload(D.committed, ctab))) return rc;
+  DevChannel &d = D.ch;
+  d.name = D.name.as<uint8_t>();
+  d.name_len = (uint32_t)name.size();
+  d.nident = (uint32_t)idents.size();
+  d.idents = D.idents.as<DevIdent>();
+  d.ident_bytes = D.ibytes.as<uint8_t>();
+  d.ident_table = D.itable.as<uint32_t>();
+  d.ident_hash = D.ihash.as<uint64_t>();
+  d.ident_mask = (uint32_t)(icap - 1);
+  d.ncc = (uint32_t)(cc.size() / 3);
+  d.cc = D.cc.as<uint32_t>();
+  d.cc_bytes = D.ccb.as<uint8_t>();
+  d.policies = D.pol.as<DevPolicy>();
+  d.nodes = D.nodes.as<DevPNode>();
+  d.kids = D.kids.as<uint32_t>();
+  d.committed = ccap ? D.committed.as<uint8_t>() : nullptr;
+  d.committed_mask = ccap ? (uint32_t)(ccap - 1) : 0u;
+  d.committed_zero = zero;
+  return FGV_OK;
+}
+
+__global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, DevChannel ch, DevTx *out,
+                           uint32_t *flags);
+__global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
+__global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs);
+__global__ void k_bd_scan(uint32_t ntx, DevJobIdx *jobs, uint32_t *totals);
+__global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
+                          const DevJobIdx *jobs, const uint32_t *totals, ShaJob *sha, uint64_t *sig_ptr,
+                          uint32_t *sig_len, uint32_t *key_slot, uint32_t *dig_idx, unsigned long long *nblk);
+__global__ void k_bd_fold(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
+                          const DevJobIdx *jobs, const uint32_t *totals, const uint8_t *digests,
+                          const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags);
+
+int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
+                           const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                           const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out) {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+  auto t0 = clk::now();
+  if (S->dev_dirty) {
+    int rc = build_dev_image(S);
+    if (rc) return rc;
+    S->dev_dirty = false;
+  }
+  // --- host: split the blocks into envelope spans (tag / length walk)
+  std::vector<std::vector<Span>> envs(nblocks);
+  std::vector<uint32_t> lo(nblocks), hi(nblocks);
+  std::atomic<bool> bad{false};
+  S->pool.run(nblocks, [&](size_t b) {
+    VBlock blk;
+    if (!pbw::decode(h_blocks[b], lens[b], blk)) { bad = true; return; }
+    envs[b] = std::move(blk.data.data);
+  });
+  if (bad) return FGV_EINVAL;
+  size_t total = 0;
+  std::vector<size_t> first(nblocks);
+  for (size_t b = 0; b < nblocks; b++) {
+    ntx_out[b] = envs[b].size();
+    lo[b] = tx_lo ? std::min<uint32_t>(tx_lo[b], (uint32_t)envs[b].size()) : 0;
+    hi[b] = tx_hi ? std::min<uint32_t>(tx_hi[b], (uint32_t)envs[b].size()) : (uint32_t)envs[b].size();
+    if (hi[b] < lo[b]) hi[b] = lo[b];
+    first[b] = total;
+    total += hi[b] - lo[b];
+    if (lens[b] > 0xFFFFFFFFull) return FGV_EINVAL;
+  }
+  if (total > res_cap || total >= 0x7FFFFFFFull) return FGV_EINVAL;
+  c->n_sha_jobs = c->n_sha_blocks = c->n_verifies = 0;
+  if (total == 0) return FGV_OK;
+  const uint32_t N = (uint32_t)total;
+  if (!c->hb_env.ensure(total * 12) || !c->hb_bases.ensure(nblocks * 8) || !c->hb_misc.ensure(64) ||
+      !c->bd_env.ensure(total * 12) || !c->bd_bases.ensure(nblocks * 8) || !c->bd_misc.ensure(64) ||
+      !c->bd_tx.ensure(total * sizeof(DevTx)) || !c->bd_ident.ensure(total * BD_OCC * 4) ||
+      !c->bd_jobs.ensure(total * sizeof(DevJobIdx)))
+    return FGV_ENOMEM;
+  uint32_t *et = c->hb_env.as<uint32_t>();
+  uint64_t *bs = c->hb_bases.as<uint64_t>();
+  S->pool.run(nblocks, [&](size_t b) {
+    bs[b] = (uint64_t)(uintptr_t)d_blocks[b];
+    uint32_t *o = et + 3 * first[b];
+    for (uint32_t i = lo[b]; i < hi[b]; i++, o += 3) {
+      o[0] = (uint32_t)b;
+      o[1] = (uint32_t)(envs[b][i].p - h_blocks[b]);
+      o[2] = envs[b][i].n;
+    }
+  });
+  c->t_host_parse = ms_since(t0);
+  auto t1 = clk::now();
+  hipStream_t st = c->stream;
+  uint32_t *misc = c->bd_misc.as<uint32_t>();  // [0..5) totals, [5] flags, bytes 24..32 compressions
+  HIP_TRY(hipMemcpyAsync(c->bd_env.p, et, total * 12, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(c->bd_bases.p, bs, nblocks * 8, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(misc, 0, 64, st));
+  const DevChannel ch = S->dimg.ch;
+  DevTx *dtx = c->bd_tx.as<DevTx>();
+  int32_t *did = c->bd_ident.as<int32_t>();
+  DevJobIdx *dj = c->bd_jobs.as<DevJobIdx>();
+  const uint64_t *dbs = c->bd_bases.as<uint64_t>();
+  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, st, N, c->bd_env.as<uint32_t>(), dbs, ch, dtx,
+                     misc + 5);
+  const uint64_t nocc = (uint64_t)N * BD_OCC;
+  hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)((nocc + 255) / 256)), dim3(256), 0, st, N, dtx, dbs, ch, did);
+  hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, ch, did, dj);
+  hipLaunchKernelGGL(k_bd_scan, dim3(1), dim3(1024), 0, st, N, dj, misc);
+  HIP_TRY(hipGetLastError());
+  uint32_t *hm = c->hb_misc.as<uint32_t>();
+  HIP_TRY(hipMemcpyAsync(hm, misc, 32, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (hm[5] & 1u) return 1;  // capacity overflow: host parser
+  const size_t nj = (size_t)hm[0] + hm[1] + hm[2] + hm[3] + hm[4], nv = (size_t)hm[0] + hm[3];
+  c->t_bd_pre = ms_since(t1);
+  c->t_host_assemble = c->t_bd_pre;
+  auto t2 = clk::now();
+  if (!c->bj_jobs.ensure(nj * sizeof(ShaJob) + 64) || !c->bj_sigp.ensure(nv * 20 + 64) ||
+      !c->bj_dig.ensure(nj * 32 + 64) || !c->bj_vst.ensure(nv + 64))
+    return FGV_ENOMEM;
+  uint8_t *sp = c->bj_sigp.as<uint8_t>();
+  unsigned long long *nblk = reinterpret_cast<unsigned long long *>(misc + 6);
+  hipLaunchKernelGGL(k_bd_emit, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
+                     c->bj_jobs.as<ShaJob>(), reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + nv * 8),
+                     reinterpret_cast<uint32_t *>(sp + nv * 12), reinterpret_cast<uint32_t *>(sp + nv * 16), nblk);
+  HIP_TRY(hipGetLastError());
+  int rc = fgv_run_block_jobs_device(c, nj, nv, 0);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
+                     c->bj_dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(hm, misc, 32, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  fgv_read_block_job_times(c);
+  uint64_t nb;
+  memcpy(&nb, hm + 6, 8);
+  c->n_sha_blocks = nb;
+  c->t_host_device = ms_since(t2);
+  c->t_host_fold = 0;
+  if (hm[5] & 1u) return 1;
+  if (hm[5] & 2u) return FGV_EUNSUPPORTED;
   return FGV_OK;
 }

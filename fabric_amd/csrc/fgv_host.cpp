@@ -590,6 +590,56 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
   return FGV_OK;
 }
 
+// Device-resident variant (blockdev path): the jobs were written by k_bd_emit straight into
+// c->bj_jobs / c->bj_sigp (layout of fgv_block_jobs_reserve); digests stay in c->bj_dig and
+// verify status in c->bj_vst.  Enqueued on c->stream; no host copies, no synchronisation.
+int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks) {
+  c->n_sha_jobs = nj;
+  c->n_verifies = nv;
+  c->n_sha_blocks = sha_blocks;
+  if (nj == 0) return FGV_OK;
+  bool ran = false;
+  if (nv) {
+    const uint32_t N = (uint32_t)nv;
+    if (!c->r.ensure(nv * 32) || !c->s.ensure(nv * 32)) return FGV_ENOMEM;
+    uint8_t *dsig = c->bj_sigp.as<uint8_t>();
+    const uint64_t *d_sigp = reinterpret_cast<const uint64_t *>(dsig);
+    const uint32_t *d_sigl = reinterpret_cast<const uint32_t *>(dsig + nv * 8);
+    const uint32_t *d_slot = reinterpret_cast<const uint32_t *>(dsig + nv * 12);
+    hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr, d_sigp,
+                       d_sigl, N, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(), c->s.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[7], c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev[7], 0));
+    int rc = launch_inv(c, c->stream2, N, c->bj_vst.as<uint8_t>(), d_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>());
+    if (rc) return rc;
+  }
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  hipLaunchKernelGGL(k_sha256_jobs, dim3((uint32_t)((nj + 255) / 256)), dim3(256), 0, c->stream,
+                     c->bj_jobs.as<ShaJob>(), (uint32_t)nj, c->bj_dig.as<uint8_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  if (nv) {
+    const uint32_t N = (uint32_t)nv;
+    const uint8_t *dsig = c->bj_sigp.as<uint8_t>();
+    int rc = launch_prep_point(c, N, c->bj_vst.as<uint8_t>(), reinterpret_cast<const uint32_t *>(dsig + nv * 12),
+                               c->r.as<uint32_t>(), c->bj_dig.as<uint8_t>(),
+                               reinterpret_cast<const uint32_t *>(dsig + nv * 16));
+    if (rc) return rc;
+    ran = true;
+  }
+  c->stage_ran = ran;
+  return FGV_OK;
+}
+
+// stage times of the last fgv_run_block_jobs_device (after the stream has been synchronised)
+void fgv_read_block_job_times(fgv_ctx *c) {
+  float ms = 0;
+  c->t_sha = 0;
+  if (c->n_sha_jobs && hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->t_sha = ms;
+  read_stage_times(c, c->stage_ran);
+}
+
 extern "C" {
 
 int fgv_channel_init(fgv_ctx *c, const char *name) {
@@ -704,6 +754,22 @@ static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks
   return FGV_OK;
 }
 
+static size_t shard_count(size_t nblocks, const size_t *ntx, const uint32_t *tx_lo, const uint32_t *tx_hi) {
+  size_t n = 0;
+  for (size_t b = 0; b < nblocks; b++) {
+    const size_t lo = tx_lo ? std::min<size_t>(tx_lo[b], ntx[b]) : 0;
+    const size_t hi = tx_hi ? std::min<size_t>(tx_hi[b], ntx[b]) : ntx[b];
+    if (hi > lo) n += hi - lo;
+  }
+  return n;
+}
+
+int fgv_set_parse_mode(fgv_ctx *c, int mode) {
+  if (!c) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_set_parse_mode(c->blk, mode);
+}
+
 int fgv_validate_shard(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                        const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
                        fgv_tx_result *results, size_t results_cap, size_t *ntx) {
@@ -714,6 +780,17 @@ int fgv_validate_shard(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks,
   std::vector<const uint8_t *> dev;
   int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
   if (rc) return rc;
+  if (fgv_block_parse_mode(c->blk) == 0) {
+    if (!c->fz_res.ensure(results_cap * sizeof(fgv_tx_result) + 64)) return FGV_ENOMEM;
+    rc = fgv_block_validate_dev(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi,
+                                c->fz_res.as<fgv_tx_result>(), results_cap, ntx);
+    if (rc != 1) {
+      if (rc) return rc;
+      const size_t n = shard_count(nblocks, ntx, tx_lo, tx_hi);
+      if (n) HIP_TRY(hipMemcpy(results, c->fz_res.p, n * sizeof(fgv_tx_result), hipMemcpyDeviceToHost));
+      return FGV_OK;
+    }
+  }
   return fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi, results,
                                  results_cap, ntx);
 }
@@ -728,6 +805,11 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   std::vector<const uint8_t *> dev;
   int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
   if (rc) return rc;
+  if (fgv_block_parse_mode(c->blk) == 0) {
+    rc = fgv_block_validate_dev(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi,
+                                static_cast<fgv_tx_result *>(d_results), results_cap, ntx);
+    if (rc != 1) return rc;
+  }
   if (!c->hb_res.ensure(results_cap * sizeof(fgv_tx_result) + 64)) return FGV_ENOMEM;
   fgv_tx_result *res = c->hb_res.as<fgv_tx_result>();
   rc = fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi, res, results_cap, ntx);
@@ -781,6 +863,12 @@ int fgv_validate_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks
   }
   if (!c->hb_res.ensure(total * sizeof(fgv_tx_result) + 64) || !c->fz_res.ensure(total * sizeof(fgv_tx_result)))
     return FGV_ENOMEM;
+  if (fgv_block_parse_mode(c->blk) == 0) {
+    rc = fgv_block_validate_dev(c, c->blk, nblocks, blocks, lens, dev.data(), nullptr, nullptr,
+                                c->fz_res.as<fgv_tx_result>(), total, ntx);
+    if (rc == 0) return finalize_dev_core(c, nblocks, ntx, 1, total, c->fz_res.as<uint8_t>(), flags);
+    if (rc != 1) return rc;
+  }
   fgv_tx_result *res = c->hb_res.as<fgv_tx_result>();
   rc = fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), nullptr, nullptr, res, total, ntx);
   if (rc) return rc;

@@ -124,6 +124,11 @@ struct fgv_ctx {
   // with committer calls on the same context
   ThreadPool *integ_pool = nullptr;
   std::mutex integ_mu;
+  // device-resident committer path (blockdev.hip)
+  bool stage_ran = false;
+  DevBuf bd_env, bd_bases, bd_tx, bd_ident, bd_jobs, bd_misc;
+  HostBuf hb_env, hb_bases, hb_misc;
+  double t_bd_split = 0, t_bd_pre = 0, t_bd_fold = 0;
 };
 void fgv_integrity_free(fgv_ctx *c);
 
@@ -164,3 +169,14 @@ int fgv_block_jobs_reserve(fgv_ctx *c, size_t nj, size_t nv, BlockJobs *out);
 // context.  sha_blocks: compressions of the batch (statistics).  Implemented in fgv_host.cpp.
 int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, const uint8_t **digests,
                        const uint8_t **vstatus);
+// device-resident variant: jobs already in c->bj_jobs / c->bj_sigp; results stay in HBM
+int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks);
+void fgv_read_block_job_times(fgv_ctx *c);
+int fgv_block_set_parse_mode(fgv_block_state *S, int mode);
+int fgv_block_parse_mode(fgv_block_state *S);
+// device-resident committer pass (fgv_block.cpp + blockdev.hip): records -> d_res (HBM).
+// Returns FGV_OK, FGV_EUNSUPPORTED, an error, or 1 = "a transaction exceeded a device
+// capacity: run the host parser for this batch".
+int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
+                           const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                           const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out);

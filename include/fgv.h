@@ -154,6 +154,12 @@ typedef struct fgv_tx_result {
   uint8_t index_txid[32];
 } fgv_tx_result; /* 68 bytes */
 
+/* Where transactions are parsed: 0 (default) = on the GPU from the HBM-resident blocks
+ * (parse, identity resolution, job assembly and policy fold as kernels; a transaction whose
+ * shape exceeds a device capacity -- more than 16 endorsements, 8 namespaces, ... -- sends
+ * its batch through the host parser), 1 = host parser (C++ threads).  Same results. */
+int fgv_set_parse_mode(fgv_ctx *ctx, int mode);
+
 int fgv_validate_shard(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                        const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
                        fgv_tx_result *results, size_t results_cap, size_t *ntx);

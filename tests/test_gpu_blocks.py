@@ -11,10 +11,15 @@ from tests.blockfix import C5_ENDORSE, SPECIAL, block_from_envs, corrupt_envelop
 pytestmark = pytest.mark.gpu
 
 
-def _engine_for(net, committed=()):
+def _engine_for(net, committed=(), mode=0):
+    """mode 0: device-resident parse (default), 1: host parser."""
     eng = _lib.Engine(0)
+    eng.set_parse_mode(mode)
     txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes, committed)
     return eng
+
+
+MODES = pytest.mark.parametrize("mode", [0, 1], ids=["devparse", "hostparse"])
 
 
 def _oracle(net, blks, committed=()):
@@ -31,9 +36,10 @@ def _check(eng, net, blks, committed=()):
     return exp
 
 
-def test_c2_blocks_and_fault_classes():
+@MODES
+def test_c2_blocks_and_fault_classes(mode):
     net = network()
-    eng = _engine_for(net)
+    eng = _engine_for(net, mode=mode)
     blks = [blocks.make_block(net, 500, number=1 + i, seed=i)[0] for i in range(2)]
     blks.append(blocks.make_block(net, len(SPECIAL), number=3, seed=3, faults=(), force=SPECIAL)[0])
     exp = _check(eng, net, blks)
@@ -42,18 +48,20 @@ def test_c2_blocks_and_fault_classes():
     eng.close()
 
 
+@MODES
 @pytest.mark.parametrize("seed", [11, 12, 13])
-def test_corruption_fuzz(seed):
+def test_corruption_fuzz(seed, mode):
     """Mutated envelopes exercise every protobuf rule and code-precedence branch."""
     net = network()
-    eng = _engine_for(net)
+    eng = _engine_for(net, mode=mode)
     _, _, envs = blocks.make_block(net, 60, number=1, seed=seed)
     bad = corrupt_envelopes(envs, seed, 300)
     _check(eng, net, [block_from_envs(envs + bad, number=2)])
     eng.close()
 
 
-def test_multi_block_txid_index_and_ledger():
+@MODES
+def test_multi_block_txid_index_and_ledger(mode):
     net = network()
     txs = []
     b1, _, envs1 = blocks.make_block(net, 20, number=1, seed=21, faults=(), out_txs=txs)
@@ -61,15 +69,16 @@ def test_multi_block_txid_index_and_ledger():
                                                                                  9: (txs[7].creator, txs[7].nonce)})
     committed = [v20.index_txid(envs1[0])]
     b3, _, _ = blocks.make_block(net, 5, number=3, seed=23, faults=(), reuse={1: (txs[0].creator, txs[0].nonce)})
-    eng = _engine_for(net, committed)
+    eng = _engine_for(net, committed, mode=mode)
     exp = _check(eng, net, [b1, b2, b3], committed)
     assert exp[0][0] == 9 and exp[1][5] == 9 and exp[1][9] == 9 and exp[2][1] == 9
     eng.close()
 
 
-def test_empty_and_degenerate_blocks():
+@MODES
+def test_empty_and_degenerate_blocks(mode):
     net = network()
-    eng = _engine_for(net)
+    eng = _engine_for(net, mode=mode)
     _, _, envs = blocks.make_block(net, 3, number=1, seed=31, faults=())
     blks = [block_from_envs([]), block_from_envs([b"", b"\x0a\x00", envs[0], b"\x12\x00"]),
             block_from_envs([envs[1]] * 3)]
@@ -78,18 +87,21 @@ def test_empty_and_degenerate_blocks():
     eng.close()
 
 
-def test_policy_variants():
+@MODES
+def test_policy_variants(mode):
     for n in (1, 3):
         net = network(policy_n=n)
-        eng = _engine_for(net)
+        eng = _engine_for(net, mode=mode)
         blk, _, _ = blocks.make_block(net, 50, number=1, seed=40 + n)
         _check(eng, net, [blk])
         eng.close()
 
 
-def test_unsupported_is_reported_not_guessed():
+@MODES
+def test_unsupported_is_reported_not_guessed(mode):
     net = network()
     eng = _lib.Engine(0)
+    eng.set_parse_mode(mode)
     txvalidator.setup_channel(eng, net.channel, net.identities(), {"mycc": blocks.f_str(2, "/Channel/Application/E")})
     blk, _, _ = blocks.make_block(net, 4, number=1, seed=50, faults=())
     with pytest.raises(_lib.Unsupported):
@@ -233,10 +245,11 @@ def test_device_finalize_matches_host_finalize(seed, pool, world):
     eng.close()
 
 
-def test_c5_mixed_ed25519_blocks_match_oracle():
+@MODES
+def test_c5_mixed_ed25519_blocks_match_oracle(mode):
     """C5 shape at oracle-sized blocks: 8 orgs, 5-of-8, 5-6 endorsements, Ed25519 identities."""
     net = network_c5()
-    eng = _engine_for(net)
+    eng = _engine_for(net, mode=mode)
     blks = [blocks.make_block(net, 300, number=1 + i, seed=100 + i, endorse_dist=C5_ENDORSE)[0] for i in range(2)]
     _check(eng, net, blks)
     eng.close()
@@ -257,4 +270,28 @@ def test_c5_full_size_block_and_integrity():
     chain = _lib.ChainState(number=0, valid=1, has_hash=0)
     chk = eng.blocks_verify([blk, blk], chain)
     assert [c[0] for c in chk] == [_lib.BLK_OK, _lib.BLK_NUMBER] and chain.number == 1
+    eng.close()
+
+
+def test_device_capacity_overflow_falls_back_to_host_parser():
+    """17 endorsements exceed the device parser's capacity (BD_MAX_END): the batch is parsed
+    by the host parser and the flags still equal the oracle's."""
+    net = network()
+    _, _, envs = blocks.make_block(net, 4, number=1, seed=111, faults=())
+    import fabric_amd.synth.blocks as B
+    txs = []
+    blocks.make_block(net, 3, number=2, seed=112, faults=(), out_txs=txs)
+    # a tx with 17 copies of one endorsement (dedup -> 1 identity -> policy failure, code 10)
+    t = txs[0]
+    e = B.f_msg(2, B.f_bytes(1, t.endorsers[0].serialized) + B.f_bytes(2, t.esigs[0]))
+    big = B.f_bytes(1, t.prp) + e * 17
+    cap = B.f_bytes(1, t.ccpp) + B.f_msg(2, big)
+    action = B.f_msg(1, B.f_bytes(1, t.shdr) + B.f_bytes(2, cap))
+    payload = B.f_msg(1, B.f_bytes(1, t.chdr) + B.f_bytes(2, t.shdr)) + B.f_bytes(2, action)
+    from fabric_amd import synth
+    sig = synth.sign(t.creator.key, blocks.hashlib.sha256(payload).digest())
+    env = B.f_bytes(1, payload) + B.f_bytes(2, sig)
+    eng = _engine_for(net)
+    exp = _check(eng, net, [block_from_envs(envs + [env], number=1)])
+    assert exp[0][-1] == 10
     eng.close()
