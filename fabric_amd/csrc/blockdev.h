@@ -7,8 +7,9 @@
 //               device code with fixed capacities) -> DevTx: spans + structural codes
 //   k_bd_ident  MSP identity resolution of the creator and every endorser: decode the
 //               SerializedIdentity, hash, probe the HBM identity table, exact byte compare
-//   k_bd_count  creator checks + device job counts; k_bd_scan exclusive scan; k_bd_emit writes
-//               the SHA-256 jobs and the ECDSA verify jobs straight into the job arrays
+//   k_bd_count  creator checks + device job counts, job slots claimed by wave-aggregated
+//               atomics; k_bd_emit writes the SHA-256 jobs and the ECDSA verify jobs straight
+//               into the job arrays
 //   (k_sha256_jobs, k_der, k_inv, k_prep, k_point as for host-assembled batches)
 //   k_bd_fold   code precedence, SignatureSetToValidIdentities, cauthdsl NOutOf fold, txid
 //               index entries -> fgv_tx_result records in HBM (input of the device finalize)
@@ -46,7 +47,7 @@ struct DevTx {
 enum { BJ_C = 0, BJ_T, BJ_P, BJ_E, BJ_I, BJ_KINDS };
 struct DevJobIdx {
   uint32_t cnt[BJ_KINDS];  // jobs of each kind (creator-payload, txid, proposal, endorsement, index)
-  uint32_t base[BJ_KINDS]; // first job of each kind (exclusive scan)
+  uint32_t base[BJ_KINDS]; // first job of each kind (slot within the kind's group)
 };
 
 // identity registry in HBM (built on the host from the channel model)
@@ -90,20 +91,22 @@ struct DevChannel {  // device pointers + sizes (passed by value to the kernels)
 };
 
 // identity-index hash (host builds the table with it, device probes with it): Mspid bytes,
-// id_bytes length, and the first 64 / last 192 bytes of id_bytes (a PEM certificate: serial
-// number near the front, signature at the end).  Not cryptographic: every hit is confirmed
-// by an exact compare of both fields.
+// id_bytes length, and the last <= 96 bytes of id_bytes as little-endian 32-bit words (a
+// certificate ends in its signature, so the tail tells identities apart; the device reads it
+// with 25 word loads instead of a byte walk).  Not cryptographic: every hit is confirmed by an
+// exact compare of both fields.
 #if defined(__HIPCC__)
 #define BD_HD __host__ __device__
 #else
 #define BD_HD
 #endif
+#define BD_HASH_TAIL 96u
 BD_HD inline uint64_t bd_mix(uint64_t h, uint64_t v) {
   h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
   h *= 0xC2B2AE3D27D4EB4Full;
   return h ^ (h >> 29);
 }
-BD_HD inline uint64_t bd_ident_hash(const uint8_t *msp, uint32_t ml, const uint8_t *idb, uint32_t il) {
+BD_HD inline uint64_t bd_ident_hash_msp(const uint8_t *msp, uint32_t ml, uint32_t il) {
   uint64_t h = bd_mix(0x243F6A8885A308D3ull, ((uint64_t)ml << 32) | il);
   uint64_t w = 0;
   uint32_t k = 0;
@@ -111,15 +114,16 @@ BD_HD inline uint64_t bd_ident_hash(const uint8_t *msp, uint32_t ml, const uint8
     w |= (uint64_t)msp[i] << (8 * (k++));
     if (k == 8) { h = bd_mix(h, w); w = 0; k = 0; }
   }
-  h = bd_mix(h, w ^ 0xA5);
-  w = 0;
-  k = 0;
-  const uint32_t head = il < 64 ? il : 64;
-  const uint32_t tail0 = il > 192 ? il - 192 : 0;
-  for (uint32_t i = 0; i < il; i++) {
-    if (i == head && i < tail0) i = tail0;  // skip the middle
-    w |= (uint64_t)idb[i] << (8 * (k++));
-    if (k == 8) { h = bd_mix(h, w); w = 0; k = 0; }
+  return bd_mix(h, w ^ 0xA5);
+}
+// host form (byte loads); blockdev.hip has the word-load form of the same function
+inline uint64_t bd_ident_hash(const uint8_t *msp, uint32_t ml, const uint8_t *idb, uint32_t il) {
+  uint64_t h = bd_ident_hash_msp(msp, ml, il);
+  const uint32_t T = il < BD_HASH_TAIL ? il : BD_HASH_TAIL, s = il - T;
+  for (uint32_t j = 0; 4 * j < T; j++) {
+    uint32_t w = 0;
+    for (uint32_t b = 0; b < 4 && 4 * j + b < T; b++) w |= (uint32_t)idb[s + 4 * j + b] << (8 * b);
+    h = bd_mix(h, w);
   }
-  return bd_mix(h, w ^ 0x5A);
+  return bd_mix(h, 0x5A);
 }

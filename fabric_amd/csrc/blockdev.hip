@@ -618,59 +618,101 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
 }
 
 // ============================================================ k_bd_ident
-// One thread per (tx, occurrence): occurrence 0 = creator, 1..nend = endorsers.
+// ID_LANES lanes per (tx, occurrence): occurrence 0 = creator, 1..nend = endorsers.
 // Channel::lookup restated: decode SerializedIdentity (mspid UTF-8), hash, probe, exact compare.
+// The compare is split over the group's lanes a 32-bit word at a time (block bytes at any
+// alignment via v_alignbyte; registry fields are 4-byte aligned), then one ballot.
+#define ID_LANES 16u
+DEV uint32_t ldu32(const uint8_t *p) {  // unaligned little-endian word (reads the next word too)
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
+}
+DEV uint32_t tail_mask(uint32_t n, uint32_t j) {  // bytes of word j inside [0, n)
+  const uint32_t r = n - 4u * j;
+  return r >= 4u ? 0xFFFFFFFFu : ((1u << (8u * r)) - 1u);
+}
+DEV uint64_t ident_hash_dev(S msp, S idb) {  // == bd_ident_hash (blockdev.h), word loads
+  uint64_t h = bd_ident_hash_msp(msp.p, msp.n, idb.n);
+  const uint32_t T = idb.n < BD_HASH_TAIL ? idb.n : BD_HASH_TAIL;
+  const uint8_t *s = idb.p + (idb.n - T);
+  for (uint32_t j = 0; 4u * j < T; j++) h = bd_mix(h, ldu32(s + 4u * j) & tail_mask(T, j));
+  return bd_mix(h, 0x5A);
+}
+// every lane of the group calls this with the same spans; `b` is 4-byte aligned
+DEV bool group_eq(S a, S b, uint32_t l) {
+  if (a.n != b.n) return false;
+  uint32_t diff = 0;
+  const uint32_t *bw = reinterpret_cast<const uint32_t *>(b.p);
+  for (uint32_t j = l; 4u * j < a.n; j += ID_LANES) diff |= (ldu32(a.p + 4u * j) ^ bw[j]) & tail_mask(a.n, j);
+  const uint64_t bal = __ballot(diff != 0u);
+  const uint32_t lane = threadIdx.x & 63u;
+  return ((bal >> (lane & ~(ID_LANES - 1u))) & ((1ull << ID_LANES) - 1ull)) == 0ull;
+}
 __global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__restrict__ txs,
                                                   const uint64_t *__restrict__ bases, DevChannel ch,
                                                   int32_t *__restrict__ ident) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t t = g / BD_OCC, k = g % BD_OCC;
-  if (t >= ntx) return;
+  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / ID_LANES;  // one group per tx
+  const uint32_t l = threadIdx.x % ID_LANES;
+  if (t >= ntx) return;  // whole groups exit together
   const DevTx &R = txs[t];
-  int32_t res = -1;
-  DSpan sp{0, 0};
-  bool want;
-  if (k == 0) {
-    // needed when the parse got past the channel check (pre still pending)
-    want = R.pre == C_PENDING && R.creator.len;
-    sp = R.creator;
-  } else {
-    want = k <= R.nend;
-    if (want) sp = R.end_ser[k - 1];
-  }
-  if (want && ch.nident) {
-    const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
-    VSerializedIdentity sid;
-    bool ovf = false;
-    if (decode(absl(base, sp), sid, ovf)) {
-      const uint64_t h = bd_ident_hash(sid.mspid.p, sid.mspid.n, sid.id_bytes.p, sid.id_bytes.n);
-      for (uint32_t pos = (uint32_t)h & ch.ident_mask;; pos = (pos + 1) & ch.ident_mask) {
-        const uint32_t e = ch.ident_table[pos];
-        if (e == 0) break;
-        const uint32_t i = e - 1;
-        if (ch.ident_hash[i] != h) continue;
-        const DevIdent &I = ch.idents[i];
-        if (s_eq(sid.mspid, S{ch.ident_bytes + I.msp_off, I.msp_len}) &&
-            s_eq(sid.id_bytes, S{ch.ident_bytes + I.idb_off, I.idb_len})) {
-          res = (int32_t)i;
-          break;
+  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
+  const uint32_t nend = R.nend;
+  for (uint32_t k = 0; k <= nend; k++) {
+    int32_t res = -1;
+    // the creator is needed when the parse got past the channel check (pre still pending)
+    const DSpan sp = k == 0 ? R.creator : R.end_ser[k - 1];
+    const bool want = k == 0 ? (R.pre == C_PENDING && sp.len != 0) : true;
+    if (want && ch.nident) {
+      VSerializedIdentity sid;
+      bool ovf = false;
+      if (decode(absl(base, sp), sid, ovf)) {
+        const uint64_t h = ident_hash_dev(sid.mspid, sid.id_bytes);
+        for (uint32_t pos = (uint32_t)h & ch.ident_mask;; pos = (pos + 1) & ch.ident_mask) {
+          const uint32_t e = ch.ident_table[pos];
+          if (e == 0) break;
+          const uint32_t i = e - 1;
+          if (ch.ident_hash[i] != h) continue;
+          const DevIdent &I = ch.idents[i];
+          if (group_eq(sid.mspid, S{ch.ident_bytes + I.msp_off, I.msp_len}, l) &&
+              group_eq(sid.id_bytes, S{ch.ident_bytes + I.idb_off, I.idb_len}, l)) {
+            res = (int32_t)i;
+            break;
+          }
         }
       }
     }
+    if (l == 0) ident[(size_t)t * BD_OCC + k] = res;
   }
-  if (k == 0 || k <= R.nend) ident[(size_t)t * BD_OCC + k] = res;
 }
 
 // ============================================================ k_bd_count
 // creator decision (msgvalidation.go:26-64: deserialize, Validate, then Verify) + count_jobs
+DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx &J);
+// Job slots are claimed with one atomicAdd per wave and kind (wave-inclusive scan by
+// shuffles): slots of a kind stay grouped, their order across waves is the atomics' order.
 __global__ __launch_bounds__(256) void k_bd_count(uint32_t ntx, DevTx *__restrict__ txs, DevChannel ch,
-                                                  const int32_t *__restrict__ ident, DevJobIdx *__restrict__ jobs) {
+                                                  const int32_t *__restrict__ ident, DevJobIdx *__restrict__ jobs,
+                                                  uint32_t *__restrict__ totals) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntx) return;
-  DevTx &R = txs[t];
-  const int32_t *id = ident + (size_t)t * BD_OCC;
   DevJobIdx J;
   for (int q = 0; q < BJ_KINDS; q++) J.cnt[q] = J.base[q] = 0;
+  if (t < ntx) count_jobs(txs[t], ch, ident + (size_t)t * BD_OCC, J);
+  const uint32_t lane = threadIdx.x & 63u;
+  for (int q = 0; q < BJ_KINDS; q++) {
+    uint32_t v = J.cnt[q];
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)v, d);
+      if (lane >= d) v += o;
+    }
+    uint32_t b = 0;
+    if (lane == 63u && v) b = atomicAdd(&totals[q], v);
+    b = (uint32_t)__shfl((int)b, 63);
+    J.base[q] = b + v - J.cnt[q];
+  }
+  if (t < ntx) jobs[t] = J;
+}
+DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx &J) {
   if (R.pre == C_PENDING) {
     const int32_t ci = id[0];
     if (ci < 0 || !ch.idents[ci].valid || ch.idents[ci].key_slot < 0) R.pre = C_BAD_CREATOR;
@@ -693,41 +735,6 @@ __global__ __launch_bounds__(256) void k_bd_count(uint32_t ntx, DevTx *__restric
       }
     }
   }
-  jobs[t] = J;
-}
-
-// ============================================================ k_bd_scan
-// single workgroup exclusive scan of the five job counts over all transactions
-#define SCAN_T 1024
-__global__ __launch_bounds__(SCAN_T) void k_bd_scan(uint32_t ntx, DevJobIdx *__restrict__ jobs,
-                                                    uint32_t *__restrict__ totals) {
-  __shared__ uint32_t part[BJ_KINDS][SCAN_T];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t chunk = (ntx + SCAN_T - 1) / SCAN_T;
-  const uint32_t lo = tid * chunk, hi = min(ntx, lo + chunk);
-  uint32_t sum[BJ_KINDS] = {0, 0, 0, 0, 0};
-  for (uint32_t i = lo; i < hi; i++)
-    for (int q = 0; q < BJ_KINDS; q++) sum[q] += jobs[i].cnt[q];
-  for (int q = 0; q < BJ_KINDS; q++) part[q][tid] = sum[q];
-  __syncthreads();
-  for (uint32_t off = 1; off < SCAN_T; off <<= 1) {  // Hillis-Steele inclusive scan
-    uint32_t v[BJ_KINDS];
-    for (int q = 0; q < BJ_KINDS; q++) v[q] = tid >= off ? part[q][tid - off] : 0u;
-    __syncthreads();
-    for (int q = 0; q < BJ_KINDS; q++) part[q][tid] += v[q];
-    __syncthreads();
-  }
-  uint32_t run[BJ_KINDS];
-  for (int q = 0; q < BJ_KINDS; q++) run[q] = part[q][tid] - sum[q];
-  for (uint32_t i = lo; i < hi; i++) {
-    DevJobIdx &J = jobs[i];
-    for (int q = 0; q < BJ_KINDS; q++) {
-      J.base[q] = run[q];
-      run[q] += J.cnt[q];
-    }
-  }
-  if (tid == SCAN_T - 1)
-    for (int q = 0; q < BJ_KINDS; q++) totals[q] = part[q][tid];
 }
 
 // ============================================================ k_bd_emit

@@ -881,12 +881,15 @@ static int build_dev_image(fgv_block_state *S) {
   for (size_t i = 0; i < ch.idents.size(); i++) {
     const Ident &I = ch.idents[i];
     DevIdent &d = idents[i];
+    // both fields start 4-byte aligned (k_bd_ident compares them a word at a time)
     d.msp_off = (uint32_t)ib.size();
     d.msp_len = (uint32_t)I.mspid.size();
     ib.insert(ib.end(), I.mspid.begin(), I.mspid.end());
+    ib.resize((ib.size() + 3) & ~(size_t)3, 0);
     d.idb_off = (uint32_t)ib.size();
     d.idb_len = (uint32_t)I.id_bytes.size();
     ib.insert(ib.end(), I.id_bytes.begin(), I.id_bytes.end());
+    ib.resize((ib.size() + 3) & ~(size_t)3, 0);
     d.key_slot = I.key_slot;
     d.msp = I.msp;
     d.canon = I.canon;
@@ -894,6 +897,7 @@ static int build_dev_image(fgv_block_state *S) {
     ih[i] = bd_ident_hash(reinterpret_cast<const uint8_t *>(I.mspid.data()), d.msp_len,
                           reinterpret_cast<const uint8_t *>(I.id_bytes.data()), d.idb_len);
   }
+  ib.resize(ib.size() + 64, 0);  // word loads may read past the last field
   size_t icap = 16;
   while (icap < 2 * ch.idents.size()) icap <<= 1;
   std::vector<uint32_t> itable(icap, 0);
@@ -994,8 +998,8 @@ static int build_dev_image(fgv_block_state *S) {
 __global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, DevChannel ch, DevTx *out,
                            uint32_t *flags);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
-__global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs);
-__global__ void k_bd_scan(uint32_t ntx, DevJobIdx *jobs, uint32_t *totals);
+__global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
+                           uint32_t *totals);
 __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
                           const DevJobIdx *jobs, const uint32_t *totals, ShaJob *sha, uint64_t *sig_ptr,
                           uint32_t *sig_len, uint32_t *key_slot, uint32_t *dig_idx, unsigned long long *nblk);
@@ -1069,10 +1073,9 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   const uint64_t *dbs = c->bd_bases.as<uint64_t>();
   hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, st, N, c->bd_env.as<uint32_t>(), dbs, ch, dtx,
                      misc + 5);
-  const uint64_t nocc = (uint64_t)N * BD_OCC;
-  hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)((nocc + 255) / 256)), dim3(256), 0, st, N, dtx, dbs, ch, did);
-  hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, ch, did, dj);
-  hipLaunchKernelGGL(k_bd_scan, dim3(1), dim3(1024), 0, st, N, dj, misc);
+  hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 + 255) / 256)), dim3(256), 0, st, N, dtx, dbs, ch,
+                     did);
+  hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, ch, did, dj, misc);
   HIP_TRY(hipGetLastError());
   uint32_t *hm = c->hb_misc.as<uint32_t>();
   HIP_TRY(hipMemcpyAsync(hm, misc, 32, hipMemcpyDeviceToHost, st));
