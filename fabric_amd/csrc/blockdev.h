@@ -25,6 +25,15 @@
 #define BD_MAX_GROUP 32    // nesting of unknown START_GROUP fields
 #define BD_MAX_PNODE 64    // policy tree nodes evaluated per policy (stack depth 16)
 #define BD_OCC (1 + BD_MAX_END)  // identity occurrences per tx: creator + endorsers
+// k_bd_sha digest slots per tx: payload, endorsements 0..BD_MAX_END-1, txid, proposal, index
+#define BD_DIG_T (1 + BD_MAX_END)
+#define BD_DIG_P (2 + BD_MAX_END)
+#define BD_DIG_I (3 + BD_MAX_END)
+#define BD_DIG_SLOTS (4 + BD_MAX_END)
+#define SHA_E_LANES 4u  // k_bd_sha lanes per tx for endorsement messages (grid: SHA_E_LANES + 3 rows)
+// host -> device envelope table, per tx: block, envelope offset, length, Envelope.payload
+// offset, length (0xFFFFFFFF: the envelope does not decode)
+#define BD_ENV_WORDS 5
 
 struct DSpan {  // bytes [off, off+len) of block `DevTx::blk`; len 0 == nil
   uint32_t off, len;

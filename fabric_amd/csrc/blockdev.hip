@@ -18,6 +18,7 @@
 #include "../../include/fgv.h"
 #include "blockdev.h"
 #include "fgv_kernels.h"
+#include "sha256_dev.h"
 
 namespace {
 
@@ -474,11 +475,13 @@ DEV int cc_lookup(const DevChannel &ch, S ns) {
 __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                  const uint64_t *__restrict__ bases, DevChannel ch,
                                                  DevTx *__restrict__ out, uint32_t *__restrict__ flags) {
+  __builtin_amdgcn_s_setprio(3);  // shares the SIMDs with k_bd_sha_payload
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
-  const uint32_t blk = envtab[3 * t];
+  const uint32_t *et = envtab + BD_ENV_WORDS * t;
+  const uint32_t blk = et[0];
   const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
-  const S d{base + envtab[3 * t + 1], envtab[3 * t + 2]};
+  const S d{base + et[1], et[2]};
   DevTx R;
   R.blk = blk;
   R.pre = C_PENDING;
@@ -495,6 +498,9 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
   do {
     VTwoBytes env;
     if (!decode(d, env, ovf)) { R.pre = C_OTHER; break; }
+    // k_bd_sha_payload hashed the host's Envelope.payload span: it must be this one (same
+    // protobuf rules on both sides; a disagreement sends the batch to the host parser)
+    if (env.a.n != et[4] || (env.a.n && env.a.p != base + et[3])) { ovf = true; break; }
     VPayload pl;
     if (!decode(env.a, pl, ovf)) { R.pre = C_BAD_PAYLOAD; break; }
     const VTwoBytes &hdr = pl.hdr;
@@ -652,6 +658,7 @@ DEV bool group_eq(S a, S b, uint32_t l) {
 __global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__restrict__ txs,
                                                   const uint64_t *__restrict__ bases, DevChannel ch,
                                                   int32_t *__restrict__ ident) {
+  __builtin_amdgcn_s_setprio(3);  // latency-critical chain; k_bd_sha fills the SIMDs beside it
   const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / ID_LANES;  // one group per tx
   const uint32_t l = threadIdx.x % ID_LANES;
   if (t >= ntx) return;  // whole groups exit together
@@ -694,6 +701,7 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
 __global__ __launch_bounds__(256) void k_bd_count(uint32_t ntx, DevTx *__restrict__ txs, DevChannel ch,
                                                   const int32_t *__restrict__ ident, DevJobIdx *__restrict__ jobs,
                                                   uint32_t *__restrict__ totals) {
+  __builtin_amdgcn_s_setprio(3);  // latency-critical chain; k_bd_sha fills the SIMDs beside it
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   DevJobIdx J;
   for (int q = 0; q < BJ_KINDS; q++) J.cnt[q] = J.base[q] = 0;
@@ -737,6 +745,99 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
   }
 }
 
+// ============================================================ k_bd_sha_payload
+// SHA-256(Envelope.payload) of every envelope -- the creator signature's digest
+// (msgvalidation.go:26-64 -> msp/identities.go:179), digest slot 0 -- launched on the second
+// stream BEFORE the parse, from the payload spans the host's block split found (k_bd_parse
+// checks they match its own).  Each is its transaction's longest message (~80 compressions
+// for C2): these serial chains set the SHA-256 stage, so they start first.
+__global__ __launch_bounds__(64) void k_bd_sha_payload(uint32_t ntx, const uint32_t *__restrict__ envtab,
+                                                       const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                                       unsigned long long *__restrict__ nblk) {
+  __builtin_amdgcn_s_setprio(2);
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t blocks = 0;
+  if (t < ntx) {
+    const uint32_t *et = envtab + BD_ENV_WORDS * t;
+    if (et[4] != 0xFFFFFFFFu) {
+      JobView v;
+      v.p[0] = v.p[1] = v.p[2] = reinterpret_cast<const uint8_t *>(bases[et[0]]) + et[3];
+      v.beg[0] = 0;
+      v.beg[1] = v.beg[2] = v.beg[3] = v.L = et[4];
+      sha_view(v, dig + (size_t)t * 32);
+      blocks = (v.L + 8) / 64 + 1;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
+  if ((threadIdx.x & 63) == 0 && blocks) atomicAdd(nblk, (unsigned long long)blocks);
+}
+
+// ============================================================ k_bd_sha
+// Every SHA-256 message of the batch, hashed speculatively right after the parse on the
+// second stream (beside identity resolution, the job counts and the verify-job assembly):
+// all of them are spans the parse already found; only WHETHER a digest is consumed is decided
+// later (a hash is pure, so a superset of the consumed ones is hashed).  Digest slots
+// (BD_DIG_SLOTS x ntx, slot-major):
+//   0                      SHA-256(e.Payload): creator signature digest (msgvalidation.go:26-64)
+//   1 + k (k < BD_MAX_END) SHA-256(prp || endorser_k) (statebased/validator_keylevel.go:246-260)
+//   BD_DIG_T               SHA-256(nonce || creator): TxID (protoutil/proputils.go:351-360)
+//   BD_DIG_P               SHA-256(chdr || shdr || ccpp): proposal hash (protoutil/txutils.go:449-466)
+//   BD_DIG_I               SHA-256(nonce || creator) of the txid index entry (txutils.go:503-534)
+// Lanes run slot-major, so the payloads -- each transaction's longest message (~80
+// compressions for C2), whose serial chain sets the stage -- are dispatched first; then
+// SHA_E_LANES lanes per transaction for its endorsements (lane j: endorsements j, j + SHA_E_LANES, ...),
+// then txid / proposal / index.  (k_bd_count may turn a pending creator into code 4
+// meanwhile; those digests go unused.)
+__global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__restrict__ txs,
+                                               const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                               unsigned long long *__restrict__ nblk) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t row = l / ntx, t = l - row * ntx;  // rows: E x SHA_E_LANES | T | P | I
+  uint64_t blocks = 0;
+  auto hash = [&](const DevTx &R, uint32_t s, DSpan a, DSpan b, DSpan c) {
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
+    JobView v;
+    v.p[0] = base + a.off;
+    v.p[1] = base + b.off;
+    v.p[2] = base + c.off;
+    v.beg[0] = 0;
+    v.beg[1] = a.len;
+    v.beg[2] = a.len + b.len;
+    v.beg[3] = v.L = a.len + b.len + c.len;
+    sha_view(v, dig + ((size_t)s * ntx + t) * 32);
+    blocks += (v.L + 8) / 64 + 1;
+  };
+  if (row < SHA_E_LANES) {
+    const DevTx &R = txs[t];
+    if (R.pre == C_PENDING && R.type == 3 && R.etx == C_VALID && R.disp == C_VALID)
+      for (uint32_t k = row; k < R.nend; k += SHA_E_LANES) hash(R, 1 + k, R.prp, R.end_ser[k], DSpan{0, 0});
+  } else if (row < SHA_E_LANES + 3) {
+    const uint32_t s = row - SHA_E_LANES + BD_DIG_T;  // BD_DIG_T, BD_DIG_P, BD_DIG_I
+    const DevTx &R = txs[t];
+    const DSpan z{0, 0};
+    DSpan a = z, b = z, c = z;
+    const bool live = R.pre == C_PENDING;
+    bool want;
+    if (s == BD_DIG_T) {
+      want = live && R.type == 3;
+      a = R.nonce;
+      b = R.creator;
+    } else if (s == BD_DIG_P) {
+      want = live && R.type == 3 && R.etx == C_VALID;
+      a = R.chdr;
+      b = R.act_hdr;
+      c = R.ccpp;
+    } else {
+      want = (R.flags & BDF_INDEX_OK) && !(R.flags & BDF_INDEX_FROM_TXID);
+      a = R.idx_nonce;
+      b = R.idx_creator;
+    }
+    if (want) hash(R, s, a, b, c);
+  }
+  for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
+  if ((threadIdx.x & 63) == 0 && blocks) atomicAdd(nblk, (unsigned long long)blocks);
+}
+
 // ============================================================ k_bd_emit
 // the assembly loop: SHA-256 jobs grouped by kind [creator payload | nonce||creator |
 // chdr||shdr||ccpp | prp||endorser | index txid], verify jobs [creators | endorsements]
@@ -744,58 +845,33 @@ __global__ __launch_bounds__(256) void k_bd_emit(uint32_t ntx, const DevTx *__re
                                                  const uint64_t *__restrict__ bases, DevChannel ch,
                                                  const int32_t *__restrict__ ident,
                                                  const DevJobIdx *__restrict__ jobs,
-                                                 const uint32_t *__restrict__ totals, ShaJob *__restrict__ sha,
+                                                 const uint32_t *__restrict__ totals,
                                                  uint64_t *__restrict__ sig_ptr, uint32_t *__restrict__ sig_len,
-                                                 uint32_t *__restrict__ key_slot, uint32_t *__restrict__ dig_idx,
-                                                 unsigned long long *__restrict__ nblk) {
+                                                 uint32_t *__restrict__ key_slot, uint32_t *__restrict__ dig_idx) {
+  __builtin_amdgcn_s_setprio(3);  // latency-critical chain; k_bd_sha fills the SIMDs beside it
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t blocks = 0;
-  if (t < ntx) {
-    const DevTx &R = txs[t];
-    const DevJobIdx &J = jobs[t];
-    const int32_t *id = ident + (size_t)t * BD_OCC;
-    const uint64_t base = bases[R.blk];
-    const uint32_t k0 = 0, k1 = totals[0], k2 = k1 + totals[1], k3 = k2 + totals[2], k4 = k3 + totals[3];
-    auto addr = [&](DSpan s) -> uint64_t { return s.len ? base + s.off : 0ull; };
-    auto job = [&](uint32_t idx, DSpan a, DSpan b, DSpan c) {
-      ShaJob j;
-      j.p[0] = addr(a); j.n[0] = a.len;
-      j.p[1] = addr(b); j.n[1] = b.len;
-      j.p[2] = addr(c); j.n[2] = c.len;
-      j.pad = 0;
-      sha[idx] = j;
-      blocks += (a.len + b.len + c.len + 8) / 64 + 1;
-    };
-    auto verify = [&](uint32_t vi, DSpan sig, int32_t slot, uint32_t dig) {
-      sig_ptr[vi] = addr(sig);
-      sig_len[vi] = sig.len;
-      key_slot[vi] = (uint32_t)slot;
-      dig_idx[vi] = dig;
-    };
-    const DSpan z{0, 0};
-    if (J.cnt[BJ_C]) {
-      const uint32_t cj = k0 + J.base[BJ_C];
-      job(cj, R.payload, z, z);
-      verify(J.base[BJ_C], R.env_sig, ch.idents[id[0]].key_slot, cj);
+  if (t >= ntx) return;
+  const DevTx &R = txs[t];
+  const DevJobIdx &J = jobs[t];
+  const int32_t *id = ident + (size_t)t * BD_OCC;
+  const uint64_t base = bases[R.blk];
+  auto verify = [&](uint32_t vi, DSpan sig, int32_t slot, uint32_t dig) {
+    sig_ptr[vi] = sig.len ? base + sig.off : 0ull;
+    sig_len[vi] = sig.len;
+    key_slot[vi] = (uint32_t)slot;
+    dig_idx[vi] = dig;
+  };
+  // verify jobs [creators | endorsements]; digests are k_bd_sha's slots
+  if (J.cnt[BJ_C]) verify(J.base[BJ_C], R.env_sig, ch.idents[id[0]].key_slot, t);
+  if (J.cnt[BJ_E]) {
+    uint32_t r = 0;
+    for (uint32_t k = 0; k < R.nend && r < J.cnt[BJ_E]; k++) {
+      const int32_t e = id[1 + k];
+      if (e < 0 || ch.idents[e].key_slot < 0) continue;
+      verify(totals[BJ_C] + J.base[BJ_E] + r, R.end_sig[k], ch.idents[e].key_slot, (1 + k) * ntx + t);
+      r++;
     }
-    if (J.cnt[BJ_T]) job(k1 + J.base[BJ_T], R.nonce, R.creator, z);
-    if (J.cnt[BJ_P]) job(k2 + J.base[BJ_P], R.chdr, R.act_hdr, R.ccpp);
-    if (J.cnt[BJ_E]) {
-      uint32_t r = 0;
-      for (uint32_t k = 0; k < R.nend && r < J.cnt[BJ_E]; k++) {
-        const int32_t e = id[1 + k];
-        if (e < 0 || ch.idents[e].key_slot < 0) continue;
-        const uint32_t hj = k3 + J.base[BJ_E] + r;
-        job(hj, R.prp, R.end_ser[k], z);
-        verify(totals[0] + J.base[BJ_E] + r, R.end_sig[k], ch.idents[e].key_slot, hj);
-        r++;
-      }
-    }
-    if (J.cnt[BJ_I]) job(k4 + J.base[BJ_I], R.idx_nonce, R.idx_creator, z);
   }
-  // one atomic per wave
-  for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
-  if ((threadIdx.x & 63) == 0 && blocks) atomicAdd(nblk, (unsigned long long)blocks);
 }
 
 // ============================================================ k_bd_fold
@@ -907,7 +983,8 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
   const DevJobIdx &J = jobs[t];
   const int32_t *id = ident + (size_t)t * BD_OCC;
   const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
-  const uint32_t k1 = totals[0], k2 = k1 + totals[1], k3 = k2 + totals[2], k4 = k3 + totals[3];
+  // digests: k_bd_sha's slots
+  const size_t kT = (size_t)BD_DIG_T * ntx + t, kP = (size_t)BD_DIG_P * ntx + t, kI = (size_t)BD_DIG_I * ntx + t;
   auto hexd = [](uint32_t v) -> uint8_t { return (uint8_t)(v < 10 ? '0' + v : 'a' + v - 10); };
   uint8_t code;
   bool reached = false;
@@ -921,7 +998,7 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
   } else if (R.type == 2) {
     code = C_UNSUP_PAYLOAD;
   } else {
-    txd = digests + (size_t)(k1 + J.base[BJ_T]) * 32;
+    txd = digests + kT * 32;
     const S txid = absl(base, R.txid);
     bool ok = txid.n == 64;
     for (int k = 0; ok && k < 32; k++)
@@ -932,7 +1009,7 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
       code = R.etx;
     } else {
       const S ph = absl(base, R.prop_hash);
-      const uint8_t *pd = digests + (size_t)(k2 + J.base[BJ_P]) * 32;
+      const uint8_t *pd = digests + kP * 32;
       bool same = ph.n == 32;
       for (int k = 0; same && k < 32; k++) same = ph.p[k] == pd[k];
       if (!same) {
@@ -995,7 +1072,7 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
   }
   if (R.flags & BDF_INDEX_OK) {
     if (!(R.flags & BDF_INDEX_FROM_TXID)) {
-      const uint8_t *d = digests + (size_t)(k4 + J.base[BJ_I]) * 32;
+      const uint8_t *d = digests + kI * 32;
       for (int k = 0; k < 32; k++) o.index_txid[k] = d[k];
       o.flags |= FGV_TXR_INDEXED;
     } else if (hex32(absl(base, R.index_txid), o.index_txid)) {

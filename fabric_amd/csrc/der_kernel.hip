@@ -17,6 +17,7 @@ __global__ __launch_bounds__(256) void k_der(const uint8_t *__restrict__ sig_buf
                                              uint8_t *__restrict__ status,
                                              uint32_t *__restrict__ r_limbs,
                                              uint32_t *__restrict__ s_limbs) {
+  __builtin_amdgcn_s_setprio(3);  // on the verify chain; SHA-256 may be running beside it
   __shared__ uint32_t stage[256 * DER_STAGE_DW];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -1000,9 +1000,12 @@ __global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t 
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
+__global__ void k_bd_sha(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
+__global__ void k_bd_sha_payload(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, uint8_t *dig,
+                                 unsigned long long *nblk);
 __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
-                          const DevJobIdx *jobs, const uint32_t *totals, ShaJob *sha, uint64_t *sig_ptr,
-                          uint32_t *sig_len, uint32_t *key_slot, uint32_t *dig_idx, unsigned long long *nblk);
+                          const DevJobIdx *jobs, const uint32_t *totals, uint64_t *sig_ptr, uint32_t *sig_len,
+                          uint32_t *key_slot, uint32_t *dig_idx);
 __global__ void k_bd_fold(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
                           const DevJobIdx *jobs, const uint32_t *totals, const uint8_t *digests,
                           const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags);
@@ -1043,8 +1046,8 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   c->n_sha_jobs = c->n_sha_blocks = c->n_verifies = 0;
   if (total == 0) return FGV_OK;
   const uint32_t N = (uint32_t)total;
-  if (!c->hb_env.ensure(total * 12) || !c->hb_bases.ensure(nblocks * 8) || !c->hb_misc.ensure(64) ||
-      !c->bd_env.ensure(total * 12) || !c->bd_bases.ensure(nblocks * 8) || !c->bd_misc.ensure(64) ||
+  if (!c->hb_env.ensure(total * 4 * BD_ENV_WORDS) || !c->hb_bases.ensure(nblocks * 8) || !c->hb_misc.ensure(64) ||
+      !c->bd_env.ensure(total * 4 * BD_ENV_WORDS) || !c->bd_bases.ensure(nblocks * 8) || !c->bd_misc.ensure(64) ||
       !c->bd_tx.ensure(total * sizeof(DevTx)) || !c->bd_ident.ensure(total * BD_OCC * 4) ||
       !c->bd_jobs.ensure(total * sizeof(DevJobIdx)))
     return FGV_ENOMEM;
@@ -1052,18 +1055,27 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   uint64_t *bs = c->hb_bases.as<uint64_t>();
   S->pool.run(nblocks, [&](size_t b) {
     bs[b] = (uint64_t)(uintptr_t)d_blocks[b];
-    uint32_t *o = et + 3 * first[b];
-    for (uint32_t i = lo[b]; i < hi[b]; i++, o += 3) {
+    uint32_t *o = et + BD_ENV_WORDS * first[b];
+    for (uint32_t i = lo[b]; i < hi[b]; i++, o += BD_ENV_WORDS) {
       o[0] = (uint32_t)b;
       o[1] = (uint32_t)(envs[b][i].p - h_blocks[b]);
       o[2] = envs[b][i].n;
+      // Envelope.payload (k_bd_sha_payload hashes it before the device parse)
+      VEnvelope env;
+      if (pbw::decode(envs[b][i].p, envs[b][i].n, env)) {
+        o[3] = env.payload.n ? (uint32_t)(env.payload.p - h_blocks[b]) : 0u;
+        o[4] = (uint32_t)env.payload.n;
+      } else {
+        o[3] = 0;
+        o[4] = 0xFFFFFFFFu;
+      }
     }
   });
   c->t_host_parse = ms_since(t0);
   auto t1 = clk::now();
   hipStream_t st = c->stream;
   uint32_t *misc = c->bd_misc.as<uint32_t>();  // [0..5) totals, [5] flags, bytes 24..32 compressions
-  HIP_TRY(hipMemcpyAsync(c->bd_env.p, et, total * 12, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(c->bd_env.p, et, total * 4 * BD_ENV_WORDS, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(c->bd_bases.p, bs, nblocks * 8, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(misc, 0, 64, st));
   const DevChannel ch = S->dimg.ch;
@@ -1071,8 +1083,26 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   int32_t *did = c->bd_ident.as<int32_t>();
   DevJobIdx *dj = c->bd_jobs.as<DevJobIdx>();
   const uint64_t *dbs = c->bd_bases.as<uint64_t>();
+  // k_bd_sha digest slots (blockdev.h): BD_DIG_SLOTS per tx, slot-major
+  if (!c->bj_dig.ensure((size_t)N * 32 * BD_DIG_SLOTS + 64)) return FGV_ENOMEM;
+  unsigned long long *nblk = reinterpret_cast<unsigned long long *>(misc + 6);
+  // the payload hashes (the longest serial chains) start with the parse, on the second stream
+  HIP_TRY(hipEventRecord(c->ev_pay[0], st));
+  HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_pay[0], 0));
+  hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(64), 0, c->stream2, N, c->bd_env.as<uint32_t>(), dbs,
+                     c->bj_dig.as<uint8_t>(), nblk);
   hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, st, N, c->bd_env.as<uint32_t>(), dbs, ch, dtx,
                      misc + 5);
+  // every other SHA-256 message is known after the parse: hashed on the second stream while
+  // identities, job counts and verify jobs are worked out on this one
+  // (third stream: concurrent with the payload chains still running on stream2)
+  HIP_TRY(hipEventRecord(c->ev[7], st));
+  HIP_TRY(hipStreamWaitEvent(c->stream3, c->ev[7], 0));
+  hipLaunchKernelGGL(k_bd_sha, dim3((uint32_t)(((uint64_t)N * (SHA_E_LANES + 3) + 63) / 64)), dim3(64), 0, c->stream3, N,
+                     dtx, dbs, c->bj_dig.as<uint8_t>(), nblk);
+  HIP_TRY(hipEventRecord(c->ev_pay[2], c->stream3));
+  HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_pay[2], 0));
+  HIP_TRY(hipEventRecord(c->ev_pay[1], c->stream2));  // every digest is ready
   hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 + 255) / 256)), dim3(256), 0, st, N, dtx, dbs, ch,
                      did);
   hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, ch, did, dj, misc);
@@ -1081,27 +1111,31 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   HIP_TRY(hipMemcpyAsync(hm, misc, 32, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (hm[5] & 1u) return 1;  // capacity overflow: host parser
-  const size_t nj = (size_t)hm[0] + hm[1] + hm[2] + hm[3] + hm[4], nv = (size_t)hm[0] + hm[3];
+  const size_t nv = (size_t)hm[BJ_C] + hm[BJ_E];
   c->t_bd_pre = ms_since(t1);
   c->t_host_assemble = c->t_bd_pre;
   auto t2 = clk::now();
-  if (!c->bj_jobs.ensure(nj * sizeof(ShaJob) + 64) || !c->bj_sigp.ensure(nv * 20 + 64) ||
-      !c->bj_dig.ensure(nj * 32 + 64) || !c->bj_vst.ensure(nv + 64))
-    return FGV_ENOMEM;
+  if (!c->bj_sigp.ensure(nv * 20 + 64) || !c->bj_vst.ensure(nv + 64)) return FGV_ENOMEM;
   uint8_t *sp = c->bj_sigp.as<uint8_t>();
-  unsigned long long *nblk = reinterpret_cast<unsigned long long *>(misc + 6);
   hipLaunchKernelGGL(k_bd_emit, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
-                     c->bj_jobs.as<ShaJob>(), reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + nv * 8),
-                     reinterpret_cast<uint32_t *>(sp + nv * 12), reinterpret_cast<uint32_t *>(sp + nv * 16), nblk);
+                     reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + nv * 8),
+                     reinterpret_cast<uint32_t *>(sp + nv * 12), reinterpret_cast<uint32_t *>(sp + nv * 16));
   HIP_TRY(hipGetLastError());
-  int rc = fgv_run_block_jobs_device(c, nj, nv, 0);
+  c->digests_ready = c->ev_pay[1];
+  int rc = fgv_run_block_jobs_device(c, 0, nv, 0);
+  c->digests_ready = nullptr;
   if (rc) return rc;
+  HIP_TRY(hipStreamWaitEvent(st, c->ev_pay[1], 0));  // joined even when there is nothing to verify
   hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
                      c->bj_dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(hm, misc, 32, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   fgv_read_block_job_times(c);
+  {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev_pay[0], c->ev_pay[1]) == hipSuccess) c->t_sha += ms;
+  }
   uint64_t nb;
   memcpy(&nb, hm + 6, 8);
   c->n_sha_blocks = nb;

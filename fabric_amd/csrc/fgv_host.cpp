@@ -32,7 +32,7 @@ static const uint8_t GY[32] = {0x4f, 0xe3, 0x42, 0xe2, 0xfe, 0x1a, 0x7f, 0x9b, 0
 
 // Build tables for `nk` keys (qxy: nk*16 limbs) into `tables` at `slots`.
 static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slots, uint32_t nk,
-                        apoint_raw *tables, uint8_t *ok) {
+                        apoint_raw *tables, apoint_raw *tables28, uint8_t *ok) {
   if (!c->kt_q.ensure((size_t)nk * 64) || !c->kt_slot.ensure((size_t)nk * 4) ||
       !c->kt_scratch.ensure((size_t)nk * KT_ENTRIES * sizeof(jpoint_raw)))
     return FGV_ENOMEM;
@@ -40,7 +40,7 @@ static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slo
   HIP_TRY(hipMemcpyAsync(c->kt_slot.p, h_slots, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipEventRecord(c->ev[6], c->stream));
   hipLaunchKernelGGL(k_keytab, dim3(nk), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
-                     c->kt_slot.as<uint32_t>(), tables, c->kt_scratch.as<jpoint_raw>(), ok, nk);
+                     c->kt_slot.as<uint32_t>(), tables, tables28, c->kt_scratch.as<jpoint_raw>(), ok, nk);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[7], c->stream));
   return FGV_OK;
@@ -73,15 +73,27 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     return e;
   };
   if (hipSetDevice(c->device) != hipSuccess) return fail(FGV_EDEVICE);
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
-  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
+  // the main stream carries the latency-critical chain (parse -> identities -> verify jobs ->
+  // k_point) at high priority; stream2 fills the rest of the chip with SHA-256 / k_inv
+  {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+    if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi) != hipSuccess) return fail(FGV_EDEVICE);
+    if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+    if (hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+  }
   {
     std::random_device rd;  // per-context hash seed of the finalize txid table
     c->fin_seed = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)(uintptr_t)c;
   }
   for (auto &e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
+  for (auto &e : c->ev_pay)
+    if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
   if (hipFuncSetAttribute((const void *)k_point, hipFuncAttributeMaxDynamicSharedMemorySize, (int)KT_BYTES) !=
+      hipSuccess)
+    return fail(FGV_EDEVICE);
+  if (hipFuncSetAttribute((const void *)k_point28, hipFuncAttributeMaxDynamicSharedMemorySize, (int)KT_BYTES) !=
       hipSuccess)
     return fail(FGV_EDEVICE);
   {
@@ -90,14 +102,15 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
       return fail(FGV_EDEVICE);
     c->n_cu = (uint32_t)ncu;
   }
-  if (!c->gtab.ensure(KT_BYTES) || !c->g_ok.ensure(16) ||
-      !c->ktab.ensure((size_t)c->key_slots * KT_BYTES) || !c->key_ok.ensure(c->key_slots))
+  if (!c->gtab.ensure(KT_BYTES) || !c->g_ok.ensure(16) || !c->gtab28.ensure(KT_BYTES) || !c->redo.ensure(64) ||
+      !c->ktab.ensure((size_t)c->key_slots * KT_BYTES) || !c->ktab28.ensure((size_t)c->key_slots * KT_BYTES) ||
+      !c->key_ok.ensure(c->key_slots))
     return fail(FGV_ENOMEM);
   // generator table = key table of G (same kernel)
   uint32_t q[16], slot0 = 0;
   be32_to_limbs(GX, q);
   be32_to_limbs(GY, q + 8);
-  int rc = build_tables(c, q, &slot0, 1, c->gtab.as<apoint_raw>(), c->g_ok.as<uint8_t>());
+  int rc = build_tables(c, q, &slot0, 1, c->gtab.as<apoint_raw>(), c->gtab28.as<apoint_raw>(), c->g_ok.as<uint8_t>());
   if (rc) return fail(rc);
   uint8_t gok = 0;
   if (hipMemcpyAsync(&gok, c->g_ok.p, 1, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -110,7 +123,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
 void fgv_destroy(fgv_ctx *c) {
   if (!c) return;
   if (c->stream) hipStreamSynchronize(c->stream);
-  DevBuf *d[] = {&c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->kt_q, &c->kt_slot, &c->kt_scratch,
+  DevBuf *d[] = {&c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
                  &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
                  &c->bj_dig, &c->bj_vst, &c->blk_arena, &c->fz_meta, &c->fz_rowmap, &c->fz_blkof,
@@ -125,8 +138,11 @@ void fgv_destroy(fgv_ctx *c) {
   for (auto *b : h) b->release();
   for (auto &e : c->ev)
     if (e) hipEventDestroy(e);
+  for (auto &e : c->ev_pay)
+    if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
+  if (c->stream3) hipStreamDestroy(c->stream3);
   delete c;
 }
 
@@ -179,6 +195,7 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
                              const uint32_t *d_r, const uint8_t *d_dig, const uint32_t *d_dig_idx) {
   if (!c->d1.ensure((size_t)DIG_STRIDE * N)) return FGV_ENOMEM;
   HIP_TRY(hipStreamWaitEvent(c->stream, c->ev[3], 0));
+  if (c->digests_ready) HIP_TRY(hipStreamWaitEvent(c->stream, c->digests_ready, 0));  // k_bd_sha (stream2)
   HIP_TRY(hipEventRecord(c->ev[4], c->stream));
   hipLaunchKernelGGL(k_prep, dim3((N + 255) / 256), dim3(256), 0, c->stream, N, d_status, d_r,
                      c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>());
@@ -198,8 +215,21 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
   for (uint32_t l = POINT_LANES_MAX; l >= 1; l--)
     if (waves * (64 / l) >= N) { L = l; break; }
   if (forced >= 1 && forced <= POINT_LANES_MAX) L = (uint32_t)forced;
+  // k_point28 (radix-2^28, incomplete formulas) decides every item except those that hit an
+  // exceptional addition; k_point (complete formulas) then finishes those, and returns at
+  // once when k_point28 counted none.  FGV_POINT_EXACT=1 runs k_point alone (A/B knob).
+  static const bool exact_only = [] {
+    const char *e = getenv("FGV_POINT_EXACT");
+    return e && atoi(e) == 1;
+  }();
+  uint32_t *redo = exact_only ? nullptr : c->redo.as<uint32_t>();
+  if (redo) {
+    HIP_TRY(hipMemsetAsync(redo, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_point28, dim3(c->n_cu), dim3(POINT_THREADS), KT_BYTES, c->stream, N, L, d_status, d_slot,
+                       c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
+  }
   hipLaunchKernelGGL(k_point, dim3(c->n_cu), dim3(POINT_THREADS), KT_BYTES, c->stream, N, L, d_status, d_slot,
-                     c->gtab.as<apoint_raw>(), c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(), d_r);
+                     c->gtab.as<apoint_raw>(), c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   c->last_lanes = L;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[6], c->stream));
@@ -321,7 +351,8 @@ static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, 
       next++;
       j++;
     }
-    int rc = build_tables(c, kq, ks, nk, c->ktab.as<apoint_raw>(), c->key_ok.as<uint8_t>());
+    int rc = build_tables(c, kq, ks, nk, c->ktab.as<apoint_raw>(), c->ktab28.as<apoint_raw>(),
+                          c->key_ok.as<uint8_t>());
     if (rc) return rc;
     // re-resolve every pending slot (the cache may have been flushed)
     for (size_t i = 0; i < n; i++)
@@ -471,7 +502,8 @@ static int keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint3
       be32_to_limbs(fresh[j].data() + 32, kq + 16 * j + 8);
       ks[j] = next + j;
     }
-    int rc = build_tables(c, kq, ks, nk, c->ktab.as<apoint_raw>(), c->key_ok.as<uint8_t>());
+    int rc = build_tables(c, kq, ks, nk, c->ktab.as<apoint_raw>(), c->ktab28.as<apoint_raw>(),
+                          c->key_ok.as<uint8_t>());
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (uint32_t j = 0; j < nk; j++) c->key_map.emplace(fresh[j], next + j);
@@ -593,11 +625,11 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
 // Device-resident variant (blockdev path): the jobs were written by k_bd_emit straight into
 // c->bj_jobs / c->bj_sigp (layout of fgv_block_jobs_reserve); digests stay in c->bj_dig and
 // verify status in c->bj_vst.  Enqueued on c->stream; no host copies, no synchronisation.
-int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks) {
+int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, size_t dig_off) {
   c->n_sha_jobs = nj;
   c->n_verifies = nv;
   c->n_sha_blocks = sha_blocks;
-  if (nj == 0) return FGV_OK;
+  if (nj == 0 && nv == 0) return FGV_OK;
   bool ran = false;
   if (nv) {
     const uint32_t N = (uint32_t)nv;
@@ -609,15 +641,23 @@ int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blo
     hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr, d_sigp,
                        d_sigl, N, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(), c->s.as<uint32_t>());
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(c->ev[7], c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev[7], 0));
-    int rc = launch_inv(c, c->stream2, N, c->bj_vst.as<uint8_t>(), d_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>());
+    // k_inv beside the SHA-256 jobs when this call hashes (second stream); the device-parse
+    // committer's hashes already run on the second stream (k_bd_sha), so k_inv follows k_der
+    hipStream_t ist = c->stream;
+    if (nj) {
+      ist = c->stream2;
+      HIP_TRY(hipEventRecord(c->ev[7], c->stream));
+      HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev[7], 0));
+    }
+    int rc = launch_inv(c, ist, N, c->bj_vst.as<uint8_t>(), d_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>());
     if (rc) return rc;
   }
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  hipLaunchKernelGGL(k_sha256_jobs, dim3((uint32_t)((nj + 255) / 256)), dim3(256), 0, c->stream,
-                     c->bj_jobs.as<ShaJob>(), (uint32_t)nj, c->bj_dig.as<uint8_t>());
-  HIP_TRY(hipGetLastError());
+  if (nj) {  // (the device-parse committer hashes with k_bd_sha instead: nj == 0)
+    hipLaunchKernelGGL(k_sha256_jobs, dim3((uint32_t)((nj + 255) / 256)), dim3(256), 0, c->stream,
+                       c->bj_jobs.as<ShaJob>(), (uint32_t)nj, c->bj_dig.as<uint8_t>() + dig_off);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   if (nv) {
     const uint32_t N = (uint32_t)nv;

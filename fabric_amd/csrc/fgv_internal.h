@@ -92,11 +92,14 @@ struct fgv_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // k_der + k_inv of a block batch, concurrent with SHA-256
+  hipStream_t stream3 = nullptr;  // the device-parse committer's non-payload SHA-256 (k_bd_sha)
+  hipEvent_t ev_pay[3] = {};      // [0] batch start, [1] all digests ready (stream2), [2] k_bd_sha done
   hipEvent_t ev[8] = {};          // 0/1 sha, 2/3 inv, 4/5 prep, 6 point end, 7 fork
   std::mutex mu;
   // generator table (88 KB) and the public-key table cache
   DevBuf gtab, g_ok;
   DevBuf ktab, key_ok;
+  DevBuf gtab28, ktab28, redo;  // Montgomery-280 copies of the comb tables (k_point28)
   uint32_t key_slots = 0;
   uint32_t pinned = 0;  // slots [0, pinned) hold registered keys and are never evicted
   std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_map;
@@ -126,6 +129,7 @@ struct fgv_ctx {
   std::mutex integ_mu;
   // device-resident committer path (blockdev.hip)
   bool stage_ran = false;
+  hipEvent_t digests_ready = nullptr;  // k_prep waits for it when set (digests from another stream)
   DevBuf bd_env, bd_bases, bd_tx, bd_ident, bd_jobs, bd_misc;
   HostBuf hb_env, hb_bases, hb_misc;
   double t_bd_split = 0, t_bd_pre = 0, t_bd_fold = 0;
@@ -170,7 +174,7 @@ int fgv_block_jobs_reserve(fgv_ctx *c, size_t nj, size_t nv, BlockJobs *out);
 int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, const uint8_t **digests,
                        const uint8_t **vstatus);
 // device-resident variant: jobs already in c->bj_jobs / c->bj_sigp; results stay in HBM
-int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks);
+int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, size_t dig_off = 0);
 void fgv_read_block_job_times(fgv_ctx *c);
 int fgv_block_set_parse_mode(fgv_block_state *S, int mode);
 int fgv_block_parse_mode(fgv_block_state *S);

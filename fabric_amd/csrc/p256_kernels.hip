@@ -20,6 +20,7 @@
 // fabric-lib-go bccsp/sw/ecdsa.go:41-57.  Exceptional additions (P == Q, P == -Q, inf)
 // are handled exactly, so results are bit-exact for adversarial inputs as well.
 #include "p256_field.h"
+#include "p256_fe28.h"
 #include "fgv_kernels.h"
 #include "p256_modinv.h"
 
@@ -99,6 +100,7 @@ FGV_DEV void load_fe(fe &a, const uint32_t *src) {
 __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
                                                const uint32_t *__restrict__ slots,
                                                apoint_raw *__restrict__ tables,
+                                               apoint_raw *__restrict__ tables28,
                                                jpoint_raw *__restrict__ scratch,
                                                uint8_t *__restrict__ key_ok, uint32_t nkeys) {
   const uint32_t kid = blockIdx.x;
@@ -123,6 +125,7 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
 
   jpoint_raw *scr = scratch + (size_t)kid * KT_ENTRIES + (size_t)w * TAB_K;
   apoint_raw *tab = tables + (size_t)slot * KT_ENTRIES + (size_t)w * TAB_K;
+  apoint_raw *tab28 = tables28 + (size_t)slot * KT_ENTRIES + (size_t)w * TAB_K;
   // P_1 = B, P_2 = 2B, P_k = P_{k-1} + B  (k*B != +-B for 3 <= k <= 32 < n)
   jpoint pk = b;
   fe pref;
@@ -160,6 +163,13 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
     fe_mul(ay, Y, z3);
     store_fe(tab[k - 1].x, ax);
     store_fe(tab[k - 1].y, ay);
+    // the same point in Montgomery-280 form (k_point28): x * 2^256 -> x * 2^280, canonical
+    fe c280;
+    fe_load_c(c280, C280_32);
+    fe_mul(ax, ax, c280);
+    fe_mul(ay, ay, c280);
+    store_fe(tab28[k - 1].x, ax);
+    store_fe(tab28[k - 1].y, ay);
   }
 }
 
@@ -185,7 +195,7 @@ __global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, uint8_t *__rest
                                                      uint32_t *__restrict__ w_out,
                                                      uint32_t *__restrict__ w_scratch) {
   // latency-critical: it runs beside the SHA-256 jobs (second stream); win VALU arbitration
-  __builtin_amdgcn_s_setprio(2);
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nl = gridDim.x * blockDim.x;
   uint32_t one[8], r2n[8], acc[8];
@@ -264,6 +274,7 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restr
                                               const uint8_t *__restrict__ digests,
                                               const uint32_t *__restrict__ dig_idx,
                                               int8_t *__restrict__ digits) {
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || status[i] != ST_PENDING) return;
   uint32_t w[8], r[8], e[8], u1[8], u2[8];
@@ -326,7 +337,9 @@ FGV_DEV void shfl_fe(fe &r, const fe &a, int src_lane) {
 __global__ __launch_bounds__(POINT_THREADS) void k_point(
     uint32_t n, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
     const apoint_raw *__restrict__ gtab, const apoint_raw *__restrict__ ktab,
-    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs) {
+    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, const uint32_t *__restrict__ redo) {
+  // after k_point28: only the items it left pending (exceptional additions) remain
+  if (redo && *redo == 0u) return;
   extern __shared__ uint4 lds_g[];
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(gtab);
@@ -403,6 +416,218 @@ __global__ __launch_bounds__(POINT_THREADS) void k_point(
           fe_to_mont(rm, rn);
           fe_mul(lhs, rm, z2);
           if (fe_eq(lhs, acc.x)) st = 0;
+        }
+      }
+    }
+    status[i] = st;
+  }
+}
+
+// ---------------------------------------------------------------- k_point28 (fast path)
+// Same comb and lane split as k_point, in radix-2^28 Montgomery-280 arithmetic
+// (p256_fe28.h) with INCOMPLETE addition formulas: no per-addition exceptional-case tests.
+// An exceptional addition (H == 0 mod p: P == +-Q, including a partial sum passing through
+// infinity) makes that addition's Z3 = Z1*H == 0, and every later Z stays 0 (Z3 = Z1*H,
+// Z3 = Z1*Z2*H).  So a final Z != 0 proves no exceptional case occurred and the result is
+// exact; a final Z == 0 leaves the item ST_PENDING and counts it in *redo, and k_point (the
+// complete formulas) finishes exactly those items.  Honest inputs never hit it; adversarial
+// ones (Q = +-G, u1 = +-u2 ...) do, and stay bit-exact through the exact kernel.
+//
+// Value bounds (multiples of p) of the lazy representation, per coordinate of the running
+// sum: X < 10p, Y < 6p, Z < 2p, all normalized; the constants of each f28_sub are chosen so
+// the subtrahend's top limb stays below the constant's (p256_fe28.h).
+struct jp28 {
+  f28 x, y, z;
+};
+
+// acc += (x2, y2): madd-2004-hmv, 8M + 3S
+FGV_DEV void madd28(jp28 &a, const f28 &x2, const f28 &y2) {
+  f28 z1z1, u2, t, s2, h, r, hh, hhh, v, x3, y3;
+  f28_sqr(z1z1, a.z);
+  f28_mul(u2, x2, z1z1);
+  f28_mul(t, a.z, z1z1);
+  f28_mul(s2, y2, t);
+  f28_sub(h, u2, a.x, C16P28);  // < 18p
+  f28_sub(r, s2, a.y, C8P28);   // < 10p
+  f28_sqr(hh, h);
+  f28_mul(hhh, h, hh);
+  f28_mul(v, a.x, hh);
+  f28_add(t, hhh, v);
+  f28_add(t, t, v);
+  f28_norm(t);                  // < 6p
+  f28_sqr(x3, r);
+  f28_sub(x3, x3, t, C8P28);
+  f28_norm(x3);                 // < 10p
+  f28_sub(t, v, x3, C16P28);
+  f28_mul(y3, r, t);
+  f28_mul(t, a.y, hhh);
+  f28_sub(y3, y3, t, C4P28);
+  f28_norm(y3);                 // < 6p
+  f28_mul(a.z, a.z, h);
+  a.x = x3;
+  a.y = y3;
+}
+
+// a += b (both running sums, not infinity), add-2007-bl shape without the exceptional tests
+FGV_DEV void add28(jp28 &a, const jp28 &b) {
+  f28 z1z1, z2z2, u1, u2, s1, s2, t, h, r, hh, hhh, v, x3, y3;
+  f28_sqr(z1z1, a.z);
+  f28_sqr(z2z2, b.z);
+  f28_mul(u1, a.x, z2z2);
+  f28_mul(u2, b.x, z1z1);
+  f28_mul(t, b.z, z2z2);
+  f28_mul(s1, a.y, t);
+  f28_mul(t, a.z, z1z1);
+  f28_mul(s2, b.y, t);
+  f28_sub(h, u2, u1, C4P28);
+  f28_sub(r, s2, s1, C4P28);
+  f28_sqr(hh, h);
+  f28_mul(hhh, h, hh);
+  f28_mul(v, u1, hh);
+  f28_add(t, hhh, v);
+  f28_add(t, t, v);
+  f28_norm(t);
+  f28_sqr(x3, r);
+  f28_sub(x3, x3, t, C8P28);
+  f28_norm(x3);
+  f28_sub(t, v, x3, C16P28);
+  f28_mul(y3, r, t);
+  f28_mul(t, s1, hhh);
+  f28_sub(y3, y3, t, C4P28);
+  f28_norm(y3);
+  f28_mul(t, a.z, b.z);
+  f28_mul(a.z, t, h);
+  a.x = x3;
+  a.y = y3;
+}
+
+FGV_DEV void lds_load_ap28(f28 &x, f28 &y, const uint4 *lds, uint32_t idx) {
+  const uint4 a = lds[idx * 4 + 0], b = lds[idx * 4 + 1], c = lds[idx * 4 + 2], d = lds[idx * 4 + 3];
+  const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+  f28_from32(x, wx);
+  f28_from32(y, wy);
+}
+FGV_DEV void glb_load_ap28(f28 &x, f28 &y, const apoint_raw *e) {
+  const uint4 *s = reinterpret_cast<const uint4 *>(e);
+  const uint4 a = s[0], b = s[1], c = s[2], d = s[3];
+  const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+  f28_from32(x, wx);
+  f28_from32(y, wy);
+}
+FGV_DEV void shfl_f28(f28 &r, const f28 &a, int src_lane) {
+#pragma unroll
+  for (int k = 0; k < 10; k++) r.v[k] = (uint32_t)__shfl((int)a.v[k], src_lane);
+}
+// plain 8 x 32-bit value < p -> Montgomery-280, normalized (< 2p)
+FGV_DEV void f28_to_mont(f28 &r, const uint32_t w[8]) {
+  f28 a, r2;
+  f28_from32(a, w);
+  f28_load_c(r2, R2P28);
+  f28_mul(r, a, r2);
+}
+
+__global__ __launch_bounds__(POINT_THREADS) void k_point28(
+    uint32_t n, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
+    const apoint_raw *__restrict__ gtab28, const apoint_raw *__restrict__ ktab28,
+    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo) {
+  extern __shared__ uint4 lds_g[];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(gtab28);
+    for (uint32_t j = threadIdx.x; j < KT_ENTRIES * 4; j += blockDim.x) lds_g[j] = src[j];
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t gpw = 64u / L;
+  const uint32_t g = lane / L, sub = lane % L;
+  if (g >= gpw) return;
+  const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t groups = waves * gpw;
+  const uint32_t base = lane - sub;
+  for (uint32_t i = (blockIdx.x * (blockDim.x >> 6) + wave) * gpw + g; i < n; i += groups) {
+    if (status[i] != ST_PENDING) continue;
+    const apoint_raw *qt = ktab28 + (size_t)key_slot[i] * KT_ENTRIES;
+    const int8_t *dg = digits + (size_t)i * DIG_STRIDE;
+    jp28 acc;
+    bool inf = true;
+    const int nterms = 2 * ((NWIN - (int)sub + (int)L - 1) / (int)L);
+#pragma unroll 1
+    for (int t = 0; t < nterms; t++) {
+      const int w = (int)sub + (t >> 1) * (int)L;
+      const bool isq = t & 1;
+      const int d = dg[2 * w + (isq ? 1 : 0)];
+      if (d == 0) continue;
+      const int k = (d < 0 ? -d : d) - 1;
+      f28 px, py;
+      if (!isq) lds_load_ap28(px, py, lds_g, (uint32_t)(w * TAB_K + k));
+      else glb_load_ap28(px, py, qt + w * TAB_K + k);
+      if (d < 0) {
+        f28 z;
+#pragma unroll
+        for (int j = 0; j < 10; j++) z.v[j] = 0u;
+        f28_sub(py, z, py, C4P28);
+        f28_norm(py);
+      }
+      if (inf) {
+        acc.x = px;
+        acc.y = py;
+        f28_load_c(acc.z, ONE28);
+        inf = false;
+      } else {
+        madd28(acc, px, py);
+      }
+    }
+#pragma unroll 1
+    for (uint32_t m = 1; m < L; m <<= 1) {
+      const uint32_t peer = sub ^ m;
+      const int src = (int)(base + (peer < L ? peer : sub));
+      jp28 o;
+      shfl_f28(o.x, acc.x, src);
+      shfl_f28(o.y, acc.y, src);
+      shfl_f28(o.z, acc.z, src);
+      const bool oinf = __shfl((int)inf, src) != 0;
+      if (peer < L && !oinf) {
+        if (inf) {
+          acc = o;
+          inf = false;
+        } else {
+          add28(acc, o);
+        }
+      }
+    }
+    if (sub != 0) continue;
+    uint8_t st = 1;
+    if (inf) {
+      st = 1;  // R = infinity (only u1 = u2 = 0 -> unreachable: r != 0), invalid
+    } else if (f28_is_zero(acc.z)) {
+      // an exceptional addition (or a true infinity): the complete kernel decides
+      atomicAdd(redo, 1u);
+      continue;
+    } else {
+      uint32_t r[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) r[k] = r_limbs[(size_t)k * n + i];
+      f28 z2, rm, lhs, d, one;
+      f28_sqr(z2, acc.z);
+      f28_load_c(one, ONE28);
+      f28_to_mont(rm, r);
+      f28_mul(lhs, rm, z2);
+      f28_sub(d, acc.x, lhs, C4P28);
+      f28_mul(d, d, one);
+      if (f28_is_zero(d)) {
+        st = 0;
+      } else {
+        // x_R in [n, p): x_R mod n == r  <=>  x_R == r + n  (only if r + n < p)
+        uint32_t c = 0, rn[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) rn[k] = addc(r[k], N_LIMBS[k], c, &c);
+        if (c == 0u && lt_p(rn)) {
+          f28_to_mont(rm, rn);
+          f28_mul(lhs, rm, z2);
+          f28_sub(d, acc.x, lhs, C4P28);
+          f28_mul(d, d, one);
+          if (f28_is_zero(d)) st = 0;
         }
       }
     }
