@@ -29,9 +29,10 @@ import torch
 import torch.distributed as dist
 
 METRIC = "ECDSA-P256 verifies/sec + validated tx/sec per block at 1/2/4/8 MI355X"
-# 32x32->64 multiply-add products per verify in k_point: 86 complete mixed
-# additions x (8 field mults x 64 + 3 squarings x 36) + the projective x-check (3 x 64)
-PRODUCTS_POINT = 86 * (8 * 64 + 3 * 36) + 3 * 64
+# 32x32->64 multiply-add products per verify in the comb: 65 mixed additions
+# (32 signed 8-bit windows per scalar, ~1 carry window in 2) x (8 field mults x 64 + 3 squarings
+# x 36 products) + the projective x-check (3 x 64)
+PRODUCTS_POINT = 65 * (8 * 64 + 3 * 36) + 3 * 64
 # chip-wide v_mad_u64_u32 issue rate measured by tools/valu_peak.hip (profiles/round1_valu_peak.json)
 PEAK_MAD_PER_S = float(os.environ.get("FGV_PEAK_MAD", "3.106e13"))
 

@@ -90,12 +90,6 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
   for (auto &e : c->ev_pay)
     if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
-  if (hipFuncSetAttribute((const void *)k_point, hipFuncAttributeMaxDynamicSharedMemorySize, (int)KT_BYTES) !=
-      hipSuccess)
-    return fail(FGV_EDEVICE);
-  if (hipFuncSetAttribute((const void *)k_point28, hipFuncAttributeMaxDynamicSharedMemorySize, (int)KT_BYTES) !=
-      hipSuccess)
-    return fail(FGV_EDEVICE);
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0)
@@ -201,19 +195,26 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
                      c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>());
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[5], c->stream));
-  // Persistent grid (one 1024-lane workgroup per CU: the 88 KB LDS table and ~118 VGPRs
-  // allow one per CU).  Lanes per verify L: the largest L <= 8 whose groups
-  // (n_cu * 16 waves * floor(64/L)) still cover the batch in one pass -- the per-item
-  // latency falls ~L-fold while the work grows only by the L-1 tree additions.
-  // FGV_POINT_LANES forces L (measurement knob).
+  // Persistent grid: one POINT_THREADS workgroup per CU.  Lanes per verify L (1, 2, 4, 8):
+  // k_point28 is VALU-bound; a wave carries 2 ceil(NWIN / L) window terms plus log2(L) tree
+  // additions (~1.5 mixed-addition equivalents each).  A SIMD running one wave issues at about
+  // half rate (dependent-issue latency), two or more share it at full rate, so the batch time
+  // is max(2 x wave, waves-per-SIMD x wave) on the busiest SIMD (measured on MI355X: C2
+  // 54k verifies L=1/2/4 = 586/340/393 us, C4 131k = 660/685/790 us).  FGV_POINT_LANES forces L.
   static const int forced = [] {
     const char *e = getenv("FGV_POINT_LANES");
     return e ? atoi(e) : 0;
   }();
-  const uint64_t waves = (uint64_t)c->n_cu * (POINT_THREADS / 64);
+  const uint64_t simds = (uint64_t)c->n_cu * 4, slots = (uint64_t)c->n_cu * (POINT_THREADS / 64);
   uint32_t L = 1;
-  for (uint32_t l = POINT_LANES_MAX; l >= 1; l--)
-    if (waves * (64 / l) >= N) { L = l; break; }
+  double best = 1e30;
+  for (uint32_t l = 1, lg = 0; l <= POINT_LANES_MAX; l <<= 1, lg++) {
+    const uint64_t waves = ((uint64_t)N * l + 63) / 64;
+    const uint64_t passes = (waves + slots - 1) / slots;  // the persistent grid's passes
+    const uint64_t per_simd = std::max<uint64_t>(std::max<uint64_t>((waves + simds - 1) / simds, passes), 2);
+    const double cost = (double)per_simd * (2.0 * ((NWIN + l - 1) / l) + 1.5 * lg);
+    if (cost < best - 1e-9) { best = cost; L = l; }
+  }
   if (forced >= 1 && forced <= POINT_LANES_MAX) L = (uint32_t)forced;
   // k_point28 (radix-2^28, incomplete formulas) decides every item except those that hit an
   // exceptional addition; k_point (complete formulas) then finishes those, and returns at
@@ -225,10 +226,10 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
   uint32_t *redo = exact_only ? nullptr : c->redo.as<uint32_t>();
   if (redo) {
     HIP_TRY(hipMemsetAsync(redo, 0, 4, c->stream));
-    hipLaunchKernelGGL(k_point28, dim3(c->n_cu), dim3(POINT_THREADS), KT_BYTES, c->stream, N, L, d_status, d_slot,
+    hipLaunchKernelGGL(k_point28, dim3(c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, L, d_status, d_slot,
                        c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   }
-  hipLaunchKernelGGL(k_point, dim3(c->n_cu), dim3(POINT_THREADS), KT_BYTES, c->stream, N, L, d_status, d_slot,
+  hipLaunchKernelGGL(k_point, dim3(c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, L, d_status, d_slot,
                      c->gtab.as<apoint_raw>(), c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   c->last_lanes = L;
   HIP_TRY(hipGetLastError());

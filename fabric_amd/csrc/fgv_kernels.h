@@ -3,16 +3,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Fixed-base comb: 43 windows of 6 bits (signed digits in [-31, 32]), 32 entries/window.
-#define WBITS 6
-#define NWIN 43
-#define TAB_K 32
-#define KT_ENTRIES (NWIN * TAB_K)           // 1376 affine points per table
-#define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 88,064 bytes per table
+// Fixed-base comb: 32 windows of 8 bits with signed digits in [-128, 127], plus a 33rd window
+// for the final carry (digit 0 or 1); 128 entries (|d| = 1..128) per window.
+#define WBITS 8
+#define NWIN 33
+#define TAB_K 128
+#define KT_ENTRIES (NWIN * TAB_K)           // 4224 affine points per table
+#define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 270,336 bytes per table
 #define PREP_B 2                            // items per lane in the batched inversion
-#define POINT_THREADS 1024
+#define POINT_THREADS 512   // 8 waves per CU (2 per SIMD): up to 256 VGPRs, no spills
 #define POINT_LANES_MAX 8    // lanes cooperating on one verify in k_point (partial sums + tree)
-#define DIG_STRIDE 96        // bytes per item of the digit array: (d1, d2) pairs for 43 windows
+#define DIG_STRIDE 80        // bytes per item of the digit array: (d1, d2) pairs for 33 windows
 #define ST_PENDING 0xFF
 
 struct apoint_raw {  // affine point, Montgomery limbs (64 B, 16-B aligned)

@@ -2,17 +2,18 @@
 //
 // Pipeline per batch (one HIP stream, three launches):
 //   k_keytab  (per NEW public key, cached across batches) -- fixed-base comb table
-//             T_Q[w][k-1] = k * 2^(6w) * Q, w < 43, k = 1..32, affine Montgomery (88 KB/key).
+//             T_Q[w][k-1] = k * 2^(8w) * Q, w < 33, k = 1..128, affine Montgomery (270 KB/key),
+//             plus the same points in Montgomery-280 form for k_point28.
 //             The generator table T_G is the same kernel run once on G at init.
 //   k_inv     (PREP_B items per lane) -- range checks, w = s^-1 mod n with a per-lane
 //             batched (Montgomery-trick) inversion; independent of the digests, so it runs
 //             concurrently with the SHA-256 jobs of a block batch (second stream).
-//   k_prep    (per item) -- u1 = e*w, u2 = r*w, signed 6-bit recoding into 43 digits each.
-//   k_point   (L lanes per item, L chosen per batch) -- R = sum_w T_G[w][d1_w] + T_Q[w][d2_w]: 86
+//   k_prep    (per item) -- u1 = e*w, u2 = r*w, signed 8-bit recoding into 33 digits each.
+//   k_point   (L lanes per item, L chosen per batch) -- R = sum_w T_G[w][d1_w] + T_Q[w][d2_w]: <= 66
 //             complete mixed additions and NO doublings, split over the lanes of a group
 //             (lane j sums windows j, j+L, ...), then a log2(L)-level butterfly of complete
-//             Jacobian additions across the group (cross-lane shuffles); T_G staged in LDS
-//             (88 KB), T_Q gathered from HBM/L2; x_R mod n == r checked projectively
+//             Jacobian additions across the group (cross-lane shuffles); T_G (L2-resident)
+//             and T_Q gathered from L2 / HBM; x_R mod n == r checked projectively
 //             (X == r*Z^2 or (r+n)*Z^2).  The split cuts the per-item latency ~L-fold, which
 //             is what bounds block-sized batches (tens of thousands of verifies).
 //
@@ -295,35 +296,30 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restr
   }
   sn_mul(u1, e, w);  // e * s^-1 (plain)
   sn_mul(u2, r, w);  // r * s^-1 (plain)
-  // signed base-64 recoding: digits in [-31, 32], 43 windows (top window <= 16)
+  // signed base-2^WBITS recoding: digits in [-2^(W-1), 2^(W-1) - 1]; the last window holds
+  // the final carry
+  constexpr int WMASK = (1 << WBITS) - 1, WHALF = 1 << (WBITS - 1);
   int c1 = 0, c2 = 0;
   uint16_t *dp = reinterpret_cast<uint16_t *>(digits + (size_t)i * DIG_STRIDE);
 #pragma unroll
   for (int win = 0; win < NWIN; win++) {
     const int bit = WBITS * win, li = bit >> 5, sh = bit & 31;
-    uint32_t v1 = u1[li] >> sh, v2 = u2[li] >> sh;
+    uint32_t v1 = li < 8 ? u1[li] >> sh : 0u, v2 = li < 8 ? u2[li] >> sh : 0u;
     if (sh > 32 - WBITS && li < 7) {
       v1 |= u1[li + 1] << (32 - sh);
       v2 |= u2[li + 1] << (32 - sh);
     }
-    int a1 = (int)(v1 & 63u) + c1, a2 = (int)(v2 & 63u) + c2;
-    c1 = a1 > 32;
-    c2 = a2 > 32;
-    a1 -= c1 << 6;
-    a2 -= c2 << 6;
+    int a1 = (int)(v1 & WMASK) + c1, a2 = (int)(v2 & WMASK) + c2;
+    c1 = a1 >= WHALF;
+    c2 = a2 >= WHALF;
+    a1 -= c1 << WBITS;
+    a2 -= c2 << WBITS;
     dp[win] = (uint16_t)((uint8_t)(int8_t)a1 | ((uint16_t)(uint8_t)(int8_t)a2 << 8));
   }
 }
 
 // ---------------------------------------------------------------- k_point
-// grid-stride over items; every workgroup stages T_G (KT_ENTRIES * 64 B = 88 KB) in LDS.
-FGV_DEV void lds_load_apoint(apoint &p, const uint4 *lds, uint32_t idx) {
-  uint4 a = lds[idx * 4 + 0], b = lds[idx * 4 + 1], c = lds[idx * 4 + 2], d = lds[idx * 4 + 3];
-  p.x.v[0] = a.x; p.x.v[1] = a.y; p.x.v[2] = a.z; p.x.v[3] = a.w;
-  p.x.v[4] = b.x; p.x.v[5] = b.y; p.x.v[6] = b.z; p.x.v[7] = b.w;
-  p.y.v[0] = c.x; p.y.v[1] = c.y; p.y.v[2] = c.z; p.y.v[3] = c.w;
-  p.y.v[4] = d.x; p.y.v[5] = d.y; p.y.v[6] = d.z; p.y.v[7] = d.w;
-}
+// grid-stride over items; T_G (270 KB) and T_Q are gathered from L2 / HBM (64 B per term).
 
 FGV_DEV void shfl_fe(fe &r, const fe &a, int src_lane) {
 #pragma unroll
@@ -340,12 +336,6 @@ __global__ __launch_bounds__(POINT_THREADS) void k_point(
     const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, const uint32_t *__restrict__ redo) {
   // after k_point28: only the items it left pending (exceptional additions) remain
   if (redo && *redo == 0u) return;
-  extern __shared__ uint4 lds_g[];
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(gtab);
-    for (uint32_t j = threadIdx.x; j < KT_ENTRIES * 4; j += blockDim.x) lds_g[j] = src[j];
-  }
-  __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t gpw = 64u / L;  // groups per wave
   const uint32_t g = lane / L, sub = lane % L;
@@ -373,13 +363,9 @@ __global__ __launch_bounds__(POINT_THREADS) void k_point(
       if (d == 0) continue;
       const int k = (d < 0 ? -d : d) - 1;
       apoint p;
-      if (!isq) {
-        lds_load_apoint(p, lds_g, (uint32_t)(w * TAB_K + k));
-      } else {
-        const apoint_raw *e = qt + w * TAB_K + k;
-        load_fe(p.x, e->x);
-        load_fe(p.y, e->y);
-      }
+      const apoint_raw *e = (isq ? qt : gtab) + w * TAB_K + k;
+      load_fe(p.x, e->x);
+      load_fe(p.y, e->y);
       if (d < 0) fe_neg(p.y, p.y);
       pt_madd(acc, acc, p);
     }
@@ -501,21 +487,6 @@ FGV_DEV void add28(jp28 &a, const jp28 &b) {
   a.y = y3;
 }
 
-FGV_DEV void lds_load_ap28(f28 &x, f28 &y, const uint4 *lds, uint32_t idx) {
-  const uint4 a = lds[idx * 4 + 0], b = lds[idx * 4 + 1], c = lds[idx * 4 + 2], d = lds[idx * 4 + 3];
-  const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  const uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
-  f28_from32(x, wx);
-  f28_from32(y, wy);
-}
-FGV_DEV void glb_load_ap28(f28 &x, f28 &y, const apoint_raw *e) {
-  const uint4 *s = reinterpret_cast<const uint4 *>(e);
-  const uint4 a = s[0], b = s[1], c = s[2], d = s[3];
-  const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  const uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
-  f28_from32(x, wx);
-  f28_from32(y, wy);
-}
 FGV_DEV void shfl_f28(f28 &r, const f28 &a, int src_lane) {
 #pragma unroll
   for (int k = 0; k < 10; k++) r.v[k] = (uint32_t)__shfl((int)a.v[k], src_lane);
@@ -532,12 +503,6 @@ __global__ __launch_bounds__(POINT_THREADS) void k_point28(
     uint32_t n, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
     const apoint_raw *__restrict__ gtab28, const apoint_raw *__restrict__ ktab28,
     const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo) {
-  extern __shared__ uint4 lds_g[];
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(gtab28);
-    for (uint32_t j = threadIdx.x; j < KT_ENTRIES * 4; j += blockDim.x) lds_g[j] = src[j];
-  }
-  __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t gpw = 64u / L;
   const uint32_t g = lane / L, sub = lane % L;
@@ -552,16 +517,33 @@ __global__ __launch_bounds__(POINT_THREADS) void k_point28(
     jp28 acc;
     bool inf = true;
     const int nterms = 2 * ((NWIN - (int)sub + (int)L - 1) / (int)L);
-#pragma unroll 1
-    for (int t = 0; t < nterms; t++) {
+    // the table entry of term t+1 is loaded while term t is added (one gather in flight)
+    auto entry = [&](int t, int &d) -> const uint4 * {
       const int w = (int)sub + (t >> 1) * (int)L;
       const bool isq = t & 1;
-      const int d = dg[2 * w + (isq ? 1 : 0)];
+      d = dg[2 * w + (isq ? 1 : 0)];
+      const int k = d == 0 ? 0 : (d < 0 ? -d : d) - 1;
+      return reinterpret_cast<const uint4 *>((isq ? qt : gtab28) + w * TAB_K + k);
+    };
+    int dn;
+    const uint4 *pn = entry(0, dn);
+    uint4 n0 = pn[0], n1 = pn[1], n2 = pn[2], n3 = pn[3];
+#pragma unroll 1
+    for (int t = 0; t < nterms; t++) {
+      const int d = dn;
+      const uint32_t wx[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+      const uint32_t wy[8] = {n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
+      if (t + 1 < nterms) {
+        pn = entry(t + 1, dn);
+        n0 = pn[0];
+        n1 = pn[1];
+        n2 = pn[2];
+        n3 = pn[3];
+      }
       if (d == 0) continue;
-      const int k = (d < 0 ? -d : d) - 1;
       f28 px, py;
-      if (!isq) lds_load_ap28(px, py, lds_g, (uint32_t)(w * TAB_K + k));
-      else glb_load_ap28(px, py, qt + w * TAB_K + k);
+      f28_from32(px, wx);
+      f28_from32(py, wy);
       if (d < 0) {
         f28 z;
 #pragma unroll
