@@ -17,6 +17,7 @@ SIG_VALID, SIG_FALSE, SIG_DER, SIG_HIGH_S, SIG_RANGE, SIG_BADKEY, SIG_EMPTY = ra
 
 EXPORTED = [
     "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_last_counts", "fgv_last_host_timing",
+    "fgv_last_point_handovers",
     "fgv_sha256_batch",
     "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
@@ -86,6 +87,7 @@ def load():
         L.fgv_strerror.restype = ctypes.c_char_p
         L.fgv_last_timing.argtypes = [vp] + [ctypes.POINTER(ctypes.c_double)] * 4
         L.fgv_last_counts.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 3
+        L.fgv_last_point_handovers.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
         L.fgv_last_host_timing.argtypes = [vp] + [ctypes.POINTER(ctypes.c_double)] * 4
         L.fgv_sha256_batch.argtypes = [vp, vp, sz, vp, vp, sz, vp]
         L.fgv_p256_verify_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp]
@@ -181,6 +183,11 @@ class Engine:
         v = [ctypes.c_uint64() for _ in range(3)]
         _check(self._L.fgv_last_counts(self._h, *[ctypes.byref(x) for x in v]))
         return dict(zip(("sha_jobs", "sha_blocks", "verifies"), (x.value for x in v)))
+
+    def point_handovers(self):
+        v = ctypes.c_uint64()
+        _check(self._L.fgv_last_point_handovers(self._h, ctypes.byref(v)))
+        return v.value
 
     # --- BCCSP Hash
     def sha256_batch(self, msgs):

@@ -31,9 +31,8 @@
 #define BD_DIG_I (3 + BD_MAX_END)
 #define BD_DIG_SLOTS (4 + BD_MAX_END)
 #define SHA_E_LANES 4u  // k_bd_sha lanes per tx for endorsement messages (grid: SHA_E_LANES + 3 rows)
-// host -> device envelope table, per tx: block, envelope offset, length, Envelope.payload
-// offset, length (0xFFFFFFFF: the envelope does not decode)
-#define BD_ENV_WORDS 5
+// host -> device envelope table, per tx: block, envelope offset, length
+#define BD_ENV_WORDS 3
 
 struct DSpan {  // bytes [off, off+len) of block `DevTx::blk`; len 0 == nil
   uint32_t off, len;

@@ -498,9 +498,6 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
   do {
     VTwoBytes env;
     if (!decode(d, env, ovf)) { R.pre = C_OTHER; break; }
-    // k_bd_sha_payload hashed the host's Envelope.payload span: it must be this one (same
-    // protobuf rules on both sides; a disagreement sends the batch to the host parser)
-    if (env.a.n != et[4] || (env.a.n && env.a.p != base + et[3])) { ovf = true; break; }
     VPayload pl;
     if (!decode(env.a, pl, ovf)) { R.pre = C_BAD_PAYLOAD; break; }
     const VTwoBytes &hdr = pl.hdr;
@@ -748,9 +745,9 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
 // ============================================================ k_bd_sha_payload
 // SHA-256(Envelope.payload) of every envelope -- the creator signature's digest
 // (msgvalidation.go:26-64 -> msp/identities.go:179), digest slot 0 -- launched on the second
-// stream BEFORE the parse, from the payload spans the host's block split found (k_bd_parse
-// checks they match its own).  Each is its transaction's longest message (~80 compressions
-// for C2): these serial chains set the SHA-256 stage, so they start first.
+// stream BEFORE the parse: it decodes the Envelope (two fields, the same rules and visitor as
+// k_bd_parse) and hashes field 1.  Each payload is its transaction's longest message (~80
+// compressions for C2): these serial chains set the SHA-256 stage, so they start first.
 __global__ __launch_bounds__(64) void k_bd_sha_payload(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                        const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
                                                        unsigned long long *__restrict__ nblk) {
@@ -759,11 +756,13 @@ __global__ __launch_bounds__(64) void k_bd_sha_payload(uint32_t ntx, const uint3
   uint64_t blocks = 0;
   if (t < ntx) {
     const uint32_t *et = envtab + BD_ENV_WORDS * t;
-    if (et[4] != 0xFFFFFFFFu) {
+    VTwoBytes env;
+    bool ovf = false;
+    if (decode(S{reinterpret_cast<const uint8_t *>(bases[et[0]]) + et[1], et[2]}, env, ovf)) {
       JobView v;
-      v.p[0] = v.p[1] = v.p[2] = reinterpret_cast<const uint8_t *>(bases[et[0]]) + et[3];
+      v.p[0] = v.p[1] = v.p[2] = env.a.p;
       v.beg[0] = 0;
-      v.beg[1] = v.beg[2] = v.beg[3] = v.L = et[4];
+      v.beg[1] = v.beg[2] = v.beg[3] = v.L = env.a.n;
       sha_view(v, dig + (size_t)t * 32);
       blocks = (v.L + 8) / 64 + 1;
     }

@@ -157,6 +157,18 @@ int fgv_last_counts(fgv_ctx *c, uint64_t *sha_jobs, uint64_t *sha_blocks, uint64
   return FGV_OK;
 }
 
+int fgv_last_point_handovers(fgv_ctx *c, uint64_t *handovers) {
+  if (!c || !handovers) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  uint32_t n = 0;
+  if (hipSetDevice(c->device) != hipSuccess ||
+      hipMemcpyAsync(&n, c->redo.p, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return FGV_EDEVICE;
+  *handovers = n;
+  return FGV_OK;
+}
+
 int fgv_last_timing(fgv_ctx *c, double *sha_ms, double *prep_ms, double *point_ms,
                     double *keytab_ms) {
   if (!c) return FGV_EINVAL;

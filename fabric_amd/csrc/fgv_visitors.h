@@ -356,6 +356,7 @@ struct VSerializedIdentity {
 };
 struct VBlockData {
   std::vector<Span> data;
+  VBlockData() { data.reserve(1024); }
   pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_REP_BYTES : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t, Span s) { data.push_back(s); return true; }

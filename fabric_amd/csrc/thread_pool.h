@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -20,17 +21,24 @@ struct ThreadPool {
   size_t njobs = 0;
   std::atomic<size_t> next{0};
   size_t active = 0;
-  uint64_t gen = 0;
+  std::atomic<uint64_t> gen{0};
   bool stop = false;
+  // A worker that finished a run spins this long for the next one before sleeping: the
+  // committer issues runs back to back within a call, and a futex wake-up of 16 threads
+  // costs tens of microseconds.
+  static constexpr auto kSpin = std::chrono::microseconds(200);
   explicit ThreadPool(unsigned n) {
     for (unsigned i = 0; i < n; i++)
       th.emplace_back([this] {
         uint64_t seen = 0;
         for (;;) {
+          const auto t0 = std::chrono::steady_clock::now();
+          while (gen.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() - t0 < kSpin)
+            std::this_thread::yield();
           std::unique_lock<std::mutex> lk(mu);
-          cv.wait(lk, [&] { return stop || gen != seen; });
+          cv.wait(lk, [&] { return stop || gen.load() != seen; });
           if (stop) return;
-          seen = gen;
+          seen = gen.load();
           lk.unlock();
           for (size_t i; (i = next.fetch_add(1)) < njobs;) job(i);
           lk.lock();
@@ -46,7 +54,8 @@ struct ThreadPool {
     cv.notify_all();
     for (auto &t : th) t.join();
   }
-  // run f(j) for every job j in [0, njobs) on the pool (dynamic assignment)
+  // run f(j) for every job j in [0, njobs) on the pool (dynamic assignment); the calling
+  // thread takes jobs too while the workers wake up
   void run(size_t nj, const std::function<void(size_t)> &f) {
     if (nj == 0) return;
     if (th.empty() || nj == 1) {
@@ -58,8 +67,11 @@ struct ThreadPool {
     njobs = nj;
     next = 0;
     active = th.size();
-    gen++;
+    gen.fetch_add(1, std::memory_order_release);
+    lk.unlock();
     cv.notify_all();
+    for (size_t i; (i = next.fetch_add(1)) < nj;) f(i);
+    lk.lock();
     done_cv.wait(lk, [&] { return active == 0; });
   }
   // run f(i) for i in [0, n) in chunks

@@ -62,6 +62,10 @@ int fgv_last_host_timing(fgv_ctx *ctx, double *parse_ms, double *assemble_ms, do
                          double *fold_ms);
 /* work of the last block call: SHA-256 messages, 64-byte compressions, ECDSA verifies */
 int fgv_last_counts(fgv_ctx *ctx, uint64_t *sha_jobs, uint64_t *sha_blocks, uint64_t *verifies);
+// Diagnostics: verifies of the last call that the fast point kernel (radix 2^28, incomplete
+// formulas) handed to the exact kernel because an exceptional addition occurred (P = +-Q).
+// Zero for honest inputs; reads one counter back from the device.
+int fgv_last_point_handovers(fgv_ctx *ctx, uint64_t *handovers);
 
 /* ---------------------------------------------------------- BCCSP Hash / Verify */
 

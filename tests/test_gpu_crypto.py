@@ -94,8 +94,23 @@ def test_adversarial_exceptional_additions(engine):
     st = _run(engine, vecs)
     exp = [oracle.verify_der(*v) for v in vecs]
     assert list(st) == exp
-    # sanity: the constructed cases do reach the infinity path (status 1) and doubling path
+    # sanity: the constructed cases do reach the infinity path (status 1) and doubling path,
+    # and the fast kernel handed exactly those items to the complete-formula kernel
     assert 1 in exp
+    assert engine.point_handovers() > 0
+
+
+def test_honest_batch_needs_no_handover(engine):
+    """Random honest signatures never hit an exceptional addition in the fast kernel."""
+    rng = random.Random(21)
+    k = synth.Key(44, 0)
+    vecs = []
+    for i in range(512):
+        dg = rng.randbytes(32)
+        vecs.append((k.qx, k.qy, synth.sign(k, dg), dg if i % 7 else bytes([dg[0] ^ 4]) + dg[1:]))
+    st = _run(engine, vecs)
+    assert list(st) == [oracle.verify_der(*v) for v in vecs]
+    assert engine.point_handovers() == 0
 
 
 def test_large_batch_properties(engine):
