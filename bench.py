@@ -46,7 +46,7 @@ def roofline(n_verifies, point_ms):
     point_s = point_ms / 1e3
     achieved = n_verifies * PRODUCTS_POINT / point_s / 1e12 if point_s > 0 else 0.0
     return dict(bound="valu", achieved=round(achieved, 3), peak=round(PEAK_MAD_PER_S / 1e12, 3),
-                unit="Tops/s", frac=round(achieved * 1e12 / PEAK_MAD_PER_S, 4), traffic=None, kernel="k_point",
+                unit="Tops/s", frac=round(achieved * 1e12 / PEAK_MAD_PER_S, 4), traffic=None, kernel="k_point28 (+ k_point hand-overs)",
                 kernel_avg_ms=round(point_ms, 4), per_launch_products=int(n_verifies * PRODUCTS_POINT),
                 work_unit="v_mad_u64_u32 (32x32->64 multiply-add) products of the comb algorithm")
 

@@ -79,24 +79,32 @@ def main(src, rnd):
             lines.append(f"| {k} | {v['avg_s'] * 1e6:.1f} | {v.get('SQ_INSTS_VALU', 0):.4g} | "
                          f"{v.get('SQ_INSTS_VALU_INT32', 0):.3g} | {v.get('SQ_INSTS_VALU_INT64', 0):.3g} | {lane:.3g} | "
                          f"{100 * lane / PEAK_LANE_OPS:.1f} | {busy:.0f} |")
-        kp = pmc(p).get("k_point")
+        kp = pmc(p).get("k_point28")
         if kp:
-            lines += ["", f"k_point: {kp.get('SQ_INSTS_VALU', 0) / (131072 / 64):,.0f} VALU instructions per verify "
-                          f"(one lane = one verify).", ""]
+            gui = kp.get("GRBM_GUI_ACTIVE", 0) / XCDS
+            cpi = gui * SIMDS / kp["SQ_INSTS_VALU"] if kp.get("SQ_INSTS_VALU") else 0
+            lines += ["", f"k_point28: {kp.get('SQ_INSTS_VALU', 0) / (131072 / 64):,.0f} VALU instructions per verify "
+                          f"(L = 1 at this batch size: one lane = one verify); {cpi:.2f} SIMD cycles per "
+                          f"wave-instruction (issue-bound near 4).", ""]
         lines += ["VALU busy % = 100·SQ_ACTIVE_INST_VALU·4 / SIMDs / (GRBM_GUI_ACTIVE/8) (gfx94x formula; "
                   "ROCm 7.2 ships no gfx950 derived-counter section).", ""]
-    for name, ctr in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+    for name, ctr in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE"), ("pmc_blk_fetch", "FETCH_SIZE"),
+                      ("pmc_blk_write", "WRITE_SIZE")):
         p = os.path.join(src, name, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
-        lines += [f"## {ctr} (mvcc workload, per dispatch)", "", "| kernel | avg µs | KB | GB/s |", "|---|---|---|---|"]
+        blk = name.startswith("pmc_blk")
+        lines += [f"## {ctr} ({'block' if blk else 'mvcc'} workload, per dispatch)", "",
+                  "| kernel | avg µs | KB | GB/s |", "|---|---|---|---|"]
         for k, v in pmc(p).items():
-            if not k.startswith("k_mv"):
+            if not (k.startswith("k_bd") or k.startswith("k_point") or k in ("k_inv", "k_prep", "k_der")
+                    if blk else k.startswith("k_mv")):
                 continue
             kb = v.get(ctr, 0) * (2 if ctr == "FETCH_SIZE" else 1)  # gfx950: FETCH_SIZE reads 1/2
             lines.append(f"| {k} | {v['avg_s'] * 1e6:.1f} | {kb:.1f} | {kb * 1024 / v['avg_s'] / 1e9 if v['avg_s'] else 0:.1f} |")
         lines += ["", "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 reports ½ of wide streaming reads); "
-                  "small MVCC gathers are uncalibrated, and a 1M-key table (32 MB) is Infinity-Cache resident.", ""]
+                  "small gathers are uncalibrated; the MVCC 1M-key table (32 MB) and the comb tables of the block "
+                  "workload (~70 MB) are Infinity-Cache resident.", ""]
     open(f"profiles/{rnd}_profile_summary.md", "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
