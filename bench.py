@@ -137,8 +137,12 @@ def run_block(args, world, rank, local, dev):
         dptr.append(arena.data_ptr() + o)
         o += sz
     ntx = np.array([T] * len(blks), dtype=np.int64)
-    lo, hi = shard.shard_ranges(ntx, rank, world)
-    rows = shard.padded_rows(ntx, world)
+    # contiguous transaction ranges of the batch, on block boundaries when there are at least
+    # as many blocks as ranks (fabric_amd/shard.py: a rank splits and parses only its blocks)
+    plan_mode = "block" if len(blks) >= world else "tx"
+    plan = shard.plan(ntx, world, plan_mode)
+    lo, hi = plan[0][rank], plan[1][rank]
+    rows = shard.plan_rows(*plan)
     # records stay in HBM: shard validation -> all-gather (RCCL) -> device finalize
     send = torch.zeros((rows, shard.REC), dtype=torch.uint8, device=dev)
     recv = torch.zeros((world * rows, shard.REC), dtype=torch.uint8, device=dev) if world > 1 else send
@@ -163,7 +167,7 @@ def run_block(args, world, rank, local, dev):
         nt = eng.validate_shard_dev(batch, lo, hi, send.data_ptr(), rows)
         if world > 1:
             shard.allgather_device(send, recv)
-        f = eng.finalize_flags_dev(nt, world, rows, recv.data_ptr(), out=flags_out)
+        f = eng.finalize_flags_dev(ntx, world, rows, recv.data_ptr(), out=flags_out, plan=plan)
         if th is not None:
             th.join()
         return f
@@ -218,7 +222,7 @@ def run_block(args, world, rank, local, dev):
                vs_baseline=None, dtype="u32", data="synthetic",
                config=dict(workload=spec["desc"].format(T=T),
                            blocks_per_step=len(blks), tx_per_block=T, global_batch=len(blks) * T,
-                           parallelism=f"tx-shard{world}+allgather(68B/tx)",
+                           parallelism=f"{plan_mode}-range-shard{world}+allgather(68B/tx)",
                            parse="host" if args.host_parse else "device"),
                verifies_per_s=round(all_verifies / el, 1), parity_vs_labels=ok,
                stage_ms=dict(sha=round(acc["sha"] / args.steps, 4), prep=round(acc["prep"] / args.steps, 4),

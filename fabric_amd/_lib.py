@@ -22,7 +22,7 @@ EXPORTED = [
     "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
-    "fgv_validate_shard_dev", "fgv_finalize_flags_dev",
+    "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode",
 ]
@@ -104,6 +104,7 @@ def load():
         L.fgv_finalize_flags.argtypes = [sz, vp, vp, vp]
         L.fgv_validate_shard_dev.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
         L.fgv_finalize_flags_dev.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp]
+        L.fgv_finalize_flags_dev_plan.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
         L.fgv_mvcc_validate_block.argtypes = [vp, vp, sz, vp, ctypes.c_uint64, vp, sz, ctypes.c_int]
@@ -306,12 +307,21 @@ class Engine:
                                               _ptr(hi), ctypes.c_void_p(d_results), cap, batch.ntx))
         return np.ctypeslib.as_array(batch.ntx).astype(np.uint64)
 
-    def finalize_flags_dev(self, ntx, world, rows_per_rank, d_gathered, out=None):
-        """fgv_finalize_flags_dev over world x rows_per_rank gathered records at d_gathered."""
+    def finalize_flags_dev(self, ntx, world, rows_per_rank, d_gathered, out=None, plan=None):
+        """fgv_finalize_flags_dev over world x rows_per_rank gathered records at d_gathered;
+        plan = (lo, hi) [world, nblocks] arrays of fabric_amd.shard.plan (default: the per-block
+        transaction split)."""
         ntx = np.ascontiguousarray(ntx, dtype=np.uint64)
         flags = out if out is not None else np.empty(int(ntx.sum()), dtype=np.uint8)
-        _check(self._L.fgv_finalize_flags_dev(self._h, len(ntx), _ptr(ntx), world, rows_per_rank,
-                                              ctypes.c_void_p(d_gathered), _ptr(flags)))
+        if plan is None:
+            _check(self._L.fgv_finalize_flags_dev(self._h, len(ntx), _ptr(ntx), world, rows_per_rank,
+                                                  ctypes.c_void_p(d_gathered), _ptr(flags)))
+        else:
+            lo = np.ascontiguousarray(plan[0], dtype=np.uint32)
+            hi = np.ascontiguousarray(plan[1], dtype=np.uint32)
+            assert lo.shape == hi.shape == (world, len(ntx))
+            _check(self._L.fgv_finalize_flags_dev_plan(self._h, len(ntx), _ptr(ntx), world, rows_per_rank, _ptr(lo),
+                                                       _ptr(hi), ctypes.c_void_p(d_gathered), _ptr(flags)))
         return flags
 
     # --- deliver-side block integrity (VerifyBlock minus orderer signatures)

@@ -552,6 +552,11 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   std::vector<uint32_t> lo(nblocks), hi(nblocks);
   size_t total = 0;
   for (size_t b = 0; b < nblocks; b++) {
+    if (tx_lo && tx_lo[b] == FGV_SHARD_SKIP) {  // another rank's block: not parsed
+      ntx_out[b] = 0;
+      lo[b] = hi[b] = 0;
+      continue;
+    }
     VBlock blk;
     if (!pbw::decode(h_blocks[b], lens[b], blk)) return FGV_EINVAL;  // unparsable block
     envs[b] = std::move(blk.data.data);
@@ -1026,6 +1031,7 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   std::vector<uint32_t> lo(nblocks), hi(nblocks);
   std::atomic<bool> bad{false};
   S->pool.run(nblocks, [&](size_t b) {
+    if (tx_lo && tx_lo[b] == FGV_SHARD_SKIP) return;  // another rank's block: not parsed
     VBlock blk;
     if (!pbw::decode(h_blocks[b], lens[b], blk)) { bad = true; return; }
     envs[b] = std::move(blk.data.data);
@@ -1034,7 +1040,7 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   size_t total = 0;
   std::vector<size_t> first(nblocks);
   for (size_t b = 0; b < nblocks; b++) {
-    ntx_out[b] = envs[b].size();
+    ntx_out[b] = envs[b].size();  // 0 for a skipped block
     lo[b] = tx_lo ? std::min<uint32_t>(tx_lo[b], (uint32_t)envs[b].size()) : 0;
     hi[b] = tx_hi ? std::min<uint32_t>(tx_hi[b], (uint32_t)envs[b].size()) : (uint32_t)envs[b].size();
     if (hi[b] < lo[b]) hi[b] = lo[b];

@@ -731,28 +731,46 @@ int fgv_ledger_add_txids(fgv_ctx *c, const uint8_t *buf, const uint64_t *off, co
 
 // Device finalize over W x rows gathered records (finalize.hip).  Caller holds c->mu and has
 // set the device.
+// rank_lo / rank_hi (W x nb, FGV_SHARD_SKIP = no rows) or null for the per-block split
+// [floor(n r / W), floor(n (r+1) / W)).  The ranks' ranges must tile every block.
 static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t W, size_t rows,
-                             const uint8_t *d_recs, uint8_t *flags) {
-  if (W == 0 || ((uintptr_t)d_recs & 3)) return FGV_EINVAL;
+                             const uint8_t *d_recs, uint8_t *flags, const uint32_t *rank_lo = nullptr,
+                             const uint32_t *rank_hi = nullptr) {
+  if (W == 0 || ((uintptr_t)d_recs & 3) || (!rank_lo) != (!rank_hi)) return FGV_EINVAL;
   uint64_t P = 0;
   for (size_t b = 0; b < nblocks; b++) P += ntx[b];
   if (P == 0) return FGV_OK;
   if (P >= 0x7FFFFFFFull || nblocks >= 0x7FFFFFFFull || rows * W >= 0xFFFFFFFFull) return FGV_EINVAL;
-  // host metadata: blk_start (nb+1 u64) | roff (W x nb u32)
-  const size_t meta = (nblocks + 1) * 8 + (size_t)W * nblocks * 4;
+  // host metadata: blk_start (nb+1 u64) | roff (W x nb u32) | lo (W x nb u32) | cnt (W x nb u32)
+  const size_t wn = (size_t)W * nblocks;
+  const size_t meta = (nblocks + 1) * 8 + 3 * wn * 4;
   if (!c->hb_fz.ensure(meta) || !c->fz_meta.ensure(meta)) return FGV_ENOMEM;
   uint64_t *bstart = c->hb_fz.as<uint64_t>();
-  uint32_t *roff = reinterpret_cast<uint32_t *>(bstart + nblocks + 1);
+  uint32_t *roff = reinterpret_cast<uint32_t *>(bstart + nblocks + 1), *rlo = roff + wn, *rcnt = rlo + wn;
   bstart[0] = 0;
   for (size_t b = 0; b < nblocks; b++) bstart[b + 1] = bstart[b] + ntx[b];
   for (uint32_t r = 0; r < W; r++) {
     uint64_t o = 0;
     for (size_t b = 0; b < nblocks; b++) {
-      roff[(size_t)r * nblocks + b] = (uint32_t)o;
+      const size_t k = (size_t)r * nblocks + b;
       const uint64_t n = ntx[b];
-      o += (n * (r + 1)) / W - (n * r) / W;
+      uint64_t lo = (n * r) / W, hi = (n * (r + 1)) / W;
+      if (rank_lo) {
+        lo = rank_lo[k] == FGV_SHARD_SKIP ? 0 : rank_lo[k];
+        hi = rank_lo[k] == FGV_SHARD_SKIP ? 0 : rank_hi[k];
+        if (hi < lo || hi > n) return FGV_EINVAL;
+      }
+      roff[k] = (uint32_t)o;
+      rlo[k] = (uint32_t)lo;
+      rcnt[k] = (uint32_t)(hi - lo);
+      o += hi - lo;
     }
     if (o > rows) return FGV_EINVAL;  // gathered rows cannot hold rank r's shard
+  }
+  for (size_t b = 0; b < nblocks; b++) {  // the ranges must tile the block
+    uint64_t cover = 0;
+    for (uint32_t r = 0; r < W; r++) cover += rcnt[(size_t)r * nblocks + b];
+    if (cover != ntx[b]) return FGV_EINVAL;
   }
   size_t cap = 1024;
   while (cap < 2 * P) cap <<= 1;
@@ -770,7 +788,7 @@ static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint
   const uint64_t *d_bstart = c->fz_meta.as<uint64_t>();
   const uint32_t *d_roff = reinterpret_cast<const uint32_t *>(d_bstart + nblocks + 1);
   hipLaunchKernelGGL(k_fin_rows, grid, blk, 0, st, n32, d_bstart, (uint32_t)nblocks, W, (uint32_t)rows, d_roff,
-                     c->fz_rowmap.as<uint32_t>(), c->fz_blkof.as<uint32_t>());
+                     d_roff + wn, d_roff + 2 * wn, c->fz_rowmap.as<uint32_t>(), c->fz_blkof.as<uint32_t>());
   hipLaunchKernelGGL(k_fin_index, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
                      c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask,
                      c->fin_seed);
@@ -810,6 +828,7 @@ static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks
 static size_t shard_count(size_t nblocks, const size_t *ntx, const uint32_t *tx_lo, const uint32_t *tx_hi) {
   size_t n = 0;
   for (size_t b = 0; b < nblocks; b++) {
+    if (tx_lo && tx_lo[b] == FGV_SHARD_SKIP) continue;
     const size_t lo = tx_lo ? std::min<size_t>(tx_lo[b], ntx[b]) : 0;
     const size_t hi = tx_hi ? std::min<size_t>(tx_hi[b], ntx[b]) : ntx[b];
     if (hi > lo) n += hi - lo;
@@ -867,12 +886,7 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   fgv_tx_result *res = c->hb_res.as<fgv_tx_result>();
   rc = fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi, res, results_cap, ntx);
   if (rc) return rc;
-  size_t n = 0;
-  for (size_t b = 0; b < nblocks; b++) {
-    const size_t lo = tx_lo ? std::min<size_t>(tx_lo[b], ntx[b]) : 0;
-    const size_t hi = tx_hi ? std::min<size_t>(tx_hi[b], ntx[b]) : ntx[b];
-    if (hi > lo) n += hi - lo;
-  }
+  const size_t n = shard_count(nblocks, ntx, tx_lo, tx_hi);
   if (n) {
     HIP_TRY(hipMemcpyAsync(d_results, res, n * sizeof(fgv_tx_result), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -887,6 +901,17 @@ int fgv_finalize_flags_dev(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
   return finalize_dev_core(c, nblocks, ntx, world, rows_per_rank, static_cast<const uint8_t *>(d_gathered), flags);
+}
+
+int fgv_finalize_flags_dev_plan(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t world, size_t rows_per_rank,
+                                const uint32_t *rank_lo, const uint32_t *rank_hi, const void *d_gathered,
+                                uint8_t *flags) {
+  if (!c || (nblocks && (!ntx || !flags || !d_gathered || !rank_lo || !rank_hi))) return FGV_EINVAL;
+  if (nblocks == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  return finalize_dev_core(c, nblocks, ntx, world, rows_per_rank, static_cast<const uint8_t *>(d_gathered), flags,
+                           rank_lo, rank_hi);
 }
 
 int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *results, uint8_t *flags) {

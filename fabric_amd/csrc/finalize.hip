@@ -70,8 +70,11 @@ __device__ inline int64_t tab_find(const uint32_t k[8], uint64_t h, const uint32
 
 }  // namespace
 
+// rank r holds transactions [rlo[r][b], rlo[r][b] + rcnt[r][b]) of block b, at its rows from
+// roff[r][b] (any shard plan whose ranges tile every block)
 __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, uint32_t W, uint32_t rows,
-                           const uint32_t *roff, uint32_t *rowmap, uint32_t *blkof) {
+                           const uint32_t *roff, const uint32_t *rlo, const uint32_t *rcnt, uint32_t *rowmap,
+                           uint32_t *blkof) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   uint32_t lo = 0, hi = nb;  // last b with blk_start[b] <= p
@@ -81,13 +84,14 @@ __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, u
     else hi = mid;
   }
   const uint32_t b = lo;
-  const uint64_t n = blk_start[b + 1] - blk_start[b], i = p - blk_start[b];
-  uint32_t r = (uint32_t)((i * W) / n);
-  if (r >= W) r = W - 1;
-  while (r > 0 && (n * r) / W > i) r--;
-  while (r + 1 < W && (n * (r + 1)) / W <= i) r++;
-  const uint64_t lo_r = (n * r) / W;
-  rowmap[p] = r * rows + roff[(size_t)r * nb + b] + (uint32_t)(i - lo_r);
+  const uint32_t i = (uint32_t)(p - blk_start[b]);
+  uint32_t r = 0;
+  for (; r + 1 < W; r++) {
+    const size_t k = (size_t)r * nb + b;
+    if (i >= rlo[k] && i < rlo[k] + rcnt[k]) break;
+  }
+  const size_t k = (size_t)r * nb + b;
+  rowmap[p] = r * rows + roff[k] + (i - rlo[k]);
   blkof[p] = b;
 }
 

@@ -1,17 +1,56 @@
 """Multi-GPU committer protocol: transaction-index sharding + one all-gather.
 
-Every rank holds the block batch (bytes in host memory and HBM), validates transactions
-[lo_b, hi_b) of every block b with fgv_validate_shard, then the ranks all-gather their
+Every rank holds the block batch (bytes in host memory and HBM) and validates a contiguous
+range of the batch's transactions with fgv_validate_shard[_dev]; the ranks all-gather their
 fgv_tx_result records (68 B/tx; RCCL over xGMI with backend "nccl", gloo on CPU) and each
-rank runs fgv_finalize_flags -- the only cross-transaction steps of the reference
+rank runs fgv_finalize_flags[_dev] -- the only cross-transaction steps of the reference
 (block-store txid index of earlier blocks, validator.go:460-481; markTXIdDuplicates,
 validator.go:279-295).  No other collective touches the data path.
+
+Shard plans (`plan`): with at least as many blocks as ranks, the ranges fall on block
+boundaries ("block": rank r takes blocks [B r / W, B (r+1) / W) whole, so it splits and parses
+only its own blocks -- the host block split does not grow with W); otherwise every block is
+split by transaction index ("tx": [n r / W, n (r+1) / W) of each block).  Either way a
+transaction's creator and endorsements stay on one GPU.
 """
 import numpy as np
 import torch
 import torch.distributed as dist
 
 REC = 68  # sizeof(fgv_tx_result)
+SKIP = 0xFFFFFFFF  # FGV_SHARD_SKIP: another rank's block
+
+
+def plan(ntx, world, mode="auto"):
+    """(lo, hi): uint32 [world, nblocks]; rank r validates transactions [lo[r,b], hi[r,b]) of
+    block b (SKIP: none, block not parsed)."""
+    ntx = np.asarray(ntx, dtype=np.int64)
+    B = len(ntx)
+    if mode == "auto":
+        mode = "block" if B >= world else "tx"
+    lo = np.zeros((world, B), np.uint32)
+    hi = np.zeros((world, B), np.uint32)
+    for r in range(world):
+        if mode == "tx":
+            lo[r] = (ntx * r) // world
+            hi[r] = (ntx * (r + 1)) // world
+        else:
+            b0, b1 = (B * r) // world, (B * (r + 1)) // world
+            lo[r, :] = SKIP
+            hi[r, :] = SKIP
+            lo[r, b0:b1] = 0
+            hi[r, b0:b1] = ntx[b0:b1]
+    return lo, hi
+
+
+def plan_counts(lo, hi):
+    """transactions per (rank, block)"""
+    return np.where(lo == SKIP, 0, hi.astype(np.int64) - lo.astype(np.int64))
+
+
+def plan_rows(lo, hi):
+    """rows per rank after padding (the largest shard)"""
+    return int(plan_counts(lo, hi).sum(axis=1).max()) if lo.size else 0
 
 
 def shard_ranges(ntx, rank, world):
@@ -27,10 +66,10 @@ def padded_rows(ntx, world):
     return int(max(((ntx * (r + 1)) // world - (ntx * r) // world).sum() for r in range(world)))
 
 
-def allgather_results(local, ntx, world, device=None, group=None, out=None):
+def allgather_results(local, ntx, world, device=None, group=None, out=None, plan_=None):
     """local: (rows, 68) uint8 results of this rank's shard.  Returns (sum(ntx), 68) uint8 in
     block-major transaction order, identical on every rank."""
-    rows = padded_rows(ntx, world)
+    rows = padded_rows(ntx, world) if plan_ is None else plan_rows(*plan_)
     if dist.get_backend(group) == "gloo":
         device = "cpu"
         out = None
@@ -39,7 +78,7 @@ def allgather_results(local, ntx, world, device=None, group=None, out=None):
     recv = torch.empty((world * rows, REC), dtype=torch.uint8, device=device) if out is None else out
     dist.all_gather_into_tensor(recv, send, group=group)
     g = recv.cpu().numpy() if recv.device.type != "cpu" else recv.numpy()
-    return reorder(g, ntx, world, rows)
+    return reorder(g, ntx, world, rows, plan_)
 
 
 def allgather_device(send, recv, group=None):
@@ -56,13 +95,14 @@ def allgather_device(send, recv, group=None):
     torch.cuda.current_stream(recv.device).synchronize()
 
 
-def reorder(gathered, ntx, world, rows):
+def reorder(gathered, ntx, world, rows, plan_=None):
     """rank-major padded rows -> block-major transaction order"""
     ntx = np.asarray(ntx, dtype=np.int64)
+    lo, hi = plan_ if plan_ is not None else plan(ntx, world, "tx")
+    cnt = plan_counts(lo, hi)
     parts = []
     for b in range(len(ntx)):
-        for r in range(world):
-            lo, hi = shard_ranges(ntx, r, world)
-            off = int((hi[:b].astype(np.int64) - lo[:b]).sum())
-            parts.append(gathered[r * rows + off: r * rows + off + int(hi[b]) - int(lo[b])])
+        for r in sorted(range(world), key=lambda r: (0 if cnt[r, b] == 0 else int(lo[r, b]))):
+            off = int(cnt[r, :b].sum())
+            parts.append(gathered[r * rows + off: r * rows + off + int(cnt[r, b])])
     return np.concatenate(parts) if parts else np.zeros((0, REC), np.uint8)

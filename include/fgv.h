@@ -164,6 +164,9 @@ typedef struct fgv_tx_result {
  * its batch through the host parser), 1 = host parser (C++ threads).  Same results. */
 int fgv_set_parse_mode(fgv_ctx *ctx, int mode);
 
+/* tx_lo[b] == FGV_SHARD_SKIP: block b belongs to another rank -- it is not parsed, adds no
+ * records, and ntx[b] comes back 0 (the block-granular plan of fabric_amd/shard.py). */
+#define FGV_SHARD_SKIP 0xFFFFFFFFu
 int fgv_validate_shard(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                        const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
                        fgv_tx_result *results, size_t results_cap, size_t *ntx);
@@ -186,6 +189,12 @@ int fgv_validate_shard_dev(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *b
                            const uint32_t *tx_hi, void *d_results, size_t results_cap, size_t *ntx);
 int fgv_finalize_flags_dev(fgv_ctx *ctx, size_t nblocks, const size_t *ntx, uint32_t world,
                            size_t rows_per_rank, const void *d_gathered, uint8_t *flags);
+/* Any shard plan: rank r's rows hold transactions [rank_lo[r*nblocks+b], rank_hi[r*nblocks+b])
+ * of every block b in block order (FGV_SHARD_SKIP = none of block b); the ranks' ranges of a
+ * block must tile [0, ntx[b]). */
+int fgv_finalize_flags_dev_plan(fgv_ctx *ctx, size_t nblocks, const size_t *ntx, uint32_t world,
+                                size_t rows_per_rank, const uint32_t *rank_lo, const uint32_t *rank_hi,
+                                const void *d_gathered, uint8_t *flags);
 
 /* ------------------------------------------------------------------------------ MVCC */
 

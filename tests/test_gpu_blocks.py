@@ -171,8 +171,8 @@ def test_sharded_validation_matches_single(shards):
     eng.close()
 
 
-@pytest.mark.parametrize("shards", [1, 2, 3, 8])
-def test_device_sharded_protocol(shards):
+@pytest.mark.parametrize("shards,mode", [(1, "tx"), (2, "tx"), (3, "tx"), (8, "tx"), (2, "block"), (3, "block")])
+def test_device_sharded_protocol(shards, mode):
     """fgv_validate_shard_dev per rank into the rank-major gathered buffer (what
     all_gather_into_tensor produces) + fgv_finalize_flags_dev == whole-batch flags == oracle."""
     import torch
@@ -186,14 +186,15 @@ def test_device_sharded_protocol(shards):
     blks = [b1, b2, b3]
     ntx = np.array([40, 3, 29], dtype=np.int64)
     eng = _engine_for(net)
-    rows = shard.padded_rows(ntx, shards)
+    plan = shard.plan(ntx, shards, mode)
+    rows = shard.plan_rows(*plan)
     recv = torch.zeros((shards * rows, shard.REC), dtype=torch.uint8, device="cuda")
     batch = eng.block_batch(blks)
     for r in range(shards):
-        lo, hi = shard.shard_ranges(ntx, r, shards)
+        lo, hi = plan[0][r], plan[1][r]
         nt = eng.validate_shard_dev(batch, lo, hi, recv[r * rows:].data_ptr(), rows)
-        assert list(nt) == list(ntx)
-    flags = eng.finalize_flags_dev(ntx, shards, rows, recv.data_ptr())
+        assert list(nt) == [0 if lo[b] == shard.SKIP else ntx[b] for b in range(len(ntx))]
+    flags = eng.finalize_flags_dev(ntx, shards, rows, recv.data_ptr(), plan=None if mode == "tx" else plan)
     exp = _oracle(net, blks)
     assert list(flags) == exp[0] + exp[1] + exp[2]
     assert np.array_equal(flags, np.concatenate(eng.validate_blocks(blks)))

@@ -4,6 +4,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -32,26 +33,29 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, ntx, seed, q):
+def _worker(rank, world, port, ntx, seed, mode, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     full = _records(seed, ntx)
-    lo, hi = shard.shard_ranges(ntx, rank, world)
+    plan = shard.plan(ntx, world, mode)
+    cnt = shard.plan_counts(*plan)
+    lo = np.where(cnt[rank] > 0, plan[0][rank], 0).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(ntx)])
-    local = np.concatenate([full[offs[b] + lo[b]: offs[b] + hi[b]] for b in range(len(ntx))])
-    got = shard.allgather_results(local, ntx, world)
+    local = np.concatenate([full[offs[b] + lo[b]: offs[b] + lo[b] + cnt[rank, b]] for b in range(len(ntx))])
+    got = shard.allgather_results(local, ntx, world, plan_=plan)
     flags = _lib.finalize_flags(ntx, got)
     q.put((rank, bool(np.array_equal(got, full)), flags.tolist()))
     dist.destroy_process_group()
 
 
-def test_allgather_finalize_world2():
+@pytest.mark.parametrize("mode", ["tx", "block"])
+def test_allgather_finalize_world2(mode):
     ntx = [37, 0, 64, 5]
     world, seed = 2, 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, ntx, seed, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ntx, seed, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=120) for _ in range(world)]
