@@ -115,11 +115,19 @@ def run_block(args, world, rank, local, dev):
         prev = blocks.header_hash(num, prev, envs)
     my_blocks = [m[0] for m in mine]
     my_labels = [m[1] for m in mine]
+    # The batch is every rank's blocks in rank order.  With at least one block per rank the
+    # shard plan is block-granular (below): a rank needs only its own blocks' bytes -- the
+    # others' results arrive as all-gathered records -- so only the labels (for the parity
+    # check) are exchanged; the per-block transaction split needs every block everywhere.
+    plan_mode = "block" if B >= 1 else "tx"
     if world > 1:
         allb = [None] * world
-        dist.all_gather_object(allb, (my_blocks, my_labels))
-        blks = [b for r in range(world) for b in allb[r][0]]
+        dist.all_gather_object(allb, (my_blocks if plan_mode == "tx" else None, my_labels))
         labels = [l for r in range(world) for l in allb[r][1]]
+        if plan_mode == "tx":
+            blks = [b for r in range(world) for b in allb[r][0]]
+        else:
+            blks = [my_blocks[i] if r == rank else b"" for r in range(world) for i in range(B)]
     else:
         blks, labels = my_blocks, my_labels
     log(f"[bench] rank {rank}: {len(blks)} blocks x {T} tx ready in {time.time() - t0:.1f}s")
@@ -133,13 +141,13 @@ def run_block(args, world, rank, local, dev):
     arena = torch.zeros(sum(sizes), dtype=torch.uint8, device=dev)
     dptr, o = [], 0
     for b, sz in zip(blks, sizes):
-        arena[o:o + len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+        if len(b):  # (other ranks' blocks are empty placeholders under the block plan)
+            arena[o:o + len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
         dptr.append(arena.data_ptr() + o)
         o += sz
     ntx = np.array([T] * len(blks), dtype=np.int64)
-    # contiguous transaction ranges of the batch, on block boundaries when there are at least
-    # as many blocks as ranks (fabric_amd/shard.py: a rank splits and parses only its blocks)
-    plan_mode = "block" if len(blks) >= world else "tx"
+    # contiguous transaction ranges of the batch (fabric_amd/shard.py): on block boundaries, a
+    # rank splits and parses only its own blocks
     plan = shard.plan(ntx, world, plan_mode)
     lo, hi = plan[0][rank], plan[1][rank]
     rows = shard.plan_rows(*plan)

@@ -780,15 +780,15 @@ static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint
     return FGV_ENOMEM;
   hipStream_t st = c->stream;
   HIP_TRY(hipMemcpyAsync(c->fz_meta.p, c->hb_fz.p, meta, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemsetAsync(c->fz_owner.p, 0, cap * 4, st));
-  HIP_TRY(hipMemsetAsync(c->fz_minblk.p, 0x7F, cap * 4, st));
-  HIP_TRY(hipMemsetAsync(c->fz_minvalid.p, 0xFF, cap * 4, st));
   const uint32_t n32 = (uint32_t)P, mask = (uint32_t)(cap - 1);
   const dim3 grid((n32 + 255) / 256), blk(256);
   const uint64_t *d_bstart = c->fz_meta.as<uint64_t>();
   const uint32_t *d_roff = reinterpret_cast<const uint32_t *>(d_bstart + nblocks + 1);
-  hipLaunchKernelGGL(k_fin_rows, grid, blk, 0, st, n32, d_bstart, (uint32_t)nblocks, W, (uint32_t)rows, d_roff,
-                     d_roff + wn, d_roff + 2 * wn, c->fz_rowmap.as<uint32_t>(), c->fz_blkof.as<uint32_t>());
+  // (k_fin_rows also resets the cap-slot txid table)
+  hipLaunchKernelGGL(k_fin_rows, dim3((uint32_t)((std::max<size_t>(P, cap) + 255) / 256)), blk, 0, st, n32, d_bstart,
+                     (uint32_t)nblocks, W, (uint32_t)rows, d_roff, d_roff + wn, d_roff + 2 * wn,
+                     c->fz_rowmap.as<uint32_t>(), c->fz_blkof.as<uint32_t>(), (uint32_t)cap, c->fz_owner.as<uint32_t>(),
+                     c->fz_minblk.as<int32_t>(), c->fz_minvalid.as<uint32_t>());
   hipLaunchKernelGGL(k_fin_index, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
                      c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask,
                      c->fin_seed);

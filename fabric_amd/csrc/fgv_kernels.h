@@ -97,7 +97,7 @@ __global__ void k_mv_flags(uint32_t ntx, const uint8_t *part, const uint8_t *st,
 // finalize.hip -- batch txid index + markTXIdDuplicates over gathered fgv_tx_result records
 __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, uint32_t W, uint32_t rows,
                            const uint32_t *roff, const uint32_t *rlo, const uint32_t *rcnt, uint32_t *rowmap,
-                           uint32_t *blkof);
+                           uint32_t *blkof, uint32_t cap, uint32_t *owner, int32_t *minblk, uint32_t *minvalid);
 __global__ void k_fin_index(uint32_t P, const uint8_t *recs, const uint32_t *rowmap, const uint32_t *blkof,
                             uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed);
 __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *rowmap, const uint32_t *blkof,

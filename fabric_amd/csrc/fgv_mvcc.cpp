@@ -10,6 +10,8 @@
 // internal/version/version.go:82-90 (AreSame: nil == nil).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <cstring>
 #include <functional>
 #include <string>
 #include <unordered_map>
@@ -34,15 +36,22 @@ struct MvWrite {
 };
 struct MvTx {
   uint8_t code = 0;  // 0 participates; 16 / 255 decided here; 0xFD unsupported; 0xFF skipped
-  std::vector<MvRead> reads;
+  bool new_ns = false;             // names a namespace not yet registered (resolved serially)
+  std::vector<MvRead> reads;       // (vectors keep their capacity across blocks)
   std::vector<MvWrite> writes;
+  std::vector<uint32_t> rns, wns;  // namespace id of each read / write
+  uint64_t wbytes = 0;
 };
 
 constexpr uint8_t MV_UNSUP = 0xFD, MV_SKIP = 0xFF;
 
 // GetActionFromEnvelope + TxRwSet.FromProtoBytes for one committer-valid transaction
 void mv_parse(Span d, MvTx &T) {
-  T = MvTx();
+  T.code = 0;
+  T.new_ns = false;
+  T.reads.clear();
+  T.writes.clear();
+  T.wbytes = 0;
   VEnvelope env;
   VPayload pl;
   VHeader hdr;
@@ -68,9 +77,11 @@ void mv_parse(Span d, MvTx &T) {
   VTxRwSet rw;
   if (!pbw::decode(cca.results.p, cca.results.n, rw)) { T.code = 255; return; }
   bool unsup = false;
+  static thread_local std::vector<VKVRead> reads;
+  static thread_local std::vector<VKVWrite> writes;
   for (VNsRwSet &ns : rw.ns) {
-    std::vector<VKVRead> reads;
-    std::vector<VKVWrite> writes;
+    reads.clear();
+    writes.clear();
     VKVRWSet kv;
     kv.reads = &reads;
     kv.writes = &writes;
@@ -82,7 +93,10 @@ void mv_parse(Span d, MvTx &T) {
     }
     if (kv.nrq || kv.nmeta) unsup = true;  // phantom checks / metadata writes: not modelled
     for (const VKVRead &r : reads) T.reads.push_back(MvRead{ns.ns, r.key, r.has_ver, r.ver.block, r.ver.tx});
-    for (const VKVWrite &w : writes) T.writes.push_back(MvWrite{ns.ns, w.key, w.is_delete});
+    for (const VKVWrite &w : writes) {
+      T.writes.push_back(MvWrite{ns.ns, w.key, w.is_delete});
+      T.wbytes += w.key.n;
+    }
   }
   if (unsup) T.code = MV_UNSUP;
 }
@@ -95,6 +109,7 @@ struct fgv_mvcc_state {
   DevBuf tbl, arena, top;
   DevBuf reads, writes, rtags, wtags, btbl, wslot, rslot, rbeg, part, bad, st, undec, pend, npend, flags, lbytes, lkeys;
   std::vector<MvTx> txs;
+  HostBuf hreads, hwrites, hmeta;  // pinned staging of the MvKey arrays, rbeg and part
   uint32_t last_rounds = 0;
 };
 
@@ -104,7 +119,36 @@ void fgv_mvcc_free(fgv_mvcc_state *M) {
                  &M->rslot, &M->rbeg, &M->part, &M->bad, &M->st, &M->undec, &M->pend, &M->npend, &M->flags,
                  &M->lbytes, &M->lkeys};
   for (auto *b : d) b->release();
+  M->hreads.release();
+  M->hwrites.release();
+  M->hmeta.release();
   delete M;
+}
+
+// namespace ids of one parsed transaction, read-only on the map (parallel phase): a span equal
+// to the previous one reuses its id; an unknown namespace sets new_ns
+static void mv_resolve_ns(const fgv_mvcc_state *M, MvTx &T) {
+  T.rns.resize(T.reads.size());
+  T.wns.resize(T.writes.size());
+  Span last{nullptr, 0};
+  uint32_t last_id = 0;
+  bool have = false;
+  auto id_of = [&](const Span &s, uint32_t &id) {
+    if (have && s.n == last.n && (s.n == 0 || memcmp(s.p, last.p, s.n) == 0)) {
+      id = last_id;
+      return true;
+    }
+    auto it = M->ns_ids.find(s.str());
+    if (it == M->ns_ids.end()) return false;
+    last = s;
+    last_id = id = it->second;
+    have = true;
+    return true;
+  };
+  for (size_t k = 0; k < T.reads.size(); k++)
+    if (!id_of(T.reads[k].ns, T.rns[k])) T.new_ns = true;
+  for (size_t k = 0; k < T.writes.size(); k++)
+    if (!id_of(T.writes[k].ns, T.wns[k])) T.new_ns = true;
 }
 
 static bool ns_lookup(fgv_mvcc_state *M, const Span &s, bool create, uint32_t &id) {
@@ -200,43 +244,68 @@ int fgv_mvcc_validate_block(fgv_ctx *c, const uint8_t *block, size_t len, const 
     HIP_TRY(hipMemcpyAsync(c->blk_arena.p, block, len, hipMemcpyHostToDevice, c->stream));
     dblk = c->blk_arena.as<uint8_t>();
   }
-  // --- host: rwsets of committer-valid txs (parallel)
+  // --- host: rwsets of committer-valid txs, namespace ids (parallel; the map is read-only)
   M->txs.resize(ntx);
   fgv_parallel_for(c->blk, ntx, [&](size_t i) {
+    MvTx &T = M->txs[i];
     if (flags[i] != 0) {
-      M->txs[i] = MvTx();
-      M->txs[i].code = MV_SKIP;
+      T.code = MV_SKIP;
       return;
     }
-    mv_parse(envs[i], M->txs[i]);
+    mv_parse(envs[i], T);
+    if (T.code == 0) mv_resolve_ns(M, T);
   });
-  auto dev = [&](const Span &s) { return (uint64_t)(uintptr_t)dblk + (uint64_t)(s.p - block); };
-  std::vector<MvKey> reads, writes;
-  std::vector<uint32_t> rbeg(ntx + 1, 0);
-  std::vector<uint8_t> part(ntx, 0);
+  // serial: unsupported txs, first sightings of a namespace (rare), read / write offsets
+  if (!M->hmeta.ensure((ntx + 1) * 4 * 2 + ntx + 64)) return FGV_ENOMEM;
+  uint32_t *rbeg = M->hmeta.as<uint32_t>(), *wbeg = rbeg + ntx + 1;
+  uint8_t *part = reinterpret_cast<uint8_t *>(wbeg + ntx + 1);
+  size_t nr = 0, nw = 0, wbytes = 0;
   for (size_t i = 0; i < ntx; i++) {
     MvTx &T = M->txs[i];
-    rbeg[i] = (uint32_t)reads.size();
+    rbeg[i] = (uint32_t)nr;
+    wbeg[i] = (uint32_t)nw;
+    part[i] = 0;
     if (T.code == MV_UNSUP) return FGV_EUNSUPPORTED;
     if (T.code != 0) continue;
+    if (T.new_ns) {
+      for (size_t k = 0; k < T.reads.size(); k++)
+        if (!ns_lookup(M, T.reads[k].ns, true, T.rns[k])) return FGV_EUNSUPPORTED;
+      for (size_t k = 0; k < T.writes.size(); k++)
+        if (!ns_lookup(M, T.writes[k].ns, true, T.wns[k])) return FGV_EUNSUPPORTED;
+    }
     part[i] = 1;
-    for (const MvRead &r : T.reads) {
-      uint32_t ns;
-      if (!ns_lookup(M, r.ns, true, ns) || r.key.n > 0xffff) return FGV_EUNSUPPORTED;
-      reads.push_back(MvKey{dev(r.key), r.key.n, ns, (uint32_t)i, r.has_ver ? 1u : 0u, r.blk, r.txn});
-    }
-    for (const MvWrite &w : T.writes) {
-      uint32_t ns;
-      if (!ns_lookup(M, w.ns, true, ns) || w.key.n > 0xffff) return FGV_EUNSUPPORTED;
-      writes.push_back(MvKey{dev(w.key), w.key.n, ns, (uint32_t)i, w.del ? 1u : 0u, 0, 0});
-    }
+    nr += T.reads.size();
+    nw += T.writes.size();
+    wbytes += T.wbytes;
   }
-  rbeg[ntx] = (uint32_t)reads.size();
-  const size_t nr = reads.size(), nw = writes.size();
+  rbeg[ntx] = (uint32_t)nr;
+  wbeg[ntx] = (uint32_t)nw;
+  // parallel: the MvKey arrays, straight into pinned staging
+  if (!M->hreads.ensure(std::max<size_t>(nr, 1) * sizeof(MvKey)) ||
+      !M->hwrites.ensure(std::max<size_t>(nw, 1) * sizeof(MvKey)))
+    return FGV_ENOMEM;
+  MvKey *hr = M->hreads.as<MvKey>(), *hw = M->hwrites.as<MvKey>();
+  std::atomic<bool> too_long{false};
+  fgv_parallel_for(c->blk, ntx, [&](size_t i) {
+    const MvTx &T = M->txs[i];
+    if (!part[i]) return;
+    const uint64_t base = (uint64_t)(uintptr_t)dblk - (uint64_t)(uintptr_t)block;
+    MvKey *r = hr + rbeg[i], *w = hw + wbeg[i];
+    for (size_t k = 0; k < T.reads.size(); k++) {
+      const MvRead &x = T.reads[k];
+      if (x.key.n > 0xffff) too_long = true;
+      r[k] = MvKey{base + (uint64_t)(uintptr_t)x.key.p, x.key.n, T.rns[k], (uint32_t)i, x.has_ver ? 1u : 0u, x.blk,
+                   x.txn};
+    }
+    for (size_t k = 0; k < T.writes.size(); k++) {
+      const MvWrite &x = T.writes[k];
+      if (x.key.n > 0xffff) too_long = true;
+      w[k] = MvKey{base + (uint64_t)(uintptr_t)x.key.p, x.key.n, T.wns[k], (uint32_t)i, x.del ? 1u : 0u, 0, 0};
+    }
+  });
+  if (too_long) return FGV_EUNSUPPORTED;
   uint32_t bcap = 1024;
   while (bcap < 2 * nw) bcap <<= 1;
-  size_t wbytes = 0;
-  for (const MvKey &w : writes) wbytes += w.len;
   if (commit && ((M->nkeys + nw) * 10 > M->cap * 7 || M->arena_used + wbytes > M->arena_cap)) return FGV_ENOMEM;
   if (!M->reads.ensure(std::max<size_t>(nr, 1) * sizeof(MvKey)) || !M->writes.ensure(std::max<size_t>(nw, 1) * sizeof(MvKey)) ||
       !M->rtags.ensure(std::max<size_t>(nr, 1) * 8) || !M->wtags.ensure(std::max<size_t>(nw, 1) * 8) ||
@@ -246,10 +315,10 @@ int fgv_mvcc_validate_block(fgv_ctx *c, const uint8_t *block, size_t len, const 
       !M->npend.ensure(4) || !M->flags.ensure(ntx + 1))
     return FGV_ENOMEM;
   hipStream_t s = c->stream;
-  if (nr) HIP_TRY(hipMemcpyAsync(M->reads.p, reads.data(), nr * sizeof(MvKey), hipMemcpyHostToDevice, s));
-  if (nw) HIP_TRY(hipMemcpyAsync(M->writes.p, writes.data(), nw * sizeof(MvKey), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(M->rbeg.p, rbeg.data(), (ntx + 1) * 4, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(M->part.p, part.data(), ntx, hipMemcpyHostToDevice, s));
+  if (nr) HIP_TRY(hipMemcpyAsync(M->reads.p, hr, nr * sizeof(MvKey), hipMemcpyHostToDevice, s));
+  if (nw) HIP_TRY(hipMemcpyAsync(M->writes.p, hw, nw * sizeof(MvKey), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(M->rbeg.p, rbeg, (ntx + 1) * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(M->part.p, part, ntx, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(M->bad.p, 0, ntx + 1, s));
   HIP_TRY(hipMemsetAsync(M->btbl.p, 0, bcap * sizeof(BlkSlot), s));
   HIP_TRY(hipEventRecord(c->ev[0], s));

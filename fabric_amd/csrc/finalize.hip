@@ -71,11 +71,17 @@ __device__ inline int64_t tab_find(const uint32_t k[8], uint64_t h, const uint32
 }  // namespace
 
 // rank r holds transactions [rlo[r][b], rlo[r][b] + rcnt[r][b]) of block b, at its rows from
-// roff[r][b] (any shard plan whose ranges tile every block)
+// roff[r][b] (any shard plan whose ranges tile every block).  Also resets the txid table
+// (slots [0, cap)): the grid covers max(P, cap).
 __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, uint32_t W, uint32_t rows,
                            const uint32_t *roff, const uint32_t *rlo, const uint32_t *rcnt, uint32_t *rowmap,
-                           uint32_t *blkof) {
+                           uint32_t *blkof, uint32_t cap, uint32_t *owner, int32_t *minblk, uint32_t *minvalid) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < cap) {
+    owner[p] = 0u;
+    minblk[p] = 0x7F7F7F7F;
+    minvalid[p] = 0xFFFFFFFFu;
+  }
   if (p >= P) return;
   uint32_t lo = 0, hi = nb;  // last b with blk_start[b] <= p
   while (hi - lo > 1) {

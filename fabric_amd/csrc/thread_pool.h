@@ -23,10 +23,11 @@ struct ThreadPool {
   size_t active = 0;
   std::atomic<uint64_t> gen{0};
   bool stop = false;
-  // A worker that finished a run spins this long for the next one before sleeping: the
-  // committer issues runs back to back within a call, and a futex wake-up of 16 threads
-  // costs tens of microseconds.
-  static constexpr auto kSpin = std::chrono::microseconds(200);
+  // A worker that finished a run may spin this long for the next one before sleeping (a
+  // futex wake-up of 16 threads costs tens of microseconds).  Off: the committer's device
+  // path issues one run per call, and spinning threads only compete with the caller when
+  // the host's CPU share is tight.
+  static constexpr auto kSpin = std::chrono::microseconds(0);
   explicit ThreadPool(unsigned n) {
     for (unsigned i = 0; i < n; i++)
       th.emplace_back([this] {
