@@ -29,10 +29,11 @@ import torch
 import torch.distributed as dist
 
 METRIC = "ECDSA-P256 verifies/sec + validated tx/sec per block at 1/2/4/8 MI355X"
-# 32x32->64 multiply-add products per verify in the comb: 65 mixed additions
-# (32 signed 8-bit windows per scalar, ~1 carry window in 2) x (8 field mults x 64 + 3 squarings
-# x 36 products) + the projective x-check (3 x 64)
-PRODUCTS_POINT = 65 * (8 * 64 + 3 * 36) + 3 * 64
+# 32x32->64 multiply-add products per verify in the comb: 49 terms (16 signed
+# 16-bit generator windows + 32 signed 8-bit key windows + the two carry windows, each nonzero
+# about every other verify), the first one loaded, so 48 mixed additions x (8 field mults x 64
+# + 3 squarings x 36 products) + the projective x-check (3 x 64)
+PRODUCTS_POINT = 48 * (8 * 64 + 3 * 36) + 3 * 64
 # chip-wide v_mad_u64_u32 issue rate measured by tools/valu_peak.hip (profiles/round1_valu_peak.json)
 PEAK_MAD_PER_S = float(os.environ.get("FGV_PEAK_MAD", "3.106e13"))
 
@@ -173,6 +174,10 @@ def run_block(args, world, rank, local, dev):
             th = threading.Thread(target=verify_mine)
             th.start()
         nt = eng.validate_shard_dev(batch, lo, hi, send.data_ptr(), rows)
+        if not args.no_presplit:
+            # the next batch's framing walk (here: the same blocks) overlaps this batch's
+            # all-gather + finalize, as a peer splits block k+1 while block k commits
+            eng.presplit(batch, lo, hi)
         if world > 1:
             shard.allgather_device(send, recv)
         f = eng.finalize_flags_dev(ntx, world, rows, recv.data_ptr(), out=flags_out, plan=plan)
@@ -231,7 +236,8 @@ def run_block(args, world, rank, local, dev):
                config=dict(workload=spec["desc"].format(T=T),
                            blocks_per_step=len(blks), tx_per_block=T, global_batch=len(blks) * T,
                            parallelism=f"{plan_mode}-range-shard{world}+allgather(68B/tx)",
-                           parse="host" if args.host_parse else "device"),
+                           parse="host" if args.host_parse else "device",
+                           block_split="serial" if args.no_presplit else "pipelined (fgv_presplit)"),
                verifies_per_s=round(all_verifies / el, 1), parity_vs_labels=ok,
                stage_ms=dict(sha=round(acc["sha"] / args.steps, 4), prep=round(acc["prep"] / args.steps, 4),
                              point=round(acc["point"] / args.steps, 4)),
@@ -432,6 +438,7 @@ def main():
     ap.add_argument("--per-gpu", type=int, default=131072)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--host-parse", action="store_true", help="parse transactions on host threads (A/B)")
+    ap.add_argument("--no-presplit", action="store_true", help="walk each batch's framing inside its validation call (A/B)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

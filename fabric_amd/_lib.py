@@ -23,6 +23,7 @@ EXPORTED = [
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
+    "fgv_presplit", "fgv_last_presplit",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode",
 ]
@@ -104,6 +105,8 @@ def load():
         L.fgv_finalize_flags.argtypes = [sz, vp, vp, vp]
         L.fgv_validate_shard_dev.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
         L.fgv_finalize_flags_dev.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp]
+        L.fgv_presplit.argtypes = [vp, sz, vp, vp, vp, vp]
+        L.fgv_last_presplit.argtypes = [vp]
         L.fgv_finalize_flags_dev_plan.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
@@ -306,6 +309,18 @@ class Engine:
         _check(self._L.fgv_validate_shard_dev(self._h, batch.nb, batch.ptrs, batch.lens, batch.dptr, _ptr(lo),
                                               _ptr(hi), ctypes.c_void_p(d_results), cap, batch.ntx))
         return np.ctypeslib.as_array(batch.ntx).astype(np.uint64)
+
+    def presplit(self, batch, tx_lo=None, tx_hi=None):
+        """fgv_presplit: walk the batch's block framing on a background host thread for the
+        next validate_shard_dev of the same batch (block_batch(...) keeps the buffers alive)."""
+        assert isinstance(batch, _BlockBatch)
+        lo = None if tx_lo is None else np.ascontiguousarray(tx_lo, dtype=np.uint32)
+        hi = None if tx_hi is None else np.ascontiguousarray(tx_hi, dtype=np.uint32)
+        _check(self._L.fgv_presplit(self._h, batch.nb, batch.ptrs, batch.lens, None if lo is None else _ptr(lo),
+                                    None if hi is None else _ptr(hi)))
+
+    def last_presplit(self):
+        return bool(self._L.fgv_last_presplit(self._h))
 
     def finalize_flags_dev(self, ntx, world, rows_per_rank, d_gathered, out=None, plan=None):
         """fgv_finalize_flags_dev over world x rows_per_rank gathered records at d_gathered;

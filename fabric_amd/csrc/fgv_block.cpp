@@ -294,9 +294,93 @@ struct DevImage {
   }
 };
 
+// Envelope spans of a batch (the block data framing walk, the only host-side parse of the
+// device path) and the envelope table k_bd_parse reads: per transaction (block, offset, len).
+struct SplitOut {
+  std::vector<uint32_t> lo, hi;
+  std::vector<size_t> ntx, first;
+  size_t total = 0;
+};
+
+// A batch split ahead of its fgv_validate_shard_dev call (fgv_presplit): a peer walks block
+// k+1's framing while block k validates.  The result is used only by a call whose batch --
+// block addresses, lengths and shard ranges -- is the one split here.  One persistent worker
+// thread (a thread start would cost more than the overlap gains).
+static int split_batch(ThreadPool &pool, size_t nblocks, const uint8_t *const *h_blocks, const size_t *lens,
+                       const uint32_t *tx_lo, const uint32_t *tx_hi, SplitOut &o, HostBuf &et);
+struct PreSplit {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool req = false, done = false, stop = false;
+  bool active = false;  // requested and neither used nor discarded (owner thread only)
+  int device = 0;
+  std::vector<const uint8_t *> blocks;
+  std::vector<size_t> lens;
+  std::vector<uint32_t> lo_in, hi_in;
+  int rc = FGV_OK;
+  SplitOut out;
+  HostBuf et;  // pinned envelope table, swapped with the context's on use
+  std::unique_ptr<ThreadPool> pool;
+  bool matches(size_t nb, const uint8_t *const *b, const size_t *l, const uint32_t *lo, const uint32_t *hi) const {
+    if (nb != blocks.size() || (lo == nullptr) != lo_in.empty() || (hi == nullptr) != hi_in.empty()) return false;
+    for (size_t i = 0; i < nb; i++)
+      if (b[i] != blocks[i] || l[i] != lens[i] || (lo && lo[i] != lo_in[i]) || (hi && hi[i] != hi_in[i])) return false;
+    return true;
+  }
+  void worker() {
+    bool dev_set = false;
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || req; });
+      if (stop) return;
+      req = false;
+      lk.unlock();
+      int r = FGV_OK;
+      if (!dev_set) r = hipSetDevice(device) == hipSuccess ? FGV_OK : FGV_EDEVICE;  // (pinned staging)
+      dev_set = r == FGV_OK;
+      if (r == FGV_OK)
+        r = split_batch(*pool, blocks.size(), blocks.data(), lens.data(), lo_in.empty() ? nullptr : lo_in.data(),
+                        hi_in.empty() ? nullptr : hi_in.data(), out, et);
+      lk.lock();
+      rc = r;
+      done = true;
+      cv.notify_all();
+    }
+  }
+  void start() {
+    if (!th.joinable()) {
+      pool.reset(new ThreadPool(8));
+      th = std::thread([this] { worker(); });
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    done = false;
+    req = true;
+    active = true;
+    cv.notify_all();
+  }
+  void join() {  // wait for the requested split (if any); the result stays readable
+    if (!active) return;
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done; });
+    active = false;
+  }
+  ~PreSplit() {
+    join();
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+      cv.notify_all();
+    }
+    if (th.joinable()) th.join();
+    et.release();
+  }
+};
+
 struct fgv_block_state {
   Channel ch;
   ThreadPool pool;
+  PreSplit pre;
   // per-call scratch
   std::vector<TxRec> recs;
   // device image of `ch`, rebuilt when the channel model changes
@@ -1015,6 +1099,62 @@ __global__ void k_bd_fold(uint32_t ntx, const DevTx *txs, const uint64_t *bases,
                           const DevJobIdx *jobs, const uint32_t *totals, const uint8_t *digests,
                           const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags);
 
+// host: split each block into envelope spans (tag / length walk of the block data framing)
+// and write the envelope table into `et`
+static int split_batch(ThreadPool &pool, size_t nblocks, const uint8_t *const *h_blocks, const size_t *lens,
+                       const uint32_t *tx_lo, const uint32_t *tx_hi, SplitOut &o, HostBuf &et) {
+  std::vector<std::vector<Span>> envs(nblocks);
+  std::atomic<bool> bad{false};
+  pool.run(nblocks, [&](size_t b) {
+    if (tx_lo && tx_lo[b] == FGV_SHARD_SKIP) return;  // another rank's block: not parsed
+    VBlock blk;
+    if (!pbw::decode(h_blocks[b], lens[b], blk)) { bad = true; return; }
+    envs[b] = std::move(blk.data.data);
+  });
+  if (bad) return FGV_EINVAL;
+  o.lo.assign(nblocks, 0);
+  o.hi.assign(nblocks, 0);
+  o.ntx.assign(nblocks, 0);
+  o.first.assign(nblocks, 0);
+  o.total = 0;
+  for (size_t b = 0; b < nblocks; b++) {
+    o.ntx[b] = envs[b].size();  // 0 for a skipped block
+    o.lo[b] = tx_lo ? std::min<uint32_t>(tx_lo[b], (uint32_t)envs[b].size()) : 0;
+    o.hi[b] = tx_hi ? std::min<uint32_t>(tx_hi[b], (uint32_t)envs[b].size()) : (uint32_t)envs[b].size();
+    if (o.hi[b] < o.lo[b]) o.hi[b] = o.lo[b];
+    o.first[b] = o.total;
+    o.total += o.hi[b] - o.lo[b];
+    if (lens[b] > 0xFFFFFFFFull) return FGV_EINVAL;
+  }
+  if (o.total >= 0x7FFFFFFFull) return FGV_EINVAL;
+  if (!et.ensure(o.total * 4 * BD_ENV_WORDS + 64)) return FGV_ENOMEM;
+  uint32_t *e = et.as<uint32_t>();
+  for (size_t b = 0; b < nblocks; b++) {  // writes only (the spans are already known)
+    uint32_t *w = e + BD_ENV_WORDS * o.first[b];
+    for (uint32_t i = o.lo[b]; i < o.hi[b]; i++, w += BD_ENV_WORDS) {
+      w[0] = (uint32_t)b;
+      w[1] = (uint32_t)(envs[b][i].p - h_blocks[b]);
+      w[2] = envs[b][i].n;
+    }
+  }
+  return FGV_OK;
+}
+
+int fgv_block_presplit(fgv_block_state *S, int device, size_t nblocks, const uint8_t *const *h_blocks,
+                       const size_t *lens, const uint32_t *tx_lo, const uint32_t *tx_hi) {
+  PreSplit &P = S->pre;
+  P.join();  // an earlier pre-split nobody used
+  P.device = device;
+  P.blocks.assign(h_blocks, h_blocks + nblocks);
+  P.lens.assign(lens, lens + nblocks);
+  P.lo_in.clear();
+  P.hi_in.clear();
+  if (tx_lo) P.lo_in.assign(tx_lo, tx_lo + nblocks);
+  if (tx_hi) P.hi_in.assign(tx_hi, tx_hi + nblocks);
+  P.start();
+  return FGV_OK;
+}
+
 int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
                            const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                            const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out) {
@@ -1026,48 +1166,36 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
     if (rc) return rc;
     S->dev_dirty = false;
   }
-  // --- host: split the blocks into envelope spans (tag / length walk)
-  std::vector<std::vector<Span>> envs(nblocks);
-  std::vector<uint32_t> lo(nblocks), hi(nblocks);
-  std::atomic<bool> bad{false};
-  S->pool.run(nblocks, [&](size_t b) {
-    if (tx_lo && tx_lo[b] == FGV_SHARD_SKIP) return;  // another rank's block: not parsed
-    VBlock blk;
-    if (!pbw::decode(h_blocks[b], lens[b], blk)) { bad = true; return; }
-    envs[b] = std::move(blk.data.data);
-  });
-  if (bad) return FGV_EINVAL;
-  size_t total = 0;
-  std::vector<size_t> first(nblocks);
-  for (size_t b = 0; b < nblocks; b++) {
-    ntx_out[b] = envs[b].size();  // 0 for a skipped block
-    lo[b] = tx_lo ? std::min<uint32_t>(tx_lo[b], (uint32_t)envs[b].size()) : 0;
-    hi[b] = tx_hi ? std::min<uint32_t>(tx_hi[b], (uint32_t)envs[b].size()) : (uint32_t)envs[b].size();
-    if (hi[b] < lo[b]) hi[b] = lo[b];
-    first[b] = total;
-    total += hi[b] - lo[b];
-    if (lens[b] > 0xFFFFFFFFull) return FGV_EINVAL;
+  // --- host: the batch's envelope spans, split ahead by fgv_presplit or here
+  SplitOut so;
+  bool presplit = false;
+  if (S->pre.active) {
+    S->pre.join();  // (the worker is idle from here on)
+    if (S->pre.rc == FGV_OK && S->pre.matches(nblocks, h_blocks, lens, tx_lo, tx_hi)) {
+      so = std::move(S->pre.out);
+      std::swap(c->hb_env, S->pre.et);
+      presplit = true;
+    }
   }
-  if (total > res_cap || total >= 0x7FFFFFFFull) return FGV_EINVAL;
+  if (!presplit) {
+    int rc = split_batch(S->pool, nblocks, h_blocks, lens, tx_lo, tx_hi, so, c->hb_env);
+    if (rc) return rc;
+  }
+  for (size_t b = 0; b < nblocks; b++) ntx_out[b] = so.ntx[b];
+  const size_t total = so.total;
+  if (total > res_cap) return FGV_EINVAL;
   c->n_sha_jobs = c->n_sha_blocks = c->n_verifies = 0;
+  c->last_presplit = presplit;
   if (total == 0) return FGV_OK;
   const uint32_t N = (uint32_t)total;
-  if (!c->hb_env.ensure(total * 4 * BD_ENV_WORDS) || !c->hb_bases.ensure(nblocks * 8) || !c->hb_misc.ensure(64) ||
+  if (!c->hb_bases.ensure(nblocks * 8) || !c->hb_misc.ensure(64) ||
       !c->bd_env.ensure(total * 4 * BD_ENV_WORDS) || !c->bd_bases.ensure(nblocks * 8) || !c->bd_misc.ensure(64) ||
       !c->bd_tx.ensure(total * sizeof(DevTx)) || !c->bd_ident.ensure(total * BD_OCC * 4) ||
       !c->bd_jobs.ensure(total * sizeof(DevJobIdx)))
     return FGV_ENOMEM;
   uint32_t *et = c->hb_env.as<uint32_t>();
   uint64_t *bs = c->hb_bases.as<uint64_t>();
-  for (size_t b = 0; b < nblocks; b++) {  // writes only (the spans are already known)
-    bs[b] = (uint64_t)(uintptr_t)d_blocks[b];
-    uint32_t *o = et + BD_ENV_WORDS * first[b];
-    for (uint32_t i = lo[b]; i < hi[b]; i++, o += BD_ENV_WORDS) {
-      o[0] = (uint32_t)b;
-      o[1] = (uint32_t)(envs[b][i].p - h_blocks[b]);
-      o[2] = envs[b][i].n;
-    }
-  }
+  for (size_t b = 0; b < nblocks; b++) bs[b] = (uint64_t)(uintptr_t)d_blocks[b];
   c->t_host_parse = ms_since(t0);
   auto t1 = clk::now();
   hipStream_t st = c->stream;
@@ -1088,6 +1216,7 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_pay[0], 0));
   hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(64), 0, c->stream2, N, c->bd_env.as<uint32_t>(), dbs,
                      c->bj_dig.as<uint8_t>(), nblk);
+  HIP_TRY(hipEventRecord(c->ev_pay[3], c->stream2));  // payload digests ready
   hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, st, N, c->bd_env.as<uint32_t>(), dbs, ch, dtx,
                      misc + 5);
   // every other SHA-256 message is known after the parse: hashed on the second stream while
@@ -1118,11 +1247,14 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
                      reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + nv * 8),
                      reinterpret_cast<uint32_t *>(sp + nv * 12), reinterpret_cast<uint32_t *>(sp + nv * 16));
   HIP_TRY(hipGetLastError());
-  c->digests_ready = c->ev_pay[1];
+  c->digests_ready = c->ev_pay[3];
+  c->digests_ready2 = c->ev_pay[2];
   int rc = fgv_run_block_jobs_device(c, 0, nv, 0);
-  c->digests_ready = nullptr;
+  c->digests_ready = c->digests_ready2 = nullptr;
   if (rc) return rc;
-  HIP_TRY(hipStreamWaitEvent(st, c->ev_pay[1], 0));  // joined even when there is nothing to verify
+  // joined even when there is nothing to verify
+  HIP_TRY(hipStreamWaitEvent(st, c->ev_pay[3], 0));
+  HIP_TRY(hipStreamWaitEvent(st, c->ev_pay[2], 0));
   hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
                      c->bj_dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5);
   HIP_TRY(hipGetLastError());

@@ -23,13 +23,6 @@
 #include "fgv_internal.h"
 #include "fgv_kernels.h"
 
-static const uint8_t GX[32] = {0x6b, 0x17, 0xd1, 0xf2, 0xe1, 0x2c, 0x42, 0x47, 0xf8, 0xbc, 0xe6,
-                               0xe5, 0x63, 0xa4, 0x40, 0xf2, 0x77, 0x03, 0x7d, 0x81, 0x2d, 0xeb,
-                               0x33, 0xa0, 0xf4, 0xa1, 0x39, 0x45, 0xd8, 0x98, 0xc2, 0x96};
-static const uint8_t GY[32] = {0x4f, 0xe3, 0x42, 0xe2, 0xfe, 0x1a, 0x7f, 0x9b, 0x8e, 0xe7, 0xeb,
-                               0x4a, 0x7c, 0x0f, 0x9e, 0x16, 0x2b, 0xce, 0x33, 0x57, 0x6b, 0x31,
-                               0x5e, 0xce, 0xcb, 0xb6, 0x40, 0x68, 0x37, 0xbf, 0x51, 0xf5};
-
 // Build tables for `nk` keys (qxy: nk*16 limbs) into `tables` at `slots`.
 static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slots, uint32_t nk,
                         apoint_raw *tables, apoint_raw *tables28, uint8_t *ok) {
@@ -96,20 +89,20 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
       return fail(FGV_EDEVICE);
     c->n_cu = (uint32_t)ncu;
   }
-  if (!c->gtab.ensure(KT_BYTES) || !c->g_ok.ensure(16) || !c->gtab28.ensure(KT_BYTES) || !c->redo.ensure(64) ||
+  if (!c->gtab.ensure(GT_BYTES) || !c->g_ok.ensure(16) || !c->gtab28.ensure(GT_BYTES) || !c->redo.ensure(64) ||
       !c->ktab.ensure((size_t)c->key_slots * KT_BYTES) || !c->ktab28.ensure((size_t)c->key_slots * KT_BYTES) ||
       !c->key_ok.ensure(c->key_slots))
     return fail(FGV_ENOMEM);
-  // generator table = key table of G (same kernel)
-  uint32_t q[16], slot0 = 0;
-  be32_to_limbs(GX, q);
-  be32_to_limbs(GY, q + 8);
-  int rc = build_tables(c, q, &slot0, 1, c->gtab.as<apoint_raw>(), c->gtab28.as<apoint_raw>(), c->g_ok.as<uint8_t>());
-  if (rc) return fail(rc);
-  uint8_t gok = 0;
-  if (hipMemcpyAsync(&gok, c->g_ok.p, 1, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-      hipStreamSynchronize(c->stream) != hipSuccess || gok != 1)
-    return fail(FGV_EDEVICE);
+  // generator comb table (k_gtab), built once per context
+  {
+    DevBuf scr;
+    if (!scr.ensure((size_t)GT_THREADS * GT_CHUNK * sizeof(jpoint_raw))) return fail(FGV_ENOMEM);
+    hipLaunchKernelGGL(k_gtab, dim3((GT_THREADS + 63) / 64), dim3(64), 0, c->stream, c->gtab.as<apoint_raw>(),
+                       c->gtab28.as<apoint_raw>(), scr.as<jpoint_raw>());
+    const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(c->stream) == hipSuccess;
+    scr.release();
+    if (!ok) return fail(FGV_EDEVICE);
+  }
   *out = c;
   return FGV_OK;
 }
@@ -201,14 +194,16 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
                              const uint32_t *d_r, const uint8_t *d_dig, const uint32_t *d_dig_idx) {
   if (!c->d1.ensure((size_t)DIG_STRIDE * N)) return FGV_ENOMEM;
   HIP_TRY(hipStreamWaitEvent(c->stream, c->ev[3], 0));
-  if (c->digests_ready) HIP_TRY(hipStreamWaitEvent(c->stream, c->digests_ready, 0));  // k_bd_sha (stream2)
+  // the digests' producers, waited on directly (a chained cross-stream event adds ~30 us)
+  if (c->digests_ready) HIP_TRY(hipStreamWaitEvent(c->stream, c->digests_ready, 0));
+  if (c->digests_ready2) HIP_TRY(hipStreamWaitEvent(c->stream, c->digests_ready2, 0));
   HIP_TRY(hipEventRecord(c->ev[4], c->stream));
   hipLaunchKernelGGL(k_prep, dim3((N + 255) / 256), dim3(256), 0, c->stream, N, d_status, d_r,
                      c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>());
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[5], c->stream));
   // Persistent grid: one POINT_THREADS workgroup per CU.  Lanes per verify L (1, 2, 4, 8):
-  // k_point28 is VALU-bound; a wave carries 2 ceil(NWIN / L) window terms plus log2(L) tree
+  // k_point28 is VALU-bound; a wave carries ceil(NTERMS / L) comb terms plus log2(L) tree
   // additions (~1.5 mixed-addition equivalents each).  A SIMD running one wave issues at about
   // half rate (dependent-issue latency), two or more share it at full rate, so the batch time
   // is max(2 x wave, waves-per-SIMD x wave) on the busiest SIMD (measured on MI355X: C2
@@ -224,7 +219,7 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
     const uint64_t waves = ((uint64_t)N * l + 63) / 64;
     const uint64_t passes = (waves + slots - 1) / slots;  // the persistent grid's passes
     const uint64_t per_simd = std::max<uint64_t>(std::max<uint64_t>((waves + simds - 1) / simds, passes), 2);
-    const double cost = (double)per_simd * (2.0 * ((NWIN + l - 1) / l) + 1.5 * lg);
+    const double cost = (double)per_simd * ((double)((NTERMS + l - 1) / l) + 1.5 * lg);
     if (cost < best - 1e-9) { best = cost; L = l; }
   }
   if (forced >= 1 && forced <= POINT_LANES_MAX) L = (uint32_t)forced;
@@ -893,6 +888,16 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   }
   return FGV_OK;
 }
+
+int fgv_presplit(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens, const uint32_t *tx_lo,
+                 const uint32_t *tx_hi) {
+  if (!c || (nblocks && (!blocks || !lens))) return FGV_EINVAL;
+  if (nblocks == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_presplit(c->blk, c->device, nblocks, blocks, lens, tx_lo, tx_hi);
+}
+
+int fgv_last_presplit(fgv_ctx *c) { return c && c->last_presplit ? 1 : 0; }
 
 int fgv_finalize_flags_dev(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t world, size_t rows_per_rank,
                            const void *d_gathered, uint8_t *flags) {

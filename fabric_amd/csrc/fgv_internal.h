@@ -93,7 +93,8 @@ struct fgv_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // k_der + k_inv of a block batch, concurrent with SHA-256
   hipStream_t stream3 = nullptr;  // the device-parse committer's non-payload SHA-256 (k_bd_sha)
-  hipEvent_t ev_pay[3] = {};      // [0] batch start, [1] all digests ready (stream2), [2] k_bd_sha done
+  hipEvent_t ev_pay[4] = {};      // [0] batch start, [1] all digests ready (stream2), [2] k_bd_sha done (stream3),
+                                  // [3] k_bd_sha_payload done (stream2)
   hipEvent_t ev[8] = {};          // 0/1 sha, 2/3 inv, 4/5 prep, 6 point end, 7 fork
   std::mutex mu;
   // generator table (88 KB) and the public-key table cache
@@ -130,6 +131,8 @@ struct fgv_ctx {
   // device-resident committer path (blockdev.hip)
   bool stage_ran = false;
   hipEvent_t digests_ready = nullptr;  // k_prep waits for it when set (digests from another stream)
+  hipEvent_t digests_ready2 = nullptr;
+  bool last_presplit = false;  // the last device-parse call used a fgv_presplit result  // ... and for this one (a second producing stream)
   DevBuf bd_env, bd_bases, bd_tx, bd_ident, bd_jobs, bd_misc;
   HostBuf hb_env, hb_bases, hb_misc;
   double t_bd_split = 0, t_bd_pre = 0, t_bd_fold = 0;
@@ -177,6 +180,8 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
 int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, size_t dig_off = 0);
 void fgv_read_block_job_times(fgv_ctx *c);
 int fgv_block_set_parse_mode(fgv_block_state *S, int mode);
+int fgv_block_presplit(fgv_block_state *S, int device, size_t nblocks, const uint8_t *const *h_blocks,
+                       const size_t *lens, const uint32_t *tx_lo, const uint32_t *tx_hi);
 int fgv_block_parse_mode(fgv_block_state *S);
 // device-resident committer pass (fgv_block.cpp + blockdev.hip): records -> d_res (HBM).
 // Returns FGV_OK, FGV_EUNSUPPORTED, an error, or 1 = "a transaction exceeded a device

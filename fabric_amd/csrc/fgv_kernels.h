@@ -10,10 +10,22 @@
 #define TAB_K 128
 #define KT_ENTRIES (NWIN * TAB_K)           // 4224 affine points per table
 #define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 270,336 bytes per table
+// Generator comb (u1 * G): 16 windows of 16 bits with signed digits in [-2^15, 2^15 - 1], plus
+// a 17th window for the final carry (digit 0 or 1); 32768 entries per window (33.5 MB per copy,
+// MALL / HBM resident, built once per context by k_gtab).  17 G terms instead of 33.
+#define GWBITS 16
+#define NGWIN 17
+#define GT_K 32768
+#define GT_ENTRIES ((NGWIN - 1) * GT_K + 1)
+#define GT_BYTES ((size_t)GT_ENTRIES * 64)
+#define GT_CHUNK 32                   // consecutive entries per k_gtab thread
+#define GT_THREADS ((NGWIN - 1) * (GT_K / GT_CHUNK) + 1)
+#define NTERMS (NGWIN + NWIN)         // comb terms per verify: 17 G + 33 Q
+#define DIG_Q_OFF 40                  // digit array item: G digits int16 x 17 at 0, Q digits int8 x 33 here
 #define PREP_B 2                            // items per lane in the batched inversion
 #define POINT_THREADS 512   // 8 waves per CU (2 per SIMD): up to 256 VGPRs, no spills
 #define POINT_LANES_MAX 8    // lanes cooperating on one verify in k_point (partial sums + tree)
-#define DIG_STRIDE 80        // bytes per item of the digit array: (d1, d2) pairs for 33 windows
+#define DIG_STRIDE 80        // bytes per item of the digit array (G digits, then Q digits at DIG_Q_OFF)
 #define ST_PENDING 0xFF
 
 struct apoint_raw {  // affine point, Montgomery limbs (64 B, 16-B aligned)
@@ -29,6 +41,7 @@ struct jpoint_raw {  // key-table build scratch: Jacobian point + prefix product
 
 __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw *tables, apoint_raw *tables28,
                          jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys);
+__global__ void k_gtab(apoint_raw *tables, apoint_raw *tables28, jpoint_raw *scratch);
 __global__ void k_inv(uint32_t n, uint8_t *status, const uint32_t *key_slot, const uint8_t *key_ok,
                       const uint32_t *r_limbs, const uint32_t *s_limbs, uint32_t *w_out, uint32_t *w_scratch);
 __global__ void k_prep(uint32_t n, const uint8_t *status, const uint32_t *r_limbs, const uint32_t *w_in,

@@ -174,6 +174,82 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
   }
 }
 
+// ---------------------------------------------------------------- k_gtab
+// Generator comb table T_G[w][k-1] = k * 2^(16w) * G, w < 16, k = 1..32768, plus T_G[16][0] =
+// 2^256 * G (the carry window).  Thread t builds GT_CHUNK consecutive entries k0..k0+31 of one
+// window: B = 2^(16w) G by doublings, P = k0 * B by double-and-add, then P += B, and one
+// Montgomery-trick inversion for the chunk's Z's (complete formulas throughout: pt_add routes
+// P == B to a doubling).  Both the Montgomery-2^256 (k_point) and 2^280 (k_point28) forms.
+__constant__ static const uint32_t G_PLAIN[16] = {
+    0xD898C296u, 0xF4A13945u, 0x2DEB33A0u, 0x77037D81u, 0x63A440F2u, 0xF8BCE6E5u, 0xE12C4247u, 0x6B17D1F2u,
+    0x37BF51F5u, 0xCBB64068u, 0x6B315ECEu, 0x2BCE3357u, 0x7C0F9E16u, 0x8EE7EB4Au, 0xFE1A7F9Bu, 0x4FE342E2u};
+
+__global__ __launch_bounds__(64) void k_gtab(apoint_raw *__restrict__ tables, apoint_raw *__restrict__ tables28,
+                                             jpoint_raw *__restrict__ scratch) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= GT_THREADS) return;
+  constexpr uint32_t CPW = GT_K / GT_CHUNK;  // chunks per window
+  const uint32_t w = t / CPW, ch = t % CPW;
+  const uint32_t k0 = ch * GT_CHUNK + 1, cnt = w == NGWIN - 1 ? 1u : (uint32_t)GT_CHUNK;
+  fe gx, gy;
+  fe_load_c(gx, G_PLAIN);
+  fe_load_c(gy, G_PLAIN + 8);
+  jpoint b;
+  fe_to_mont(b.x, gx);
+  fe_to_mont(b.y, gy);
+  fe_set_one(b.z);
+  for (uint32_t i = 0; i < GWBITS * w; i++) pt_dbl(b, b);
+  // P = k0 * B, left to right
+  jpoint pk = b;
+  for (int bit = 30 - __builtin_clz(k0 | 1u); bit >= 0; bit--) {
+    jpoint t2 = pk;
+    pt_dbl(pk, t2);
+    if ((k0 >> bit) & 1u) {
+      t2 = pk;
+      pt_add(pk, t2, b);
+    }
+  }
+  jpoint_raw *scr = scratch + (size_t)t * GT_CHUNK;
+  const size_t e0 = (size_t)w * GT_K + (k0 - 1);
+  fe pref;
+  fe_set_one(pref);
+  for (uint32_t j = 0; j < cnt; j++) {
+    if (j > 0) {
+      jpoint t2 = pk;
+      pt_add(pk, t2, b);
+    }
+    fe_mul(pref, pref, pk.z);
+    store_fe(scr[j].x, pk.x);
+    store_fe(scr[j].y, pk.y);
+    store_fe(scr[j].z, pk.z);
+    store_fe(scr[j].pref, pref);
+  }
+  fe inv;
+  fe_inv(inv, pref);
+  fe c280;
+  fe_load_c(c280, C280_32);
+  for (int j = (int)cnt - 1; j >= 0; j--) {
+    fe X, Y, Z, prev, zinv, z2, z3, ax, ay;
+    load_fe(X, scr[j].x);
+    load_fe(Y, scr[j].y);
+    load_fe(Z, scr[j].z);
+    if (j > 0) load_fe(prev, scr[j - 1].pref);
+    else fe_set_one(prev);
+    fe_mul(zinv, inv, prev);
+    fe_mul(inv, inv, Z);
+    fe_sqr(z2, zinv);
+    fe_mul(z3, z2, zinv);
+    fe_mul(ax, X, z2);
+    fe_mul(ay, Y, z3);
+    store_fe(tables[e0 + j].x, ax);
+    store_fe(tables[e0 + j].y, ay);
+    fe_mul(ax, ax, c280);
+    fe_mul(ay, ay, c280);
+    store_fe(tables28[e0 + j].x, ax);
+    store_fe(tables28[e0 + j].y, ay);
+  }
+}
+
 // ---------------------------------------------------------------- k_inv / k_prep
 // Scalar preparation is split so the long part (s^-1, which needs only s) can run
 // concurrently with the SHA-256 jobs that produce the digests:
@@ -296,25 +372,33 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restr
   }
   sn_mul(u1, e, w);  // e * s^-1 (plain)
   sn_mul(u2, r, w);  // r * s^-1 (plain)
-  // signed base-2^WBITS recoding: digits in [-2^(W-1), 2^(W-1) - 1]; the last window holds
-  // the final carry
+  // signed recoding, digits in [-2^(W-1), 2^(W-1) - 1], the last window holding the final
+  // carry: u1 in base 2^16 (17 int16 digits, generator comb), u2 in base 2^8 (33 int8 digits)
+  int8_t *dp = digits + (size_t)i * DIG_STRIDE;
+  {
+    uint16_t *g = reinterpret_cast<uint16_t *>(dp);
+    int c1 = 0;
+#pragma unroll
+    for (int win = 0; win < NGWIN - 1; win++) {
+      int a1 = (int)((u1[win >> 1] >> (16 * (win & 1))) & 0xFFFFu) + c1;
+      c1 = a1 >= (1 << 15);
+      a1 -= c1 << 16;
+      g[win] = (uint16_t)(int16_t)a1;
+    }
+    g[NGWIN - 1] = (uint16_t)c1;
+  }
   constexpr int WMASK = (1 << WBITS) - 1, WHALF = 1 << (WBITS - 1);
-  int c1 = 0, c2 = 0;
-  uint16_t *dp = reinterpret_cast<uint16_t *>(digits + (size_t)i * DIG_STRIDE);
+  int c2 = 0;
+  uint8_t *q = reinterpret_cast<uint8_t *>(dp + DIG_Q_OFF);
 #pragma unroll
   for (int win = 0; win < NWIN; win++) {
     const int bit = WBITS * win, li = bit >> 5, sh = bit & 31;
-    uint32_t v1 = li < 8 ? u1[li] >> sh : 0u, v2 = li < 8 ? u2[li] >> sh : 0u;
-    if (sh > 32 - WBITS && li < 7) {
-      v1 |= u1[li + 1] << (32 - sh);
-      v2 |= u2[li + 1] << (32 - sh);
-    }
-    int a1 = (int)(v1 & WMASK) + c1, a2 = (int)(v2 & WMASK) + c2;
-    c1 = a1 >= WHALF;
+    uint32_t v2 = li < 8 ? u2[li] >> sh : 0u;
+    if (sh > 32 - WBITS && li < 7) v2 |= u2[li + 1] << (32 - sh);
+    int a2 = (int)(v2 & WMASK) + c2;
     c2 = a2 >= WHALF;
-    a1 -= c1 << WBITS;
     a2 -= c2 << WBITS;
-    dp[win] = (uint16_t)((uint8_t)(int8_t)a1 | ((uint16_t)(uint8_t)(int8_t)a2 << 8));
+    q[win] = (uint8_t)(int8_t)a2;
   }
 }
 
@@ -353,17 +437,18 @@ __global__ __launch_bounds__(POINT_THREADS) void k_point(
     fe_set_zero(acc.x);
     fe_set_zero(acc.y);
     fe_set_zero(acc.z);
-    // terms t = 2*k + {0: G, 1: Q} of windows w = sub + k*L (one madd call site)
-    const int nterms = 2 * ((NWIN - (int)sub + (int)L - 1) / (int)L);
+    // comb terms tt = sub + t*L: tt < NGWIN generator window tt, else key window tt - NGWIN
+    // (one madd call site)
+    const int nterms = (NTERMS - (int)sub + (int)L - 1) / (int)L;
 #pragma unroll 1
     for (int t = 0; t < nterms; t++) {
-      const int w = (int)sub + (t >> 1) * (int)L;
-      const bool isq = t & 1;
-      const int d = dg[2 * w + (isq ? 1 : 0)];
+      const int tt = (int)sub + t * (int)L;
+      const bool isq = tt >= NGWIN;
+      const int d = isq ? (int)dg[DIG_Q_OFF + tt - NGWIN] : (int)reinterpret_cast<const int16_t *>(dg)[tt];
       if (d == 0) continue;
       const int k = (d < 0 ? -d : d) - 1;
       apoint p;
-      const apoint_raw *e = (isq ? qt : gtab) + w * TAB_K + k;
+      const apoint_raw *e = isq ? qt + (tt - NGWIN) * TAB_K + k : gtab + (size_t)tt * GT_K + k;
       load_fe(p.x, e->x);
       load_fe(p.y, e->y);
       if (d < 0) fe_neg(p.y, p.y);
@@ -516,14 +601,15 @@ __global__ __launch_bounds__(POINT_THREADS) void k_point28(
     const int8_t *dg = digits + (size_t)i * DIG_STRIDE;
     jp28 acc;
     bool inf = true;
-    const int nterms = 2 * ((NWIN - (int)sub + (int)L - 1) / (int)L);
-    // the table entry of term t+1 is loaded while term t is added (one gather in flight)
+    const int nterms = (NTERMS - (int)sub + (int)L - 1) / (int)L;
+    // the table entry of term t+1 is loaded while term t is added (one gather in flight);
+    // comb term tt = sub + t*L: generator window tt (tt < NGWIN), else key window tt - NGWIN
     auto entry = [&](int t, int &d) -> const uint4 * {
-      const int w = (int)sub + (t >> 1) * (int)L;
-      const bool isq = t & 1;
-      d = dg[2 * w + (isq ? 1 : 0)];
+      const int tt = (int)sub + t * (int)L;
+      const bool isq = tt >= NGWIN;
+      d = isq ? (int)dg[DIG_Q_OFF + tt - NGWIN] : (int)reinterpret_cast<const int16_t *>(dg)[tt];
       const int k = d == 0 ? 0 : (d < 0 ? -d : d) - 1;
-      return reinterpret_cast<const uint4 *>((isq ? qt : gtab28) + w * TAB_K + k);
+      return reinterpret_cast<const uint4 *>(isq ? qt + (tt - NGWIN) * TAB_K + k : gtab28 + (size_t)tt * GT_K + k);
     };
     int dn;
     const uint4 *pn = entry(0, dn);

@@ -187,6 +187,18 @@ int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *r
 int fgv_validate_shard_dev(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
                            const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                            const uint32_t *tx_hi, void *d_results, size_t results_cap, size_t *ntx);
+/* Deliver-side pre-split (no reference counterpart: the Go committer re-walks each block
+ * inside TxValidator.Validate, validator.go:180-265).  Starts walking the block data framing
+ * (the envelope spans) of a batch on a background host thread and returns at once; the next
+ * fgv_validate_shard_dev whose batch has the same block addresses, lengths and tx_lo/tx_hi
+ * uses that split instead of walking the blocks itself -- a peer splits block k+1 while
+ * block k validates.  The block buffers must stay unchanged until that call.  A pre-split
+ * that no call matches is discarded by the next fgv_presplit or validation call; results
+ * never depend on whether a pre-split was used.  fgv_last_presplit: 1 if the last
+ * device-parse validation used one (diagnostic). */
+int fgv_presplit(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                 const uint32_t *tx_lo, const uint32_t *tx_hi);
+int fgv_last_presplit(fgv_ctx *ctx);
 int fgv_finalize_flags_dev(fgv_ctx *ctx, size_t nblocks, const size_t *ntx, uint32_t world,
                            size_t rows_per_rank, const void *d_gathered, uint8_t *flags);
 /* Any shard plan: rank r's rows hold transactions [rank_lo[r*nblocks+b], rank_hi[r*nblocks+b])

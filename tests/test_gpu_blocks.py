@@ -201,6 +201,44 @@ def test_device_sharded_protocol(shards, mode):
     eng.close()
 
 
+@pytest.mark.parametrize("shards,mode", [(1, "tx"), (3, "tx"), (2, "block")])
+def test_presplit_is_used_only_for_its_batch(shards, mode):
+    """fgv_presplit (the batch's framing walked ahead on a host thread): a validation of the
+    same batch and shard range uses it, any other call ignores it; flags identical to the
+    oracle either way."""
+    import torch
+    from fabric_amd import shard
+    net = network()
+    blks = [blocks.make_block(net, n, number=1 + i, seed=95 + i)[0] for i, n in enumerate([40, 7, 29])]
+    ntx = np.array([40, 7, 29], dtype=np.int64)
+    eng = _engine_for(net)
+    plan = shard.plan(ntx, shards, mode)
+    rows = shard.plan_rows(*plan)
+    batch = eng.block_batch(blks)
+    other = eng.block_batch([blocks.make_block(net, 12, number=9, seed=99)[0]])
+    exp = _oracle(net, blks)
+    exp = exp[0] + exp[1] + exp[2]
+    for presplit_plan in ("same", "other_rank", "other_batch"):
+        recv = torch.zeros((shards * rows, shard.REC), dtype=torch.uint8, device="cuda")
+        for r in range(shards):
+            lo, hi = plan[0][r], plan[1][r]
+            if presplit_plan == "same":
+                eng.presplit(batch, lo, hi)
+            elif presplit_plan == "other_rank":
+                q = (r + 1) % shards
+                eng.presplit(batch, plan[0][q], plan[1][q])
+            else:
+                eng.presplit(other)
+            nt = eng.validate_shard_dev(batch, lo, hi, recv[r * rows:].data_ptr(), rows)
+            used = eng.last_presplit()
+            assert used == (presplit_plan == "same" or (presplit_plan == "other_rank" and shards == 1)), presplit_plan
+            assert list(nt) == [0 if lo[b] == shard.SKIP else ntx[b] for b in range(len(ntx))]
+        flags = eng.finalize_flags_dev(ntx, shards, rows, recv.data_ptr(), plan=None if mode == "tx" else plan)
+        assert list(flags) == exp, presplit_plan
+    eng.presplit(batch)  # left pending at close
+    eng.close()
+
+
 def _random_records(rng, ntx, pool):
     """fgv_tx_result records honouring the engine's invariants: VALID => REACHED;
     REACHED => INDEXED with index_txid == txid."""
