@@ -168,19 +168,21 @@ def run_block(args, world, rank, local, dev):
         integ["ms"] += (time.perf_counter() - t) * 1e3
         integ["ok"] &= all(r[0] == _lib.BLK_OK for r in res) and chain.number == rank * B + B
 
+    # every ctypes argument bound once (fabric_amd._lib.BlockStep); the pre-split of the next
+    # batch (here: the same blocks) overlaps this batch's all-gather + finalize, as a peer
+    # splits block k+1 while block k commits
+    bs = _lib.BlockStep(eng, batch, lo, hi, send.data_ptr(), rows, ntx, world, recv.data_ptr(), flags_out,
+                        plan=plan, presplit=not args.no_presplit)
+
     def step():
         th = None
         if spec["integrity"]:  # concurrent with the committer pass, as in a pipelined peer
             th = threading.Thread(target=verify_mine)
             th.start()
-        nt = eng.validate_shard_dev(batch, lo, hi, send.data_ptr(), rows)
-        if not args.no_presplit:
-            # the next batch's framing walk (here: the same blocks) overlaps this batch's
-            # all-gather + finalize, as a peer splits block k+1 while block k commits
-            eng.presplit(batch, lo, hi)
+        bs.validate()
         if world > 1:
             shard.allgather_device(send, recv)
-        f = eng.finalize_flags_dev(ntx, world, rows, recv.data_ptr(), out=flags_out, plan=plan)
+        f = bs.finalize()
         if th is not None:
             th.join()
         return f
@@ -206,14 +208,14 @@ def run_block(args, world, rank, local, dev):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        tm, cn = eng.timing(), eng.counts()
-        for k, v in eng.host_timing().items():
+        tm, cn = bs.stats()
+        for k, v in zip(("parse_ms", "assemble_ms", "device_ms", "fold_ms"), tm[4:]):
             host[k] += v
-        acc["point"] += tm["point_ms"]
-        acc["prep"] += tm["prep_ms"]
-        acc["sha"] += tm["sha_ms"]
-        acc["verifies"] += cn["verifies"]
-        acc["sha_blocks"] += cn["sha_blocks"]
+        acc["sha"] += tm[0]
+        acc["prep"] += tm[1]
+        acc["point"] += tm[2]
+        acc["sha_blocks"] += cn[1]
+        acc["verifies"] += cn[2]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -152,6 +152,58 @@ class _BlockBatch:
         self.ntx = (ctypes.c_size_t * self.nb)()
 
 
+class BlockStep:
+    """One committer pass over a resident batch with every ctypes argument bound once (the
+    bench loop): fgv_validate_shard_dev -> [pre-split of the next batch] -> (caller's
+    all-gather) -> fgv_finalize_flags_dev[_plan], plus the per-call diagnostics read into
+    preallocated cells.  Same C calls as Engine.validate_shard_dev / presplit /
+    finalize_flags_dev."""
+
+    def __init__(self, eng, batch, tx_lo, tx_hi, d_send, rows, ntx, world, d_recv, flags_out, plan=None,
+                 presplit=True):
+        L, h = eng._L, eng._h
+        self._L = L
+        self._lo = np.ascontiguousarray(tx_lo, dtype=np.uint32)
+        self._hi = np.ascontiguousarray(tx_hi, dtype=np.uint32)
+        self._ntx = np.ascontiguousarray(ntx, dtype=np.uint64)
+        self.flags = flags_out
+        self._val = (h, batch.nb, batch.ptrs, batch.lens, batch.dptr, _ptr(self._lo), _ptr(self._hi),
+                     ctypes.c_void_p(d_send), rows, batch.ntx)
+        self._pre = (h, batch.nb, batch.ptrs, batch.lens, _ptr(self._lo), _ptr(self._hi)) if presplit else None
+        if plan is None:
+            self._fin_fn = L.fgv_finalize_flags_dev
+            self._fin = (h, len(self._ntx), _ptr(self._ntx), world, rows, ctypes.c_void_p(d_recv), _ptr(flags_out))
+        else:
+            self._plo = np.ascontiguousarray(plan[0], dtype=np.uint32)
+            self._phi = np.ascontiguousarray(plan[1], dtype=np.uint32)
+            assert self._plo.shape == self._phi.shape == (world, len(self._ntx))
+            self._fin_fn = L.fgv_finalize_flags_dev_plan
+            self._fin = (h, len(self._ntx), _ptr(self._ntx), world, rows, _ptr(self._plo), _ptr(self._phi),
+                         ctypes.c_void_p(d_recv), _ptr(flags_out))
+        self._t = [ctypes.c_double() for _ in range(8)]
+        self._c = [ctypes.c_uint64() for _ in range(3)]
+        self._tr = (h,) + tuple(ctypes.byref(x) for x in self._t[:4])
+        self._hr = (h,) + tuple(ctypes.byref(x) for x in self._t[4:])
+        self._cr = (h,) + tuple(ctypes.byref(x) for x in self._c)
+
+    def validate(self):
+        _check(self._L.fgv_validate_shard_dev(*self._val))
+        if self._pre is not None:
+            _check(self._L.fgv_presplit(*self._pre))
+
+    def finalize(self):
+        _check(self._fin_fn(*self._fin))
+        return self.flags
+
+    def stats(self):
+        """(sha_ms, prep_ms, point_ms, keytab_ms, parse_ms, assemble_ms, device_ms, fold_ms),
+        (sha_jobs, sha_blocks, verifies) of the last validation."""
+        self._L.fgv_last_timing(*self._tr)
+        self._L.fgv_last_host_timing(*self._hr)
+        self._L.fgv_last_counts(*self._cr)
+        return [x.value for x in self._t], [x.value for x in self._c]
+
+
 class Engine:
     """One libfgv context = one GPU (one process per GPU)."""
 
