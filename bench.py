@@ -29,11 +29,11 @@ import torch
 import torch.distributed as dist
 
 METRIC = "ECDSA-P256 verifies/sec + validated tx/sec per block at 1/2/4/8 MI355X"
-# 32x32->64 multiply-add products per verify in the comb: 49 terms (16 signed
-# 16-bit generator windows + 32 signed 8-bit key windows + the two carry windows, each nonzero
-# about every other verify), the first one loaded, so 48 mixed additions x (8 field mults x 64
-# + 3 squarings x 36 products) + the projective x-check (3 x 64)
-PRODUCTS_POINT = 48 * (8 * 64 + 3 * 36) + 3 * 64
+# 32x32->64 multiply-add products per verify in the comb: ~42.5 terms (16 signed
+# 16-bit generator windows + their carry window, nonzero about every other verify, + 26 signed
+# 10-bit key windows), the first one loaded, so 41 mixed additions (rounded down) x (8 field
+# mults x 64 + 3 squarings x 36 products) + the projective x-check (3 x 64)
+PRODUCTS_POINT = 41 * (8 * 64 + 3 * 36) + 3 * 64
 # chip-wide v_mad_u64_u32 issue rate measured by tools/valu_peak.hip (profiles/round1_valu_peak.json)
 PEAK_MAD_PER_S = float(os.environ.get("FGV_PEAK_MAD", "3.106e13"))
 
@@ -43,11 +43,28 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def roofline(n_verifies, point_ms):
+def pmc_traffic(workload):
+    """HBM bytes per launch of the workload's dominant kernel from the committed rocprofv3 PMC
+    passes (profiles/*_traffic.json, written by tools/summarize_profiles.py); None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        t = d["workloads"][workload]
+        return t["hbm_bytes"], f"{os.path.basename(files[-1])}: {t['kernel']} fetch {t['fetch_bytes']} B + write {t['write_bytes']} B"
+    except (KeyError, ValueError, OSError):
+        return None, None
+
+
+def roofline(n_verifies, point_ms, workload):
     point_s = point_ms / 1e3
     achieved = n_verifies * PRODUCTS_POINT / point_s / 1e12 if point_s > 0 else 0.0
+    traffic, src = pmc_traffic(workload)
     return dict(bound="valu", achieved=round(achieved, 3), peak=round(PEAK_MAD_PER_S / 1e12, 3),
-                unit="Tops/s", frac=round(achieved * 1e12 / PEAK_MAD_PER_S, 4), traffic=None, kernel="k_point28 (+ k_point hand-overs)",
+                unit="Tops/s", frac=round(achieved * 1e12 / PEAK_MAD_PER_S, 4), traffic=traffic, traffic_source=src,
+                kernel="k_point28 (+ k_point hand-overs)",
                 kernel_avg_ms=round(point_ms, 4), per_launch_products=int(n_verifies * PRODUCTS_POINT),
                 work_unit="v_mad_u64_u32 (32x32->64 multiply-add) products of the comb algorithm")
 
@@ -246,7 +263,7 @@ def run_block(args, world, rank, local, dev):
                sha256_compressions_per_step=int(acc["sha_blocks"] / args.steps),
                host_ms=dict({k: round(v / args.steps, 3) for k, v in host.items()},
                             **({"integrity_ms": round(integ["ms"] / args.steps, 3)} if spec["integrity"] else {})),
-               roofline=roofline(acc["verifies"] / args.steps, acc["point"] / args.steps), cpu_baseline=None)
+               roofline=roofline(acc["verifies"] / args.steps, acc["point"] / args.steps, args.workload), cpu_baseline=None)
     if rank == 0 and world == 1 and args.cpu_threads > 0:
         # crypto-bound upper bound of the reference's CPU committer on this host: every
         # verify is SHA-256(msg) + Go-rule DER + low-S + OpenSSL P-256 (what identity.Verify
@@ -328,6 +345,7 @@ def run_mvcc(args, world, rank, local, dev):
         dist.all_reduce(mn, op=dist.ReduceOp.MIN)
         el, ok = float(mx[0]), bool(mn[1] > 0)
     per_block_ms = total / K
+    mv_traffic, mv_src = pmc_traffic("mvcc")
     achieved = T * MVCC_BYTES_PER_TX / (per_block_ms / 1e3) / 1e9
     return dict(metric=METRIC, value=round(T * K * world / el, 1), unit="MVCC-validated tx/s", n_gpus=world, steps=K,
                 warmup=W, ms_per_step=round(el / K * 1e3, 3), higher_is_better=True, scaling="weak",
@@ -338,7 +356,8 @@ def run_mvcc(args, world, rank, local, dev):
                 parity_vs_labels=ok, fixpoint_rounds=rounds,
                 stage_ms=dict(lookup=round(lookup / K, 4), gpu_total=round(per_block_ms, 4)),
                 roofline=dict(bound="hbm", achieved=round(achieved, 2), peak=8000.0, unit="GB/s",
-                              frac=round(achieved / 8000.0, 5), traffic=None, kernel="MVCC GPU stages (per block)",
+                              frac=round(achieved / 8000.0, 5), traffic=mv_traffic, traffic_source=mv_src,
+                              kernel="MVCC GPU stages (per block)",
                               per_launch_bytes=T * MVCC_BYTES_PER_TX,
                               note="latency-bound: ~14 launches + 2 host syncs per 10k-tx block"),
                 cpu_baseline=None)
@@ -414,7 +433,7 @@ def run_sig(args, world, rank, local, dev):
                parity_vs_labels=ok,
                stage_ms=dict(sha=round(acc["sha"] / args.steps, 4), prep=round(acc["prep"] / args.steps, 4),
                              point=round(acc["point"] / args.steps, 4)),
-               roofline=roofline(n, acc["point"] / args.steps), cpu_baseline=None)
+               roofline=roofline(n, acc["point"] / args.steps, "sig"), cpu_baseline=None)
     if rank == 0 and world == 1 and args.cpu_threads > 0:
         rate, done, cel = cpu_verify_rate(pool["keymat"], [m.tobytes() for m in pool["msgs"]], pool["sigs"],
                                           args.cpu_threads)
@@ -431,7 +450,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="block", choices=["block", "c5", "sig", "mvcc"])
-    ap.add_argument("--c5-blocks-per-gpu", type=int, default=2)
+    ap.add_argument("--c5-blocks-per-gpu", type=int, default=8)
     ap.add_argument("--c5-tx-per-block", type=int, default=20000)
     ap.add_argument("--tx-per-mvcc-block", type=int, default=10000)
     ap.add_argument("--state-keys", type=int, default=1_000_000)

@@ -23,18 +23,24 @@
 #include "fgv_internal.h"
 #include "fgv_kernels.h"
 
-// Build tables for `nk` keys (qxy: nk*16 limbs) into `tables` at `slots`.
+// Build tables for `nk` keys (qxy: nk*16 limbs) into `tables` at `slots`, KT_BUILD_KEYS keys
+// per k_keytab launch (its scratch is KT_ENTRIES Jacobian points per key).
 static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slots, uint32_t nk,
                         apoint_raw *tables, apoint_raw *tables28, uint8_t *ok) {
+  const uint32_t per = nk < KT_BUILD_KEYS ? nk : KT_BUILD_KEYS;
   if (!c->kt_q.ensure((size_t)nk * 64) || !c->kt_slot.ensure((size_t)nk * 4) ||
-      !c->kt_scratch.ensure((size_t)nk * KT_ENTRIES * sizeof(jpoint_raw)))
+      !c->kt_scratch.ensure((size_t)per * KT_ENTRIES * sizeof(jpoint_raw)))
     return FGV_ENOMEM;
   HIP_TRY(hipMemcpyAsync(c->kt_q.p, h_qxy, (size_t)nk * 64, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->kt_slot.p, h_slots, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipEventRecord(c->ev[6], c->stream));
-  hipLaunchKernelGGL(k_keytab, dim3(nk), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
-                     c->kt_slot.as<uint32_t>(), tables, tables28, c->kt_scratch.as<jpoint_raw>(), ok, nk);
-  HIP_TRY(hipGetLastError());
+  for (uint32_t k = 0; k < nk; k += per) {
+    const uint32_t m = nk - k < per ? nk - k : per;
+    const uint32_t threads = m * KT_THREADS_PER_KEY;
+    hipLaunchKernelGGL(k_keytab, dim3((threads + 63) / 64), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>() + 16 * k,
+                       c->kt_slot.as<uint32_t>() + k, tables, tables28, c->kt_scratch.as<jpoint_raw>(), ok, m);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipEventRecord(c->ev[7], c->stream));
   return FGV_OK;
 }

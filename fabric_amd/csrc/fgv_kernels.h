@@ -3,13 +3,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Fixed-base comb: 32 windows of 8 bits with signed digits in [-128, 127], plus a 33rd window
-// for the final carry (digit 0 or 1); 128 entries (|d| = 1..128) per window.
-#define WBITS 8
-#define NWIN 33
-#define TAB_K 128
-#define KT_ENTRIES (NWIN * TAB_K)           // 4224 affine points per table
-#define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 270,336 bytes per table
+// Key comb (u2 * Q): 26 windows of 10 bits with signed digits in [-512, 511] (26 x 10 = 260 bits:
+// the top window, bits 250..259 of a scalar < 2^256, absorbs the final carry); 512 entries
+// (|d| = 1..512) per window, 852 KB per key per copy, built by k_keytab (KT_CHUNK entries per thread).
+#define WBITS 10
+#define NWIN 26
+#define TAB_K 512
+#define KT_CHUNK 32
+#define KT_THREADS_PER_KEY (NWIN * (TAB_K / KT_CHUNK))  // 416
+#define KT_BUILD_KEYS 128                                // keys per k_keytab launch (scratch bound)
+#define KT_ENTRIES (NWIN * TAB_K)           // 13,312 affine points per table
+#define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 851,968 bytes per table
 // Generator comb (u1 * G): 16 windows of 16 bits with signed digits in [-2^15, 2^15 - 1], plus
 // a 17th window for the final carry (digit 0 or 1); 32768 entries per window (33.5 MB per copy,
 // MALL / HBM resident, built once per context by k_gtab).  17 G terms instead of 33.
@@ -20,12 +24,12 @@
 #define GT_BYTES ((size_t)GT_ENTRIES * 64)
 #define GT_CHUNK 32                   // consecutive entries per k_gtab thread
 #define GT_THREADS ((NGWIN - 1) * (GT_K / GT_CHUNK) + 1)
-#define NTERMS (NGWIN + NWIN)         // comb terms per verify: 17 G + 33 Q
-#define DIG_Q_OFF 40                  // digit array item: G digits int16 x 17 at 0, Q digits int8 x 33 here
+#define NTERMS (NGWIN + NWIN)         // comb terms per verify: 17 G + 26 Q
+#define DIG_Q_OFF 40                  // digit array item: G digits int16 x 17 at 0, Q digits int16 x 26 here
 #define PREP_B 2                            // items per lane in the batched inversion
 #define POINT_THREADS 512   // 8 waves per CU (2 per SIMD): up to 256 VGPRs, no spills
 #define POINT_LANES_MAX 8    // lanes cooperating on one verify in k_point (partial sums + tree)
-#define DIG_STRIDE 80        // bytes per item of the digit array (G digits, then Q digits at DIG_Q_OFF)
+#define DIG_STRIDE 96        // bytes per item of the digit array (G digits, then Q digits at DIG_Q_OFF)
 #define ST_PENDING 0xFF
 
 struct apoint_raw {  // affine point, Montgomery limbs (64 B, 16-B aligned)

@@ -95,18 +95,23 @@ FGV_DEV void load_fe(fe &a, const uint32_t *src) {
 }
 
 // ---------------------------------------------------------------- k_keytab
-// grid.x = number of keys, block = 64 (one wave per key, lane w < NWIN owns window w).
-// qxy: [nkeys][16] plain little-endian limbs (x then y).
-// scratch: [nkeys][KT_ENTRIES] Jacobian points + prefix products (jpoint_raw = X,Y,Z,pref).
+// T_Q[w][k-1] = k * 2^(10w) * Q, w < 26, k = 1..512.  KT_THREADS_PER_KEY threads per key, thread
+// (w, chunk) builds entries k0..k0+31 of window w: B = 2^(10w) Q by doublings, P = k0 * B by
+// double-and-add, then P += B, one Montgomery-trick inversion per chunk (complete formulas:
+// pt_add routes P == B to a doubling).  Both Montgomery forms (k_point / k_point28).
+// qxy: [nkeys][16] plain little-endian limbs (x then y); scratch: [nkeys][KT_ENTRIES] jpoint_raw.
 __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
                                                const uint32_t *__restrict__ slots,
                                                apoint_raw *__restrict__ tables,
                                                apoint_raw *__restrict__ tables28,
                                                jpoint_raw *__restrict__ scratch,
                                                uint8_t *__restrict__ key_ok, uint32_t nkeys) {
-  const uint32_t kid = blockIdx.x;
-  const int w = threadIdx.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t kid = t / KT_THREADS_PER_KEY, r = t % KT_THREADS_PER_KEY;
   if (kid >= nkeys) return;
+  constexpr uint32_t CPW = TAB_K / KT_CHUNK;  // chunks per window
+  const uint32_t w = r / CPW, ch = r % CPW;
+  const uint32_t k0 = ch * KT_CHUNK + 1;
   fe x, y, xm, ym;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -115,62 +120,61 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
   }
   const bool ok = on_curve(x, y, xm, ym);
   const uint32_t slot = slots[kid];
-  if (w == 0) key_ok[slot] = ok ? 1 : 0;
-  if (!ok || w >= NWIN) return;
-
+  if (r == 0) key_ok[slot] = ok ? 1 : 0;
+  if (!ok) return;
   jpoint b;
   b.x = xm;
   b.y = ym;
   fe_set_one(b.z);
-  for (int i = 0; i < WBITS * w; i++) pt_dbl(b, b);
-
-  jpoint_raw *scr = scratch + (size_t)kid * KT_ENTRIES + (size_t)w * TAB_K;
-  apoint_raw *tab = tables + (size_t)slot * KT_ENTRIES + (size_t)w * TAB_K;
-  apoint_raw *tab28 = tables28 + (size_t)slot * KT_ENTRIES + (size_t)w * TAB_K;
-  // P_1 = B, P_2 = 2B, P_k = P_{k-1} + B  (k*B != +-B for 3 <= k <= 32 < n)
+  for (uint32_t i = 0; i < WBITS * w; i++) pt_dbl(b, b);
   jpoint pk = b;
+  for (int bit = 30 - __builtin_clz(k0 | 1u); bit >= 0; bit--) {
+    jpoint t2 = pk;
+    pt_dbl(pk, t2);
+    if ((k0 >> bit) & 1u) {
+      t2 = pk;
+      pt_add(pk, t2, b);
+    }
+  }
+  jpoint_raw *scr = scratch + (size_t)kid * KT_ENTRIES + (size_t)w * TAB_K + (k0 - 1);
+  const size_t e0 = (size_t)slot * KT_ENTRIES + (size_t)w * TAB_K + (k0 - 1);
   fe pref;
   fe_set_one(pref);
-  for (int k = 1; k <= TAB_K; k++) {
-    if (k == 2) {
-      pt_dbl(pk, b);
-    } else if (k > 2) {
-      jpoint t = pk;
-      pt_add(pk, t, b);
+  for (uint32_t j = 0; j < KT_CHUNK; j++) {
+    if (j > 0) {
+      jpoint t2 = pk;
+      pt_add(pk, t2, b);
     }
     fe_mul(pref, pref, pk.z);
-    jpoint_raw *e = scr + (k - 1);
-    store_fe(e->x, pk.x);
-    store_fe(e->y, pk.y);
-    store_fe(e->z, pk.z);
-    store_fe(e->pref, pref);
+    store_fe(scr[j].x, pk.x);
+    store_fe(scr[j].y, pk.y);
+    store_fe(scr[j].z, pk.z);
+    store_fe(scr[j].pref, pref);
   }
-  // Montgomery trick: one Fermat inversion for the 32 Z's of this window
   fe inv;
   fe_inv(inv, pref);
-  for (int k = TAB_K; k >= 1; k--) {
-    jpoint_raw *e = scr + (k - 1);
+  fe c280;
+  fe_load_c(c280, C280_32);
+  for (int j = KT_CHUNK - 1; j >= 0; j--) {
     fe X, Y, Z, prev, zinv, z2, z3, ax, ay;
-    load_fe(X, e->x);
-    load_fe(Y, e->y);
-    load_fe(Z, e->z);
-    if (k > 1) load_fe(prev, (e - 1)->pref);
+    load_fe(X, scr[j].x);
+    load_fe(Y, scr[j].y);
+    load_fe(Z, scr[j].z);
+    if (j > 0) load_fe(prev, scr[j - 1].pref);
     else fe_set_one(prev);
-    fe_mul(zinv, inv, prev);  // Z_k^-1 = (Z_1..Z_k)^-1 * (Z_1..Z_{k-1})
-    fe_mul(inv, inv, Z);      // (Z_1..Z_{k-1})^-1
+    fe_mul(zinv, inv, prev);  // Z_j^-1 = (Z_0..Z_j)^-1 * (Z_0..Z_{j-1})
+    fe_mul(inv, inv, Z);      // (Z_0..Z_{j-1})^-1
     fe_sqr(z2, zinv);
     fe_mul(z3, z2, zinv);
     fe_mul(ax, X, z2);
     fe_mul(ay, Y, z3);
-    store_fe(tab[k - 1].x, ax);
-    store_fe(tab[k - 1].y, ay);
-    // the same point in Montgomery-280 form (k_point28): x * 2^256 -> x * 2^280, canonical
-    fe c280;
-    fe_load_c(c280, C280_32);
+    store_fe(tables[e0 + j].x, ax);
+    store_fe(tables[e0 + j].y, ay);
+    // the same point in Montgomery-280 form (k_point28): x * 2^256 -> x * 2^280
     fe_mul(ax, ax, c280);
     fe_mul(ay, ay, c280);
-    store_fe(tab28[k - 1].x, ax);
-    store_fe(tab28[k - 1].y, ay);
+    store_fe(tables28[e0 + j].x, ax);
+    store_fe(tables28[e0 + j].y, ay);
   }
 }
 
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, uint8_t *__rest
 
 // in:  status, r limbs, w = s^-1 (Montgomery) from k_inv, digests [*][32] big-endian, item i
 //      using digest dig_idx[i] (or i when dig_idx is null).
-// out: digits [n][DIG_STRIDE] int8: (d1_w, d2_w) pairs.
+// out: digits [n][DIG_STRIDE]: u1 digits (int16 x NGWIN) at 0, u2 digits (int16 x NWIN) at DIG_Q_OFF.
 __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restrict__ status,
                                               const uint32_t *__restrict__ r_limbs,
                                               const uint32_t *__restrict__ w_in,
@@ -373,7 +377,8 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restr
   sn_mul(u1, e, w);  // e * s^-1 (plain)
   sn_mul(u2, r, w);  // r * s^-1 (plain)
   // signed recoding, digits in [-2^(W-1), 2^(W-1) - 1], the last window holding the final
-  // carry: u1 in base 2^16 (17 int16 digits, generator comb), u2 in base 2^8 (33 int8 digits)
+  // carry: u1 in base 2^16 (17 int16 digits, generator comb), u2 in base 2^10 (26 int16 digits;
+  // the top window of a scalar < 2^256 is < 2^6 + 1, so it never carries out)
   int8_t *dp = digits + (size_t)i * DIG_STRIDE;
   {
     uint16_t *g = reinterpret_cast<uint16_t *>(dp);
@@ -389,7 +394,7 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restr
   }
   constexpr int WMASK = (1 << WBITS) - 1, WHALF = 1 << (WBITS - 1);
   int c2 = 0;
-  uint8_t *q = reinterpret_cast<uint8_t *>(dp + DIG_Q_OFF);
+  uint16_t *q = reinterpret_cast<uint16_t *>(dp + DIG_Q_OFF);
 #pragma unroll
   for (int win = 0; win < NWIN; win++) {
     const int bit = WBITS * win, li = bit >> 5, sh = bit & 31;
@@ -398,7 +403,7 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restr
     int a2 = (int)(v2 & WMASK) + c2;
     c2 = a2 >= WHALF;
     a2 -= c2 << WBITS;
-    q[win] = (uint8_t)(int8_t)a2;
+    q[win] = (uint16_t)(int16_t)a2;
   }
 }
 
@@ -444,7 +449,7 @@ __global__ __launch_bounds__(POINT_THREADS) void k_point(
     for (int t = 0; t < nterms; t++) {
       const int tt = (int)sub + t * (int)L;
       const bool isq = tt >= NGWIN;
-      const int d = isq ? (int)dg[DIG_Q_OFF + tt - NGWIN] : (int)reinterpret_cast<const int16_t *>(dg)[tt];
+      const int d = (int)reinterpret_cast<const int16_t *>(dg + (isq ? DIG_Q_OFF : 0))[isq ? tt - NGWIN : tt];
       if (d == 0) continue;
       const int k = (d < 0 ? -d : d) - 1;
       apoint p;
@@ -607,7 +612,7 @@ __global__ __launch_bounds__(POINT_THREADS) void k_point28(
     auto entry = [&](int t, int &d) -> const uint4 * {
       const int tt = (int)sub + t * (int)L;
       const bool isq = tt >= NGWIN;
-      d = isq ? (int)dg[DIG_Q_OFF + tt - NGWIN] : (int)reinterpret_cast<const int16_t *>(dg)[tt];
+      d = (int)reinterpret_cast<const int16_t *>(dg + (isq ? DIG_Q_OFF : 0))[isq ? tt - NGWIN : tt];
       const int k = d == 0 ? 0 : (d < 0 ? -d : d) - 1;
       return reinterpret_cast<const uint4 *>(isq ? qt + (tt - NGWIN) * TAB_K + k : gtab28 + (size_t)tt * GT_K + k);
     };
