@@ -1099,6 +1099,13 @@ __global__ void k_bd_fold(uint32_t ntx, const DevTx *txs, const uint64_t *bases,
                           const DevJobIdx *jobs, const uint32_t *totals, const uint8_t *digests,
                           const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags);
 
+// The batch head, one H2D copy: envelope table | block base addresses | 64 zero bytes (the
+// kernels' counters), each part 64-byte aligned.
+static size_t head_env_bytes(size_t total) { return (total * 4 * BD_ENV_WORDS + 63) & ~(size_t)63; }
+static size_t head_bytes(size_t total, size_t nblocks) {
+  return head_env_bytes(total) + ((nblocks * 8 + 63) & ~(size_t)63) + 64;
+}
+
 // host: split each block into envelope spans (tag / length walk of the block data framing)
 // and write the envelope table into `et`
 static int split_batch(ThreadPool &pool, size_t nblocks, const uint8_t *const *h_blocks, const size_t *lens,
@@ -1127,7 +1134,7 @@ static int split_batch(ThreadPool &pool, size_t nblocks, const uint8_t *const *h
     if (lens[b] > 0xFFFFFFFFull) return FGV_EINVAL;
   }
   if (o.total >= 0x7FFFFFFFull) return FGV_EINVAL;
-  if (!et.ensure(o.total * 4 * BD_ENV_WORDS + 64)) return FGV_ENOMEM;
+  if (!et.ensure(head_bytes(o.total, nblocks) + 64)) return FGV_ENOMEM;
   uint32_t *e = et.as<uint32_t>();
   for (size_t b = 0; b < nblocks; b++) {  // writes only (the spans are already known)
     uint32_t *w = e + BD_ENV_WORDS * o.first[b];
@@ -1188,26 +1195,27 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   c->last_presplit = presplit;
   if (total == 0) return FGV_OK;
   const uint32_t N = (uint32_t)total;
-  if (!c->hb_bases.ensure(nblocks * 8) || !c->hb_misc.ensure(64) ||
-      !c->bd_env.ensure(total * 4 * BD_ENV_WORDS) || !c->bd_bases.ensure(nblocks * 8) || !c->bd_misc.ensure(64) ||
+  const size_t hbytes = head_bytes(total, nblocks), eoff = head_env_bytes(total);
+  const size_t moff = eoff + ((nblocks * 8 + 63) & ~(size_t)63);
+  // (hb_env already holds hbytes: split_batch sized it)
+  if (!c->hb_misc.ensure(64) || !c->bd_env.ensure(hbytes) ||
       !c->bd_tx.ensure(total * sizeof(DevTx)) || !c->bd_ident.ensure(total * BD_OCC * 4) ||
       !c->bd_jobs.ensure(total * sizeof(DevJobIdx)))
     return FGV_ENOMEM;
-  uint32_t *et = c->hb_env.as<uint32_t>();
-  uint64_t *bs = c->hb_bases.as<uint64_t>();
+  uint8_t *head = c->hb_env.as<uint8_t>();  // the envelope table is already in place
+  uint64_t *bs = reinterpret_cast<uint64_t *>(head + eoff);
   for (size_t b = 0; b < nblocks; b++) bs[b] = (uint64_t)(uintptr_t)d_blocks[b];
+  memset(head + moff, 0, 64);
   c->t_host_parse = ms_since(t0);
   auto t1 = clk::now();
   hipStream_t st = c->stream;
-  uint32_t *misc = c->bd_misc.as<uint32_t>();  // [0..5) totals, [5] flags, bytes 24..32 compressions
-  HIP_TRY(hipMemcpyAsync(c->bd_env.p, et, total * 4 * BD_ENV_WORDS, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(c->bd_bases.p, bs, nblocks * 8, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemsetAsync(misc, 0, 64, st));
+  HIP_TRY(hipMemcpyAsync(c->bd_env.p, head, hbytes, hipMemcpyHostToDevice, st));
+  uint32_t *misc = reinterpret_cast<uint32_t *>(c->bd_env.as<uint8_t>() + moff);  // [0..5) totals, [5] flags, bytes 24..32 compressions
   const DevChannel ch = S->dimg.ch;
   DevTx *dtx = c->bd_tx.as<DevTx>();
   int32_t *did = c->bd_ident.as<int32_t>();
   DevJobIdx *dj = c->bd_jobs.as<DevJobIdx>();
-  const uint64_t *dbs = c->bd_bases.as<uint64_t>();
+  const uint64_t *dbs = reinterpret_cast<const uint64_t *>(c->bd_env.as<uint8_t>() + eoff);
   // k_bd_sha digest slots (blockdev.h): BD_DIG_SLOTS per tx, slot-major
   if (!c->bj_dig.ensure((size_t)N * 32 * BD_DIG_SLOTS + 64)) return FGV_ENOMEM;
   unsigned long long *nblk = reinterpret_cast<unsigned long long *>(misc + 6);

@@ -204,8 +204,16 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
   if (c->digests_ready) HIP_TRY(hipStreamWaitEvent(c->stream, c->digests_ready, 0));
   if (c->digests_ready2) HIP_TRY(hipStreamWaitEvent(c->stream, c->digests_ready2, 0));
   HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+  // k_point28 (radix-2^28, incomplete formulas) decides every item except those that hit an
+  // exceptional addition; k_point (complete formulas) then finishes those, and returns at
+  // once when k_point28 counted none.  FGV_POINT_EXACT=1 runs k_point alone (A/B knob).
+  static const bool exact_only = [] {
+    const char *e = getenv("FGV_POINT_EXACT");
+    return e && atoi(e) == 1;
+  }();
+  uint32_t *redo = exact_only ? nullptr : c->redo.as<uint32_t>();
   hipLaunchKernelGGL(k_prep, dim3((N + 255) / 256), dim3(256), 0, c->stream, N, d_status, d_r,
-                     c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>());
+                     c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>(), redo);  // (k_prep zeroes *redo)
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[5], c->stream));
   // Persistent grid: one POINT_THREADS workgroup per CU.  Lanes per verify L (1, 2, 4, 8):
@@ -229,16 +237,8 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
     if (cost < best - 1e-9) { best = cost; L = l; }
   }
   if (forced >= 1 && forced <= POINT_LANES_MAX) L = (uint32_t)forced;
-  // k_point28 (radix-2^28, incomplete formulas) decides every item except those that hit an
-  // exceptional addition; k_point (complete formulas) then finishes those, and returns at
-  // once when k_point28 counted none.  FGV_POINT_EXACT=1 runs k_point alone (A/B knob).
-  static const bool exact_only = [] {
-    const char *e = getenv("FGV_POINT_EXACT");
-    return e && atoi(e) == 1;
-  }();
-  uint32_t *redo = exact_only ? nullptr : c->redo.as<uint32_t>();
+
   if (redo) {
-    HIP_TRY(hipMemsetAsync(redo, 0, 4, c->stream));
     hipLaunchKernelGGL(k_point28, dim3(c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, L, d_status, d_slot,
                        c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   }

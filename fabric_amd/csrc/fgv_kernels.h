@@ -49,7 +49,7 @@ __global__ void k_gtab(apoint_raw *tables, apoint_raw *tables28, jpoint_raw *scr
 __global__ void k_inv(uint32_t n, uint8_t *status, const uint32_t *key_slot, const uint8_t *key_ok,
                       const uint32_t *r_limbs, const uint32_t *s_limbs, uint32_t *w_out, uint32_t *w_scratch);
 __global__ void k_prep(uint32_t n, const uint8_t *status, const uint32_t *r_limbs, const uint32_t *w_in,
-                       const uint8_t *digests, const uint32_t *dig_idx, int8_t *digits);
+                       const uint8_t *digests, const uint32_t *dig_idx, int8_t *digits, uint32_t *redo);
 __global__ void k_point(uint32_t n, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot, const apoint_raw *gtab,
                         const apoint_raw *ktab, const int8_t *digits, const uint32_t *r_limbs, const uint32_t *redo);
 __global__ void k_point28(uint32_t n, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot,

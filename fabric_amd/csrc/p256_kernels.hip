@@ -354,9 +354,10 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restr
                                               const uint32_t *__restrict__ w_in,
                                               const uint8_t *__restrict__ digests,
                                               const uint32_t *__restrict__ dig_idx,
-                                              int8_t *__restrict__ digits) {
+                                              int8_t *__restrict__ digits, uint32_t *__restrict__ redo) {
   __builtin_amdgcn_s_setprio(3);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 && redo) *redo = 0u;  // k_point28's hand-over count (read by k_point)
   if (i >= n || status[i] != ST_PENDING) return;
   uint32_t w[8], r[8], e[8], u1[8], u2[8];
 #pragma unroll

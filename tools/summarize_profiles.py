@@ -105,6 +105,36 @@ def main(src, rnd):
         lines += ["", "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 reports ½ of wide streaming reads); "
                   "small gathers are uncalibrated; the MVCC 1M-key table (32 MB) and the comb tables of the block "
                   "workload (~70 MB) are Infinity-Cache resident.", ""]
+    # HBM traffic per launch of each workload's dominant kernel (bench.py roofline.traffic):
+    # FETCH_SIZE (doubled, gfx950) + WRITE_SIZE from the separate --pmc passes, KB -> bytes
+    traffic = {}
+    for wl, fe, wr, kern in (("block", "pmc_blk_fetch", "pmc_blk_write", "k_point28"),
+                             ("sig", "pmc_sig_fetch", "pmc_sig_write", "k_point28"),
+                             ("mvcc", "pmc_fetch", "pmc_write", None)):
+        pf = os.path.join(src, fe, "run_counter_collection.csv")
+        pw = os.path.join(src, wr, "run_counter_collection.csv")
+        if not (os.path.exists(pf) and os.path.exists(pw)):
+            continue
+        F, W = pmc(pf), pmc(pw)
+        if kern:
+            if kern in F and kern in W:
+                fb, wb = F[kern]["FETCH_SIZE"] * 2 * 1024, W[kern]["WRITE_SIZE"] * 1024
+                traffic[wl] = dict(kernel=kern, fetch_bytes=round(fb), write_bytes=round(wb), hbm_bytes=round(fb + wb),
+                                   avg_us=round(F[kern]["avg_s"] * 1e6, 1))
+        else:  # MVCC: all per-block kernels (the one-time k_mv_load excluded), per block
+            nblk = F.get("k_mv_lookup", {}).get("dispatches", 0)
+            if nblk:
+                fb = sum(v["FETCH_SIZE"] * 2 * 1024 * v["dispatches"] for k, v in F.items()
+                         if k.startswith("k_mv") and k != "k_mv_load") / nblk
+                wb = sum(v["WRITE_SIZE"] * 1024 * v["dispatches"] for k, v in W.items()
+                         if k.startswith("k_mv") and k != "k_mv_load") / nblk
+                traffic[wl] = dict(kernel="k_mv_* per block", fetch_bytes=round(fb), write_bytes=round(wb),
+                                   hbm_bytes=round(fb + wb))
+    if traffic:
+        json.dump(dict(round=rnd, source="rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, separate passes "
+                                        "(tools/profile_round.sh)", workloads=traffic),
+                  open(f"profiles/{rnd}_traffic.json", "w"), indent=1)
+        lines += ["## HBM traffic per launch (bench.py roofline.traffic)", "", "```", json.dumps(traffic, indent=1), "```", ""]
     open(f"profiles/{rnd}_profile_summary.md", "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
