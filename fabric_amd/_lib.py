@@ -23,7 +23,7 @@ EXPORTED = [
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
-    "fgv_presplit", "fgv_last_presplit",
+    "fgv_presplit", "fgv_last_presplit", "fgv_validate_shard_dev_next",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode",
 ]
@@ -106,6 +106,7 @@ def load():
         L.fgv_validate_shard_dev.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
         L.fgv_finalize_flags_dev.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp]
         L.fgv_presplit.argtypes = [vp, sz, vp, vp, vp, vp]
+        L.fgv_validate_shard_dev_next.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp, vp, vp, vp]
         L.fgv_last_presplit.argtypes = [vp]
         L.fgv_finalize_flags_dev_plan.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
@@ -169,7 +170,9 @@ class BlockStep:
         self.flags = flags_out
         self._val = (h, batch.nb, batch.ptrs, batch.lens, batch.dptr, _ptr(self._lo), _ptr(self._hi),
                      ctypes.c_void_p(d_send), rows, batch.ntx)
-        self._pre = (h, batch.nb, batch.ptrs, batch.lens, _ptr(self._lo), _ptr(self._hi)) if presplit else None
+        # presplit: the next batch (the same blocks in a bench loop) is split while this one's
+        # GPU work runs (fgv_validate_shard_dev_next)
+        self._next = (batch.nb, batch.ptrs, batch.lens, _ptr(self._lo), _ptr(self._hi)) if presplit else None
         if plan is None:
             self._fin_fn = L.fgv_finalize_flags_dev
             self._fin = (h, len(self._ntx), _ptr(self._ntx), world, rows, ctypes.c_void_p(d_recv), _ptr(flags_out))
@@ -187,9 +190,10 @@ class BlockStep:
         self._cr = (h,) + tuple(ctypes.byref(x) for x in self._c)
 
     def validate(self):
-        _check(self._L.fgv_validate_shard_dev(*self._val))
-        if self._pre is not None:
-            _check(self._L.fgv_presplit(*self._pre))
+        if self._next is None:
+            _check(self._L.fgv_validate_shard_dev(*self._val))
+        else:
+            _check(self._L.fgv_validate_shard_dev_next(*self._val, *self._next))
 
     def finalize(self):
         _check(self._fin_fn(*self._fin))
@@ -370,6 +374,19 @@ class Engine:
         hi = None if tx_hi is None else np.ascontiguousarray(tx_hi, dtype=np.uint32)
         _check(self._L.fgv_presplit(self._h, batch.nb, batch.ptrs, batch.lens, None if lo is None else _ptr(lo),
                                     None if hi is None else _ptr(hi)))
+
+    def validate_shard_dev_next(self, batch, tx_lo, tx_hi, d_results, cap, next_batch, next_lo=None, next_hi=None):
+        """fgv_validate_shard_dev_next: validate `batch`, pre-splitting `next_batch` while the
+        GPU works.  Returns ntx per block of `batch`."""
+        lo = np.ascontiguousarray(tx_lo, dtype=np.uint32)
+        hi = np.ascontiguousarray(tx_hi, dtype=np.uint32)
+        nlo = None if next_lo is None else np.ascontiguousarray(next_lo, dtype=np.uint32)
+        nhi = None if next_hi is None else np.ascontiguousarray(next_hi, dtype=np.uint32)
+        _check(self._L.fgv_validate_shard_dev_next(self._h, batch.nb, batch.ptrs, batch.lens, batch.dptr, _ptr(lo),
+                                                   _ptr(hi), ctypes.c_void_p(d_results), cap, batch.ntx,
+                                                   next_batch.nb, next_batch.ptrs, next_batch.lens, _ptr(nlo),
+                                                   _ptr(nhi)))
+        return np.ctypeslib.as_array(batch.ntx).astype(np.uint64)
 
     def last_presplit(self):
         return bool(self._L.fgv_last_presplit(self._h))

@@ -787,9 +787,11 @@ __global__ __launch_bounds__(64) void k_bd_sha_payload(uint32_t ntx, const uint3
 // SHA_E_LANES lanes per transaction for its endorsements (lane j: endorsements j, j + SHA_E_LANES, ...),
 // then txid / proposal / index.  (k_bd_count may turn a pending creator into code 4
 // meanwhile; those digests go unused.)
-__global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__restrict__ txs,
-                                               const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
-                                               unsigned long long *__restrict__ nblk) {
+template <int PRIO>
+__device__ __forceinline__ void bd_sha_body(uint32_t ntx, const DevTx *__restrict__ txs,
+                                            const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                            unsigned long long *__restrict__ nblk) {
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t row = l / ntx, t = l - row * ntx;  // rows: E x SHA_E_LANES | T | P | I
   uint64_t blocks = 0;
@@ -835,6 +837,18 @@ __global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__rest
   }
   for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
   if ((threadIdx.x & 63) == 0 && blocks) atomicAdd(nblk, (unsigned long long)blocks);
+}
+// wave priority of the non-payload hashes (A/B: FGV_SHA_PRIO; the main-stream chain runs at 3,
+// the payload chains at 2)
+__global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__restrict__ txs,
+                                               const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                               unsigned long long *__restrict__ nblk) {
+  bd_sha_body<0>(ntx, txs, bases, dig, nblk);
+}
+__global__ __launch_bounds__(64) void k_bd_sha_p2(uint32_t ntx, const DevTx *__restrict__ txs,
+                                                  const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                                  unsigned long long *__restrict__ nblk) {
+  bd_sha_body<2>(ntx, txs, bases, dig, nblk);
 }
 
 // ============================================================ k_bd_emit

@@ -1090,6 +1090,7 @@ __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
 __global__ void k_bd_sha(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
+__global__ void k_bd_sha_p2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
 __global__ void k_bd_sha_payload(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, uint8_t *dig,
                                  unsigned long long *nblk);
 __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
@@ -1232,7 +1233,11 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   // (third stream: concurrent with the payload chains still running on stream2)
   HIP_TRY(hipEventRecord(c->ev[7], st));
   HIP_TRY(hipStreamWaitEvent(c->stream3, c->ev[7], 0));
-  hipLaunchKernelGGL(k_bd_sha, dim3((uint32_t)(((uint64_t)N * (SHA_E_LANES + 3) + 63) / 64)), dim3(64), 0, c->stream3, N,
+  static const int sha_prio = [] {
+    const char *e = getenv("FGV_SHA_PRIO");
+    return e ? atoi(e) : 0;
+  }();
+  hipLaunchKernelGGL(sha_prio == 2 ? k_bd_sha_p2 : k_bd_sha, dim3((uint32_t)(((uint64_t)N * (SHA_E_LANES + 3) + 63) / 64)), dim3(64), 0, c->stream3, N,
                      dtx, dbs, c->bj_dig.as<uint8_t>(), nblk);
   HIP_TRY(hipEventRecord(c->ev_pay[2], c->stream3));
   HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_pay[2], 0));
@@ -1243,6 +1248,10 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   HIP_TRY(hipGetLastError());
   uint32_t *hm = c->hb_misc.as<uint32_t>();
   HIP_TRY(hipMemcpyAsync(hm, misc, 32, hipMemcpyDeviceToHost, st));
+  if (c->next.n) {  // the next batch's framing walk, while this batch's parse runs on the GPU
+    fgv_block_presplit(S, c->device, c->next.n, c->next.blocks, c->next.lens, c->next.lo, c->next.hi);
+    c->next.n = 0;
+  }
   HIP_TRY(hipStreamSynchronize(st));
   if (hm[5] & 1u) return 1;  // capacity overflow: host parser
   const size_t nv = (size_t)hm[BJ_C] + hm[BJ_E];

@@ -895,6 +895,25 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   return FGV_OK;
 }
 
+int fgv_validate_shard_dev_next(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                                void *d_results, size_t results_cap, size_t *ntx, size_t next_nblocks,
+                                const uint8_t *const *next_blocks, const size_t *next_lens, const uint32_t *next_lo,
+                                const uint32_t *next_hi) {
+  if (!c || (next_nblocks && (!next_blocks || !next_lens))) return FGV_EINVAL;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks, next_lens, next_lo, next_hi};
+  }
+  int rc = fgv_validate_shard_dev(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->next.n) {  // not started inside (host-parse path, empty batch, early error): start it now
+    fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, c->next.lo, c->next.hi);
+    c->next.n = 0;
+  }
+  return rc;
+}
+
 int fgv_presplit(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens, const uint32_t *tx_lo,
                  const uint32_t *tx_hi) {
   if (!c || (nblocks && (!blocks || !lens))) return FGV_EINVAL;

@@ -131,8 +131,15 @@ struct fgv_ctx {
   // device-resident committer path (blockdev.hip)
   bool stage_ran = false;
   hipEvent_t digests_ready = nullptr;  // k_prep waits for it when set (digests from another stream)
-  hipEvent_t digests_ready2 = nullptr;
-  bool last_presplit = false;  // the last device-parse call used a fgv_presplit result  // ... and for this one (a second producing stream)
+  hipEvent_t digests_ready2 = nullptr;  // ... and for this one (a second producing stream)
+  bool last_presplit = false;  // the last device-parse call used a fgv_presplit result
+  // fgv_validate_shard_dev_next: the batch to pre-split once this call's GPU work is queued
+  struct NextBatch {
+    size_t n = 0;
+    const uint8_t *const *blocks = nullptr;
+    const size_t *lens = nullptr;
+    const uint32_t *lo = nullptr, *hi = nullptr;
+  } next;
   DevBuf bd_env, bd_bases, bd_tx, bd_ident, bd_jobs, bd_misc;
   HostBuf hb_env, hb_bases, hb_misc;
   double t_bd_split = 0, t_bd_pre = 0, t_bd_fold = 0;

@@ -199,6 +199,15 @@ int fgv_validate_shard_dev(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *b
 int fgv_presplit(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                  const uint32_t *tx_lo, const uint32_t *tx_hi);
 int fgv_last_presplit(fgv_ctx *ctx);
+/* fgv_validate_shard_dev of the current batch that also pre-splits the NEXT batch (next_*,
+ * same meaning as fgv_presplit's arguments) as soon as the current batch's GPU work is
+ * queued, so the walk overlaps the current validation instead of following it. */
+int fgv_validate_shard_dev_next(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
+                                const size_t *lens, const uint8_t *const *d_blocks,
+                                const uint32_t *tx_lo, const uint32_t *tx_hi, void *d_results,
+                                size_t results_cap, size_t *ntx, size_t next_nblocks,
+                                const uint8_t *const *next_blocks, const size_t *next_lens,
+                                const uint32_t *next_lo, const uint32_t *next_hi);
 int fgv_finalize_flags_dev(fgv_ctx *ctx, size_t nblocks, const size_t *ntx, uint32_t world,
                            size_t rows_per_rank, const void *d_gathered, uint8_t *flags);
 /* Any shard plan: rank r's rows hold transactions [rank_lo[r*nblocks+b], rank_hi[r*nblocks+b])

@@ -239,6 +239,32 @@ def test_presplit_is_used_only_for_its_batch(shards, mode):
     eng.close()
 
 
+@pytest.mark.parametrize("shards,mode", [(1, "tx"), (3, "tx"), (2, "block")])
+def test_validate_next_presplits_the_following_call(shards, mode):
+    """fgv_validate_shard_dev_next: rank r's call pre-splits rank r+1's range during its own
+    GPU work; every following call uses it; flags identical to the oracle."""
+    import torch
+    from fabric_amd import shard
+    net = network()
+    blks = [blocks.make_block(net, n, number=1 + i, seed=95 + i)[0] for i, n in enumerate([40, 7, 29])]
+    ntx = np.array([40, 7, 29], dtype=np.int64)
+    eng = _engine_for(net)
+    plan = shard.plan(ntx, shards, mode)
+    rows = shard.plan_rows(*plan)
+    batch = eng.block_batch(blks)
+    exp = _oracle(net, blks)
+    recv = torch.zeros((shards * rows, shard.REC), dtype=torch.uint8, device="cuda")
+    for rep in range(2):
+        for r in range(shards):
+            q = (r + 1) % shards
+            eng.validate_shard_dev_next(batch, plan[0][r], plan[1][r], recv[r * rows:].data_ptr(), rows, batch,
+                                        plan[0][q], plan[1][q])
+            assert eng.last_presplit() == (rep > 0 or r > 0)
+        flags = eng.finalize_flags_dev(ntx, shards, rows, recv.data_ptr(), plan=None if mode == "tx" else plan)
+        assert list(flags) == exp[0] + exp[1] + exp[2]
+    eng.close()
+
+
 def _random_records(rng, ntx, pool):
     """fgv_tx_result records honouring the engine's invariants: VALID => REACHED;
     REACHED => INDEXED with index_txid == txid."""
