@@ -85,21 +85,26 @@ struct StateSlot {  // committed state: open addressing, key bytes in the arena
 };
 struct BlkSlot {    // keys written in the block
   uint32_t owner;   // write index + 1 (0 = empty)
-  uint32_t fw_cand, fw_valid, pad;
+  uint32_t pad;
+  // fixpoint round r's first writers, (r << 32) | (0xFFFFFFFF - tx) by atomicMax: a value left
+  // by an earlier round reads as "none", so no per-round reset pass is needed
+  uint64_t fw_cand, fw_valid;
   uint64_t last;    // (tx << 32) | (write index + 1) of the last VALID writer
 };
 __global__ void k_mv_tags(const MvKey *keys, uint32_t n, uint64_t *tags);
+__global__ void k_mv_tags2(const MvKey *reads, uint32_t nr, uint64_t *rtags, const MvKey *writes, uint32_t nw,
+                           uint64_t *wtags);
+__global__ void k_mv_find_init(const MvKey *reads, const uint64_t *rtags, uint32_t n, const BlkSlot *tbl, uint32_t mask,
+                               const MvKey *writes, const uint64_t *wtags, uint32_t *rslot, uint32_t ntx,
+                               const uint8_t *part, const uint8_t *bad_tx, uint8_t *st);
 __global__ void k_mv_lookup(const MvKey *reads, const uint64_t *tags, uint32_t n, const StateSlot *tbl, uint64_t mask,
                             const uint8_t *arena, uint8_t *bad_tx);
 __global__ void k_mv_blk_insert(const MvKey *writes, const uint64_t *tags, uint32_t n, BlkSlot *tbl, uint32_t mask,
                                 uint32_t *wslot);
-__global__ void k_mv_blk_find(const MvKey *reads, const uint64_t *rtags, uint32_t n, const BlkSlot *tbl, uint32_t mask,
-                              const MvKey *writes, const uint64_t *wtags, uint32_t *rslot);
-__global__ void k_mv_init(uint32_t ntx, const uint8_t *part, const uint8_t *bad_tx, uint8_t *st);
-__global__ void k_mv_reset(BlkSlot *tbl, uint32_t cap);
-__global__ void k_mv_min(const MvKey *writes, const uint32_t *wslot, uint32_t n, const uint8_t *st, BlkSlot *tbl);
+__global__ void k_mv_min(const MvKey *writes, const uint32_t *wslot, uint32_t n, const uint8_t *st, BlkSlot *tbl,
+                         uint32_t round, uint32_t *undecided);
 __global__ void k_mv_decide(uint32_t ntx, const uint32_t *rbeg, const uint32_t *rslot, const BlkSlot *tbl, uint8_t *st,
-                            uint32_t *undecided);
+                            uint32_t round, uint32_t *undecided);
 __global__ void k_mv_lastwriter(const MvKey *writes, const uint32_t *wslot, uint32_t n, const uint8_t *st, BlkSlot *tbl);
 __global__ void k_mv_apply_find(const BlkSlot *btbl, uint32_t bcap, const MvKey *writes, const uint64_t *wtags,
                                 StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint64_t block_num, uint32_t *pend,

@@ -322,8 +322,9 @@ int fgv_mvcc_validate_block(fgv_ctx *c, const uint8_t *block, size_t len, const 
   HIP_TRY(hipMemsetAsync(M->bad.p, 0, ntx + 1, s));
   HIP_TRY(hipMemsetAsync(M->btbl.p, 0, bcap * sizeof(BlkSlot), s));
   HIP_TRY(hipEventRecord(c->ev[0], s));
-  if (nr) hipLaunchKernelGGL(k_mv_tags, grid_for(nr), dim3(256), 0, s, M->reads.as<MvKey>(), (uint32_t)nr, M->rtags.as<uint64_t>());
-  if (nw) hipLaunchKernelGGL(k_mv_tags, grid_for(nw), dim3(256), 0, s, M->writes.as<MvKey>(), (uint32_t)nw, M->wtags.as<uint64_t>());
+  if (nr + nw)
+    hipLaunchKernelGGL(k_mv_tags2, grid_for(nr + nw), dim3(256), 0, s, M->reads.as<MvKey>(), (uint32_t)nr,
+                       M->rtags.as<uint64_t>(), M->writes.as<MvKey>(), (uint32_t)nw, M->wtags.as<uint64_t>());
   if (nr)
     hipLaunchKernelGGL(k_mv_lookup, grid_for(nr), dim3(256), 0, s, M->reads.as<MvKey>(), M->rtags.as<uint64_t>(),
                        (uint32_t)nr, M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(), M->bad.as<uint8_t>());
@@ -331,25 +332,21 @@ int fgv_mvcc_validate_block(fgv_ctx *c, const uint8_t *block, size_t len, const 
   if (nw)
     hipLaunchKernelGGL(k_mv_blk_insert, grid_for(nw), dim3(256), 0, s, M->writes.as<MvKey>(), M->wtags.as<uint64_t>(),
                        (uint32_t)nw, M->btbl.as<BlkSlot>(), bcap - 1, M->wslot.as<uint32_t>());
-  if (nr)
-    hipLaunchKernelGGL(k_mv_blk_find, grid_for(nr), dim3(256), 0, s, M->reads.as<MvKey>(), M->rtags.as<uint64_t>(),
-                       (uint32_t)nr, M->btbl.as<BlkSlot>(), bcap - 1, M->writes.as<MvKey>(), M->wtags.as<uint64_t>(),
-                       M->rslot.as<uint32_t>());
-  hipLaunchKernelGGL(k_mv_init, grid_for(ntx), dim3(256), 0, s, (uint32_t)ntx, M->part.as<uint8_t>(),
-                     M->bad.as<uint8_t>(), M->st.as<uint8_t>());
+  hipLaunchKernelGGL(k_mv_find_init, grid_for(nr + ntx), dim3(256), 0, s, M->reads.as<MvKey>(), M->rtags.as<uint64_t>(),
+                     (uint32_t)nr, M->btbl.as<BlkSlot>(), bcap - 1, M->writes.as<MvKey>(), M->wtags.as<uint64_t>(),
+                     M->rslot.as<uint32_t>(), (uint32_t)ntx, M->part.as<uint8_t>(), M->bad.as<uint8_t>(),
+                     M->st.as<uint8_t>());
   HIP_TRY(hipGetLastError());
   // fixpoint: two rounds per host check
   uint32_t undec = 1, rounds = 0;
   while (undec) {
     for (int k = 0; k < 2; k++) {
-      hipLaunchKernelGGL(k_mv_reset, grid_for(bcap), dim3(256), 0, s, M->btbl.as<BlkSlot>(), bcap);
-      if (nw)
-        hipLaunchKernelGGL(k_mv_min, grid_for(nw), dim3(256), 0, s, M->writes.as<MvKey>(), M->wslot.as<uint32_t>(),
-                           (uint32_t)nw, M->st.as<uint8_t>(), M->btbl.as<BlkSlot>());
-      HIP_TRY(hipMemsetAsync(M->undec.p, 0, 4, s));
+      rounds++;  // round tags start at 1 (the write table was zeroed above)
+      hipLaunchKernelGGL(k_mv_min, grid_for(nw ? nw : 1), dim3(256), 0, s, M->writes.as<MvKey>(), M->wslot.as<uint32_t>(),
+                         (uint32_t)nw, M->st.as<uint8_t>(), M->btbl.as<BlkSlot>(), rounds, M->undec.as<uint32_t>());
       hipLaunchKernelGGL(k_mv_decide, grid_for(ntx), dim3(256), 0, s, (uint32_t)ntx, M->rbeg.as<uint32_t>(),
-                         M->rslot.as<uint32_t>(), M->btbl.as<BlkSlot>(), M->st.as<uint8_t>(), M->undec.as<uint32_t>());
-      rounds++;
+                         M->rslot.as<uint32_t>(), M->btbl.as<BlkSlot>(), M->st.as<uint8_t>(), rounds,
+                         M->undec.as<uint32_t>());
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(&undec, M->undec.p, 4, hipMemcpyDeviceToHost, s));

@@ -46,6 +46,16 @@ __global__ __launch_bounds__(256) void k_mv_tags(const MvKey *__restrict__ keys,
   tags[i] = mv_tag(reinterpret_cast<const uint8_t *>(k.ptr), k.len, k.ns);
 }
 
+// reads and writes of a block in one launch
+__global__ __launch_bounds__(256) void k_mv_tags2(const MvKey *__restrict__ reads, uint32_t nr,
+                                                  uint64_t *__restrict__ rtags, const MvKey *__restrict__ writes,
+                                                  uint32_t nw, uint64_t *__restrict__ wtags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nr + nw) return;
+  const MvKey k = i < nr ? reads[i] : writes[i - nr];
+  (i < nr ? rtags[i] : wtags[i - nr]) = mv_tag(reinterpret_cast<const uint8_t *>(k.ptr), k.len, k.ns);
+}
+
 // ---- committed state lookups (reads): static version check
 __device__ __forceinline__ int64_t state_find(const StateSlot *tbl, uint64_t mask, const uint8_t *arena,
                                               uint64_t tag, const uint8_t *key, uint32_t len, uint32_t ns) {
@@ -97,12 +107,29 @@ __global__ __launch_bounds__(256) void k_mv_blk_insert(const MvKey *__restrict__
   wslot[i] = FW_INF;  // table full: host sizes it at >= 2x the writes, unreachable
 }
 
-__global__ __launch_bounds__(256) void k_mv_blk_find(const MvKey *__restrict__ reads, const uint64_t *__restrict__ rtags,
-                                                     uint32_t n, const BlkSlot *__restrict__ tbl, uint32_t mask,
-                                                     const MvKey *__restrict__ writes,
-                                                     const uint64_t *__restrict__ wtags, uint32_t *__restrict__ rslot) {
+// ---- fixpoint
+__device__ __forceinline__ uint64_t fw_enc(uint32_t round, uint32_t tx) {
+  return ((uint64_t)round << 32) | (0xFFFFFFFFu - tx);
+}
+__device__ __forceinline__ uint32_t fw_dec(uint64_t v, uint32_t round) {  // FW_INF: no writer this round
+  return (uint32_t)(v >> 32) == round ? 0xFFFFFFFFu - (uint32_t)v : FW_INF;
+}
+
+// read -> written-key slot for i < n (a probe of the block's write table; exact key compare),
+// then the initial fixpoint state of
+// transaction i - n (after k_mv_lookup's static version check)
+__global__ __launch_bounds__(256) void k_mv_find_init(const MvKey *__restrict__ reads, const uint64_t *__restrict__ rtags,
+                                                      uint32_t n, const BlkSlot *__restrict__ tbl, uint32_t mask,
+                                                      const MvKey *__restrict__ writes,
+                                                      const uint64_t *__restrict__ wtags, uint32_t *__restrict__ rslot,
+                                                      uint32_t ntx, const uint8_t *__restrict__ part,
+                                                      const uint8_t *__restrict__ bad_tx, uint8_t *__restrict__ st) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n) {
+    const uint32_t t = i - n;
+    if (t < ntx) st[t] = (part[t] && !bad_tx[t]) ? ST_UNDEC : ST_INVALID;
+    return;
+  }
   const MvKey r = reads[i];
   const uint64_t tag = rtags[i];
   uint32_t idx = (uint32_t)tag & mask;
@@ -121,47 +148,37 @@ __global__ __launch_bounds__(256) void k_mv_blk_find(const MvKey *__restrict__ r
   rslot[i] = out;
 }
 
-// ---- fixpoint
-__global__ __launch_bounds__(256) void k_mv_init(uint32_t ntx, const uint8_t *__restrict__ part,
-                                                 const uint8_t *__restrict__ bad_tx, uint8_t *__restrict__ st) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ntx) return;
-  st[i] = (part[i] && !bad_tx[i]) ? ST_UNDEC : ST_INVALID;
-}
-
-__global__ __launch_bounds__(256) void k_mv_reset(BlkSlot *__restrict__ tbl, uint32_t cap) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cap) return;
-  tbl[i].fw_cand = FW_INF;
-  tbl[i].fw_valid = FW_INF;
-}
-
+// round r (>= 1): first non-invalid and first valid writer of every written key; also zeroes
+// the round's undecided count (k_mv_decide follows on the stream)
 __global__ __launch_bounds__(256) void k_mv_min(const MvKey *__restrict__ writes, const uint32_t *__restrict__ wslot,
-                                                uint32_t n, const uint8_t *__restrict__ st, BlkSlot *__restrict__ tbl) {
+                                                uint32_t n, const uint8_t *__restrict__ st, BlkSlot *__restrict__ tbl,
+                                                uint32_t round, uint32_t *__restrict__ undecided) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *undecided = 0u;
   if (i >= n) return;
   const uint32_t tx = writes[i].tx;
   const uint8_t s = st[tx];
   if (s == ST_INVALID) return;
   const uint32_t k = wslot[i];
-  atomicMin(&tbl[k].fw_cand, tx);
-  if (s == ST_VALID) atomicMin(&tbl[k].fw_valid, tx);
+  atomicMax(reinterpret_cast<unsigned long long *>(&tbl[k].fw_cand), (unsigned long long)fw_enc(round, tx));
+  if (s == ST_VALID) atomicMax(reinterpret_cast<unsigned long long *>(&tbl[k].fw_valid), (unsigned long long)fw_enc(round, tx));
 }
 
 __global__ __launch_bounds__(256) void k_mv_decide(uint32_t ntx, const uint32_t *__restrict__ rbeg,
                                                    const uint32_t *__restrict__ rslot, const BlkSlot *__restrict__ tbl,
-                                                   uint8_t *__restrict__ st, uint32_t *__restrict__ undecided) {
+                                                   uint8_t *__restrict__ st, uint32_t round,
+                                                   uint32_t *__restrict__ undecided) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= ntx || st[i] != ST_UNDEC) return;
   bool all_clear = true, conflict = false;
   for (uint32_t r = rbeg[i]; r < rbeg[i + 1]; r++) {
     const uint32_t k = rslot[r];
     if (k == FW_INF) continue;  // key never written in this block
-    if (tbl[k].fw_valid < i) {
+    if (fw_dec(tbl[k].fw_valid, round) < i) {
       conflict = true;
       break;
     }
-    if (tbl[k].fw_cand < i) all_clear = false;
+    if (fw_dec(tbl[k].fw_cand, round) < i) all_clear = false;
   }
   if (conflict) st[i] = ST_INVALID;
   else if (all_clear) st[i] = ST_VALID;
