@@ -316,17 +316,21 @@ def run_mvcc(args, world, rank, local, dev):
     ok = True
     for i in range(W):
         b, labels, flags = blocks[i]
-        ok &= bool((eng.mvcc_validate(b, 1001 + i, flags, commit=True, d_block=dptr[i]) == labels).all())
+        nb = blocks[i + 1][0] if not args.no_presplit else None
+        ok &= bool((eng.mvcc_validate(b, 1001 + i, flags, commit=True, d_block=dptr[i], next_block=nb) == labels).all())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     lookup = total = 0.0
     rounds = []
     outs = []
+    # block i+1's framing is walked on the engine's host worker while block i validates
+    # (fgv_mvcc_validate_block_next; a peer has the next block in hand while it commits this one)
     t0 = time.perf_counter()
     for i in range(W, W + K):
         b, labels, flags = blocks[i]
-        outs.append(eng.mvcc_validate(b, 1001 + i, flags, commit=True, d_block=dptr[i]))
+        nb = blocks[i + 1][0] if i + 1 < W + K and not args.no_presplit else None
+        outs.append(eng.mvcc_validate(b, 1001 + i, flags, commit=True, d_block=dptr[i], next_block=nb))
         s = eng.mvcc_stats()
         lookup += s["lookup_ms"]
         total += s["total_ms"]

@@ -23,7 +23,7 @@ EXPORTED = [
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
-    "fgv_presplit", "fgv_last_presplit", "fgv_validate_shard_dev_next",
+    "fgv_presplit", "fgv_last_presplit", "fgv_validate_shard_dev_next", "fgv_mvcc_validate_block_next",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode",
 ]
@@ -112,6 +112,7 @@ def load():
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
         L.fgv_mvcc_validate_block.argtypes = [vp, vp, sz, vp, ctypes.c_uint64, vp, sz, ctypes.c_int]
+        L.fgv_mvcc_validate_block_next.argtypes = [vp, vp, sz, vp, ctypes.c_uint64, vp, sz, ctypes.c_int, vp, sz]
         L.fgv_mvcc_last_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.POINTER(ctypes.c_uint32)]
@@ -423,12 +424,19 @@ class Engine:
         _check(self._L.fgv_statedb_load(self._h, ns.encode(), _ptr(arena), _ptr(offs), _ptr(lens), _ptr(blk),
                                         _ptr(txn), len(keys)))
 
-    def mvcc_validate(self, block: bytes, block_num: int, flags, commit=True, d_block=None):
-        """flags: committer TxValidationFlags (updated copy returned)."""
+    def mvcc_validate(self, block: bytes, block_num: int, flags, commit=True, d_block=None, next_block=None):
+        """flags: committer TxValidationFlags (updated copy returned).  next_block: bytes of the
+        block validated next (its framing is walked meanwhile; keep the object alive)."""
         f = np.array(flags, dtype=np.uint8)
         buf = np.frombuffer(block, dtype=np.uint8)
-        _check(self._L.fgv_mvcc_validate_block(self._h, buf.ctypes.data, len(block), d_block, block_num, _ptr(f),
-                                               len(f), 1 if commit else 0))
+        if next_block is None:
+            _check(self._L.fgv_mvcc_validate_block(self._h, buf.ctypes.data, len(block), d_block, block_num, _ptr(f),
+                                                   len(f), 1 if commit else 0))
+        else:
+            nb = np.frombuffer(next_block, dtype=np.uint8)
+            _check(self._L.fgv_mvcc_validate_block_next(self._h, buf.ctypes.data, len(block), d_block, block_num,
+                                                        _ptr(f), len(f), 1 if commit else 0, nb.ctypes.data,
+                                                        len(next_block)))
         return f
 
     def mvcc_stats(self):

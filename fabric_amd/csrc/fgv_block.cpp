@@ -1163,6 +1163,19 @@ int fgv_block_presplit(fgv_block_state *S, int device, size_t nblocks, const uin
   return FGV_OK;
 }
 
+// MVCC (fgv_mvcc_validate_block): the envelope spans of `block` from a pre-split of exactly
+// this one block, if one was requested; a pre-split of another batch is left pending.
+bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t len, std::vector<Span> &out) {
+  PreSplit &P = S->pre;
+  if (!P.active || !P.matches(1, &block, &len, nullptr, nullptr)) return false;
+  P.join();
+  if (P.rc != FGV_OK || P.out.ntx.size() != 1) return false;
+  const uint32_t *e = P.et.as<uint32_t>();
+  out.resize(P.out.total);
+  for (size_t i = 0; i < P.out.total; i++, e += BD_ENV_WORDS) out[i] = Span{block + e[1], e[2]};
+  return true;
+}
+
 int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
                            const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                            const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out) {

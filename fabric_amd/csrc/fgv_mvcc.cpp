@@ -21,6 +21,8 @@
 #include "fgv_internal.h"
 #include "fgv_visitors.h"
 
+bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t len, std::vector<Span> &out);
+
 using namespace fgvb;
 
 namespace {
@@ -109,6 +111,7 @@ struct fgv_mvcc_state {
   DevBuf tbl, arena, top;
   DevBuf reads, writes, rtags, wtags, btbl, wslot, rslot, rbeg, part, bad, st, undec, pend, npend, flags, lbytes, lkeys;
   std::vector<MvTx> txs;
+  std::vector<Span> pre_envs;  // envelope spans taken from a pre-split
   HostBuf hreads, hwrites, hmeta;  // pinned staging of the MvKey arrays, rbeg and part
   uint32_t last_rounds = 0;
 };
@@ -227,16 +230,37 @@ int fgv_statedb_load(fgv_ctx *c, const char *ns, const uint8_t *key_buf, const u
   return FGV_OK;
 }
 
+static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block, uint64_t block_num,
+                         uint8_t *flags, size_t ntx, int commit, const uint8_t *next, size_t next_len);
+
 int fgv_mvcc_validate_block(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block,
                             uint64_t block_num, uint8_t *flags, size_t ntx, int commit) {
+  return mvcc_validate(c, block, len, d_block, block_num, flags, ntx, commit, nullptr, 0);
+}
+
+int fgv_mvcc_validate_block_next(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block,
+                                 uint64_t block_num, uint8_t *flags, size_t ntx, int commit, const uint8_t *next,
+                                 size_t next_len) {
+  if (next && !next_len) return FGV_EINVAL;
+  return mvcc_validate(c, block, len, d_block, block_num, flags, ntx, commit, next, next_len);
+}
+
+}  // extern "C"
+
+static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block, uint64_t block_num,
+                         uint8_t *flags, size_t ntx, int commit, const uint8_t *next, size_t next_len) {
   if (!c || !block || (ntx && !flags)) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   fgv_mvcc_state *M = c->mv;
   if (!M) return FGV_ESTATE;
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  // the block's envelope spans: from fgv_presplit of this block (walked while the previous
+  // block validated), else walked here (one dependent load per envelope)
   VBlock blk;
-  if (!pbw::decode(block, len, blk)) return FGV_EINVAL;
-  const std::vector<Span> &envs = blk.data.data;
+  const bool pre = fgv_block_take_presplit(c->blk, block, len, M->pre_envs);
+  if (!pre && !pbw::decode(block, len, blk)) return FGV_EINVAL;
+  const std::vector<Span> &envs = pre ? M->pre_envs : blk.data.data;
+  if (next) fgv_block_presplit(c->blk, c->device, 1, &next, &next_len, nullptr, nullptr);  // the next block's walk
   if (envs.size() != ntx) return FGV_EINVAL;
   const uint8_t *dblk = d_block;
   if (!dblk) {
@@ -390,6 +414,8 @@ int fgv_mvcc_validate_block(fgv_ctx *c, const uint8_t *block, size_t len, const 
   }
   return FGV_OK;
 }
+
+extern "C" {
 
 int fgv_mvcc_last_stats(fgv_ctx *c, double *lookup_ms, double *total_ms, uint64_t *reads, uint64_t *writes,
                         uint32_t *rounds) {

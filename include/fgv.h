@@ -238,6 +238,13 @@ int fgv_statedb_load(fgv_ctx *ctx, const char *ns, const uint8_t *key_buf, const
  * FGV_EUNSUPPORTED. */
 int fgv_mvcc_validate_block(fgv_ctx *ctx, const uint8_t *block, size_t len, const uint8_t *d_block,
                             uint64_t block_num, uint8_t *flags, size_t ntx, int commit);
+/* fgv_mvcc_validate_block that also walks the NEXT block's framing (next, next_len; the
+ * buffer must stay unchanged until that block's call) on the engine's host worker while this
+ * block validates; that call then starts from the walked envelope spans (fgv_presplit of one
+ * block does the same from outside).  Results never depend on it. */
+int fgv_mvcc_validate_block_next(fgv_ctx *ctx, const uint8_t *block, size_t len, const uint8_t *d_block,
+                                 uint64_t block_num, uint8_t *flags, size_t ntx, int commit,
+                                 const uint8_t *next, size_t next_len);
 int fgv_mvcc_last_stats(fgv_ctx *ctx, double *lookup_ms, double *total_ms, uint64_t *reads,
                         uint64_t *writes, uint32_t *rounds);
 

@@ -30,6 +30,24 @@ def test_blocks_match_oracle_and_labels():
     eng.close()
 
 
+def test_next_block_presplit_matches():
+    """fgv_mvcc_validate_block_next (block k+1's framing walked while block k validates) and a
+    pre-split of an unrelated block left pending: same codes as the oracle and the labels."""
+    st = M.MvccState(50_000, seed=5)
+    db = _db(st)
+    eng = _engine(st)
+    blks = [M.make_block(st, 1500, number=1001 + b, seed=20 + b) for b in range(4)]
+    stray = eng.block_batch([M.make_block(st, 50, number=9999, seed=99)[0]])
+    for b, (blk, labels, flags) in enumerate(blks):
+        if b == 2:
+            eng.presplit(stray)  # not this block's: must be ignored
+        nxt = blks[b + 1][0] if b + 1 < len(blks) else None
+        exp = OM.validate_block(db, blk, flags, 1001 + b, commit=True)
+        got = eng.mvcc_validate(blk, 1001 + b, flags, commit=True, next_block=nxt)
+        assert list(got) == list(exp) == list(labels), b
+    eng.close()
+
+
 def test_known_answers_and_chains():
     db = OM.StateDB({("ns1", "key%d" % i): (1, i - 1) for i in range(1, 6)})
     eng = _lib.Engine(0)
