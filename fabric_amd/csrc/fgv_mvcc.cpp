@@ -42,10 +42,15 @@ struct MvTx {
   std::vector<MvRead> reads;       // (vectors keep their capacity across blocks)
   std::vector<MvWrite> writes;
   std::vector<uint32_t> rns, wns;  // namespace id of each read / write
+  std::vector<std::string> hashed_ns;  // ns + "$$h" + coll of the private-data sets read/written
   uint64_t wbytes = 0;
 };
 
 constexpr uint8_t MV_UNSUP = 0xFD, MV_SKIP = 0xFF;
+// SHA-256("") = rwsetutil.hashOfZeroLengthByteArray (rwset_proto_util.go:370)
+constexpr uint8_t kEmptySha256[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
+                                      0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
+                                      0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
 
 // GetActionFromEnvelope + TxRwSet.FromProtoBytes for one committer-valid transaction
 void mv_parse(Span d, MvTx &T) {
@@ -81,6 +86,12 @@ void mv_parse(Span d, MvTx &T) {
   bool unsup = false;
   static thread_local std::vector<VKVRead> reads;
   static thread_local std::vector<VKVWrite> writes;
+  static thread_local std::vector<VHashRead> hreads;
+  static thread_local std::vector<VHashWrite> hwrites;
+  size_t ncoll = 0;
+  for (const VNsRwSet &ns : rw.ns) ncoll += ns.coll.size();
+  T.hashed_ns.clear();
+  T.hashed_ns.reserve(ncoll);  // spans below point into these strings: no reallocation after this
   for (VNsRwSet &ns : rw.ns) {
     reads.clear();
     writes.clear();
@@ -88,16 +99,38 @@ void mv_parse(Span d, MvTx &T) {
     kv.reads = &reads;
     kv.writes = &writes;
     if (!pbw::decode(ns.rwset.p, ns.rwset.n, kv)) { T.code = 255; return; }
-    for (const VCollHashed &c : ns.coll) {
-      VHashedRWSet h;
-      if (!pbw::decode(c.hashed.p, c.hashed.n, h)) { T.code = 255; return; }
-      if (h.nreads || h.nwrites || h.nmeta) unsup = true;  // private data: not modelled
-    }
     if (kv.nrq || kv.nmeta) unsup = true;  // phantom checks / metadata writes: not modelled
     for (const VKVRead &r : reads) T.reads.push_back(MvRead{ns.ns, r.key, r.has_ver, r.ver.block, r.ver.tx});
+    // IsKVWriteDelete (rwsetutil/rwset_proto_util.go:366-368): is_delete or an empty value
     for (const VKVWrite &w : writes) {
-      T.writes.push_back(MvWrite{ns.ns, w.key, w.is_delete});
+      T.writes.push_back(MvWrite{ns.ns, w.key, w.is_delete || w.value.n == 0});
       T.wbytes += w.key.n;
+    }
+    // private data: validateKVReadHash (validation/validator.go:272-293) is a point read of the
+    // key hash in the hashed-data namespace ns + "$$h" + coll (privacyenabledstate/db.go:355-357)
+    for (const VCollHashed &c : ns.coll) {
+      hreads.clear();
+      hwrites.clear();
+      VHashedRWSet h;
+      h.reads = &hreads;
+      h.writes = &hwrites;
+      if (!pbw::decode(c.hashed.p, c.hashed.n, h)) { T.code = 255; return; }
+      if (h.nmeta) unsup = true;  // hashed metadata writes: not modelled
+      if (hreads.empty() && hwrites.empty()) continue;
+      T.hashed_ns.emplace_back();
+      std::string &hn = T.hashed_ns.back();
+      hn.reserve(ns.ns.n + 3 + c.name.n);
+      hn.append((const char *)ns.ns.p, ns.ns.n).append("$$h").append((const char *)c.name.p, c.name.n);
+      const Span hs{(const uint8_t *)hn.data(), (uint32_t)hn.size()};
+      for (const VHashRead &r : hreads) T.reads.push_back(MvRead{hs, r.key, r.has_ver, r.ver.block, r.ver.tx});
+      // IsKVWriteHashDelete (rwset_proto_util.go:373-375): is_delete, empty value hash, or the
+      // hash of the empty string
+      for (const VHashWrite &w : hwrites) {
+        const bool del = w.is_delete || w.value_hash.n == 0 ||
+                         (w.value_hash.n == 32 && memcmp(w.value_hash.p, kEmptySha256, 32) == 0);
+        T.writes.push_back(MvWrite{hs, w.key, del});
+        T.wbytes += w.key.n;
+      }
     }
   }
   if (unsup) T.code = MV_UNSUP;

@@ -278,19 +278,24 @@ struct VKVRWSet {
     return pbw::decode(s.p, s.n, m);
   }
 };
-struct VHashRead {
+struct VHashRead {  // KVReadHash {key_hash bytes=1, version=2}
+  Span key;
+  bool has_ver = false;
+  VVersion ver;
   pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
-    if (n == 1) return true;
-    VVersion v;
-    return pbw::decode(s.p, s.n, v);
+    if (n == 1) { key = s; return true; }
+    has_ver = true;
+    return pbw::decode(s.p, s.n, ver);
   }
 };
-struct VHashWrite {
+struct VHashWrite {  // KVWriteHash {key_hash=1, is_delete=2, value_hash=3, is_purge=4}
+  Span key, value_hash;
+  bool is_delete = false;
   pbw::Kind kind(uint32_t n) { return (n == 1 || n == 3) ? pbw::K_BYTES : (n == 2 || n == 4) ? pbw::K_VARINT : pbw::K_NONE; }
-  void on_varint(uint32_t, uint64_t) {}
-  bool on_len(uint32_t, Span) { return true; }
+  void on_varint(uint32_t n, uint64_t v) { if (n == 2) is_delete = v != 0; }
+  bool on_len(uint32_t n, Span s) { (n == 1 ? key : value_hash) = s; return true; }
 };
 struct VHashMeta {
   pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
@@ -303,11 +308,25 @@ struct VHashMeta {
 };
 struct VHashedRWSet {
   uint32_t nreads = 0, nwrites = 0, nmeta = 0;
+  std::vector<VHashRead> *reads = nullptr;  // optional capture (MVCC)
+  std::vector<VHashWrite> *writes = nullptr;
   pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_REP_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
-    if (n == 1) { nreads++; VHashRead r; return pbw::decode(s.p, s.n, r); }
-    if (n == 2) { nwrites++; VHashWrite w; return pbw::decode(s.p, s.n, w); }
+    if (n == 1) {
+      nreads++;
+      VHashRead r;
+      if (!pbw::decode(s.p, s.n, r)) return false;
+      if (reads) reads->push_back(r);
+      return true;
+    }
+    if (n == 2) {
+      nwrites++;
+      VHashWrite w;
+      if (!pbw::decode(s.p, s.n, w)) return false;
+      if (writes) writes->push_back(w);
+      return true;
+    }
     nmeta++;
     VHashMeta m;
     return pbw::decode(s.p, s.n, m);

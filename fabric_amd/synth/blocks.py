@@ -93,9 +93,26 @@ def kv_rwset(reads, writes) -> bytes:
     return out
 
 
+def hashed_rwset(reads, writes) -> bytes:
+    """HashedRWSet{hashed_reads: KVReadHash{key_hash, version}, hashed_writes: KVWriteHash{key_hash,
+    is_delete, value_hash}}: reads [(key_hash, ver|None)], writes [(key_hash, value_hash, is_delete)]"""
+    out = b""
+    for k, ver in reads:
+        v = b"" if ver is None else f_msg(2, f_varint(1, ver[0]) + f_varint(2, ver[1]))
+        out += f_msg(1, f_bytes(1, k) + v)
+    for k, vh, is_del in writes:
+        out += f_msg(2, f_bytes(1, k) + f_varint(2, 1 if is_del else 0) + f_bytes(3, vh))
+    return out
+
+
 def tx_rwset(ns_sets) -> bytes:
-    """TxReadWriteSet{data_model KV, ns_rwset: [(ns, kvrwset_bytes)]}"""
-    return b"".join(f_msg(2, f_str(1, ns) + f_bytes(2, rw)) for ns, rw in ns_sets)
+    """TxReadWriteSet{data_model KV, ns_rwset: [(ns, kvrwset_bytes[, [(collection, hashed_rwset_bytes)]])]}"""
+    out = b""
+    for ns_set in ns_sets:
+        ns, rw = ns_set[0], ns_set[1]
+        colls = b"".join(f_msg(3, f_str(1, c) + f_bytes(2, h)) for c, h in (ns_set[2] if len(ns_set) > 2 else ()))
+        out += f_msg(2, f_str(1, ns) + f_bytes(2, rw) + colls)
+    return out
 
 
 def chaincode_id(name: str, version: str = "") -> bytes:

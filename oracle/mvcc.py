@@ -9,14 +9,29 @@ Follows (citations under /root/reference/core/ledger/kvledger/txmgmt):
   validation/validator.go:134-200       validateTx / validateKVRead: MVCC_READ_CONFLICT(11) if
         the key was written by an earlier VALID tx of this block (updates.Exists) or the
         committed version differs from the read version (version.AreSame; nil <=> absent)
-  validation/tx_ops.go + types.go:81-112 applyWriteSet: puts and deletes enter `updates`
-Range queries (phantom checks), hashed/private reads and metadata writes are outside the
-modelled state and raise Unsupported.
+  validation/tx_ops.go + types.go:81-112 applyWriteSet: puts and deletes enter `updates`;
+        a write is a delete when rwsetutil.IsKVWriteDelete / IsKVWriteHashDelete say so
+        (rwsetutil/rwset_proto_util.go:366-375: is_delete, empty value, or value hash ==
+        SHA-256 of the empty string)
+  validation/validator.go:246-293       validateNsHashedReadSets / validateKVReadHash: hashed
+        reads are point reads of the key hash in the hashed-data namespace; the state DB keeps
+        them under ns + "$$h" + coll (privacyenabledstate/db.go:31-33,355-357), which is the
+        (namespace, key) the oracle and the engine use for them
+Range queries (phantom checks) and metadata writes are outside the modelled state and raise
+Unsupported.
 """
+import hashlib
+
 from .protowire import DecodeError, decode
 from .v20 import Unsupported, get_action_from_envelope, parse_rwset
 
 MVCC_READ_CONFLICT, NIL_TXACTION, INVALID_OTHER_REASON = 11, 16, 255
+_EMPTY_HASH = hashlib.sha256(b"").digest()
+
+
+def hashed_ns(ns, coll):
+    """privacyenabledstate.deriveHashedDataNs (privacyenabledstate/db.go:355-357)"""
+    return ns + "$$h" + coll
 
 
 class StateDB:
@@ -44,15 +59,28 @@ def _tx_rwsets(env_bytes):
         kv = ns["kv"]
         if kv.get("range_queries_info") or kv.get("metadata_writes"):
             raise Unsupported("range queries / metadata writes")
-        if any(c["hashed"].get("hashed_reads") or c["hashed"].get("hashed_writes") or c["hashed"].get("metadata_writes")
-               for c in ns["coll"]):
-            raise Unsupported("private data")
+        if any(c["hashed"].get("metadata_writes") for c in ns["coll"]):
+            raise Unsupported("private-data metadata writes")
         reads = []
         for r in kv.get("reads", []):
             v = r.get("version")
             reads.append((r.get("key", ""), None if v is None else (v.get("block_num", 0), v.get("tx_num", 0))))
-        writes = [(w.get("key", ""), bool(w.get("is_delete", False))) for w in kv.get("writes", [])]
+        writes = [(w.get("key", ""), bool(w.get("is_delete", False)) or not w.get("value"))
+                  for w in kv.get("writes", [])]
         out.append((ns["namespace"], reads, writes))
+        for c in ns["coll"]:
+            hns, h = hashed_ns(ns["namespace"], c["name"]), c["hashed"]
+            hreads = []
+            for r in h.get("hashed_reads", []):
+                v = r.get("version")
+                hreads.append((bytes(r.get("key_hash") or b""),
+                               None if v is None else (v.get("block_num", 0), v.get("tx_num", 0))))
+            hwrites = []
+            for w in h.get("hashed_writes", []):
+                vh = bytes(w.get("value_hash") or b"")
+                hwrites.append((bytes(w.get("key_hash") or b""),
+                                bool(w.get("is_delete", False)) or not vh or vh == _EMPTY_HASH))
+            out.append((hns, hreads, hwrites))
     return out
 
 

@@ -92,3 +92,24 @@ def test_long_dependency_chain():
     assert list(got) == exp
     assert eng.mvcc_stats()["rounds"] >= 10
     eng.close()
+
+
+def test_hashed_reads_and_delete_rules():
+    """Private-data hashed reads/writes (ns + "$$h" + coll) and the empty-value / empty-hash
+    delete rules: same flags and committed state as the oracle over two blocks."""
+    from tests.test_oracle_mvcc import hashed_case
+    committed, blocks, expected = hashed_case()
+    db = OM.StateDB(committed)
+    eng = _lib.Engine(0)
+    eng.statedb_init(1 << 12, 1 << 20)
+    by_ns = {}
+    for (ns, k), (b, t) in committed.items():
+        by_ns.setdefault(ns, []).append((k, b, t))
+    for ns, items in by_ns.items():
+        eng.statedb_load(ns, [k for k, _, _ in items], [b for _, b, _ in items], [t for _, _, t in items])
+    for n, (envs, exp) in enumerate(zip(blocks, expected)):
+        blk = _blk(envs)
+        want = OM.validate_block(db, blk, [0] * len(envs), 2 + n, commit=True)
+        got = eng.mvcc_validate(blk, 2 + n, [0] * len(envs), commit=True)
+        assert list(got) == want == exp, n
+    eng.close()

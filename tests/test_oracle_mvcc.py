@@ -58,3 +58,41 @@ def test_skips_committer_invalid_and_nil_action():
     assert out == [10, 0, 3]  # the invalid tx's write is not in updates
     with pytest.raises(Unsupported):  # a committer-VALID tx without header: the reference panics
         OM.validate_block(db, _blk(envs), [10, 0, 0], 2)
+
+
+def _hk(s):
+    import hashlib
+    return hashlib.sha256(s).digest()
+
+
+def hashed_case():
+    """Private-data hashed reads/writes (validator.go:246-293 validateKVReadHash; the hashed state
+    lives under ns + "$$h" + coll) and the delete rules of rwset_proto_util.go:366-375 (empty
+    value; value hash of the empty string). Returns (committed, blocks, expected flags)."""
+    h1, h2, h3, e = _hk(b"k1"), _hk(b"k2"), _hk(b"k3"), _hk(b"")
+    hns = OM.hashed_ns("ns1", "coll1")
+    committed = {("ns1", "key1"): (1, 0), (hns, h1): (1, 0), (hns, h2): (1, 1)}
+
+    def tx(reads=(), writes=(), coll="coll1", hreads=(), hwrites=()):
+        return M._envelope(B.tx_rwset([("ns1", B.kv_rwset(list(reads), list(writes)),
+                                        [(coll, B.hashed_rwset(list(hreads), list(hwrites)))])]), 0, 1)
+    b1 = [
+        tx(hreads=[(h1, (1, 0))], hwrites=[(h2, b"\x01" * 32, False)]),            # valid
+        tx(hreads=[(h2, (1, 1))]),                                                  # h2 written by tx 0 -> 11
+        tx(hreads=[(h1, (1, 5))]),                                                  # stale hashed version -> 11
+        tx(reads=[("key1", (1, 0))], writes=[("key1", b"", False)],                 # empty value = delete
+           hreads=[(h3, None)], hwrites=[(h1, e, False)]),                          # hash of b"" = delete
+        tx(reads=[("key1", (1, 0))]),                                               # key1 updated by tx 3 -> 11
+        tx(coll="coll2", hreads=[(h1, None)]),                                      # other collection -> valid
+    ]
+    b2 = [tx(reads=[("key1", None)], hreads=[(h1, None), (h2, (2, 0))]), tx(hreads=[(h1, (1, 0))])]
+    return committed, [b1, b2], [[0, 11, 11, 0, 11, 0], [0, 11]]
+
+
+def test_hashed_reads_and_delete_rules():
+    committed, blocks, expected = hashed_case()
+    db = OM.StateDB(committed)
+    for n, (envs, exp) in enumerate(zip(blocks, expected)):
+        assert OM.validate_block(db, _blk(envs), [0] * len(envs), 2 + n, commit=True) == exp
+    assert db.get_version("ns1", "key1") is None
+    assert db.get_version(OM.hashed_ns("ns1", "coll1"), _hk(b"k2")) == (2, 0)
