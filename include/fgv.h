@@ -223,6 +223,8 @@ int fgv_finalize_flags_dev_plan(fgv_ctx *ctx, size_t nblocks, const size_t *ntx,
  * open-addressing table of (namespace, key) -> version Height{blockNum, txNum}, exact key
  * compare.  It is a cache of the state DB, loaded from it at start (fgv_statedb_load) and
  * kept current by fgv_mvcc_validate_block(..., commit=1); the DB stays authoritative.
+ * Private-data key hashes are loaded under the state DB's own hashed-data namespace
+ * ns + "$$h" + collection (privacyenabledstate/db.go:355-357), key = the key hash bytes.
  *   slots: table capacity (rounded up to a power of two, load factor kept <= 0.7)
  *   arena_bytes: capacity for key bytes */
 int fgv_statedb_init(fgv_ctx *ctx, uint64_t slots, uint64_t arena_bytes);
@@ -234,8 +236,10 @@ int fgv_statedb_load(fgv_ctx *ctx, const char *ns, const uint8_t *key_buf, const
  * updated in place -- committer-invalid txs are skipped, others become NIL_TXACTION(16),
  * INVALID_OTHER_REASON(255), MVCC_READ_CONFLICT(11) or stay VALID.  commit != 0 then applies
  * the valid write sets to the state cache at Height{block_num, txIdx}.  d_block: optional
- * device copy of the block bytes.  Range queries, private data and metadata writes return
- * FGV_EUNSUPPORTED. */
+ * device copy of the block bytes.  Hashed (private-data) reads are checked like public reads
+ * against ns + "$$h" + coll (validator.go:246-293); writes are deletes by IsKVWriteDelete /
+ * IsKVWriteHashDelete (rwset_proto_util.go:366-375).  Range queries and metadata writes
+ * (public or hashed) return FGV_EUNSUPPORTED. */
 int fgv_mvcc_validate_block(fgv_ctx *ctx, const uint8_t *block, size_t len, const uint8_t *d_block,
                             uint64_t block_num, uint8_t *flags, size_t ntx, int commit);
 /* fgv_mvcc_validate_block that also walks the NEXT block's framing (next, next_len; the
