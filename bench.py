@@ -298,11 +298,14 @@ def run_mvcc(args, world, rank, local, dev):
 
     T, K, W = args.tx_per_mvcc_block, args.steps, args.warmup
     t0 = time.time()
-    st = M.MvccState(args.state_keys, seed=4 + rank)
+    st = M.MvccState(args.state_keys, seed=4 + rank, private_every=args.mvcc_private_every)
     keys, blk, txn = st.items()
     eng = _lib.Engine(local)
     eng.statedb_init(4 * args.state_keys, 64 << 20)
     eng.statedb_load("mycc", keys, blk, txn)
+    if args.mvcc_private_every > 0:  # private-data keys: hashed namespace mycc$$hpvt
+        hk, hb, ht = st.items_hashed()
+        eng.statedb_load(M.HASHED_NS, hk, hb, ht)
     blocks = [M.make_block(st, T, number=1001 + i, seed=100 * rank + i) for i in range(W + K)]
     log(f"[bench] rank {rank}: {args.state_keys} keys + {W + K} x {T}-tx blocks ready in {time.time() - t0:.1f}s")
     sizes = [(len(b[0]) + 64 + 255) // 256 * 256 for b in blocks]
@@ -355,7 +358,9 @@ def run_mvcc(args, world, rank, local, dev):
                 warmup=W, ms_per_step=round(el / K * 1e3, 3), higher_is_better=True, scaling="weak",
                 vs_baseline=None, dtype="u64", data="synthetic",
                 config=dict(workload=f"C3: {T}-tx blocks, {args.state_keys}-key state DB, 4R/4W, 5% intra-block "
-                                     f"conflicts, 1% stale, 0.5% invalid-writer chains, commit per block",
+                                     f"conflicts, 1% stale, 0.5% invalid-writer chains, commit per block"
+                                     + (f", every {args.mvcc_private_every}th key private (hashed reads/writes)"
+                                        if args.mvcc_private_every > 0 else ""),
                             parallelism=f"replicas{world} (sequential per channel)"),
                 parity_vs_labels=ok, fixpoint_rounds=rounds,
                 stage_ms=dict(lookup=round(lookup / K, 4), gpu_total=round(per_block_ms, 4)),
@@ -458,6 +463,8 @@ def main():
     ap.add_argument("--c5-tx-per-block", type=int, default=20000)
     ap.add_argument("--tx-per-mvcc-block", type=int, default=10000)
     ap.add_argument("--state-keys", type=int, default=1_000_000)
+    ap.add_argument("--mvcc-private-every", type=int, default=0,
+                    help="C3 variant: every Nth key is private data (collection hashed rwsets)")
     ap.add_argument("--blocks-per-gpu", type=int, default=32)
     ap.add_argument("--tx-per-block", type=int, default=500)
     ap.add_argument("--per-gpu", type=int, default=131072)

@@ -8,21 +8,29 @@ replacement), then faults are injected with the generator's own label:
   conflict (5 %):   one read key is written by an earlier clean tx -> 11
   chain    (0.5 %): one read key is written by an earlier STALE tx (invalid, so its write is
                     not in `updates`)                              -> 0
+private_every=P > 0 makes every key index divisible by P a private-data key: it lives in the
+hashed-data namespace "mycc$$hpvt" under SHA-256(key) and transactions read/write it through
+the collection "pvt" hashed rwset (validator.go:246-293); the labels do not change.
 Envelope signatures are not real (MVCC never checks them): the committer flags passed in say
 which transactions are valid.  After each block the generator applies its own expectation of
 the commit (valid writes at Height{block, tx}) so consecutive blocks read current versions.
 """
+import hashlib
+
 import numpy as np
 
-from .blocks import f_bytes, f_msg, f_str, f_varint, kv_rwset, tx_rwset
+from .blocks import f_bytes, f_msg, f_str, f_varint, hashed_rwset, kv_rwset, tx_rwset
 
 NS = "mycc"
+COLL = "pvt"
+HASHED_NS = NS + "$$h" + COLL   # privacyenabledstate.deriveHashedDataNs
 
 
 class MvccState:
-    def __init__(self, nkeys=1_000_000, seed=4):
+    def __init__(self, nkeys=1_000_000, seed=4, private_every=0):
         rng = np.random.default_rng(seed)
         self.nkeys = nkeys
+        self.private_every = private_every
         self.blk = rng.integers(1, 1001, size=nkeys, dtype=np.int64)
         self.txn = rng.integers(0, 500, size=nkeys, dtype=np.int64)
         self.present = np.ones(nkeys, dtype=bool)
@@ -31,10 +39,27 @@ class MvccState:
     def key(i):
         return "k%07d" % i
 
+    def is_private(self, i):
+        return self.private_every > 0 and i % self.private_every == 0
+
+    @staticmethod
+    def key_hash(i):
+        return hashlib.sha256(MvccState.key(i).encode()).digest()
+
     def items(self):
-        """(keys list, blk, txn) of present keys -- the bulk load"""
+        """(keys list, blk, txn) of present public keys -- the bulk load of namespace NS"""
         idx = np.nonzero(self.present)[0]
+        if self.private_every > 0:
+            idx = idx[idx % self.private_every != 0]
         return [self.key(i) for i in idx], self.blk[idx], self.txn[idx]
+
+    def items_hashed(self):
+        """(key hashes, blk, txn) of present private keys -- the bulk load of HASHED_NS"""
+        if self.private_every <= 0:
+            return [], self.blk[:0], self.txn[:0]
+        idx = np.nonzero(self.present)[0]
+        idx = idx[idx % self.private_every == 0]
+        return [self.key_hash(i) for i in idx], self.blk[idx], self.txn[idx]
 
     def version(self, i):
         return (int(self.blk[i]), int(self.txn[i])) if self.present[i] else None
@@ -79,16 +104,22 @@ def make_block(state: MvccState, ntx=10_000, number=1001, seed=0, stale=0.01, co
         elif kind[i] == 1:
             stale_seen.append(i)
     envs = []
+    vhash = hashlib.sha256(b"v" * 16).digest()
     for i in range(ntx):
-        rd = []
+        rd, hrd = [], []
         for r in range(reads):
             k = int(read_keys[i, r])
             ver = state.version(k)
             if r == 1 and kind[i] == 1:
                 ver = (ver[0] + 1, ver[1]) if ver else (1, 1)
-            rd.append((state.key(k), ver))
-        wr = [(state.key(int(k)), b"v" * 16, False) for k in keys[i]]
-        envs.append(_envelope(tx_rwset([(NS, kv_rwset(rd, wr))]), i, number))
+            if state.is_private(k):
+                hrd.append((state.key_hash(k), ver))
+            else:
+                rd.append((state.key(k), ver))
+        wr = [(state.key(int(k)), b"v" * 16, False) for k in keys[i] if not state.is_private(int(k))]
+        hwr = [(state.key_hash(int(k)), vhash, False) for k in keys[i] if state.is_private(int(k))]
+        ns_set = (NS, kv_rwset(rd, wr), [(COLL, hashed_rwset(hrd, hwr))]) if hrd or hwr else (NS, kv_rwset(rd, wr))
+        envs.append(_envelope(tx_rwset([ns_set]), i, number))
     header = f_varint(1, number) + f_bytes(2, b"\x00" * 32) + f_bytes(3, b"\x00" * 32)
     block = f_msg(1, header) + f_msg(2, b"".join(f_msg(1, e) for e in envs)) + \
         f_msg(3, b"".join(f_msg(1, b"") for _ in range(5)))

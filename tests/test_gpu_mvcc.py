@@ -113,3 +113,21 @@ def test_hashed_reads_and_delete_rules():
         got = eng.mvcc_validate(blk, 2 + n, [0] * len(envs), commit=True)
         assert list(got) == want == exp, n
     eng.close()
+
+
+def test_private_data_blocks_match_oracle_and_labels():
+    """C3 shape with every 8th key private-data (hashed namespace mycc$$hpvt): flags and the
+    committed state over consecutive blocks match the oracle and the generator's labels."""
+    from tests.test_oracle_mvcc import _db_with_private
+    st = M.MvccState(60_000, seed=6, private_every=8)
+    db = _db_with_private(st)
+    eng = _engine(st)
+    hk, hb, ht = st.items_hashed()
+    eng.statedb_load(M.HASHED_NS, hk, hb, ht)
+    for b in range(3):
+        blk, labels, flags = M.make_block(st, 3000, number=1001 + b, seed=40 + b)
+        assert blk.count(b"pvt") > 500  # private reads/writes are really in the block
+        exp = OM.validate_block(db, blk, flags, 1001 + b, commit=True)
+        got = eng.mvcc_validate(blk, 1001 + b, flags, commit=True)
+        assert list(got) == list(exp) == list(labels), b
+    eng.close()

@@ -96,3 +96,21 @@ def test_hashed_reads_and_delete_rules():
         assert OM.validate_block(db, _blk(envs), [0] * len(envs), 2 + n, commit=True) == exp
     assert db.get_version("ns1", "key1") is None
     assert db.get_version(OM.hashed_ns("ns1", "coll1"), _hk(b"k2")) == (2, 0)
+
+
+def _db_with_private(st):
+    db = _db(st)
+    hk, hb, ht = st.items_hashed()
+    db.v.update({(M.HASHED_NS, k): (int(b), int(x)) for k, b, x in zip(hk, hb, ht)})
+    return db
+
+
+def test_labels_with_private_data():
+    """C3 shape with every 8th key private (hashed reads/writes in collection "pvt")."""
+    st = M.MvccState(20_000, seed=6, private_every=8)
+    db = _db_with_private(st)
+    for b in range(2):
+        blk, labels, flags = M.make_block(st, 800, number=1001 + b, seed=30 + b)
+        out = OM.validate_block(db, blk, flags, 1001 + b, commit=True)
+        assert list(out) == list(labels)
+        assert 11 in out
