@@ -131,3 +131,14 @@ def test_private_data_blocks_match_oracle_and_labels():
         got = eng.mvcc_validate(blk, 1001 + b, flags, commit=True)
         assert list(got) == list(exp) == list(labels), b
     eng.close()
+
+
+def test_hashed_metadata_write_unsupported():
+    from tests.test_oracle_mvcc import hashed_metadata_block
+    eng = _lib.Engine(0)
+    eng.statedb_init(1 << 12, 1 << 20)
+    blk = hashed_metadata_block()
+    with pytest.raises(_lib.Unsupported):
+        eng.mvcc_validate(blk, 2, [0, 0], commit=False)
+    assert list(eng.mvcc_validate(blk, 2, [0, 10], commit=False)) == [0, 10]
+    eng.close()

@@ -114,3 +114,18 @@ def test_labels_with_private_data():
         out = OM.validate_block(db, blk, flags, 1001 + b, commit=True)
         assert list(out) == list(labels)
         assert 11 in out
+
+
+def hashed_metadata_block():
+    """a committer-valid tx with a hashed metadata write (KVMetadataWriteHash): outside the model"""
+    meta = B.f_msg(3, B.f_bytes(1, _hk(b"k1")) + B.f_msg(2, B.f_str(1, "VALIDATION_PARAMETER") + B.f_bytes(2, b"x")))
+    env = M._envelope(B.tx_rwset([("ns1", B.kv_rwset([], []), [("coll1", meta)])]), 0, 1)
+    return _blk([_tx([("a", None)], []), env])
+
+
+def test_hashed_metadata_write_unsupported():
+    import pytest
+    from oracle.v20 import Unsupported
+    with pytest.raises(Unsupported):
+        OM.validate_block(OM.StateDB(), hashed_metadata_block(), [0, 0], 2)
+    assert OM.validate_block(OM.StateDB(), hashed_metadata_block(), [0, 10], 2) == [0, 10]  # skipped: fine
