@@ -212,9 +212,12 @@ class BlockStep:
 class Engine:
     """One libfgv context = one GPU (one process per GPU)."""
 
-    def __init__(self, device: int = 0, key_slots: int = 4096):
+    def __init__(self, device: int = 0, key_slots: int = 4096, host_threads: int = 0):
+        """host_threads: fgv_config.host_threads (0 = the library default, 24); the
+        FGV_HOST_THREADS environment variable sets it when the argument is 0"""
         self._L = load()
-        cfg = _Config(device, key_slots, 0)
+        host_threads = host_threads or int(os.environ.get("FGV_HOST_THREADS", "0"))
+        cfg = _Config(device, key_slots, host_threads)
         h = ctypes.c_void_p()
         _check(self._L.fgv_init(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

@@ -66,7 +66,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   if (!c) return FGV_ENOMEM;
   c->device = cfg ? cfg->device : 0;
   c->key_slots = (cfg && cfg->key_slots) ? cfg->key_slots : 4096;
-  c->blk = fgv_block_state_new((cfg && cfg->host_threads) ? cfg->host_threads : 16);
+  c->blk = fgv_block_state_new((cfg && cfg->host_threads) ? cfg->host_threads : 24);  // measured: tools/sweep_threads.sh
   auto fail = [&](int e) {
     fgv_destroy(c);
     return e;

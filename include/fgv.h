@@ -44,7 +44,7 @@ typedef struct fgv_ctx fgv_ctx;
 typedef struct fgv_config {
   int device;            /* HIP device ordinal (one process per GPU)                 */
   uint32_t key_slots;    /* capacity of the device public-key table cache (0 = 4096) */
-  uint32_t host_threads; /* host worker threads for parsing / policy fold (0 = 16)    */
+  uint32_t host_threads; /* host worker threads for parsing / policy fold (0 = 24)    */
 } fgv_config;
 
 /* Replaces factory.GetDefault() / sw.NewDefaultSecurityLevel* for the verify + hash
