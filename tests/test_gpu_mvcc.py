@@ -142,3 +142,14 @@ def test_hashed_metadata_write_unsupported():
         eng.mvcc_validate(blk, 2, [0, 0], commit=False)
     assert list(eng.mvcc_validate(blk, 2, [0, 10], commit=False)) == [0, 10]
     eng.close()
+
+
+def test_reference_bulkload_known_answers():
+    from tests.test_oracle_mvcc import bulkload_case
+    committed, blk, exp = bulkload_case()
+    eng = _lib.Engine(0)
+    eng.statedb_init(1 << 12, 1 << 20)
+    for (ns, k), (b, t) in committed.items():
+        eng.statedb_load(ns, [k], [b], [t])
+    assert list(eng.mvcc_validate(blk, 2, [0, 0, 0], commit=False)) == exp
+    eng.close()

@@ -129,3 +129,25 @@ def test_hashed_metadata_write_unsupported():
     with pytest.raises(Unsupported):
         OM.validate_block(OM.StateDB(), hashed_metadata_block(), [0, 0], 2)
     assert OM.validate_block(OM.StateDB(), hashed_metadata_block(), [0, 10], 2) == [0, 10]  # skipped: fine
+
+
+def bulkload_case():
+    """TestValidatorBulkLoadingOfCache's data (validation/validator_test.go:66-196): two public and
+    two hashed committed keys; tx 0 reads all four at their versions, tx 1 reads an absent public
+    and an absent hashed key as nil -> both VALID.  tx 2 (ours) reads hashedKV1 at a wrong height."""
+    h1, h2 = _hk(b"hashedPvtKey1"), _hk(b"hashedPvtKey2")
+    committed = {("ns1", "key1"): (1, 0), ("ns1", "key2"): (1, 1),
+                 (OM.hashed_ns("ns2", "col1"), h1): (1, 2), (OM.hashed_ns("ns2", "col2"), h2): (1, 3)}
+    tx0 = M._envelope(B.tx_rwset([
+        ("ns1", B.kv_rwset([("key1", (1, 0)), ("key2", (1, 1))], [])),
+        ("ns2", B.kv_rwset([], []), [("col1", B.hashed_rwset([(h1, (1, 2))], [])),
+                                     ("col2", B.hashed_rwset([(h2, (1, 3))], []))])]), 0, 1)
+    tx1 = M._envelope(B.tx_rwset([("ns3", B.kv_rwset([("key1", None)], []),
+                                   [("col1", B.hashed_rwset([(h1, None)], []))])]), 1, 1)
+    tx2 = M._envelope(B.tx_rwset([("ns2", B.kv_rwset([], []), [("col1", B.hashed_rwset([(h1, (1, 3))], []))])]), 2, 1)
+    return committed, _blk([tx0, tx1, tx2]), [0, 0, 11]
+
+
+def test_reference_bulkload_known_answers():
+    committed, blk, exp = bulkload_case()
+    assert OM.validate_block(OM.StateDB(committed), blk, [0, 0, 0], 2) == exp
