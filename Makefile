@@ -8,7 +8,7 @@ CSRC := fabric_amd/csrc
 OBJDIR := build
 KOBJS := $(OBJDIR)/sha256.o $(OBJDIR)/p256_kernels.o $(OBJDIR)/der_kernel.o $(OBJDIR)/fgv_host.o $(OBJDIR)/fgv_block.o $(OBJDIR)/mvcc.o $(OBJDIR)/fgv_mvcc.o \
 	$(OBJDIR)/finalize.o $(OBJDIR)/fgv_integrity.o $(OBJDIR)/blockdev.o
-HDRS := $(CSRC)/p256_field.h $(CSRC)/fgv_kernels.h $(CSRC)/fgv_der.h $(CSRC)/fgv_internal.h include/fgv.h $(CSRC)/blockdev.h
+HDRS := $(CSRC)/p256_field.h $(CSRC)/fgv_kernels.h $(CSRC)/fgv_der.h $(CSRC)/fgv_internal.h include/fgv.h $(CSRC)/blockdev.h $(CSRC)/pbwire_dev.h
 
 all: fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so
 

@@ -24,7 +24,7 @@ EXPORTED = [
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
     "fgv_presplit", "fgv_last_presplit", "fgv_validate_shard_dev_next", "fgv_mvcc_validate_block_next",
-    "fgv_statedb_init", "fgv_statedb_load", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
+    "fgv_statedb_init", "fgv_statedb_load", "fgv_statedb_apply", "fgv_statedb_stats", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode",
 ]
 TX_RESULT_BYTES = 68
@@ -111,6 +111,8 @@ def load():
         L.fgv_finalize_flags_dev_plan.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
+        L.fgv_statedb_apply.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, vp, sz]
+        L.fgv_statedb_stats.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 4
         L.fgv_mvcc_validate_block.argtypes = [vp, vp, sz, vp, ctypes.c_uint64, vp, sz, ctypes.c_int]
         L.fgv_mvcc_validate_block_next.argtypes = [vp, vp, sz, vp, ctypes.c_uint64, vp, sz, ctypes.c_int, vp, sz]
         L.fgv_mvcc_last_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -426,6 +428,21 @@ class Engine:
         txn = np.ascontiguousarray(txn, dtype=np.uint64)
         _check(self._L.fgv_statedb_load(self._h, ns.encode(), _ptr(arena), _ptr(offs), _ptr(lens), _ptr(blk),
                                         _ptr(txn), len(keys)))
+
+    def statedb_apply(self, ns, keys, blk, txn, is_delete):
+        """fgv_statedb_apply: a block's update batch for namespace `ns` committed outside the
+        engine (puts at their version, deletes)."""
+        arena, offs, lens = pack([k.encode() if isinstance(k, str) else k for k in keys])
+        blk = np.ascontiguousarray(blk, dtype=np.uint64)
+        txn = np.ascontiguousarray(txn, dtype=np.uint64)
+        dl = np.ascontiguousarray(is_delete, dtype=np.uint8)
+        _check(self._L.fgv_statedb_apply(self._h, ns.encode(), _ptr(arena), _ptr(offs), _ptr(lens), _ptr(blk),
+                                         _ptr(txn), _ptr(dl), len(keys)))
+
+    def statedb_stats(self):
+        v = [ctypes.c_uint64() for _ in range(4)]
+        _check(self._L.fgv_statedb_stats(self._h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("keys", "arena_used", "slots", "arena_cap"), (x.value for x in v)))
 
     def mvcc_validate(self, block: bytes, block_num: int, flags, commit=True, d_block=None, next_block=None):
         """flags: committer TxValidationFlags (updated copy returned).  next_block: bytes of the

@@ -68,53 +68,72 @@ __global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_
                       uint8_t *status, uint32_t *r_limbs, uint32_t *s_limbs);
 
 // ---- MVCC (mvcc.hip)
-struct MvKey {  // one read or write of a transaction; key bytes live in the block (device)
-  uint64_t ptr;
-  uint32_t len;
-  uint32_t ns;     // namespace id (< 32768)
-  uint32_t tx;     // transaction index in the block
-  uint32_t flags;  // reads: bit0 = has version; writes: bit0 = is_delete
-  uint64_t blk, txn;
+#define MV_NIL 16       // NIL_TXACTION
+#define MV_OTHER 255    // INVALID_OTHER_REASON
+#define MV_UNSUP 0xFD   // outside the engine's model
+#define MV_SKIP 0xFF    // committer-invalid: not validated
+#define MVR_HASVER 1u   // read: has a version
+#define MVR_DELETE 1u   // write: is a delete
+#define MVR_HASHED 2u   // private-data key: namespace = ns + "$$h" + coll
+#define MV_TAG_OCC 1ull      // tag bit 0: slot occupied (tags are never 0)
+#define MV_TAG_PRESENT 2ull  // committed-state tag bit 1: the key exists (clear = deleted)
+struct MvRec {  // one read or write: spans into the block (or a host-supplied key arena)
+  uint64_t tag;
+  uint64_t blk, txn;  // reads: version (load/apply records: the version to store)
+  uint32_t tx;
+  uint32_t key_off, ns_off, coll_off;
+  uint16_t key_len, ns_len, coll_len, flags;
 };
-struct StateSlot {  // committed state: open addressing, key bytes in the arena
-  uint64_t tag;     // 0 = empty
+struct MvTxInfo {  // per transaction
+  uint32_t rbeg, rcnt, wbeg, wcnt;  // record ranges
+  uint32_t rws_off, rws_len;        // TxReadWriteSet span in the block
+  uint8_t code, pad[7];             // 0 participates; MV_NIL / MV_OTHER / MV_UNSUP / MV_SKIP
+};
+struct MvCounters {  // device-side counters of one block (zeroed by the head copy)
+  unsigned long long wbytes;  // arena bytes the block's writes could need
+  uint32_t nr, nw;            // records
+  uint32_t unsup, done, rounds, nomem;
+  uint32_t undec[4];          // undecided txs after round r (slot r & 3)
+  uint32_t pad[2];
+};
+struct StateSlot {  // committed state: open addressing; arena holds flattened ns || key
+  uint64_t tag;     // 0 = empty; bit 1 = present
   uint64_t blk, txn;
-  uint32_t key_off;
-  uint16_t key_len;
-  uint16_t nsf;     // ns id | 0x8000 when the key is present (not deleted)
+  uint32_t off8;    // arena offset / 8 (arena up to 32 GiB)
+  uint16_t ns_len, key_len;
 };
 struct BlkSlot {    // keys written in the block
-  uint32_t owner;   // write index + 1 (0 = empty)
-  uint32_t pad;
-  // fixpoint round r's first writers, (r << 32) | (0xFFFFFFFF - tx) by atomicMax: a value left
-  // by an earlier round reads as "none", so no per-round reset pass is needed
-  uint64_t fw_cand, fw_valid;
-  uint64_t last;    // (tx << 32) | (write index + 1) of the last VALID writer
+  uint64_t owner;   // (block epoch << 32) | (write index + 1); an older epoch = free
+  // fixpoint first writers, double buffered by round parity: (global round << 32) |
+  // (0xFFFFFFFF - tx) by atomicMax, so a value left by an earlier round reads as "none"
+  uint64_t fw_cand[2], fw_valid[2];
+  uint64_t last;    // (epoch << 32) | (tx + 1) of the last VALID writer
 };
-__global__ void k_mv_tags(const MvKey *keys, uint32_t n, uint64_t *tags);
-__global__ void k_mv_tags2(const MvKey *reads, uint32_t nr, uint64_t *rtags, const MvKey *writes, uint32_t nw,
-                           uint64_t *wtags);
-__global__ void k_mv_find_init(const MvKey *reads, const uint64_t *rtags, uint32_t n, const BlkSlot *tbl, uint32_t mask,
-                               const MvKey *writes, const uint64_t *wtags, uint32_t *rslot, uint32_t ntx,
-                               const uint8_t *part, const uint8_t *bad_tx, uint8_t *st);
-__global__ void k_mv_lookup(const MvKey *reads, const uint64_t *tags, uint32_t n, const StateSlot *tbl, uint64_t mask,
-                            const uint8_t *arena, uint8_t *bad_tx);
-__global__ void k_mv_blk_insert(const MvKey *writes, const uint64_t *tags, uint32_t n, BlkSlot *tbl, uint32_t mask,
-                                uint32_t *wslot);
-__global__ void k_mv_min(const MvKey *writes, const uint32_t *wslot, uint32_t n, const uint8_t *st, BlkSlot *tbl,
-                         uint32_t round, uint32_t *undecided);
-__global__ void k_mv_decide(uint32_t ntx, const uint32_t *rbeg, const uint32_t *rslot, const BlkSlot *tbl, uint8_t *st,
-                            uint32_t round, uint32_t *undecided);
-__global__ void k_mv_lastwriter(const MvKey *writes, const uint32_t *wslot, uint32_t n, const uint8_t *st, BlkSlot *tbl);
-__global__ void k_mv_apply_find(const BlkSlot *btbl, uint32_t bcap, const MvKey *writes, const uint64_t *wtags,
-                                StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint64_t block_num, uint32_t *pend,
-                                uint32_t *npend);
-__global__ void k_mv_apply_insert(const BlkSlot *btbl, const uint32_t *pend, uint32_t np, const MvKey *writes,
-                                  const uint64_t *wtags, StateSlot *tbl, uint64_t mask, uint8_t *arena,
-                                  unsigned long long *arena_top, uint64_t block_num);
-__global__ void k_mv_load(const MvKey *keys, const uint64_t *tags, uint32_t n, StateSlot *tbl, uint64_t mask,
-                          uint8_t *arena, unsigned long long *arena_top);
-__global__ void k_mv_flags(uint32_t ntx, const uint8_t *part, const uint8_t *st, uint8_t *out);
+__global__ void k_mvx_count(uint32_t ntx, const uint8_t *base, const uint32_t *envtab, const uint8_t *in_flags,
+                            MvTxInfo *info, MvCounters *c);
+__global__ void k_mvx_emit(uint32_t ntx, const uint8_t *base, MvTxInfo *info, MvRec *reads, MvRec *writes,
+                           MvCounters *c);
+__global__ void k_mvx_prep(const uint8_t *base, const MvRec *reads, const MvRec *writes, BlkSlot *btbl, uint32_t epoch,
+                           uint32_t *wslot, const StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint8_t *bad,
+                           const MvCounters *c);
+__global__ void k_mvx_find(uint32_t ntx, const uint8_t *base, const MvRec *reads, const MvRec *writes,
+                           const BlkSlot *btbl_r, BlkSlot *btbl, uint32_t epoch, const uint32_t *wslot, uint32_t *rslot,
+                           const MvTxInfo *info, const uint8_t *bad, uint8_t *st, uint32_t rg1, const MvCounters *c);
+__global__ void k_mvx_round(uint32_t ntx, uint32_t r, uint32_t rg, const MvTxInfo *info, const uint32_t *rslot,
+                            const uint32_t *wslot, BlkSlot *btbl, uint8_t *st, MvCounters *c);
+__global__ void k_mvx_flags(uint32_t ntx, uint32_t rlast, const uint8_t *in_flags, const MvTxInfo *info,
+                            const uint8_t *st, uint8_t *out, MvCounters *c);
+__global__ void k_mv_last(uint32_t rlast, const MvRec *writes, const uint32_t *wslot, const uint8_t *st, BlkSlot *btbl,
+                          uint32_t epoch, MvCounters *c, const unsigned long long *top, uint64_t slots_cap,
+                          uint64_t arena_cap);
+__global__ void k_mv_upsert_find(uint32_t mode, uint32_t rlast, uint32_t n_host, const uint8_t *base, const MvRec *recs,
+                                 const uint32_t *wslot, const uint8_t *st, const BlkSlot *btbl, uint32_t epoch,
+                                 StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint64_t block_num, uint8_t *pend,
+                                 const MvCounters *c);
+__global__ void k_mv_upsert_insert(uint32_t mode, uint32_t rlast, uint32_t n_host, const uint8_t *base,
+                                   const MvRec *recs, const uint8_t *pend, StateSlot *tbl, uint64_t mask, uint8_t *arena,
+                                   unsigned long long *top, uint64_t block_num, const MvCounters *c);
+__global__ void k_mv_tags(const uint8_t *base, MvRec *recs, uint32_t n);
 
 // finalize.hip -- batch txid index + markTXIdDuplicates over gathered fgv_tx_result records
 __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, uint32_t W, uint32_t rows,

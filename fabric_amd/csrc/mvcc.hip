@@ -1,279 +1,704 @@
-// mvcc.hip -- MVCC validation of a block on the GPU (gfx950), HBM-bound integer work.
+// mvcc.hip -- MVCC validation of a block on the GPU (gfx950): rwset extraction, the committed
+// version check, the intra-block read/write conflict fixpoint and the commit, all on the device.
 //
-// Reference semantics (core/ledger/kvledger/txmgmt/validation/validator.go:81-200): in block
-// order, a transaction is MVCC_READ_CONFLICT if one of its read keys was written by an
-// EARLIER VALID transaction of the block, or if the committed version differs from the read
-// version.  Validity is sequential, so the GPU decides it by a monotone fixpoint over the
-// per-key first writers:
-//   st[i] in {UNDECIDED, VALID, INVALID}; INVALID initially for committer-invalid txs and
-//   for static version conflicts.  Each round:
-//     fw_cand(k)  = min{ j : st[j] != INVALID, k in W_j }      (atomicMin)
-//     fw_valid(k) = min{ j : st[j] == VALID,   k in W_j }
-//     undecided i -> INVALID if some read key k has fw_valid(k) < i
-//                 -> VALID   if every read key k has fw_cand(k) >= i (or is never written)
-//   The lowest undecided tx is always decided, so it terminates; rounds = longest chain.
+// Reference semantics (core/ledger/kvledger/txmgmt/validation):
+//   batch_preparer.go:192-286  preprocessProtoBlock: committer-invalid txs are skipped;
+//        GetActionFromEnvelope errors -> NIL_TXACTION(16); rwset unmarshal errors ->
+//        INVALID_OTHER_REASON(255)
+//   validator.go:81-200        in block order, tx i is MVCC_READ_CONFLICT(11) if a read key was
+//        written by an EARLIER VALID tx of the block (updates.Exists) or the committed version
+//        differs from the read version (version.AreSame, nil <=> absent)
+//   validator.go:246-293       hashed (private-data) reads are point reads of the key hash in
+//        ns + "$$h" + coll (privacyenabledstate/db.go:355-357)
+//   types.go:81-112, tx_ops.go:17-51  valid write sets enter `updates` at Height{blk, tx};
+//        IsKVWriteDelete / IsKVWriteHashDelete (rwsetutil/rwset_proto_util.go:366-375)
 //
-// Keys are (namespace id, key bytes).  Tables compare FULL key bytes (exact), with a 64-bit
-// tag only as the probe start / fast reject.
+// Pipeline of one block (one H2D head copy, one D2H tail copy, no host sync in between):
+//   k_mvx_count   one lane per tx: envelope -> ... -> TxReadWriteSet walk (pbwire_dev.h rules),
+//                 codes 16 / 255 / unsupported, read/write counts, record ranges claimed by
+//                 wave-aggregated atomics
+//   k_mvx_emit    one lane per tx: the TxReadWriteSet walked again from the span k_mvx_count
+//                 kept, 48-byte records + 64-bit tags; duplicate writes of one key in one tx
+//                 (tx_ops.go:183-191 adds flags: undefined semantics) -> unsupported
+//   k_mvx_prep    writes -> block write table (claim by CAS, epoch-tagged: never cleared);
+//                 reads  -> committed-state table, static version check
+//   k_mvx_find    reads -> write-table slot; initial state per tx + round-1 first writers
+//   k_mvx_round   one launch per fixpoint round (enqueued speculatively; a converged round
+//                 exits at once): every undecided tx decides from round r's first writers,
+//                 every non-invalid tx publishes its writes for round r+1 (double buffered)
+//   k_mvx_flags   TRANSACTIONS_FILTER codes
+//   k_mv_last / k_mv_upsert_find / k_mv_upsert_insert   commit: the last valid writer of each
+//                 key updates or inserts the committed-state entry
+//
+// Fixpoint (validity is sequential; decided by a monotone fixpoint over per-key first writers):
+//   st[i] in {UNDEC, VALID, INVALID}; INVALID initially for static conflicts / parse codes.
+//   Round r: fw_cand(k)  = min{ j : st[j] != INVALID, k in W_j },
+//            fw_valid(k) = min{ j : st[j] == VALID,   k in W_j };
+//            undecided i -> INVALID if some read key k has fw_valid(k) < i,
+//                        -> VALID   if every read key k has fw_cand(k) >= i.
+//   The lowest undecided tx is always decided, so rounds <= longest alternating chain.
 #include "fgv_kernels.h"
+#include "pbwire_dev.h"
 
-#define MV_EMPTY 0ull
+using namespace pbd;
+
 #define ST_UNDEC 0
 #define ST_VALID 1
 #define ST_INVALID 2
 #define FW_INF 0xFFFFFFFFu
 
-__device__ __forceinline__ uint64_t mv_tag(const uint8_t *p, uint32_t n, uint32_t ns) {
-  uint64_t h = 0xcbf29ce484222325ull ^ ((uint64_t)ns * 0x9E3779B97F4A7C15ull);
+// ------------------------------------------------------------------ keys and tags
+// A key is (namespace, key bytes); a private-data key's namespace is ns + "$$h" + coll.  The
+// tag hashes the flattened namespace, a separator and the key (FNV-1a 64 + a finalizer); the
+// committed-state arena stores the flattened namespace followed by the key.
+__device__ __forceinline__ uint64_t th(uint64_t h, const uint8_t *p, uint32_t n) {
   for (uint32_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
+  return h;
+}
+__device__ __forceinline__ uint64_t th_fin(uint64_t h) {
   h ^= h >> 33;
   h *= 0xff51afd7ed558ccdull;
   h ^= h >> 33;
-  return h | 1ull;  // never MV_EMPTY
+  return h | MV_TAG_OCC;  // never 0 (empty)
 }
-
+__device__ __forceinline__ uint64_t rec_tag(const uint8_t *base, const MvRec &r) {
+  uint64_t h = th(0xcbf29ce484222325ull, base + r.ns_off, r.ns_len);
+  if (r.flags & MVR_HASHED) {
+    const uint8_t sep[3] = {'$', '$', 'h'};
+    h = th(h, sep, 3);
+    h = th(h, base + r.coll_off, r.coll_len);
+  }
+  h = (h ^ 0xFFu) * 0x100000001b3ull;  // (0xFF never occurs in UTF-8 namespace strings)
+  return th_fin(th(h, base + r.key_off, r.key_len));
+}
+__device__ __forceinline__ uint32_t flat_ns_len(const MvRec &r) {
+  return r.ns_len + ((r.flags & MVR_HASHED) ? 3u + r.coll_len : 0u);
+}
 __device__ __forceinline__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
     if (a[i] != b[i]) return false;
   return true;
 }
-
-__global__ __launch_bounds__(256) void k_mv_tags(const MvKey *__restrict__ keys, uint32_t n,
-                                                 uint64_t *__restrict__ tags) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const MvKey k = keys[i];
-  tags[i] = mv_tag(reinterpret_cast<const uint8_t *>(k.ptr), k.len, k.ns);
+// record == committed-state entry (flattened namespace + key at arena offset)
+__device__ __forceinline__ bool rec_eq_state(const uint8_t *base, const MvRec &r, const StateSlot &s,
+                                             const uint8_t *arena) {
+  if (s.ns_len != flat_ns_len(r) || s.key_len != r.key_len) return false;
+  const uint8_t *a = arena + ((uint64_t)s.off8 << 3);
+  if (!bytes_eq(a, base + r.ns_off, r.ns_len)) return false;
+  a += r.ns_len;
+  if (r.flags & MVR_HASHED) {
+    if (a[0] != '$' || a[1] != '$' || a[2] != 'h') return false;
+    if (!bytes_eq(a + 3, base + r.coll_off, r.coll_len)) return false;
+    a += 3 + r.coll_len;
+  }
+  return bytes_eq(a, base + r.key_off, r.key_len);
+}
+// two records of the block name the same key of the same update map: public and hashed updates
+// are separate maps in the reference (privacyenabledstate UpdateBatch), so the kind must agree
+__device__ __forceinline__ bool rec_eq(const uint8_t *base, const MvRec &a, const MvRec &b) {
+  if (a.tag != b.tag || ((a.flags ^ b.flags) & MVR_HASHED) || a.ns_len != b.ns_len || a.key_len != b.key_len)
+    return false;
+  if ((a.flags & MVR_HASHED) &&
+      (a.coll_len != b.coll_len || !bytes_eq(base + a.coll_off, base + b.coll_off, a.coll_len)))
+    return false;
+  return bytes_eq(base + a.ns_off, base + b.ns_off, a.ns_len) && bytes_eq(base + a.key_off, base + b.key_off, a.key_len);
 }
 
-// reads and writes of a block in one launch
-__global__ __launch_bounds__(256) void k_mv_tags2(const MvKey *__restrict__ reads, uint32_t nr,
-                                                  uint64_t *__restrict__ rtags, const MvKey *__restrict__ writes,
-                                                  uint32_t nw, uint64_t *__restrict__ wtags) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nr + nw) return;
-  const MvKey k = i < nr ? reads[i] : writes[i - nr];
-  (i < nr ? rtags[i] : wtags[i - nr]) = mv_tag(reinterpret_cast<const uint8_t *>(k.ptr), k.len, k.ns);
-}
-
-// ---- committed state lookups (reads): static version check
+// committed-state probe: slot index or -1
 __device__ __forceinline__ int64_t state_find(const StateSlot *tbl, uint64_t mask, const uint8_t *arena,
-                                              uint64_t tag, const uint8_t *key, uint32_t len, uint32_t ns) {
-  uint64_t idx = tag & mask;
+                                              const uint8_t *base, const MvRec &r) {
+  uint64_t idx = r.tag & mask;
   for (uint64_t probe = 0; probe <= mask; probe++, idx = (idx + 1) & mask) {
     const uint64_t t = tbl[idx].tag;
-    if (t == MV_EMPTY) return -1;
-    if (t == tag && tbl[idx].key_len == len && (tbl[idx].nsf & 0x7fff) == ns &&
-        bytes_eq(arena + tbl[idx].key_off, key, len))
-      return (int64_t)idx;
+    if (t == 0) return -1;
+    if ((t | MV_TAG_PRESENT) == (r.tag | MV_TAG_PRESENT) && rec_eq_state(base, r, tbl[idx], arena)) return (int64_t)idx;
   }
   return -1;
 }
 
-__global__ __launch_bounds__(256) void k_mv_lookup(const MvKey *__restrict__ reads, const uint64_t *__restrict__ tags,
-                                                   uint32_t n, const StateSlot *__restrict__ tbl, uint64_t mask,
-                                                   const uint8_t *__restrict__ arena, uint8_t *__restrict__ bad_tx) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const MvKey r = reads[i];
-  const int64_t s = state_find(tbl, mask, arena, tags[i], reinterpret_cast<const uint8_t *>(r.ptr), r.len, r.ns);
-  const bool committed = s >= 0 && (tbl[s].nsf & 0x8000);
-  const bool has_ver = (r.flags & 1) != 0;
-  bool same;
-  if (!committed || !has_ver) same = committed == has_ver;  // version.AreSame with nil
-  else same = tbl[s].blk == r.blk && tbl[s].txn == r.txn;
-  if (!same) bad_tx[r.tx] = 1;
+// ------------------------------------------------------------------ device rwset walk
+namespace {
+
+// record sink: pass 1 counts, pass 2 writes records at the tx's claimed ranges
+struct Sink {
+  const uint8_t *base;
+  MvRec *rout, *wout;  // null in the counting pass
+  uint32_t tx, nr, nw;
+  uint64_t wbytes;     // arena bytes the writes could need (capacity check of the commit)
+  bool big;            // a length exceeds the record fields
+  __device__ void rec(MvRec *out, uint32_t k, S ns, bool hashed, S coll, S key, uint32_t flags, uint64_t b,
+                      uint64_t t) {
+    if (ns.n > 0xFFFF || key.n > 0xFFFF || coll.n > 0xFFFF || ns.n + 3u + coll.n > 0xFFFF) { big = true; return; }
+    if (!out) return;
+    MvRec r;
+    r.ns_off = (uint32_t)(ns.p - base);
+    r.key_off = (uint32_t)(key.p - base);
+    r.coll_off = hashed ? (uint32_t)(coll.p - base) : 0u;
+    r.ns_len = (uint16_t)ns.n;
+    r.key_len = (uint16_t)key.n;
+    r.coll_len = hashed ? (uint16_t)coll.n : 0;
+    r.flags = (uint16_t)(flags | (hashed ? MVR_HASHED : 0));
+    r.tx = tx;
+    r.blk = b;
+    r.txn = t;
+    r.tag = rec_tag(base, r);
+    out[k] = r;
+  }
+  __device__ void read(S ns, bool hashed, S coll, S key, bool has_ver, uint64_t b, uint64_t t) {
+    rec(rout, nr++, ns, hashed, coll, key, has_ver ? MVR_HASVER : 0u, b, t);
+  }
+  __device__ void write(S ns, bool hashed, S coll, S key, bool del) {
+    rec(wout, nw++, ns, hashed, coll, key, del ? MVR_DELETE : 0u, 0, 0);
+    wbytes += ((uint64_t)ns.n + (hashed ? 3u + coll.n : 0u) + key.n + 7u) & ~7ull;
+  }
+};
+
+struct VVer {  // Version {block_num = 1, tx_num = 2}; occurrences merge
+  uint64_t b = 0, t = 0;
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_VARINT : K_NONE; }
+  DEV void on_varint(uint32_t n, uint64_t v) { (n == 1 ? b : t) = v; }
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VRead {  // KVRead {key string = 1, version = 2} / KVReadHash {key_hash bytes = 1, version = 2}
+  bool hashed;
+  S key{nullptr, 0};
+  bool has_ver = false;
+  VVer v;
+  DEV Kind kind(uint32_t n) { return n == 1 ? (hashed ? K_BYTES : K_STRING) : n == 2 ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { key = s; return true; }
+    has_ver = true;
+    return decode(s, v, ovf);
+  }
+};
+struct VWrite {  // KVWrite {key string 1, is_delete 2, value 3} / KVWriteHash {key_hash 1, is_delete 2, value_hash 3, is_purge 4}
+  bool hashed;
+  S key{nullptr, 0}, val{nullptr, 0};
+  bool del = false;
+  DEV Kind kind(uint32_t n) {
+    if (n == 1) return hashed ? K_BYTES : K_STRING;
+    if (n == 2) return K_VARINT;
+    if (n == 3) return K_BYTES;
+    return (hashed && n == 4) ? K_VARINT : K_NONE;
+  }
+  DEV void on_varint(uint32_t n, uint64_t v) { if (n == 2) del = v != 0; }
+  DEV bool on_len(uint32_t n, S s, bool &) { (n == 1 ? key : val) = s; return true; }
+};
+struct VMetaEnt {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VMetaW {  // KVMetadataWrite {key string 1, entries 2} / KVMetadataWriteHash {key_hash bytes 1, entries 2}
+  bool hashed;
+  DEV Kind kind(uint32_t n) { return n == 1 ? (hashed ? K_BYTES : K_STRING) : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) return true;
+    VMetaEnt e;
+    return decode(s, e, ovf);
+  }
+};
+struct VQReads {
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) { VRead r{false}; return decode(s, r, ovf); }
+};
+struct VMerk {
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_VARINT : n == 3 ? K_REP_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S, bool &) { return true; }
+};
+struct VRQ {  // RangeQueryInfo (validated; phantom checks are outside the model)
+  DEV Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_STRING : n == 3 ? K_VARINT : (n == 4 || n == 5) ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 4) { VQReads q; return decode(s, q, ovf); }
+    if (n == 5) { VMerk m; return decode(s, m, ovf); }
+    return true;
+  }
+};
+// KVRWSet (hashed = false) or HashedRWSet (hashed = true): reads / writes go to the sink
+struct VRW {
+  Sink *sk;
+  S ns, coll;
+  bool hashed;
+  bool unsup = false;
+  DEV Kind kind(uint32_t n) { return (n >= 1 && n <= (hashed ? 3u : 4u)) ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) {
+      VRead r{hashed};
+      if (!decode(s, r, ovf)) return false;
+      sk->read(ns, hashed, coll, r.key, r.has_ver, r.v.b, r.v.t);
+      return true;
+    }
+    if (!hashed && n == 2) { unsup = true; VRQ q; return decode(s, q, ovf); }  // range query
+    if (n == (hashed ? 2u : 3u)) {
+      VWrite w{hashed};
+      if (!decode(s, w, ovf)) return false;
+      bool del = w.del || w.val.n == 0;
+      if (hashed && !del && w.val.n == 32) {  // value hash == SHA-256("") (rwset_proto_util.go:370)
+        const uint8_t e[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4, 0xc8, 0x99, 0x6f, 0xb9, 0x24,
+                               0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+        del = bytes_eq(w.val.p, e, 32);
+      }
+      sk->write(ns, hashed, coll, w.key, del);
+      return true;
+    }
+    unsup = true;  // metadata write (key-level endorsement / metadata): outside the model
+    VMetaW m{hashed};
+    return decode(s, m, ovf);
+  }
+};
+struct VColl {  // CollectionHashedReadWriteSet {collection_name 1, hashed_rwset 2, pvt_rwset_hash 3}
+  S name{nullptr, 0}, hashed{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : (n == 2 || n == 3) ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &) {
+    if (n == 1) name = s;
+    else if (n == 2) hashed = s;
+    return true;
+  }
+};
+// NsReadWriteSet pass 1: namespace (last occurrence wins), rwset span; collections validated
+struct VNsHdr {
+  S ns{nullptr, 0}, rwset{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : n == 3 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) ns = s;
+    else if (n == 2) rwset = s;
+    else { VColl c; return decode(s, c, ovf); }
+    return true;
+  }
+};
+// NsReadWriteSet pass 2: each collection's hashed rwset, in order
+struct VNsColls {
+  Sink *sk;
+  S ns;
+  bool fail = false, unsup = false;
+  DEV Kind kind(uint32_t n) { return n == 3 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) {
+    VColl c;
+    if (!decode(s, c, ovf)) return false;
+    VRW h{sk, ns, c.name, true};
+    if (!decode(c.hashed, h, ovf)) { fail = true; return true; }
+    unsup |= h.unsup;
+    return true;
+  }
+};
+// TxReadWriteSet {data_model 1, ns_rwset 2}; decode failures anywhere -> 255 (rwsetutil
+// TxRwSet.FromProtoBytes unmarshals every namespace and collection before any check)
+struct VTxRW {
+  Sink *sk;
+  bool fail = false, unsup = false;
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_VARINT : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) {
+    VNsHdr h;
+    if (!decode(s, h, ovf)) return false;
+    VRW kv{sk, h.ns, S{nullptr, 0}, false};
+    if (!decode(h.rwset, kv, ovf)) fail = true;
+    unsup |= kv.unsup;
+    VNsColls cs{sk, h.ns};
+    if (!decode(s, cs, ovf)) return false;
+    fail |= cs.fail;
+    unsup |= cs.unsup;
+    return true;
+  }
+};
+struct VEndLite {  // ChaincodeEndorsedAction: prp span; endorsements validated only
+  S prp{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { prp = s; return true; }
+    VTwoBytes e;
+    return decode(s, e, ovf);
+  }
+};
+struct VCapLite {
+  bool has_action = false;
+  VEndLite action;
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) return true;
+    has_action = true;
+    return decode(s, action, ovf);
+  }
+};
+
+// GetActionFromEnvelope (protoutil/txutils.go) up to ChaincodeAction.results; code or 0
+// (a decode that failed on a device capacity -- START_GROUP nesting -- is not a verdict: `ovf`
+// turns it into "unsupported")
+DEV uint8_t find_results(S d, S &results) {
+  bool ovf = false;
+  VTwoBytes env;
+  VPayload pl;
+  VChannelHeader chdr;
+  // an unparsable committer-valid envelope / nil header: the reference errors out (halt) --
+  // not ours to decide; non-endorser txs go through custom processors
+  if (!decode(d, env, ovf) || !decode(env.a, pl, ovf) || !pl.has_header || !decode(pl.hdr.a, chdr, ovf))
+    return MV_UNSUP;
+  if (chdr.type != 3) return MV_UNSUP;
+  VTransaction tx;
+  if (!decode(pl.data, tx, ovf) || tx.nact == 0) return ovf ? MV_UNSUP : MV_NIL;
+  VCapLite cap;
+  if (!decode(tx.first.b, cap, ovf) || !cap.has_action || cap.action.prp.n == 0) return ovf ? MV_UNSUP : MV_NIL;
+  VTwoBytes prp;
+  if (!decode(cap.action.prp, prp, ovf) || prp.b.n == 0) return ovf ? MV_UNSUP : MV_NIL;
+  VCcAction cca;
+  if (!decode(prp.b, cca, ovf)) return ovf ? MV_UNSUP : MV_NIL;
+  results = cca.results;
+  return 0;
 }
 
-// ---- per-block table of written keys (claim = CAS owner := write index + 1)
-__global__ __launch_bounds__(256) void k_mv_blk_insert(const MvKey *__restrict__ writes, const uint64_t *__restrict__ tags,
-                                                       uint32_t n, BlkSlot *__restrict__ tbl, uint32_t mask,
-                                                       uint32_t *__restrict__ wslot) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const MvKey w = writes[i];
-  const uint64_t tag = tags[i];
-  uint32_t idx = (uint32_t)tag & mask;
-  for (uint32_t probe = 0; probe <= mask; probe++, idx = (idx + 1) & mask) {
-    uint32_t owner = atomicCAS(&tbl[idx].owner, 0u, i + 1);
-    if (owner == 0) owner = i + 1;
-    const MvKey o = writes[owner - 1];
-    if (tags[owner - 1] == tag && o.len == w.len && o.ns == w.ns &&
-        bytes_eq(reinterpret_cast<const uint8_t *>(o.ptr), reinterpret_cast<const uint8_t *>(w.ptr), w.len)) {
-      wslot[i] = idx;
-      return;
+DEV uint8_t walk_rwset(S results, Sink &sk) {
+  bool ovf = false;
+  VTxRW rw{&sk};
+  const bool ok = decode(results, rw, ovf);
+  if (ovf) return MV_UNSUP;
+  if (!ok || rw.fail) return MV_OTHER;
+  if (rw.unsup || sk.big) return MV_UNSUP;
+  return 0;
+}
+
+// wave-aggregated claim of `cnt` consecutive slots of a counter
+DEV uint32_t wave_claim(uint32_t cnt, uint32_t *counter) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t v = cnt;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)v, d);
+    if (lane >= d) v += o;
+  }
+  uint32_t b = 0;
+  if (lane == 63u && v) b = atomicAdd(counter, v);
+  b = (uint32_t)__shfl((int)b, 63);
+  return b + v - cnt;
+}
+
+DEV uint32_t bmask_of(uint32_t nw) {
+  uint32_t cap = 1024;
+  while (cap < 2u * nw) cap <<= 1;
+  return cap - 1;
+}
+
+}  // namespace
+
+// ============================================================ rwset extraction
+__global__ __launch_bounds__(64) void k_mvx_count(uint32_t ntx, const uint8_t *__restrict__ base,
+                                                  const uint32_t *__restrict__ envtab,
+                                                  const uint8_t *__restrict__ in_flags, MvTxInfo *__restrict__ info,
+                                                  MvCounters *__restrict__ c) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t nr = 0, nw = 0;
+  uint64_t wb = 0;
+  MvTxInfo I{};
+  if (t < ntx) {
+    I.code = MV_SKIP;
+    if (in_flags[t] == 0) {
+      S results{nullptr, 0};
+      I.code = find_results(S{base + envtab[2 * t], envtab[2 * t + 1]}, results);
+      if (I.code == 0) {
+        Sink sk{base, nullptr, nullptr, t, 0, 0, 0, false};
+        I.code = walk_rwset(results, sk);
+        I.rws_off = (uint32_t)(results.p - base);
+        I.rws_len = results.n;
+        if (I.code == 0) { nr = sk.nr; nw = sk.nw; wb = sk.wbytes; }
+      }
+      if (I.code == MV_UNSUP) atomicOr(&c->unsup, 1u);
     }
   }
-  wslot[i] = FW_INF;  // table full: host sizes it at >= 2x the writes, unreachable
+  I.rbeg = wave_claim(nr, &c->nr);
+  I.wbeg = wave_claim(nw, &c->nw);
+  I.rcnt = nr;
+  I.wcnt = nw;
+  for (int off = 32; off > 0; off >>= 1) wb += __shfl_down(wb, off);
+  if ((threadIdx.x & 63u) == 0 && wb) atomicAdd(&c->wbytes, (unsigned long long)wb);
+  if (t < ntx) info[t] = I;
 }
 
-// ---- fixpoint
-__device__ __forceinline__ uint64_t fw_enc(uint32_t round, uint32_t tx) {
-  return ((uint64_t)round << 32) | (0xFFFFFFFFu - tx);
-}
-__device__ __forceinline__ uint32_t fw_dec(uint64_t v, uint32_t round) {  // FW_INF: no writer this round
-  return (uint32_t)(v >> 32) == round ? 0xFFFFFFFFu - (uint32_t)v : FW_INF;
+__global__ __launch_bounds__(64) void k_mvx_emit(uint32_t ntx, const uint8_t *__restrict__ base,
+                                                 MvTxInfo *__restrict__ info, MvRec *__restrict__ reads,
+                                                 MvRec *__restrict__ writes, MvCounters *__restrict__ c) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  MvTxInfo I = info[t];
+  if (I.code != 0) return;
+  Sink sk{base, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
+  walk_rwset(S{base + I.rws_off, I.rws_len}, sk);
+  // one key written twice by one tx: txOps adds the flags (tx_ops.go:183-191) -> semantics
+  // the engine does not model (upsert+upsert reads as a metadata-only update)
+  const MvRec *w = writes + I.wbeg;
+  bool dup = false;
+  for (uint32_t a = 0; a < I.wcnt && !dup; a++)
+    for (uint32_t b = a + 1; b < I.wcnt; b++)
+      if (rec_eq(base, w[a], w[b])) { dup = true; break; }
+  if (dup) {
+    info[t].code = MV_UNSUP;
+    atomicOr(&c->unsup, 1u);
+  }
 }
 
-// read -> written-key slot for i < n (a probe of the block's write table; exact key compare),
-// then the initial fixpoint state of
-// transaction i - n (after k_mv_lookup's static version check)
-__global__ __launch_bounds__(256) void k_mv_find_init(const MvKey *__restrict__ reads, const uint64_t *__restrict__ rtags,
-                                                      uint32_t n, const BlkSlot *__restrict__ tbl, uint32_t mask,
-                                                      const MvKey *__restrict__ writes,
-                                                      const uint64_t *__restrict__ wtags, uint32_t *__restrict__ rslot,
-                                                      uint32_t ntx, const uint8_t *__restrict__ part,
-                                                      const uint8_t *__restrict__ bad_tx, uint8_t *__restrict__ st) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) {
-    const uint32_t t = i - n;
-    if (t < ntx) st[t] = (part[t] && !bad_tx[t]) ? ST_UNDEC : ST_INVALID;
+// ============================================================ lookups
+// writes: claim a block write-table slot (epoch-tagged owner; a slot of an older block is free)
+// reads: committed-state probe, static version check (version.AreSame; nil <=> absent)
+__global__ __launch_bounds__(256) void k_mvx_prep(const uint8_t *__restrict__ base, const MvRec *__restrict__ reads,
+                                                  const MvRec *__restrict__ writes, BlkSlot *__restrict__ btbl,
+                                                  uint32_t epoch, uint32_t *__restrict__ wslot,
+                                                  const StateSlot *__restrict__ tbl, uint64_t mask,
+                                                  const uint8_t *__restrict__ arena, uint8_t *__restrict__ bad,
+                                                  const MvCounters *__restrict__ c) {
+  const uint32_t nr = c->nr, nw = c->nw, bm = bmask_of(nw);
+  if (c->unsup) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nr + nw; i += gridDim.x * blockDim.x) {
+    if (i < nw) {
+      const MvRec w = writes[i];
+      const uint64_t mine = ((uint64_t)epoch << 32) | (i + 1);
+      uint32_t idx = (uint32_t)w.tag & bm, out = FW_INF;
+      for (uint32_t probe = 0; probe <= bm && out == FW_INF; probe++, idx = (idx + 1) & bm) {
+        unsigned long long *o = reinterpret_cast<unsigned long long *>(&btbl[idx].owner);
+        unsigned long long cur = *reinterpret_cast<volatile unsigned long long *>(o);
+        // a slot owned by an older block is free: claim it (at most two tries -- a failed CAS
+        // means another write of this block claimed the slot)
+        while ((uint32_t)(cur >> 32) != epoch) {
+          const unsigned long long prev = atomicCAS(o, cur, (unsigned long long)mine);
+          if (prev == cur) { cur = mine; break; }
+          cur = prev;
+        }
+        if (cur == mine || rec_eq(base, writes[(uint32_t)cur - 1], w)) out = idx;
+      }
+      wslot[i] = out;
+    } else {
+      const MvRec r = reads[i - nw];
+      const int64_t s = state_find(tbl, mask, arena, base, r);
+      const bool committed = s >= 0 && (tbl[s].tag & MV_TAG_PRESENT);
+      const bool has_ver = (r.flags & MVR_HASVER) != 0;
+      bool same;
+      if (!committed || !has_ver) same = committed == has_ver;
+      else same = tbl[s].blk == r.blk && tbl[s].txn == r.txn;
+      if (!same) bad[r.tx] = 1;
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t fw_enc(uint32_t rg, uint32_t tx) { return ((uint64_t)rg << 32) | (0xFFFFFFFFu - tx); }
+__device__ __forceinline__ uint32_t fw_dec(uint64_t v, uint32_t rg) {
+  return (uint32_t)(v >> 32) == rg ? 0xFFFFFFFFu - (uint32_t)v : FW_INF;
+}
+__device__ __forceinline__ void publish(BlkSlot *btbl, const uint32_t *wslot, const MvTxInfo &I, uint32_t t,
+                                        uint8_t s, uint32_t rg) {
+  if (s == ST_INVALID) return;
+  const unsigned long long e = fw_enc(rg, t);
+  for (uint32_t w = I.wbeg; w < I.wbeg + I.wcnt; w++) {
+    BlkSlot &B = btbl[wslot[w]];
+    atomicMax(reinterpret_cast<unsigned long long *>(&B.fw_cand[rg & 1]), e);
+    if (s == ST_VALID) atomicMax(reinterpret_cast<unsigned long long *>(&B.fw_valid[rg & 1]), e);
+  }
+}
+
+// reads -> block write-table slot; tx -> initial state + round-1 first writers (global round rg1)
+__global__ __launch_bounds__(256) void k_mvx_find(uint32_t ntx, const uint8_t *__restrict__ base,
+                                                  const MvRec *__restrict__ reads, const MvRec *__restrict__ writes,
+                                                  const BlkSlot *__restrict__ btbl_r, BlkSlot *__restrict__ btbl,
+                                                  uint32_t epoch, const uint32_t *__restrict__ wslot,
+                                                  uint32_t *__restrict__ rslot, const MvTxInfo *__restrict__ info,
+                                                  const uint8_t *__restrict__ bad, uint8_t *__restrict__ st,
+                                                  uint32_t rg1, const MvCounters *__restrict__ c) {
+  const uint32_t nr = c->nr, bm = bmask_of(c->nw);
+  if (c->unsup) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nr + ntx; i += gridDim.x * blockDim.x) {
+    if (i < nr) {
+      const MvRec r = reads[i];
+      uint32_t idx = (uint32_t)r.tag & bm, out = FW_INF;
+      for (uint32_t probe = 0; probe <= bm; probe++, idx = (idx + 1) & bm) {
+        const uint64_t own = btbl_r[idx].owner;
+        if ((uint32_t)(own >> 32) != epoch) break;
+        const MvRec &o = writes[(uint32_t)own - 1];
+        if (o.tag == r.tag && rec_eq(base, o, r)) { out = idx; break; }
+      }
+      rslot[i] = out;
+    } else {
+      const uint32_t t = i - nr;
+      const MvTxInfo I = info[t];
+      const uint8_t s = (I.code == 0 && !bad[t]) ? ST_UNDEC : ST_INVALID;
+      st[t] = s;
+      if (I.code == 0) publish(btbl, wslot, I, t, s, rg1);
+    }
+  }
+}
+
+// fixpoint round r (1-based within the block; global round tag rg = rg0 + r)
+__global__ __launch_bounds__(64) void k_mvx_round(uint32_t ntx, uint32_t r, uint32_t rg, const MvTxInfo *__restrict__ info,
+                                                  const uint32_t *__restrict__ rslot, const uint32_t *__restrict__ wslot,
+                                                  BlkSlot *__restrict__ btbl, uint8_t *__restrict__ st,
+                                                  MvCounters *__restrict__ c) {
+  if (c->done || c->unsup) return;
+  if (r > 1 && c->undec[(r - 1) & 3] == 0) {  // round r-1 decided everything
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      c->done = 1;
+      c->rounds = r - 1;
+    }
     return;
   }
-  const MvKey r = reads[i];
-  const uint64_t tag = rtags[i];
-  uint32_t idx = (uint32_t)tag & mask;
-  uint32_t out = FW_INF;
-  for (uint32_t probe = 0; probe <= mask; probe++, idx = (idx + 1) & mask) {
-    const uint32_t owner = tbl[idx].owner;
-    if (owner == 0) break;
-    if (wtags[owner - 1] != tag) continue;
-    const MvKey o = writes[owner - 1];
-    if (o.len == r.len && o.ns == r.ns &&
-        bytes_eq(reinterpret_cast<const uint8_t *>(o.ptr), reinterpret_cast<const uint8_t *>(r.ptr), r.len)) {
-      out = idx;
-      break;
+  if (blockIdx.x == 0 && threadIdx.x == 0) c->undec[(r + 1) & 3] = 0;  // the slot round r+1 counts into
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t und = 0;
+  if (t < ntx) {
+    uint8_t s = st[t];
+    const MvTxInfo I = info[t];
+    if (s == ST_UNDEC) {
+      bool conflict = false, clear = true;
+      for (uint32_t j = I.rbeg; j < I.rbeg + I.rcnt; j++) {
+        const uint32_t k = rslot[j];
+        if (k == FW_INF) continue;  // key never written in this block
+        if (fw_dec(btbl[k].fw_valid[rg & 1], rg) < t) { conflict = true; break; }
+        if (fw_dec(btbl[k].fw_cand[rg & 1], rg) < t) clear = false;
+      }
+      s = conflict ? ST_INVALID : clear ? ST_VALID : ST_UNDEC;
+      st[t] = s;
+      und = s == ST_UNDEC;
     }
+    if (I.code == 0) publish(btbl, wslot, I, t, s, rg + 1);
   }
-  rslot[i] = out;
+  for (int off = 32; off > 0; off >>= 1) und += __shfl_down(und, off);
+  if ((threadIdx.x & 63u) == 0 && und) atomicAdd(&c->undec[r & 3], und);
 }
 
-// round r (>= 1): first non-invalid and first valid writer of every written key; also zeroes
-// the round's undecided count (k_mv_decide follows on the stream)
-__global__ __launch_bounds__(256) void k_mv_min(const MvKey *__restrict__ writes, const uint32_t *__restrict__ wslot,
-                                                uint32_t n, const uint8_t *__restrict__ st, BlkSlot *__restrict__ tbl,
-                                                uint32_t round, uint32_t *__restrict__ undecided) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) *undecided = 0u;
-  if (i >= n) return;
-  const uint32_t tx = writes[i].tx;
-  const uint8_t s = st[tx];
-  if (s == ST_INVALID) return;
-  const uint32_t k = wslot[i];
-  atomicMax(reinterpret_cast<unsigned long long *>(&tbl[k].fw_cand), (unsigned long long)fw_enc(round, tx));
-  if (s == ST_VALID) atomicMax(reinterpret_cast<unsigned long long *>(&tbl[k].fw_valid), (unsigned long long)fw_enc(round, tx));
+// the fixpoint has converged after round `rlast` (or earlier)
+__device__ __forceinline__ bool converged(const MvCounters *c, uint32_t rlast) {
+  return !c->unsup && (c->done || c->undec[rlast & 3] == 0);
 }
 
-__global__ __launch_bounds__(256) void k_mv_decide(uint32_t ntx, const uint32_t *__restrict__ rbeg,
-                                                   const uint32_t *__restrict__ rslot, const BlkSlot *__restrict__ tbl,
-                                                   uint8_t *__restrict__ st, uint32_t round,
-                                                   uint32_t *__restrict__ undecided) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ntx || st[i] != ST_UNDEC) return;
-  bool all_clear = true, conflict = false;
-  for (uint32_t r = rbeg[i]; r < rbeg[i + 1]; r++) {
-    const uint32_t k = rslot[r];
-    if (k == FW_INF) continue;  // key never written in this block
-    if (fw_dec(tbl[k].fw_valid, round) < i) {
-      conflict = true;
-      break;
+// TRANSACTIONS_FILTER after MVCC: committer-invalid txs keep their code
+__global__ __launch_bounds__(256) void k_mvx_flags(uint32_t ntx, uint32_t rlast, const uint8_t *__restrict__ in_flags,
+                                                   const MvTxInfo *__restrict__ info, const uint8_t *__restrict__ st,
+                                                   uint8_t *__restrict__ out, MvCounters *__restrict__ c) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!converged(c, rlast)) return;
+  if (t == 0 && !c->done) {
+    c->done = 1;
+    c->rounds = rlast;
+  }
+  if (t >= ntx) return;
+  const uint8_t code = info[t].code;
+  uint8_t f;
+  if (code == MV_SKIP) f = in_flags[t];
+  else if (code != 0) f = code;
+  else f = st[t] == ST_INVALID ? 11 : 0;
+  out[t] = f;
+}
+
+// ============================================================ commit
+// last VALID writer of each key (a key is written at most once per tx: duplicates are
+// unsupported), and the capacity check of the whole commit
+__global__ __launch_bounds__(256) void k_mv_last(uint32_t rlast, const MvRec *__restrict__ writes,
+                                                 const uint32_t *__restrict__ wslot, const uint8_t *__restrict__ st,
+                                                 BlkSlot *__restrict__ btbl, uint32_t epoch, MvCounters *__restrict__ c,
+                                                 const unsigned long long *__restrict__ top, uint64_t slots_cap,
+                                                 uint64_t arena_cap) {
+  if (!converged(c, rlast)) return;
+  const uint32_t nw = c->nw;
+  // load factor <= 0.7 and arena room for every write (upper bounds): else nothing is committed
+  if ((top[1] + nw) * 10 > slots_cap * 7 || top[0] + c->wbytes > arena_cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) c->nomem = 1;
+    return;
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += gridDim.x * blockDim.x) {
+    const uint32_t tx = writes[i].tx;
+    if (st[tx] == ST_VALID)
+      atomicMax(reinterpret_cast<unsigned long long *>(&btbl[wslot[i]].last), ((unsigned long long)epoch << 32) | (tx + 1));
+  }
+}
+
+// Upsert phase 1: keys already in the table are updated in place (version, present bit);
+// absent, non-deleted keys are marked for phase 2.  mode 1 = block commit (only the last
+// valid writer of each key; Height{block_num, tx}); mode 0 = host-supplied batch (every record,
+// its own version: fgv_statedb_load / fgv_statedb_apply).
+__global__ __launch_bounds__(256) void k_mv_upsert_find(uint32_t mode, uint32_t rlast, uint32_t n_host,
+                                                        const uint8_t *__restrict__ base, const MvRec *__restrict__ recs,
+                                                        const uint32_t *__restrict__ wslot, const uint8_t *__restrict__ st,
+                                                        const BlkSlot *__restrict__ btbl, uint32_t epoch,
+                                                        StateSlot *__restrict__ tbl, uint64_t mask,
+                                                        const uint8_t *__restrict__ arena, uint64_t block_num,
+                                                        uint8_t *__restrict__ pend, const MvCounters *__restrict__ c) {
+  uint32_t n = n_host;
+  if (mode == 1) {
+    if (!converged(c, rlast) || c->nomem) return;
+    n = c->nw;
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const MvRec w = recs[i];
+    uint64_t vb = w.blk, vt = w.txn;
+    pend[i] = 0;
+    if (mode == 1) {
+      if (st[w.tx] != ST_VALID || btbl[wslot[i]].last != (((uint64_t)epoch << 32) | (w.tx + 1))) continue;
+      vb = block_num;
+      vt = w.tx;
     }
-    if (fw_dec(tbl[k].fw_cand, round) < i) all_clear = false;
-  }
-  if (conflict) st[i] = ST_INVALID;
-  else if (all_clear) st[i] = ST_VALID;
-  else atomicAdd(undecided, 1u);
-}
-
-// ---- commit: last valid writer per key (txops: later writes overwrite earlier ones)
-__global__ __launch_bounds__(256) void k_mv_lastwriter(const MvKey *__restrict__ writes, const uint32_t *__restrict__ wslot,
-                                                       uint32_t n, const uint8_t *__restrict__ st,
-                                                       BlkSlot *__restrict__ tbl) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t tx = writes[i].tx;
-  if (st[tx] != ST_VALID) return;
-  atomicMax(reinterpret_cast<unsigned long long *>(&tbl[wslot[i]].last), ((unsigned long long)tx << 32) | (i + 1));
-}
-
-// apply (phase 1): update existing state entries in place, mark the rest for insertion
-__global__ __launch_bounds__(256) void k_mv_apply_find(const BlkSlot *__restrict__ btbl, uint32_t bcap,
-                                                       const MvKey *__restrict__ writes, const uint64_t *__restrict__ wtags,
-                                                       StateSlot *__restrict__ tbl, uint64_t mask,
-                                                       const uint8_t *__restrict__ arena, uint64_t block_num,
-                                                       uint32_t *__restrict__ pend, uint32_t *__restrict__ npend) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= bcap) return;
-  const uint64_t last = btbl[b].last;
-  if (last == 0) return;
-  const uint32_t wi = (uint32_t)(last & 0xffffffffu) - 1, tx = (uint32_t)(last >> 32);
-  const MvKey w = writes[wi];
-  const int64_t s = state_find(tbl, mask, arena, wtags[wi], reinterpret_cast<const uint8_t *>(w.ptr), w.len, w.ns);
-  const bool del = (w.flags & 1) != 0;
-  if (s >= 0) {
-    tbl[s].blk = block_num;
-    tbl[s].txn = tx;
-    tbl[s].nsf = (uint16_t)((tbl[s].nsf & 0x7fff) | (del ? 0 : 0x8000));
-  } else if (!del) {
-    pend[atomicAdd(npend, 1u)] = b;
-  }
-}
-
-// apply (phase 2): claim empty slots for keys known to be absent (no byte compares needed:
-// every key of this launch is distinct and absent from the table)
-__global__ __launch_bounds__(256) void k_mv_apply_insert(const BlkSlot *__restrict__ btbl, const uint32_t *__restrict__ pend,
-                                                         uint32_t np, const MvKey *__restrict__ writes,
-                                                         const uint64_t *__restrict__ wtags, StateSlot *__restrict__ tbl,
-                                                         uint64_t mask, uint8_t *__restrict__ arena,
-                                                         unsigned long long *__restrict__ arena_top,
-                                                         uint64_t block_num) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= np) return;
-  const uint64_t last = btbl[pend[j]].last;
-  const uint32_t wi = (uint32_t)(last & 0xffffffffu) - 1, tx = (uint32_t)(last >> 32);
-  const MvKey w = writes[wi];
-  const uint64_t tag = wtags[wi];
-  const uint64_t off = atomicAdd(arena_top, (unsigned long long)w.len);
-  for (uint32_t q = 0; q < w.len; q++) arena[off + q] = reinterpret_cast<const uint8_t *>(w.ptr)[q];
-  uint64_t idx = tag & mask;
-  for (uint64_t probe = 0; probe <= mask; probe++, idx = (idx + 1) & mask) {
-    if (atomicCAS(reinterpret_cast<unsigned long long *>(&tbl[idx].tag), MV_EMPTY, (unsigned long long)tag) == MV_EMPTY) {
-      tbl[idx].key_off = (uint32_t)off;
-      tbl[idx].key_len = (uint16_t)w.len;
-      tbl[idx].nsf = (uint16_t)(w.ns | 0x8000);
-      tbl[idx].blk = block_num;
-      tbl[idx].txn = tx;
-      return;
+    const bool del = (w.flags & MVR_DELETE) != 0;
+    const int64_t s = state_find(tbl, mask, arena, base, w);
+    if (s >= 0) {
+      tbl[s].blk = vb;
+      tbl[s].txn = vt;
+      tbl[s].tag = del ? (tbl[s].tag & ~MV_TAG_PRESENT) : (tbl[s].tag | MV_TAG_PRESENT);
+    } else if (!del) {
+      pend[i] = 1;
     }
   }
 }
 
-// bulk load: `keys` distinct, versions in blk/txn fields -> insert (same claim protocol)
-__global__ __launch_bounds__(256) void k_mv_load(const MvKey *__restrict__ keys, const uint64_t *__restrict__ tags,
-                                                 uint32_t n, StateSlot *__restrict__ tbl, uint64_t mask,
-                                                 uint8_t *__restrict__ arena, unsigned long long *__restrict__ arena_top) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const MvKey k = keys[i];
-  const uint64_t off = atomicAdd(arena_top, (unsigned long long)k.len);
-  for (uint32_t q = 0; q < k.len; q++) arena[off + q] = reinterpret_cast<const uint8_t *>(k.ptr)[q];
-  uint64_t idx = tags[i] & mask;
-  for (uint64_t probe = 0; probe <= mask; probe++, idx = (idx + 1) & mask) {
-    if (atomicCAS(reinterpret_cast<unsigned long long *>(&tbl[idx].tag), MV_EMPTY, (unsigned long long)tags[i]) ==
-        MV_EMPTY) {
-      tbl[idx].key_off = (uint32_t)off;
-      tbl[idx].key_len = (uint16_t)k.len;
-      tbl[idx].nsf = (uint16_t)(k.ns | 0x8000);
-      tbl[idx].blk = k.blk;
-      tbl[idx].txn = k.txn;
-      return;
+// Upsert phase 2: claim empty slots for keys known to be absent and distinct (no compares).
+// top[0] = arena bytes used, top[1] = occupied slots.
+__global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_t rlast, uint32_t n_host,
+                                                          const uint8_t *__restrict__ base, const MvRec *__restrict__ recs,
+                                                          const uint8_t *__restrict__ pend, StateSlot *__restrict__ tbl,
+                                                          uint64_t mask, uint8_t *__restrict__ arena,
+                                                          unsigned long long *__restrict__ top, uint64_t block_num,
+                                                          const MvCounters *__restrict__ c) {
+  uint32_t n = n_host;
+  if (mode == 1) {
+    if (!converged(c, rlast) || c->nomem) return;
+    n = c->nw;
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (!pend[i]) continue;
+    const MvRec w = recs[i];
+    const uint32_t fl = flat_ns_len(w);
+    const uint64_t off = atomicAdd(&top[0], (unsigned long long)((fl + w.key_len + 7u) & ~7u));
+    uint8_t *a = arena + off;
+    for (uint32_t q = 0; q < w.ns_len; q++) a[q] = base[w.ns_off + q];
+    a += w.ns_len;
+    if (w.flags & MVR_HASHED) {
+      a[0] = '$';
+      a[1] = '$';
+      a[2] = 'h';
+      for (uint32_t q = 0; q < w.coll_len; q++) a[3 + q] = base[w.coll_off + q];
+      a += 3 + w.coll_len;
+    }
+    for (uint32_t q = 0; q < w.key_len; q++) a[q] = base[w.key_off + q];
+    atomicAdd(&top[1], 1ull);
+    const unsigned long long tag = (unsigned long long)(w.tag | MV_TAG_PRESENT);
+    uint64_t idx = w.tag & mask;
+    for (uint64_t probe = 0; probe <= mask; probe++, idx = (idx + 1) & mask) {
+      if (atomicCAS(reinterpret_cast<unsigned long long *>(&tbl[idx].tag), 0ull, tag) == 0ull) {
+        tbl[idx].off8 = (uint32_t)(off >> 3);
+        tbl[idx].ns_len = (uint16_t)fl;
+        tbl[idx].key_len = w.key_len;
+        tbl[idx].blk = mode == 1 ? block_num : w.blk;
+        tbl[idx].txn = mode == 1 ? (uint64_t)w.tx : w.txn;
+        break;
+      }
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_mv_flags(uint32_t ntx, const uint8_t *__restrict__ part,
-                                                  const uint8_t *__restrict__ st, uint8_t *__restrict__ out) {
+// host-supplied key records (load / apply): tags
+__global__ __launch_bounds__(256) void k_mv_tags(const uint8_t *__restrict__ base, MvRec *__restrict__ recs, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ntx) return;
-  out[i] = (part[i] && st[i] == ST_INVALID) ? 11 : 0;
+  if (i < n) recs[i].tag = rec_tag(base, recs[i]);
 }

@@ -222,14 +222,28 @@ int fgv_finalize_flags_dev_plan(fgv_ctx *ctx, size_t nblocks, const size_t *ntx,
 /* Committed-state cache on the GPU (statedb GetVersion, stateleveldb.go:128-137): an
  * open-addressing table of (namespace, key) -> version Height{blockNum, txNum}, exact key
  * compare.  It is a cache of the state DB, loaded from it at start (fgv_statedb_load) and
- * kept current by fgv_mvcc_validate_block(..., commit=1); the DB stays authoritative.
- * Private-data key hashes are loaded under the state DB's own hashed-data namespace
- * ns + "$$h" + collection (privacyenabledstate/db.go:355-357), key = the key hash bytes.
+ * kept current by fgv_mvcc_validate_block(..., commit=1) -- or, for a block the caller
+ * committed through the reference path (e.g. after FGV_EUNSUPPORTED), by fgv_statedb_apply
+ * with that block's update batch (the puts and deletes lockbased_txmgr.go:168-202 commits);
+ * the DB stays authoritative.  Private-data key hashes live under the state DB's own
+ * hashed-data namespace ns + "$$h" + collection (privacyenabledstate/db.go:355-357), key = the
+ * key hash bytes.
  *   slots: table capacity (rounded up to a power of two, load factor kept <= 0.7)
- *   arena_bytes: capacity for key bytes */
+ *   arena_bytes: capacity for namespace + key bytes (8-byte aligned entries; <= 32 GiB, else
+ *                FGV_EINVAL) */
 int fgv_statedb_init(fgv_ctx *ctx, uint64_t slots, uint64_t arena_bytes);
+/* Keys of one call must be distinct (FGV_EINVAL otherwise); a key already in the table gets the
+ * new version.  Namespace and key lengths <= 65535 bytes (else FGV_EUNSUPPORTED). */
 int fgv_statedb_load(fgv_ctx *ctx, const char *ns, const uint8_t *key_buf, const uint64_t *key_off,
                      const uint32_t *key_len, const uint64_t *blk, const uint64_t *txn, size_t n);
+/* The update batch of a block committed outside the engine, one namespace per call (distinct
+ * keys): is_delete[i] != 0 removes the key, else key i gets version (blk[i], txn[i]). */
+int fgv_statedb_apply(fgv_ctx *ctx, const char *ns, const uint8_t *key_buf, const uint64_t *key_off,
+                      const uint32_t *key_len, const uint64_t *blk, const uint64_t *txn,
+                      const uint8_t *is_delete, size_t n);
+/* occupied table slots (keys ever inserted, deleted ones included), arena bytes used, capacities */
+int fgv_statedb_stats(fgv_ctx *ctx, uint64_t *keys, uint64_t *arena_used, uint64_t *slots,
+                      uint64_t *arena_cap);
 
 /* MVCC validation of one block (txmgmt/validation/batch_preparer.go:72-119 +
  * validator.go:81-200): `flags` holds the committer's TxValidationFlags (ntx bytes) and is
@@ -238,8 +252,12 @@ int fgv_statedb_load(fgv_ctx *ctx, const char *ns, const uint8_t *key_buf, const
  * the valid write sets to the state cache at Height{block_num, txIdx}.  d_block: optional
  * device copy of the block bytes.  Hashed (private-data) reads are checked like public reads
  * against ns + "$$h" + coll (validator.go:246-293); writes are deletes by IsKVWriteDelete /
- * IsKVWriteHashDelete (rwset_proto_util.go:366-375).  Range queries and metadata writes
- * (public or hashed) return FGV_EUNSUPPORTED. */
+ * IsKVWriteHashDelete (rwset_proto_util.go:366-375).  Range queries, metadata writes (public
+ * or hashed) and a key written twice by one transaction (txOps adds the operation flags,
+ * tx_ops.go:183-191) return FGV_EUNSUPPORTED; so does a committer-valid envelope the reference
+ * would halt on.  Nothing is committed then, nor on FGV_ENOMEM (table / arena full).  The
+ * rwsets are extracted, checked and committed on the device: one upload of the envelope table
+ * and the flags, one read-back of the codes. */
 int fgv_mvcc_validate_block(fgv_ctx *ctx, const uint8_t *block, size_t len, const uint8_t *d_block,
                             uint64_t block_num, uint8_t *flags, size_t ntx, int commit);
 /* fgv_mvcc_validate_block that also walks the NEXT block's framing (next, next_len; the

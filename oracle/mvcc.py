@@ -17,8 +17,8 @@ Follows (citations under /root/reference/core/ledger/kvledger/txmgmt):
         reads are point reads of the key hash in the hashed-data namespace; the state DB keeps
         them under ns + "$$h" + coll (privacyenabledstate/db.go:31-33,355-357), which is the
         (namespace, key) the oracle and the engine use for them
-Range queries (phantom checks) and metadata writes are outside the modelled state and raise
-Unsupported.
+Range queries (phantom checks), metadata writes and a key written twice by one transaction
+are outside the modelled state and raise Unsupported.
 """
 import hashlib
 
@@ -34,18 +34,23 @@ def hashed_ns(ns, coll):
     return ns + "$$h" + coll
 
 
+def _kb(key):
+    """state DB keys are bytes (public keys are UTF-8 strings, hashed keys raw hash bytes)"""
+    return key.encode() if isinstance(key, str) else bytes(key)
+
+
 class StateDB:
-    """committed versions: {(ns, key): (block_num, tx_num)}"""
+    """committed versions: {(ns, key bytes): (block_num, tx_num)}"""
 
     def __init__(self, versions=None):
-        self.v = dict(versions or {})
+        self.v = {(ns, _kb(k)): h for (ns, k), h in dict(versions or {}).items()}
 
     def get_version(self, ns, key):
-        return self.v.get((ns, key))
+        return self.v.get((ns, _kb(key)))
 
 
 def _tx_rwsets(env_bytes):
-    """-> list of (ns, reads[(key, ver|None)], writes[(key, is_delete)]) or an int code."""
+    """-> list of (ns, reads[(key, ver|None)], writes[(key, is_delete)], hashed) or an int code."""
     try:
         cca, _ = get_action_from_envelope(env_bytes)
     except (DecodeError, ValueError, KeyError, IndexError):
@@ -54,7 +59,7 @@ def _tx_rwsets(env_bytes):
         rw = parse_rwset(cca.get("results"))
     except DecodeError:
         return INVALID_OTHER_REASON
-    out = []
+    out, kinds = [], []
     for ns in rw:
         kv = ns["kv"]
         if kv.get("range_queries_info") or kv.get("metadata_writes"):
@@ -68,6 +73,7 @@ def _tx_rwsets(env_bytes):
         writes = [(w.get("key", ""), bool(w.get("is_delete", False)) or not w.get("value"))
                   for w in kv.get("writes", [])]
         out.append((ns["namespace"], reads, writes))
+        kinds.append(False)
         for c in ns["coll"]:
             hns, h = hashed_ns(ns["namespace"], c["name"]), c["hashed"]
             hreads = []
@@ -81,11 +87,23 @@ def _tx_rwsets(env_bytes):
                 hwrites.append((bytes(w.get("key_hash") or b""),
                                 bool(w.get("is_delete", False)) or not vh or vh == _EMPTY_HASH))
             out.append((hns, hreads, hwrites))
-    return out
+            kinds.append(True)
+    # a key written twice by one transaction: txOps adds the operation flags
+    # (validation/tx_ops.go:183-191), a state the engine does not model
+    seen = set()
+    for hashed, (nsname, _, writes) in zip(kinds, out):
+        for key, _ in writes:
+            if (hashed, nsname, key) in seen:
+                raise Unsupported("key written twice by one transaction")
+            seen.add((hashed, nsname, key))
+    # public and hashed updates are separate maps (privacyenabledstate.UpdateBatch); committed
+    # versions of both live under the flattened namespace (one state DB key space)
+    return [(ns, reads, writes, hashed) for hashed, (ns, reads, writes) in zip(kinds, out)]
 
 
-def validate_block(state, block_bytes, flags, block_num, commit=False):
-    """flags: committer TxValidationFlags (list of ints) -> new flags list."""
+def validate_block(state, block_bytes, flags, block_num, commit=False, updates_out=None):
+    """flags: committer TxValidationFlags (list of ints) -> new flags list.  updates_out (dict):
+    receives the block's update batch {(hashed, ns, key bytes): (height, is_delete)}."""
     blk = decode("Block", block_bytes)
     data = (blk.get("data") or {}).get("data", [])
     flags = list(flags)
@@ -108,9 +126,9 @@ def validate_block(state, block_bytes, flags, block_num, commit=False):
             flags[i] = sets
             continue
         ok = True
-        for ns, reads, _ in sets:
+        for ns, reads, _, hashed in sets:
             for key, ver in reads:
-                if (ns, key) in updates or state.get_version(ns, key) != ver:
+                if (hashed, ns, _kb(key)) in updates or state.get_version(ns, key) != ver:
                     ok = False
                     break
             if not ok:
@@ -118,13 +136,15 @@ def validate_block(state, block_bytes, flags, block_num, commit=False):
         if not ok:
             flags[i] = MVCC_READ_CONFLICT
             continue
-        for ns, _, writes in sets:
+        for ns, _, writes, hashed in sets:
             for key, is_del in writes:
-                updates[(ns, key)] = ((block_num, i), is_del)
+                updates[(hashed, ns, _kb(key))] = ((block_num, i), is_del)
+    if updates_out is not None:
+        updates_out.update(updates)
     if commit:
-        for k, (h, is_del) in updates.items():
+        for (_, ns, key), (h, is_del) in updates.items():
             if is_del:
-                state.v.pop(k, None)
+                state.v.pop((ns, _kb(key)), None)
             else:
-                state.v[k] = h
+                state.v[(ns, _kb(key))] = h
     return flags

@@ -153,3 +153,108 @@ def test_reference_bulkload_known_answers():
         eng.statedb_load(ns, [k], [b], [t])
     assert list(eng.mvcc_validate(blk, 2, [0, 0, 0], commit=False)) == exp
     eng.close()
+
+
+def test_duplicate_write_unsupported_and_kind_separation():
+    """A key written twice by one tx -> Unsupported, nothing committed; public vs hashed update
+    maps stay separate while sharing the committed key space."""
+    from tests.test_oracle_mvcc import dup_write_blocks, kind_separation_case
+    eng = _lib.Engine(0)
+    eng.statedb_init(1 << 12, 1 << 20)
+    a, b, c = dup_write_blocks()
+    for blk in (a, b):
+        with pytest.raises(_lib.Unsupported):
+            eng.mvcc_validate(blk, 2, [0], commit=True)
+    assert eng.statedb_stats()["keys"] == 0
+    assert list(eng.mvcc_validate(c, 2, [0], commit=True)) == [0]
+    assert eng.statedb_stats()["keys"] == 2  # public "k1" and hashed (ns1, c1, "k1")
+    committed, blk, exp = kind_separation_case()
+    eng2 = _lib.Engine(0)
+    eng2.statedb_init(1 << 12, 1 << 20)
+    for (ns, k), (bn, t) in committed.items():
+        eng2.statedb_load(ns, [k], [bn], [t])
+    assert list(eng2.mvcc_validate(blk, 2, [0, 0, 0], commit=False)) == exp
+    eng.close()
+    eng2.close()
+
+
+def test_fallback_block_applied_then_gpu_matches_oracle():
+    """Block 1 validated + committed by the engine, block 2 committed by the reference path (the
+    oracle stands in) and handed over with fgv_statedb_apply, block 3 by the engine again: the
+    flags of block 3 equal the oracle's, i.e. the GPU cache did not go stale."""
+    st = M.MvccState(30_000, seed=11)
+    db = _db(st)
+    eng = _engine(st, slots=1 << 17)
+    b1, l1, f1 = M.make_block(st, 1500, number=1001, seed=1)
+    assert list(eng.mvcc_validate(b1, 1001, f1, commit=True)) == list(OM.validate_block(db, b1, f1, 1001, commit=True))
+    b2, l2, f2 = M.make_block(st, 1500, number=1002, seed=2)
+    upd = {}
+    OM.validate_block(db, b2, f2, 1002, commit=True, updates_out=upd)
+    by_ns = {}
+    for (_, ns, key), ((bn, t), dl) in upd.items():
+        by_ns.setdefault(ns, []).append((key, bn, t, dl))
+    for ns, items in by_ns.items():
+        eng.statedb_apply(ns, [k for k, *_ in items], [x[1] for x in items], [x[2] for x in items],
+                          [1 if x[3] else 0 for x in items])
+    b3, l3, f3 = M.make_block(st, 1500, number=1003, seed=3)
+    exp = OM.validate_block(db, b3, f3, 1003, commit=True)
+    got = eng.mvcc_validate(b3, 1003, f3, commit=True)
+    assert list(got) == list(exp) == list(l3)
+    # the same block 3 without the hand-over would have read stale versions
+    eng.close()
+
+
+def test_many_blocks_commit_exact_arena_accounting():
+    """300 consecutive committed blocks over a fixed key set: overwrites reuse their entries, so
+    the arena and slot counts stay where the load left them (no ENOMEM after N blocks)."""
+    st = M.MvccState(20_000, seed=12)
+    eng = _lib.Engine(0)
+    keys, blk, txn = st.items()
+    eng.statedb_init(1 << 16, 20_000 * 16 + (64 << 10))   # the loaded keys + one block of writes
+    eng.statedb_load("mycc", keys, blk, txn)
+    s0 = eng.statedb_stats()
+    for b in range(300):
+        blkb, labels, flags = M.make_block(st, 400, number=1001 + b, seed=100 + b)
+        assert list(eng.mvcc_validate(blkb, 1001 + b, flags, commit=True)) == list(labels), b
+    s1 = eng.statedb_stats()
+    assert s1["keys"] == s0["keys"] == 20_000 and s1["arena_used"] == s0["arena_used"]
+    eng.close()
+
+
+def test_c3_full_size_matches_oracle():
+    """BASELINE configs[2] at its size: 10k-tx blocks against a 1M-key state DB, two consecutive
+    committed blocks, flags == oracle == generator labels."""
+    st = M.MvccState(1_000_000, seed=4)
+    db = _db(st)
+    eng = _lib.Engine(0)
+    keys, blk, txn = st.items()
+    eng.statedb_init(1 << 22, 64 << 20)
+    eng.statedb_load("mycc", keys, blk, txn)
+    for b in range(2):
+        blkb, labels, flags = M.make_block(st, 10_000, number=1001 + b, seed=500 + b)
+        exp = OM.validate_block(db, blkb, flags, 1001 + b, commit=True)
+        got = eng.mvcc_validate(blkb, 1001 + b, flags, commit=True)
+        assert list(got) == list(exp) == list(labels), b
+        assert 11 in list(got)
+    eng.close()
+
+
+def test_load_semantics():
+    """re-loading a key updates it in place; duplicate keys in one call -> EINVAL; an arena
+    beyond 32 GiB -> EINVAL; apply deletes a key (a later nil read is valid)"""
+    eng = _lib.Engine(0)
+    with pytest.raises(_lib.FgvError):
+        eng.statedb_init(1 << 12, 33 << 30)
+    eng.statedb_init(1 << 12, 1 << 20)
+    eng.statedb_load("ns1", ["a", "b"], [1, 1], [0, 1])
+    eng.statedb_load("ns1", ["a"], [5], [7])
+    with pytest.raises(_lib.FgvError):
+        eng.statedb_load("ns1", ["c", "c"], [1, 1], [0, 0])
+    assert eng.statedb_stats()["keys"] == 2
+    from tests.test_oracle_mvcc import _tx, _blk
+    envs = [_tx([("a", (5, 7)), ("b", (1, 1))], []), _tx([("a", (1, 0))], [])]
+    assert list(eng.mvcc_validate(_blk(envs), 9, [0, 0], commit=False)) == [0, 11]
+    eng.statedb_apply("ns1", ["b"], [0], [0], [1])
+    envs = [_tx([("b", None)], []), _tx([("b", (1, 1))], [])]
+    assert list(eng.mvcc_validate(_blk(envs), 9, [0, 0], commit=False)) == [0, 11]
+    eng.close()

@@ -151,3 +151,42 @@ def bulkload_case():
 def test_reference_bulkload_known_answers():
     committed, blk, exp = bulkload_case()
     assert OM.validate_block(OM.StateDB(committed), blk, [0, 0, 0], 2) == exp
+
+
+def dup_write_blocks():
+    """A key written twice by one tx (public, then hashed) -> Unsupported; the same key bytes
+    written once publicly and once in a collection of the same namespace are different keys."""
+    h1 = _hk(b"k1")
+    pub_dup = _tx([], [("a", b"x", False), ("a", b"y", False)])
+    hashed_dup = M._envelope(B.tx_rwset([("ns1", B.kv_rwset([], []),
+                                          [("c1", B.hashed_rwset([], [(h1, b"\x01" * 32, False), (h1, b"\x02" * 32, False)]))])]), 0, 1)
+    no_dup = M._envelope(B.tx_rwset([("ns1", B.kv_rwset([], [("k1", b"x", False)]),
+                                      [("c1", B.hashed_rwset([], [(b"k1", b"\x01" * 32, False)]))])]), 0, 1)
+    return _blk([pub_dup]), _blk([hashed_dup]), _blk([no_dup])
+
+
+def test_duplicate_write_unsupported():
+    import pytest
+    from oracle.v20 import Unsupported
+    a, b, c = dup_write_blocks()
+    for blk in (a, b):
+        with pytest.raises(Unsupported):
+            OM.validate_block(OM.StateDB(), blk, [0], 2)
+    assert OM.validate_block(OM.StateDB(), c, [0], 2) == [0]
+
+
+def kind_separation_case():
+    """Public and hashed updates are separate maps (privacyenabledstate.UpdateBatch): a public
+    write to the namespace string "ns1$$hc1" does not conflict with a hashed read of (ns1, c1)
+    in the same block, while both share one committed-state key space."""
+    pub_ns = OM.hashed_ns("ns1", "c1")
+    w_pub = M._envelope(B.tx_rwset([(pub_ns, B.kv_rwset([], [("kk", b"x", False)]))]), 0, 1)
+    r_hashed = M._envelope(B.tx_rwset([("ns1", B.kv_rwset([], []), [("c1", B.hashed_rwset([(b"kk", (1, 0))], []))])]), 1, 1)
+    r_pub = M._envelope(B.tx_rwset([(pub_ns, B.kv_rwset([("kk", (1, 0))], []))]), 2, 1)
+    committed = {(pub_ns, "kk"): (1, 0)}
+    return committed, _blk([w_pub, r_hashed, r_pub]), [0, 0, 11]
+
+
+def test_kind_separation():
+    committed, blk, exp = kind_separation_case()
+    assert OM.validate_block(OM.StateDB(committed), blk, [0, 0, 0], 2) == exp
