@@ -25,7 +25,7 @@ EXPORTED = [
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
     "fgv_presplit", "fgv_last_presplit", "fgv_validate_shard_dev_next", "fgv_mvcc_validate_block_next",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_statedb_apply", "fgv_statedb_stats", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
-    "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode",
+    "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -121,6 +121,7 @@ def load():
         L.fgv_blocks_verify.argtypes = [vp, sz, vp, vp, vp, vp]
         L.fgv_set_parse_mode.argtypes = [vp, ctypes.c_int]
         L.fgv_sha256_host.argtypes = [vp, sz, vp]
+        L.fgv_commit_hash.argtypes = [vp, sz, vp, sz, ctypes.c_uint64, vp, sz, vp]
         _L = L
     return _L
 
@@ -498,3 +499,15 @@ def sha256_host(buf: bytes):
     b = np.frombuffer(buf, dtype=np.uint8) if len(buf) else np.zeros(1, np.uint8)
     ni = L.fgv_sha256_host(b.ctypes.data, len(buf), out)
     return out.raw, bool(ni)
+
+
+def commit_hash(block: bytes, flags, block_num: int, prev: bytes = b""):
+    """fgv_commit_hash: the ledger commit hash of a block (kv_ledger.go:806-817)."""
+    L = load()
+    f = np.ascontiguousarray(flags, dtype=np.uint8)
+    b = np.frombuffer(block, dtype=np.uint8)
+    out = ctypes.create_string_buffer(32)
+    pv = np.frombuffer(prev, dtype=np.uint8) if prev else None
+    _check(L.fgv_commit_hash(b.ctypes.data, len(block), _ptr(f), len(f), block_num,
+                             pv.ctypes.data if pv is not None else None, len(prev), out))
+    return out.raw

@@ -303,6 +303,18 @@ typedef struct fgv_block_check {
 } fgv_block_check;
 int fgv_blocks_verify(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                       fgv_chain_state *chain, fgv_block_check *out);
+/* ------------------------------------------------------------------- ledger commit hash (a21)
+ * kvLedger.addBlockCommitHash (core/ledger/kvledger/kv_ledger.go:806-817):
+ *   out = SHA-256(varint(ntx) || flags || updateBatchBytes || prev)
+ * flags: the block's final TRANSACTIONS_FILTER (after MVCC); updateBatchBytes =
+ * deterministicBytesForPubAndHashUpdates (txmgr/update_batch_bytes.go:29-105) of the puts and
+ * deletes of its VALID endorser transactions at Height{block_num, tx}; prev: the previous
+ * block's commit hash (prev_len 0 for block 1).  Host function (no context, no GPU).
+ * FGV_EUNSUPPORTED for metadata writes (the batch merges them with state-DB values) or a key
+ * written twice by one transaction; FGV_EINVAL if a VALID transaction does not parse. */
+int fgv_commit_hash(const uint8_t *block, size_t len, const uint8_t *flags, size_t ntx, uint64_t block_num,
+                    const uint8_t *prev, size_t prev_len, uint8_t out[32]);
+
 /* host SHA-256 of one buffer (the data-hash primitive); returns 1 when the SHA extensions
  * were used, 0 for the portable path */
 int fgv_sha256_host(const uint8_t *buf, size_t n, uint8_t out[32]);
