@@ -26,6 +26,8 @@ EXPORTED = [
     "fgv_presplit", "fgv_last_presplit", "fgv_validate_shard_dev_next", "fgv_mvcc_validate_block_next",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_statedb_apply", "fgv_statedb_stats", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash",
+    "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
+    "fgv_collection_define",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -55,6 +57,17 @@ class BlockCheck(ctypes.Structure):
 # fgv_block_check.status (include/fgv.h)
 BLK_OK, BLK_UNPARSABLE, BLK_NO_HEADER, BLK_NUMBER, BLK_PREV_HASH, BLK_METADATA, BLK_EMPTY, BLK_TX_MALFORMED, \
     BLK_DATA_HASH = range(9)
+
+
+KEY_TYPES = {"p256": 1, "p384": 2, "other": 3, "undeserializable": 4}
+ROLES_UNKNOWN = 0x80000000
+CC_COLLECTIONS_KNOWN, CC_KEY_LEVEL_EP = 1, 2
+
+
+class IdentityInfo(ctypes.Structure):
+    """fgv_identity_info (include/fgv.h)"""
+    _fields_ = [("key_type", ctypes.c_uint32), ("hash_family", ctypes.c_uint32), ("valid", ctypes.c_uint32),
+                ("roles", ctypes.c_uint32), ("pubkey", ctypes.c_uint8 * 64), ("id_digest", ctypes.c_uint8 * 32)]
 
 
 class _Config(ctypes.Structure):
@@ -99,6 +112,11 @@ def load():
         L.fgv_channel_init.argtypes = [vp, ctypes.c_char_p]
         L.fgv_msp_add_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
         L.fgv_chaincode_define.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
+        L.fgv_chaincode_define2.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_uint32]
+        L.fgv_collection_define.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz]
+        L.fgv_channel_config.argtypes = [vp, ctypes.c_char_p, sz]
+        L.fgv_msp_declare.argtypes = [vp, ctypes.c_char_p]
+        L.fgv_msp_register_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(IdentityInfo)]
         L.fgv_ledger_add_txids.argtypes = [vp, vp, vp, vp, sz]
         L.fgv_validate_blocks.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp]
         L.fgv_validate_shard.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
@@ -316,8 +334,36 @@ class Engine:
         _check(self._L.fgv_msp_add_identity(self._h, serialized, len(serialized), pubkey64, 1 if valid else 0,
                                             id_digest))
 
-    def chaincode_define(self, ns: str, policy: bytes):
-        _check(self._L.fgv_chaincode_define(self._h, ns.encode(), policy, len(policy)))
+    def chaincode_define(self, ns: str, policy: bytes, plugin: str = None, flags: int = 0):
+        """fgv_chaincode_define (plugin None) / fgv_chaincode_define2"""
+        if plugin is None and not flags:
+            _check(self._L.fgv_chaincode_define(self._h, ns.encode(), policy, len(policy)))
+        else:
+            _check(self._L.fgv_chaincode_define2(self._h, ns.encode(), (plugin or "vscc").encode(), policy, len(policy),
+                                                 flags))
+
+    def collection_define(self, ns: str, coll: str, policy: bytes = b""):
+        """fgv_collection_define: policy b"" = none (the chaincode EP applies)"""
+        _check(self._L.fgv_collection_define(self._h, ns.encode(), coll.encode(), policy or None, len(policy or b"")))
+
+    def channel_config(self, config: bytes):
+        """fgv_channel_config: the channel's common.Config bytes"""
+        _check(self._L.fgv_channel_config(self._h, config, len(config)))
+
+    def msp_declare(self, mspid: str):
+        _check(self._L.fgv_msp_declare(self._h, mspid.encode()))
+
+    def msp_register_identity(self, serialized: bytes, key: str, pub, valid: bool, id_digest: bytes, roles=None,
+                              hash_family: str = "SHA2"):
+        info = IdentityInfo()
+        info.key_type = KEY_TYPES[key]
+        info.hash_family = 1 if hash_family == "SHA3" else 0
+        info.valid = 1 if valid else 0
+        info.roles = ROLES_UNKNOWN if roles is None else int(roles)
+        if pub is not None:
+            ctypes.memmove(info.pubkey, bytes(pub)[:64], min(64, len(pub)))
+        ctypes.memmove(info.id_digest, bytes(id_digest), 32)
+        _check(self._L.fgv_msp_register_identity(self._h, serialized, len(serialized), ctypes.byref(info)))
 
     def ledger_add_txids(self, txids):
         arena, offs, lens = pack([t.encode() for t in txids])

@@ -20,7 +20,7 @@
 
 #define BD_MAX_END 16      // endorsements per transaction
 #define BD_MAX_NS 8        // namespaces per rwset
-#define BD_MAX_POL 8       // policies to evaluate (written namespaces + invoked chaincode)
+#define BD_MAX_POL 16      // policies to evaluate (chaincode / collection EPs of the written namespaces)
 #define BD_MAX_MERGE 4     // occurrences of one singular message field (protobuf merge)
 #define BD_MAX_GROUP 32    // nesting of unknown START_GROUP fields
 #define BD_MAX_PNODE 64    // policy tree nodes evaluated per policy (stack depth 16)
@@ -61,22 +61,36 @@ struct DevJobIdx {
 // identity registry in HBM (built on the host from the channel model)
 struct DevIdent {
   uint32_t msp_off, msp_len, idb_off, idb_len;  // into the identity byte arena
-  int32_t key_slot;   // -1: not a P-256 key
+  int32_t key_slot;   // P-256 key table slot (vclass 0)
   int32_t msp;        // interned Mspid
   uint32_t canon;     // dedup id (Mspid + Id)
   uint32_t valid;
+  uint32_t vclass;    // Verify: 0 on the GPU, 1 always fails, 2 outside the engine; 3 undeserializable
+  uint32_t roles;     // SatisfiesPrincipal(ROLE r) bits
+  uint32_t roles_known;
+  uint32_t pad;
 };
 
 struct DevPNode {
   int32_t type;       // 1 NOutOf, 2 SignedBy
   int32_t n;          // NOutOf threshold
   int32_t msp;        // SignedBy: interned principal Mspid (-1: undecodable principal)
+  int32_t role;       // SignedBy: MSPRole.role
   uint32_t kid0, nkids;  // NOutOf: kids[kid0 .. kid0+nkids) in the kid array
 };
+enum : uint32_t { DP_REJECT = 0, DP_SIG = 1, DP_IMPLICIT = 2, DP_UNSUP = 3 };
 struct DevPolicy {
-  uint32_t decode_ok, compile_ok, unsupported;
-  int32_t root;       // node index
+  uint32_t kind;      // DP_*
+  uint32_t decode_ok, compile_ok, needs_roles;
+  int32_t root;       // DP_SIG: node index
+  int32_t threshold;  // DP_IMPLICIT
+  uint32_t sub0, nsub;  // DP_IMPLICIT: policy indices subs[sub0 .. sub0+nsub)
 };
+// chaincode table entry: namespace bytes, compiled EP, status (0 ok, 1 INVALID_CHAINCODE, 2
+// outside the model), collections known, its collections [coll0, coll0+ncoll) in the coll table
+#define BD_CC_WORDS 7
+// collection table entry: name bytes, EP (-1: the chaincode EP); implicit table: mspid bytes, EP
+#define BD_COLL_WORDS 3
 
 struct DevChannel {  // device pointers + sizes (passed by value to the kernels)
   const uint8_t *name;
@@ -88,11 +102,17 @@ struct DevChannel {  // device pointers + sizes (passed by value to the kernels)
   const uint64_t *ident_hash;   // hash of each ident (same order as idents)
   uint32_t ident_mask;
   uint32_t ncc;
-  const uint32_t *cc;           // ncc x (ns_off, ns_len, policy)
-  const uint8_t *cc_bytes;
+  const uint32_t *cc;           // ncc x BD_CC_WORDS
+  const uint32_t *colls;        // BD_COLL_WORDS per collection
+  uint32_t nimpl;
+  const uint32_t *impl;         // nimpl x BD_COLL_WORDS (implicit org collections by mspid)
+  uint32_t nmsp;
+  const uint32_t *msps;         // nmsp x (off, len): the channel's MSP ids
+  const uint8_t *cc_bytes;      // names of all the tables above
   const DevPolicy *policies;
   const DevPNode *nodes;
   const uint32_t *kids;
+  const uint32_t *subs;
   const uint8_t *committed;     // committed ledger txids: open-addressing table of 32-byte keys
   uint32_t committed_mask;      // (all-zero key == empty; a zero txid is kept in committed_zero)
   uint32_t committed_zero;

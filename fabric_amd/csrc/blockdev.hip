@@ -161,8 +161,10 @@ struct VNsRwSet {
 };
 struct VTxRwSet {
   uint32_t nns = 0;
-  S ns[BD_MAX_NS], rwset[BD_MAX_NS];
-  uint8_t coll_writes[BD_MAX_NS];  // bit0: a collection has writes/metadata; bit1: a collection failed to decode
+  S ns[BD_MAX_NS], rwset[BD_MAX_NS], msg[BD_MAX_NS];  // msg: the NsReadWriteSet (collections re-walked)
+  // bit0: a collection has hashed writes, bit1: a collection failed to decode, bit2: a
+  // collection has metadata writes
+  uint8_t coll_writes[BD_MAX_NS];
   DEV Kind kind(uint32_t n) { return n == 1 ? K_VARINT : n == 2 ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
   DEV bool on_len(uint32_t, S s, bool &ovf) {
@@ -171,14 +173,33 @@ struct VTxRwSet {
     if (nns == BD_MAX_NS) { ovf = true; return false; }
     ns[nns] = r.ns;
     rwset[nns] = r.rwset;
+    msg[nns] = s;
     uint8_t cw = 0;
     for (uint32_t k = 0; k < r.ncoll; k++) {
       VHashedRWSet h;
       if (!decode(r.coll_hashed[k], h, ovf)) { cw |= 2; break; }
-      if (h.nwrites || h.nmeta) cw |= 1;
+      if (h.nwrites) cw |= 1;
+      if (h.nmeta) cw |= 4;
     }
     coll_writes[nns] = cw;
     nns++;
+    return true;
+  }
+};
+// the collections of one NsReadWriteSet with hashed writes, in order (their EPs)
+struct VNsCollNames {
+  S names[BD_MAX_COLL];
+  uint32_t n = 0;
+  DEV Kind kind(uint32_t f) { return f == 3 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) {
+    VCollHashed c;
+    if (!decode(s, c, ovf)) return false;
+    VHashedRWSet h;
+    if (!decode(c.hashed, h, ovf)) return false;
+    if (!h.nwrites) return true;
+    if (n == BD_MAX_COLL) { ovf = true; return false; }
+    names[n++] = c.name;
     return true;
   }
 };
@@ -192,13 +213,26 @@ struct VSerializedIdentity {
 DEV DSpan rel(const uint8_t *base, S s) { return DSpan{s.n ? (uint32_t)(s.p - base) : 0u, s.n}; }
 DEV S absl(const uint8_t *base, DSpan d) { return S{base + d.off, d.len}; }
 
-// chaincode definition lookup (lifecycle ValidationInfo): policy index or -1
-DEV int cc_lookup(const DevChannel &ch, S ns) {
+// chaincode definition lookup (lifecycle ValidationInfo): cc table entry or -1
+DEV int cc_find(const DevChannel &ch, S ns) {
   for (uint32_t i = 0; i < ch.ncc; i++) {
-    const uint32_t *e = ch.cc + 3 * i;
-    if (e[1] == ns.n && s_eq(S{ch.cc_bytes + e[0], e[1]}, ns)) return (int)e[2];
+    const uint32_t *e = ch.cc + BD_CC_WORDS * i;
+    if (e[1] == ns.n && s_eq(S{ch.cc_bytes + e[0], e[1]}, ns)) return (int)i;
   }
   return -1;
+}
+// a word table of (name off, name len, value): value of `name`, or `dflt`
+DEV int32_t name_find(const DevChannel &ch, const uint32_t *tab, uint32_t n, S name, int32_t dflt) {
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t *e = tab + BD_COLL_WORDS * i;
+    if (e[1] == name.n && s_eq(S{ch.cc_bytes + e[0], e[1]}, name)) return (int32_t)e[2];
+  }
+  return dflt;
+}
+DEV bool msp_known(const DevChannel &ch, S mspid) {
+  for (uint32_t i = 0; i < ch.nmsp; i++)
+    if (ch.msps[2 * i + 1] == mspid.n && s_eq(S{ch.cc_bytes + ch.msps[2 * i], ch.msps[2 * i + 1]}, mspid)) return true;
+  return false;
 }
 
 }  // namespace
@@ -299,15 +333,17 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
     if (!decode(prp.b, cca, ovf)) { R.disp = C_BAD_RESP; break; }
     VTxRwSet rw;
     if (!decode(cca.results, rw, ovf)) { R.disp = C_BAD_RWSET; break; }
+    // per namespace: 1 written (kv / metadata / collections), 2 metadata writes, 4 public writes
     uint8_t wflags[BD_MAX_NS];
     bool bad_rw = false;
     for (uint32_t k = 0; k < rw.nns && !bad_rw; k++) {
       VKVRWSet kv;
       if (!decode(rw.rwset[k], kv, ovf) || (rw.coll_writes[k] & 2)) { bad_rw = true; break; }
-      const bool cw = rw.coll_writes[k] & 1;
-      wflags[k] = (uint8_t)(((kv.nwrites || kv.nmeta || cw) ? 1 : 0) | ((kv.nmeta || cw) ? 2 : 0));
+      const uint8_t cw = rw.coll_writes[k];
+      wflags[k] = (uint8_t)(((kv.nwrites || kv.nmeta || (cw & 5)) ? 1 : 0) | ((kv.nmeta || (cw & 4)) ? 2 : 0) |
+                            (kv.nwrites ? 4 : 0));
     }
-    if (bad_rw) { R.disp = C_BAD_RWSET; break; }
+    if (bad_rw) { R.disp = ovf ? C_UNSUPPORTED : C_BAD_RWSET; break; }
     if (!ext.has_ccid || !cca.has_ccid) { R.disp = C_OTHER; break; }
     const S ccid = ext.ccid.name;
     if (ccid.n == 0 || !s_eq(ccid, cca.ccid.name) || cca.ccid.version.n == 0) { R.disp = C_INVALID_CC; break; }
@@ -320,7 +356,7 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
       for (uint32_t b = a + 1; b < rw.nns; b++)
         if (s_eq(rw.ns[a], rw.ns[b])) { dup = true; break; }
     if (dup) { R.disp = C_ILLEGAL_WS; break; }
-    // written namespaces + the invoked chaincode, sorted (Go string order), one policy each
+    // written namespaces + the invoked chaincode, sorted (Go string order)
     S wr[BD_MAX_POL];
     uint32_t nwr = 0;
     wr[nwr++] = ccid;
@@ -341,9 +377,48 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
         wr[j] = wr[j - 1];
         wr[j - 1] = tmp;
       }
+    // the EPs each namespace's vscc evaluates (fgv_block.cpp parse_tx restated): -1
+    // INVALID_CHAINCODE, -2 outside the model, else a policy index
+    uint32_t np = 0;
+    auto push = [&](int32_t p) {
+      for (uint32_t q = 0; q < np; q++)
+        if (R.pol[q] == p) return;
+      if (np == BD_MAX_POL) { ovf = true; return; }
+      R.pol[np++] = (int16_t)p;
+    };
+    for (uint32_t i = 0; i < nwr && !ovf; i++) {
+      const int ci = cc_find(ch, wr[i]);
+      const uint32_t *e = ci >= 0 ? ch.cc + BD_CC_WORDS * ci : nullptr;
+      if (!e || e[3] == 1) { push(-1); continue; }
+      if (e[3] != 0) { push(-2); continue; }
+      const int32_t ep = (int32_t)e[2];
+      int k = -1;
+      for (uint32_t q = 0; q < rw.nns; q++)
+        if (s_eq(rw.ns[q], wr[i])) { k = (int)q; break; }
+      bool any = false;
+      if (k >= 0 && (wflags[k] & 4)) { push(ep); any = true; }
+      if (k >= 0 && (rw.coll_writes[k] & 1)) {
+        VNsCollNames cn;
+        if (!decode(rw.msg[k], cn, ovf)) break;
+        for (uint32_t c = 0; c < cn.n; c++) {
+          any = true;
+          const S nm = cn.names[c];
+          const uint32_t pl = 14;  // "_implicit_org_" (core/chaincode/implicitcollection/name.go:24-29)
+          const uint8_t pre[14] = {'_', 'i', 'm', 'p', 'l', 'i', 'c', 'i', 't', '_', 'o', 'r', 'g', '_'};
+          if (nm.n >= pl && s_eq(S{nm.p, pl}, S{pre, pl})) {
+            push(name_find(ch, ch.impl, ch.nimpl, S{nm.p + pl, nm.n - pl}, -2));
+            continue;
+          }
+          if (!e[4]) { push(-2); continue; }
+          const int32_t cep = name_find(ch, ch.colls + BD_COLL_WORDS * e[5], e[6], nm, -3);
+          push(cep == -3 ? 0 : cep < 0 ? ep : cep);  // "no such collection" -> reject
+        }
+      }
+      if (!any) push(ep);
+    }
+    if (ovf) break;
     R.disp = C_VALID;
-    for (uint32_t i = 0; i < nwr; i++) R.pol[i] = (int16_t)cc_lookup(ch, wr[i]);
-    R.npol = (uint8_t)nwr;
+    R.npol = (uint8_t)np;
     R.nend = (uint8_t)cap.action.nend;
     for (uint32_t k = 0; k < cap.action.nend; k++) {
       R.end_ser[k] = rel(base, cap.action.ser[k]);
@@ -406,6 +481,7 @@ __global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__r
       bool ovf = false;
       if (decode(absl(base, sp), sid, ovf)) {
         const uint64_t h = ident_hash_dev(sid.mspid, sid.id_bytes);
+        bool found = false;
         for (uint32_t pos = (uint32_t)h & ch.ident_mask;; pos = (pos + 1) & ch.ident_mask) {
           const uint32_t e = ch.ident_table[pos];
           if (e == 0) break;
@@ -414,10 +490,13 @@ __global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__r
           const DevIdent &I = ch.idents[i];
           if (group_eq(sid.mspid, S{ch.ident_bytes + I.msp_off, I.msp_len}, l) &&
               group_eq(sid.id_bytes, S{ch.ident_bytes + I.idb_off, I.idb_len}, l)) {
-            res = (int32_t)i;
+            found = true;
+            res = I.vclass == 3 ? -1 : (int32_t)i;  // undeserializable key: deserialize error
             break;
           }
         }
+        // a certificate of a channel MSP that was never registered: outside the engine
+        if (!found && msp_known(ch, sid.mspid)) res = -2;
       }
     }
     if (l == 0) ident[(size_t)t * BD_OCC + k] = res;
@@ -452,9 +531,11 @@ __global__ __launch_bounds__(256) void k_bd_count(uint32_t ntx, DevTx *__restric
   if (t < ntx) jobs[t] = J;
 }
 DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx &J) {
-  if (R.pre == C_PENDING) {
+  if (R.pre == C_PENDING) {  // DeserializeIdentity -> Validate -> Verify (msgvalidation.go:26-64)
     const int32_t ci = id[0];
-    if (ci < 0 || !ch.idents[ci].valid || ch.idents[ci].key_slot < 0) R.pre = C_BAD_CREATOR;
+    if (ci == -2) R.pre = C_UNSUPPORTED;
+    else if (ci < 0 || !ch.idents[ci].valid || ch.idents[ci].vclass == 1) R.pre = C_BAD_CREATOR;
+    else if (ch.idents[ci].vclass != 0) R.pre = C_UNSUPPORTED;  // P-384 key / SHA3 MSP
   }
   if ((R.flags & BDF_INDEX_OK) && !(R.flags & BDF_INDEX_FROM_TXID)) J.cnt[BJ_I] = 1;
   if (R.pre == C_PENDING) {
@@ -467,7 +548,7 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
           uint32_t ne = 0;
           for (uint32_t k = 0; k < R.nend; k++) {
             const int32_t e = id[1 + k];
-            if (e >= 0 && ch.idents[e].key_slot >= 0) ne++;
+            if (e >= 0 && ch.idents[e].vclass == 0) ne++;
           }
           J.cnt[BJ_E] = ne;
         }
@@ -614,7 +695,7 @@ __global__ __launch_bounds__(256) void k_bd_emit(uint32_t ntx, const DevTx *__re
     uint32_t r = 0;
     for (uint32_t k = 0; k < R.nend && r < J.cnt[BJ_E]; k++) {
       const int32_t e = id[1 + k];
-      if (e < 0 || ch.idents[e].key_slot < 0) continue;
+      if (e < 0 || ch.idents[e].vclass != 0) continue;
       verify(totals[BJ_C] + J.base[BJ_E] + r, R.end_sig[k], ch.idents[e].key_slot, (1 + k) * ntx + t);
       r++;
     }
@@ -625,9 +706,10 @@ __global__ __launch_bounds__(256) void k_bd_emit(uint32_t ntx, const DevTx *__re
 namespace {
 
 // cauthdsl greedy evaluation (common/cauthdsl/cauthdsl.go:24-92): SignedBy takes the first
-// unused signer satisfying the principal; NOutOf tries each sub-rule on a copy of `used`
-// and keeps the copy when it succeeds.  Iterative DFS; returns -1 on stack overflow.
-DEV int eval_policy(const DevChannel &ch, const DevPolicy &P, const int32_t *ids, uint32_t nids) {
+// unused signer satisfying the principal (same MSP; MEMBER = valid, other roles from the role
+// bits); NOutOf tries each sub-rule on a copy of `used` and keeps the copy when it succeeds.
+// Iterative DFS; returns -1 on stack overflow.
+DEV int eval_sig(const DevChannel &ch, const DevPolicy &P, const int32_t *ids, uint32_t nids) {
   struct F {
     uint32_t node, k;
     int32_t verified;
@@ -636,7 +718,6 @@ DEV int eval_policy(const DevChannel &ch, const DevPolicy &P, const int32_t *ids
   F st[16];
   int sp = 0;
   uint32_t used = 0;
-  // evaluate `node`; for NOutOf push a frame and iterate its kids
   uint32_t node = (uint32_t)P.root;
   int ret = -2;  // -2: descend into `node`; else result of the last finished node (0/1)
   for (;;) {
@@ -648,7 +729,9 @@ DEV int eval_policy(const DevChannel &ch, const DevPolicy &P, const int32_t *ids
           for (uint32_t i = 0; i < nids; i++) {
             if ((used >> i) & 1u) continue;
             const DevIdent &I = ch.idents[ids[i]];
-            if (I.msp == N.msp && I.valid) {
+            const bool sat = I.msp == N.msp &&
+                             (N.role == 0 ? I.valid != 0 : (N.role > 0 && N.role < 32 && ((I.roles >> N.role) & 1u)));
+            if (sat) {
               used |= 1u << i;
               ret = 1;
               break;
@@ -679,6 +762,28 @@ DEV int eval_policy(const DevChannel &ch, const DevPolicy &P, const int32_t *ids
     sp--;
     if (sp == 0) return ret;
   }
+}
+// 1 satisfied, 0 not, 2 outside the model, -1 device stack overflow (host redo)
+DEV int eval_policy(const DevChannel &ch, uint32_t pi, const int32_t *ids, uint32_t nids, int depth) {
+  const DevPolicy &P = ch.policies[pi];
+  if (P.kind == DP_REJECT) return 0;
+  if (P.kind == DP_SIG) {
+    if (!P.decode_ok || !P.compile_ok) return 0;
+    if (P.needs_roles)
+      for (uint32_t i = 0; i < nids; i++)
+        if (!ch.idents[ids[i]].roles_known) return 2;
+    return eval_sig(ch, P, ids, nids);
+  }
+  if (P.kind == DP_IMPLICIT && depth == 0) {  // ImplicitMetaPolicy (implicitmeta.go:69-104)
+    int32_t ok = 0;
+    for (uint32_t q = 0; q < P.nsub; q++) {
+      const int v = eval_policy(ch, ch.subs[P.sub0 + q], ids, nids, 1);
+      if (v == 2 || v < 0) return v;
+      ok += v;
+    }
+    return ok >= P.threshold ? 1 : 0;
+  }
+  return 2;
 }
 
 DEV bool hex32(S s, uint8_t out[32]) {
@@ -766,44 +871,44 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
       } else if (R.disp != C_VALID) {
         code = R.disp;
       } else {
-        // SignatureSetToValidIdentities: dedup before verify, insert after success
+        // SignatureSetToValidIdentities (policy.go:363-395): deserialize, dedup, verify -- when
+        // some policy is evaluated
+        bool evaluates = false, unsup = false;
+        for (uint32_t i = 0; i < R.npol; i++) evaluates |= R.pol[i] >= 0;
         int32_t ids[BD_MAX_END];
         uint32_t seen[BD_MAX_END];
         uint32_t nids = 0, r = 0;
-        for (uint32_t k = 0; k < R.nend; k++) {
+        for (uint32_t k = 0; k < R.nend && evaluates; k++) {
           const int32_t e = id[1 + k];
+          if (e == -2) { unsup = true; break; }
           if (e < 0) continue;
-          const bool has_job = ch.idents[e].key_slot >= 0;
+          const DevIdent &I = ch.idents[e];
+          const bool has_job = I.vclass == 0;
           const uint32_t vj = has_job ? totals[0] + J.base[BJ_E] + r : 0u;
           if (has_job) r++;
-          const uint32_t canon = ch.idents[e].canon;
           bool dup = false;
-          for (uint32_t q = 0; q < nids; q++) dup |= seen[q] == canon;
+          for (uint32_t q = 0; q < nids; q++) dup |= seen[q] == I.canon;
           if (dup) continue;
+          if (I.vclass == 2) { unsup = true; break; }
           if (!has_job || vstatus[vj] != 0) continue;
-          seen[nids] = canon;
+          seen[nids] = I.canon;
           ids[nids++] = e;
         }
         bool has25 = false, has10 = false;
         code = C_VALID;
-        for (uint32_t i = 0; i < R.npol; i++) {
+        for (uint32_t i = 0; i < R.npol && !unsup; i++) {
           const int pi = R.pol[i];
+          if (pi == -2) { unsup = true; break; }
           if (pi < 0) { has25 = true; continue; }
-          const DevPolicy &P = ch.policies[pi];
-          if (P.unsupported) { code = C_UNSUPPORTED; break; }
-          bool ok2 = false;
-          if (P.decode_ok && P.compile_ok) {
-            const int v = eval_policy(ch, P, ids, nids);
-            if (v < 0) atomicOr(flags, 1u);  // deeper than the device stack: host redo
-            ok2 = v == 1;
-          }
-          if (!ok2) has10 = true;
+          const int v = eval_policy(ch, (uint32_t)pi, ids, nids, 0);
+          if (v < 0) atomicOr(flags, 1u);  // deeper than the device stack: host redo
+          if (v == 2) { unsup = true; break; }
+          if (v != 1) has10 = true;
         }
-        if (code != C_UNSUPPORTED) {
-          if (has25 && has10) code = C_UNSUPPORTED;
-          else if (has25) code = C_INVALID_CC;
-          else if (has10) code = C_POLICY;
-        }
+        if (unsup) code = C_UNSUPPORTED;
+        else if (has25 && has10) code = C_UNSUPPORTED;
+        else if (has25) code = C_INVALID_CC;
+        else if (has10) code = C_POLICY;
       }
     }
   }

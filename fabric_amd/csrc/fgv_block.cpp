@@ -41,203 +41,12 @@
 #include "pbwire.h"
 
 #include "fgv_visitors.h"
+#include "fgv_channel.h"
 #include "blockdev.h"
 
 // ======================================================================= channel model
+// (fgv_channel.h)
 namespace fgvb {
-
-struct Ident {
-  std::string mspid;
-  std::string id_bytes;
-  int32_t key_slot = -1;  // -1: not a P-256 key (Verify errors)
-  bool valid = false;     // msp Validate() result
-  uint32_t canon = 0;     // dedup identity id: Mspid + Id (Id = hex SHA-256(cert))
-  int32_t msp = -1;       // interned Mspid (Channel::intern)
-};
-
-struct PNode {
-  int type = 0;  // 1 NOutOf, 2 SignedBy
-  int32_t n = 0;
-  int principal = -1;
-  std::vector<int> kids;
-};
-struct Policy {
-  bool decode_ok = false, compile_ok = false, unsupported = false;
-  std::vector<PNode> nodes;
-  int root = -1;
-  std::vector<std::string> principal_msp;  // "" + bad flag for undecodable principal
-  std::vector<bool> principal_bad;
-  std::vector<int32_t> principal_mspi;     // interned principal_msp, -1 for a bad principal
-};
-
-// SignaturePolicy decoding into the node list (recursive, oneof: last member wins)
-struct VSigPolicy;
-struct VNOutOf {
-  int32_t n = 0;
-  std::vector<Span> rules;
-  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_VARINT : f == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
-  void on_varint(uint32_t, uint64_t v) { n = pbw::as_int32(v); }
-  bool on_len(uint32_t, Span s) { rules.push_back(s); return true; }
-};
-struct VSigPolicyRaw {
-  int which = 0;  // 0 none, 1 signed_by, 2 n_out_of
-  int32_t signed_by = 0;
-  std::vector<Span> noutof;  // merged occurrences
-  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_VARINT : f == 2 ? pbw::K_MSG : pbw::K_NONE; }
-  void on_varint(uint32_t, uint64_t v) { which = 1; signed_by = pbw::as_int32(v); noutof.clear(); }
-  bool on_len(uint32_t, Span s) {
-    if (which != 2) noutof.clear();
-    which = 2;
-    noutof.push_back(s);
-    return true;
-  }
-};
-struct VSPE {
-  int32_t version = 0;
-  bool has_rule = false;
-  std::vector<Span> rule;
-  std::vector<Span> identities;
-  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_VARINT : f == 2 ? pbw::K_MSG : f == 3 ? pbw::K_REP_MSG : pbw::K_NONE; }
-  void on_varint(uint32_t, uint64_t v) { version = pbw::as_int32(v); }
-  bool on_len(uint32_t f, Span s) {
-    if (f == 2) { has_rule = true; rule.push_back(s); }
-    else identities.push_back(s);
-    return true;
-  }
-};
-struct VAppPolicy {
-  int which = 0;  // 1 signature_policy, 2 channel ref
-  std::vector<Span> spe;
-  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_MSG : f == 2 ? pbw::K_STRING : pbw::K_NONE; }
-  void on_varint(uint32_t, uint64_t) {}
-  bool on_len(uint32_t f, Span s) {
-    if (f == 1) {
-      if (which != 1) spe.clear();
-      which = 1;
-      spe.push_back(s);
-    } else {
-      which = 2;
-      spe.clear();
-    }
-    return true;
-  }
-};
-
-// decode a (merged) SignaturePolicy fully; returns false on wire error
-static bool decode_sigpolicy(const std::vector<Span> &occ, VSigPolicyRaw &out) {
-  for (const Span &s : occ)
-    if (!pbw::decode(s.p, s.n, out)) return false;
-  return true;
-}
-
-// Build nodes (cauthdsl.compile shape).  Returns node index or -1 on compile error.
-static int build_node(Policy &P, const std::vector<Span> &occ, bool &wire_ok, int depth) {
-  if (depth > 1000) { wire_ok = false; return -1; }
-  VSigPolicyRaw raw;
-  if (!decode_sigpolicy(occ, raw)) { wire_ok = false; return -1; }
-  PNode node;
-  if (raw.which == 1) {
-    node.type = 2;
-    if (raw.signed_by < 0 || raw.signed_by >= (int32_t)P.principal_msp.size()) return -1;
-    node.principal = raw.signed_by;
-  } else if (raw.which == 2) {
-    node.type = 1;
-    VNOutOf no;
-    for (const Span &s : raw.noutof)
-      if (!pbw::decode(s.p, s.n, no)) { wire_ok = false; return -1; }
-    node.n = no.n;
-    // sub-rules must all decode (eager protobuf) before compile errors matter
-    std::vector<int> kids;
-    bool compile_fail = false;
-    for (const Span &r : no.rules) {
-      std::vector<Span> one{r};
-      int k = build_node(P, one, wire_ok, depth + 1);
-      if (!wire_ok) return -1;
-      if (k < 0) compile_fail = true;
-      kids.push_back(k);
-    }
-    if (compile_fail) return -1;
-    node.kids = kids;
-  } else {
-    return -1;  // "Unknown type" (nil rule handled by caller)
-  }
-  P.nodes.push_back(node);
-  return (int)P.nodes.size() - 1;
-}
-
-static Policy compile_policy(const uint8_t *b, size_t n) {
-  Policy P;
-  VAppPolicy ap;
-  if (!pbw::decode(b, n, ap)) return P;  // unmarshal error -> evaluation error
-  if (ap.which == 2) { P.decode_ok = true; P.unsupported = true; return P; }
-  if (ap.which != 1) { P.decode_ok = true; return P; }  // unsupported policy type -> error
-  VSPE spe;
-  for (const Span &s : ap.spe)
-    if (!pbw::decode(s.p, s.n, spe)) return P;
-  // 1) wire: every MSPPrincipal and the whole rule tree decode eagerly (proto.Unmarshal)
-  std::vector<VPrincipal> prs(spe.identities.size());
-  for (size_t i = 0; i < spe.identities.size(); i++)
-    if (!pbw::decode(spe.identities[i].p, spe.identities[i].n, prs[i])) return P;
-  for (const VPrincipal &pr : prs) {
-    VMSPRole role;
-    bool ok = pbw::decode(pr.principal.p, pr.principal.n, role);
-    P.principal_msp.push_back(ok ? role.mspid.str() : std::string());
-    P.principal_bad.push_back(!ok);
-  }
-  bool wire_ok = true;
-  int root = -1;
-  if (spe.has_rule) root = build_node(P, spe.rule, wire_ok, 0);
-  if (!wire_ok) return Policy();
-  // 2) principals outside ROLE/MEMBER need MSP data the engine does not model
-  for (size_t i = 0; i < prs.size(); i++) {
-    if (prs[i].cls != 0) { P.decode_ok = true; P.unsupported = true; return P; }
-    if (!P.principal_bad[i]) {
-      VMSPRole role;
-      pbw::decode(prs[i].principal.p, prs[i].principal.n, role);
-      if (role.role != 0) { P.decode_ok = true; P.unsupported = true; return P; }
-    }
-  }
-  P.decode_ok = true;
-  P.root = root;
-  P.compile_ok = root >= 0;
-  return P;
-}
-
-struct Channel {
-  std::string name;
-  std::vector<Ident> idents;
-  std::unordered_multimap<uint64_t, uint32_t> ident_index;
-  std::unordered_map<std::string, uint32_t> canon_ids;
-  std::unordered_map<std::string, int32_t> msp_ids;  // Mspid interning (policy principals, idents)
-  std::vector<Policy> policies;
-  std::unordered_map<std::string, int> chaincodes;  // namespace -> policies index
-  std::deque<std::string> committed_store;          // ledger txids (stable storage)
-  std::unordered_set<std::string_view> committed;
-
-  int32_t intern(const std::string &msp) {
-    auto it = msp_ids.find(msp);
-    if (it == msp_ids.end()) it = msp_ids.emplace(msp, (int32_t)msp_ids.size()).first;
-    return it->second;
-  }
-  bool is_committed(const Span &txid) const {
-    return committed.count(std::string_view(reinterpret_cast<const char *>(txid.p), txid.n)) != 0;
-  }
-
-  int lookup(const Span &ser) const {
-    VSerializedIdentity sid;
-    if (!pbw::decode(ser.p, ser.n, sid)) return -1;
-    uint64_t h = hash_bytes(sid.mspid.p, sid.mspid.n);
-    h = hash_bytes(sid.id_bytes.p, sid.id_bytes.n, h ^ 0xA5);
-    auto range = ident_index.equal_range(h);
-    for (auto it = range.first; it != range.second; ++it) {
-      const Ident &I = idents[it->second];
-      if (sid.mspid.eq(I.mspid.data(), I.mspid.size()) && sid.id_bytes.eq(I.id_bytes.data(), I.id_bytes.size()))
-        return (int)it->second;
-    }
-    return -1;
-  }
-};
-
 // ======================================================================= per-tx records
 enum : uint8_t { C_VALID = 0, C_BAD_PAYLOAD = 2, C_BAD_HDR = 3, C_BAD_CREATOR = 4, C_BAD_ETX = 5,
                  C_UNSUP_PAYLOAD = 7, C_BAD_TXID = 8, C_DUP_TXID = 9, C_POLICY = 10,
@@ -286,10 +95,11 @@ using namespace fgvb;
 
 // channel model image in HBM for the device-resident path (blockdev.h DevChannel)
 struct DevImage {
-  DevBuf name, idents, ibytes, itable, ihash, cc, ccb, pol, nodes, kids, committed;
+  DevBuf name, idents, ibytes, itable, ihash, cc, colls, impl, msps, ccb, pol, nodes, kids, subs, committed;
   DevChannel ch{};
   void release() {
-    for (DevBuf *b : {&name, &idents, &ibytes, &itable, &ihash, &cc, &ccb, &pol, &nodes, &kids, &committed})
+    for (DevBuf *b : {&name, &idents, &ibytes, &itable, &ihash, &cc, &colls, &impl, &msps, &ccb, &pol, &nodes, &kids,
+                      &subs, &committed})
       b->release();
   }
 };
@@ -446,10 +256,13 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
   if (env.signature.nil()) { R.pre = C_BAD_CREATOR; return; }
   if (chdr.channel_id.n == 0) { R.pre = C_UNSUPPORTED; return; }  // peer-local MSP
   if (!chdr.channel_id.eq(ch.name.data(), ch.name.size())) { R.pre = C_BAD_CREATOR; return; }
+  // DeserializeIdentity -> Validate -> Verify (msgvalidation.go:26-64)
   R.creator_ident = ch.lookup(shdr.creator);
+  if (R.creator_ident == -2) { R.pre = C_UNSUPPORTED; return; }  // unregistered certificate of a channel MSP
   if (R.creator_ident < 0) { R.pre = C_BAD_CREATOR; return; }
   const Ident &ci = ch.idents[R.creator_ident];
-  if (!ci.valid || ci.key_slot < 0) { R.pre = C_BAD_CREATOR; return; }
+  if (!ci.valid || ci.verify_class() == 1) { R.pre = C_BAD_CREATOR; return; }
+  if (ci.verify_class() == 2) { R.pre = C_UNSUPPORTED; return; }  // P-384 key / SHA3 MSP
   if (chdr.type != 3) return;  // CONFIG (unsupported) / CONFIG_UPDATE (7) decided in the fold
 
   // validateEndorserTransaction (msgvalidation.go:165-245)
@@ -482,18 +295,23 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
   if (!pbw::decode(prp.extension.p, prp.extension.n, cca)) { R.disp = C_BAD_RESP; return; }
   VTxRwSet rw;
   if (!pbw::decode(cca.results.p, cca.results.n, rw)) { R.disp = C_BAD_RWSET; return; }
-  // per namespace: 1 = writes (kv / metadata / collection), 2 = metadata or collection writes
+  // per namespace: 1 = writes (kv / metadata / collection), 2 = metadata writes, 4 = public
+  // writes; the collections with hashed writes (policyCheckerV20 collection EPs)
   pbw::SmallVec<uint8_t, 8> wflags;
+  pbw::SmallVec<std::pair<uint32_t, Span>, 8> wcolls;  // (namespace index, collection name)
   for (size_t k = 0; k < rw.ns.size(); k++) {
     VKVRWSet kv;
     if (!pbw::decode(rw.ns[k].rwset.p, rw.ns[k].rwset.n, kv)) { R.disp = C_BAD_RWSET; return; }
-    bool coll_writes = false;
+    bool coll_writes = false, coll_meta = false;
     for (const VCollHashed &c : rw.ns[k].coll) {
       VHashedRWSet h;
       if (!pbw::decode(c.hashed.p, c.hashed.n, h)) { R.disp = C_BAD_RWSET; return; }
-      if (h.nwrites || h.nmeta) coll_writes = true;
+      if (h.nwrites) wcolls.push_back({(uint32_t)k, c.name});
+      coll_writes |= h.nwrites != 0;
+      coll_meta |= h.nmeta != 0;
     }
-    wflags.push_back((uint8_t)(((kv.nwrites || kv.nmeta || coll_writes) ? 1 : 0) | ((kv.nmeta || coll_writes) ? 2 : 0)));
+    wflags.push_back((uint8_t)(((kv.nwrites || kv.nmeta || coll_writes || coll_meta) ? 1 : 0) |
+                               ((kv.nmeta || coll_meta) ? 2 : 0) | (kv.nwrites ? 4 : 0)));
   }
   if (!ext.has_ccid || !cca.has_ccid) { R.disp = C_OTHER; return; }
   const Span ccid = ext.ccid.name;
@@ -516,8 +334,8 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
   std::sort(nss.begin(), nss.end());
   for (size_t k = 1; k < nss.size(); k++)
     if (nss[k].eq(nss[k - 1])) { R.disp = C_ILLEGAL_WS; return; }
-  // written namespaces + the invoked chaincode; key-level / collection endorsement policies
-  // are outside the modelled state
+  // written namespaces + the invoked chaincode; metadata (key-level endorsement) writes are
+  // outside the modelled state
   pbw::SmallVec<Span, 8> wr;
   wr.push_back(ccid);
   for (size_t k = 0; k < rw.ns.size(); k++) {
@@ -527,9 +345,37 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
   }
   std::sort(wr.begin(), wr.end());
   R.disp = C_VALID;
+  // the policies each namespace's vscc evaluates (statebased/validator_keylevel.go:173-233,
+  // v20.go:105-167, no key-level validation parameters): public writes -> the chaincode EP; a
+  // collection with hashed writes -> its collection EP (or the chaincode EP); none of these ->
+  // the chaincode EP.  -1: INVALID_CHAINCODE, -2: outside the model.
+  auto push = [&](int p) {
+    if (std::find(R.policies.begin(), R.policies.end(), p) == R.policies.end()) R.policies.push_back(p);
+  };
   for (const Span &ns : wr) {
-    auto it = ch.chaincodes.find(ns.str());
-    R.policies.push_back(it == ch.chaincodes.end() ? -1 : it->second);
+    auto it = ch.ccs.find(ns.str());
+    if (it == ch.ccs.end() || it->second.status == 1) { push(-1); continue; }
+    const CCInfo &cc = it->second;
+    if (cc.status != 0) { push(-2); continue; }
+    int k = -1;
+    for (size_t q = 0; q < rw.ns.size(); q++)
+      if (rw.ns[q].ns.eq(ns)) { k = (int)q; break; }
+    bool any = false;
+    if (k >= 0 && (wflags[k] & 4)) { push(cc.ep); any = true; }
+    for (const auto &wc : wcolls) {
+      if ((int)wc.first != k) continue;
+      any = true;
+      const std::string coll = wc.second.str();
+      if (coll.compare(0, strlen(kImplicitPrefix), kImplicitPrefix) == 0) {
+        auto ie = ch.implicit_ep.find(coll.substr(strlen(kImplicitPrefix)));
+        push(ie == ch.implicit_ep.end() ? -2 : ie->second);
+        continue;
+      }
+      if (!cc.colls_known) { push(-2); continue; }
+      auto ce = cc.colls.find(coll);
+      push(ce == cc.colls.end() ? 0 : ce->second < 0 ? cc.ep : ce->second);  // "no such collection" -> reject
+    }
+    if (!any) push(cc.ep);
   }
   // endorsement signature set (validator_keylevel.go:246-260)
   R.ends.resize(cap.action.ends.size());
@@ -560,11 +406,14 @@ static bool eval_node(const Policy &P, int node, const int *ids, size_t nids, co
   const PNode &N = P.nodes[node];
   if (N.type == 2) {
     const int32_t msp = P.principal_mspi[N.principal];  // -1: undecodable principal
+    const int32_t role = P.principal_role[N.principal];
     if (msp < 0) return false;
     for (size_t i = 0; i < nids; i++) {
       if (used.get(i)) continue;
       const Ident &I = ch.idents[ids[i]];
-      if (I.msp == msp && I.valid) {
+      // SatisfiesPrincipal(ROLE): same MSP, MEMBER = Validate, other roles from the MSP layer
+      const bool sat = I.msp == msp && (role == 0 ? I.valid : (role > 0 && role < 32 && ((I.roles >> role) & 1u)));
+      if (sat) {
         used.set(i);
         return true;
       }
@@ -581,14 +430,36 @@ static bool eval_node(const Policy &P, int node, const int *ids, size_t nids, co
   }
   return verified >= N.n;
 }
-static bool eval_policy(const Policy &P, const int *ids, size_t nids, const Channel &ch) {
-  if (nids <= 64) {
-    UsedBits u;
-    return eval_node(P, P.root, ids, nids, ch, u);
+// 1 satisfied, 0 not, 2 outside the model
+static int eval_policy(const Channel &ch, int pi, const int *ids, size_t nids, int depth = 0) {
+  const Policy &P = ch.policies[pi];
+  switch (P.kind) {
+    case PK_REJECT: return 0;
+    case PK_SIG: {
+      if (!P.decode_ok || !P.compile_ok) return 0;
+      if (P.needs_roles)
+        for (size_t i = 0; i < nids; i++)
+          if (!ch.idents[ids[i]].roles_known) return 2;
+      if (nids <= 64) {
+        UsedBits u;
+        return eval_node(P, P.root, ids, nids, ch, u) ? 1 : 0;
+      }
+      UsedVec u;
+      u.v.assign(nids, 0);
+      return eval_node(P, P.root, ids, nids, ch, u) ? 1 : 0;
+    }
+    case PK_IMPLICIT: {  // ImplicitMetaPolicy.EvaluateSignedData (implicitmeta.go:69-104)
+      if (depth > 0) return 2;
+      int ok = 0;
+      for (int s : P.subs) {
+        const int v = eval_policy(ch, s, ids, nids, depth + 1);
+        if (v == 2) return 2;
+        ok += v;
+      }
+      return ok >= P.threshold ? 1 : 0;
+    }
+    default: return 2;
   }
-  UsedVec u;
-  u.v.assign(nids, 0);
-  return eval_node(P, P.root, ids, nids, ch, u);
 }
 
 // ======================================================================= API
@@ -618,7 +489,7 @@ static void count_jobs(const Channel &ch, TxRec &R) {
   if (R.disp != C_VALID) return;
   uint32_t ne = 0;
   for (const EndRec &e : R.ends)
-    if (e.ident >= 0 && ch.idents[e.ident].key_slot >= 0) ne++;
+    if (e.ident >= 0 && ch.idents[e.ident].verify_class() == 0) ne++;
   R.n_ej = (uint16_t)std::min<uint32_t>(ne, 0xFFFF);
 }
 
@@ -628,6 +499,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
                             const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                             const uint32_t *tx_hi, fgv_tx_result *res_out, size_t res_cap, size_t *ntx_out) {
   Channel &ch = S->ch;
+  if (ch.dirty) ch.compile();
   using clk = std::chrono::steady_clock;
   auto t_start = clk::now();
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
@@ -729,7 +601,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         uint32_t left = R.n_ej;
         for (EndRec &e2 : R.ends) {
           if (!left) break;
-          if (e2.ident < 0 || ch.idents[e2.ident].key_slot < 0) continue;
+          if (e2.ident < 0 || ch.idents[e2.ident].verify_class() != 0) continue;
           const uint32_t hj = o[3]++;
           job(hj, b, R.prp, e2.endorser);
           e2.vjob = ov3++;
@@ -785,31 +657,38 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
       } else if (R.disp != C_VALID) {
         code = R.disp;
       } else {
-        // SignatureSetToValidIdentities (policy.go:363-395): dedup before verify
+        // SignatureSetToValidIdentities (policy.go:363-395): deserialize, dedup, verify; only
+        // when some policy is evaluated
+        bool evaluates = false, unsup = false;
+        for (int pi : R.policies) evaluates |= pi >= 0;
         pbw::SmallVec<int, 16> ids;
-        pbw::SmallVec<uint32_t, 16> seen;
-        for (const EndRec &e : R.ends) {
-          if (e.ident < 0) continue;
-          const uint32_t canon = ch.idents[e.ident].canon;
-          if (std::find(seen.begin(), seen.end(), canon) != seen.end()) continue;
-          if (e.vjob == UINT32_MAX || vstatus[e.vjob] != 0) continue;
-          seen.push_back(canon);
-          ids.push_back(e.ident);
+        if (evaluates) {
+          pbw::SmallVec<uint32_t, 16> seen;
+          for (const EndRec &e : R.ends) {
+            if (e.ident == -2) { unsup = true; break; }
+            if (e.ident < 0) continue;
+            const Ident &I = ch.idents[e.ident];
+            if (std::find(seen.begin(), seen.end(), I.canon) != seen.end()) continue;
+            const int vc = I.verify_class();
+            if (vc == 2) { unsup = true; break; }
+            if (vc == 1 || e.vjob == UINT32_MAX || vstatus[e.vjob] != 0) continue;
+            seen.push_back(I.canon);
+            ids.push_back(e.ident);
+          }
         }
         bool has25 = false, has10 = false;
         code = C_VALID;
         for (int pi : R.policies) {
-          if (pi < 0) { has25 = true; continue; }
-          const Policy &P = ch.policies[pi];
-          if (P.unsupported) { code = C_UNSUPPORTED; break; }
-          const bool ok2 = P.decode_ok && P.compile_ok && eval_policy(P, ids.data(), ids.size(), ch);
-          if (!ok2) has10 = true;
+          if (unsup || pi == -2) { unsup = true; break; }
+          if (pi == -1) { has25 = true; continue; }
+          const int v = eval_policy(ch, pi, ids.data(), ids.size());
+          if (v == 2) { unsup = true; break; }
+          if (v == 0) has10 = true;
         }
-        if (code != C_UNSUPPORTED) {
-          if (has25 && has10) code = C_UNSUPPORTED;  // Go map order decides the reported code
-          else if (has25) code = C_INVALID_CC;
-          else if (has10) code = C_POLICY;
-        }
+        if (unsup) code = C_UNSUPPORTED;
+        else if (has25 && has10) code = C_UNSUPPORTED;  // Go map order decides the reported code
+        else if (has25) code = C_INVALID_CC;
+        else if (has10) code = C_POLICY;
       }
     }
     if (code == C_UNSUPPORTED) unsupported = true;
@@ -889,41 +768,83 @@ int fgv_block_set_channel(fgv_block_state *S, const char *name) {
   return FGV_OK;
 }
 
-int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, int32_t key_slot, int valid,
-                           const uint8_t id_digest[32]) {
-  S->dev_dirty = true;
+// key_slot: the P-256 key table slot (or -1); info: key type, hash family, Validate() result,
+// role bits and the identity digest (include/fgv.h fgv_identity_info).  Registering the same
+// (mspid, id_bytes) again replaces its record.
+int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, int32_t key_slot,
+                           const fgv_identity_info *info) {
   VSerializedIdentity sid;
   if (!pbw::decode(ser, len, sid)) return FGV_EINVAL;
+  if (info->key_type < FGV_KEY_P256 || info->key_type > FGV_KEY_UNDESERIALIZABLE || info->hash_family > FGV_HASH_SHA3)
+    return FGV_EINVAL;
+  S->dev_dirty = true;
+  Channel &ch = S->ch;
+  ch.dirty = true;
   Ident I;
   I.mspid = sid.mspid.str();
   I.id_bytes = sid.id_bytes.str();
-  I.key_slot = key_slot;
-  I.valid = valid != 0;
-  std::string canon = I.mspid + std::string(reinterpret_cast<const char *>(id_digest), 32);
-  auto it = S->ch.canon_ids.find(canon);
-  if (it == S->ch.canon_ids.end()) it = S->ch.canon_ids.emplace(canon, (uint32_t)S->ch.canon_ids.size()).first;
+  I.kind = (uint8_t)info->key_type;
+  I.key_slot = info->key_type == FGV_KEY_P256 ? key_slot : -1;
+  I.hash3 = info->hash_family == FGV_HASH_SHA3;
+  I.valid = info->valid != 0;
+  I.roles_known = (info->roles & FGV_ROLES_UNKNOWN) == 0;
+  I.roles = I.roles_known ? info->roles : 0;
+  std::string canon = I.mspid + std::string(reinterpret_cast<const char *>(info->id_digest), 32);
+  auto it = ch.canon_ids.find(canon);
+  if (it == ch.canon_ids.end()) it = ch.canon_ids.emplace(canon, (uint32_t)ch.canon_ids.size()).first;
   I.canon = it->second;
-  I.msp = S->ch.intern(I.mspid);
+  I.msp = ch.intern(I.mspid);
   uint64_t h = hash_bytes(sid.mspid.p, sid.mspid.n);
   h = hash_bytes(sid.id_bytes.p, sid.id_bytes.n, h ^ 0xA5);
-  if (S->ch.lookup(Span{ser, (uint32_t)len}) >= 0) return FGV_OK;  // already registered
-  S->ch.idents.push_back(I);
-  S->ch.ident_index.emplace(h, (uint32_t)S->ch.idents.size() - 1);
+  auto range = ch.ident_index.equal_range(h);
+  for (auto r = range.first; r != range.second; ++r) {
+    Ident &old = ch.idents[r->second];
+    if (old.mspid == I.mspid && old.id_bytes == I.id_bytes) {
+      old = I;
+      return FGV_OK;
+    }
+  }
+  ch.idents.push_back(I);
+  ch.ident_index.emplace(h, (uint32_t)ch.idents.size() - 1);
   return FGV_OK;
 }
 
-int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const uint8_t *policy, size_t len) {
+int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const char *plugin, const uint8_t *policy,
+                               size_t len, uint32_t flags) {
   S->dev_dirty = true;
-  Policy P = compile_policy(policy, len);
-  for (size_t i = 0; i < P.principal_msp.size(); i++)
-    P.principal_mspi.push_back(P.principal_bad[i] ? -1 : S->ch.intern(P.principal_msp[i]));
-  auto it = S->ch.chaincodes.find(ns);
-  if (it == S->ch.chaincodes.end()) {
-    S->ch.policies.push_back(std::move(P));
-    S->ch.chaincodes.emplace(ns, (int)S->ch.policies.size() - 1);
-  } else {
-    S->ch.policies[it->second] = std::move(P);
-  }
+  S->ch.dirty = true;
+  CCDef &d = S->ch.ccdefs[ns];
+  d.plugin = plugin;
+  d.policy.assign(reinterpret_cast<const char *>(policy), len);
+  d.flags = flags;
+  d.colls.clear();
+  return FGV_OK;
+}
+
+int fgv_block_define_collection(fgv_block_state *S, const char *ns, const char *coll, const uint8_t *policy,
+                                size_t len) {
+  auto it = S->ch.ccdefs.find(ns);
+  if (it == S->ch.ccdefs.end()) return FGV_ESTATE;
+  S->dev_dirty = true;
+  S->ch.dirty = true;
+  it->second.flags |= FGV_CC_COLLECTIONS_KNOWN;
+  it->second.colls[coll].assign(reinterpret_cast<const char *>(policy), len);
+  return FGV_OK;
+}
+
+int fgv_block_channel_config(fgv_block_state *S, const uint8_t *config, size_t len) {
+  RawConfig rc;
+  if (!parse_channel_config(config, len, rc)) return FGV_EINVAL;
+  S->dev_dirty = true;
+  S->ch.dirty = true;
+  S->ch.config = std::move(rc);
+  return FGV_OK;
+}
+
+int fgv_block_declare_msp(fgv_block_state *S, const char *mspid) {
+  S->dev_dirty = true;
+  S->ch.dirty = true;
+  S->ch.declared_msps.insert(mspid);
   return FGV_OK;
 }
 
@@ -983,6 +904,10 @@ static int build_dev_image(fgv_block_state *S) {
     d.msp = I.msp;
     d.canon = I.canon;
     d.valid = I.valid ? 1u : 0u;
+    d.vclass = I.kind == FGV_KEY_UNDESERIALIZABLE ? 3u : (uint32_t)I.verify_class();
+    d.roles = I.roles;
+    d.roles_known = I.roles_known ? 1u : 0u;
+    d.pad = 0;
     ih[i] = bd_ident_hash(reinterpret_cast<const uint8_t *>(I.mspid.data()), d.msp_len,
                           reinterpret_cast<const uint8_t *>(I.id_bytes.data()), d.idb_len);
   }
@@ -998,38 +923,66 @@ static int build_dev_image(fgv_block_state *S) {
   if ((rc = upload(D.idents, idents)) || (rc = upload(D.ibytes, ib)) || (rc = upload(D.itable, itable)) ||
       (rc = upload(D.ihash, ih)))
     return rc;
-  // chaincodes -> policies; policies -> flat node / kid arrays
-  std::vector<uint32_t> cc;
+  // chaincodes (+ their collections), implicit collections, channel MSPs -> word tables over
+  // one byte arena; policies -> flat node / kid / sub arrays
+  std::vector<uint32_t> cc, colls, impl, msps;
   std::vector<uint8_t> ccb;
-  for (const auto &kv : ch.chaincodes) {
-    cc.push_back((uint32_t)ccb.size());
-    cc.push_back((uint32_t)kv.first.size());
-    cc.push_back((uint32_t)kv.second);
-    ccb.insert(ccb.end(), kv.first.begin(), kv.first.end());
+  auto str = [&](const std::string &x, std::vector<uint32_t> &out) {
+    out.push_back((uint32_t)ccb.size());
+    out.push_back((uint32_t)x.size());
+    ccb.insert(ccb.end(), x.begin(), x.end());
+  };
+  for (const auto &kv : ch.ccs) {
+    const CCInfo &c = kv.second;
+    str(kv.first, cc);
+    cc.push_back((uint32_t)c.ep);
+    cc.push_back(c.status);
+    cc.push_back(c.colls_known ? 1u : 0u);
+    cc.push_back((uint32_t)(colls.size() / BD_COLL_WORDS));
+    cc.push_back((uint32_t)c.colls.size());
+    for (const auto &cl : c.colls) {
+      str(cl.first, colls);
+      colls.push_back((uint32_t)cl.second);
+    }
   }
+  for (const auto &kv : ch.implicit_ep) {
+    str(kv.first, impl);
+    impl.push_back((uint32_t)kv.second);
+  }
+  for (const auto &kv : ch.msp_ids)
+    if (ch.known_msps.count(kv.second)) str(kv.first, msps);
   std::vector<DevPolicy> pol(ch.policies.size());
   std::vector<DevPNode> nodes;
-  std::vector<uint32_t> kids;
+  std::vector<uint32_t> kids, subs;
   for (size_t p = 0; p < ch.policies.size(); p++) {
     const Policy &P = ch.policies[p];
     const uint32_t nbase = (uint32_t)nodes.size();
-    pol[p].decode_ok = P.decode_ok;
-    pol[p].compile_ok = P.compile_ok;
-    pol[p].unsupported = P.unsupported;
-    pol[p].root = P.root >= 0 ? (int32_t)(nbase + P.root) : -1;
+    DevPolicy &d = pol[p];
+    d.kind = P.kind == PK_SIG ? DP_SIG : P.kind == PK_IMPLICIT ? DP_IMPLICIT : P.kind == PK_UNSUP ? DP_UNSUP : DP_REJECT;
+    d.decode_ok = P.decode_ok;
+    d.compile_ok = P.compile_ok;
+    d.needs_roles = P.needs_roles;
+    d.root = P.root >= 0 ? (int32_t)(nbase + P.root) : -1;
+    d.threshold = P.threshold;
+    d.sub0 = (uint32_t)subs.size();
+    d.nsub = (uint32_t)P.subs.size();
+    for (int x : P.subs) subs.push_back((uint32_t)x);
     for (const PNode &N : P.nodes) {
-      DevPNode d;
-      d.type = N.type;
-      d.n = N.n;
-      d.msp = (N.type == 2) ? P.principal_mspi[N.principal] : -1;
-      d.kid0 = (uint32_t)kids.size();
-      d.nkids = (uint32_t)N.kids.size();
+      DevPNode dn;
+      dn.type = N.type;
+      dn.n = N.n;
+      dn.msp = (N.type == 2) ? P.principal_mspi[N.principal] : -1;
+      dn.role = (N.type == 2) ? P.principal_role[N.principal] : 0;
+      dn.kid0 = (uint32_t)kids.size();
+      dn.nkids = (uint32_t)N.kids.size();
       for (int k : N.kids) kids.push_back(nbase + (uint32_t)k);
-      nodes.push_back(d);
+      nodes.push_back(dn);
     }
   }
-  if ((rc = upload(D.cc, cc)) || (rc = upload(D.ccb, ccb)) || (rc = upload(D.pol, pol)) ||
-      (rc = upload(D.nodes, nodes)) || (rc = upload(D.kids, kids)))
+  ccb.resize(ccb.size() + 64, 0);
+  if ((rc = upload(D.cc, cc)) || (rc = upload(D.colls, colls)) || (rc = upload(D.impl, impl)) ||
+      (rc = upload(D.msps, msps)) || (rc = upload(D.ccb, ccb)) || (rc = upload(D.pol, pol)) ||
+      (rc = upload(D.nodes, nodes)) || (rc = upload(D.kids, kids)) || (rc = upload(D.subs, subs)))
     return rc;
   // committed ledger txids: only 64-char lowercase hex can equal a txid that passed CheckTxID
   std::vector<std::array<uint8_t, 32>> keys;
@@ -1072,12 +1025,18 @@ static int build_dev_image(fgv_block_state *S) {
   d.ident_table = D.itable.as<uint32_t>();
   d.ident_hash = D.ihash.as<uint64_t>();
   d.ident_mask = (uint32_t)(icap - 1);
-  d.ncc = (uint32_t)(cc.size() / 3);
+  d.ncc = (uint32_t)(cc.size() / BD_CC_WORDS);
   d.cc = D.cc.as<uint32_t>();
+  d.colls = D.colls.as<uint32_t>();
+  d.nimpl = (uint32_t)(impl.size() / BD_COLL_WORDS);
+  d.impl = D.impl.as<uint32_t>();
+  d.nmsp = (uint32_t)(msps.size() / 2);
+  d.msps = D.msps.as<uint32_t>();
   d.cc_bytes = D.ccb.as<uint8_t>();
   d.policies = D.pol.as<DevPolicy>();
   d.nodes = D.nodes.as<DevPNode>();
   d.kids = D.kids.as<uint32_t>();
+  d.subs = D.subs.as<uint32_t>();
   d.committed = ccap ? D.committed.as<uint8_t>() : nullptr;
   d.committed_mask = ccap ? (uint32_t)(ccap - 1) : 0u;
   d.committed_zero = zero;
@@ -1182,6 +1141,7 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   auto t0 = clk::now();
+  if (S->ch.dirty) S->ch.compile();
   if (S->dev_dirty) {
     int rc = build_dev_image(S);
     if (rc) return rc;

@@ -702,25 +702,60 @@ int fgv_channel_init(fgv_ctx *c, const char *name) {
   return fgv_block_set_channel(c->blk, name);
 }
 
-int fgv_msp_add_identity(fgv_ctx *c, const uint8_t *serialized, size_t len, const uint8_t *pubkey, int valid,
-                         const uint8_t *id_digest) {
-  if (!c || !serialized || !id_digest) return FGV_EINVAL;
+int fgv_msp_register_identity(fgv_ctx *c, const uint8_t *serialized, size_t len, const fgv_identity_info *info) {
+  if (!c || !serialized || !info) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
   int32_t slot = -1;
-  if (pubkey) {
+  if (info->key_type == FGV_KEY_P256) {
     uint32_t s;
-    int rc = keys_register_locked(c, pubkey, 1, &s);
+    int rc = keys_register_locked(c, info->pubkey, 1, &s);
     if (rc) return rc;
     slot = (int32_t)s;
   }
-  return fgv_block_add_identity(c->blk, serialized, len, slot, valid, id_digest);
+  return fgv_block_add_identity(c->blk, serialized, len, slot, info);
+}
+
+int fgv_msp_add_identity(fgv_ctx *c, const uint8_t *serialized, size_t len, const uint8_t *pubkey, int valid,
+                         const uint8_t *id_digest) {
+  if (!c || !serialized || !id_digest) return FGV_EINVAL;
+  fgv_identity_info info{};
+  info.key_type = pubkey ? FGV_KEY_P256 : FGV_KEY_OTHER;
+  info.hash_family = FGV_HASH_SHA2;
+  info.valid = valid != 0;
+  info.roles = FGV_ROLES_UNKNOWN;
+  if (pubkey) memcpy(info.pubkey, pubkey, 64);
+  memcpy(info.id_digest, id_digest, 32);
+  return fgv_msp_register_identity(c, serialized, len, &info);
+}
+
+int fgv_chaincode_define2(fgv_ctx *c, const char *ns, const char *plugin, const uint8_t *policy, size_t len,
+                          uint32_t flags) {
+  if (!c || !ns || !plugin || (len && !policy)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_define_chaincode(c->blk, ns, plugin, policy, len, flags);
 }
 
 int fgv_chaincode_define(fgv_ctx *c, const char *ns, const uint8_t *policy, size_t len) {
-  if (!c || !ns || (len && !policy)) return FGV_EINVAL;
+  return fgv_chaincode_define2(c, ns, "vscc", policy, len, 0);
+}
+
+int fgv_collection_define(fgv_ctx *c, const char *ns, const char *coll, const uint8_t *policy, size_t len) {
+  if (!c || !ns || !coll || (len && !policy)) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  return fgv_block_define_chaincode(c->blk, ns, policy, len);
+  return fgv_block_define_collection(c->blk, ns, coll, policy, len);
+}
+
+int fgv_channel_config(fgv_ctx *c, const uint8_t *config, size_t len) {
+  if (!c || (len && !config)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_channel_config(c->blk, config, len);
+}
+
+int fgv_msp_declare(fgv_ctx *c, const char *mspid) {
+  if (!c || !mspid) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_declare_msp(c->blk, mspid);
 }
 
 int fgv_ledger_add_txids(fgv_ctx *c, const uint8_t *buf, const uint64_t *off, const uint32_t *len, size_t n) {

@@ -160,9 +160,14 @@ void fgv_parallel_for(fgv_block_state *S, size_t n, const std::function<void(siz
 void fgv_mvcc_free(fgv_mvcc_state *M);
 
 int fgv_block_set_channel(fgv_block_state *S, const char *name);
-int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, int32_t key_slot, int valid,
-                           const uint8_t id_digest[32]);
-int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const uint8_t *policy, size_t len);
+int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, int32_t key_slot,
+                           const fgv_identity_info *info);
+int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const char *plugin, const uint8_t *policy,
+                               size_t len, uint32_t flags);
+int fgv_block_define_collection(fgv_block_state *S, const char *ns, const char *coll, const uint8_t *policy,
+                                size_t len);
+int fgv_block_channel_config(fgv_block_state *S, const uint8_t *config, size_t len);
+int fgv_block_declare_msp(fgv_block_state *S, const char *mspid);
 int fgv_block_add_txids(fgv_block_state *S, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
                         size_t n);
 int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,

@@ -206,17 +206,32 @@ class Network:
         return [i.pem for i in self.peers + self.clients] + [self.rogue.pem, self.forged.pem]
 
     def identities(self):
-        """What the MSP layer knows: (serialized, mspid, pubkey64, valid, id_digest).
-        RogueMSP is unknown to the channel, so it is NOT listed (deserialize error).  Neither
-        are Ed25519 identities: the reference's BCCSP x509 key importer accepts only ECDSA/RSA
-        keys (vendor/github.com/hyperledger/fabric-lib-go/bccsp/sw/keyimport.go:130-150, SURVEY
-        F4), so DeserializeIdentity fails for them -- creator -> BAD_CREATOR_SIGNATURE,
-        endorser -> skipped by SignatureSetToValidIdentities (common/policies/policy.go:363-395)."""
+        """What the MSP layer knows: (serialized, txvalidator.Identity).  RogueMSP is unknown to
+        the channel, so it is NOT listed (deserialize error).  Ed25519 identities are listed as
+        "undeserializable": the reference's BCCSP x509 key importer accepts only ECDSA/RSA keys
+        (vendor/github.com/hyperledger/fabric-lib-go/bccsp/sw/keyimport.go:130-150),
+        so DeserializeIdentity fails for them -- creator -> BAD_CREATOR_SIGNATURE, endorser ->
+        skipped by SignatureSetToValidIdentities (common/policies/policy.go:363-395).  Role bits
+        follow NodeOU classification (peers PEER, clients CLIENT; an invalid identity satisfies
+        no role, msp/mspimpl.go:331-376)."""
+        from ..txvalidator import Identity
         out = []
         for ident in self.peers + self.clients:
+            role_bit = 1 << (3 if ident.role == "peer" else 2)
             if ident.kind != "p256":
+                out.append((ident.serialized, Identity(ident.mspid, None, True, ident.id_digest, key="undeserializable")))
                 continue
-            out.append((ident.serialized, ident.mspid, ident.key.pub, True, ident.id_digest))
+            out.append((ident.serialized, Identity(ident.mspid, ident.key.pub, True, ident.id_digest, roles=1 | role_bit)))
+        out.append((self.forged.serialized, Identity(self.forged.mspid, self.forged.key.pub, False,
+                                                     self.forged.id_digest, roles=0)))
+        return out
+
+    def identities_legacy(self):
+        """the round-1 registration: (serialized, mspid, pubkey64, valid, id_digest), P-256 only"""
+        out = []
+        for ident in self.peers + self.clients:
+            if ident.kind == "p256":
+                out.append((ident.serialized, ident.mspid, ident.key.pub, True, ident.id_digest))
         out.append((self.forged.serialized, self.forged.mspid, self.forged.key.pub, False, self.forged.id_digest))
         return out
 
@@ -240,10 +255,13 @@ class _Tx:
 
 def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FAULTS_C2, endorse_dist=((2, 0.6), (3, 0.4)),
                reads=4, writes=4, value_len=200, threads=8, prev_hash=b"\x00" * 32, force=None, ns="mycc",
-               key_space=1_000_000, reuse=None, out_txs=None):
+               key_space=1_000_000, reuse=None, out_txs=None, collections=None):
     """Returns (block_bytes, labels list, envelopes list).
     reuse: {tx index: (creator Identity, nonce)} -> that tx re-uses an earlier txid (label
-    'dup_txid_prev'); out_txs: list that receives the generated tx objects."""
+    'dup_txid_prev'); out_txs: list that receives the generated tx objects; collections: names
+    of private-data collections -- every tx then also writes one key hash into one of them
+    (chosen per tx), so its namespace checks that collection's endorsement policy (the codes
+    are then the oracle's to decide, labels stay as generated)."""
     rng = random.Random((net.seed << 20) ^ (number << 4) ^ seed)
     txs = []
     fault_names = [f for f, _ in faults]
@@ -332,7 +350,13 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         ph = hashlib.sha256(t.chdr + t.shdr + t.ccpp).digest()
         if t.label == "bad_proposal_hash":
             ph = bytes([ph[0] ^ 1]) + ph[1:]
-        rw = tx_rwset([(ccname, kv_rwset(t.reads, t.writes))])
+        if collections:
+            t.coll = collections[rng.randrange(len(collections))]
+            kh = hashlib.sha256(b"%d/%d/%s" % (number, len(e_refs) + len(ed_refs), t.nonce)).digest()
+            rw = tx_rwset([(ccname, kv_rwset(t.reads, t.writes),
+                            [(t.coll, hashed_rwset([], [(kh, hashlib.sha256(kh).digest(), False)]))])])
+        else:
+            rw = tx_rwset([(ccname, kv_rwset(t.reads, t.writes))])
         events = b""
         if t.label == "event_other_cc":
             events = f_str(1, "someothercc") + f_str(3, "ev")

@@ -8,25 +8,65 @@
 There is no CPU fallback: FGV_EUNSUPPORTED / device errors propagate as exceptions so the
 caller (a Go shim in production) runs the reference code for that batch.
 """
+from dataclasses import dataclass
+from typing import Optional
+
 import numpy as np
 
-from ._lib import Engine, Unsupported  # noqa: F401
+from ._lib import CC_COLLECTIONS_KNOWN, CC_KEY_LEVEL_EP, Engine, Unsupported  # noqa: F401
 
 
-def setup_channel(engine: Engine, channel: str, identities, chaincodes, committed_txids=()):
-    """identities: iterable of (serialized, mspid, pubkey64 | None, valid, id_digest)."""
+@dataclass
+class Identity:
+    """What the peer's MSP layer knows of one SerializedIdentity (fgv_identity_info):
+    key "p256" | "p384" | "other" | "undeserializable"; hash_family of its MSP; roles: bit r set
+    iff msp.SatisfiesPrincipal(id, ROLE{mspid, r}) (None = unknown)."""
+    mspid: str
+    pub: Optional[bytes]
+    valid: bool
+    id_digest: bytes
+    key: str = "p256"
+    hash_family: str = "SHA2"
+    roles: Optional[int] = None
+
+
+def _as_identity(entry):
+    """(serialized, Identity-like) or the round-1 (serialized, mspid, pub | None, valid, id_digest)"""
+    if len(entry) == 2:
+        return entry[0], entry[1]
+    ser, mspid, pub, valid, dig = entry
+    return ser, Identity(mspid, pub, valid, dig, key="p256" if pub is not None else "other")
+
+
+def setup_channel(engine: Engine, channel: str, identities, chaincodes, committed_txids=(), config=None, msps=()):
+    """identities: iterable of (serialized, Identity) or (serialized, mspid, pubkey64 | None,
+    valid, id_digest).  chaincodes: ns -> ApplicationPolicy bytes, or a dict {policy,
+    plugin="vscc", collections=None | {name: EP bytes | None}, sbe=False}.  config: the channel's
+    common.Config bytes (channel policies, MSPs, application orgs); msps: further MSP ids."""
     engine.channel_init(channel)
-    identities = list(identities)
+    if config is not None:
+        engine.channel_config(config)
+    for m in msps:
+        engine.msp_declare(m)
+    identities = [_as_identity(e) for e in identities]
     # all public keys first, in one fgv_keys_register call: their comb tables are then built by
     # batched k_keytab launches (up to KT_BUILD_KEYS keys each) instead of one launch per key,
-    # and every msp_add_identity below finds its key cached (same slots, first-seen order)
-    pubs = [pub for _ser, _mspid, pub, _valid, _dig in identities if pub is not None]
+    # and every registration below finds its key cached (same slots, first-seen order)
+    pubs = [i.pub for _s, i in identities if i.key == "p256" and i.pub is not None]
     if pubs:
         engine.keys_register(np.frombuffer(b"".join(bytes(p) for p in pubs), dtype=np.uint8))
-    for ser, _mspid, pub, valid, dig in identities:
-        engine.msp_add_identity(ser, pub, valid, dig)
-    for ns, pol in chaincodes.items():
-        engine.chaincode_define(ns, pol)
+    for ser, i in identities:
+        engine.msp_register_identity(ser, i.key, i.pub, i.valid, i.id_digest, roles=i.roles,
+                                     hash_family=i.hash_family)
+    for ns, d in chaincodes.items():
+        if not isinstance(d, dict):
+            engine.chaincode_define(ns, d)
+            continue
+        colls = d.get("collections")
+        flags = (CC_COLLECTIONS_KNOWN if colls is not None else 0) | (CC_KEY_LEVEL_EP if d.get("sbe") else 0)
+        engine.chaincode_define(ns, d.get("policy") or b"", plugin=d.get("plugin", "vscc"), flags=flags)
+        for name, ep in (colls or {}).items():
+            engine.collection_define(ns, name, ep or b"")
     if committed_txids:
         engine.ledger_add_txids(list(committed_txids))
 

@@ -113,21 +113,67 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *ctx, const uint8_t *d_msg_buf, const uint6
 /* Channel model the block validator runs against (what the peer's channel resources give
  * the reference validator):
  *   fgv_channel_init      -- channel name (chdr.ChannelId of valid txs; validator.go:155-158)
- *   fgv_msp_add_identity  -- one MSP identity, keyed by its exact SerializedIdentity
- *                            (mspid, id_bytes) pair (msp/mspmgrimpl.go:75-100): P-256 public
- *                            key X||Y (NULL if the key is not P-256 -> Verify always fails),
- *                            Validate() result, and SHA-256 of the certificate (identity Id,
- *                            used for de-duplication, common/policies/policy.go:375).
- *                            The Go shim adds identities as its MSP cache deserializes them.
- *   fgv_chaincode_define  -- ValidationInfo of a namespace: ApplicationPolicy bytes
- *                            (plugin "vscc"; dispatcher.go:237-275)
- *   fgv_ledger_add_txids  -- txids already in the block store (TxIDExists, kv_ledger.go:496) */
+ *   fgv_channel_config    -- the channel's common.Config (configtx.pb.go Config: sequence +
+ *                            channel_group): channel policies for channel_config_policy_reference
+ *                            endorsement policies (core/policy/application.go:139-159; SIGNATURE
+ *                            and IMPLICIT_META, common/policies/implicitmeta.go:27-104), the MSPs
+ *                            of the channel and their SignatureHashFamily, the application orgs
+ *                            (implicit-collection policies, deployedcc_infoprovider.go:270-305)
+ *   fgv_msp_declare       -- an MSP of the channel without a config (identities of a declared
+ *                            MSP that were never registered -> FGV_EUNSUPPORTED, not "unknown")
+ *   fgv_msp_register_identity -- one MSP identity keyed by its exact SerializedIdentity
+ *                            (mspid, id_bytes) pair, as the Go shim's MSP cache deserializes it
+ *                            (msp/mspmgrimpl.go:75-100, msp/cache/cache.go:65-83)
+ *   fgv_chaincode_define2 -- ValidationInfo of a namespace (dispatcher.go:237-275): plugin name
+ *                            and ApplicationPolicy bytes; an empty plugin or policy means
+ *                            INVALID_CHAINCODE, a plugin other than "vscc" FGV_EUNSUPPORTED
+ *   fgv_collection_define -- a collection of a chaincode definition and its endorsement policy
+ *                            (StaticCollectionConfig.endorsement_policy; len 0 = none: the
+ *                            chaincode EP applies).  A defined chaincode whose collections were
+ *                            never declared (no call, no FGV_CC_COLLECTIONS_KNOWN) makes hashed
+ *                            writes to it FGV_EUNSUPPORTED; with them known, an undefined
+ *                            collection is an ENDORSEMENT_POLICY_FAILURE (v20.go:84-100)
+ *   fgv_ledger_add_txids  -- txids already in the block store (TxIDExists, kv_ledger.go:496)
+ * Identities a transaction names that the engine cannot judge exactly -- an unregistered
+ * certificate of a channel MSP, a P-384 key, a SHA3 MSP, a role principal for an identity
+ * registered without role bits -- make the batch FGV_EUNSUPPORTED (the reference decides). */
+#define FGV_KEY_P256 1             /* verified on the GPU                                      */
+#define FGV_KEY_P384 2             /* bccsp verifies it: outside the engine                    */
+#define FGV_KEY_OTHER 3            /* RSA etc.: Verify fails                        */
+#define FGV_KEY_UNDESERIALIZABLE 4 /* DeserializeIdentity fails (Ed25519 under Fabric 2.x, F4)  */
+#define FGV_HASH_SHA2 0
+#define FGV_HASH_SHA3 1
+#define FGV_ROLES_UNKNOWN 0x80000000u /* roles: only MEMBER (= valid) is known                 */
+typedef struct fgv_identity_info {
+  uint32_t key_type;      /* FGV_KEY_*                                                        */
+  uint32_t hash_family;   /* the MSP's SignatureHashFamily: FGV_HASH_SHA2 / FGV_HASH_SHA3      */
+  uint32_t valid;         /* msp.Validate(id) == nil                                          */
+  uint32_t roles;         /* bit r <=> msp.SatisfiesPrincipal(id, ROLE{its mspid, r}) == nil,
+                             r = MSPRole_MSPRoleType (MEMBER 0, ADMIN 1, CLIENT 2, PEER 3,
+                             ORDERER 4): NodeOU classification / admin list (mspimpl.go:331-376,
+                             477-660); or FGV_ROLES_UNKNOWN                                    */
+  uint8_t pubkey[64];     /* P-256 X || Y (FGV_KEY_P256)                                      */
+  uint8_t id_digest[32];  /* identity Id: SHA-256 of the certificate (common/policies/policy.go:375) */
+} fgv_identity_info;
+#define FGV_CC_COLLECTIONS_KNOWN 1u /* the definition's collections are all declared           */
+#define FGV_CC_KEY_LEVEL_EP 2u      /* the state holds key-level endorsement (SBE) metadata for
+                                       this namespace: its writes are FGV_EUNSUPPORTED           */
 int fgv_channel_init(fgv_ctx *ctx, const char *channel_name);
+int fgv_channel_config(fgv_ctx *ctx, const uint8_t *config, size_t len);
+int fgv_msp_declare(fgv_ctx *ctx, const char *mspid);
+int fgv_msp_register_identity(fgv_ctx *ctx, const uint8_t *serialized, size_t len, const fgv_identity_info *info);
+int fgv_chaincode_define2(fgv_ctx *ctx, const char *ns, const char *plugin, const uint8_t *policy, size_t len,
+                          uint32_t flags);
+int fgv_collection_define(fgv_ctx *ctx, const char *ns, const char *collection, const uint8_t *policy,
+                          size_t len);
+int fgv_ledger_add_txids(fgv_ctx *ctx, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
+                         size_t n);
+/* Round-1 forms: fgv_msp_add_identity = register with FGV_KEY_P256 (pubkey64 != NULL) or
+ * FGV_KEY_OTHER, SHA2, FGV_ROLES_UNKNOWN; fgv_chaincode_define = fgv_chaincode_define2 with
+ * plugin "vscc", flags 0. */
 int fgv_msp_add_identity(fgv_ctx *ctx, const uint8_t *serialized, size_t len, const uint8_t *pubkey64,
                          int valid, const uint8_t *id_digest32);
 int fgv_chaincode_define(fgv_ctx *ctx, const char *ns, const uint8_t *policy, size_t len);
-int fgv_ledger_add_txids(fgv_ctx *ctx, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
-                         size_t n);
 
 /* TxValidator.Validate (core/committer/txvalidator/v20/validator.go:180-265) for `nblocks`
  * consecutive blocks (marshalled common.Block).  Writes one TxValidationCode byte per

@@ -126,11 +126,41 @@ S = {
     "NOutOf": {1: ("n", "int32"), 2: ("rules", "rep msg:SignaturePolicy")},
     "MSPPrincipal": {1: ("principal_classification", "enum"), 2: ("principal", "bytes")},
     "MSPRole": {1: ("msp_identifier", "string"), 2: ("role", "enum")},
+    # channel configuration (common/configtx.pb.go, common/policies.pb.go, msp/msp_config.pb.go);
+    # map<string, V> fields are repeated {key = 1, value = 2} entries
+    "Config": {1: ("sequence", "uint64"), 2: ("channel_group", "msg:ConfigGroup")},
+    "ConfigEnvelope": {1: ("config", "msg:Config"), 2: ("last_update", "bytes")},
+    "ConfigGroup": {1: ("version", "uint64"), 2: ("groups", "rep msg:ConfigGroupEntry"),
+                    3: ("values", "rep msg:ConfigValueEntry"), 4: ("policies", "rep msg:ConfigPolicyEntry"),
+                    5: ("mod_policy", "string")},
+    "ConfigGroupEntry": {1: ("key", "string"), 2: ("value", "msg:ConfigGroup")},
+    "ConfigValueEntry": {1: ("key", "string"), 2: ("value", "msg:ConfigValue")},
+    "ConfigPolicyEntry": {1: ("key", "string"), 2: ("value", "msg:ConfigPolicy")},
+    "ConfigValue": {1: ("version", "uint64"), 2: ("value", "bytes"), 3: ("mod_policy", "string")},
+    "ConfigPolicy": {1: ("version", "uint64"), 2: ("policy", "msg:Policy"), 3: ("mod_policy", "string")},
+    "Policy": {1: ("type", "int32"), 2: ("value", "bytes")},
+    "ImplicitMetaPolicy": {1: ("sub_policy", "string"), 2: ("rule", "enum")},
+    "MSPConfig": {1: ("type", "int32"), 2: ("config", "bytes")},
+    "FabricMSPConfig": {1: ("name", "string"), 2: ("root_certs", "rep bytes"), 3: ("intermediate_certs", "rep bytes"),
+                        4: ("admins", "rep bytes"), 5: ("revocation_list", "rep bytes"),
+                        8: ("crypto_config", "msg:FabricCryptoConfig"), 11: ("fabric_node_ous", "msg:FabricNodeOUs")},
+    "FabricCryptoConfig": {1: ("signature_hash_family", "string"), 2: ("identity_identifier_hash_function", "string")},
+    "FabricNodeOUs": {1: ("enable", "bool"), 2: ("client_ou_identifier", "msg:FabricOUIdentifier"),
+                      3: ("peer_ou_identifier", "msg:FabricOUIdentifier"), 4: ("admin_ou_identifier", "msg:FabricOUIdentifier"),
+                      5: ("orderer_ou_identifier", "msg:FabricOUIdentifier")},
+    "FabricOUIdentifier": {1: ("certificate", "bytes"), 2: ("organizational_unit_identifier", "string")},
+    # lifecycle state (peer/lifecycle/db.pb.go, chaincode_definition.pb.go, peer/collection.pb.go)
+    "StateData": {1: ("Int64", "int64"), 2: ("Bytes", "bytes"), 3: ("String", "string")},
+    "ChaincodeValidationInfo": {1: ("validation_plugin", "string"), 2: ("validation_parameter", "bytes")},
+    "CollectionConfigPackage": {1: ("config", "rep msg:CollectionConfig")},
+    "CollectionConfig": {1: ("static_collection_config", "msg:StaticCollectionConfig")},
+    "StaticCollectionConfig": {1: ("name", "string"), 8: ("endorsement_policy", "bytes")},
 }
 ONEOF = {
     "RangeQueryInfo": ("raw_reads", "reads_merkle_hashes"),
     "ApplicationPolicy": ("signature_policy", "channel_config_policy_reference"),
     "SignaturePolicy": ("signed_by", "n_out_of"),
+    "StateData": ("Int64", "Bytes", "String"),
 }
 # oneof members keep presence even for zero values (a "set" oneof field is present)
 _ONEOF_MEMBERS = {f for v in ONEOF.values() for f in v}

@@ -43,43 +43,148 @@ class Unsupported(Exception):
     """Input outside the modelled environment (config tx, channel-reference policy, ...)."""
 
 
+KEY_P256, KEY_P384, KEY_OTHER, KEY_UNDESERIALIZABLE = "p256", "p384", "other", "undeserializable"
+IMPLICIT_PREFIX = "_implicit_org_"  # core/chaincode/implicitcollection/name.go:24-29
+
+
 class Ident:
-    def __init__(self, mspid, pub, valid, id_digest):
+    """An MSP identity as the peer's MSP layer knows it.
+    key: KEY_P256 (verified on the GPU), KEY_P384 (bccsp verifies it: outside the engine ->
+    Unsupported when a verify is needed), KEY_OTHER (RSA...: Verify fails),
+    KEY_UNDESERIALIZABLE (e.g. Ed25519 under Fabric 2.x: DeserializeIdentity fails, F4).
+    hash: the MSP's SignatureHashFamily (identities.go:219-227); SHA3 -> Unsupported.
+    roles: bit r <=> msp.SatisfiesPrincipal(id, ROLE{mspid, r}) (MEMBER 0, ADMIN 1, CLIENT 2,
+    PEER 3, ORDERER 4; msp/mspimpl.go:331-376, 477-660); None = unknown (legacy registration)."""
+
+    def __init__(self, mspid, pub, valid, id_digest, key=KEY_P256, hash_family="SHA2", roles=None):
         self.mspid, self.pub, self.valid, self.id_digest = mspid, pub, valid, id_digest
+        self.key, self.hash_family, self.roles = key, hash_family, roles
 
     @property
     def dedup_key(self):  # identity.GetIdentifier().Mspid + .Id
         return self.mspid + self.id_digest.hex()
 
 
+class ChannelPolicy:
+    """A policy of the channel configuration (common/policies/policy.go ManagerImpl)."""
+    REJECT, SIGNATURE, IMPLICIT_META, UNSUPPORTED = range(4)
+
+    def __init__(self, kind, spe=None, threshold=0, subs=()):
+        self.kind, self.spe, self.threshold, self.subs = kind, spe, threshold, list(subs)
+
+
+def _config_policies(group, path, out, msps, app_orgs, is_app=False):
+    """Walk a ConfigGroup: flattened policies {"Application/org1/Endorsement": ChannelPolicy}
+    (ManagerImpl folds sub-manager policies into its map under "group/name", policy.go), MSPs
+    {name: FabricMSPConfig}, application orgs {mspid: org group name}."""
+    children = [(e.get("key", ""), e.get("value") or {}) for e in group.get("groups", [])]
+    for e in group.get("values", []):
+        if e.get("key") == "MSP":
+            mc = decode("MSPConfig", (e.get("value") or {}).get("value"))
+            if mc.get("type", 0) != 0:
+                raise Unsupported("non-X.509 MSP")
+            fc = decode("FabricMSPConfig", mc.get("config"))
+            msps[fc.get("name", "")] = fc
+            if is_app:
+                app_orgs[fc.get("name", "")] = path.rsplit("/", 1)[-1]
+    for e in group.get("policies", []):
+        name = e.get("key", "")
+        pol = (e.get("value") or {}).get("policy") or {}
+        t = pol.get("type", 0)
+        key = (path + "/" + name) if path else name
+        if t == 1:  # SIGNATURE: cauthdsl.NewPolicy (policy.go): version 0 only
+            spe = decode("SignaturePolicyEnvelope", pol.get("value"))
+            out[key] = ChannelPolicy(ChannelPolicy.SIGNATURE if spe.get("version", 0) == 0 else ChannelPolicy.UNSUPPORTED, spe=spe)
+        elif t == 3:  # IMPLICIT_META (implicitmeta.go:27-60): one sub-policy per child group
+            im = decode("ImplicitMetaPolicy", pol.get("value"))
+            rule, sub = im.get("rule", 0), im.get("sub_policy", "")
+            subs = [((path + "/" + c + "/" + sub) if path else (c + "/" + sub)) for c, _ in children]
+            n = len(subs)
+            thr = 1 if rule == 0 else n if rule == 1 else n // 2 + 1 if rule == 2 else 0
+            out[key] = ChannelPolicy(ChannelPolicy.IMPLICIT_META, threshold=0 if n == 0 else thr, subs=subs)
+        else:
+            out[key] = ChannelPolicy(ChannelPolicy.UNSUPPORTED)
+    for c, g in children:
+        _config_policies(g, (path + "/" + c) if path else c, out, msps, app_orgs, is_app=(path == "Application"))
+
+
 class ChannelModel:
-    def __init__(self, channel, identities, chaincodes, committed_txids=()):
-        """identities: iterable of (serialized, mspid, pub64, valid, id_digest)."""
+    def __init__(self, channel, identities, chaincodes, committed_txids=(), config=None, msps=()):
+        """identities: iterable of (serialized, mspid, pub64, valid, id_digest) or
+        (serialized, Ident).  chaincodes: ns -> ApplicationPolicy bytes, or a dict
+        {policy, plugin="vscc", collections=None | {name: EP bytes | None}, sbe=False}
+        (collections None: not known -> hashed writes Unsupported).  config: common.Config bytes
+        (channel policies, MSPs, application orgs).  msps: further MSP ids of the channel."""
         self.channel = channel
         self.msp = {}
-        self.mspids = set()
-        for ser, mspid, pub, valid, dig in identities:
+        self.mspids = set(msps)
+        for entry in identities:
+            if len(entry) == 2:
+                ser, o = entry  # any object with the Ident fields (e.g. fabric_amd.txvalidator.Identity)
+                ident = Ident(o.mspid, o.pub, o.valid, o.id_digest, key=o.key, hash_family=o.hash_family, roles=o.roles)
+            else:
+                ser, mspid, pub, valid, dig = entry
+                ident = Ident(mspid, pub, valid, dig, key=KEY_P256 if pub else KEY_OTHER)
             sid = decode("SerializedIdentity", ser)
-            self.msp[(sid.get("mspid", ""), sid.get("id_bytes") or b"")] = Ident(mspid, pub, valid, dig)
-            self.mspids.add(mspid)
-        self.chaincodes = dict(chaincodes)
+            self.msp[(sid.get("mspid", ""), sid.get("id_bytes") or b"")] = ident
+            self.mspids.add(ident.mspid)
+        self.chaincodes = {ns: (d if isinstance(d, dict) else dict(policy=d)) for ns, d in dict(chaincodes).items()}
         self.committed = set(committed_txids)
         self.verify_calls = 0
+        self.policies, self.config_msps, self.app_orgs = None, {}, {}
+        self.config_unsupported = False
+        if config is not None:
+            cfg = decode("Config", config)
+            self.policies = {}
+            _config_policies(cfg.get("channel_group") or {}, "", self.policies, self.config_msps, self.app_orgs)
+            self.mspids |= set(self.config_msps)
+            for name, fc in self.config_msps.items():
+                fam = (fc.get("crypto_config") or {}).get("signature_hash_family", "")
+                if fam not in ("SHA2", "SHA3"):
+                    self.config_unsupported = True  # the peer would not have set this MSP up
+                if fam == "SHA3":  # the MSP's identities hash with SHA3 (identities.go:219-227)
+                    for ident in self.msp.values():
+                        if ident.mspid == name:
+                            ident.hash_family = "SHA3"
 
     def deserialize(self, ser):
-        """mspManagerImpl.DeserializeIdentity (msp/mspmgrimpl.go:75-100) over the registry."""
+        """mspManagerImpl.DeserializeIdentity (msp/mspmgrimpl.go:75-100) over the registry.  A
+        certificate of a channel MSP that was never registered cannot be judged (x509 parse +
+        Validate happen in the MSP layer) -> Unsupported; an unknown MSP -> deserialize error."""
         try:
             sid = decode("SerializedIdentity", ser)
         except DecodeError:
             return None
-        return self.msp.get((sid.get("mspid", ""), sid.get("id_bytes") or b""))
+        key = (sid.get("mspid", ""), sid.get("id_bytes") or b"")
+        ident = self.msp.get(key)
+        if ident is None:
+            if key[0] in self.mspids:
+                raise Unsupported("unregistered identity of channel MSP %s" % key[0])
+            return None
+        if ident.key == KEY_UNDESERIALIZABLE:
+            return None
+        return ident
 
     def verify(self, ident, msg, sig):
         """identity.Verify: 0 iff valid (msp/identities.go:170-199)."""
         self.verify_calls += 1
+        if ident.key == KEY_OTHER:
+            return 5
+        if ident.key != KEY_P256 or ident.hash_family != "SHA2":
+            raise Unsupported("P-384 key or SHA3 hash family")
         if not sig:
             return 6
         return verify_der(ident.pub[:32], ident.pub[32:], sig, sha256(msg))
+
+    def channel_policy(self, ref):
+        """ChannelPolicyReferenceProviderImpl -> ManagerImpl.GetPolicy (policy.go:330-358)"""
+        if self.policies is None or self.config_unsupported:
+            raise Unsupported("channel config policy reference without a (usable) channel config")
+        if ref.startswith("/"):
+            if not ref.startswith("/Channel/"):
+                return ChannelPolicy(ChannelPolicy.REJECT)
+            ref = ref[len("/Channel/"):]
+        return self.policies.get(ref, ChannelPolicy(ChannelPolicy.REJECT)) if ref else ChannelPolicy(ChannelPolicy.REJECT)
 
 
 # ----------------------------------------------------------------- policies
@@ -127,18 +232,22 @@ def _principal(p):
     try:
         role = decode("MSPRole", p.get("principal") or b"")
     except DecodeError:
-        return ("bad", None)
-    if role.get("role", 0) != 0:
-        raise Unsupported("MSP role %d needs NodeOU data" % role.get("role", 0))
-    return ("member", role.get("msp_identifier", ""))
+        return ("bad", None, 0)
+    return ("role", role.get("msp_identifier", ""), role.get("role", 0))
 
 
 def _satisfies(ident, pr):
-    """bccspmsp.satisfiesPrincipalInternal* for ROLE/MEMBER (msp/mspimpl.go:477-501)."""
-    kind, mspid = pr
-    if kind != "member":
+    """bccspmsp.satisfiesPrincipalInternalV142 / V13 / PreV13 for ROLE principals
+    (msp/mspimpl.go:477-660): same MSP, then MEMBER = Validate, other roles from the identity's
+    role bits (NodeOU classification / admin list, computed by the MSP layer)."""
+    kind, mspid, role = pr
+    if kind != "role" or ident.mspid != mspid:
         return False
-    return ident.mspid == mspid and ident.valid
+    if role == 0:
+        return ident.valid
+    if ident.roles is None:
+        raise Unsupported("role principal %d needs the identity's role bits" % role)
+    return bool((ident.roles >> role) & 1) if 0 <= role < 32 else False
 
 
 def signature_set_to_valid_identities(model, sigset):
@@ -157,6 +266,34 @@ def signature_set_to_valid_identities(model, sigset):
     return out
 
 
+def _eval_spe(model, spe, sigset):
+    """cauthdsl policy.EvaluateSignedData (common/cauthdsl/policy.go:86-108)"""
+    principals = [_principal(p) for p in spe.get("identities", [])]
+    try:
+        ev = _compile(spe.get("rule"), principals)
+    except ValueError:
+        return False
+    ids = signature_set_to_valid_identities(model, sigset)
+    # a role principal needs every candidate's role bits (the engine checks this up front)
+    if any(k == "role" and r != 0 for k, _, r in principals) and any(i.roles is None for i in ids):
+        raise Unsupported("role principal needs the identities' role bits")
+    return ev(ids, [False] * len(ids))
+
+
+def _eval_channel_policy(model, pol, sigset, depth=0):
+    """ImplicitMetaPolicy.EvaluateSignedData (implicitmeta.go:69-104): every sub-policy is
+    evaluated (the reference stops early in Go map order; outcomes are pure, so the count decides)"""
+    if pol.kind == ChannelPolicy.REJECT:
+        return False
+    if pol.kind == ChannelPolicy.UNSUPPORTED or (pol.kind == ChannelPolicy.IMPLICIT_META and depth > 0):
+        raise Unsupported("channel policy outside the model")
+    if pol.kind == ChannelPolicy.SIGNATURE:
+        return _eval_spe(model, pol.spe, sigset)
+    ok = sum(1 for sub in pol.subs
+             if _eval_channel_policy(model, model.policies.get(sub, ChannelPolicy(ChannelPolicy.REJECT)), sigset, depth + 1))
+    return ok >= pol.threshold
+
+
 def evaluate_policy(model, policy_bytes, sigset):
     """ApplicationPolicyEvaluator.Evaluate (core/policy/application.go:148-163).  True iff ok."""
     try:
@@ -164,16 +301,58 @@ def evaluate_policy(model, policy_bytes, sigset):
     except DecodeError:
         return False
     if "signature_policy" in ap:
-        spe = ap["signature_policy"]
-        principals = [_principal(p) for p in spe.get("identities", [])]
-        try:
-            ev = _compile(spe.get("rule"), principals)
-        except ValueError:
-            return False
-        ids = signature_set_to_valid_identities(model, sigset)
-        return ev(ids, [False] * len(ids))
+        return _eval_spe(model, ap["signature_policy"], sigset)
     if "channel_config_policy_reference" in ap:
-        raise Unsupported("channel config policy reference")
+        return _eval_channel_policy(model, model.channel_policy(ap["channel_config_policy_reference"]), sigset)
+    return False
+
+
+def signed_by_any_member(mspid):
+    """policydsl.SignedByAnyMember([mspid]) as ApplicationPolicy bytes"""
+    def fb(num, b):
+        return _pv(num << 3 | 2) + _pv(len(b)) + b
+    role = fb(1, mspid.encode())  # MSPRole{msp_identifier, role MEMBER}
+    spe = fb(2, fb(2, b"\x08\x01" + fb(2, b"\x08\x00"))) + fb(3, fb(2, role))
+    return fb(1, spe)
+
+
+def _pv(v):
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+def collection_policy(model, ns, coll):
+    """ValidatorCommitter.CollectionValidationInfo (core/chaincode/lifecycle/
+    deployedcc_infoprovider.go:343-382) -> ("app", bytes) | ("cc",) | ("reject",)"""
+    if coll.startswith(IMPLICIT_PREFIX):
+        mspid = coll[len(IMPLICIT_PREFIX):]
+        if model.policies is None or model.config_unsupported or mspid not in model.app_orgs:
+            raise Unsupported("implicit collection of an org outside the channel config")
+        path = "Application/%s/Endorsement" % model.app_orgs[mspid]  # :277-300
+        if path in model.policies:
+            return ("ref", path)
+        return ("app", signed_by_any_member(mspid))
+    cc = model.chaincodes[ns]
+    colls = cc.get("collections")
+    if colls is None:
+        raise Unsupported("collections of %s not known" % ns)
+    if coll not in colls:
+        return ("reject",)  # "no such collection" -> validation error -> policy failure
+    return ("app", colls[coll]) if colls[coll] else ("cc",)
+
+
+def _run(model, pol, cc_policy, sigset):
+    if pol[0] == "cc":
+        return evaluate_policy(model, cc_policy, sigset)
+    if pol[0] == "app":
+        return evaluate_policy(model, pol[1], sigset)
+    if pol[0] == "ref":
+        return _eval_channel_policy(model, model.policies[pol[1]], sigset)
     return False
 
 
@@ -299,7 +478,7 @@ def get_action_from_envelope(env_bytes):
     return decode("ChaincodeAction", prp["extension"]), cap
 
 
-def vscc_validate(model, env_bytes, ns, policy):
+def vscc_validate(model, env_bytes, ns):
     """builtin v20 Validate (validation_logic.go:185-217) -> True iff endorsement policy holds."""
     try:
         env = decode("Envelope", env_bytes)
@@ -325,16 +504,28 @@ def vscc_validate(model, env_bytes, ns, policy):
         rw = parse_rwset(cca.get("results"))
     except DecodeError:
         return False
+    cc = model.chaincodes[ns]
+    if cc.get("plugin", "vscc") != "vscc" or cc.get("sbe"):
+        raise Unsupported("validation plugin other than the builtin vscc / key-level endorsement")
+    # statebased/validator_keylevel.go:173-233 (no key-level validation parameters in the
+    # modelled state): each public write checks the chaincode EP, each collection with hashed
+    # writes its collection EP (or the chaincode EP), and a namespace with neither checks the
+    # chaincode EP (CheckCCEPIfNoEPChecked).  Outcomes are pure, so the set of policies decides.
+    pols = []
     for nsrw in rw:
         if nsrw["namespace"] != ns:
             continue
-        if nsrw["kv"].get("metadata_writes") or any(c["hashed"].get("metadata_writes") or c["hashed"].get("hashed_writes")
-                                                   for c in nsrw["coll"]):
-            raise Unsupported("key-level / collection endorsement policies")
-    # without key-level validation parameters every write checks the chaincode EP once
-    # (CheckCCEPIfNotChecked), and a namespace without writes checks it via
-    # CheckCCEPIfNoEPChecked: one evaluation either way.
-    return evaluate_policy(model, policy, sigset)
+        if nsrw["kv"].get("metadata_writes") or any(c["hashed"].get("metadata_writes") for c in nsrw["coll"]):
+            raise Unsupported("metadata writes (key-level endorsement)")
+        if nsrw["kv"].get("writes"):
+            pols.append(("cc",))
+        for c in nsrw["coll"]:
+            if c["hashed"].get("hashed_writes"):
+                pols.append(collection_policy(model, ns, c["name"]))
+    if not pols:
+        pols = [("cc",)]
+    results = [_run(model, p, cc["policy"], sigset) for p in pols]
+    return all(results)
 
 
 def dispatch(model, payload, env_bytes):
@@ -376,16 +567,15 @@ def dispatch(model, payload, env_bytes):
     # The reference iterates a Go map (random order).  Results only differ in the
     # reported code when namespaces fail with DIFFERENT codes; we report the first in
     # sorted order and flag multi-namespace disagreement as unsupported.
-    for nsrw in rw:
-        if nsrw["namespace"] in wr and (nsrw["kv"].get("metadata_writes") or any(
-                c["hashed"].get("metadata_writes") or c["hashed"].get("hashed_writes") for c in nsrw["coll"])):
-            raise Unsupported("key-level / collection endorsement policies")
     codes = set()
     for ns in sorted(wr):
-        if ns not in model.chaincodes:
+        cc = model.chaincodes.get(ns)
+        # getCDataForCC (dispatcher.go:237-264): undefined chaincode, empty plugin or empty
+        # validation parameter -> INVALID_CHAINCODE
+        if cc is None or not cc.get("policy") or cc.get("plugin", "vscc") == "":
             codes.add(INVALID_CHAINCODE)
             continue
-        if not vscc_validate(model, env_bytes, ns, model.chaincodes[ns]):
+        if not vscc_validate(model, env_bytes, ns):
             codes.add(ENDORSEMENT_POLICY_FAILURE)
     if len(codes) > 1:
         raise Unsupported("namespaces fail with different codes (map-order dependent)")

@@ -86,3 +86,64 @@ def test_engine_commit_hash_chain(name):
         h = _lib.commit_hash(b["block"], b["flags"], b["number"], prev)
         assert h.hex() == b["commit_hash"], b["number"]
         prev = h
+
+
+def test_committer_replay_v20():
+    """The restated committer (oracle/v20.py) on the reference's v2.0 network blocks: creator
+    signatures of admins / clients, single-org approvals validated against implicit-collection
+    policies (/Channel/Application/orgN/Endorsement = OR('OrgN.peer')), 3-org commits against
+    /Channel/Application/LifecycleEndorsement (ImplicitMeta MAJORITY), marbles-private
+    collection writes -> every stored flag (VALID) reproduced."""
+    from oracle import v20
+    from tests.sample_channel import v20_channel
+    blocks, config, idents, defs = v20_channel()
+    n = 0
+    for b in blocks:
+        if b["number"] < 5:
+            continue
+        model = v20.ChannelModel("testchannel", idents, defs[b["number"]], config=config)
+        assert v20.validate_block(model, b["block"]) == b["flags"], b["number"]
+        n += 1
+    assert n == 15
+
+
+def test_committer_v20_derived_negatives():
+    """Perturbing the MODEL (not the signed blocks) flips outcomes the way the reference's rules
+    say: peers without the PEER role -> approvals and commits fail their org / MAJORITY
+    policies (10); a marbles-private definition without collectionMarbles -> 10 ("no such
+    collection"); unknown collections / an unregistered channel identity / a P-384 creator ->
+    Unsupported (never a guess)."""
+    import copy
+
+    import pytest
+
+    from oracle import v20
+    from tests.sample_channel import v20_channel
+    blocks, config, idents, defs = v20_channel()
+    by_num = {b["number"]: b for b in blocks}
+
+    def run(num, idents_=idents, defs_=None):
+        model = v20.ChannelModel("testchannel", idents_, defs_ or defs[num], config=config)
+        out = v20.validate_block(model, by_num[num]["block"])
+        return out, model.verify_calls
+
+    assert run(8) == ([0], 10)  # creator + 3 endorsements x 3 sub-policies (each re-verifies, policy.go:363-395)
+    no_peer = [(s, v20.Ident(i.mspid, i.pub, i.valid, i.id_digest, roles=i.roles & ~(1 << 3))) for s, i in idents]
+    assert run(5, no_peer)[0] == [10] and run(8, no_peer)[0] == [10]
+    one_peer = [(s, v20.Ident(i.mspid, i.pub, i.valid, i.id_digest,
+                              roles=i.roles if i.mspid == "Org1MSP" else i.roles & ~(1 << 3))) for s, i in idents]
+    assert run(5, one_peer)[0] == [0]   # Org1's implicit collection: OR('Org1MSP.peer')
+    assert run(8, one_peer)[0] == [10]  # LifecycleEndorsement: MAJORITY of 3 orgs
+    d = copy.deepcopy(defs[13])
+    del d["marblesp"]["collections"]["collectionMarbles"]
+    assert run(13, defs_=d)[0] == [10]
+    d["marblesp"]["collections"] = None
+    with pytest.raises(v20.Unsupported):
+        run(13, defs_=d)
+    from tests.sample_channel import tx_identities
+    creator13 = tx_identities(decode("Block", by_num[13]["block"])["data"]["data"][0])[0]
+    with pytest.raises(v20.Unsupported):  # a known MSP's certificate the engine was never given
+        run(13, idents_=[(s, i) for s, i in idents if s != creator13])
+    p384 = [(s, v20.Ident(i.mspid, i.pub, i.valid, i.id_digest, key=v20.KEY_P384, roles=i.roles)) for s, i in idents]
+    with pytest.raises(v20.Unsupported):
+        run(5, p384)
