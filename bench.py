@@ -1,19 +1,27 @@
 """bench.py -- MI355X block-validation engine for Hyperledger Fabric's committer.
 
-python bench.py --gpus N --steps K --warmup W [--workload block|sig]
+python bench.py --gpus N --steps K --warmup W [--workload block|c5|sig|mvcc]
 
 block (default; BASELINE configs[1], C2 shape): 500-tx endorser blocks, 2-of-3 endorsement
   policy (OutOf(2, Org1..3.member)), 60 % of txs with 2 endorsements / 40 % with 3, 4 reads +
   4 writes of 200 B values, 100 client identities, injected faults (2 % bad creator sig, 2 %
   one bad endorsement of 3, 2 % policy unsatisfied, 0.5 % duplicate txid).  Weak scaling:
-  every GPU owns --blocks-per-gpu blocks' worth of transactions; the batch of N x B blocks is
-  resident in every GPU's HBM, each rank validates its transaction-index shard of every block
-  (fgv_validate_shard: host parse + GPU SHA-256 + ECDSA-P256 + policy fold), the ranks
-  all-gather their 68-byte per-tx records over RCCL and finalize TxValidationFlags.
-  value = validated tx/s over all ranks (max-over-ranks wall time of the timed steps).
+  every GPU owns --blocks-per-gpu blocks per step; a step is one committer pass over the
+  world x B blocks: each rank validates its own blocks (fgv_validate_shard_dev_next: device
+  parse + SHA-256 + ECDSA-P256 + policy fold), the ranks all-gather their 68-byte per-tx
+  records over RCCL and finalize TxValidationFlags.  --batches distinct batches (default 6,
+  ~366 MB per GPU, more than the 256 MiB Infinity Cache) are rotated through the timed loop.
+  value = validated tx/s over all ranks with the blocks resident in HBM (max-over-ranks wall
+  time of the timed steps).  Beside it: pcie_inclusive (the same rotation from page-locked
+  host memory, each batch's H2D overlapped with the previous batch's validation),
+  latency_1block_ms, per-kernel device times (kernel_ms), the roofline of the dominant kernel,
+  and cpu_baseline = the restated full v20 validator (oracle/) on this host's CPU share and on
+  one core, plus the identity.Verify-only bound.
 
+c5 (configs[4]): 20k-tx blocks, 5-of-8 policy, P-256 + Ed25519, + deliver-side integrity.
 sig (configs[3], C4 shape): 131,072 P-256 identity.Verify calls per GPU on 1.85 KB
   messages, inputs resident in HBM; value = verifies/s.
+mvcc (configs[2], C3): 10k-tx blocks against a 1M-key state DB, validated and committed.
 """
 import argparse
 import json
@@ -36,6 +44,9 @@ METRIC = "ECDSA-P256 verifies/sec + validated tx/sec per block at 1/2/4/8 MI355X
 PRODUCTS_POINT = 41 * (8 * 64 + 3 * 36) + 3 * 64
 # chip-wide v_mad_u64_u32 issue rate measured by tools/valu_peak.hip (profiles/round1_valu_peak.json)
 PEAK_MAD_PER_S = float(os.environ.get("FGV_PEAK_MAD", "3.106e13"))
+# 256 CU x 4 SIMD x 32 lanes x 2.4 GHz simple int32 VALU lane-ops
+PEAK_INT32_OPS = 78.6e12
+SHA_OPS_PER_COMPRESSION = 2.7e3
 
 
 def log(*a):
@@ -67,6 +78,26 @@ def roofline(n_verifies, point_ms, workload):
                 kernel="k_point28 (+ k_point hand-overs)",
                 kernel_avg_ms=round(point_ms, 4), per_launch_products=int(n_verifies * PRODUCTS_POINT),
                 work_unit="v_mad_u64_u32 (32x32->64 multiply-add) products of the comb algorithm")
+
+
+def block_roofline(kavg, pay_blocks, verifies, workload):
+    """roofline of the committer step: the kernel with the largest per-step device time
+    (fgv_last_kernel_times, HIP events on each kernel's own stream) -- k_bd_sha_payload at
+    C2 sizes: SHA-256 compressions x 2.7e3 int32 ops / its time vs the 78.6 T
+    int32 lane-op peak -- and k_point28 as the second entry."""
+    cands = {k: v for k, v in kavg.items() if k != "batch"}
+    dom = max(cands, key=cands.get) if cands else "k_bd_sha_payload"
+    t_pay = kavg.get("k_bd_sha_payload", 0.0) / 1e3
+    ach = pay_blocks * SHA_OPS_PER_COMPRESSION / t_pay / 1e12 if t_pay > 0 else 0.0
+    traffic, src = pmc_traffic(workload)
+    r = dict(bound="valu", achieved=round(ach, 3), peak=round(PEAK_INT32_OPS / 1e12, 1), unit="Tops/s",
+             frac=round(ach * 1e12 / PEAK_INT32_OPS, 4), traffic=traffic, traffic_source=src,
+             kernel="k_bd_sha_payload", dominant_kernel=dom, kernel_avg_ms=round(t_pay * 1e3, 4),
+             per_launch_compressions=int(pay_blocks),
+             work_unit="SHA-256 compressions x 2.7e3 simple int32 ops (SURVEY.md s8(d))")
+    r["second"] = roofline(verifies, kavg.get("k_point28", 0.0), workload)
+    r["second"]["kernel"] = "k_point28 (+ k_point hand-overs)"
+    return r
 
 
 def cpu_verify_rate(keymat, msgs, sigs, threads, target_s=12.0):
@@ -104,7 +135,63 @@ BLOCK_SPECS = {
 }
 
 
-def run_block(args, world, rank, local, dev):
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_share():
+    """host threads this rank may use: the affinity mask, capped by OMP_NUM_THREADS (16 on a
+    one-GPU lease, whose nproc shows the whole machine)"""
+    n = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
+
+
+_CPU_MODEL = None  # the forked full-validator workers' channel model
+
+
+def _oracle_block(blk):
+    from oracle import v20
+    t = time.perf_counter()
+    f = v20.validate_block(_CPU_MODEL, blk)
+    return len(f), time.perf_counter() - t
+
+
+def cpu_full_validator(net, blks, procs, target_s):
+    """The restated v20 committer (oracle/v20.py: protobuf walk, MSP lookup, OpenSSL P-256
+    identity.Verify through oracle/liboracle.so, policy evaluation, flag fold) on `procs`
+    forked worker processes, one block per task, until ~target_s of wall time.  Runs before
+    this process touches the GPU (fork)."""
+    import multiprocessing as mp
+    from oracle import v20
+    global _CPU_MODEL
+    _CPU_MODEL = v20.ChannelModel(net.channel, net.identities(), net.chaincodes)
+    if procs == 1:
+        done, t0 = 0, time.perf_counter()
+        i = 0
+        while time.perf_counter() - t0 < target_s:
+            done += _oracle_block(blks[i % len(blks)])[0]
+            i += 1
+        return done / (time.perf_counter() - t0), done, time.perf_counter() - t0, i
+    ctx = mp.get_context("fork")
+    with ctx.Pool(procs) as pool:
+        pool.map(int, range(procs))  # workers up
+        per = _oracle_block(blks[0])[1]  # seconds per block on one core (sizes the sample)
+        nblk = max(procs, int(round(target_s * procs / max(per, 1e-3) / procs)) * procs)
+        t0 = time.perf_counter()
+        res = pool.map(_oracle_block, [blks[i % len(blks)] for i in range(nblk)], chunksize=1)
+        el = time.perf_counter() - t0
+    done = sum(r[0] for r in res)
+    return done / el, done, el, nblk
+
+
+def run_block(args, world, rank, local, dev_fn):
     import threading
 
     from fabric_amd import _lib, shard, txvalidator
@@ -120,81 +207,94 @@ def run_block(args, world, rank, local, dev):
         dist.broadcast_object_list(obj, src=0)
         pems = obj[0]
     net = blocks.Network(pems=pems, **spec["net"])
-    B, T = args.blocks_per_gpu, args.tx_per_block
+    B, T, NB = args.blocks_per_gpu, args.tx_per_block, args.batches
     if args.workload == "c5":
-        B = args.c5_blocks_per_gpu
-        T = args.c5_tx_per_block
-    mine, prev = [], b"\x00" * 32
-    for i in range(B):  # each rank's blocks form a hash chain (numbers 1 + rank*B + i)
-        num = 1 + rank * B + i
-        blk, lab, envs = blocks.make_block(net, T, number=num, seed=7919 * rank + i, threads=8,
-                                           endorse_dist=spec["endorse"], prev_hash=prev)
-        mine.append((blk, lab))
-        prev = blocks.header_hash(num, prev, envs)
-    my_blocks = [m[0] for m in mine]
-    my_labels = [m[1] for m in mine]
-    # The batch is every rank's blocks in rank order.  With at least one block per rank the
-    # shard plan is block-granular (below): a rank needs only its own blocks' bytes -- the
-    # others' results arrive as all-gathered records -- so only the labels (for the parity
-    # check) are exchanged; the per-block transaction split needs every block everywhere.
-    plan_mode = "block" if B >= 1 else "tx"
+        B, T, NB = args.c5_blocks_per_gpu, args.c5_tx_per_block, args.c5_batches
+    # NB distinct batches per rank, rotated through the timed loop (their bytes together exceed
+    # the 256 MiB Infinity Cache at the default sizes); each rank's blocks of a batch form a
+    # hash chain numbered 1 + (k * world + rank) * B + i
+    mine = []
+    for k in range(NB):
+        prev, cur = b"\x00" * 32, []
+        for i in range(B):
+            num = 1 + (k * world + rank) * B + i
+            blk, lab, envs = blocks.make_block(net, T, number=num, seed=7919 * rank + 100003 * k + i, threads=8,
+                                               endorse_dist=spec["endorse"], prev_hash=prev)
+            cur.append((blk, lab))
+            prev = blocks.header_hash(num, prev, envs)
+        mine.append(cur)
+    my_blocks = [[m[0] for m in cur] for cur in mine]
+    log(f"[bench] rank {rank}: {NB} x {B} blocks x {T} tx ready in {time.time() - t0:.1f}s")
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_threads != 0:
+        # CPU baselines first: the full-validator workers are forked before any GPU use
+        procs = args.cpu_threads if args.cpu_threads > 0 else _cpu_share()
+        sample = my_blocks[0][:max(1, min(B, 2 * procs))]
+        full_n = cpu_full_validator(net, sample, procs, args.cpu_seconds)
+        full_1 = cpu_full_validator(net, sample[:2], 1, args.cpu_seconds / 2)
+        cpu = dict(procs=procs, full=full_n, full1=full_1)
+        log(f"[bench] cpu full validator: {full_n[0]:,.0f} tx/s on {procs} procs, {full_1[0]:,.0f} tx/s on 1")
+    dev = dev_fn()
+
+    # Under the block plan a rank needs only its own blocks' bytes -- the others' results
+    # arrive as all-gathered records -- so only the labels (for the parity check) travel.
+    my_labels = [[m[1] for m in cur] for cur in mine]
     if world > 1:
         allb = [None] * world
-        dist.all_gather_object(allb, (my_blocks if plan_mode == "tx" else None, my_labels))
-        labels = [l for r in range(world) for l in allb[r][1]]
-        if plan_mode == "tx":
-            blks = [b for r in range(world) for b in allb[r][0]]
-        else:
-            blks = [my_blocks[i] if r == rank else b"" for r in range(world) for i in range(B)]
+        dist.all_gather_object(allb, my_labels)
+        labels = [[l for r in range(world) for l in allb[r][k]] for k in range(NB)]
+        blks = [[my_blocks[k][i] if r == rank else b"" for r in range(world) for i in range(B)] for k in range(NB)]
     else:
-        blks, labels = my_blocks, my_labels
-    log(f"[bench] rank {rank}: {len(blks)} blocks x {T} tx ready in {time.time() - t0:.1f}s")
+        labels, blks = my_labels, my_blocks
 
-    eng = _lib.Engine(local)
+    eng = _lib.Engine(local, host_threads=args.host_threads or min(24, _cpu_share()))
     if args.host_parse:
         eng.set_parse_mode(1)
     txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes)
-    # the batch resident in HBM (64 B tail padding per block)
-    sizes = [(len(b) + 64 + 255) // 256 * 256 for b in blks]
-    arena = torch.zeros(sum(sizes), dtype=torch.uint8, device=dev)
-    dptr, o = [], 0
-    for b, sz in zip(blks, sizes):
-        if len(b):  # (other ranks' blocks are empty placeholders under the block plan)
-            arena[o:o + len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
-        dptr.append(arena.data_ptr() + o)
-        o += sz
-    ntx = np.array([T] * len(blks), dtype=np.int64)
-    # contiguous transaction ranges of the batch (fabric_amd/shard.py): on block boundaries, a
-    # rank splits and parses only its own blocks
-    plan = shard.plan(ntx, world, plan_mode)
+    ntx = np.array([T] * (world * B), dtype=np.int64)
+    plan = shard.plan(ntx, world, "block")
     lo, hi = plan[0][rank], plan[1][rank]
     rows = shard.plan_rows(*plan)
-    # records stay in HBM: shard validation -> all-gather (RCCL) -> device finalize
     send = torch.zeros((rows, shard.REC), dtype=torch.uint8, device=dev)
     recv = torch.zeros((world * rows, shard.REC), dtype=torch.uint8, device=dev) if world > 1 else send
-    batch = eng.block_batch(blks, dptr)
     flags_out = np.empty(int(ntx.sum()), dtype=np.uint8)
+
+    # (1) every batch resident in HBM (64 B tail padding per block): the headline `value`
+    sizes = [(len(b) + 64 + 255) // 256 * 256 for bl in blks for b in bl]
+    arena = torch.zeros(sum(sizes), dtype=torch.uint8, device=dev)
+    dptrs, o = [], 0
+    for bl in blks:
+        cur = []
+        for b in bl:
+            if len(b):  # (other ranks' blocks are empty placeholders)
+                arena[o:o + len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+            cur.append(arena.data_ptr() + o)
+            o += (len(b) + 64 + 255) // 256 * 256
+        dptrs.append(cur)
+    hbm_batches = [eng.block_batch(blks[k], dptrs[k]) for k in range(NB)]
     torch.cuda.synchronize()
+
+    def steps_for(batches):
+        # batch k's call pre-splits (and, host-resident, pre-copies) batch k+1 of the rotation
+        return [_lib.BlockStep(eng, batches[k], lo, hi, send.data_ptr(), rows, ntx, world, recv.data_ptr(), flags_out,
+                               plan=plan, presplit=not args.no_presplit, next_batch=batches[(k + 1) % NB])
+                for k in range(NB)]
 
     integ = dict(ms=0.0, ok=True)
 
-    def verify_mine():  # deliver-side VerifyBlock of this rank's blocks (own host pool)
-        chain = _lib.ChainState(number=rank * B, valid=1, has_hash=0)
+    def verify_mine(k):  # deliver-side VerifyBlock of this rank's blocks of batch k (own host pool)
+        first = 1 + (k * world + rank) * B
+        chain = _lib.ChainState(number=first - 1, valid=1, has_hash=0)
         t = time.perf_counter()
-        res = eng.blocks_verify(my_blocks, chain)
+        res = eng.blocks_verify(my_blocks[k], chain)
         integ["ms"] += (time.perf_counter() - t) * 1e3
-        integ["ok"] &= all(r[0] == _lib.BLK_OK for r in res) and chain.number == rank * B + B
+        integ["ok"] &= all(r[0] == _lib.BLK_OK for r in res) and chain.number == first - 1 + B
 
-    # every ctypes argument bound once (fabric_amd._lib.BlockStep); the pre-split of the next
-    # batch (here: the same blocks) overlaps this batch's all-gather + finalize, as a peer
-    # splits block k+1 while block k commits
-    bs = _lib.BlockStep(eng, batch, lo, hi, send.data_ptr(), rows, ntx, world, recv.data_ptr(), flags_out,
-                        plan=plan, presplit=not args.no_presplit)
-
-    def step():
+    def step(bs, k):
         th = None
         if spec["integrity"]:  # concurrent with the committer pass, as in a pipelined peer
-            th = threading.Thread(target=verify_mine)
+            th = threading.Thread(target=verify_mine, args=(k,))
             th.start()
         bs.validate()
         if world > 1:
@@ -204,12 +304,31 @@ def run_block(args, world, rank, local, dev):
             th.join()
         return f
 
-    flags = None
-    for _ in range(args.warmup):
-        flags = step()
-    exp = np.array([e if e is not None else 255 for bl in labels for e in blocks.expected_codes(bl)], np.int64)
-    known = np.array([e is not None for bl in labels for e in blocks.expected_codes(bl)])
-    mism = int(((flags.astype(np.int64) != exp) & known).sum()) if flags is not None else -1
+    def parity(k, flags):
+        exp = np.array([e if e is not None else 255 for bl in labels[k] for e in blocks.expected_codes(bl)], np.int64)
+        known = np.array([e is not None for bl in labels[k] for e in blocks.expected_codes(bl)])
+        return int(((flags.astype(np.int64) != exp) & known).sum())
+
+    def timed(steps_list, K, per_step=None):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(K):
+            step(steps_list[s % NB], s % NB)
+            if per_step is not None:
+                per_step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    hsteps = steps_for(hbm_batches)
+    mism = 0
+    for k in range(NB):  # parity of every batch of the rotation (untimed)
+        mism += parity(k, step(hsteps[k], k).copy())
+    for s in range(args.warmup):
+        step(hsteps[s % NB], s % NB)
     if not integ["ok"]:
         mism = max(mism, 1)
         log(f"[bench] rank {rank}: block integrity check failed")
@@ -217,26 +336,27 @@ def run_block(args, world, rank, local, dev):
     if mism:
         log(f"[bench] rank {rank}: {mism} flags differ from generator labels")
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    acc = dict(point=0.0, prep=0.0, sha=0.0, verifies=0, sha_blocks=0)
+    acc = dict(point=0.0, prep=0.0, sha=0.0, verifies=0, sha_blocks=0, pay_blocks=0)
+    kern = {n: 0.0 for n in _lib.Engine.KERNELS}
     host = dict(parse_ms=0.0, assemble_ms=0.0, device_ms=0.0, fold_ms=0.0)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        tm, cn = bs.stats()
-        for k, v in zip(("parse_ms", "assemble_ms", "device_ms", "fold_ms"), tm[4:]):
-            host[k] += v
+    cur = [0]
+
+    def collect():
+        tm, cn = hsteps[cur[0] % NB].stats()
+        cur[0] += 1
+        for key, v in zip(("parse_ms", "assemble_ms", "device_ms", "fold_ms"), tm[4:]):
+            host[key] += v
         acc["sha"] += tm[0]
         acc["prep"] += tm[1]
         acc["point"] += tm[2]
         acc["sha_blocks"] += cn[1]
         acc["verifies"] += cn[2]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+        kt, npay = eng.kernel_times()
+        for key, v in kt.items():
+            kern[key] += v
+        acc["pay_blocks"] += npay
+
+    el = timed(hsteps, args.steps, collect)
     tot = torch.tensor([el, acc["verifies"], 1.0 if mism == 0 else 0.0], dtype=torch.float64, device=dev)
     if world > 1:
         mx = tot.clone()
@@ -248,36 +368,117 @@ def run_block(args, world, rank, local, dev):
         el, all_verifies, ok = float(mx[0]), float(sm[1]), bool(mn[2] > 0)
     else:
         all_verifies, ok = float(acc["verifies"]), mism == 0
-    total_tx = len(blks) * T * args.steps
-    out = dict(metric=METRIC, value=round(total_tx / el, 1), unit="validated tx/s", n_gpus=world, steps=args.steps,
-               warmup=args.warmup, ms_per_step=round(el / args.steps * 1e3, 3), higher_is_better=True, scaling="weak",
+    K = args.steps
+    total_tx = world * B * T * K
+    batch_mb = sum(len(b) for b in my_blocks[0]) / 1e6
+
+    # (2) PCIe-inclusive: the batches in page-locked host memory; each call copies nothing
+    # itself -- the previous call queued its H2D on the copy stream (fgv_validate_shard_dev_next)
+    pcie = None
+    if not args.no_pcie:
+        pins, pin_batches = [], []
+        for k in range(NB):
+            pb = eng.host_alloc(max(1, sum(len(b) for b in blks[k])))
+            views, o = [], 0
+            for b in blks[k]:
+                pb.a[o:o + len(b)] = np.frombuffer(b, np.uint8)
+                views.append(pb.a[o:o + len(b)])
+                o += len(b)
+            pins.append(pb)
+            pin_batches.append(eng.block_batch(views))
+        psteps = steps_for(pin_batches)
+        pm = 0
+        for k in range(NB):
+            pm += parity(k, step(psteps[k], k).copy())
+        # raw H2D rate of one batch from pinned memory (the PCIe link's share of the step)
+        hb = torch.from_numpy(pins[0].a)
+        dbuf = torch.empty(hb.numel(), dtype=torch.uint8, device=dev)
+        dbuf.copy_(hb, non_blocking=True)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(5):
+            dbuf.copy_(hb, non_blocking=True)
+        torch.cuda.synchronize()
+        h2d = hb.numel() * 5 / (time.perf_counter() - t) / 1e9
+        del dbuf
+        Kp = max(K, 2 * NB)
+        pel = timed(psteps, Kp)
+        if world > 1:
+            t2 = torch.tensor([pel, float(pm)], dtype=torch.float64, device=dev)
+            dist.all_reduce(t2, op=dist.ReduceOp.MAX)
+            pel, pm = float(t2[0]), int(t2[1])
+        pcie = dict(value=round(world * B * T * Kp / pel, 1), unit="validated tx/s", steps=Kp,
+                    ms_per_step=round(pel / Kp * 1e3, 3), parity_vs_labels=pm == 0,
+                    h2d_GBps=round(h2d, 2), batch_MB=round(batch_mb, 2),
+                    note="blocks in fgv_host_alloc'd host memory; batch k+1's H2D is queued on the copy "
+                         "stream during batch k's validation")
+        for pb in pins:
+            pb.close()
+
+    # (3) single-block latency (block in hand -> flags), no pre-split, HBM- and host-resident
+    lat = None
+    if world == 1 and not args.no_latency:
+        lat = {}
+        one = np.array([T], dtype=np.int64)
+        f1 = np.empty(T, dtype=np.uint8)
+        b0 = my_blocks[0][0]
+        pb = eng.host_alloc(len(b0))
+        pb.a[:] = np.frombuffer(b0, np.uint8)
+        for name, bb in (("hbm", eng.block_batch([b0], [dptrs[0][0]])), ("host_pinned", eng.block_batch([pb.a]))):
+            st1 = _lib.BlockStep(eng, bb, [0], [T], send.data_ptr(), T, one, 1, send.data_ptr(), f1, presplit=False)
+            ts = []
+            for _ in range(args.latency_reps + 2):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                st1.validate()
+                st1.finalize()
+                ts.append((time.perf_counter() - t) * 1e3)
+            lat[name] = round(float(np.median(ts[2:])), 4)
+        pb.close()
+
+    kavg = {k: round(v / K, 4) for k, v in kern.items()}
+    out = dict(metric=METRIC, value=round(total_tx / el, 1), unit="validated tx/s", n_gpus=world, steps=K,
+               warmup=args.warmup, ms_per_step=round(el / K * 1e3, 3), higher_is_better=True, scaling="weak",
                vs_baseline=None, dtype="u32", data="synthetic",
                config=dict(workload=spec["desc"].format(T=T),
-                           blocks_per_step=len(blks), tx_per_block=T, global_batch=len(blks) * T,
-                           parallelism=f"{plan_mode}-range-shard{world}+allgather(68B/tx)",
+                           blocks_per_step=world * B, tx_per_block=T, global_batch=world * B * T,
+                           distinct_batches=NB, resident_MB=round(NB * batch_mb * world, 1),
+                           parallelism=f"block-range-shard{world}+allgather(68B/tx)",
                            parse="host" if args.host_parse else "device",
-                           block_split="serial" if args.no_presplit else "pipelined (fgv_presplit)"),
+                           block_split="serial" if args.no_presplit else "pipelined (fgv_validate_shard_dev_next)"),
+               value_basis=f"blocks resident in HBM, {NB} distinct batches rotated (PCIe-inclusive rate in "
+                           f"pcie_inclusive)",
                verifies_per_s=round(all_verifies / el, 1), parity_vs_labels=ok,
-               stage_ms=dict(sha=round(acc["sha"] / args.steps, 4), prep=round(acc["prep"] / args.steps, 4),
-                             point=round(acc["point"] / args.steps, 4)),
-               sha256_compressions_per_step=int(acc["sha_blocks"] / args.steps),
-               host_ms=dict({k: round(v / args.steps, 3) for k, v in host.items()},
-                            **({"integrity_ms": round(integ["ms"] / args.steps, 3)} if spec["integrity"] else {})),
-               roofline=roofline(acc["verifies"] / args.steps, acc["point"] / args.steps, args.workload), cpu_baseline=None)
-    if rank == 0 and world == 1 and args.cpu_threads > 0:
-        # crypto-bound upper bound of the reference's CPU committer on this host: every
-        # verify is SHA-256(msg) + Go-rule DER + low-S + OpenSSL P-256 (what identity.Verify
-        # costs), divided by the verifies per transaction of this workload
+               pcie_inclusive=pcie, latency_1block_ms=lat,
+               kernel_ms=kavg,
+               stage_ms=dict(sha=round(acc["sha"] / K, 4), prep=round(acc["prep"] / K, 4),
+                             point=round(acc["point"] / K, 4)),
+               sha256_compressions_per_step=int(acc["sha_blocks"] / K),
+               host_ms=dict({k: round(v / K, 3) for k, v in host.items()},
+                            **({"integrity_ms": round(integ["ms"] / K, 3)} if spec["integrity"] else {})),
+               roofline=block_roofline(kavg, acc["pay_blocks"] / K, acc["verifies"] / K, args.workload),
+               cpu_baseline=None)
+    if cpu is not None:
+        rate, n, cel, nb = cpu["full"]
+        r1, n1, c1, nb1 = cpu["full1"]
+        out["cpu_baseline"] = dict(
+            value=round(rate, 1), unit="validated tx/s", cores=cpu["procs"], kind="port",
+            sample=f"{nb} blocks x {T} tx of this workload through the restated v20 committer (oracle/v20.py: "
+                   f"protobuf walk, MSP lookup, OpenSSL 3 P-256 Verify via oracle/liboracle.so, policy fold) on "
+                   f"{cpu['procs']} processes in {cel:.1f}s; 1 process: {r1:,.1f} tx/s ({n1} tx in {c1:.1f}s); "
+                   f"CPU {_cpu_model()}; Python restatement, not the Go peer (no Go toolchain on the box)",
+            one_thread=round(r1, 1), cpu_model=_cpu_model())
+        vpt = acc["verifies"] / (B * T * K)
         from fabric_amd.synth.workloads import sig_pool
         pool = sig_pool(4096, seed=99, msg_len=1850)
-        rate, n, cel = cpu_verify_rate(pool["keymat"], [m.tobytes() for m in pool["msgs"]], pool["sigs"],
-                                       args.cpu_threads)
-        vpt = acc["verifies"] / (len(blks) * T * args.steps)
-        out["cpu_baseline"] = dict(value=round(rate / vpt, 1), unit="validated tx/s (crypto-bound upper bound)",
-                                   cores=args.cpu_threads, kind="port",
-                                   sample=f"{n} identity.Verify (SHA-256 1.85KB + Go DER/low-S + OpenSSL P-256) in "
-                                          f"{cel:.1f}s on {args.cpu_threads} threads = {rate:,.0f} verifies/s, / "
-                                          f"{vpt:.2f} verifies per tx; parse/policy cost not included")
+        msgs = [m.tobytes() for m in pool["msgs"]]
+        vr, vn, vel = cpu_verify_rate(pool["keymat"], msgs, pool["sigs"], cpu["procs"], args.cpu_seconds / 2)
+        vr1, _, _ = cpu_verify_rate(pool["keymat"], msgs, pool["sigs"], 1, args.cpu_seconds / 4)
+        out["cpu_crypto_bound"] = dict(
+            value=round(vr / vpt, 1), unit="validated tx/s (identity.Verify only)", cores=cpu["procs"],
+            one_thread=round(vr1 / vpt, 1),
+            sample=f"{vn} identity.Verify (SHA-256 1.85KB + Go DER/low-S + OpenSSL P-256) in {vel:.1f}s = "
+                   f"{vr:,.0f}/s on {cpu['procs']} threads, {vr1:,.0f}/s on 1, / {vpt:.2f} verifies per tx")
     eng.close()
     return out
 
@@ -468,7 +669,16 @@ def main():
     ap.add_argument("--blocks-per-gpu", type=int, default=32)
     ap.add_argument("--tx-per-block", type=int, default=500)
     ap.add_argument("--per-gpu", type=int, default=131072)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--batches", type=int, default=6,
+                    help="distinct blocks-per-gpu batches rotated through the timed loop (block workload)")
+    ap.add_argument("--c5-batches", type=int, default=1)
+    ap.add_argument("--cpu-threads", type=int, default=-1,
+                    help="CPU baseline processes/threads (-1: this rank's CPU share, 0: skip the baseline)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall time of each CPU baseline sample")
+    ap.add_argument("--host-threads", type=int, default=0, help="fgv_config.host_threads (0: min(24, CPU share))")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-resident) pass")
+    ap.add_argument("--no-latency", action="store_true", help="skip the single-block latency pass")
+    ap.add_argument("--latency-reps", type=int, default=20)
     ap.add_argument("--host-parse", action="store_true", help="parse transactions on host threads (A/B)")
     ap.add_argument("--no-presplit", action="store_true", help="walk each batch's framing inside its validation call (A/B)")
     args = ap.parse_args()
@@ -479,15 +689,25 @@ def main():
     # rehearsal knobs (never set by the driver): several ranks on one GPU over gloo
     if os.environ.get("FGV_BENCH_SAME_DEVICE"):
         local = 0
-    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+
+    def dev_fn():  # the GPU is first touched here (the block workload forks CPU workers before)
+        torch.cuda.set_device(local)
+        return dev
+
     if world > 1:
+        dev_fn()
         backend = os.environ.get("FGV_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    out = dict(block=run_block, c5=run_block, sig=run_sig, mvcc=run_mvcc)[args.workload](args, world, rank, local, dev)
+    if args.workload in ("block", "c5"):
+        out = run_block(args, world, rank, local, dev_fn)
+    else:
+        if args.cpu_threads < 0:
+            args.cpu_threads = _cpu_share()
+        out = dict(sig=run_sig, mvcc=run_mvcc)[args.workload](args, world, rank, local, dev_fn())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

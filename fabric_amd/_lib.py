@@ -17,7 +17,7 @@ SIG_VALID, SIG_FALSE, SIG_DER, SIG_HIGH_S, SIG_RANGE, SIG_BADKEY, SIG_EMPTY = ra
 
 EXPORTED = [
     "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_last_counts", "fgv_last_host_timing",
-    "fgv_last_point_handovers",
+    "fgv_last_point_handovers", "fgv_last_kernel_times",
     "fgv_sha256_batch",
     "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
@@ -27,7 +27,7 @@ EXPORTED = [
     "fgv_statedb_init", "fgv_statedb_load", "fgv_statedb_apply", "fgv_statedb_stats", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash",
     "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
-    "fgv_collection_define",
+    "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -102,6 +102,7 @@ def load():
         L.fgv_last_timing.argtypes = [vp] + [ctypes.POINTER(ctypes.c_double)] * 4
         L.fgv_last_counts.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 3
         L.fgv_last_point_handovers.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+        L.fgv_last_kernel_times.argtypes = [vp, vp, sz]
         L.fgv_last_host_timing.argtypes = [vp] + [ctypes.POINTER(ctypes.c_double)] * 4
         L.fgv_sha256_batch.argtypes = [vp, vp, sz, vp, vp, sz, vp]
         L.fgv_p256_verify_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp]
@@ -140,6 +141,9 @@ def load():
         L.fgv_set_parse_mode.argtypes = [vp, ctypes.c_int]
         L.fgv_sha256_host.argtypes = [vp, sz, vp]
         L.fgv_commit_hash.argtypes = [vp, sz, vp, sz, ctypes.c_uint64, vp, sz, vp]
+        L.fgv_host_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
+        L.fgv_host_free.argtypes = [vp, vp]
+        L.fgv_last_h2d.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         _L = L
     return _L
 
@@ -167,10 +171,11 @@ def pack(blobs):
 
 class _BlockBatch:
     def __init__(self, blocks, d_blocks):
+        """blocks: list of bytes / uint8 arrays (e.g. views into a PinnedBuffer)"""
         self.nb = len(blocks)
-        self._bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+        self._bufs = [b if isinstance(b, np.ndarray) else np.frombuffer(b, dtype=np.uint8) for b in blocks]
         self.ptrs = (ctypes.c_void_p * self.nb)(*[b.ctypes.data for b in self._bufs])
-        self.lens = (ctypes.c_size_t * self.nb)(*[len(b) for b in blocks])
+        self.lens = (ctypes.c_size_t * self.nb)(*[b.size for b in self._bufs])
         self.dptr = (ctypes.c_void_p * self.nb)(*d_blocks) if d_blocks is not None else None
         self.ntx = (ctypes.c_size_t * self.nb)()
 
@@ -183,7 +188,7 @@ class BlockStep:
     finalize_flags_dev."""
 
     def __init__(self, eng, batch, tx_lo, tx_hi, d_send, rows, ntx, world, d_recv, flags_out, plan=None,
-                 presplit=True):
+                 presplit=True, next_batch=None):
         L, h = eng._L, eng._h
         self._L = L
         self._lo = np.ascontiguousarray(tx_lo, dtype=np.uint32)
@@ -192,9 +197,10 @@ class BlockStep:
         self.flags = flags_out
         self._val = (h, batch.nb, batch.ptrs, batch.lens, batch.dptr, _ptr(self._lo), _ptr(self._hi),
                      ctypes.c_void_p(d_send), rows, batch.ntx)
-        # presplit: the next batch (the same blocks in a bench loop) is split while this one's
-        # GPU work runs (fgv_validate_shard_dev_next)
-        self._next = (batch.nb, batch.ptrs, batch.lens, _ptr(self._lo), _ptr(self._hi)) if presplit else None
+        # presplit: the next batch (default: the same blocks) is split -- and, when host-resident,
+        # copied to the device -- while this one's GPU work runs (fgv_validate_shard_dev_next)
+        nb = next_batch or batch
+        self._next = (nb.nb, nb.ptrs, nb.lens, _ptr(self._lo), _ptr(self._hi)) if presplit else None
         if plan is None:
             self._fin_fn = L.fgv_finalize_flags_dev
             self._fin = (h, len(self._ntx), _ptr(self._ntx), world, rows, ctypes.c_void_p(d_recv), _ptr(flags_out))
@@ -228,6 +234,23 @@ class BlockStep:
         self._L.fgv_last_host_timing(*self._hr)
         self._L.fgv_last_counts(*self._cr)
         return [x.value for x in self._t], [x.value for x in self._c]
+
+
+class PinnedBuffer:
+    """fgv_host_alloc'd page-locked bytes; .a is a uint8 numpy view, freed by close()."""
+
+    def __init__(self, eng, nbytes):
+        self._eng = eng
+        p = ctypes.c_void_p()
+        _check(eng._L.fgv_host_alloc(eng._h, nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+        self.a = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.ptr))
+
+    def close(self):
+        if self.ptr and self._eng._h:
+            self.a = None
+            _check(self._eng._L.fgv_host_free(self._eng._h, ctypes.c_void_p(self.ptr)))
+        self.ptr = None
 
 
 class Engine:
@@ -268,6 +291,25 @@ class Engine:
         v = [ctypes.c_uint64() for _ in range(3)]
         _check(self._L.fgv_last_counts(self._h, *[ctypes.byref(x) for x in v]))
         return dict(zip(("sha_jobs", "sha_blocks", "verifies"), (x.value for x in v)))
+
+    def host_alloc(self, nbytes):
+        """fgv_host_alloc: page-locked host memory as a PinnedBuffer (uint8 array in .a)"""
+        return PinnedBuffer(self, nbytes)
+
+    def last_h2d(self):
+        """fgv_last_h2d: (bytes the last call copied itself, blocks found prefetched)"""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._L.fgv_last_h2d(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    KERNELS = ("k_bd_sha_payload", "k_bd_parse", "k_bd_sha", "k_bd_ident+count", "k_bd_emit", "k_der+k_inv",
+               "k_prep", "k_point28", "k_bd_fold", "batch")
+
+    def kernel_times(self):
+        """fgv_last_kernel_times: ({kernel: ms}, payload SHA-256 compressions)"""
+        out = (ctypes.c_double * 11)()
+        _check(self._L.fgv_last_kernel_times(self._h, out, 11))
+        return dict(zip(self.KERNELS, out[:10])), int(out[10])
 
     def point_handovers(self):
         v = ctypes.c_uint64()

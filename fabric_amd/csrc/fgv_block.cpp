@@ -1184,7 +1184,7 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   auto t1 = clk::now();
   hipStream_t st = c->stream;
   HIP_TRY(hipMemcpyAsync(c->bd_env.p, head, hbytes, hipMemcpyHostToDevice, st));
-  uint32_t *misc = reinterpret_cast<uint32_t *>(c->bd_env.as<uint8_t>() + moff);  // [0..5) totals, [5] flags, bytes 24..32 compressions
+  uint32_t *misc = reinterpret_cast<uint32_t *>(c->bd_env.as<uint8_t>() + moff);  // [0..5) totals, [5] flags, bytes 24..32 compressions, 32..40 payload compressions
   const DevChannel ch = S->dimg.ch;
   DevTx *dtx = c->bd_tx.as<DevTx>();
   int32_t *did = c->bd_ident.as<int32_t>();
@@ -1196,11 +1196,14 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   // the payload hashes (the longest serial chains) start with the parse, on the second stream
   HIP_TRY(hipEventRecord(c->ev_pay[0], st));
   HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_pay[0], 0));
+  HIP_TRY(hipEventRecord(c->kev[0], c->stream2));
   hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(64), 0, c->stream2, N, c->bd_env.as<uint32_t>(), dbs,
-                     c->bj_dig.as<uint8_t>(), nblk);
+                     c->bj_dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
   HIP_TRY(hipEventRecord(c->ev_pay[3], c->stream2));  // payload digests ready
+  HIP_TRY(hipEventRecord(c->kev[1], st));
   hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, st, N, c->bd_env.as<uint32_t>(), dbs, ch, dtx,
                      misc + 5);
+  HIP_TRY(hipEventRecord(c->kev[2], st));
   // every other SHA-256 message is known after the parse: hashed on the second stream while
   // identities, job counts and verify jobs are worked out on this one
   // (third stream: concurrent with the payload chains still running on stream2)
@@ -1210,14 +1213,17 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
     const char *e = getenv("FGV_SHA_PRIO");
     return e ? atoi(e) : 0;
   }();
+  HIP_TRY(hipEventRecord(c->kev[3], c->stream3));
   hipLaunchKernelGGL(sha_prio == 2 ? k_bd_sha_p2 : k_bd_sha, dim3((uint32_t)(((uint64_t)N * (SHA_E_LANES + 3) + 63) / 64)), dim3(64), 0, c->stream3, N,
                      dtx, dbs, c->bj_dig.as<uint8_t>(), nblk);
   HIP_TRY(hipEventRecord(c->ev_pay[2], c->stream3));
   HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_pay[2], 0));
   HIP_TRY(hipEventRecord(c->ev_pay[1], c->stream2));  // every digest is ready
+  HIP_TRY(hipEventRecord(c->kev[4], st));
   hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 + 255) / 256)), dim3(256), 0, st, N, dtx, dbs, ch,
                      did);
   hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, ch, did, dj, misc);
+  HIP_TRY(hipEventRecord(c->kev[5], st));
   HIP_TRY(hipGetLastError());
   uint32_t *hm = c->hb_misc.as<uint32_t>();
   HIP_TRY(hipMemcpyAsync(hm, misc, 32, hipMemcpyDeviceToHost, st));
@@ -1233,10 +1239,12 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   auto t2 = clk::now();
   if (!c->bj_sigp.ensure(nv * 20 + 64) || !c->bj_vst.ensure(nv + 64)) return FGV_ENOMEM;
   uint8_t *sp = c->bj_sigp.as<uint8_t>();
+  HIP_TRY(hipEventRecord(c->kev[6], st));
   hipLaunchKernelGGL(k_bd_emit, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
                      reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + nv * 8),
                      reinterpret_cast<uint32_t *>(sp + nv * 12), reinterpret_cast<uint32_t *>(sp + nv * 16));
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->kev[7], st));
   c->digests_ready = c->ev_pay[3];
   c->digests_ready2 = c->ev_pay[2];
   int rc = fgv_run_block_jobs_device(c, 0, nv, 0);
@@ -1245,19 +1253,39 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   // joined even when there is nothing to verify
   HIP_TRY(hipStreamWaitEvent(st, c->ev_pay[3], 0));
   HIP_TRY(hipStreamWaitEvent(st, c->ev_pay[2], 0));
+  HIP_TRY(hipEventRecord(c->kev[8], st));
   hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
                      c->bj_dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(hm, misc, 32, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipEventRecord(c->kev[9], st));
+  HIP_TRY(hipMemcpyAsync(hm, misc, 48, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   fgv_read_block_job_times(c);
+  {  // per-kernel device times (fgv_last_kernel_times)
+    auto el = [&](hipEvent_t a, hipEvent_t b) {
+      float ms = 0;
+      return hipEventElapsedTime(&ms, a, b) == hipSuccess ? (double)ms : 0.0;
+    };
+    c->t_kern[0] = el(c->kev[0], c->ev_pay[3]);  // k_bd_sha_payload
+    c->t_kern[1] = el(c->kev[1], c->kev[2]);     // k_bd_parse
+    c->t_kern[2] = el(c->kev[3], c->ev_pay[2]);  // k_bd_sha
+    c->t_kern[3] = el(c->kev[4], c->kev[5]);     // k_bd_ident + k_bd_count
+    c->t_kern[4] = el(c->kev[6], c->kev[7]);     // k_bd_emit
+    c->t_kern[5] = c->stage_ran ? el(c->ev[2], c->ev[3]) : 0.0;  // k_der + k_inv
+    c->t_kern[6] = c->stage_ran ? el(c->ev[4], c->ev[5]) : 0.0;  // k_prep
+    c->t_kern[7] = c->stage_ran ? el(c->ev[5], c->ev[6]) : 0.0;  // k_point28 (+ k_point hand-overs)
+    c->t_kern[8] = el(c->kev[8], c->kev[9]);     // k_bd_fold
+    c->t_kern[9] = el(c->ev_pay[0], c->kev[9]);  // the batch, first kernel to last
+  }
   {
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->ev_pay[0], c->ev_pay[1]) == hipSuccess) c->t_sha += ms;
   }
-  uint64_t nb;
+  uint64_t nb, np;
   memcpy(&nb, hm + 6, 8);
-  c->n_sha_blocks = nb;
+  memcpy(&np, hm + 8, 8);
+  c->n_sha_blocks = nb + np;
+  c->n_pay_blocks = np;
   c->t_host_device = ms_since(t2);
   c->t_host_fold = 0;
   if (hm[5] & 1u) return 1;

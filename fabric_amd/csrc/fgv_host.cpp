@@ -80,7 +80,9 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+    if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
   }
+  if (hipEventCreateWithFlags(&c->pf.ev, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
   {
     std::random_device rd;  // per-context hash seed of the finalize txid table
     c->fin_seed = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)(uintptr_t)c;
@@ -88,6 +90,8 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   for (auto &e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
   for (auto &e : c->ev_pay)
+    if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
+  for (auto &e : c->kev)
     if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
   {
     int ncu = 0;
@@ -116,7 +120,9 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
 void fgv_destroy(fgv_ctx *c) {
   if (!c) return;
   if (c->stream) hipStreamSynchronize(c->stream);
-  DevBuf *d[] = {&c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
+  if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+  DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
+                 &c->bd_misc, &c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
                  &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
                  &c->bj_dig, &c->bj_vst, &c->blk_arena, &c->fz_meta, &c->fz_rowmap, &c->fz_blkof,
@@ -127,15 +133,20 @@ void fgv_destroy(fgv_ctx *c) {
   for (auto *b : d) b->release();
   HostBuf *h[] = {&c->h_status, &c->h_slot, &c->h_r, &c->h_s, &c->h_dig, &c->h_kq, &c->h_kslot,
                   &c->h_moff, &c->h_mlen, &c->hb_dig, &c->hb_vst, &c->hb_jobs, &c->hb_sigp,
-                  &c->hb_sigl, &c->hb_slot, &c->hb_didx, &c->hb_fz, &c->hb_fflags, &c->hb_res};
+                  &c->hb_sigl, &c->hb_slot, &c->hb_didx, &c->hb_fz, &c->hb_fflags, &c->hb_res,
+                  &c->hb_env, &c->hb_bases, &c->hb_misc};
   for (auto *b : h) b->release();
   for (auto &e : c->ev)
     if (e) hipEventDestroy(e);
   for (auto &e : c->ev_pay)
     if (e) hipEventDestroy(e);
+  for (auto &e : c->kev)
+    if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream3) hipStreamDestroy(c->stream3);
+  if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+  if (c->pf.ev) hipEventDestroy(c->pf.ev);
   delete c;
 }
 
@@ -145,6 +156,14 @@ int fgv_last_host_timing(fgv_ctx *c, double *parse_ms, double *assemble_ms, doub
   if (assemble_ms) *assemble_ms = c->t_host_assemble;
   if (device_ms) *device_ms = c->t_host_device;
   if (fold_ms) *fold_ms = c->t_host_fold;
+  return FGV_OK;
+}
+
+int fgv_last_kernel_times(fgv_ctx *c, double *out, size_t n) {
+  if (!c || (n && !out)) return FGV_EINVAL;
+  for (size_t i = 0; i < n && i < 12; i++) out[i] = c->t_kern[i];
+  for (size_t i = 12; i < n; i++) out[i] = 0;
+  if (n > 10) out[10] = (double)c->n_pay_blocks;
   return FGV_OK;
 }
 
@@ -841,23 +860,72 @@ static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint
   return FGV_OK;
 }
 
+static size_t stage_bytes(size_t nblocks, const size_t *lens) {
+  size_t total = 0;
+  for (size_t b = 0; b < nblocks; b++) total += (lens[b] + 64 + 255) & ~(size_t)255;
+  return total;
+}
+
+// Host-resident blocks -> device.  A batch that the previous _next call prefetched is already
+// on its way (copy stream): the compute stream waits for that copy instead of copying again.
 static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                         const uint8_t *const *d_blocks, std::vector<const uint8_t *> &dev) {
   dev.resize(nblocks);
+  c->n_prefetch_hits = 0;
+  c->h2d_bytes = 0;
   if (d_blocks) {
     for (size_t b = 0; b < nblocks; b++) dev[b] = d_blocks[b];
     return FGV_OK;
   }
-  // stage the blocks into one device arena (64 B padding after each block)
-  size_t total = 0;
-  for (size_t b = 0; b < nblocks; b++) total += (lens[b] + 64 + 255) & ~(size_t)255;
-  if (!c->blk_arena.ensure(total)) return FGV_ENOMEM;
+  if (c->pf.on && c->pf.src.size() == nblocks) {
+    bool hit = true;
+    for (size_t b = 0; b < nblocks && hit; b++) hit = c->pf.src[b] == blocks[b] && c->pf.lens[b] == lens[b];
+    if (hit) {
+      c->pf.on = false;
+      c->stage_cur = c->pf.slot;
+      for (size_t b = 0; b < nblocks; b++) dev[b] = c->pf.dev[b];
+      c->n_prefetch_hits = nblocks;
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->pf.ev, 0));
+      return FGV_OK;
+    }
+  }
+  // copy now, into the arena no prefetch is writing (64 B padding after each block)
+  const int slot = c->pf.on ? 1 - c->pf.slot : c->stage_cur;
+  c->pf.on = false;
+  DevBuf &A = c->stage[slot];
+  if (!A.ensure(stage_bytes(nblocks, lens))) return FGV_ENOMEM;
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->pf.ev, 0));  // (an abandoned prefetch may still write the other arena)
   size_t o = 0;
   for (size_t b = 0; b < nblocks; b++) {
-    HIP_TRY(hipMemcpyAsync(c->blk_arena.as<uint8_t>() + o, blocks[b], lens[b], hipMemcpyHostToDevice, c->stream));
-    dev[b] = c->blk_arena.as<uint8_t>() + o;
+    HIP_TRY(hipMemcpyAsync(A.as<uint8_t>() + o, blocks[b], lens[b], hipMemcpyHostToDevice, c->stream));
+    dev[b] = A.as<uint8_t>() + o;
     o += (lens[b] + 64 + 255) & ~(size_t)255;
   }
+  c->stage_cur = slot;
+  c->h2d_bytes = o;
+  return FGV_OK;
+}
+
+// Queue the next batch's H2D copy into the idle arena on the copy stream (it overlaps this
+// batch's kernels).  Called after stage_blocks of the current batch; every earlier user of the
+// idle arena has completed (each validation call ends synchronised).
+static int prefetch_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens) {
+  if (!nblocks) return FGV_OK;
+  const int slot = 1 - c->stage_cur;
+  DevBuf &A = c->stage[slot];
+  if (!A.ensure(stage_bytes(nblocks, lens))) return FGV_ENOMEM;
+  c->pf.src.assign(blocks, blocks + nblocks);
+  c->pf.lens.assign(lens, lens + nblocks);
+  c->pf.dev.resize(nblocks);
+  size_t o = 0;
+  for (size_t b = 0; b < nblocks; b++) {
+    HIP_TRY(hipMemcpyAsync(A.as<uint8_t>() + o, blocks[b], lens[b], hipMemcpyHostToDevice, c->copy_stream));
+    c->pf.dev[b] = A.as<uint8_t>() + o;
+    o += (lens[b] + 64 + 255) & ~(size_t)255;
+  }
+  HIP_TRY(hipEventRecord(c->pf.ev, c->copy_stream));
+  c->pf.slot = slot;
+  c->pf.on = true;
   return FGV_OK;
 }
 
@@ -913,6 +981,10 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   std::vector<const uint8_t *> dev;
   int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
   if (rc) return rc;
+  if (c->next.n && c->next.prefetch) {
+    rc = prefetch_blocks(c, c->next.n, c->next.blocks, c->next.lens);
+    if (rc) return rc;
+  }
   if (fgv_block_parse_mode(c->blk) == 0) {
     rc = fgv_block_validate_dev(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi,
                                 static_cast<fgv_tx_result *>(d_results), results_cap, ntx);
@@ -938,7 +1010,9 @@ int fgv_validate_shard_dev_next(fgv_ctx *c, size_t nblocks, const uint8_t *const
   if (!c || (next_nblocks && (!next_blocks || !next_lens))) return FGV_EINVAL;
   {
     std::lock_guard<std::mutex> g(c->mu);
-    c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks, next_lens, next_lo, next_hi};
+    // the next batch's bytes travel H2D now only when this batch is host-resident too (a
+    // caller holding device copies passes d_blocks for both)
+    c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks, next_lens, next_lo, next_hi, d_blocks == nullptr};
   }
   int rc = fgv_validate_shard_dev(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
   std::lock_guard<std::mutex> g(c->mu);
@@ -955,6 +1029,30 @@ int fgv_presplit(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const
   if (nblocks == 0) return FGV_OK;
   std::lock_guard<std::mutex> g(c->mu);
   return fgv_block_presplit(c->blk, c->device, nblocks, blocks, lens, tx_lo, tx_hi);
+}
+
+int fgv_host_alloc(fgv_ctx *c, size_t bytes, void **out) {
+  if (!c || !out) return FGV_EINVAL;
+  *out = nullptr;
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? FGV_OK : FGV_ENOMEM;
+}
+
+int fgv_host_free(fgv_ctx *c, void *p) {
+  if (!c) return FGV_EINVAL;
+  if (!p) return FGV_OK;
+  {  // a prefetch may still read it
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+  }
+  return hipHostFree(p) == hipSuccess ? FGV_OK : FGV_EINVAL;
+}
+
+int fgv_last_h2d(fgv_ctx *c, uint64_t *copied_bytes, uint64_t *prefetched_blocks) {
+  if (!c) return FGV_EINVAL;
+  if (copied_bytes) *copied_bytes = c->h2d_bytes;
+  if (prefetched_blocks) *prefetched_blocks = c->n_prefetch_hits;
+  return FGV_OK;
 }
 
 int fgv_last_presplit(fgv_ctx *c) { return c && c->last_presplit ? 1 : 0; }

@@ -96,6 +96,9 @@ struct fgv_ctx {
   hipEvent_t ev_pay[4] = {};      // [0] batch start, [1] all digests ready (stream2), [2] k_bd_sha done (stream3),
                                   // [3] k_bd_sha_payload done (stream2)
   hipEvent_t ev[8] = {};          // 0/1 sha, 2/3 inv, 4/5 prep, 6 point end, 7 fork
+  hipEvent_t kev[12] = {};        // per-kernel brackets of the device-parse committer (fgv_last_kernel_times)
+  double t_kern[12] = {};
+  uint64_t n_pay_blocks = 0;      // SHA-256 compressions of the payload hashes (last block call)
   std::mutex mu;
   // generator table (88 KB) and the public-key table cache
   DevBuf gtab, g_ok;
@@ -139,7 +142,21 @@ struct fgv_ctx {
     const uint8_t *const *blocks = nullptr;
     const size_t *lens = nullptr;
     const uint32_t *lo = nullptr, *hi = nullptr;
+    bool prefetch = false;  // also queue its H2D copy (host-resident batches)
   } next;
+  // host-resident batches: two device staging arenas; fgv_validate_shard_dev_next copies the
+  // NEXT batch into the idle one on the copy stream while this batch's kernels run
+  DevBuf stage[2];
+  int stage_cur = 0;
+  hipStream_t copy_stream = nullptr;
+  struct Prefetch {
+    bool on = false;
+    int slot = 0;
+    std::vector<const uint8_t *> src, dev;
+    std::vector<size_t> lens;
+    hipEvent_t ev = nullptr;
+  } pf;
+  uint64_t n_prefetch_hits = 0, h2d_bytes = 0;  // last call: blocks found prefetched / bytes copied in the call
   DevBuf bd_env, bd_bases, bd_tx, bd_ident, bd_jobs, bd_misc;
   HostBuf hb_env, hb_bases, hb_misc;
   double t_bd_split = 0, t_bd_pre = 0, t_bd_fold = 0;

@@ -62,6 +62,12 @@ int fgv_last_host_timing(fgv_ctx *ctx, double *parse_ms, double *assemble_ms, do
                          double *fold_ms);
 /* work of the last block call: SHA-256 messages, 64-byte compressions, ECDSA verifies */
 int fgv_last_counts(fgv_ctx *ctx, uint64_t *sha_jobs, uint64_t *sha_blocks, uint64_t *verifies);
+/* per-kernel device time of the last device-parse block call (ms; HIP events recorded on each
+ * kernel's own stream): out[0] k_bd_sha_payload, [1] k_bd_parse, [2] k_bd_sha, [3] k_bd_ident +
+ * k_bd_count, [4] k_bd_emit, [5] k_der + k_inv, [6] k_prep, [7] k_point28 (+ k_point hand-overs),
+ * [8] k_bd_fold, [9] the batch (first kernel to last); out[10] = SHA-256 compressions of the
+ * payload hashes (k_bd_sha_payload's work).  n entries are written. */
+int fgv_last_kernel_times(fgv_ctx *ctx, double *out, size_t n);
 // Diagnostics: verifies of the last call that the fast point kernel (radix 2^28, incomplete
 // formulas) handed to the exact kernel because an exceptional addition occurred (P = +-Q).
 // Zero for honest inputs; reads one counter back from the device.
@@ -247,13 +253,24 @@ int fgv_presplit(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, con
 int fgv_last_presplit(fgv_ctx *ctx);
 /* fgv_validate_shard_dev of the current batch that also pre-splits the NEXT batch (next_*,
  * same meaning as fgv_presplit's arguments) as soon as the current batch's GPU work is
- * queued, so the walk overlaps the current validation instead of following it. */
+ * queued, so the walk overlaps the current validation instead of following it.  When the
+ * current batch is host-resident (d_blocks NULL) the next batch's bytes are also copied to the
+ * device now, on the engine's copy stream into a second staging arena, overlapping this
+ * batch's kernels; the next call with those blocks waits for that copy instead of copying.
+ * The next batch's buffers must then stay valid and unchanged until that call (or
+ * fgv_destroy); for the copy to run asynchronously they should be pinned (fgv_host_alloc). */
 int fgv_validate_shard_dev_next(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
                                 const size_t *lens, const uint8_t *const *d_blocks,
                                 const uint32_t *tx_lo, const uint32_t *tx_hi, void *d_results,
                                 size_t results_cap, size_t *ntx, size_t next_nblocks,
                                 const uint8_t *const *next_blocks, const size_t *next_lens,
                                 const uint32_t *next_lo, const uint32_t *next_hi);
+/* Page-locked host memory for block buffers (hipHostMalloc): H2D copies from it run on the copy
+ * engine at PCIe rate, asynchronously.  fgv_last_h2d: bytes the last validation call copied
+ * itself, and blocks it found already copied by the previous call's prefetch. */
+int fgv_host_alloc(fgv_ctx *ctx, size_t bytes, void **out);
+int fgv_host_free(fgv_ctx *ctx, void *p);
+int fgv_last_h2d(fgv_ctx *ctx, uint64_t *copied_bytes, uint64_t *prefetched_blocks);
 int fgv_finalize_flags_dev(fgv_ctx *ctx, size_t nblocks, const size_t *ntx, uint32_t world,
                            size_t rows_per_rank, const void *d_gathered, uint8_t *flags);
 /* Any shard plan: rank r's rows hold transactions [rank_lo[r*nblocks+b], rank_hi[r*nblocks+b])

@@ -279,6 +279,57 @@ def test_validate_next_presplits_the_following_call(shards, mode):
     eng.close()
 
 
+@pytest.mark.parametrize("pinned", [True, False], ids=["pinned", "pageable"])
+def test_host_resident_rotation_prefetches_next_batch(pinned):
+    """Host-resident batches A, B, C, A, ... through fgv_validate_shard_dev_next: every call
+    after the first finds its blocks already copied by the previous call's prefetch (copy
+    stream, second staging arena); a call whose batch was not the announced one copies itself.
+    Flags equal the oracle's on every call."""
+    import torch
+    net = network()
+    sizes = [[23, 5], [31], [9, 17, 3]]
+    sets, exps = [], []
+    for k, sz in enumerate(sizes):
+        blks = [blocks.make_block(net, n, number=1 + i, seed=300 + 10 * k + i)[0] for i, n in enumerate(sz)]
+        sets.append(blks)
+        exps.append([f for fl in _oracle(net, blks) for f in fl])
+    eng = _engine_for(net)
+    bufs = []
+    batches = []
+    for blks in sets:
+        if pinned:
+            pb = eng.host_alloc(sum(len(b) for b in blks))
+            views, o = [], 0
+            for b in blks:
+                pb.a[o:o + len(b)] = np.frombuffer(b, np.uint8)
+                views.append(pb.a[o:o + len(b)])
+                o += len(b)
+            bufs.append(pb)
+            batches.append(eng.block_batch(views))
+        else:
+            batches.append(eng.block_batch(blks))
+    order = [0, 1, 2, 0, 2, 1, 1]
+    res = torch.zeros((64, _lib.TX_RESULT_BYTES), dtype=torch.uint8, device="cuda")
+    for i, k in enumerate(order):
+        nxt = order[i + 1] if i + 1 < len(order) else 0
+        ntx_b = eng.validate_shard_dev_next(batches[k], [0] * batches[k].nb, [1 << 30] * batches[k].nb,
+                                            res.data_ptr(), 64, batches[nxt])
+        copied, hits = eng.last_h2d()
+        assert hits == (batches[k].nb if i > 0 else 0), (i, hits)
+        assert (copied == 0) == (i > 0), (i, copied)
+        flags = eng.finalize_flags_dev(ntx_b, 1, 64, res.data_ptr())
+        assert list(flags) == exps[k], (i, k)
+    # a call that is not the announced batch copies itself; the rotation then resumes
+    eng.validate_shard_dev_next(batches[2], [0] * 3, [1 << 30] * 3, res.data_ptr(), 64, batches[1])
+    assert eng.last_h2d()[1] == 0 and eng.last_h2d()[0] > 0
+    ntx_b = eng.validate_shard_dev_next(batches[1], [0], [1 << 30], res.data_ptr(), 64, batches[0])
+    assert eng.last_h2d() == (0, 1)
+    assert list(eng.finalize_flags_dev(ntx_b, 1, 64, res.data_ptr())) == exps[1]
+    for pb in bufs:
+        pb.close()
+    eng.close()
+
+
 def _random_records(rng, ntx, pool):
     """fgv_tx_result records honouring the engine's invariants: VALID => REACHED;
     REACHED => INDEXED with index_txid == txid."""
