@@ -28,6 +28,7 @@ EXPORTED = [
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash",
     "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
     "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d",
+    "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -127,6 +128,9 @@ def load():
         L.fgv_presplit.argtypes = [vp, sz, vp, vp, vp, vp]
         L.fgv_validate_shard_dev_next.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp, vp, vp, vp]
         L.fgv_last_presplit.argtypes = [vp]
+        L.fgv_validate_shard_dev_pipelined.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp, vp, vp, vp, vp]
+        L.fgv_last_ahead.argtypes = [vp]
+        L.fgv_set_ahead.argtypes = [vp, ctypes.c_int]
         L.fgv_finalize_flags_dev_plan.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
@@ -199,8 +203,10 @@ class BlockStep:
                      ctypes.c_void_p(d_send), rows, batch.ntx)
         # presplit: the next batch (default: the same blocks) is split -- and, when host-resident,
         # copied to the device -- while this one's GPU work runs (fgv_validate_shard_dev_next)
+        # (fgv_validate_shard_dev_pipelined: a device-resident next batch's front half is enqueued
+        # ahead of its call)
         nb = next_batch or batch
-        self._next = (nb.nb, nb.ptrs, nb.lens, _ptr(self._lo), _ptr(self._hi)) if presplit else None
+        self._next = (nb.nb, nb.ptrs, nb.lens, nb.dptr, _ptr(self._lo), _ptr(self._hi)) if presplit else None
         if plan is None:
             self._fin_fn = L.fgv_finalize_flags_dev
             self._fin = (h, len(self._ntx), _ptr(self._ntx), world, rows, ctypes.c_void_p(d_recv), _ptr(flags_out))
@@ -221,7 +227,7 @@ class BlockStep:
         if self._next is None:
             _check(self._L.fgv_validate_shard_dev(*self._val))
         else:
-            _check(self._L.fgv_validate_shard_dev_next(*self._val, *self._next))
+            _check(self._L.fgv_validate_shard_dev_pipelined(*self._val, *self._next))
 
     def finalize(self):
         _check(self._fin_fn(*self._fin))
@@ -485,6 +491,27 @@ class Engine:
 
     def last_presplit(self):
         return bool(self._L.fgv_last_presplit(self._h))
+
+    def last_ahead(self):
+        return bool(self._L.fgv_last_ahead(self._h))
+
+    def set_ahead(self, mode: int):
+        """fgv_set_ahead: 0 off (default), 1 after ECDSA, 2 at once, 3 after the fold"""
+        _check(self._L.fgv_set_ahead(self._h, mode))
+
+    def validate_shard_dev_pipelined(self, batch, tx_lo, tx_hi, d_results, cap, next_batch, next_lo=None,
+                                     next_hi=None):
+        """fgv_validate_shard_dev_pipelined: validate `batch` and enqueue `next_batch`'s front half
+        (its device copy: next_batch.dptr, or the copy stream's) ahead of its call."""
+        lo = np.ascontiguousarray(tx_lo, dtype=np.uint32)
+        hi = np.ascontiguousarray(tx_hi, dtype=np.uint32)
+        nlo = None if next_lo is None else np.ascontiguousarray(next_lo, dtype=np.uint32)
+        nhi = None if next_hi is None else np.ascontiguousarray(next_hi, dtype=np.uint32)
+        _check(self._L.fgv_validate_shard_dev_pipelined(self._h, batch.nb, batch.ptrs, batch.lens, batch.dptr,
+                                                        _ptr(lo), _ptr(hi), ctypes.c_void_p(d_results), cap,
+                                                        batch.ntx, next_batch.nb, next_batch.ptrs, next_batch.lens,
+                                                        next_batch.dptr, _ptr(nlo), _ptr(nhi)))
+        return np.ctypeslib.as_array(batch.ntx).astype(np.uint64)
 
     def finalize_flags_dev(self, ntx, world, rows_per_rank, d_gathered, out=None, plan=None):
         """fgv_finalize_flags_dev over world x rows_per_rank gathered records at d_gathered;

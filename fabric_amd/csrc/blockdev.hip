@@ -141,12 +141,23 @@ struct VCollHashed {
     return true;
   }
 };
-// NsReadWriteSet: namespace, rwset bytes, collection hashed rwsets (kept for the second pass)
+// k_bd_parse keeps its per-transaction arrays in LDS, element k of lane l at [k][l] (field-major,
+// lane-minor): in private memory they were ~2 KB of scratch per lane -- HBM-backed reads in the
+// middle of a walk that is one long chain of dependent reads.
 #define BD_MAX_COLL 8
+#define PL 64u  // lanes per k_bd_parse workgroup
+struct ParseLds {
+  S ns[BD_MAX_NS][PL], rwset[BD_MAX_NS][PL], msg[BD_MAX_NS][PL];  // TxReadWriteSet namespaces
+  S wr[BD_MAX_POL][PL];   // written namespaces + the invoked chaincode, sorted
+  S coll[BD_MAX_COLL][PL];  // a namespace's collection hashed rwsets / collection names
+  uint8_t cw[BD_MAX_NS][PL];
+  int16_t pol[BD_MAX_POL][PL];
+};
+// NsReadWriteSet: namespace, rwset bytes, collection hashed rwsets (kept for the second pass)
 struct VNsRwSet {
   S ns{nullptr, 0}, rwset{nullptr, 0};
   uint32_t ncoll = 0;
-  S coll_hashed[BD_MAX_COLL];
+  S *coll_hashed;  // LDS, stride PL
   DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : n == 3 ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
   DEV bool on_len(uint32_t n, S s, bool &ovf) {
@@ -155,40 +166,42 @@ struct VNsRwSet {
     VCollHashed c;
     if (!decode(s, c, ovf)) return false;
     if (ncoll == BD_MAX_COLL) { ovf = true; return false; }
-    coll_hashed[ncoll++] = c.hashed;
+    coll_hashed[PL * ncoll++] = c.hashed;
     return true;
   }
 };
 struct VTxRwSet {
   uint32_t nns = 0;
-  S ns[BD_MAX_NS], rwset[BD_MAX_NS], msg[BD_MAX_NS];  // msg: the NsReadWriteSet (collections re-walked)
-  // bit0: a collection has hashed writes, bit1: a collection failed to decode, bit2: a
-  // collection has metadata writes
-  uint8_t coll_writes[BD_MAX_NS];
+  ParseLds *L;
+  uint32_t lane;
+  // L->ns / rwset / msg (msg: the NsReadWriteSet, collections re-walked); L->cw bit0: a
+  // collection has hashed writes, bit1: a collection failed to decode, bit2: a collection has
+  // metadata writes
   DEV Kind kind(uint32_t n) { return n == 1 ? K_VARINT : n == 2 ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
   DEV bool on_len(uint32_t, S s, bool &ovf) {
     VNsRwSet r;
+    r.coll_hashed = &L->coll[0][lane];
     if (!decode(s, r, ovf)) return false;
     if (nns == BD_MAX_NS) { ovf = true; return false; }
-    ns[nns] = r.ns;
-    rwset[nns] = r.rwset;
-    msg[nns] = s;
+    L->ns[nns][lane] = r.ns;
+    L->rwset[nns][lane] = r.rwset;
+    L->msg[nns][lane] = s;
     uint8_t cw = 0;
     for (uint32_t k = 0; k < r.ncoll; k++) {
       VHashedRWSet h;
-      if (!decode(r.coll_hashed[k], h, ovf)) { cw |= 2; break; }
+      if (!decode(L->coll[k][lane], h, ovf)) { cw |= 2; break; }
       if (h.nwrites) cw |= 1;
       if (h.nmeta) cw |= 4;
     }
-    coll_writes[nns] = cw;
+    L->cw[nns][lane] = cw;
     nns++;
     return true;
   }
 };
 // the collections of one NsReadWriteSet with hashed writes, in order (their EPs)
 struct VNsCollNames {
-  S names[BD_MAX_COLL];
+  S *names;  // LDS, stride PL
   uint32_t n = 0;
   DEV Kind kind(uint32_t f) { return f == 3 ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
@@ -199,8 +212,41 @@ struct VNsCollNames {
     if (!decode(c.hashed, h, ovf)) return false;
     if (!h.nwrites) return true;
     if (n == BD_MAX_COLL) { ovf = true; return false; }
-    names[n++] = c.name;
+    names[PL * n++] = c.name;
     return true;
+  }
+};
+DEV DSpan rel(const uint8_t *base, S s);
+// ChaincodeEndorsedAction / ChaincodeActionPayload: endorsements written straight to the
+// transaction's record (read only for k < nend, set once the parse succeeds)
+struct VEndorsedActionOut {
+  S prp{nullptr, 0};
+  uint32_t nend = 0;
+  const uint8_t *base;
+  DevTx *o;
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { prp = s; return true; }
+    VTwoBytes e;
+    if (!decode(s, e, ovf)) return false;
+    if (nend == BD_MAX_END) { ovf = true; return false; }
+    o->end_ser[nend] = rel(base, e.a);
+    o->end_sig[nend] = rel(base, e.b);
+    nend++;
+    return true;
+  }
+};
+struct VCcActionPayloadOut {
+  S ccpp{nullptr, 0};
+  bool has_action = false;
+  VEndorsedActionOut action;
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { ccpp = s; return true; }
+    has_action = true;
+    return decode(s, action, ovf);
   }
 };
 struct VSerializedIdentity {
@@ -240,17 +286,28 @@ DEV bool msp_known(const DevChannel &ch, S mspid) {
 // ============================================================ k_bd_parse
 // fgv_block.cpp parse_tx, speculatively past the creator lookup (resolved by k_bd_ident;
 // k_bd_count applies the creator decision before anything downstream reads the rest).
-__global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
+__global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                  const uint64_t *__restrict__ bases, DevChannel ch,
                                                  DevTx *__restrict__ out, uint32_t *__restrict__ flags) {
-  __builtin_amdgcn_s_setprio(3);  // shares the SIMDs with k_bd_sha_payload
+  // front half: below the back half's verify chain (3), above k_bd_sha_payload (1)
+  __builtin_amdgcn_s_setprio(2);
+  __shared__ ParseLds L;
+  const uint32_t lane = threadIdx.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntx) return;
+  if (t >= ntx) return;  // (no barrier below: every lane works on its own LDS column)
   const uint32_t *et = envtab + BD_ENV_WORDS * t;
   const uint32_t blk = et[0];
   const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
   const S d{base + et[1], et[2]};
-  DevTx R;
+  DevTx &O = out[t];  // endorsements are written straight into it; the rest at the end
+  struct {
+    uint32_t blk;
+    uint8_t pre, etx, disp, flags;
+    int32_t type;
+    DSpan payload, env_sig, nonce, creator, chdr, act_hdr, ccpp, prop_hash, prp, txid;
+    DSpan idx_nonce, idx_creator, index_txid;
+    uint8_t npol, nend;
+  } R;
   R.blk = blk;
   R.pre = C_PENDING;
   R.etx = C_PENDING;
@@ -312,7 +369,9 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
     if (!decode(pl.data, tx, ovf) || tx.nact != 1) break;
     VTwoBytes ash;
     if (!decode(tx.first.a, ash, ovf) || ash.b.n == 0 || ash.a.n == 0) break;
-    VCcActionPayload cap;
+    VCcActionPayloadOut cap;
+    cap.action.base = base;
+    cap.action.o = &O;
     if (!decode(tx.first.b, cap, ovf)) break;
     if (!cap.has_action) { R.etx = C_UNSUPPORTED; break; }
     VTwoBytes prp;  // proposal_hash, extension
@@ -332,14 +391,16 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
     VCcAction cca;
     if (!decode(prp.b, cca, ovf)) { R.disp = C_BAD_RESP; break; }
     VTxRwSet rw;
+    rw.L = &L;
+    rw.lane = lane;
     if (!decode(cca.results, rw, ovf)) { R.disp = C_BAD_RWSET; break; }
     // per namespace: 1 written (kv / metadata / collections), 2 metadata writes, 4 public writes
     uint8_t wflags[BD_MAX_NS];
     bool bad_rw = false;
     for (uint32_t k = 0; k < rw.nns && !bad_rw; k++) {
       VKVRWSet kv;
-      if (!decode(rw.rwset[k], kv, ovf) || (rw.coll_writes[k] & 2)) { bad_rw = true; break; }
-      const uint8_t cw = rw.coll_writes[k];
+      if (!decode(L.rwset[k][lane], kv, ovf) || (L.cw[k][lane] & 2)) { bad_rw = true; break; }
+      const uint8_t cw = L.cw[k][lane];
       wflags[k] = (uint8_t)(((kv.nwrites || kv.nmeta || (cw & 5)) ? 1 : 0) | ((kv.nmeta || (cw & 4)) ? 2 : 0) |
                             (kv.nwrites ? 4 : 0));
     }
@@ -354,58 +415,60 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
     bool dup = false;
     for (uint32_t a = 0; a < rw.nns && !dup; a++)
       for (uint32_t b = a + 1; b < rw.nns; b++)
-        if (s_eq(rw.ns[a], rw.ns[b])) { dup = true; break; }
+        if (s_eq(L.ns[a][lane], L.ns[b][lane])) { dup = true; break; }
     if (dup) { R.disp = C_ILLEGAL_WS; break; }
     // written namespaces + the invoked chaincode, sorted (Go string order)
-    S wr[BD_MAX_POL];
     uint32_t nwr = 0;
-    wr[nwr++] = ccid;
+    L.wr[nwr++][lane] = ccid;
     bool unsup = false;
     for (uint32_t k = 0; k < rw.nns; k++) {
       if (!(wflags[k] & 1)) continue;
       if (wflags[k] & 2) { unsup = true; break; }
-      if (!s_eq(rw.ns[k], ccid)) {
+      const S nk = L.ns[k][lane];
+      if (!s_eq(nk, ccid)) {
         if (nwr == BD_MAX_POL) { ovf = true; break; }
-        wr[nwr++] = rw.ns[k];
+        L.wr[nwr++][lane] = nk;
       }
     }
     if (ovf) break;
     if (unsup) { R.disp = C_UNSUPPORTED; break; }
     for (uint32_t i = 1; i < nwr; i++)  // insertion sort
-      for (uint32_t j = i; j > 0 && s_lt(wr[j], wr[j - 1]); j--) {
-        const S tmp = wr[j];
-        wr[j] = wr[j - 1];
-        wr[j - 1] = tmp;
+      for (uint32_t j = i; j > 0 && s_lt(L.wr[j][lane], L.wr[j - 1][lane]); j--) {
+        const S tmp = L.wr[j][lane];
+        L.wr[j][lane] = L.wr[j - 1][lane];
+        L.wr[j - 1][lane] = tmp;
       }
     // the EPs each namespace's vscc evaluates (fgv_block.cpp parse_tx restated): -1
     // INVALID_CHAINCODE, -2 outside the model, else a policy index
     uint32_t np = 0;
     auto push = [&](int32_t p) {
       for (uint32_t q = 0; q < np; q++)
-        if (R.pol[q] == p) return;
+        if (L.pol[q][lane] == p) return;
       if (np == BD_MAX_POL) { ovf = true; return; }
-      R.pol[np++] = (int16_t)p;
+      L.pol[np++][lane] = (int16_t)p;
     };
     for (uint32_t i = 0; i < nwr && !ovf; i++) {
-      const int ci = cc_find(ch, wr[i]);
+      const S wi = L.wr[i][lane];
+      const int ci = cc_find(ch, wi);
       const uint32_t *e = ci >= 0 ? ch.cc + BD_CC_WORDS * ci : nullptr;
       if (!e || e[3] == 1) { push(-1); continue; }
       if (e[3] != 0) { push(-2); continue; }
       const int32_t ep = (int32_t)e[2];
       int k = -1;
       for (uint32_t q = 0; q < rw.nns; q++)
-        if (s_eq(rw.ns[q], wr[i])) { k = (int)q; break; }
+        if (s_eq(L.ns[q][lane], wi)) { k = (int)q; break; }
       bool any = false;
       if (k >= 0 && (wflags[k] & 4)) { push(ep); any = true; }
-      if (k >= 0 && (rw.coll_writes[k] & 1)) {
+      if (k >= 0 && (L.cw[k][lane] & 1)) {
         VNsCollNames cn;
-        if (!decode(rw.msg[k], cn, ovf)) break;
+        cn.names = &L.coll[0][lane];
+        if (!decode(L.msg[k][lane], cn, ovf)) break;
         for (uint32_t c = 0; c < cn.n; c++) {
           any = true;
-          const S nm = cn.names[c];
+          const S nm = L.coll[c][lane];
           const uint32_t pl = 14;  // "_implicit_org_" (core/chaincode/implicitcollection/name.go:24-29)
-          const uint8_t pre[14] = {'_', 'i', 'm', 'p', 'l', 'i', 'c', 'i', 't', '_', 'o', 'r', 'g', '_'};
-          if (nm.n >= pl && s_eq(S{nm.p, pl}, S{pre, pl})) {
+          if (nm.n >= pl && ld4(nm.p) == 0x706d695fu /* _imp */ && ld4(nm.p + 4) == 0x6963696cu /* lici */ &&
+              ld4(nm.p + 8) == 0x726f5f74u /* t_or */ && (ld4(nm.p + 12) & 0xFFFFu) == 0x5f67u /* g_ */) {
             push(name_find(ch, ch.impl, ch.nimpl, S{nm.p + pl, nm.n - pl}, -2));
             continue;
           }
@@ -420,13 +483,30 @@ __global__ __launch_bounds__(64) void k_bd_parse(uint32_t ntx, const uint32_t *_
     R.disp = C_VALID;
     R.npol = (uint8_t)np;
     R.nend = (uint8_t)cap.action.nend;
-    for (uint32_t k = 0; k < cap.action.nend; k++) {
-      R.end_ser[k] = rel(base, cap.action.ser[k]);
-      R.end_sig[k] = rel(base, cap.action.sig[k]);
-    }
+    for (uint32_t q = 0; q < np; q++) O.pol[q] = L.pol[q][lane];
   } while (0);
   if (ovf) atomicOr(flags, 1u);
-  out[t] = R;
+  O.blk = R.blk;
+  O.pre = R.pre;
+  O.etx = R.etx;
+  O.disp = R.disp;
+  O.flags = R.flags;
+  O.type = R.type;
+  O.payload = R.payload;
+  O.env_sig = R.env_sig;
+  O.nonce = R.nonce;
+  O.creator = R.creator;
+  O.chdr = R.chdr;
+  O.act_hdr = R.act_hdr;
+  O.ccpp = R.ccpp;
+  O.prop_hash = R.prop_hash;
+  O.prp = R.prp;
+  O.txid = R.txid;
+  O.idx_nonce = R.idx_nonce;
+  O.idx_creator = R.idx_creator;
+  O.index_txid = R.index_txid;
+  O.npol = R.npol;
+  O.nend = R.nend;
 }
 
 // ============================================================ k_bd_ident
@@ -464,7 +544,7 @@ DEV bool group_eq(S a, S b, uint32_t l) {
 __global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__restrict__ txs,
                                                   const uint64_t *__restrict__ bases, DevChannel ch,
                                                   int32_t *__restrict__ ident) {
-  __builtin_amdgcn_s_setprio(3);  // latency-critical chain; k_bd_sha fills the SIMDs beside it
+  __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
   const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / ID_LANES;  // one group per tx
   const uint32_t l = threadIdx.x % ID_LANES;
   if (t >= ntx) return;  // whole groups exit together
@@ -511,7 +591,7 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
 __global__ __launch_bounds__(256) void k_bd_count(uint32_t ntx, DevTx *__restrict__ txs, DevChannel ch,
                                                   const int32_t *__restrict__ ident, DevJobIdx *__restrict__ jobs,
                                                   uint32_t *__restrict__ totals) {
-  __builtin_amdgcn_s_setprio(3);  // latency-critical chain; k_bd_sha fills the SIMDs beside it
+  __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   DevJobIdx J;
   for (int q = 0; q < BJ_KINDS; q++) J.cnt[q] = J.base[q] = 0;
@@ -566,7 +646,7 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
 __global__ __launch_bounds__(64) void k_bd_sha_payload(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                        const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
                                                        unsigned long long *__restrict__ nblk) {
-  __builtin_amdgcn_s_setprio(2);
+  __builtin_amdgcn_s_setprio(1);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t blocks = 0;
   if (t < ntx) {
@@ -602,11 +682,9 @@ __global__ __launch_bounds__(64) void k_bd_sha_payload(uint32_t ntx, const uint3
 // SHA_E_LANES lanes per transaction for its endorsements (lane j: endorsements j, j + SHA_E_LANES, ...),
 // then txid / proposal / index.  (k_bd_count may turn a pending creator into code 4
 // meanwhile; those digests go unused.)
-template <int PRIO>
-__device__ __forceinline__ void bd_sha_body(uint32_t ntx, const DevTx *__restrict__ txs,
-                                            const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
-                                            unsigned long long *__restrict__ nblk) {
-  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+__global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__restrict__ txs,
+                                               const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                               unsigned long long *__restrict__ nblk) {
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t row = l / ntx, t = l - row * ntx;  // rows: E x SHA_E_LANES | T | P | I
   uint64_t blocks = 0;
@@ -652,18 +730,6 @@ __device__ __forceinline__ void bd_sha_body(uint32_t ntx, const DevTx *__restric
   }
   for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
   if ((threadIdx.x & 63) == 0 && blocks) atomicAdd(nblk, (unsigned long long)blocks);
-}
-// wave priority of the non-payload hashes (A/B: FGV_SHA_PRIO; the main-stream chain runs at 3,
-// the payload chains at 2)
-__global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__restrict__ txs,
-                                               const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
-                                               unsigned long long *__restrict__ nblk) {
-  bd_sha_body<0>(ntx, txs, bases, dig, nblk);
-}
-__global__ __launch_bounds__(64) void k_bd_sha_p2(uint32_t ntx, const DevTx *__restrict__ txs,
-                                                  const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
-                                                  unsigned long long *__restrict__ nblk) {
-  bd_sha_body<2>(ntx, txs, bases, dig, nblk);
 }
 
 // ============================================================ k_bd_emit
@@ -800,23 +866,28 @@ DEV bool hex32(S s, uint8_t out[32]) {
   return true;
 }
 
+// d: a 32-byte aligned digest slot; table entries are 32-byte aligned too (word compares)
 DEV bool committed(const DevChannel &ch, const uint8_t *d) {
-  bool zero = true;
-  for (int i = 0; i < 32; i++) zero &= d[i] == 0;
-  if (zero) return ch.committed_zero != 0;
+  const uint4 *dv = reinterpret_cast<const uint4 *>(d);
+  const uint4 d0 = dv[0], d1 = dv[1];
+  if (!(d0.x | d0.y | d0.z | d0.w | d1.x | d1.y | d1.z | d1.w)) return ch.committed_zero != 0;
   if (!ch.committed) return false;
-  uint32_t h;
-  memcpy(&h, d, 4);  // SHA-256 output: uniform
+  const uint32_t h = d0.x;  // SHA-256 output: uniform
   for (uint32_t pos = h & ch.committed_mask;; pos = (pos + 1) & ch.committed_mask) {
-    const uint8_t *e = ch.committed + (size_t)pos * 32;
-    bool empty = true, eq = true;
-    for (int i = 0; i < 32; i++) {
-      empty &= e[i] == 0;
-      eq &= e[i] == d[i];
-    }
-    if (eq) return true;
-    if (empty) return false;
+    const uint4 *ev = reinterpret_cast<const uint4 *>(ch.committed + (size_t)pos * 32);
+    const uint4 e0 = ev[0], e1 = ev[1];
+    if (!((e0.x ^ d0.x) | (e0.y ^ d0.y) | (e0.z ^ d0.z) | (e0.w ^ d0.w) | (e1.x ^ d1.x) | (e1.y ^ d1.y) |
+          (e1.z ^ d1.z) | (e1.w ^ d1.w)))
+      return true;
+    if (!(e0.x | e0.y | e0.z | e0.w | e1.x | e1.y | e1.z | e1.w)) return false;
   }
+}
+
+// the 4 lowercase hex characters of digest bytes 2j and 2j+1, as a little-endian word
+DEV uint32_t hex_word(const uint32_t *dw, uint32_t j) {
+  const uint32_t two = (dw[j >> 1] >> (16u * (j & 1u))) & 0xFFFFu;
+  auto hx = [](uint32_t v) -> uint32_t { return v < 10 ? '0' + v : 'a' + v - 10; };
+  return hx((two >> 4) & 15u) | hx(two & 15u) << 8 | hx((two >> 12) & 15u) << 16 | hx((two >> 8) & 15u) << 24;
 }
 
 }  // namespace
@@ -829,6 +900,7 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
                                                  const uint8_t *__restrict__ digests,
                                                  const uint8_t *__restrict__ vstatus,
                                                  fgv_tx_result *__restrict__ res, uint32_t *__restrict__ flags) {
+  __builtin_amdgcn_s_setprio(3);  // back half; a next batch's front half may run beside it
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
   const DevTx &R = txs[t];
@@ -837,7 +909,6 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
   const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
   // digests: k_bd_sha's slots
   const size_t kT = (size_t)BD_DIG_T * ntx + t, kP = (size_t)BD_DIG_P * ntx + t, kI = (size_t)BD_DIG_I * ntx + t;
-  auto hexd = [](uint32_t v) -> uint8_t { return (uint8_t)(v < 10 ? '0' + v : 'a' + v - 10); };
   uint8_t code;
   bool reached = false;
   const uint8_t *txd = nullptr;
@@ -852,18 +923,26 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
   } else {
     txd = digests + kT * 32;
     const S txid = absl(base, R.txid);
-    bool ok = txid.n == 64;
-    for (int k = 0; ok && k < 32; k++)
-      ok = txid.p[2 * k] == hexd(txd[k] >> 4) && txid.p[2 * k + 1] == hexd(txd[k] & 15);
+    bool ok = txid.n == 64;  // chdr.TxId == hex(SHA-256(nonce || creator)), 16 independent word reads
+    if (ok) {
+      const uint32_t *dw = reinterpret_cast<const uint32_t *>(txd);
+      uint32_t diff = 0;
+      for (uint32_t j = 0; j < 16; j++) diff |= ld4(txid.p + 4 * j) ^ hex_word(dw, j);
+      ok = diff == 0;
+    }
     if (!ok) {
       code = C_BAD_TXID;
     } else if (R.etx != C_VALID) {
       code = R.etx;
     } else {
       const S ph = absl(base, R.prop_hash);
-      const uint8_t *pd = digests + kP * 32;
+      const uint32_t *pd = reinterpret_cast<const uint32_t *>(digests + kP * 32);
       bool same = ph.n == 32;
-      for (int k = 0; same && k < 32; k++) same = ph.p[k] == pd[k];
+      if (same) {
+        uint32_t diff = 0;
+        for (uint32_t j = 0; j < 8; j++) diff |= ld4(ph.p + 4 * j) ^ pd[j];
+        same = diff == 0;
+      }
       if (!same) {
         code = C_BAD_ETX;
       } else if ((reached = true, committed(ch, txd))) {

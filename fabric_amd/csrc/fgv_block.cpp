@@ -187,18 +187,62 @@ struct PreSplit {
   }
 };
 
+// One batch's device-parse state.  There are two: batch k+1's front half (head upload, payload
+// and message hashes, parse, identities, job counts -- the side streams) is enqueued while
+// batch k's back half (verify jobs, ECDSA, fold -- the main stream) runs.
+struct BdSet {
+  DevBuf env, tx, ident, jobs, dig;  // env: envelope table | block bases | counters (the head)
+  HostBuf head, misc;                // pinned head staging / counters read back
+  // 0 start, 1 payload hashes done (stream2), 2 k_bd_sha done (stream3), 3 head uploaded,
+  // 4 parse done, 5 k_bd_sha start, 6 counts read back, 7 k_bd_ident start
+  hipEvent_t ev[8] = {};
+  SplitOut so;
+  bool presplit = false;
+  size_t eoff = 0, moff = 0;
+  uint32_t N = 0;
+  // the batch this set holds (the match key of a front half enqueued ahead)
+  std::vector<const uint8_t *> hb, db;
+  std::vector<size_t> lens;
+  std::vector<uint32_t> lo, hi;
+  bool has_lo = false, has_hi = false;
+  bool matches(size_t nb, const uint8_t *const *h, const size_t *l, const uint8_t *const *d, const uint32_t *lo_,
+               const uint32_t *hi_) const {
+    if (nb != hb.size() || (lo_ != nullptr) != has_lo || (hi_ != nullptr) != has_hi) return false;
+    for (size_t i = 0; i < nb; i++)
+      if (h[i] != hb[i] || l[i] != lens[i] || d[i] != db[i] || (lo_ && lo_[i] != lo[i]) || (hi_ && hi_[i] != hi[i]))
+        return false;
+    return true;
+  }
+  void release() {
+    for (DevBuf *b : {&env, &tx, &ident, &jobs, &dig}) b->release();
+    head.release();
+    misc.release();
+    for (auto &e : ev)
+      if (e) hipEventDestroy(e);
+  }
+};
+
 struct fgv_block_state {
   Channel ch;
   ThreadPool pool;
   PreSplit pre;
   // per-call scratch
   std::vector<TxRec> recs;
-  // device image of `ch`, rebuilt when the channel model changes
+  // device image of `ch`, rebuilt when the channel model changes (the committed txid table
+  // alone when only ledger txids were added)
   DevImage dimg;
   bool dev_dirty = true;
+  bool txid_dirty = false;
   int parse_mode = 0;  // 0: device parse (host parser for capacity overflows), 1: host parse
+  BdSet set[2];
+  int ahead = -1;  // set holding a front half enqueued ahead of its call (-1: none)
+  int last = 1;    // set of the last call
   explicit fgv_block_state(unsigned threads) : pool(threads) {}
-  ~fgv_block_state() { dimg.release(); }
+  ~fgv_block_state() {
+    dimg.release();
+    set[0].release();
+    set[1].release();
+  }
 };
 
 fgv_block_state *fgv_block_state_new(unsigned threads) { return new fgv_block_state(threads); }
@@ -850,7 +894,7 @@ int fgv_block_declare_msp(fgv_block_state *S, const char *mspid) {
 
 int fgv_block_add_txids(fgv_block_state *S, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
                         size_t n) {
-  S->dev_dirty = true;
+  S->txid_dirty = true;
   for (size_t i = 0; i < n; i++) {
     std::string_view v(reinterpret_cast<const char *>(buf + off[i]), len[i]);
     if (S->ch.committed.count(v)) continue;
@@ -877,6 +921,7 @@ static int upload(DevBuf &b, const std::vector<T> &v) {
   return FGV_OK;
 }
 
+static int build_committed(fgv_block_state *S);
 // Flatten the channel model into the HBM image the kernels read (blockdev.h).
 static int build_dev_image(fgv_block_state *S) {
   const Channel &ch = S->ch;
@@ -984,7 +1029,40 @@ static int build_dev_image(fgv_block_state *S) {
       (rc = upload(D.msps, msps)) || (rc = upload(D.ccb, ccb)) || (rc = upload(D.pol, pol)) ||
       (rc = upload(D.nodes, nodes)) || (rc = upload(D.kids, kids)) || (rc = upload(D.subs, subs)))
     return rc;
-  // committed ledger txids: only 64-char lowercase hex can equal a txid that passed CheckTxID
+  int rc2 = build_committed(S);
+  if (rc2) return rc2;
+  DevChannel &d = D.ch;
+  d.name = D.name.as<uint8_t>();
+  d.name_len = (uint32_t)name.size();
+  d.nident = (uint32_t)idents.size();
+  d.idents = D.idents.as<DevIdent>();
+  d.ident_bytes = D.ibytes.as<uint8_t>();
+  d.ident_table = D.itable.as<uint32_t>();
+  d.ident_hash = D.ihash.as<uint64_t>();
+  d.ident_mask = (uint32_t)(icap - 1);
+  d.ncc = (uint32_t)(cc.size() / BD_CC_WORDS);
+  d.cc = D.cc.as<uint32_t>();
+  d.colls = D.colls.as<uint32_t>();
+  d.nimpl = (uint32_t)(impl.size() / BD_COLL_WORDS);
+  d.impl = D.impl.as<uint32_t>();
+  d.nmsp = (uint32_t)(msps.size() / 2);
+  d.msps = D.msps.as<uint32_t>();
+  d.cc_bytes = D.ccb.as<uint8_t>();
+  d.policies = D.pol.as<DevPolicy>();
+  d.nodes = D.nodes.as<DevPNode>();
+  d.kids = D.kids.as<uint32_t>();
+  d.subs = D.subs.as<uint32_t>();
+  return FGV_OK;
+}
+
+// The committed ledger txids (checkTxIdDupsLedger) as an open-addressing table in HBM.  Read by
+// k_bd_fold only, so a front half enqueued ahead never sees it change under it.
+static int build_committed(fgv_block_state *S) {
+  const Channel &ch = S->ch;
+  DevImage &D = S->dimg;
+  int rc;
+  S->txid_dirty = false;
+  // only 64-char lowercase hex can equal a txid that passed CheckTxID
   std::vector<std::array<uint8_t, 32>> keys;
   uint32_t zero = 0;
   for (const std::string_view &v : ch.committed) {
@@ -1017,26 +1095,6 @@ static int build_dev_image(fgv_block_state *S) {
   }
   if ((rc = upload(D.committed, ctab))) return rc;
   DevChannel &d = D.ch;
-  d.name = D.name.as<uint8_t>();
-  d.name_len = (uint32_t)name.size();
-  d.nident = (uint32_t)idents.size();
-  d.idents = D.idents.as<DevIdent>();
-  d.ident_bytes = D.ibytes.as<uint8_t>();
-  d.ident_table = D.itable.as<uint32_t>();
-  d.ident_hash = D.ihash.as<uint64_t>();
-  d.ident_mask = (uint32_t)(icap - 1);
-  d.ncc = (uint32_t)(cc.size() / BD_CC_WORDS);
-  d.cc = D.cc.as<uint32_t>();
-  d.colls = D.colls.as<uint32_t>();
-  d.nimpl = (uint32_t)(impl.size() / BD_COLL_WORDS);
-  d.impl = D.impl.as<uint32_t>();
-  d.nmsp = (uint32_t)(msps.size() / 2);
-  d.msps = D.msps.as<uint32_t>();
-  d.cc_bytes = D.ccb.as<uint8_t>();
-  d.policies = D.pol.as<DevPolicy>();
-  d.nodes = D.nodes.as<DevPNode>();
-  d.kids = D.kids.as<uint32_t>();
-  d.subs = D.subs.as<uint32_t>();
   d.committed = ccap ? D.committed.as<uint8_t>() : nullptr;
   d.committed_mask = ccap ? (uint32_t)(ccap - 1) : 0u;
   d.committed_zero = zero;
@@ -1049,7 +1107,6 @@ __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
 __global__ void k_bd_sha(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
-__global__ void k_bd_sha_p2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
 __global__ void k_bd_sha_payload(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, uint8_t *dig,
                                  unsigned long long *nblk);
 __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
@@ -1135,130 +1192,207 @@ bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t le
   return true;
 }
 
+// Front half of a batch into set B, on the side streams: envelope spans (pre-split or walked
+// here), head upload, k_bd_sha_payload (stream2), k_bd_parse -> k_bd_ident -> k_bd_count ->
+// counters read back (streamF), k_bd_sha (stream3).  `wait` (optional): an event the head
+// upload waits for (the H2D copy of host-resident blocks).  Nothing here reads the committed
+// txid table (k_bd_fold does), so ledger txids added afterwards never stale it.
+static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks, const uint8_t *const *h_blocks,
+                        const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                        const uint32_t *tx_hi, hipEvent_t wait, hipEvent_t wait2 = nullptr) {
+  B.hb.assign(h_blocks, h_blocks + nblocks);
+  B.db.assign(d_blocks, d_blocks + nblocks);
+  B.lens.assign(lens, lens + nblocks);
+  B.has_lo = tx_lo != nullptr;
+  B.has_hi = tx_hi != nullptr;
+  B.lo.clear();
+  B.hi.clear();
+  if (tx_lo) B.lo.assign(tx_lo, tx_lo + nblocks);
+  if (tx_hi) B.hi.assign(tx_hi, tx_hi + nblocks);
+  B.N = 0;
+  B.presplit = false;
+  for (auto &e : B.ev)
+    if (!e) HIP_TRY(hipEventCreate(&e));
+  // --- host: the batch's envelope spans, split ahead by fgv_presplit or here
+  if (S->pre.active) {
+    S->pre.join();  // (the worker is idle from here on)
+    if (S->pre.rc == FGV_OK && S->pre.matches(nblocks, h_blocks, lens, tx_lo, tx_hi)) {
+      B.so = std::move(S->pre.out);
+      std::swap(B.head, S->pre.et);  // (B's old head: no copy from it is pending)
+      B.presplit = true;
+    }
+  }
+  if (!B.presplit) {
+    int rc = split_batch(S->pool, nblocks, h_blocks, lens, tx_lo, tx_hi, B.so, B.head);
+    if (rc) return rc;
+  }
+  const size_t total = B.so.total;
+  if (total == 0) return FGV_OK;
+  const uint32_t N = (uint32_t)total;
+  const size_t hbytes = head_bytes(total, nblocks);
+  B.eoff = head_env_bytes(total);
+  B.moff = B.eoff + ((nblocks * 8 + 63) & ~(size_t)63);
+  // (B.head already holds hbytes: split_batch sized it)
+  if (!B.misc.ensure(64) || !B.env.ensure(hbytes) || !B.tx.ensure(total * sizeof(DevTx)) ||
+      !B.ident.ensure(total * BD_OCC * 4) || !B.jobs.ensure(total * sizeof(DevJobIdx)) ||
+      !B.dig.ensure((size_t)N * 32 * BD_DIG_SLOTS + 64))  // k_bd_sha digest slots (blockdev.h), slot-major
+    return FGV_ENOMEM;
+  uint8_t *head = B.head.as<uint8_t>();  // the envelope table is already in place
+  uint64_t *bs = reinterpret_cast<uint64_t *>(head + B.eoff);
+  for (size_t b = 0; b < nblocks; b++) bs[b] = (uint64_t)(uintptr_t)d_blocks[b];
+  memset(head + B.moff, 0, 64);
+  const DevChannel ch = S->dimg.ch;
+  hipStream_t sf = c->streamF;
+  if (wait) HIP_TRY(hipStreamWaitEvent(sf, wait, 0));
+  if (wait2) HIP_TRY(hipStreamWaitEvent(sf, wait2, 0));
+  HIP_TRY(hipEventRecord(B.ev[0], sf));
+  HIP_TRY(hipMemcpyAsync(B.env.p, head, hbytes, hipMemcpyHostToDevice, sf));
+  HIP_TRY(hipEventRecord(B.ev[3], sf));
+  // [0..5) totals, [5] flags, bytes 24..32 k_bd_sha compressions, 32..40 payload compressions
+  uint32_t *misc = reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff);
+  const uint32_t *envtab = B.env.as<uint32_t>();
+  const uint64_t *dbs = reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff);
+  DevTx *dtx = B.tx.as<DevTx>();
+  // the payload hashes (the longest serial chains) start with the parse, on the second stream
+  HIP_TRY(hipStreamWaitEvent(c->stream2, B.ev[3], 0));
+  hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(64), 0, c->stream2, N, envtab, dbs,
+                     B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
+  HIP_TRY(hipEventRecord(B.ev[1], c->stream2));
+  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5);
+  HIP_TRY(hipEventRecord(B.ev[4], sf));
+  // every other SHA-256 message is known after the parse: hashed on the third stream while
+  // identities and job counts are worked out on this one
+  HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[4], 0));
+  HIP_TRY(hipEventRecord(B.ev[5], c->stream3));
+  hipLaunchKernelGGL(k_bd_sha, dim3((uint32_t)(((uint64_t)N * (SHA_E_LANES + 3) + 63) / 64)), dim3(64), 0,
+                     c->stream3, N, dtx, dbs, B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 6));
+  HIP_TRY(hipEventRecord(B.ev[2], c->stream3));
+  HIP_TRY(hipEventRecord(B.ev[7], sf));
+  hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 + 255) / 256)), dim3(256), 0, sf, N, dtx, dbs, ch,
+                     B.ident.as<int32_t>());
+  hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
+                     B.jobs.as<DevJobIdx>(), misc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(B.misc.p, misc, 32, hipMemcpyDeviceToHost, sf));
+  HIP_TRY(hipEventRecord(B.ev[6], sf));
+  B.N = N;
+  return FGV_OK;
+}
+
+// Wait for a front half enqueued ahead and forget it (its batch was not the next call's, or
+// the channel model is about to change under it).
+static void drain_ahead(fgv_ctx *c, fgv_block_state *S) {
+  if (S->ahead < 0) return;
+  hipStreamSynchronize(c->streamF);
+  hipStreamSynchronize(c->stream2);
+  hipStreamSynchronize(c->stream3);
+  S->ahead = -1;
+}
+
+void fgv_block_drain(fgv_ctx *c) { drain_ahead(c, c->blk); }
+
 int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
                            const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                            const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   auto t0 = clk::now();
-  if (S->ch.dirty) S->ch.compile();
-  if (S->dev_dirty) {
+  fgv_ctx::NextBatch nx = c->next;  // the batch whose front half this call enqueues ahead
+  if (S->ch.dirty || S->dev_dirty) {
+    drain_ahead(c, S);  // (its kernels read the image about to be rebuilt; its results are stale)
+    if (S->ch.dirty) S->ch.compile();
     int rc = build_dev_image(S);
     if (rc) return rc;
     S->dev_dirty = false;
-  }
-  // --- host: the batch's envelope spans, split ahead by fgv_presplit or here
-  SplitOut so;
-  bool presplit = false;
-  if (S->pre.active) {
-    S->pre.join();  // (the worker is idle from here on)
-    if (S->pre.rc == FGV_OK && S->pre.matches(nblocks, h_blocks, lens, tx_lo, tx_hi)) {
-      so = std::move(S->pre.out);
-      std::swap(c->hb_env, S->pre.et);
-      presplit = true;
-    }
-  }
-  if (!presplit) {
-    int rc = split_batch(S->pool, nblocks, h_blocks, lens, tx_lo, tx_hi, so, c->hb_env);
+  } else if (S->txid_dirty) {
+    int rc = build_committed(S);
     if (rc) return rc;
   }
-  for (size_t b = 0; b < nblocks; b++) ntx_out[b] = so.ntx[b];
-  const size_t total = so.total;
-  if (total > res_cap) return FGV_EINVAL;
+  // --- front half: enqueued by the previous call, or now
+  int cur;
+  bool ahead_hit = false;
+  if (S->ahead >= 0 && S->set[S->ahead].matches(nblocks, h_blocks, lens, d_blocks, tx_lo, tx_hi)) {
+    cur = S->ahead;
+    ahead_hit = true;
+    S->ahead = -1;
+  } else {
+    drain_ahead(c, S);
+    cur = S->last ^ 1;
+    int rc = front_launch(c, S, S->set[cur], nblocks, h_blocks, lens, d_blocks, tx_lo, tx_hi, nullptr);
+    if (rc) return rc;
+  }
+  S->last = cur;
+  BdSet &B = S->set[cur];
+  for (size_t b = 0; b < nblocks; b++) ntx_out[b] = B.so.ntx[b];
   c->n_sha_jobs = c->n_sha_blocks = c->n_verifies = 0;
-  c->last_presplit = presplit;
-  if (total == 0) return FGV_OK;
-  const uint32_t N = (uint32_t)total;
-  const size_t hbytes = head_bytes(total, nblocks), eoff = head_env_bytes(total);
-  const size_t moff = eoff + ((nblocks * 8 + 63) & ~(size_t)63);
-  // (hb_env already holds hbytes: split_batch sized it)
-  if (!c->hb_misc.ensure(64) || !c->bd_env.ensure(hbytes) ||
-      !c->bd_tx.ensure(total * sizeof(DevTx)) || !c->bd_ident.ensure(total * BD_OCC * 4) ||
-      !c->bd_jobs.ensure(total * sizeof(DevJobIdx)))
-    return FGV_ENOMEM;
-  uint8_t *head = c->hb_env.as<uint8_t>();  // the envelope table is already in place
-  uint64_t *bs = reinterpret_cast<uint64_t *>(head + eoff);
-  for (size_t b = 0; b < nblocks; b++) bs[b] = (uint64_t)(uintptr_t)d_blocks[b];
-  memset(head + moff, 0, 64);
+  c->last_presplit = B.presplit;
+  c->last_ahead = ahead_hit;
+  if (B.so.total > res_cap) return FGV_EINVAL;
+  const uint32_t N = B.N;
+  if (N == 0) return FGV_OK;
   c->t_host_parse = ms_since(t0);
   auto t1 = clk::now();
-  hipStream_t st = c->stream;
-  HIP_TRY(hipMemcpyAsync(c->bd_env.p, head, hbytes, hipMemcpyHostToDevice, st));
-  uint32_t *misc = reinterpret_cast<uint32_t *>(c->bd_env.as<uint8_t>() + moff);  // [0..5) totals, [5] flags, bytes 24..32 compressions, 32..40 payload compressions
-  const DevChannel ch = S->dimg.ch;
-  DevTx *dtx = c->bd_tx.as<DevTx>();
-  int32_t *did = c->bd_ident.as<int32_t>();
-  DevJobIdx *dj = c->bd_jobs.as<DevJobIdx>();
-  const uint64_t *dbs = reinterpret_cast<const uint64_t *>(c->bd_env.as<uint8_t>() + eoff);
-  // k_bd_sha digest slots (blockdev.h): BD_DIG_SLOTS per tx, slot-major
-  if (!c->bj_dig.ensure((size_t)N * 32 * BD_DIG_SLOTS + 64)) return FGV_ENOMEM;
-  unsigned long long *nblk = reinterpret_cast<unsigned long long *>(misc + 6);
-  // the payload hashes (the longest serial chains) start with the parse, on the second stream
-  HIP_TRY(hipEventRecord(c->ev_pay[0], st));
-  HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_pay[0], 0));
-  HIP_TRY(hipEventRecord(c->kev[0], c->stream2));
-  hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(64), 0, c->stream2, N, c->bd_env.as<uint32_t>(), dbs,
-                     c->bj_dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
-  HIP_TRY(hipEventRecord(c->ev_pay[3], c->stream2));  // payload digests ready
-  HIP_TRY(hipEventRecord(c->kev[1], st));
-  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, st, N, c->bd_env.as<uint32_t>(), dbs, ch, dtx,
-                     misc + 5);
-  HIP_TRY(hipEventRecord(c->kev[2], st));
-  // every other SHA-256 message is known after the parse: hashed on the second stream while
-  // identities, job counts and verify jobs are worked out on this one
-  // (third stream: concurrent with the payload chains still running on stream2)
-  HIP_TRY(hipEventRecord(c->ev[7], st));
-  HIP_TRY(hipStreamWaitEvent(c->stream3, c->ev[7], 0));
-  static const int sha_prio = [] {
-    const char *e = getenv("FGV_SHA_PRIO");
-    return e ? atoi(e) : 0;
-  }();
-  HIP_TRY(hipEventRecord(c->kev[3], c->stream3));
-  hipLaunchKernelGGL(sha_prio == 2 ? k_bd_sha_p2 : k_bd_sha, dim3((uint32_t)(((uint64_t)N * (SHA_E_LANES + 3) + 63) / 64)), dim3(64), 0, c->stream3, N,
-                     dtx, dbs, c->bj_dig.as<uint8_t>(), nblk);
-  HIP_TRY(hipEventRecord(c->ev_pay[2], c->stream3));
-  HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_pay[2], 0));
-  HIP_TRY(hipEventRecord(c->ev_pay[1], c->stream2));  // every digest is ready
-  HIP_TRY(hipEventRecord(c->kev[4], st));
-  hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 + 255) / 256)), dim3(256), 0, st, N, dtx, dbs, ch,
-                     did);
-  hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, ch, did, dj, misc);
-  HIP_TRY(hipEventRecord(c->kev[5], st));
-  HIP_TRY(hipGetLastError());
-  uint32_t *hm = c->hb_misc.as<uint32_t>();
-  HIP_TRY(hipMemcpyAsync(hm, misc, 32, hipMemcpyDeviceToHost, st));
-  if (c->next.n) {  // the next batch's framing walk, while this batch's parse runs on the GPU
-    fgv_block_presplit(S, c->device, c->next.n, c->next.blocks, c->next.lens, c->next.lo, c->next.hi);
+  // the next batch's framing walk, on the host worker while this batch's front half finishes
+  if (nx.n) {
+    fgv_block_presplit(S, c->device, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi);
     c->next.n = 0;
   }
-  HIP_TRY(hipStreamSynchronize(st));
+  HIP_TRY(hipEventSynchronize(B.ev[6]));
+  const uint32_t *hm = B.misc.as<uint32_t>();
   if (hm[5] & 1u) return 1;  // capacity overflow: host parser
   const size_t nv = (size_t)hm[BJ_C] + hm[BJ_E];
   c->t_bd_pre = ms_since(t1);
   c->t_host_assemble = c->t_bd_pre;
   auto t2 = clk::now();
+  // --- back half on the main stream
+  hipStream_t st = c->stream;
+  const DevChannel ch = S->dimg.ch;
+  uint32_t *misc = reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff);
+  const uint64_t *dbs = reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff);
+  DevTx *dtx = B.tx.as<DevTx>();
+  int32_t *did = B.ident.as<int32_t>();
+  DevJobIdx *dj = B.jobs.as<DevJobIdx>();
   if (!c->bj_sigp.ensure(nv * 20 + 64) || !c->bj_vst.ensure(nv + 64)) return FGV_ENOMEM;
   uint8_t *sp = c->bj_sigp.as<uint8_t>();
+  HIP_TRY(hipStreamWaitEvent(st, B.ev[6], 0));
   HIP_TRY(hipEventRecord(c->kev[6], st));
   hipLaunchKernelGGL(k_bd_emit, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
                      reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + nv * 8),
                      reinterpret_cast<uint32_t *>(sp + nv * 12), reinterpret_cast<uint32_t *>(sp + nv * 16));
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->kev[7], st));
-  c->digests_ready = c->ev_pay[3];
-  c->digests_ready2 = c->ev_pay[2];
-  int rc = fgv_run_block_jobs_device(c, 0, nv, 0);
+  c->digests_ready = B.ev[1];
+  c->digests_ready2 = B.ev[2];
+  int rc = fgv_run_block_jobs_device(c, 0, nv, 0, 0, B.dig.as<uint8_t>());
   c->digests_ready = c->digests_ready2 = nullptr;
   if (rc) return rc;
   // joined even when there is nothing to verify
-  HIP_TRY(hipStreamWaitEvent(st, c->ev_pay[3], 0));
-  HIP_TRY(hipStreamWaitEvent(st, c->ev_pay[2], 0));
+  HIP_TRY(hipStreamWaitEvent(st, B.ev[1], 0));
+  HIP_TRY(hipStreamWaitEvent(st, B.ev[2], 0));
   HIP_TRY(hipEventRecord(c->kev[8], st));
   hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
-                     c->bj_dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5);
+                     B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->kev[9], st));
-  HIP_TRY(hipMemcpyAsync(hm, misc, 48, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(B.misc.p, misc, 48, hipMemcpyDeviceToHost, st));
+  // --- the next batch's front half, ahead of its call, while this back half runs: its
+  // device copy is known (caller-resident, or being prefetched by the copy stream)
+  // Measured on MI355X (C2, 32 x 500-tx batches): every overlap placement loses.
+  // k_point28 is VALU-issue-bound (64-bit MADs) and the front half's SHA-256 chains are VALU
+  // work too, so running them side by side stretches both; the byte-walking kernels slow each
+  // other through memory latency.  Step times: not ahead 0.91 ms; enqueued at once (2) 0.92-0.94;
+  // after this batch's ECDSA (1) 1.01; after its fold (3) 1.05.  So the default keeps one batch
+  // on the GPU at a time (the next batch's framing is still pre-split on the host meanwhile);
+  // fgv_set_ahead / FGV_AHEAD=1/2/3 selects a placement (A/B).
+  const int ahead_mode = c->ahead_mode;
+  if (nx.n && nx.d_blocks && ahead_mode) {
+    BdSet &A = S->set[cur ^ 1];
+    hipEvent_t after = (ahead_mode == 1 && c->stage_ran) ? c->ev[6] : ahead_mode == 3 ? c->kev[9] : nullptr;
+    if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, nx.wait, after) == FGV_OK)
+      S->ahead = cur ^ 1;
+    else
+      drain_ahead(c, S), S->ahead = -1;  // (the next call starts it again and reports any error)
+  }
   HIP_TRY(hipStreamSynchronize(st));
   fgv_read_block_job_times(c);
   {  // per-kernel device times (fgv_last_kernel_times)
@@ -1266,20 +1400,17 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
       float ms = 0;
       return hipEventElapsedTime(&ms, a, b) == hipSuccess ? (double)ms : 0.0;
     };
-    c->t_kern[0] = el(c->kev[0], c->ev_pay[3]);  // k_bd_sha_payload
-    c->t_kern[1] = el(c->kev[1], c->kev[2]);     // k_bd_parse
-    c->t_kern[2] = el(c->kev[3], c->ev_pay[2]);  // k_bd_sha
-    c->t_kern[3] = el(c->kev[4], c->kev[5]);     // k_bd_ident + k_bd_count
-    c->t_kern[4] = el(c->kev[6], c->kev[7]);     // k_bd_emit
+    c->t_kern[0] = el(B.ev[3], B.ev[1]);      // k_bd_sha_payload
+    c->t_kern[1] = el(B.ev[3], B.ev[4]);      // k_bd_parse
+    c->t_kern[2] = el(B.ev[5], B.ev[2]);      // k_bd_sha
+    c->t_kern[3] = el(B.ev[7], B.ev[6]);      // k_bd_ident + k_bd_count (+ the counters' read-back)
+    c->t_kern[4] = el(c->kev[6], c->kev[7]);  // k_bd_emit
     c->t_kern[5] = c->stage_ran ? el(c->ev[2], c->ev[3]) : 0.0;  // k_der + k_inv
     c->t_kern[6] = c->stage_ran ? el(c->ev[4], c->ev[5]) : 0.0;  // k_prep
     c->t_kern[7] = c->stage_ran ? el(c->ev[5], c->ev[6]) : 0.0;  // k_point28 (+ k_point hand-overs)
-    c->t_kern[8] = el(c->kev[8], c->kev[9]);     // k_bd_fold
-    c->t_kern[9] = el(c->ev_pay[0], c->kev[9]);  // the batch, first kernel to last
-  }
-  {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev_pay[0], c->ev_pay[1]) == hipSuccess) c->t_sha += ms;
+    c->t_kern[8] = el(c->kev[8], c->kev[9]);  // k_bd_fold
+    c->t_kern[9] = el(B.ev[0], c->kev[9]);    // the batch, head upload to fold
+    c->t_sha = std::max(c->t_kern[0], el(B.ev[3], B.ev[2]));
   }
   uint64_t nb, np;
   memcpy(&nb, hm + 6, 8);

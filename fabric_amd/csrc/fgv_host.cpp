@@ -7,6 +7,7 @@
 //   dev:  [k_keytab for keys not yet cached] -> [k_sha256] -> k_prep -> k_point
 //   D2H:  status (1 B/item)
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <array>
@@ -66,7 +67,21 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   if (!c) return FGV_ENOMEM;
   c->device = cfg ? cfg->device : 0;
   c->key_slots = (cfg && cfg->key_slots) ? cfg->key_slots : 4096;
-  c->blk = fgv_block_state_new((cfg && cfg->host_threads) ? cfg->host_threads : 24);  // measured: tools/sweep_threads.sh
+  // host workers: fgv_config.host_threads, else min(24, this process's CPU share) -- 24 measured
+  // best on a whole machine (tools/sweep_threads.sh); eight ranks on one node each get their
+  // affinity mask's share, not the whole machine
+  unsigned share = 0;
+  {
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) share = (unsigned)CPU_COUNT(&cs);
+    if (const char *e = getenv("OMP_NUM_THREADS")) {
+      const int v = atoi(e);
+      if (v > 0 && (share == 0 || (unsigned)v < share)) share = (unsigned)v;
+    }
+  }
+  const unsigned dflt = share ? std::min(24u, share) : 24u;
+  c->blk = fgv_block_state_new((cfg && cfg->host_threads) ? cfg->host_threads : dflt);
+  if (const char *e = getenv("FGV_AHEAD")) c->ahead_mode = std::max(0, std::min(3, atoi(e)));
   auto fail = [&](int e) {
     fgv_destroy(c);
     return e;
@@ -81,6 +96,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
+    if (hipStreamCreateWithPriority(&c->streamF, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
   }
   if (hipEventCreateWithFlags(&c->pf.ev, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
   {
@@ -88,8 +104,6 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     c->fin_seed = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)(uintptr_t)c;
   }
   for (auto &e : c->ev)
-    if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
-  for (auto &e : c->ev_pay)
     if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
   for (auto &e : c->kev)
     if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
@@ -121,6 +135,8 @@ void fgv_destroy(fgv_ctx *c) {
   if (!c) return;
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+  for (hipStream_t x : {c->stream2, c->stream3, c->streamF})  // (a front half enqueued ahead)
+    if (x) hipStreamSynchronize(x);
   DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
                  &c->bd_misc, &c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
@@ -138,14 +154,13 @@ void fgv_destroy(fgv_ctx *c) {
   for (auto *b : h) b->release();
   for (auto &e : c->ev)
     if (e) hipEventDestroy(e);
-  for (auto &e : c->ev_pay)
-    if (e) hipEventDestroy(e);
   for (auto &e : c->kev)
     if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream3) hipStreamDestroy(c->stream3);
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+  if (c->streamF) hipStreamDestroy(c->streamF);
   if (c->pf.ev) hipEventDestroy(c->pf.ev);
   delete c;
 }
@@ -235,7 +250,9 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
                      c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>(), redo);  // (k_prep zeroes *redo)
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[5], c->stream));
-  // Persistent grid: one POINT_THREADS workgroup per CU.  Lanes per verify L (1, 2, 4, 8):
+  // Grid: two POINT_THREADS workgroups per CU (2 waves per SIMD) taking chunks of items from a
+  // device counter (k_point*: waves placed late, beside a next batch's front half, take fewer).
+  // Lanes per verify L (1, 2, 4, 8):
   // k_point28 is VALU-bound; a wave carries ceil(NTERMS / L) comb terms plus log2(L) tree
   // additions (~1.5 mixed-addition equivalents each).  A SIMD running one wave issues at about
   // half rate (dependent-issue latency), two or more share it at full rate, so the batch time
@@ -245,7 +262,7 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
     const char *e = getenv("FGV_POINT_LANES");
     return e ? atoi(e) : 0;
   }();
-  const uint64_t simds = (uint64_t)c->n_cu * 4, slots = (uint64_t)c->n_cu * (POINT_THREADS / 64);
+  const uint64_t simds = (uint64_t)c->n_cu * 4, slots = (uint64_t)c->n_cu * 2 * (POINT_THREADS / 64);
   uint32_t L = 1;
   double best = 1e30;
   for (uint32_t l = 1, lg = 0; l <= POINT_LANES_MAX; l <<= 1, lg++) {
@@ -258,10 +275,10 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
   if (forced >= 1 && forced <= POINT_LANES_MAX) L = (uint32_t)forced;
 
   if (redo) {
-    hipLaunchKernelGGL(k_point28, dim3(c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, L, d_status, d_slot,
+    hipLaunchKernelGGL(k_point28, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, L, d_status, d_slot,
                        c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   }
-  hipLaunchKernelGGL(k_point, dim3(c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, L, d_status, d_slot,
+  hipLaunchKernelGGL(k_point, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, L, d_status, d_slot,
                      c->gtab.as<apoint_raw>(), c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   c->last_lanes = L;
   HIP_TRY(hipGetLastError());
@@ -658,7 +675,9 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
 // Device-resident variant (blockdev path): the jobs were written by k_bd_emit straight into
 // c->bj_jobs / c->bj_sigp (layout of fgv_block_jobs_reserve); digests stay in c->bj_dig and
 // verify status in c->bj_vst.  Enqueued on c->stream; no host copies, no synchronisation.
-int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, size_t dig_off) {
+int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, size_t dig_off,
+                              const uint8_t *dig) {
+  const uint8_t *digs = dig ? dig : c->bj_dig.as<uint8_t>();
   c->n_sha_jobs = nj;
   c->n_verifies = nv;
   c->n_sha_blocks = sha_blocks;
@@ -696,7 +715,7 @@ int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blo
     const uint32_t N = (uint32_t)nv;
     const uint8_t *dsig = c->bj_sigp.as<uint8_t>();
     int rc = launch_prep_point(c, N, c->bj_vst.as<uint8_t>(), reinterpret_cast<const uint32_t *>(dsig + nv * 12),
-                               c->r.as<uint32_t>(), c->bj_dig.as<uint8_t>(),
+                               c->r.as<uint32_t>(), digs,
                                reinterpret_cast<const uint32_t *>(dsig + nv * 16));
     if (rc) return rc;
     ran = true;
@@ -889,7 +908,9 @@ static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks
       return FGV_OK;
     }
   }
-  // copy now, into the arena no prefetch is writing (64 B padding after each block)
+  // copy now, into the arena no prefetch is writing (64 B padding after each block).  A front
+  // half enqueued ahead reads the prefetched arena, which this call's own prefetch may reuse.
+  if (c->pf.on) fgv_block_drain(c);
   const int slot = c->pf.on ? 1 - c->pf.slot : c->stage_cur;
   c->pf.on = false;
   DevBuf &A = c->stage[slot];
@@ -971,12 +992,10 @@ int fgv_validate_shard(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks,
                                  results_cap, ntx);
 }
 
-int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
-                           const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
-                           void *d_results, size_t results_cap, size_t *ntx) {
-  if (!c || (nblocks && (!blocks || !lens || !ntx || (results_cap && !d_results)))) return FGV_EINVAL;
+static int shard_dev_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                            const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                            void *d_results, size_t results_cap, size_t *ntx) {
   if (nblocks == 0) return FGV_OK;
-  std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
   std::vector<const uint8_t *> dev;
   int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
@@ -984,6 +1003,8 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   if (c->next.n && c->next.prefetch) {
     rc = prefetch_blocks(c, c->next.n, c->next.blocks, c->next.lens);
     if (rc) return rc;
+    c->next.d_blocks = c->pf.dev.data();  // its front half can be enqueued ahead of its call
+    c->next.wait = c->pf.ev;
   }
   if (fgv_block_parse_mode(c->blk) == 0) {
     rc = fgv_block_validate_dev(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi,
@@ -1002,25 +1023,54 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   return FGV_OK;
 }
 
+int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                           const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                           void *d_results, size_t results_cap, size_t *ntx) {
+  if (!c || (nblocks && (!blocks || !lens || !ntx || (results_cap && !d_results)))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->next = fgv_ctx::NextBatch{};
+  return shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+}
+
+int fgv_validate_shard_dev_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                     const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                                     void *d_results, size_t results_cap, size_t *ntx, size_t next_nblocks,
+                                     const uint8_t *const *next_blocks, const size_t *next_lens,
+                                     const uint8_t *const *next_d_blocks, const uint32_t *next_lo,
+                                     const uint32_t *next_hi) {
+  if (!c || (nblocks && (!blocks || !lens || !ntx || (results_cap && !d_results))) ||
+      (next_nblocks && (!next_blocks || !next_lens)))
+    return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  // a host-resident next batch travels H2D now (copy stream) when this batch is host-resident
+  // too; a device-resident one (next_d_blocks) is read in place
+  c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks,   next_lens, next_lo, next_hi,
+                               !next_d_blocks && !d_blocks, next_d_blocks, nullptr};
+  int rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  if (c->next.n) {  // not started inside (host-parse path, empty batch, early error): start it now
+    fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, c->next.lo, c->next.hi);
+  }
+  c->next = fgv_ctx::NextBatch{};
+  return rc;
+}
+
 int fgv_validate_shard_dev_next(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                                 const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
                                 void *d_results, size_t results_cap, size_t *ntx, size_t next_nblocks,
                                 const uint8_t *const *next_blocks, const size_t *next_lens, const uint32_t *next_lo,
                                 const uint32_t *next_hi) {
-  if (!c || (next_nblocks && (!next_blocks || !next_lens))) return FGV_EINVAL;
-  {
-    std::lock_guard<std::mutex> g(c->mu);
-    // the next batch's bytes travel H2D now only when this batch is host-resident too (a
-    // caller holding device copies passes d_blocks for both)
-    c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks, next_lens, next_lo, next_hi, d_blocks == nullptr};
-  }
-  int rc = fgv_validate_shard_dev(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  return fgv_validate_shard_dev_pipelined(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap,
+                                          ntx, next_nblocks, next_blocks, next_lens, nullptr, next_lo, next_hi);
+}
+
+int fgv_last_ahead(fgv_ctx *c) { return c && c->last_ahead ? 1 : 0; }
+
+int fgv_set_ahead(fgv_ctx *c, int mode) {
+  if (!c || mode < 0 || mode > 3) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->next.n) {  // not started inside (host-parse path, empty batch, early error): start it now
-    fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, c->next.lo, c->next.hi);
-    c->next.n = 0;
-  }
-  return rc;
+  fgv_block_drain(c);  // (a front half already enqueued ahead is discarded)
+  c->ahead_mode = mode;
+  return FGV_OK;
 }
 
 int fgv_presplit(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens, const uint32_t *tx_lo,

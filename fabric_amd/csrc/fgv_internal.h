@@ -93,8 +93,7 @@ struct fgv_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // k_der + k_inv of a block batch, concurrent with SHA-256
   hipStream_t stream3 = nullptr;  // the device-parse committer's non-payload SHA-256 (k_bd_sha)
-  hipEvent_t ev_pay[4] = {};      // [0] batch start, [1] all digests ready (stream2), [2] k_bd_sha done (stream3),
-                                  // [3] k_bd_sha_payload done (stream2)
+  hipStream_t streamF = nullptr;  // the device-parse committer's front half (parse, identities, job counts)
   hipEvent_t ev[8] = {};          // 0/1 sha, 2/3 inv, 4/5 prep, 6 point end, 7 fork
   hipEvent_t kev[12] = {};        // per-kernel brackets of the device-parse committer (fgv_last_kernel_times)
   double t_kern[12] = {};
@@ -143,7 +142,11 @@ struct fgv_ctx {
     const size_t *lens = nullptr;
     const uint32_t *lo = nullptr, *hi = nullptr;
     bool prefetch = false;  // also queue its H2D copy (host-resident batches)
+    const uint8_t *const *d_blocks = nullptr;  // its device copy (known: its front half is enqueued ahead)
+    hipEvent_t wait = nullptr;                 // ... once this event (the prefetch copy) has fired
   } next;
+  bool last_ahead = false;  // the last device-parse call found its front half enqueued ahead
+  int ahead_mode = 0;       // fgv_set_ahead: 0 off, 1 after the ECDSA kernels, 2 at once, 3 after the fold
   // host-resident batches: two device staging arenas; fgv_validate_shard_dev_next copies the
   // NEXT batch into the idle one on the copy stream while this batch's kernels run
   DevBuf stage[2];
@@ -206,7 +209,11 @@ int fgv_block_jobs_reserve(fgv_ctx *c, size_t nj, size_t nv, BlockJobs *out);
 int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, const uint8_t **digests,
                        const uint8_t **vstatus);
 // device-resident variant: jobs already in c->bj_jobs / c->bj_sigp; results stay in HBM
-int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, size_t dig_off = 0);
+// dig: the digest buffer (default c->bj_dig)
+int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, size_t dig_off = 0,
+                              const uint8_t *dig = nullptr);
+// wait for (and forget) a device-parse front half enqueued ahead of its call
+void fgv_block_drain(fgv_ctx *c);
 void fgv_read_block_job_times(fgv_ctx *c);
 int fgv_block_set_parse_mode(fgv_block_state *S, int mode);
 int fgv_block_presplit(fgv_block_state *S, int device, size_t nblocks, const uint8_t *const *h_blocks,

@@ -27,7 +27,7 @@
 #define NTERMS (NGWIN + NWIN)         // comb terms per verify: 17 G + 26 Q
 #define DIG_Q_OFF 40                  // digit array item: G digits int16 x 17 at 0, Q digits int16 x 26 here
 #define PREP_B 2                            // items per lane in the batched inversion
-#define POINT_THREADS 512   // 8 waves per CU (2 per SIMD): up to 256 VGPRs, no spills
+#define POINT_THREADS 256   // 4 waves per workgroup, 2 x n_cu workgroups: 2 waves per SIMD, <= 256 VGPRs
 #define POINT_LANES_MAX 8    // lanes cooperating on one verify in k_point (partial sums + tree)
 #define DIG_STRIDE 96        // bytes per item of the digit array (G digits, then Q digits at DIG_Q_OFF)
 #define ST_PENDING 0xFF
@@ -51,7 +51,7 @@ __global__ void k_inv(uint32_t n, uint8_t *status, const uint32_t *key_slot, con
 __global__ void k_prep(uint32_t n, const uint8_t *status, const uint32_t *r_limbs, const uint32_t *w_in,
                        const uint8_t *digests, const uint32_t *dig_idx, int8_t *digits, uint32_t *redo);
 __global__ void k_point(uint32_t n, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot, const apoint_raw *gtab,
-                        const apoint_raw *ktab, const int8_t *digits, const uint32_t *r_limbs, const uint32_t *redo);
+                        const apoint_raw *ktab, const int8_t *digits, const uint32_t *r_limbs, uint32_t *redo);
 __global__ void k_point28(uint32_t n, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot,
                           const apoint_raw *gtab28, const apoint_raw *ktab28, const int8_t *digits,
                           const uint32_t *r_limbs, uint32_t *redo);

@@ -357,7 +357,11 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restr
                                               int8_t *__restrict__ digits, uint32_t *__restrict__ redo) {
   __builtin_amdgcn_s_setprio(3);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0 && redo) *redo = 0u;  // k_point28's hand-over count (read by k_point)
+  if (i == 0 && redo) {  // k_point28's hand-over count (read by k_point) + both kernels' work counters
+    redo[0] = 0u;
+    redo[1] = 0u;
+    redo[2] = 0u;
+  }
   if (i >= n || status[i] != ST_PENDING) return;
   uint32_t w[8], r[8], e[8], u1[8], u2[8];
 #pragma unroll
@@ -420,23 +424,41 @@ FGV_DEV void shfl_fe(fe &r, const fe &a, int src_lane) {
 // idle); lane `sub` of a group sums windows sub, sub+L, ...; then a binary tree over the
 // group's lanes (level m: lane sub takes lane sub^m's sum when that lane exists), leaving the
 // total in lane 0.  Persistent grid: one workgroup per CU, groups stride over the items.
-__global__ __launch_bounds__(POINT_THREADS) void k_point(
+// Work distribution (k_point and k_point28): a wave takes chunks of gpw items (one per lane
+// group) from a device counter until they run out, so waves that start late -- a workgroup
+// placed only once another kernel's waves left the CU -- or run beside other kernels' waves
+// simply take fewer chunks.  counter == nullptr: static grid stride (no work-counter word).
+FGV_DEV bool next_chunk(uint32_t *counter, uint32_t &chunk, uint32_t waves, uint32_t gpw, uint32_t n) {
+  if (counter) {
+    uint32_t c = 0;
+    if ((threadIdx.x & 63u) == 0u) c = atomicAdd(counter, 1u);
+    chunk = __builtin_amdgcn_readfirstlane(c);
+  } else {
+    chunk += waves;
+  }
+  return (uint64_t)chunk * gpw < n;
+}
+
+__global__ __launch_bounds__(POINT_THREADS, 2) void k_point(
     uint32_t n, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
     const apoint_raw *__restrict__ gtab, const apoint_raw *__restrict__ ktab,
-    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, const uint32_t *__restrict__ redo) {
+    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo) {
   // after k_point28: only the items it left pending (exceptional additions) remain
   if (redo && *redo == 0u) return;
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t gpw = 64u / L;  // groups per wave
   const uint32_t g = lane / L, sub = lane % L;
-  if (g >= gpw) return;  // idle tail lanes of the wave (no barrier follows)
+  if (g >= gpw) return;  // idle tail lanes of the wave (no barrier follows; lane 0 stays)
   const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t groups = waves * gpw;
   const uint32_t base = lane - sub;  // lane of sub 0 in this group
+  uint32_t *ctr = redo ? redo + 2 : nullptr;
+  uint32_t chunk = blockIdx.x * (blockDim.x >> 6) + wave - waves;
   // every lane of a group runs the same iterations (item-uniform control flow), so the
   // cross-lane reads below always find their partners active
-  for (uint32_t i = (blockIdx.x * (blockDim.x >> 6) + wave) * gpw + g; i < n; i += groups) {
-    if (status[i] != ST_PENDING) continue;
+  while (next_chunk(ctr, chunk, waves, gpw, n)) {
+    const uint32_t i = chunk * gpw + g;
+    if (i >= n || status[i] != ST_PENDING) continue;
     const apoint_raw *qt = ktab + (size_t)key_slot[i] * KT_ENTRIES;
     const int8_t *dg = digits + (size_t)i * DIG_STRIDE;
     jpoint acc;
@@ -590,19 +612,21 @@ FGV_DEV void f28_to_mont(f28 &r, const uint32_t w[8]) {
   f28_mul(r, a, r2);
 }
 
-__global__ __launch_bounds__(POINT_THREADS) void k_point28(
+__global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
     uint32_t n, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
     const apoint_raw *__restrict__ gtab28, const apoint_raw *__restrict__ ktab28,
     const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo) {
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  __builtin_amdgcn_s_setprio(3);  // the verify chain; a next batch's front half may run beside it
+  const uint32_t lane = threadIdx.x & 63u;
   const uint32_t gpw = 64u / L;
   const uint32_t g = lane / L, sub = lane % L;
   if (g >= gpw) return;
   const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t groups = waves * gpw;
   const uint32_t base = lane - sub;
-  for (uint32_t i = (blockIdx.x * (blockDim.x >> 6) + wave) * gpw + g; i < n; i += groups) {
-    if (status[i] != ST_PENDING) continue;
+  uint32_t chunk = 0;
+  while (next_chunk(redo + 1, chunk, waves, gpw, n)) {
+    const uint32_t i = chunk * gpw + g;
+    if (i >= n || status[i] != ST_PENDING) continue;
     const apoint_raw *qt = ktab28 + (size_t)key_slot[i] * KT_ENTRIES;
     const int8_t *dg = digits + (size_t)i * DIG_STRIDE;
     jp28 acc;

@@ -8,6 +8,13 @@
 // dependency chains, so the per-lane latency that bounds k_inv drops ~6x.  Control flow is
 // input-independent (fixed trip counts, masks instead of branches): lanes never diverge.
 //
+// Attribution: the branch-free 30-divstep inner loop (divsteps_30: the c1/c2 masks of a
+// "zeta < 0 and g odd" swap-and-negate, then the conditional add and halving) and the signed
+// 30-bit limb layout follow libsecp256k1's modinv32 implementation (src/modinv32_impl.h,
+// secp256k1_modinv32_divsteps_30; MIT licence, (c) Pieter Wuille, Peter Dettman),
+// which restates the paper's algorithm; the rest (P-256 group order constants, the
+// matrix-application and normalisation code, the device batching) is ours.
+//
 // __host__ __device__ so the same code is checked on the host (tools/modinv_check.cpp)
 // against an independent big-integer inverse.
 #pragma once

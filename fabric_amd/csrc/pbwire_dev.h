@@ -18,16 +18,32 @@ struct S {  // absolute device span
   const uint8_t *p;
   uint32_t n;
 };
+
+// Message bytes are read a word at a time where the rules allow it: these kernels are bound by
+// chains of dependent loads (one lane walks one transaction), not by bandwidth, so reading 4 or
+// 16 bytes per load shortens the chains.  ld4: the 4 bytes at p (any alignment, little-endian)
+// from the two aligned dwords covering them -- independent loads.  Over-read contract: up to 7
+// bytes past a span's end (block arenas and the channel image carry >= 64 B of tail padding).
+DEV uint32_t ld4(const uint8_t *p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
+}
+DEV uint32_t lo_mask(uint32_t r) { return r >= 4u ? 0xFFFFFFFFu : ((1u << (8u * r)) - 1u); }
+
 DEV bool s_eq(S a, S b) {
   if (a.n != b.n) return false;
-  for (uint32_t i = 0; i < a.n; i++)
-    if (a.p[i] != b.p[i]) return false;
+  for (uint32_t i = 0; i < a.n; i += 4)
+    if ((ld4(a.p + i) ^ ld4(b.p + i)) & lo_mask(a.n - i)) return false;
   return true;
 }
-DEV bool s_lt(S a, S b) {  // byte-lexicographic (Go string order)
+DEV bool s_lt(S a, S b) {  // byte-lexicographic (Go string order): big-endian word compares
   const uint32_t m = a.n < b.n ? a.n : b.n;
-  for (uint32_t i = 0; i < m; i++)
-    if (a.p[i] != b.p[i]) return a.p[i] < b.p[i];
+  for (uint32_t i = 0; i < m; i += 4) {
+    const uint32_t k = lo_mask(m - i);
+    const uint32_t x = __builtin_bswap32(ld4(a.p + i) & k), y = __builtin_bswap32(ld4(b.p + i) & k);
+    if (x != y) return x < y;
+  }
   return a.n < b.n;
 }
 
@@ -35,7 +51,22 @@ enum Kind : uint8_t { K_NONE = 0, K_VARINT, K_BYTES, K_STRING, K_MSG, K_REP_MSG,
 
 DEV bool rd_varint(const uint8_t *&p, const uint8_t *e, uint64_t &v) {
   v = 0;
-  for (int i = 0; i < 10; i++) {
+  int i = 0;
+  if (e - p >= 4) {  // the first 4 bytes in one read (tags and lengths are 1-3 bytes)
+    const uint32_t w = ld4(p);
+    const uint32_t stop = ~w & 0x80808080u;  // bit 7 of byte k clear: the varint ends at k
+    if (stop) {
+      const uint32_t k = (uint32_t)__builtin_ctz(stop) >> 3;  // 0..3
+      const uint32_t b0 = w & 0x7Fu, b1 = (w >> 8) & 0x7Fu, b2 = (w >> 16) & 0x7Fu, b3 = (w >> 24) & 0x7Fu;
+      v = k == 0 ? b0 : k == 1 ? (b0 | b1 << 7) : k == 2 ? (b0 | b1 << 7 | b2 << 14) : (b0 | b1 << 7 | b2 << 14 | b3 << 21);
+      p += k + 1;
+      return true;
+    }
+    v = (w & 0x7Fu) | ((w >> 8) & 0x7Fu) << 7 | ((w >> 16) & 0x7Fu) << 14 | (uint64_t)((w >> 24) & 0x7Fu) << 21;
+    p += 4;
+    i = 4;
+  }
+  for (; i < 10; i++) {
     if (p >= e) return false;
     const uint8_t c = *p++;
     if (i == 9 && c > 1) return false;
@@ -92,6 +123,13 @@ DEV bool skip_value(const uint8_t *&p, const uint8_t *e, uint32_t num, int wt, b
 DEV bool utf8_valid(const uint8_t *s, uint32_t n) {  // Go utf8.Valid
   uint32_t i = 0;
   while (i < n) {
+    if (n - i >= 16) {  // ASCII runs 16 bytes per step (5 aligned dword loads)
+      const uint32_t w = ld4(s + i) | ld4(s + i + 4) | ld4(s + i + 8) | ld4(s + i + 12);
+      if (!(w & 0x80808080u)) { i += 16; continue; }
+    } else if (n - i >= 4 && !(ld4(s + i) & 0x80808080u)) {
+      i += 4;
+      continue;
+    }
     const uint8_t c = s[i];
     if (c < 0x80) { i++; continue; }
     uint32_t len, cp;

@@ -109,8 +109,11 @@ __device__ __forceinline__ void sha_view(const JobView &v, uint8_t *out) {
     const int k = s < v.beg[1] ? 0 : (s < v.beg[2] ? 1 : 2);
     fast = s + 64 <= v.beg[k + 1];
     if (fast) {
+      // global (not flat) loads: the 17 dwords merge into 4 x dwordx4 + 1 -- a quarter of the
+      // per-lane cache-line requests of dword loads, where 64 lanes read 64 scattered messages
       const uintptr_t a = reinterpret_cast<uintptr_t>(v.p[k] + (s - v.beg[k]));
-      const uint32_t *al = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+      const __attribute__((address_space(1))) uint32_t *al =
+          reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(a & ~(uintptr_t)3);
       sh = (uint32_t)(a & 3u);
 #pragma unroll
       for (int q = 0; q < 17; q++) raw[q] = al[q];

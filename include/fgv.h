@@ -265,6 +265,32 @@ int fgv_validate_shard_dev_next(fgv_ctx *ctx, size_t nblocks, const uint8_t *con
                                 size_t results_cap, size_t *ntx, size_t next_nblocks,
                                 const uint8_t *const *next_blocks, const size_t *next_lens,
                                 const uint32_t *next_lo, const uint32_t *next_hi);
+/* The committer pipeline: fgv_validate_shard_dev of the current batch that also enqueues the
+ * NEXT batch's front half -- envelope split, head upload, payload and message SHA-256, parse,
+ * identity resolution, job counts -- on the engine's side streams while the current batch's
+ * back half (verify jobs, ECDSA, policy fold) runs, so two batches are in flight on the GPU.
+ * The next call whose batch (host and device block addresses, lengths, tx_lo/tx_hi) is that
+ * one continues from it; any other call discards it.  next_d_blocks: the next batch's device
+ * copy (NULL: host-resident -- copied on the copy stream when the current batch is
+ * host-resident too, as fgv_validate_shard_dev_next does; else only pre-split).  The next
+ * batch's host and device buffers must stay valid and unchanged until that call.  Channel-model
+ * changes in between (identities, chaincodes, config) discard it; ledger txids added in between
+ * (fgv_ledger_add_txids) do not -- only k_bd_fold, in the back half, reads them.  Results never
+ * depend on whether a front half was enqueued ahead (fgv_last_ahead: it was, for the last call). */
+int fgv_validate_shard_dev_pipelined(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
+                                     const size_t *lens, const uint8_t *const *d_blocks,
+                                     const uint32_t *tx_lo, const uint32_t *tx_hi, void *d_results,
+                                     size_t results_cap, size_t *ntx, size_t next_nblocks,
+                                     const uint8_t *const *next_blocks, const size_t *next_lens,
+                                     const uint8_t *const *next_d_blocks, const uint32_t *next_lo,
+                                     const uint32_t *next_hi);
+int fgv_last_ahead(fgv_ctx *ctx);
+/* Where the next batch's front half is enqueued by fgv_validate_shard_dev_pipelined: 0 = not
+ * ahead (default; the environment variable FGV_AHEAD sets the initial value): one batch on the
+ * GPU at a time, the next one pre-split on the host -- the fastest on MI355X for C2-shaped
+ * batches; 1 = once the current batch's ECDSA kernels are done; 2 = at once;
+ * 3 = once its policy fold is done.  Results never depend on it. */
+int fgv_set_ahead(fgv_ctx *ctx, int mode);
 /* Page-locked host memory for block buffers (hipHostMalloc): H2D copies from it run on the copy
  * engine at PCIe rate, asynchronously.  fgv_last_h2d: bytes the last validation call copied
  * itself, and blocks it found already copied by the previous call's prefetch. */

@@ -425,3 +425,98 @@ def test_device_capacity_overflow_falls_back_to_host_parser():
     exp = _check(eng, net, [block_from_envs(envs + [env], number=1)])
     assert exp[0][-1] == 10
     eng.close()
+
+
+def _device_copies(blks):
+    import torch
+    sizes = [(len(b) + 64 + 255) // 256 * 256 for b in blks]
+    arena = torch.zeros(max(1, sum(sizes)), dtype=torch.uint8, device="cuda")
+    ptrs, o = [], 0
+    for b, sz in zip(blks, sizes):
+        if len(b):
+            arena[o:o + len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+        ptrs.append(arena.data_ptr() + o)
+        o += sz
+    return arena, ptrs
+
+
+def _flags(eng, batch, ntx, res, cap, nxt, lo=None, hi=None):
+    lo = [0] * batch.nb if lo is None else lo
+    hi = [1 << 30] * batch.nb if hi is None else hi
+    nt = eng.validate_shard_dev_pipelined(batch, lo, hi, res.data_ptr(), cap, nxt, [0] * nxt.nb,
+                                          [1 << 30] * nxt.nb)
+    return list(eng.finalize_flags_dev(nt, 1, cap, res.data_ptr()))
+
+
+def test_pipelined_front_half_ahead_rotation():
+    """fgv_validate_shard_dev_pipelined over HBM-resident batches A, B, C, A, ...: each call
+    enqueues the next batch's front half (parse, identities, hashes) while its own back half
+    runs; every following call continues from it (fgv_last_ahead) and the flags equal the
+    oracle's.  A call for a batch other than the announced one discards the front half."""
+    import torch
+    net = network()
+    sizes = [[23, 5], [31], [9, 17, 3]]
+    sets, exps, keep = [], [], []
+    eng = _engine_for(net)
+    for k, sz in enumerate(sizes):
+        blks = [blocks.make_block(net, n, number=1 + i, seed=400 + 10 * k + i)[0] for i, n in enumerate(sz)]
+        arena, ptrs = _device_copies(blks)
+        keep.append(arena)
+        sets.append(eng.block_batch(blks, ptrs))
+        exps.append([f for fl in _oracle(net, blks) for f in fl])
+    res = torch.zeros((64, _lib.TX_RESULT_BYTES), dtype=torch.uint8, device="cuda")
+    order = [0, 1, 2, 0, 0, 2, 1, 1, 2]
+    for mode in (0, 3, 1, 2):  # 0: never ahead (the default); the others place it differently
+        eng.set_ahead(mode)
+        for i, k in enumerate(order):
+            nxt = order[i + 1] if i + 1 < len(order) else 0
+            got = _flags(eng, sets[k], None, res, 64, sets[nxt])
+            assert eng.last_ahead() == (mode > 0 and i > 0), (mode, i)
+            assert got == exps[k], (mode, i, k)
+    # the announced batch is 0; a call for batch 1 discards it and starts its own
+    assert _flags(eng, sets[1], None, res, 64, sets[2]) == exps[1]
+    assert not eng.last_ahead()
+    # a shard range other than the announced one is another batch too
+    lo, hi = [0, 4, 0], [9, 17, 3]
+    nt = eng.validate_shard_dev_pipelined(sets[2], lo, hi, res.data_ptr(), 64, sets[2], lo, hi)
+    assert not eng.last_ahead()
+    nt = eng.validate_shard_dev_pipelined(sets[2], lo, hi, res.data_ptr(), 64, sets[0])
+    assert eng.last_ahead()
+    assert list(nt) == [9, 17, 3]
+    eng.close()
+
+
+def test_pipelined_ahead_and_channel_or_ledger_changes():
+    """Between two pipelined calls: ledger txids added (fgv_ledger_add_txids) keep the front
+    half enqueued ahead (only the back half reads them) and its duplicates come out as 9; a
+    chaincode redefinition discards it and the new policy applies -- both equal the oracle."""
+    import torch
+    net = network()
+    a = [blocks.make_block(net, n, number=1 + i, seed=500 + i)[0] for i, n in enumerate([20, 11])]
+    b = [blocks.make_block(net, n, number=3 + i, seed=510 + i)[0] for i, n in enumerate([15, 8])]
+    eng = _engine_for(net)
+    eng.set_ahead(2)
+    aa, ap = _device_copies(a)
+    ba, bp = _device_copies(b)
+    A, Bt = eng.block_batch(a, ap), eng.block_batch(b, bp)
+    res = torch.zeros((64, _lib.TX_RESULT_BYTES), dtype=torch.uint8, device="cuda")
+    assert _flags(eng, A, None, res, 64, Bt) == [f for fl in _oracle(net, a) for f in fl]
+    # the ledger already holds some of B's txids
+    txids = []
+    for blk in b:
+        for env in v20.decode("Block", blk)["data"]["data"][:4]:
+            pl = v20.decode("Payload", v20.decode("Envelope", env)["payload"])
+            txids.append(v20.decode("ChannelHeader", pl["header"]["channel_header"])["tx_id"])
+    eng.ledger_add_txids(txids)
+    got = _flags(eng, Bt, None, res, 64, A)
+    assert eng.last_ahead()
+    exp = [f for fl in _oracle(net, b, committed=txids) for f in fl]
+    assert got == exp and exp.count(9) >= 4
+    # the chaincode's policy changes: 3-of-3 -> the front half enqueued for A is discarded
+    pol = blocks.out_of_policy(3, net.mspids)
+    eng.chaincode_define("mycc", pol)
+    got = _flags(eng, A, None, res, 64, A)
+    assert not eng.last_ahead()
+    m = v20.ChannelModel(net.channel, net.identities(), dict(net.chaincodes, mycc=pol), txids)
+    assert got == [f for fl in v20.validate_blocks(m, a) for f in fl]
+    eng.close()

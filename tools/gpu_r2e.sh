@@ -1,0 +1,17 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r2e
+mkdir -p $O
+true
+tail -2 $O/tests.log
+for a in 1 2 0; do
+FGV_AHEAD=$a timeout -k 10 300 python -u bench.py --cpu-threads 0 --no-latency --no-pcie > $O/bench_$a.json 2> $O/bench_$a.err || { echo bench failed; tail -30 $O/bench_$a.err; exit 1; }
+done
+python3 - <<'PY'
+import json
+for f in ("1", "2", "0"):
+    d = json.load(open(f"gpurun_out/r2e/bench_{f}.json"))
+    print(f, d["value"], d["ms_per_step"], d["parity_vs_labels"], d["kernel_ms"], d["host_ms"])
+PY
