@@ -75,6 +75,8 @@ __global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_
 #define MVR_HASVER 1u   // read: has a version
 #define MVR_DELETE 1u   // write: is a delete
 #define MVR_HASHED 2u   // private-data key: namespace = ns + "$$h" + coll
+#define MV_UNSUP_RQ 2u  // MvCounters.unsup bit: range queries present -> the host phantom path
+#define MVRANGE_UNBOUNDED 1u  // MvRange.flags: end key "" (to the end of the namespace)
 #define MV_TAG_OCC 1ull      // tag bit 0: slot occupied (tags are never 0)
 #define MV_TAG_PRESENT 2ull  // committed-state tag bit 1: the key exists (clear = deleted)
 struct MvRec {  // one read or write: spans into the block (or a host-supplied key arena)
@@ -134,6 +136,14 @@ __global__ void k_mv_upsert_insert(uint32_t mode, uint32_t rlast, uint32_t n_hos
                                    const MvRec *recs, const uint8_t *pend, StateSlot *tbl, uint64_t mask, uint8_t *arena,
                                    unsigned long long *top, uint64_t block_num, const MvCounters *c);
 __global__ void k_mv_tags(const uint8_t *base, MvRec *recs, uint32_t n);
+struct MvRange {  // a range query's scan bounds (bytes in a host-built buffer)
+  uint32_t ns_off, ns_len, s_off, s_len, e_off, e_len, flags, pad;
+};
+__global__ void k_mv_lookup(uint32_t n, const uint8_t *base, const MvRec *recs, const StateSlot *tbl, uint64_t mask,
+                            const uint8_t *arena, uint64_t *ver, uint8_t *present);
+__global__ void k_mv_range_scan(uint64_t cap, const StateSlot *tbl, const uint8_t *arena, uint32_t nranges,
+                                const MvRange *ranges, const uint8_t *rbytes, uint8_t *out, uint64_t out_cap,
+                                unsigned long long *used);
 
 // finalize.hip -- batch txid index + markTXIdDuplicates over gathered fgv_tx_result records
 __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, uint32_t W, uint32_t rows,

@@ -15,14 +15,17 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <string>
 #include <string_view>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
 #include "../../include/fgv.h"
 #include "fgv_internal.h"
 #include "fgv_visitors.h"
+#include "sha256_host.h"
 
 bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t len, std::vector<Span> &out);
 
@@ -40,6 +43,7 @@ struct fgv_mvcc_state {
   DevBuf tbl, arena, top;              // top: [0] arena bytes used, [1] occupied slots
   DevBuf head, info, reads, writes, btbl, wslot, rslot, bad, st, pend, tail;
   DevBuf lrecs, lbytes;                // load / apply staging
+  DevBuf qver, qpres, qrange, qout;    // phantom path: lookups and range scans
   HostBuf hhead, htail;
   std::vector<Span> pre_envs;          // envelope spans taken from a pre-split
   uint32_t epoch = 0;                  // block-table epoch (BlkSlot.owner)
@@ -51,7 +55,8 @@ struct fgv_mvcc_state {
 void fgv_mvcc_free(fgv_mvcc_state *M) {
   if (!M) return;
   DevBuf *d[] = {&M->tbl, &M->arena, &M->top, &M->head, &M->info, &M->reads, &M->writes, &M->btbl, &M->wslot,
-                 &M->rslot, &M->bad, &M->st, &M->pend, &M->tail, &M->lrecs, &M->lbytes};
+                 &M->rslot, &M->bad, &M->st, &M->pend, &M->tail, &M->lrecs, &M->lbytes, &M->qver, &M->qpres,
+                 &M->qrange, &M->qout};
   for (auto *b : d) b->release();
   M->hhead.release();
   M->htail.release();
@@ -188,6 +193,618 @@ int fgv_statedb_stats(fgv_ctx *c, uint64_t *keys, uint64_t *arena_used, uint64_t
 
 }  // extern "C"
 
+// ======================================================================= phantom path
+// A block with range queries (validator.go:205-244) is validated here, in block order, exactly
+// as validateAndPrepareBatch does (validator.go:81-162): per namespace public reads (11), range
+// queries (PHANTOM_READ_CONFLICT 12), hashed reads (11); a valid tx's writes enter the update
+// batch at Height{block, tx}.  The device pass already classified every transaction (codes 16 /
+// 255, committer-invalid skips, unsupported shapes) and located its TxReadWriteSet; the
+// committed versions come from the GPU table (k_mv_lookup), the committed keys of each range
+// from one scan of it (k_mv_range_scan).  The combined iterator (combined_iterator.go), the raw
+// and the merkle-hash validators (rangequery_validator.go, rwsetutil/query_results_helper.go)
+// are restated below.
+namespace {
+
+using pbw::Kind;
+using pbw::K_BYTES;
+using pbw::K_MSG;
+using pbw::K_NONE;
+using pbw::K_REP_BYTES;
+using pbw::K_REP_MSG;
+using pbw::K_STRING;
+using pbw::K_VARINT;
+
+// host visitors with the field rules of mvcc.hip's (the device walked these rwsets cleanly)
+struct HVer {
+  uint64_t b = 0, t = 0;
+  Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_VARINT : K_NONE; }
+  void on_varint(uint32_t n, uint64_t v) { (n == 1 ? b : t) = v; }
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct HRead {
+  bool hashed = false;
+  Span key;
+  bool has_ver = false;
+  HVer v;
+  Kind kind(uint32_t n) { return n == 1 ? (hashed ? K_BYTES : K_STRING) : n == 2 ? K_MSG : K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { key = s; return true; }
+    has_ver = true;
+    return pbw::decode(s.p, s.n, v);
+  }
+};
+struct HWrite {
+  bool hashed = false;
+  Span key, val;
+  bool del = false;
+  Kind kind(uint32_t n) {
+    if (n == 1) return hashed ? K_BYTES : K_STRING;
+    if (n == 2) return K_VARINT;
+    if (n == 3) return K_BYTES;
+    return (hashed && n == 4) ? K_VARINT : K_NONE;
+  }
+  void on_varint(uint32_t n, uint64_t v) { if (n == 2) del = v != 0; }
+  bool on_len(uint32_t n, Span s) { (n == 1 ? key : val) = s; return true; }
+};
+struct HQReads {
+  std::vector<HRead> *out;
+  Kind kind(uint32_t n) { return n == 1 ? K_REP_MSG : K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    HRead r;
+    if (!pbw::decode(s.p, s.n, r)) return false;
+    out->push_back(r);
+    return true;
+  }
+};
+struct HMerk {  // QueryReadsMerkleSummary {max_degree uint32 1, max_level uint32 2, max_level_hashes 3}
+  uint32_t degree = 0, level = 0;
+  std::vector<Span> hashes;
+  Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_VARINT : n == 3 ? K_REP_BYTES : K_NONE; }
+  void on_varint(uint32_t n, uint64_t v) { (n == 1 ? degree : level) = (uint32_t)v; }
+  bool on_len(uint32_t, Span s) { hashes.push_back(s); return true; }
+};
+struct HRQ {  // RangeQueryInfo
+  Span start, end;
+  bool exhausted = false, raw = false, merk = false;
+  std::vector<HRead> reads;
+  HMerk m;
+  Kind kind(uint32_t n) { return (n == 1 || n == 2) ? K_STRING : n == 3 ? K_VARINT : (n == 4 || n == 5) ? K_MSG : K_NONE; }
+  void on_varint(uint32_t n, uint64_t v) { if (n == 3) exhausted = v != 0; }
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) { start = s; return true; }
+    if (n == 2) { end = s; return true; }
+    if (n == 4) {
+      raw = true;
+      HQReads q{&reads};
+      return pbw::decode(s.p, s.n, q);
+    }
+    merk = true;
+    return pbw::decode(s.p, s.n, m);
+  }
+};
+struct HRW {  // KVRWSet / HashedRWSet
+  bool hashed = false;
+  std::vector<HRead> reads;
+  std::vector<HRQ> rqs;
+  std::vector<HWrite> writes;
+  Kind kind(uint32_t n) { return (n >= 1 && n <= (hashed ? 3u : 4u)) ? K_REP_MSG : K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) {
+      HRead r;
+      r.hashed = hashed;
+      if (!pbw::decode(s.p, s.n, r)) return false;
+      reads.push_back(r);
+      return true;
+    }
+    if (!hashed && n == 2) {
+      HRQ q;
+      if (!pbw::decode(s.p, s.n, q)) return false;
+      rqs.push_back(std::move(q));
+      return true;
+    }
+    if (n == (hashed ? 2u : 3u)) {
+      HWrite w;
+      w.hashed = hashed;
+      if (!pbw::decode(s.p, s.n, w)) return false;
+      writes.push_back(w);
+      return true;
+    }
+    return false;  // metadata write: the device pass reported the block unsupported
+  }
+};
+struct HColl {
+  Span name, hashed;
+  Kind kind(uint32_t n) { return n == 1 ? K_STRING : (n == 2 || n == 3) ? K_BYTES : K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) name = s;
+    else if (n == 2) hashed = s;
+    return true;
+  }
+};
+struct HNs {
+  Span ns, rwset;
+  std::vector<HColl> colls;
+  Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : n == 3 ? K_REP_MSG : K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) ns = s;
+    else if (n == 2) rwset = s;
+    else {
+      HColl c;
+      if (!pbw::decode(s.p, s.n, c)) return false;
+      colls.push_back(c);
+    }
+    return true;
+  }
+};
+struct HTxRW {
+  std::vector<HNs> ns;
+  Kind kind(uint32_t n) { return n == 1 ? K_VARINT : n == 2 ? K_REP_MSG : K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    HNs h;
+    if (!pbw::decode(s.p, s.n, h)) return false;
+    ns.push_back(std::move(h));
+    return true;
+  }
+};
+
+struct Ver {
+  uint64_t b = 0, t = 0;
+  bool operator==(const Ver &o) const { return b == o.b && t == o.t; }
+};
+struct Upd {
+  Ver v;
+  bool del = false;
+};
+struct TxNs {  // one NsReadWriteSet, decoded
+  std::string ns;
+  HRW kv;
+  std::vector<std::pair<std::string, HRW>> colls;  // flattened hashed ns, hashed rwset
+};
+std::string sv(const Span &s) { return std::string(reinterpret_cast<const char *>(s.p), s.n); }
+// (namespace, key) as one map key: 4-byte namespace length, namespace, key (keys and hashed
+// keys may hold any byte)
+std::string flat_key(const std::string &ns, const std::string &key) {
+  const uint32_t n = (uint32_t)ns.size();
+  std::string o(reinterpret_cast<const char *>(&n), 4);
+  return o + ns + key;
+}
+void split_flat(const std::string &fk, std::string &ns, std::string &key) {
+  uint32_t n;
+  memcpy(&n, fk.data(), 4);
+  ns = fk.substr(4, n);
+  key = fk.substr(4 + n);
+}
+
+constexpr uint8_t kEmptySha256[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
+                                      0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
+                                      0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+bool is_delete(const HWrite &w) {  // IsKVWriteDelete / IsKVWriteHashDelete
+  if (w.del || w.val.n == 0) return true;
+  return w.hashed && w.val.n == 32 && memcmp(w.val.p, kEmptySha256, 32) == 0;
+}
+
+// ---- merkle summary (rwsetutil/query_results_helper.go)
+void put_varint(std::string &o, uint64_t v) {
+  while (v >= 0x80) {
+    o.push_back((char)(uint8_t)(v | 0x80));
+    v >>= 7;
+  }
+  o.push_back((char)(uint8_t)v);
+}
+void put_len(std::string &o, uint32_t field, const std::string &b) {
+  put_varint(o, (uint64_t)field << 3 | 2);
+  put_varint(o, b.size());
+  o += b;
+}
+using KV = std::pair<std::string, Ver>;
+// proto.Marshal(&kvrwset.QueryReads{KvReads}): KVRead{key 1 (omitted when empty), version 2
+// (present: NewKVRead of a committed / updated height)}, Version{block_num 1, tx_num 2}
+std::string marshal_query_reads(const std::vector<KV> &kvs) {
+  std::string out;
+  for (const KV &kv : kvs) {
+    std::string ver, msg;
+    if (kv.second.b) { put_varint(ver, 1 << 3); put_varint(ver, kv.second.b); }
+    if (kv.second.t) { put_varint(ver, 2 << 3); put_varint(ver, kv.second.t); }
+    if (!kv.first.empty()) put_len(msg, 1, kv.first);
+    put_len(msg, 2, ver);
+    put_len(out, 1, msg);
+  }
+  return out;
+}
+std::string sha(const std::string &b) {
+  uint8_t d[32];
+  fgvsha::sha256(reinterpret_cast<const uint8_t *>(b.data()), b.size(), d);
+  return std::string(reinterpret_cast<const char *>(d), 32);
+}
+struct Merkle {
+  std::map<uint32_t, std::vector<std::string>> tree;
+  uint32_t max_level = 1, max_degree;
+  explicit Merkle(uint32_t d) : max_degree(d) {}
+  static std::string combine(const std::vector<std::string> &hs) {
+    std::string b;
+    for (const auto &h : hs) b += h;
+    return sha(b);
+  }
+  void update(const std::string &h) {
+    tree[1].push_back(h);
+    uint32_t level = 1;
+    for (;;) {
+      auto it = tree.find(level);
+      if (it == tree.end() || it->second.size() <= max_degree) return;
+      const std::string next = combine(it->second);
+      tree.erase(it);
+      level++;
+      tree[level].push_back(next);
+      if (level > max_level) max_level = level;
+    }
+  }
+  void done() {
+    uint32_t level = 1;
+    while (level < max_level) {
+      auto it = tree.find(level);
+      if (it == tree.end() || it->second.empty()) {
+        level++;
+        continue;
+      }
+      const std::string h = it->second.size() == 1 ? it->second[0] : combine(it->second);
+      tree.erase(it);
+      level++;
+      tree[level].push_back(h);
+    }
+    auto it = tree.find(max_level);
+    if (it != tree.end() && it->second.size() > max_degree) {
+      const std::string h = combine(it->second);
+      tree.erase(it);
+      max_level++;
+      tree[max_level] = {h};
+    }
+  }
+  const std::vector<std::string> &top() {
+    static const std::vector<std::string> none;
+    auto it = tree.find(max_level);
+    return it == tree.end() ? none : it->second;
+  }
+  bool empty() {
+    auto it = tree.find(1);
+    return max_level == 1 && (it == tree.end() || it->second.empty());
+  }
+};
+
+// the combined iterator's output for one range query (combined_iterator.go)
+std::vector<KV> combined(const std::vector<KV> &db, const std::map<std::string, Upd> *upd, const std::string &start,
+                         const std::string &end, bool unbounded, bool include_end, bool end_known, const Upd &end_val) {
+  std::vector<KV> out;
+  std::map<std::string, Upd>::const_iterator u, ue;
+  if (upd) {
+    u = start.empty() ? upd->begin() : upd->lower_bound(start);
+    ue = unbounded ? upd->end() : upd->lower_bound(end);
+    if (!unbounded && !start.empty() && start > end) u = ue;  // SearchStrings: next >= last -> empty
+  }
+  size_t i = 0;
+  const bool has_u = upd != nullptr;
+  for (;;) {
+    const bool db_left = i < db.size(), u_left = has_u && u != ue;
+    if (!db_left && !u_left) break;
+    int cmp;
+    if (!u_left) cmp = -1;
+    else if (!db_left) cmp = 1;
+    else cmp = db[i].first < u->first ? -1 : (u->first < db[i].first ? 1 : 0);
+    if (cmp < 0) {
+      out.push_back(db[i++]);
+      continue;
+    }
+    const std::string &k = u->first;
+    const Upd uv = u->second;
+    ++u;
+    if (cmp == 0) i++;
+    if (!uv.del) out.push_back(KV{k, uv.v});
+  }
+  if (include_end && end_known && !end_val.del) out.push_back(KV{end, end_val.v});
+  return out;
+}
+
+// rangeQueryResultsValidator / rangeQueryHashValidator: 1 valid, 0 phantom, -1 the reference
+// errors out (maxDegree < 2; a raw read without a version dereferences nil)
+int rq_validate(const HRQ &q, const std::vector<KV> &res) {
+  if (q.merk) {
+    if (q.m.degree < 2) return -1;
+    Merkle mt(q.m.degree);
+    std::vector<KV> pending;
+    int last = -1;
+    for (const KV &kv : res) {
+      pending.push_back(kv);
+      if (pending.size() > q.m.degree) {
+        mt.update(sha(marshal_query_reads(pending)));
+        pending.clear();
+      }
+      if (mt.max_level < q.m.level) continue;
+      const std::vector<std::string> &h = mt.top();
+      if (last == (int)h.size() - 1) continue;
+      if (h.size() > q.m.hashes.size()) return 0;
+      last++;
+      if (!q.m.hashes[last].eq(h[last].data(), h[last].size())) return 0;
+    }
+    if (mt.empty()) return 0;  // Done() -> nil summary: never equal
+    if (!pending.empty()) mt.update(sha(marshal_query_reads(pending)));
+    mt.done();
+    const std::vector<std::string> &h = mt.top();
+    if (mt.max_level != q.m.level || h.size() != q.m.hashes.size()) return 0;
+    for (size_t k = 0; k < h.size(); k++)
+      if (!q.m.hashes[k].eq(h[k].data(), h[k].size())) return 0;
+    return 1;
+  }
+  if (q.reads.empty()) return res.empty() ? 1 : 0;
+  size_t j = 0;
+  for (const HRead &r : q.reads) {
+    if (j >= res.size() || !r.key.eq(res[j].first.data(), res[j].first.size())) return 0;
+    if (!r.has_ver) return -1;
+    if (!(res[j].second == Ver{r.v.b, r.v.t})) return 0;
+    j++;
+  }
+  return j == res.size() ? 1 : 0;
+}
+
+}  // namespace
+
+static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, uint64_t block_num,
+                         const uint8_t *in_flags, uint8_t *flags, size_t ntx, int commit) {
+  hipStream_t s = c->stream;
+  std::vector<MvTxInfo> info(ntx);
+  HIP_TRY(hipMemcpyAsync(info.data(), M->info.p, ntx * sizeof(MvTxInfo), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  // 1. decode the participating transactions' rwsets
+  std::vector<std::vector<TxNs>> txs(ntx);
+  for (size_t i = 0; i < ntx; i++) {
+    if (info[i].code != 0) continue;
+    HTxRW rw;
+    if (!pbw::decode(block + info[i].rws_off, info[i].rws_len, rw)) return FGV_EUNSUPPORTED;  // (cannot happen)
+    for (HNs &h : rw.ns) {
+      TxNs e;
+      e.ns = sv(h.ns);
+      e.kv.hashed = false;
+      if (!pbw::decode(h.rwset.p, h.rwset.n, e.kv)) return FGV_EUNSUPPORTED;
+      for (const HColl &cl : h.colls) {
+        HRW hr;
+        hr.hashed = true;
+        if (!pbw::decode(cl.hashed.p, cl.hashed.n, hr)) return FGV_EUNSUPPORTED;
+        e.colls.emplace_back(e.ns + "$$h" + sv(cl.name), std::move(hr));
+      }
+      txs[i].push_back(std::move(e));
+    }
+  }
+  // 2. committed versions of every point-read key and range end key; committed keys of every range
+  std::unordered_map<std::string, uint32_t> qidx;  // flat key -> lookup index
+  std::vector<std::pair<std::string, std::string>> qkeys;
+  auto want = [&](const std::string &ns, const std::string &key) {
+    const std::string fk = flat_key(ns, key);
+    if (qidx.emplace(fk, (uint32_t)qkeys.size()).second) qkeys.emplace_back(ns, key);
+  };
+  struct RangeQ {
+    std::string ns, start, end;
+    bool unbounded;
+  };
+  std::vector<RangeQ> ranges;
+  for (size_t i = 0; i < ntx; i++)
+    for (const TxNs &e : txs[i]) {
+      for (const HRead &r : e.kv.reads) want(e.ns, sv(r.key));
+      for (const HRQ &q : e.kv.rqs) {
+        ranges.push_back(RangeQ{e.ns, sv(q.start), sv(q.end), q.end.n == 0});
+        if (!q.exhausted) want(e.ns, sv(q.end));
+      }
+      for (const auto &cl : e.colls)
+        for (const HRead &r : cl.second.reads) want(cl.first, sv(r.key));
+    }
+  for (const auto &k : qkeys)
+    if (k.first.size() > 0xFFFF || k.second.size() > 0xFFFF || k.first.size() + k.second.size() > 0xFFFF)
+      return FGV_EUNSUPPORTED;
+  // staging: bytes [ns | key]... then the range bounds; one MvRec per lookup (flattened ns)
+  std::string bytes;
+  std::vector<MvRec> recs(qkeys.size());
+  for (size_t k = 0; k < qkeys.size(); k++) {
+    MvRec &r = recs[k];
+    memset(&r, 0, sizeof r);
+    r.ns_off = (uint32_t)bytes.size();
+    r.ns_len = (uint16_t)qkeys[k].first.size();
+    bytes += qkeys[k].first;
+    r.key_off = (uint32_t)bytes.size();
+    r.key_len = (uint16_t)qkeys[k].second.size();
+    bytes += qkeys[k].second;
+  }
+  std::vector<MvRange> rdesc(ranges.size());
+  for (size_t k = 0; k < ranges.size(); k++) {
+    MvRange &d = rdesc[k];
+    memset(&d, 0, sizeof d);
+    d.ns_off = (uint32_t)bytes.size();
+    d.ns_len = (uint32_t)ranges[k].ns.size();
+    bytes += ranges[k].ns;
+    d.s_off = (uint32_t)bytes.size();
+    d.s_len = (uint32_t)ranges[k].start.size();
+    bytes += ranges[k].start;
+    d.e_off = (uint32_t)bytes.size();
+    d.e_len = (uint32_t)ranges[k].end.size();
+    bytes += ranges[k].end;
+    d.flags = ranges[k].unbounded ? MVRANGE_UNBOUNDED : 0u;
+  }
+  if (bytes.size() >= 0xFFFFFFFFull) return FGV_EUNSUPPORTED;
+  const size_t nq = qkeys.size();
+  if (!M->lbytes.ensure(bytes.size() + 64) || !M->lrecs.ensure((nq + 1) * sizeof(MvRec)) ||
+      !M->qver.ensure((nq + 1) * 16) || !M->qpres.ensure(nq + 64) || !M->qrange.ensure((ranges.size() + 1) * sizeof(MvRange)) ||
+      !M->qout.ensure(1 << 20) || !M->top.ensure(64))
+    return FGV_ENOMEM;
+  uint8_t *lb = M->lbytes.as<uint8_t>();
+  if (!bytes.empty()) HIP_TRY(hipMemcpyAsync(lb, bytes.data(), bytes.size(), hipMemcpyHostToDevice, s));
+  std::vector<uint64_t> qver(2 * nq);
+  std::vector<uint8_t> qpres(nq);
+  if (nq) {
+    HIP_TRY(hipMemcpyAsync(M->lrecs.p, recs.data(), nq * sizeof(MvRec), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_mv_tags, grid_for(nq), dim3(256), 0, s, lb, M->lrecs.as<MvRec>(), (uint32_t)nq);
+    hipLaunchKernelGGL(k_mv_lookup, grid_stride(nq), dim3(256), 0, s, (uint32_t)nq, lb, M->lrecs.as<MvRec>(),
+                       M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(), M->qver.as<uint64_t>(),
+                       M->qpres.as<uint8_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(qver.data(), M->qver.p, nq * 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(qpres.data(), M->qpres.p, nq, hipMemcpyDeviceToHost, s));
+  }
+  std::vector<std::vector<KV>> scanned(ranges.size());
+  if (!ranges.empty()) {
+    HIP_TRY(hipMemcpyAsync(M->qrange.p, rdesc.data(), ranges.size() * sizeof(MvRange), hipMemcpyHostToDevice, s));
+    unsigned long long *used = reinterpret_cast<unsigned long long *>(M->top.as<uint8_t>() + 32);
+    std::vector<uint8_t> out;
+    for (int attempt = 0; attempt < 2; attempt++) {
+      HIP_TRY(hipMemsetAsync(used, 0, 8, s));
+      hipLaunchKernelGGL(k_mv_range_scan, grid_stride(M->cap, 4096), dim3(256), 0, s, M->cap, M->tbl.as<StateSlot>(),
+                         M->arena.as<uint8_t>(), (uint32_t)ranges.size(), M->qrange.as<MvRange>(), lb,
+                         M->qout.as<uint8_t>(), (uint64_t)M->qout.cap, used);
+      HIP_TRY(hipGetLastError());
+      unsigned long long u = 0;
+      HIP_TRY(hipMemcpyAsync(&u, used, 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      if (u <= M->qout.cap) {
+        out.resize(u);
+        if (u) HIP_TRY(hipMemcpy(out.data(), M->qout.p, u, hipMemcpyDeviceToHost));
+        break;
+      }
+      if (attempt == 1 || !M->qout.ensure(u + (1 << 20))) return FGV_ENOMEM;
+    }
+    for (size_t o = 0; o + 24 <= out.size();) {
+      uint32_t h[2];
+      uint64_t v[2];
+      memcpy(h, out.data() + o, 8);
+      memcpy(v, out.data() + o + 8, 16);
+      if (h[0] >= ranges.size() || o + 24 + h[1] > out.size()) return FGV_EDEVICE;
+      scanned[h[0]].push_back(KV{std::string(reinterpret_cast<const char *>(out.data() + o + 24), h[1]), Ver{v[0], v[1]}});
+      o += 24 + ((h[1] + 7u) & ~7u);
+    }
+    for (auto &v : scanned) std::sort(v.begin(), v.end(), [](const KV &a, const KV &b) { return a.first < b.first; });
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  auto committed = [&](const std::string &ns, const std::string &key, Ver &v) -> bool {
+    const uint32_t k = qidx.at(flat_key(ns, key));
+    v = Ver{qver[2 * k], qver[2 * k + 1]};
+    return qpres[k] != 0;
+  };
+  // 3. validateAndPrepareBatch, in block order
+  std::map<std::string, std::map<std::string, Upd>> pub;  // ns -> key -> update (sorted: range scans)
+  std::unordered_map<std::string, Upd> hsh;               // flat hashed ns + key
+  auto read_ok = [&](const std::string &ns, const HRead &r, bool hashed) {
+    const std::string key = sv(r.key);
+    if (hashed) {
+      if (hsh.count(flat_key(ns, key))) return false;
+    } else {
+      auto it = pub.find(ns);
+      if (it != pub.end() && it->second.count(key)) return false;
+    }
+    Ver v;
+    const bool present = committed(ns, key, v);
+    if (!present || !r.has_ver) return present == r.has_ver;  // version.AreSame (nil <=> absent)
+    return v == Ver{r.v.b, r.v.t};
+  };
+  std::vector<size_t> rq_base(ntx + 1, 0);  // the first range index of each tx
+  for (size_t i = 0; i < ntx; i++) {
+    size_t k = 0;
+    for (const TxNs &e : txs[i]) k += e.kv.rqs.size();
+    rq_base[i + 1] = rq_base[i] + k;
+  }
+  for (size_t i = 0; i < ntx; i++) {
+    size_t rq_at = rq_base[i];
+    const uint8_t code = info[i].code;
+    if (code == MV_SKIP) { flags[i] = in_flags[i]; continue; }
+    if (code != 0) { flags[i] = code; continue; }
+    uint8_t verdict = 0;
+    for (const TxNs &e : txs[i]) {
+      for (const HRead &r : e.kv.reads)
+        if (!read_ok(e.ns, r, false)) { verdict = 11; break; }
+      if (verdict) break;
+      for (const HRQ &q : e.kv.rqs) {
+        const size_t ri = rq_at++;
+        if (verdict) continue;
+        auto pit = pub.find(e.ns);
+        const std::string end = sv(q.end);
+        Upd ev;
+        bool end_known = false;
+        if (!q.exhausted) {  // serveEndKeyIfNeeded: updates.Get, else db.GetState
+          auto u = pit != pub.end() ? pit->second.find(end) : std::map<std::string, Upd>::const_iterator();
+          if (pit != pub.end() && u != pit->second.end()) {
+            ev = u->second;
+            end_known = true;
+          } else {
+            Ver v;
+            end_known = committed(e.ns, end, v);
+            ev = Upd{v, false};
+          }
+        }
+        const std::vector<KV> res = combined(scanned[ri], pit != pub.end() ? &pit->second : nullptr, sv(q.start), end,
+                                             q.end.n == 0, !q.exhausted, end_known, ev);
+        const int ok = rq_validate(q, res);
+        if (ok < 0) return FGV_EUNSUPPORTED;  // the reference returns an error (the peer stops)
+        if (!ok) verdict = 12;
+      }
+      if (verdict) break;
+      for (const auto &cl : e.colls) {
+        for (const HRead &r : cl.second.reads)
+          if (!read_ok(cl.first, r, true)) { verdict = 11; break; }
+        if (verdict) break;
+      }
+      if (verdict) break;
+    }
+    if (verdict) {
+      flags[i] = verdict;
+      continue;
+    }
+    flags[i] = 0;
+    const Ver h{block_num, (uint64_t)i};
+    for (const TxNs &e : txs[i]) {
+      for (const HWrite &w : e.kv.writes) pub[e.ns][sv(w.key)] = Upd{h, is_delete(w)};
+      for (const auto &cl : e.colls)
+        for (const HWrite &w : cl.second.writes) hsh[flat_key(cl.first, sv(w.key))] = Upd{h, is_delete(w)};
+    }
+  }
+  if (!commit) return FGV_OK;
+  // 4. commit the update batch: one upsert per flattened namespace (capacity checked first, so
+  // a block is committed whole or not at all)
+  std::map<std::string, std::vector<std::pair<std::string, Upd>>> groups;
+  for (const auto &nsm : pub)
+    for (const auto &kv : nsm.second) groups[nsm.first].emplace_back(kv.first, kv.second);
+  for (const auto &kv : hsh) {
+    std::string ns, key;
+    split_flat(kv.first, ns, key);
+    groups[ns].emplace_back(key, kv.second);
+  }
+  int rc = read_top(c, M);
+  if (rc) return rc;
+  size_t n_all = 0, need = 0;
+  for (const auto &g : groups)
+    for (const auto &kv : g.second) {
+      n_all++;
+      if (!kv.second.del) need += (g.first.size() + kv.first.size() + 7) & ~(size_t)7;
+    }
+  if ((M->nkeys + n_all) * 10 > M->cap * 7 || M->arena_used + need > M->arena_cap) return FGV_ENOMEM;
+  for (const auto &g : groups) {
+    std::string kb;
+    std::vector<uint64_t> off, blk, txn;
+    std::vector<uint32_t> len;
+    std::vector<uint8_t> del;
+    for (const auto &kv : g.second) {
+      off.push_back(kb.size());
+      len.push_back((uint32_t)kv.first.size());
+      kb += kv.first;
+      blk.push_back(kv.second.v.b);
+      txn.push_back(kv.second.v.t);
+      del.push_back(kv.second.del ? 1 : 0);
+    }
+    rc = upsert_host(c, g.first.c_str(), reinterpret_cast<const uint8_t *>(kb.data()), off.data(), len.data(), blk.data(),
+                     txn.data(), del.data(), g.second.size());
+    if (rc) return rc;
+  }
+  return FGV_OK;
+}
+
 static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block, uint64_t block_num,
                          uint8_t *flags, size_t ntx, int commit, const uint8_t *next, size_t next_len) {
   if (!c || !block || (ntx && !flags)) return FGV_EINVAL;
@@ -314,6 +931,10 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   c->n_mvcc_reads = hc->nr;
   c->n_mvcc_writes = hc->nw;
   M->last_rounds = hc->rounds;
+  if (hc->unsup == MV_UNSUP_RQ) {  // range queries, nothing else outside the model: phantom path
+    c->t_mvcc_total = 0;
+    return phantom_block(c, M, block, block_num, flags, flags, ntx, commit);
+  }
   if (hc->unsup) return FGV_EUNSUPPORTED;  // nothing was committed
   if (commit) {
     rc = read_top(c, M);

@@ -225,6 +225,7 @@ struct VRW {
   S ns, coll;
   bool hashed;
   bool unsup = false;
+  bool rq = false;  // range queries: validated here, checked by the host phantom path
   DEV Kind kind(uint32_t n) { return (n >= 1 && n <= (hashed ? 3u : 4u)) ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
   DEV bool on_len(uint32_t n, S s, bool &ovf) {
@@ -234,7 +235,7 @@ struct VRW {
       sk->read(ns, hashed, coll, r.key, r.has_ver, r.v.b, r.v.t);
       return true;
     }
-    if (!hashed && n == 2) { unsup = true; VRQ q; return decode(s, q, ovf); }  // range query
+    if (!hashed && n == 2) { rq = true; VRQ q; return decode(s, q, ovf); }  // range query
     if (n == (hashed ? 2u : 3u)) {
       VWrite w{hashed};
       if (!decode(s, w, ovf)) return false;
@@ -294,7 +295,7 @@ struct VNsColls {
 // TxRwSet.FromProtoBytes unmarshals every namespace and collection before any check)
 struct VTxRW {
   Sink *sk;
-  bool fail = false, unsup = false;
+  bool fail = false, unsup = false, rq = false;
   DEV Kind kind(uint32_t n) { return n == 1 ? K_VARINT : n == 2 ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
   DEV bool on_len(uint32_t, S s, bool &ovf) {
@@ -303,6 +304,7 @@ struct VTxRW {
     VRW kv{sk, h.ns, S{nullptr, 0}, false};
     if (!decode(h.rwset, kv, ovf)) fail = true;
     unsup |= kv.unsup;
+    rq |= kv.rq;
     VNsColls cs{sk, h.ns};
     if (!decode(s, cs, ovf)) return false;
     fail |= cs.fail;
@@ -357,13 +359,14 @@ DEV uint8_t find_results(S d, S &results) {
   return 0;
 }
 
-DEV uint8_t walk_rwset(S results, Sink &sk) {
+DEV uint8_t walk_rwset(S results, Sink &sk, bool &rq) {
   bool ovf = false;
   VTxRW rw{&sk};
   const bool ok = decode(results, rw, ovf);
   if (ovf) return MV_UNSUP;
   if (!ok || rw.fail) return MV_OTHER;
   if (rw.unsup || sk.big) return MV_UNSUP;
+  rq = rw.rq;
   return 0;
 }
 
@@ -405,10 +408,14 @@ __global__ __launch_bounds__(64) void k_mvx_count(uint32_t ntx, const uint8_t *_
       I.code = find_results(S{base + envtab[2 * t], envtab[2 * t + 1]}, results);
       if (I.code == 0) {
         Sink sk{base, nullptr, nullptr, t, 0, 0, 0, false};
-        I.code = walk_rwset(results, sk);
+        bool rq = false;
+        I.code = walk_rwset(results, sk, rq);
         I.rws_off = (uint32_t)(results.p - base);
         I.rws_len = results.n;
         if (I.code == 0) { nr = sk.nr; nw = sk.nw; wb = sk.wbytes; }
+        // range queries: the block goes to the host phantom path (fgv_mvcc.cpp), which takes
+        // these codes and result spans (MV_UNSUP_RQ stops the device pipeline like MV_UNSUP)
+        if (I.code == 0 && rq) atomicOr(&c->unsup, MV_UNSUP_RQ);
       }
       if (I.code == MV_UNSUP) atomicOr(&c->unsup, 1u);
     }
@@ -430,7 +437,8 @@ __global__ __launch_bounds__(64) void k_mvx_emit(uint32_t ntx, const uint8_t *__
   MvTxInfo I = info[t];
   if (I.code != 0) return;
   Sink sk{base, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
-  walk_rwset(S{base + I.rws_off, I.rws_len}, sk);
+  bool rq = false;
+  walk_rwset(S{base + I.rws_off, I.rws_len}, sk, rq);
   // one key written twice by one tx: txOps adds the flags (tx_ops.go:183-191) -> semantics
   // the engine does not model (upsert+upsert reads as a metadata-only update)
   const MvRec *w = writes + I.wbeg;
@@ -701,4 +709,59 @@ __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_
 __global__ __launch_bounds__(256) void k_mv_tags(const uint8_t *__restrict__ base, MvRec *__restrict__ recs, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) recs[i].tag = rec_tag(base, recs[i]);
+}
+
+// ============================================================ host phantom path support
+// Point lookups of host-given keys (flattened namespace at ns_off, key at key_off of `base`):
+// found-and-present flag + committed version.
+__global__ __launch_bounds__(256) void k_mv_lookup(uint32_t n, const uint8_t *__restrict__ base,
+                                                   const MvRec *__restrict__ recs, const StateSlot *__restrict__ tbl,
+                                                   uint64_t mask, const uint8_t *__restrict__ arena,
+                                                   uint64_t *__restrict__ ver, uint8_t *__restrict__ present) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int64_t s = state_find(tbl, mask, arena, base, recs[i]);
+    const bool p = s >= 0 && (tbl[s].tag & MV_TAG_PRESENT);
+    present[i] = p ? 1 : 0;
+    ver[2 * i] = p ? tbl[s].blk : 0;
+    ver[2 * i + 1] = p ? tbl[s].txn : 0;
+  }
+}
+
+// GetStateRangeScanIterator without an ordered index: every present committed key is tested
+// against the block's ranges (namespace equal, start <= key, key < end unless unbounded) and
+// matches are appended as {range, key_len, blk, txn} + key bytes (8-byte padded).  The host
+// sorts each range's matches.  *used may exceed cap: the host then grows the buffer and reruns.
+DEV bool key_lt(const uint8_t *a, uint32_t an, const uint8_t *b, uint32_t bn) {  // Go string order
+  const uint32_t m = an < bn ? an : bn;
+  for (uint32_t i = 0; i < m; i++)
+    if (a[i] != b[i]) return a[i] < b[i];
+  return an < bn;
+}
+__global__ __launch_bounds__(256) void k_mv_range_scan(uint64_t cap, const StateSlot *__restrict__ tbl,
+                                                       const uint8_t *__restrict__ arena, uint32_t nranges,
+                                                       const MvRange *__restrict__ ranges,
+                                                       const uint8_t *__restrict__ rbytes, uint8_t *__restrict__ out,
+                                                       uint64_t out_cap, unsigned long long *__restrict__ used) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
+    const StateSlot sl = tbl[i];
+    if (!(sl.tag & MV_TAG_OCC) || !(sl.tag & MV_TAG_PRESENT)) continue;
+    const uint8_t *a = arena + ((uint64_t)sl.off8 << 3);
+    const uint8_t *key = a + sl.ns_len;
+    for (uint32_t r = 0; r < nranges; r++) {
+      const MvRange R = ranges[r];
+      if (R.ns_len != sl.ns_len || !bytes_eq(a, rbytes + R.ns_off, R.ns_len)) continue;
+      if (key_lt(key, sl.key_len, rbytes + R.s_off, R.s_len)) continue;
+      if (!(R.flags & MVRANGE_UNBOUNDED) && !key_lt(key, sl.key_len, rbytes + R.e_off, R.e_len)) continue;
+      const uint64_t sz = 24 + (((uint64_t)sl.key_len + 7) & ~7ull);
+      const uint64_t o = atomicAdd(used, (unsigned long long)sz);
+      if (o + sz > out_cap) continue;  // counted: the host reruns with room
+      uint32_t *h = reinterpret_cast<uint32_t *>(out + o);
+      h[0] = r;
+      h[1] = sl.key_len;
+      uint64_t *v = reinterpret_cast<uint64_t *>(out + o + 8);
+      v[0] = sl.blk;
+      v[1] = sl.txn;
+      for (uint32_t k = 0; k < sl.key_len; k++) out[o + 24 + k] = key[k];
+    }
+  }
 }

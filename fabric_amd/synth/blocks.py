@@ -83,11 +83,31 @@ def out_of_policy(n: int, mspids) -> bytes:
     return f_msg(1, spe)
 
 
-def kv_rwset(reads, writes) -> bytes:
+def _kvread(k, ver) -> bytes:
+    v = b"" if ver is None else f_msg(2, f_varint(1, ver[0]) + f_varint(2, ver[1]))
+    return f_str(1, k) + v
+
+
+def range_query_info(start, end, exhausted, raw=None, merkle=None) -> bytes:
+    """RangeQueryInfo{start_key, end_key, itr_exhausted, raw_reads: QueryReads{kv_reads} (raw:
+    [(key, ver|None)]), reads_merkle_hashes: QueryReadsMerkleSummary (merkle: (max_degree,
+    max_level, [hashes]))} -- rwsetutil.SetRawReads / SetMerkelSummary shapes"""
+    out = f_str(1, start) + f_str(2, end) + f_varint(3, 1 if exhausted else 0)
+    if raw is not None:
+        out += f_msg(4, b"".join(f_msg(1, _kvread(k, v)) for k, v in raw))
+    if merkle is not None:
+        deg, lvl, hashes = merkle
+        out += f_msg(5, f_varint(1, deg) + f_varint(2, lvl) + b"".join(f_msg(3, h) for h in hashes))
+    return out
+
+
+def kv_rwset(reads, writes, rqs=()) -> bytes:
+    """KVRWSet{reads 1, range_queries_info 2 (rqs: range_query_info bytes), writes 3}"""
     out = b""
     for k, ver in reads:
-        v = b"" if ver is None else f_msg(2, f_varint(1, ver[0]) + f_varint(2, ver[1]))
-        out += f_msg(1, f_str(1, k) + v)
+        out += f_msg(1, _kvread(k, ver))
+    for q in rqs:
+        out += f_msg(2, q)
     for k, val, is_del in writes:
         out += f_msg(3, f_str(1, k) + f_varint(2, 1 if is_del else 0) + f_bytes(3, val))
     return out

@@ -17,15 +17,21 @@ Follows (citations under /root/reference/core/ledger/kvledger/txmgmt):
         reads are point reads of the key hash in the hashed-data namespace; the state DB keeps
         them under ns + "$$h" + coll (privacyenabledstate/db.go:31-33,355-357), which is the
         (namespace, key) the oracle and the engine use for them
-Range queries (phantom checks), metadata writes and a key written twice by one transaction
-are outside the modelled state and raise Unsupported.
+  validation/validator.go:134-162       per namespace in order: public reads (11), then range
+        queries (PHANTOM_READ_CONFLICT 12, oracle/rangequery.py), then the collections' hashed
+        reads (11)
+Metadata writes and a key written twice by one transaction are outside the modelled state and
+raise Unsupported; so does a range query the reference errors out on (maxDegree < 2, a raw read
+without a version).
 """
+import bisect
 import hashlib
 
 from .protowire import DecodeError, decode
+from .rangequery import RangeQueryError, combined_iterator, validate_range_query
 from .v20 import Unsupported, get_action_from_envelope, parse_rwset
 
-MVCC_READ_CONFLICT, NIL_TXACTION, INVALID_OTHER_REASON = 11, 16, 255
+MVCC_READ_CONFLICT, PHANTOM_READ_CONFLICT, NIL_TXACTION, INVALID_OTHER_REASON = 11, 12, 16, 255
 _EMPTY_HASH = hashlib.sha256(b"").digest()
 
 
@@ -48,9 +54,21 @@ class StateDB:
     def get_version(self, ns, key):
         return self.v.get((ns, _kb(key)))
 
+    def range(self, ns, start, end):
+        """GetStateRangeScanIterator: keys of ns in [start, end), end b"" = no bound; sorted"""
+        out = sorted((k, h) for (n, k), h in self.v.items()
+                     if n == ns and k >= start and (end == b"" or k < end))
+        return out
+
+
+def _ver(v):
+    return None if v is None else (v.get("block_num", 0), v.get("tx_num", 0))
+
 
 def _tx_rwsets(env_bytes):
-    """-> list of (ns, reads[(key, ver|None)], writes[(key, is_delete)], hashed) or an int code."""
+    """-> list, per NsReadWriteSet in order, of dict(ns, reads [(key, ver|None)], rqs [dict],
+    colls [(hashed ns, hashed reads [(key hash, ver|None)])], writes [(hashed, ns, key,
+    is_delete)]) -- or an int code."""
     try:
         cca, _ = get_action_from_envelope(env_bytes)
     except (DecodeError, ValueError, KeyError, IndexError):
@@ -59,46 +77,71 @@ def _tx_rwsets(env_bytes):
         rw = parse_rwset(cca.get("results"))
     except DecodeError:
         return INVALID_OTHER_REASON
-    out, kinds = [], []
+    out = []
     for ns in rw:
         kv = ns["kv"]
-        if kv.get("range_queries_info") or kv.get("metadata_writes"):
-            raise Unsupported("range queries / metadata writes")
+        if kv.get("metadata_writes"):
+            raise Unsupported("metadata writes")
         if any(c["hashed"].get("metadata_writes") for c in ns["coll"]):
             raise Unsupported("private-data metadata writes")
-        reads = []
+        name = ns["namespace"]
+        e = dict(ns=name, reads=[], rqs=[], colls=[], writes=[])
         for r in kv.get("reads", []):
-            v = r.get("version")
-            reads.append((r.get("key", ""), None if v is None else (v.get("block_num", 0), v.get("tx_num", 0))))
-        writes = [(w.get("key", ""), bool(w.get("is_delete", False)) or not w.get("value"))
-                  for w in kv.get("writes", [])]
-        out.append((ns["namespace"], reads, writes))
-        kinds.append(False)
+            e["reads"].append((r.get("key", ""), _ver(r.get("version"))))
+        for q in kv.get("range_queries_info", []):
+            rq = dict(start=_kb(q.get("start_key", "")), end=_kb(q.get("end_key", "")),
+                      exhausted=bool(q.get("itr_exhausted", False)), raw=None, merkle=None)
+            if q.get("raw_reads") is not None:
+                rq["raw"] = [(_kb(r.get("key", "")), _ver(r.get("version")))
+                             for r in q["raw_reads"].get("kv_reads", [])]
+            if q.get("reads_merkle_hashes") is not None:
+                m = q["reads_merkle_hashes"]
+                rq["merkle"] = (m.get("max_degree", 0), m.get("max_level", 0),
+                                [bytes(h) for h in m.get("max_level_hashes", [])])
+            e["rqs"].append(rq)
+        for w in kv.get("writes", []):
+            e["writes"].append((False, name, w.get("key", ""), bool(w.get("is_delete", False)) or not w.get("value")))
         for c in ns["coll"]:
-            hns, h = hashed_ns(ns["namespace"], c["name"]), c["hashed"]
-            hreads = []
-            for r in h.get("hashed_reads", []):
-                v = r.get("version")
-                hreads.append((bytes(r.get("key_hash") or b""),
-                               None if v is None else (v.get("block_num", 0), v.get("tx_num", 0))))
-            hwrites = []
+            hns, h = hashed_ns(name, c["name"]), c["hashed"]
+            e["colls"].append((hns, [(bytes(r.get("key_hash") or b""), _ver(r.get("version")))
+                                     for r in h.get("hashed_reads", [])]))
             for w in h.get("hashed_writes", []):
                 vh = bytes(w.get("value_hash") or b"")
-                hwrites.append((bytes(w.get("key_hash") or b""),
-                                bool(w.get("is_delete", False)) or not vh or vh == _EMPTY_HASH))
-            out.append((hns, hreads, hwrites))
-            kinds.append(True)
+                e["writes"].append((True, hns, bytes(w.get("key_hash") or b""),
+                                    bool(w.get("is_delete", False)) or not vh or vh == _EMPTY_HASH))
+        out.append(e)
     # a key written twice by one transaction: txOps adds the operation flags
     # (validation/tx_ops.go:183-191), a state the engine does not model
     seen = set()
-    for hashed, (nsname, _, writes) in zip(kinds, out):
-        for key, _ in writes:
-            if (hashed, nsname, key) in seen:
+    for e in out:
+        for hashed, nsname, key, _ in e["writes"]:
+            if (hashed, nsname, _kb(key)) in seen:
                 raise Unsupported("key written twice by one transaction")
-            seen.add((hashed, nsname, key))
-    # public and hashed updates are separate maps (privacyenabledstate.UpdateBatch); committed
-    # versions of both live under the flattened namespace (one state DB key space)
-    return [(ns, reads, writes, hashed) for hashed, (ns, reads, writes) in zip(kinds, out)]
+            seen.add((hashed, nsname, _kb(key)))
+    return out
+
+
+def _range_ok(state, updates, ns, rq):
+    """validateRangeQuery (validator.go:218-244) over committed state + public updates"""
+    start, end = rq["start"], rq["end"]
+    db_items = [(k, h, False) for k, h in state.range(ns, start, end)]
+    keys = sorted(k for (hashed, n, k) in updates if not hashed and n == ns)
+    lo = bisect.bisect_left(keys, start) if start else 0
+    hi = bisect.bisect_left(keys, end) if end else len(keys)
+    upd_items = [(k, updates[(False, ns, k)][0], updates[(False, ns, k)][1]) for k in keys[lo:hi]]
+
+    def end_lookup():  # serveEndKeyIfNeeded: updates.Get, else db.GetState
+        u = updates.get((False, ns, end))
+        if u is not None:
+            return u
+        h = state.get_version(ns, end)
+        return None if h is None else (h, False)
+
+    itr = combined_iterator(db_items, upd_items, end, not rq["exhausted"], end_lookup)
+    try:
+        return validate_range_query(rq, itr)
+    except RangeQueryError as e:
+        raise Unsupported("range query the reference errors out on: %s" % e)
 
 
 def validate_block(state, block_bytes, flags, block_num, commit=False, updates_out=None):
@@ -125,19 +168,23 @@ def validate_block(state, block_bytes, flags, block_num, commit=False, updates_o
         if isinstance(sets, int):
             flags[i] = sets
             continue
-        ok = True
-        for ns, reads, _, hashed in sets:
-            for key, ver in reads:
-                if (hashed, ns, _kb(key)) in updates or state.get_version(ns, key) != ver:
-                    ok = False
-                    break
-            if not ok:
+        code = 0
+        for e in sets:  # validateTx (validator.go:134-162)
+            ns = e["ns"]
+            if any((False, ns, _kb(k)) in updates or state.get_version(ns, k) != v for k, v in e["reads"]):
+                code = MVCC_READ_CONFLICT
+            elif not all(_range_ok(state, updates, ns, rq) for rq in e["rqs"]):
+                code = PHANTOM_READ_CONFLICT
+            elif any((True, hns, _kb(k)) in updates or state.get_version(hns, k) != v
+                     for hns, hreads in e["colls"] for k, v in hreads):
+                code = MVCC_READ_CONFLICT
+            if code:
                 break
-        if not ok:
-            flags[i] = MVCC_READ_CONFLICT
+        if code:
+            flags[i] = code
             continue
-        for ns, _, writes, hashed in sets:
-            for key, is_del in writes:
+        for e in sets:
+            for hashed, ns, key, is_del in e["writes"]:
                 updates[(hashed, ns, _kb(key))] = ((block_num, i), is_del)
     if updates_out is not None:
         updates_out.update(updates)
