@@ -75,7 +75,7 @@ __global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_
 #define MVR_HASVER 1u   // read: has a version
 #define MVR_DELETE 1u   // write: is a delete
 #define MVR_HASHED 2u   // private-data key: namespace = ns + "$$h" + coll
-#define MV_UNSUP_RQ 2u  // MvCounters.unsup bit: range queries present -> the host phantom path
+#define MV_HOSTPATH 2u  // MvCounters.unsup bit: range queries / metadata writes -> the host path
 #define MVRANGE_UNBOUNDED 1u  // MvRange.flags: end key "" (to the end of the namespace)
 #define MV_TAG_OCC 1ull      // tag bit 0: slot occupied (tags are never 0)
 #define MV_TAG_PRESENT 2ull  // committed-state tag bit 1: the key exists (clear = deleted)

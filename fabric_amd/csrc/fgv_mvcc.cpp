@@ -284,11 +284,22 @@ struct HRQ {  // RangeQueryInfo
     return pbw::decode(s.p, s.n, m);
   }
 };
+struct HMetaW {  // KVMetadataWrite {key string 1, entries 2} / KVMetadataWriteHash {key_hash bytes 1, entries 2}
+  bool hashed = false;
+  Span key;
+  Kind kind(uint32_t n) { return n == 1 ? (hashed ? K_BYTES : K_STRING) : n == 2 ? K_REP_MSG : K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) key = s;
+    return true;  // (entries: validated by the device pass; their bytes never affect a version)
+  }
+};
 struct HRW {  // KVRWSet / HashedRWSet
   bool hashed = false;
   std::vector<HRead> reads;
   std::vector<HRQ> rqs;
   std::vector<HWrite> writes;
+  std::vector<Span> meta;  // keys of the metadata writes
   Kind kind(uint32_t n) { return (n >= 1 && n <= (hashed ? 3u : 4u)) ? K_REP_MSG : K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
@@ -312,7 +323,11 @@ struct HRW {  // KVRWSet / HashedRWSet
       writes.push_back(w);
       return true;
     }
-    return false;  // metadata write: the device pass reported the block unsupported
+    HMetaW m;
+    m.hashed = hashed;
+    if (!pbw::decode(s.p, s.n, m)) return false;
+    meta.push_back(m.key);
+    return true;
   }
 };
 struct HColl {
@@ -578,7 +593,37 @@ static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, ui
       txs[i].push_back(std::move(e));
     }
   }
-  // 2. committed versions of every point-read key and range end key; committed keys of every range
+  // metadata writes not combined with a KVWrite of the same key in the same tx (those follow
+  // the write: upsert+metadata puts, delete+metadata deletes); a key with two metadata writes
+  // or two KVWrites (txOps adds the flags: tx_ops.go:183-203) is outside the model
+  struct TxMeta {
+    bool hashed;
+    std::string ns, key;
+  };
+  std::vector<std::vector<TxMeta>> metas(ntx);
+  for (size_t i = 0; i < ntx; i++) {
+    std::unordered_set<std::string> written, meta_seen;
+    for (const TxNs &e : txs[i]) {
+      for (const HWrite &w : e.kv.writes) written.insert(flat_key("p" + e.ns, sv(w.key)));
+      for (const auto &cl : e.colls)
+        for (const HWrite &w : cl.second.writes) written.insert(flat_key("h" + cl.first, sv(w.key)));
+    }
+    for (const TxNs &e : txs[i]) {
+      for (const Span &k : e.kv.meta) {
+        const std::string fk = flat_key("p" + e.ns, sv(k));
+        if (!meta_seen.insert(fk).second) return FGV_EUNSUPPORTED;
+        if (!written.count(fk)) metas[i].push_back(TxMeta{false, e.ns, sv(k)});
+      }
+      for (const auto &cl : e.colls)
+        for (const Span &k : cl.second.meta) {
+          const std::string fk = flat_key("h" + cl.first, sv(k));
+          if (!meta_seen.insert(fk).second) return FGV_EUNSUPPORTED;
+          if (!written.count(fk)) metas[i].push_back(TxMeta{true, cl.first, sv(k)});
+        }
+    }
+  }
+  // 2. committed versions of every point-read key, range end key and metadata-only key;
+  // committed keys of every range
   std::unordered_map<std::string, uint32_t> qidx;  // flat key -> lookup index
   std::vector<std::pair<std::string, std::string>> qkeys;
   auto want = [&](const std::string &ns, const std::string &key) {
@@ -600,6 +645,8 @@ static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, ui
       for (const auto &cl : e.colls)
         for (const HRead &r : cl.second.reads) want(cl.first, sv(r.key));
     }
+  for (size_t i = 0; i < ntx; i++)
+    for (const TxMeta &m : metas[i]) want(m.ns, m.key);
   for (const auto &k : qkeys)
     if (k.first.size() > 0xFFFF || k.second.size() > 0xFFFF || k.first.size() + k.second.size() > 0xFFFF)
       return FGV_EUNSUPPORTED;
@@ -758,11 +805,39 @@ static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, ui
       continue;
     }
     flags[i] = 0;
+    // applyWriteSet / prepareTxOps (types.go:81-112, tx_ops.go:17-53): per key, a delete wins,
+    // an upsert puts; a metadata-only write puts the key's latest value again -- a new version
+    // -- if the key exists (preceding updates, else committed state) and is a no-op otherwise.
+    // A key deleted earlier in the block makes the reference panic (PutValAndMetadata(nil)).
     const Ver h{block_num, (uint64_t)i};
     for (const TxNs &e : txs[i]) {
       for (const HWrite &w : e.kv.writes) pub[e.ns][sv(w.key)] = Upd{h, is_delete(w)};
       for (const auto &cl : e.colls)
         for (const HWrite &w : cl.second.writes) hsh[flat_key(cl.first, sv(w.key))] = Upd{h, is_delete(w)};
+    }
+    for (const TxMeta &m : metas[i]) {
+      Upd *prev = nullptr;
+      if (m.hashed) {
+        auto it = hsh.find(flat_key(m.ns, m.key));
+        if (it != hsh.end()) prev = &it->second;
+      } else {
+        auto it = pub.find(m.ns);
+        if (it != pub.end()) {
+          auto k = it->second.find(m.key);
+          if (k != it->second.end()) prev = &k->second;
+        }
+      }
+      bool exists;
+      if (prev) {
+        if (prev->del) return FGV_EUNSUPPORTED;
+        exists = true;
+      } else {
+        Ver v;
+        exists = committed(m.ns, m.key, v);
+      }
+      if (!exists) continue;
+      if (m.hashed) hsh[flat_key(m.ns, m.key)] = Upd{h, false};
+      else pub[m.ns][m.key] = Upd{h, false};
     }
   }
   if (!commit) return FGV_OK;
@@ -931,7 +1006,7 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   c->n_mvcc_reads = hc->nr;
   c->n_mvcc_writes = hc->nw;
   M->last_rounds = hc->rounds;
-  if (hc->unsup == MV_UNSUP_RQ) {  // range queries, nothing else outside the model: phantom path
+  if (hc->unsup == MV_HOSTPATH) {  // range queries / metadata writes, nothing else outside the model
     c->t_mvcc_total = 0;
     return phantom_block(c, M, block, block_num, flags, flags, ntx, commit);
   }

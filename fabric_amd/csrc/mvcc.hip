@@ -225,7 +225,7 @@ struct VRW {
   S ns, coll;
   bool hashed;
   bool unsup = false;
-  bool rq = false;  // range queries: validated here, checked by the host phantom path
+  bool host = false;  // range queries / metadata writes: validated here, decided by the host path
   DEV Kind kind(uint32_t n) { return (n >= 1 && n <= (hashed ? 3u : 4u)) ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
   DEV bool on_len(uint32_t n, S s, bool &ovf) {
@@ -235,7 +235,7 @@ struct VRW {
       sk->read(ns, hashed, coll, r.key, r.has_ver, r.v.b, r.v.t);
       return true;
     }
-    if (!hashed && n == 2) { rq = true; VRQ q; return decode(s, q, ovf); }  // range query
+    if (!hashed && n == 2) { host = true; VRQ q; return decode(s, q, ovf); }  // range query
     if (n == (hashed ? 2u : 3u)) {
       VWrite w{hashed};
       if (!decode(s, w, ovf)) return false;
@@ -248,7 +248,7 @@ struct VRW {
       sk->write(ns, hashed, coll, w.key, del);
       return true;
     }
-    unsup = true;  // metadata write (key-level endorsement / metadata): outside the model
+    host = true;  // metadata write (conditional on the key existing: the host path)
     VMetaW m{hashed};
     return decode(s, m, ovf);
   }
@@ -279,7 +279,7 @@ struct VNsHdr {
 struct VNsColls {
   Sink *sk;
   S ns;
-  bool fail = false, unsup = false;
+  bool fail = false, unsup = false, host = false;
   DEV Kind kind(uint32_t n) { return n == 3 ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
   DEV bool on_len(uint32_t, S s, bool &ovf) {
@@ -288,6 +288,7 @@ struct VNsColls {
     VRW h{sk, ns, c.name, true};
     if (!decode(c.hashed, h, ovf)) { fail = true; return true; }
     unsup |= h.unsup;
+    host |= h.host;
     return true;
   }
 };
@@ -295,7 +296,7 @@ struct VNsColls {
 // TxRwSet.FromProtoBytes unmarshals every namespace and collection before any check)
 struct VTxRW {
   Sink *sk;
-  bool fail = false, unsup = false, rq = false;
+  bool fail = false, unsup = false, host = false;
   DEV Kind kind(uint32_t n) { return n == 1 ? K_VARINT : n == 2 ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
   DEV bool on_len(uint32_t, S s, bool &ovf) {
@@ -304,11 +305,12 @@ struct VTxRW {
     VRW kv{sk, h.ns, S{nullptr, 0}, false};
     if (!decode(h.rwset, kv, ovf)) fail = true;
     unsup |= kv.unsup;
-    rq |= kv.rq;
+    host |= kv.host;
     VNsColls cs{sk, h.ns};
     if (!decode(s, cs, ovf)) return false;
     fail |= cs.fail;
     unsup |= cs.unsup;
+    host |= cs.host;
     return true;
   }
 };
@@ -359,14 +361,14 @@ DEV uint8_t find_results(S d, S &results) {
   return 0;
 }
 
-DEV uint8_t walk_rwset(S results, Sink &sk, bool &rq) {
+DEV uint8_t walk_rwset(S results, Sink &sk, bool &host) {
   bool ovf = false;
   VTxRW rw{&sk};
   const bool ok = decode(results, rw, ovf);
   if (ovf) return MV_UNSUP;
   if (!ok || rw.fail) return MV_OTHER;
   if (rw.unsup || sk.big) return MV_UNSUP;
-  rq = rw.rq;
+  host = rw.host;
   return 0;
 }
 
@@ -408,14 +410,14 @@ __global__ __launch_bounds__(64) void k_mvx_count(uint32_t ntx, const uint8_t *_
       I.code = find_results(S{base + envtab[2 * t], envtab[2 * t + 1]}, results);
       if (I.code == 0) {
         Sink sk{base, nullptr, nullptr, t, 0, 0, 0, false};
-        bool rq = false;
-        I.code = walk_rwset(results, sk, rq);
+        bool host = false;
+        I.code = walk_rwset(results, sk, host);
         I.rws_off = (uint32_t)(results.p - base);
         I.rws_len = results.n;
         if (I.code == 0) { nr = sk.nr; nw = sk.nw; wb = sk.wbytes; }
-        // range queries: the block goes to the host phantom path (fgv_mvcc.cpp), which takes
-        // these codes and result spans (MV_UNSUP_RQ stops the device pipeline like MV_UNSUP)
-        if (I.code == 0 && rq) atomicOr(&c->unsup, MV_UNSUP_RQ);
+        // range queries / metadata writes: the block goes to the host path (fgv_mvcc.cpp),
+        // which takes these codes and rwset spans (MV_HOSTPATH stops the device pipeline)
+        if (I.code == 0 && host) atomicOr(&c->unsup, MV_HOSTPATH);
       }
       if (I.code == MV_UNSUP) atomicOr(&c->unsup, 1u);
     }
@@ -437,8 +439,8 @@ __global__ __launch_bounds__(64) void k_mvx_emit(uint32_t ntx, const uint8_t *__
   MvTxInfo I = info[t];
   if (I.code != 0) return;
   Sink sk{base, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
-  bool rq = false;
-  walk_rwset(S{base + I.rws_off, I.rws_len}, sk, rq);
+  bool host = false;
+  walk_rwset(S{base + I.rws_off, I.rws_len}, sk, host);
   // one key written twice by one tx: txOps adds the flags (tx_ops.go:183-191) -> semantics
   // the engine does not model (upsert+upsert reads as a metadata-only update)
   const MvRec *w = writes + I.wbeg;

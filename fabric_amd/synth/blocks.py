@@ -101,8 +101,14 @@ def range_query_info(start, end, exhausted, raw=None, merkle=None) -> bytes:
     return out
 
 
-def kv_rwset(reads, writes, rqs=()) -> bytes:
-    """KVRWSet{reads 1, range_queries_info 2 (rqs: range_query_info bytes), writes 3}"""
+def _meta_entries() -> bytes:
+    """KVMetadataEntry{name "VALIDATION_PARAMETER", value}: a key-level endorsement policy slot"""
+    return f_msg(2, f_str(1, "VALIDATION_PARAMETER") + f_bytes(2, b"x"))
+
+
+def kv_rwset(reads, writes, rqs=(), meta=()) -> bytes:
+    """KVRWSet{reads 1, range_queries_info 2 (rqs: range_query_info bytes), writes 3,
+    metadata_writes 4 (meta: keys)}"""
     out = b""
     for k, ver in reads:
         out += f_msg(1, _kvread(k, ver))
@@ -110,10 +116,12 @@ def kv_rwset(reads, writes, rqs=()) -> bytes:
         out += f_msg(2, q)
     for k, val, is_del in writes:
         out += f_msg(3, f_str(1, k) + f_varint(2, 1 if is_del else 0) + f_bytes(3, val))
+    for k in meta:
+        out += f_msg(4, f_str(1, k) + _meta_entries())
     return out
 
 
-def hashed_rwset(reads, writes) -> bytes:
+def hashed_rwset(reads, writes, meta=()) -> bytes:
     """HashedRWSet{hashed_reads: KVReadHash{key_hash, version}, hashed_writes: KVWriteHash{key_hash,
     is_delete, value_hash}}: reads [(key_hash, ver|None)], writes [(key_hash, value_hash, is_delete)]"""
     out = b""
@@ -122,6 +130,8 @@ def hashed_rwset(reads, writes) -> bytes:
         out += f_msg(1, f_bytes(1, k) + v)
     for k, vh, is_del in writes:
         out += f_msg(2, f_bytes(1, k) + f_varint(2, 1 if is_del else 0) + f_bytes(3, vh))
+    for k in meta:
+        out += f_msg(3, f_bytes(1, k) + _meta_entries())
     return out
 
 

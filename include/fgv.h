@@ -341,12 +341,18 @@ int fgv_statedb_stats(fgv_ctx *ctx, uint64_t *keys, uint64_t *arena_used, uint64
  * the valid write sets to the state cache at Height{block_num, txIdx}.  d_block: optional
  * device copy of the block bytes.  Hashed (private-data) reads are checked like public reads
  * against ns + "$$h" + coll (validator.go:246-293); writes are deletes by IsKVWriteDelete /
- * IsKVWriteHashDelete (rwset_proto_util.go:366-375).  Range queries, metadata writes (public
- * or hashed) and a key written twice by one transaction (txOps adds the operation flags,
- * tx_ops.go:183-191) return FGV_EUNSUPPORTED; so does a committer-valid envelope the reference
- * would halt on.  Nothing is committed then, nor on FGV_ENOMEM (table / arena full).  The
- * rwsets are extracted, checked and committed on the device: one upload of the envelope table
- * and the flags, one read-back of the codes. */
+ * IsKVWriteHashDelete (rwset_proto_util.go:366-375).  The rwsets are extracted, checked and
+ * committed on the device: one upload of the envelope table and the flags, one read-back of
+ * the codes.  A block with range queries or metadata writes takes the host path instead
+ * (validator.go:205-244 phantom checks -> PHANTOM_READ_CONFLICT(12), with the raw-reads and
+ * merkle-summary validators; tx_ops.go:17-53 metadata-only writes re-put an existing key at the
+ * writer's height): the device classifies the transactions and answers committed-version
+ * lookups and range scans of the state table, the host runs the block in order.  A key written
+ * twice (or given two metadata writes) by one transaction (txOps adds the operation flags,
+ * tx_ops.go:183-203) returns FGV_EUNSUPPORTED, as does what the reference halts or panics on: a
+ * committer-valid envelope it cannot parse, a merkle summary with maxDegree < 2, a versionless
+ * raw range read it compares, a metadata write to a key deleted earlier in the block.  Nothing
+ * is committed then, nor on FGV_ENOMEM (table / arena full). */
 int fgv_mvcc_validate_block(fgv_ctx *ctx, const uint8_t *block, size_t len, const uint8_t *d_block,
                             uint64_t block_num, uint8_t *flags, size_t ntx, int commit);
 /* fgv_mvcc_validate_block that also walks the NEXT block's framing (next, next_len; the

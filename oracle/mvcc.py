@@ -20,9 +20,13 @@ Follows (citations under /root/reference/core/ledger/kvledger/txmgmt):
   validation/validator.go:134-162       per namespace in order: public reads (11), then range
         queries (PHANTOM_READ_CONFLICT 12, oracle/rangequery.py), then the collections' hashed
         reads (11)
-Metadata writes and a key written twice by one transaction are outside the modelled state and
-raise Unsupported; so does a range query the reference errors out on (maxDegree < 2, a raw read
-without a version).
+  validation/tx_ops.go:17-53,97-230     prepareTxOps: per key a delete wins, an upsert puts, and a
+        metadata-only write puts the key's latest value again (a new version) if the key exists
+        in the preceding updates or the committed state, else it is a no-op
+A key written twice (or given two metadata writes) by one transaction is outside the modelled
+state (txOps adds the operation flags) and raises Unsupported; so does what the reference errors
+out or panics on: a range query with maxDegree < 2 or a versionless raw read, a metadata write to
+a key an earlier transaction of the block deleted (PutValAndMetadata(nil value)).
 """
 import bisect
 import hashlib
@@ -80,12 +84,10 @@ def _tx_rwsets(env_bytes):
     out = []
     for ns in rw:
         kv = ns["kv"]
-        if kv.get("metadata_writes"):
-            raise Unsupported("metadata writes")
-        if any(c["hashed"].get("metadata_writes") for c in ns["coll"]):
-            raise Unsupported("private-data metadata writes")
         name = ns["namespace"]
-        e = dict(ns=name, reads=[], rqs=[], colls=[], writes=[])
+        e = dict(ns=name, reads=[], rqs=[], colls=[], writes=[], meta=[])
+        for m in kv.get("metadata_writes", []):
+            e["meta"].append((False, name, m.get("key", "")))
         for r in kv.get("reads", []):
             e["reads"].append((r.get("key", ""), _ver(r.get("version"))))
         for q in kv.get("range_queries_info", []):
@@ -109,15 +111,24 @@ def _tx_rwsets(env_bytes):
                 vh = bytes(w.get("value_hash") or b"")
                 e["writes"].append((True, hns, bytes(w.get("key_hash") or b""),
                                     bool(w.get("is_delete", False)) or not vh or vh == _EMPTY_HASH))
+            for m in h.get("metadata_writes", []):
+                e["meta"].append((True, hns, bytes(m.get("key_hash") or b"")))
         out.append(e)
     # a key written twice by one transaction: txOps adds the operation flags
     # (validation/tx_ops.go:183-191), a state the engine does not model
-    seen = set()
+    seen, mseen = set(), set()
     for e in out:
         for hashed, nsname, key, _ in e["writes"]:
             if (hashed, nsname, _kb(key)) in seen:
                 raise Unsupported("key written twice by one transaction")
             seen.add((hashed, nsname, _kb(key)))
+    for e in out:
+        for hashed, nsname, key in e["meta"]:
+            if (hashed, nsname, _kb(key)) in mseen:
+                raise Unsupported("two metadata writes of one key in one transaction")
+            mseen.add((hashed, nsname, _kb(key)))
+    for e in out:  # a metadata write beside a KVWrite of the key follows the write
+        e["meta"] = [m for m in e["meta"] if (m[0], m[1], _kb(m[2])) not in seen]
     return out
 
 
@@ -186,6 +197,13 @@ def validate_block(state, block_bytes, flags, block_num, commit=False, updates_o
         for e in sets:
             for hashed, ns, key, is_del in e["writes"]:
                 updates[(hashed, ns, _kb(key))] = ((block_num, i), is_del)
+        for e in sets:  # metadata-only writes (prepareTxOps: retrieveLatestState)
+            for hashed, ns, key in e["meta"]:
+                u = updates.get((hashed, ns, _kb(key)))
+                if u is not None and u[1]:
+                    raise Unsupported("metadata write to a key deleted earlier in the block (the reference panics)")
+                if u is not None or state.get_version(ns, key) is not None:
+                    updates[(hashed, ns, _kb(key))] = ((block_num, i), False)
     if updates_out is not None:
         updates_out.update(updates)
     if commit:

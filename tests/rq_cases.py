@@ -151,12 +151,13 @@ def random_blocks(seed, nblocks=4, ntx=120, nkeys=60):
                 else:
                     rqs.append(rqi(start, end, exhausted, raw=res))
             writes = []
-            for k in rnd.sample(keys, rnd.randint(0, 2)):
+            for k in rnd.sample(keys[10:], rnd.randint(0, 2)):  # (keys[:10] are never deleted)
                 writes.append((k, b"" if rnd.random() < 0.25 else b"val", False))
-            ns_sets = [(ns, B.kv_rwset(reads, writes, rqs))]
+            meta = rnd.sample(keys[:10], 1) if rnd.random() < 0.12 else []  # metadata-only writes
+            ns_sets = [(ns, B.kv_rwset(reads, writes, rqs, meta))]
             if rnd.random() < 0.15:
                 kh = bytes([rnd.randrange(256) for _ in range(32)])
-                ns_sets = [(ns, B.kv_rwset(reads, writes, rqs), [("coll", B.hashed_rwset([(kh, None)], [(kh, b"h" * 32, False)]))])]
+                ns_sets = [(ns, B.kv_rwset(reads, writes, rqs, meta), [("coll", B.hashed_rwset([(kh, None)], [(kh, b"h" * 32, False)]))])]
             envs.append(env(ns_sets, i, number))
             flags.append(0 if rnd.random() < 0.95 else 10)
         from tests.blockfix import block_from_envs
@@ -168,3 +169,37 @@ def random_blocks(seed, nblocks=4, ntx=120, nkeys=60):
         OM.validate_block(sdb, blk, flags, number, commit=True)
         state = {(n, k.decode() if isinstance(k, bytes) and n in ("ns1", "ns2") else k): v for (n, k), v in sdb.v.items()}
     return db, blocks
+
+
+def _hk(s):
+    import hashlib
+    return hashlib.sha256(s).digest()
+
+
+def meta_db():
+    return {("ns1", "key1"): (1, 0), ("ns1", "key2"): (1, 1), ("ns1$$hcoll1", _hk(b"k1")): (1, 2)}
+
+
+def meta_cases():
+    """metadata writes (tx_ops.go:17-53): -> [(name, [envelopes], committer flags, expected codes
+    or "unsupported")], validated against meta_db() at block 5"""
+    def mtx(reads=(), writes=(), meta=(), hreads=(), hwrites=(), hmeta=()):
+        sets = [("ns1", B.kv_rwset(reads, writes, (), meta))]
+        if hreads or hwrites or hmeta:
+            sets = [("ns1", B.kv_rwset(reads, writes, (), meta), [("coll1", B.hashed_rwset(hreads, hwrites, hmeta))])]
+        return env(sets)
+    return [
+        ("meta_existing_key_bumps_version", [mtx(meta=["key1"]), mtx(reads=[("key1", (1, 0))])], [0, 0], [0, 11]),
+        ("meta_absent_key_is_noop", [mtx(meta=["key9"]), mtx(reads=[("key9", None)])], [0, 0], [0, 0]),
+        ("meta_after_delete_panics", [mtx(writes=[("key2", b"", True)]), mtx(meta=["key2"])], [0, 0], "unsupported"),
+        ("meta_on_key_put_earlier", [mtx(writes=[("key9", b"v", False)]), mtx(meta=["key9"]), mtx(reads=[("key9", None)])],
+         [0, 0, 0], [0, 0, 11]),
+        ("write_plus_meta_same_tx", [mtx(writes=[("key1", b"v", False)], meta=["key1"]), mtx(reads=[("key1", (1, 0))])],
+         [0, 0], [0, 11]),
+        ("hashed_meta_existing", [mtx(hmeta=[_hk(b"k1")]), mtx(hreads=[(_hk(b"k1"), (1, 2))])], [0, 0], [0, 11]),
+        ("hashed_meta_absent_noop", [mtx(hmeta=[_hk(b"zz")]), mtx(hreads=[(_hk(b"zz"), None)])], [0, 0], [0, 0]),
+        ("two_meta_writes_one_key", [mtx(meta=["key1", "key1"])], [0], "unsupported"),
+        ("committer_invalid_meta_skipped", [mtx(reads=[("key1", (1, 0))]), mtx(meta=["key1"])], [0, 10], [0, 10]),
+        ("invalid_tx_meta_not_applied", [mtx(reads=[("key1", (7, 7))], meta=["key2"]), mtx(reads=[("key2", (1, 1))])],
+         [0, 0], [11, 0]),
+    ]

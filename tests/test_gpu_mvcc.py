@@ -133,15 +133,28 @@ def test_private_data_blocks_match_oracle_and_labels():
     eng.close()
 
 
-def test_hashed_metadata_write_unsupported():
-    from tests.test_oracle_mvcc import hashed_metadata_block
-    eng = _lib.Engine(0)
-    eng.statedb_init(1 << 12, 1 << 20)
-    blk = hashed_metadata_block()
-    with pytest.raises(_lib.Unsupported):
-        eng.mvcc_validate(blk, 2, [0, 0], commit=False)
-    assert list(eng.mvcc_validate(blk, 2, [0, 10], commit=False)) == [0, 10]
-    eng.close()
+def test_metadata_write_known_answers():
+    """metadata writes go to the host path (fgv_mvcc.cpp): codes, unsupported cases and the
+    committed versions equal the oracle's"""
+    from tests import rq_cases as RQ
+    from tests.test_gpu_rangequery import _engine as rq_engine
+    for name, envs, flags, exp in RQ.meta_cases():
+        eng = rq_engine(RQ.meta_db())
+        blk = _blk(envs)
+        if exp == "unsupported":
+            with pytest.raises(_lib.Unsupported):
+                eng.mvcc_validate(blk, 5, flags, commit=True)
+            eng.close()
+            continue
+        st = OM.StateDB(RQ.meta_db())
+        assert list(eng.mvcc_validate(blk, 5, flags, commit=True)) == exp == OM.validate_block(st, blk, flags, 5,
+                                                                                               commit=True), name
+        # the next block reads every key at the oracle's committed version
+        keys = sorted({k for (ns, k) in st.v if ns == "ns1"} | {b"key1", b"key2", b"key9"})
+        reads = [(k.decode(), st.get_version("ns1", k)) for k in keys]
+        nxt = _blk([_tx(reads, [])])
+        assert list(eng.mvcc_validate(nxt, 6, [0], commit=False)) == [0], name
+        eng.close()
 
 
 def test_reference_bulkload_known_answers():

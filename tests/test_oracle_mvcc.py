@@ -116,19 +116,22 @@ def test_labels_with_private_data():
         assert 11 in out
 
 
-def hashed_metadata_block():
-    """a committer-valid tx with a hashed metadata write (KVMetadataWriteHash): outside the model"""
-    meta = B.f_msg(3, B.f_bytes(1, _hk(b"k1")) + B.f_msg(2, B.f_str(1, "VALIDATION_PARAMETER") + B.f_bytes(2, b"x")))
-    env = M._envelope(B.tx_rwset([("ns1", B.kv_rwset([], []), [("coll1", meta)])]), 0, 1)
-    return _blk([_tx([("a", None)], []), env])
-
-
-def test_hashed_metadata_write_unsupported():
+def test_metadata_write_known_answers():
+    """metadata writes (tx_ops.go:17-53): a metadata-only write re-puts an existing key at the
+    writer's height, is a no-op on an absent key, and makes the reference panic after a delete"""
     import pytest
     from oracle.v20 import Unsupported
-    with pytest.raises(Unsupported):
-        OM.validate_block(OM.StateDB(), hashed_metadata_block(), [0, 0], 2)
-    assert OM.validate_block(OM.StateDB(), hashed_metadata_block(), [0, 10], 2) == [0, 10]  # skipped: fine
+    from tests import rq_cases as RQ
+    for name, envs, flags, exp in RQ.meta_cases():
+        st = OM.StateDB(RQ.meta_db())
+        if exp == "unsupported":
+            with pytest.raises(Unsupported):
+                OM.validate_block(st, _blk(envs), flags, 5)
+            continue
+        assert OM.validate_block(st, _blk(envs), flags, 5, commit=True) == exp, name
+    st = OM.StateDB(RQ.meta_db())  # the committed version of a metadata-only update
+    OM.validate_block(st, _blk(RQ.meta_cases()[0][1]), [0, 0], 5, commit=True)
+    assert st.get_version("ns1", "key1") == (5, 0)
 
 
 def bulkload_case():
