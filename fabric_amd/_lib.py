@@ -28,7 +28,7 @@ EXPORTED = [
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash",
     "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
     "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d",
-    "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead",
+    "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead", "fgv_blocks_verify_signed",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -57,7 +57,7 @@ class BlockCheck(ctypes.Structure):
 
 # fgv_block_check.status (include/fgv.h)
 BLK_OK, BLK_UNPARSABLE, BLK_NO_HEADER, BLK_NUMBER, BLK_PREV_HASH, BLK_METADATA, BLK_EMPTY, BLK_TX_MALFORMED, \
-    BLK_DATA_HASH = range(9)
+    BLK_DATA_HASH, BLK_SIGNATURES, BLK_SIG_UNSUPPORTED = range(11)
 
 
 KEY_TYPES = {"p256": 1, "p384": 2, "other": 3, "undeserializable": 4}
@@ -142,6 +142,7 @@ def load():
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.POINTER(ctypes.c_uint32)]
         L.fgv_blocks_verify.argtypes = [vp, sz, vp, vp, vp, vp]
+        L.fgv_blocks_verify_signed.argtypes = [vp, sz, vp, vp, vp, ctypes.c_char_p, ctypes.c_int, vp]
         L.fgv_set_parse_mode.argtypes = [vp, ctypes.c_int]
         L.fgv_sha256_host.argtypes = [vp, sz, vp]
         L.fgv_commit_hash.argtypes = [vp, sz, vp, sz, ctypes.c_uint64, vp, sz, vp]
@@ -530,9 +531,19 @@ class Engine:
                                                        _ptr(hi), ctypes.c_void_p(d_gathered), _ptr(flags)))
         return flags
 
-    # --- deliver-side block integrity (VerifyBlock minus orderer signatures)
+    # --- deliver-side block integrity (VerifyBlock; _signed: with the orderer signatures)
     def blocks_verify(self, blocks, chain=None):
         return blocks_verify(blocks, chain, ctx=self._h)
+
+    def blocks_verify_signed(self, blocks, chain=None, policy=None, bft=False):
+        """fgv_blocks_verify_signed -> (per-block tuples as blocks_verify, unsupported): when
+        `unsupported`, the blocks from the first BLK_SIG_UNSUPPORTED on were not decided."""
+        pol = policy.encode() if policy is not None else None
+        rc, out = _verify_call(lambda *a: self._L.fgv_blocks_verify_signed(self._h, *a[:4], pol, 1 if bft else 0,
+                                                                            a[4]), blocks, chain)
+        if rc != FGV_EUNSUPPORTED:
+            _check(rc)
+        return out, rc == FGV_EUNSUPPORTED
 
     # --- MVCC
     def statedb_init(self, slots=1 << 22, arena_bytes=64 << 20):
@@ -598,13 +609,19 @@ def blocks_verify(blocks, chain=None, ctx=None):
     """fgv_blocks_verify: per-block (status, bad_tx, number, data_hash, header_hash); `chain`
     (ChainState) is advanced past every verified block.  ctx None -> one host thread."""
     L = load()
+    rc, out = _verify_call(lambda *a: L.fgv_blocks_verify(ctx, *a), blocks, chain)
+    _check(rc)
+    return out
+
+
+def _verify_call(fn, blocks, chain, *extra):
     nb = len(blocks)
     bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
     ptrs = (ctypes.c_void_p * nb)(*[b.ctypes.data for b in bufs])
     lens = (ctypes.c_size_t * nb)(*[len(b) for b in blocks])
     out = (BlockCheck * nb)()
-    _check(L.fgv_blocks_verify(ctx, nb, ptrs, lens, ctypes.byref(chain) if chain is not None else None, out))
-    return [(o.status, o.bad_tx, o.number, bytes(o.data_hash), bytes(o.header_hash)) for o in out]
+    rc = fn(nb, ptrs, lens, ctypes.byref(chain) if chain is not None else None, *extra, out)
+    return rc, [(o.status, o.bad_tx, o.number, bytes(o.data_hash), bytes(o.header_hash)) for o in out]
 
 
 def sha256_host(buf: bytes):

@@ -847,7 +847,9 @@ DEV int eval_policy(const DevChannel &ch, uint32_t pi, const int32_t *ids, uint3
       if (v == 2 || v < 0) return v;
       ok += v;
     }
-    return ok >= P.threshold ? 1 : 0;
+    // threshold 0 (no sub-policies, or an unknown rule): `remaining` starts at 0 and every
+    // satisfied sub-policy drives it negative, so only "none satisfied" succeeds
+    return (P.threshold == 0 ? ok == 0 : ok >= P.threshold) ? 1 : 0;
   }
   return 2;
 }

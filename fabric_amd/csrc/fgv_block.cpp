@@ -500,7 +500,9 @@ static int eval_policy(const Channel &ch, int pi, const int *ids, size_t nids, i
         if (v == 2) return 2;
         ok += v;
       }
-      return ok >= P.threshold ? 1 : 0;
+      // threshold 0 (no sub-policies, or an unknown rule): `remaining` starts at 0 and every
+      // satisfied sub-policy drives it negative, so only "none satisfied" succeeds
+      return (P.threshold == 0 ? ok == 0 : ok >= P.threshold) ? 1 : 0;
     }
     default: return 2;
   }
@@ -1421,5 +1423,174 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   c->t_host_fold = 0;
   if (hm[5] & 1u) return 1;
   if (hm[5] & 2u) return FGV_EUNSUPPORTED;
+  return FGV_OK;
+}
+
+// ======================================================================= orderer signatures
+// BlockSignatureVerifier (protoutil/blockutils.go:245-290) for a channel that does not run BFT,
+// then policy.EvaluateSignedData of the channel policy it was built with
+// (deliverclient/verifier_assembler.go:32-56: /Channel/Orderer/BlockValidation):
+//   Metadata = proto.Unmarshal(metadata[SIGNATURES])            error -> fail
+//   per MetadataSignature, in order: SignatureHeader unmarshal   error -> fail
+//     SignedData{Identity: header.Creator, Signature, Data: md.Value || signature_header ||
+//                BlockHeaderBytes(header)}
+//   EvaluateSignedData: SignatureSetToValidIdentities (policy.go:363-395: deserialize, dedup on
+//   Mspid+Id, verify, in order) feeding the cauthdsl / ImplicitMeta evaluation.
+// Under BFT a signature with an empty signature header and an identifier header names a
+// consenter by number (blockutils.go:262-273): outside the model -> FGV_SIGV_UNSUP.  Verify bits
+// are pure functions of (key, message, signature), so every block's signatures are verified in
+// one GPU pass ahead of the sequential fold.
+namespace {
+struct VMetaSig {  // MetadataSignature {signature_header = 1, signature = 2, identifier_header = 3}
+  Span sig_header, signature, id_header;
+  pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    (n == 1 ? sig_header : n == 2 ? signature : id_header) = s;
+    return true;
+  }
+};
+struct VMetadata {  // Metadata {value = 1, repeated MetadataSignature signatures = 2}
+  Span value;
+  std::vector<VMetaSig> sigs;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 1) {
+      value = s;
+      return true;
+    }
+    VMetaSig m;
+    if (!pbw::decode(s.p, s.n, m)) return false;
+    sigs.push_back(m);
+    return true;
+  }
+};
+struct SigItem {
+  int ident;          // Channel::lookup: index, -1 deserialize error, -2 outside the model
+  uint32_t vjob;      // verify job (UINT32_MAX: none)
+  Span sig;
+};
+}  // namespace
+
+// ManagerImpl.GetPolicy on the root manager (policy.go:330-358): index, 0 = reject (absent,
+// or not under /Channel/), -1 = no usable channel config
+static int channel_policy_index(const Channel &ch, const std::string &path) {
+  if (!ch.config.present || ch.config.unsupported) return -1;
+  std::string ref = path;
+  if (!ref.empty() && ref[0] == '/') {
+    static const std::string root = "/Channel/";
+    if (ref.compare(0, root.size(), root) != 0) return 0;
+    ref = ref.substr(root.size());
+  }
+  auto it = ch.chan_idx.find(ref);
+  return (ref.empty() || it == ch.chan_idx.end()) ? 0 : it->second;
+}
+
+int fgv_block_sig_verdicts(fgv_ctx *c, size_t n, const fgv_sig_block *in, const char *policy, int bft,
+                           uint8_t *verdict) {
+  std::lock_guard<std::mutex> g(c->mu);
+  Channel &ch = c->blk->ch;
+  if (ch.dirty) ch.compile();
+  const int pi = channel_policy_index(ch, policy ? policy : "/Channel/Orderer/BlockValidation");
+  // does the evaluation reach SignatureSetToValidIdentities?  A signature policy does; an
+  // ImplicitMeta policy does through any signature sub-policy (a rejecting sub-policy never
+  // satisfies, so the walk cannot stop before the first signature one); a reject policy never.
+  bool reads_ids = false;
+  if (pi > 0) {
+    const Policy &P = ch.policies[pi];
+    reads_ids = P.kind == PK_SIG || P.kind == PK_UNSUP;
+    if (P.kind == PK_IMPLICIT)
+      for (int s : P.subs) reads_ids |= ch.policies[s].kind != PK_REJECT;
+  }
+  std::vector<std::vector<SigItem>> items(n);
+  std::vector<uint8_t> msgs;
+  std::vector<uint64_t> moff, soff;
+  std::vector<uint32_t> mlen, slen, slots;
+  std::vector<const uint8_t *> sptr;
+  for (size_t b = 0; b < n; b++) {
+    verdict[b] = FGV_SIGV_FAIL;
+    if (!in[b].want) continue;
+    if (pi < 0) {
+      verdict[b] = FGV_SIGV_UNSUP;
+      continue;
+    }
+    VMetadata md;
+    if (!pbw::decode(in[b].meta, in[b].meta_n, md)) continue;  // "error unmarshalling signatures"
+    bool bad = false, unsup = false;
+    std::vector<SigItem> &its = items[b];
+    const size_t m0 = msgs.size(), j0 = moff.size();
+    for (const VMetaSig &ms : md.sigs) {
+      if (bft && ms.sig_header.n == 0 && ms.id_header.n > 0) {
+        unsup = true;
+        break;
+      }
+      VSignatureHeader sh;
+      if (!pbw::decode(ms.sig_header.p, ms.sig_header.n, sh)) {
+        bad = true;
+        break;
+      }
+      SigItem it{ch.lookup(sh.creator), UINT32_MAX, ms.signature};
+      if (it.ident >= 0 && ch.idents[it.ident].verify_class() == 0 && reads_ids) {
+        it.vjob = (uint32_t)moff.size();
+        moff.push_back(msgs.size());
+        msgs.insert(msgs.end(), md.value.p, md.value.p + md.value.n);
+        msgs.insert(msgs.end(), ms.sig_header.p, ms.sig_header.p + ms.sig_header.n);
+        msgs.insert(msgs.end(), in[b].hdr_der.begin(), in[b].hdr_der.end());
+        mlen.push_back((uint32_t)(msgs.size() - moff.back()));
+        sptr.push_back(ms.signature.p);
+        slen.push_back(ms.signature.n);
+        slots.push_back((uint32_t)ch.idents[it.ident].key_slot);
+      }
+      its.push_back(it);
+    }
+    if (bad || unsup) {
+      verdict[b] = unsup ? FGV_SIGV_UNSUP : FGV_SIGV_FAIL;
+      its.clear();
+      msgs.resize(m0);
+      moff.resize(j0);
+      mlen.resize(j0);
+      sptr.resize(j0);
+      slen.resize(j0);
+      slots.resize(j0);
+      continue;
+    }
+    verdict[b] = 0xFF;  // evaluated below
+  }
+  // one GPU pass over every signature the evaluations may read
+  const size_t nv = moff.size();
+  std::vector<uint8_t> vst(nv, 1);
+  if (nv) {
+    std::vector<uint8_t> sigs;
+    soff.resize(nv);
+    for (size_t j = 0; j < nv; j++) {
+      soff[j] = sigs.size();
+      sigs.insert(sigs.end(), sptr[j], sptr[j] + slen[j]);
+    }
+    const int rc = fgv_verify_msgs_slots_locked(c, msgs.data(), msgs.size(), moff.data(), mlen.data(), sigs.data(),
+                                                sigs.size(), soff.data(), slen.data(), slots.data(), nv, vst.data());
+    if (rc) return rc;
+  }
+  for (size_t b = 0; b < n; b++) {
+    if (verdict[b] != 0xFF) continue;
+    pbw::SmallVec<int, 16> ids;
+    bool unsup = false;
+    if (reads_ids) {
+      pbw::SmallVec<uint32_t, 16> seen;
+      for (const SigItem &it : items[b]) {
+        if (it.ident == -2) { unsup = true; break; }
+        if (it.ident < 0) continue;
+        const Ident &I = ch.idents[it.ident];
+        if (std::find(seen.begin(), seen.end(), I.canon) != seen.end()) continue;
+        const int vc = I.verify_class();
+        if (vc == 2) { unsup = true; break; }
+        if (vc == 1 || it.vjob == UINT32_MAX || vst[it.vjob] != 0) continue;
+        seen.push_back(I.canon);
+        ids.push_back(it.ident);
+      }
+    }
+    int v = unsup ? 2 : pi == 0 ? 0 : eval_policy(ch, pi, ids.data(), ids.size());
+    verdict[b] = v == 2 ? FGV_SIGV_UNSUP : v == 1 ? FGV_SIGV_OK : FGV_SIGV_FAIL;
+  }
   return FGV_OK;
 }

@@ -304,13 +304,72 @@ static void read_stage_times(fgv_ctx *c, bool ran) {
 }
 
 // ------------------------------------------------------------------ verify core
+// Host half of verifyECDSA for item i: Go-rule DER (utils.UnmarshalECDSASignature) + low-S;
+// writes r, s (zero unless pending) and returns ST_PENDING when the device must finish it,
+// FGV_SIG_* otherwise, or -1 for an offset outside sig_buf.
+static int der_prepare(const uint8_t *sig_buf, size_t sig_buf_len, size_t so, size_t sl, uint32_t r[8],
+                       uint32_t s[8]) {
+  int code = ST_PENDING;
+  if (sl == 0) {
+    code = FGV_SIG_EMPTY;
+  } else if (so > sig_buf_len || sl > sig_buf_len - so) {
+    return -1;
+  } else {
+    bool rb, sb;
+    if (fgv::der_decode_sig(sig_buf + so, sl, r, s, rb, sb)) {
+      code = FGV_SIG_DER;
+    } else if (sb || !fgv::is_low_s(s)) {
+      code = FGV_SIG_HIGH_S;
+    } else if (rb) {
+      // r >= 2^256: force an out-of-range value (n) so the device reports RANGE after
+      // the key check, matching ecdsa.Verify's order
+      static const uint32_t NL[8] = {0xFC632551u, 0xF3B9CAC2u, 0xA7179E84u, 0xBCE6FAADu,
+                                     0xFFFFFFFFu, 0xFFFFFFFFu, 0x00000000u, 0xFFFFFFFFu};
+      memcpy(r, NL, 32);
+    }
+  }
+  if (code != ST_PENDING) {
+    memset(r, 0, 32);
+    memset(s, 0, 32);
+  }
+  return code;
+}
+
+// upload the prepared items (status / slot / r / s columns in the host staging buffers) and
+// digests, run the device stages for the pending ones, read the statuses back
+static int verify_run(fgv_ctx *c, size_t n, size_t pending, const uint8_t *h_digests, bool dev_digests,
+                      uint8_t *status_out) {
+  uint8_t *st = c->h_status.as<uint8_t>();
+  if (!c->status.ensure(n) || !c->slot.ensure(n * 4) || !c->r.ensure(n * 32) ||
+      !c->s.ensure(n * 32) || !c->dig.ensure(n * 32))
+    return FGV_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(c->status.p, st, n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->slot.p, c->h_slot.p, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->r.p, c->h_r.p, n * 32, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->s.p, c->h_s.p, n * 32, hipMemcpyHostToDevice, c->stream));
+  if (!dev_digests) {
+    if (!c->h_dig.ensure(n * 32)) return FGV_ENOMEM;
+    memcpy(c->h_dig.p, h_digests, n * 32);
+    HIP_TRY(hipMemcpyAsync(c->dig.p, c->h_dig.p, n * 32, hipMemcpyHostToDevice, c->stream));
+  }
+  if (pending) {
+    int rc = launch_verify_stages(c, (uint32_t)n, c->status.as<uint8_t>(), c->slot.as<uint32_t>(),
+                                  c->r.as<uint32_t>(), c->s.as<uint32_t>(), c->dig.as<uint8_t>());
+    if (rc) return rc;
+  }
+  HIP_TRY(hipMemcpyAsync(st, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  memcpy(status_out, st, n);
+  read_stage_times(c, pending != 0);
+  return FGV_OK;
+}
+
 // digests: host pointer (n*32) or nullptr when ctx->dig already holds device digests.
 static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, size_t sig_buf_len,
                        const uint64_t *sig_off, const uint32_t *sig_len, const uint8_t *h_digests,
                        size_t n, uint8_t *status_out, bool dev_digests) {
   if (n == 0) return FGV_OK;
   if (n > 0x7fffffffu) return FGV_EINVAL;
-  const uint32_t N = (uint32_t)n;
   if (!c->h_status.ensure(n) || !c->h_slot.ensure(n * 4) || !c->h_r.ensure(n * 32) ||
       !c->h_s.ensure(n * 32))
     return FGV_ENOMEM;
@@ -322,30 +381,10 @@ static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, 
   size_t pending = 0;
   for (size_t i = 0; i < n; i++) {
     uint32_t r[8], s[8];
-    uint8_t code = ST_PENDING;
-    const size_t so = sig_off[i], sl = sig_len[i];
-    if (sl == 0) {
-      code = FGV_SIG_EMPTY;
-    } else if (so > sig_buf_len || sl > sig_buf_len - so) {
-      return FGV_EINVAL;
-    } else {
-      bool rb, sb;
-      if (fgv::der_decode_sig(sig_buf + so, sl, r, s, rb, sb)) {
-        code = FGV_SIG_DER;
-      } else if (sb || !fgv::is_low_s(s)) {
-        code = FGV_SIG_HIGH_S;
-      } else if (rb) {
-        // r >= 2^256: force an out-of-range value (n) so the device reports RANGE after
-        // the key check, matching ecdsa.Verify's order
-        static const uint32_t NL[8] = {0xFC632551u, 0xF3B9CAC2u, 0xA7179E84u, 0xBCE6FAADu,
-                                       0xFFFFFFFFu, 0xFFFFFFFFu, 0x00000000u, 0xFFFFFFFFu};
-        memcpy(r, NL, 32);
-      }
-    }
-    st[i] = code;
+    const int code = der_prepare(sig_buf, sig_buf_len, sig_off[i], sig_len[i], r, s);
+    if (code < 0) return FGV_EINVAL;
+    st[i] = (uint8_t)code;
     if (code != ST_PENDING) {
-      memset(r, 0, 32);
-      memset(s, 0, 32);
       slot[i] = 0;
     } else {
       pending++;
@@ -413,27 +452,8 @@ static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, 
       }
   }
   // 3) upload + kernels
-  if (!c->status.ensure(n) || !c->slot.ensure(n * 4) || !c->r.ensure(n * 32) ||
-      !c->s.ensure(n * 32) || !c->dig.ensure(n * 32))
-    return FGV_ENOMEM;
-  HIP_TRY(hipMemcpyAsync(c->status.p, st, n, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->slot.p, slot, n * 4, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->r.p, R, n * 32, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->s.p, S, n * 32, hipMemcpyHostToDevice, c->stream));
-  if (!dev_digests) {
-    if (!c->h_dig.ensure(n * 32)) return FGV_ENOMEM;
-    memcpy(c->h_dig.p, h_digests, n * 32);
-    HIP_TRY(hipMemcpyAsync(c->dig.p, c->h_dig.p, n * 32, hipMemcpyHostToDevice, c->stream));
-  }
-  if (pending) {
-    int rc = launch_verify_stages(c, N, c->status.as<uint8_t>(), c->slot.as<uint32_t>(),
-                                  c->r.as<uint32_t>(), c->s.as<uint32_t>(), c->dig.as<uint8_t>());
-    if (rc) return rc;
-  }
-  HIP_TRY(hipMemcpyAsync(st, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  memcpy(status_out, st, n);
-  read_stage_times(c, pending != 0);
+  const int rc = verify_run(c, n, pending, h_digests, dev_digests, status_out);
+  if (rc) return rc;
   float ms = 0;
   if (!new_keys.empty() && hipEventElapsedTime(&ms, c->ev[6], c->ev[7]) == hipSuccess)
     c->t_keytab = ms;
@@ -463,6 +483,41 @@ static int sha_core(fgv_ctx *c, const uint8_t *buf, size_t buf_len, const uint64
   HIP_TRY(hipMemcpyAsync(c->moff.p, off, n * 8, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->mlen.p, len, n * 4, hipMemcpyHostToDevice, c->stream));
   return launch_sha(c, c->msg.as<uint8_t>(), c->moff.as<uint64_t>(), c->mlen.as<uint32_t>(), n);
+}
+
+// identity.Verify(msg, sig) for identities of the channel model (registered key slots), host
+// buffers: SHA-256 of the messages and the ECDSA stages on the device.  Caller holds c->mu.
+int fgv_verify_msgs_slots_locked(fgv_ctx *c, const uint8_t *msg_buf, size_t msg_buf_len, const uint64_t *msg_off,
+                                 const uint32_t *msg_len, const uint8_t *sig_buf, size_t sig_buf_len,
+                                 const uint64_t *sig_off, const uint32_t *sig_len, const uint32_t *slots, size_t n,
+                                 uint8_t *status_out) {
+  if (n == 0) return FGV_OK;
+  if (n > 0x7fffffffu) return FGV_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  if (!c->h_status.ensure(n) || !c->h_slot.ensure(n * 4) || !c->h_r.ensure(n * 32) || !c->h_s.ensure(n * 32))
+    return FGV_ENOMEM;
+  uint8_t *st = c->h_status.as<uint8_t>();
+  uint32_t *slot = c->h_slot.as<uint32_t>(), *R = c->h_r.as<uint32_t>(), *S = c->h_s.as<uint32_t>();
+  size_t pending = 0;
+  for (size_t i = 0; i < n; i++) {
+    uint32_t r[8], s[8];
+    const int code = der_prepare(sig_buf, sig_buf_len, sig_off[i], sig_len[i], r, s);
+    if (code < 0 || slots[i] >= c->pinned) return FGV_EINVAL;  // registered (pinned) keys only
+    st[i] = (uint8_t)code;
+    slot[i] = code == ST_PENDING ? slots[i] : 0;
+    pending += code == ST_PENDING;
+    for (int k = 0; k < 8; k++) {
+      R[(size_t)k * n + i] = r[k];
+      S[(size_t)k * n + i] = s[k];
+    }
+  }
+  int rc = sha_core(c, msg_buf, msg_buf_len, msg_off, msg_len, n);
+  if (rc) return rc;
+  rc = verify_run(c, n, pending, nullptr, true, status_out);
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->t_sha = ms;
+  c->t_keytab = 0;
+  return rc;
 }
 
 extern "C" {

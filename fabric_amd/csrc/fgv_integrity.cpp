@@ -1,12 +1,14 @@
 // fgv_integrity.cpp -- deliver-side block integrity for the committer's input
-// (BlockVerificationAssistant.VerifyBlock, common/deliverclient/block_verification.go:243-273,
-// minus the orderer signature policy):
+// (BlockVerificationAssistant.VerifyBlock, common/deliverclient/block_verification.go:243-273):
 //   verifyHeader    :311-331  header present; number == last + 1; PreviousHash == SHA-256 of
 //                             the last verified header's ASN.1 bytes (when that hash is known)
 //   verifyMetadata  :303-309  at least len(BlockMetadataIndex_name) = 5 metadata entries
 //   BlockDataHash   protoutil/blockutils.go:69-74 -> VerifyTransactionsAreWellFormed
 //                   (:310-350) then ComputeBlockDataHash (:76-79) = SHA-256(concat(Data))
 //   DataHash compare :258-263
+//   sigVerifierFunc :265-268  (fgv_blocks_verify_signed only) the orderer signatures against the
+//                             channel's BlockValidation policy, fgv_block_sig_verdicts in
+//                             fgv_block.cpp (GPU verify + the channel model's policy fold)
 // and on success the chain state advances to BlockHeaderHash (blockutils.go:48-67: SHA-256
 // of DER SEQUENCE{INTEGER number, OCTET STRING previous_hash, OCTET STRING data_hash}).
 //
@@ -117,11 +119,15 @@ struct VHdrFields {  // BlockHeader {number = 1, previous_hash = 2, data_hash = 
   void on_varint(uint32_t, uint64_t v) { number = v; }
   bool on_len(uint32_t n, Span s) { (n == 2 ? prev : data_hash) = s; return true; }
 };
-struct VMetaCount {  // BlockMetadata {repeated bytes metadata = 1}
+struct VMetaCount {  // BlockMetadata {repeated bytes metadata = 1}: count + metadata[SIGNATURES]
   size_t n = 0;
+  Span sigs;
   pbw::Kind kind(uint32_t k) { return k == 1 ? pbw::K_REP_BYTES : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
-  bool on_len(uint32_t, Span) { n++; return true; }
+  bool on_len(uint32_t, Span s) {
+    if (n++ == 0) sigs = s;
+    return true;
+  }
 };
 struct VBlockAll {
   bool has_header = false, has_data = false, has_meta = false;
@@ -206,9 +212,10 @@ static size_t der_len(uint8_t *o, size_t n) {
 
 }  // namespace
 
-// BlockHeaderBytes (asn1.Marshal of {Number *big.Int, PreviousHash, DataHash []byte}) hashed
-void fgv_block_header_hash(uint64_t number, const uint8_t *prev, size_t prev_n, const uint8_t *dh, size_t dh_n,
-                           uint8_t out[32]) {
+// BlockHeaderBytes (protoutil/blockutils.go:48-67): asn1.Marshal of {Number *big.Int,
+// PreviousHash, DataHash []byte} -- DER SEQUENCE{INTEGER, OCTET STRING, OCTET STRING}
+void fgv_block_header_der(uint64_t number, const uint8_t *prev, size_t prev_n, const uint8_t *dh, size_t dh_n,
+                          std::vector<uint8_t> &out) {
   uint8_t integer[10];
   size_t in = 0;
   {  // minimal two's-complement big-endian, positive
@@ -231,18 +238,26 @@ void fgv_block_header_hash(uint64_t number, const uint8_t *prev, size_t prev_n, 
   body.push_back(0x04);
   body.insert(body.end(), l, l + der_len(l, dh_n));
   if (dh_n) body.insert(body.end(), dh, dh + dh_n);
-  fgvsha::Stream s;
-  const uint8_t seq = 0x30;
-  s.update(&seq, 1);
-  const size_t ln = der_len(l, body.size());
-  s.update(l, ln);
-  s.update(body.data(), body.size());
-  s.final(out);
+  out.clear();
+  out.reserve(body.size() + 10);
+  out.push_back(0x30);
+  out.insert(out.end(), l, l + der_len(l, body.size()));
+  out.insert(out.end(), body.begin(), body.end());
 }
 
-extern "C" int fgv_blocks_verify(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
-                                 fgv_chain_state *chain, fgv_block_check *out) {
+void fgv_block_header_hash(uint64_t number, const uint8_t *prev, size_t prev_n, const uint8_t *dh, size_t dh_n,
+                           uint8_t out[32]) {
+  std::vector<uint8_t> der;
+  fgv_block_header_der(number, prev, prev_n, dh, dh_n, der);
+  fgvsha::sha256(der.data(), der.size(), out);
+}
+
+// sig: evaluate the orderer signatures (fgv_blocks_verify_signed) after the data hash, as
+// VerifyBlock does (block_verification.go:265-268)
+static int verify_impl(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                       fgv_chain_state *chain, fgv_block_check *out, bool sig, const char *policy, int bft) {
   if (!out || (nblocks && (!blocks || !lens))) return FGV_EINVAL;  // ctx NULL: one host thread
+  if (sig && !ctx) return FGV_EINVAL;
   struct Pre {
     VBlockAll b;
     bool parsed = false;
@@ -290,6 +305,28 @@ extern "C" int fgv_blocks_verify(fgv_ctx *ctx, size_t nblocks, const uint8_t *co
     for (size_t i = 0; i < nblocks; i++) work(i);
   }
 
+  if (lk.owns_lock()) lk.unlock();
+
+  // orderer-signature verdicts of every block that can reach the signature check (speculative:
+  // the chain checks come below; verdicts are pure functions of the block and the channel model)
+  std::vector<uint8_t> verdict;
+  if (sig) {
+    std::vector<fgv_sig_block> in(nblocks);
+    for (size_t i = 0; i < nblocks; i++) {
+      const VBlockAll &B = pre[i].b;
+      if (out[i].status != FGV_BLK_OK || !B.has_header || !B.has_meta || B.meta.n < 5) continue;
+      if (B.hdr.data_hash.n != 32 || memcmp(B.hdr.data_hash.p, out[i].data_hash, 32) != 0) continue;
+      in[i].want = true;
+      in[i].meta = B.meta.sigs.p;
+      in[i].meta_n = B.meta.sigs.n;
+      fgv_block_header_der(B.hdr.number, B.hdr.prev.p, B.hdr.prev.n, B.hdr.data_hash.p, B.hdr.data_hash.n,
+                           in[i].hdr_der);
+    }
+    verdict.assign(nblocks, FGV_SIGV_FAIL);
+    const int rc = fgv_block_sig_verdicts(ctx, nblocks, in.data(), policy, bft, verdict.data());
+    if (rc) return rc;
+  }
+
   // sequential chain checks in the reference's order; only a verified block advances it
   for (size_t i = 0; i < nblocks; i++) {
     fgv_block_check &o = out[i];
@@ -310,6 +347,15 @@ extern "C" int fgv_blocks_verify(fgv_ctx *ctx, size_t nblocks, const uint8_t *co
       o.status = FGV_BLK_DATA_HASH;
       continue;
     }
+    if (sig && verdict[i] != FGV_SIGV_OK) {
+      if (verdict[i] == FGV_SIGV_FAIL) {
+        o.status = FGV_BLK_SIGNATURES;
+        continue;
+      }
+      // outside the model: the reference decides this block, and with it the chain from here on
+      for (size_t k = i; k < nblocks; k++) out[k].status = FGV_BLK_SIG_UNSUPPORTED;
+      return FGV_EUNSUPPORTED;
+    }
     o.status = FGV_BLK_OK;
     if (chain) {
       chain->valid = 1;
@@ -319,6 +365,17 @@ extern "C" int fgv_blocks_verify(fgv_ctx *ctx, size_t nblocks, const uint8_t *co
     }
   }
   return FGV_OK;
+}
+
+extern "C" int fgv_blocks_verify(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                 fgv_chain_state *chain, fgv_block_check *out) {
+  return verify_impl(ctx, nblocks, blocks, lens, chain, out, false, nullptr, 0);
+}
+
+extern "C" int fgv_blocks_verify_signed(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
+                                        const size_t *lens, fgv_chain_state *chain, const char *policy, int bft,
+                                        fgv_block_check *out) {
+  return verify_impl(ctx, nblocks, blocks, lens, chain, out, true, policy, bft);
 }
 
 void fgv_integrity_free(fgv_ctx *c) {

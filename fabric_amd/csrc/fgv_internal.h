@@ -225,3 +225,29 @@ int fgv_block_parse_mode(fgv_block_state *S);
 int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
                            const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                            const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out);
+
+// identity.Verify(msg, sig) of registered identities (pinned key slots), host buffers; the
+// caller holds c->mu (fgv_host.cpp)
+int fgv_verify_msgs_slots_locked(fgv_ctx *c, const uint8_t *msg_buf, size_t msg_buf_len, const uint64_t *msg_off,
+                                 const uint32_t *msg_len, const uint8_t *sig_buf, size_t sig_buf_len,
+                                 const uint64_t *sig_off, const uint32_t *sig_len, const uint32_t *slots, size_t n,
+                                 uint8_t *status_out);
+// BlockHeaderBytes (protoutil/blockutils.go:48-67): ASN.1 DER of {number, previous_hash, data_hash}
+void fgv_block_header_der(uint64_t number, const uint8_t *prev, size_t prev_n, const uint8_t *dh, size_t dh_n,
+                          std::vector<uint8_t> &out);
+// The orderer-signature input of one block (fgv_integrity.cpp -> fgv_block.cpp): the marshalled
+// Metadata at metadata[SIGNATURES] and the header's BlockHeaderBytes
+struct fgv_sig_block {
+  bool want = false;  // evaluate this block (it passed every earlier check that needs no chain)
+  const uint8_t *meta = nullptr;
+  size_t meta_n = 0;
+  std::vector<uint8_t> hdr_der;
+};
+#define FGV_SIGV_FAIL 0   // the verifier returns an error (policy unsatisfied, malformed metadata)
+#define FGV_SIGV_OK 1
+#define FGV_SIGV_UNSUP 2  // outside the engine's model: the reference decides
+// BlockSignatureVerifier (protoutil/blockutils.go:245-290) + policy.EvaluateSignedData for every
+// block with want set; locks c->mu (the channel model, the GPU verify).  policy: a channel policy
+// path; bft: the channel runs BFT (identifier headers are then outside the model).
+int fgv_block_sig_verdicts(fgv_ctx *c, size_t n, const fgv_sig_block *in, const char *policy, int bft,
+                           uint8_t *verdict);

@@ -7,6 +7,10 @@ Fabric v2 `configtxgen` profile produces for an application channel (SURVEY s8(d
   /Channel/Application/<orgN>/{Readers,Writers,Admins}
   /Channel/Application/<orgN> value MSP      FabricMSPConfig{name, crypto_config SHA2/SHA256,
                                              fabric_node_ous enabled}
+and, with orderer orgs (the policies the deliver client verifies blocks with,
+deliverclient/verifier_assembler.go:32-56):
+  /Channel/Orderer/BlockValidation           IMPLICIT_META ANY Writers (configtxgen default)
+  /Channel/Orderer/<ordN>/Writers            SIGNATURE OR('OrdererMSP.member')
 
 Message layout: common/configtx.pb.go (Config, ConfigGroup with map<string, ...> entries),
 common/policies.pb.go (Policy, ImplicitMetaPolicy), msp/msp_config.pb.go."""
@@ -14,7 +18,7 @@ from .blocks import f_bytes, f_msg, f_str, f_varint, msp_role_principal, n_out_o
 
 SIGNATURE, IMPLICIT_META = 1, 3
 ANY, ALL, MAJORITY = 0, 1, 2
-MEMBER, ADMIN, CLIENT, PEER = 0, 1, 2, 3
+MEMBER, ADMIN, CLIENT, PEER, ORDERER = 0, 1, 2, 3, 4
 
 
 def _entry(key, value_msg):
@@ -54,8 +58,11 @@ def group(groups=(), values=(), policies=()):
     return out
 
 
-def make_config(mspids, endorsement_rule=MAJORITY, org_endorsement_role=PEER, hash_families=None):
-    """-> common.Config bytes; org group names org1..orgN (the MSP ids are separate names)"""
+def make_config(mspids, endorsement_rule=MAJORITY, org_endorsement_role=PEER, hash_families=None, orderer_mspids=(),
+                block_validation=None, orderer_writers_role=MEMBER):
+    """-> common.Config bytes; org group names org1..orgN (the MSP ids are separate names).
+    orderer_mspids: orderer orgs (group names ord1..ordN) -> an Orderer group; block_validation:
+    its BlockValidation policy bytes (ConfigPolicy), default IMPLICIT_META ANY Writers."""
     orgs = []
     for i, m in enumerate(mspids):
         fam = (hash_families or {}).get(m, "SHA2")
@@ -69,7 +76,21 @@ def make_config(mspids, endorsement_rule=MAJORITY, org_endorsement_role=PEER, ha
                                        ("Readers", implicit_meta(ANY, "Readers")),
                                        ("Writers", implicit_meta(ANY, "Writers")),
                                        ("Admins", implicit_meta(MAJORITY, "Admins"))])
-    root = group(groups=[("Application", app)], policies=[("Readers", implicit_meta(ANY, "Readers")),
+    groups = [("Application", app)]
+    if orderer_mspids:
+        ords = []
+        for i, m in enumerate(orderer_mspids):
+            fam = (hash_families or {}).get(m, "SHA2")
+            pols = [("Readers", config_policy(SIGNATURE, signature_policy(1, [(m, MEMBER)]))),
+                    ("Writers", config_policy(SIGNATURE, signature_policy(1, [(m, orderer_writers_role)]))),
+                    ("Admins", config_policy(SIGNATURE, signature_policy(1, [(m, ADMIN)])))]
+            ords.append(("ord%d" % (i + 1), group(values=[("MSP", msp_value(m, fam))], policies=pols)))
+        bv = block_validation if block_validation is not None else implicit_meta(ANY, "Writers")
+        groups.append(("Orderer", group(groups=ords, policies=[("BlockValidation", bv),
+                                                                ("Readers", implicit_meta(ANY, "Readers")),
+                                                                ("Writers", implicit_meta(ANY, "Writers")),
+                                                                ("Admins", implicit_meta(MAJORITY, "Admins"))])))
+    root = group(groups=groups, policies=[("Readers", implicit_meta(ANY, "Readers")),
                                                           ("Writers", implicit_meta(ANY, "Writers")),
                                                           ("Admins", implicit_meta(MAJORITY, "Admins"))])
     return f_varint(1, 1) + f_msg(2, root)

@@ -365,9 +365,10 @@ int fgv_mvcc_validate_block_next(fgv_ctx *ctx, const uint8_t *block, size_t len,
 int fgv_mvcc_last_stats(fgv_ctx *ctx, double *lookup_ms, double *total_ms, uint64_t *reads,
                         uint64_t *writes, uint32_t *rounds);
 
-/* ------------------------------------------------- deliver-side block integrity (a20)
- * BlockVerificationAssistant.VerifyBlock (common/deliverclient/block_verification.go:243-273)
- * without the orderer-signature policy: verifyHeader (:311-331), verifyMetadata (:303-309),
+/* ------------------------------------------------- deliver-side block integrity (a20, f3)
+ * BlockVerificationAssistant.VerifyBlock (common/deliverclient/block_verification.go:243-273):
+ * fgv_blocks_verify without, fgv_blocks_verify_signed with the orderer-signature policy.
+ * verifyHeader (:311-331), verifyMetadata (:303-309),
  * VerifyTransactionsAreWellFormed (protoutil/blockutils.go:310-350), Header.DataHash ==
  * ComputeBlockDataHash (blockutils.go:76-79).  The chain state is the last verified header
  * (number + BlockHeaderHash, blockutils.go:48-67); only a verified block advances it, as in
@@ -382,6 +383,10 @@ int fgv_mvcc_last_stats(fgv_ctx *ctx, double *lookup_ms, double *total_ms, uint6
 #define FGV_BLK_EMPTY 6        /* no transactions ("empty block")                         */
 #define FGV_BLK_TX_MALFORMED 7 /* envelope bad_tx is not well formed                      */
 #define FGV_BLK_DATA_HASH 8    /* Header.DataHash != SHA-256(concat(Data.Data))            */
+#define FGV_BLK_SIGNATURES 9   /* the orderer signatures do not satisfy the policy, or the
+                                  signatures metadata / a signature header does not unmarshal */
+#define FGV_BLK_SIG_UNSUPPORTED 10 /* signature check outside the engine's model (this block and
+                                  every later one of the call; the call returns FGV_EUNSUPPORTED) */
 typedef struct fgv_chain_state {
   uint64_t number;          /* last verified block number                     */
   uint8_t header_hash[32];  /* its BlockHeaderHash                             */
@@ -398,6 +403,19 @@ typedef struct fgv_block_check {
 } fgv_block_check;
 int fgv_blocks_verify(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                       fgv_chain_state *chain, fgv_block_check *out);
+/* VerifyBlock with sigVerifierFunc (:265-268): after the data-hash check, the block's orderer
+ * signatures -- protoutil.BlockSignatureVerifier (protoutil/blockutils.go:245-290): Metadata at
+ * metadata[SIGNATURES], per MetadataSignature the SignedData{creator of its SignatureHeader,
+ * md.Value || signature_header || BlockHeaderBytes(header), signature} -- must satisfy the
+ * channel policy `policy` (NULL: "/Channel/Orderer/BlockValidation", the policy
+ * deliverclient/verifier_assembler.go:32-56 takes) of the context's channel model
+ * (fgv_channel_config + the orderer identities registered like any other).  Signatures are
+ * verified on the GPU in one pass for the whole call.  bft != 0: the channel runs BFT; a
+ * signature that names its consenter by an identifier header is outside the model.
+ * Outside the model too: no channel config, an unregistered identity of a channel MSP, a
+ * P-384 / SHA3 orderer identity -> FGV_BLK_SIG_UNSUPPORTED from that block on, FGV_EUNSUPPORTED. */
+int fgv_blocks_verify_signed(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                             fgv_chain_state *chain, const char *policy, int bft, fgv_block_check *out);
 /* ------------------------------------------------------------------- ledger commit hash (a21)
  * kvLedger.addBlockCommitHash (core/ledger/kvledger/kv_ledger.go:806-817):
  *   out = SHA-256(varint(ntx) || flags || updateBatchBytes || prev)

@@ -1,7 +1,7 @@
 """Restated deliver-side block verification (TEST INFRASTRUCTURE ONLY -- the oracle).
 
-BlockVerificationAssistant.VerifyBlock (common/deliverclient/block_verification.go:243-273)
-without the orderer signature policy (sigVerifierFunc):
+BlockVerificationAssistant.VerifyBlock (common/deliverclient/block_verification.go:243-273),
+with the orderer signature policy (sigVerifierFunc, :265-268) when a channel model is given:
   verifyHeader   :311-331  header != nil; Number == last.Number + 1; PreviousHash ==
                            lastBlockHeaderHash when that hash is non-empty
   verifyMetadata :303-309  len(Metadata.Metadata) >= len(BlockMetadataIndex_name) == 5
@@ -10,7 +10,14 @@ without the orderer signature policy (sigVerifierFunc):
       (protoutil/commonutils.go:198-230) skips the check, else every envelope unmarshals,
       has payload and signature, and proto.Marshal(env) == raw bytes
       ComputeBlockDataHash (:76-79) = SHA-256(bytes.Join(Data, nil))
-  Header.DataHash == that hash (:258-263); then lastBlockHeader(Hash) advance (:268-270)
+  Header.DataHash == that hash (:258-263)
+  sigVerifierFunc = protoutil.BlockSignatureVerifier(bft, consenters, policy) (blockutils.go:
+      245-290) with policy = /Channel/Orderer/BlockValidation (verifier_assembler.go:32-56):
+      Metadata at metadata[SIGNATURES] -> SignedData{creator of each SignatureHeader,
+      md.Value || signature_header || BlockHeaderBytes(header), signature} ->
+      policy.EvaluateSignedData (oracle/v20.py: SignatureSetToValidIdentities + cauthdsl /
+      ImplicitMeta over the channel config); BFT identifier headers are outside the model
+  then lastBlockHeader(Hash) advance (:268-270)
   BlockHeaderHash (:48-67) = SHA-256(asn1.Marshal{Number *big.Int, PreviousHash, DataHash})
 
 proto.Marshal is restated from google.golang.org/protobuf v1.33.0 (vendored): known fields
@@ -20,8 +27,11 @@ fields' raw bytes in the order they were read (impl/encode.go appendUnknown).
 import hashlib
 
 from .protowire import DecodeError, _skip, _varint, decode
+from .v20 import Unsupported, _eval_channel_policy
 
-OK, UNPARSABLE, NO_HEADER, NUMBER, PREV_HASH, METADATA, EMPTY, TX_MALFORMED, DATA_HASH = range(9)
+OK, UNPARSABLE, NO_HEADER, NUMBER, PREV_HASH, METADATA, EMPTY, TX_MALFORMED, DATA_HASH, SIGNATURES, \
+    SIG_UNSUPPORTED = range(11)
+BLOCK_VALIDATION = "/Channel/Orderer/BlockValidation"  # common/policies/policy.go BlockValidation
 
 
 def _enc_varint(v):
@@ -111,11 +121,46 @@ def block_header_hash(number, prev, data_hash):
     return hashlib.sha256(block_header_bytes(number, prev, data_hash)).digest()
 
 
-def verify_blocks(blocks, chain=None):
-    """chain: None or dict(number=, header_hash=) (mutated).  Returns per block
-    (status, bad_tx, data_hash, header_hash)."""
+def block_signature_set(blk, bft=False):
+    """BlockSignatureVerifier up to EvaluateSignedData (blockutils.go:247-287): the SignedData
+    set [(data, identity, signature)], or None when the verifier returns an error first
+    (Metadata or a SignatureHeader does not unmarshal)."""
+    md_raw = (blk["metadata"].get("metadata") or [b""])[0] or b""
+    try:
+        md = decode("Metadata", md_raw)
+    except DecodeError:
+        return None
+    hdr = blk["header"]
+    hb = block_header_bytes(hdr.get("number", 0), hdr.get("previous_hash"), hdr.get("data_hash"))
     out = []
-    for raw in blocks:
+    for ms in md.get("signatures", []):
+        sh_raw = ms.get("signature_header") or b""
+        if bft and not sh_raw and ms.get("identifier_header"):
+            raise Unsupported("BFT identifier header (consenter lookup by id)")
+        try:
+            sh = decode("SignatureHeader", sh_raw)
+        except DecodeError:
+            return None
+        out.append(((md.get("value") or b"") + sh_raw + hb, sh.get("creator") or b"", ms.get("signature") or b""))
+    return out
+
+
+def block_signatures_ok(model, blk, policy=BLOCK_VALIDATION, bft=False):
+    """sigVerifierFunc(header, metadata) == nil; raises v20.Unsupported outside the model"""
+    pol = model.channel_policy(policy)
+    sigset = block_signature_set(blk, bft)
+    if sigset is None:
+        return False
+    return _eval_channel_policy(model, pol, sigset)
+
+
+def verify_blocks(blocks, chain=None, sig=None):
+    """chain: None or dict(number=, header_hash=) (mutated).  sig: None, or dict(model=
+    v20.ChannelModel, policy=, bft=) to check the orderer signatures.  Returns per block
+    (status, bad_tx, data_hash, header_hash); a signature check outside the model gives
+    SIG_UNSUPPORTED for that block and every later one (the reference decides them)."""
+    out = []
+    for k, raw in enumerate(blocks):
         try:
             blk = decode("Block", raw)
         except DecodeError:
@@ -148,6 +193,18 @@ def verify_blocks(blocks, chain=None):
         if (hdr.get("data_hash") or b"") != dh:
             out.append((DATA_HASH, None, dh, hh))
             continue
+        if sig is not None:
+            try:
+                ok = block_signatures_ok(sig["model"], blk, sig.get("policy") or BLOCK_VALIDATION,
+                                         sig.get("bft", False))
+            except Unsupported:
+                out.append((SIG_UNSUPPORTED, None, dh, hh))
+                for rest in blocks[k + 1:]:
+                    out.append((SIG_UNSUPPORTED, None, None, None))
+                return out
+            if not ok:
+                out.append((SIGNATURES, None, dh, hh))
+                continue
         out.append((OK, None, dh, hh))
         if chain is not None:
             chain["number"] = hdr.get("number", 0)

@@ -73,6 +73,9 @@ S = {
     "BlockHeader": {1: ("number", "uint64"), 2: ("previous_hash", "bytes"), 3: ("data_hash", "bytes")},
     "BlockData": {1: ("data", "rep bytes")},
     "BlockMetadata": {1: ("metadata", "rep bytes")},
+    "Metadata": {1: ("value", "bytes"), 2: ("signatures", "rep msg:MetadataSignature")},
+    "MetadataSignature": {1: ("signature_header", "bytes"), 2: ("signature", "bytes"),
+                          3: ("identifier_header", "bytes")},
     "Envelope": {1: ("payload", "bytes"), 2: ("signature", "bytes")},
     "Payload": {1: ("header", "msg:Header"), 2: ("data", "bytes")},
     "Header": {1: ("channel_header", "bytes"), 2: ("signature_header", "bytes")},

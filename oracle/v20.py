@@ -282,7 +282,9 @@ def _eval_spe(model, spe, sigset):
 
 def _eval_channel_policy(model, pol, sigset, depth=0):
     """ImplicitMetaPolicy.EvaluateSignedData (implicitmeta.go:69-104): every sub-policy is
-    evaluated (the reference stops early in Go map order; outcomes are pure, so the count decides)"""
+    evaluated (the reference stops early in Go map order; outcomes are pure, so the count decides).
+    Threshold 0 (no sub-policies, or a rule outside ANY/ALL/MAJORITY, :45-58): `remaining`
+    starts at 0 and each satisfied sub-policy takes it below 0, so only "none satisfied" passes."""
     if pol.kind == ChannelPolicy.REJECT:
         return False
     if pol.kind == ChannelPolicy.UNSUPPORTED or (pol.kind == ChannelPolicy.IMPLICIT_META and depth > 0):
@@ -291,7 +293,7 @@ def _eval_channel_policy(model, pol, sigset, depth=0):
         return _eval_spe(model, pol.spe, sigset)
     ok = sum(1 for sub in pol.subs
              if _eval_channel_policy(model, model.policies.get(sub, ChannelPolicy(ChannelPolicy.REJECT)), sigset, depth + 1))
-    return ok >= pol.threshold
+    return ok == 0 if pol.threshold == 0 else ok >= pol.threshold
 
 
 def evaluate_policy(model, policy_bytes, sigset):

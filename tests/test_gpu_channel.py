@@ -51,6 +51,24 @@ def test_default_v2_endorsement_policy(mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+def test_implicit_meta_unknown_rule(mode):
+    """/Channel/Application/Endorsement with an ImplicitMeta rule outside ANY/ALL/MAJORITY:
+    threshold 0, and implicitmeta.go:85-103 counts `remaining` down from 0 -- a tx passes only
+    when NO org Endorsement policy is satisfied (properly endorsed txs fail with 10)."""
+    net = blocks.Network(seed=3, orgs=3, clients=30)
+    cfg = chanconfig.make_config(net.mspids, endorsement_rule=7)
+    ccs = {"mycc": chanconfig.channel_ref("/Channel/Application/Endorsement")}
+    eng = _engine(net, ccs, cfg, mode=mode)
+    blk, labels, _ = blocks.make_block(net, 300, number=1, seed=21)
+    exp = v20.validate_block(_oracle(net, ccs, cfg), blk)
+    got = list(eng.validate_blocks([blk])[0])
+    assert got == exp
+    clean = [g for g, lab in zip(got, labels) if lab == "clean"]
+    assert clean and all(g == 10 for g in clean)
+    eng.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_peer_role_required(mode):
     """The same policy with endorsers registered as CLIENTs: every endorsement fails its org's
     OR('OrgN.peer') -> ENDORSEMENT_POLICY_FAILURE (oracle agrees)."""
