@@ -29,6 +29,7 @@ EXPORTED = [
     "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
     "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d",
     "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead", "fgv_blocks_verify_signed",
+    "fgv_validate_blocks_pipelined", "fgv_set_timing",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -121,6 +122,7 @@ def load():
         L.fgv_msp_register_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(IdentityInfo)]
         L.fgv_ledger_add_txids.argtypes = [vp, vp, vp, vp, sz]
         L.fgv_validate_blocks.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp]
+        L.fgv_validate_blocks_pipelined.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp, sz, vp, vp, vp]
         L.fgv_validate_shard.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
         L.fgv_finalize_flags.argtypes = [sz, vp, vp, vp]
         L.fgv_validate_shard_dev.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
@@ -131,6 +133,7 @@ def load():
         L.fgv_validate_shard_dev_pipelined.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp, vp, vp, vp, vp]
         L.fgv_last_ahead.argtypes = [vp]
         L.fgv_set_ahead.argtypes = [vp, ctypes.c_int]
+        L.fgv_set_timing.argtypes = [vp, ctypes.c_int]
         L.fgv_finalize_flags_dev_plan.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
@@ -193,9 +196,17 @@ class BlockStep:
     finalize_flags_dev."""
 
     def __init__(self, eng, batch, tx_lo, tx_hi, d_send, rows, ntx, world, d_recv, flags_out, plan=None,
-                 presplit=True, next_batch=None):
+                 presplit=True, next_batch=None, fused=False):
+        """fused (one GPU): fgv_validate_blocks_pipelined -- validation and finalize queued back to
+        back, one synchronisation -- instead of the shard / all-gather / finalize protocol."""
         L, h = eng._L, eng._h
         self._L = L
+        self._fused = None
+        if fused:
+            nb = next_batch or batch
+            self._fused = (h, batch.nb, batch.ptrs, batch.lens, batch.dptr, flags_out.ctypes.data_as(ctypes.c_void_p),
+                           flags_out.size, batch.ntx) + ((nb.nb, nb.ptrs, nb.lens, nb.dptr) if presplit else
+                                                         (0, None, None, None))
         self._lo = np.ascontiguousarray(tx_lo, dtype=np.uint32)
         self._hi = np.ascontiguousarray(tx_hi, dtype=np.uint32)
         self._ntx = np.ascontiguousarray(ntx, dtype=np.uint64)
@@ -225,13 +236,17 @@ class BlockStep:
         self._cr = (h,) + tuple(ctypes.byref(x) for x in self._c)
 
     def validate(self):
+        if self._fused is not None:
+            _check(self._L.fgv_validate_blocks_pipelined(*self._fused))
+            return
         if self._next is None:
             _check(self._L.fgv_validate_shard_dev(*self._val))
         else:
             _check(self._L.fgv_validate_shard_dev_pipelined(*self._val, *self._next))
 
     def finalize(self):
-        _check(self._fin_fn(*self._fin))
+        if self._fused is None:
+            _check(self._fin_fn(*self._fin))
         return self.flags
 
     def stats(self):
@@ -453,6 +468,18 @@ class Engine:
         return res[:cap], np.array(list(ntx), dtype=np.uint64)
 
 
+    def validate_blocks_pipelined(self, batch, next_batch=None):
+        """fgv_validate_blocks_pipelined over block_batch()es: validate `batch` (flags of every
+        block, concatenated) while `next_batch` is pre-split (and, both host-resident, copied)."""
+        cap = int(sum(batch.lens))
+        flags = np.zeros(cap, dtype=np.uint8)
+        nb = next_batch
+        _check(self._L.fgv_validate_blocks_pipelined(self._h, batch.nb, batch.ptrs, batch.lens, batch.dptr,
+                                                     _ptr(flags), cap, batch.ntx, nb.nb if nb else 0,
+                                                     nb.ptrs if nb else None, nb.lens if nb else None,
+                                                     nb.dptr if nb else None))
+        return flags[:int(sum(batch.ntx))].copy()
+
     def block_batch(self, blocks, d_blocks=None):
         """Pre-packed ctypes arguments for a batch validated repeatedly (bench loop)."""
         return _BlockBatch(blocks, d_blocks)
@@ -495,6 +522,10 @@ class Engine:
 
     def last_ahead(self):
         return bool(self._L.fgv_last_ahead(self._h))
+
+    def set_timing(self, on: bool):
+        """fgv_set_timing: per-kernel device times of the block committer (timestamp events)"""
+        _check(self._L.fgv_set_timing(self._h, 1 if on else 0))
 
     def set_ahead(self, mode: int):
         """fgv_set_ahead: 0 off (default), 1 after ECDSA, 2 at once, 3 after the fold"""

@@ -30,7 +30,7 @@
 #define BD_DIG_P (2 + BD_MAX_END)
 #define BD_DIG_I (3 + BD_MAX_END)
 #define BD_DIG_SLOTS (4 + BD_MAX_END)
-#define SHA_E_LANES 4u  // k_bd_sha lanes per tx for endorsement messages (grid: SHA_E_LANES + 3 rows)
+#define SHA_GPW 21u     // k_bd_sha: transactions per 64-lane wave (3 lanes each)
 // host -> device envelope table, per tx: block, envelope offset, length
 #define BD_ENV_WORDS 3
 

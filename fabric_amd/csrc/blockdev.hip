@@ -646,7 +646,8 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
 __global__ __launch_bounds__(64) void k_bd_sha_payload(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                        const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
                                                        unsigned long long *__restrict__ nblk) {
-  __builtin_amdgcn_s_setprio(1);
+  // the longest serial chains of the batch (~80 compressions for C2): first in issue order
+  __builtin_amdgcn_s_setprio(2);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t blocks = 0;
   if (t < ntx) {
@@ -667,69 +668,224 @@ __global__ __launch_bounds__(64) void k_bd_sha_payload(uint32_t ntx, const uint3
 }
 
 // ============================================================ k_bd_sha
-// Every SHA-256 message of the batch, hashed speculatively right after the parse on the
-// second stream (beside identity resolution, the job counts and the verify-job assembly):
-// all of them are spans the parse already found; only WHETHER a digest is consumed is decided
-// later (a hash is pure, so a superset of the consumed ones is hashed).  Digest slots
-// (BD_DIG_SLOTS x ntx, slot-major):
-//   0                      SHA-256(e.Payload): creator signature digest (msgvalidation.go:26-64)
+// Every other SHA-256 message of the batch, hashed speculatively right after the parse on the
+// third stream (beside identity resolution and the job counts): all of them are spans the parse
+// already found; only WHETHER a digest is consumed is decided later (a hash is pure, so a
+// superset of the consumed ones is hashed).  Digest slots (BD_DIG_SLOTS x ntx, slot-major):
+//   0                      SHA-256(e.Payload): k_bd_sha_payload (msgvalidation.go:26-64)
 //   1 + k (k < BD_MAX_END) SHA-256(prp || endorser_k) (statebased/validator_keylevel.go:246-260)
 //   BD_DIG_T               SHA-256(nonce || creator): TxID (protoutil/proputils.go:351-360)
 //   BD_DIG_P               SHA-256(chdr || shdr || ccpp): proposal hash (protoutil/txutils.go:449-466)
 //   BD_DIG_I               SHA-256(nonce || creator) of the txid index entry (txutils.go:503-534)
-// Lanes run slot-major, so the payloads -- each transaction's longest message (~80
-// compressions for C2), whose serial chain sets the stage -- are dispatched first; then
-// SHA_E_LANES lanes per transaction for its endorsements (lane j: endorsements j, j + SHA_E_LANES, ...),
-// then txid / proposal / index.  (k_bd_count may turn a pending creator into code 4
-// meanwhile; those digests go unused.)
+// A transaction's endorsement messages share the prefix prp: the SHA-256 state after its H =
+// floor(|prp| / 64) whole blocks (the midstate) is the same for all of them.  SHA_GROUP = 3 lanes
+// per transaction, 21 transactions per wave:
+//   lane 0: prp || endorser_0 in full (its state after block H-1 is the midstate), then the
+//           tails (blocks H.. from the midstate) of endorsements 3, 6, ...
+//   lane 1: nonce || creator (TxID), then the tails of endorsements 1, 4, ...
+//   lane 2: chdr || shdr || ccpp, the index txid message when needed, then the tails 2, 5, ...
+// Lanes run in lockstep, one compression per step; at step H every lane of the group copies
+// lane 0's state (cross-lane read), so a tail never starts before step H.  For C2 this is ~33
+// steps per wave in 750 waves instead of 7 lanes per tx in 1750 -- the prp prefix is hashed once
+// instead of once per endorsement, and the waves fit beside the payload hashes on the SIMDs.
+#define SHA_GROUP 3u  // lanes per transaction (SHA_GPW groups per wave, blockdev.h; lane 63 idles)
+namespace {
+// one message (or its tail) of a lane: up to three spans held as scalars (an indexed array of
+// span pointers would be placed in scratch)
+struct ShaSeg {
+  uint64_t a, b, c;    // span addresses
+  uint32_t la, lb, lc; // span lengths; message = a || b || c, L = la + lb + lc
+  uint32_t b0, nblk;   // blocks [b0, nblk) of the padded message
+  uint32_t slot;       // digest slot
+  bool mid;            // starts from the midstate (b0 = H)
+  bool ok;
+};
+DEV void seg_set(ShaSeg &g, const uint8_t *base, DSpan x, DSpan y, DSpan z, uint32_t slot) {
+  g.a = (uint64_t)(uintptr_t)(base + x.off);
+  g.b = (uint64_t)(uintptr_t)(base + y.off);
+  g.c = (uint64_t)(uintptr_t)(base + z.off);
+  g.la = x.len;
+  g.lb = y.len;
+  g.lc = z.len;
+  g.slot = slot;
+  g.ok = true;
+}
+// segment s of lane r of transaction R (ok = false: the lane's list ended)
+DEV ShaSeg lane_seg(const DevTx &R, const uint8_t *base, uint32_t r, uint32_t s, uint32_t H, bool live_t, bool live_p,
+                    bool live_i, uint32_t nE) {
+  ShaSeg g{};
+  const DSpan z{0, 0};
+  uint32_t nfull = 0;  // full messages ahead of this lane's tails
+  if (r == 0) {
+    if (nE > 0) {
+      if (s == 0) seg_set(g, base, R.prp, R.end_ser[0], z, 1);
+      nfull = 1;
+    }
+  } else if (r == 1) {
+    if (live_t) {
+      if (s == 0) seg_set(g, base, R.nonce, R.creator, z, BD_DIG_T);
+      nfull = 1;
+    }
+  } else {
+    if (live_p) {
+      if (s == nfull) seg_set(g, base, R.chdr, R.act_hdr, R.ccpp, BD_DIG_P);
+      nfull++;
+    }
+    if (live_i) {
+      if (s == nfull) seg_set(g, base, R.idx_nonce, R.idx_creator, z, BD_DIG_I);
+      nfull++;
+    }
+  }
+  if (!g.ok && s >= nfull) {  // tails: endorsements k = r + 3 j (lane 0 hashed k = 0 in full)
+    const uint32_t k = r + SHA_GROUP * (s - nfull + (r == 0 ? 1u : 0u));
+    if (k < nE) {
+      seg_set(g, base, R.prp, R.end_ser[k], z, 1 + k);
+      g.b0 = H;
+      g.mid = true;
+    }
+  }
+  if (g.ok) g.nblk = (g.la + g.lb + g.lc + 8) / 64 + 1;
+  return g;
+}
+// choose one of three values by masks (a select chain on a position would be turned into a
+// table in scratch indexed by the span number)
+DEV uint64_t pick3(bool c0, bool c1, uint64_t x0, uint64_t x1, uint64_t x2) {
+  const uint64_t m0 = 0ull - (uint64_t)c0, m1 = (0ull - (uint64_t)c1) & ~m0, m2 = ~(m0 | m1);
+  return (x0 & m0) | (x1 & m1) | (x2 & m2);
+}
+// message byte q (padding: 0x80 at L, zeros after)
+DEV uint32_t seg_byte(const ShaSeg &g, uint32_t q) {
+  const uint32_t L = g.la + g.lb + g.lc;
+  if (q >= L) return q == L ? 0x80u : 0u;
+  const bool in_a = q < g.la, in_b = q < g.la + g.lb;
+  const uint64_t p = pick3(in_a, in_b, g.a + q, g.b + (q - g.la), g.c + (q - g.la - g.lb));
+  return *reinterpret_cast<const uint8_t *>(p);
+}
+// block `blk` of g: the span holding all 64 bytes (fast: 17 raw dwords + byte shift) or not
+DEV void seg_fetch(const ShaSeg &g, uint32_t blk, uint32_t raw[17], uint32_t &sh, bool &fast) {
+  const uint32_t s = blk * 64, ab = g.la + g.lb;
+  const bool in_a = s + 64 <= g.la, in_b = s >= g.la && s + 64 <= ab;
+  fast = in_a || in_b || (s >= ab && s + 64 <= ab + g.lc);
+  const uint64_t p = pick3(in_a, in_b, g.a + s, g.b + (s - g.la), g.c + (s - ab));
+  if (fast) {
+    const __attribute__((address_space(1))) uint32_t *al =
+        reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(p & ~(uint64_t)3);
+    sh = (uint32_t)(p & 3u);
+#pragma unroll
+    for (int q = 0; q < 17; q++) raw[q] = al[q];
+  }
+}
+// big-endian message word at byte position pos: one unaligned dword load when the word lies
+// inside a span, bytes only when it straddles a span boundary or the end (0x80, then zeros)
+DEV uint32_t seg_word(const ShaSeg &g, uint32_t pos) {
+  const uint32_t L = g.la + g.lb + g.lc;
+  if (pos >= L) return pos == L ? 0x80000000u : 0u;
+  const bool in_a = pos < g.la, in_b = pos < g.la + g.lb;
+  const uint64_t p = pick3(in_a, in_b, g.a + pos, g.b + (pos - g.la), g.c + (pos - g.la - g.lb));
+  const uint32_t room = (uint32_t)pick3(in_a, in_b, g.la - pos, g.la + g.lb - pos, L - pos);
+  if (room >= 4) return __builtin_bswap32(ld_u32(reinterpret_cast<const uint8_t *>(p)));
+  uint32_t w = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) w = (w << 8) | seg_byte(g, pos + q);
+  return w;
+}
+// a block that is not inside one span (span boundaries, the padding and length)
+DEV void seg_block_slow(const ShaSeg &g, uint32_t blk, uint32_t w[16]) {
+  const uint32_t s = blk * 64;
+#pragma unroll
+  for (int k = 0; k < 16; k++) w[k] = seg_word(g, s + 4 * k);
+  if (blk == g.nblk - 1) {
+    const uint64_t bits = (uint64_t)(g.la + g.lb + g.lc) * 8;
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+  }
+}
+}  // namespace
+
 __global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__restrict__ txs,
                                                const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
-                                               unsigned long long *__restrict__ nblk) {
-  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t row = l / ntx, t = l - row * ntx;  // rows: E x SHA_E_LANES | T | P | I
-  uint64_t blocks = 0;
-  auto hash = [&](const DevTx &R, uint32_t s, DSpan a, DSpan b, DSpan c) {
-    const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
-    JobView v;
-    v.p[0] = base + a.off;
-    v.p[1] = base + b.off;
-    v.p[2] = base + c.off;
-    v.beg[0] = 0;
-    v.beg[1] = a.len;
-    v.beg[2] = a.len + b.len;
-    v.beg[3] = v.L = a.len + b.len + c.len;
-    sha_view(v, dig + ((size_t)s * ntx + t) * 32);
-    blocks += (v.L + 8) / 64 + 1;
-  };
-  if (row < SHA_E_LANES) {
+                                               unsigned long long *__restrict__ nblk_out) {
+  // ~33 compressions per lane against the payload hashes' ~80: it has slack (k_prep waits for
+  // both), so it yields to them and to the parse -> identity chain
+  __builtin_amdgcn_s_setprio(1);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t grp = lane / SHA_GROUP, r = lane - grp * SHA_GROUP;
+  const uint32_t t = blockIdx.x * SHA_GPW + grp;
+  const bool in = grp < SHA_GPW && t < ntx;
+  uint32_t H = 0, nE = 0;
+  bool live_t = false, live_p = false, live_i = false;
+  const uint8_t *base = nullptr;
+  ShaSeg g;
+  g.ok = false;
+  if (in) {
     const DevTx &R = txs[t];
-    if (R.pre == C_PENDING && R.type == 3 && R.etx == C_VALID && R.disp == C_VALID)
-      for (uint32_t k = row; k < R.nend; k += SHA_E_LANES) hash(R, 1 + k, R.prp, R.end_ser[k], DSpan{0, 0});
-  } else if (row < SHA_E_LANES + 3) {
-    const uint32_t s = row - SHA_E_LANES + BD_DIG_T;  // BD_DIG_T, BD_DIG_P, BD_DIG_I
-    const DevTx &R = txs[t];
-    const DSpan z{0, 0};
-    DSpan a = z, b = z, c = z;
+    base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
     const bool live = R.pre == C_PENDING;
-    bool want;
-    if (s == BD_DIG_T) {
-      want = live && R.type == 3;
-      a = R.nonce;
-      b = R.creator;
-    } else if (s == BD_DIG_P) {
-      want = live && R.type == 3 && R.etx == C_VALID;
-      a = R.chdr;
-      b = R.act_hdr;
-      c = R.ccpp;
-    } else {
-      want = (R.flags & BDF_INDEX_OK) && !(R.flags & BDF_INDEX_FROM_TXID);
-      a = R.idx_nonce;
-      b = R.idx_creator;
+    live_t = live && R.type == 3;
+    live_p = live_t && R.etx == C_VALID;
+    live_i = (R.flags & BDF_INDEX_OK) && !(R.flags & BDF_INDEX_FROM_TXID);
+    nE = (live_p && R.disp == C_VALID) ? R.nend : 0u;
+    H = R.prp.len / 64;
+    g = lane_seg(R, base, r, 0, H, live_t, live_p, live_i, nE);
+  }
+  uint32_t s = 0, blk = g.ok ? g.b0 : 0;
+  uint32_t h[8], mid[8];
+  const uint32_t IV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+#pragma unroll
+  for (int k = 0; k < 8; k++) h[k] = mid[k] = IV[k];
+  uint64_t blocks = 0;
+  uint32_t raw[17], sh = 0, w[16];
+  bool fast = false;
+  if (g.ok) seg_fetch(g, blk, raw, sh, fast);
+  const int src = (int)(grp * SHA_GROUP);  // lane 0 of the group
+#pragma unroll 1
+  for (uint32_t step = 0;; step++) {
+    // the midstate: lane 0's state after its first H blocks (every lane runs the reads)
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t v = (uint32_t)__shfl((int)h[k], src);
+      if (step == H) mid[k] = v;
     }
-    if (want) hash(R, s, a, b, c);
+    const bool waiting = g.ok && g.mid && step < H;
+    if (__ballot(g.ok) == 0ull) break;
+    if (g.ok && !waiting) {
+      if (blk == g.b0 && g.mid) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) h[k] = mid[k];
+      }
+      if (fast) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh));
+      } else {
+        seg_block_slow(g, blk, w);
+      }
+      // the lane's next block (or the next segment's first), fetched while this one compresses
+      ShaSeg gn = g;
+      uint32_t bn = blk + 1;
+      bool next_seg = bn >= g.nblk;
+      if (next_seg) {
+        gn = lane_seg(txs[t], base, r, s + 1, H, live_t, live_p, live_i, nE);
+        bn = gn.ok ? gn.b0 : 0;
+      }
+      if (gn.ok) seg_fetch(gn, bn, raw, sh, fast);
+      sha_compress(h, w);
+      blocks++;
+      if (next_seg) {
+        uint32_t *o = reinterpret_cast<uint32_t *>(dig + ((size_t)g.slot * ntx + t) * 32);
+#pragma unroll
+        for (int k = 0; k < 8; k++) o[k] = __builtin_bswap32(h[k]);
+        g = gn;
+        s++;
+        if (g.ok && !g.mid) {  // (a tail takes the midstate at its first block)
+#pragma unroll
+          for (int k = 0; k < 8; k++) h[k] = IV[k];
+        }
+      }
+      blk = bn;
+    }
   }
   for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
-  if ((threadIdx.x & 63) == 0 && blocks) atomicAdd(nblk, (unsigned long long)blocks);
+  if (lane == 0 && blocks) atomicAdd(nblk_out, (unsigned long long)blocks);
 }
 
 // ============================================================ k_bd_emit
@@ -741,9 +897,12 @@ __global__ __launch_bounds__(256) void k_bd_emit(uint32_t ntx, const DevTx *__re
                                                  const DevJobIdx *__restrict__ jobs,
                                                  const uint32_t *__restrict__ totals,
                                                  uint64_t *__restrict__ sig_ptr, uint32_t *__restrict__ sig_len,
-                                                 uint32_t *__restrict__ key_slot, uint32_t *__restrict__ dig_idx) {
+                                                 uint32_t *__restrict__ key_slot, uint32_t *__restrict__ dig_idx,
+                                                 uint32_t *__restrict__ nv_out) {
   __builtin_amdgcn_s_setprio(3);  // latency-critical chain; k_bd_sha fills the SIMDs beside it
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  // the verify count, read in device memory by the verify stages enqueued behind this kernel
+  if (t == 0) *nv_out = totals[BJ_C] + totals[BJ_E];
   if (t >= ntx) return;
   const DevTx &R = txs[t];
   const DevJobIdx &J = jobs[t];

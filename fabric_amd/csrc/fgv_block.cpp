@@ -194,10 +194,13 @@ struct BdSet {
   DevBuf env, tx, ident, jobs, dig;  // env: envelope table | block bases | counters (the head)
   HostBuf head, misc;                // pinned head staging / counters read back
   // 0 start, 1 payload hashes done (stream2), 2 k_bd_sha done (stream3), 3 head uploaded,
-  // 4 parse done, 5 k_bd_sha start, 6 counts read back, 7 k_bd_ident start
-  hipEvent_t ev[8] = {};
+  // 4 parse done, 5 k_bd_sha start, 6 counts done, 7 k_bd_ident start (0, 5, 7: timing only),
+  // 8 every digest done (stream3, after joining stream2: the back half waits on this one only)
+  hipEvent_t ev[9] = {};
   SplitOut so;
   bool presplit = false;
+  bool timed = false;  // its front half recorded the timing-only events
+  hipStream_t stream = nullptr;  // the stream its parse / identity / count chain ran on
   size_t eoff = 0, moff = 0;
   uint32_t N = 0;
   // the batch this set holds (the match key of a front half enqueued ahead)
@@ -237,6 +240,9 @@ struct fgv_block_state {
   BdSet set[2];
   int ahead = -1;  // set holding a front half enqueued ahead of its call (-1: none)
   int last = 1;    // set of the last call
+  int pending = -1;           // set enqueued by _enqueue and not yet finished
+  double nv_per_tx = 0;       // verifies per tx of the last batch (lanes-per-verify estimate)
+  std::chrono::steady_clock::time_point t_enq;
   explicit fgv_block_state(unsigned threads) : pool(threads) {}
   ~fgv_block_state() {
     dimg.release();
@@ -1113,7 +1119,7 @@ __global__ void k_bd_sha_payload(uint32_t ntx, const uint32_t *envtab, const uin
                                  unsigned long long *nblk);
 __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
                           const DevJobIdx *jobs, const uint32_t *totals, uint64_t *sig_ptr, uint32_t *sig_len,
-                          uint32_t *key_slot, uint32_t *dig_idx);
+                          uint32_t *key_slot, uint32_t *dig_idx, uint32_t *nv_out);
 __global__ void k_bd_fold(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
                           const DevJobIdx *jobs, const uint32_t *totals, const uint8_t *digests,
                           const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags);
@@ -1196,12 +1202,15 @@ bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t le
 
 // Front half of a batch into set B, on the side streams: envelope spans (pre-split or walked
 // here), head upload, k_bd_sha_payload (stream2), k_bd_parse -> k_bd_ident -> k_bd_count ->
-// counters read back (streamF), k_bd_sha (stream3).  `wait` (optional): an event the head
+// job counters in device memory (streamF), k_bd_sha (stream3).  `wait` (optional): an event the head
 // upload waits for (the H2D copy of host-resident blocks).  Nothing here reads the committed
 // txid table (k_bd_fold does), so ledger txids added afterwards never stale it.
+// `sf` carries the parse -> identities -> counts chain: the main stream for the call's own batch
+// (its back half then follows in order, with no cross-stream hop), c->streamF for a front half
+// enqueued ahead beside the current batch's back half.
 static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks, const uint8_t *const *h_blocks,
                         const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
-                        const uint32_t *tx_hi, hipEvent_t wait, hipEvent_t wait2 = nullptr) {
+                        const uint32_t *tx_hi, hipStream_t sf, hipEvent_t wait, hipEvent_t wait2 = nullptr) {
   B.hb.assign(h_blocks, h_blocks + nblocks);
   B.db.assign(d_blocks, d_blocks + nblocks);
   B.lens.assign(lens, lens + nblocks);
@@ -1244,10 +1253,14 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   for (size_t b = 0; b < nblocks; b++) bs[b] = (uint64_t)(uintptr_t)d_blocks[b];
   memset(head + B.moff, 0, 64);
   const DevChannel ch = S->dimg.ch;
-  hipStream_t sf = c->streamF;
+  B.stream = sf;
   if (wait) HIP_TRY(hipStreamWaitEvent(sf, wait, 0));
   if (wait2) HIP_TRY(hipStreamWaitEvent(sf, wait2, 0));
-  HIP_TRY(hipEventRecord(B.ev[0], sf));
+  // events: ev3 (head uploaded), ev4 (parsed), ev1 (payload digests), ev2 (other digests), ev6
+  // (job counts) order the streams; ev0 / ev5 / ev7 only time kernels (fgv_set_timing)
+  const bool tim = c->timing;
+  B.timed = tim;
+  if (tim) HIP_TRY(hipEventRecord(B.ev[0], sf));
   HIP_TRY(hipMemcpyAsync(B.env.p, head, hbytes, hipMemcpyHostToDevice, sf));
   HIP_TRY(hipEventRecord(B.ev[3], sf));
   // [0..5) totals, [5] flags, bytes 24..32 k_bd_sha compressions, 32..40 payload compressions
@@ -1265,17 +1278,18 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one
   HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[4], 0));
-  HIP_TRY(hipEventRecord(B.ev[5], c->stream3));
-  hipLaunchKernelGGL(k_bd_sha, dim3((uint32_t)(((uint64_t)N * (SHA_E_LANES + 3) + 63) / 64)), dim3(64), 0,
+  if (tim) HIP_TRY(hipEventRecord(B.ev[5], c->stream3));
+  hipLaunchKernelGGL(k_bd_sha, dim3((N + SHA_GPW - 1) / SHA_GPW), dim3(64), 0,
                      c->stream3, N, dtx, dbs, B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 6));
   HIP_TRY(hipEventRecord(B.ev[2], c->stream3));
-  HIP_TRY(hipEventRecord(B.ev[7], sf));
+  HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[1], 0));
+  HIP_TRY(hipEventRecord(B.ev[8], c->stream3));
+  if (tim) HIP_TRY(hipEventRecord(B.ev[7], sf));
   hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 + 255) / 256)), dim3(256), 0, sf, N, dtx, dbs, ch,
                      B.ident.as<int32_t>());
   hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
                      B.jobs.as<DevJobIdx>(), misc);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(B.misc.p, misc, 32, hipMemcpyDeviceToHost, sf));
   HIP_TRY(hipEventRecord(B.ev[6], sf));
   B.N = N;
   return FGV_OK;
@@ -1293,10 +1307,11 @@ static void drain_ahead(fgv_ctx *c, fgv_block_state *S) {
 
 void fgv_block_drain(fgv_ctx *c) { drain_ahead(c, c->blk); }
 
-int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
-                           const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
-                           const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out) {
+int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
+                                   const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                                   const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out) {
   using clk = std::chrono::steady_clock;
+  S->pending = -1;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   auto t0 = clk::now();
   fgv_ctx::NextBatch nx = c->next;  // the batch whose front half this call enqueues ahead
@@ -1320,7 +1335,7 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   } else {
     drain_ahead(c, S);
     cur = S->last ^ 1;
-    int rc = front_launch(c, S, S->set[cur], nblocks, h_blocks, lens, d_blocks, tx_lo, tx_hi, nullptr);
+    int rc = front_launch(c, S, S->set[cur], nblocks, h_blocks, lens, d_blocks, tx_lo, tx_hi, c->stream, nullptr);
     if (rc) return rc;
   }
   S->last = cur;
@@ -1334,19 +1349,16 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   if (N == 0) return FGV_OK;
   c->t_host_parse = ms_since(t0);
   auto t1 = clk::now();
-  // the next batch's framing walk, on the host worker while this batch's front half finishes
+  // the next batch's framing walk, on the host worker while this batch's GPU work runs
   if (nx.n) {
     fgv_block_presplit(S, c->device, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi);
     c->next.n = 0;
   }
-  HIP_TRY(hipEventSynchronize(B.ev[6]));
-  const uint32_t *hm = B.misc.as<uint32_t>();
-  if (hm[5] & 1u) return 1;  // capacity overflow: host parser
-  const size_t nv = (size_t)hm[BJ_C] + hm[BJ_E];
-  c->t_bd_pre = ms_since(t1);
-  c->t_host_assemble = c->t_bd_pre;
-  auto t2 = clk::now();
-  // --- back half on the main stream
+  // --- back half on the main stream, enqueued without reading the job counts back: the verify
+  // columns are sized for the batch's capacity (a creator + BD_MAX_END endorsements per tx) and
+  // k_bd_emit leaves the verify count in device memory (misc[10]) for k_der ... k_point
+  const size_t cap = (size_t)N * (1 + BD_MAX_END);
+  const size_t n_est = (size_t)((double)N * (S->nv_per_tx > 0 ? S->nv_per_tx : 3.5) + 0.5);
   hipStream_t st = c->stream;
   const DevChannel ch = S->dimg.ch;
   uint32_t *misc = reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff);
@@ -1354,76 +1366,109 @@ int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const
   DevTx *dtx = B.tx.as<DevTx>();
   int32_t *did = B.ident.as<int32_t>();
   DevJobIdx *dj = B.jobs.as<DevJobIdx>();
-  if (!c->bj_sigp.ensure(nv * 20 + 64) || !c->bj_vst.ensure(nv + 64)) return FGV_ENOMEM;
+  if (!c->bj_sigp.ensure(cap * 20 + 64) || !c->bj_vst.ensure(cap + 64)) return FGV_ENOMEM;
   uint8_t *sp = c->bj_sigp.as<uint8_t>();
-  HIP_TRY(hipStreamWaitEvent(st, B.ev[6], 0));
-  HIP_TRY(hipEventRecord(c->kev[6], st));
+  const bool tim = c->timing && B.timed;
+  if (B.stream != st) HIP_TRY(hipStreamWaitEvent(st, B.ev[6], 0));  // (a front half enqueued ahead)
+  if (tim) HIP_TRY(hipEventRecord(c->kev[6], st));
   hipLaunchKernelGGL(k_bd_emit, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
-                     reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + nv * 8),
-                     reinterpret_cast<uint32_t *>(sp + nv * 12), reinterpret_cast<uint32_t *>(sp + nv * 16));
+                     reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + cap * 8),
+                     reinterpret_cast<uint32_t *>(sp + cap * 12), reinterpret_cast<uint32_t *>(sp + cap * 16),
+                     misc + 10);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->kev[7], st));
-  c->digests_ready = B.ev[1];
-  c->digests_ready2 = B.ev[2];
-  int rc = fgv_run_block_jobs_device(c, 0, nv, 0, 0, B.dig.as<uint8_t>());
+  if (tim) HIP_TRY(hipEventRecord(c->kev[7], st));
+  c->digests_ready = B.ev[8];  // (payload and the other digests, joined on stream3)
+  c->digests_ready2 = nullptr;
+  int rc = fgv_run_block_jobs_device(c, 0, cap, 0, 0, B.dig.as<uint8_t>(), misc + 10, n_est);
   c->digests_ready = c->digests_ready2 = nullptr;
   if (rc) return rc;
-  // joined even when there is nothing to verify
-  HIP_TRY(hipStreamWaitEvent(st, B.ev[1], 0));
-  HIP_TRY(hipStreamWaitEvent(st, B.ev[2], 0));
-  HIP_TRY(hipEventRecord(c->kev[8], st));
+  // (the digests were joined before k_prep: the verify stages always run, for the capacity)
+  if (tim) HIP_TRY(hipEventRecord(c->kev[8], st));
   hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
                      B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->kev[9], st));
+  if (tim || c->ahead_mode == 3) HIP_TRY(hipEventRecord(c->kev[9], st));  // (ahead mode 3 waits on it)
   HIP_TRY(hipMemcpyAsync(B.misc.p, misc, 48, hipMemcpyDeviceToHost, st));
+  c->t_bd_pre = ms_since(t1);
+  c->t_host_assemble = c->t_bd_pre;
+  S->t_enq = clk::now();
   // --- the next batch's front half, ahead of its call, while this back half runs: its
   // device copy is known (caller-resident, or being prefetched by the copy stream)
-  // Measured on MI355X (C2, 32 x 500-tx batches): every overlap placement loses.
-  // k_point28 is VALU-issue-bound (64-bit MADs) and the front half's SHA-256 chains are VALU
-  // work too, so running them side by side stretches both; the byte-walking kernels slow each
-  // other through memory latency.  Step times: not ahead 0.91 ms; enqueued at once (2) 0.92-0.94;
-  // after this batch's ECDSA (1) 1.01; after its fold (3) 1.05.  So the default keeps one batch
-  // on the GPU at a time (the next batch's framing is still pre-split on the host meanwhile);
-  // fgv_set_ahead / FGV_AHEAD=1/2/3 selects a placement (A/B).
+  // Measured on MI355X (C2, 32 x 500-tx batches, fused single-GPU call), step
+  // times: not ahead (0) 0.81-0.82 ms; enqueued at once (2) 0.74-0.80 (within run-to-run noise of
+  // 0 once the payload hashes issue first, and every kernel then runs stretched); after this
+  // batch's ECDSA (1) 0.86-0.92; after its fold (3) 0.98-1.12 (they collide with k_point28, which
+  // is VALU-issue-bound, or with the next call's own kernels).  So the default keeps one batch on
+  // the GPU at a time, the next one pre-split on the host meanwhile; fgv_set_ahead / FGV_AHEAD
+  // select a placement (A/B).
   const int ahead_mode = c->ahead_mode;
   if (nx.n && nx.d_blocks && ahead_mode) {
     BdSet &A = S->set[cur ^ 1];
     hipEvent_t after = (ahead_mode == 1 && c->stage_ran) ? c->ev[6] : ahead_mode == 3 ? c->kev[9] : nullptr;
-    if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, nx.wait, after) == FGV_OK)
+    if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after) ==
+        FGV_OK)
       S->ahead = cur ^ 1;
     else
       drain_ahead(c, S), S->ahead = -1;  // (the next call starts it again and reports any error)
   }
-  HIP_TRY(hipStreamSynchronize(st));
+  S->pending = cur;
+  return FGV_OK;
+}
+
+// Wait for the batch enqueued by fgv_block_validate_dev_enqueue (the caller may have enqueued
+// more work on c->stream after it, e.g. the finalize kernels) and read its outcome: FGV_OK,
+// FGV_EUNSUPPORTED, or 1 = a transaction exceeded a device capacity (run the host parser).
+int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
+  using clk = std::chrono::steady_clock;
+  if (S->pending < 0) return FGV_OK;
+  BdSet &B = S->set[S->pending];
+  S->pending = -1;
+  HIP_TRY(hipStreamSynchronize(c->stream));
   fgv_read_block_job_times(c);
   {  // per-kernel device times (fgv_last_kernel_times)
     auto el = [&](hipEvent_t a, hipEvent_t b) {
       float ms = 0;
       return hipEventElapsedTime(&ms, a, b) == hipSuccess ? (double)ms : 0.0;
     };
-    c->t_kern[0] = el(B.ev[3], B.ev[1]);      // k_bd_sha_payload
-    c->t_kern[1] = el(B.ev[3], B.ev[4]);      // k_bd_parse
-    c->t_kern[2] = el(B.ev[5], B.ev[2]);      // k_bd_sha
-    c->t_kern[3] = el(B.ev[7], B.ev[6]);      // k_bd_ident + k_bd_count (+ the counters' read-back)
-    c->t_kern[4] = el(c->kev[6], c->kev[7]);  // k_bd_emit
-    c->t_kern[5] = c->stage_ran ? el(c->ev[2], c->ev[3]) : 0.0;  // k_der + k_inv
-    c->t_kern[6] = c->stage_ran ? el(c->ev[4], c->ev[5]) : 0.0;  // k_prep
-    c->t_kern[7] = c->stage_ran ? el(c->ev[5], c->ev[6]) : 0.0;  // k_point28 (+ k_point hand-overs)
-    c->t_kern[8] = el(c->kev[8], c->kev[9]);  // k_bd_fold
-    c->t_kern[9] = el(B.ev[0], c->kev[9]);    // the batch, head upload to fold
+    // always (stream-ordering events): payload, parse, k_bd_sha, identities + counts
+    c->t_kern[0] = el(B.ev[3], B.ev[1]);  // k_bd_sha_payload
+    c->t_kern[1] = el(B.ev[3], B.ev[4]);  // k_bd_parse
+    c->t_kern[2] = el(B.timed ? B.ev[5] : B.ev[4], B.ev[2]);  // k_bd_sha
+    c->t_kern[3] = el(B.timed ? B.ev[7] : B.ev[4], B.ev[6]);  // k_bd_ident + k_bd_count
+    const bool tim = c->timing && B.timed;  // with fgv_set_timing only
+    c->t_kern[4] = tim ? el(c->kev[6], c->kev[7]) : 0.0;                     // k_bd_emit
+    c->t_kern[5] = tim && c->stage_ran ? el(c->ev[2], c->ev[3]) : 0.0;  // k_der + k_inv
+    c->t_kern[6] = tim && c->stage_ran ? el(c->ev[4], c->ev[5]) : 0.0;  // k_prep
+    c->t_kern[7] = tim && c->stage_ran ? el(c->ev[5], c->ev[6]) : 0.0;  // k_point28 (+ k_point hand-overs)
+    c->t_kern[8] = tim ? el(c->kev[8], c->kev[9]) : 0.0;               // k_bd_fold
+    c->t_kern[9] = tim ? el(B.ev[0], c->kev[9]) : 0.0;                 // the batch, head upload to fold
     c->t_sha = std::max(c->t_kern[0], el(B.ev[3], B.ev[2]));
   }
+  const uint32_t *hm = B.misc.as<uint32_t>();
   uint64_t nb, np;
   memcpy(&nb, hm + 6, 8);
   memcpy(&np, hm + 8, 8);
   c->n_sha_blocks = nb + np;
   c->n_pay_blocks = np;
-  c->t_host_device = ms_since(t2);
+  c->n_verifies = hm[10];
+  if (B.N) S->nv_per_tx = (double)hm[10] / B.N;  // the next batch's lanes-per-verify estimate
+  c->t_host_device = std::chrono::duration<double, std::milli>(clk::now() - S->t_enq).count();
   c->t_host_fold = 0;
   if (hm[5] & 1u) return 1;
   if (hm[5] & 2u) return FGV_EUNSUPPORTED;
   return FGV_OK;
+}
+
+int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
+                           const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                           const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out) {
+  const int rc = fgv_block_validate_dev_enqueue(c, S, nblocks, h_blocks, lens, d_blocks, tx_lo, tx_hi, d_res,
+                                                res_cap, ntx_out);
+  if (rc) {
+    S->pending = -1;
+    return rc;
+  }
+  return fgv_block_validate_dev_finish(c, S);
 }
 
 // ======================================================================= orderer signatures
@@ -1463,6 +1508,28 @@ struct VMetadata {  // Metadata {value = 1, repeated MetadataSignature signature
     VMetaSig m;
     if (!pbw::decode(s.p, s.n, m)) return false;
     sigs.push_back(m);
+    return true;
+  }
+};
+struct VMeta0 {  // BlockMetadata: metadata[SIGNATURES]
+  bool has = false;
+  Span sigs;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_REP_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    if (!has) sigs = s, has = true;
+    return true;
+  }
+};
+struct VBlockMeta0 {  // Block: field 3 only
+  bool has = false;
+  Span sigs;
+  pbw::Kind kind(uint32_t n) { return n == 3 ? pbw::K_MSG : (n == 1 || n == 2) ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    VMeta0 m;
+    if (!pbw::decode(s.p, s.n, m)) return false;
+    if (m.has) has = true, sigs = m.sigs;
     return true;
   }
 };
@@ -1593,4 +1660,59 @@ int fgv_block_sig_verdicts(fgv_ctx *c, size_t n, const fgv_sig_block *in, const 
     verdict[b] = v == 2 ? FGV_SIGV_UNSUP : v == 1 ? FGV_SIGV_OK : FGV_SIGV_FAIL;
   }
   return FGV_OK;
+}
+
+// ======================================================================= sanitizer probe
+// The host parser alone, for the CPU sanitizer build (tools/sanitize): every envelope of a
+// block through parse_tx + count_jobs against a channel with the given identities (valid P-256,
+// key slot 0, roles unknown) and chaincode definition, the policy fold over each transaction's
+// resolved endorsers (as if every signature verified), then the block's orderer-signature
+// metadata (Metadata / SignatureHeader decode, identity lookup).  No GPU call.  Returns a digest
+// of the decided codes (the harness only needs the parse to be memory-safe).
+uint64_t fgv_block_parse_probe(const char *channel, const uint8_t *const *ids, const size_t *id_lens, size_t nids,
+                               const char *ns, const uint8_t *policy, size_t policy_len, const uint8_t *blk,
+                               size_t n) {
+  fgv_block_state S(1);
+  fgv_block_set_channel(&S, channel);
+  fgv_identity_info info{};
+  info.key_type = FGV_KEY_P256;
+  info.valid = 1;
+  info.roles = FGV_ROLES_UNKNOWN;
+  for (size_t i = 0; i < nids; i++) {
+    for (int k = 0; k < 32; k++) info.id_digest[k] = (uint8_t)(i * 31 + k);
+    fgv_block_add_identity(&S, ids[i], id_lens[i], 0, &info);
+  }
+  if (ns) fgv_block_define_chaincode(&S, ns, "vscc", policy, policy_len, 0);
+  Channel &ch = S.ch;
+  ch.compile();
+  uint64_t h = 0xcbf29ce484222325ull;
+  auto mix = [&](uint64_t v) { h = (h ^ v) * 0x100000001b3ull; };
+  VBlock b;
+  if (!pbw::decode(blk, n, b)) return 0;
+  TxRec R;
+  for (const Span &d : b.data.data) {
+    parse_tx(ch, d, R);
+    count_jobs(ch, R);
+    mix(R.pre);
+    mix(R.etx);
+    mix(R.disp);
+    mix(R.n_ej);
+    if (R.disp != C_VALID) continue;
+    pbw::SmallVec<int, 16> ids_ok;
+    for (const EndRec &e : R.ends)
+      if (e.ident >= 0 && std::find(ids_ok.begin(), ids_ok.end(), e.ident) == ids_ok.end()) ids_ok.push_back(e.ident);
+    for (int pi : R.policies)
+      if (pi >= 0) mix((uint64_t)eval_policy(ch, pi, ids_ok.data(), ids_ok.size()));
+  }
+  // the orderer-signature metadata (fgv_block_sig_verdicts' decode)
+  VBlockMeta0 m;
+  if (pbw::decode(blk, n, m) && m.has) {
+    VMetadata md;
+    if (pbw::decode(m.sigs.p, m.sigs.n, md))
+      for (const VMetaSig &ms : md.sigs) {
+        VSignatureHeader sh;
+        if (pbw::decode(ms.sig_header.p, ms.sig_header.n, sh)) mix((uint64_t)(int64_t)ch.lookup(sh.creator));
+      }
+  }
+  return h;
 }

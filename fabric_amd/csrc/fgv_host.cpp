@@ -82,6 +82,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   const unsigned dflt = share ? std::min(24u, share) : 24u;
   c->blk = fgv_block_state_new((cfg && cfg->host_threads) ? cfg->host_threads : dflt);
   if (const char *e = getenv("FGV_AHEAD")) c->ahead_mode = std::max(0, std::min(3, atoi(e)));
+  if (const char *e = getenv("FGV_TIMING")) c->timing = atoi(e) != 0;
   auto fail = [&](int e) {
     fgv_destroy(c);
     return e;
@@ -216,28 +217,33 @@ int fgv_last_timing(fgv_ctx *c, double *sha_ms, double *prep_ms, double *point_m
 
 // k_prep + k_point on device-resident SoA inputs (events ev[2..4] bracket them)
 // k_inv on stream `st` (events ev[2]/ev[3]); the caller orders it after k_der.
-static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, uint8_t *d_status, const uint32_t *d_slot,
-                      const uint32_t *d_r, const uint32_t *d_s) {
+// N: capacity (column stride); dn: device-side item count (nullptr: N items)
+static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn, uint8_t *d_status,
+                      const uint32_t *d_slot, const uint32_t *d_r, const uint32_t *d_s) {
   uint32_t nl = (N + PREP_B - 1) / PREP_B;
   nl = (nl + INV_THREADS - 1) / INV_THREADS * INV_THREADS;
   if (!c->wscr.ensure((size_t)PREP_B * 8 * nl * 4) || !c->wv.ensure((size_t)N * 32)) return FGV_ENOMEM;
-  HIP_TRY(hipEventRecord(c->ev[2], st));
-  hipLaunchKernelGGL(k_inv, dim3(nl / INV_THREADS), dim3(INV_THREADS), 0, st, N, d_status, d_slot,
+  const bool tim = c->timing || !dn;  // (host-count callers always time their stages)
+  if (tim) HIP_TRY(hipEventRecord(c->ev[2], st));
+  hipLaunchKernelGGL(k_inv, dim3(nl / INV_THREADS), dim3(INV_THREADS), 0, st, N, dn, d_status, d_slot,
                      c->key_ok.as<uint8_t>(), d_r, d_s, c->wv.as<uint32_t>(), c->wscr.as<uint32_t>());
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[3], st));
+  if (tim) HIP_TRY(hipEventRecord(c->ev[3], st));
   return FGV_OK;
 }
 
-// k_prep + k_point on the main stream, after k_inv (ev[3]) and the digests.
-static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const uint32_t *d_slot,
-                             const uint32_t *d_r, const uint8_t *d_dig, const uint32_t *d_dig_idx) {
+// k_prep + k_point on the main stream, after k_inv (ev[3]) and the digests.  N: capacity;
+// dn: device-side item count (nullptr: N), n_est: the host's estimate of it (lanes per verify)
+static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_t n_est, uint8_t *d_status,
+                             const uint32_t *d_slot, const uint32_t *d_r, const uint8_t *d_dig,
+                             const uint32_t *d_dig_idx) {
   if (!c->d1.ensure((size_t)DIG_STRIDE * N)) return FGV_ENOMEM;
-  HIP_TRY(hipStreamWaitEvent(c->stream, c->ev[3], 0));
+  const bool tim = c->timing || !dn;
+  if (tim) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev[3], 0));  // (k_inv may run on stream2)
   // the digests' producers, waited on directly (a chained cross-stream event adds ~30 us)
   if (c->digests_ready) HIP_TRY(hipStreamWaitEvent(c->stream, c->digests_ready, 0));
   if (c->digests_ready2) HIP_TRY(hipStreamWaitEvent(c->stream, c->digests_ready2, 0));
-  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+  if (tim) HIP_TRY(hipEventRecord(c->ev[4], c->stream));
   // k_point28 (radix-2^28, incomplete formulas) decides every item except those that hit an
   // exceptional addition; k_point (complete formulas) then finishes those, and returns at
   // once when k_point28 counted none.  FGV_POINT_EXACT=1 runs k_point alone (A/B knob).
@@ -246,10 +252,10 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
     return e && atoi(e) == 1;
   }();
   uint32_t *redo = exact_only ? nullptr : c->redo.as<uint32_t>();
-  hipLaunchKernelGGL(k_prep, dim3((N + 255) / 256), dim3(256), 0, c->stream, N, d_status, d_r,
+  hipLaunchKernelGGL(k_prep, dim3((N + 255) / 256), dim3(256), 0, c->stream, N, dn, d_status, d_r,
                      c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>(), redo);  // (k_prep zeroes *redo)
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+  if (tim) HIP_TRY(hipEventRecord(c->ev[5], c->stream));
   // Grid: two POINT_THREADS workgroups per CU (2 waves per SIMD) taking chunks of items from a
   // device counter (k_point*: waves placed late, beside a next batch's front half, take fewer).
   // Lanes per verify L (1, 2, 4, 8):
@@ -266,7 +272,7 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
   uint32_t L = 1;
   double best = 1e30;
   for (uint32_t l = 1, lg = 0; l <= POINT_LANES_MAX; l <<= 1, lg++) {
-    const uint64_t waves = ((uint64_t)N * l + 63) / 64;
+    const uint64_t waves = ((uint64_t)(dn ? n_est : N) * l + 63) / 64;
     const uint64_t passes = (waves + slots - 1) / slots;  // the persistent grid's passes
     const uint64_t per_simd = std::max<uint64_t>(std::max<uint64_t>((waves + simds - 1) / simds, passes), 2);
     const double cost = (double)per_simd * ((double)((NTERMS + l - 1) / l) + 1.5 * lg);
@@ -275,29 +281,30 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, uint8_t *d_status, const ui
   if (forced >= 1 && forced <= POINT_LANES_MAX) L = (uint32_t)forced;
 
   if (redo) {
-    hipLaunchKernelGGL(k_point28, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, L, d_status, d_slot,
+    hipLaunchKernelGGL(k_point28, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, dn, L, d_status, d_slot,
                        c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   }
-  hipLaunchKernelGGL(k_point, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, L, d_status, d_slot,
+  hipLaunchKernelGGL(k_point, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, dn, L, d_status, d_slot,
                      c->gtab.as<apoint_raw>(), c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   c->last_lanes = L;
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[6], c->stream));
+  if (tim || c->ahead_mode == 1) HIP_TRY(hipEventRecord(c->ev[6], c->stream));  // (ahead mode 1 waits on it)
   return FGV_OK;
 }
 
 static int launch_verify_stages(fgv_ctx *c, uint32_t N, uint8_t *d_status, const uint32_t *d_slot,
                                 const uint32_t *d_r, const uint32_t *d_s, const uint8_t *d_dig,
                                 const uint32_t *d_dig_idx = nullptr) {
-  int rc = launch_inv(c, c->stream, N, d_status, d_slot, d_r, d_s);
+  c->timing_ran = true;
+  int rc = launch_inv(c, c->stream, N, nullptr, d_status, d_slot, d_r, d_s);
   if (rc) return rc;
-  return launch_prep_point(c, N, d_status, d_slot, d_r, d_dig, d_dig_idx);
+  return launch_prep_point(c, N, nullptr, N, d_status, d_slot, d_r, d_dig, d_dig_idx);
 }
 
 static void read_stage_times(fgv_ctx *c, bool ran) {
   float ms = 0;
   c->t_prep = c->t_point = 0;
-  if (!ran) return;
+  if (!ran || !c->timing_ran) return;
   if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->t_prep = ms;
   if (hipEventElapsedTime(&ms, c->ev[4], c->ev[5]) == hipSuccess) c->t_prep += ms;
   if (hipEventElapsedTime(&ms, c->ev[5], c->ev[6]) == hipSuccess) c->t_point = ms;
@@ -640,7 +647,7 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *c, const uint8_t *d_msg_buf, const uint64_
   int rc = launch_sha(c, d_msg_buf, d_msg_off, d_msg_len, n);
   if (rc) return rc;
   hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, d_sig_buf, d_sig_off,
-                     d_sig_len, N, d_status, c->r.as<uint32_t>(), c->s.as<uint32_t>());
+                     d_sig_len, N, (const uint32_t *)nullptr, d_status, c->r.as<uint32_t>(), c->s.as<uint32_t>());
   HIP_TRY(hipGetLastError());
   rc = launch_verify_stages(c, N, d_status, d_key_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>(),
                             c->dig.as<uint8_t>());
@@ -697,11 +704,14 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
     // DER decode first (short), then fork: s^-1 on stream2 while the SHA-256 jobs run on the
     // main stream (launched together, the SHA workgroups would occupy the CUs first)
     hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr, d_sigp,
-                       d_sigl, N, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(), c->s.as<uint32_t>());
+                       d_sigl, N, (const uint32_t *)nullptr, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(),
+                       c->s.as<uint32_t>());
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[7], c->stream));
     HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev[7], 0));
-    int rc = launch_inv(c, c->stream2, N, c->bj_vst.as<uint8_t>(), d_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>());
+    c->timing_ran = true;
+    int rc = launch_inv(c, c->stream2, N, nullptr, c->bj_vst.as<uint8_t>(), d_slot, c->r.as<uint32_t>(),
+                        c->s.as<uint32_t>());
     if (rc) return rc;
   }
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
@@ -712,9 +722,9 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
   if (nv) {
     const uint32_t N = (uint32_t)nv;
     const uint8_t *dsig = c->bj_sigp.as<uint8_t>();
-    int rc = launch_prep_point(c, N, c->bj_vst.as<uint8_t>(), reinterpret_cast<const uint32_t *>(dsig + nv * 12),
-                               c->r.as<uint32_t>(), c->bj_dig.as<uint8_t>(),
-                               reinterpret_cast<const uint32_t *>(dsig + nv * 16));
+    int rc = launch_prep_point(c, N, nullptr, N, c->bj_vst.as<uint8_t>(),
+                               reinterpret_cast<const uint32_t *>(dsig + nv * 12), c->r.as<uint32_t>(),
+                               c->bj_dig.as<uint8_t>(), reinterpret_cast<const uint32_t *>(dsig + nv * 16));
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->hb_vst.p, c->bj_vst.p, nv, hipMemcpyDeviceToHost, c->stream));
     ran = true;
@@ -728,14 +738,17 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
 }
 
 // Device-resident variant (blockdev path): the jobs were written by k_bd_emit straight into
-// c->bj_jobs / c->bj_sigp (layout of fgv_block_jobs_reserve); digests stay in c->bj_dig and
-// verify status in c->bj_vst.  Enqueued on c->stream; no host copies, no synchronisation.
+// c->bj_jobs / c->bj_sigp (layout of fgv_block_jobs_reserve, columns of stride nv); digests stay
+// in c->bj_dig and verify status in c->bj_vst.  Enqueued on c->stream; no host copies, no
+// synchronisation.  dn: the verify count in device memory (nv is then the capacity, n_est the
+// host's estimate of the count), so the stages need no host round trip after the job counts.
 int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, size_t dig_off,
-                              const uint8_t *dig) {
+                              const uint8_t *dig, const uint32_t *dn, size_t n_est) {
   const uint8_t *digs = dig ? dig : c->bj_dig.as<uint8_t>();
   c->n_sha_jobs = nj;
-  c->n_verifies = nv;
+  c->n_verifies = dn ? n_est : nv;
   c->n_sha_blocks = sha_blocks;
+  c->timing_ran = c->timing || !dn;
   if (nj == 0 && nv == 0) return FGV_OK;
   bool ran = false;
   if (nv) {
@@ -746,7 +759,7 @@ int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blo
     const uint32_t *d_sigl = reinterpret_cast<const uint32_t *>(dsig + nv * 8);
     const uint32_t *d_slot = reinterpret_cast<const uint32_t *>(dsig + nv * 12);
     hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr, d_sigp,
-                       d_sigl, N, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(), c->s.as<uint32_t>());
+                       d_sigl, N, dn, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(), c->s.as<uint32_t>());
     HIP_TRY(hipGetLastError());
     // k_inv beside the SHA-256 jobs when this call hashes (second stream); the device-parse
     // committer's hashes already run on the second stream (k_bd_sha), so k_inv follows k_der
@@ -756,21 +769,21 @@ int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blo
       HIP_TRY(hipEventRecord(c->ev[7], c->stream));
       HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev[7], 0));
     }
-    int rc = launch_inv(c, ist, N, c->bj_vst.as<uint8_t>(), d_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>());
+    int rc = launch_inv(c, ist, N, dn, c->bj_vst.as<uint8_t>(), d_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>());
     if (rc) return rc;
   }
-  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   if (nj) {  // (the device-parse committer hashes with k_bd_sha instead: nj == 0)
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     hipLaunchKernelGGL(k_sha256_jobs, dim3((uint32_t)((nj + 255) / 256)), dim3(256), 0, c->stream,
                        c->bj_jobs.as<ShaJob>(), (uint32_t)nj, c->bj_dig.as<uint8_t>() + dig_off);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   }
-  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   if (nv) {
     const uint32_t N = (uint32_t)nv;
     const uint8_t *dsig = c->bj_sigp.as<uint8_t>();
-    int rc = launch_prep_point(c, N, c->bj_vst.as<uint8_t>(), reinterpret_cast<const uint32_t *>(dsig + nv * 12),
-                               c->r.as<uint32_t>(), digs,
+    int rc = launch_prep_point(c, N, dn, (uint32_t)std::min(n_est, nv), c->bj_vst.as<uint8_t>(),
+                               reinterpret_cast<const uint32_t *>(dsig + nv * 12), c->r.as<uint32_t>(), digs,
                                reinterpret_cast<const uint32_t *>(dsig + nv * 16));
     if (rc) return rc;
     ran = true;
@@ -862,9 +875,11 @@ int fgv_ledger_add_txids(fgv_ctx *c, const uint8_t *buf, const uint64_t *off, co
 // set the device.
 // rank_lo / rank_hi (W x nb, FGV_SHARD_SKIP = no rows) or null for the per-block split
 // [floor(n r / W), floor(n (r+1) / W)).  The ranks' ranges must tile every block.
+// defer: leave the flags' D2H copy (into c->hb_fflags) queued -- the caller synchronises and
+// copies them out (fgv_validate_blocks: one synchronisation for validation + finalize).
 static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t W, size_t rows,
                              const uint8_t *d_recs, uint8_t *flags, const uint32_t *rank_lo = nullptr,
-                             const uint32_t *rank_hi = nullptr) {
+                             const uint32_t *rank_hi = nullptr, bool defer = false) {
   if (W == 0 || ((uintptr_t)d_recs & 3) || (!rank_lo) != (!rank_hi)) return FGV_EINVAL;
   uint64_t P = 0;
   for (size_t b = 0; b < nblocks; b++) P += ntx[b];
@@ -929,6 +944,7 @@ static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint
                      c->fz_flags.as<uint8_t>());
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->hb_fflags.p, c->fz_flags.p, P, hipMemcpyDeviceToHost, st));
+  if (defer) return FGV_OK;
   HIP_TRY(hipStreamSynchronize(st));
   memcpy(flags, c->hb_fflags.p, P);
   return FGV_OK;
@@ -1120,6 +1136,13 @@ int fgv_validate_shard_dev_next(fgv_ctx *c, size_t nblocks, const uint8_t *const
 
 int fgv_last_ahead(fgv_ctx *c) { return c && c->last_ahead ? 1 : 0; }
 
+int fgv_set_timing(fgv_ctx *c, int on) {
+  if (!c) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->timing = on != 0;
+  return FGV_OK;
+}
+
 int fgv_set_ahead(fgv_ctx *c, int mode) {
   if (!c || mode < 0 || mode > 3) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1187,10 +1210,45 @@ int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *r
   return fgv_finalize_impl(nblocks, ntx, results, flags);
 }
 
-int fgv_validate_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
-                        const uint8_t *const *d_blocks, uint8_t *flags, size_t flags_cap, size_t *ntx) {
-  if (!c || (nblocks && (!blocks || !lens || !flags || !ntx))) return FGV_EINVAL;
-  if (nblocks == 0) return FGV_OK;
+// TxValidator.Validate of a batch on one GPU: the device-parse pass and the finalize kernels
+// (markTXIdDuplicates + the batch's txid index) are queued back to back and the call waits once.
+static int validate_blocks_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                  const uint8_t *const *d_blocks, uint8_t *flags, size_t flags_cap, size_t *ntx) {
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  std::vector<const uint8_t *> dev;
+  int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
+  if (rc) return rc;
+  if (c->next.n && c->next.prefetch) {
+    rc = prefetch_blocks(c, c->next.n, c->next.blocks, c->next.lens);
+    if (rc) return rc;
+    c->next.d_blocks = c->pf.dev.data();
+    c->next.wait = c->pf.ev;
+  }
+  if (fgv_block_parse_mode(c->blk) == 0) {
+    // records: at most one per 2 bytes of block data (an envelope's framing), and flags_cap
+    size_t bytes = 0;
+    for (size_t b = 0; b < nblocks; b++) bytes += lens[b];
+    const size_t bound = std::min(flags_cap, bytes / 2 + nblocks);
+    if (!c->fz_res.ensure(bound * sizeof(fgv_tx_result) + 64)) return FGV_ENOMEM;
+    rc = fgv_block_validate_dev_enqueue(c, c->blk, nblocks, blocks, lens, dev.data(), nullptr, nullptr,
+                                        c->fz_res.as<fgv_tx_result>(), bound, ntx);
+    if (rc) {
+      fgv_block_validate_dev_finish(c, c->blk);  // (waits for anything already queued)
+      return rc;
+    }
+    size_t total = 0;
+    for (size_t b = 0; b < nblocks; b++) total += ntx[b];
+    if (total) rc = finalize_dev_core(c, nblocks, ntx, 1, total, c->fz_res.as<uint8_t>(), flags, nullptr, nullptr, true);
+    const int rv = fgv_block_validate_dev_finish(c, c->blk);
+    if (rc) return rc;
+    if (rv == FGV_OK) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (total) memcpy(flags, c->hb_fflags.p, total);
+      return FGV_OK;
+    }
+    if (rv != 1) return rv;
+    // a transaction exceeded a device capacity: the host parser redoes the batch
+  }
   size_t total = 0;
   for (size_t b = 0; b < nblocks; b++) {
     long k = fgv_block_count_txs(blocks[b], lens[b]);
@@ -1198,28 +1256,40 @@ int fgv_validate_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks
     total += (size_t)k;
   }
   if (total > flags_cap) return FGV_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
-  std::vector<const uint8_t *> dev;
-  int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
-  if (rc) return rc;
   if (total == 0) {
     for (size_t b = 0; b < nblocks; b++) ntx[b] = 0;
     return FGV_OK;
   }
   if (!c->hb_res.ensure(total * sizeof(fgv_tx_result) + 64) || !c->fz_res.ensure(total * sizeof(fgv_tx_result)))
     return FGV_ENOMEM;
-  if (fgv_block_parse_mode(c->blk) == 0) {
-    rc = fgv_block_validate_dev(c, c->blk, nblocks, blocks, lens, dev.data(), nullptr, nullptr,
-                                c->fz_res.as<fgv_tx_result>(), total, ntx);
-    if (rc == 0) return finalize_dev_core(c, nblocks, ntx, 1, total, c->fz_res.as<uint8_t>(), flags);
-    if (rc != 1) return rc;
-  }
   fgv_tx_result *res = c->hb_res.as<fgv_tx_result>();
   rc = fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), nullptr, nullptr, res, total, ntx);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(c->fz_res.p, res, total * sizeof(fgv_tx_result), hipMemcpyHostToDevice, c->stream));
   return finalize_dev_core(c, nblocks, ntx, 1, total, c->fz_res.as<uint8_t>(), flags);
+}
+
+int fgv_validate_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                        const uint8_t *const *d_blocks, uint8_t *flags, size_t flags_cap, size_t *ntx) {
+  return fgv_validate_blocks_pipelined(c, nblocks, blocks, lens, d_blocks, flags, flags_cap, ntx, 0, nullptr,
+                                       nullptr, nullptr);
+}
+
+int fgv_validate_blocks_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                  const uint8_t *const *d_blocks, uint8_t *flags, size_t flags_cap, size_t *ntx,
+                                  size_t next_nblocks, const uint8_t *const *next_blocks, const size_t *next_lens,
+                                  const uint8_t *const *next_d_blocks) {
+  if (!c || (nblocks && (!blocks || !lens || !flags || !ntx)) || (next_nblocks && (!next_blocks || !next_lens)))
+    return FGV_EINVAL;
+  if (nblocks == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks,   next_lens, nullptr, nullptr,
+                               !next_d_blocks && !d_blocks, next_d_blocks, nullptr};
+  int rc = validate_blocks_locked(c, nblocks, blocks, lens, d_blocks, flags, flags_cap, ntx);
+  if (c->next.n)  // not started inside (host-parse path, empty batch, early error): start it now
+    fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, nullptr, nullptr);
+  c->next = fgv_ctx::NextBatch{};
+  return rc;
 }
 
 }  // extern "C"

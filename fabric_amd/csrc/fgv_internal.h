@@ -146,7 +146,11 @@ struct fgv_ctx {
     hipEvent_t wait = nullptr;                 // ... once this event (the prefetch copy) has fired
   } next;
   bool last_ahead = false;  // the last device-parse call found its front half enqueued ahead
-  int ahead_mode = 0;       // fgv_set_ahead: 0 off, 1 after the ECDSA kernels, 2 at once, 3 after the fold
+  int ahead_mode = 0;       // fgv_set_ahead: 0 off (default), 1 after the ECDSA kernels, 2 at once, 3 after the fold
+  // fgv_set_timing: record the committer's timing-only events (per-kernel device times); each
+  // is a timestamp packet on the critical path (~5 us on MI355X), so off by default
+  bool timing = false;
+  bool timing_ran = true;  // the last verify stages recorded their events (read_stage_times)
   // host-resident batches: two device staging arenas; fgv_validate_shard_dev_next copies the
   // NEXT batch into the idle one on the copy stream while this batch's kernels run
   DevBuf stage[2];
@@ -210,8 +214,9 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
                        const uint8_t **vstatus);
 // device-resident variant: jobs already in c->bj_jobs / c->bj_sigp; results stay in HBM
 // dig: the digest buffer (default c->bj_dig)
+// dn: the verify count in device memory (nv = capacity, n_est = the host's estimate)
 int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, size_t dig_off = 0,
-                              const uint8_t *dig = nullptr);
+                              const uint8_t *dig = nullptr, const uint32_t *dn = nullptr, size_t n_est = 0);
 // wait for (and forget) a device-parse front half enqueued ahead of its call
 void fgv_block_drain(fgv_ctx *c);
 void fgv_read_block_job_times(fgv_ctx *c);
@@ -225,6 +230,13 @@ int fgv_block_parse_mode(fgv_block_state *S);
 int fgv_block_validate_dev(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
                            const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                            const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out);
+// the same in two halves: _enqueue queues the whole batch (no host synchronisation) and returns
+// FGV_OK or an error; more work may then be queued on c->stream behind it (the finalize
+// kernels); _finish synchronises and returns fgv_block_validate_dev's outcome
+int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
+                                   const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                                   const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out);
+int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S);
 
 // identity.Verify(msg, sig) of registered identities (pinned key slots), host buffers; the
 // caller holds c->mu (fgv_host.cpp)
@@ -251,3 +263,9 @@ struct fgv_sig_block {
 // path; bft: the channel runs BFT (identifier headers are then outside the model).
 int fgv_block_sig_verdicts(fgv_ctx *c, size_t n, const fgv_sig_block *in, const char *policy, int bft,
                            uint8_t *verdict);
+
+// Sanitizer probes (tools/sanitize/harness.cpp): the host parsers alone, no GPU call
+uint64_t fgv_block_parse_probe(const char *channel, const uint8_t *const *ids, const size_t *id_lens, size_t nids,
+                               const char *ns, const uint8_t *policy, size_t policy_len, const uint8_t *blk,
+                               size_t n);
+uint64_t fgv_mvcc_parse_probe(const uint8_t *rws, size_t n);

@@ -46,13 +46,13 @@ struct jpoint_raw {  // key-table build scratch: Jacobian point + prefix product
 __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw *tables, apoint_raw *tables28,
                          jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys);
 __global__ void k_gtab(apoint_raw *tables, apoint_raw *tables28, jpoint_raw *scratch);
-__global__ void k_inv(uint32_t n, uint8_t *status, const uint32_t *key_slot, const uint8_t *key_ok,
+__global__ void k_inv(uint32_t n, const uint32_t *dn, uint8_t *status, const uint32_t *key_slot, const uint8_t *key_ok,
                       const uint32_t *r_limbs, const uint32_t *s_limbs, uint32_t *w_out, uint32_t *w_scratch);
-__global__ void k_prep(uint32_t n, const uint8_t *status, const uint32_t *r_limbs, const uint32_t *w_in,
+__global__ void k_prep(uint32_t n, const uint32_t *dn, const uint8_t *status, const uint32_t *r_limbs, const uint32_t *w_in,
                        const uint8_t *digests, const uint32_t *dig_idx, int8_t *digits, uint32_t *redo);
-__global__ void k_point(uint32_t n, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot, const apoint_raw *gtab,
+__global__ void k_point(uint32_t n, const uint32_t *dn, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot, const apoint_raw *gtab,
                         const apoint_raw *ktab, const int8_t *digits, const uint32_t *r_limbs, uint32_t *redo);
-__global__ void k_point28(uint32_t n, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot,
+__global__ void k_point28(uint32_t n, const uint32_t *dn, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot,
                           const apoint_raw *gtab28, const apoint_raw *ktab28, const int8_t *digits,
                           const uint32_t *r_limbs, uint32_t *redo);
 #define INV_THREADS 128
@@ -64,8 +64,11 @@ struct ShaJob {  // message = span0 || span1 || span2 (absolute device addresses
 __global__ void k_sha256_jobs(const ShaJob *jobs, uint32_t n, uint8_t *out);
 __global__ void k_sha256(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint32_t n,
                          uint8_t *out);
+// Verify stages: n is the batch capacity (the column stride of r / s / w); dn (optional) points
+// to the item count in device memory, written by an earlier kernel on the stream (the block
+// committer's job counts), so the stages are enqueued without the host knowing it.
 __global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_t *len, uint32_t n,
-                      uint8_t *status, uint32_t *r_limbs, uint32_t *s_limbs);
+                      const uint32_t *dn, uint8_t *status, uint32_t *r_limbs, uint32_t *s_limbs);
 
 // ---- MVCC (mvcc.hip)
 #define MV_NIL 16       // NIL_TXACTION

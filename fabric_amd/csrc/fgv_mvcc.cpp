@@ -567,6 +567,31 @@ int rq_validate(const HRQ &q, const std::vector<KV> &res) {
 
 }  // namespace
 
+// Sanitizer probe (tools/sanitize): the phantom path's host decode of one TxReadWriteSet --
+// namespaces, KV and hashed rwsets, range queries with their raw reads or merkle summaries --
+// and both range-query validators over an empty and a one-result iterator.  No GPU call.
+uint64_t fgv_mvcc_parse_probe(const uint8_t *rws, size_t n) {
+  HTxRW rw;
+  if (!pbw::decode(rws, n, rw)) return 0;
+  uint64_t h = 1;
+  for (HNs &ns : rw.ns) {
+    HRW kv;
+    kv.hashed = false;
+    if (!pbw::decode(ns.rwset.p, ns.rwset.n, kv)) continue;
+    h = h * 31 + kv.reads.size() + 7 * kv.writes.size() + 13 * kv.rqs.size();
+    for (const HRQ &q : kv.rqs) {
+      const std::vector<KV> none, one{KV{"k", Ver{1, 1}}};
+      h = h * 31 + (uint64_t)(rq_validate(q, none) + 2) + 5 * (uint64_t)(rq_validate(q, one) + 2);
+    }
+    for (const HColl &cl : ns.colls) {
+      HRW hr;
+      hr.hashed = true;
+      if (pbw::decode(cl.hashed.p, cl.hashed.n, hr)) h = h * 31 + hr.reads.size() + 7 * hr.writes.size();
+    }
+  }
+  return h;
+}
+
 static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, uint64_t block_num,
                          const uint8_t *in_flags, uint8_t *flags, size_t ntx, int commit) {
   hipStream_t s = c->stream;

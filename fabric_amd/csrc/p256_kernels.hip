@@ -268,7 +268,8 @@ __global__ __launch_bounds__(64) void k_gtab(apoint_raw *__restrict__ tables, ap
 __constant__ static const uint32_t R3N[8] = {0x0b65a624u, 0xac8ebec9u, 0x0c0555c9u, 0x111f28aeu,
                                               0x6ba5e93fu, 0x2543b924u, 0x6407be65u, 0x503a54e7u};
 
-__global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, uint8_t *__restrict__ status,
+__global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, const uint32_t *__restrict__ dn,
+                                                     uint8_t *__restrict__ status,
                                                      const uint32_t *__restrict__ key_slot,
                                                      const uint8_t *__restrict__ key_ok,
                                                      const uint32_t *__restrict__ r_limbs,
@@ -278,7 +279,12 @@ __global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, uint8_t *__rest
   // latency-critical: it runs beside the SHA-256 jobs (second stream); win VALU arbitration
   __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nl = gridDim.x * blockDim.x;
+  // lanes in use: the grid, or -- for a device-side count -- just enough lanes for PREP_B items
+  // each (the grid is sized for the capacity; the rest exit), so the batch inversion amortises
+  const uint32_t cnt = dn ? min(n, *dn) : n;
+  const uint32_t nl = dn ? ((cnt + PREP_B - 1) / PREP_B + INV_THREADS - 1) / INV_THREADS * INV_THREADS
+                         : gridDim.x * blockDim.x;
+  if (lane >= nl) return;
   uint32_t one[8], r2n[8], acc[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -293,7 +299,7 @@ __global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, uint8_t *__rest
     const uint32_t i = lane + (uint32_t)b * nl;
     uint32_t sm[8];
     bool use = false;
-    if (i < n && status[i] == ST_PENDING) {
+    if (i < cnt && status[i] == ST_PENDING) {
       uint32_t r[8], s[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) {
@@ -349,7 +355,8 @@ __global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, uint8_t *__rest
 // in:  status, r limbs, w = s^-1 (Montgomery) from k_inv, digests [*][32] big-endian, item i
 //      using digest dig_idx[i] (or i when dig_idx is null).
 // out: digits [n][DIG_STRIDE]: u1 digits (int16 x NGWIN) at 0, u2 digits (int16 x NWIN) at DIG_Q_OFF.
-__global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restrict__ status,
+__global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint32_t *__restrict__ dn,
+                                              const uint8_t *__restrict__ status,
                                               const uint32_t *__restrict__ r_limbs,
                                               const uint32_t *__restrict__ w_in,
                                               const uint8_t *__restrict__ digests,
@@ -362,7 +369,7 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint8_t *__restr
     redo[1] = 0u;
     redo[2] = 0u;
   }
-  if (i >= n || status[i] != ST_PENDING) return;
+  if (i >= (dn ? min(n, *dn) : n) || status[i] != ST_PENDING) return;
   uint32_t w[8], r[8], e[8], u1[8], u2[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
@@ -440,7 +447,7 @@ FGV_DEV bool next_chunk(uint32_t *counter, uint32_t &chunk, uint32_t waves, uint
 }
 
 __global__ __launch_bounds__(POINT_THREADS, 2) void k_point(
-    uint32_t n, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
+    uint32_t n, const uint32_t *__restrict__ dn, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
     const apoint_raw *__restrict__ gtab, const apoint_raw *__restrict__ ktab,
     const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo) {
   // after k_point28: only the items it left pending (exceptional additions) remain
@@ -456,9 +463,10 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point(
   uint32_t chunk = blockIdx.x * (blockDim.x >> 6) + wave - waves;
   // every lane of a group runs the same iterations (item-uniform control flow), so the
   // cross-lane reads below always find their partners active
-  while (next_chunk(ctr, chunk, waves, gpw, n)) {
+  const uint32_t cnt = dn ? min(n, *dn) : n;  // items (n: the column stride of r_limbs)
+  while (next_chunk(ctr, chunk, waves, gpw, cnt)) {
     const uint32_t i = chunk * gpw + g;
-    if (i >= n || status[i] != ST_PENDING) continue;
+    if (i >= cnt || status[i] != ST_PENDING) continue;
     const apoint_raw *qt = ktab + (size_t)key_slot[i] * KT_ENTRIES;
     const int8_t *dg = digits + (size_t)i * DIG_STRIDE;
     jpoint acc;
@@ -613,7 +621,7 @@ FGV_DEV void f28_to_mont(f28 &r, const uint32_t w[8]) {
 }
 
 __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
-    uint32_t n, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
+    uint32_t n, const uint32_t *__restrict__ dn, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
     const apoint_raw *__restrict__ gtab28, const apoint_raw *__restrict__ ktab28,
     const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo) {
   __builtin_amdgcn_s_setprio(3);  // the verify chain; a next batch's front half may run beside it
@@ -624,9 +632,10 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
   const uint32_t waves = gridDim.x * (blockDim.x >> 6);
   const uint32_t base = lane - sub;
   uint32_t chunk = 0;
-  while (next_chunk(redo + 1, chunk, waves, gpw, n)) {
+  const uint32_t cnt = dn ? min(n, *dn) : n;  // items (n: the column stride of r_limbs)
+  while (next_chunk(redo + 1, chunk, waves, gpw, cnt)) {
     const uint32_t i = chunk * gpw + g;
-    if (i >= n || status[i] != ST_PENDING) continue;
+    if (i >= cnt || status[i] != ST_PENDING) continue;
     const apoint_raw *qt = ktab28 + (size_t)key_slot[i] * KT_ENTRIES;
     const int8_t *dg = digits + (size_t)i * DIG_STRIDE;
     jp28 acc;

@@ -68,15 +68,25 @@ __device__ __forceinline__ uint32_t ld_u32(const uint8_t *p) {  // unaligned lit
   const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
 }
+// span k's base and start by selects (a dynamically indexed JobView would live in scratch)
+__device__ __forceinline__ const uint8_t *span_p(const JobView &v, int k) {
+  return k == 0 ? v.p[0] : (k == 1 ? v.p[1] : v.p[2]);
+}
+__device__ __forceinline__ uint32_t span_beg(const JobView &v, int k) {
+  return k == 0 ? 0u : (k == 1 ? v.beg[1] : v.beg[2]);
+}
+__device__ __forceinline__ uint32_t span_end(const JobView &v, int k) {
+  return k == 0 ? v.beg[1] : (k == 1 ? v.beg[2] : v.beg[3]);
+}
 __device__ __forceinline__ uint32_t job_byte(const JobView &v, uint32_t q) {
   if (q >= v.L) return q == v.L ? 0x80u : 0u;
   const int k = q < v.beg[1] ? 0 : (q < v.beg[2] ? 1 : 2);
-  return v.p[k][q - v.beg[k]];
+  return span_p(v, k)[q - span_beg(v, k)];
 }
 // big-endian message word at byte offset pos of the padded message (bit length excluded)
 __device__ __forceinline__ uint32_t job_word(const JobView &v, uint32_t pos) {
   const int k = pos < v.beg[1] ? 0 : (pos < v.beg[2] ? 1 : 2);
-  if (pos + 4 <= v.beg[k + 1]) return __builtin_bswap32(ld_u32(v.p[k] + (pos - v.beg[k])));
+  if (pos + 4 <= span_end(v, k)) return __builtin_bswap32(ld_u32(span_p(v, k) + (pos - span_beg(v, k))));
   if (pos >= v.L + 1) return 0u;
   uint32_t w = 0;
 #pragma unroll
@@ -107,11 +117,11 @@ __device__ __forceinline__ void sha_view(const JobView &v, uint8_t *out) {
   auto fetch = [&](uint32_t b) {
     const uint32_t s = b * 64;
     const int k = s < v.beg[1] ? 0 : (s < v.beg[2] ? 1 : 2);
-    fast = s + 64 <= v.beg[k + 1];
+    fast = s + 64 <= span_end(v, k);
     if (fast) {
       // global (not flat) loads: the 17 dwords merge into 4 x dwordx4 + 1 -- a quarter of the
       // per-lane cache-line requests of dword loads, where 64 lanes read 64 scattered messages
-      const uintptr_t a = reinterpret_cast<uintptr_t>(v.p[k] + (s - v.beg[k]));
+      const uintptr_t a = reinterpret_cast<uintptr_t>(span_p(v, k) + (s - span_beg(v, k)));
       const __attribute__((address_space(1))) uint32_t *al =
           reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(a & ~(uintptr_t)3);
       sh = (uint32_t)(a & 3u);

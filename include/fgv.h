@@ -191,6 +191,16 @@ int fgv_chaincode_define(fgv_ctx *ctx, const char *ns, const uint8_t *policy, si
 int fgv_validate_blocks(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
                         const size_t *lens, const uint8_t *const *d_blocks, uint8_t *flags,
                         size_t flags_cap, size_t *ntx);
+/* fgv_validate_blocks that also prepares the NEXT batch while this one runs on the GPU (the
+ * single-GPU committer pipeline): its envelope framing is walked on a host worker and, when both
+ * batches are host-resident, its bytes are copied to the device on the copy stream
+ * (next_d_blocks: its device copy, or NULL).  The next batch's buffers must stay valid and
+ * unchanged until its call.  Results never depend on it. */
+int fgv_validate_blocks_pipelined(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
+                                  const size_t *lens, const uint8_t *const *d_blocks, uint8_t *flags,
+                                  size_t flags_cap, size_t *ntx, size_t next_nblocks,
+                                  const uint8_t *const *next_blocks, const size_t *next_lens,
+                                  const uint8_t *const *next_d_blocks);
 
 /* ----------------------------------------------- multi-GPU committer (one process per GPU)
  * fgv_validate_blocks = fgv_validate_shard over every transaction + fgv_finalize_flags.
@@ -285,12 +295,19 @@ int fgv_validate_shard_dev_pipelined(fgv_ctx *ctx, size_t nblocks, const uint8_t
                                      const uint8_t *const *next_d_blocks, const uint32_t *next_lo,
                                      const uint32_t *next_hi);
 int fgv_last_ahead(fgv_ctx *ctx);
-/* Where the next batch's front half is enqueued by fgv_validate_shard_dev_pipelined: 0 = not
- * ahead (default; the environment variable FGV_AHEAD sets the initial value): one batch on the
- * GPU at a time, the next one pre-split on the host -- the fastest on MI355X for C2-shaped
- * batches; 1 = once the current batch's ECDSA kernels are done; 2 = at once;
- * 3 = once its policy fold is done.  Results never depend on it. */
+/* Where the next batch's front half is enqueued by the pipelined calls (fgv_validate_shard_dev_
+ * pipelined, fgv_validate_blocks_pipelined) when its device copy is known: 0 = not ahead (default;
+ * the environment variable FGV_AHEAD sets the initial value): one batch on the GPU at a time, the
+ * next one pre-split on the host; 2 = at once, beside the current batch's back half (equal to 0
+ * within noise on MI355X for C2-shaped batches); 1 = once the current batch's ECDSA
+ * kernels are done; 3 = once its policy fold is done.  Results never depend on it. */
 int fgv_set_ahead(fgv_ctx *ctx, int mode);
+/* Per-kernel device times of the block committer (fgv_last_kernel_times, fgv_last_timing): on,
+ * every kernel of the back half is bracketed by timestamp events -- each a packet on the
+ * critical path (~5 us on MI355X) -- off (default; the environment variable FGV_TIMING sets the
+ * initial value), only the events that order the streams are recorded, which time the payload
+ * hashes, the parse, the other hashes and the identity/count kernels.  Results never depend on it. */
+int fgv_set_timing(fgv_ctx *ctx, int on);
 /* Page-locked host memory for block buffers (hipHostMalloc): H2D copies from it run on the copy
  * engine at PCIe rate, asynchronously.  fgv_last_h2d: bytes the last validation call copied
  * itself, and blocks it found already copied by the previous call's prefetch. */

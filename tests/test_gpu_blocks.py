@@ -330,6 +330,62 @@ def test_host_resident_rotation_prefetches_next_batch(pinned):
     eng.close()
 
 
+@pytest.mark.parametrize("where", ["hbm", "pinned", "pageable"])
+def test_single_gpu_pipelined_rotation(where):
+    """fgv_validate_blocks_pipelined (validation + finalize queued back to back, one
+    synchronisation; the next batch pre-split -- and, host-resident, pre-copied -- during the
+    call) over a rotation A, B, C, A, C, B, B: flags equal the oracle's on every call, the
+    pre-split is used exactly when the call's batch was the announced one, host-resident calls
+    find their blocks prefetched, and a mid-rotation call of an unannounced batch still matches."""
+    import torch
+    net = network()
+    sizes = [[23, 5], [31], [9, 17, 3]]
+    sets, exps = [], []
+    for k, sz in enumerate(sizes):
+        blks = [blocks.make_block(net, n, number=1 + i, seed=700 + 10 * k + i)[0] for i, n in enumerate(sz)]
+        sets.append(blks)
+        exps.append([f for fl in _oracle(net, blks) for f in fl])
+    eng = _engine_for(net)
+    bufs, batches, keep = [], [], []
+    for blks in sets:
+        if where == "hbm":
+            arena = torch.zeros(sum((len(b) + 64 + 255) // 256 * 256 for b in blks), dtype=torch.uint8, device="cuda")
+            dp, o = [], 0
+            for b in blks:
+                arena[o:o + len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+                dp.append(arena.data_ptr() + o)
+                o += (len(b) + 64 + 255) // 256 * 256
+            keep.append(arena)
+            batches.append(eng.block_batch(blks, dp))
+        elif where == "pinned":
+            pb = eng.host_alloc(sum(len(b) for b in blks))
+            views, o = [], 0
+            for b in blks:
+                pb.a[o:o + len(b)] = np.frombuffer(b, np.uint8)
+                views.append(pb.a[o:o + len(b)])
+                o += len(b)
+            bufs.append(pb)
+            batches.append(eng.block_batch(views))
+        else:
+            batches.append(eng.block_batch(blks))
+    torch.cuda.synchronize()
+    order = [0, 1, 2, 0, 2, 1, 1]
+    for i, k in enumerate(order):
+        nxt = batches[order[i + 1]] if i + 1 < len(order) else None
+        flags = eng.validate_blocks_pipelined(batches[k], nxt)
+        assert list(flags) == exps[k], (i, k)
+        assert eng.last_presplit() == (i > 0), i
+        if where != "hbm":
+            assert eng.last_h2d()[1] == (batches[k].nb if i > 0 else 0), (i, eng.last_h2d())
+    # an unannounced batch (announced: 0, called: 2), then the plain single-batch call
+    eng.validate_blocks_pipelined(batches[1], batches[0])
+    assert list(eng.validate_blocks_pipelined(batches[2])) == exps[2] and not eng.last_presplit()
+    assert [f for fl in eng.validate_blocks(sets[0]) for f in fl] == exps[0]
+    for pb in bufs:
+        pb.close()
+    eng.close()
+
+
 def _random_records(rng, ntx, pool):
     """fgv_tx_result records honouring the engine's invariants: VALID => REACHED;
     REACHED => INDEXED with index_txid == txid."""
