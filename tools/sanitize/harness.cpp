@@ -9,6 +9,7 @@
 //   kind 3 chaincode policy bytes (ApplicationPolicy) of namespace "mycc"
 //   kind 4 TxReadWriteSet bytes: fgv_mvcc_parse_probe (phantom-path decode + range validators)
 //   kind 5 channel name
+//   kind 9 canary: reads one byte past its record (proves the sanitizer is live)
 // Any sanitizer report aborts the process (halt_on_error); exit 0 = clean.
 #include <stdint.h>
 #include <stdio.h>
@@ -66,6 +67,9 @@ int main(int argc, char **argv) {
       }
       acc = acc * 31 + fgv_block_parse_probe(channel.c_str(), ids.data(), id_lens.data(), ids.size(), "mycc",
                                              policy.data(), policy.size(), blocks[0], n);
+    } else if (r.first == 9) {
+      // canary (tests/test_sanitize.py): one byte read past the record -- the run must abort
+      acc += buf.data()[buf.size()];
     } else if (r.first == 4) {
       nrws++;
       acc = acc * 31 + fgv_mvcc_parse_probe(p ? p : reinterpret_cast<const uint8_t *>(""), n);
