@@ -7,7 +7,8 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-functi
 CSRC := fabric_amd/csrc
 OBJDIR := build
 KOBJS := $(OBJDIR)/sha256.o $(OBJDIR)/p256_kernels.o $(OBJDIR)/der_kernel.o $(OBJDIR)/fgv_host.o $(OBJDIR)/fgv_block.o $(OBJDIR)/mvcc.o $(OBJDIR)/fgv_mvcc.o \
-	$(OBJDIR)/finalize.o $(OBJDIR)/fgv_integrity.o $(OBJDIR)/blockdev.o $(OBJDIR)/fgv_commit.o $(OBJDIR)/fgv_channel.o
+	$(OBJDIR)/finalize.o $(OBJDIR)/fgv_integrity.o $(OBJDIR)/blockdev.o $(OBJDIR)/fgv_commit.o $(OBJDIR)/fgv_channel.o \
+	$(OBJDIR)/fgv_group.o
 HDRS := $(CSRC)/p256_field.h $(CSRC)/fgv_kernels.h $(CSRC)/fgv_der.h $(CSRC)/fgv_internal.h include/fgv.h $(CSRC)/blockdev.h $(CSRC)/pbwire_dev.h
 
 all: fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so
@@ -31,6 +32,9 @@ $(OBJDIR)/fgv_integrity.o: $(CSRC)/fgv_integrity.cpp $(HDRS) $(CSRC)/pbwire.h $(
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/fgv_channel.o: $(CSRC)/fgv_channel.cpp $(CSRC)/fgv_channel.h $(HDRS) $(CSRC)/pbwire.h $(CSRC)/fgv_visitors.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/fgv_group.o: $(CSRC)/fgv_group.cpp $(HDRS) $(CSRC)/thread_pool.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/fgv_commit.o: $(CSRC)/fgv_commit.cpp $(HDRS) $(CSRC)/pbwire.h $(CSRC)/fgv_visitors.h $(CSRC)/sha256_host.h | $(OBJDIR)

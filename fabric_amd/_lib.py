@@ -30,6 +30,7 @@ EXPORTED = [
     "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d",
     "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead", "fgv_blocks_verify_signed",
     "fgv_validate_blocks_pipelined", "fgv_set_timing",
+    "fgv_group_init", "fgv_group_destroy", "fgv_group_size", "fgv_group_ctx", "fgv_group_validate_blocks",
 ]
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
@@ -134,6 +135,14 @@ def load():
         L.fgv_last_ahead.argtypes = [vp]
         L.fgv_set_ahead.argtypes = [vp, ctypes.c_int]
         L.fgv_set_timing.argtypes = [vp, ctypes.c_int]
+        L.fgv_group_init.argtypes = [vp, sz, ctypes.POINTER(_Config), ctypes.POINTER(vp)]
+        L.fgv_group_destroy.argtypes = [vp]
+        L.fgv_group_destroy.restype = None
+        L.fgv_group_size.argtypes = [vp]
+        L.fgv_group_size.restype = sz
+        L.fgv_group_ctx.argtypes = [vp, sz]
+        L.fgv_group_ctx.restype = vp
+        L.fgv_group_validate_blocks.argtypes = [vp, sz, vp, vp, vp, sz, vp]
         L.fgv_finalize_flags_dev_plan.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
@@ -275,6 +284,49 @@ class PinnedBuffer:
         self.ptr = None
 
 
+class Group:
+    """fgv_group: several GPUs driven from one process.  .engines[i] is device i's context
+    (set each one up like an Engine: txvalidator.setup_channel(...) on every one)."""
+
+    def __init__(self, devices, key_slots: int = 4096, host_threads: int = 0):
+        self._L = load()
+        arr = (ctypes.c_int * len(devices))(*devices)
+        cfg = _Config(devices[0], key_slots, host_threads)
+        h = ctypes.c_void_p()
+        _check(self._L.fgv_group_init(arr, len(devices), ctypes.byref(cfg), ctypes.byref(h)))
+        self._g = h
+        self.engines = [Engine._borrow(self._L.fgv_group_ctx(h, i)) for i in range(self._L.fgv_group_size(h))]
+
+    def validate_blocks(self, blocks):
+        """fgv_group_validate_blocks: per-block flag arrays, as Engine.validate_blocks"""
+        nb = len(blocks)
+        bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+        ptrs = (ctypes.c_void_p * nb)(*[b.ctypes.data for b in bufs])
+        lens = (ctypes.c_size_t * nb)(*[len(b) for b in blocks])
+        cap = sum(len(b) for b in blocks) // 16 + 1024
+        flags = np.zeros(cap, dtype=np.uint8)
+        ntx = (ctypes.c_size_t * nb)()
+        _check(self._L.fgv_group_validate_blocks(self._g, nb, ptrs, lens, _ptr(flags), cap, ntx))
+        out, o = [], 0
+        for i in range(nb):
+            out.append(flags[o:o + ntx[i]].copy())
+            o += ntx[i]
+        return out
+
+    def close(self):
+        if getattr(self, "_g", None):
+            for e in self.engines:
+                e._h = None
+            self._L.fgv_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Engine:
     """One libfgv context = one GPU (one process per GPU)."""
 
@@ -287,10 +339,21 @@ class Engine:
         h = ctypes.c_void_p()
         _check(self._L.fgv_init(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
+        self._owned = True
+
+    @classmethod
+    def _borrow(cls, handle):
+        """an Engine over a context owned by someone else (a Group's device context)"""
+        e = cls.__new__(cls)
+        e._L = load()
+        e._h = ctypes.c_void_p(handle)
+        e._owned = False
+        return e
 
     def close(self):
         if getattr(self, "_h", None):
-            self._L.fgv_destroy(self._h)
+            if getattr(self, "_owned", True):
+                self._L.fgv_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -44,7 +44,8 @@ typedef struct fgv_ctx fgv_ctx;
 typedef struct fgv_config {
   int device;            /* HIP device ordinal (one process per GPU)                 */
   uint32_t key_slots;    /* capacity of the device public-key table cache (0 = 4096) */
-  uint32_t host_threads; /* host worker threads for parsing / policy fold (0 = 24)    */
+  uint32_t host_threads; /* host worker threads for parsing / policy fold (0 = min(24,
+                            the process's CPU share: affinity mask, OMP_NUM_THREADS)) */
 } fgv_config;
 
 /* Replaces factory.GetDefault() / sw.NewDefaultSecurityLevel* for the verify + hash
@@ -249,6 +250,23 @@ int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *r
 int fgv_validate_shard_dev(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks,
                            const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                            const uint32_t *tx_hi, void *d_results, size_t results_cap, size_t *ntx);
+/* Several GPUs from one process (a peer that drives all its GPUs through this ABI): one
+ * context per device; fgv_group_ctx(g, i) is device i's context, which the caller sets up
+ * like any other (channel model, identities, chaincodes, ledger txids: the same calls on every
+ * context).  fgv_group_validate_blocks = fgv_validate_blocks over all devices: the blocks are
+ * split into contiguous ranges of about equal bytes, one per device (each device stages, splits
+ * and parses only its own), the devices validate in parallel (fgv_validate_shard_dev), their
+ * records are gathered onto the first device by peer copies (xGMI), and the first device runs
+ * the batch's cross-transaction steps (fgv_finalize_flags_dev_plan).  Same flags as one GPU.
+ * host_threads 0 in cfg: the process's CPU share divided among the devices. */
+typedef struct fgv_group fgv_group;
+int fgv_group_init(const int *devices, size_t ndev, const fgv_config *cfg, fgv_group **out);
+void fgv_group_destroy(fgv_group *g);
+size_t fgv_group_size(const fgv_group *g);
+fgv_ctx *fgv_group_ctx(fgv_group *g, size_t i);
+int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                              uint8_t *flags, size_t flags_cap, size_t *ntx);
+
 /* Deliver-side pre-split (no reference counterpart: the Go committer re-walks each block
  * inside TxValidator.Validate, validator.go:180-265).  Starts walking the block data framing
  * (the envelope spans) of a batch on a background host thread and returns at once; the next

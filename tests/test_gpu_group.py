@@ -1,0 +1,76 @@
+"""GPU: fgv_group (several devices driven from one process through the C ABI) against the
+single-GPU engine and the oracle.  The box has one MI355X, so the group's devices are the same
+GPU several times -- every part of the protocol runs (block plan, per-device contexts and
+host workers, the gather by peer copies, the finalize of the whole batch on the first device)
+except that the copies stay inside one HBM."""
+import pytest
+
+from fabric_amd import _lib, txvalidator
+from fabric_amd.synth import blocks
+from oracle import v20
+from tests.blockfix import network
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(eng, net, committed=()):
+    txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes, committed)
+
+
+@pytest.mark.parametrize("ndev", [1, 2, 3])
+def test_group_matches_single_gpu_and_oracle(ndev):
+    """C2 blocks with duplicate txids across blocks (a txid of block 1 again in blocks 3 and 5,
+    which the block plan puts on other devices): the finalize on the first device sees the whole
+    batch, so flags equal the single GPU's and the oracle's."""
+    net = network()
+    txs1 = []
+    blks = [blocks.make_block(net, 40, number=1, seed=901, faults=(), out_txs=txs1)[0]]
+    for i in range(2, 7):
+        reuse = {2: (txs1[i].creator, txs1[i].nonce), 7: (txs1[0].creator, txs1[0].nonce)} if i in (3, 5) else None
+        blks.append(blocks.make_block(net, 25 + 7 * i, number=i, seed=900 + i, reuse=reuse)[0])
+    g = _lib.Group([0] * ndev)
+    assert len(g.engines) == ndev
+    for e in g.engines:
+        _setup(e, net)
+    got = g.validate_blocks(blks)
+    one = _lib.Engine(0)
+    _setup(one, net)
+    single = one.validate_blocks(blks)
+    exp = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), net.chaincodes), blks)
+    for b in range(len(blks)):
+        assert list(got[b]) == list(single[b]) == list(exp[b]), b
+    assert any(9 in list(f) for f in got[2:])  # the cross-device duplicates were caught
+    one.close()
+    g.close()
+
+
+def test_group_more_devices_than_blocks_and_ledger_txids():
+    """4 devices, 2 blocks (two devices idle); ledger txids registered on every context"""
+    net = network()
+    b0, _, envs0 = blocks.make_block(net, 30, number=1, seed=777, faults=())
+    b1 = blocks.make_block(net, 30, number=2, seed=778)[0]
+    committed = [v20.index_txid(e) for e in envs0[:4]]
+    g = _lib.Group([0, 0, 0, 0])
+    for e in g.engines:
+        _setup(e, net, committed)
+    got = g.validate_blocks([b0, b1])
+    exp = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), net.chaincodes, committed), [b0, b1])
+    assert [list(f) for f in got] == [list(f) for f in exp]
+    assert list(got[0][:4]) == [9, 9, 9, 9]
+    g.close()
+
+
+def test_group_unsupported_propagates():
+    """a block outside the model on any device makes the whole batch FGV_EUNSUPPORTED"""
+    net = network()
+    blks = [blocks.make_block(net, 20, number=i, seed=950 + i)[0] for i in range(1, 4)]
+    g = _lib.Group([0, 0])
+    for e in g.engines:
+        txvalidator.setup_channel(e, net.channel, net.identities(), {})  # no chaincode definitions...
+        e.msp_declare("Org1MSP")
+    # ...and an unregistered identity of a declared MSP in the last block: unsupported
+    rogue = blocks.Network(seed=99, orgs=1, clients=2)
+    blks[-1] = blocks.make_block(rogue, 5, number=3, seed=3)[0]
+    with pytest.raises(_lib.Unsupported):
+        g.validate_blocks(blks)
+    g.close()
