@@ -8,7 +8,7 @@ CSRC := fabric_amd/csrc
 OBJDIR := build
 KOBJS := $(OBJDIR)/sha256.o $(OBJDIR)/p256_kernels.o $(OBJDIR)/der_kernel.o $(OBJDIR)/fgv_host.o $(OBJDIR)/fgv_block.o $(OBJDIR)/mvcc.o $(OBJDIR)/fgv_mvcc.o \
 	$(OBJDIR)/finalize.o $(OBJDIR)/fgv_integrity.o $(OBJDIR)/blockdev.o $(OBJDIR)/fgv_commit.o $(OBJDIR)/fgv_channel.o \
-	$(OBJDIR)/fgv_group.o
+	$(OBJDIR)/fgv_group.o $(OBJDIR)/fgv_msp.o $(OBJDIR)/fgv_x509.o
 HDRS := $(CSRC)/p256_field.h $(CSRC)/fgv_kernels.h $(CSRC)/fgv_der.h $(CSRC)/fgv_internal.h include/fgv.h $(CSRC)/blockdev.h $(CSRC)/pbwire_dev.h
 
 all: fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so
@@ -35,6 +35,12 @@ $(OBJDIR)/fgv_channel.o: $(CSRC)/fgv_channel.cpp $(CSRC)/fgv_channel.h $(HDRS) $
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/fgv_group.o: $(CSRC)/fgv_group.cpp $(HDRS) $(CSRC)/thread_pool.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/fgv_msp.o: $(CSRC)/fgv_msp.cpp $(HDRS) $(CSRC)/fgv_channel.h $(CSRC)/fgv_x509.h $(CSRC)/pbwire.h $(CSRC)/fgv_visitors.h $(CSRC)/sha256_host.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/fgv_x509.o: $(CSRC)/fgv_x509.cpp $(CSRC)/fgv_x509.h $(CSRC)/pbwire.h $(CSRC)/sha256_host.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/fgv_commit.o: $(CSRC)/fgv_commit.cpp $(HDRS) $(CSRC)/pbwire.h $(CSRC)/fgv_visitors.h $(CSRC)/sha256_host.h | $(OBJDIR)

@@ -31,7 +31,10 @@ EXPORTED = [
     "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead", "fgv_blocks_verify_signed",
     "fgv_validate_blocks_pipelined", "fgv_set_timing",
     "fgv_group_init", "fgv_group_destroy", "fgv_group_size", "fgv_group_ctx", "fgv_group_validate_blocks",
+    "fgv_msp_resolve", "fgv_msp_resolve_blocks", "fgv_set_auto_resolve", "fgv_msp_identity",
 ]
+# fgv_msp_resolve status (include/fgv.h)
+RESOLVE_KNOWN, RESOLVE_OK, RESOLVE_FAILED, RESOLVE_UNSUPPORTED, RESOLVE_REPEAT = range(5)
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
 
@@ -161,6 +164,11 @@ def load():
         L.fgv_host_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
         L.fgv_host_free.argtypes = [vp, vp]
         L.fgv_last_h2d.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.fgv_msp_resolve.argtypes = [vp, sz, vp, vp, vp]
+        L.fgv_msp_resolve_blocks.argtypes = [vp, sz, vp, vp, ctypes.POINTER(sz)]
+        L.fgv_set_auto_resolve.argtypes = [vp, ctypes.c_int]
+        L.fgv_msp_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(IdentityInfo)]
+        L.fgv_x509_probe.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz]
         _L = L
     return _L
 
@@ -492,6 +500,40 @@ class Engine:
         ctypes.memmove(info.id_digest, bytes(id_digest), 32)
         _check(self._L.fgv_msp_register_identity(self._h, serialized, len(serialized), ctypes.byref(info)))
 
+    def msp_resolve(self, serialized):
+        """fgv_msp_resolve: the MSP cache miss for a list of SerializedIdentity bytes ->
+        list of RESOLVE_* statuses"""
+        n = len(serialized)
+        bufs = [np.frombuffer(b, dtype=np.uint8) for b in serialized]
+        ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+        lens = (ctypes.c_size_t * n)(*[len(b) for b in serialized])
+        st = (ctypes.c_int * n)()
+        _check(self._L.fgv_msp_resolve(self._h, n, ptrs, lens, st))
+        return list(st)
+
+    def msp_resolve_blocks(self, blocks):
+        """fgv_msp_resolve_blocks: the batch's unregistered creators / endorsers resolved ->
+        the number registered"""
+        nb = len(blocks)
+        bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+        ptrs = (ctypes.c_void_p * nb)(*[b.ctypes.data for b in bufs])
+        lens = (ctypes.c_size_t * nb)(*[len(b) for b in blocks])
+        reg = ctypes.c_size_t()
+        _check(self._L.fgv_msp_resolve_blocks(self._h, nb, ptrs, lens, ctypes.byref(reg)))
+        return reg.value
+
+    def set_auto_resolve(self, on: bool):
+        _check(self._L.fgv_set_auto_resolve(self._h, 1 if on else 0))
+
+    def msp_identity(self, serialized: bytes):
+        """fgv_msp_identity: the registry's record (dict) or None"""
+        info = IdentityInfo()
+        rc = self._L.fgv_msp_identity(self._h, serialized, len(serialized), ctypes.byref(info))
+        if rc != 0:
+            return None
+        return dict(key=info.key_type, hash_family=info.hash_family, valid=bool(info.valid), roles=info.roles,
+                    pub=bytes(info.pubkey), id_digest=bytes(info.id_digest))
+
     def ledger_add_txids(self, txids):
         arena, offs, lens = pack([t.encode() for t in txids])
         _check(self._L.fgv_ledger_add_txids(self._h, _ptr(arena), _ptr(offs), _ptr(lens), len(txids)))
@@ -737,3 +779,15 @@ def commit_hash(block: bytes, flags, block_num: int, prev: bytes = b""):
     _check(L.fgv_commit_hash(b.ctypes.data, len(block), _ptr(f), len(f), block_num,
                              pv.ctypes.data if pv is not None else None, len(prev), out))
     return out.raw
+
+
+def x509_probe(pem: bytes):
+    """fgv_x509_probe (CPU, no GPU): the engine's PEM -> X.509 parse -> sanitizeCert of one
+    certificate, as a dict (the parity tests compare it with oracle/x509.py)"""
+    import json
+    L = load()
+    out = ctypes.create_string_buffer(1 << 16)
+    n = L.fgv_x509_probe(pem, len(pem), out, len(out))
+    if n < 0:
+        raise FgvError("x509 probe output too large")
+    return json.loads(out.raw[:n].decode())

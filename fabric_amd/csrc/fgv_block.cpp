@@ -252,6 +252,7 @@ struct fgv_block_state {
 };
 
 fgv_block_state *fgv_block_state_new(unsigned threads) { return new fgv_block_state(threads); }
+Channel &fgv_block_channel(fgv_block_state *S) { return S->ch; }
 void fgv_parallel_for(fgv_block_state *S, size_t n, const std::function<void(size_t)> &f) {
   S->pool.parallel_for(n, f);
 }
@@ -841,6 +842,8 @@ int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, i
   I.valid = info->valid != 0;
   I.roles_known = (info->roles & FGV_ROLES_UNKNOWN) == 0;
   I.roles = I.roles_known ? info->roles : 0;
+  memcpy(I.digest, info->id_digest, 32);
+  if (I.kind == FGV_KEY_P256) memcpy(I.pub, info->pubkey, 64);
   std::string canon = I.mspid + std::string(reinterpret_cast<const char *>(info->id_digest), 32);
   auto it = ch.canon_ids.find(canon);
   if (it == ch.canon_ids.end()) it = ch.canon_ids.emplace(canon, (uint32_t)ch.canon_ids.size()).first;
@@ -1559,6 +1562,31 @@ int fgv_block_sig_verdicts(fgv_ctx *c, size_t n, const fgv_sig_block *in, const 
   std::lock_guard<std::mutex> g(c->mu);
   Channel &ch = c->blk->ch;
   if (ch.dirty) ch.compile();
+  // orderer identities the registry has not seen: the MSP cache miss first (fgv_msp.cpp)
+  if (fgv_msp_auto(c)) {
+    std::vector<std::string> miss;
+    for (size_t b = 0; b < n; b++) {
+      VMetadata md;
+      if (!in[b].want || !pbw::decode(in[b].meta, in[b].meta_n, md)) continue;
+      for (const VMetaSig &ms : md.sigs) {
+        VSignatureHeader sh;
+        if (pbw::decode(ms.sig_header.p, ms.sig_header.n, sh) && ch.lookup(sh.creator) == -2)
+          miss.push_back(sh.creator.str());
+      }
+    }
+    if (!miss.empty()) {
+      std::vector<const uint8_t *> mp(miss.size());
+      std::vector<size_t> ml(miss.size());
+      std::vector<int> st(miss.size());
+      for (size_t i = 0; i < miss.size(); i++) {
+        mp[i] = reinterpret_cast<const uint8_t *>(miss[i].data());
+        ml[i] = miss[i].size();
+      }
+      const int rc = fgv_msp_resolve_locked(c, miss.size(), mp.data(), ml.data(), st.data(), nullptr);
+      if (rc) return rc;
+      if (ch.dirty) ch.compile();
+    }
+  }
   const int pi = channel_policy_index(ch, policy ? policy : "/Channel/Orderer/BlockValidation");
   // does the evaluation reach SignatureSetToValidIdentities?  A signature policy does; an
   // ImplicitMeta policy does through any signature sub-policy (a rejecting sub-policy never
@@ -1660,6 +1688,45 @@ int fgv_block_sig_verdicts(fgv_ctx *c, size_t n, const fgv_sig_block *in, const 
     verdict[b] = v == 2 ? FGV_SIGV_UNSUP : v == 1 ? FGV_SIGV_OK : FGV_SIGV_FAIL;
   }
   return FGV_OK;
+}
+
+// ======================================================================= MSP cache misses
+void fgv_block_misses(fgv_block_state *S, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                      std::vector<std::string> &out) {
+  Channel &ch = S->ch;
+  if (ch.dirty) ch.compile();
+  std::vector<Span> envs;
+  for (size_t b = 0; b < nblocks; b++) {
+    VBlock blk;
+    if (pbw::decode(blocks[b], lens[b], blk)) envs.insert(envs.end(), blk.data.data.begin(), blk.data.data.end());
+  }
+  std::vector<std::vector<Span>> per(envs.size());
+  S->pool.parallel_for(envs.size(), [&](size_t t) {
+    auto add = [&](const Span &id) {
+      if (ch.lookup(id) == -2) per[t].push_back(id);
+    };
+    VEnvelope env;
+    VPayload pl;
+    VHeader hdr;
+    if (!pbw::decode(envs[t].p, envs[t].n, env) || !pbw::decode(env.payload.p, env.payload.n, pl) ||
+        !pl.header.decode_into(hdr))
+      return;
+    VSignatureHeader sh;
+    if (pbw::decode(hdr.signature_header.p, hdr.signature_header.n, sh)) add(sh.creator);
+    VTransaction tx;
+    if (!pbw::decode(pl.data.p, pl.data.n, tx)) return;
+    for (const VTransactionAction &act : tx.actions) {
+      VCcActionPayload cap;
+      if (!pbw::decode(act.payload.p, act.payload.n, cap) || !cap.has_action) continue;
+      for (const auto &e : cap.action.ends) add(e.endorser);
+    }
+  });
+  std::unordered_set<std::string_view> seen;
+  for (const auto &v : per)
+    for (const Span &id : v) {
+      const std::string_view k(reinterpret_cast<const char *>(id.p), id.n);
+      if (seen.insert(k).second) out.push_back(std::string(k));
+    }
 }
 
 // ======================================================================= sanitizer probe

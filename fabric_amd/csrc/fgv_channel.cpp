@@ -380,6 +380,7 @@ bool walk(const std::vector<Span> &occ, const std::string &path, const std::stri
       const std::string name = fc.name.str(), fam = cc.family.str();
       if (fam != "SHA2" && fam != "SHA3") out.unsupported = true;
       out.msps[name] = fam == "SHA3";
+      out.msp_conf[name] = mc.config.str();  // (the cache-miss path builds its MSP model from it)
       if (parent == "Application") out.app_orgs[name] = path.substr(path.rfind('/') + 1);
     }
   }

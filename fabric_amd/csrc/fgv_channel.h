@@ -39,6 +39,8 @@ struct Ident {
   uint32_t roles = 0;           // bit r: satisfies ROLE principal r of its own MSP
   uint32_t canon = 0;           // dedup identity id: Mspid + Id (Id = hex SHA-256(cert))
   int32_t msp = -1;             // interned Mspid
+  uint8_t digest[32] = {};      // identity Id (SHA-256 of the certificate)
+  uint8_t pub[64] = {};         // P-256 X || Y (FGV_KEY_P256)
   // Verify outcome class: 0 = verified on the GPU, 1 = always fails (RSA, F5), 2 = outside
   // the engine (P-384, SHA3 MSP)
   int verify_class() const {
@@ -79,6 +81,7 @@ struct RawConfig {
   bool unsupported = false;                       // e.g. an MSP with an unknown hash family
   std::map<std::string, RawChanPolicy> policies;  // "Application/org1/Endorsement" (relative to /Channel)
   std::map<std::string, bool> msps;               // MSP name -> SHA3
+  std::map<std::string, std::string> msp_conf;    // MSP name -> FabricMSPConfig bytes (fgv_msp.cpp)
   std::map<std::string, std::string> app_orgs;    // mspid -> application org group name
 };
 bool parse_channel_config(const uint8_t *p, size_t n, RawConfig &out);

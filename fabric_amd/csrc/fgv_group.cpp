@@ -129,6 +129,7 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
       rcs[r] = FGV_ENOMEM;
       return;
     }
+    // (an identity this device's registry has not seen is resolved inside, MSP cache miss)
     rcs[r] = fgv_validate_shard_dev(g->ctx[r], nb, blocks + b0[r], lens + b0[r], nullptr, nullptr, nullptr,
                                     g->res[r].p, cap[r], ntx + b0[r]);
   });

@@ -147,6 +147,7 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->blk) fgv_block_state_free(c->blk);
   if (c->mv) fgv_mvcc_free(c->mv);
   fgv_integrity_free(c);
+  fgv_msp_cache_free(c);
   for (auto *b : d) b->release();
   HostBuf *h[] = {&c->h_status, &c->h_slot, &c->h_r, &c->h_s, &c->h_dig, &c->h_kq, &c->h_kslot,
                   &c->h_moff, &c->h_mlen, &c->hb_dig, &c->hb_vst, &c->hb_jobs, &c->hb_sigp,
@@ -662,6 +663,10 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *c, const uint8_t *d_msg_buf, const uint64_
 
 }  // extern "C"
 
+int fgv_keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots) {
+  return keys_register_locked(c, keys, n, slots);
+}
+
 // ======================================================================= block engine glue
 // verify-job arrays share one staging block (one H2D copy): [sig_ptr u64 | sig_len | key_slot
 // | dig_idx u32], each of nv entries
@@ -1038,12 +1043,18 @@ int fgv_set_parse_mode(fgv_ctx *c, int mode) {
   return fgv_block_set_parse_mode(c->blk, mode);
 }
 
-int fgv_validate_shard(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
-                       const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
-                       fgv_tx_result *results, size_t results_cap, size_t *ntx) {
-  if (!c || (nblocks && (!blocks || !lens || !ntx || (results_cap && !results)))) return FGV_EINVAL;
-  if (nblocks == 0) return FGV_OK;
-  std::lock_guard<std::mutex> g(c->mu);
+// An FGV_EUNSUPPORTED batch whose obstacle may be identities the registry has not seen: resolve
+// them through the channel's MSPs (the MSP cache miss, fgv_msp.cpp); true when any was added,
+// so that one retry of the batch can help.
+static bool resolve_for_retry(fgv_ctx *c, int rc, size_t nblocks, const uint8_t *const *blocks, const size_t *lens) {
+  if (rc != FGV_EUNSUPPORTED || !fgv_msp_auto(c)) return false;
+  size_t reg = 0;
+  return fgv_msp_resolve_blocks_locked(c, nblocks, blocks, lens, &reg) == FGV_OK && reg > 0;
+}
+
+static int shard_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                        const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                        fgv_tx_result *results, size_t results_cap, size_t *ntx) {
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
   std::vector<const uint8_t *> dev;
   int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
@@ -1061,6 +1072,18 @@ int fgv_validate_shard(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks,
   }
   return fgv_block_validate_impl(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi, results,
                                  results_cap, ntx);
+}
+
+int fgv_validate_shard(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                       const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                       fgv_tx_result *results, size_t results_cap, size_t *ntx) {
+  if (!c || (nblocks && (!blocks || !lens || !ntx || (results_cap && !results)))) return FGV_EINVAL;
+  if (nblocks == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  int rc = shard_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, results, results_cap, ntx);
+  if (resolve_for_retry(c, rc, nblocks, blocks, lens))
+    rc = shard_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, results, results_cap, ntx);
+  return rc;
 }
 
 static int shard_dev_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
@@ -1100,7 +1123,10 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   if (!c || (nblocks && (!blocks || !lens || !ntx || (results_cap && !d_results)))) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   c->next = fgv_ctx::NextBatch{};
-  return shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  int rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  if (resolve_for_retry(c, rc, nblocks, blocks, lens))
+    rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  return rc;
 }
 
 int fgv_validate_shard_dev_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
@@ -1118,6 +1144,8 @@ int fgv_validate_shard_dev_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *
   c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks,   next_lens, next_lo, next_hi,
                                !next_d_blocks && !d_blocks, next_d_blocks, nullptr};
   int rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  if (resolve_for_retry(c, rc, nblocks, blocks, lens))
+    rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
   if (c->next.n) {  // not started inside (host-parse path, empty batch, early error): start it now
     fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, c->next.lo, c->next.hi);
   }
@@ -1286,6 +1314,8 @@ int fgv_validate_blocks_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *con
   c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks,   next_lens, nullptr, nullptr,
                                !next_d_blocks && !d_blocks, next_d_blocks, nullptr};
   int rc = validate_blocks_locked(c, nblocks, blocks, lens, d_blocks, flags, flags_cap, ntx);
+  if (resolve_for_retry(c, rc, nblocks, blocks, lens))
+    rc = validate_blocks_locked(c, nblocks, blocks, lens, d_blocks, flags, flags_cap, ntx);
   if (c->next.n)  // not started inside (host-parse path, empty batch, early error): start it now
     fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, nullptr, nullptr);
   c->next = fgv_ctx::NextBatch{};

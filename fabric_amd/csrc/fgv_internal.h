@@ -18,7 +18,11 @@
 
 struct fgv_block_state;
 struct fgv_mvcc_state;
+struct fgv_msp_cache;
 struct ThreadPool;
+namespace fgvb {
+struct Channel;
+}
 
 namespace fgvh {
 
@@ -167,6 +171,7 @@ struct fgv_ctx {
   DevBuf bd_env, bd_bases, bd_tx, bd_ident, bd_jobs, bd_misc;
   HostBuf hb_env, hb_bases, hb_misc;
   double t_bd_split = 0, t_bd_pre = 0, t_bd_fold = 0;
+  fgv_msp_cache *msp = nullptr;  // MSP models of the cache-miss path (fgv_msp.cpp)
 };
 void fgv_integrity_free(fgv_ctx *c);
 
@@ -263,6 +268,22 @@ struct fgv_sig_block {
 // path; bft: the channel runs BFT (identifier headers are then outside the model).
 int fgv_block_sig_verdicts(fgv_ctx *c, size_t n, const fgv_sig_block *in, const char *policy, int bft,
                            uint8_t *verdict);
+
+// registered (pinned) P-256 keys -> key-table slots; c->mu held (fgv_host.cpp)
+int fgv_keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots);
+// the channel model of a block state (fgv_block.cpp)
+fgvb::Channel &fgv_block_channel(fgv_block_state *S);
+// the identities a batch names (creators, endorsers) that the registry does not hold but a
+// channel MSP may (Channel::lookup == -2), deduplicated (fgv_block.cpp)
+void fgv_block_misses(fgv_block_state *S, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                      std::vector<std::string> &out);
+// the MSP cache miss (fgv_msp.cpp); c->mu held.  registered: identities added to the registry
+int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, const size_t *lens, int *status,
+                           size_t *registered);
+int fgv_msp_resolve_blocks_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                  size_t *registered);
+bool fgv_msp_auto(fgv_ctx *c);  // fgv_set_auto_resolve (default on)
+void fgv_msp_cache_free(fgv_ctx *c);
 
 // Sanitizer probes (tools/sanitize/harness.cpp): the host parsers alone, no GPU call
 uint64_t fgv_block_parse_probe(const char *channel, const uint8_t *const *ids, const size_t *id_lens, size_t nids,

@@ -1,0 +1,508 @@
+// fgv_msp.cpp -- the MSP cache miss on the engine side (fgv_msp_resolve*, include/fgv.h).
+//
+// The peer's MSP cache (msp/cache/cache.go:65-83) hands an identity it has not seen to the
+// channel's MSP, which deserializes and validates the certificate (bccspmsp, MSP version 1.4.3):
+//   mspimpl.go:398-422   deserializeIdentityInternal: pem.Decode, x509.ParseCertificate, bccsp
+//                        KeyImport (Ed25519 fails)
+//   identities.go:48-84  newIdentity: sanitizeCert, then Id = SHA-256 of the sanitized cert
+//   mspimpl.go:892-938   sanitizeCert: chain to a root (x509 Verify at NotBefore + 1 s, exactly
+//                        one chain; else DeserializeIdentity fails), re-marshal with a low-S
+//                        signature
+//   mspimplvalidate.go   validateIdentity: the chain, the signing CA's SubjectKeyIdentifier,
+//                        validateIdentityOUsV142 (OU identifiers; NodeOUs: exactly one role OU)
+//   mspimpl.go:607-680   ROLE principals: MEMBER = Validate; ADMIN = in admins or (valid and
+//                        admin OU); CLIENT / PEER / ORDERER = valid and that OU
+// The MSP model is built from the channel configuration's FabricMSPConfig (root CAs only, no
+// intermediates, no CRLs, OU certificates that are roots); the CA signatures of a batch of
+// misses are verified on the GPU in one pass (the root keys are pinned key-table slots) and the
+// results registered like fgv_msp_register_identity.  Shapes outside the model stay
+// unregistered (the batch stays FGV_EUNSUPPORTED: the reference decides).  The same rules as
+// oracle/msp.py + oracle/x509.py, which the parity tests compare against.
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <map>
+#include <memory>
+#include <unordered_set>
+
+#include "fgv_channel.h"
+#include "fgv_internal.h"
+#include "fgv_x509.h"
+#include "sha256_host.h"
+
+using fgvb::Channel;
+using fgvb::Ident;
+using pbw::Span;
+
+namespace {
+
+// ---- FabricMSPConfig (msp/msp_config.pb.go) visitors
+struct VOUIdent {  // FabricOUIdentifier {certificate 1, organizational_unit_identifier 2}
+  Span cert, ou;
+  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_BYTES : f == 2 ? pbw::K_STRING : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t f, Span s) {
+    (f == 1 ? cert : ou) = s;
+    return true;
+  }
+};
+struct VNodeOUs {  // FabricNodeOUs {enable 1, client 2, peer 3, admin 4, orderer 5}
+  bool enable = false;
+  std::vector<Span> role[6];  // by field number
+  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_VARINT : (f >= 2 && f <= 5) ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { enable = v != 0; }
+  bool on_len(uint32_t f, Span s) {
+    role[f].push_back(s);
+    return true;
+  }
+};
+struct VCryptoCfg {  // FabricCryptoConfig {signature_hash_family 1, identity_identifier_hash_function 2}
+  Span fam, idhash;
+  pbw::Kind kind(uint32_t f) { return (f == 1 || f == 2) ? pbw::K_STRING : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t f, Span s) {
+    (f == 1 ? fam : idhash) = s;
+    return true;
+  }
+};
+struct VMspCfg {  // FabricMSPConfig {name 1, root_certs 2, intermediate_certs 3, admins 4,
+                  // revocation_list 5, organizational_unit_identifiers 7, crypto_config 8,
+                  // fabric_node_ous 11}
+  Span name;
+  std::vector<Span> roots, inters, admins, crls, ous, crypto, node;
+  pbw::Kind kind(uint32_t f) {
+    switch (f) {
+      case 1: return pbw::K_STRING;
+      case 2: case 3: case 4: case 5: return pbw::K_REP_BYTES;
+      case 7: return pbw::K_REP_MSG;
+      case 8: case 11: return pbw::K_MSG;
+      default: return pbw::K_NONE;
+    }
+  }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t f, Span s) {
+    switch (f) {
+      case 1: name = s; break;
+      case 2: roots.push_back(s); break;
+      case 3: inters.push_back(s); break;
+      case 4: admins.push_back(s); break;
+      case 5: crls.push_back(s); break;
+      case 7: ous.push_back(s); break;
+      case 8: crypto.push_back(s); break;
+      default: node.push_back(s); break;
+    }
+    return true;
+  }
+};
+
+template <class V>
+bool decode_all(const std::vector<Span> &occ, V &v) {
+  for (const Span &s : occ)
+    if (!pbw::decode(s.p, s.n, v)) return false;
+  return true;
+}
+
+using Dig = std::array<uint8_t, 32>;
+
+Dig sha(const std::vector<uint8_t> &v) {
+  Dig d;
+  fgvsha::sha256(v.data(), v.size(), d.data());
+  return d;
+}
+
+enum : int { R_CLIENT = 2, R_PEER = 3, R_ADMIN = 1, R_ORDERER = 4 };
+
+struct Root {
+  fgvx::Cert c;
+  Dig certifier;  // SHA-256 of the sanitized root (the OU certifier identifier)
+  uint32_t slot = 0;
+};
+struct RoleOU {
+  bool present = false;
+  std::string name;
+  bool has_cert = false;
+  Dig cert{};
+};
+
+}  // namespace
+
+struct MspModel {
+  bool unsup = false;
+  bool sha3 = false;
+  std::vector<Root> roots;
+  std::map<std::string, std::vector<Dig>> ou_ids;
+  bool node_ous = false;
+  RoleOU role_ou[5];
+  std::vector<std::vector<uint8_t>> admins;  // sanitized admin certificates
+
+  // oracle/msp.py MSP.__init__; c->mu held (registers the root keys)
+  void build(fgv_ctx *c, const std::string &conf) {
+    VMspCfg fc;
+    if (!pbw::decode(reinterpret_cast<const uint8_t *>(conf.data()), conf.size(), fc)) return fail();
+    if (!fc.inters.empty() || !fc.crls.empty()) return fail();
+    VCryptoCfg cc;
+    if (!decode_all(fc.crypto, cc)) return fail();
+    if (!cc.idhash.eq("SHA256", 6) && cc.idhash.n) return fail();
+    sha3 = cc.fam.eq("SHA3", 4);
+    if (fc.roots.empty()) return fail();
+    std::vector<uint8_t> keys;
+    for (const Span &pem : fc.roots) {
+      std::vector<uint8_t> der, raw2;
+      Root r;
+      if (fgvx::pem_decode(pem.p, pem.n, der) != fgvx::X_OK) return fail();
+      if (fgvx::parse_certificate(std::move(der), r.c) != fgvx::X_OK || r.c.key != fgvx::XK_P256) return fail();
+      if (fgvx::sanitized_raw(r.c, raw2) != fgvx::X_OK) return fail();
+      r.certifier = sha(raw2);
+      keys.insert(keys.end(), r.c.pub, r.c.pub + 64);
+      roots.push_back(std::move(r));
+    }
+    std::vector<uint32_t> slots(roots.size());
+    if (fgv_keys_register_locked(c, keys.data(), roots.size(), slots.data()) != FGV_OK) return fail();
+    for (size_t i = 0; i < roots.size(); i++) roots[i].slot = slots[i];
+    // certifier of an OU: the root whose certificate it is
+    auto certifier = [&](const Span &pem, Dig &out) -> bool {
+      std::vector<uint8_t> der;
+      if (fgvx::pem_decode(pem.p, pem.n, der) != fgvx::X_OK) return false;
+      for (const Root &r : roots)
+        if (der == r.c.der) {
+          out = r.certifier;
+          return true;
+        }
+      return false;
+    };
+    for (const Span &o : fc.ous) {
+      VOUIdent id;
+      Dig d;
+      if (!pbw::decode(o.p, o.n, id) || id.cert.nil() || !certifier(id.cert, d)) return fail();
+      ou_ids[id.ou.str()].push_back(d);
+    }
+    VNodeOUs n;
+    if (!decode_all(fc.node, n)) return fail();
+    node_ous = n.enable;
+    static const int field_role[6] = {0, 0, R_CLIENT, R_PEER, R_ADMIN, R_ORDERER};
+    for (int f = 2; f <= 5 && node_ous; f++) {
+      if (n.role[f].empty()) continue;
+      VOUIdent id;
+      if (!decode_all(n.role[f], id)) return fail();
+      RoleOU &ro = role_ou[field_role[f]];
+      ro.present = true;
+      ro.name = id.ou.str();
+      if (!id.cert.nil()) {
+        if (!certifier(id.cert, ro.cert)) return fail();
+        ro.has_cert = true;
+      }
+    }
+    for (const Span &pem : fc.admins) {
+      std::vector<uint8_t> der, raw2;
+      fgvx::Cert ac;
+      if (fgvx::pem_decode(pem.p, pem.n, der) != fgvx::X_OK) return fail();
+      if (fgvx::parse_certificate(std::move(der), ac) != fgvx::X_OK) return fail();
+      if (fgvx::sanitized_raw(ac, raw2) != fgvx::X_OK) return fail();
+      admins.push_back(std::move(raw2));
+    }
+  }
+  void fail() { unsup = true; }
+  bool has(int role, const fgvx::Cert &c) const {
+    const RoleOU &ro = role_ou[role];
+    return ro.present && std::find(c.ous.begin(), c.ous.end(), ro.name) != c.ous.end();
+  }
+};
+
+struct fgv_msp_cache {
+  struct Entry {
+    std::string conf;
+    std::unique_ptr<MspModel> m;
+  };
+  std::map<std::string, Entry> by_name;
+  bool auto_resolve = true;
+};
+
+void fgv_msp_cache_free(fgv_ctx *c) {
+  delete c->msp;
+  c->msp = nullptr;
+}
+
+namespace {
+
+const MspModel *model_of(fgv_ctx *c, const Channel &ch, const std::string &mspid) {
+  auto it = ch.config.msp_conf.find(mspid);
+  if (!ch.config.present || it == ch.config.msp_conf.end()) return nullptr;
+  if (!c->msp) c->msp = new fgv_msp_cache();
+  fgv_msp_cache::Entry &e = c->msp->by_name[mspid];
+  if (!e.m || e.conf != it->second) {
+    e.conf = it->second;
+    e.m.reset(new MspModel());
+    e.m->build(c, e.conf);
+  }
+  return e.m.get();
+}
+
+struct Pending {
+  size_t i;                 // input index
+  const MspModel *m;
+  fgvx::Cert c;
+  const Root *root = nullptr;
+  std::vector<uint8_t> ser;
+};
+
+}  // namespace
+
+// c->mu held.  status[i]: FGV_RESOLVE_*.  *registered: identities added to the registry.
+int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, const size_t *lens, int *status,
+                           size_t *registered) {
+  if (registered) *registered = 0;
+  if (n == 0) return FGV_OK;
+  Channel &ch = fgv_block_channel(c->blk);
+  if (ch.dirty) ch.compile();
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  std::vector<Pending> pend;
+  std::vector<size_t> undeser;  // DeserializeIdentity fails: registered as undeserializable
+  std::unordered_set<std::string> seen;
+  for (size_t i = 0; i < n; i++) {
+    status[i] = FGV_RESOLVE_KNOWN;
+    const Span s{ser[i], (uint32_t)lens[i]};
+    if (ch.lookup(s) != -2) continue;  // registered, or not an identity of a channel MSP
+    if (!seen.insert(s.str()).second) {  // (a repeat within the call: resolved with the first)
+      status[i] = FGV_RESOLVE_REPEAT;
+      continue;
+    }
+    fgvb::VSerializedIdentity sid;
+    pbw::decode(s.p, s.n, sid);
+    const MspModel *m = model_of(c, ch, sid.mspid.str());
+    if (!m || m->unsup) {
+      status[i] = FGV_RESOLVE_UNSUPPORTED;
+      continue;
+    }
+    Pending p;
+    p.i = i;
+    p.m = m;
+    p.ser.assign(s.p, s.p + s.n);
+    std::vector<uint8_t> der;
+    int rc = fgvx::pem_decode(sid.id_bytes.p, sid.id_bytes.n, der);
+    if (rc == fgvx::X_OK) rc = fgvx::parse_certificate(std::move(der), p.c);
+    if (rc == fgvx::X_UNSUP) {
+      status[i] = FGV_RESOLVE_UNSUPPORTED;
+      continue;
+    }
+    if (rc != fgvx::X_OK || p.c.key == fgvx::XK_UNDESERIALIZABLE) {
+      undeser.push_back(i);
+      continue;
+    }
+    // getUniqueValidationChain (oracle/msp.py MSP._chain)
+    if (p.c.is_ca) {
+      status[i] = FGV_RESOLVE_UNSUPPORTED;
+      continue;
+    }
+    const int64_t now = p.c.not_before + 1;
+    if (p.c.unhandled_critical || !(p.c.not_before <= now && now <= p.c.not_after)) {
+      undeser.push_back(i);
+      continue;
+    }
+    size_t nc = 0;
+    for (const Root &r : m->roots)
+      if (p.c.same_issuer_as_subject_of(r.c)) {
+        nc++;
+        p.root = &r;
+      }
+    if (nc > 1) {
+      status[i] = FGV_RESOLVE_UNSUPPORTED;
+      continue;
+    }
+    if (nc == 0) {
+      undeser.push_back(i);
+      continue;
+    }
+    // CheckSignatureFrom: the parent must be allowed to sign certificates
+    const fgvx::Cert &rc_ = p.root->c;
+    if ((rc_.version == 3 && !rc_.bc_valid) || (rc_.bc_valid && !rc_.is_ca) ||
+        (rc_.key_usage && !(rc_.key_usage & (1u << 5))) || !(rc_.not_before <= now && now <= rc_.not_after)) {
+      undeser.push_back(i);
+      continue;
+    }
+    pend.push_back(std::move(p));
+  }
+  // the CA signatures over the TBS certificates, one GPU pass (Go's ecdsa accepts high S: the
+  // engine's verifier takes the low-S equivalent)
+  std::vector<uint8_t> msgs, sigs, vst(pend.size(), 1);
+  std::vector<uint64_t> moff, soff;
+  std::vector<uint32_t> mlen, slen, slots;
+  std::vector<size_t> job(pend.size(), SIZE_MAX);
+  for (size_t k = 0; k < pend.size(); k++) {
+    const Pending &p = pend[k];
+    uint8_t r[32], s[32];
+    if (!fgvx::strict_sig(p.c.sig(), p.c.sig_len, r, s) || fgvx::is_zero(r) || fgvx::is_zero(s) || !fgvx::lt_n(r) ||
+        !fgvx::lt_n(s))
+      continue;  // the verify fails
+    fgvx::to_low_s(s);
+    const std::vector<uint8_t> low = fgvx::der_sig(r, s);
+    job[k] = moff.size();
+    moff.push_back(msgs.size());
+    msgs.insert(msgs.end(), p.c.tbs(), p.c.tbs() + p.c.tbs_len);
+    mlen.push_back((uint32_t)p.c.tbs_len);
+    soff.push_back(sigs.size());
+    sigs.insert(sigs.end(), low.begin(), low.end());
+    slen.push_back((uint32_t)low.size());
+    slots.push_back(p.root->slot);
+  }
+  std::vector<uint8_t> jst(moff.size(), 1);
+  if (!moff.empty()) {
+    const int rc = fgv_verify_msgs_slots_locked(c, msgs.data(), msgs.size(), moff.data(), mlen.data(), sigs.data(),
+                                                sigs.size(), soff.data(), slen.data(), slots.data(), moff.size(),
+                                                jst.data());
+    if (rc) return rc;
+  }
+  // register: verified identities with their Validate / role results, the rest undeserializable
+  std::vector<uint8_t> keys;
+  struct Reg {
+    size_t i;
+    fgv_identity_info info;
+  };
+  std::vector<Reg> regs;
+  for (size_t k = 0; k < pend.size(); k++) {
+    const Pending &p = pend[k];
+    if (job[k] == SIZE_MAX || jst[job[k]] != 0) {
+      undeser.push_back(p.i);
+      continue;
+    }
+    std::vector<uint8_t> raw2;
+    if (fgvx::sanitized_raw(p.c, raw2) != fgvx::X_OK) {
+      status[p.i] = FGV_RESOLVE_UNSUPPORTED;
+      continue;
+    }
+    const MspModel &m = *p.m;
+    Reg g{p.i, fgv_identity_info{}};
+    const Dig dg = sha(raw2);
+    memcpy(g.info.id_digest, dg.data(), 32);
+    // Validate: the signing CA's SKI, then the OUs (validateIdentityOUsV142)
+    bool valid = p.root->c.has_ski;
+    const Dig &cid = p.root->certifier;
+    if (valid && !m.ou_ids.empty()) {
+      bool any = false;
+      for (const std::string &o : p.c.ous) {
+        auto it = m.ou_ids.find(o);
+        if (it != m.ou_ids.end() && std::find(it->second.begin(), it->second.end(), cid) != it->second.end()) any = true;
+      }
+      valid = any;
+    }
+    if (valid && m.node_ous) {
+      int cnt = 0;
+      static const int order[4] = {R_CLIENT, R_PEER, R_ADMIN, R_ORDERER};  // (a later role's identical OU wins)
+      for (const std::string &o : p.c.ous) {
+        const RoleOU *hit = nullptr;
+        for (int r : order)
+          if (m.role_ou[r].present && m.role_ou[r].name == o) hit = &m.role_ou[r];
+        if (!hit) continue;
+        if (hit->has_cert && hit->cert != cid) {
+          valid = false;
+          break;
+        }
+        if (++cnt > 1) break;
+      }
+      if (cnt != 1) valid = false;
+    }
+    uint32_t roles = valid ? 1u : 0u;
+    const bool admin_listed = std::find(m.admins.begin(), m.admins.end(), raw2) != m.admins.end();
+    if (admin_listed || (valid && m.node_ous && m.has(R_ADMIN, p.c))) roles |= 1u << R_ADMIN;
+    for (int r : {R_CLIENT, R_PEER, R_ORDERER})
+      if (valid && m.node_ous && m.has(r, p.c)) roles |= 1u << r;
+    g.info.valid = valid;
+    g.info.roles = roles;
+    g.info.hash_family = m.sha3 ? FGV_HASH_SHA3 : FGV_HASH_SHA2;
+    g.info.key_type = p.c.key == fgvx::XK_P256 ? FGV_KEY_P256 : p.c.key == fgvx::XK_P384 ? FGV_KEY_P384 : FGV_KEY_OTHER;
+    if (g.info.key_type == FGV_KEY_P256) memcpy(g.info.pubkey, p.c.pub, 64);
+    regs.push_back(g);
+  }
+  // one key-table build for every new P-256 key
+  for (const Reg &g : regs)
+    if (g.info.key_type == FGV_KEY_P256) keys.insert(keys.end(), g.info.pubkey, g.info.pubkey + 64);
+  std::vector<uint32_t> kslots(keys.size() / 64);
+  if (!kslots.empty()) {
+    const int rc = fgv_keys_register_locked(c, keys.data(), kslots.size(), kslots.data());
+    if (rc) return rc;
+  }
+  size_t kq = 0, nreg = 0;
+  for (const Reg &g : regs) {
+    const int32_t slot = g.info.key_type == FGV_KEY_P256 ? (int32_t)kslots[kq++] : -1;
+    if (fgv_block_add_identity(c->blk, ser[g.i], lens[g.i], slot, &g.info) == FGV_OK) nreg++;
+    status[g.i] = FGV_RESOLVE_OK;
+  }
+  for (size_t i : undeser) {
+    fgv_identity_info info{};
+    info.key_type = FGV_KEY_UNDESERIALIZABLE;
+    info.roles = 0;
+    if (fgv_block_add_identity(c->blk, ser[i], lens[i], -1, &info) == FGV_OK) nreg++;
+    status[i] = FGV_RESOLVE_FAILED;
+  }
+  if (registered) *registered = nreg;
+  return FGV_OK;
+}
+
+// the misses a batch of blocks names (fgv_block_misses), resolved; c->mu held
+int fgv_msp_resolve_blocks_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                  size_t *registered) {
+  if (registered) *registered = 0;
+  std::vector<std::string> miss;
+  fgv_block_misses(c->blk, nblocks, blocks, lens, miss);
+  if (miss.empty()) return FGV_OK;
+  std::vector<const uint8_t *> p(miss.size());
+  std::vector<size_t> l(miss.size());
+  for (size_t i = 0; i < miss.size(); i++) {
+    p[i] = reinterpret_cast<const uint8_t *>(miss[i].data());
+    l[i] = miss[i].size();
+  }
+  std::vector<int> st(miss.size());
+  return fgv_msp_resolve_locked(c, miss.size(), p.data(), l.data(), st.data(), registered);
+}
+
+bool fgv_msp_auto(fgv_ctx *c) { return !c->msp || c->msp->auto_resolve; }
+
+extern "C" {
+
+int fgv_msp_resolve(fgv_ctx *c, size_t n, const uint8_t *const *serialized, const size_t *lens, int *status) {
+  if (!c || (n && (!serialized || !lens || !status))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_msp_resolve_locked(c, n, serialized, lens, status, nullptr);
+}
+
+int fgv_msp_resolve_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                           size_t *registered) {
+  if (!c || (nblocks && (!blocks || !lens))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_msp_resolve_blocks_locked(c, nblocks, blocks, lens, registered);
+}
+
+int fgv_set_auto_resolve(fgv_ctx *c, int on) {
+  if (!c) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->msp) c->msp = new fgv_msp_cache();
+  c->msp->auto_resolve = on != 0;
+  return FGV_OK;
+}
+
+int fgv_msp_identity(fgv_ctx *c, const uint8_t *serialized, size_t len, fgv_identity_info *out) {
+  if (!c || !serialized || !out) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  Channel &ch = fgv_block_channel(c->blk);
+  if (ch.dirty) ch.compile();
+  fgvb::VSerializedIdentity sid;
+  if (!pbw::decode(serialized, len, sid)) return FGV_ESTATE;
+  uint64_t h = fgvb::hash_bytes(sid.mspid.p, sid.mspid.n);
+  h = fgvb::hash_bytes(sid.id_bytes.p, sid.id_bytes.n, h ^ 0xA5);
+  auto range = ch.ident_index.equal_range(h);
+  for (auto it = range.first; it != range.second; ++it) {
+    const Ident &I = ch.idents[it->second];
+    if (!sid.mspid.eq(I.mspid.data(), I.mspid.size()) || !sid.id_bytes.eq(I.id_bytes.data(), I.id_bytes.size()))
+      continue;
+    *out = fgv_identity_info{};
+    out->key_type = I.kind;
+    out->hash_family = I.hash3 ? FGV_HASH_SHA3 : FGV_HASH_SHA2;
+    out->valid = I.valid;
+    out->roles = I.roles_known ? I.roles : FGV_ROLES_UNKNOWN;
+    memcpy(out->pubkey, I.pub, 64);
+    memcpy(out->id_digest, I.digest, 32);
+    return FGV_OK;
+  }
+  return FGV_ESTATE;
+}
+
+}  // extern "C"

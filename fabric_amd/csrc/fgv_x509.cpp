@@ -1,0 +1,642 @@
+// fgv_x509.cpp -- X.509 subset of the MSP cache-miss path (see fgv_x509.h).
+// Go 1.21 crypto/x509 ParseCertificate / encoding/asn1 / encoding/pem, restricted to the shapes
+// Fabric CAs issue; the oracle's restatement of the same rules is oracle/x509.py.
+#include "fgv_x509.h"
+
+#include <string.h>
+#include <time.h>
+
+#include <algorithm>
+
+#include "pbwire.h"
+
+namespace fgvx {
+namespace {
+
+struct XErr {
+  int code;
+};
+[[noreturn]] void perr() { throw XErr{X_PARSE}; }
+[[noreturn]] void unsup() { throw XErr{X_UNSUP}; }
+
+struct T {  // one DER element
+  uint8_t tag;
+  size_t hs, cs, ce;  // header start, content start, content end
+};
+
+// strict definite-length DER header at b[i..end)
+T tlv(const uint8_t *b, size_t i, size_t end) {
+  if (i + 2 > end) perr();
+  const uint8_t tag = b[i];
+  if ((tag & 0x1F) == 0x1F) perr();
+  size_t ln = b[i + 1], o = i + 2;
+  if (ln & 0x80) {
+    const size_t nb = ln & 0x7F;
+    if (nb == 0 || nb > 4 || o + nb > end) perr();
+    if (b[o] == 0) perr();
+    ln = 0;
+    for (size_t k = 0; k < nb; k++) ln = (ln << 8) | b[o + k];
+    if (ln < 128) perr();
+    o += nb;
+  }
+  if (ln > end - o) perr();
+  return T{tag, i, o, o + ln};
+}
+
+std::vector<T> children(const uint8_t *b, size_t s, size_t e) {
+  std::vector<T> out;
+  while (s < e) {
+    out.push_back(tlv(b, s, e));
+    s = out.back().ce;
+  }
+  return out;
+}
+
+bool eq(const uint8_t *b, const T &t, const char *hex_bytes, size_t n) {
+  return t.ce - t.cs == n && memcmp(b + t.cs, hex_bytes, n) == 0;
+}
+
+#define OIDV(name, ...) const char name[] = {__VA_ARGS__}
+OIDV(OID_EC_KEY, '\x2a', '\x86', '\x48', '\xce', '\x3d', '\x02', '\x01');
+OIDV(OID_P256, '\x2a', '\x86', '\x48', '\xce', '\x3d', '\x03', '\x01', '\x07');
+OIDV(OID_ED25519, '\x2b', '\x65', '\x70');
+OIDV(OID_OU, '\x55', '\x04', '\x0b');
+#undef OIDV
+// AlgorithmIdentifier{ecdsa-with-SHA256} with no parameters
+const uint8_t ALG_ECDSA_SHA256[12] = {0x30, 0x0a, 0x06, 0x08, 0x2a, 0x86, 0x48, 0xce, 0x3d, 0x04, 0x03, 0x02};
+
+// id-ce-* extension (2.5.29.x) number, or -1
+int ce_ext(const uint8_t *b, const T &t) {
+  if (t.ce - t.cs == 3 && b[t.cs] == 0x55 && b[t.cs + 1] == 0x1d) return b[t.cs + 2];
+  return -1;
+}
+const uint8_t OID_AIA[8] = {0x2b, 0x06, 0x01, 0x05, 0x05, 0x07, 0x01, 0x01};
+
+// cryptobyte ReadASN1ObjectIdentifier: non-empty, every subidentifier minimal (no leading 0x80),
+// at most 5 bytes and below 2^31, none truncated
+bool valid_oid(const uint8_t *b, size_t n) {
+  if (n == 0) return false;
+  size_t i = 0;
+  while (i < n) {
+    uint32_t ret = 0;
+    for (int k = 0;; k++) {
+      if (k == 5 || i >= n || ret >= (1u << 24)) return false;
+      const uint8_t c = b[i++];
+      if (k == 0 && c == 0x80) return false;
+      ret = (ret << 7) | (c & 0x7F);
+      if (!(c & 0x80)) break;
+    }
+  }
+  return true;
+}
+bool valid_oid(const uint8_t *b, const T &t) { return t.tag == 0x06 && valid_oid(b + t.cs, t.ce - t.cs); }
+
+// minimal two's-complement INTEGER content: false if empty / non-minimal
+bool int_minimal(const uint8_t *b, size_t s, size_t e) {
+  if (e == s) return false;
+  if (e - s > 1 && ((b[s] == 0 && b[s + 1] < 0x80) || (b[s] == 0xFF && b[s + 1] >= 0x80))) return false;
+  return true;
+}
+
+int64_t days_from_civil(int64_t y, unsigned m, unsigned d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = (unsigned)(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + (int64_t)doe - 719468;
+}
+
+int64_t parse_time(const uint8_t *b, const T &t) {
+  const size_t n = t.ce - t.cs;
+  const uint8_t *v = b + t.cs;
+  auto digits = [&](size_t k) {
+    for (size_t i = 0; i < k; i++)
+      if (v[i] < '0' || v[i] > '9') return false;
+    return true;
+  };
+  auto two = [](const uint8_t *p) { return (p[0] - '0') * 10 + (p[1] - '0'); };
+  int64_t y;
+  const uint8_t *rest;
+  if (t.tag == 0x17 && n == 13 && v[12] == 'Z' && digits(12)) {
+    const int yy = two(v);
+    y = yy >= 50 ? 1900 + yy : 2000 + yy;
+    rest = v + 2;
+  } else if (t.tag == 0x18 && n == 15 && v[14] == 'Z' && digits(14)) {
+    y = two(v) * 100 + two(v + 2);
+    rest = v + 4;
+  } else {
+    unsup();
+  }
+  const int mo = two(rest), d = two(rest + 2), hh = two(rest + 4), mm = two(rest + 6), ss = two(rest + 8);
+  static const int mdays[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+  if (!(mo >= 1 && mo <= 12)) perr();
+  const int dim = mdays[mo - 1] + (mo == 2 && leap ? 1 : 0);
+  if (!(d >= 1 && d <= dim && hh < 24 && mm < 60 && ss < 60)) perr();  // (time.Parse: day out of range)
+  return days_from_civil(y, (unsigned)mo, 1) * 86400 + (int64_t)(d - 1) * 86400 + hh * 3600 + mm * 60 + ss;
+}
+
+std::string name_string(const uint8_t *b, const T &t) {
+  const uint8_t *p = b + t.cs;
+  const size_t n = t.ce - t.cs;
+  if (t.tag == 0x0C) {
+    if (!pbw::utf8_valid(p, n)) perr();
+  } else if (t.tag == 0x13) {
+    for (size_t i = 0; i < n; i++) {
+      const uint8_t c = p[i];
+      const bool ok = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') ||
+                      (c && strchr(" '()+,-./:=?*&", c));
+      if (!ok) perr();
+    }
+  } else if (t.tag == 0x16) {
+    for (size_t i = 0; i < n; i++)
+      if (p[i] >= 0x80) perr();
+  } else if (t.tag == 0x12 || t.tag == 0x14 || t.tag == 0x1E) {  // Numeric, T61, BMP: not restated
+    unsup();
+  } else {
+    perr();  // parseASN1String: unsupported string type
+  }
+  return std::string((const char *)p, n);
+}
+
+void name_ous(const uint8_t *b, const T &name, std::vector<std::string> *out) {
+  for (const T &rdn : children(b, name.cs, name.ce)) {
+    if (rdn.tag != 0x31) perr();
+    for (const T &atv : children(b, rdn.cs, rdn.ce)) {
+      if (atv.tag != 0x30) perr();
+      // parseName reads the type and the value; anything after them is not read
+      const T t1 = tlv(b, atv.cs, atv.ce);
+      if (!valid_oid(b, t1)) perr();
+      const T t2 = tlv(b, t1.ce, atv.ce);
+      std::string s = name_string(b, t2);  // every attribute value parses
+      if (out && eq(b, t1, OID_OU, sizeof OID_OU)) out->push_back(std::move(s));
+    }
+  }
+}
+
+bool der_bool(const uint8_t *b, const T &t) {
+  if (t.ce - t.cs != 1 || (b[t.cs] != 0x00 && b[t.cs] != 0xFF)) perr();
+  return b[t.cs] == 0xFF;
+}
+
+void parse(Cert &c) {
+  const uint8_t *b = c.der.data();
+  const size_t n = c.der.size();
+  const T top = tlv(b, 0, n);
+  if (top.tag != 0x30 || top.ce != n) perr();
+  const std::vector<T> k3 = children(b, top.cs, top.ce);
+  if (k3.size() != 3 || k3[0].tag != 0x30 || k3[1].tag != 0x30 || k3[2].tag != 0x03) perr();
+  const T &tbs = k3[0], &oalg = k3[1], &sigb = k3[2];
+  c.tbs_off = tbs.hs;
+  c.tbs_len = tbs.ce - tbs.hs;
+  if (sigb.ce == sigb.cs || b[sigb.cs] != 0) unsup();
+  c.sig_off = sigb.cs + 1;
+  c.sig_len = sigb.ce - sigb.cs - 1;
+  const std::vector<T> f = children(b, tbs.cs, tbs.ce);
+  size_t i = 0;
+  int version = 0;
+  if (!f.empty() && f[0].tag == 0xA0) {
+    const std::vector<T> vk = children(b, f[0].cs, f[0].ce);
+    if (vk.size() != 1 || vk[0].tag != 0x02 || !int_minimal(b, vk[0].cs, vk[0].ce)) perr();
+    version = (vk[0].ce - vk[0].cs == 1) ? (int8_t)b[vk[0].cs] : -1;
+    i = 1;
+  }
+  if (version != 2) unsup();
+  c.version = 3;
+  if (f.size() < i + 6) perr();
+  const T &serial = f[i], &alg = f[i + 1], &issuer = f[i + 2], &validity = f[i + 3], &subject = f[i + 4],
+          &spki = f[i + 5];
+  if (serial.tag != 0x02 || !int_minimal(b, serial.cs, serial.ce)) perr();
+  if (alg.ce - alg.hs != oalg.ce - oalg.hs || memcmp(b + alg.hs, b + oalg.hs, alg.ce - alg.hs)) perr();
+  if (oalg.ce - oalg.hs != sizeof ALG_ECDSA_SHA256 || memcmp(b + oalg.hs, ALG_ECDSA_SHA256, sizeof ALG_ECDSA_SHA256))
+    unsup();
+  const std::vector<T> vk = children(b, validity.cs, validity.ce);
+  if (vk.size() != 2) perr();
+  c.not_before = parse_time(b, vk[0]);
+  c.not_after = parse_time(b, vk[1]);
+  if (issuer.tag != 0x30 || subject.tag != 0x30) perr();
+  name_ous(b, subject, &c.ous);
+  name_ous(b, issuer, nullptr);
+  c.issuer_off = issuer.hs;
+  c.issuer_len = issuer.ce - issuer.hs;
+  c.subject_off = subject.hs;
+  c.subject_len = subject.ce - subject.hs;
+  // public key
+  const std::vector<T> sk = children(b, spki.cs, spki.ce);
+  if (sk.size() != 2 || sk[0].tag != 0x30 || sk[1].tag != 0x03) perr();
+  const std::vector<T> ak = children(b, sk[0].cs, sk[0].ce);
+  if (ak.empty() || !valid_oid(b, ak[0])) perr();  // malformed public key algorithm identifier
+  c.key = XK_OTHER;
+  if (eq(b, ak[0], OID_EC_KEY, sizeof OID_EC_KEY)) {
+    const bool curve = ak.size() == 2 && ak[1].tag == 0x06;
+    if (curve && eq(b, ak[1], OID_P256, sizeof OID_P256)) {
+      const uint8_t *bits = b + sk[1].cs;
+      const size_t bl = sk[1].ce - sk[1].cs;
+      if (bl != 66 || bits[0] != 0 || bits[1] != 4) unsup();
+      if (!p256_on_curve(bits + 2, bits + 34)) perr();
+      memcpy(c.pub, bits + 2, 64);
+      c.key = XK_P256;
+    } else {  // (P-384: Go checks the point on the curve -- not restated; no GPU verify either)
+      unsup();
+    }
+  } else if (eq(b, ak[0], OID_ED25519, sizeof OID_ED25519)) {
+    c.key = XK_UNDESERIALIZABLE;
+  } else {  // (RSA: Go's PKCS#1 key checks are not restated)
+    unsup();
+  }
+  // extensions
+  struct Ext {
+    int id;
+    T val;
+    bool crit;
+  };
+  std::vector<Ext> exts;
+  std::vector<std::vector<uint8_t>> seen;
+  for (size_t r = i + 6; r < f.size(); r++) {
+    if (f[r].tag == 0x81 || f[r].tag == 0x82) unsup();
+    if (f[r].tag != 0xA3) perr();
+    const std::vector<T> ek = children(b, f[r].cs, f[r].ce);
+    if (ek.size() != 1 || ek[0].tag != 0x30) perr();
+    for (const T &e : children(b, ek[0].cs, ek[0].ce)) {
+      const std::vector<T> ef = children(b, e.cs, e.ce);
+      if (e.tag != 0x30 || ef.empty() || !valid_oid(b, ef[0])) perr();
+      bool crit = false;
+      size_t j = 1;
+      if (ef.size() > j && ef[j].tag == 0x01) {
+        crit = der_bool(b, ef[j]);
+        j++;
+      }
+      if (ef.size() != j + 1 || ef[j].tag != 0x04) perr();
+      std::vector<uint8_t> oid(b + ef[0].cs, b + ef[0].ce);
+      if (std::find(seen.begin(), seen.end(), oid) != seen.end()) perr();
+      seen.push_back(oid);
+      const int id = ce_ext(b, ef[0]);
+      // extensions Go parses that this restatement does not: name constraints (30), CRL
+      // distribution points (31), certificate policies (32), AIA, freshest CRL (46)
+      if (id == 30 || id == 31 || id == 32 || id == 46 ||
+          (oid.size() == sizeof OID_AIA && memcmp(oid.data(), OID_AIA, sizeof OID_AIA) == 0))
+        unsup();
+      if (id == 14 || id == 15 || id == 17 || id == 19 || id == 35 || id == 37) {
+        exts.push_back(Ext{id, ef[j], crit});
+      } else if (crit) {
+        c.unhandled_critical = true;
+      }
+    }
+  }
+  for (const Ext &x : exts) {
+    const uint8_t *v = b + x.val.cs;
+    const size_t vn = x.val.ce - x.val.cs;
+    const T t = tlv(v, 0, vn);
+    if (x.id == 19) {  // basicConstraints
+      if (t.tag != 0x30 || t.ce != vn) perr();
+      std::vector<T> k = children(v, t.cs, t.ce);
+      size_t a = 0;
+      if (!k.empty() && k[0].tag == 0x01) {
+        c.is_ca = der_bool(v, k[0]);
+        a = 1;
+      }
+      if (k.size() > a && (k[a].tag != 0x02 || k.size() - a > 1)) perr();
+      c.bc_valid = true;
+    } else if (x.id == 14) {  // subjectKeyIdentifier
+      if (t.tag != 0x04 || t.ce != vn) perr();
+      c.has_ski = true;
+    } else if (x.id == 15) {  // keyUsage
+      // cryptobyte ReadASN1BitString, then parseKeyUsageExtension's first 9 bits
+      if (t.tag != 0x03 || t.ce != vn || t.ce == t.cs || v[t.cs] > 7 || (t.ce - t.cs == 1 && v[t.cs]) ||
+          (v[t.ce - 1] & ((1u << v[t.cs]) - 1)))
+        perr();
+      uint32_t ku = 0;
+      for (size_t q = t.cs + 1, kk = 0; q < t.ce; q++, kk++)
+        for (int bit = 0; bit < 8; bit++)
+          if (v[q] & (0x80 >> bit) && 8 * kk + bit < 9) ku |= 1u << (8 * kk + bit);
+      c.key_usage = ku;
+    } else {  // authorityKeyIdentifier, extKeyUsage, subjectAltName
+      if (t.tag != 0x30 || t.ce != vn) perr();
+      int names = 0;
+      for (const T &k : children(v, t.cs, t.ce)) {
+        if (x.id == 37 && !valid_oid(v, k)) perr();  // invalid extended key usages
+        if (x.id == 17) {  // parseSANExtension (by tag ^ 0x80)
+          if (k.tag == 0x81 || k.tag == 0x82)
+            for (size_t q = k.cs; q < k.ce; q++)
+              if (v[q] >= 0x80) perr();  // rfc822Name / dNSName malformed
+          if (k.tag == 0x86) unsup();  // URI (url.Parse not restated)
+          if (k.tag == 0x87 && k.ce - k.cs != 4 && k.ce - k.cs != 16) perr();
+          names += k.tag == 0x81 || k.tag == 0x82 || k.tag == 0x87;
+        }
+      }
+      if (x.id == 17 && !names && x.crit) c.unhandled_critical = true;  // (nothing parsed)
+    }
+  }
+}
+
+// ---- P-256 field arithmetic for the on-curve check (4 x 64-bit limbs, little-endian) ----
+typedef unsigned __int128 u128;
+struct U256 {
+  uint64_t w[4];
+};
+const U256 P = {{0xFFFFFFFFFFFFFFFFull, 0x00000000FFFFFFFFull, 0x0000000000000000ull, 0xFFFFFFFF00000001ull}};
+const U256 Bc = {{0x3BCE3C3E27D2604Bull, 0x651D06B0CC53B0F6ull, 0xB3EBBD55769886BCull, 0x5AC635D8AA3A93E7ull}};
+const U256 N = {{0xF3B9CAC2FC632551ull, 0xBCE6FAADA7179E84ull, 0xFFFFFFFFFFFFFFFFull, 0xFFFFFFFF00000000ull}};
+const U256 NH = {{0x79DCE5617E3192A8ull, 0xDE737D56D38BCF42ull, 0x7FFFFFFFFFFFFFFFull, 0x7FFFFFFF80000000ull}};
+
+U256 from_be(const uint8_t *p) {
+  U256 r;
+  for (int i = 0; i < 4; i++) {
+    uint64_t v = 0;
+    for (int k = 0; k < 8; k++) v = (v << 8) | p[(3 - i) * 8 + k];
+    r.w[i] = v;
+  }
+  return r;
+}
+void to_be(const U256 &a, uint8_t *p) {
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 8; k++) p[(3 - i) * 8 + k] = (uint8_t)(a.w[i] >> (56 - 8 * k));
+}
+int cmp(const U256 &a, const U256 &b) {
+  for (int i = 3; i >= 0; i--)
+    if (a.w[i] != b.w[i]) return a.w[i] < b.w[i] ? -1 : 1;
+  return 0;
+}
+uint64_t sub(U256 &r, const U256 &a, const U256 &b) {
+  uint64_t br = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 d = (u128)a.w[i] - b.w[i] - br;
+    r.w[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+  return br;
+}
+uint64_t add(U256 &r, const U256 &a, const U256 &b) {
+  uint64_t c = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 s = (u128)a.w[i] + b.w[i] + c;
+    r.w[i] = (uint64_t)s;
+    c = (uint64_t)(s >> 64);
+  }
+  return c;
+}
+U256 addm(const U256 &a, const U256 &b) {
+  U256 r;
+  const uint64_t c = add(r, a, b);
+  if (c || cmp(r, P) >= 0) sub(r, r, P);
+  return r;
+}
+U256 subm(const U256 &a, const U256 &b) {
+  U256 r;
+  if (sub(r, a, b)) add(r, r, P);
+  return r;
+}
+// a*b mod p by double-and-add over b's bits (host check, a few microseconds)
+U256 mulm(const U256 &a, const U256 &b) {
+  U256 r = {{0, 0, 0, 0}};
+  for (int i = 255; i >= 0; i--) {
+    r = addm(r, r);
+    if ((b.w[i / 64] >> (i % 64)) & 1) r = addm(r, a);
+  }
+  return r;
+}
+
+}  // namespace
+
+int pem_decode(const uint8_t *p, size_t n, std::vector<uint8_t> &der) {
+  const std::string s((const char *)p, n);
+  const size_t i = s.find("-----BEGIN ");
+  if (i == std::string::npos) return X_PARSE;
+  const size_t j = s.find("-----", i + 11);
+  if (j == std::string::npos) return X_PARSE;
+  const std::string end_tag = "-----END " + s.substr(i + 11, j - (i + 11)) + "-----";
+  const size_t k = s.find(end_tag, j);
+  if (k == std::string::npos) return X_PARSE;
+  // body lines, stripped of whitespace (Python bytes.strip: space \t \n \r \x0b \x0c)
+  std::string b64;
+  bool colon = false;
+  size_t a = j + 5;
+  while (a < k) {
+    size_t e = s.find('\n', a);
+    if (e == std::string::npos || e > k) e = k;
+    size_t x = a, y = e;
+    auto ws = [](char ch) { return ch == ' ' || ch == '\t' || ch == '\n' || ch == '\r' || ch == '\x0b' || ch == '\x0c'; };
+    while (x < y && ws(s[x])) x++;
+    while (y > x && ws(s[y - 1])) y--;
+    if (y > x) {
+      const std::string ln = s.substr(x, y - x);
+      if (ln.find(':') != std::string::npos) colon = true;
+      b64 += ln;
+    }
+    a = e + 1;
+  }
+  if (colon) return X_UNSUP;
+  // strict base64 (validate=True): alphabet A-Za-z0-9+/, padding only at the end, length % 4 == 0
+  if (b64.size() % 4) return X_PARSE;
+  der.clear();
+  der.reserve(b64.size() / 4 * 3);
+  auto val = [](char ch) -> int {
+    if (ch >= 'A' && ch <= 'Z') return ch - 'A';
+    if (ch >= 'a' && ch <= 'z') return ch - 'a' + 26;
+    if (ch >= '0' && ch <= '9') return ch - '0' + 52;
+    if (ch == '+') return 62;
+    if (ch == '/') return 63;
+    return -1;
+  };
+  for (size_t q = 0; q < b64.size(); q += 4) {
+    int v[4], pad = 0;
+    for (int t = 0; t < 4; t++) {
+      const char ch = b64[q + t];
+      if (ch == '=') {
+        if (q + 4 != b64.size() || t < 2) return X_PARSE;
+        v[t] = 0;
+        pad++;
+      } else {
+        if (pad) return X_PARSE;
+        v[t] = val(ch);
+        if (v[t] < 0) return X_PARSE;
+      }
+    }
+    const uint32_t w = (uint32_t)v[0] << 18 | (uint32_t)v[1] << 12 | (uint32_t)v[2] << 6 | (uint32_t)v[3];
+    der.push_back((uint8_t)(w >> 16));
+    if (pad < 2) der.push_back((uint8_t)(w >> 8));
+    if (pad < 1) der.push_back((uint8_t)w);
+  }
+  return X_OK;
+}
+
+int parse_certificate(std::vector<uint8_t> der, Cert &c) {
+  c = Cert();
+  c.der = std::move(der);
+  try {
+    parse(c);
+  } catch (const XErr &e) {
+    return e.code;
+  }
+  return X_OK;
+}
+
+bool strict_sig(const uint8_t *sig, size_t n, uint8_t r[32], uint8_t s[32]) {
+  try {
+    const T t = tlv(sig, 0, n);
+    if (t.tag != 0x30 || t.ce != n) return false;
+    const std::vector<T> k = children(sig, t.cs, t.ce);
+    if (k.size() != 2 || k[0].tag != 0x02 || k[1].tag != 0x02) return false;
+    uint8_t *out[2] = {r, s};
+    for (int q = 0; q < 2; q++) {
+      size_t a = k[q].cs, e = k[q].ce;
+      if (!int_minimal(sig, a, e)) return false;
+      if (sig[a] & 0x80) return false;  // negative: outside (0, n)
+      if (sig[a] == 0) a++;
+      if (e - a > 32) return false;
+      memset(out[q], 0, 32);
+      memcpy(out[q] + 32 - (e - a), sig + a, e - a);
+    }
+    return true;
+  } catch (const XErr &) {
+    return false;
+  }
+}
+
+static void put_len(std::vector<uint8_t> &o, size_t n) {
+  if (n < 128) {
+    o.push_back((uint8_t)n);
+  } else if (n < 256) {
+    o.push_back(0x81);
+    o.push_back((uint8_t)n);
+  } else if (n < 65536) {
+    o.push_back(0x82);
+    o.push_back((uint8_t)(n >> 8));
+    o.push_back((uint8_t)n);
+  } else {
+    o.push_back(0x83);
+    o.push_back((uint8_t)(n >> 16));
+    o.push_back((uint8_t)(n >> 8));
+    o.push_back((uint8_t)n);
+  }
+}
+
+static void put_int(std::vector<uint8_t> &o, const uint8_t v[32]) {
+  size_t a = 0;
+  while (a < 31 && v[a] == 0) a++;
+  const bool pad = v[a] & 0x80;
+  o.push_back(0x02);
+  put_len(o, 32 - a + pad);
+  if (pad) o.push_back(0);
+  o.insert(o.end(), v + a, v + 32);
+}
+
+std::vector<uint8_t> der_sig(const uint8_t r[32], const uint8_t s[32]) {
+  std::vector<uint8_t> body;
+  put_int(body, r);
+  put_int(body, s);
+  std::vector<uint8_t> o{0x30};
+  put_len(o, body.size());
+  o.insert(o.end(), body.begin(), body.end());
+  return o;
+}
+
+bool lt_n(const uint8_t v[32]) { return cmp(from_be(v), N) < 0; }
+
+bool is_zero(const uint8_t v[32]) {
+  for (int i = 0; i < 32; i++)
+    if (v[i]) return false;
+  return true;
+}
+
+bool to_low_s(uint8_t s[32]) {
+  const U256 v = from_be(s);
+  if (cmp(v, NH) <= 0) return false;
+  U256 r;
+  sub(r, N, v);
+  to_be(r, s);
+  return true;
+}
+
+int sanitized_raw(const Cert &c, std::vector<uint8_t> &out) {
+  uint8_t r[32], s[32];
+  std::vector<uint8_t> sig;
+  // (a strict parse with r or s wider than 256 bits or negative: outside the model)
+  if (!strict_sig(c.sig(), c.sig_len, r, s) || is_zero(r) || is_zero(s) || !lt_n(r) || !lt_n(s)) return X_UNSUP;
+  if (to_low_s(s)) {
+    sig = der_sig(r, s);
+  } else {
+    sig.assign(c.sig(), c.sig() + c.sig_len);
+  }
+  std::vector<uint8_t> body(c.tbs(), c.tbs() + c.tbs_len);
+  body.insert(body.end(), ALG_ECDSA_SHA256, ALG_ECDSA_SHA256 + sizeof ALG_ECDSA_SHA256);
+  body.push_back(0x03);
+  put_len(body, sig.size() + 1);
+  body.push_back(0);
+  body.insert(body.end(), sig.begin(), sig.end());
+  out.assign(1, 0x30);
+  put_len(out, body.size());
+  out.insert(out.end(), body.begin(), body.end());
+  return X_OK;
+}
+
+bool p256_on_curve(const uint8_t xb[32], const uint8_t yb[32]) {
+  const U256 x = from_be(xb), y = from_be(yb);
+  if (cmp(x, P) >= 0 || cmp(y, P) >= 0) return false;
+  const U256 y2 = mulm(y, y);
+  const U256 x3 = mulm(mulm(x, x), x);
+  const U256 t3 = addm(addm(x, x), x);
+  const U256 rhs = addm(subm(x3, t3), Bc);
+  return cmp(y2, rhs) == 0;
+}
+
+}  // namespace fgvx
+
+// ---- CPU probe for the parity tests (tests/test_x509_parity.py) and the sanitizer harness: a
+// PEM certificate through pem_decode -> parse_certificate -> sanitized_raw, the fields the MSP
+// path reads as one JSON object (no GPU call)
+#include <stdio.h>
+
+#include "sha256_host.h"
+
+static std::string hex(const uint8_t *p, size_t n) {
+  static const char *d = "0123456789abcdef";
+  std::string s(2 * n, '0');
+  for (size_t i = 0; i < n; i++) s[2 * i] = d[p[i] >> 4], s[2 * i + 1] = d[p[i] & 15];
+  return s;
+}
+
+extern "C" int fgv_x509_probe(const uint8_t *pem, size_t n, char *out, size_t cap) {
+  using namespace fgvx;
+  std::vector<uint8_t> der;
+  std::string j;
+  int st = pem_decode(pem, n, der);
+  if (st != X_OK) {
+    j = "{\"stage\":\"pem\",\"status\":" + std::to_string(st) + "}";
+  } else {
+    Cert c;
+    st = parse_certificate(der, c);
+    if (st != X_OK) {
+      j = "{\"stage\":\"parse\",\"status\":" + std::to_string(st) + "}";
+    } else {
+      uint8_t h[32];
+      std::vector<uint8_t> raw2;
+      const int rs = sanitized_raw(c, raw2);
+      j = "{\"stage\":\"ok\",\"status\":0,\"key\":" + std::to_string(c.key) + ",\"version\":" +
+          std::to_string(c.version) + ",\"is_ca\":" + std::to_string(c.is_ca) + ",\"bc_valid\":" +
+          std::to_string(c.bc_valid) + ",\"has_ski\":" + std::to_string(c.has_ski) + ",\"key_usage\":" +
+          std::to_string(c.key_usage) + ",\"unhandled_critical\":" + std::to_string(c.unhandled_critical) +
+          ",\"not_before\":" + std::to_string(c.not_before) + ",\"not_after\":" + std::to_string(c.not_after) +
+          ",\"pub\":\"" + (c.key == XK_P256 ? hex(c.pub, 64) : std::string()) + "\"";
+      fgvsha::sha256(c.tbs(), c.tbs_len, h);
+      j += ",\"tbs\":\"" + hex(h, 32) + "\"";
+      fgvsha::sha256(c.der.data() + c.issuer_off, c.issuer_len, h);
+      j += ",\"issuer\":\"" + hex(h, 32) + "\"";
+      fgvsha::sha256(c.der.data() + c.subject_off, c.subject_len, h);
+      j += ",\"subject\":\"" + hex(h, 32) + "\"";
+      j += ",\"sig\":\"" + hex(c.sig(), c.sig_len) + "\"";
+      j += ",\"raw2_status\":" + std::to_string(rs);
+      if (rs == X_OK) {
+        fgvsha::sha256(raw2.data(), raw2.size(), h);
+        j += ",\"raw2\":\"" + hex(h, 32) + "\"";
+      }
+      j += ",\"ous\":[";
+      for (size_t i = 0; i < c.ous.size(); i++) j += (i ? ",\"" : "\"") + hex((const uint8_t *)c.ous[i].data(), c.ous[i].size()) + "\"";
+      j += "]}";
+    }
+  }
+  if (j.size() + 1 > cap) return -1;
+  memcpy(out, j.c_str(), j.size() + 1);
+  return (int)j.size();
+}

@@ -175,6 +175,33 @@ int fgv_collection_define(fgv_ctx *ctx, const char *ns, const char *collection, 
                           size_t len);
 int fgv_ledger_add_txids(fgv_ctx *ctx, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
                          size_t n);
+/* The MSP cache miss (msp/cache/cache.go:65-83 -> the channel MSP's DeserializeIdentity,
+ * Validate and SatisfiesPrincipal; msp/mspimpl.go:398-422, identities.go:48-84,
+ * mspimpl.go:892-938, mspimplvalidate.go): identities of a channel MSP (from fgv_channel_config's
+ * FabricMSPConfig: root CAs, OU identifiers, NodeOUs, admins) that were never registered are
+ * deserialized here -- PEM, X.509 parse, the chain to a root (the CA signatures verified on the
+ * GPU, one pass per call), sanitizeCert's low-S re-marshal, Id = SHA-256 of it, Validate's SKI /
+ * OU rules and the role bits -- and registered like fgv_msp_register_identity (one that fails
+ * DeserializeIdentity is registered as FGV_KEY_UNDESERIALIZABLE).  Modelled MSPs: root CAs only
+ * (no intermediates, no CRLs), OU certificates that are roots, ECDSA P-256 / Ed25519 leaf keys.
+ *   fgv_msp_resolve        -- n SerializedIdentity bytes -> status[i] FGV_RESOLVE_*
+ *   fgv_msp_resolve_blocks -- every creator / endorser of the blocks the registry lacks;
+ *                             *registered = identities added (NULL allowed)
+ *   fgv_set_auto_resolve   -- the validate calls (fgv_validate_blocks*, fgv_validate_shard*,
+ *                             fgv_group_validate_blocks, fgv_blocks_verify_signed) resolve a
+ *                             batch's misses and run it once more instead of returning
+ *                             FGV_EUNSUPPORTED for them; on by default
+ *   fgv_msp_identity       -- the registry's record of one identity (FGV_ESTATE: none) */
+#define FGV_RESOLVE_KNOWN 0       /* registered already, or not an identity of a channel MSP    */
+#define FGV_RESOLVE_OK 1          /* deserialized and registered (valid or not: see Validate)   */
+#define FGV_RESOLVE_FAILED 2      /* DeserializeIdentity fails: registered as undeserializable  */
+#define FGV_RESOLVE_UNSUPPORTED 3 /* outside the modelled MSP / certificate shapes: left out     */
+#define FGV_RESOLVE_REPEAT 4      /* the same bytes earlier in this call                        */
+int fgv_msp_resolve(fgv_ctx *ctx, size_t n, const uint8_t *const *serialized, const size_t *lens, int *status);
+int fgv_msp_resolve_blocks(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                           size_t *registered);
+int fgv_set_auto_resolve(fgv_ctx *ctx, int on);
+int fgv_msp_identity(fgv_ctx *ctx, const uint8_t *serialized, size_t len, fgv_identity_info *out);
 /* Round-1 forms: fgv_msp_add_identity = register with FGV_KEY_P256 (pubkey64 != NULL) or
  * FGV_KEY_OTHER, SHA2, FGV_ROLES_UNKNOWN; fgv_chaincode_define = fgv_chaincode_define2 with
  * plugin "vscc", flags 0. */

@@ -146,6 +146,7 @@ S = {
     "MSPConfig": {1: ("type", "int32"), 2: ("config", "bytes")},
     "FabricMSPConfig": {1: ("name", "string"), 2: ("root_certs", "rep bytes"), 3: ("intermediate_certs", "rep bytes"),
                         4: ("admins", "rep bytes"), 5: ("revocation_list", "rep bytes"),
+                        7: ("organizational_unit_identifiers", "rep msg:FabricOUIdentifier"),
                         8: ("crypto_config", "msg:FabricCryptoConfig"), 11: ("fabric_node_ous", "msg:FabricNodeOUs")},
     "FabricCryptoConfig": {1: ("signature_hash_family", "string"), 2: ("identity_identifier_hash_function", "string")},
     "FabricNodeOUs": {1: ("enable", "bool"), 2: ("client_ou_identifier", "msg:FabricOUIdentifier"),

@@ -158,12 +158,28 @@ class ChannelModel:
         key = (sid.get("mspid", ""), sid.get("id_bytes") or b"")
         ident = self.msp.get(key)
         if ident is None:
-            if key[0] in self.mspids:
+            if key[0] not in self.mspids:
+                return None
+            # a cache miss: the channel's MSP deserializes and validates the certificate
+            # (oracle/msp.py); an MSP outside that model -> Unsupported
+            m = self.msp_models().get(key[0])
+            if m is None or isinstance(m, Unsupported):
                 raise Unsupported("unregistered identity of channel MSP %s" % key[0])
-            return None
+            ident = m.resolve(key[1])
+            if ident is None:
+                ident = Ident(key[0], None, False, b"\0" * 32, key=KEY_UNDESERIALIZABLE)
+            elif self.config_msps.get(key[0], {}).get("crypto_config", {}).get("signature_hash_family") == "SHA3":
+                ident.hash_family = "SHA3"
+            self.msp[key] = ident
         if ident.key == KEY_UNDESERIALIZABLE:
             return None
         return ident
+
+    def msp_models(self):
+        if getattr(self, "_msp_models", None) is None:
+            from .msp import msps_of_config
+            self._msp_models = msps_of_config(self.config_msps) if self.policies is not None else {}
+        return self._msp_models
 
     def verify(self, ident, msg, sig):
         """identity.Verify: 0 iff valid (msp/identities.go:170-199)."""

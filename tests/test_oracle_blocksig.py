@@ -68,12 +68,34 @@ def test_reference_ledger_tampered_signature_fails(what):
     assert [r[0] for r in res] == [BV.OK, BV.OK, BV.SIGNATURES, BV.NUMBER, BV.NUMBER]
 
 
-def test_reference_ledger_without_orderer_identity_is_unsupported():
+def test_reference_ledger_without_orderer_identity_resolves_through_the_msp():
+    """The orderer's certificate was never registered: the MSP cache miss deserializes it through
+    the channel config's OrdererOrgMSP (oracle/msp.py) -- the same identity the registration
+    carried (Id, key, Validate, roles) -- and the blocks verify."""
     blocks, (n0, h0), idents, config = ledger_setup()
+    dropped = [(s, i) for s, i in idents if i.mspid == "OrdererOrgMSP"]
     idents = [(s, i) for s, i in idents if i.mspid != "OrdererOrgMSP"]
     model = v20.ChannelModel("testchannel", idents, {}, config=config)
     res = BV.verify_blocks(blocks[:3], dict(number=n0, header_hash=h0), sig=dict(model=model))
+    assert [r[0] for r in res] == [BV.OK] * 3
+    for ser, reg in dropped:
+        got = model.deserialize(ser)
+        assert got is not None and got.id_digest == reg.id_digest and got.pub == reg.pub
+        assert got.valid == reg.valid and got.roles == reg.roles
+
+
+def test_reference_ledger_orderer_msp_outside_the_model_is_unsupported():
+    """A channel MSP outside the modelled shapes (here: no root CAs left) cannot judge the miss."""
+    from oracle.protowire import decode
+    blocks, (n0, h0), idents, config = ledger_setup()
+    idents = [(s, i) for s, i in idents if i.mspid != "OrdererOrgMSP"]
+    model = v20.ChannelModel("testchannel", idents, {}, config=config)
+    fc = dict(model.config_msps["OrdererOrgMSP"])
+    fc["root_certs"] = []
+    model.config_msps["OrdererOrgMSP"] = fc
+    res = BV.verify_blocks(blocks[:3], dict(number=n0, header_hash=h0), sig=dict(model=model))
     assert [r[0] for r in res] == [BV.SIG_UNSUPPORTED] * 3
+    assert decode  # (the config bytes themselves are unchanged)
 
 
 @pytest.mark.parametrize("case", BC.cases(), ids=lambda c: c["name"])

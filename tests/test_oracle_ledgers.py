@@ -111,8 +111,8 @@ def test_committer_v20_derived_negatives():
     """Perturbing the MODEL (not the signed blocks) flips outcomes the way the reference's rules
     say: peers without the PEER role -> approvals and commits fail their org / MAJORITY
     policies (10); a marbles-private definition without collectionMarbles -> 10 ("no such
-    collection"); unknown collections / an unregistered channel identity / a P-384 creator ->
-    Unsupported (never a guess)."""
+    collection"); unknown collections / a P-384 creator -> Unsupported (never a guess); an
+    unregistered channel identity resolves through its MSP."""
     import copy
 
     import pytest
@@ -142,8 +142,32 @@ def test_committer_v20_derived_negatives():
         run(13, defs_=d)
     from tests.sample_channel import tx_identities
     creator13 = tx_identities(decode("Block", by_num[13]["block"])["data"]["data"][0])[0]
-    with pytest.raises(v20.Unsupported):  # a known MSP's certificate the engine was never given
-        run(13, idents_=[(s, i) for s, i in idents if s != creator13])
+    # a known MSP's certificate never registered: the MSP cache miss resolves it (oracle/msp.py)
+    assert run(13, idents_=[(s, i) for s, i in idents if s != creator13])[0] == run(13)[0]
     p384 = [(s, v20.Ident(i.mspid, i.pub, i.valid, i.id_digest, key=v20.KEY_P384, roles=i.roles)) for s, i in idents]
     with pytest.raises(v20.Unsupported):
         run(5, p384)
+
+
+def test_committer_v20_without_registered_identities():
+    """No identity registered at all: every creator and endorser of the v2.0 sample ledger is an
+    MSP cache miss, deserialized and validated through the channel config's MSPs (root CAs,
+    NodeOUs, admins -- oracle/msp.py), and the replay still reproduces every block's stored
+    TRANSACTIONS_FILTER; the resolved identities equal the registered ones."""
+    from oracle import v20
+    from tests.sample_channel import v20_channel
+    blocks, config, idents, defs = v20_channel()
+    n = 0
+    for b in blocks:
+        if b["number"] < 5:
+            continue
+        model = v20.ChannelModel("testchannel", [], defs[b["number"]], config=config)
+        assert v20.validate_block(model, b["block"]) == b["flags"], b["number"]
+        n += 1
+    assert n == 15
+    model = v20.ChannelModel("testchannel", [], {}, config=config)
+    for ser, reg in idents:
+        got = model.deserialize(ser)
+        assert got is not None, reg.mspid
+        assert (got.mspid, got.pub, got.valid, got.id_digest, got.roles) == \
+            (reg.mspid, reg.pub, reg.valid, reg.id_digest, reg.roles)
