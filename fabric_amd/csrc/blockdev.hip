@@ -556,13 +556,14 @@ __global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__r
     // the creator is needed when the parse got past the channel check (pre still pending)
     const DSpan sp = k == 0 ? R.creator : R.end_ser[k - 1];
     const bool want = k == 0 ? (R.pre == C_PENDING && sp.len != 0) : true;
-    if (want && ch.nident) {
+    if (want) {
       VSerializedIdentity sid;
       bool ovf = false;
       if (decode(absl(base, sp), sid, ovf)) {
         const uint64_t h = ident_hash_dev(sid.mspid, sid.id_bytes);
         bool found = false;
-        for (uint32_t pos = (uint32_t)h & ch.ident_mask;; pos = (pos + 1) & ch.ident_mask) {
+        // (an empty registry has no table: every identity of a channel MSP is a miss)
+        for (uint32_t pos = (uint32_t)h & ch.ident_mask; ch.nident; pos = (pos + 1) & ch.ident_mask) {
           const uint32_t e = ch.ident_table[pos];
           if (e == 0) break;
           const uint32_t i = e - 1;

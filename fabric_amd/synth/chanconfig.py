@@ -47,6 +47,33 @@ def msp_value(mspid, hash_family="SHA2"):
     return f_bytes(2, f_varint(1, 0) + f_bytes(2, fabric))  # ConfigValue{value: MSPConfig{type 0, config}}
 
 
+def fabric_msp_config(mspid, root_certs=(), admins=(), ou_ids=(), node_ous=("client", "peer", "admin", "orderer"),
+                      node_ou_certs=None, hash_family="SHA2"):
+    """FabricMSPConfig bytes: root CA PEMs, admin PEMs, OrganizationalUnitIdentifiers [(cert PEM,
+    ou)], NodeOUs (client, peer, admin, orderer identifiers; None entries are left out; node_ous
+    None = disabled; node_ou_certs: role index -> certificate PEM)"""
+    out = f_str(1, mspid)
+    for c in root_certs:
+        out += f_bytes(2, c)
+    for c in admins:
+        out += f_bytes(4, c)
+    for cert, ou in ou_ids:
+        out += f_msg(7, f_bytes(1, cert) + f_str(2, ou))
+    out += f_msg(8, f_str(1, hash_family) + f_str(2, "SHA256"))
+    if node_ous is not None:
+        body = f_varint(1, 1)
+        for k, o in enumerate(node_ous):
+            if o is not None:
+                cert = (node_ou_certs or {}).get(k)
+                body += f_msg(2 + k, (f_bytes(1, cert) if cert else b"") + f_str(2, o))
+        out += f_msg(11, body)
+    return out
+
+
+def msp_value_raw(fabric):
+    return f_bytes(2, f_varint(1, 0) + f_bytes(2, fabric))
+
+
 def group(groups=(), values=(), policies=()):
     out = b""
     for k, g in groups:
@@ -59,10 +86,15 @@ def group(groups=(), values=(), policies=()):
 
 
 def make_config(mspids, endorsement_rule=MAJORITY, org_endorsement_role=PEER, hash_families=None, orderer_mspids=(),
-                block_validation=None, orderer_writers_role=MEMBER):
+                block_validation=None, orderer_writers_role=MEMBER, msp_configs=None):
     """-> common.Config bytes; org group names org1..orgN (the MSP ids are separate names).
     orderer_mspids: orderer orgs (group names ord1..ordN) -> an Orderer group; block_validation:
-    its BlockValidation policy bytes (ConfigPolicy), default IMPLICIT_META ANY Writers."""
+    its BlockValidation policy bytes (ConfigPolicy), default IMPLICIT_META ANY Writers.
+    msp_configs: mspid -> FabricMSPConfig bytes (fabric_msp_config) replacing the default MSP
+    value (root CAs etc. for the MSP cache-miss path)."""
+    def mspv(m, fam):
+        raw = (msp_configs or {}).get(m)
+        return msp_value_raw(raw) if raw is not None else msp_value(m, fam)
     orgs = []
     for i, m in enumerate(mspids):
         fam = (hash_families or {}).get(m, "SHA2")
@@ -70,7 +102,7 @@ def make_config(mspids, endorsement_rule=MAJORITY, org_endorsement_role=PEER, ha
                 ("Readers", config_policy(SIGNATURE, signature_policy(1, [(m, ADMIN), (m, PEER), (m, CLIENT)]))),
                 ("Writers", config_policy(SIGNATURE, signature_policy(1, [(m, ADMIN), (m, CLIENT)]))),
                 ("Admins", config_policy(SIGNATURE, signature_policy(1, [(m, ADMIN)])))]
-        orgs.append(("org%d" % (i + 1), group(values=[("MSP", msp_value(m, fam))], policies=pols)))
+        orgs.append(("org%d" % (i + 1), group(values=[("MSP", mspv(m, fam))], policies=pols)))
     app = group(groups=orgs, policies=[("Endorsement", implicit_meta(endorsement_rule, "Endorsement")),
                                        ("LifecycleEndorsement", implicit_meta(MAJORITY, "Endorsement")),
                                        ("Readers", implicit_meta(ANY, "Readers")),
@@ -84,7 +116,7 @@ def make_config(mspids, endorsement_rule=MAJORITY, org_endorsement_role=PEER, ha
             pols = [("Readers", config_policy(SIGNATURE, signature_policy(1, [(m, MEMBER)]))),
                     ("Writers", config_policy(SIGNATURE, signature_policy(1, [(m, orderer_writers_role)]))),
                     ("Admins", config_policy(SIGNATURE, signature_policy(1, [(m, ADMIN)])))]
-            ords.append(("ord%d" % (i + 1), group(values=[("MSP", msp_value(m, fam))], policies=pols)))
+            ords.append(("ord%d" % (i + 1), group(values=[("MSP", mspv(m, fam))], policies=pols)))
         bv = block_validation if block_validation is not None else implicit_meta(ANY, "Writers")
         groups.append(("Orderer", group(groups=ords, policies=[("BlockValidation", bv),
                                                                 ("Readers", implicit_meta(ANY, "Readers")),

@@ -56,11 +56,11 @@ def test_reference_ledger_orderer_signatures():
     bad[4] = tamper(bad[4], "value")
     assert _compare(eng, model, bad, chain) == [BV.OK, BV.SIGNATURES] + [BV.NUMBER] * 4
     eng.close()
-    # the orderer's certificate unregistered: outside the model
+    # the orderer's certificate unregistered: resolved through OrdererOrgMSP (MSP cache miss)
     idents2 = [(s, i) for s, i in idents if i.mspid != "OrdererOrgMSP"]
     eng = _engine(idents2, config, "testchannel")
     model = v20.ChannelModel("testchannel", idents2, {}, config=config)
-    assert _compare(eng, model, blocks[:3], chain) == [BV.SIG_UNSUPPORTED] * 3
+    assert _compare(eng, model, blocks[:3], chain) == [BV.OK] * 3
     eng.close()
 
 

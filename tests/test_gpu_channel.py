@@ -145,8 +145,8 @@ def test_v20_sample_ledger(mode):
 
 def test_v20_derived_negatives_match_oracle():
     """Model perturbations (peers stripped of PEER role, only Org1's peer a PEER, a collection
-    removed from marbles-private) give the oracle's codes on the GPU; unknown collections, an
-    unregistered channel identity and a P-384 creator give Unsupported."""
+    removed from marbles-private, the creator of block 13 unregistered -- resolved through its MSP)
+    give the oracle's codes on the GPU; unknown collections and a P-384 creator give Unsupported."""
     from tests.sample_channel import tx_identities, v20_channel
     from oracle.protowire import decode
     blocks_, config, idents, defs = v20_channel()
@@ -160,7 +160,10 @@ def test_v20_derived_negatives_match_oracle():
     one_peer = conv(idents, lambda i: i.roles if i.mspid == "Org1MSP" else i.roles & ~(1 << 3))
     d13 = copy.deepcopy(defs[13])
     del d13["marblesp"]["collections"]["collectionMarbles"]
-    cases = [(5, no_peer, None), (8, no_peer, None), (5, one_peer, None), (8, one_peer, None), (13, idents, d13)]
+    creator13 = tx_identities(decode("Block", by[13]["block"])["data"]["data"][0])[0]
+    unreg13 = [(s, i) for s, i in idents if s != creator13]  # resolved through its MSP (cache miss)
+    cases = [(5, no_peer, None), (8, no_peer, None), (5, one_peer, None), (8, one_peer, None), (13, idents, d13),
+             (13, unreg13, None)]
     for num, ids, dd in cases:
         d = dd or defs[num]
         exp = v20.validate_block(v20.ChannelModel("testchannel", ids, d, config=config), by[num]["block"])
@@ -171,12 +174,10 @@ def test_v20_derived_negatives_match_oracle():
     # outside the model
     d_unknown = copy.deepcopy(defs[13])
     d_unknown["marblesp"]["collections"] = None
-    creator13 = tx_identities(decode("Block", by[13]["block"])["data"]["data"][0])[0]
     p384 = conv(idents, lambda i: i.roles)
     for s, i in p384:
         i.key = "p384"
-    for ids, dd, num in [(idents, d_unknown, 13), ([(s, i) for s, i in idents if s != creator13], None, 13),
-                         (p384, None, 5)]:
+    for ids, dd, num in [(idents, d_unknown, 13), (p384, None, 5)]:
         eng = _v20_engine(0, ids, config)
         _define(eng, dd or defs[num])
         with pytest.raises(_lib.Unsupported):

@@ -204,3 +204,34 @@ def test_engine_pem_rules():
              b"\r\n-----END CERTIFICATE-----\r\n"]
     for c in cases:
         assert L.x509_probe(c) == _oracle_view(c), c[:60]
+
+
+def test_synthetic_cases_oracle():
+    """tests/msp_cases.py: the restatement gives the outcome each synthetic case is built for"""
+    from oracle import v20
+    from tests.msp_cases import FAILED, MSPID, OK, REPEAT, UNSUP, synthetic
+    cfg, cases = synthetic()
+    m = v20.ChannelModel("ch", [], {}, config=cfg).msp_models()[MSPID]
+    assert not isinstance(m, Exception), m
+    for label, ser, st, valid, roles in cases:
+        if st == REPEAT:
+            continue
+        idb = decode("SerializedIdentity", ser).get("id_bytes") or b""
+        try:
+            got = m.resolve(idb)
+        except Unsupported:
+            assert st == UNSUP, label
+            continue
+        if got is None:
+            assert st == FAILED, label
+            continue
+        assert st == OK and (got.valid, got.roles) == (valid, roles), (label, got.valid, got.roles)
+
+
+def test_engine_parser_matches_on_synthetic_certificates():
+    L = _lib()
+    from tests.msp_cases import synthetic
+    _, cases = synthetic()
+    for label, ser, *_ in cases:
+        pem = decode("SerializedIdentity", ser).get("id_bytes") or b""
+        assert L.x509_probe(pem) == _oracle_view(pem), label
