@@ -290,3 +290,5 @@ uint64_t fgv_block_parse_probe(const char *channel, const uint8_t *const *ids, c
                                const char *ns, const uint8_t *policy, size_t policy_len, const uint8_t *blk,
                                size_t n);
 uint64_t fgv_mvcc_parse_probe(const uint8_t *rws, size_t n);
+uint64_t fgv_msp_config_probe(const uint8_t *conf, size_t n);
+extern "C" int fgv_x509_probe(const uint8_t *pem, size_t n, char *out, size_t cap);

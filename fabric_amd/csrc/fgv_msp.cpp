@@ -135,7 +135,8 @@ struct MspModel {
   RoleOU role_ou[5];
   std::vector<std::vector<uint8_t>> admins;  // sanitized admin certificates
 
-  // oracle/msp.py MSP.__init__; c->mu held (registers the root keys)
+  // oracle/msp.py MSP.__init__; c->mu held (registers the root keys; c NULL: the sanitizer
+  // probe, no key registration)
   void build(fgv_ctx *c, const std::string &conf) {
     VMspCfg fc;
     if (!pbw::decode(reinterpret_cast<const uint8_t *>(conf.data()), conf.size(), fc)) return fail();
@@ -157,7 +158,7 @@ struct MspModel {
       roots.push_back(std::move(r));
     }
     std::vector<uint32_t> slots(roots.size());
-    if (fgv_keys_register_locked(c, keys.data(), roots.size(), slots.data()) != FGV_OK) return fail();
+    if (c && fgv_keys_register_locked(c, keys.data(), roots.size(), slots.data()) != FGV_OK) return fail();
     for (size_t i = 0; i < roots.size(); i++) roots[i].slot = slots[i];
     // certifier of an OU: the root whose certificate it is
     auto certifier = [&](const Span &pem, Dig &out) -> bool {
@@ -506,3 +507,11 @@ int fgv_msp_identity(fgv_ctx *c, const uint8_t *serialized, size_t len, fgv_iden
 }
 
 }  // extern "C"
+
+// Sanitizer probe (tools/sanitize/harness.cpp): FabricMSPConfig bytes through the MSP model's
+// parse (visitors, root / admin / OU certificates) without the key registration; 1 = modelled
+uint64_t fgv_msp_config_probe(const uint8_t *conf, size_t n) {
+  MspModel m;
+  m.build(nullptr, std::string(reinterpret_cast<const char *>(conf), n));
+  return m.unsup ? 0 : 1 + m.roots.size() * 16 + m.admins.size() * 256;
+}

@@ -142,3 +142,34 @@ def test_sanitizer_is_live(tmp_path):
     r = subprocess.run([_harness(), str(p)], env=dict(os.environ, ASAN_OPTIONS="halt_on_error=1:detect_leaks=0"),
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "heap-buffer-overflow" in r.stderr
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_harness_clean_on_certificates_and_msp_configs(tmp_path, seed):
+    """the MSP cache miss's host parsers: PEM / X.509 / sanitizeCert over the reference's MSP
+    certificates, the synthetic cases and their mutations; FabricMSPConfig bytes and mutations"""
+    import base64
+    import json
+    from oracle import x509 as X
+    from oracle.protowire import decode
+    from tests.msp_cases import synthetic
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "msp_fixtures.json")))
+    pems = [p.encode() for p in fx["certs"].values()]
+    pems += [decode("SerializedIdentity", c[1]).get("id_bytes") or b"" for c in synthetic()[1]]
+    confs = [bytes.fromhex(m["config"]) for m in fx["msps"].values()]
+    rng = random.Random(seed)
+    recs = [_rec(6, p) for p in pems] + [_rec(7, c) for c in confs]
+    for p in pems[:60]:
+        der = X.pem_decode(p)
+        if not der:
+            continue
+        for d in _mutate(rng, der, 25):
+            recs.append(_rec(6, b"-----BEGIN CERTIFICATE-----\n" + base64.encodebytes(d) + b"-----END CERTIFICATE-----\n"))
+        for m in _mutate(rng, p, 5):  # the PEM text itself
+            recs.append(_rec(6, m))
+    for c in confs:
+        recs += [_rec(7, m) for m in _mutate(rng, c, 20)]
+    path = tmp_path / ("certs%d.bin" % seed)
+    path.write_bytes(b"".join(recs))
+    out = _run(str(path))
+    assert "%d certs" % len(recs) in out

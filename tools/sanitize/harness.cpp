@@ -9,6 +9,8 @@
 //   kind 3 chaincode policy bytes (ApplicationPolicy) of namespace "mycc"
 //   kind 4 TxReadWriteSet bytes: fgv_mvcc_parse_probe (phantom-path decode + range validators)
 //   kind 5 channel name
+//   kind 6 PEM certificate: fgv_x509_probe (the MSP cache miss's PEM / X.509 / sanitizeCert)
+//   kind 7 FabricMSPConfig bytes: fgv_msp_config_probe (the cache miss's MSP model parse)
 //   kind 9 canary: reads one byte past its record (proves the sanitizer is live)
 // Any sanitizer report aborts the process (halt_on_error); exit 0 = clean.
 #include <stdint.h>
@@ -45,7 +47,7 @@ int main(int argc, char **argv) {
     if (r.first == 5) channel.assign(r.second.begin(), r.second.end());
   }
   uint64_t acc = 0;
-  size_t nblocks = 0, nrws = 0;
+  size_t nblocks = 0, nrws = 0, ncerts = 0;
   for (auto &r : recs) {
     // an exact-size heap copy: ASan sees any read past the record
     std::vector<uint8_t> buf(r.second);
@@ -70,11 +72,19 @@ int main(int argc, char **argv) {
     } else if (r.first == 9) {
       // canary (tests/test_sanitize.py): one byte read past the record -- the run must abort
       acc += buf.data()[buf.size()];
+    } else if (r.first == 6) {
+      ncerts++;
+      static char out[1 << 16];
+      acc = acc * 31 + (uint64_t)(fgv_x509_probe(p ? p : reinterpret_cast<const uint8_t *>(""), n, out, sizeof out) + 2);
+    } else if (r.first == 7) {
+      ncerts++;
+      acc = acc * 31 + fgv_msp_config_probe(p ? p : reinterpret_cast<const uint8_t *>(""), n);
     } else if (r.first == 4) {
       nrws++;
       acc = acc * 31 + fgv_mvcc_parse_probe(p ? p : reinterpret_cast<const uint8_t *>(""), n);
     }
   }
-  printf("sanitize harness: %zu blocks, %zu rwsets, digest %016llx\n", nblocks, nrws, (unsigned long long)acc);
+  printf("sanitize harness: %zu blocks, %zu rwsets, %zu certs, digest %016llx\n", nblocks, nrws, ncerts,
+         (unsigned long long)acc);
   return 0;
 }
