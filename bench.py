@@ -95,7 +95,7 @@ def block_roofline(kavg, pay_blocks, verifies, workload):
              kernel="k_bd_sha_payload", dominant_kernel=dom, kernel_avg_ms=round(t_pay * 1e3, 4),
              per_launch_compressions=int(pay_blocks),
              work_unit="SHA-256 compressions x 2.7e3 simple int32 ops (SURVEY.md s8(d))")
-    r["second"] = roofline(verifies, kavg.get("k_point28", 0.0), workload)
+    r["second"] = roofline(verifies, kavg.get("k_point28", 0.0), workload + "_point")
     r["second"]["kernel"] = "k_point28 (+ k_point hand-overs)"
     return r
 

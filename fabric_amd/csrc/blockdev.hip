@@ -642,30 +642,138 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
 // SHA-256(Envelope.payload) of every envelope -- the creator signature's digest
 // (msgvalidation.go:26-64 -> msp/identities.go:179), digest slot 0 -- launched on the second
 // stream BEFORE the parse: it decodes the Envelope (two fields, the same rules and visitor as
-// k_bd_parse) and hashes field 1.  Each payload is its transaction's longest message (~80
-// compressions for C2): these serial chains set the SHA-256 stage, so they start first.
-__global__ __launch_bounds__(64) void k_bd_sha_payload(uint32_t ntx, const uint32_t *__restrict__ envtab,
-                                                       const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
-                                                       unsigned long long *__restrict__ nblk) {
-  // the longest serial chains of the batch (~80 compressions for C2): first in issue order
+// k_bd_parse) and hashes field 1.  Each payload is its transaction's longest message (~58
+// compressions for C2), a serial chain; a batch has far fewer chains (16k) than the chip has
+// lanes, so the kernel is bound by ONE chain's latency, not by throughput.  Each chain is
+// therefore split over two waves of a workgroup on two SIMDs (64 payloads per workgroup):
+//   wave 1 (schedule): loads block b+1 (one block ahead), expands W[0..63] and writes
+//                      KW[t] = W[t] + K[t] to LDS (double-buffered, [t/4][lane] x 16 B)
+//   wave 0 (rounds):   the 64 rounds of block b from LDS (16 x ds_read_b128)
+// one barrier per block.  The rounds wave carries ~950 VALU instructions per compression
+// instead of ~1,650 for the whole compression in one lane.
+#define PAY_KW_BYTES (2 * 16 * 64 * 16)
+__device__ __forceinline__ void pay_view(uint32_t ntx, uint32_t t, const uint32_t *envtab, const uint64_t *bases,
+                                         JobView &v, uint32_t &nblk) {
+  nblk = 0;
+  v.p[0] = v.p[1] = v.p[2] = nullptr;
+  v.beg[0] = v.beg[1] = v.beg[2] = v.beg[3] = v.L = 0;
+  if (t >= ntx) return;
+  const uint32_t *et = envtab + BD_ENV_WORDS * t;
+  VTwoBytes env;
+  bool ovf = false;
+  if (!decode(S{reinterpret_cast<const uint8_t *>(bases[et[0]]) + et[1], et[2]}, env, ovf)) return;
+  v.p[0] = v.p[1] = v.p[2] = env.a.p;
+  v.beg[1] = v.beg[2] = v.beg[3] = v.L = env.a.n;
+  nblk = (v.L + 8) / 64 + 1;
+}
+
+__global__ __launch_bounds__(128) void k_bd_sha_payload(uint32_t ntx, const uint32_t *__restrict__ envtab,
+                                                        const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                                        unsigned long long *__restrict__ nblk_total) {
+  // the longest serial chains of the batch: first in issue order
   __builtin_amdgcn_s_setprio(2);
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t blocks = 0;
-  if (t < ntx) {
-    const uint32_t *et = envtab + BD_ENV_WORDS * t;
-    VTwoBytes env;
-    bool ovf = false;
-    if (decode(S{reinterpret_cast<const uint8_t *>(bases[et[0]]) + et[1], et[2]}, env, ovf)) {
-      JobView v;
-      v.p[0] = v.p[1] = v.p[2] = env.a.p;
-      v.beg[0] = 0;
-      v.beg[1] = v.beg[2] = v.beg[3] = v.L = env.a.n;
-      sha_view(v, dig + (size_t)t * 32);
-      blocks = (v.L + 8) / 64 + 1;
+  __shared__ uint4 KW[2][16][64];  // [buffer][t / 4][lane]: KW[t] = W[t] + K[t] of one block
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool sched = threadIdx.x >= 64;  // wave-uniform
+  const uint32_t t = blockIdx.x * 64 + lane;
+  JobView v;
+  uint32_t nblk;
+  pay_view(ntx, t, envtab, bases, v, nblk);
+  uint32_t maxb = nblk;
+  for (int off = 32; off > 0; off >>= 1) maxb = max(maxb, (uint32_t)__shfl_xor((int)maxb, off));
+  if (sched) {
+    // ---- schedule wave: block b's words (fetched one block ahead), expansion, KW to LDS
+    uint32_t raw[17], sh = 0;
+    bool fast = false;
+    auto fetch = [&](uint32_t b) {
+      const uint32_t s0 = b * 64;
+      const int k = s0 < v.beg[1] ? 0 : (s0 < v.beg[2] ? 1 : 2);
+      fast = s0 + 64 <= span_end(v, k);
+      if (fast) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(span_p(v, k) + (s0 - span_beg(v, k)));
+        const __attribute__((address_space(1))) uint32_t *al =
+            reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(a & ~(uintptr_t)3);
+        sh = (uint32_t)(a & 3u);
+#pragma unroll
+        for (int q = 0; q < 17; q++) raw[q] = al[q];
+      }
+    };
+    auto produce = [&](uint32_t b) {
+      if (b >= nblk) return;
+      uint32_t w[16];
+      if (fast) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh));
+      } else {
+        job_block(v, b, nblk, w);
+      }
+      if (b + 1 < nblk) fetch(b + 1);
+      uint4 *o = &KW[b & 1][0][lane];
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        uint32_t kw[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int i = 4 * q + j;
+          uint32_t wi;
+          if (i < 16) {
+            wi = w[i];
+          } else {
+            const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+            w[i & 15] = wi;
+          }
+          kw[j] = wi + SHA_K[i];
+        }
+        o[q * 64] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+      }
+    };
+    if (nblk) fetch(0);
+    produce(0);
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t b = 0; b < maxb; b++) {
+      if (b + 1 < maxb) produce(b + 1);
+      __syncthreads();
     }
+    return;
   }
+  // ---- rounds wave
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t b = 0; b < maxb; b++) {
+    if (b < nblk) {
+      const uint4 *in = &KW[b & 1][0][lane];
+      uint32_t a = h[0], bb = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const uint4 x = in[q * 64];
+        const uint32_t kw4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+          const uint32_t ch = (e & f) ^ (~e & g);
+          const uint32_t t1 = k + S1 + ch + kw4[j];
+          const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+          const uint32_t mj = (a & bb) | (c & (a | bb));
+          k = g; g = f; f = e; e = d + t1; d = c; c = bb; bb = a; a = t1 + S0 + mj;
+        }
+      }
+      h[0] += a; h[1] += bb; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
+    }
+    __syncthreads();
+  }
+  if (nblk) {
+    uint32_t *o = reinterpret_cast<uint32_t *>(dig + (size_t)t * 32);
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[k] = __builtin_bswap32(h[k]);
+  }
+  uint64_t blocks = nblk;
   for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
-  if ((threadIdx.x & 63) == 0 && blocks) atomicAdd(nblk, (unsigned long long)blocks);
+  if (lane == 0 && blocks) atomicAdd(nblk_total, (unsigned long long)blocks);
 }
 
 // ============================================================ k_bd_sha
@@ -803,12 +911,8 @@ DEV void seg_block_slow(const ShaSeg &g, uint32_t blk, uint32_t w[16]) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__restrict__ txs,
-                                               const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
-                                               unsigned long long *__restrict__ nblk_out) {
-  // ~33 compressions per lane against the payload hashes' ~80: it has slack (k_prep waits for
-  // both), so it yields to them and to the parse -> identity chain
-  __builtin_amdgcn_s_setprio(1);
+DEV void bd_sha_body(uint32_t ntx, const DevTx *__restrict__ txs, const uint64_t *__restrict__ bases,
+                     uint8_t *__restrict__ dig, unsigned long long *__restrict__ nblk_out) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t grp = lane / SHA_GROUP, r = lane - grp * SHA_GROUP;
   const uint32_t t = blockIdx.x * SHA_GPW + grp;
@@ -887,6 +991,26 @@ __global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__rest
   }
   for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
   if (lane == 0 && blocks) atomicAdd(nblk_out, (unsigned long long)blocks);
+}
+// k_prep waits for these digests and for the parse -> identities -> counts -> emit -> der ->
+// inv chain: the wave priority decides which of the two finishes first (FGV_SHA_PRIO A/B)
+__global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__restrict__ txs,
+                                               const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                               unsigned long long *__restrict__ nblk_out) {
+  __builtin_amdgcn_s_setprio(1);
+  bd_sha_body(ntx, txs, bases, dig, nblk_out);
+}
+__global__ __launch_bounds__(64) void k_bd_sha_p2(uint32_t ntx, const DevTx *__restrict__ txs,
+                                                  const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                                  unsigned long long *__restrict__ nblk_out) {
+  __builtin_amdgcn_s_setprio(2);
+  bd_sha_body(ntx, txs, bases, dig, nblk_out);
+}
+__global__ __launch_bounds__(64) void k_bd_sha_p3(uint32_t ntx, const DevTx *__restrict__ txs,
+                                                  const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                                  unsigned long long *__restrict__ nblk_out) {
+  __builtin_amdgcn_s_setprio(3);
+  bd_sha_body(ntx, txs, bases, dig, nblk_out);
 }
 
 // ============================================================ k_bd_emit

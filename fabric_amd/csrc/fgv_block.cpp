@@ -1118,6 +1118,10 @@ __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
 __global__ void k_bd_sha(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
+__global__ void k_bd_sha_p2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig,
+                            unsigned long long *nblk);
+__global__ void k_bd_sha_p3(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig,
+                            unsigned long long *nblk);
 __global__ void k_bd_sha_payload(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, uint8_t *dig,
                                  unsigned long long *nblk);
 __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
@@ -1273,7 +1277,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   DevTx *dtx = B.tx.as<DevTx>();
   // the payload hashes (the longest serial chains) start with the parse, on the second stream
   HIP_TRY(hipStreamWaitEvent(c->stream2, B.ev[3], 0));
-  hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(64), 0, c->stream2, N, envtab, dbs,
+  hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(128), 0, c->stream2, N, envtab, dbs,
                      B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
   HIP_TRY(hipEventRecord(B.ev[1], c->stream2));
   hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5);
@@ -1282,7 +1286,12 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   // identities and job counts are worked out on this one
   HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[4], 0));
   if (tim) HIP_TRY(hipEventRecord(B.ev[5], c->stream3));
-  hipLaunchKernelGGL(k_bd_sha, dim3((N + SHA_GPW - 1) / SHA_GPW), dim3(64), 0,
+  static const int sha_prio = [] {
+    const char *e = getenv("FGV_SHA_PRIO");
+    return e ? atoi(e) : 1;
+  }();
+  hipLaunchKernelGGL(sha_prio == 3 ? k_bd_sha_p3 : sha_prio == 2 ? k_bd_sha_p2 : k_bd_sha,
+                     dim3((N + SHA_GPW - 1) / SHA_GPW), dim3(64), 0,
                      c->stream3, N, dtx, dbs, B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 6));
   HIP_TRY(hipEventRecord(B.ev[2], c->stream3));
   HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[1], 0));
@@ -1407,7 +1416,10 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   const int ahead_mode = c->ahead_mode;
   if (nx.n && nx.d_blocks && ahead_mode) {
     BdSet &A = S->set[cur ^ 1];
-    hipEvent_t after = (ahead_mode == 1 && c->stage_ran) ? c->ev[6] : ahead_mode == 3 ? c->kev[9] : nullptr;
+    hipEvent_t after = (ahead_mode == 1 && c->stage_ran)   ? c->ev[6]
+                       : (ahead_mode == 4 && c->stage_ran) ? c->ev[5]
+                       : ahead_mode == 3                   ? c->kev[9]
+                                                           : nullptr;
     if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after) ==
         FGV_OK)
       S->ahead = cur ^ 1;

@@ -81,7 +81,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   }
   const unsigned dflt = share ? std::min(24u, share) : 24u;
   c->blk = fgv_block_state_new((cfg && cfg->host_threads) ? cfg->host_threads : dflt);
-  if (const char *e = getenv("FGV_AHEAD")) c->ahead_mode = std::max(0, std::min(3, atoi(e)));
+  if (const char *e = getenv("FGV_AHEAD")) c->ahead_mode = std::max(0, std::min(4, atoi(e)));
   if (const char *e = getenv("FGV_TIMING")) c->timing = atoi(e) != 0;
   auto fail = [&](int e) {
     fgv_destroy(c);
@@ -256,7 +256,7 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
   hipLaunchKernelGGL(k_prep, dim3((N + 255) / 256), dim3(256), 0, c->stream, N, dn, d_status, d_r,
                      c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>(), redo);  // (k_prep zeroes *redo)
   HIP_TRY(hipGetLastError());
-  if (tim) HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+  if (tim || c->ahead_mode == 4) HIP_TRY(hipEventRecord(c->ev[5], c->stream));  // (ahead mode 4 waits on it)
   // Grid: two POINT_THREADS workgroups per CU (2 waves per SIMD) taking chunks of items from a
   // device counter (k_point*: waves placed late, beside a next batch's front half, take fewer).
   // Lanes per verify L (1, 2, 4, 8):
@@ -1172,7 +1172,7 @@ int fgv_set_timing(fgv_ctx *c, int on) {
 }
 
 int fgv_set_ahead(fgv_ctx *c, int mode) {
-  if (!c || mode < 0 || mode > 3) return FGV_EINVAL;
+  if (!c || mode < 0 || mode > 4) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   fgv_block_drain(c);  // (a front half already enqueued ahead is discarded)
   c->ahead_mode = mode;

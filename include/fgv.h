@@ -141,9 +141,10 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *ctx, const uint8_t *d_msg_buf, const uint6
  *                            writes to it FGV_EUNSUPPORTED; with them known, an undefined
  *                            collection is an ENDORSEMENT_POLICY_FAILURE (v20.go:84-100)
  *   fgv_ledger_add_txids  -- txids already in the block store (TxIDExists, kv_ledger.go:496)
- * Identities a transaction names that the engine cannot judge exactly -- an unregistered
- * certificate of a channel MSP, a P-384 key, a SHA3 MSP, a role principal for an identity
- * registered without role bits -- make the batch FGV_EUNSUPPORTED (the reference decides). */
+ * Identities a transaction names that the engine cannot judge exactly -- a certificate of a
+ * channel MSP neither registered nor resolvable by the MSP cache-miss path below, a P-384 key, a
+ * SHA3 MSP, a role principal for an identity registered without role bits -- make the batch
+ * FGV_EUNSUPPORTED (the reference decides). */
 #define FGV_KEY_P256 1             /* verified on the GPU                                      */
 #define FGV_KEY_P384 2             /* bccsp verifies it: outside the engine                    */
 #define FGV_KEY_OTHER 3            /* RSA etc.: Verify fails                        */
@@ -345,7 +346,9 @@ int fgv_last_ahead(fgv_ctx *ctx);
  * the environment variable FGV_AHEAD sets the initial value): one batch on the GPU at a time, the
  * next one pre-split on the host; 2 = at once, beside the current batch's back half (equal to 0
  * within noise on MI355X for C2-shaped batches); 1 = once the current batch's ECDSA
- * kernels are done; 3 = once its policy fold is done.  Results never depend on it. */
+ * kernels are done; 3 = once its policy fold is done; 4 = once its k_prep is done (beside its
+ * k_point28, which is VALU-issue-bound while the front half is latency-bound).  Results never
+ * depend on it. */
 int fgv_set_ahead(fgv_ctx *ctx, int mode);
 /* Per-kernel device times of the block committer (fgv_last_kernel_times, fgv_last_timing): on,
  * every kernel of the back half is bracketed by timestamp events -- each a packet on the
@@ -474,8 +477,10 @@ int fgv_blocks_verify(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks
  * (fgv_channel_config + the orderer identities registered like any other).  Signatures are
  * verified on the GPU in one pass for the whole call.  bft != 0: the channel runs BFT; a
  * signature that names its consenter by an identifier header is outside the model.
- * Outside the model too: no channel config, an unregistered identity of a channel MSP, a
- * P-384 / SHA3 orderer identity -> FGV_BLK_SIG_UNSUPPORTED from that block on, FGV_EUNSUPPORTED. */
+ * An orderer identity never registered is resolved through its channel MSP first (the MSP cache
+ * miss, fgv_msp_resolve).  Outside the model: no channel config, an identity of a channel MSP the
+ * cache-miss path cannot judge, a P-384 / SHA3 orderer identity -> FGV_BLK_SIG_UNSUPPORTED from
+ * that block on, FGV_EUNSUPPORTED. */
 int fgv_blocks_verify_signed(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                              fgv_chain_state *chain, const char *policy, int bft, fgv_block_check *out);
 /* ------------------------------------------------------------------- ledger commit hash (a21)

@@ -65,9 +65,11 @@ def main(src, rnd):
         for k, v in sorted(kernel_stats(p).items(), key=lambda kv: -kv[1]["pct"]):
             lines.append(f"| {k[:60]} | {v['calls']} | {v['avg_us']:.1f} | {v['pct']:.1f} |")
         lines.append("")
-    p = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
-    if os.path.exists(p):
-        lines += ["## VALU counters (sig workload: 131,072 verifies per dispatch)", "",
+    for vname, title in (("pmc_valu", "sig workload: 131,072 verifies per dispatch"),
+                         ("pmc_blk_valu", "block workload: one C2 step of 16k transactions")):
+      p = os.path.join(src, vname, "run_counter_collection.csv")
+      if os.path.exists(p):
+        lines += [f"## VALU counters ({title})", "",
                   "| kernel | avg µs | VALU wave-insts | INT32 | INT64 | lane-ops/s | % of 78.6 T full-rate peak | VALU busy % |",
                   "|---|---|---|---|---|---|---|---|"]
         for k, v in pmc(p).items():
@@ -79,7 +81,7 @@ def main(src, rnd):
             lines.append(f"| {k} | {v['avg_s'] * 1e6:.1f} | {v.get('SQ_INSTS_VALU', 0):.4g} | "
                          f"{v.get('SQ_INSTS_VALU_INT32', 0):.3g} | {v.get('SQ_INSTS_VALU_INT64', 0):.3g} | {lane:.3g} | "
                          f"{100 * lane / PEAK_LANE_OPS:.1f} | {busy:.0f} |")
-        kp = pmc(p).get("k_point28")
+        kp = pmc(p).get("k_point28") if vname == "pmc_valu" else None
         if kp:
             gui = kp.get("GRBM_GUI_ACTIVE", 0) / XCDS
             cpi = gui * SIMDS / kp["SQ_INSTS_VALU"] if kp.get("SQ_INSTS_VALU") else 0
@@ -108,7 +110,8 @@ def main(src, rnd):
     # HBM traffic per launch of each workload's dominant kernel (bench.py roofline.traffic):
     # FETCH_SIZE (doubled, gfx950) + WRITE_SIZE from the separate --pmc passes, KB -> bytes
     traffic = {}
-    for wl, fe, wr, kern in (("block", "pmc_blk_fetch", "pmc_blk_write", "k_point28"),
+    for wl, fe, wr, kern in (("block", "pmc_blk_fetch", "pmc_blk_write", "k_bd_sha_payload"),
+                             ("block_point", "pmc_blk_fetch", "pmc_blk_write", "k_point28"),
                              ("sig", "pmc_sig_fetch", "pmc_sig_write", "k_point28"),
                              ("mvcc", "pmc_fetch", "pmc_write", None)):
         pf = os.path.join(src, fe, "run_counter_collection.csv")
