@@ -1438,7 +1438,7 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   if (S->pending < 0) return FGV_OK;
   BdSet &B = S->set[S->pending];
   S->pending = -1;
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(fgv_stream_wait(c->stream, c->spin));
   fgv_read_block_job_times(c);
   {  // per-kernel device times (fgv_last_kernel_times)
     auto el = [&](hipEvent_t a, hipEvent_t b) {

@@ -83,6 +83,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   c->blk = fgv_block_state_new((cfg && cfg->host_threads) ? cfg->host_threads : dflt);
   if (const char *e = getenv("FGV_AHEAD")) c->ahead_mode = std::max(0, std::min(4, atoi(e)));
   if (const char *e = getenv("FGV_TIMING")) c->timing = atoi(e) != 0;
+  if (const char *e = getenv("FGV_SPIN")) c->spin = atoi(e) != 0;
   auto fail = [&](int e) {
     fgv_destroy(c);
     return e;

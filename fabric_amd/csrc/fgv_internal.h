@@ -154,6 +154,7 @@ struct fgv_ctx {
   // fgv_set_timing: record the committer's timing-only events (per-kernel device times); each
   // is a timestamp packet on the critical path (~5 us on MI355X), so off by default
   bool timing = false;
+  bool spin = false;  // FGV_SPIN=1: poll the committer's final wait (fgv_stream_wait; equal within noise on MI355X)
   bool timing_ran = true;  // the last verify stages recorded their events (read_stage_times)
   // host-resident batches: two device staging arenas; fgv_validate_shard_dev_next copies the
   // NEXT batch into the idle one on the copy stream while this batch's kernels run
@@ -174,6 +175,18 @@ struct fgv_ctx {
   fgv_msp_cache *msp = nullptr;  // MSP models of the cache-miss path (fgv_msp.cpp)
 };
 void fgv_integrity_free(fgv_ctx *c);
+
+// Wait for a stream: polled (hipStreamQuery) when `spin`, else a blocking synchronize.  The
+// committer's calls wait ~0.8 ms for their batch; polling returns as soon as the last copy lands
+// instead of after the blocking wait's wake-up.
+inline hipError_t fgv_stream_wait(hipStream_t s, bool spin) {
+  if (!spin) return hipStreamSynchronize(s);
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) return e;
+    __builtin_ia32_pause();
+  }
+}
 
 #define HIP_TRY(x)                                     \
   do {                                                 \
