@@ -12,9 +12,11 @@
 //                        validateIdentityOUsV142 (OU identifiers; NodeOUs: exactly one role OU)
 //   mspimpl.go:607-680   ROLE principals: MEMBER = Validate; ADMIN = in admins or (valid and
 //                        admin OU); CLIENT / PEER / ORDERER = valid and that OU
-// The MSP model is built from the channel configuration's FabricMSPConfig (root CAs only, no
-// intermediates, no CRLs, OU certificates that are roots); the CA signatures of a batch of
-// misses are verified on the GPU in one pass (the root keys are pinned key-table slots) and the
+// The MSP model is built from the channel configuration's FabricMSPConfig: root and intermediate
+// CAs (each a CA with a SubjectKeyIdentifier, chains by unique issuer names, verified on the GPU
+// at build; parents of intermediates are internal nodes of the certification tree, mspimpl.go:
+// 835-858), no CRLs, OU certificates that are CAs of the MSP.  The CA signatures of a batch of
+// misses are verified on the GPU in one pass (the CA keys are pinned key-table slots) and the
 // results registered like fgv_msp_register_identity.  Shapes outside the model stay
 // unregistered (the batch stays FGV_EUNSUPPORTED: the reference decides).  The same rules as
 // oracle/msp.py + oracle/x509.py, which the parity tests compare against.
@@ -23,6 +25,7 @@
 #include <array>
 #include <map>
 #include <memory>
+#include <set>
 #include <unordered_set>
 
 #include "fgv_channel.h"
@@ -112,11 +115,48 @@ Dig sha(const std::vector<uint8_t> &v) {
 
 enum : int { R_CLIENT = 2, R_PEER = 3, R_ADMIN = 1, R_ORDERER = 4 };
 
-struct Root {
+// a CA of the MSP (root or intermediate), parsed and sanitized at model build
+struct CA {
   fgvx::Cert c;
-  Dig certifier;  // SHA-256 of the sanitized root (the OU certifier identifier)
-  uint32_t slot = 0;
+  std::vector<uint8_t> raw2;  // sanitized certificate
+  bool root = false;
+  uint32_t slot = 0;          // its P-256 key in the key table (pinned)
+  std::vector<int> chain;     // itself, its parent, ..., a root (setup's validation chain)
+  bool internal = false;      // the parent of an intermediate (certificationTreeInternalNodesMap)
+  Dig chain_id{};             // SHA-256 over the sanitized certificates of `chain`
 };
+constexpr size_t kMaxChain = 8;
+
+// x509 isValid for a CA with `below` intermediates under it + CheckSignatureFrom's rules
+// (oracle/msp.py MSP._parent_ok)
+bool parent_ok(const fgvx::Cert &p, int64_t now, size_t below) {
+  if ((p.version == 3 && !p.bc_valid) || (p.bc_valid && !p.is_ca)) return false;
+  if (p.key_usage && !(p.key_usage & (1u << 5))) return false;
+  if (!(p.not_before <= now && now <= p.not_after)) return false;
+  if (p.bc_valid && p.path_len >= 0 && (int64_t)below > p.path_len) return false;  // TooManyIntermediates
+  return true;
+}
+
+// child's CA signature as a verify job of the parent's key (false: not a strict DER signature
+// with 0 < r, s < n -- the verify fails); Go's ecdsa accepts high S: the low-S equivalent
+bool ca_job(const fgvx::Cert &child, uint32_t parent_slot, std::vector<uint8_t> &msgs, std::vector<uint64_t> &moff,
+            std::vector<uint32_t> &mlen, std::vector<uint8_t> &sigs, std::vector<uint64_t> &soff,
+            std::vector<uint32_t> &slen, std::vector<uint32_t> &slots) {
+  uint8_t r[32], s[32];
+  if (!fgvx::strict_sig(child.sig(), child.sig_len, r, s) || fgvx::is_zero(r) || fgvx::is_zero(s) || !fgvx::lt_n(r) ||
+      !fgvx::lt_n(s))
+    return false;
+  fgvx::to_low_s(s);
+  const std::vector<uint8_t> low = fgvx::der_sig(r, s);
+  moff.push_back(msgs.size());
+  msgs.insert(msgs.end(), child.tbs(), child.tbs() + child.tbs_len);
+  mlen.push_back((uint32_t)child.tbs_len);
+  soff.push_back(sigs.size());
+  sigs.insert(sigs.end(), low.begin(), low.end());
+  slen.push_back((uint32_t)low.size());
+  slots.push_back(parent_slot);
+  return true;
+}
 struct RoleOU {
   bool present = false;
   std::string name;
@@ -129,44 +169,102 @@ struct RoleOU {
 struct MspModel {
   bool unsup = false;
   bool sha3 = false;
-  std::vector<Root> roots;
+  std::vector<CA> cas;  // roots first, then intermediates
   std::map<std::string, std::vector<Dig>> ou_ids;
   bool node_ous = false;
   RoleOU role_ou[5];
   std::vector<std::vector<uint8_t>> admins;  // sanitized admin certificates
 
-  // oracle/msp.py MSP.__init__; c->mu held (registers the root keys; c NULL: the sanitizer
-  // probe, no key registration)
+  // the CA whose subject is x's issuer: index, -1 none, -2 several (x509 could build several
+  // chains: outside the model)
+  int unique_parent(const fgvx::Cert &x, int self) const {
+    int found = -1;
+    for (size_t j = 0; j < cas.size(); j++)
+      if ((int)j != self && x.same_issuer_as_subject_of(cas[j].c)) {
+        if (found >= 0) return -2;
+        found = (int)j;
+      }
+    return found;
+  }
+
+  // oracle/msp.py MSP.__init__; c->mu held (registers the CA keys, verifies the CA chains on the
+  // GPU; c NULL: the sanitizer probe -- no key registration, signatures taken as verified)
   void build(fgv_ctx *c, const std::string &conf) {
     VMspCfg fc;
     if (!pbw::decode(reinterpret_cast<const uint8_t *>(conf.data()), conf.size(), fc)) return fail();
-    if (!fc.inters.empty() || !fc.crls.empty()) return fail();
+    if (!fc.crls.empty()) return fail();
     VCryptoCfg cc;
     if (!decode_all(fc.crypto, cc)) return fail();
     if (!cc.idhash.eq("SHA256", 6) && cc.idhash.n) return fail();
     sha3 = cc.fam.eq("SHA3", 4);
     if (fc.roots.empty()) return fail();
     std::vector<uint8_t> keys;
-    for (const Span &pem : fc.roots) {
-      std::vector<uint8_t> der, raw2;
-      Root r;
-      if (fgvx::pem_decode(pem.p, pem.n, der) != fgvx::X_OK) return fail();
-      if (fgvx::parse_certificate(std::move(der), r.c) != fgvx::X_OK || r.c.key != fgvx::XK_P256) return fail();
-      if (fgvx::sanitized_raw(r.c, raw2) != fgvx::X_OK) return fail();
-      r.certifier = sha(raw2);
-      keys.insert(keys.end(), r.c.pub, r.c.pub + 64);
-      roots.push_back(std::move(r));
+    for (int pass = 0; pass < 2; pass++)
+      for (const Span &pem : pass == 0 ? fc.roots : fc.inters) {
+        std::vector<uint8_t> der;
+        CA a;
+        a.root = pass == 0;
+        if (fgvx::pem_decode(pem.p, pem.n, der) != fgvx::X_OK) return fail();
+        if (fgvx::parse_certificate(std::move(der), a.c) != fgvx::X_OK || a.c.key != fgvx::XK_P256) return fail();
+        if (!a.c.is_ca || !a.c.has_ski) return fail();  // finalizeSetupCAs: the MSP would not set up
+        if (fgvx::sanitized_raw(a.c, a.raw2) != fgvx::X_OK) return fail();
+        keys.insert(keys.end(), a.c.pub, a.c.pub + 64);
+        cas.push_back(std::move(a));
+      }
+    std::vector<uint32_t> slots(cas.size());
+    if (c && fgv_keys_register_locked(c, keys.data(), cas.size(), slots.data()) != FGV_OK) return fail();
+    for (size_t i = 0; i < cas.size(); i++) cas[i].slot = c ? slots[i] : 0;
+    // the validation chains: a root verifies itself; an intermediate walks to a root, checked at
+    // its own NotBefore + 1 s; every (child, parent) signature is verified in one GPU pass
+    std::vector<uint8_t> msgs, sigs;
+    std::vector<uint64_t> moff, soff;
+    std::vector<uint32_t> mlen, slen, jslots;
+    std::set<std::pair<int, int>> linked;
+    auto link = [&](int child, int parent) -> bool {
+      if (!linked.insert({child, parent}).second) return true;
+      return ca_job(cas[child].c, cas[parent].slot, msgs, moff, mlen, sigs, soff, slen, jslots);
+    };
+    for (size_t i = 0; i < cas.size(); i++) {
+      CA &a = cas[i];
+      a.chain.assign(1, (int)i);
+      if (a.root) {
+        if (!a.c.same_issuer_as_subject_of(a.c) || !link((int)i, (int)i)) return fail();
+        continue;
+      }
+      const int64_t now = a.c.not_before + 1;
+      int cur = (int)i;
+      while (!cas[cur].root) {
+        if (a.chain.size() > kMaxChain) return fail();
+        const int p = unique_parent(cas[cur].c, cur);
+        if (p < 0 || std::find(a.chain.begin(), a.chain.end(), p) != a.chain.end()) return fail();
+        if (!parent_ok(cas[p].c, now, a.chain.size() - 1) || !link(cur, p)) return fail();
+        a.chain.push_back(p);
+        cur = p;
+      }
     }
-    std::vector<uint32_t> slots(roots.size());
-    if (c && fgv_keys_register_locked(c, keys.data(), roots.size(), slots.data()) != FGV_OK) return fail();
-    for (size_t i = 0; i < roots.size(); i++) roots[i].slot = slots[i];
-    // certifier of an OU: the root whose certificate it is
+    if (c && !moff.empty()) {
+      std::vector<uint8_t> st(moff.size(), 1);
+      if (fgv_verify_msgs_slots_locked(c, msgs.data(), msgs.size(), moff.data(), mlen.data(), sigs.data(), sigs.size(),
+                                       soff.data(), slen.data(), jslots.data(), moff.size(), st.data()) != FGV_OK)
+        return fail();
+      for (uint8_t v : st)
+        if (v != 0) return fail();
+    }
+    for (CA &a : cas) {
+      if (!a.root)
+        for (size_t k = 1; k < a.chain.size(); k++) cas[a.chain[k]].internal = true;
+      std::vector<uint8_t> cat;
+      for (int k : a.chain) cat.insert(cat.end(), cas[k].raw2.begin(), cas[k].raw2.end());
+      a.chain_id = sha(cat);
+    }
+    // certifier of an OU: the chain of the CA whose certificate it is (getCertifiersIdentifier)
     auto certifier = [&](const Span &pem, Dig &out) -> bool {
       std::vector<uint8_t> der;
       if (fgvx::pem_decode(pem.p, pem.n, der) != fgvx::X_OK) return false;
-      for (const Root &r : roots)
-        if (der == r.c.der) {
-          out = r.certifier;
+      for (const CA &a : cas)
+        if (der == a.c.der) {
+          if (!a.root && a.internal) return false;  // getValidationChain(cert, true): parent position 0
+          out = a.chain_id;
           return true;
         }
       return false;
@@ -242,7 +340,7 @@ struct Pending {
   size_t i;                 // input index
   const MspModel *m;
   fgvx::Cert c;
-  const Root *root = nullptr;
+  int p1 = -1;  // the issuing CA (cas index)
   std::vector<uint8_t> ser;
 };
 
@@ -299,24 +397,19 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
       undeser.push_back(i);
       continue;
     }
-    size_t nc = 0;
-    for (const Root &r : m->roots)
-      if (p.c.same_issuer_as_subject_of(r.c)) {
-        nc++;
-        p.root = &r;
-      }
-    if (nc > 1) {
+    p.p1 = m->unique_parent(p.c, -1);
+    if (p.p1 == -2) {
       status[i] = FGV_RESOLVE_UNSUPPORTED;
       continue;
     }
-    if (nc == 0) {
-      undeser.push_back(i);
-      continue;
+    // the chain above the leaf is the issuer's setup chain (unique parents); each CA on it is
+    // checked at this leaf's time and depth (CheckSignatureFrom's rules, validity, MaxPathLen)
+    bool ok = p.p1 >= 0;
+    if (ok) {
+      const std::vector<int> &up = m->cas[p.p1].chain;
+      for (size_t k = 0; k < up.size() && ok; k++) ok = parent_ok(m->cas[up[k]].c, now, k);
     }
-    // CheckSignatureFrom: the parent must be allowed to sign certificates
-    const fgvx::Cert &rc_ = p.root->c;
-    if ((rc_.version == 3 && !rc_.bc_valid) || (rc_.bc_valid && !rc_.is_ca) ||
-        (rc_.key_usage && !(rc_.key_usage & (1u << 5))) || !(rc_.not_before <= now && now <= rc_.not_after)) {
+    if (!ok) {
       undeser.push_back(i);
       continue;
     }
@@ -330,20 +423,8 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
   std::vector<size_t> job(pend.size(), SIZE_MAX);
   for (size_t k = 0; k < pend.size(); k++) {
     const Pending &p = pend[k];
-    uint8_t r[32], s[32];
-    if (!fgvx::strict_sig(p.c.sig(), p.c.sig_len, r, s) || fgvx::is_zero(r) || fgvx::is_zero(s) || !fgvx::lt_n(r) ||
-        !fgvx::lt_n(s))
-      continue;  // the verify fails
-    fgvx::to_low_s(s);
-    const std::vector<uint8_t> low = fgvx::der_sig(r, s);
-    job[k] = moff.size();
-    moff.push_back(msgs.size());
-    msgs.insert(msgs.end(), p.c.tbs(), p.c.tbs() + p.c.tbs_len);
-    mlen.push_back((uint32_t)p.c.tbs_len);
-    soff.push_back(sigs.size());
-    sigs.insert(sigs.end(), low.begin(), low.end());
-    slen.push_back((uint32_t)low.size());
-    slots.push_back(p.root->slot);
+    const size_t j = moff.size();
+    if (ca_job(p.c, p.m->cas[p.p1].slot, msgs, moff, mlen, sigs, soff, slen, slots)) job[k] = j;
   }
   std::vector<uint8_t> jst(moff.size(), 1);
   if (!moff.empty()) {
@@ -374,9 +455,11 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
     Reg g{p.i, fgv_identity_info{}};
     const Dig dg = sha(raw2);
     memcpy(g.info.id_digest, dg.data(), 32);
-    // Validate: the signing CA's SKI, then the OUs (validateIdentityOUsV142)
-    bool valid = p.root->c.has_ski;
-    const Dig &cid = p.root->certifier;
+    // Validate: the issuer must be a leaf of the certification tree (its SKI exists: setup),
+    // then the OUs (validateIdentityOUsV142) with the chain above the identity as certifier
+    const CA &issuer = m.cas[p.p1];
+    bool valid = !issuer.internal && issuer.c.has_ski;
+    const Dig &cid = issuer.chain_id;
     if (valid && !m.ou_ids.empty()) {
       bool any = false;
       for (const std::string &o : p.c.ous) {
@@ -513,5 +596,5 @@ int fgv_msp_identity(fgv_ctx *c, const uint8_t *serialized, size_t len, fgv_iden
 uint64_t fgv_msp_config_probe(const uint8_t *conf, size_t n) {
   MspModel m;
   m.build(nullptr, std::string(reinterpret_cast<const char *>(conf), n));
-  return m.unsup ? 0 : 1 + m.roots.size() * 16 + m.admins.size() * 256;
+  return m.unsup ? 0 : 1 + m.cas.size() * 16 + m.admins.size() * 256;
 }

@@ -297,6 +297,13 @@ void parse(Cert &c) {
         a = 1;
       }
       if (k.size() > a && (k[a].tag != 0x02 || k.size() - a > 1)) perr();
+      if (k.size() > a) {  // MaxPathLen: ReadASN1Integer into a 64-bit int
+        const T &pl = k[a];
+        if (!int_minimal(v, pl.cs, pl.ce) || pl.ce - pl.cs > 8) perr();
+        int64_t x = (v[pl.cs] & 0x80) ? -1 : 0;
+        for (size_t q = pl.cs; q < pl.ce; q++) x = (int64_t)(((uint64_t)x << 8) | v[q]);
+        c.path_len = x;
+      }
       c.bc_valid = true;
     } else if (x.id == 14) {  // subjectKeyIdentifier
       if (t.tag != 0x04 || t.ce != vn) perr();
@@ -615,7 +622,7 @@ extern "C" int fgv_x509_probe(const uint8_t *pem, size_t n, char *out, size_t ca
       const int rs = sanitized_raw(c, raw2);
       j = "{\"stage\":\"ok\",\"status\":0,\"key\":" + std::to_string(c.key) + ",\"version\":" +
           std::to_string(c.version) + ",\"is_ca\":" + std::to_string(c.is_ca) + ",\"bc_valid\":" +
-          std::to_string(c.bc_valid) + ",\"has_ski\":" + std::to_string(c.has_ski) + ",\"key_usage\":" +
+          std::to_string(c.bc_valid) + ",\"path_len\":" + std::to_string(c.path_len) + ",\"has_ski\":" + std::to_string(c.has_ski) + ",\"key_usage\":" +
           std::to_string(c.key_usage) + ",\"unhandled_critical\":" + std::to_string(c.unhandled_critical) +
           ",\"not_before\":" + std::to_string(c.not_before) + ",\"not_after\":" + std::to_string(c.not_after) +
           ",\"pub\":\"" + (c.key == XK_P256 ? hex(c.pub, 64) : std::string()) + "\"";

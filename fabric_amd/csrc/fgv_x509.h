@@ -27,6 +27,7 @@ struct Cert {
   int key = XK_OTHER;                       // subject public key class
   uint8_t pub[64] = {};                     // P-256 X || Y
   bool is_ca = false, bc_valid = false, has_ski = false, unhandled_critical = false;
+  int64_t path_len = -1;                    // basicConstraints MaxPathLen (-1: none)
   uint32_t key_usage = 0;                   // Go KeyUsage bits
   int version = 0;                          // 1..3
   const uint8_t *tbs() const { return der.data() + tbs_off; }

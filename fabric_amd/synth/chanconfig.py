@@ -48,13 +48,15 @@ def msp_value(mspid, hash_family="SHA2"):
 
 
 def fabric_msp_config(mspid, root_certs=(), admins=(), ou_ids=(), node_ous=("client", "peer", "admin", "orderer"),
-                      node_ou_certs=None, hash_family="SHA2"):
+                      node_ou_certs=None, hash_family="SHA2", intermediate_certs=()):
     """FabricMSPConfig bytes: root CA PEMs, admin PEMs, OrganizationalUnitIdentifiers [(cert PEM,
     ou)], NodeOUs (client, peer, admin, orderer identifiers; None entries are left out; node_ous
     None = disabled; node_ou_certs: role index -> certificate PEM)"""
     out = f_str(1, mspid)
     for c in root_certs:
         out += f_bytes(2, c)
+    for c in intermediate_certs:
+        out += f_bytes(3, c)
     for c in admins:
         out += f_bytes(4, c)
     for cert, ou in ou_ids:

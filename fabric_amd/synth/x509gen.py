@@ -51,8 +51,9 @@ def ski(key):
     return ext("551d0e", tlv(0x04, hashlib.sha256(key.pub).digest()[:20]))
 
 
-def basic_constraints(ca, critical=True):
-    return ext("551d13", seq(tlv(0x01, b"\xff")) if ca else seq(), critical)
+def basic_constraints(ca, critical=True, path_len=None):
+    body = (tlv(0x01, b"\xff") if ca else b"") + (integer(path_len) if path_len is not None else b"")
+    return ext("551d13", seq(body) if body else seq(), critical)
 
 
 def key_usage(bits, critical=True):
@@ -83,7 +84,9 @@ def cert(subject_key: Key, issuer_key: Key, subject, issuer, serial=1, not_befor
     return b"-----BEGIN CERTIFICATE-----\n" + b64 + b"-----END CERTIFICATE-----\n"
 
 
-def ca_cert(key: Key, cn="ca.org1", org="Org1", with_ski=True, usage=(0, 5, 6), serial=1):
+def ca_cert(key: Key, cn="ca.org1", org="Org1", with_ski=True, usage=(0, 5, 6), serial=1, issuer_key=None,
+            issuer_cn=None, path_len=None):
+    """a root CA (self-signed), or an intermediate when issuer_key / issuer_cn are given"""
     nm = name(cn, org)
-    exts = [key_usage(usage), basic_constraints(True)] + ([ski(key)] if with_ski else [])
-    return cert(key, key, nm, nm, serial=serial, extensions=exts)
+    exts = [key_usage(usage), basic_constraints(True, path_len=path_len)] + ([ski(key)] if with_ski else [])
+    return cert(key, issuer_key or key, nm, name(issuer_cn, org) if issuer_cn else nm, serial=serial, extensions=exts)

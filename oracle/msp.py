@@ -16,8 +16,14 @@ validated by the channel's MSP (bccspmsp, MSP version 1.4.3 -- Fabric v2 channel
   mspimpl.go:607-680   satisfiesPrincipalInternalV142 / PreV13 for ROLE principals: MEMBER =
                        Validate; ADMIN = in the admins list or (valid and admin OU); CLIENT / PEER
                        / ORDERER = valid and that OU (NodeOUs required)
-Modelled MSP shapes: root CAs only (no intermediates), no CRLs, OU identifiers whose
-certificate (if any) is one of the roots; anything else raises Unsupported.
+Intermediate CAs (mspimplsetup.go finalizeSetupCAs, mspimpl.go:835-858 getValidationChain):
+every CA must be a CA with a SubjectKeyIdentifier (else the MSP does not set up); the parents of
+intermediates are internal nodes of the certification tree, and an identity whose issuer is an
+internal node is invalid; the certifier identifier of a chain is SHA-256 over its certificates
+(getCertificationChainIdentifierFromChain).  x509 Verify (Go 1.21) per hop: CheckSignatureFrom,
+validity at the leaf's NotBefore + 1 s, an intermediate needs basicConstraints CA, MaxPathLen.
+Modelled MSP shapes: no CRLs, P-256 CAs, at most one candidate parent per hop, OU certificates
+that are CAs of the MSP; anything else raises Unsupported.
 """
 import hashlib
 
@@ -27,34 +33,53 @@ from .protowire import decode
 from .v20 import KEY_OTHER, KEY_P256, KEY_P384, Ident, Unsupported
 
 ROLE_MEMBER, ROLE_ADMIN, ROLE_CLIENT, ROLE_PEER, ROLE_ORDERER = range(5)
+MAX_CHAIN = 8
+
+
+def _ca(pem, what):
+    der = X.pem_decode(pem)
+    if der is None:
+        raise Unsupported(what + " PEM")
+    try:
+        c = X.parse_certificate(der)
+    except X.ParseError:
+        raise Unsupported(what + " does not parse")
+    if c["key"] != "p256":
+        raise Unsupported(what + " key")
+    if not c["is_ca"] or c["ski"] is None:  # finalizeSetupCAs: the MSP would not set up
+        raise Unsupported(what + " without the CA attribute or a SubjectKeyIdentifier")
+    c["raw2"] = X.sanitized_raw(c)  # (setupCAs sanitizes the CAs)
+    return c
 
 
 class MSP:
     def __init__(self, fc):
         """fc: decoded FabricMSPConfig"""
         self.name = fc.get("name", "")
-        if fc.get("intermediate_certs"):
-            raise Unsupported("intermediate CAs")
         if fc.get("revocation_list"):
             raise Unsupported("CRLs")
         cc = fc.get("crypto_config") or {}
         if cc.get("identity_identifier_hash_function", "SHA256") not in ("SHA256", ""):
             raise Unsupported("identity identifier hash")
-        self.roots = []
         if not fc.get("root_certs"):
             raise Unsupported("MSP without root CAs")  # (setupCAs: "expected at least one CA certificate")
-        for pem in fc.get("root_certs", []):
-            der = X.pem_decode(pem)
-            if der is None:
-                raise Unsupported("root CA PEM")
-            try:
-                c = X.parse_certificate(der)
-            except X.ParseError:
-                raise Unsupported("root CA does not parse")
-            if c["key"] != "p256":
-                raise Unsupported("root CA key")
-            c["raw2"] = X.sanitized_raw(c)  # (setupCAs sanitizes the roots too)
-            self.roots.append(c)
+        self.roots = [_ca(pem, "root CA") for pem in fc.get("root_certs", [])]
+        self.inters = [_ca(pem, "intermediate CA") for pem in fc.get("intermediate_certs", [])]
+        for r in self.roots:  # a root verifies itself (validateCAIdentity: a chain of length 1)
+            if r["issuer"] != r["subject"] or not X.ca_verifies(r, r, verify_der):
+                raise Unsupported("root CA that is not self-signed")
+        # the chains of the intermediates, checked at their own NotBefore + 1 s; their parents
+        # are the internal nodes of the certification tree
+        self.internal = set()
+        self.inter_chain = {}
+        for c in self.inters:
+            ch = self._chain_of(c, c["not_before"] + 1)
+            if ch is None or len(ch) < 2:
+                raise Unsupported("intermediate CA without a validation chain")
+            self.inter_chain[c["raw2"]] = ch
+            for p in ch[1:]:
+                self.internal.add(p["raw2"])
+
         # certifier identifiers: SHA-256 over the chain of the OU's certificate (a root: itself)
         def certifier(pem):
             if not pem:
@@ -63,7 +88,12 @@ class MSP:
             for r in self.roots:
                 if der == r["der"]:
                     return hashlib.sha256(r["raw2"]).digest()
-            raise Unsupported("OU certificate that is not a root CA")
+            for c in self.inters:
+                if der == c["der"]:
+                    if c["raw2"] in self.internal:  # getValidationChain(cert, true): parent position 0
+                        raise Unsupported("OU certificate that is an internal CA")
+                    return hashlib.sha256(b"".join(x["raw2"] for x in self.inter_chain[c["raw2"]])).digest()
+            raise Unsupported("OU certificate that is not a CA of the MSP")
         self.ou_ids = {}
         for ou in fc.get("organizational_unit_identifiers", []):
             if not ou.get("certificate"):
@@ -87,8 +117,44 @@ class MSP:
             except (X.ParseError, TypeError):
                 raise Unsupported("admin certificate")
 
+    def _parent_ok(self, parent, now, below):
+        """x509 isValid for a CA at `below` intermediates under it + CheckSignatureFrom's rules"""
+        if (parent["version"] == 3 and not parent["bc_valid"]) or (parent["bc_valid"] and not parent["is_ca"]):
+            return False
+        if parent["key_usage"] and not (parent["key_usage"] & (1 << 5)):
+            return False
+        if not (parent["not_before"] <= now <= parent["not_after"]):
+            return False
+        if parent["bc_valid"] and parent["path_len"] >= 0 and below > parent["path_len"]:
+            return False  # TooManyIntermediates
+        return True
+
+    def _chain_of(self, c, now):
+        """getUniqueValidationChain: [c, parent, ..., root] or None; Unsupported when a hop has
+        several candidate parents (Go could build several chains)"""
+        chain = [c]
+        cur = c
+        while not any(cur is r for r in self.roots):
+            if len(chain) > MAX_CHAIN:
+                raise Unsupported("certificate chain too long")
+            cands = [x for x in self.roots + self.inters if x["subject"] == cur["issuer"] and x is not cur]
+            if len(cands) > 1:
+                raise Unsupported("several CAs with the issuer name")
+            if not cands:
+                return None
+            p = cands[0]
+            if p in chain:
+                return None
+            if not self._parent_ok(p, now, len(chain) - 1):
+                return None
+            if not X.ca_verifies(p, cur, verify_der):
+                return None
+            chain.append(p)
+            cur = p
+        return chain
+
     def _chain(self, c):
-        """getUniqueValidationChain for a leaf: the one root that signed it, or None"""
+        """getUniqueValidationChain for a leaf: its chain to a root, or None"""
         if c["is_ca"]:
             raise Unsupported("CA certificate as an identity")
         if c["unhandled_critical"]:
@@ -96,20 +162,7 @@ class MSP:
         now = c["not_before"] + 1
         if not (c["not_before"] <= now <= c["not_after"]):
             return None
-        cands = [r for r in self.roots if r["subject"] == c["issuer"]]
-        if len(cands) > 1:
-            raise Unsupported("several roots with the leaf's issuer name")
-        for r in cands:
-            # CheckSignatureFrom: the parent must be allowed to sign certificates
-            if (r["version"] == 3 and not r["bc_valid"]) or (r["bc_valid"] and not r["is_ca"]):
-                return None
-            if r["key_usage"] and not (r["key_usage"] & (1 << 5)):
-                return None
-            if not (r["not_before"] <= now <= r["not_after"]):
-                return None
-            if X.ca_verifies(r, c, verify_der):
-                return r
-        return None
+        return self._chain_of(c, now)
 
     def resolve(self, id_bytes):
         """-> v20.Ident, or None when DeserializeIdentity fails"""
@@ -122,14 +175,15 @@ class MSP:
             return None
         if c["key"] == "undeserializable":  # bccsp KeyImport fails (Ed25519)
             return None
-        root = self._chain(c)
-        if root is None:
+        chain = self._chain(c)
+        if chain is None:
             return None  # sanitizeCert: no validation chain -> newIdentity fails
         raw2 = X.sanitized_raw(c)
         digest = hashlib.sha256(raw2).digest()
-        # Validate: the signing CA's SKI, then the OUs
-        valid = root["ski"] is not None
-        certifier = hashlib.sha256(root["raw2"]).digest()
+        # Validate: the issuer must be a leaf of the certification tree, its SKI must exist
+        # (setup guarantees it), then the OUs; the certifier is the chain above the identity
+        valid = chain[1]["raw2"] not in self.internal and chain[1]["ski"] is not None
+        certifier = hashlib.sha256(b"".join(x["raw2"] for x in chain[1:])).digest()
         ous = [(o, certifier) for o in c["ous"]]
         if valid and self.ou_ids:
             valid = any(cid in self.ou_ids.get(o, []) for o, cid in ous)

@@ -284,7 +284,7 @@ def parse_certificate(der):
                 raise Unsupported("extension %s" % oid.hex())
             if oid not in (EXT_SKI, EXT_KU, EXT_BC, EXT_AKI, EXT_EKU, EXT_SAN) and crit:
                 unhandled_critical = True
-    is_ca, bc_valid = False, False
+    is_ca, bc_valid, path_len = False, False, -1
     if EXT_BC in exts:
         v = exts[EXT_BC][1]
         t, s, e = tlv(v, 0)
@@ -298,6 +298,10 @@ def parse_certificate(der):
             k = k[1:]
         if k and (k[0][0] != 0x02 or len(k) > 1):
             raise ParseError("bad pathLen")
+        if k:  # MaxPathLen (ReadASN1Integer into an int: must fit in 64 bits)
+            path_len = der_int(v, k[0][1], k[0][2])
+            if not -(1 << 63) <= path_len < (1 << 63):
+                raise ParseError("pathLen out of range")
         bc_valid = True
     ski = None
     if EXT_SKI in exts:
@@ -341,7 +345,7 @@ def parse_certificate(der):
                 unhandled_critical = True  # (nothing parsed: Go's critical check applies)
     return dict(der=der, tbs=tbs_raw, sig=sig_bits[1:], serial=serial, issuer=der[issuer[3]:issuer[2]],
                 subject=der[subject[3]:subject[2]], not_before=not_before, not_after=not_after, ous=ous,
-                key=key, pub=pub, is_ca=is_ca, bc_valid=bc_valid, ski=ski, key_usage=key_usage,
+                key=key, pub=pub, is_ca=is_ca, bc_valid=bc_valid, path_len=path_len, ski=ski, key_usage=key_usage,
                 unhandled_critical=unhandled_critical, version=version + 1)
 
 

@@ -1,11 +1,14 @@
 """Synthetic MSP cache-miss cases shared by tests/test_oracle_msp.py (the oracle against the
 expected outcomes written here) and tests/test_gpu_msp.py (the engine against the oracle).
 
-One channel MSP "Org1MSP" with three roots -- CA1 (SKI, keyCertSign), CA2 (no SKI), CA3 (key
-usage without keyCertSign) -- NodeOUs client / peer / admin / orderer, one listed admin; and
-leaves covering each rule of the miss path: role OUs, two role OUs, no OU, a listed admin, a
-high-S CA signature, unknown issuer, wrong CA key, an unhandled critical extension, a CA as an
-identity, SAN (DNS / URI), an empty validity window, Ed25519, a malformed IA5 OU, not PEM."""
+Channel MSP "Org1MSP": roots CA1 (SKI, keyCertSign), CA3 (key usage without keyCertSign), CA4
+(parent of intermediate INT1: an internal node of the certification tree), CA5 (pathLen 0, parent
+of INT2); NodeOUs client / peer / admin / orderer; one listed admin.  "Org2MSP": a root without a
+SubjectKeyIdentifier (the MSP would not set up: outside the model).  Leaves cover each rule of
+the miss path: role OUs, two role OUs, no OU, a listed admin, a high-S CA signature, unknown
+issuer, wrong CA key, an unhandled critical extension, a CA as an identity, SAN (DNS / URI), an
+empty validity window, Ed25519, a malformed IA5 OU, not PEM, a chain through an intermediate, an
+issuer that is an internal node, a path length exceeded."""
 from fabric_amd.synth import EdKey, Key, make_cert_ed25519
 from fabric_amd.synth import x509gen as G
 from fabric_amd.synth.blocks import serialized_identity
@@ -25,11 +28,17 @@ def _roles(*rs):
 
 def synthetic():
     """-> (config bytes, [(label, serialized, status, valid, roles)]) -- valid / roles only for OK"""
-    ca1, ca2, ca3 = Key(77, 1), Key(77, 2), Key(77, 3)
-    n1, n2, n3 = G.name("ca1.org1"), G.name("ca2.org1"), G.name("ca3.org1")
+    ca1, ca2, ca3, ca4, ca5 = Key(77, 1), Key(77, 2), Key(77, 3), Key(77, 4), Key(77, 5)
+    int1, int2 = Key(77, 6), Key(77, 7)
+    n1, n3, n4 = G.name("ca1.org1"), G.name("ca3.org1"), G.name("ca4.org1")
+    nI1, nI2 = G.name("int1.org1"), G.name("int2.org1")
     r1 = G.ca_cert(ca1, "ca1.org1")
-    r2 = G.ca_cert(ca2, "ca2.org1", with_ski=False)
     r3 = G.ca_cert(ca3, "ca3.org1", usage=(0,))
+    r4 = G.ca_cert(ca4, "ca4.org1")                       # parent of int1: an internal node
+    r5 = G.ca_cert(ca5, "ca5.org1", path_len=0)           # pathLen 0: no intermediate below int2
+    i1 = G.ca_cert(int1, "int1.org1", issuer_key=ca4, issuer_cn="ca4.org1", serial=11)
+    i2 = G.ca_cert(int2, "int2.org1", issuer_key=ca5, issuer_cn="ca5.org1", serial=12)
+    r2 = G.ca_cert(ca2, "ca2.org2", org="Org2", with_ski=False)  # Org2MSP: a root without SKI
     k = [Key(77, 100 + i) for i in range(40)]
 
     def leaf(i, ous, issuer_key=ca1, issuer=n1, **kw):
@@ -50,7 +59,10 @@ def synthetic():
     add("peer_plus_other_ou", leaf(7, ["dept1", "peer"]), OK, True, _roles(MEMBER, PEER))
     add("listed_admin", listed_admin, OK, True, _roles(MEMBER, ADMIN, CLIENT))
     add("high_s_ca_signature", leaf(9, ["peer"], high_s=True), OK, True, _roles(MEMBER, PEER))
-    add("ca_without_ski", leaf(10, ["peer"], issuer_key=ca2, issuer=n2), OK, False, 0)
+    add("via_intermediate", leaf(10, ["peer"], issuer_key=int1, issuer=nI1), OK, True, _roles(MEMBER, PEER))
+    add("issued_by_internal_ca", leaf(22, ["peer"], issuer_key=ca4, issuer=n4), OK, False, 0)
+    add("path_len_exceeded", leaf(23, ["peer"], issuer_key=int2, issuer=nI2), FAILED)
+    add("intermediate_as_identity", i1, UNSUP)
     add("unknown_issuer", leaf(11, ["peer"], issuer=G.name("ca.other")), FAILED)
     add("wrong_ca_key", leaf(12, ["peer"], issuer_key=ca2, issuer=n1), FAILED)
     add("unhandled_critical_ext", leaf(13, ["peer"], extensions=[G.ext("2a0304", b"\x05\x00", critical=True)]),
@@ -68,6 +80,10 @@ def synthetic():
     add("key_usage_critical_ok", leaf(21, ["client"], extensions=[G.key_usage((0,))]), OK, True,
         _roles(MEMBER, CLIENT))
     out.append(("repeat", out[0][1], REPEAT, None, None))  # the same bytes again in one call
-    fabric = fabric_msp_config(MSPID, root_certs=[r1, r2, r3], admins=[listed_admin])
-    cfg = make_config([MSPID], msp_configs={MSPID: fabric})
+    out.append(("msp_root_without_ski", serialized_identity("Org2MSP", leaf(24, ["peer"], issuer_key=ca2,
+                                                                           issuer=G.name("ca2.org2", "Org2"))),
+                UNSUP, None, None))
+    fabric = fabric_msp_config(MSPID, root_certs=[r1, r3, r4, r5], intermediate_certs=[i1, i2], admins=[listed_admin])
+    fabric2 = fabric_msp_config("Org2MSP", root_certs=[r2])
+    cfg = make_config([MSPID, "Org2MSP"], msp_configs={MSPID: fabric, "Org2MSP": fabric2})
     return cfg, out

@@ -78,7 +78,7 @@ def test_reference_msp_fixtures(rel):
 
 def test_synthetic_cases():
     cfg, cases = MC.synthetic()
-    m = v20.ChannelModel("ch", [], {}, config=cfg).msp_models()[MC.MSPID]
+    models = v20.ChannelModel("ch", [], {}, config=cfg).msp_models()
     eng = _lib.Engine(0)
     eng.channel_init("ch")
     eng.channel_config(cfg)
@@ -87,7 +87,7 @@ def test_synthetic_cases():
         if want == MC.REPEAT:
             assert st == MC.REPEAT, label
             continue
-        exp_st, ident = _expect(m, ser)
+        exp_st, ident = _expect(models.get(decode("SerializedIdentity", ser).get("mspid", "")), ser)
         assert exp_st == want, label
         _check(eng, ser, st, exp_st, ident, label)
         if want == MC.OK:

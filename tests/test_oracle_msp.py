@@ -101,9 +101,26 @@ def test_ca_certificate_as_identity_is_outside_the_model():
 
 
 def test_msps_outside_the_model():
-    for rel in ("msp/testdata/intermediate", "msp/testdata/revocation"):
+    for rel in ("msp/testdata/external", "msp/testdata/revocation"):  # CRL distribution points, CRLs
         with pytest.raises(Unsupported):
             _msp(rel)
+
+
+# ---- msp/mspwithintermediatecas_test.go
+def test_intermediate_ca_identity_validates():  # TestMSPWithIntermediateCAs
+    i = _one("intermediate", "signcerts")
+    assert i is not None and i.valid
+
+
+def test_identity_issued_by_an_internal_ca_is_invalid():  # TestMSPWithIntermediateCAs2
+    assert _one("intermediate2", "signcerts").valid
+    u = _ident("intermediate2", "users/user2-cert.pem")
+    assert u is not None and not u.valid  # deserializes; "Parent certificate should be a leaf"
+
+
+def test_intermediate_ca_as_identity():  # TestIntermediateCAIdentityValidity: CAs are no identities
+    with pytest.raises(Unsupported):
+        _one("intermediate", "intermediatecerts")
 
 
 # ---- the engine's CPU X.509 parser against the restatement
@@ -122,7 +139,7 @@ def _oracle_view(pem):
         return {"stage": "parse", "status": 2}
     h = lambda b: hashlib.sha256(b).hexdigest()
     v = {"stage": "ok", "status": 0, "key": {"p256": 1, "undeserializable": 4}[c["key"]], "version": c["version"],
-         "is_ca": int(c["is_ca"]), "bc_valid": int(c["bc_valid"]), "has_ski": int(c["ski"] is not None),
+         "is_ca": int(c["is_ca"]), "bc_valid": int(c["bc_valid"]), "path_len": c["path_len"], "has_ski": int(c["ski"] is not None),
          "key_usage": c["key_usage"], "unhandled_critical": int(c["unhandled_critical"]),
          "not_before": c["not_before"], "not_after": c["not_after"],
          "pub": c["pub"].hex() if c["pub"] else "", "tbs": h(c["tbs"]), "issuer": h(c["issuer"]),
@@ -211,12 +228,17 @@ def test_synthetic_cases_oracle():
     from oracle import v20
     from tests.msp_cases import FAILED, MSPID, OK, REPEAT, UNSUP, synthetic
     cfg, cases = synthetic()
-    m = v20.ChannelModel("ch", [], {}, config=cfg).msp_models()[MSPID]
-    assert not isinstance(m, Exception), m
+    models = v20.ChannelModel("ch", [], {}, config=cfg).msp_models()
+    assert not isinstance(models[MSPID], Exception), models[MSPID]
     for label, ser, st, valid, roles in cases:
         if st == REPEAT:
             continue
-        idb = decode("SerializedIdentity", ser).get("id_bytes") or b""
+        sid = decode("SerializedIdentity", ser)
+        m = models[sid.get("mspid", "")]
+        if isinstance(m, Exception):
+            assert st == UNSUP, label
+            continue
+        idb = sid.get("id_bytes") or b""
         try:
             got = m.resolve(idb)
         except Unsupported:
