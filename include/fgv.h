@@ -183,8 +183,9 @@ int fgv_ledger_add_txids(fgv_ctx *ctx, const uint8_t *buf, const uint64_t *off, 
  * deserialized here -- PEM, X.509 parse, the chain to a root (the CA signatures verified on the
  * GPU, one pass per call), sanitizeCert's low-S re-marshal, Id = SHA-256 of it, Validate's SKI /
  * OU rules and the role bits -- and registered like fgv_msp_register_identity (one that fails
- * DeserializeIdentity is registered as FGV_KEY_UNDESERIALIZABLE).  Modelled MSPs: root CAs only
- * (no intermediates, no CRLs), OU certificates that are roots, ECDSA P-256 / Ed25519 leaf keys.
+ * DeserializeIdentity is registered as FGV_KEY_UNDESERIALIZABLE).  Modelled MSPs: root and
+ * intermediate CAs (P-256, each a CA with a SubjectKeyIdentifier, unique issuer names), no CRLs,
+ * OU certificates that are CAs of the MSP, ECDSA P-256 / Ed25519 leaf keys.
  *   fgv_msp_resolve        -- n SerializedIdentity bytes -> status[i] FGV_RESOLVE_*
  *   fgv_msp_resolve_blocks -- every creator / endorser of the blocks the registry lacks;
  *                             *registered = identities added (NULL allowed)
