@@ -32,6 +32,7 @@ EXPORTED = [
     "fgv_validate_blocks_pipelined", "fgv_set_timing",
     "fgv_group_init", "fgv_group_destroy", "fgv_group_size", "fgv_group_ctx", "fgv_group_validate_blocks",
     "fgv_msp_resolve", "fgv_msp_resolve_blocks", "fgv_set_auto_resolve", "fgv_msp_identity",
+    "fgv_kvmeta_set", "fgv_kvmeta_count", "fgv_kvmeta_get",
 ]
 # fgv_msp_resolve status (include/fgv.h)
 RESOLVE_KNOWN, RESOLVE_OK, RESOLVE_FAILED, RESOLVE_UNSUPPORTED, RESOLVE_REPEAT = range(5)
@@ -121,6 +122,11 @@ def load():
         L.fgv_chaincode_define.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
         L.fgv_chaincode_define2.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_uint32]
         L.fgv_collection_define.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz]
+        L.fgv_kvmeta_set.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
+        L.fgv_kvmeta_count.argtypes = [vp]
+        L.fgv_kvmeta_count.restype = sz
+        L.fgv_kvmeta_get.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz, vp, sz,
+                                     ctypes.POINTER(ctypes.c_size_t)]
         L.fgv_channel_config.argtypes = [vp, ctypes.c_char_p, sz]
         L.fgv_msp_declare.argtypes = [vp, ctypes.c_char_p]
         L.fgv_msp_register_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(IdentityInfo)]
@@ -480,6 +486,27 @@ class Engine:
     def collection_define(self, ns: str, coll: str, policy: bytes = b""):
         """fgv_collection_define: policy b"" = none (the chaincode EP applies)"""
         _check(self._L.fgv_collection_define(self._h, ns.encode(), coll.encode(), policy or None, len(policy or b"")))
+
+    def kvmeta_set(self, ns: str, coll: str, key: bytes, vp: bytes = b""):
+        """fgv_kvmeta_set: the committed VALIDATION_PARAMETER of (ns, coll, key) (coll "" = a
+        public key, else the key hash); vp b"" removes it"""
+        key = key.encode() if isinstance(key, str) else bytes(key)
+        _check(self._L.fgv_kvmeta_set(self._h, ns.encode(), coll.encode(), key, len(key), vp or None, len(vp or b"")))
+
+    def kvmeta_count(self) -> int:
+        return int(self._L.fgv_kvmeta_count(self._h))
+
+    def kvmeta_get(self, ns: str, coll: str, key: bytes):
+        """the committed VALIDATION_PARAMETER the engine holds for (ns, coll, key), or None"""
+        key = key.encode() if isinstance(key, str) else bytes(key)
+        n = ctypes.c_size_t()
+        _check(self._L.fgv_kvmeta_get(self._h, ns.encode(), coll.encode(), key, len(key), None, 0, ctypes.byref(n)))
+        if n.value == 0:
+            return None
+        buf = ctypes.create_string_buffer(n.value)
+        _check(self._L.fgv_kvmeta_get(self._h, ns.encode(), coll.encode(), key, len(key), buf, n.value,
+                                      ctypes.byref(n)))
+        return buf.raw[:n.value]
 
     def channel_config(self, config: bytes):
         """fgv_channel_config: the channel's common.Config bytes"""

@@ -38,7 +38,13 @@ struct DSpan {  // bytes [off, off+len) of block `DevTx::blk`; len 0 == nil
   uint32_t off, len;
 };
 
-enum : uint8_t { BDF_INDEX_OK = 1, BDF_INDEX_FROM_TXID = 2, BDF_IDX_SHDR = 4 };
+enum : uint8_t { BDF_INDEX_OK = 1, BDF_INDEX_FROM_TXID = 2, BDF_IDX_SHDR = 4,
+                 BDF_VW = 8,      // a vscc that runs reads a written key (GetValidationParameterForKey)
+                 BDF_VANY = 16 }; // some vscc runs (PreValidate)
+// per-block dependency-extraction hazards (validator_keylevel.go:184-222), after the head's
+// counters: [2*blk] = 1 + the first batch tx index whose extraction fails, [2*blk+1] = the same
+// for a panic; 0 = a transaction before the shard; UINT32_MAX = none.  k_bd_fold: a tx t of the
+// block is past one iff the word <= t.
 
 struct DevTx {
   uint32_t blk;
@@ -87,8 +93,9 @@ struct DevPolicy {
   uint32_t sub0, nsub;  // DP_IMPLICIT: policy indices subs[sub0 .. sub0+nsub)
 };
 // chaincode table entry: namespace bytes, compiled EP, status (0 ok, 1 INVALID_CHAINCODE, 2
-// outside the model), collections known, its collections [coll0, coll0+ncoll) in the coll table
-#define BD_CC_WORDS 7
+// outside the model), collections known, its collections [coll0, coll0+ncoll) in the coll table,
+// key-level validation parameters in the state (writes to the namespace: host parser)
+#define BD_CC_WORDS 8
 // collection table entry: name bytes, EP (-1: the chaincode EP); implicit table: mspid bytes, EP
 #define BD_COLL_WORDS 3
 

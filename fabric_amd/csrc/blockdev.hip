@@ -284,11 +284,73 @@ DEV bool msp_known(const DevChannel &ch, S mspid) {
 }  // namespace
 
 // ============================================================ k_bd_parse
+// ChaincodeEndorsedAction decoded for its errors only (the dependency-extraction walk)
+struct VEndorsedActionChk {
+  S prp{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) { prp = s; return true; }
+    VTwoBytes e;
+    return decode(s, e, ovf);
+  }
+};
+struct VCcActionPayloadChk {
+  bool has_action = false;
+  VEndorsedActionChk action;  // every occurrence decoded into it (protobuf merge)
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_BYTES : n == 2 ? K_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == 1) return true;
+    has_action = true;
+    return decode(s, action, ovf);
+  }
+};
+enum : uint8_t { X_OK = 0, X_FAIL = 1, X_PANIC = 2, X_UNKNOWN = 0xFF };
+// metadata writes of a TxReadWriteSet (rwset.FromProtoBytes: a decode error -> none)
+DEV bool rwset_md(S results, ParseLds &L, uint32_t lane, bool &ovf) {
+  VTxRwSet rw;
+  rw.L = &L;
+  rw.lane = lane;
+  if (!decode(results, rw, ovf)) return false;
+  bool md = false;
+  for (uint32_t k = 0; k < rw.nns; k++) {
+    VKVRWSet kv;
+    if (!decode(L.rwset[k][lane], kv, ovf) || (L.cw[k][lane] & 2)) return false;
+    md |= kv.nmeta != 0 || (L.cw[k][lane] & 4) != 0;
+  }
+  return md;
+}
+// extractDependenciesForTx (validator_keylevel.go:184-222) for a tx whose validation walk
+// stopped before its ChaincodeAction (fgv_block.cpp extract_walk)
+DEV uint8_t extract_walk(S d, ParseLds &L, uint32_t lane, bool &md, bool &ovf) {
+  md = false;
+  VTwoBytes env;
+  if (!decode(d, env, ovf)) return X_FAIL;
+  VPayload pl;
+  if (!decode(env.a, pl, ovf)) return X_FAIL;
+  VTransaction tx;
+  if (!decode(pl.data, tx, ovf)) return X_FAIL;
+  if (tx.nact == 0) return X_PANIC;
+  VCcActionPayloadChk cap;
+  if (!decode(tx.first.b, cap, ovf)) return X_FAIL;
+  if (!cap.has_action) return X_PANIC;
+  VTwoBytes prp;
+  if (!decode(cap.action.prp, prp, ovf)) return X_FAIL;
+  VCcAction cca;
+  if (!decode(prp.b, cca, ovf)) return X_FAIL;
+  md = rwset_md(cca.results, L, lane, ovf);
+  return X_OK;
+}
+
 // fgv_block.cpp parse_tx, speculatively past the creator lookup (resolved by k_bd_ident;
 // k_bd_count applies the creator decision before anything downstream reads the rest).
+// Metadata writes and writes to namespaces with key-level parameters send the batch to the host
+// parser (flag 1); dependency-extraction failures and panics are recorded per block (xhaz).
 __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                  const uint64_t *__restrict__ bases, DevChannel ch,
-                                                 DevTx *__restrict__ out, uint32_t *__restrict__ flags) {
+                                                 DevTx *__restrict__ out, uint32_t *__restrict__ flags,
+                                                 uint32_t *__restrict__ xhaz) {
   // front half: below the back half's verify chain (3), above k_bd_sha_payload (1)
   __builtin_amdgcn_s_setprio(2);
   __shared__ ParseLds L;
@@ -320,6 +382,8 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
   R.npol = 0;
   R.nend = 0;
   bool ovf = false;
+  uint8_t xs = X_UNKNOWN;
+  bool md = false, vpns = false;
   do {
     VTwoBytes env;
     if (!decode(d, env, ovf)) { R.pre = C_OTHER; break; }
@@ -390,6 +454,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
     if (prp.b.n == 0) { R.disp = C_BAD_RESP; break; }
     VCcAction cca;
     if (!decode(prp.b, cca, ovf)) { R.disp = C_BAD_RESP; break; }
+    xs = X_OK;  // (the dependency extraction decodes the same messages)
     VTxRwSet rw;
     rw.L = &L;
     rw.lane = lane;
@@ -405,6 +470,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
                             (kv.nwrites ? 4 : 0));
     }
     if (bad_rw) { R.disp = ovf ? C_UNSUPPORTED : C_BAD_RWSET; break; }
+    for (uint32_t k = 0; k < rw.nns; k++) md |= (wflags[k] & 2) != 0;
     if (!ext.has_ccid || !cca.has_ccid) { R.disp = C_OTHER; break; }
     const S ccid = ext.ccid.name;
     if (ccid.n == 0 || !s_eq(ccid, cca.ccid.name) || cca.ccid.version.n == 0) { R.disp = C_INVALID_CC; break; }
@@ -420,10 +486,8 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
     // written namespaces + the invoked chaincode, sorted (Go string order)
     uint32_t nwr = 0;
     L.wr[nwr++][lane] = ccid;
-    bool unsup = false;
     for (uint32_t k = 0; k < rw.nns; k++) {
       if (!(wflags[k] & 1)) continue;
-      if (wflags[k] & 2) { unsup = true; break; }
       const S nk = L.ns[k][lane];
       if (!s_eq(nk, ccid)) {
         if (nwr == BD_MAX_POL) { ovf = true; break; }
@@ -431,7 +495,6 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
       }
     }
     if (ovf) break;
-    if (unsup) { R.disp = C_UNSUPPORTED; break; }
     for (uint32_t i = 1; i < nwr; i++)  // insertion sort
       for (uint32_t j = i; j > 0 && s_lt(L.wr[j][lane], L.wr[j - 1][lane]); j--) {
         const S tmp = L.wr[j][lane];
@@ -452,11 +515,16 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
       const int ci = cc_find(ch, wi);
       const uint32_t *e = ci >= 0 ? ch.cc + BD_CC_WORDS * ci : nullptr;
       if (!e || e[3] == 1) { push(-1); continue; }
+      R.flags |= BDF_VANY;
       if (e[3] != 0) { push(-2); continue; }
       const int32_t ep = (int32_t)e[2];
       int k = -1;
       for (uint32_t q = 0; q < rw.nns; q++)
         if (s_eq(L.ns[q][lane], wi)) { k = (int)q; break; }
+      if (k >= 0 && (wflags[k] & 1)) {
+        R.flags |= BDF_VW;
+        vpns |= e[7] != 0;
+      }
       bool any = false;
       if (k >= 0 && (wflags[k] & 4)) { push(ep); any = true; }
       if (k >= 0 && (L.cw[k][lane] & 1)) {
@@ -466,6 +534,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
         for (uint32_t c = 0; c < cn.n; c++) {
           any = true;
           const S nm = L.coll[c][lane];
+          if (nm.n == 0) { push(ep); continue; }  // the collection "": public metadata + the chaincode EP
           const uint32_t pl = 14;  // "_implicit_org_" (core/chaincode/implicitcollection/name.go:24-29)
           if (nm.n >= pl && ld4(nm.p) == 0x706d695fu /* _imp */ && ld4(nm.p + 4) == 0x6963696cu /* lici */ &&
               ld4(nm.p + 8) == 0x726f5f74u /* t_or */ && (ld4(nm.p + 12) & 0xFFFFu) == 0x5f67u /* g_ */) {
@@ -485,7 +554,10 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
     R.nend = (uint8_t)cap.action.nend;
     for (uint32_t q = 0; q < np; q++) O.pol[q] = L.pol[q][lane];
   } while (0);
-  if (ovf) atomicOr(flags, 1u);
+  if (xs == X_UNKNOWN && !ovf) xs = extract_walk(d, L, lane, md, ovf);
+  if (xs == X_FAIL) atomicMin(&xhaz[2 * blk], t + 1);
+  if (xs == X_PANIC) atomicMin(&xhaz[2 * blk + 1], t + 1);
+  if (ovf || md || vpns) atomicOr(flags, 1u);  // capacity, or key-level endorsement: host parser
   O.blk = R.blk;
   O.pre = R.pre;
   O.etx = R.etx;
@@ -1185,7 +1257,8 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
                                                  const uint32_t *__restrict__ totals,
                                                  const uint8_t *__restrict__ digests,
                                                  const uint8_t *__restrict__ vstatus,
-                                                 fgv_tx_result *__restrict__ res, uint32_t *__restrict__ flags) {
+                                                 fgv_tx_result *__restrict__ res, uint32_t *__restrict__ flags,
+                                                 const uint32_t *__restrict__ xhaz) {
   __builtin_amdgcn_s_setprio(3);  // back half; a next batch's front half may run beside it
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
@@ -1235,6 +1308,8 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
         code = C_DUP_TXID;
       } else if (R.disp != C_VALID) {
         code = R.disp;
+      } else if (((R.flags & BDF_VANY) && xhaz[2 * R.blk + 1] <= t) || ((R.flags & BDF_VW) && xhaz[2 * R.blk] <= t)) {
+        code = C_UNSUPPORTED;  // the reference panics / waits forever (validator_keylevel.go:184-241)
       } else {
         // SignatureSetToValidIdentities (policy.go:363-395): deserialize, dedup, verify -- when
         // some policy is evaluated

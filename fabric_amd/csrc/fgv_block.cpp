@@ -53,6 +53,10 @@ enum : uint8_t { C_VALID = 0, C_BAD_PAYLOAD = 2, C_BAD_HDR = 3, C_BAD_CREATOR = 
                  C_BAD_HDR_EXT = 19, C_BAD_RESP = 21, C_BAD_RWSET = 22, C_ILLEGAL_WS = 23,
                  C_INVALID_CC = 25, C_OTHER = 255, C_PENDING = 0xFE, C_UNSUPPORTED = 0xFD };
 
+// extractDependenciesForTx (validator_keylevel.go:184-222): an unmarshal error returns before
+// the dependency is signalled (X_FAIL), Actions[0] of none / a nil action panic (X_PANIC)
+enum : uint8_t { X_OK = 0, X_FAIL = 1, X_PANIC = 2, X_UNKNOWN = 0xFF };
+
 struct EndRec {
   int ident = -1;
   uint32_t vjob = UINT32_MAX;  // verify job (UINT32_MAX: no verification possible)
@@ -76,6 +80,13 @@ struct TxRec {
   // device job counts of this tx, by kind (filled after parsing; see the assembly stage)
   uint8_t n_cj = 0, n_tj = 0, n_pj = 0, n_ij = 0;
   uint16_t n_ej = 0;
+  // key-level endorsement (statebased/validator_keylevel.go, vpmanagerimpl.go)
+  uint8_t xstat = X_UNKNOWN;  // extractDependenciesForTx outcome (X_OK / X_FAIL / X_PANIC)
+  bool has_md = false;        // metadata writes (public or hashed) in some namespace
+  bool vw = false;            // some vscc that runs reads a written key (GetValidationParameterForKey)
+  bool vany = false;          // some vscc runs (PreValidate)
+  bool vpns = false;          // writes a namespace the state holds key-level parameters for
+  Span results, ccid;         // ChaincodeAction.results, the invoked chaincode
 
   void reset() {  // keep the vectors' capacity across calls
     std::vector<int> p = std::move(policies);
@@ -199,6 +210,7 @@ struct BdSet {
   hipEvent_t ev[9] = {};
   SplitOut so;
   bool presplit = false;
+  bool force_host = false;  // a shard's block prefix writes metadata (host parser)
   bool timed = false;  // its front half recorded the timing-only events
   hipStream_t stream = nullptr;  // the stream its parse / identity / count chain ran on
   size_t eoff = 0, moff = 0;
@@ -259,8 +271,56 @@ void fgv_parallel_for(fgv_block_state *S, size_t n, const std::function<void(siz
 void fgv_block_state_free(fgv_block_state *s) { delete s; }
 
 // ======================================================================= parsing
+// metadata writes in a TxReadWriteSet (rwset.FromProtoBytes: any decode error -> none)
+static bool rwset_has_md(const Span &results) {
+  VTxRwSet rw;
+  if (!pbw::decode(results.p, results.n, rw)) return false;
+  bool md = false;
+  for (size_t k = 0; k < rw.ns.size(); k++) {
+    VKVRWSet kv;
+    if (!pbw::decode(rw.ns[k].rwset.p, rw.ns[k].rwset.n, kv)) return false;
+    md |= kv.nmeta != 0;
+    for (const VCollHashed &c : rw.ns[k].coll) {
+      VHashedRWSet h;
+      if (!pbw::decode(c.hashed.p, c.hashed.n, h)) return false;
+      md |= h.nmeta != 0;
+    }
+  }
+  return md;
+}
+
+// extractDependenciesForTx (validator_keylevel.go:184-222) for a tx whose validation walk
+// stopped before its ChaincodeAction
+static void extract_walk(Span d, TxRec &R) {
+  R.xstat = X_FAIL;
+  VEnvelope env;
+  if (!pbw::decode(d.p, d.n, env)) return;
+  VPayload pl;
+  VHeader hdr;
+  if (!pbw::decode(env.payload.p, env.payload.n, pl) || !pl.header.decode_into(hdr)) return;
+  VTransaction tx;
+  if (!pbw::decode(pl.data.p, pl.data.n, tx)) return;
+  if (tx.actions.size() == 0) { R.xstat = X_PANIC; return; }
+  VCcActionPayload cap;
+  if (!pbw::decode(tx.actions[0].payload.p, tx.actions[0].payload.n, cap)) return;
+  if (!cap.has_action) { R.xstat = X_PANIC; return; }
+  VPrp prp;
+  if (!pbw::decode(cap.action.prp.p, cap.action.prp.n, prp)) return;
+  VCcAction cca;
+  if (!pbw::decode(prp.extension.p, prp.extension.n, cca)) return;
+  R.xstat = X_OK;
+  R.results = cca.results;
+  R.has_md = rwset_has_md(cca.results);
+}
+
+static void parse_tx_flow(const Channel &ch, Span d, TxRec &R);
 static void parse_tx(const Channel &ch, Span d, TxRec &R) {
   R.reset();
+  parse_tx_flow(ch, d, R);
+  if (R.xstat == X_UNKNOWN) extract_walk(d, R);
+}
+
+static void parse_tx_flow(const Channel &ch, Span d, TxRec &R) {
   VEnvelope env;
   if (!pbw::decode(d.p, d.n, env)) { R.pre = C_OTHER; return; }
   VPayload pl;
@@ -344,6 +404,8 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
   if (prp.extension.nil()) { R.disp = C_BAD_RESP; return; }
   VCcAction cca;
   if (!pbw::decode(prp.extension.p, prp.extension.n, cca)) { R.disp = C_BAD_RESP; return; }
+  R.xstat = X_OK;  // (the dependency extraction decodes the same messages)
+  R.results = cca.results;
   VTxRwSet rw;
   if (!pbw::decode(cca.results.p, cca.results.n, rw)) { R.disp = C_BAD_RWSET; return; }
   // per namespace: 1 = writes (kv / metadata / collection), 2 = metadata writes, 4 = public
@@ -364,8 +426,10 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
     wflags.push_back((uint8_t)(((kv.nwrites || kv.nmeta || coll_writes || coll_meta) ? 1 : 0) |
                                ((kv.nmeta || coll_meta) ? 2 : 0) | (kv.nwrites ? 4 : 0)));
   }
+  for (uint8_t f : wflags) R.has_md |= (f & 2) != 0;
   if (!ext.has_ccid || !cca.has_ccid) { R.disp = C_OTHER; return; }
   const Span ccid = ext.ccid.name;
+  R.ccid = ccid;
   if (ccid.n == 0 || !ccid.eq(reinterpret_cast<const char *>(cca.ccid.name.p), cca.ccid.name.n) ||
       cca.ccid.version.n == 0) {
     R.disp = C_INVALID_CC;
@@ -385,21 +449,20 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
   std::sort(nss.begin(), nss.end());
   for (size_t k = 1; k < nss.size(); k++)
     if (nss[k].eq(nss[k - 1])) { R.disp = C_ILLEGAL_WS; return; }
-  // written namespaces + the invoked chaincode; metadata (key-level endorsement) writes are
-  // outside the modelled state
+  // written namespaces + the invoked chaincode
   pbw::SmallVec<Span, 8> wr;
   wr.push_back(ccid);
   for (size_t k = 0; k < rw.ns.size(); k++) {
     if (!(wflags[k] & 1)) continue;
-    if (wflags[k] & 2) { R.disp = C_UNSUPPORTED; return; }  // (every such namespace is in wr)
     if (!rw.ns[k].ns.eq(ccid)) wr.push_back(rw.ns[k].ns);
   }
   std::sort(wr.begin(), wr.end());
   R.disp = C_VALID;
-  // the policies each namespace's vscc evaluates (statebased/validator_keylevel.go:173-233,
-  // v20.go:105-167, no key-level validation parameters): public writes -> the chaincode EP; a
-  // collection with hashed writes -> its collection EP (or the chaincode EP); none of these ->
-  // the chaincode EP.  -1: INVALID_CHAINCODE, -2: outside the model.
+  // the policies each namespace's vscc evaluates (statebased/validator_keylevel.go:87-143,
+  // v20.go:105-167) when no written key has a key-level parameter and no metadata is written
+  // (those txs take the sequential fold): public writes -> the chaincode EP; a collection with
+  // hashed writes -> its collection EP (or the chaincode EP; the collection "" is the public
+  // path); none of these -> the chaincode EP.  -1: INVALID_CHAINCODE, -2: outside the model.
   auto push = [&](int p) {
     if (std::find(R.policies.begin(), R.policies.end(), p) == R.policies.end()) R.policies.push_back(p);
   };
@@ -407,15 +470,21 @@ static void parse_tx(const Channel &ch, Span d, TxRec &R) {
     auto it = ch.ccs.find(ns.str());
     if (it == ch.ccs.end() || it->second.status == 1) { push(-1); continue; }
     const CCInfo &cc = it->second;
+    R.vany = true;
     if (cc.status != 0) { push(-2); continue; }
     int k = -1;
     for (size_t q = 0; q < rw.ns.size(); q++)
       if (rw.ns[q].ns.eq(ns)) { k = (int)q; break; }
+    if (k >= 0 && (wflags[k] & 1)) {
+      R.vw = true;
+      R.vpns |= cc.has_vp;
+    }
     bool any = false;
     if (k >= 0 && (wflags[k] & 4)) { push(cc.ep); any = true; }
     for (const auto &wc : wcolls) {
       if ((int)wc.first != k) continue;
       any = true;
+      if (wc.second.n == 0) { push(cc.ep); continue; }  // GetStateMetadata + CheckCCEPIfNotChecked(cc, "")
       const std::string coll = wc.second.str();
       if (coll.compare(0, strlen(kImplicitPrefix), kImplicitPrefix) == 0) {
         auto ie = ch.implicit_ep.find(coll.substr(strlen(kImplicitPrefix)));
@@ -544,6 +613,141 @@ static void count_jobs(const Channel &ch, TxRec &R) {
   for (const EndRec &e : R.ends)
     if (e.ident >= 0 && ch.idents[e.ident].verify_class() == 0) ne++;
   R.n_ej = (uint16_t)std::min<uint32_t>(ne, 0xFFFF);
+}
+
+// ======================================================================= key-level endorsement
+// KeyLevelValidationParameterManagerImpl's per-block state (vpmanagerimpl.go:113-233), restated
+// for a fold in block order: the metadata writers of every key, and each tx's vscc result per
+// namespace -- VR_PASS (nil), VR_FAIL, VR_INDET (whether it runs depends on Go map order);
+// absent: it never runs, so a later GetValidationParameterForKey waiting on it never returns.
+enum : int8_t { VR_FAIL = 0, VR_PASS = 1, VR_INDET = 2 };
+static inline std::string_view sv(const Span &s) { return std::string_view(reinterpret_cast<const char *>(s.p), s.n); }
+struct SbeBlock {
+  std::unordered_map<std::string, std::vector<uint32_t>> deps;  // kvkey -> metadata writers (tx index)
+  std::vector<std::vector<std::pair<std::string, int8_t>>> res;  // per tx index of the block
+  int result(uint32_t j, std::string_view ns) const {
+    if (j >= res.size()) return -1;
+    for (const auto &p : res[j])
+      if (p.first == ns) return p.second;
+    return -1;
+  }
+};
+
+// ExtractValidationParameterDependency (vpmanagerimpl.go:258-292): the metadata-write keys of
+// every namespace; a rwset that does not decode adds none
+static void add_deps(const Span &results, uint32_t i, SbeBlock &B) {
+  VTxRwSet rw;
+  if (!pbw::decode(results.p, results.n, rw)) return;
+  std::vector<std::string> keys;
+  for (const VNsRwSet &n : rw.ns) {
+    std::vector<Span> mk;
+    VKVRWSet kv;
+    kv.meta_keys = &mk;
+    if (!pbw::decode(n.rwset.p, n.rwset.n, kv)) return;
+    for (const Span &k : mk) keys.push_back(Channel::kvkey(sv(n.ns), "", sv(k)));
+    for (const VCollHashed &c : n.coll) {
+      std::vector<Span> hk;
+      VHashedRWSet h;
+      h.meta_keys = &hk;
+      if (!pbw::decode(c.hashed.p, c.hashed.n, h)) return;
+      for (const Span &k : hk) keys.push_back(Channel::kvkey(sv(n.ns), sv(c.name), sv(k)));
+    }
+  }
+  for (std::string &k : keys) B.deps[std::move(k)].push_back(i);
+}
+
+// The builtin vscc v20 of one namespace (validator_keylevel.go:87-143 over policyCheckerV20,
+// v20.go:105-167): per written key -- public writes, public metadata writes, hashed writes,
+// hashed metadata writes -- an earlier valid metadata writer fails it (ValidationParameterUpdated-
+// Error), else its key-level parameter, else CheckCCEPIfNotChecked; none -> the chaincode EP.
+// 1 nil, 0 an error, 2 outside the model.  Every step is evaluated (the reference returns at the
+// first error; the outcomes are pure, so the verdict is the same) and a step outside the model
+// anywhere makes the tx unsupported, as in the oracle.  `hang`: an earlier tx never signalled
+// its dependencies (GetValidationParameterForKey would wait forever).
+static int sbe_vscc(const Channel &ch, const CCInfo &cc, std::string_view ns, const VNsRwSet *nrw, uint32_t i,
+                    const SbeBlock &B, bool hang, const std::function<int(int)> &eval) {
+  int ok = 1;
+  bool some = false, cc_checked = false;
+  pbw::SmallVec<Span, 4> colls_checked;
+  auto step = [&](const Span &coll, const Span &key) -> bool {  // false: outside the model
+    some = true;
+    if (hang) return false;
+    auto d = B.deps.find(Channel::kvkey(ns, sv(coll), sv(key)));
+    bool updated = false;
+    if (d != B.deps.end())
+      for (uint32_t j : d->second) {
+        if (j >= i) continue;
+        const int r = B.result(j, ns);
+        if (r < 0 || r == VR_INDET) return false;
+        updated |= r == VR_PASS;
+      }
+    if (updated) { ok = 0; return true; }
+    const int pi = ch.kv_policy(ns, sv(coll), sv(key));
+    if (pi == -3) return false;
+    if (pi >= 0) {
+      const int v = eval(pi);
+      ok &= v;
+      return v != 2;
+    }
+    if (coll.n) {
+      for (const Span &c : colls_checked)
+        if (c.eq(coll)) return true;
+      const std::string cs = coll.str();
+      int cp;
+      if (cs.compare(0, strlen(kImplicitPrefix), kImplicitPrefix) == 0) {
+        auto ie = ch.implicit_ep.find(cs.substr(strlen(kImplicitPrefix)));
+        if (ie == ch.implicit_ep.end()) return false;
+        cp = ie->second;
+      } else {
+        if (!cc.colls_known) return false;
+        auto ce = cc.colls.find(cs);
+        if (ce == cc.colls.end()) { ok = 0; return true; }  // no such collection -> policyErr
+        cp = ce->second;
+      }
+      if (cp >= 0) {
+        const int v = eval(cp);
+        ok &= v;
+        colls_checked.push_back(coll);
+        return v != 2;
+      }
+    }
+    if (!cc_checked) {
+      const int v = eval(cc.ep);
+      ok &= v;
+      cc_checked = true;
+      return v != 2;
+    }
+    return true;
+  };
+  if (nrw) {
+    std::vector<VKVWrite> ws;
+    std::vector<Span> mk;
+    VKVRWSet kv;
+    kv.writes = &ws;
+    kv.meta_keys = &mk;
+    if (!pbw::decode(nrw->rwset.p, nrw->rwset.n, kv)) return 2;  // (decoded by the parse already)
+    std::vector<std::vector<VHashWrite>> hw(nrw->coll.size());
+    std::vector<std::vector<Span>> hm(nrw->coll.size());
+    for (size_t c = 0; c < nrw->coll.size(); c++) {
+      VHashedRWSet h;
+      h.writes = &hw[c];
+      h.meta_keys = &hm[c];
+      if (!pbw::decode(nrw->coll[c].hashed.p, nrw->coll[c].hashed.n, h)) return 2;
+    }
+    const Span pub{};
+    for (const VKVWrite &w : ws)
+      if (!step(pub, w.key)) return 2;
+    for (const Span &k : mk)
+      if (!step(pub, k)) return 2;
+    for (size_t c = 0; c < nrw->coll.size(); c++)
+      for (const VHashWrite &w : hw[c])
+        if (!step(nrw->coll[c].name, w.key)) return 2;
+    for (size_t c = 0; c < nrw->coll.size(); c++)
+      for (const Span &k : hm[c])
+        if (!step(nrw->coll[c].name, k)) return 2;
+  }
+  if (!some) return eval(cc.ep);  // CheckCCEPIfNoEPChecked (FAB-9473)
+  return ok;
 }
 
 static inline uint32_t sha_blocks(const ShaJob &j) { return (j.n[0] + j.n[1] + j.n[2] + 8) / 64 + 1; }
@@ -679,10 +883,45 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   auto t_fold = clk::now();
 
   // --- C. fold (code precedence, validator.go:297-453) + result records
+  // Blocks the reference cannot validate (key-level dependency tracking, validator_keylevel.go:
+  // 184-241): a tx whose dependency extraction failed before a later tx's vscc reads a written
+  // key, or panicked before a later tx's vscc runs.  Per block, the first such tx index; a shard
+  // starting inside a block walks the block's earlier transactions too.
+  std::vector<uint32_t> xfail(nblocks, UINT32_MAX), xpanic(nblocks, UINT32_MAX);
+  bool sequential = false;
+  std::vector<std::vector<std::pair<uint32_t, Span>>> pre_md(nblocks);  // prefix metadata writers
+  for (size_t b = 0; b < nblocks; b++)
+    for (uint32_t i = 0; i < lo[b]; i++) {
+      TxRec tmp;
+      extract_walk(envs[b][i], tmp);
+      if (tmp.xstat == X_FAIL) xfail[b] = std::min(xfail[b], i);
+      if (tmp.xstat == X_PANIC) xpanic[b] = std::min(xpanic[b], i);
+      if (tmp.has_md) pre_md[b].push_back({i, tmp.results}), sequential = true;
+    }
+  for (size_t t = 0; t < total; t++) {
+    const TxRec &R = recs[t];
+    const size_t b = where[t].first;
+    const uint32_t i = where[t].second;
+    if (R.xstat == X_FAIL) xfail[b] = std::min(xfail[b], i);
+    if (R.xstat == X_PANIC) xpanic[b] = std::min(xpanic[b], i);
+    sequential |= R.has_md || R.vpns;
+  }
+  // key-level endorsement state (a batch with metadata writes or writes to keys with parameters)
+  std::vector<SbeBlock> sbe(sequential ? nblocks : 0);
+  if (sequential) {
+    for (size_t b = 0; b < nblocks; b++) {
+      sbe[b].res.resize(hi[b]);
+      for (const auto &pm : pre_md[b]) add_deps(pm.second, pm.first, sbe[b]);
+    }
+    for (size_t t = 0; t < total; t++)
+      if (recs[t].has_md && recs[t].xstat == X_OK) add_deps(recs[t].results, where[t].second, sbe[where[t].first]);
+  }
   static const char HEX[] = "0123456789abcdef";
   std::atomic<bool> unsupported{false};
-  S->pool.parallel_for(total, [&](size_t t) {
+  auto fold_one = [&](size_t t) {
     const TxRec &R = recs[t];
+    const size_t b = where[t].first;
+    const uint32_t bi = where[t].second;
     uint8_t code;
     bool reached = false;
     if (R.pre != C_PENDING) {
@@ -709,35 +948,90 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         code = C_DUP_TXID;  // checkTxIdDupsLedger (initial ledger; batch-earlier blocks: finalize)
       } else if (R.disp != C_VALID) {
         code = R.disp;
+      } else if ((R.vany && xpanic[b] < bi) || (R.vw && xfail[b] < bi)) {
+        code = C_UNSUPPORTED;  // the reference panics / waits forever (validator_keylevel.go:184-241)
       } else {
         // SignatureSetToValidIdentities (policy.go:363-395): deserialize, dedup, verify; only
         // when some policy is evaluated
-        bool evaluates = false, unsup = false;
-        for (int pi : R.policies) evaluates |= pi >= 0;
         pbw::SmallVec<int, 16> ids;
-        if (evaluates) {
+        bool ids_done = false, ids_unsup = false;
+        auto get_ids = [&] {
+          if (ids_done) return;
+          ids_done = true;
           pbw::SmallVec<uint32_t, 16> seen;
           for (const EndRec &e : R.ends) {
-            if (e.ident == -2) { unsup = true; break; }
+            if (e.ident == -2) { ids_unsup = true; return; }
             if (e.ident < 0) continue;
             const Ident &I = ch.idents[e.ident];
             if (std::find(seen.begin(), seen.end(), I.canon) != seen.end()) continue;
             const int vc = I.verify_class();
-            if (vc == 2) { unsup = true; break; }
+            if (vc == 2) { ids_unsup = true; return; }
             if (vc == 1 || e.vjob == UINT32_MAX || vstatus[e.vjob] != 0) continue;
             seen.push_back(I.canon);
             ids.push_back(e.ident);
           }
+        };
+        bool has25 = false, has10 = false, unsup = false;
+        if (!sequential) {
+          for (int pi : R.policies) {
+            if (pi == -2) { unsup = true; break; }
+            if (pi == -1) { has25 = true; continue; }
+            get_ids();
+            if (ids_unsup) { unsup = true; break; }
+            const int v = eval_policy(ch, pi, ids.data(), ids.size());
+            if (v == 2) { unsup = true; break; }
+            if (v == 0) has10 = true;
+          }
+        } else {
+          // Dispatch over the written namespaces (dispatcher.go:185-214) with the key-level
+          // vscc; each namespace's result is recorded for the block's later transactions
+          auto eval = [&](int pi) -> int {
+            get_ids();
+            return ids_unsup ? 2 : eval_policy(ch, pi, ids.data(), ids.size());
+          };
+          VTxRwSet rw;
+          pbw::decode(R.results.p, R.results.n, rw);  // (decoded by the parse already)
+          pbw::SmallVec<Span, 8> wr;
+          pbw::SmallVec<int, 8> wk;
+          wr.push_back(R.ccid);
+          for (size_t k = 0; k < rw.ns.size(); k++) {
+            VKVRWSet kv;
+            pbw::decode(rw.ns[k].rwset.p, rw.ns[k].rwset.n, kv);
+            bool w = kv.nwrites || kv.nmeta;
+            for (const VCollHashed &c : rw.ns[k].coll) {
+              VHashedRWSet h;
+              pbw::decode(c.hashed.p, c.hashed.n, h);
+              w |= h.nwrites || h.nmeta;
+            }
+            if (w && !rw.ns[k].ns.eq(R.ccid)) wr.push_back(rw.ns[k].ns);
+          }
+          std::sort(wr.begin(), wr.end());
+          pbw::SmallVec<int, 8> rs;  // -1 INVALID_CHAINCODE, 0 / 1 vscc result, 2 outside the model
+          for (const Span &ns : wr) {
+            int k = -1;
+            for (size_t q = 0; q < rw.ns.size(); q++)
+              if (rw.ns[q].ns.eq(ns)) { k = (int)q; break; }
+            auto it = ch.ccs.find(ns.str());
+            int r;
+            if (it == ch.ccs.end() || it->second.status == 1) r = -1;
+            else if (it->second.status != 0) r = 2;
+            else r = sbe_vscc(ch, it->second, sv(ns), k >= 0 ? &rw.ns[k] : nullptr, bi, sbe[b],
+                              xfail[b] < bi, eval);
+            rs.push_back(r);
+          }
+          for (size_t q = 0; q < wr.size(); q++) {
+            unsup |= rs[q] == 2;
+            has25 |= rs[q] == -1;
+            has10 |= rs[q] == 0;
+          }
+          for (size_t q = 0; q < wr.size(); q++) {
+            if (rs[q] != 0 && rs[q] != 1) continue;
+            bool others = false;
+            for (size_t o = 0; o < wr.size(); o++) others |= o != q && (rs[o] == -1 || rs[o] == 0);
+            sbe[b].res[bi].push_back({wr[q].str(), others ? VR_INDET : (int8_t)rs[q]});
+          }
         }
-        bool has25 = false, has10 = false;
         code = C_VALID;
-        for (int pi : R.policies) {
-          if (unsup || pi == -2) { unsup = true; break; }
-          if (pi == -1) { has25 = true; continue; }
-          const int v = eval_policy(ch, pi, ids.data(), ids.size());
-          if (v == 2) { unsup = true; break; }
-          if (v == 0) has10 = true;
-        }
         if (unsup) code = C_UNSUPPORTED;
         else if (has25 && has10) code = C_UNSUPPORTED;  // Go map order decides the reported code
         else if (has25) code = C_INVALID_CC;
@@ -762,7 +1056,11 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         o.flags |= FGV_TXR_INDEXED;
       }
     }
-  });
+  };
+  if (sequential)  // block order: a tx reads the vscc results of earlier ones
+    for (size_t t = 0; t < total; t++) fold_one(t);
+  else
+    S->pool.parallel_for(total, fold_one);
   c->t_host_fold = ms_since(t_fold);
   if (unsupported) return FGV_EUNSUPPORTED;
   return FGV_OK;
@@ -887,6 +1185,34 @@ int fgv_block_define_collection(fgv_block_state *S, const char *ns, const char *
   return FGV_OK;
 }
 
+int fgv_block_kvmeta_set(fgv_block_state *S, const std::string &ns, const std::string &coll, const uint8_t *key,
+                         size_t key_len, const uint8_t *vp, size_t vp_len) {
+  Channel &ch = S->ch;
+  const std::string k = Channel::kvkey(ns, coll, std::string(reinterpret_cast<const char *>(key), key_len));
+  auto it = ch.kvmeta.find(k);
+  if (vp_len == 0) {
+    if (it == ch.kvmeta.end()) return FGV_OK;
+    ch.kvmeta.erase(it);
+    if (--ch.kvmeta_ns[ns] == 0) ch.kvmeta_ns.erase(ns);
+  } else if (it == ch.kvmeta.end()) {
+    ch.kvmeta.emplace(k, std::string(reinterpret_cast<const char *>(vp), vp_len));
+    ch.kvmeta_ns[ns]++;
+  } else {
+    it->second.assign(reinterpret_cast<const char *>(vp), vp_len);
+  }
+  S->dev_dirty = true;
+  S->ch.dirty = true;
+  return FGV_OK;
+}
+
+size_t fgv_block_kvmeta_count(fgv_block_state *S) { return S->ch.kvmeta.size(); }
+
+const std::string *fgv_block_kvmeta_get(fgv_block_state *S, const std::string &ns, const std::string &coll,
+                                        const uint8_t *key, size_t key_len) {
+  auto it = S->ch.kvmeta.find(Channel::kvkey(ns, coll, std::string_view(reinterpret_cast<const char *>(key), key_len)));
+  return it == S->ch.kvmeta.end() ? nullptr : &it->second;
+}
+
 int fgv_block_channel_config(fgv_block_state *S, const uint8_t *config, size_t len) {
   RawConfig rc;
   if (!parse_channel_config(config, len, rc)) return FGV_EINVAL;
@@ -996,6 +1322,7 @@ static int build_dev_image(fgv_block_state *S) {
     cc.push_back(c.colls_known ? 1u : 0u);
     cc.push_back((uint32_t)(colls.size() / BD_COLL_WORDS));
     cc.push_back((uint32_t)c.colls.size());
+    cc.push_back(c.has_vp ? 1u : 0u);
     for (const auto &cl : c.colls) {
       str(cl.first, colls);
       colls.push_back((uint32_t)cl.second);
@@ -1113,7 +1440,7 @@ static int build_committed(fgv_block_state *S) {
 }
 
 __global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, DevChannel ch, DevTx *out,
-                           uint32_t *flags);
+                           uint32_t *flags, uint32_t *xhaz);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
@@ -1129,13 +1456,14 @@ __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases,
                           uint32_t *key_slot, uint32_t *dig_idx, uint32_t *nv_out);
 __global__ void k_bd_fold(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
                           const DevJobIdx *jobs, const uint32_t *totals, const uint8_t *digests,
-                          const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags);
+                          const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags, const uint32_t *xhaz);
 
 // The batch head, one H2D copy: envelope table | block base addresses | 64 zero bytes (the
-// kernels' counters), each part 64-byte aligned.
+// kernels' counters) | per-block dependency-extraction hazards (blockdev.h), each part 64-byte
+// aligned.
 static size_t head_env_bytes(size_t total) { return (total * 4 * BD_ENV_WORDS + 63) & ~(size_t)63; }
 static size_t head_bytes(size_t total, size_t nblocks) {
-  return head_env_bytes(total) + ((nblocks * 8 + 63) & ~(size_t)63) + 64;
+  return head_env_bytes(total) + 2 * ((nblocks * 8 + 63) & ~(size_t)63) + 64;
 }
 
 // host: split each block into envelope spans (tag / length walk of the block data framing)
@@ -1207,6 +1535,22 @@ bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t le
   return true;
 }
 
+// The dependency-extraction hazards of transactions [0, lo) of a block (a shard starting inside
+// it): extraction failures, panics, metadata writes.
+static void prefix_hazards(const uint8_t *blk, size_t len, uint32_t lo, uint8_t &fail, uint8_t &panic, bool &md) {
+  fail = panic = 0;
+  md = false;
+  VBlock B;
+  if (!pbw::decode(blk, len, B)) return;
+  for (uint32_t i = 0; i < lo && i < B.data.data.size(); i++) {
+    TxRec tmp;
+    extract_walk(B.data.data[i], tmp);
+    fail |= tmp.xstat == X_FAIL;
+    panic |= tmp.xstat == X_PANIC;
+    md |= tmp.has_md;
+  }
+}
+
 // Front half of a batch into set B, on the side streams: envelope spans (pre-split or walked
 // here), head upload, k_bd_sha_payload (stream2), k_bd_parse -> k_bd_ident -> k_bd_count ->
 // job counters in device memory (streamF), k_bd_sha (stream3).  `wait` (optional): an event the head
@@ -1259,6 +1603,20 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   uint64_t *bs = reinterpret_cast<uint64_t *>(head + B.eoff);
   for (size_t b = 0; b < nblocks; b++) bs[b] = (uint64_t)(uintptr_t)d_blocks[b];
   memset(head + B.moff, 0, 64);
+  // dependency-extraction hazards: none yet; a shard starting inside a block walks the block's
+  // earlier transactions (their metadata writes would need their vscc results: host parser)
+  uint32_t *xh = reinterpret_cast<uint32_t *>(head + B.moff + 64);
+  B.force_host = false;
+  for (size_t b = 0; b < nblocks; b++) {
+    xh[2 * b] = xh[2 * b + 1] = UINT32_MAX;
+    if (!tx_lo || tx_lo[b] == 0 || tx_lo[b] == FGV_SHARD_SKIP) continue;
+    uint8_t fail, panic;
+    bool md;
+    prefix_hazards(h_blocks[b], lens[b], tx_lo[b], fail, panic, md);
+    if (fail) xh[2 * b] = 0;
+    if (panic) xh[2 * b + 1] = 0;
+    B.force_host |= md;
+  }
   const DevChannel ch = S->dimg.ch;
   B.stream = sf;
   if (wait) HIP_TRY(hipStreamWaitEvent(sf, wait, 0));
@@ -1280,7 +1638,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(128), 0, c->stream2, N, envtab, dbs,
                      B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
   HIP_TRY(hipEventRecord(B.ev[1], c->stream2));
-  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5);
+  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16);
   HIP_TRY(hipEventRecord(B.ev[4], sf));
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one
@@ -1397,7 +1755,7 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   // (the digests were joined before k_prep: the verify stages always run, for the capacity)
   if (tim) HIP_TRY(hipEventRecord(c->kev[8], st));
   hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
-                     B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5);
+                     B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5, misc + 16);
   HIP_TRY(hipGetLastError());
   if (tim || c->ahead_mode == 3) HIP_TRY(hipEventRecord(c->kev[9], st));  // (ahead mode 3 waits on it)
   HIP_TRY(hipMemcpyAsync(B.misc.p, misc, 48, hipMemcpyDeviceToHost, st));
@@ -1469,7 +1827,7 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   if (B.N) S->nv_per_tx = (double)hm[10] / B.N;  // the next batch's lanes-per-verify estimate
   c->t_host_device = std::chrono::duration<double, std::milli>(clk::now() - S->t_enq).count();
   c->t_host_fold = 0;
-  if (hm[5] & 1u) return 1;
+  if ((hm[5] & 1u) || B.force_host) return 1;
   if (hm[5] & 2u) return FGV_EUNSUPPORTED;
   return FGV_OK;
 }

@@ -256,7 +256,18 @@ void Channel::compile() {
       c.colls_known = (d.flags & FGV_CC_COLLECTIONS_KNOWN) != 0;
       for (const auto &cl : d.colls) c.colls[cl.first] = cl.second.empty() ? -1 : compile_app(cl.second);
     }
+    c.has_vp = kvmeta_ns.count(kv.first) != 0;
     ccs[kv.first] = std::move(c);
+  }
+  // key-level validation parameters: toApplicationPolicyTranslator (builtin/v20/
+  // validation_logic.go:50-66) wraps the SignaturePolicyEnvelope as an ApplicationPolicy, which
+  // the evaluator takes without the version check; an envelope that does not unmarshal fails
+  // the translation
+  kvmeta_pi.clear();
+  for (const auto &kv : kvmeta) {
+    std::vector<Span> one{Span{reinterpret_cast<const uint8_t *>(kv.second.data()), (uint32_t)kv.second.size()}};
+    Policy P = compile_spe(*this, one, false);
+    kvmeta_pi[kv.first] = (P.kind == PK_SIG && !P.decode_ok) ? -3 : push_policy(*this, std::move(P));
   }
   dirty = false;
 }

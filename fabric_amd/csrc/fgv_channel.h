@@ -96,6 +96,7 @@ struct CCInfo {  // compiled
   int ep = 0;
   bool colls_known = false;
   std::map<std::string, int> colls;  // -1 = the chaincode EP
+  bool has_vp = false;               // the state holds key-level validation parameters of this namespace
 };
 
 struct Channel {
@@ -115,7 +116,28 @@ struct Channel {
   std::unordered_map<std::string, CCInfo> ccs;
   std::unordered_map<std::string, int> implicit_ep;  // mspid -> EP of _implicit_org_<mspid>
   std::map<std::string, int> chan_idx;               // channel policy path -> index
+  // committed key-level validation parameters (fgv_kvmeta_set): kvkey(ns, coll, key) -> the
+  // VALIDATION_PARAMETER bytes (a SignaturePolicyEnvelope); entries per namespace
+  std::unordered_map<std::string, std::string> kvmeta;
+  std::unordered_map<std::string, uint32_t> kvmeta_ns;
+  // compiled: kvkey -> policy index, or -3 when it does not unmarshal (the translation fails:
+  // VSCCExecutionFailureError, the reference halts)
+  std::unordered_map<std::string, int> kvmeta_pi;
   bool dirty = true;
+
+  static std::string kvkey(std::string_view ns, std::string_view coll, std::string_view key) {
+    std::string k;
+    k.reserve(8 + ns.size() + coll.size() + key.size());
+    const uint32_t a = (uint32_t)ns.size(), b = (uint32_t)coll.size();
+    k.append(reinterpret_cast<const char *>(&a), 4).append(ns).append(reinterpret_cast<const char *>(&b), 4);
+    return k.append(coll).append(key);
+  }
+  // -1: no parameter, -3: untranslatable, else the compiled policy
+  int kv_policy(std::string_view ns, std::string_view coll, std::string_view key) const {
+    if (kvmeta_pi.empty()) return -1;
+    auto it = kvmeta_pi.find(kvkey(ns, coll, key));
+    return it == kvmeta_pi.end() ? -1 : it->second;
+  }
 
   int32_t intern(const std::string &msp) {
     auto it = msp_ids.find(msp);

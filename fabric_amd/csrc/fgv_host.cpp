@@ -858,6 +858,29 @@ int fgv_collection_define(fgv_ctx *c, const char *ns, const char *coll, const ui
   return fgv_block_define_collection(c->blk, ns, coll, policy, len);
 }
 
+int fgv_kvmeta_set(fgv_ctx *c, const char *ns, const char *coll, const uint8_t *key, size_t key_len,
+                   const uint8_t *vp, size_t vp_len) {
+  if (!c || !ns || (key_len && !key) || (vp_len && !vp)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_kvmeta_set(c->blk, ns, coll ? coll : "", key, key_len, vp, vp_len);
+}
+
+int fgv_kvmeta_get(fgv_ctx *c, const char *ns, const char *coll, const uint8_t *key, size_t key_len, uint8_t *buf,
+                   size_t cap, size_t *len) {
+  if (!c || !ns || !len || (key_len && !key) || (cap && !buf)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  const std::string *v = fgv_block_kvmeta_get(c->blk, ns, coll ? coll : "", key, key_len);
+  *len = v ? v->size() : 0;
+  if (v && cap) memcpy(buf, v->data(), std::min(cap, v->size()));
+  return FGV_OK;
+}
+
+size_t fgv_kvmeta_count(fgv_ctx *c) {
+  if (!c) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_kvmeta_count(c->blk);
+}
+
 int fgv_channel_config(fgv_ctx *c, const uint8_t *config, size_t len) {
   if (!c || (len && !config)) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);

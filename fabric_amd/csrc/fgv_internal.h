@@ -208,6 +208,11 @@ int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const char *p
                                size_t len, uint32_t flags);
 int fgv_block_define_collection(fgv_block_state *S, const char *ns, const char *coll, const uint8_t *policy,
                                 size_t len);
+int fgv_block_kvmeta_set(fgv_block_state *S, const std::string &ns, const std::string &coll, const uint8_t *key,
+                         size_t key_len, const uint8_t *vp, size_t vp_len);
+size_t fgv_block_kvmeta_count(fgv_block_state *S);
+const std::string *fgv_block_kvmeta_get(fgv_block_state *S, const std::string &ns, const std::string &coll,
+                                        const uint8_t *key, size_t key_len);
 int fgv_block_channel_config(fgv_block_state *S, const uint8_t *config, size_t len);
 int fgv_block_declare_msp(fgv_block_state *S, const char *mspid);
 int fgv_block_add_txids(fgv_block_state *S, const uint8_t *buf, const uint64_t *off, const uint32_t *len,

@@ -284,14 +284,24 @@ struct HRQ {  // RangeQueryInfo
     return pbw::decode(s.p, s.n, m);
   }
 };
+struct HMetaEntry {  // KVMetadataEntry {name string 1, value bytes 2}
+  Span name, value;
+  Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) { (n == 1 ? name : value) = s; return true; }
+};
 struct HMetaW {  // KVMetadataWrite {key string 1, entries 2} / KVMetadataWriteHash {key_hash bytes 1, entries 2}
   bool hashed = false;
   Span key;
+  Span vp;  // the VALIDATION_PARAMETER entry (the last one: statemetadata.Deserialize's map)
   Kind kind(uint32_t n) { return n == 1 ? (hashed ? K_BYTES : K_STRING) : n == 2 ? K_REP_MSG : K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
-    if (n == 1) key = s;
-    return true;  // (entries: validated by the device pass; their bytes never affect a version)
+    if (n == 1) { key = s; return true; }
+    HMetaEntry e;
+    if (!pbw::decode(s.p, s.n, e)) return false;
+    if (e.name.eq("VALIDATION_PARAMETER", 20)) vp = e.value;
+    return true;
   }
 };
 struct HRW {  // KVRWSet / HashedRWSet
@@ -300,6 +310,7 @@ struct HRW {  // KVRWSet / HashedRWSet
   std::vector<HRQ> rqs;
   std::vector<HWrite> writes;
   std::vector<Span> meta;  // keys of the metadata writes
+  std::vector<Span> meta_vp;  // their VALIDATION_PARAMETER values (empty: none)
   Kind kind(uint32_t n) { return (n >= 1 && n <= (hashed ? 3u : 4u)) ? K_REP_MSG : K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
@@ -327,6 +338,7 @@ struct HRW {  // KVRWSet / HashedRWSet
     m.hashed = hashed;
     if (!pbw::decode(s.p, s.n, m)) return false;
     meta.push_back(m.key);
+    meta_vp.push_back(m.vp);
     return true;
   }
 };
@@ -380,6 +392,12 @@ struct TxNs {  // one NsReadWriteSet, decoded
   std::string ns;
   HRW kv;
   std::vector<std::pair<std::string, HRW>> colls;  // flattened hashed ns, hashed rwset
+  std::vector<std::string> coll_names;
+};
+// a change of a key's VALIDATION_PARAMETER in the committed state (fgv_kvmeta_set)
+struct KvOp {
+  std::string ns, coll, key;
+  Span vp;  // empty: none
 };
 std::string sv(const Span &s) { return std::string(reinterpret_cast<const char *>(s.p), s.n); }
 // (namespace, key) as one map key: 4-byte namespace length, namespace, key (keys and hashed
@@ -614,6 +632,7 @@ static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, ui
         hr.hashed = true;
         if (!pbw::decode(cl.hashed.p, cl.hashed.n, hr)) return FGV_EUNSUPPORTED;
         e.colls.emplace_back(e.ns + "$$h" + sv(cl.name), std::move(hr));
+        e.coll_names.push_back(sv(cl.name));
       }
       txs[i].push_back(std::move(e));
     }
@@ -777,6 +796,7 @@ static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, ui
     if (!present || !r.has_ver) return present == r.has_ver;  // version.AreSame (nil <=> absent)
     return v == Ver{r.v.b, r.v.t};
   };
+  std::vector<KvOp> kvops;                   // key-level parameter changes, in block order
   std::vector<size_t> rq_base(ntx + 1, 0);  // the first range index of each tx
   for (size_t i = 0; i < ntx; i++) {
     size_t k = 0;
@@ -864,6 +884,39 @@ static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, ui
       if (m.hashed) hsh[flat_key(m.ns, m.key)] = Upd{h, false};
       else pub[m.ns][m.key] = Upd{h, false};
     }
+    // the keys' metadata (statedb VALIDATION_PARAMETER, tx_ops.go:17-53 + 97-148): a delete drops
+    // it, an upsert keeps it, a metadata write beside an upsert replaces it, a metadata-only
+    // write replaces it when the key exists (its update now carries this tx's height)
+    for (const TxNs &e : txs[i]) {
+      auto track = [&](const std::string &coll, const std::string &fns, const HRW &rw) {
+        for (const HWrite &w : rw.writes)
+          if (is_delete(w)) kvops.push_back(KvOp{e.ns, coll, sv(w.key), Span{}});
+        for (size_t m = 0; m < rw.meta.size(); m++) {
+          const HWrite *w = nullptr;
+          for (const HWrite &x : rw.writes)
+            if (x.key.eq(rw.meta[m])) w = &x;
+          if (w) {
+            if (!is_delete(*w)) kvops.push_back(KvOp{e.ns, coll, sv(rw.meta[m]), rw.meta_vp[m]});
+            continue;
+          }
+          const std::string key = sv(rw.meta[m]);
+          bool ex = false;
+          if (rw.hashed) {
+            auto it = hsh.find(flat_key(fns, key));
+            ex = it != hsh.end() && it->second.v == h;
+          } else {
+            auto it = pub.find(fns);
+            if (it != pub.end()) {
+              auto k = it->second.find(key);
+              ex = k != it->second.end() && k->second.v == h;
+            }
+          }
+          if (ex) kvops.push_back(KvOp{e.ns, coll, key, rw.meta_vp[m]});
+        }
+      };
+      track("", e.ns, e.kv);
+      for (size_t k = 0; k < e.colls.size(); k++) track(e.coll_names[k], e.colls[k].first, e.colls[k].second);
+    }
   }
   if (!commit) return FGV_OK;
   // 4. commit the update batch: one upsert per flattened namespace (capacity checked first, so
@@ -901,6 +954,36 @@ static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, ui
     rc = upsert_host(c, g.first.c_str(), reinterpret_cast<const uint8_t *>(kb.data()), off.data(), len.data(), blk.data(),
                      txn.data(), del.data(), g.second.size());
     if (rc) return rc;
+  }
+  for (const KvOp &o : kvops)
+    fgv_block_kvmeta_set(c->blk, o.ns, o.coll, reinterpret_cast<const uint8_t *>(o.key.data()), o.key.size(), o.vp.p,
+                         o.vp.n);
+  return FGV_OK;
+}
+
+// A block committed by the device path (no metadata writes): its valid deletes drop the deleted
+// keys' validation parameters
+static int kvmeta_deletes(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, const uint8_t *flags, size_t ntx) {
+  std::vector<MvTxInfo> info(ntx);
+  HIP_TRY(hipMemcpy(info.data(), M->info.p, ntx * sizeof(MvTxInfo), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < ntx; i++) {
+    if (flags[i] != 0 || info[i].code != 0) continue;
+    HTxRW rw;
+    if (!pbw::decode(block + info[i].rws_off, info[i].rws_len, rw)) continue;
+    for (const HNs &n : rw.ns) {
+      HRW kv;
+      if (!pbw::decode(n.rwset.p, n.rwset.n, kv)) continue;
+      const std::string ns = sv(n.ns);
+      for (const HWrite &w : kv.writes)
+        if (is_delete(w)) fgv_block_kvmeta_set(c->blk, ns, "", w.key.p, w.key.n, nullptr, 0);
+      for (const HColl &cl : n.colls) {
+        HRW hr;
+        hr.hashed = true;
+        if (!pbw::decode(cl.hashed.p, cl.hashed.n, hr)) continue;
+        for (const HWrite &w : hr.writes)
+          if (is_delete(w)) fgv_block_kvmeta_set(c->blk, ns, sv(cl.name), w.key.p, w.key.n, nullptr, 0);
+      }
+    }
   }
   return FGV_OK;
 }
@@ -1042,6 +1125,7 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
     if (hc->nomem) return FGV_ENOMEM;  // nothing was committed
   }
   memcpy(flags, M->htail.as<uint8_t>() + kCounterBytes, ntx);
+  if (commit && fgv_block_kvmeta_count(c->blk) > 0) return kvmeta_deletes(c, M, block, flags, ntx);
   return FGV_OK;
 }
 

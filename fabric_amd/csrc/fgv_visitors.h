@@ -243,10 +243,11 @@ struct VMetaEntry {
   bool on_len(uint32_t, Span) { return true; }
 };
 struct VMetaWrite {  // KVMetadataWrite {key string=1, entries=2}
+  Span key;
   pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_STRING : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
-    if (n == 1) return true;
+    if (n == 1) { key = s; return true; }
     VMetaEntry e;
     return pbw::decode(s.p, s.n, e);
   }
@@ -255,6 +256,7 @@ struct VKVRWSet {
   uint32_t nreads = 0, nrq = 0, nwrites = 0, nmeta = 0;
   std::vector<VKVRead> *reads = nullptr;     // optional capture (MVCC)
   std::vector<VKVWrite> *writes = nullptr;
+  std::vector<Span> *meta_keys = nullptr;    // optional capture (key-level endorsement)
   pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 4) ? pbw::K_REP_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
@@ -275,7 +277,9 @@ struct VKVRWSet {
     }
     nmeta++;
     VMetaWrite m;
-    return pbw::decode(s.p, s.n, m);
+    if (!pbw::decode(s.p, s.n, m)) return false;
+    if (meta_keys) meta_keys->push_back(m.key);
+    return true;
   }
 };
 struct VHashRead {  // KVReadHash {key_hash bytes=1, version=2}
@@ -297,11 +301,12 @@ struct VHashWrite {  // KVWriteHash {key_hash=1, is_delete=2, value_hash=3, is_p
   void on_varint(uint32_t n, uint64_t v) { if (n == 2) is_delete = v != 0; }
   bool on_len(uint32_t n, Span s) { (n == 1 ? key : value_hash) = s; return true; }
 };
-struct VHashMeta {
+struct VHashMeta {  // KVMetadataWriteHash {key_hash bytes=1, entries=2}
+  Span key;
   pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : n == 2 ? pbw::K_REP_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
-    if (n == 1) return true;
+    if (n == 1) { key = s; return true; }
     VMetaEntry e;
     return pbw::decode(s.p, s.n, e);
   }
@@ -310,6 +315,7 @@ struct VHashedRWSet {
   uint32_t nreads = 0, nwrites = 0, nmeta = 0;
   std::vector<VHashRead> *reads = nullptr;  // optional capture (MVCC)
   std::vector<VHashWrite> *writes = nullptr;
+  std::vector<Span> *meta_keys = nullptr;   // optional capture (key-level endorsement)
   pbw::Kind kind(uint32_t n) { return (n >= 1 && n <= 3) ? pbw::K_REP_MSG : pbw::K_NONE; }
   void on_varint(uint32_t, uint64_t) {}
   bool on_len(uint32_t n, Span s) {
@@ -329,7 +335,9 @@ struct VHashedRWSet {
     }
     nmeta++;
     VHashMeta m;
-    return pbw::decode(s.p, s.n, m);
+    if (!pbw::decode(s.p, s.n, m)) return false;
+    if (meta_keys) meta_keys->push_back(m.key);
+    return true;
   }
 };
 struct VCollHashed {

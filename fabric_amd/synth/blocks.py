@@ -285,13 +285,14 @@ class _Tx:
 
 def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FAULTS_C2, endorse_dist=((2, 0.6), (3, 0.4)),
                reads=4, writes=4, value_len=200, threads=8, prev_hash=b"\x00" * 32, force=None, ns="mycc",
-               key_space=1_000_000, reuse=None, out_txs=None, collections=None):
+               key_space=1_000_000, reuse=None, out_txs=None, collections=None, rwsets=None):
     """Returns (block_bytes, labels list, envelopes list).
     reuse: {tx index: (creator Identity, nonce)} -> that tx re-uses an earlier txid (label
     'dup_txid_prev'); out_txs: list that receives the generated tx objects; collections: names
     of private-data collections -- every tx then also writes one key hash into one of them
     (chosen per tx), so its namespace checks that collection's endorsement policy (the codes
-    are then the oracle's to decide, labels stay as generated)."""
+    are then the oracle's to decide, labels stay as generated); rwsets: the TxReadWriteSet bytes
+    of each tx instead of the generated ones (codes then the oracle's to decide)."""
     rng = random.Random((net.seed << 20) ^ (number << 4) ^ seed)
     txs = []
     fault_names = [f for f, _ in faults]
@@ -302,6 +303,7 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         cum.append(acc)
     for i in range(ntx):
         t = _Tx()
+        t.index = i
         u = rng.random()
         t.label = "clean"
         for name, c in zip(fault_names, cum):
@@ -387,6 +389,8 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
                             [(t.coll, hashed_rwset([], [(kh, hashlib.sha256(kh).digest(), False)]))])])
         else:
             rw = tx_rwset([(ccname, kv_rwset(t.reads, t.writes))])
+        if rwsets is not None:
+            rw = rwsets[t.index]
         events = b""
         if t.label == "event_other_cc":
             events = f_str(1, "someothercc") + f_str(3, "ev")

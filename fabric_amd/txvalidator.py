@@ -38,11 +38,13 @@ def _as_identity(entry):
     return ser, Identity(mspid, pub, valid, dig, key="p256" if pub is not None else "other")
 
 
-def setup_channel(engine: Engine, channel: str, identities, chaincodes, committed_txids=(), config=None, msps=()):
+def setup_channel(engine: Engine, channel: str, identities, chaincodes, committed_txids=(), config=None, msps=(),
+                  kvmeta=None):
     """identities: iterable of (serialized, Identity) or (serialized, mspid, pubkey64 | None,
     valid, id_digest).  chaincodes: ns -> ApplicationPolicy bytes, or a dict {policy,
     plugin="vscc", collections=None | {name: EP bytes | None}, sbe=False}.  config: the channel's
-    common.Config bytes (channel policies, MSPs, application orgs); msps: further MSP ids."""
+    common.Config bytes (channel policies, MSPs, application orgs); msps: further MSP ids.
+    kvmeta: {(ns, coll, key bytes): VALIDATION_PARAMETER bytes} of the committed state."""
     engine.channel_init(channel)
     if config is not None:
         engine.channel_config(config)
@@ -67,6 +69,8 @@ def setup_channel(engine: Engine, channel: str, identities, chaincodes, committe
         engine.chaincode_define(ns, d.get("policy") or b"", plugin=d.get("plugin", "vscc"), flags=flags)
         for name, ep in (colls or {}).items():
             engine.collection_define(ns, name, ep or b"")
+    for (ns, coll, key), vp in (kvmeta or {}).items():
+        engine.kvmeta_set(ns, coll, key, vp)
     if committed_txids:
         engine.ledger_add_txids(list(committed_txids))
 

@@ -141,6 +141,21 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *ctx, const uint8_t *d_msg_buf, const uint6
  *                            writes to it FGV_EUNSUPPORTED; with them known, an undefined
  *                            collection is an ENDORSEMENT_POLICY_FAILURE (v20.go:84-100)
  *   fgv_ledger_add_txids  -- txids already in the block store (TxIDExists, kv_ledger.go:496)
+ *   fgv_kvmeta_set        -- key-level (state-based) endorsement: the VALIDATION_PARAMETER metadata
+ *                            value of one committed key (GetStateMetadata / GetPrivateDataMetadataByHash,
+ *                            statebased/vpmanagerimpl.go:316-341); coll NULL or "" = a public key, a
+ *                            private key is given by its key hash; vp NULL / len 0 = none.  The vscc
+ *                            of a written key with one evaluates it (validator_keylevel.go:38-85,
+ *                            translated as builtin/v20/validation_logic.go:50-66) instead of the
+ *                            collection / chaincode EP; an earlier tx of the block that validly
+ *                            wrote the key's metadata fails it (vpmanagerimpl.go:199-233).
+ *                            fgv_mvcc_validate_block's commit keeps this state current; a block the
+ *                            reference commits needs the caller's updates.  Blocks with metadata
+ *                            writes or writes to keys with a parameter run the host parser.
+ * Blocks the reference cannot validate are FGV_EUNSUPPORTED: a tx whose dependency extraction
+ * (validator_keylevel.go:184-222) fails before a later tx's vscc reads a written key (the
+ * reference waits forever, vpmanagerimpl.go:300-303) or panics (Actions[0] of none, a nil
+ * ChaincodeEndorsedAction) before a later tx's vscc runs.
  * Identities a transaction names that the engine cannot judge exactly -- a certificate of a
  * channel MSP neither registered nor resolvable by the MSP cache-miss path below, a P-384 key, a
  * SHA3 MSP, a role principal for an identity registered without role bits -- make the batch
@@ -165,7 +180,8 @@ typedef struct fgv_identity_info {
 } fgv_identity_info;
 #define FGV_CC_COLLECTIONS_KNOWN 1u /* the definition's collections are all declared           */
 #define FGV_CC_KEY_LEVEL_EP 2u      /* the state holds key-level endorsement (SBE) metadata for
-                                       this namespace: its writes are FGV_EUNSUPPORTED           */
+                                       this namespace that was NOT given by fgv_kvmeta_set: its
+                                       validation is FGV_EUNSUPPORTED                            */
 int fgv_channel_init(fgv_ctx *ctx, const char *channel_name);
 int fgv_channel_config(fgv_ctx *ctx, const uint8_t *config, size_t len);
 int fgv_msp_declare(fgv_ctx *ctx, const char *mspid);
@@ -176,6 +192,12 @@ int fgv_collection_define(fgv_ctx *ctx, const char *ns, const char *collection, 
                           size_t len);
 int fgv_ledger_add_txids(fgv_ctx *ctx, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
                          size_t n);
+int fgv_kvmeta_set(fgv_ctx *ctx, const char *ns, const char *coll, const uint8_t *key, size_t key_len,
+                   const uint8_t *vp, size_t vp_len);
+size_t fgv_kvmeta_count(fgv_ctx *ctx);
+/* the parameter held for (ns, coll, key): *len = its size (0: none); copies min(*len, cap) bytes */
+int fgv_kvmeta_get(fgv_ctx *ctx, const char *ns, const char *coll, const uint8_t *key, size_t key_len, uint8_t *buf,
+                   size_t cap, size_t *len);
 /* The MSP cache miss (msp/cache/cache.go:65-83 -> the channel MSP's DeserializeIdentity,
  * Validate and SatisfiesPrincipal; msp/mspimpl.go:398-422, identities.go:48-84,
  * mspimpl.go:892-938, mspimplvalidate.go): identities of a channel MSP (from fgv_channel_config's

@@ -23,6 +23,11 @@ Follows (citations under /root/reference/core/ledger/kvledger/txmgmt):
   validation/tx_ops.go:17-53,97-230     prepareTxOps: per key a delete wins, an upsert puts, and a
         metadata-only write puts the key's latest value again (a new version) if the key exists
         in the preceding updates or the committed state, else it is a no-op
+  validation/tx_ops.go:17-53,97-148 + statemetadata/metadata.go  the keys' metadata at commit:
+        a delete drops it, an upsert keeps it (retrieveLatestMetadata), a metadata write beside
+        an upsert replaces it, a metadata-only write replaces it when the key exists (entries
+        nil: deleted); the state's VALIDATION_PARAMETER (last entry of that name) is what the
+        key-level endorsement check reads (StateDB.kvmeta, oracle/v20.py ChannelModel.kvmeta)
 A key written twice (or given two metadata writes) by one transaction is outside the modelled
 state (txOps adds the operation flags) and raises Unsupported; so does what the reference errors
 out or panics on: a range query with maxDegree < 2 or a versionless raw read, a metadata write to
@@ -50,10 +55,12 @@ def _kb(key):
 
 
 class StateDB:
-    """committed versions: {(ns, key bytes): (block_num, tx_num)}"""
+    """committed versions: {(ns, key bytes): (block_num, tx_num)}; kvmeta: the keys'
+    VALIDATION_PARAMETER metadata {(ns, coll, key bytes): bytes} (coll "" = public)"""
 
-    def __init__(self, versions=None):
+    def __init__(self, versions=None, kvmeta=None):
         self.v = {(ns, _kb(k)): h for (ns, k), h in dict(versions or {}).items()}
+        self.kvmeta = dict(kvmeta or {})
 
     def get_version(self, ns, key):
         return self.v.get((ns, _kb(key)))
@@ -85,9 +92,10 @@ def _tx_rwsets(env_bytes):
     for ns in rw:
         kv = ns["kv"]
         name = ns["namespace"]
-        e = dict(ns=name, reads=[], rqs=[], colls=[], writes=[], meta=[])
+        e = dict(ns=name, reads=[], rqs=[], colls=[], writes=[], meta=[], mdw=[], dels=[])
         for m in kv.get("metadata_writes", []):
             e["meta"].append((False, name, m.get("key", "")))
+            e["mdw"].append((False, "", name, _kb(m.get("key", "")), _vp(m)))
         for r in kv.get("reads", []):
             e["reads"].append((r.get("key", ""), _ver(r.get("version"))))
         for q in kv.get("range_queries_info", []):
@@ -103,6 +111,8 @@ def _tx_rwsets(env_bytes):
             e["rqs"].append(rq)
         for w in kv.get("writes", []):
             e["writes"].append((False, name, w.get("key", ""), bool(w.get("is_delete", False)) or not w.get("value")))
+            if e["writes"][-1][3]:
+                e["dels"].append(("", _kb(w.get("key", ""))))
         for c in ns["coll"]:
             hns, h = hashed_ns(name, c["name"]), c["hashed"]
             e["colls"].append((hns, [(bytes(r.get("key_hash") or b""), _ver(r.get("version")))
@@ -111,8 +121,11 @@ def _tx_rwsets(env_bytes):
                 vh = bytes(w.get("value_hash") or b"")
                 e["writes"].append((True, hns, bytes(w.get("key_hash") or b""),
                                     bool(w.get("is_delete", False)) or not vh or vh == _EMPTY_HASH))
+                if e["writes"][-1][3]:
+                    e["dels"].append((c["name"], bytes(w.get("key_hash") or b"")))
             for m in h.get("metadata_writes", []):
                 e["meta"].append((True, hns, bytes(m.get("key_hash") or b"")))
+                e["mdw"].append((True, c["name"], hns, bytes(m.get("key_hash") or b""), _vp(m)))
         out.append(e)
     # a key written twice by one transaction: txOps adds the operation flags
     # (validation/tx_ops.go:183-191), a state the engine does not model
@@ -130,6 +143,15 @@ def _tx_rwsets(env_bytes):
     for e in out:  # a metadata write beside a KVWrite of the key follows the write
         e["meta"] = [m for m in e["meta"] if (m[0], m[1], _kb(m[2])) not in seen]
     return out
+
+
+def _vp(mw):
+    """statemetadata.Deserialize(...)[VALIDATION_PARAMETER]: the last entry of that name"""
+    vp = b""
+    for en in mw.get("entries", []):
+        if en.get("name", "") == "VALIDATION_PARAMETER":
+            vp = bytes(en.get("value") or b"")
+    return vp
 
 
 def _range_ok(state, updates, ns, rq):
@@ -162,6 +184,7 @@ def validate_block(state, block_bytes, flags, block_num, commit=False, updates_o
     data = (blk.get("data") or {}).get("data", [])
     flags = list(flags)
     updates = {}  # (ns, key) -> (height, is_delete)
+    kvops = []    # key-level parameter changes in block order: ((ns, coll, key), vp | b"")
     for i, d in enumerate(data):
         if flags[i] != 0:
             continue
@@ -204,6 +227,19 @@ def validate_block(state, block_bytes, flags, block_num, commit=False, updates_o
                     raise Unsupported("metadata write to a key deleted earlier in the block (the reference panics)")
                 if u is not None or state.get_version(ns, key) is not None:
                     updates[(hashed, ns, _kb(key))] = ((block_num, i), False)
+        for e in sets:  # the keys' metadata (tx_ops.go:17-53, 97-148)
+            wr = {(h, n, _kb(k)): d for h, n, k, d in e["writes"]}
+            for coll, key in e["dels"]:
+                kvops.append(((e["ns"], coll, key), b""))
+            for hashed, coll, fns, key, vp in e["mdw"]:
+                d = wr.get((hashed, fns, key))
+                if d is None:  # metadata only: replaced iff the key exists (its update is this tx's)
+                    u = updates.get((hashed, fns, key))
+                    if u is None or u[0] != (block_num, i):
+                        continue
+                elif d:
+                    continue
+                kvops.append(((e["ns"], coll, key), vp))
     if updates_out is not None:
         updates_out.update(updates)
     if commit:
@@ -212,4 +248,9 @@ def validate_block(state, block_bytes, flags, block_num, commit=False, updates_o
                 state.v.pop((ns, _kb(key)), None)
             else:
                 state.v[(ns, _kb(key))] = h
+        for k, vp in kvops:
+            if vp:
+                state.kvmeta[k] = vp
+            else:
+                state.kvmeta.pop(k, None)
     return flags

@@ -9,9 +9,10 @@ Follows, line by line in behaviour (citations under /root/reference):
   protoutil/proputils.go:198-223 + txutils.go:21-46 (GetActionFromEnvelope / GetPayloads)
   core/committer/txvalidator/v20/plugindispatcher/dispatcher.go:102-302  Dispatch
   core/handlers/validation/builtin/v20/validation_logic.go:109-217       builtin vscc v20
-  core/common/validation/statebased/validator_keylevel.go:38-282, v20.go:105-167
-        (no key-level validation parameters in the modelled state -> the chaincode EP is
-         evaluated once per written namespace)
+  core/common/validation/statebased/validator_keylevel.go:38-282, v20.go:105-167,
+        vpmanagerimpl.go:253-365  key-level (state-based) endorsement: each written key's
+        VALIDATION_PARAMETER from committed state, the in-block dependency on an earlier tx's
+        metadata write, the collection / chaincode EPs otherwise
   core/policy/application.go:148-163, common/cauthdsl/cauthdsl.go:24-92, policy.go:86-108
   common/policies/policy.go:363-395   SignatureSetToValidIdentities (dedup before verify,
         insert after successful verify, order preserved)
@@ -22,7 +23,9 @@ Modelled environment (the same one the engine is configured with):
     of a SerializedIdentity, each with its P-256 key, Validate() result and identity digest
     (Id = hex SHA-256 of the certificate); unknown pairs fail DeserializeIdentity;
   * chaincode definitions: namespace -> ApplicationPolicy bytes (lifecycle ValidationInfo);
-  * the ledger's committed txids (TxIDExists).
+  * the ledger's committed txids (TxIDExists);
+  * the committed state's key-level validation parameters: (ns, coll, key bytes) -> the
+    VALIDATION_PARAMETER metadata value (GetStateMetadata / GetPrivateDataMetadataByHash).
 Anything outside that model raises Unsupported (the engine returns an error for such blocks).
 """
 import hashlib
@@ -109,12 +112,15 @@ def _config_policies(group, path, out, msps, app_orgs, is_app=False):
 
 
 class ChannelModel:
-    def __init__(self, channel, identities, chaincodes, committed_txids=(), config=None, msps=()):
+    def __init__(self, channel, identities, chaincodes, committed_txids=(), config=None, msps=(), kvmeta=None):
         """identities: iterable of (serialized, mspid, pub64, valid, id_digest) or
         (serialized, Ident).  chaincodes: ns -> ApplicationPolicy bytes, or a dict
         {policy, plugin="vscc", collections=None | {name: EP bytes | None}, sbe=False}
         (collections None: not known -> hashed writes Unsupported).  config: common.Config bytes
-        (channel policies, MSPs, application orgs).  msps: further MSP ids of the channel."""
+        (channel policies, MSPs, application orgs).  msps: further MSP ids of the channel.
+        kvmeta: {(ns, coll, key bytes): VALIDATION_PARAMETER bytes} of the committed state
+        (coll "" = public key; a hashed key is its key hash)."""
+        self.kvmeta = dict(kvmeta or {})
         self.channel = channel
         self.msp = {}
         self.mspids = set(msps)
@@ -496,8 +502,110 @@ def get_action_from_envelope(env_bytes):
     return decode("ChaincodeAction", prp["extension"]), cap
 
 
-def vscc_validate(model, env_bytes, ns):
-    """builtin v20 Validate (validation_logic.go:185-217) -> True iff endorsement policy holds."""
+EXTRACT_OK, EXTRACT_FAIL, EXTRACT_PANIC = 0, 1, 2
+_NEVER, _INDET = "never", "indeterminate"
+
+
+def extract_dependencies(d):
+    """KeyLevelValidator.extractDependenciesForTx (validator_keylevel.go:184-222) and
+    ExtractValidationParameterDependency (vpmanagerimpl.go:258-292) -> (status, keys).
+    keys: (ns, coll, key bytes) of every metadata write of the tx, public and hashed, in any
+    namespace (none when the rwset does not decode: the dependency is still signalled).
+    EXTRACT_FAIL: an unmarshal error returns before ExtractValidationParameterDependency, so the
+    tx's dependency is never signalled and a later GetValidationParameterForKey waits for it
+    forever (vpmanagerimpl.go:300-303).  EXTRACT_PANIC: tx.Actions[0] of an empty list (:203) or
+    cap.Action == nil (:209) panics the peer."""
+    try:
+        env = decode("Envelope", d)
+        payl = decode("Payload", env.get("payload"))
+        tx = decode("Transaction", payl.get("data"))
+    except DecodeError:
+        return EXTRACT_FAIL, []
+    acts = tx.get("actions", [])
+    if not acts:
+        return EXTRACT_PANIC, []
+    try:
+        cap = decode("ChaincodeActionPayload", acts[0].get("payload"))
+    except DecodeError:
+        return EXTRACT_FAIL, []
+    if "action" not in cap:
+        return EXTRACT_PANIC, []
+    try:
+        prp = decode("ProposalResponsePayload", cap["action"].get("proposal_response_payload"))
+        cca = decode("ChaincodeAction", prp.get("extension"))
+    except DecodeError:
+        return EXTRACT_FAIL, []
+    try:
+        rw = parse_rwset(cca.get("results"))
+    except DecodeError:
+        return EXTRACT_OK, []
+    keys = []
+    for nsrw in rw:
+        for mw in nsrw["kv"].get("metadata_writes", []):
+            keys.append((nsrw["namespace"], "", mw.get("key", "").encode()))
+        for c in nsrw["coll"]:
+            for mw in c["hashed"].get("metadata_writes", []):
+                keys.append((nsrw["namespace"], c["name"], mw.get("key_hash") or b""))
+    return EXTRACT_OK, keys
+
+
+class BlockContext:
+    """The per-block state of KeyLevelValidationParameterManagerImpl (vpmanagerimpl.go:113-233),
+    restated sequentially: transactions are validated in block order, so every earlier tx's
+    dependencies and vscc results are known when a later tx asks.  res[j][ns]: True (the vscc
+    of ns returned nil), False (an error), _INDET (whether it runs depends on Go map order) or
+    absent (it never runs: a GetValidationParameterForKey waiting on it blocks forever)."""
+
+    def __init__(self, data):
+        self.data, self.i = data, 0
+        self.ext, self.deps, self.res = [], {}, []
+
+    def _extract_upto(self, i):  # PreValidate(i): txDepOnce for every tx <= i
+        while len(self.ext) <= i:
+            j = len(self.ext)
+            st, keys = extract_dependencies(self.data[j])
+            self.ext.append(st)
+            for k in keys:
+                self.deps.setdefault(k, []).append(j)
+
+    def pre_validate(self):
+        self._extract_upto(self.i)
+        if EXTRACT_PANIC in self.ext[:self.i]:
+            raise Unsupported("the peer panics extracting an earlier tx's dependencies (validator_keylevel.go:203-209)")
+
+    def validation_parameter_updated(self, ns, coll, key):
+        """GetValidationParameterForKey's wait (vpmanagerimpl.go:296-311) -> True iff an earlier
+        tx of the block validly (vscc nil for ns) wrote this key's metadata."""
+        if EXTRACT_FAIL in self.ext[:self.i]:
+            raise Unsupported("an earlier tx never signals its dependencies: the reference waits forever")
+        rs = [self.res[j].get(ns, _NEVER) for j in self.deps.get((ns, coll, key), ()) if j < self.i]
+        if any(r in (_NEVER, _INDET) for r in rs):
+            raise Unsupported("the vscc result of an earlier metadata writer never arrives (or map order)")
+        return any(r is True for r in rs)
+
+
+def validation_parameter(model, ns, coll, key, ctx):
+    """GetValidationParameterForKey (vpmanagerimpl.go:296-351) + toApplicationPolicyTranslator
+    (builtin/v20/validation_logic.go:50-66) -> "updated", None (no key-level parameter) or the
+    SignaturePolicyEnvelope."""
+    if ctx is not None and ctx.validation_parameter_updated(ns, coll, key):
+        return "updated"  # ValidationParameterUpdatedError -> policyErr
+    vp = model.kvmeta.get((ns, coll, key), b"")
+    if not vp:
+        return None
+    try:
+        return decode("SignaturePolicyEnvelope", vp)
+    except DecodeError:
+        raise Unsupported("untranslatable validation parameter: VSCCExecutionFailureError halts the channel")
+
+
+def vscc_validate(model, env_bytes, ns, ctx=None):
+    """builtin v20 Validate (validation_logic.go:185-217) -> True iff it returns nil."""
+    cc = model.chaincodes[ns]
+    if cc.get("plugin", "vscc") != "vscc" or cc.get("sbe"):
+        raise Unsupported("validation plugin other than the builtin vscc / undeclared key-level state")
+    if ctx is not None:
+        ctx.pre_validate()
     try:
         env = decode("Envelope", env_bytes)
         payl = decode("Payload", env.get("payload"))
@@ -522,31 +630,45 @@ def vscc_validate(model, env_bytes, ns):
         rw = parse_rwset(cca.get("results"))
     except DecodeError:
         return False
-    cc = model.chaincodes[ns]
-    if cc.get("plugin", "vscc") != "vscc" or cc.get("sbe"):
-        raise Unsupported("validation plugin other than the builtin vscc / key-level endorsement")
-    # statebased/validator_keylevel.go:173-233 (no key-level validation parameters in the
-    # modelled state): each public write checks the chaincode EP, each collection with hashed
-    # writes its collection EP (or the chaincode EP), and a namespace with neither checks the
-    # chaincode EP (CheckCCEPIfNoEPChecked).  Outcomes are pure, so the set of policies decides.
-    pols = []
+    # baseEvaluator.Evaluate (validator_keylevel.go:87-143) over policyCheckerV20 (v20.go:105-167):
+    # public writes, public metadata writes, hashed writes, hashed metadata writes; per key its
+    # validation parameter, else CheckCCEPIfNotChecked (collection EP, else the chaincode EP
+    # once).  The reference returns at the first error; every step's outcome is pure, so the
+    # conjunction over ALL steps is the same verdict -- and a step outside the model anywhere
+    # makes the tx Unsupported (never a guess, possibly where the reference had already stopped).
+    ok, checked, some = True, set(), False
     for nsrw in rw:
         if nsrw["namespace"] != ns:
             continue
-        if nsrw["kv"].get("metadata_writes") or any(c["hashed"].get("metadata_writes") for c in nsrw["coll"]):
-            raise Unsupported("metadata writes (key-level endorsement)")
-        if nsrw["kv"].get("writes"):
-            pols.append(("cc",))
-        for c in nsrw["coll"]:
-            if c["hashed"].get("hashed_writes"):
-                pols.append(collection_policy(model, ns, c["name"]))
-    if not pols:
-        pols = [("cc",)]
-    results = [_run(model, p, cc["policy"], sigset) for p in pols]
-    return all(results)
+        keys = [("", w.get("key", "").encode()) for w in nsrw["kv"].get("writes", [])]
+        keys += [("", w.get("key", "").encode()) for w in nsrw["kv"].get("metadata_writes", [])]
+        keys += [(c["name"], w.get("key_hash") or b"") for c in nsrw["coll"] for w in c["hashed"].get("hashed_writes", [])]
+        keys += [(c["name"], w.get("key_hash") or b"") for c in nsrw["coll"] for w in c["hashed"].get("metadata_writes", [])]
+        for coll, key in keys:
+            some = True
+            vp = validation_parameter(model, ns, coll, key, ctx)
+            if vp == "updated":
+                ok = False
+            elif vp is not None:
+                ok &= _eval_spe(model, vp, sigset)
+            elif coll and coll in checked:
+                pass
+            else:
+                p = collection_policy(model, ns, coll) if coll else ("cc",)
+                if p[0] == "reject":
+                    ok = False
+                elif p[0] != "cc":
+                    ok &= _run(model, p, cc["policy"], sigset)
+                    checked.add(coll)
+                elif "" not in checked:
+                    ok &= evaluate_policy(model, cc["policy"], sigset)
+                    checked.add("")
+    if not some:  # CheckCCEPIfNoEPChecked (FAB-9473)
+        return evaluate_policy(model, cc["policy"], sigset)
+    return ok
 
 
-def dispatch(model, payload, env_bytes):
+def dispatch(model, payload, env_bytes, ctx=None):
     """plugindispatcher.Dispatch (dispatcher.go:102-221) -> code."""
     chdr = decode("ChannelHeader", payload["header"].get("channel_header"))
     try:
@@ -582,27 +704,34 @@ def dispatch(model, payload, env_bytes):
         seen.add(nsrw["namespace"])
         if _writes_to_ns(nsrw) and nsrw["namespace"] not in wr:
             wr.append(nsrw["namespace"])
-    # The reference iterates a Go map (random order).  Results only differ in the
-    # reported code when namespaces fail with DIFFERENT codes; we report the first in
-    # sorted order and flag multi-namespace disagreement as unsupported.
-    codes = set()
+    # The reference iterates a Go map (random order) and stops at the first failing namespace.
+    # Results only differ in the reported code when namespaces fail with DIFFERENT codes; we
+    # report the first in sorted order and flag multi-namespace disagreement as unsupported.
+    # A namespace's vscc result (read by later txs' key-level checks) is determined only when
+    # it runs in every order: no OTHER namespace fails.
+    codes, ran = {}, {}
     for ns in sorted(wr):
         cc = model.chaincodes.get(ns)
         # getCDataForCC (dispatcher.go:237-264): undefined chaincode, empty plugin or empty
         # validation parameter -> INVALID_CHAINCODE
         if cc is None or not cc.get("policy") or cc.get("plugin", "vscc") == "":
-            codes.add(INVALID_CHAINCODE)
+            codes[ns] = INVALID_CHAINCODE
             continue
-        if not vscc_validate(model, env_bytes, ns):
-            codes.add(ENDORSEMENT_POLICY_FAILURE)
-    if len(codes) > 1:
+        ok = vscc_validate(model, env_bytes, ns, ctx)
+        ran[ns] = ok
+        if not ok:
+            codes[ns] = ENDORSEMENT_POLICY_FAILURE
+    if ctx is not None:
+        for ns, ok in ran.items():
+            ctx.res[ctx.i][ns] = _INDET if any(n != ns for n in codes) else ok
+    if len(set(codes.values())) > 1:
         raise Unsupported("namespaces fail with different codes (map-order dependent)")
-    return codes.pop() if codes else VALID
+    return next(iter(codes.values())) if codes else VALID
 
 
 # ----------------------------------------------------------------- block level
 
-def validate_tx(model, d):
+def validate_tx(model, d, ctx=None):
     """validator.go:297-453 -> (code, txid)."""
     try:
         env = decode("Envelope", d)
@@ -617,7 +746,7 @@ def validate_tx(model, d):
         txid = chdr.get("tx_id", "")
         if txid in model.committed:
             return DUPLICATE_TXID, ""
-        code = dispatch(model, payload, d)
+        code = dispatch(model, payload, d, ctx)
         if code != VALID:
             return code, ""
         return VALID, txid
@@ -659,8 +788,11 @@ def validate_block(model, block_bytes):
     blk = decode("Block", block_bytes)
     data = (blk.get("data") or {}).get("data", [])
     flags, txids = [], []
-    for d in data:
-        code, txid = validate_tx(model, d)
+    ctx = BlockContext(data)
+    for i, d in enumerate(data):
+        ctx.i = i
+        ctx.res.append({})
+        code, txid = validate_tx(model, d, ctx)
         flags.append(code)
         txids.append(txid if code == VALID else "")
     seen = set()

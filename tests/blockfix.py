@@ -3,9 +3,12 @@ import random
 
 from fabric_amd.synth import blocks
 
+# bad_payload last: its Payload does not unmarshal, so the key-level validator never signals its
+# dependencies and the vscc of any later writer would wait for them forever (validator_keylevel.go:
+# 184-222, vpmanagerimpl.go:300-303) -- a block the reference cannot validate
 SPECIAL = ["bad_txid", "bad_proposal_hash", "bad_epoch", "unknown_cc", "two_actions", "rogue_creator",
-           "high_s_creator", "dup_endorser", "forged_endorser", "event_other_cc", "bad_payload", "no_sig",
-           "clean", "dup_txid"]
+           "high_s_creator", "dup_endorser", "forged_endorser", "event_other_cc", "no_sig",
+           "clean", "dup_txid", "bad_payload"]
 
 _NET = {}
 

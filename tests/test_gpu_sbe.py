@@ -1,0 +1,147 @@
+"""GPU: key-level (state-based) endorsement through libfgv (fgv_kvmeta_set + the sequential
+key-level fold; the device parser hands such batches to the host parser, verification stays on
+the GPU) equals the oracle code for code and reproduces the reference tests' assertions
+(tests/golden/sbe_known_answers.json); blocks the reference cannot validate (dependency
+extraction failing / panicking before a later vscc) are FGV_EUNSUPPORTED on both sides."""
+import pytest
+
+from fabric_amd import _lib, txvalidator
+from fabric_amd.synth import blocks
+from oracle import v20
+from tests import sbe_cases
+from tests.blockfix import block_from_envs, network
+
+pytestmark = pytest.mark.gpu
+CASES = sbe_cases.load()
+MODES = pytest.mark.parametrize("mode", [0, 1], ids=["devparse", "hostparse"])
+
+
+def _eng(channel, identities, chaincodes, kvmeta, mode):
+    eng = _lib.Engine(0)
+    eng.set_parse_mode(mode)
+    txvalidator.setup_channel(eng, channel, identities, chaincodes, kvmeta=kvmeta)
+    return eng
+
+
+def _same(eng, model_fn, blks):
+    """engine flags == oracle flags, or both Unsupported"""
+    try:
+        exp = v20.validate_blocks(model_fn(), blks)
+    except v20.Unsupported:
+        with pytest.raises(_lib.Unsupported):
+            eng.validate_blocks(blks)
+        return None
+    got = [list(f) for f in eng.validate_blocks(blks)]
+    assert got == exp
+    return exp
+
+
+@MODES
+def test_known_answers(mode):
+    for case in CASES:
+        eng = _eng("testchannelid", case["identities"], case["chaincodes"], case["kvmeta"], mode)
+        assert eng.kvmeta_count() == len(case["kvmeta"])
+        got = list(eng.validate_blocks([case["block"]])[0])
+        exp = v20.validate_block(v20.ChannelModel("testchannelid", case["identities"], case["chaincodes"],
+                                                  kvmeta=case["kvmeta"]), case["block"])
+        assert got == exp, case["name"]
+        assert all(sbe_cases.matches(g, e) for g, e in zip(got, case["expected"])), case["name"]
+        eng.close()
+
+
+def _net_ccs(net):
+    return {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
+
+
+@MODES
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_synthetic_blocks(mode, seed):
+    """generated key-level blocks (parameters in state, metadata writes, in-block dependencies,
+    collections) batched with a plain C2 block: equal to the oracle"""
+    net = network()
+    ccs = _net_ccs(net)
+    sb = [sbe_cases.make_sbe_block(net, 60, 100 * seed + k, number=1 + k) for k in range(3)]
+    kvmeta = {}
+    for _, kv in sb:
+        kvmeta.update(kv)
+    plain = blocks.make_block(net, 200, number=4, seed=seed)[0]
+    blks = [b for b, _ in sb] + [plain]
+    eng = _eng(net.channel, net.identities(), ccs, kvmeta, mode)
+    exp = _same(eng, lambda: v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=kvmeta), blks)
+    assert exp is not None and any(0 in f for f in exp) and any(10 in f for f in exp)
+    # parameters removed again: the same blocks without key-level state
+    for k in kvmeta:
+        eng.kvmeta_set(k[0], k[1], k[2], b"")
+    assert eng.kvmeta_count() == 0
+    _same(eng, lambda: v20.ChannelModel(net.channel, net.identities(), ccs), blks)
+    eng.close()
+
+
+@MODES
+def test_untranslatable_parameter(mode):
+    """a written key whose parameter does not unmarshal: the reference halts -> Unsupported; a
+    parameter on a key nobody writes changes nothing"""
+    net = network()
+    ccs = _net_ccs(net)
+    blk, kvmeta = sbe_cases.make_sbe_block(net, 40, 7)
+    written = next(k for k in kvmeta)
+    bad = dict(kvmeta)
+    bad[written] = b"\xff\x01"
+    eng = _eng(net.channel, net.identities(), ccs, bad, mode)
+    _same(eng, lambda: v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=bad), [blk])
+    eng.kvmeta_set(written[0], written[1], written[2], b"")
+    eng.kvmeta_set("mycc", "", b"never-written", b"\xff\x01")
+    _same(eng, lambda: v20.ChannelModel(net.channel, net.identities(), ccs,
+                                        kvmeta={**{k: v for k, v in bad.items() if k != written},
+                                                ("mycc", "", b"never-written"): b"\xff\x01"}), [blk])
+    eng.close()
+
+
+def _bad_payload():
+    return blocks.f_bytes(1, b"\x0a\x05ab") + blocks.f_bytes(2, b"sig")
+
+
+def _no_actions(env_bytes):
+    env = v20.decode("Envelope", env_bytes)
+    pl = v20.decode("Payload", env["payload"])
+    hdr = blocks.f_msg(1, blocks.f_bytes(1, pl["header"]["channel_header"]) +
+                       blocks.f_bytes(2, pl["header"]["signature_header"]))
+    return blocks.f_bytes(1, hdr) + blocks.f_bytes(2, env["signature"])
+
+
+@MODES
+def test_extraction_hazards(mode):
+    """a failed dependency extraction before a later writer, or a panic before a later vscc:
+    Unsupported; the same transactions after the last vscc: flags as usual"""
+    net = network()
+    _, _, envs = blocks.make_block(net, 300, number=1, seed=21)
+    eng = _eng(net.channel, net.identities(), net.chaincodes, None, mode)
+    model = lambda: v20.ChannelModel(net.channel, net.identities(), net.chaincodes)  # noqa: E731
+    bad, noact = _bad_payload(), _no_actions(envs[5])
+    for blk in [block_from_envs(envs[:100] + [bad] + envs[100:]), block_from_envs(envs[:10] + [noact] + envs[10:])]:
+        with pytest.raises(v20.Unsupported):
+            v20.validate_block(model(), blk)
+        with pytest.raises(_lib.Unsupported):
+            eng.validate_blocks([blk])
+    # after the last transaction that reaches a vscc; and in a block of its own next to others
+    ok = _same(eng, model, [block_from_envs(envs + [bad, noact], number=2),
+                            block_from_envs([noact, bad], number=3), blocks.make_block(net, 50, number=4, seed=22)[0]])
+    assert ok is not None
+    eng.close()
+
+
+@MODES
+def test_shard_prefix_hazard(mode):
+    """a shard starting after a failed extraction in its block: the transactions before it still
+    leave its writers waiting -> Unsupported; a shard before it is unaffected"""
+    net = network()
+    _, _, envs = blocks.make_block(net, 40, number=1, seed=23, faults=())
+    blk = block_from_envs(envs[:10] + [_bad_payload()] + envs[10:])
+    eng = _eng(net.channel, net.identities(), net.chaincodes, None, mode)
+    with pytest.raises(_lib.Unsupported):
+        eng.validate_shard([blk], [20], [41])
+    res, ntx = eng.validate_shard([blk], [0], [10])
+    exp = v20.validate_block(v20.ChannelModel(net.channel, net.identities(), net.chaincodes),
+                             block_from_envs(envs[:10]))
+    assert int(ntx[0]) == 41 and list(res[:, 0]) == exp
+    eng.close()
