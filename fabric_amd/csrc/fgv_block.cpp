@@ -1440,7 +1440,7 @@ static int build_committed(fgv_block_state *S) {
 }
 
 __global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, DevChannel ch, DevTx *out,
-                           uint32_t *flags, uint32_t *xhaz);
+                           uint32_t *flags, uint32_t *xhaz, uint32_t prefetch);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
@@ -1638,7 +1638,12 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(128), 0, c->stream2, N, envtab, dbs,
                      B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
   HIP_TRY(hipEventRecord(B.ev[1], c->stream2));
-  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16);
+  static const uint32_t parse_pf = [] {  // A/B knob: bytes of each envelope touched up front
+    const char *e = getenv("FGV_PARSE_PF");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16,
+                     parse_pf);
   HIP_TRY(hipEventRecord(B.ev[4], sf));
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one

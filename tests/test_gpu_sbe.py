@@ -145,3 +145,41 @@ def test_shard_prefix_hazard(mode):
                              block_from_envs(envs[:10]))
     assert int(ntx[0]) == 41 and list(res[:, 0]) == exp
     eng.close()
+
+
+def test_mvcc_commit_keeps_parameters():
+    """committer -> MVCC commit -> next block's committer, over generated key-level blocks: the
+    engine's parameter state after each commit equals the oracle's StateDB.kvmeta (deletes drop a
+    key's parameter, metadata writes beside an upsert or on an existing key replace it), and the
+    next block validates against it -- flags equal to the oracle at every step"""
+    import hashlib
+    from oracle import mvcc as OM
+    net = network()
+    ccs = _net_ccs(net)
+    keys = ["k%d" % i for i in range(12)]
+    hkeys = [hashlib.sha256(k.encode()).digest() for k in keys]
+    _, kvmeta0 = sbe_cases.make_sbe_block(net, 4, 900)
+    eng = _eng(net.channel, net.identities(), ccs, kvmeta0, 1)
+    eng.statedb_init(1 << 16, 8 << 20)
+    # keys k0..k7 exist (public and hashed); k8..k11 only once written
+    eng.statedb_load("mycc", keys[:8], [1] * 8, list(range(8)))
+    eng.statedb_load("mycc$$hpvt1", hkeys[:8], [1] * 8, list(range(8)))
+    db = OM.StateDB({**{("mycc", k): (1, i) for i, k in enumerate(keys[:8])},
+                     **{("mycc$$hpvt1", k): (1, i) for i, k in enumerate(hkeys[:8])}}, kvmeta=kvmeta0)
+    seen = set(kvmeta0)
+    changed = 0
+    for b in range(6):
+        blk, _ = sbe_cases.make_sbe_block(net, 50, 910 + b, number=2 + b)
+        model = v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=dict(db.kvmeta))
+        flags = v20.validate_block(model, blk)
+        assert list(eng.validate_blocks([blk])[0]) == flags
+        before = dict(db.kvmeta)
+        exp = OM.validate_block(db, blk, flags, 2 + b, commit=True)
+        assert list(eng.mvcc_validate(blk, 2 + b, flags, commit=True)) == list(exp)
+        changed += db.kvmeta != before
+        seen |= set(db.kvmeta)
+        for ns, coll, key in seen:
+            assert eng.kvmeta_get(ns, coll, key) == db.kvmeta.get((ns, coll, key)), (b, coll, key)
+        assert eng.kvmeta_count() == len(db.kvmeta)
+    assert changed >= 3
+    eng.close()
