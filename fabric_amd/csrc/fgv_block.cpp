@@ -1716,6 +1716,14 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   S->last = cur;
   BdSet &B = S->set[cur];
   for (size_t b = 0; b < nblocks; b++) ntx_out[b] = B.so.ntx[b];
+  // the fused single-device call: its finalize's txid index runs on stream3 right after the
+  // batch's digests, beside the verify chain (fgv_finalize_early_index)
+  if (c->want_early_fin && !tx_lo && !tx_hi && B.N) {
+    int rc = fgv_finalize_early_index(c, nblocks, B.so.ntx.data(), B.tx.as<DevTx>(),
+                                      reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff),
+                                      B.dig.as<uint8_t>(), c->stream3);
+    if (rc) return rc;
+  }
   c->n_sha_jobs = c->n_sha_blocks = c->n_verifies = 0;
   c->last_presplit = B.presplit;
   c->last_ahead = ahead_hit;
@@ -2125,6 +2133,10 @@ uint64_t fgv_block_parse_probe(const char *channel, const uint8_t *const *ids, c
     fgv_block_add_identity(&S, ids[i], id_lens[i], 0, &info);
   }
   if (ns) fgv_block_define_chaincode(&S, ns, "vscc", policy, policy_len, 0);
+  if (ns) {  // key-level parameters: the policy bytes as a (maybe untranslatable) envelope
+    fgv_block_kvmeta_set(&S, ns, "", reinterpret_cast<const uint8_t *>("k0000001"), 8, policy, policy_len);
+    fgv_block_kvmeta_set(&S, ns, "collA", reinterpret_cast<const uint8_t *>("k0000002"), 8, policy, policy_len);
+  }
   Channel &ch = S.ch;
   ch.compile();
   uint64_t h = 0xcbf29ce484222325ull;
@@ -2132,6 +2144,9 @@ uint64_t fgv_block_parse_probe(const char *channel, const uint8_t *const *ids, c
   VBlock b;
   if (!pbw::decode(blk, n, b)) return 0;
   TxRec R;
+  SbeBlock sb;
+  sb.res.resize(b.data.data.size());
+  uint32_t i = 0;
   for (const Span &d : b.data.data) {
     parse_tx(ch, d, R);
     count_jobs(ch, R);
@@ -2139,12 +2154,27 @@ uint64_t fgv_block_parse_probe(const char *channel, const uint8_t *const *ids, c
     mix(R.etx);
     mix(R.disp);
     mix(R.n_ej);
-    if (R.disp != C_VALID) continue;
-    pbw::SmallVec<int, 16> ids_ok;
-    for (const EndRec &e : R.ends)
-      if (e.ident >= 0 && std::find(ids_ok.begin(), ids_ok.end(), e.ident) == ids_ok.end()) ids_ok.push_back(e.ident);
-    for (int pi : R.policies)
-      if (pi >= 0) mix((uint64_t)eval_policy(ch, pi, ids_ok.data(), ids_ok.size()));
+    mix(R.xstat);
+    if (R.has_md && R.xstat == X_OK) add_deps(R.results, i, sb);
+    if (R.disp == C_VALID) {
+      pbw::SmallVec<int, 16> ids_ok;
+      for (const EndRec &e : R.ends)
+        if (e.ident >= 0 && std::find(ids_ok.begin(), ids_ok.end(), e.ident) == ids_ok.end()) ids_ok.push_back(e.ident);
+      for (int pi : R.policies)
+        if (pi >= 0) mix((uint64_t)eval_policy(ch, pi, ids_ok.data(), ids_ok.size()));
+      // the key-level vscc walk of every namespace of the rwset
+      VTxRwSet rw;
+      if (pbw::decode(R.results.p, R.results.n, rw))
+        for (const VNsRwSet &nr : rw.ns) {
+          auto it = ch.ccs.find(nr.ns.str());
+          if (it == ch.ccs.end() || it->second.status != 0) continue;
+          auto eval = [&](int pi) { return eval_policy(ch, pi, ids_ok.data(), ids_ok.size()); };
+          const int r = sbe_vscc(ch, it->second, sv(nr.ns), &nr, i, sb, false, eval);
+          mix((uint64_t)r);
+          if (r == 0 || r == 1) sb.res[i].push_back({nr.ns.str(), (int8_t)r});
+        }
+    }
+    i++;
   }
   // the orderer-signature metadata (fgv_block_sig_verdicts' decode)
   VBlockMeta0 m;

@@ -906,12 +906,19 @@ int fgv_ledger_add_txids(fgv_ctx *c, const uint8_t *buf, const uint64_t *off, co
 // [floor(n r / W), floor(n (r+1) / W)).  The ranks' ranges must tile every block.
 // defer: leave the flags' D2H copy (into c->hb_fflags) queued -- the caller synchronises and
 // copies them out (fgv_validate_blocks: one synchronisation for validation + finalize).
-static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t W, size_t rows,
-                             const uint8_t *d_recs, uint8_t *flags, const uint32_t *rank_lo = nullptr,
-                             const uint32_t *rank_hi = nullptr, bool defer = false) {
-  if (W == 0 || ((uintptr_t)d_recs & 3) || (!rank_lo) != (!rank_hi)) return FGV_EINVAL;
+// Three parts: fin_prepare (host metadata, buffers), fin_front (metadata upload, row map +
+// table reset, the txid index) and fin_back (codes, duplicates, flags D2H).  A single-device
+// batch runs fin_front early, beside its verify chain (fgv_finalize_early_index).
+struct FinPlan {
+  uint64_t P = 0;
+  size_t cap = 0, wn = 0, meta = 0;
+};
+static int fin_prepare(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t W, size_t rows, const uint32_t *rank_lo,
+                       const uint32_t *rank_hi, FinPlan &F) {
+  if (W == 0 || (!rank_lo) != (!rank_hi)) return FGV_EINVAL;
   uint64_t P = 0;
   for (size_t b = 0; b < nblocks; b++) P += ntx[b];
+  F.P = P;
   if (P == 0) return FGV_OK;
   if (P >= 0x7FFFFFFFull || nblocks >= 0x7FFFFFFFull || rows * W >= 0xFFFFFFFFull) return FGV_EINVAL;
   // host metadata: blk_start (nb+1 u64) | roff (W x nb u32) | lo (W x nb u32) | cnt (W x nb u32)
@@ -951,31 +958,89 @@ static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint
       !c->fz_minblk.ensure(cap * 4) || !c->fz_minvalid.ensure(cap * 4) || !c->fz_flags.ensure(P) ||
       !c->fz_pslot.ensure(P * 4) || !c->hb_fflags.ensure(P))
     return FGV_ENOMEM;
-  hipStream_t st = c->stream;
-  HIP_TRY(hipMemcpyAsync(c->fz_meta.p, c->hb_fz.p, meta, hipMemcpyHostToDevice, st));
-  const uint32_t n32 = (uint32_t)P, mask = (uint32_t)(cap - 1);
+  F.cap = cap;
+  F.wn = wn;
+  F.meta = meta;
+  return FGV_OK;
+}
+// index from the gathered records (recs != null) or from a single-device batch's parse and
+// digests (dtx != null: the owners' keys go to c->fz_keys)
+static int fin_front(fgv_ctx *c, hipStream_t st, size_t nblocks, uint32_t W, size_t rows, const FinPlan &F,
+                     const uint8_t *d_recs, const DevTx *dtx, const uint64_t *bases, const uint8_t *digests) {
+  HIP_TRY(hipMemcpyAsync(c->fz_meta.p, c->hb_fz.p, F.meta, hipMemcpyHostToDevice, st));
+  const uint32_t n32 = (uint32_t)F.P, mask = (uint32_t)(F.cap - 1);
   const dim3 grid((n32 + 255) / 256), blk(256);
   const uint64_t *d_bstart = c->fz_meta.as<uint64_t>();
   const uint32_t *d_roff = reinterpret_cast<const uint32_t *>(d_bstart + nblocks + 1);
   // (k_fin_rows also resets the cap-slot txid table)
-  hipLaunchKernelGGL(k_fin_rows, dim3((uint32_t)((std::max<size_t>(P, cap) + 255) / 256)), blk, 0, st, n32, d_bstart,
-                     (uint32_t)nblocks, W, (uint32_t)rows, d_roff, d_roff + wn, d_roff + 2 * wn,
-                     c->fz_rowmap.as<uint32_t>(), c->fz_blkof.as<uint32_t>(), (uint32_t)cap, c->fz_owner.as<uint32_t>(),
-                     c->fz_minblk.as<int32_t>(), c->fz_minvalid.as<uint32_t>());
-  hipLaunchKernelGGL(k_fin_index, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
-                     c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask,
-                     c->fin_seed);
+  hipLaunchKernelGGL(k_fin_rows, dim3((uint32_t)((std::max<size_t>(F.P, F.cap) + 255) / 256)), blk, 0, st, n32,
+                     d_bstart, (uint32_t)nblocks, W, (uint32_t)rows, d_roff, d_roff + F.wn, d_roff + 2 * F.wn,
+                     c->fz_rowmap.as<uint32_t>(), c->fz_blkof.as<uint32_t>(), (uint32_t)F.cap,
+                     c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), c->fz_minvalid.as<uint32_t>());
+  if (dtx)
+    hipLaunchKernelGGL(k_fin_index_dev, grid, blk, 0, st, n32, dtx, bases, digests, c->fz_keys.as<uint8_t>(),
+                       c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask, c->fin_seed);
+  else
+    hipLaunchKernelGGL(k_fin_index, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
+                       c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask,
+                       c->fin_seed);
+  HIP_TRY(hipGetLastError());
+  return FGV_OK;
+}
+static int fin_back(fgv_ctx *c, hipStream_t st, const FinPlan &F, const uint8_t *d_recs, const uint8_t *keys) {
+  const uint32_t n32 = (uint32_t)F.P, mask = (uint32_t)(F.cap - 1);
+  const dim3 grid((n32 + 255) / 256), blk(256);
   hipLaunchKernelGGL(k_fin_codes, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
                      c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(),
                      c->fz_minvalid.as<uint32_t>(), mask, c->fin_seed, c->fz_flags.as<uint8_t>(),
-                     c->fz_pslot.as<uint32_t>());
+                     c->fz_pslot.as<uint32_t>(), keys);
   hipLaunchKernelGGL(k_fin_dups, grid, blk, 0, st, n32, c->fz_pslot.as<uint32_t>(), c->fz_minvalid.as<uint32_t>(),
                      c->fz_flags.as<uint8_t>());
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(c->hb_fflags.p, c->fz_flags.p, P, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(c->hb_fflags.p, c->fz_flags.p, F.P, hipMemcpyDeviceToHost, st));
+  return FGV_OK;
+}
+
+// the single-device fused call's finalize front, enqueued on `st` once the batch's digests are
+// there (stream order), recorded as c->fin_ev
+int fgv_finalize_early_index(fgv_ctx *c, size_t nblocks, const size_t *ntx, const DevTx *dtx, const uint64_t *bases,
+                             const uint8_t *digests, hipStream_t st) {
+  c->early_fin = false;
+  FinPlan F;
+  size_t total = 0;
+  for (size_t b = 0; b < nblocks; b++) total += ntx[b];
+  int rc = fin_prepare(c, nblocks, ntx, 1, total, nullptr, nullptr, F);
+  if (rc || F.P == 0) return rc;
+  if (!c->fz_keys.ensure(F.P * 32)) return FGV_ENOMEM;
+  if (!c->fin_ev) HIP_TRY(hipEventCreateWithFlags(&c->fin_ev, hipEventDisableTiming));
+  rc = fin_front(c, st, nblocks, 1, total, F, nullptr, dtx, bases, digests);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c->fin_ev, st));
+  c->early_fin = true;
+  return FGV_OK;
+}
+
+static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t W, size_t rows,
+                             const uint8_t *d_recs, uint8_t *flags, const uint32_t *rank_lo = nullptr,
+                             const uint32_t *rank_hi = nullptr, bool defer = false) {
+  const bool early = c->early_fin;
+  c->early_fin = false;
+  if (((uintptr_t)d_recs & 3)) return FGV_EINVAL;
+  FinPlan F;
+  int rc = fin_prepare(c, nblocks, ntx, W, rows, rank_lo, rank_hi, F);
+  if (rc || F.P == 0) return rc;
+  hipStream_t st = c->stream;
+  if (early && W == 1) {  // the front ran beside the verify chain (same plan: W = 1, rows = P)
+    HIP_TRY(hipStreamWaitEvent(st, c->fin_ev, 0));
+    rc = fin_back(c, st, F, d_recs, c->fz_keys.as<uint8_t>());
+  } else {
+    rc = fin_front(c, st, nblocks, W, rows, F, d_recs, nullptr, nullptr, nullptr);
+    if (!rc) rc = fin_back(c, st, F, d_recs, nullptr);
+  }
+  if (rc) return rc;
   if (defer) return FGV_OK;
   HIP_TRY(hipStreamSynchronize(st));
-  memcpy(flags, c->hb_fflags.p, P);
+  memcpy(flags, c->hb_fflags.p, F.P);
   return FGV_OK;
 }
 
@@ -1282,10 +1347,13 @@ static int validate_blocks_locked(fgv_ctx *c, size_t nblocks, const uint8_t *con
     for (size_t b = 0; b < nblocks; b++) bytes += lens[b];
     const size_t bound = std::min(flags_cap, bytes / 2 + nblocks);
     if (!c->fz_res.ensure(bound * sizeof(fgv_tx_result) + 64)) return FGV_ENOMEM;
+    c->want_early_fin = c->early_fin_on;
     rc = fgv_block_validate_dev_enqueue(c, c->blk, nblocks, blocks, lens, dev.data(), nullptr, nullptr,
                                         c->fz_res.as<fgv_tx_result>(), bound, ntx);
+    c->want_early_fin = false;
     if (rc) {
       fgv_block_validate_dev_finish(c, c->blk);  // (waits for anything already queued)
+      c->early_fin = false;
       return rc;
     }
     size_t total = 0;

@@ -1,6 +1,7 @@
 // fgv_internal.h -- host-internal interfaces between fgv_host.cpp (context, device buffers,
 // kernels) and fgv_block.cpp (block parse / fold).  Not part of the C ABI.
 #pragma once
+#include <cstdlib>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -118,6 +119,15 @@ struct fgv_ctx {
   DevBuf fz_meta, fz_rowmap, fz_blkof, fz_owner, fz_minblk, fz_minvalid, fz_flags, fz_pslot, fz_res;
   HostBuf hb_fz, hb_fflags, hb_res;
   uint64_t fin_seed = 0;
+  // early txid index of a single-device batch (fgv_finalize_early_index): set by the fused
+  // validate call before the device enqueue, consumed by its finalize
+  bool want_early_fin = false, early_fin = false;
+  bool early_fin_on = [] {  // A/B knob FGV_EARLY_FIN=0: the whole finalize after the fold
+    const char *e = getenv("FGV_EARLY_FIN");
+    return !(e && atoi(e) == 0);
+  }();
+  hipEvent_t fin_ev = nullptr;
+  DevBuf fz_keys;
   uint32_t n_cu = 0;        // compute units (persistent k_point grid)
   uint32_t last_lanes = 0;  // lanes per verify of the last k_point launch
   // per-batch device buffers
@@ -208,6 +218,10 @@ int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const char *p
                                size_t len, uint32_t flags);
 int fgv_block_define_collection(fgv_block_state *S, const char *ns, const char *coll, const uint8_t *policy,
                                 size_t len);
+struct DevTx;
+extern "C" int fgv_finalize_early_index(fgv_ctx *c, size_t nblocks, const size_t *ntx, const DevTx *dtx,
+                                        const uint64_t *bases,
+                             const uint8_t *digests, hipStream_t st);
 int fgv_block_kvmeta_set(fgv_block_state *S, const std::string &ns, const std::string &coll, const uint8_t *key,
                          size_t key_len, const uint8_t *vp, size_t vp_len);
 size_t fgv_block_kvmeta_count(fgv_block_state *S);

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/fgv.h"
+#include "blockdev.h"
 #include "fgv_kernels.h"
 
 namespace {
@@ -48,8 +49,12 @@ __device__ inline void load_key(const uint8_t *recs, uint32_t row, uint32_t off,
   for (int i = 0; i < 8; i++) k[i] = q[i];
 }
 
-__device__ inline bool key_eq(const uint32_t a[8], const uint8_t *recs, uint32_t row) {
-  const uint32_t *q = reinterpret_cast<const uint32_t *>(recs + (size_t)row * REC + OFF_INDEX);
+// the owner's index key: its record's index_txid, or (keys != null) its entry of the early
+// index's key array (k_fin_index_dev), indexed by position
+__device__ inline bool key_eq(const uint32_t a[8], const uint8_t *recs, uint32_t row, const uint8_t *keys = nullptr,
+                              uint32_t pos = 0) {
+  const uint32_t *q = keys ? reinterpret_cast<const uint32_t *>(keys + (size_t)pos * 32)
+                           : reinterpret_cast<const uint32_t *>(recs + (size_t)row * REC + OFF_INDEX);
   bool eq = true;
 #pragma unroll
   for (int i = 0; i < 8; i++) eq &= q[i] == a[i];
@@ -58,14 +63,42 @@ __device__ inline bool key_eq(const uint32_t a[8], const uint8_t *recs, uint32_t
 
 // slot of key k, or -1 (owners' keys are their index_txid)
 __device__ inline int64_t tab_find(const uint32_t k[8], uint64_t h, const uint32_t *owner, const uint32_t *rowmap,
-                                   const uint8_t *recs, uint32_t mask) {
+                                   const uint8_t *recs, uint32_t mask, const uint8_t *keys) {
   for (uint32_t probe = 0; probe <= mask; probe++) {
     const uint32_t s = (uint32_t)(h + probe) & mask;
     const uint32_t o = owner[s];
     if (o == 0) return -1;
-    if (key_eq(k, recs, rowmap[o - 1])) return s;
+    if (keys ? key_eq(k, recs, 0, keys, o - 1) : key_eq(k, recs, rowmap[o - 1])) return s;
   }
   return -1;
+}
+// index key of a transaction of the device-parsed batch, as k_bd_fold writes it into the record
+// (blockdev.hip): the computed txid digest, or the hex-decoded chdr.TxId
+__device__ inline bool dev_index_key(const DevTx &R, const uint64_t *bases, const uint8_t *digests, uint32_t ntx,
+                                     uint32_t t, uint32_t k[8]) {
+  if (!(R.flags & BDF_INDEX_OK)) return false;
+  if (!(R.flags & BDF_INDEX_FROM_TXID)) {
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(digests + ((size_t)BD_DIG_I * ntx + t) * 32);
+#pragma unroll
+    for (int i = 0; i < 8; i++) k[i] = d[i];
+    return true;
+  }
+  if (R.index_txid.len != 64) return false;
+  const uint8_t *s = reinterpret_cast<const uint8_t *>(bases[R.blk]) + R.index_txid.off;
+  uint8_t o[32];
+  for (int i = 0; i < 64; i++) {
+    const uint8_t c = s[i];
+    int v;
+    if (c >= '0' && c <= '9') v = c - '0';
+    else if (c >= 'a' && c <= 'f') v = c - 'a' + 10;
+    else return false;  // only lowercase hex can equal a VALID txid
+    if (i & 1) o[i >> 1] |= (uint8_t)v;
+    else o[i >> 1] = (uint8_t)(v << 4);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = (uint32_t)o[4 * i] | (uint32_t)o[4 * i + 1] << 8 | (uint32_t)o[4 * i + 2] << 16 |
+                                   (uint32_t)o[4 * i + 3] << 24;
+  return true;
 }
 
 }  // namespace
@@ -127,10 +160,46 @@ __global__ void k_fin_index(uint32_t P, const uint8_t *recs, const uint32_t *row
     }
   }
 }
+// k_fin_index for a single-device batch straight from the parse and the digests (one rank,
+// position p == tx t), so it runs beside the verify chain instead of after the fold: the
+// owners' keys go to `keys` (32 B per position), which k_fin_codes then compares against
+__global__ void k_fin_index_dev(uint32_t P, const DevTx *txs, const uint64_t *bases, const uint8_t *digests,
+                                uint8_t *keys, uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const DevTx &R = txs[p];
+  uint32_t k[8];
+  if (!dev_index_key(R, bases, digests, P, p, k)) return;
+  uint32_t *kd = reinterpret_cast<uint32_t *>(keys + (size_t)p * 32);
+#pragma unroll
+  for (int i = 0; i < 8; i++) kd[i] = k[i];
+  __threadfence();  // (the key is visible before the slot names its owner)
+  const uint64_t h = fin_hash(k, seed);
+  const int32_t b = (int32_t)R.blk;
+  for (uint32_t probe = 0; probe <= mask; probe++) {
+    const uint32_t s = (uint32_t)(h + probe) & mask;
+    uint32_t o = owner[s];
+    if (o == 0) {
+      o = atomicCAS(&owner[s], 0u, p + 1);
+      if (o == 0) {
+        atomicMin(&minblk[s], b);
+        return;
+      }
+    }
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(keys + (size_t)(o - 1) * 32);
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) eq &= __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k[i];
+    if (eq) {
+      atomicMin(&minblk[s], b);
+      return;
+    }
+  }
+}
 
 __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *rowmap, const uint32_t *blkof,
                             const uint32_t *owner, const int32_t *minblk, uint32_t *minvalid, uint32_t mask,
-                            uint64_t seed, uint8_t *flags, uint32_t *pslot) {
+                            uint64_t seed, uint8_t *flags, uint32_t *pslot, const uint8_t *keys) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   const uint32_t row = rowmap[p];
@@ -140,7 +209,7 @@ __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *row
   if (r[1] & FGV_TXR_REACHED) {
     uint32_t k[8];
     load_key(recs, row, OFF_TXID, k);
-    const int64_t s = tab_find(k, fin_hash(k, seed), owner, rowmap, recs, mask);
+    const int64_t s = tab_find(k, fin_hash(k, seed), owner, rowmap, recs, mask, keys);
     if (s >= 0) {
       if (minblk[s] < (int32_t)blkof[p]) code = 9;  // txid indexed by an earlier block of the batch
       slot = (uint32_t)s;

@@ -92,6 +92,10 @@ def corpus():
         case_envs = case[2]
         blks.append(block_from_envs(case_envs))
         rws += _rwsets(case_envs)
+    # key-level endorsement known answers (metadata writes, hashed metadata writes, dependencies)
+    from tests import sbe_cases
+    for case in sbe_cases.load()[:8]:
+        blks.append(case["block"])
     # orderer-signed blocks (metadata[SIGNATURES])
     from tests import blocksig_cases as BC
     for c in BC.cases()[:8]:

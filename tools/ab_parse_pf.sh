@@ -1,12 +1,14 @@
 #!/bin/bash
-# A/B: k_bd_parse prefetch of each envelope's first N bytes (FGV_PARSE_PF), alternating runs
+# A/B, alternating runs: k_bd_parse prefetch of each envelope's first N bytes (FGV_PARSE_PF) and
+# the finalize's txid index beside the verify chain (FGV_EARLY_FIN)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/ab_pf
 mkdir -p $O
 for rep in 1 2; do
-  for pf in 0 1024 4096 8192; do
-    FGV_PARSE_PF=$pf timeout -k 10 200 python -u bench.py --cpu-threads 0 --no-pcie --no-latency --steps 20 > $O/pf${pf}_$rep.json 2> $O/pf${pf}_$rep.err || { echo bench failed; tail -20 $O/pf${pf}_$rep.err; exit 1; }
-    python3 -c "import json; d=json.load(open('$O/pf${pf}_$rep.json')); kt=d.get('kernel_ms') or {}; print('pf=$pf', d['ms_per_step'], d['parity_vs_labels'], kt.get('k_bd_parse', kt))"
+  for cfg in "0 1" "0 0" "4096 1" "1024 1"; do
+    set -- $cfg
+    FGV_PARSE_PF=$1 FGV_EARLY_FIN=$2 timeout -k 10 200 python -u bench.py --cpu-threads 0 --no-pcie --no-latency --steps 20 > $O/pf$1_ef$2_$rep.json 2> $O/pf$1_ef$2_$rep.err || { echo bench failed; tail -20 $O/pf$1_ef$2_$rep.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/pf$1_ef$2_$rep.json')); k=d.get('kernel_ms') or {}; print('pf=$1 early_fin=$2', d['ms_per_step'], d['parity_vs_labels'], round(k.get('k_bd_parse', 0), 4), round(k.get('batch', 0), 4))"
   done
 done
