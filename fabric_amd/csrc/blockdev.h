@@ -25,6 +25,10 @@
 #define BD_MAX_GROUP 32    // nesting of unknown START_GROUP fields
 #define BD_MAX_PNODE 64    // policy tree nodes evaluated per policy (stack depth 16)
 #define BD_OCC (1 + BD_MAX_END)  // identity occurrences per tx: creator + endorsers
+// k_bd_ident: 16-lane groups per tx (launch: ntx x 16 x BD_ID_PAR threads).  4 resolves a C2
+// tx's occurrences at once, but its 4x waves slow k_bd_sha beside it more than they gain
+// (MI355X, C2 step 0.79 -> 0.83-0.86 ms): 1
+#define BD_ID_PAR 1u
 // k_bd_sha digest slots per tx: payload, endorsements 0..BD_MAX_END-1, txid, proposal, index
 #define BD_DIG_T (1 + BD_MAX_END)
 #define BD_DIG_P (2 + BD_MAX_END)

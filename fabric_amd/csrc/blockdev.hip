@@ -13,6 +13,7 @@
 // occurrence (k_bd_ident).  These are byte-walking kernels: latency-bound on dependent loads,
 // with every transaction of the batch in flight at once.
 #include <hip/hip_runtime.h>
+#include "fin_dev.h"
 #include <stdint.h>
 
 #include "../../include/fgv.h"
@@ -603,6 +604,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
 // The compare is split over the group's lanes a 32-bit word at a time (block bytes at any
 // alignment via v_alignbyte; registry fields are 4-byte aligned), then one ballot.
 #define ID_LANES 16u
+#define ID_PAR BD_ID_PAR
 DEV uint32_t ldu32(const uint8_t *p) {  // unaligned little-endian word (reads the next word too)
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
@@ -633,13 +635,16 @@ __global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__r
                                                   const uint64_t *__restrict__ bases, DevChannel ch,
                                                   int32_t *__restrict__ ident) {
   __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
-  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / ID_LANES;  // one group per tx
+  // ID_PAR groups per tx (one wave): group g resolves occurrences g, g + ID_PAR, ... -- a C2
+  // transaction's creator and endorsers in one pass instead of one after the other
+  const uint32_t grp = (blockIdx.x * blockDim.x + threadIdx.x) / ID_LANES;
+  const uint32_t t = grp / ID_PAR, g = grp % ID_PAR;
   const uint32_t l = threadIdx.x % ID_LANES;
   if (t >= ntx) return;  // whole groups exit together
   const DevTx &R = txs[t];
   const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
   const uint32_t nend = R.nend;
-  for (uint32_t k = 0; k <= nend; k++) {
+  for (uint32_t k = g; k <= nend; k += ID_PAR) {
     int32_t res = -1;
     // the creator is needed when the parse got past the channel check (pre still pending)
     const DSpan sp = k == 0 ? R.creator : R.end_ser[k - 1];
@@ -1274,7 +1279,7 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
                                                  const uint8_t *__restrict__ digests,
                                                  const uint8_t *__restrict__ vstatus,
                                                  fgv_tx_result *__restrict__ res, uint32_t *__restrict__ flags,
-                                                 const uint32_t *__restrict__ xhaz) {
+                                                 const uint32_t *__restrict__ xhaz, FinDev fin) {
   __builtin_amdgcn_s_setprio(3);  // back half; a next batch's front half may run beside it
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
@@ -1369,6 +1374,24 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
     }
   }
   if (code == C_UNSUPPORTED) atomicOr(flags, 2u);
+  if (fin.owner) {  // k_fin_codes (finalize.hip) for the single-device fused call
+    uint32_t slot = 0xFFFFFFFFu;
+    uint8_t c2 = code;
+    if (reached) {
+      uint32_t k[8];
+      const uint32_t *dw = reinterpret_cast<const uint32_t *>(txd);
+#pragma unroll
+      for (int i = 0; i < 8; i++) k[i] = dw[i];
+      const int64_t s = fin_find_keys(k, fin_hash(k, fin.seed), fin.owner, fin.keys, fin.mask);
+      if (s >= 0) {
+        if (fin.minblk[s] < (int32_t)R.blk) c2 = C_DUP_TXID;  // indexed by an earlier block of the batch
+        slot = (uint32_t)s;
+      }
+    }
+    if (c2 == C_VALID && slot != 0xFFFFFFFFu) atomicMin(&fin.minvalid[slot], t);
+    fin.flags[t] = c2;
+    fin.pslot[t] = slot;
+  }
   fgv_tx_result o;
   o.code = code;
   o.flags = 0;

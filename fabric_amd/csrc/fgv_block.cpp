@@ -43,6 +43,7 @@
 #include "fgv_visitors.h"
 #include "fgv_channel.h"
 #include "blockdev.h"
+#include "fin_dev.h"
 
 // ======================================================================= channel model
 // (fgv_channel.h)
@@ -1456,7 +1457,8 @@ __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases,
                           uint32_t *key_slot, uint32_t *dig_idx, uint32_t *nv_out);
 __global__ void k_bd_fold(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
                           const DevJobIdx *jobs, const uint32_t *totals, const uint8_t *digests,
-                          const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags, const uint32_t *xhaz);
+                          const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags, const uint32_t *xhaz,
+                          FinDev fin);
 
 // The batch head, one H2D copy: envelope table | block base addresses | 64 zero bytes (the
 // kernels' counters) | per-block dependency-extraction hazards (blockdev.h), each part 64-byte
@@ -1660,7 +1662,8 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[1], 0));
   HIP_TRY(hipEventRecord(B.ev[8], c->stream3));
   if (tim) HIP_TRY(hipEventRecord(B.ev[7], sf));
-  hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 + 255) / 256)), dim3(256), 0, sf, N, dtx, dbs, ch,
+  hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 * BD_ID_PAR + 255) / 256)), dim3(256), 0, sf, N, dtx,
+                     dbs, ch,
                      B.ident.as<int32_t>());
   hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
                      B.jobs.as<DevJobIdx>(), misc);
@@ -1767,8 +1770,20 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   if (rc) return rc;
   // (the digests were joined before k_prep: the verify stages always run, for the capacity)
   if (tim) HIP_TRY(hipEventRecord(c->kev[8], st));
+  // the finalize's codes step inside the fold once the early index (stream3) is there
+  FinDev fin{};
+  c->fold_codes = false;
+  if (c->early_fin) {
+    HIP_TRY(hipStreamWaitEvent(st, c->fin_ev, 0));
+    size_t cap = 1024;
+    while (cap < 2 * (size_t)N) cap <<= 1;
+    fin = FinDev{c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), c->fz_minvalid.as<uint32_t>(),
+                 c->fz_keys.as<uint8_t>(), c->fz_flags.as<uint8_t>(), c->fz_pslot.as<uint32_t>(),
+                 (uint32_t)(cap - 1), c->fin_seed};
+    c->fold_codes = true;
+  }
   hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
-                     B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5, misc + 16);
+                     B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5, misc + 16, fin);
   HIP_TRY(hipGetLastError());
   if (tim || c->ahead_mode == 3) HIP_TRY(hipEventRecord(c->kev[9], st));  // (ahead mode 3 waits on it)
   HIP_TRY(hipMemcpyAsync(B.misc.p, misc, 48, hipMemcpyDeviceToHost, st));

@@ -987,10 +987,12 @@ static int fin_front(fgv_ctx *c, hipStream_t st, size_t nblocks, uint32_t W, siz
   HIP_TRY(hipGetLastError());
   return FGV_OK;
 }
-static int fin_back(fgv_ctx *c, hipStream_t st, const FinPlan &F, const uint8_t *d_recs, const uint8_t *keys) {
+static int fin_back(fgv_ctx *c, hipStream_t st, const FinPlan &F, const uint8_t *d_recs, const uint8_t *keys,
+                    bool codes_done = false) {
   const uint32_t n32 = (uint32_t)F.P, mask = (uint32_t)(F.cap - 1);
   const dim3 grid((n32 + 255) / 256), blk(256);
-  hipLaunchKernelGGL(k_fin_codes, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
+  if (!codes_done)
+    hipLaunchKernelGGL(k_fin_codes, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
                      c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(),
                      c->fz_minvalid.as<uint32_t>(), mask, c->fin_seed, c->fz_flags.as<uint8_t>(),
                      c->fz_pslot.as<uint32_t>(), keys);
@@ -1023,8 +1025,8 @@ int fgv_finalize_early_index(fgv_ctx *c, size_t nblocks, const size_t *ntx, cons
 static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t W, size_t rows,
                              const uint8_t *d_recs, uint8_t *flags, const uint32_t *rank_lo = nullptr,
                              const uint32_t *rank_hi = nullptr, bool defer = false) {
-  const bool early = c->early_fin;
-  c->early_fin = false;
+  const bool early = c->early_fin, codes_done = c->fold_codes;
+  c->early_fin = c->fold_codes = false;
   if (((uintptr_t)d_recs & 3)) return FGV_EINVAL;
   FinPlan F;
   int rc = fin_prepare(c, nblocks, ntx, W, rows, rank_lo, rank_hi, F);
@@ -1032,7 +1034,7 @@ static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint
   hipStream_t st = c->stream;
   if (early && W == 1) {  // the front ran beside the verify chain (same plan: W = 1, rows = P)
     HIP_TRY(hipStreamWaitEvent(st, c->fin_ev, 0));
-    rc = fin_back(c, st, F, d_recs, c->fz_keys.as<uint8_t>());
+    rc = fin_back(c, st, F, d_recs, c->fz_keys.as<uint8_t>(), codes_done);
   } else {
     rc = fin_front(c, st, nblocks, W, rows, F, d_recs, nullptr, nullptr, nullptr);
     if (!rc) rc = fin_back(c, st, F, d_recs, nullptr);
@@ -1353,7 +1355,7 @@ static int validate_blocks_locked(fgv_ctx *c, size_t nblocks, const uint8_t *con
     c->want_early_fin = false;
     if (rc) {
       fgv_block_validate_dev_finish(c, c->blk);  // (waits for anything already queued)
-      c->early_fin = false;
+      c->early_fin = c->fold_codes = false;
       return rc;
     }
     size_t total = 0;

@@ -122,6 +122,7 @@ struct fgv_ctx {
   // early txid index of a single-device batch (fgv_finalize_early_index): set by the fused
   // validate call before the device enqueue, consumed by its finalize
   bool want_early_fin = false, early_fin = false;
+  bool fold_codes = false;  // k_bd_fold ran the finalize's codes step (the finalize runs the rest)
   bool early_fin_on = [] {  // A/B knob FGV_EARLY_FIN=0: the whole finalize after the fold
     const char *e = getenv("FGV_EARLY_FIN");
     return !(e && atoi(e) == 0);

@@ -24,24 +24,13 @@
 
 #include "../../include/fgv.h"
 #include "blockdev.h"
+#include "fin_dev.h"
 #include "fgv_kernels.h"
 
 namespace {
 
 constexpr uint32_t REC = 68;
 constexpr uint32_t OFF_TXID = 4, OFF_INDEX = 36;
-
-__device__ inline uint64_t fin_hash(const uint32_t *k, uint64_t seed) {
-  uint64_t h = seed;
-#pragma unroll
-  for (int i = 0; i < 8; i += 2) {
-    const uint64_t w = (uint64_t)k[i] | ((uint64_t)k[i + 1] << 32);
-    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
-    h ^= h >> 29;
-  }
-  h *= 0xBF58476D1CE4E5B9ull;
-  return h ^ (h >> 31);
-}
 
 __device__ inline void load_key(const uint8_t *recs, uint32_t row, uint32_t off, uint32_t k[8]) {
   const uint32_t *q = reinterpret_cast<const uint32_t *>(recs + (size_t)row * REC + off);
