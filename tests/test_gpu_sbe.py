@@ -183,3 +183,35 @@ def test_mvcc_commit_keeps_parameters():
         assert eng.kvmeta_count() == len(db.kvmeta)
     assert changed >= 3
     eng.close()
+
+
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_group_and_block_shards(ndev):
+    """key-level blocks through fgv_group (several device contexts, block plan, gather, finalize
+    on the first) and through block-granular shards (fgv_validate_shard): equal to the oracle"""
+    net = network()
+    ccs = _net_ccs(net)
+    sb = [sbe_cases.make_sbe_block(net, 40, 700 + k, number=1 + k) for k in range(4)]
+    kvmeta = {}
+    for _, kv in sb:
+        kvmeta.update(kv)
+    blks = [b for b, _ in sb] + [blocks.make_block(net, 60, number=5, seed=705)[0]]
+    exp = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=kvmeta), blks)
+    g = _lib.Group([0] * ndev)
+    for e in g.engines:
+        txvalidator.setup_channel(e, net.channel, net.identities(), ccs, kvmeta=kvmeta)
+    got = g.validate_blocks(blks)
+    assert [list(f) for f in got] == exp
+    g.close()
+    eng = _eng(net.channel, net.identities(), ccs, kvmeta, 0)
+    # block-granular shards of the batch: each shard's records equal the whole-batch oracle's
+    # codes before the batch finalize (no duplicate txids in these blocks)
+    nb = len(blks)
+    for lo_b, hi_b in [(0, 2), (2, nb)]:
+        from fabric_amd import shard
+        lo = [0 if lo_b <= b < hi_b else shard.SKIP for b in range(nb)]
+        hi = [len(exp[b]) if lo_b <= b < hi_b else shard.SKIP for b in range(nb)]
+        res, ntx = eng.validate_shard(blks, lo, hi)
+        want = [c for b in range(lo_b, hi_b) for c in exp[b]]
+        assert list(res[:, 0]) == want
+    eng.close()
