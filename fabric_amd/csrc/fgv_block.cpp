@@ -665,8 +665,10 @@ static void add_deps(const Span &results, uint32_t i, SbeBlock &B) {
 // first error; the outcomes are pure, so the verdict is the same) and a step outside the model
 // anywhere makes the tx unsupported, as in the oracle.  `hang`: an earlier tx never signalled
 // its dependencies (GetValidationParameterForKey would wait forever).
+// touched != null (the parallel first pass): an earlier metadata writer of a key only sets
+// *touched -- the tx is folded again in block order once the writers' results are final.
 static int sbe_vscc(const Channel &ch, const CCInfo &cc, std::string_view ns, const VNsRwSet *nrw, uint32_t i,
-                    const SbeBlock &B, bool hang, const std::function<int(int)> &eval) {
+                    const SbeBlock &B, bool hang, const std::function<int(int)> &eval, bool *touched = nullptr) {
   int ok = 1;
   bool some = false, cc_checked = false;
   pbw::SmallVec<Span, 4> colls_checked;
@@ -678,6 +680,10 @@ static int sbe_vscc(const Channel &ch, const CCInfo &cc, std::string_view ns, co
     if (d != B.deps.end())
       for (uint32_t j : d->second) {
         if (j >= i) continue;
+        if (touched) {
+          *touched = true;
+          continue;
+        }
         const int r = B.result(j, ns);
         if (r < 0 || r == VR_INDET) return false;
         updated |= r == VR_PASS;
@@ -919,7 +925,10 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   }
   static const char HEX[] = "0123456789abcdef";
   std::atomic<bool> unsupported{false};
-  auto fold_one = [&](size_t t) {
+  // pass 0: no key-level state (parallel); 1: key-level, every tx in parallel, a tx whose written
+  // key has an earlier metadata writer only marked; 2: the marked txs again, in block order
+  std::vector<uint8_t> touched(sequential ? total : 0, 0);
+  auto fold_one = [&](size_t t, int pass) {
     const TxRec &R = recs[t];
     const size_t b = where[t].first;
     const uint32_t bi = where[t].second;
@@ -973,7 +982,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
           }
         };
         bool has25 = false, has10 = false, unsup = false;
-        if (!sequential) {
+        if (pass == 0) {
           for (int pi : R.policies) {
             if (pi == -2) { unsup = true; break; }
             if (pi == -1) { has25 = true; continue; }
@@ -1016,10 +1025,15 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
             int r;
             if (it == ch.ccs.end() || it->second.status == 1) r = -1;
             else if (it->second.status != 0) r = 2;
-            else r = sbe_vscc(ch, it->second, sv(ns), k >= 0 ? &rw.ns[k] : nullptr, bi, sbe[b],
-                              xfail[b] < bi, eval);
+            else {
+              bool tch = false;
+              r = sbe_vscc(ch, it->second, sv(ns), k >= 0 ? &rw.ns[k] : nullptr, bi, sbe[b], xfail[b] < bi, eval,
+                           pass == 1 ? &tch : nullptr);
+              if (tch) touched[t] = 1;
+            }
             rs.push_back(r);
           }
+          sbe[b].res[bi].clear();
           for (size_t q = 0; q < wr.size(); q++) {
             unsup |= rs[q] == 2;
             has25 |= rs[q] == -1;
@@ -1058,10 +1072,13 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
       }
     }
   };
-  if (sequential)  // block order: a tx reads the vscc results of earlier ones
-    for (size_t t = 0; t < total; t++) fold_one(t);
-  else
-    S->pool.parallel_for(total, fold_one);
+  if (sequential) {  // block order for the txs that read the vscc results of earlier ones
+    S->pool.parallel_for(total, [&](size_t t) { fold_one(t, 1); });
+    for (size_t t = 0; t < total; t++)
+      if (touched[t]) fold_one(t, 2);
+  } else {
+    S->pool.parallel_for(total, [&](size_t t) { fold_one(t, 0); });
+  }
   c->t_host_fold = ms_since(t_fold);
   if (unsupported) return FGV_EUNSUPPORTED;
   return FGV_OK;

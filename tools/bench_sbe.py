@@ -1,0 +1,48 @@
+"""Throughput of key-level-endorsement batches (profiling aid, not the bench contract): 32
+generated 500-tx blocks of namespace mycc with key-level parameters in state, metadata writes and
+in-block dependencies (tests/sbe_cases.py) -- the sequential host fold with GPU verification --
+against the same blocks with no key-level state, which the device fold takes.  Parity with the
+oracle is checked on the first batch of each; prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    from fabric_amd import _lib, txvalidator
+    from oracle import v20
+    from tests import sbe_cases
+    from tests.blockfix import network
+    net = network()
+    ccs = {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
+    nb, ntx, steps = 32, 500, 10
+    made = [sbe_cases.make_sbe_block(net, ntx, 5000 + k, number=1 + k, nkeys=2000, vp_keys=400) for k in range(nb)]
+    blks = [b for b, _ in made]
+    kvmeta = {}
+    for _, kv in made:
+        kvmeta.update(kv)
+    out = {}
+    for name, kv in (("key_level", kvmeta), ("plain", {})):
+        eng = _lib.Engine(0)
+        txvalidator.setup_channel(eng, net.channel, net.identities(), ccs, kvmeta=kv)
+        exp = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=kv), blks)
+        got = [list(f) for f in eng.validate_blocks(blks)]
+        assert got == exp, name
+        eng.validate_blocks(blks)
+        t = time.perf_counter()
+        for _ in range(steps):
+            eng.validate_blocks(blks)
+        el = (time.perf_counter() - t) / steps
+        out[name] = dict(ms_per_batch=round(el * 1e3, 3), tx_per_s=round(nb * ntx / el, 1),
+                         valid=sum(f.count(0) for f in exp), policy_failures=sum(f.count(10) for f in exp),
+                         host_timing_ms=eng.host_timing())
+        eng.close()
+    print(json.dumps(dict(workload="32 x 500-tx key-level blocks (tools/bench_sbe.py)", parity=True, **out)))
+
+
+if __name__ == "__main__":
+    main()
