@@ -351,7 +351,7 @@ DEV uint8_t extract_walk(S d, ParseLds &L, uint32_t lane, bool &md, bool &ovf) {
 __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                  const uint64_t *__restrict__ bases, DevChannel ch,
                                                  DevTx *__restrict__ out, uint32_t *__restrict__ flags,
-                                                 uint32_t *__restrict__ xhaz, uint32_t prefetch) {
+                                                 uint32_t *__restrict__ xhaz) {
   // front half: below the back half's verify chain (3), above k_bd_sha_payload (1)
   __builtin_amdgcn_s_setprio(2);
   __shared__ ParseLds L;
@@ -362,21 +362,6 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
   const uint32_t blk = et[0];
   const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
   const S d{base + et[1], et[2]};
-  // optional: touch every 128-byte line of the envelope up to `prefetch` bytes, 8 independent
-  // loads per wait, so the walk's dependent loads hit the cache (A/B knob FGV_PARSE_PF)
-  uint32_t pf = 0;
-  {
-    // (lines from the one holding d.p up to the one holding byte lim - 1: all inside the block)
-    const uint32_t *w0 = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(d.p) & ~(uintptr_t)127);
-    const uint32_t end = (uint32_t)(reinterpret_cast<uintptr_t>(d.p) & 127u) + (d.n < prefetch ? d.n : prefetch);
-    for (uint32_t o = 0; o < end; o += 8 * 128) {
-      uint32_t x[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) x[k] = o + 128u * k < end ? w0[(o + 128u * k) / 4] : 0u;
-#pragma unroll
-      for (int k = 0; k < 8; k++) pf ^= x[k];
-    }
-  }
   DevTx &O = out[t];  // endorsements are written straight into it; the rest at the end
   struct {
     uint32_t blk;
@@ -574,7 +559,6 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
   if (xs == X_FAIL) atomicMin(&xhaz[2 * blk], t + 1);
   if (xs == X_PANIC) atomicMin(&xhaz[2 * blk + 1], t + 1);
   if (ovf || md || vpns) atomicOr(flags, 1u);  // capacity, or key-level endorsement: host parser
-  if (pf == 0x9E3779B9u && d.n == 1u) atomicOr(flags, 0u);  // (keeps the prefetch loads)
   O.blk = R.blk;
   O.pre = R.pre;
   O.etx = R.etx;

@@ -212,6 +212,7 @@ struct BdSet {
   SplitOut so;
   bool presplit = false;
   bool force_host = false;  // a shard's block prefix writes metadata (host parser)
+  const uint32_t *misc_src = nullptr;  // the batch counters in HBM (copied back by the finish)
   bool timed = false;  // its front half recorded the timing-only events
   hipStream_t stream = nullptr;  // the stream its parse / identity / count chain ran on
   size_t eoff = 0, moff = 0;
@@ -1458,7 +1459,7 @@ static int build_committed(fgv_block_state *S) {
 }
 
 __global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, DevChannel ch, DevTx *out,
-                           uint32_t *flags, uint32_t *xhaz, uint32_t prefetch);
+                           uint32_t *flags, uint32_t *xhaz);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
@@ -1657,12 +1658,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(128), 0, c->stream2, N, envtab, dbs,
                      B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
   HIP_TRY(hipEventRecord(B.ev[1], c->stream2));
-  static const uint32_t parse_pf = [] {  // A/B knob: bytes of each envelope touched up front
-    const char *e = getenv("FGV_PARSE_PF");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
-  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16,
-                     parse_pf);
+  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16);
   HIP_TRY(hipEventRecord(B.ev[4], sf));
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one
@@ -1803,7 +1799,9 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
                      B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5, misc + 16, fin);
   HIP_TRY(hipGetLastError());
   if (tim || c->ahead_mode == 3) HIP_TRY(hipEventRecord(c->kev[9], st));  // (ahead mode 3 waits on it)
-  HIP_TRY(hipMemcpyAsync(B.misc.p, misc, 48, hipMemcpyDeviceToHost, st));
+  // (the counters' D2H is queued by fgv_block_validate_dev_finish, behind whatever the caller
+  // queues after the fold -- the finalize -- so it never sits between the fold and the finalize)
+  B.misc_src = misc;
   c->t_bd_pre = ms_since(t1);
   c->t_host_assemble = c->t_bd_pre;
   S->t_enq = clk::now();
@@ -1841,6 +1839,8 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   if (S->pending < 0) return FGV_OK;
   BdSet &B = S->set[S->pending];
   S->pending = -1;
+  if (B.misc_src) HIP_TRY(hipMemcpyAsync(B.misc.p, B.misc_src, 48, hipMemcpyDeviceToHost, c->stream));
+  B.misc_src = nullptr;
   HIP_TRY(fgv_stream_wait(c->stream, c->spin));
   fgv_read_block_job_times(c);
   {  // per-kernel device times (fgv_last_kernel_times)

@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B, alternating runs: k_bd_parse prefetch of each envelope's first N bytes (FGV_PARSE_PF) and
+# A/B, alternating runs (round 2, kept as the record of profiles/round2_ab/): k_bd_parse prefetch of each
+# envelope's first N bytes (FGV_PARSE_PF, measured no gain and removed from the kernel) and
 # the finalize's txid index beside the verify chain (FGV_EARLY_FIN)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
