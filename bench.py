@@ -64,7 +64,11 @@ def pmc_traffic(workload):
     try:
         d = json.load(open(files[-1]))
         t = d["workloads"][workload]
-        return t["hbm_bytes"], f"{os.path.basename(files[-1])}: {t['kernel']} fetch {t['fetch_bytes']} B + write {t['write_bytes']} B"
+        if "hbm_bytes" in t:
+            return t["hbm_bytes"], (f"{os.path.basename(files[-1])}: {t['kernel']} fetch {t['fetch_bytes']} B + "
+                                    f"write {t['write_bytes']} B")
+        return t["hbm_bytes_per_block"], (f"{os.path.basename(files[-1])}: per block, {len(t['kernels'])} kernels, "
+                                          f"fetch {t['fetch_bytes_per_block']} B + write {t['write_bytes_per_block']} B")
     except (KeyError, ValueError, OSError):
         return None, None
 
@@ -81,22 +85,23 @@ def roofline(n_verifies, point_ms, workload):
 
 
 def block_roofline(kavg, pay_blocks, verifies, workload):
-    """roofline of the committer step: the kernel with the largest per-step device time
-    (fgv_last_kernel_times, HIP events on each kernel's own stream) -- k_bd_sha_payload at
-    C2 sizes: SHA-256 compressions x 2.7e3 int32 ops / its time vs the 78.6 T
-    int32 lane-op peak -- and k_point28 as the second entry."""
+    """roofline of the committer step's dominant kernel, k_point28 (the longest per-step kernel in
+    the rocprofv3 kernel trace of a 32-block-step run, profiles/round3_block_kernel_stats.csv):
+    v_mad_u64_u32 products of the comb (PRODUCTS_POINT per verify) / its per-step time (HIP
+    events on its own stream) vs the measured 31.06 T/s chip peak.  Second: k_bd_sha_payload,
+    SHA-256 compressions x 2.7e3 int32 ops vs the 78.6 T int32 lane-op peak."""
     cands = {k: v for k, v in kavg.items() if k != "batch"}
-    dom = max(cands, key=cands.get) if cands else "k_bd_sha_payload"
+    r = roofline(verifies, kavg.get("k_point28", 0.0), workload + "_point")
+    r["dominant_kernel_live"] = max(cands, key=cands.get) if cands else None
+    r["per_launch_verifies"] = int(verifies)
     t_pay = kavg.get("k_bd_sha_payload", 0.0) / 1e3
     ach = pay_blocks * SHA_OPS_PER_COMPRESSION / t_pay / 1e12 if t_pay > 0 else 0.0
     traffic, src = pmc_traffic(workload)
-    r = dict(bound="valu", achieved=round(ach, 3), peak=round(PEAK_INT32_OPS / 1e12, 1), unit="Tops/s",
-             frac=round(ach * 1e12 / PEAK_INT32_OPS, 4), traffic=traffic, traffic_source=src,
-             kernel="k_bd_sha_payload", dominant_kernel=dom, kernel_avg_ms=round(t_pay * 1e3, 4),
-             per_launch_compressions=int(pay_blocks),
-             work_unit="SHA-256 compressions x 2.7e3 simple int32 ops (SURVEY.md s8(d))")
-    r["second"] = roofline(verifies, kavg.get("k_point28", 0.0), workload + "_point")
-    r["second"]["kernel"] = "k_point28 (+ k_point hand-overs)"
+    r["second"] = dict(bound="valu", achieved=round(ach, 3), peak=round(PEAK_INT32_OPS / 1e12, 1), unit="Tops/s",
+                       frac=round(ach * 1e12 / PEAK_INT32_OPS, 4), traffic=traffic, traffic_source=src,
+                       kernel="k_bd_sha_payload", kernel_avg_ms=round(t_pay * 1e3, 4),
+                       per_launch_compressions=int(pay_blocks),
+                       work_unit="SHA-256 compressions x 2.7e3 simple int32 ops (SURVEY.md s8(d))")
     return r
 
 

@@ -758,6 +758,44 @@ static int sbe_vscc(const Channel &ch, const CCInfo &cc, std::string_view ns, co
   return ok;
 }
 
+// (oracle keylevel_writes) the kvkeys one tx may change the key-level state of -- its metadata
+// writes, its deletes of keys holding a VALIDATION_PARAMETER (tx_ops.go:17-51) -- and every key it
+// writes or metadata-writes; nothing when the rwset does not decode
+static void kl_keys(const Channel &ch, const Span &results, std::vector<std::string> &changed,
+                    std::vector<std::string> &touched) {
+  VTxRwSet rw;
+  if (!pbw::decode(results.p, results.n, rw)) return;
+  std::vector<std::string> c, t;
+  for (const VNsRwSet &n : rw.ns) {
+    std::vector<VKVWrite> ws;
+    std::vector<Span> mk;
+    VKVRWSet kv;
+    kv.writes = &ws;
+    kv.meta_keys = &mk;
+    if (!pbw::decode(n.rwset.p, n.rwset.n, kv)) return;
+    for (const VKVWrite &w : ws) {
+      t.push_back(Channel::kvkey(sv(n.ns), "", sv(w.key)));
+      if (w.is_delete && ch.kvmeta.count(t.back())) c.push_back(t.back());
+    }
+    for (const Span &k : mk) t.push_back(Channel::kvkey(sv(n.ns), "", sv(k))), c.push_back(t.back());
+    for (const VCollHashed &cl : n.coll) {
+      std::vector<VHashWrite> hw;
+      std::vector<Span> hk;
+      VHashedRWSet h;
+      h.writes = &hw;
+      h.meta_keys = &hk;
+      if (!pbw::decode(cl.hashed.p, cl.hashed.n, h)) return;
+      for (const VHashWrite &w : hw) {
+        t.push_back(Channel::kvkey(sv(n.ns), sv(cl.name), sv(w.key)));
+        if (w.is_delete && ch.kvmeta.count(t.back())) c.push_back(t.back());
+      }
+      for (const Span &k : hk) t.push_back(Channel::kvkey(sv(n.ns), sv(cl.name), sv(k))), c.push_back(t.back());
+    }
+  }
+  changed.insert(changed.end(), c.begin(), c.end());
+  touched.insert(touched.end(), t.begin(), t.end());
+}
+
 static inline uint32_t sha_blocks(const ShaJob &j) { return (j.n[0] + j.n[1] + j.n[2] + 8) / 64 + 1; }
 
 int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
@@ -924,8 +962,52 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     for (size_t t = 0; t < total; t++)
       if (recs[t].has_md && recs[t].xstat == X_OK) add_deps(recs[t].results, where[t].second, sbe[where[t].first]);
   }
+  // The batch validates every block against the key-level state committed before it, but the
+  // reference commits block k before block k+1's vscc reads GetStateMetadata.  A key whose
+  // parameter an earlier block may change (metadata write; delete of a key holding one) and a
+  // later block writes: the outcome depends on block k's validity and MVCC -> unsupported (oracle
+  // check_keylevel_batch).  Another rank's later block (SKIP) is walked when its bytes are there;
+  // an empty placeholder is unknown: a change before it is enough.
+  c->kl_changes = false;
+  if (sequential) {
+    std::vector<std::vector<std::string>> chg(nblocks), tch(nblocks);
+    std::vector<uint8_t> unknown(nblocks, 0);
+    for (size_t b = 0; b < nblocks; b++) {
+      if (tx_lo && tx_lo[b] == FGV_SHARD_SKIP) {
+        VBlock blk;
+        if (!lens[b] || !pbw::decode(h_blocks[b], lens[b], blk)) {
+          unknown[b] = 1;
+          continue;
+        }
+        for (const Span &d : blk.data.data) {
+          TxRec tmp;
+          extract_walk(d, tmp);
+          if (tmp.xstat == X_OK) kl_keys(ch, tmp.results, chg[b], tch[b]);
+        }
+        continue;
+      }
+      for (uint32_t i = 0; i < (uint32_t)envs[b].size(); i++) {
+        if (i >= lo[b] && i < hi[b]) continue;  // (another rank's transactions of this block)
+        TxRec tmp;
+        extract_walk(envs[b][i], tmp);
+        if (tmp.xstat == X_OK) kl_keys(ch, tmp.results, chg[b], tch[b]);
+      }
+    }
+    for (size_t t = 0; t < total; t++)
+      if (recs[t].xstat == X_OK) kl_keys(ch, recs[t].results, chg[where[t].first], tch[where[t].first]);
+    std::unordered_set<std::string> changed;
+    for (size_t b = 0; b < nblocks; b++) {
+      if (unknown[b]) {
+        if (!changed.empty()) return FGV_EUNSUPPORTED;
+        continue;
+      }
+      for (const std::string &k : tch[b])
+        if (changed.count(k)) return FGV_EUNSUPPORTED;
+      changed.insert(chg[b].begin(), chg[b].end());
+    }
+    c->kl_changes = !changed.empty();
+  }
   static const char HEX[] = "0123456789abcdef";
-  std::atomic<bool> unsupported{false};
   // pass 0: no key-level state (parallel); 1: key-level, every tx in parallel, a tx whose written
   // key has an earlier metadata writer only marked; 2: the marked txs again, in block order
   std::vector<uint8_t> touched(sequential ? total : 0, 0);
@@ -1054,7 +1136,6 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         else if (has10) code = C_POLICY;
       }
     }
-    if (code == C_UNSUPPORTED) unsupported = true;
     fgv_tx_result &o = res_out[t];
     memset(&o, 0, sizeof o);
     o.code = code;
@@ -1081,7 +1162,33 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     S->pool.parallel_for(total, [&](size_t t) { fold_one(t, 0); });
   }
   c->t_host_fold = ms_since(t_fold);
-  if (unsupported) return FGV_EUNSUPPORTED;
+  // (from the final codes: a pass-1 verdict of a tx folded again in pass 2 does not count)
+  for (size_t t = 0; t < total; t++)
+    if (res_out[t].code == C_UNSUPPORTED) return FGV_EUNSUPPORTED;
+  return FGV_OK;
+}
+
+int fgv_block_kl_check(fgv_block_state *S, size_t nblocks, const uint8_t *const *blocks, const size_t *lens) {
+  Channel &ch = S->ch;
+  if (ch.dirty) ch.compile();
+  std::vector<std::vector<std::string>> chg(nblocks), tch(nblocks);
+  std::vector<int> bad(nblocks, 0);
+  S->pool.parallel_for(nblocks, [&](size_t b) {
+    VBlock blk;
+    if (!pbw::decode(blocks[b], lens[b], blk)) { bad[b] = 1; return; }
+    for (const Span &d : blk.data.data) {
+      TxRec tmp;
+      extract_walk(d, tmp);
+      if (tmp.xstat == X_OK) kl_keys(ch, tmp.results, chg[b], tch[b]);
+    }
+  });
+  std::unordered_set<std::string> changed;
+  for (size_t b = 0; b < nblocks; b++) {
+    if (bad[b]) return FGV_EINVAL;
+    for (const std::string &k : tch[b])
+      if (changed.count(k)) return FGV_EUNSUPPORTED;
+    changed.insert(chg[b].begin(), chg[b].end());
+  }
   return FGV_OK;
 }
 

@@ -139,6 +139,14 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
     else if (rc) return rc;
   }
   if (unsup) return FGV_EUNSUPPORTED;
+  // a device whose blocks may change key-level state while a later device's blocks were
+  // validated against the state before them (fgv_block_validate_impl's batch rule across devices)
+  for (size_t r = 0; r + 1 < W; r++)
+    if (b0[r + 1] > b0[r] && b0[r + 1] < nblocks && g->ctx[r]->kl_changes) {
+      const int rc = fgv_block_kl_check(g->ctx[0]->blk, nblocks, blocks, lens);  // (the whole batch, host)
+      if (rc) return rc;
+      break;
+    }
   size_t all = 0, rows = 0;
   std::vector<size_t> nrec(W, 0);
   for (size_t r = 0; r < W; r++) {

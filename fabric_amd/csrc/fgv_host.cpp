@@ -909,10 +909,6 @@ int fgv_ledger_add_txids(fgv_ctx *c, const uint8_t *buf, const uint64_t *off, co
 // Three parts: fin_prepare (host metadata, buffers), fin_front (metadata upload, row map +
 // table reset, the txid index) and fin_back (codes, duplicates, flags D2H).  A single-device
 // batch runs fin_front early, beside its verify chain (fgv_finalize_early_index).
-struct FinPlan {
-  uint64_t P = 0;
-  size_t cap = 0, wn = 0, meta = 0;
-};
 static int fin_prepare(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t W, size_t rows, const uint32_t *rank_lo,
                        const uint32_t *rank_hi, FinPlan &F) {
   if (W == 0 || (!rank_lo) != (!rank_hi)) return FGV_EINVAL;
@@ -1018,6 +1014,7 @@ int fgv_finalize_early_index(fgv_ctx *c, size_t nblocks, const size_t *ntx, cons
   rc = fin_front(c, st, nblocks, 1, total, F, nullptr, dtx, bases, digests);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c->fin_ev, st));
+  c->early_plan = F;
   c->early_fin = true;
   return FGV_OK;
 }
@@ -1029,13 +1026,21 @@ static int finalize_dev_core(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint
   c->early_fin = c->fold_codes = false;
   if (((uintptr_t)d_recs & 3)) return FGV_EINVAL;
   FinPlan F;
-  int rc = fin_prepare(c, nblocks, ntx, W, rows, rank_lo, rank_hi, F);
-  if (rc || F.P == 0) return rc;
+  int rc;
   hipStream_t st = c->stream;
-  if (early && W == 1) {  // the front ran beside the verify chain (same plan: W = 1, rows = P)
+  uint64_t P = 0;
+  for (size_t b = 0; b < nblocks; b++) P += ntx[b];
+  if (early && W == 1 && c->early_plan.P == P) {  // the front ran beside the verify chain (W = 1, rows = P)
+    // (its plan is reused: preparing again would rewrite the pinned metadata while the front's
+    // copy of it may still be queued)
+    F = c->early_plan;
+    if (F.P == 0) return FGV_OK;
     HIP_TRY(hipStreamWaitEvent(st, c->fin_ev, 0));
     rc = fin_back(c, st, F, d_recs, c->fz_keys.as<uint8_t>(), codes_done);
   } else {
+    if (early) HIP_TRY(hipEventSynchronize(c->fin_ev));  // (its metadata copy reads c->hb_fz)
+    rc = fin_prepare(c, nblocks, ntx, W, rows, rank_lo, rank_hi, F);
+    if (rc || F.P == 0) return rc;
     rc = fin_front(c, st, nblocks, W, rows, F, d_recs, nullptr, nullptr, nullptr);
     if (!rc) rc = fin_back(c, st, F, d_recs, nullptr);
   }
@@ -1180,6 +1185,7 @@ int fgv_validate_shard(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks,
 static int shard_dev_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                             const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
                             void *d_results, size_t results_cap, size_t *ntx) {
+  c->kl_changes = false;  // (set by the host-parse path only: plain batches change no key-level state)
   if (nblocks == 0) return FGV_OK;
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
   std::vector<const uint8_t *> dev;

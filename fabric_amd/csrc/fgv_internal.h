@@ -92,6 +92,12 @@ inline void be32_to_limbs(const uint8_t *b, uint32_t *l) {
 }  // namespace fgvh
 using namespace fgvh;
 
+// the finalize's plan for one batch (fgv_host.cpp fin_prepare)
+struct FinPlan {
+  uint64_t P = 0;
+  size_t cap = 0, wn = 0, meta = 0;
+};
+
 struct fgv_ctx {
   fgv_mvcc_state *mv = nullptr;
   int device = 0;
@@ -140,6 +146,10 @@ struct fgv_ctx {
   uint64_t n_sha_jobs = 0, n_sha_blocks = 0, n_verifies = 0;  // last call
   double t_mvcc_lookup = 0, t_mvcc_total = 0;
   double t_host_parse = 0, t_host_assemble = 0, t_host_device = 0, t_host_fold = 0;
+  // the last validate call saw a tx that may change key-level state (a metadata write, a delete
+  // of a key holding a parameter): a group with later blocks on another device is unsupported
+  bool kl_changes = false;
+  FinPlan early_plan;  // the plan fgv_finalize_early_index prepared (its metadata copy may be pending)
   uint64_t n_mvcc_reads = 0, n_mvcc_writes = 0;
   // deliver-side integrity (fgv_integrity.cpp): own host pool, own lock -- runs concurrently
   // with committer calls on the same context
@@ -236,6 +246,9 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
                             const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                             const uint32_t *tx_hi, fgv_tx_result *res_out, size_t res_cap, size_t *ntx_out);
 long fgv_block_count_txs(const uint8_t *b, size_t n);
+// the key-level batch rule of fgv_block_validate_impl over whole blocks (a group's device ranges
+// together): FGV_EUNSUPPORTED when a block may change the parameter of a key a later block writes
+int fgv_block_kl_check(fgv_block_state *S, size_t nblocks, const uint8_t *const *blocks, const size_t *lens);
 int fgv_finalize_impl(size_t nblocks, const size_t *ntx, const fgv_tx_result *res, uint8_t *flags);
 
 // Pinned host staging for one block batch's device jobs (valid until the next reserve).

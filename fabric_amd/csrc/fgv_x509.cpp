@@ -160,181 +160,238 @@ std::string name_string(const uint8_t *b, const T &t) {
   return std::string((const char *)p, n);
 }
 
+// cryptobyte.String over b[s..e): each read mirrors the Go call named beside it.  A read Go
+// makes that fails is a parse error (X_PARSE, Go's ParseCertificate returns an error); bytes Go
+// leaves unread where this restatement would need to know what Go does with them are X_UNSUP.
+struct Rd {
+  const uint8_t *b;
+  size_t s, e;
+  bool empty() const { return s >= e; }
+  bool peek(uint8_t tag) const { return s < e && b[s] == tag; }  // PeekASN1Tag
+  T any() {  // ReadAnyASN1Element
+    const T t = tlv(b, s, e);
+    s = t.ce;
+    return t;
+  }
+  T elem(uint8_t tag) {  // ReadASN1Element / ReadASN1 with a tag
+    const T t = any();
+    if (t.tag != tag) perr();
+    return t;
+  }
+  Rd in(const T &t) const { return Rd{b, t.cs, t.ce}; }
+  void rest_unread() const {  // Go ignores what is left here: outside the model
+    if (!empty()) unsup();
+  }
+};
+
+// ReadASN1BitString's validity rules (padding count <= 7, none without data, padding bits zero)
+void bitstring_ok(const uint8_t *b, const T &t) {
+  if (t.ce == t.cs || b[t.cs] > 7 || (t.ce - t.cs == 1 && b[t.cs]) || (b[t.ce - 1] & ((1u << b[t.cs]) - 1))) perr();
+}
+
+// parseName: RDNSequence of SETs of AttributeTypeAndValue {OID, any string}; what an attribute
+// holds after its value is never read by Go (nor here)
 void name_ous(const uint8_t *b, const T &name, std::vector<std::string> *out) {
-  for (const T &rdn : children(b, name.cs, name.ce)) {
-    if (rdn.tag != 0x31) perr();
-    for (const T &atv : children(b, rdn.cs, rdn.ce)) {
-      if (atv.tag != 0x30) perr();
-      // parseName reads the type and the value; anything after them is not read
-      const T t1 = tlv(b, atv.cs, atv.ce);
+  Rd raw{b, name.cs, name.ce};
+  while (!raw.empty()) {
+    Rd set = raw.in(raw.elem(0x31));
+    while (!set.empty()) {
+      Rd atv = set.in(set.elem(0x30));
+      const T t1 = atv.elem(0x06);
       if (!valid_oid(b, t1)) perr();
-      const T t2 = tlv(b, t1.ce, atv.ce);
-      std::string s = name_string(b, t2);  // every attribute value parses
+      const T t2 = atv.any();
+      std::string s = name_string(b, t2);  // parseASN1String: every attribute value parses
       if (out && eq(b, t1, OID_OU, sizeof OID_OU)) out->push_back(std::move(s));
     }
   }
 }
 
-bool der_bool(const uint8_t *b, const T &t) {
+bool der_bool(const uint8_t *b, const T &t) {  // ReadASN1Boolean
   if (t.ce - t.cs != 1 || (b[t.cs] != 0x00 && b[t.cs] != 0xFF)) perr();
   return b[t.cs] == 0xFF;
 }
 
+// ReadASN1Integer into a Go int (64-bit): minimal, at most 8 bytes
+int64_t int64_of(const uint8_t *b, const T &t) {
+  if (t.tag != 0x02 || !int_minimal(b, t.cs, t.ce) || t.ce - t.cs > 8) perr();
+  int64_t x = (b[t.cs] & 0x80) ? -1 : 0;
+  for (size_t q = t.cs; q < t.ce; q++) x = (int64_t)(((uint64_t)x << 8) | b[q]);
+  return x;
+}
+
+// parseAI: OID, then at most one parameters element; anything after it is never read by Go
+void parse_ai(const uint8_t *b, const T &ai, T *oid, T *params, bool *has_params) {
+  Rd r{b, ai.cs, ai.ce};
+  *oid = r.elem(0x06);
+  if (!valid_oid(b, *oid)) perr();
+  *has_params = !r.empty();
+  if (*has_params) *params = r.any();
+  r.rest_unread();
+}
+
+// x509.ParseCertificate (Go 1.21 crypto/x509/parser.go parseCertificate), in Go's read order
 void parse(Cert &c) {
   const uint8_t *b = c.der.data();
   const size_t n = c.der.size();
-  const T top = tlv(b, 0, n);
-  if (top.tag != 0x30 || top.ce != n) perr();
-  const std::vector<T> k3 = children(b, top.cs, top.ce);
-  if (k3.size() != 3 || k3[0].tag != 0x30 || k3[1].tag != 0x30 || k3[2].tag != 0x03) perr();
-  const T &tbs = k3[0], &oalg = k3[1], &sigb = k3[2];
+  Rd all{b, 0, n};
+  const T top = all.elem(0x30);  // "x509: malformed certificate"
+  if (top.ce != n) perr();       // "x509: trailing data"
+  Rd input = all.in(top);
+  const T tbs = input.elem(0x30);  // "x509: malformed tbs certificate"
   c.tbs_off = tbs.hs;
   c.tbs_len = tbs.ce - tbs.hs;
-  if (sigb.ce == sigb.cs || b[sigb.cs] != 0) unsup();
-  c.sig_off = sigb.cs + 1;
-  c.sig_len = sigb.ce - sigb.cs - 1;
-  const std::vector<T> f = children(b, tbs.cs, tbs.ce);
-  size_t i = 0;
-  int version = 0;
-  if (!f.empty() && f[0].tag == 0xA0) {
-    const std::vector<T> vk = children(b, f[0].cs, f[0].ce);
-    if (vk.size() != 1 || vk[0].tag != 0x02 || !int_minimal(b, vk[0].cs, vk[0].ce)) perr();
-    version = (vk[0].ce - vk[0].cs == 1) ? (int8_t)b[vk[0].cs] : -1;
-    i = 1;
+  Rd t = input.in(tbs);
+  int64_t version = 0;
+  if (t.peek(0xA0)) {  // ReadOptionalASN1Integer([0] EXPLICIT, default 0)
+    Rd vr = t.in(t.elem(0xA0));
+    version = int64_of(b, vr.elem(0x02));
+    if (!vr.empty()) perr();
   }
-  if (version != 2) unsup();
+  if (version < 0 || version > 2) perr();  // "x509: malformed version" / "invalid version"
+  if (version != 2) unsup();               // v1 / v2 certificates: not restated
   c.version = 3;
-  if (f.size() < i + 6) perr();
-  const T &serial = f[i], &alg = f[i + 1], &issuer = f[i + 2], &validity = f[i + 3], &subject = f[i + 4],
-          &spki = f[i + 5];
-  if (serial.tag != 0x02 || !int_minimal(b, serial.cs, serial.ce)) perr();
-  if (alg.ce - alg.hs != oalg.ce - oalg.hs || memcmp(b + alg.hs, b + oalg.hs, alg.ce - alg.hs)) perr();
+  const T serial = t.elem(0x02);  // ReadASN1Integer(*big.Int)
+  if (!int_minimal(b, serial.cs, serial.ce)) perr();
+  const T alg = t.elem(0x30);
+  const T oalg = input.elem(0x30);
+  if (alg.ce - alg.cs != oalg.ce - oalg.cs || memcmp(b + alg.cs, b + oalg.cs, alg.ce - alg.cs)) perr();
+  T aoid, apar;
+  bool ahas;
+  parse_ai(b, alg, &aoid, &apar, &ahas);
   if (oalg.ce - oalg.hs != sizeof ALG_ECDSA_SHA256 || memcmp(b + oalg.hs, ALG_ECDSA_SHA256, sizeof ALG_ECDSA_SHA256))
     unsup();
-  const std::vector<T> vk = children(b, validity.cs, validity.ce);
-  if (vk.size() != 2) perr();
-  c.not_before = parse_time(b, vk[0]);
-  c.not_after = parse_time(b, vk[1]);
-  if (issuer.tag != 0x30 || subject.tag != 0x30) perr();
-  name_ous(b, subject, &c.ous);
+  const T issuer = t.elem(0x30);
   name_ous(b, issuer, nullptr);
+  Rd validity = t.in(t.elem(0x30));
+  const bool time_tag = validity.peek(0x17) || validity.peek(0x18);  // parseTime
+  if (!time_tag) perr();  // "x509: unsupported time format"
+  c.not_before = parse_time(b, validity.any());
+  if (!(validity.peek(0x17) || validity.peek(0x18))) perr();
+  c.not_after = parse_time(b, validity.any());
+  validity.rest_unread();
+  const T subject = t.elem(0x30);
+  name_ous(b, subject, &c.ous);
   c.issuer_off = issuer.hs;
   c.issuer_len = issuer.ce - issuer.hs;
   c.subject_off = subject.hs;
   c.subject_len = subject.ce - subject.hs;
   // public key
-  const std::vector<T> sk = children(b, spki.cs, spki.ce);
-  if (sk.size() != 2 || sk[0].tag != 0x30 || sk[1].tag != 0x03) perr();
-  const std::vector<T> ak = children(b, sk[0].cs, sk[0].ce);
-  if (ak.empty() || !valid_oid(b, ak[0])) perr();  // malformed public key algorithm identifier
+  Rd spki = t.in(t.elem(0x30));
+  const T pkai = spki.elem(0x30);
+  T koid, kpar;
+  bool khas;
+  parse_ai(b, pkai, &koid, &kpar, &khas);
+  const T spk = spki.elem(0x03);
+  bitstring_ok(b, spk);
+  spki.rest_unread();
   c.key = XK_OTHER;
-  if (eq(b, ak[0], OID_EC_KEY, sizeof OID_EC_KEY)) {
-    const bool curve = ak.size() == 2 && ak[1].tag == 0x06;
-    if (curve && eq(b, ak[1], OID_P256, sizeof OID_P256)) {
-      const uint8_t *bits = b + sk[1].cs;
-      const size_t bl = sk[1].ce - sk[1].cs;
+  if (eq(b, koid, OID_EC_KEY, sizeof OID_EC_KEY)) {
+    if (khas && kpar.tag == 0x06 && eq(b, kpar, OID_P256, sizeof OID_P256)) {
+      const uint8_t *bits = b + spk.cs;
+      const size_t bl = spk.ce - spk.cs;
       if (bl != 66 || bits[0] != 0 || bits[1] != 4) unsup();
-      if (!p256_on_curve(bits + 2, bits + 34)) perr();
+      if (!p256_on_curve(bits + 2, bits + 34)) perr();  // elliptic.Unmarshal fails
       memcpy(c.pub, bits + 2, 64);
       c.key = XK_P256;
-    } else {  // (P-384: Go checks the point on the curve -- not restated; no GPU verify either)
+    } else {  // (P-384 and other curves: not restated; no GPU verify either)
       unsup();
     }
-  } else if (eq(b, ak[0], OID_ED25519, sizeof OID_ED25519)) {
-    c.key = XK_UNDESERIALIZABLE;
+  } else if (eq(b, koid, OID_ED25519, sizeof OID_ED25519)) {
+    c.key = XK_UNDESERIALIZABLE;  // (a parse error or a KeyImport error: undeserializable either way)
   } else {  // (RSA: Go's PKCS#1 key checks are not restated)
     unsup();
   }
-  // extensions
+  // issuerUniqueID / subjectUniqueID: not restated
+  if (t.peek(0x81) || t.peek(0x82)) unsup();
   struct Ext {
     int id;
     T val;
     bool crit;
   };
   std::vector<Ext> exts;
-  std::vector<std::vector<uint8_t>> seen;
-  for (size_t r = i + 6; r < f.size(); r++) {
-    if (f[r].tag == 0x81 || f[r].tag == 0x82) unsup();
-    if (f[r].tag != 0xA3) perr();
-    const std::vector<T> ek = children(b, f[r].cs, f[r].ce);
-    if (ek.size() != 1 || ek[0].tag != 0x30) perr();
-    for (const T &e : children(b, ek[0].cs, ek[0].ce)) {
-      const std::vector<T> ef = children(b, e.cs, e.ce);
-      if (e.tag != 0x30 || ef.empty() || !valid_oid(b, ef[0])) perr();
+  if (t.peek(0xA3)) {
+    Rd xr = t.in(t.elem(0xA3));
+    Rd er = xr.in(xr.elem(0x30));  // "x509: malformed extensions"
+    xr.rest_unread();
+    std::vector<std::vector<uint8_t>> seen;
+    while (!er.empty()) {
+      Rd e = er.in(er.elem(0x30));  // parseExtension
+      const T eo = e.elem(0x06);
+      if (!valid_oid(b, eo)) perr();
       bool crit = false;
-      size_t j = 1;
-      if (ef.size() > j && ef[j].tag == 0x01) {
-        crit = der_bool(b, ef[j]);
-        j++;
-      }
-      if (ef.size() != j + 1 || ef[j].tag != 0x04) perr();
-      std::vector<uint8_t> oid(b + ef[0].cs, b + ef[0].ce);
-      if (std::find(seen.begin(), seen.end(), oid) != seen.end()) perr();
+      if (e.peek(0x01)) crit = der_bool(b, e.elem(0x01));
+      const T val = e.elem(0x04);
+      e.rest_unread();
+      std::vector<uint8_t> oid(b + eo.cs, b + eo.ce);
+      if (std::find(seen.begin(), seen.end(), oid) != seen.end()) perr();  // duplicate extensions
       seen.push_back(oid);
-      const int id = ce_ext(b, ef[0]);
+      const int id = ce_ext(b, eo);
       // extensions Go parses that this restatement does not: name constraints (30), CRL
-      // distribution points (31), certificate policies (32), AIA, freshest CRL (46)
+      // distribution points (31), certificate policies (32), AIA, freshest CRL (46); a critical
+      // SKI / AKI (rejected by some Go versions' parsers)
       if (id == 30 || id == 31 || id == 32 || id == 46 ||
-          (oid.size() == sizeof OID_AIA && memcmp(oid.data(), OID_AIA, sizeof OID_AIA) == 0))
+          (oid.size() == sizeof OID_AIA && memcmp(oid.data(), OID_AIA, sizeof OID_AIA) == 0) ||
+          ((id == 14 || id == 35) && crit))
         unsup();
       if (id == 14 || id == 15 || id == 17 || id == 19 || id == 35 || id == 37) {
-        exts.push_back(Ext{id, ef[j], crit});
+        exts.push_back(Ext{id, val, crit});
       } else if (crit) {
         c.unhandled_critical = true;
       }
     }
   }
-  for (const Ext &x : exts) {
-    const uint8_t *v = b + x.val.cs;
-    const size_t vn = x.val.ce - x.val.cs;
-    const T t = tlv(v, 0, vn);
-    if (x.id == 19) {  // basicConstraints
-      if (t.tag != 0x30 || t.ce != vn) perr();
-      std::vector<T> k = children(v, t.cs, t.ce);
-      size_t a = 0;
-      if (!k.empty() && k[0].tag == 0x01) {
-        c.is_ca = der_bool(v, k[0]);
-        a = 1;
-      }
-      if (k.size() > a && (k[a].tag != 0x02 || k.size() - a > 1)) perr();
-      if (k.size() > a) {  // MaxPathLen: ReadASN1Integer into a 64-bit int
-        const T &pl = k[a];
-        if (!int_minimal(v, pl.cs, pl.ce) || pl.ce - pl.cs > 8) perr();
-        int64_t x = (v[pl.cs] & 0x80) ? -1 : 0;
-        for (size_t q = pl.cs; q < pl.ce; q++) x = (int64_t)(((uint64_t)x << 8) | v[q]);
-        c.path_len = x;
-      }
+  t.rest_unread();  // what follows the extensions in the TBS is never read by Go
+  for (const Ext &x : exts) {  // processExtensions
+    Rd v{b, x.val.cs, x.val.ce};
+    if (x.id == 19) {  // parseBasicConstraintsExtension
+      Rd k = v.in(v.elem(0x30));
+      v.rest_unread();
+      if (k.peek(0x01)) c.is_ca = der_bool(b, k.elem(0x01));
+      if (k.peek(0x02)) c.path_len = int64_of(b, k.elem(0x02));
+      k.rest_unread();
       c.bc_valid = true;
     } else if (x.id == 14) {  // subjectKeyIdentifier
-      if (t.tag != 0x04 || t.ce != vn) perr();
+      v.elem(0x04);
+      v.rest_unread();
       c.has_ski = true;
-    } else if (x.id == 15) {  // keyUsage
-      // cryptobyte ReadASN1BitString, then parseKeyUsageExtension's first 9 bits
-      if (t.tag != 0x03 || t.ce != vn || t.ce == t.cs || v[t.cs] > 7 || (t.ce - t.cs == 1 && v[t.cs]) ||
-          (v[t.ce - 1] & ((1u << v[t.cs]) - 1)))
-        perr();
+    } else if (x.id == 15) {  // parseKeyUsageExtension: ReadASN1BitString, its first 9 bits
+      const T bs = v.elem(0x03);
+      bitstring_ok(b, bs);
+      v.rest_unread();
       uint32_t ku = 0;
-      for (size_t q = t.cs + 1, kk = 0; q < t.ce; q++, kk++)
+      for (size_t q = bs.cs + 1, kk = 0; q < bs.ce; q++, kk++)
         for (int bit = 0; bit < 8; bit++)
-          if (v[q] & (0x80 >> bit) && 8 * kk + bit < 9) ku |= 1u << (8 * kk + bit);
+          if (b[q] & (0x80 >> bit) && 8 * kk + bit < 9) ku |= 1u << (8 * kk + bit);
       c.key_usage = ku;
-    } else {  // authorityKeyIdentifier, extKeyUsage, subjectAltName
-      if (t.tag != 0x30 || t.ce != vn) perr();
+    } else if (x.id == 35) {  // authorityKeyIdentifier: SEQUENCE, an optional [0] keyIdentifier
+      Rd k = v.in(v.elem(0x30));
+      v.rest_unread();
+      if (k.peek(0x80)) k.elem(0x80);  // (the rest of the SEQUENCE is never read by Go)
+    } else {  // extKeyUsage (37), subjectAltName (17): SEQUENCE, every element read
+      Rd k = v.in(v.elem(0x30));
+      v.rest_unread();
       int names = 0;
-      for (const T &k : children(v, t.cs, t.ce)) {
-        if (x.id == 37 && !valid_oid(v, k)) perr();  // invalid extended key usages
-        if (x.id == 17) {  // parseSANExtension (by tag ^ 0x80)
-          if (k.tag == 0x81 || k.tag == 0x82)
-            for (size_t q = k.cs; q < k.ce; q++)
-              if (v[q] >= 0x80) perr();  // rfc822Name / dNSName malformed
-          if (k.tag == 0x86) unsup();  // URI (url.Parse not restated)
-          if (k.tag == 0x87 && k.ce - k.cs != 4 && k.ce - k.cs != 16) perr();
-          names += k.tag == 0x81 || k.tag == 0x82 || k.tag == 0x87;
+      while (!k.empty()) {
+        const T e = k.any();
+        if (x.id == 37 && !valid_oid(b, e)) perr();  // "x509: invalid extended key usages"
+        if (x.id == 17) {                            // parseSANExtension (by tag ^ 0x80)
+          if (e.tag == 0x81 || e.tag == 0x82)
+            for (size_t q = e.cs; q < e.ce; q++)
+              if (b[q] >= 0x80) perr();  // rfc822Name / dNSName malformed
+          if (e.tag == 0x86) unsup();    // URI (url.Parse not restated)
+          if (e.tag == 0x87 && e.ce - e.cs != 4 && e.ce - e.cs != 16) perr();
+          names += e.tag == 0x81 || e.tag == 0x82 || e.tag == 0x87;
         }
       }
       if (x.id == 17 && !names && x.crit) c.unhandled_critical = true;  // (nothing parsed)
     }
   }
+  const T sigb = input.elem(0x03);  // "x509: malformed signature"
+  bitstring_ok(b, sigb);
+  if (b[sigb.cs] != 0) unsup();  // (RightAlign of a padded signature: not restated)
+  c.sig_off = sigb.cs + 1;
+  c.sig_len = sigb.ce - sigb.cs - 1;
+  input.rest_unread();  // elements after the signature: Go ignores them (cert.Raw keeps them)
 }
 
 // ---- P-256 field arithmetic for the on-curve check (4 x 64-bit limbs, little-endian) ----
@@ -406,36 +463,49 @@ U256 mulm(const U256 &a, const U256 &b) {
 
 }  // namespace
 
+// encoding/pem Decode, first block, for the one shape the engine models (X_OK):
+//   "-----BEGIN <type>-----" at offset 0, lines of base64 alphabet only, "-----END <type>-----"
+//   at a line start, then nothing, "\n" or "\r\n" (what follows that line is never read);
+//   line ends "\n" or "\r\n"; canonical padding.
+// X_PARSE only where Go's Decode certainly returns nil: no "-----BEGIN " anywhere in the input.
+// Every other shape is X_UNSUP: Go's Decode may still find a block there (a BEGIN after a '\n',
+// a later block after a malformed one, headers, spaces and tabs it strips, ...).
 int pem_decode(const uint8_t *p, size_t n, std::vector<uint8_t> &der) {
-  const std::string s((const char *)p, n);
-  const size_t i = s.find("-----BEGIN ");
-  if (i == std::string::npos) return X_PARSE;
-  const size_t j = s.find("-----", i + 11);
-  if (j == std::string::npos) return X_PARSE;
-  const std::string end_tag = "-----END " + s.substr(i + 11, j - (i + 11)) + "-----";
-  const size_t k = s.find(end_tag, j);
-  if (k == std::string::npos) return X_PARSE;
-  // body lines, stripped of whitespace (Python bytes.strip: space \t \n \r \x0b \x0c)
+  static const char BEGIN[] = "-----BEGIN ", END[] = "-----END ", DASH[] = "-----";
+  if (!memmem(p, n, BEGIN, 11)) return X_PARSE;
+  if (n < 11 || memcmp(p, BEGIN, 11)) return X_UNSUP;
+  size_t i = 11;
+  const size_t ts = i;
+  while (i < n && p[i] != '-' && p[i] >= 0x20 && p[i] < 0x7F) i++;
+  const size_t te = i;
+  auto eol = [&](size_t &k) {
+    if (k < n && p[k] == '\n') return k++, true;
+    if (k + 1 < n && p[k] == '\r' && p[k + 1] == '\n') return k += 2, true;
+    return false;
+  };
+  auto b64c = [](uint8_t ch) {
+    return (ch >= 'A' && ch <= 'Z') || (ch >= 'a' && ch <= 'z') || (ch >= '0' && ch <= '9') || ch == '+' ||
+           ch == '/' || ch == '=';
+  };
+  if (n - i < 5 || memcmp(p + i, DASH, 5)) return X_UNSUP;
+  i += 5;
+  if (!eol(i)) return X_UNSUP;
   std::string b64;
-  bool colon = false;
-  size_t a = j + 5;
-  while (a < k) {
-    size_t e = s.find('\n', a);
-    if (e == std::string::npos || e > k) e = k;
-    size_t x = a, y = e;
-    auto ws = [](char ch) { return ch == ' ' || ch == '\t' || ch == '\n' || ch == '\r' || ch == '\x0b' || ch == '\x0c'; };
-    while (x < y && ws(s[x])) x++;
-    while (y > x && ws(s[y - 1])) y--;
-    if (y > x) {
-      const std::string ln = s.substr(x, y - x);
-      if (ln.find(':') != std::string::npos) colon = true;
-      b64 += ln;
-    }
-    a = e + 1;
+  for (;;) {
+    if (i >= n) return X_UNSUP;  // no END line
+    if (n - i >= 9 && !memcmp(p + i, END, 9)) break;
+    const size_t a = i;
+    while (i < n && b64c(p[i])) i++;
+    b64.append((const char *)p + a, i - a);
+    if (!eol(i)) return X_UNSUP;
   }
-  if (colon) return X_UNSUP;
-  // strict base64 (validate=True): alphabet A-Za-z0-9+/, padding only at the end, length % 4 == 0
-  if (b64.size() % 4) return X_PARSE;
+  i += 9;
+  const size_t tl = te - ts;
+  if (n - i < tl + 5 || memcmp(p + i, p + ts, tl) || memcmp(p + i + tl, DASH, 5)) return X_UNSUP;
+  i += tl + 5;
+  if (i != n && !eol(i)) return X_UNSUP;
+  // base64.StdEncoding: whole quanta, '=' only as the last one or two characters
+  if (b64.size() % 4) return X_UNSUP;
   der.clear();
   der.reserve(b64.size() / 4 * 3);
   auto val = [](char ch) -> int {
@@ -451,13 +521,12 @@ int pem_decode(const uint8_t *p, size_t n, std::vector<uint8_t> &der) {
     for (int t = 0; t < 4; t++) {
       const char ch = b64[q + t];
       if (ch == '=') {
-        if (q + 4 != b64.size() || t < 2) return X_PARSE;
+        if (q + 4 != b64.size() || t < 2) return X_UNSUP;
         v[t] = 0;
         pad++;
       } else {
-        if (pad) return X_PARSE;
+        if (pad) return X_UNSUP;
         v[t] = val(ch);
-        if (v[t] < 0) return X_PARSE;
       }
     }
     const uint32_t w = (uint32_t)v[0] << 18 | (uint32_t)v[1] << 12 | (uint32_t)v[2] << 6 | (uint32_t)v[3];

@@ -769,9 +769,62 @@ def index_txid(d):
         return None
 
 
+def keylevel_writes(model, d):
+    """-> (changed, touched): the (ns, coll, key) this tx may change the key-level state of --
+    its metadata writes, and its deletes of keys holding a VALIDATION_PARAMETER in the committed
+    state (tx_ops.go:17-51: a metadata write replaces the metadata, a delete drops it) -- and
+    every key it writes or metadata-writes (what its vscc reads the parameter of)."""
+    try:
+        cca, _ = get_action_from_envelope(d)
+        rw = parse_rwset(cca.get("results"))
+    except (DecodeError, ValueError, KeyError, IndexError, TypeError):
+        return set(), set()
+    changed, touched = set(), set()
+    for nsrw in rw:
+        ns = nsrw["namespace"]
+        sets = [("", nsrw["kv"].get("writes", []), "key", nsrw["kv"].get("metadata_writes", []), "key")]
+        sets += [(c["name"], c["hashed"].get("hashed_writes", []), "key_hash", c["hashed"].get("metadata_writes", []),
+                  "key_hash") for c in nsrw["coll"]]
+        for coll, ws, wk, ms, mk in sets:
+            for w in ws:
+                k = w.get(wk) or (b"" if wk == "key_hash" else "")
+                k = (ns, coll, k.encode() if isinstance(k, str) else k)
+                touched.add(k)
+                if w.get("is_delete") and model.kvmeta.get(k):
+                    changed.add(k)
+            for m in ms:
+                k = m.get(mk) or (b"" if mk == "key_hash" else "")
+                k = (ns, coll, k.encode() if isinstance(k, str) else k)
+                touched.add(k)
+                changed.add(k)
+    return changed, touched
+
+
+def check_keylevel_batch(model, blocks):
+    """A batch validates every block against the key-level state committed before it; the
+    reference commits block k (its valid metadata writes and deletes) before block k+1's vscc
+    reads GetStateMetadata.  When a block other than the last may change the parameter of a key
+    that a later block of the batch writes, the outcome depends on block k's validity and MVCC
+    results: Unsupported (the caller validates the blocks one call at a time)."""
+    if len(blocks) < 2:
+        return
+    seen_changed = set()
+    for blk in blocks:
+        data = (decode("Block", blk).get("data") or {}).get("data", [])
+        ch_b, tc_b = set(), set()
+        for d in data:
+            c, t = keylevel_writes(model, d)
+            ch_b |= c
+            tc_b |= t
+        if seen_changed & tc_b:
+            raise Unsupported("a key-level parameter changed by an earlier block of the batch is written by a later one")
+        seen_changed |= ch_b
+
+
 def validate_blocks(model, blocks):
     """Consecutive blocks: block k sees the txids indexed by blocks < k (blkstorage indexes
     every transaction's txid at commit, block_serialization.go:95-115)."""
+    check_keylevel_batch(model, blocks)
     out = []
     for blk in blocks:
         out.append(validate_block(model, blk))

@@ -101,25 +101,60 @@ def valid_oid(b):
 
 
 def pem_decode(data):
-    """encoding/pem Decode of the first block (any type; trailing text ignored) -> DER or None"""
-    i = data.find(b"-----BEGIN ")
-    if i < 0:
+    """encoding/pem Decode of the first block (Go 1.21 encoding/pem/pem.go Decode), for the one
+    shape the engine models: "-----BEGIN <type>-----" at offset 0, lines of base64 alphabet only,
+    "-----END <type>-----" at a line start followed by nothing, "\n" or "\r\n"; line ends "\n" or
+    "\r\n"; canonical padding.  -> DER.  None only where Go's Decode certainly returns nil (no
+    "-----BEGIN " anywhere).  Any other shape raises Unsupported: Go may still find a block there
+    (a BEGIN after a newline, a later block after a malformed one, headers, stripped blanks...)."""
+    if b"-----BEGIN " not in data:
         return None
-    j = data.find(b"-----", i + 11)
-    if j < 0:
+    if not data.startswith(b"-----BEGIN "):
+        raise Unsupported("PEM: BEGIN not at offset 0")
+    i = 11
+    ts = i
+    while i < len(data) and data[i] != 0x2D and 0x20 <= data[i] < 0x7F:
+        i += 1
+    typ = data[ts:i]
+
+    def eol(k):
+        if data[k:k + 1] == b"\n":
+            return k + 1
+        if data[k:k + 2] == b"\r\n":
+            return k + 2
         return None
-    end_tag = b"-----END " + data[i + 11:j] + b"-----"
-    k = data.find(end_tag, j)
-    if k < 0:
-        return None
-    body = data[j + 5:k]
-    lines = [ln.strip() for ln in body.split(b"\n") if ln.strip()]
-    if any(b":" in ln for ln in lines):
-        raise Unsupported("PEM headers")
-    try:
-        return base64.b64decode(b"".join(lines), validate=True)
-    except Exception:
-        return None
+
+    if data[i:i + 5] != b"-----":
+        raise Unsupported("PEM: type line")
+    i = eol(i + 5)
+    if i is None:
+        raise Unsupported("PEM: type line")
+    alpha = set(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/=")
+    b64 = bytearray()
+    while True:
+        if i >= len(data):
+            raise Unsupported("PEM: no END line")
+        if data.startswith(b"-----END ", i):
+            break
+        a = i
+        while i < len(data) and data[i] in alpha:
+            i += 1
+        b64 += data[a:i]
+        i = eol(i)
+        if i is None:
+            raise Unsupported("PEM: body line")
+    i += 9
+    if data[i:i + len(typ) + 5] != typ + b"-----":
+        raise Unsupported("PEM: END line")
+    i += len(typ) + 5
+    if i != len(data) and eol(i) is None:
+        raise Unsupported("PEM: END line")
+    if len(b64) % 4:
+        raise Unsupported("PEM: base64 length")
+    core = b64.rstrip(b"=")
+    if b"=" in core or len(b64) - len(core) > 2:
+        raise Unsupported("PEM: base64 padding")
+    return base64.b64decode(bytes(b64))  # (non-zero trailing bits accepted, as Go's StdEncoding)
 
 
 def _time(b, t, s, e):
@@ -160,81 +195,142 @@ def _string(b, t, s, e):
     raise ParseError("unsupported string type %#x" % t)  # (parseASN1String)
 
 
+class _Rd:
+    """cryptobyte.String over b[s:e]; each read mirrors the Go call named beside it.  A failing
+    read Go makes is a ParseError; bytes Go leaves unread where the restatement would need to know
+    what Go does with them raise Unsupported."""
+
+    def __init__(self, b, s, e):
+        self.b, self.s, self.e = b, s, e
+
+    def empty(self):
+        return self.s >= self.e
+
+    def peek(self, tag):  # PeekASN1Tag
+        return self.s < self.e and self.b[self.s] == tag
+
+    def any(self):  # ReadAnyASN1Element -> (tag, cs, ce, hs)
+        t, cs, ce = tlv(self.b, self.s, self.e)
+        hs, self.s = self.s, ce
+        return t, cs, ce, hs
+
+    def elem(self, tag):  # ReadASN1Element / ReadASN1 with a tag
+        x = self.any()
+        if x[0] != tag:
+            raise ParseError("tag %#x where %#x expected" % (x[0], tag))
+        return x
+
+    def into(self, x):
+        return _Rd(self.b, x[1], x[2])
+
+    def rest_unread(self):
+        if not self.empty():
+            raise Unsupported("bytes Go leaves unread")
+
+
 def _ous(b, s, e):
+    """parseName: RDNSequence of SETs of AttributeTypeAndValue {OID, any string}; what an
+    attribute holds after its value is never read by Go (nor here)"""
     out = []
-    for st, ss, se, _ in children(b, s, e):
-        if st != 0x31:
-            raise ParseError("RDN is not a SET")
-        for at, as_, ae, _ in children(b, ss, se):
-            if at != 0x30:
-                raise ParseError("attribute is not a SEQUENCE")
-            # (parseName reads the type and the value; anything after them is not read)
-            t1 = tlv(b, as_, ae)
-            if t1[0] != 0x06 or not valid_oid(b[t1[1]:t1[2]]):
+    raw = _Rd(b, s, e)
+    while not raw.empty():
+        st = raw.into(raw.elem(0x31))
+        while not st.empty():
+            atv = st.into(st.elem(0x30))
+            t1 = atv.elem(0x06)
+            if not valid_oid(b[t1[1]:t1[2]]):
                 raise ParseError("bad attribute type")
-            t2 = tlv(b, t1[2], ae)
+            t2 = atv.any()
             v = _string(b, t2[0], t2[1], t2[2])  # every attribute value parses (parseASN1String)
             if b[t1[1]:t1[2]] == OID_OU:
                 out.append(v)
     return out
 
 
+def _bool(b, x):  # ReadASN1Boolean
+    if b[x[1]:x[2]] not in (b"\x00", b"\xff"):
+        raise ParseError("bad BOOLEAN")
+    return b[x[1]] == 0xFF
+
+
+def _int64(b, x):  # ReadASN1Integer into a Go int (64-bit)
+    if x[0] != 0x02 or x[2] - x[1] > 8:
+        raise ParseError("bad integer")
+    return der_int(b, x[1], x[2])
+
+
+def _bitstring_ok(b, x):  # ReadASN1BitString's validity rules
+    s, e = x[1], x[2]
+    if e == s or b[s] > 7 or (e - s == 1 and b[s]) or (b[e - 1] & ((1 << b[s]) - 1)):
+        raise ParseError("bad BIT STRING")
+
+
+def _ai(b, x):
+    """parseAI: OID, then at most one parameters element (anything after it: Unsupported)"""
+    r = _Rd(b, x[1], x[2])
+    o = r.elem(0x06)
+    if not valid_oid(b[o[1]:o[2]]):
+        raise ParseError("malformed OID")
+    par = None if r.empty() else r.any()
+    r.rest_unread()
+    return b[o[1]:o[2]], par
+
+
+ALG_ECDSA_SHA256 = bytes.fromhex("300a06082a8648ce3d040302")
+
+
 def parse_certificate(der):
-    """-> dict of the fields the MSP path reads; ParseError / Unsupported"""
-    t, cs, ce = tlv(der, 0)
-    if t != 0x30 or ce != len(der):
-        raise ParseError("not a single SEQUENCE (trailing data)")
-    top = children(der, cs, ce)
-    if len(top) != 3 or top[0][0] != 0x30 or top[1][0] != 0x30 or top[2][0] != 0x03:
-        raise ParseError("bad certificate structure")
-    tbs_raw = der[top[0][3]:top[0][2]]
-    outer_alg = der[top[1][3]:top[1][2]]
-    sig_bits = der[top[2][1]:top[2][2]]
-    if not sig_bits or sig_bits[0] != 0:
-        raise Unsupported("signature BIT STRING with unused bits")
-    f = children(der, top[0][1], top[0][2])
-    i = 0
+    """x509.ParseCertificate (Go 1.21 crypto/x509/parser.go parseCertificate), in Go's read
+    order -> dict of the fields the MSP path reads; ParseError / Unsupported"""
+    top = _Rd(der, 0, len(der)).elem(0x30)  # "x509: malformed certificate"
+    if top[2] != len(der):
+        raise ParseError("x509: trailing data")
+    inp = _Rd(der, top[1], top[2])
+    tbs = inp.elem(0x30)
+    tbs_raw = der[tbs[3]:tbs[2]]
+    t = inp.into(tbs)
     version = 0
-    if f and f[0][0] == 0xA0:
-        vk = children(der, f[0][1], f[0][2])
-        if len(vk) != 1 or vk[0][0] != 0x02:
+    if t.peek(0xA0):  # ReadOptionalASN1Integer([0] EXPLICIT, default 0)
+        vr = t.into(t.elem(0xA0))
+        version = _int64(der, vr.elem(0x02))
+        if not vr.empty():
             raise ParseError("bad version")
-        version = der_int(der, vk[0][1], vk[0][2])
-        i = 1
+    if not 0 <= version <= 2:
+        raise ParseError("x509: malformed / invalid version")
     if version != 2:
         raise Unsupported("certificate version %d" % (version + 1))
-    if len(f) < i + 6:
-        raise ParseError("short TBSCertificate")
-    serial_t, alg, issuer, validity, subject, spki = f[i:i + 6]
-    if serial_t[0] != 0x02:
-        raise ParseError("bad serial")
+    serial_t = t.elem(0x02)
     serial = der_int(der, serial_t[1], serial_t[2])
-    if der[alg[3]:alg[2]] != outer_alg:
+    alg = t.elem(0x30)
+    oalg = inp.elem(0x30)
+    if der[alg[1]:alg[2]] != der[oalg[1]:oalg[2]]:
         raise ParseError("signature algorithm identifier mismatch")
-    if outer_alg != bytes.fromhex("300a06082a8648ce3d040302"):
+    _ai(der, alg)
+    if der[oalg[3]:oalg[2]] != ALG_ECDSA_SHA256:
         raise Unsupported("signature algorithm other than ecdsa-with-SHA256 (no parameters)")
-    vk = children(der, validity[1], validity[2])
-    if len(vk) != 2:
-        raise ParseError("bad validity")
-    not_before = _time(der, vk[0][0], vk[0][1], vk[0][2])
-    not_after = _time(der, vk[1][0], vk[1][1], vk[1][2])
-    if issuer[0] != 0x30 or subject[0] != 0x30:
-        raise ParseError("bad name")
-    ous = _ous(der, subject[1], subject[2])
+    issuer = t.elem(0x30)
     _ous(der, issuer[1], issuer[2])  # (issuer names parse too)
+    vr = t.into(t.elem(0x30))
+    times = []
+    for _ in range(2):  # parseTime
+        if not (vr.peek(0x17) or vr.peek(0x18)):
+            raise ParseError("x509: unsupported time format")
+        x = vr.any()
+        times.append(_time(der, x[0], x[1], x[2]))
+    vr.rest_unread()
+    not_before, not_after = times
+    subject = t.elem(0x30)
+    ous = _ous(der, subject[1], subject[2])
     # public key
-    sk = children(der, spki[1], spki[2])
-    if len(sk) != 2 or sk[0][0] != 0x30 or sk[1][0] != 0x03:
-        raise ParseError("bad SubjectPublicKeyInfo")
-    ak = children(der, sk[0][1], sk[0][2])
-    if not ak or ak[0][0] != 0x06 or not valid_oid(der[ak[0][1]:ak[0][2]]):
-        raise ParseError("malformed public key algorithm identifier")
-    koid = der[ak[0][1]:ak[0][2]]
-    bits = der[sk[1][1]:sk[1][2]]
+    sp = t.into(t.elem(0x30))
+    koid, kpar = _ai(der, sp.elem(0x30))
+    spk = sp.elem(0x03)
+    _bitstring_ok(der, spk)
+    sp.rest_unread()
+    bits = der[spk[1]:spk[2]]
     key, pub = "other", None
     if koid == OID_EC_KEY:
-        curve = der[ak[1][1]:ak[1][2]] if len(ak) == 2 and ak[1][0] == 0x06 else b""
-        if curve == OID_P256:
+        if kpar is not None and kpar[0] == 0x06 and der[kpar[1]:kpar[2]] == OID_P256:
             pt = bits[1:] if bits[:1] == b"\x00" else b""
             if len(pt) != 65 or pt[0] != 4:
                 raise Unsupported("P-256 point encoding")
@@ -242,107 +338,92 @@ def parse_certificate(der):
             if x >= P256_P or y >= P256_P or (y * y - (x * x * x - 3 * x + P256_B)) % P256_P:
                 raise ParseError("point not on curve")
             key, pub = "p256", pt[1:]
-        else:  # (P-384: Go checks the point on the curve -- not restated; the engine cannot verify it either)
+        else:  # (P-384 and other curves: not restated; the engine cannot verify them either)
             raise Unsupported("EC curve")
     elif koid == OID_ED25519:
-        key = "undeserializable"  # bccsp KeyImport rejects it
+        key = "undeserializable"  # (a parse or a KeyImport error: undeserializable either way)
     else:  # (RSA: Go's PKCS#1 key checks are not restated)
         raise Unsupported("public key algorithm")
-    # extensions
-    rest = f[i + 6:]
+    if t.peek(0x81) or t.peek(0x82):
+        raise Unsupported("issuer/subject unique id")
     exts = {}
     unhandled_critical = False
-    for r in rest:
-        if r[0] in (0x81, 0x82):
-            raise Unsupported("issuer/subject unique id")
-        if r[0] != 0xA3:
-            raise ParseError("unexpected TBSCertificate field")
-        ek = children(der, r[1], r[2])
-        if len(ek) != 1 or ek[0][0] != 0x30:
-            raise ParseError("bad extensions")
-        for et, es, ee, _ in children(der, ek[0][1], ek[0][2]):
-            ef = children(der, es, ee)
-            if et != 0x30 or not ef or ef[0][0] != 0x06:
-                raise ParseError("bad extension")
-            oid = der[ef[0][1]:ef[0][2]]
+    if t.peek(0xA3):
+        xr = t.into(t.elem(0xA3))
+        er = xr.into(xr.elem(0x30))
+        xr.rest_unread()
+        while not er.empty():
+            e = er.into(er.elem(0x30))  # parseExtension
+            o = e.elem(0x06)
+            oid = der[o[1]:o[2]]
             if not valid_oid(oid):
                 raise ParseError("malformed extension OID")
-            crit = False
-            j = 1
-            if len(ef) > j and ef[j][0] == 0x01:
-                if der[ef[j][1]:ef[j][2]] not in (b"\x00", b"\xff"):
-                    raise ParseError("bad BOOLEAN")
-                crit = der[ef[j][1]] == 0xFF
-                j += 1
-            if len(ef) != j + 1 or ef[j][0] != 0x04:
-                raise ParseError("bad extension value")
+            crit = _bool(der, e.elem(0x01)) if e.peek(0x01) else False
+            val = e.elem(0x04)
+            e.rest_unread()
             if oid in exts:
                 raise ParseError("duplicate extension")
-            val = der[ef[j][1]:ef[j][2]]
             exts[oid] = (crit, val)
-            if oid in EXT_GO_PARSED:
+            if oid in EXT_GO_PARSED or (oid in (EXT_SKI, EXT_AKI) and crit):
                 raise Unsupported("extension %s" % oid.hex())
             if oid not in (EXT_SKI, EXT_KU, EXT_BC, EXT_AKI, EXT_EKU, EXT_SAN) and crit:
                 unhandled_critical = True
+    t.rest_unread()  # what follows the extensions in the TBS is never read by Go
     is_ca, bc_valid, path_len = False, False, -1
-    if EXT_BC in exts:
-        v = exts[EXT_BC][1]
-        t, s, e = tlv(v, 0)
-        if t != 0x30 or e != len(v):
-            raise ParseError("bad basicConstraints")
-        k = children(v, s, e)
-        if k and k[0][0] == 0x01:
-            if v[k[0][1]:k[0][2]] not in (b"\x00", b"\xff"):
-                raise ParseError("bad BOOLEAN")
-            is_ca = v[k[0][1]] == 0xFF
-            k = k[1:]
-        if k and (k[0][0] != 0x02 or len(k) > 1):
-            raise ParseError("bad pathLen")
-        if k:  # MaxPathLen (ReadASN1Integer into an int: must fit in 64 bits)
-            path_len = der_int(v, k[0][1], k[0][2])
-            if not -(1 << 63) <= path_len < (1 << 63):
-                raise ParseError("pathLen out of range")
-        bc_valid = True
     ski = None
-    if EXT_SKI in exts:
-        v = exts[EXT_SKI][1]
-        t, s, e = tlv(v, 0)
-        if t != 0x04 or e != len(v):
-            raise ParseError("bad SKI")
-        ski = v[s:e]
     key_usage = 0
-    if EXT_KU in exts:
-        v = exts[EXT_KU][1]
-        t, s, e = tlv(v, 0)
-        # cryptobyte ReadASN1BitString: unused-bit count <= 7, none with no data, unused bits zero
-        if t != 0x03 or e != len(v) or e == s or v[s] > 7 or (e - s == 1 and v[s]) or \
-                (v[e - 1] & ((1 << v[s]) - 1)):
-            raise ParseError("bad keyUsage")
-        # parseKeyUsageExtension reads the first 9 bits
-        for k, byte in enumerate(v[s + 1:e]):
-            for bit in range(8):
-                if byte & (0x80 >> bit) and 8 * k + bit < 9:
-                    key_usage |= 1 << (8 * k + bit)
-    for oid in (EXT_AKI, EXT_EKU, EXT_SAN):
-        if oid in exts:
-            v = exts[oid][1]
-            t, s, e = tlv(v, 0)
-            if t != 0x30 or e != len(v):
-                raise ParseError("bad extension content")
+    for oid, (crit, val) in exts.items():  # processExtensions
+        v = _Rd(der, val[1], val[2])
+        if oid == EXT_BC:
+            k = v.into(v.elem(0x30))
+            v.rest_unread()
+            if k.peek(0x01):
+                is_ca = _bool(der, k.elem(0x01))
+            if k.peek(0x02):
+                path_len = _int64(der, k.elem(0x02))
+            k.rest_unread()
+            bc_valid = True
+        elif oid == EXT_SKI:
+            x = v.elem(0x04)
+            v.rest_unread()
+            ski = der[x[1]:x[2]]
+        elif oid == EXT_KU:
+            x = v.elem(0x03)
+            _bitstring_ok(der, x)
+            v.rest_unread()
+            for k, byte in enumerate(der[x[1] + 1:x[2]]):  # parseKeyUsageExtension: the first 9 bits
+                for bit in range(8):
+                    if byte & (0x80 >> bit) and 8 * k + bit < 9:
+                        key_usage |= 1 << (8 * k + bit)
+        elif oid == EXT_AKI:
+            k = v.into(v.elem(0x30))
+            v.rest_unread()
+            if k.peek(0x80):
+                k.elem(0x80)  # (the rest of the SEQUENCE is never read by Go)
+        elif oid in (EXT_EKU, EXT_SAN):
+            k = v.into(v.elem(0x30))
+            v.rest_unread()
             names = 0
-            for kt, ks, ke, _ in children(v, s, e):
-                if oid == EXT_EKU and (kt != 0x06 or not valid_oid(v[ks:ke])):
+            while not k.empty():
+                kt, ks, ke, _ = k.any()
+                if oid == EXT_EKU and (kt != 0x06 or not valid_oid(der[ks:ke])):
                     raise ParseError("invalid extended key usages")
                 if oid == EXT_SAN:  # parseSANExtension (by tag ^ 0x80)
-                    if kt in (0x81, 0x82) and any(c >= 0x80 for c in v[ks:ke]):
+                    if kt in (0x81, 0x82) and any(c >= 0x80 for c in der[ks:ke]):
                         raise ParseError("SAN rfc822Name / dNSName is malformed")
                     if kt == 0x86:
                         raise Unsupported("SAN URI (url.Parse not restated)")
                     if kt == 0x87 and ke - ks not in (4, 16):
                         raise ParseError("SAN iPAddress of wrong length")
                     names += kt in (0x81, 0x82, 0x87)
-            if oid == EXT_SAN and not names and exts[oid][0]:
+            if oid == EXT_SAN and not names and crit:
                 unhandled_critical = True  # (nothing parsed: Go's critical check applies)
+    sig_t = inp.elem(0x03)  # "x509: malformed signature"
+    _bitstring_ok(der, sig_t)
+    sig_bits = der[sig_t[1]:sig_t[2]]
+    if sig_bits[0] != 0:
+        raise Unsupported("signature BIT STRING with unused bits")
+    inp.rest_unread()  # elements after the signature: Go ignores them (cert.Raw keeps them)
     return dict(der=der, tbs=tbs_raw, sig=sig_bits[1:], serial=serial, issuer=der[issuer[3]:issuer[2]],
                 subject=der[subject[3]:subject[2]], not_before=not_before, not_after=not_after, ous=ous,
                 key=key, pub=pub, is_ca=is_ca, bc_valid=bc_valid, path_len=path_len, ski=ski, key_usage=key_usage,

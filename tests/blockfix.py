@@ -61,3 +61,58 @@ def network_c5():
     if k not in _NET:
         _NET[k] = blocks.Network(**C5_NET)
     return _NET[k]
+
+
+def _varint_at(b, o):
+    v = s = 0
+    while True:
+        c = b[o]
+        o += 1
+        v |= (c & 0x7F) << s
+        s += 7
+        if not c & 0x80:
+            return v, o
+
+
+def _venc(v):
+    out = bytearray()
+    while True:
+        c = v & 0x7F
+        v >>= 7
+        out.append(c | (0x80 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+def replace_field(msg, path, new):
+    """msg with the length-delimited field at path replaced by `new`; path: [(field number,
+    occurrence)] from the outermost message inward (every enclosing length re-encoded)"""
+    (num, occ), rest = path[0], path[1:]
+    o, seen = 0, 0
+    while o < len(msg):
+        start = o
+        key, o = _varint_at(msg, o)
+        wt = key & 7
+        if wt == 0:
+            _, o = _varint_at(msg, o)
+        elif wt == 1:
+            o += 8
+        elif wt == 5:
+            o += 4
+        elif wt == 2:
+            ln, vs = _varint_at(msg, o)
+            o = vs + ln
+            if key >> 3 == num:
+                if seen == occ:
+                    inner = replace_field(msg[vs:o], rest, new) if rest else new
+                    return msg[:start] + _venc(key) + _venc(len(inner)) + inner + msg[o:]
+                seen += 1
+        else:
+            raise ValueError("wire type %d" % wt)
+    raise KeyError(num)
+
+
+# Block.data(2) -> BlockData.data(1)[tx] -> Envelope.payload(1) -> Payload.header(1) ->
+# Header.signature_header(2) -> SignatureHeader.creator(1) -> SerializedIdentity.id_bytes(2)
+def creator_idbytes_path(tx):
+    return [(2, 0), (1, tx), (1, 0), (1, 0), (2, 0), (1, 0), (2, 0)]

@@ -8,7 +8,10 @@ SubjectKeyIdentifier (the MSP would not set up: outside the model).  Leaves cove
 the miss path: role OUs, two role OUs, no OU, a listed admin, a high-S CA signature, unknown
 issuer, wrong CA key, an unhandled critical extension, a CA as an identity, SAN (DNS / URI), an
 empty validity window, Ed25519, a malformed IA5 OU, not PEM, a chain through an intermediate, an
-issuer that is an internal node, a path length exceeded."""
+issuer that is an internal node, a path length exceeded.  Shapes Go's pem / x509 parsers may accept
+and the restatement does not model (fork_hazard_variants) must come out Unsupported, never a code."""
+import base64
+
 from fabric_amd.synth import EdKey, Key, make_cert_ed25519
 from fabric_amd.synth import x509gen as G
 from fabric_amd.synth.blocks import serialized_identity
@@ -24,6 +27,42 @@ def _roles(*rs):
     for r in rs:
         v |= 1 << r
     return v
+
+
+def _der(pem):
+    return base64.b64decode(b"".join(pem.split(b"-----")[2].split()))
+
+
+def _pem(der, typ=b"CERTIFICATE"):
+    return b"-----BEGIN " + typ + b"-----\n" + base64.encodebytes(der) + b"-----END " + typ + b"-----\n"
+
+
+def _outer_content(der):
+    ln, o = der[1], 2
+    if ln & 0x80:
+        o = 2 + (ln & 0x7F)
+        ln = int.from_bytes(der[2:o], "big")
+    return der[o:o + ln]
+
+
+def fork_hazard_variants(pem):
+    """[(label, pem')]: a valid PEM certificate re-framed into shapes Go's encoding/pem and
+    crypto/x509 accept (or may accept) and the engine does not model -> Unsupported"""
+    der = _der(pem)
+    b64 = base64.encodebytes(der)
+    first = b64.index(b"\n")
+    return [
+        ("extra_outer_element", _pem(G.seq(_outer_content(der) + G.tlv(0x05, b"")))),
+        ("junk_prefixed_pem", b"junk\n" + pem),
+        ("begin_mid_line", b"junk " + pem),
+        ("malformed_block_then_valid", b"-----BEGIN CERTIFICATE-----\n!!!!\n-----END CERTIFICATE-----\n" + pem),
+        ("blank_in_base64", b"-----BEGIN CERTIFICATE-----\n" + b64[:10] + b" " + b64[10:] + b"-----END CERTIFICATE-----\n"),
+        ("tab_after_type", b"-----BEGIN CERTIFICATE-----\t\n" + b64 + b"-----END CERTIFICATE-----\n"),
+        ("text_after_end_line", pem.rstrip(b"\n") + b" trailing\n"),
+        ("pem_header", b"-----BEGIN CERTIFICATE-----\nX-Note: hi\n" + b64 + b"-----END CERTIFICATE-----\n"),
+        ("short_line_wrap", b"-----BEGIN CERTIFICATE-----\n" + b64[:first - 3] + b"\n" + b64[first - 3:] +
+         b"-----END CERTIFICATE-----\n"),
+    ]
 
 
 def synthetic():
@@ -79,6 +118,20 @@ def synthetic():
     add("not_pem", b"definitely not a certificate", FAILED)
     add("key_usage_critical_ok", leaf(21, ["client"], extensions=[G.key_usage((0,))]), OK, True,
         _roles(MEMBER, CLIENT))
+    # re-framings of a valid peer certificate: Go's parsers may accept each (extra outer element,
+    # PEM framing) -> Unsupported; a canonical CRLF / 64-column framing -> the same identity
+    for j in range(9):
+        lbl, p = fork_hazard_variants(leaf(25 + j, ["peer"]))[j]
+        add(lbl, p, OK if lbl == "short_line_wrap" else UNSUP, *((True, _roles(MEMBER, PEER)) if lbl == "short_line_wrap" else ()))
+    crlf = base64.b64encode(_der(leaf(35, ["peer"])))
+    add("crlf_64_columns", b"-----BEGIN CERTIFICATE-----\r\n" + b"\r\n".join(crlf[i:i + 64] for i in range(0, len(crlf), 64))
+        + b"\r\n-----END CERTIFICATE-----\r\n", OK, True, _roles(MEMBER, PEER))
+    add("critical_ski", leaf(36, ["peer"], extensions=[G.ext("551d0e", G.tlv(0x04, b"\x01" * 20), critical=True)]), UNSUP)
+    add("key_usage_trailing_bytes", leaf(37, ["peer"], extensions=[G.ext("551d0f", G.tlv(0x03, b"\x00\x80") + b"\x05\x00")]),
+        UNSUP)
+    add("basic_constraints_trailing_element",
+        leaf(38, ["peer"], extensions=[G.ext("551d13", G.seq(G.tlv(0x01, b"\x00"), G.tlv(0x04, b"x")))]), UNSUP)
+    add("no_begin_anywhere", b"-----END CERTIFICATE-----\n", FAILED)
     out.append(("repeat", out[0][1], REPEAT, None, None))  # the same bytes again in one call
     out.append(("msp_root_without_ski", serialized_identity("Org2MSP", leaf(24, ["peer"], issuer_key=ca2,
                                                                            issuer=G.name("ca2.org2", "Org2"))),

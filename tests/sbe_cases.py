@@ -52,25 +52,26 @@ def _spe_any(mspids):
         b"".join(f_msg(3, blocks.msp_role_principal(m)) for m in mspids)
 
 
-def make_sbe_block(net, ntx, seed, number=1, coll="pvt1", nkeys=12, vp_keys=6, garbage_vp=False):
+def make_sbe_block(net, ntx, seed, number=1, coll="pvt1", nkeys=12, vp_keys=6, garbage_vp=False, prefix="k"):
     """A block of namespace mycc over a small key space (public keys k0.. and the same names in
     collection `coll`, by key hash): value writes, metadata writes setting or clearing a key's
     VALIDATION_PARAMETER (one org's members; with garbage_vp also bytes that do not unmarshal),
     endorser sets of 1-3 orgs so that the chaincode EP and the parameters hold or fail; and the
-    committed state's parameters (one org / all orgs).  Returns (block, kvmeta)."""
+    committed state's parameters (one org / all orgs).  prefix: the key names' prefix (blocks of a
+batch over disjoint key spaces).  Returns (block, kvmeta)."""
     rng = random.Random(seed)
     orgs = sorted({p.mspid for ps in net.org_peers for p in ps})
     all_orgs = f_msg(2, blocks.n_out_of(len(orgs), [blocks.signed_by(i) for i in range(len(orgs))])) + \
         b"".join(f_msg(3, blocks.msp_role_principal(m)) for m in orgs)
     kvmeta = {}
     for _ in range(vp_keys):
-        k = ("k%d" % rng.randrange(nkeys)).encode()
+        k = ("%s%d" % (prefix, rng.randrange(nkeys))).encode()
         vp = _spe_any([rng.choice(orgs)]) if rng.random() < 0.8 else all_orgs
         kvmeta[("mycc", "", k) if rng.random() < 0.5 else ("mycc", coll, hashlib.sha256(k).digest())] = vp
     rws = []
     for _ in range(ntx):
         kind = rng.choice(["w", "w", "md", "pw", "pmd", "w2", "none"])
-        keys = ["k%d" % rng.randrange(nkeys) for _ in range(1 + (kind == "w2"))]
+        keys = ["%s%d" % (prefix, rng.randrange(nkeys)) for _ in range(1 + (kind == "w2"))]
         r = rng.random()
         md = {} if r < 0.2 else {VP: _spe_any([rng.choice(orgs)])}
         if garbage_vp and r > 0.9:

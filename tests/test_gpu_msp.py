@@ -168,3 +168,44 @@ def test_group_resolves_on_every_device():
     exp = v20.validate_blocks(v20.ChannelModel("testchannel", [], defs[7], config=config), [b["block"] for b in sel])
     assert [list(f) for f in got] == [list(f) for f in exp]
     g.close()
+
+
+def test_fork_hazard_reframings_are_unsupported():
+    """a real msp/testdata leaf re-framed into shapes Go's parsers accept (extra
+    element after the outer signature, junk before the PEM, a malformed block before a valid one,
+    ...) is Unsupported in the engine and the oracle, never an undeserializable identity; and a
+    block whose creator is such a re-framing is an Unsupported batch on both sides."""
+    from tests.blockfix import creator_idbytes_path, replace_field
+    from tests.sample_channel import tx_identities, v20_channel
+    rel = "msp/testdata/nodeous3"
+    conf = bytes.fromhex(FX["msps"][rel]["config"])
+    m = MSP(decode("FabricMSPConfig", conf))
+    ids = FX["msps"][rel]["identities"]
+    pem = ids[[k for k in ids if k.startswith("signcerts/")][0]].encode()
+    eng = _lib.Engine(0)
+    eng.channel_init("ch")
+    eng.channel_config(make_config(["SampleOrg"], msp_configs={"SampleOrg": conf}))
+    variants = MC.fork_hazard_variants(pem)
+    sers = [serialized_identity("SampleOrg", p) for _, p in variants]
+    for (label, p), ser, st in zip(variants, sers, eng.msp_resolve(sers)):
+        exp_st, ident = _expect(m, ser)
+        assert exp_st == (MC.OK if label == "short_line_wrap" else MC.UNSUP), label
+        _check(eng, ser, st, exp_st, ident, label)
+    eng.close()
+    # end to end: block 13 of the v2.0 sample ledger with its creator unregistered and re-framed
+    blocks_, config, idents, defs = v20_channel()
+    b13 = [b for b in blocks_ if b["number"] == 13][0]["block"]
+    creator = tx_identities(decode("Block", b13)["data"]["data"][0])[0]
+    unreg = [(s, i) for s, i in idents if s != creator]
+    idb = decode("SerializedIdentity", creator)["id_bytes"]
+    for label, p in MC.fork_hazard_variants(idb)[:4]:
+        blk = replace_field(b13, creator_idbytes_path(0), p)
+        eng = _lib.Engine(0)
+        txvalidator.setup_channel(eng, "testchannel", unreg, {}, config=config)
+        from tests.test_gpu_channel import _define
+        _define(eng, defs[13])
+        with pytest.raises(_lib.Unsupported):
+            eng.validate_blocks([blk])
+        with pytest.raises(v20.Unsupported):
+            v20.validate_block(v20.ChannelModel("testchannel", unreg, defs[13], config=config), blk)
+        eng.close()

@@ -60,7 +60,7 @@ def test_synthetic_blocks(mode, seed):
     collections) batched with a plain C2 block: equal to the oracle"""
     net = network()
     ccs = _net_ccs(net)
-    sb = [sbe_cases.make_sbe_block(net, 60, 100 * seed + k, number=1 + k) for k in range(3)]
+    sb = [sbe_cases.make_sbe_block(net, 60, 100 * seed + k, number=1 + k, prefix="b%dk" % k) for k in range(3)]
     kvmeta = {}
     for _, kv in sb:
         kvmeta.update(kv)
@@ -191,7 +191,7 @@ def test_group_and_block_shards(ndev):
     on the first) and through block-granular shards (fgv_validate_shard): equal to the oracle"""
     net = network()
     ccs = _net_ccs(net)
-    sb = [sbe_cases.make_sbe_block(net, 40, 700 + k, number=1 + k) for k in range(4)]
+    sb = [sbe_cases.make_sbe_block(net, 40, 700 + k, number=1 + k, prefix="b%dk" % k) for k in range(4)]
     kvmeta = {}
     for _, kv in sb:
         kvmeta.update(kv)
@@ -214,4 +214,73 @@ def test_group_and_block_shards(ndev):
         res, ntx = eng.validate_shard(blks, lo, hi)
         want = [c for b in range(lo_b, hi_b) for c in exp[b]]
         assert list(res[:, 0]) == want
+    eng.close()
+
+
+@MODES
+def test_batch_keylevel_hazard(mode):
+    """block 1 sets / clears key-level parameters that block 2 writes.  The
+    reference commits block 1 before block 2's vscc reads GetStateMetadata, so one batch of both is
+    Unsupported on both sides (also through a group whose devices split them); one block per call
+    with the MVCC commit between equals the oracle validating block 1, committing it, then
+    validating block 2 -- and block 2's flags do depend on block 1's commit."""
+    from oracle import mvcc as OM
+    net = network()
+    ccs = _net_ccs(net)
+    (b1, kvmeta0), (b2, _) = [sbe_cases.make_sbe_block(net, 50, 948 + k, number=2 + k) for k in range(2)]
+    model = lambda kv: v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=dict(kv))  # noqa: E731
+    with pytest.raises(v20.Unsupported):
+        v20.validate_blocks(model(kvmeta0), [b1, b2])
+    eng = _eng(net.channel, net.identities(), ccs, kvmeta0, mode)
+    with pytest.raises(_lib.Unsupported):
+        eng.validate_blocks([b1, b2])
+    g = _lib.Group([0, 0])
+    for e in g.engines:
+        txvalidator.setup_channel(e, net.channel, net.identities(), ccs, kvmeta=kvmeta0)
+        e.set_parse_mode(mode)
+    with pytest.raises(_lib.Unsupported):
+        g.validate_blocks([b1, b2])
+    g.close()
+    eng.statedb_init(1 << 16, 8 << 20)
+    db = OM.StateDB({}, kvmeta=dict(kvmeta0))
+    f1 = v20.validate_block(model(db.kvmeta), b1)
+    assert list(eng.validate_blocks([b1])[0]) == f1
+    assert list(eng.mvcc_validate(b1, 2, f1, commit=True)) == list(OM.validate_block(db, b1, f1, 2, commit=True))
+    assert db.kvmeta != kvmeta0
+    f2 = v20.validate_block(model(db.kvmeta), b2)
+    assert list(eng.validate_blocks([b2])[0]) == f2
+    assert f2 != v20.validate_block(model(kvmeta0), b2)  # (the stale state would give other flags)
+    eng.close()
+
+
+@MODES
+def test_updated_key_skips_out_of_model_policy(mode):
+    """tx 0 validly writes key K's metadata; a later tx writes K endorsed by an
+    identity outside the model.  The reference stops at ValidationParameterUpdatedError (10) and
+    never evaluates a policy, so the batch is not Unsupported even though the parallel first pass
+    would have evaluated K's policy with that identity."""
+    import random
+    net = network()
+    orgs = sorted({p.mspid for ps in net.org_peers for p in ps})
+    Id = txvalidator.Identity
+    p384 = {p.serialized for p in net.org_peers[-1]}  # the last org's peers: outside the model
+    ids = [(s, Id(i.mspid, i.pub, i.valid, i.id_digest, key="p384" if s in p384 else i.key,
+                  hash_family=i.hash_family, roles=i.roles)) for s, i in net.identities()]
+    md = sbe_cases._entries({sbe_cases.VP: sbe_cases._spe_any([orgs[0]])})
+    rws = [blocks.tx_rwset([("mycc", blocks.f_msg(4, blocks.f_str(1, "hz") + md), [])])]
+    rws += [blocks.tx_rwset([("mycc", blocks.kv_rwset([], [("hz", b"v", False)]), [])])] * 7
+    for seed in range(200):
+        blk, _, _ = blocks.make_block(net, 8, number=1, seed=seed, faults=(), rwsets=rws,
+                                      endorse_dist=((2, 1.0),))
+        txs = v20.decode("Block", blk)["data"]["data"]
+        from tests.sample_channel import tx_identities
+        e_orgs = [{v20.decode("SerializedIdentity", e)["mspid"] for e in tx_identities(d)[1:]} for d in txs]
+        if orgs[-1] not in e_orgs[0] and any(orgs[-1] in e for e in e_orgs[1:]):
+            break
+    else:
+        raise AssertionError("no seed with the wanted endorsers")
+    exp = v20.validate_block(v20.ChannelModel(net.channel, ids, net.chaincodes), blk)
+    assert exp[0] == 0 and exp.count(10) == 7
+    eng = _eng(net.channel, ids, net.chaincodes, None, mode)
+    assert list(eng.validate_blocks([blk])[0]) == exp
     eng.close()

@@ -257,3 +257,57 @@ def test_engine_parser_matches_on_synthetic_certificates():
     for label, ser, *_ in cases:
         pem = decode("SerializedIdentity", ser).get("id_bytes") or b""
         assert L.x509_probe(pem) == _oracle_view(pem), label
+
+
+# ---- fork hazards: shapes Go's encoding/pem / crypto/x509 accept that the engine
+# does not model come out Unsupported on both sides, never as an undeserializable identity
+def test_reference_leaf_reframings_are_unsupported():
+    from tests.msp_cases import fork_hazard_variants
+    L = _lib()
+    rel = "msp/testdata/nodeous3"
+    m = _msp(rel)
+    ids = FX["msps"][rel]["identities"]
+    pem = ids[[k for k in ids if k.startswith("signcerts/")][0]].encode()
+    assert m.resolve(pem).valid  # the leaf as issued
+    for label, p in fork_hazard_variants(pem):
+        want = "OK" if label == "short_line_wrap" else "UNSUP"
+        try:
+            got = m.resolve(p)
+            got = "OK" if got is not None and got.valid else "FAILED"
+        except Unsupported:
+            got = "UNSUP"
+        assert got == want, label
+        v = L.x509_probe(p)
+        assert v == _oracle_view(p), label
+        assert (v["status"] == 2) == (want == "UNSUP"), (label, v)
+
+
+def test_engine_parser_matches_on_mutated_pem_text():
+    """byte-level mutations of the PEM text: the engine's framing decision equals the oracle's,
+    and nothing that still holds a "-----BEGIN " is ever a PEM parse error"""
+    L = _lib()
+    rng = random.Random(7)
+    seeds = [p.encode() for _, p in sorted(FX["certs"].items())][:30]
+    n_unsup = 0
+    for pem in seeds:
+        for _ in range(40):
+            d = bytearray(pem)
+            k = rng.randrange(5)
+            i = rng.randrange(len(d))
+            if k == 0:
+                d[i] = rng.choice(b" \t\r\n-=:A/+!\x00")
+            elif k == 1:
+                d.insert(i, rng.choice(b" \t\r\n-=:A"))
+            elif k == 2:
+                del d[i]
+            elif k == 3:
+                d = bytearray(rng.choice([b"x\n", b"\n", b" ", b"-----BEGIN X-----\n-----END X-----\n"])) + d
+            else:
+                d += rng.choice([b"x", b"\n\n", b"-----BEGIN CERTIFICATE-----\n"])
+            m = bytes(d)
+            a, b = L.x509_probe(m), _oracle_view(m)
+            assert a == b, m[:80]
+            if a["stage"] == "pem":
+                assert a["status"] == 2 or b"-----BEGIN " not in m
+                n_unsup += a["status"] == 2
+    assert n_unsup > 100

@@ -22,7 +22,7 @@ HARNESS = os.path.join(ROOT, "build", "asan", "fgv_sanitize")
 
 
 def _harness():
-    if not os.path.exists(HARNESS):
+    if True:  # (make rebuilds it when a host source changed)
         subprocess.run(["make", "-C", os.path.join(ROOT, "tools", "sanitize"), "-j8"], check=True,
                        stdout=subprocess.DEVNULL)
     return HARNESS
@@ -162,15 +162,22 @@ def test_harness_clean_on_certificates_and_msp_configs(tmp_path, seed):
     pems += [decode("SerializedIdentity", c[1]).get("id_bytes") or b"" for c in synthetic()[1]]
     confs = [bytes.fromhex(m["config"]) for m in fx["msps"].values()]
     rng = random.Random(seed)
-    recs = [_rec(6, p) for p in pems] + [_rec(7, c) for c in confs]
+    recs = []
+    from oracle.v20 import Unsupported
+    from tests.msp_cases import fork_hazard_variants
+    pems += [v for p in pems[:6] for _, v in fork_hazard_variants(p)]  # (the PEM / outer-shape branches)
     for p in pems[:60]:
-        der = X.pem_decode(p)
+        try:
+            der = X.pem_decode(p)
+        except Unsupported:
+            continue
         if not der:
             continue
         for d in _mutate(rng, der, 25):
             recs.append(_rec(6, b"-----BEGIN CERTIFICATE-----\n" + base64.encodebytes(d) + b"-----END CERTIFICATE-----\n"))
         for m in _mutate(rng, p, 5):  # the PEM text itself
             recs.append(_rec(6, m))
+    recs = [_rec(6, p) for p in pems] + [_rec(7, c) for c in confs] + recs
     for c in confs:
         recs += [_rec(7, m) for m in _mutate(rng, c, 20)]
     path = tmp_path / ("certs%d.bin" % seed)
