@@ -1914,13 +1914,11 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   S->t_enq = clk::now();
   // --- the next batch's front half, ahead of its call, while this back half runs: its
   // device copy is known (caller-resident, or being prefetched by the copy stream)
-  // Measured on MI355X (C2, 32 x 500-tx batches, fused single-GPU call), step
-  // times: not ahead (0) 0.81-0.82 ms; enqueued at once (2) 0.74-0.80 (within run-to-run noise of
-  // 0 once the payload hashes issue first, and every kernel then runs stretched); after this
-  // batch's ECDSA (1) 0.86-0.92; after its fold (3) 0.98-1.12 (they collide with k_point28, which
-  // is VALU-issue-bound, or with the next call's own kernels).  So the default keeps one batch on
-  // the GPU at a time, the next one pre-split on the host meanwhile; fgv_set_ahead / FGV_AHEAD
-  // select a placement (A/B).
+  // Measured on MI355X (C2, 32 x 500-tx batches, fused single-GPU call; DESIGN.md s5,
+  // profiles/round3_ab): enqueued at once (2, the default) 0.715-0.724 ms per step against 0.773-
+  // 0.799 not ahead (0), in the full default bench and in the lean A/B harness alike; after this
+  // batch's ECDSA (1) or after its fold (3) it collides with k_point28 or with the next call's own
+  // kernels.  fgv_set_ahead / FGV_AHEAD select a placement (A/B).
   const int ahead_mode = c->ahead_mode;
   if (nx.n && nx.d_blocks && ahead_mode) {
     BdSet &A = S->set[cur ^ 1];

@@ -171,7 +171,7 @@ struct fgv_ctx {
     hipEvent_t wait = nullptr;                 // ... once this event (the prefetch copy) has fired
   } next;
   bool last_ahead = false;  // the last device-parse call found its front half enqueued ahead
-  int ahead_mode = 0;       // fgv_set_ahead: 0 off (default), 1 after the ECDSA kernels, 2 at once, 3 after the fold
+  int ahead_mode = 2;       // fgv_set_ahead: 0 off, 1 after the ECDSA kernels, 2 at once (default), 3 after the fold
   // fgv_set_timing: record the committer's timing-only events (per-kernel device times); each
   // is a timestamp packet on the critical path (~5 us on MI355X), so off by default
   bool timing = false;

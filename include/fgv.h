@@ -365,14 +365,12 @@ int fgv_validate_shard_dev_pipelined(fgv_ctx *ctx, size_t nblocks, const uint8_t
                                      const uint32_t *next_hi);
 int fgv_last_ahead(fgv_ctx *ctx);
 /* Where the next batch's front half is enqueued by the pipelined calls (fgv_validate_shard_dev_
- * pipelined, fgv_validate_blocks_pipelined) when its device copy is known: 0 = not ahead (default;
- * the environment variable FGV_AHEAD sets the initial value): one batch on the GPU at a time, the
- * next one pre-split on the host; 2 = at once, beside the current batch's back half (C2 on MI355X:
- * 0.69-0.72 ms per step against 0.78 in an alternating A/B, but 1.09 ms in a full default bench
- * run); 1 = once the current batch's ECDSA
- * kernels are done; 3 = once its policy fold is done; 4 = once its k_prep is done (beside its
- * k_point28, which is VALU-issue-bound while the front half is latency-bound).  Results never
- * depend on it. */
+ * pipelined, fgv_validate_blocks_pipelined) when its device copy is known: 2 = at once, beside the
+ * current batch's back half (the default; the environment variable FGV_AHEAD sets the initial
+ * value; C2 on MI355X: 0.715-0.724 ms per step against 0.773-0.799 not ahead);
+ * 0 = not ahead: one batch on the GPU at a time, the next one pre-split on the host; 1 = once the
+ * current batch's ECDSA kernels are done; 3 = once its policy fold is done; 4 = once its k_prep
+ * is done (beside its k_point28).  Results never depend on it. */
 int fgv_set_ahead(fgv_ctx *ctx, int mode);
 /* Per-kernel device times of the block committer (fgv_last_kernel_times, fgv_last_timing): on,
  * every kernel of the back half is bracketed by timestamp events -- each a packet on the

@@ -533,7 +533,7 @@ def test_pipelined_front_half_ahead_rotation():
         exps.append([f for fl in _oracle(net, blks) for f in fl])
     res = torch.zeros((64, _lib.TX_RESULT_BYTES), dtype=torch.uint8, device="cuda")
     order = [0, 1, 2, 0, 0, 2, 1, 1, 2]
-    for mode in (0, 3, 1, 2):  # 0: never ahead (the default); the others place it differently
+    for mode in (0, 3, 1, 2):  # 0: never ahead; 2 (the default) at once; the others place it differently
         eng.set_ahead(mode)
         for i, k in enumerate(order):
             nxt = order[i + 1] if i + 1 < len(order) else 0
