@@ -32,7 +32,7 @@ EXPORTED = [
     "fgv_validate_blocks_pipelined", "fgv_set_timing",
     "fgv_group_init", "fgv_group_destroy", "fgv_group_size", "fgv_group_ctx", "fgv_group_validate_blocks",
     "fgv_msp_resolve", "fgv_msp_resolve_blocks", "fgv_set_auto_resolve", "fgv_msp_identity",
-    "fgv_kvmeta_set", "fgv_kvmeta_count", "fgv_kvmeta_get",
+    "fgv_kvmeta_set", "fgv_kvmeta_count", "fgv_kvmeta_get", "fgv_msp_identity_ous",
 ]
 # fgv_msp_resolve status (include/fgv.h)
 RESOLVE_KNOWN, RESOLVE_OK, RESOLVE_FAILED, RESOLVE_UNSUPPORTED, RESOLVE_REPEAT = range(5)
@@ -130,6 +130,7 @@ def load():
         L.fgv_channel_config.argtypes = [vp, ctypes.c_char_p, sz]
         L.fgv_msp_declare.argtypes = [vp, ctypes.c_char_p]
         L.fgv_msp_register_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(IdentityInfo)]
+        L.fgv_msp_identity_ous.argtypes = [vp, ctypes.c_char_p, sz, sz, vp, vp, vp, vp]
         L.fgv_ledger_add_txids.argtypes = [vp, vp, vp, vp, sz]
         L.fgv_validate_blocks.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp]
         L.fgv_validate_blocks_pipelined.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp, sz, vp, vp, vp]
@@ -526,6 +527,17 @@ class Engine:
             ctypes.memmove(info.pubkey, bytes(pub)[:64], min(64, len(pub)))
         ctypes.memmove(info.id_digest, bytes(id_digest), 32)
         _check(self._L.fgv_msp_register_identity(self._h, serialized, len(serialized), ctypes.byref(info)))
+
+    def msp_identity_ous(self, serialized: bytes, ous):
+        """fgv_msp_identity_ous: [(OrganizationalUnitIdentifier str, CertifiersIdentifier bytes)]"""
+        n = len(ous)
+        ob = [o.encode() for o, _ in ous]
+        cb = [bytes(c) for _, c in ous]
+        op = (ctypes.c_char_p * max(n, 1))(*ob)
+        ol = (ctypes.c_size_t * max(n, 1))(*[len(o) for o in ob])
+        cp = (ctypes.c_char_p * max(n, 1))(*cb)
+        cl = (ctypes.c_size_t * max(n, 1))(*[len(c) for c in cb])
+        _check(self._L.fgv_msp_identity_ous(self._h, serialized, len(serialized), n, op, ol, cp, cl))
 
     def msp_resolve(self, serialized):
         """fgv_msp_resolve: the MSP cache miss for a list of SerializedIdentity bytes ->

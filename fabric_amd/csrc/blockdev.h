@@ -78,14 +78,23 @@ struct DevIdent {
   uint32_t vclass;    // Verify: 0 on the GPU, 1 always fails, 2 outside the engine; 3 undeserializable
   uint32_t roles;     // SatisfiesPrincipal(ROLE r) bits
   uint32_t roles_known;
+  uint32_t ous_known;        // GetOrganizationalUnits known: ident_ous[ou_off .. ou_off + ou_n)
+  uint32_t ou_off, ou_n;
+  uint32_t pad;
+};
+// one leaf principal (fgv_channel.h Prin; kinds DPR_* = PR_*)
+enum : int32_t { DPR_ROLE = 0, DPR_IDENTITY = 1, DPR_OU = 2, DPR_NOMINAL = 3, DPR_NEVER = 4, DPR_UNRESOLVED = 5 };
+struct DevPrin {
+  int32_t kind, msp, role;
+  uint32_t canon;
+  int32_t ou;
   uint32_t pad;
 };
 
 struct DevPNode {
   int32_t type;       // 1 NOutOf, 2 SignedBy
   int32_t n;          // NOutOf threshold
-  int32_t msp;        // SignedBy: interned principal Mspid (-1: undecodable principal)
-  int32_t role;       // SignedBy: MSPRole.role
+  uint32_t p0, np;    // SignedBy: the principal's leaves prins[p0 .. p0+np), all must hold
   uint32_t kid0, nkids;  // NOutOf: kids[kid0 .. kid0+nkids) in the kid array
 };
 enum : uint32_t { DP_REJECT = 0, DP_SIG = 1, DP_IMPLICIT = 2, DP_UNSUP = 3 };
@@ -124,6 +133,8 @@ struct DevChannel {  // device pointers + sizes (passed by value to the kernels)
   const DevPNode *nodes;
   const uint32_t *kids;
   const uint32_t *subs;
+  const DevPrin *prins;
+  const int32_t *ident_ous;     // interned (OU, certifier) ids of the identities
   const uint8_t *committed;     // committed ledger txids: open-addressing table of 32-byte keys
   uint32_t committed_mask;      // (all-zero key == empty; a zero txid is kept in committed_zero)
   uint32_t committed_zero;

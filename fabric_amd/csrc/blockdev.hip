@@ -1135,7 +1135,34 @@ namespace {
 // cauthdsl greedy evaluation (common/cauthdsl/cauthdsl.go:24-92): SignedBy takes the first
 // unused signer satisfying the principal (same MSP; MEMBER = valid, other roles from the role
 // bits); NOutOf tries each sub-rule on a copy of `used` and keeps the copy when it succeeds.
-// Iterative DFS; returns -1 on stack overflow.
+// SatisfiesPrincipal of one leaf (fgv_block.cpp prin_sat, MSP v1.4.3): 1 / 0 / 2 (unknown)
+DEV int prin_sat(const DevChannel &ch, const DevPrin &p, const DevIdent &I) {
+  switch (p.kind) {
+    case DPR_ROLE: return I.msp == p.msp && (p.role == 0 ? I.valid != 0 : ((I.roles >> p.role) & 1u) != 0);
+    case DPR_IDENTITY: return I.canon == p.canon && I.msp == p.msp && I.valid != 0;
+    case DPR_OU: {
+      if (I.msp != p.msp || !I.valid) return 0;
+      if (!I.ous_known) return 2;
+      for (uint32_t k = 0; k < I.ou_n; k++)
+        if (ch.ident_ous[I.ou_off + k] == p.ou) return 1;
+      return 0;
+    }
+    case DPR_NOMINAL: return 1;
+    case DPR_UNRESOLVED: return 2;
+    default: return 0;
+  }
+}
+// the leaves of one SignedBy principal in collectPrincipals order: the first error decides
+DEV int principal_sat(const DevChannel &ch, const DevPNode &N, const DevIdent &I) {
+  int r = 1;
+  for (uint32_t k = 0; k < N.np; k++) {
+    const int v = prin_sat(ch, ch.prins[N.p0 + k], I);
+    if (v == 0) return 0;
+    if (v == 2) r = 2;
+  }
+  return r;
+}
+// Iterative DFS; returns -1 on stack overflow, 2 when a principal cannot be decided.
 DEV int eval_sig(const DevChannel &ch, const DevPolicy &P, const int32_t *ids, uint32_t nids) {
   struct F {
     uint32_t node, k;
@@ -1152,18 +1179,16 @@ DEV int eval_sig(const DevChannel &ch, const DevPolicy &P, const int32_t *ids, u
       const DevPNode &N = ch.nodes[node];
       if (N.type == 2) {
         ret = 0;
-        if (N.msp >= 0)
-          for (uint32_t i = 0; i < nids; i++) {
-            if ((used >> i) & 1u) continue;
-            const DevIdent &I = ch.idents[ids[i]];
-            const bool sat = I.msp == N.msp &&
-                             (N.role == 0 ? I.valid != 0 : (N.role > 0 && N.role < 32 && ((I.roles >> N.role) & 1u)));
-            if (sat) {
-              used |= 1u << i;
-              ret = 1;
-              break;
-            }
+        for (uint32_t i = 0; i < nids; i++) {
+          if ((used >> i) & 1u) continue;
+          const int v = principal_sat(ch, N, ch.idents[ids[i]]);
+          if (v == 2) return 2;  // (the greedy choice depends on it)
+          if (v == 1) {
+            used |= 1u << i;
+            ret = 1;
+            break;
           }
+        }
       } else {
         if (sp == 16) return -1;
         st[sp++] = F{node, 0, 0, 0};

@@ -107,11 +107,11 @@ using namespace fgvb;
 
 // channel model image in HBM for the device-resident path (blockdev.h DevChannel)
 struct DevImage {
-  DevBuf name, idents, ibytes, itable, ihash, cc, colls, impl, msps, ccb, pol, nodes, kids, subs, committed;
+  DevBuf name, idents, ibytes, itable, ihash, cc, colls, impl, msps, ccb, pol, nodes, kids, subs, prins, iou, committed;
   DevChannel ch{};
   void release() {
     for (DevBuf *b : {&name, &idents, &ibytes, &itable, &ihash, &cc, &colls, &impl, &msps, &ccb, &pol, &nodes, &kids,
-                      &subs, &committed})
+                      &subs, &prins, &iou, &committed})
       b->release();
   }
 };
@@ -523,29 +523,56 @@ struct UsedVec {
   bool get(size_t i) const { return v[i] != 0; }
   void set(size_t i) { v[i] = 1; }
 };
+static_assert(DPR_ROLE == PR_ROLE && DPR_IDENTITY == PR_IDENTITY && DPR_OU == PR_OU && DPR_NOMINAL == PR_NOMINAL &&
+                  DPR_NEVER == PR_NEVER && DPR_UNRESOLVED == PR_UNRESOLVED,
+              "device principal kinds");
+// SatisfiesPrincipal of one leaf (msp/mspimpl.go:477-660, MSP v1.4.3): 1 / 0 / 2 (unknown)
+static int prin_sat(const Prin &p, const Ident &I) {
+  switch (p.kind) {
+    case PR_ROLE:  // same MSP; MEMBER = Validate, other roles from the MSP layer's role bits
+      return I.msp == p.msp && (p.role == 0 ? I.valid : ((I.roles >> p.role) & 1u) != 0);
+    case PR_IDENTITY:  // the same sanitized certificate (cert.Raw) of the same MSP, then Validate
+      return I.canon == p.canon && I.msp == p.msp && I.valid;
+    case PR_OU:  // same MSP, Validate, then one of its (OU, certifier) pairs
+      if (I.msp != p.msp || !I.valid) return 0;
+      if (!I.ous_known) return 2;
+      return std::find(I.ous.begin(), I.ous.end(), p.ou) != I.ous.end();
+    case PR_NOMINAL: return 1;
+    case PR_UNRESOLVED: return 2;
+    default: return 0;
+  }
+}
+// the leaves of one SignedBy principal, in collectPrincipals order: the first error decides
+static int principal_sat(const Policy &P, int pr, const Ident &I) {
+  int r = 1;
+  for (uint32_t k = P.prin_off[pr], e = k + P.prin_cnt[pr]; k < e; k++) {
+    const int v = prin_sat(P.prins[k], I);
+    if (v == 0) return 0;
+    if (v == 2) r = 2;
+  }
+  return r;
+}
 template <class U>
-static bool eval_node(const Policy &P, int node, const int *ids, size_t nids, const Channel &ch, U &used) {
+static int eval_node(const Policy &P, int node, const int *ids, size_t nids, const Channel &ch, U &used) {
   const PNode &N = P.nodes[node];
   if (N.type == 2) {
-    const int32_t msp = P.principal_mspi[N.principal];  // -1: undecodable principal
-    const int32_t role = P.principal_role[N.principal];
-    if (msp < 0) return false;
     for (size_t i = 0; i < nids; i++) {
       if (used.get(i)) continue;
-      const Ident &I = ch.idents[ids[i]];
-      // SatisfiesPrincipal(ROLE): same MSP, MEMBER = Validate, other roles from the MSP layer
-      const bool sat = I.msp == msp && (role == 0 ? I.valid : (role > 0 && role < 32 && ((I.roles >> role) & 1u)));
-      if (sat) {
+      const int v = principal_sat(P, N.principal, ch.idents[ids[i]]);
+      if (v == 2) return 2;  // (the greedy choice depends on it)
+      if (v == 1) {
         used.set(i);
-        return true;
+        return 1;
       }
     }
-    return false;
+    return 0;
   }
   int32_t verified = 0;
   for (int k : N.kids) {
     U tmp = used;
-    if (eval_node(P, k, ids, nids, ch, tmp)) {
+    const int v = eval_node(P, k, ids, nids, ch, tmp);
+    if (v == 2) return 2;
+    if (v == 1) {
       verified++;
       used = std::move(tmp);
     }
@@ -564,11 +591,11 @@ static int eval_policy(const Channel &ch, int pi, const int *ids, size_t nids, i
           if (!ch.idents[ids[i]].roles_known) return 2;
       if (nids <= 64) {
         UsedBits u;
-        return eval_node(P, P.root, ids, nids, ch, u) ? 1 : 0;
+        return eval_node(P, P.root, ids, nids, ch, u);
       }
       UsedVec u;
       u.v.assign(nids, 0);
-      return eval_node(P, P.root, ids, nids, ch, u) ? 1 : 0;
+      return eval_node(P, P.root, ids, nids, ch, u);
     }
     case PK_IMPLICIT: {  // ImplicitMetaPolicy.EvaluateSignedData (implicitmeta.go:69-104)
       if (depth > 0) return 2;
@@ -1288,6 +1315,30 @@ int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, i
   return FGV_OK;
 }
 
+int fgv_block_identity_ous(fgv_block_state *S, const uint8_t *ser, size_t len, size_t n, const char *const *ou,
+                           const size_t *ou_lens, const uint8_t *const *certifiers, const size_t *cert_lens) {
+  Channel &ch = S->ch;
+  VSerializedIdentity sid;
+  if (!pbw::decode(ser, len, sid)) return FGV_EINVAL;
+  uint64_t h = hash_bytes(sid.mspid.p, sid.mspid.n);
+  h = hash_bytes(sid.id_bytes.p, sid.id_bytes.n, h ^ 0xA5);
+  auto range = ch.ident_index.equal_range(h);
+  for (auto r = range.first; r != range.second; ++r) {
+    Ident &I = ch.idents[r->second];
+    if (!sid.mspid.eq(I.mspid.data(), I.mspid.size()) || !sid.id_bytes.eq(I.id_bytes.data(), I.id_bytes.size()))
+      continue;
+    I.ous.clear();
+    for (size_t k = 0; k < n; k++)
+      I.ous.push_back(ch.ou_intern(std::string_view(reinterpret_cast<const char *>(certifiers[k]), cert_lens[k]),
+                                   std::string_view(ou[k], ou_lens[k])));
+    I.ous_known = true;
+    S->dev_dirty = true;
+    ch.dirty = true;
+    return FGV_OK;
+  }
+  return FGV_ESTATE;
+}
+
 int fgv_block_define_chaincode(fgv_block_state *S, const char *ns, const char *plugin, const uint8_t *policy,
                                size_t len, uint32_t flags) {
   S->dev_dirty = true;
@@ -1394,6 +1445,7 @@ static int build_dev_image(fgv_block_state *S) {
   if ((rc = upload(D.name, name))) return rc;
   // identities
   std::vector<DevIdent> idents(ch.idents.size());
+  std::vector<int32_t> iou;
   std::vector<uint8_t> ib;
   std::vector<uint64_t> ih(ch.idents.size());
   for (size_t i = 0; i < ch.idents.size(); i++) {
@@ -1415,6 +1467,10 @@ static int build_dev_image(fgv_block_state *S) {
     d.vclass = I.kind == FGV_KEY_UNDESERIALIZABLE ? 3u : (uint32_t)I.verify_class();
     d.roles = I.roles;
     d.roles_known = I.roles_known ? 1u : 0u;
+    d.ous_known = I.ous_known ? 1u : 0u;
+    d.ou_off = (uint32_t)iou.size();
+    d.ou_n = (uint32_t)I.ous.size();
+    iou.insert(iou.end(), I.ous.begin(), I.ous.end());
     d.pad = 0;
     ih[i] = bd_ident_hash(reinterpret_cast<const uint8_t *>(I.mspid.data()), d.msp_len,
                           reinterpret_cast<const uint8_t *>(I.id_bytes.data()), d.idb_len);
@@ -1429,7 +1485,7 @@ static int build_dev_image(fgv_block_state *S) {
     itable[pos] = (uint32_t)i + 1;
   }
   if ((rc = upload(D.idents, idents)) || (rc = upload(D.ibytes, ib)) || (rc = upload(D.itable, itable)) ||
-      (rc = upload(D.ihash, ih)))
+      (rc = upload(D.ihash, ih)) || (rc = upload(D.iou, iou)))
     return rc;
   // chaincodes (+ their collections), implicit collections, channel MSPs -> word tables over
   // one byte arena; policies -> flat node / kid / sub arrays
@@ -1462,10 +1518,12 @@ static int build_dev_image(fgv_block_state *S) {
     if (ch.known_msps.count(kv.second)) str(kv.first, msps);
   std::vector<DevPolicy> pol(ch.policies.size());
   std::vector<DevPNode> nodes;
+  std::vector<DevPrin> prins;
   std::vector<uint32_t> kids, subs;
   for (size_t p = 0; p < ch.policies.size(); p++) {
     const Policy &P = ch.policies[p];
-    const uint32_t nbase = (uint32_t)nodes.size();
+    const uint32_t nbase = (uint32_t)nodes.size(), pbase = (uint32_t)prins.size();
+    for (const Prin &x : P.prins) prins.push_back(DevPrin{x.kind, x.msp, x.role, x.canon, x.ou, 0});
     DevPolicy &d = pol[p];
     d.kind = P.kind == PK_SIG ? DP_SIG : P.kind == PK_IMPLICIT ? DP_IMPLICIT : P.kind == PK_UNSUP ? DP_UNSUP : DP_REJECT;
     d.decode_ok = P.decode_ok;
@@ -1480,8 +1538,8 @@ static int build_dev_image(fgv_block_state *S) {
       DevPNode dn;
       dn.type = N.type;
       dn.n = N.n;
-      dn.msp = (N.type == 2) ? P.principal_mspi[N.principal] : -1;
-      dn.role = (N.type == 2) ? P.principal_role[N.principal] : 0;
+      dn.p0 = (N.type == 2) ? pbase + P.prin_off[N.principal] : 0;
+      dn.np = (N.type == 2) ? P.prin_cnt[N.principal] : 0;
       dn.kid0 = (uint32_t)kids.size();
       dn.nkids = (uint32_t)N.kids.size();
       for (int k : N.kids) kids.push_back(nbase + (uint32_t)k);
@@ -1491,7 +1549,8 @@ static int build_dev_image(fgv_block_state *S) {
   ccb.resize(ccb.size() + 64, 0);
   if ((rc = upload(D.cc, cc)) || (rc = upload(D.colls, colls)) || (rc = upload(D.impl, impl)) ||
       (rc = upload(D.msps, msps)) || (rc = upload(D.ccb, ccb)) || (rc = upload(D.pol, pol)) ||
-      (rc = upload(D.nodes, nodes)) || (rc = upload(D.kids, kids)) || (rc = upload(D.subs, subs)))
+      (rc = upload(D.nodes, nodes)) || (rc = upload(D.kids, kids)) || (rc = upload(D.subs, subs)) ||
+      (rc = upload(D.prins, prins)))
     return rc;
   int rc2 = build_committed(S);
   if (rc2) return rc2;
@@ -1516,6 +1575,8 @@ static int build_dev_image(fgv_block_state *S) {
   d.nodes = D.nodes.as<DevPNode>();
   d.kids = D.kids.as<uint32_t>();
   d.subs = D.subs.as<uint32_t>();
+  d.prins = D.prins.as<DevPrin>();
+  d.ident_ous = D.iou.as<int32_t>();
   return FGV_OK;
 }
 
@@ -2247,6 +2308,9 @@ void fgv_block_misses(fgv_block_state *S, size_t nblocks, const uint8_t *const *
       const std::string_view k(reinterpret_cast<const char *>(id.p), id.n);
       if (seen.insert(k).second) out.push_back(std::string(k));
     }
+  // IDENTITY principals of the compiled policies that name a never-deserialized certificate
+  for (const std::string &p : ch.unresolved_principals)
+    if (seen.insert(p).second) out.push_back(p);
 }
 
 // ======================================================================= sanitizer probe

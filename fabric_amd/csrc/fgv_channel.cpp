@@ -77,7 +77,7 @@ int build_node(Policy &P, const std::vector<Span> &occ, bool &wire_ok, int depth
   PNode node;
   if (raw.which == 1) {
     node.type = 2;
-    if (raw.signed_by < 0 || raw.signed_by >= (int32_t)P.principal_mspi.size()) return -1;
+    if (raw.signed_by < 0 || raw.signed_by >= (int32_t)P.prin_off.size()) return -1;
     node.principal = raw.signed_by;
   } else if (raw.which == 2) {
     node.type = 1;
@@ -103,6 +103,84 @@ int build_node(Policy &P, const std::vector<Span> &occ, bool &wire_ok, int depth
   return (int)P.nodes.size() - 1;
 }
 
+struct VOrgUnit {  // OrganizationUnit {msp_identifier 1, organizational_unit_identifier 2, certifiers_identifier 3}
+  Span mspid, ou, certifier;
+  pbw::Kind kind(uint32_t f) { return f <= 2 && f ? pbw::K_STRING : f == 3 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t f, Span s) {
+    (f == 1 ? mspid : f == 2 ? ou : certifier) = s;
+    return true;
+  }
+};
+struct VAnonymity {  // MSPIdentityAnonymity {anonymity_type 1}
+  int32_t type = 0;
+  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_VARINT : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t v) { type = pbw::as_int32(v); }
+  bool on_len(uint32_t, Span) { return true; }
+};
+struct VCombined {  // CombinedPrincipal {principals 1 (repeated MSPPrincipal)}: decoded eagerly
+  std::vector<VPrincipal> prs;
+  pbw::Kind kind(uint32_t f) { return f == 1 ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    VPrincipal p;
+    if (!pbw::decode(s.p, s.n, p)) return false;
+    prs.push_back(p);
+    return true;
+  }
+};
+
+// collectPrincipals (msp/mspimpl.go:440-471) + each leaf's compiled check; a COMBINED that does
+// not decode or holds no principal is an error for every identity (a NEVER leaf: the AND of the
+// leaves fails).  false: nesting beyond the engine's bound (outside the model).
+bool compile_principal(Channel &ch, int32_t cls, const Span &body, std::vector<Prin> &out, bool &needs_roles,
+                       int depth) {
+  Prin p;
+  if (cls == 4) {  // COMBINED (MSP >= v1.1)
+    if (depth > 16) return false;
+    VCombined cp;
+    if (!pbw::decode(body.p, body.n, cp) || cp.prs.empty()) {
+      out.push_back(p);
+      return true;
+    }
+    for (const VPrincipal &q : cp.prs)
+      if (!compile_principal(ch, q.cls, q.principal, out, needs_roles, depth + 1)) return false;
+    return true;
+  }
+  if (cls == 0) {  // ROLE
+    VMSPRole role;
+    if (pbw::decode(body.p, body.n, role) && role.role >= 0 && role.role <= 4) {  // ("invalid MSP role type")
+      p.kind = PR_ROLE;
+      p.msp = ch.intern(role.mspid.str());
+      p.role = role.role;
+      needs_roles |= role.role != 0;
+    }
+  } else if (cls == 1) {  // ORGANIZATION_UNIT
+    VOrgUnit ou;
+    if (pbw::decode(body.p, body.n, ou)) {
+      p.kind = PR_OU;
+      p.msp = ch.intern(ou.mspid.str());
+      p.ou = ch.ou_intern(std::string_view(reinterpret_cast<const char *>(ou.certifier.p), ou.certifier.n),
+                          std::string_view(reinterpret_cast<const char *>(ou.ou.p), ou.ou.n));
+    }
+  } else if (cls == 2) {  // IDENTITY: the identity's MSP deserializes the principal
+    const int j = ch.lookup(body);
+    if (j >= 0) {
+      p.kind = PR_IDENTITY;
+      p.msp = ch.idents[j].msp;
+      p.canon = ch.idents[j].canon;
+    } else if (j == -2) {
+      p.kind = PR_UNRESOLVED;
+      ch.unresolved_principals.push_back(body.str());
+    }
+  } else if (cls == 3) {  // ANONYMITY: NOMINAL holds for any identity, ANONYMOUS for none
+    VAnonymity an;
+    if (pbw::decode(body.p, body.n, an) && an.type == 0) p.kind = PR_NOMINAL;
+  }
+  out.push_back(p);
+  return true;
+}
+
 }  // namespace
 
 // a SignaturePolicyEnvelope (all occurrences merged) -> Policy; check_version: the channel-config
@@ -116,11 +194,11 @@ static Policy compile_spe(Channel &ch, const std::vector<Span> &occ, bool check_
   std::vector<VPrincipal> prs(spe.identities.size());
   for (size_t i = 0; i < spe.identities.size(); i++)
     if (!pbw::decode(spe.identities[i].p, spe.identities[i].n, prs[i])) return P;
+  bool in_model = true;
   for (const VPrincipal &pr : prs) {
-    VMSPRole role;
-    const bool ok = pbw::decode(pr.principal.p, pr.principal.n, role);
-    P.principal_mspi.push_back(ok ? ch.intern(role.mspid.str()) : -1);
-    P.principal_role.push_back(ok ? role.role : 0);
+    P.prin_off.push_back((uint32_t)P.prins.size());
+    in_model &= compile_principal(ch, pr.cls, pr.principal, P.prins, P.needs_roles, 0);
+    P.prin_cnt.push_back((uint32_t)P.prins.size() - P.prin_off.back());
   }
   bool wire_ok = true;
   int root = -1;
@@ -130,13 +208,8 @@ static Policy compile_spe(Channel &ch, const std::vector<Span> &occ, bool check_
     bad.kind = PK_SIG;
     return bad;
   }
-  // principals other than ROLE (IDENTITY, ORGANIZATION_UNIT, ANONYMITY, COMBINED) need MSP data
-  // the engine does not hold
-  for (const VPrincipal &pr : prs)
-    if (pr.cls != 0) { P.kind = PK_UNSUP; return P; }
+  if (!in_model) { P.kind = PK_UNSUP; return P; }
   if (check_version && spe.version != 0) { P.kind = PK_UNSUP; return P; }
-  for (size_t i = 0; i < prs.size(); i++)
-    if (P.principal_mspi[i] >= 0 && P.principal_role[i] != 0) P.needs_roles = true;
   P.decode_ok = true;
   P.root = root;
   P.compile_ok = root >= 0;
@@ -169,6 +242,7 @@ int Channel::compile_app(const std::string &bytes) {
 }
 
 void Channel::compile() {
+  unresolved_principals.clear();
   policies.clear();
   policies.push_back(Policy());  // [0]: reject
   chan_idx.clear();
@@ -224,8 +298,12 @@ void Channel::compile() {
         Policy P;
         P.kind = PK_SIG;
         P.decode_ok = P.compile_ok = true;
-        P.principal_mspi.push_back(intern(kv.first));
-        P.principal_role.push_back(0);
+        Prin pr;
+        pr.kind = PR_ROLE;
+        pr.msp = intern(kv.first);
+        P.prin_off.push_back(0);
+        P.prin_cnt.push_back(1);
+        P.prins.push_back(pr);
         PNode sb;
         sb.type = 2;
         sb.principal = 0;

@@ -41,6 +41,11 @@ struct Ident {
   int32_t msp = -1;             // interned Mspid
   uint8_t digest[32] = {};      // identity Id (SHA-256 of the certificate)
   uint8_t pub[64] = {};         // P-256 X || Y (FGV_KEY_P256)
+  // GetOrganizationalUnits (msp/identities.go): (OU identifier, certifiers identifier) pairs,
+  // interned by Channel::ou_intern; unknown unless the MSP cache miss or fgv_msp_identity_ous
+  // gave them
+  bool ous_known = false;
+  std::vector<int32_t> ous;
   // Verify outcome class: 0 = verified on the GPU, 1 = always fails (RSA, F5), 2 = outside
   // the engine (P-384, SHA3 MSP)
   int verify_class() const {
@@ -53,8 +58,26 @@ struct Ident {
 struct PNode {
   int type = 0;  // 1 NOutOf, 2 SignedBy
   int32_t n = 0;
-  int principal = -1;
+  int principal = -1;  // SignedBy: index of the envelope's principal (Policy::prin_off / prin_cnt)
   std::vector<int> kids;
+};
+// One leaf principal of an MSPPrincipal after collectPrincipals (msp/mspimpl.go:440-471, a
+// COMBINED principal flattened into its leaves, all of which must hold), compiled for MSP v1.4.3
+// (satisfiesPrincipalInternalV142 -> V13 -> PreV13, mspimpl.go:477-660).
+enum PrinKind : uint8_t {
+  PR_ROLE = 0,        // MSPRole: same MSP, MEMBER = Validate, other roles from the identity's role bits
+  PR_IDENTITY = 1,    // SerializedIdentity: the same sanitized certificate (Mspid + Id), and Validate
+  PR_OU = 2,          // OrganizationUnit: same MSP, Validate, an OU with that identifier and certifier
+  PR_NOMINAL = 3,     // MSPIdentityAnonymity NOMINAL: every identity
+  PR_NEVER = 4,       // an error for every identity (undecodable, unknown class, ANONYMOUS, ...)
+  PR_UNRESOLVED = 5,  // IDENTITY of a channel MSP not yet deserialized: outside the model until resolved
+};
+struct Prin {
+  uint8_t kind = PR_NEVER;
+  int32_t msp = -1;    // ROLE / OU: interned MspIdentifier
+  int32_t role = 0;    // ROLE
+  uint32_t canon = 0;  // IDENTITY
+  int32_t ou = -1;     // OU: Channel::ou_intern(certifier, identifier)
 };
 enum PolKind : uint8_t { PK_REJECT = 0, PK_SIG = 1, PK_IMPLICIT = 2, PK_UNSUP = 3 };
 struct Policy {
@@ -62,9 +85,10 @@ struct Policy {
   bool decode_ok = false, compile_ok = false;  // PK_SIG: rule decoded / compiled
   std::vector<PNode> nodes;
   int root = -1;
-  std::vector<int32_t> principal_mspi;  // interned principal Mspid, -1 for an undecodable principal
-  std::vector<int32_t> principal_role;  // MSPRole.role
-  bool needs_roles = false;             // a principal with a role other than MEMBER
+  // envelope principal i = the leaves prins[prin_off[i] .. prin_off[i] + prin_cnt[i])
+  std::vector<uint32_t> prin_off, prin_cnt;
+  std::vector<Prin> prins;
+  bool needs_roles = false;             // a ROLE leaf with a role other than MEMBER
   int threshold = 0;                    // PK_IMPLICIT
   std::vector<int> subs;                // PK_IMPLICIT: policy indices (0 = reject)
 };
@@ -124,6 +148,20 @@ struct Channel {
   // VSCCExecutionFailureError, the reference halts)
   std::unordered_map<std::string, int> kvmeta_pi;
   bool dirty = true;
+  // (certifiers identifier, OU identifier) -> id, shared by identities and OU principals
+  std::unordered_map<std::string, int32_t> ou_ids;
+  // IDENTITY principals of channel MSPs never deserialized (compile()): the MSP cache miss
+  // resolves them with a batch's identities (fgv_block_misses)
+  std::vector<std::string> unresolved_principals;
+
+  int32_t ou_intern(std::string_view certifier, std::string_view ou) {
+    std::string k;
+    const uint32_t a = (uint32_t)certifier.size();
+    k.append(reinterpret_cast<const char *>(&a), 4).append(certifier).append(ou);
+    auto it = ou_ids.find(k);
+    if (it == ou_ids.end()) it = ou_ids.emplace(std::move(k), (int32_t)ou_ids.size()).first;
+    return it->second;
+  }
 
   static std::string kvkey(std::string_view ns, std::string_view coll, std::string_view key) {
     std::string k;

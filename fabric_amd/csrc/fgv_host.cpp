@@ -828,6 +828,13 @@ int fgv_msp_register_identity(fgv_ctx *c, const uint8_t *serialized, size_t len,
   return fgv_block_add_identity(c->blk, serialized, len, slot, info);
 }
 
+int fgv_msp_identity_ous(fgv_ctx *c, const uint8_t *serialized, size_t len, size_t n, const char *const *ou,
+                         const size_t *ou_lens, const uint8_t *const *certifiers, const size_t *certifier_lens) {
+  if (!c || !serialized || (n && (!ou || !ou_lens || !certifiers || !certifier_lens))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return fgv_block_identity_ous(c->blk, serialized, len, n, ou, ou_lens, certifiers, certifier_lens);
+}
+
 int fgv_msp_add_identity(fgv_ctx *c, const uint8_t *serialized, size_t len, const uint8_t *pubkey, int valid,
                          const uint8_t *id_digest) {
   if (!c || !serialized || !id_digest) return FGV_EINVAL;

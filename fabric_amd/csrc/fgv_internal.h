@@ -246,6 +246,9 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
                             const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                             const uint32_t *tx_hi, fgv_tx_result *res_out, size_t res_cap, size_t *ntx_out);
 long fgv_block_count_txs(const uint8_t *b, size_t n);
+// GetOrganizationalUnits of a registered identity (fgv_msp_identity_ous, the MSP cache miss)
+int fgv_block_identity_ous(fgv_block_state *S, const uint8_t *ser, size_t len, size_t n, const char *const *ou,
+                           const size_t *ou_lens, const uint8_t *const *certifiers, const size_t *cert_lens);
 // the key-level batch rule of fgv_block_validate_impl over whole blocks (a group's device ranges
 // together): FGV_EUNSUPPORTED when a block may change the parameter of a key a later block writes
 int fgv_block_kl_check(fgv_block_state *S, size_t nblocks, const uint8_t *const *blocks, const size_t *lens);

@@ -438,6 +438,8 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
   struct Reg {
     size_t i;
     fgv_identity_info info;
+    const std::vector<std::string> *ous;  // GetOrganizationalUnits: the subject OUs ...
+    Dig certifier;                        // ... each with the chain above the identity
   };
   std::vector<Reg> regs;
   for (size_t k = 0; k < pend.size(); k++) {
@@ -452,7 +454,7 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
       continue;
     }
     const MspModel &m = *p.m;
-    Reg g{p.i, fgv_identity_info{}};
+    Reg g{p.i, fgv_identity_info{}, &p.c.ous, p.m->cas[p.p1].chain_id};
     const Dig dg = sha(raw2);
     memcpy(g.info.id_digest, dg.data(), 32);
     // Validate: the issuer must be a leaf of the certification tree (its SKI exists: setup),
@@ -507,7 +509,19 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
   size_t kq = 0, nreg = 0;
   for (const Reg &g : regs) {
     const int32_t slot = g.info.key_type == FGV_KEY_P256 ? (int32_t)kslots[kq++] : -1;
-    if (fgv_block_add_identity(c->blk, ser[g.i], lens[g.i], slot, &g.info) == FGV_OK) nreg++;
+    if (fgv_block_add_identity(c->blk, ser[g.i], lens[g.i], slot, &g.info) == FGV_OK) {
+      nreg++;
+      std::vector<const char *> op;
+      std::vector<size_t> ol, cl;
+      std::vector<const uint8_t *> cp;
+      for (const std::string &o : *g.ous) {
+        op.push_back(o.data());
+        ol.push_back(o.size());
+        cp.push_back(g.certifier.data());
+        cl.push_back(g.certifier.size());
+      }
+      fgv_block_identity_ous(c->blk, ser[g.i], lens[g.i], op.size(), op.data(), ol.data(), cp.data(), cl.data());
+    }
     status[g.i] = FGV_RESOLVE_OK;
   }
   for (size_t i : undeser) {

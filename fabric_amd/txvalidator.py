@@ -20,7 +20,8 @@ from ._lib import CC_COLLECTIONS_KNOWN, CC_KEY_LEVEL_EP, Engine, Unsupported  # 
 class Identity:
     """What the peer's MSP layer knows of one SerializedIdentity (fgv_identity_info):
     key "p256" | "p384" | "other" | "undeserializable"; hash_family of its MSP; roles: bit r set
-    iff msp.SatisfiesPrincipal(id, ROLE{mspid, r}) (None = unknown)."""
+    iff msp.SatisfiesPrincipal(id, ROLE{mspid, r}) (None = unknown); ous: GetOrganizationalUnits
+    as [(OU identifier, certifiers identifier bytes)] (None = unknown)."""
     mspid: str
     pub: Optional[bytes]
     valid: bool
@@ -28,6 +29,7 @@ class Identity:
     key: str = "p256"
     hash_family: str = "SHA2"
     roles: Optional[int] = None
+    ous: Optional[list] = None
 
 
 def _as_identity(entry):
@@ -60,6 +62,8 @@ def setup_channel(engine: Engine, channel: str, identities, chaincodes, committe
     for ser, i in identities:
         engine.msp_register_identity(ser, i.key, i.pub, i.valid, i.id_digest, roles=i.roles,
                                      hash_family=i.hash_family)
+        if getattr(i, "ous", None) is not None:
+            engine.msp_identity_ous(ser, i.ous)
     for ns, d in chaincodes.items():
         if not isinstance(d, dict):
             engine.chaincode_define(ns, d)

@@ -158,8 +158,14 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *ctx, const uint8_t *d_msg_buf, const uint6
  * ChaincodeEndorsedAction) before a later tx's vscc runs.
  * Identities a transaction names that the engine cannot judge exactly -- a certificate of a
  * channel MSP neither registered nor resolvable by the MSP cache-miss path below, a P-384 key, a
- * SHA3 MSP, a role principal for an identity registered without role bits -- make the batch
- * FGV_EUNSUPPORTED (the reference decides). */
+ * SHA3 MSP, a role principal for an identity registered without role bits, an ORGANIZATION_UNIT
+ * principal of its MSP for a valid identity registered without its OUs -- make the batch
+ * FGV_EUNSUPPORTED (the reference decides).
+ * Principals (SatisfiesPrincipal, msp/mspimpl.go:425-660, MSP v1.4.3): ROLE (role bits), IDENTITY
+ * (the same Mspid + Id, and valid; a principal naming a certificate of a channel MSP that was never
+ * registered is resolved by the MSP cache miss like a batch's identities), ORGANIZATION_UNIT
+ * (same MSP, valid, an (OU, certifier) pair of the identity), ANONYMITY (NOMINAL: any identity)
+ * and COMBINED (every principal it collects, in order). */
 #define FGV_KEY_P256 1             /* verified on the GPU                                      */
 #define FGV_KEY_P384 2             /* bccsp verifies it: outside the engine                    */
 #define FGV_KEY_OTHER 3            /* RSA etc.: Verify fails                        */
@@ -186,6 +192,12 @@ int fgv_channel_init(fgv_ctx *ctx, const char *channel_name);
 int fgv_channel_config(fgv_ctx *ctx, const uint8_t *config, size_t len);
 int fgv_msp_declare(fgv_ctx *ctx, const char *mspid);
 int fgv_msp_register_identity(fgv_ctx *ctx, const uint8_t *serialized, size_t len, const fgv_identity_info *info);
+/* identity.GetOrganizationalUnits() of a registered identity (msp/identities.go:121-145): n pairs
+ * (OrganizationalUnitIdentifier, CertifiersIdentifier) for ORGANIZATION_UNIT principals
+ * (msp/mspimpl.go:566-596).  Registering the identity again forgets them; the MSP cache miss sets
+ * them itself.  FGV_ESTATE: the identity is not registered. */
+int fgv_msp_identity_ous(fgv_ctx *ctx, const uint8_t *serialized, size_t len, size_t n, const char *const *ou,
+                         const size_t *ou_lens, const uint8_t *const *certifiers, const size_t *certifier_lens);
 int fgv_chaincode_define2(fgv_ctx *ctx, const char *ns, const char *plugin, const uint8_t *policy, size_t len,
                           uint32_t flags);
 int fgv_collection_define(fgv_ctx *ctx, const char *ns, const char *collection, const uint8_t *policy,

@@ -209,7 +209,7 @@ class MSP:
             if valid and self.node_ous and self._has(role, c):
                 roles |= 1 << role
         key = {"p256": KEY_P256, "p384": KEY_P384}.get(c["key"], KEY_OTHER)
-        return Ident(self.name, c["pub"] if key == KEY_P256 else None, valid, digest, key=key, roles=roles)
+        return Ident(self.name, c["pub"] if key == KEY_P256 else None, valid, digest, key=key, roles=roles, ous=ous)
 
     def _has(self, role, c):
         ou = self.role_ou.get(role)

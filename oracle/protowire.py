@@ -129,6 +129,10 @@ S = {
     "NOutOf": {1: ("n", "int32"), 2: ("rules", "rep msg:SignaturePolicy")},
     "MSPPrincipal": {1: ("principal_classification", "enum"), 2: ("principal", "bytes")},
     "MSPRole": {1: ("msp_identifier", "string"), 2: ("role", "enum")},
+    "OrganizationUnit": {1: ("msp_identifier", "string"), 2: ("organizational_unit_identifier", "string"),
+                         3: ("certifiers_identifier", "bytes")},
+    "MSPIdentityAnonymity": {1: ("anonymity_type", "enum")},
+    "CombinedPrincipal": {1: ("principals", "rep msg:MSPPrincipal")},
     # channel configuration (common/configtx.pb.go, common/policies.pb.go, msp/msp_config.pb.go);
     # map<string, V> fields are repeated {key = 1, value = 2} entries
     "Config": {1: ("sequence", "uint64"), 2: ("channel_group", "msg:ConfigGroup")},

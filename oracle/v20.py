@@ -59,9 +59,12 @@ class Ident:
     roles: bit r <=> msp.SatisfiesPrincipal(id, ROLE{mspid, r}) (MEMBER 0, ADMIN 1, CLIENT 2,
     PEER 3, ORDERER 4; msp/mspimpl.go:331-376, 477-660); None = unknown (legacy registration)."""
 
-    def __init__(self, mspid, pub, valid, id_digest, key=KEY_P256, hash_family="SHA2", roles=None):
+    def __init__(self, mspid, pub, valid, id_digest, key=KEY_P256, hash_family="SHA2", roles=None, ous=None):
         self.mspid, self.pub, self.valid, self.id_digest = mspid, pub, valid, id_digest
         self.key, self.hash_family, self.roles = key, hash_family, roles
+        # GetOrganizationalUnits (msp/identities.go:121-145): [(OU identifier, certifiers
+        # identifier bytes)], None = unknown (a registration without them)
+        self.ous = None if ous is None else [(o, bytes(c)) for o, c in ous]
 
     @property
     def dedup_key(self):  # identity.GetIdentifier().Mspid + .Id
@@ -127,7 +130,8 @@ class ChannelModel:
         for entry in identities:
             if len(entry) == 2:
                 ser, o = entry  # any object with the Ident fields (e.g. fabric_amd.txvalidator.Identity)
-                ident = Ident(o.mspid, o.pub, o.valid, o.id_digest, key=o.key, hash_family=o.hash_family, roles=o.roles)
+                ident = Ident(o.mspid, o.pub, o.valid, o.id_digest, key=o.key, hash_family=o.hash_family, roles=o.roles,
+                              ous=getattr(o, "ous", None))
             else:
                 ser, mspid, pub, valid, dig = entry
                 ident = Ident(mspid, pub, valid, dig, key=KEY_P256 if pub else KEY_OTHER)
@@ -212,7 +216,9 @@ class ChannelModel:
 # ----------------------------------------------------------------- policies
 
 def _compile(rule, principals):
-    """cauthdsl.compile (common/cauthdsl/cauthdsl.go:24-92); returns closure or raises ValueError."""
+    """cauthdsl.compile (common/cauthdsl/cauthdsl.go:24-92); returns closure or raises ValueError.
+    A SignedBy whose principal cannot be decided for an identity makes the evaluation Unsupported
+    (the greedy choice depends on it)."""
     if rule is None:
         raise ValueError("Empty policy element")
     if "n_out_of" in rule:
@@ -239,7 +245,10 @@ def _compile(rule, principals):
             for i, ident in enumerate(ids):
                 if used[i]:
                     continue
-                if _satisfies(ident, pr):
+                v = _satisfies(ident, pr)
+                if v is None:
+                    raise Unsupported("a principal the engine cannot decide for this identity")
+                if v:
                     used[i] = True
                     return True
             return False
@@ -247,29 +256,91 @@ def _compile(rule, principals):
     raise ValueError("Unknown type")
 
 
-def _principal(p):
-    cls = p.get("principal_classification", 0)
-    if cls != 0:
-        raise Unsupported("principal classification %d" % cls)
+_NEVER_LEAF = ("never",)
+
+
+def _leaves(model, cls, body, depth=0):
+    """collectPrincipals (msp/mspimpl.go:440-471) + each leaf, for MSP v1.4.3: a COMBINED that
+    does not decode or holds no principal is an error for every identity (a "never" leaf)."""
+    if cls == 4:  # COMBINED
+        if depth > 16:
+            raise Unsupported("combined principals nested deeper than the engine's bound")
+        try:
+            cp = decode("CombinedPrincipal", body)
+        except DecodeError:
+            return [_NEVER_LEAF]
+        prs = cp.get("principals", [])
+        if not prs:
+            return [_NEVER_LEAF]
+        out = []
+        for q in prs:
+            out += _leaves(model, q.get("principal_classification", 0), q.get("principal") or b"", depth + 1)
+        return out
     try:
-        role = decode("MSPRole", p.get("principal") or b"")
+        if cls == 0:  # ROLE
+            role = decode("MSPRole", body)
+            r = role.get("role", 0)
+            if not 0 <= r <= 4:
+                return [_NEVER_LEAF]  # "invalid MSP role type"
+            return [("role", role.get("msp_identifier", ""), r)]
+        if cls == 1:  # ORGANIZATION_UNIT
+            ou = decode("OrganizationUnit", body)
+            return [("ou", ou.get("msp_identifier", ""), ou.get("organizational_unit_identifier", ""),
+                     ou.get("certifiers_identifier") or b"")]
+        if cls == 2:  # IDENTITY: deserialized by the identity's MSP when a signer is checked
+            return [("identity", body, model)]
+        if cls == 3:  # ANONYMITY
+            an = decode("MSPIdentityAnonymity", body)
+            return [("nominal",)] if an.get("anonymity_type", 0) == 0 else [_NEVER_LEAF]
     except DecodeError:
-        return ("bad", None, 0)
-    return ("role", role.get("msp_identifier", ""), role.get("role", 0))
+        return [_NEVER_LEAF]
+    return [_NEVER_LEAF]  # "invalid principal type"
 
 
-def _satisfies(ident, pr):
-    """bccspmsp.satisfiesPrincipalInternalV142 / V13 / PreV13 for ROLE principals
-    (msp/mspimpl.go:477-660): same MSP, then MEMBER = Validate, other roles from the identity's
-    role bits (NodeOU classification / admin list, computed by the MSP layer)."""
-    kind, mspid, role = pr
-    if kind != "role" or ident.mspid != mspid:
-        return False
-    if role == 0:
-        return ident.valid
-    if ident.roles is None:
-        raise Unsupported("role principal %d needs the identity's role bits" % role)
-    return bool((ident.roles >> role) & 1) if 0 <= role < 32 else False
+def _principal(p, model=None):
+    return _leaves(model, p.get("principal_classification", 0), p.get("principal") or b"")
+
+
+def _leaf_sat(ident, leaf):
+    """one leaf of SatisfiesPrincipal (mspimpl.go:477-660): True / False / None (undecided)"""
+    kind = leaf[0]
+    if kind == "role":  # same MSP; MEMBER = Validate, other roles from the role bits
+        _, mspid, role = leaf
+        if ident.mspid != mspid:
+            return False
+        if role == 0:
+            return ident.valid
+        if ident.roles is None:
+            raise Unsupported("role principal %d needs the identity's role bits" % role)
+        return bool((ident.roles >> role) & 1)
+    if kind == "identity":  # the same sanitized certificate (Mspid + Id), then Validate
+        _, body, model = leaf
+        try:
+            p = model.deserialize(body)
+        except Unsupported:
+            return None
+        return p is not None and p.dedup_key == ident.dedup_key and ident.valid
+    if kind == "ou":  # same MSP, Validate, then an (OU, certifier) pair of the identity
+        _, mspid, ou, cert = leaf
+        if ident.mspid != mspid or not ident.valid:
+            return False
+        if ident.ous is None:
+            return None
+        return (ou, cert) in ident.ous
+    return kind == "nominal"
+
+
+def _satisfies(ident, leaves):
+    """SatisfiesPrincipal: the collected leaves in order, the first error decides; True / False /
+    None (undecided: some leaf unknown and none failing)"""
+    r = True
+    for leaf in leaves:
+        v = _leaf_sat(ident, leaf)
+        if v is False:
+            return False
+        if v is None:
+            r = None
+    return r
 
 
 def signature_set_to_valid_identities(model, sigset):
@@ -290,14 +361,14 @@ def signature_set_to_valid_identities(model, sigset):
 
 def _eval_spe(model, spe, sigset):
     """cauthdsl policy.EvaluateSignedData (common/cauthdsl/policy.go:86-108)"""
-    principals = [_principal(p) for p in spe.get("identities", [])]
+    principals = [_principal(p, model) for p in spe.get("identities", [])]
     try:
         ev = _compile(spe.get("rule"), principals)
     except ValueError:
         return False
     ids = signature_set_to_valid_identities(model, sigset)
     # a role principal needs every candidate's role bits (the engine checks this up front)
-    if any(k == "role" and r != 0 for k, _, r in principals) and any(i.roles is None for i in ids):
+    if any(lf[0] == "role" and lf[2] != 0 for pr in principals for lf in pr) and any(i.roles is None for i in ids):
         raise Unsupported("role principal needs the identities' role bits")
     return ev(ids, [False] * len(ids))
 
