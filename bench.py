@@ -37,11 +37,10 @@ import torch
 import torch.distributed as dist
 
 METRIC = "ECDSA-P256 verifies/sec + validated tx/sec per block at 1/2/4/8 MI355X"
-# 32x32->64 multiply-add products per verify in the comb: ~42.5 terms (16 signed
-# 16-bit generator windows + their carry window, nonzero about every other verify, + 26 signed
-# 10-bit key windows), the first one loaded, so 41 mixed additions (rounded down) x (8 field
-# mults x 64 + 3 squarings x 36 products) + the projective x-check (3 x 64)
-PRODUCTS_POINT = 41 * (8 * 64 + 3 * 36) + 3 * 64
+# 32x32->64 multiply-add products per verify in the comb: 32 terms (12 signed
+# 22-bit generator windows + 20 signed 13-bit key windows), the first one loaded, so 31 mixed
+# additions x (8 field mults x 64 + 3 squarings x 36 products) + the projective x-check (3 x 64)
+PRODUCTS_POINT = 31 * (8 * 64 + 3 * 36) + 3 * 64
 # chip-wide v_mad_u64_u32 issue rate measured by tools/valu_peak.hip (profiles/round1_valu_peak.json)
 PEAK_MAD_PER_S = float(os.environ.get("FGV_PEAK_MAD", "3.106e13"))
 # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz simple int32 VALU lane-ops
@@ -455,7 +454,7 @@ def run_block(args, world, rank, local, dev_fn):
         pb.close()
 
     # live (timed region): the kernels whose bracketing events order the streams anyway
-    LIVE = ("k_bd_sha_payload", "k_bd_parse", "k_bd_sha", "k_bd_ident+count")
+    LIVE = ("k_bd_sha_payload", "k_bd_parse", "k_bd_sha", "k_bd_ident+count", "k_point28")
     kavg = {k: round(v / K, 4) if k in LIVE else round(kdiag[k], 4) for k, v in kern.items()}
     out = dict(metric=METRIC, value=round(total_tx / el, 1), unit="validated tx/s", n_gpus=world, steps=K,
                warmup=args.warmup, ms_per_step=round(el / K * 1e3, 3), higher_is_better=True, scaling="weak",

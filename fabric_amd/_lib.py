@@ -32,7 +32,7 @@ EXPORTED = [
     "fgv_validate_blocks_pipelined", "fgv_set_timing",
     "fgv_group_init", "fgv_group_destroy", "fgv_group_size", "fgv_group_ctx", "fgv_group_validate_blocks",
     "fgv_msp_resolve", "fgv_msp_resolve_blocks", "fgv_set_auto_resolve", "fgv_msp_identity",
-    "fgv_kvmeta_set", "fgv_kvmeta_count", "fgv_kvmeta_get", "fgv_msp_identity_ous",
+    "fgv_kvmeta_set", "fgv_kvmeta_count", "fgv_kvmeta_get", "fgv_msp_identity_ous", "fgv_group_p256_verify_msgs",
 ]
 # fgv_msp_resolve status (include/fgv.h)
 RESOLVE_KNOWN, RESOLVE_OK, RESOLVE_FAILED, RESOLVE_UNSUPPORTED, RESOLVE_REPEAT = range(5)
@@ -130,6 +130,7 @@ def load():
         L.fgv_channel_config.argtypes = [vp, ctypes.c_char_p, sz]
         L.fgv_msp_declare.argtypes = [vp, ctypes.c_char_p]
         L.fgv_msp_register_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(IdentityInfo)]
+        L.fgv_group_p256_verify_msgs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
         L.fgv_msp_identity_ous.argtypes = [vp, ctypes.c_char_p, sz, sz, vp, vp, vp, vp]
         L.fgv_ledger_add_txids.argtypes = [vp, vp, vp, vp, sz]
         L.fgv_validate_blocks.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp]
@@ -303,7 +304,7 @@ class Group:
     """fgv_group: several GPUs driven from one process.  .engines[i] is device i's context
     (set each one up like an Engine: txvalidator.setup_channel(...) on every one)."""
 
-    def __init__(self, devices, key_slots: int = 4096, host_threads: int = 0):
+    def __init__(self, devices, key_slots: int = 0, host_threads: int = 0):
         self._L = load()
         arr = (ctypes.c_int * len(devices))(*devices)
         cfg = _Config(devices[0], key_slots, host_threads)
@@ -328,6 +329,18 @@ class Group:
             o += ntx[i]
         return out
 
+    def verify_msgs(self, keys, msgs, sigs):
+        """fgv_group_p256_verify_msgs: Engine.verify_msgs over the group's devices"""
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        marena, moffs, mlens = pack(msgs) if isinstance(msgs, list) else msgs
+        sarena, soffs, slens = pack(sigs) if isinstance(sigs, list) else sigs
+        n = len(soffs)
+        st = np.zeros(n, dtype=np.uint8)
+        _check(self._L.fgv_group_p256_verify_msgs(self._g, _ptr(keys), _ptr(marena), marena.size, _ptr(moffs),
+                                                  _ptr(mlens), _ptr(sarena), sarena.size, _ptr(soffs), _ptr(slens),
+                                                  n, _ptr(st)))
+        return st
+
     def close(self):
         if getattr(self, "_g", None):
             for e in self.engines:
@@ -345,7 +358,7 @@ class Group:
 class Engine:
     """One libfgv context = one GPU (one process per GPU)."""
 
-    def __init__(self, device: int = 0, key_slots: int = 4096, host_threads: int = 0):
+    def __init__(self, device: int = 0, key_slots: int = 0, host_threads: int = 0):
         """host_threads: fgv_config.host_threads (0 = the library default, 24); the
         FGV_HOST_THREADS environment variable sets it when the argument is 0"""
         self._L = load()

@@ -1069,6 +1069,172 @@ DEV void bd_sha_body(uint32_t ntx, const DevTx *__restrict__ txs, const uint64_t
   for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
   if (lane == 0 && blocks) atomicAdd(nblk_out, (unsigned long long)blocks);
 }
+// ---- the same hashes, each lane's chain split over two waves of a workgroup on two SIMDs
+// (k_bd_sha_payload's scheme): wave 1 (schedule) walks the lanes' segments exactly as
+// bd_sha_body does, fetches each step's block one step ahead, expands the message schedule and
+// writes KW[t] = W[t] + K[t] to LDS (double-buffered, [t/4][lane] x 16 B); wave 0 (rounds) runs
+// the 64 rounds from LDS, takes the midstate, writes the digests.  One barrier per step; both
+// waves run the same number of steps: a lane's last step is max(full blocks, H) + tail blocks.
+DEV uint32_t lane_steps(const DevTx &R, const uint8_t *base, uint32_t r, uint32_t H, bool live_t, bool live_p,
+                        bool live_i, uint32_t nE) {
+  uint32_t pos = 0;
+  for (uint32_t s = 0;; s++) {
+    const ShaSeg g = lane_seg(R, base, r, s, H, live_t, live_p, live_i, nE);
+    if (!g.ok) return pos;
+    if (g.mid && pos < H) pos = H;
+    pos += g.nblk - g.b0;
+  }
+}
+
+DEV void bd_sha_split_body(uint32_t ntx, const DevTx *__restrict__ txs, const uint64_t *__restrict__ bases,
+                           uint8_t *__restrict__ dig, unsigned long long *__restrict__ nblk_out) {
+  __shared__ uint4 KW[2][16][64];  // [buffer][t / 4][lane]
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool sched = threadIdx.x >= 64;  // wave-uniform
+  const uint32_t grp = lane / SHA_GROUP, r = lane - grp * SHA_GROUP;
+  const uint32_t t = blockIdx.x * SHA_GPW + grp;
+  const bool in = grp < SHA_GPW && t < ntx;
+  uint32_t H = 0, nE = 0, nsteps = 0;
+  bool live_t = false, live_p = false, live_i = false;
+  const uint8_t *base = nullptr;
+  ShaSeg g;
+  g.ok = false;
+  if (in) {
+    const DevTx &R = txs[t];
+    base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
+    const bool live = R.pre == C_PENDING;
+    live_t = live && R.type == 3;
+    live_p = live_t && R.etx == C_VALID;
+    live_i = (R.flags & BDF_INDEX_OK) && !(R.flags & BDF_INDEX_FROM_TXID);
+    nE = (live_p && R.disp == C_VALID) ? R.nend : 0u;
+    H = R.prp.len / 64;
+    g = lane_seg(R, base, r, 0, H, live_t, live_p, live_i, nE);
+    nsteps = lane_steps(R, base, r, H, live_t, live_p, live_i, nE);
+  }
+  uint32_t maxs = nsteps;
+  for (int off = 32; off > 0; off >>= 1) maxs = max(maxs, (uint32_t)__shfl_xor((int)maxs, off));
+  uint32_t s = 0, blk = g.ok ? g.b0 : 0;
+  if (sched) {
+    // ---- schedule wave
+    uint32_t raw[17], sh = 0;
+    bool fast = false;
+    if (g.ok) seg_fetch(g, blk, raw, sh, fast);
+    auto produce = [&](uint32_t step) {
+      if (!g.ok || (g.mid && step < H)) return;
+      uint32_t w[16];
+      if (fast) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh));
+      } else {
+        seg_block_slow(g, blk, w);
+      }
+      ShaSeg gn = g;
+      uint32_t bn = blk + 1;
+      if (bn >= g.nblk) {
+        gn = lane_seg(txs[t], base, r, s + 1, H, live_t, live_p, live_i, nE);
+        bn = gn.ok ? gn.b0 : 0;
+        s++;
+      }
+      if (gn.ok) seg_fetch(gn, bn, raw, sh, fast);
+      g = gn;
+      blk = bn;
+      uint4 *o = &KW[step & 1][0][lane];
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        uint32_t kw[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int i = 4 * q + j;
+          uint32_t wi;
+          if (i < 16) {
+            wi = w[i];
+          } else {
+            const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+            w[i & 15] = wi;
+          }
+          kw[j] = wi + SHA_K[i];
+        }
+        o[q * 64] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+      }
+    };
+    if (maxs) produce(0);
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t step = 0; step < maxs; step++) {
+      if (step + 1 < maxs) produce(step + 1);
+      __syncthreads();
+    }
+    return;
+  }
+  // ---- rounds wave
+  const uint32_t IV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint32_t h[8], mid[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) h[k] = mid[k] = IV[k];
+  uint64_t blocks = 0;
+  const int src = (int)(grp * SHA_GROUP);  // lane 0 of the group
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t step = 0; step < maxs; step++) {
+    // the midstate: lane 0's state after its first H blocks (every lane runs the reads)
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t v = (uint32_t)__shfl((int)h[k], src);
+      if (step == H) mid[k] = v;
+    }
+    if (g.ok && !(g.mid && step < H)) {
+      if (blk == g.b0 && g.mid) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) h[k] = mid[k];
+      }
+      const uint4 *in4 = &KW[step & 1][0][lane];
+      uint32_t a = h[0], bb = h[1], c = h[2], d = h[3], e = h[4], f = h[5], gg = h[6], k = h[7];
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const uint4 x = in4[q * 64];
+        const uint32_t kw4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+          const uint32_t ch = (e & f) ^ (~e & gg);
+          const uint32_t t1 = k + S1 + ch + kw4[j];
+          const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+          const uint32_t mj = (a & bb) | (c & (a | bb));
+          k = gg; gg = f; f = e; e = d + t1; d = c; c = bb; bb = a; a = t1 + S0 + mj;
+        }
+      }
+      h[0] += a; h[1] += bb; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += gg; h[7] += k;
+      blocks++;
+      uint32_t bn = blk + 1;
+      if (bn >= g.nblk) {
+        uint32_t *o = reinterpret_cast<uint32_t *>(dig + ((size_t)g.slot * ntx + t) * 32);
+#pragma unroll
+        for (int q = 0; q < 8; q++) o[q] = __builtin_bswap32(h[q]);
+        g = lane_seg(txs[t], base, r, s + 1, H, live_t, live_p, live_i, nE);
+        s++;
+        bn = g.ok ? g.b0 : 0;
+        if (g.ok && !g.mid) {  // (a tail takes the midstate at its first block)
+#pragma unroll
+          for (int q = 0; q < 8; q++) h[q] = IV[q];
+        }
+      }
+      blk = bn;
+    }
+    __syncthreads();
+  }
+  for (int off = 32; off > 0; off >>= 1) blocks += __shfl_down(blocks, off);
+  if (lane == 0 && blocks) atomicAdd(nblk_out, (unsigned long long)blocks);
+}
+__global__ __launch_bounds__(128) void k_bd_sha2(uint32_t ntx, const DevTx *__restrict__ txs,
+                                                 const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
+                                                 unsigned long long *__restrict__ nblk_out) {
+  __builtin_amdgcn_s_setprio(1);
+  bd_sha_split_body(ntx, txs, bases, dig, nblk_out);
+}
+
 // k_prep waits for these digests and for the parse -> identities -> counts -> emit -> der ->
 // inv chain: the wave priority decides which of the two finishes first (FGV_SHA_PRIO A/B)
 __global__ __launch_bounds__(64) void k_bd_sha(uint32_t ntx, const DevTx *__restrict__ txs,

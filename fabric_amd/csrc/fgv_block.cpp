@@ -1632,6 +1632,7 @@ __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
 __global__ void k_bd_sha(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
+__global__ void k_bd_sha2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
 __global__ void k_bd_sha_p2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig,
                             unsigned long long *nblk);
 __global__ void k_bd_sha_p3(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig,
@@ -1836,9 +1837,22 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     const char *e = getenv("FGV_SHA_PRIO");
     return e ? atoi(e) : 1;
   }();
-  hipLaunchKernelGGL(sha_prio == 3 ? k_bd_sha_p3 : sha_prio == 2 ? k_bd_sha_p2 : k_bd_sha,
-                     dim3((N + SHA_GPW - 1) / SHA_GPW), dim3(64), 0,
-                     c->stream3, N, dtx, dbs, B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 6));
+  // FGV_SHA_SPLIT=1: the two-wave k_bd_sha2 (schedule wave + rounds wave per chain).  Measured
+  // on MI355X with the next batch's front half ahead (profiles/round3_ab/split*): 0.678-0.688 ms
+  // per C2 step vs 0.666-0.673 for the one-wave kernel -- beside the other batch's kernels the
+  // extra waves and the 32 KB of LDS per workgroup cost more than the shorter chain gains -- so
+  // the one-wave kernel is the default.
+  static const bool sha_split = [] {
+    const char *e = getenv("FGV_SHA_SPLIT");
+    return e && atoi(e) != 0;
+  }();
+  if (sha_split)
+    hipLaunchKernelGGL(k_bd_sha2, dim3((N + SHA_GPW - 1) / SHA_GPW), dim3(128), 0, c->stream3, N, dtx, dbs,
+                       B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 6));
+  else
+    hipLaunchKernelGGL(sha_prio == 3 ? k_bd_sha_p3 : sha_prio == 2 ? k_bd_sha_p2 : k_bd_sha,
+                       dim3((N + SHA_GPW - 1) / SHA_GPW), dim3(64), 0,
+                       c->stream3, N, dtx, dbs, B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 6));
   HIP_TRY(hipEventRecord(B.ev[2], c->stream3));
   HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[1], 0));
   HIP_TRY(hipEventRecord(B.ev[8], c->stream3));
@@ -2023,7 +2037,7 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
     c->t_kern[4] = tim ? el(c->kev[6], c->kev[7]) : 0.0;                     // k_bd_emit
     c->t_kern[5] = tim && c->stage_ran ? el(c->ev[2], c->ev[3]) : 0.0;  // k_der + k_inv
     c->t_kern[6] = tim && c->stage_ran ? el(c->ev[4], c->ev[5]) : 0.0;  // k_prep
-    c->t_kern[7] = tim && c->stage_ran ? el(c->ev[5], c->ev[6]) : 0.0;  // k_point28 (+ k_point hand-overs)
+    c->t_kern[7] = c->stage_ran ? el(c->ev[5], c->ev[6]) : 0.0;  // k_point28 (+ k_point hand-overs), live
     c->t_kern[8] = tim ? el(c->kev[8], c->kev[9]) : 0.0;               // k_bd_fold
     c->t_kern[9] = tim ? el(B.ev[0], c->kev[9]) : 0.0;                 // the batch, head upload to fold
     c->t_sha = std::max(c->t_kern[0], el(B.ev[3], B.ev[2]));

@@ -97,30 +97,58 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
   if (nblocks == 0) return FGV_OK;
   std::lock_guard<std::mutex> lk(g->mu);
   const size_t W = g->ctx.size();
-  // the block plan: contiguous ranges of about total/W bytes (a device may get none)
-  size_t total = 0;
-  for (size_t b = 0; b < nblocks; b++) total += lens[b];
+  // The plan.  At least as many blocks as devices: contiguous block ranges of about total/W
+  // bytes (a device stages, splits and parses only its own).  Fewer (one block, a short batch):
+  // contiguous ranges of the batch's transactions, block-major (shard by
+  // transaction index) -- every device stages the blocks its range touches and parses its rows.
+  const bool by_tx = nblocks < W;
   std::vector<size_t> b0(W + 1, nblocks);
-  b0[0] = 0;
-  {
+  std::vector<uint32_t> lo(W * nblocks, FGV_SHARD_SKIP), hi(W * nblocks, FGV_SHARD_SKIP);
+  std::vector<size_t> cap(W, 0), nrec(W, 0);
+  if (by_tx) {
+    std::vector<size_t> nt(nblocks);
+    size_t total = 0;
+    for (size_t b = 0; b < nblocks; b++) {
+      const long k = fgv_block_count_txs(blocks[b], lens[b]);
+      if (k < 0) return FGV_EINVAL;
+      nt[b] = (size_t)k;
+      total += nt[b];
+    }
+    for (size_t r = 0; r < W; r++) {
+      const size_t a = total * r / W, e = total * (r + 1) / W;
+      size_t base = 0;
+      for (size_t b = 0; b < nblocks; b++) {
+        const size_t x = std::max(a, base), y = std::min(e, base + nt[b]);
+        if (x < y) {
+          lo[r * nblocks + b] = (uint32_t)(x - base);
+          hi[r * nblocks + b] = (uint32_t)(y - base);
+          nrec[r] += y - x;
+        }
+        base += nt[b];
+      }
+      cap[r] = nrec[r];
+    }
+  } else {
+    size_t total = 0;
+    for (size_t b = 0; b < nblocks; b++) total += lens[b];
+    b0[0] = 0;
     size_t acc = 0, r = 1;
     for (size_t b = 0; b < nblocks && r < W; b++) {
       acc += lens[b];
       while (r < W && acc * W >= total * r) b0[r++] = b + 1;
     }
-  }
-  // records per device are bounded by its blocks' bytes (an envelope takes >= 2 bytes) and
-  // by flags_cap
-  std::vector<size_t> cap(W, 0);
-  for (size_t r = 0; r < W; r++) {
-    size_t bytes = 0;
-    for (size_t b = b0[r]; b < b0[r + 1]; b++) bytes += lens[b];
-    cap[r] = std::min(flags_cap, bytes / 2 + (b0[r + 1] - b0[r]));
+    // records per device are bounded by its blocks' bytes (an envelope takes >= 2 bytes) and
+    // by flags_cap
+    for (size_t q = 0; q < W; q++) {
+      size_t bytes = 0;
+      for (size_t b = b0[q]; b < b0[q + 1]; b++) bytes += lens[b];
+      cap[q] = std::min(flags_cap, bytes / 2 + (b0[q + 1] - b0[q]));
+    }
   }
   std::vector<int> rcs(W, FGV_OK);
+  std::vector<std::vector<size_t>> ntx_dev(W, std::vector<size_t>(nblocks, 0));
   g->pool->run(W, [&](size_t r) {
-    const size_t nb = b0[r + 1] - b0[r];
-    if (nb == 0) return;
+    if (by_tx ? nrec[r] == 0 : b0[r + 1] == b0[r]) return;
     if (hipSetDevice(g->dev[r]) != hipSuccess) {
       rcs[r] = FGV_EDEVICE;
       return;
@@ -130,8 +158,12 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
       return;
     }
     // (an identity this device's registry has not seen is resolved inside, MSP cache miss)
-    rcs[r] = fgv_validate_shard_dev(g->ctx[r], nb, blocks + b0[r], lens + b0[r], nullptr, nullptr, nullptr,
-                                    g->res[r].p, cap[r], ntx + b0[r]);
+    if (by_tx)
+      rcs[r] = fgv_validate_shard_dev(g->ctx[r], nblocks, blocks, lens, nullptr, &lo[r * nblocks], &hi[r * nblocks],
+                                      g->res[r].p, cap[r], ntx_dev[r].data());
+    else
+      rcs[r] = fgv_validate_shard_dev(g->ctx[r], b0[r + 1] - b0[r], blocks + b0[r], lens + b0[r], nullptr, nullptr,
+                                      nullptr, g->res[r].p, cap[r], ntx + b0[r]);
   });
   int unsup = 0;
   for (int rc : rcs) {
@@ -139,18 +171,29 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
     else if (rc) return rc;
   }
   if (unsup) return FGV_EUNSUPPORTED;
-  // a device whose blocks may change key-level state while a later device's blocks were
-  // validated against the state before them (fgv_block_validate_impl's batch rule across devices)
-  for (size_t r = 0; r + 1 < W; r++)
-    if (b0[r + 1] > b0[r] && b0[r + 1] < nblocks && g->ctx[r]->kl_changes) {
-      const int rc = fgv_block_kl_check(g->ctx[0]->blk, nblocks, blocks, lens);  // (the whole batch, host)
-      if (rc) return rc;
-      break;
+  if (by_tx) {
+    for (size_t b = 0; b < nblocks; b++) {  // (every device with rows saw the full counts)
+      ntx[b] = 0;
+      for (size_t r = 0; r < W; r++) ntx[b] = std::max(ntx[b], ntx_dev[r][b]);
     }
+  } else {
+    // a device whose blocks may change key-level state while a later device's blocks were
+    // validated against the state before them (fgv_block_validate_impl's batch rule across devices)
+    for (size_t r = 0; r + 1 < W; r++)
+      if (b0[r + 1] > b0[r] && b0[r + 1] < nblocks && g->ctx[r]->kl_changes) {
+        const int rc = fgv_block_kl_check(g->ctx[0]->blk, nblocks, blocks, lens);  // (the whole batch, host)
+        if (rc) return rc;
+        break;
+      }
+    for (size_t r = 0; r < W; r++)
+      for (size_t b = b0[r]; b < b0[r + 1]; b++) {
+        lo[r * nblocks + b] = 0;
+        hi[r * nblocks + b] = (uint32_t)ntx[b];
+        nrec[r] += ntx[b];
+      }
+  }
   size_t all = 0, rows = 0;
-  std::vector<size_t> nrec(W, 0);
   for (size_t r = 0; r < W; r++) {
-    for (size_t b = b0[r]; b < b0[r + 1]; b++) nrec[r] += ntx[b];
     rows = std::max(rows, nrec[r]);
     all += nrec[r];
   }
@@ -166,13 +209,46 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
                                nrec[r] * sizeof(fgv_tx_result), g->s0));
   }
   HIP_TRY(hipStreamSynchronize(g->s0));
-  std::vector<uint32_t> lo(W * nblocks, FGV_SHARD_SKIP), hi(W * nblocks, FGV_SHARD_SKIP);
-  for (size_t r = 0; r < W; r++)
-    for (size_t b = b0[r]; b < b0[r + 1]; b++) {
-      lo[r * nblocks + b] = 0;
-      hi[r * nblocks + b] = (uint32_t)ntx[b];
-    }
   return fgv_finalize_flags_dev_plan(g->ctx[0], nblocks, ntx, (uint32_t)W, rows, lo.data(), hi.data(), dst, flags);
+}
+
+int fgv_group_p256_verify_msgs(fgv_group *g, const uint8_t *keys, const uint8_t *msg_buf, size_t msg_buf_len,
+                               const uint64_t *msg_off, const uint32_t *msg_len, const uint8_t *sig_buf,
+                               size_t sig_buf_len, const uint64_t *sig_off, const uint32_t *sig_len, size_t n,
+                               uint8_t *status) {
+  if (!g || (n && (!keys || !msg_buf || !msg_off || !msg_len || !sig_buf || !sig_off || !sig_len || !status)))
+    return FGV_EINVAL;
+  if (n == 0) return FGV_OK;
+  std::lock_guard<std::mutex> lk(g->mu);
+  const size_t W = g->ctx.size();
+  std::vector<int> rcs(W, FGV_OK);
+  // item ranges [n r / W, n (r+1) / W); each device gets the byte spans its items reference
+  // (rebased offsets), verifies them with its own key cache and writes its slice of `status`
+  g->pool->run(W, [&](size_t r) {
+    const size_t a = n * r / W, e = n * (r + 1) / W;
+    if (a == e) return;
+    uint64_t m0 = UINT64_MAX, m1 = 0, s0 = UINT64_MAX, s1 = 0;
+    for (size_t i = a; i < e; i++) {
+      if (msg_off[i] + msg_len[i] > msg_buf_len || sig_off[i] + sig_len[i] > sig_buf_len) {
+        rcs[r] = FGV_EINVAL;
+        return;
+      }
+      m0 = std::min<uint64_t>(m0, msg_off[i]);
+      m1 = std::max<uint64_t>(m1, msg_off[i] + msg_len[i]);
+      s0 = std::min<uint64_t>(s0, sig_off[i]);
+      s1 = std::max<uint64_t>(s1, sig_off[i] + sig_len[i]);
+    }
+    std::vector<uint64_t> mo(e - a), so(e - a);
+    for (size_t i = a; i < e; i++) {
+      mo[i - a] = msg_off[i] - m0;
+      so[i - a] = sig_off[i] - s0;
+    }
+    rcs[r] = fgv_p256_verify_msgs(g->ctx[r], keys + 64 * a, msg_buf + m0, m1 - m0, mo.data(), msg_len + a,
+                                  sig_buf + s0, s1 - s0, so.data(), sig_len + a, e - a, status + a);
+  });
+  for (int rc : rcs)
+    if (rc) return rc;
+  return FGV_OK;
 }
 
 }  // extern "C"

@@ -66,7 +66,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   fgv_ctx *c = new (std::nothrow) fgv_ctx();
   if (!c) return FGV_ENOMEM;
   c->device = cfg ? cfg->device : 0;
-  c->key_slots = (cfg && cfg->key_slots) ? cfg->key_slots : 4096;
+  c->key_slots = (cfg && cfg->key_slots) ? cfg->key_slots : 2048;
   // host workers: fgv_config.host_threads, else min(24, this process's CPU share) -- 24 measured
   // best on a whole machine (tools/sweep_threads.sh); eight ranks on one node each get their
   // affinity mask's share, not the whole machine
@@ -115,17 +115,21 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
       return fail(FGV_EDEVICE);
     c->n_cu = (uint32_t)ncu;
   }
-  if (!c->gtab.ensure(GT_BYTES) || !c->g_ok.ensure(16) || !c->gtab28.ensure(GT_BYTES) || !c->redo.ensure(64) ||
-      !c->ktab.ensure((size_t)c->key_slots * KT_BYTES) || !c->ktab28.ensure((size_t)c->key_slots * KT_BYTES) ||
+  if (!c->g_ok.ensure(16) || !c->gtab28.ensure(GT_BYTES) || !c->redo.ensure(64) ||
+      !c->ktab28.ensure((size_t)c->key_slots * KT_BYTES) ||
       !c->key_ok.ensure(c->key_slots))
     return fail(FGV_ENOMEM);
   // generator comb table (k_gtab), built once per context
   {
     DevBuf scr;
-    if (!scr.ensure((size_t)GT_THREADS * GT_CHUNK * sizeof(jpoint_raw))) return fail(FGV_ENOMEM);
-    hipLaunchKernelGGL(k_gtab, dim3((GT_THREADS + 63) / 64), dim3(64), 0, c->stream, c->gtab.as<apoint_raw>(),
-                       c->gtab28.as<apoint_raw>(), scr.as<jpoint_raw>());
-    const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(c->stream) == hipSuccess;
+    if (!scr.ensure((size_t)GT_THREADS_PER_WIN * GT_CHUNK * sizeof(jpoint_raw))) return fail(FGV_ENOMEM);
+    bool ok = true;
+    for (uint32_t w = 0; w < NGWIN && ok; w++) {  // one window per launch (the scratch holds one)
+      hipLaunchKernelGGL(k_gtab, dim3((GT_THREADS_PER_WIN + 63) / 64), dim3(64), 0, c->stream,
+                         c->gtab28.as<apoint_raw>(), scr.as<jpoint_raw>(), w);
+      ok = hipGetLastError() == hipSuccess;
+    }
+    ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
     scr.release();
     if (!ok) return fail(FGV_EDEVICE);
   }
@@ -140,7 +144,7 @@ void fgv_destroy(fgv_ctx *c) {
   for (hipStream_t x : {c->stream2, c->stream3, c->streamF})  // (a front half enqueued ahead)
     if (x) hipStreamSynchronize(x);
   DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
-                 &c->bd_misc, &c->gtab, &c->g_ok, &c->ktab, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
+                 &c->bd_misc, &c->g_ok, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
                  &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
                  &c->bj_dig, &c->bj_vst, &c->blk_arena, &c->fz_meta, &c->fz_rowmap, &c->fz_blkof,
@@ -257,7 +261,8 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
   hipLaunchKernelGGL(k_prep, dim3((N + 255) / 256), dim3(256), 0, c->stream, N, dn, d_status, d_r,
                      c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>(), redo);  // (k_prep zeroes *redo)
   HIP_TRY(hipGetLastError());
-  if (tim || c->ahead_mode == 4) HIP_TRY(hipEventRecord(c->ev[5], c->stream));  // (ahead mode 4 waits on it)
+  // (k_point28's bracket, always: its device time is read live; ahead mode 4 waits on it)
+  HIP_TRY(hipEventRecord(c->ev[5], c->stream));
   // Grid: two POINT_THREADS workgroups per CU (2 waves per SIMD) taking chunks of items from a
   // device counter (k_point*: waves placed late, beside a next batch's front half, take fewer).
   // Lanes per verify L (1, 2, 4, 8):
@@ -287,10 +292,10 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
                        c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   }
   hipLaunchKernelGGL(k_point, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, dn, L, d_status, d_slot,
-                     c->gtab.as<apoint_raw>(), c->ktab.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
+                     c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
   c->last_lanes = L;
   HIP_TRY(hipGetLastError());
-  if (tim || c->ahead_mode == 1) HIP_TRY(hipEventRecord(c->ev[6], c->stream));  // (ahead mode 1 waits on it)
+  HIP_TRY(hipEventRecord(c->ev[6], c->stream));  // (ahead mode 1 waits on it)
   return FGV_OK;
 }
 
@@ -449,7 +454,7 @@ static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, 
       next++;
       j++;
     }
-    int rc = build_tables(c, kq, ks, nk, c->ktab.as<apoint_raw>(), c->ktab28.as<apoint_raw>(),
+    int rc = build_tables(c, kq, ks, nk, nullptr, c->ktab28.as<apoint_raw>(),
                           c->key_ok.as<uint8_t>());
     if (rc) return rc;
     // re-resolve every pending slot (the cache may have been flushed)
@@ -616,7 +621,7 @@ static int keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint3
       be32_to_limbs(fresh[j].data() + 32, kq + 16 * j + 8);
       ks[j] = next + j;
     }
-    int rc = build_tables(c, kq, ks, nk, c->ktab.as<apoint_raw>(), c->ktab28.as<apoint_raw>(),
+    int rc = build_tables(c, kq, ks, nk, nullptr, c->ktab28.as<apoint_raw>(),
                           c->key_ok.as<uint8_t>());
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1064,6 +1069,27 @@ static size_t stage_bytes(size_t nblocks, const size_t *lens) {
   return total;
 }
 
+// H2D copies of a batch into arena A on stream `st`: blocks that lie back to back in host memory
+// (a peer's pinned receive buffer, the bench's batches) travel as ONE copy per run, laid out in
+// the arena exactly as in host memory (a kernel reading past a block's end reads the next one's
+// bytes), each run followed by >= 64 B of padding; the device addresses go to dev[].  Returns the
+// bytes copied.
+static int copy_runs(size_t nblocks, const uint8_t *const *blocks, const size_t *lens, uint8_t *A, hipStream_t st,
+                     const uint8_t **dev, size_t *copied) {
+  size_t o = 0, b = 0;
+  *copied = 0;
+  while (b < nblocks) {
+    size_t e = b + 1, run = lens[b];
+    while (e < nblocks && blocks[e] == blocks[e - 1] + lens[e - 1]) run += lens[e++];
+    if (run) HIP_TRY(hipMemcpyAsync(A + o, blocks[b], run, hipMemcpyHostToDevice, st));
+    for (size_t q = b; q < e; q++) dev[q] = A + o + (size_t)(blocks[q] - blocks[b]);
+    *copied += run;
+    o += (run + 64 + 255) & ~(size_t)255;
+    b = e;
+  }
+  return FGV_OK;
+}
+
 // Host-resident blocks -> device.  A batch that the previous _next call prefetched is already
 // on its way (copy stream): the compute stream waits for that copy instead of copying again.
 static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
@@ -1095,14 +1121,11 @@ static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks
   DevBuf &A = c->stage[slot];
   if (!A.ensure(stage_bytes(nblocks, lens))) return FGV_ENOMEM;
   HIP_TRY(hipStreamWaitEvent(c->stream, c->pf.ev, 0));  // (an abandoned prefetch may still write the other arena)
-  size_t o = 0;
-  for (size_t b = 0; b < nblocks; b++) {
-    HIP_TRY(hipMemcpyAsync(A.as<uint8_t>() + o, blocks[b], lens[b], hipMemcpyHostToDevice, c->stream));
-    dev[b] = A.as<uint8_t>() + o;
-    o += (lens[b] + 64 + 255) & ~(size_t)255;
-  }
+  size_t copied = 0;
+  int rc = copy_runs(nblocks, blocks, lens, A.as<uint8_t>(), c->stream, dev.data(), &copied);
+  if (rc) return rc;
   c->stage_cur = slot;
-  c->h2d_bytes = o;
+  c->h2d_bytes = copied;
   return FGV_OK;
 }
 
@@ -1117,12 +1140,9 @@ static int prefetch_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   c->pf.src.assign(blocks, blocks + nblocks);
   c->pf.lens.assign(lens, lens + nblocks);
   c->pf.dev.resize(nblocks);
-  size_t o = 0;
-  for (size_t b = 0; b < nblocks; b++) {
-    HIP_TRY(hipMemcpyAsync(A.as<uint8_t>() + o, blocks[b], lens[b], hipMemcpyHostToDevice, c->copy_stream));
-    c->pf.dev[b] = A.as<uint8_t>() + o;
-    o += (lens[b] + 64 + 255) & ~(size_t)255;
-  }
+  size_t copied = 0;
+  int rc = copy_runs(nblocks, blocks, lens, A.as<uint8_t>(), c->copy_stream, c->pf.dev.data(), &copied);
+  if (rc) return rc;
   HIP_TRY(hipEventRecord(c->pf.ev, c->copy_stream));
   c->pf.slot = slot;
   c->pf.on = true;

@@ -111,8 +111,8 @@ struct fgv_ctx {
   uint64_t n_pay_blocks = 0;      // SHA-256 compressions of the payload hashes (last block call)
   std::mutex mu;
   // generator table (88 KB) and the public-key table cache
-  DevBuf gtab, g_ok;
-  DevBuf ktab, key_ok;
+  DevBuf g_ok;
+  DevBuf key_ok;
   DevBuf gtab28, ktab28, redo;  // Montgomery-280 copies of the comb tables (k_point28)
   uint32_t key_slots = 0;
   uint32_t pinned = 0;  // slots [0, pinned) hold registered keys and are never evicted

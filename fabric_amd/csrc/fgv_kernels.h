@@ -3,29 +3,33 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Key comb (u2 * Q): 26 windows of 10 bits with signed digits in [-512, 511] (26 x 10 = 260 bits:
-// the top window, bits 250..259 of a scalar < 2^256, absorbs the final carry); 512 entries
-// (|d| = 1..512) per window, 852 KB per key per copy, built by k_keytab (KT_CHUNK entries per thread).
-#define WBITS 10
-#define NWIN 26
-#define TAB_K 512
+// Key comb (u2 * Q): 20 windows of 13 bits with signed digits in [-4096, 4095] (20 x 13 = 260 bits:
+// the top window, bits 247..259 of a scalar < 2^256, absorbs the final carry); 4096 entries
+// (|d| = 1..4096) per window, 5.2 MB per key, one copy in Montgomery-280 form (k_point28; the exact
+// k_point converts an entry with one multiplication), built by k_keytab (KT_CHUNK entries per thread).
+// 13-bit windows: 37 comb terms per verify instead of 43 with 10-bit windows.
+#define WBITS 13
+#define NWIN 20
+#define TAB_K 4096
 #define KT_CHUNK 32
-#define KT_THREADS_PER_KEY (NWIN * (TAB_K / KT_CHUNK))  // 416
-#define KT_BUILD_KEYS 128                                // keys per k_keytab launch (scratch bound)
-#define KT_ENTRIES (NWIN * TAB_K)           // 13,312 affine points per table
-#define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 851,968 bytes per table
-// Generator comb (u1 * G): 16 windows of 16 bits with signed digits in [-2^15, 2^15 - 1], plus
-// a 17th window for the final carry (digit 0 or 1); 32768 entries per window (33.5 MB per copy,
-// MALL / HBM resident, built once per context by k_gtab).  17 G terms instead of 33.
-#define GWBITS 16
-#define NGWIN 17
-#define GT_K 32768
-#define GT_ENTRIES ((NGWIN - 1) * GT_K + 1)
+#define KT_THREADS_PER_KEY (NWIN * (TAB_K / KT_CHUNK))  // 2,560
+#define KT_BUILD_KEYS 32                                 // keys per k_keytab launch (scratch bound)
+#define KT_ENTRIES (NWIN * TAB_K)           // 81,920 affine points per table
+#define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 5,242,880 bytes per table
+// Generator comb (u1 * G): 12 windows of 22 bits with signed digits in [-2^21, 2^21 - 1] (12 x 22
+// = 264 bits: the top window, bits 242..263 of a scalar < 2^256, absorbs the final carry);
+// 2^21 entries per window, 1.61 GB, one copy in Montgomery-280 form (the exact k_point converts
+// an entry with one multiplication), HBM resident, built once per context by k_gtab (one launch
+// per window).  12 G terms instead of 16.5 with 16-bit windows.
+#define GWBITS 22
+#define NGWIN 12
+#define GT_K 2097152
+#define GT_ENTRIES ((size_t)NGWIN * GT_K)
 #define GT_BYTES ((size_t)GT_ENTRIES * 64)
-#define GT_CHUNK 32                   // consecutive entries per k_gtab thread
-#define GT_THREADS ((NGWIN - 1) * (GT_K / GT_CHUNK) + 1)
-#define NTERMS (NGWIN + NWIN)         // comb terms per verify: 17 G + 26 Q
-#define DIG_Q_OFF 40                  // digit array item: G digits int16 x 17 at 0, Q digits int16 x 26 here
+#define GT_CHUNK 32                            // consecutive entries per k_gtab thread
+#define GT_THREADS_PER_WIN (GT_K / GT_CHUNK)   // 65,536 threads per k_gtab launch (one window)
+#define NTERMS (NGWIN + NWIN)         // comb terms per verify: 12 G + 20 Q
+#define DIG_Q_OFF 48                  // digit array item: G digits int32 x 12 at 0, Q digits int16 x 20 here
 #define PREP_B 2                            // items per lane in the batched inversion
 #define POINT_THREADS 256   // 4 waves per workgroup, 2 x n_cu workgroups: 2 waves per SIMD, <= 256 VGPRs
 #define POINT_LANES_MAX 8    // lanes cooperating on one verify in k_point (partial sums + tree)
@@ -45,7 +49,7 @@ struct jpoint_raw {  // key-table build scratch: Jacobian point + prefix product
 
 __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw *tables, apoint_raw *tables28,
                          jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys);
-__global__ void k_gtab(apoint_raw *tables, apoint_raw *tables28, jpoint_raw *scratch);
+__global__ void k_gtab(apoint_raw *tables28, jpoint_raw *scratch, uint32_t w);
 __global__ void k_inv(uint32_t n, const uint32_t *dn, uint8_t *status, const uint32_t *key_slot, const uint8_t *key_ok,
                       const uint32_t *r_limbs, const uint32_t *s_limbs, uint32_t *w_out, uint32_t *w_scratch);
 __global__ void k_prep(uint32_t n, const uint32_t *dn, const uint8_t *status, const uint32_t *r_limbs, const uint32_t *w_in,
@@ -114,10 +118,8 @@ struct BlkSlot {    // keys written in the block
   uint64_t fw_cand[2], fw_valid[2];
   uint64_t last;    // (epoch << 32) | (tx + 1) of the last VALID writer
 };
-__global__ void k_mvx_count(uint32_t ntx, const uint8_t *base, const uint32_t *envtab, const uint8_t *in_flags,
-                            MvTxInfo *info, MvCounters *c);
-__global__ void k_mvx_emit(uint32_t ntx, const uint8_t *base, MvTxInfo *info, MvRec *reads, MvRec *writes,
-                           MvCounters *c);
+__global__ void k_mvx_extract(uint32_t ntx, const uint8_t *base, const uint32_t *envtab, const uint8_t *in_flags,
+                              MvTxInfo *info, MvRec *reads, MvRec *writes, MvCounters *c);
 __global__ void k_mvx_prep(const uint8_t *base, const MvRec *reads, const MvRec *writes, BlkSlot *btbl, uint32_t epoch,
                            uint32_t *wslot, const StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint8_t *bad,
                            const MvCounters *c);

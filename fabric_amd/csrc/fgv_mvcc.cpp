@@ -1025,7 +1025,7 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
       !M->reads.ensure(rcap * sizeof(MvRec)) || !M->writes.ensure(rcap * sizeof(MvRec)) ||
       !M->wslot.ensure(rcap * 4) || !M->rslot.ensure(rcap * 4) || !M->pend.ensure(rcap + 64) ||
       !M->bad.ensure(ntx + 64) || !M->st.ensure(ntx + 64) || !M->tail.ensure(kCounterBytes + ntx + 64) ||
-      !M->htail.ensure(kCounterBytes + ntx + 64))
+      !M->htail.ensure(kCounterBytes + ntx + 64 + 16))
     return FGV_ENOMEM;
   if (bcap > M->btbl_cap) {  // (re)allocated tables start with epoch 0 everywhere
     M->btbl.release();
@@ -1059,11 +1059,11 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   BlkSlot *d_b = M->btbl.as<BlkSlot>();
   uint8_t *d_out = M->tail.as<uint8_t>() + kCounterBytes;
   const uint32_t N = (uint32_t)ntx;
+  const size_t top_off = (kCounterBytes + ntx + 7) & ~(size_t)7;  // (in htail, behind the flags)
   HIP_TRY(hipMemcpyAsync(dh, h, hbytes, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(M->bad.p, 0, ntx, s));
   HIP_TRY(hipEventRecord(c->ev[0], s));
-  hipLaunchKernelGGL(k_mvx_count, dim3((N + 63) / 64), dim3(64), 0, s, N, dblk, d_et, d_in, d_info, d_c);
-  hipLaunchKernelGGL(k_mvx_emit, dim3((N + 63) / 64), dim3(64), 0, s, N, dblk, d_info, d_r, d_w, d_c);
+  hipLaunchKernelGGL(k_mvx_extract, dim3((N + 63) / 64), dim3(64), 0, s, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c);
   hipLaunchKernelGGL(k_mvx_prep, grid_stride(rcap), dim3(256), 0, s, dblk, d_r, d_w, d_b, epoch,
                      M->wslot.as<uint32_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
                      M->bad.as<uint8_t>(), d_c);
@@ -1095,6 +1095,8 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(M->tail.p, d_c, sizeof(MvCounters), hipMemcpyDeviceToDevice, s));
     HIP_TRY(hipMemcpyAsync(M->htail.p, M->tail.p, kCounterBytes + ntx, hipMemcpyDeviceToHost, s));
+    // the arena top after the commit rides on the same synchronisation (no second one)
+    if (commit) HIP_TRY(hipMemcpyAsync(M->htail.as<uint8_t>() + top_off, M->top.p, 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(c->ev[2], s));
     HIP_TRY(hipStreamSynchronize(s));
     return FGV_OK;
@@ -1120,8 +1122,10 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   }
   if (hc->unsup) return FGV_EUNSUPPORTED;  // nothing was committed
   if (commit) {
-    rc = read_top(c, M);
-    if (rc) return rc;
+    uint64_t t[2];
+    memcpy(t, M->htail.as<uint8_t>() + top_off, 16);
+    M->arena_used = t[0];
+    M->nkeys = t[1];
     if (hc->nomem) return FGV_ENOMEM;  // nothing was committed
   }
   memcpy(flags, M->htail.as<uint8_t>() + kCounterBytes, ntx);

@@ -14,11 +14,10 @@
 //        IsKVWriteDelete / IsKVWriteHashDelete (rwsetutil/rwset_proto_util.go:366-375)
 //
 // Pipeline of one block (one H2D head copy, one D2H tail copy, no host sync in between):
-//   k_mvx_count   one lane per tx: envelope -> ... -> TxReadWriteSet walk (pbwire_dev.h rules),
+//   k_mvx_extract one lane per tx: envelope -> ... -> TxReadWriteSet walk (pbwire_dev.h rules),
 //                 codes 16 / 255 / unsupported, read/write counts, record ranges claimed by
-//                 wave-aggregated atomics
-//   k_mvx_emit    one lane per tx: the TxReadWriteSet walked again from the span k_mvx_count
-//                 kept, 48-byte records + 64-bit tags; duplicate writes of one key in one tx
+//                 wave-aggregated atomics, then the same walk again by the same lane (cache hits)
+//                 writing 48-byte records + 64-bit tags; duplicate writes of one key in one tx
 //                 (tx_ops.go:183-191 adds flags: undefined semantics) -> unsupported
 //   k_mvx_prep    writes -> block write table (claim by CAS, epoch-tagged: never cleared);
 //                 reads  -> committed-state table, static version check
@@ -395,10 +394,16 @@ DEV uint32_t bmask_of(uint32_t nw) {
 }  // namespace
 
 // ============================================================ rwset extraction
-__global__ __launch_bounds__(64) void k_mvx_count(uint32_t ntx, const uint8_t *__restrict__ base,
-                                                  const uint32_t *__restrict__ envtab,
-                                                  const uint8_t *__restrict__ in_flags, MvTxInfo *__restrict__ info,
-                                                  MvCounters *__restrict__ c) {
+// One lane per tx: the TxReadWriteSet walked twice by the same lane -- counting, then (its
+// record ranges claimed by wave-aggregated atomics) emitting 48-byte records + 64-bit tags --
+// so the second walk finds the rwset bytes in the lane's caches: the block is read from HBM once.
+// Duplicate writes of one key in one tx (tx_ops.go:183-191 adds flags: undefined semantics)
+// -> unsupported.
+__global__ __launch_bounds__(64) void k_mvx_extract(uint32_t ntx, const uint8_t *__restrict__ base,
+                                                    const uint32_t *__restrict__ envtab,
+                                                    const uint8_t *__restrict__ in_flags, MvTxInfo *__restrict__ info,
+                                                    MvRec *__restrict__ reads, MvRec *__restrict__ writes,
+                                                    MvCounters *__restrict__ c) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t nr = 0, nw = 0;
   uint64_t wb = 0;
@@ -428,30 +433,22 @@ __global__ __launch_bounds__(64) void k_mvx_count(uint32_t ntx, const uint8_t *_
   I.wcnt = nw;
   for (int off = 32; off > 0; off >>= 1) wb += __shfl_down(wb, off);
   if ((threadIdx.x & 63u) == 0 && wb) atomicAdd(&c->wbytes, (unsigned long long)wb);
-  if (t < ntx) info[t] = I;
-}
-
-__global__ __launch_bounds__(64) void k_mvx_emit(uint32_t ntx, const uint8_t *__restrict__ base,
-                                                 MvTxInfo *__restrict__ info, MvRec *__restrict__ reads,
-                                                 MvRec *__restrict__ writes, MvCounters *__restrict__ c) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
-  MvTxInfo I = info[t];
-  if (I.code != 0) return;
-  Sink sk{base, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
-  bool host = false;
-  walk_rwset(S{base + I.rws_off, I.rws_len}, sk, host);
-  // one key written twice by one tx: txOps adds the flags (tx_ops.go:183-191) -> semantics
-  // the engine does not model (upsert+upsert reads as a metadata-only update)
-  const MvRec *w = writes + I.wbeg;
-  bool dup = false;
-  for (uint32_t a = 0; a < I.wcnt && !dup; a++)
-    for (uint32_t b = a + 1; b < I.wcnt; b++)
-      if (rec_eq(base, w[a], w[b])) { dup = true; break; }
-  if (dup) {
-    info[t].code = MV_UNSUP;
-    atomicOr(&c->unsup, 1u);
+  if (I.code == 0) {
+    Sink sk{base, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
+    bool host = false;
+    walk_rwset(S{base + I.rws_off, I.rws_len}, sk, host);
+    const MvRec *w = writes + I.wbeg;
+    bool dup = false;
+    for (uint32_t a = 0; a < I.wcnt && !dup; a++)
+      for (uint32_t b = a + 1; b < I.wcnt; b++)
+        if (rec_eq(base, w[a], w[b])) { dup = true; break; }
+    if (dup) {
+      I.code = MV_UNSUP;
+      atomicOr(&c->unsup, 1u);
+    }
   }
+  info[t] = I;
 }
 
 // ============================================================ lookups

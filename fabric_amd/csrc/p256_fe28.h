@@ -42,6 +42,9 @@ __constant__ static const uint32_t R2P28[10] = {0x50000u,    0x300000u,  0u,    
                                                 0xfffffbfu,  0xffffeffu, 0xfffafffu, 0x2ffffu,   0u};
 __constant__ static const uint32_t ONE28[10] = {0x1000000u, 0u,         0u,         0u,         0xfffff00u,
                                                 0xfffffffu, 0xfffffffu, 0xfefffffu, 0xffffffu,  0u};
+// 2^232 (< p) as 8 x 32-bit limbs: fe_mul(x * 2^280, C232) = x * 2^256 (the exact kernel's view of a
+// Montgomery-280 key-comb entry)
+__constant__ static const uint32_t C232_32[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0x100u};
 // 2^280 mod p as 8 x 32-bit limbs: fe_mul(x * 2^256, C280) = x * 2^280 (table conversion)
 __constant__ static const uint32_t C280_32[8] = {0x1000000u, 0u,         0u,         0xff000000u,
                                                  0xffffffffu, 0xffffffffu, 0xfeffffffu, 0xffffffu};
@@ -103,6 +106,25 @@ FGV_DEV void f28_mul(f28 &r, const f28 &a, const f28 &b) {
     for (int i = 0; i < 10; i++) {
       const int j = k - i;
       if (j >= 0 && j < 10) acc += (uint64_t)a.v[i] * b.v[j];
+    }
+    t[k] = acc;
+  }
+  t[19] = 0;
+  f28_redc(r, t);
+}
+
+// r = (a*b + c*d) / 2^280 mod p: the two products summed column by column, ONE reduction.
+// a, b, c loose (limbs < 2^30), d normalized: a column stays below 10 * 2^60 + 10 * 2^58 <
+// 2^63.7, the reduction's terms fit in the rest; output normalized, < 2p when a*b + c*d < 2^280 p
+FGV_DEV void f28_mul2(f28 &r, const f28 &a, const f28 &b, const f28 &c, const f28 &d) {
+  uint64_t t[20];
+#pragma unroll
+  for (int k = 0; k < 19; k++) {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < 10) acc += (uint64_t)a.v[i] * b.v[j] + (uint64_t)c.v[i] * d.v[j];
     }
     t[k] = acc;
   }

@@ -168,8 +168,10 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
     fe_mul(z3, z2, zinv);
     fe_mul(ax, X, z2);
     fe_mul(ay, Y, z3);
-    store_fe(tables[e0 + j].x, ax);
-    store_fe(tables[e0 + j].y, ay);
+    if (tables) {  // (the exact Montgomery-256 copy: the generator table only)
+      store_fe(tables[e0 + j].x, ax);
+      store_fe(tables[e0 + j].y, ay);
+    }
     // the same point in Montgomery-280 form (k_point28): x * 2^256 -> x * 2^280
     fe_mul(ax, ax, c280);
     fe_mul(ay, ay, c280);
@@ -188,13 +190,11 @@ __constant__ static const uint32_t G_PLAIN[16] = {
     0xD898C296u, 0xF4A13945u, 0x2DEB33A0u, 0x77037D81u, 0x63A440F2u, 0xF8BCE6E5u, 0xE12C4247u, 0x6B17D1F2u,
     0x37BF51F5u, 0xCBB64068u, 0x6B315ECEu, 0x2BCE3357u, 0x7C0F9E16u, 0x8EE7EB4Au, 0xFE1A7F9Bu, 0x4FE342E2u};
 
-__global__ __launch_bounds__(64) void k_gtab(apoint_raw *__restrict__ tables, apoint_raw *__restrict__ tables28,
-                                             jpoint_raw *__restrict__ scratch) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= GT_THREADS) return;
-  constexpr uint32_t CPW = GT_K / GT_CHUNK;  // chunks per window
-  const uint32_t w = t / CPW, ch = t % CPW;
-  const uint32_t k0 = ch * GT_CHUNK + 1, cnt = w == NGWIN - 1 ? 1u : (uint32_t)GT_CHUNK;
+__global__ __launch_bounds__(64) void k_gtab(apoint_raw *__restrict__ tables28, jpoint_raw *__restrict__ scratch,
+                                             uint32_t w) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // chunk of window w
+  if (t >= GT_THREADS_PER_WIN) return;
+  const uint32_t k0 = t * GT_CHUNK + 1;
   fe gx, gy;
   fe_load_c(gx, G_PLAIN);
   fe_load_c(gy, G_PLAIN + 8);
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(64) void k_gtab(apoint_raw *__restrict__ tables, ap
   const size_t e0 = (size_t)w * GT_K + (k0 - 1);
   fe pref;
   fe_set_one(pref);
-  for (uint32_t j = 0; j < cnt; j++) {
+  for (uint32_t j = 0; j < GT_CHUNK; j++) {
     if (j > 0) {
       jpoint t2 = pk;
       pt_add(pk, t2, b);
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(64) void k_gtab(apoint_raw *__restrict__ tables, ap
   fe_inv(inv, pref);
   fe c280;
   fe_load_c(c280, C280_32);
-  for (int j = (int)cnt - 1; j >= 0; j--) {
+  for (int j = GT_CHUNK - 1; j >= 0; j--) {
     fe X, Y, Z, prev, zinv, z2, z3, ax, ay;
     load_fe(X, scr[j].x);
     load_fe(Y, scr[j].y);
@@ -245,9 +245,7 @@ __global__ __launch_bounds__(64) void k_gtab(apoint_raw *__restrict__ tables, ap
     fe_mul(z3, z2, zinv);
     fe_mul(ax, X, z2);
     fe_mul(ay, Y, z3);
-    store_fe(tables[e0 + j].x, ax);
-    store_fe(tables[e0 + j].y, ay);
-    fe_mul(ax, ax, c280);
+    fe_mul(ax, ax, c280);  // Montgomery-256 -> Montgomery-280 (k_point28's form)
     fe_mul(ay, ay, c280);
     store_fe(tables28[e0 + j].x, ax);
     store_fe(tables28[e0 + j].y, ay);
@@ -388,21 +386,24 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint32_t *__rest
   }
   sn_mul(u1, e, w);  // e * s^-1 (plain)
   sn_mul(u2, r, w);  // r * s^-1 (plain)
-  // signed recoding, digits in [-2^(W-1), 2^(W-1) - 1], the last window holding the final
-  // carry: u1 in base 2^16 (17 int16 digits, generator comb), u2 in base 2^10 (26 int16 digits;
-  // the top window of a scalar < 2^256 is < 2^6 + 1, so it never carries out)
+  // signed recoding, digits in [-2^(W-1), 2^(W-1) - 1]: u1 in base 2^22 (12 int32 digits,
+  // generator comb), u2 in base 2^13 (20 int16 digits); the top window of a scalar < 2^256
+  // (bits 242.. / 247..) is far below half its range, so the final carry never leaves it
   int8_t *dp = digits + (size_t)i * DIG_STRIDE;
   {
-    uint16_t *g = reinterpret_cast<uint16_t *>(dp);
+    constexpr int GMASK = (1 << GWBITS) - 1, GHALF = 1 << (GWBITS - 1);
+    int32_t *g = reinterpret_cast<int32_t *>(dp);
     int c1 = 0;
 #pragma unroll
-    for (int win = 0; win < NGWIN - 1; win++) {
-      int a1 = (int)((u1[win >> 1] >> (16 * (win & 1))) & 0xFFFFu) + c1;
-      c1 = a1 >= (1 << 15);
-      a1 -= c1 << 16;
-      g[win] = (uint16_t)(int16_t)a1;
+    for (int win = 0; win < NGWIN; win++) {
+      const int bit = GWBITS * win, li = bit >> 5, sh = bit & 31;
+      uint32_t v1 = li < 8 ? u1[li] >> sh : 0u;
+      if (sh > 32 - GWBITS && li < 7) v1 |= u1[li + 1] << (32 - sh);
+      int a1 = (int)(v1 & GMASK) + c1;
+      c1 = a1 >= GHALF;
+      a1 -= c1 << GWBITS;
+      g[win] = a1;
     }
-    g[NGWIN - 1] = (uint16_t)c1;
   }
   constexpr int WMASK = (1 << WBITS) - 1, WHALF = 1 << (WBITS - 1);
   int c2 = 0;
@@ -480,13 +481,20 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point(
     for (int t = 0; t < nterms; t++) {
       const int tt = (int)sub + t * (int)L;
       const bool isq = tt >= NGWIN;
-      const int d = (int)reinterpret_cast<const int16_t *>(dg + (isq ? DIG_Q_OFF : 0))[isq ? tt - NGWIN : tt];
+      const int d = isq ? (int)reinterpret_cast<const int16_t *>(dg + DIG_Q_OFF)[tt - NGWIN]
+                        : reinterpret_cast<const int32_t *>(dg)[tt];
       if (d == 0) continue;
       const int k = (d < 0 ? -d : d) - 1;
       apoint p;
-      const apoint_raw *e = isq ? qt + (tt - NGWIN) * TAB_K + k : gtab + (size_t)tt * GT_K + k;
+      const apoint_raw *e = isq ? qt + (size_t)(tt - NGWIN) * TAB_K + k : gtab + (size_t)tt * GT_K + k;
       load_fe(p.x, e->x);
       load_fe(p.y, e->y);
+      {  // the combs are held in Montgomery-280 form: x 2^280 * 2^232 / 2^256 = x 2^256
+        fe c232;
+        fe_load_c(c232, C232_32);
+        fe_mul(p.x, p.x, c232);
+        fe_mul(p.y, p.y, c232);
+      }
       if (d < 0) fe_neg(p.y, p.y);
       pt_madd(acc, acc, p);
     }
@@ -541,7 +549,7 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point(
 // ones (Q = +-G, u1 = +-u2 ...) do, and stay bit-exact through the exact kernel.
 //
 // Value bounds (multiples of p) of the lazy representation, per coordinate of the running
-// sum: X < 10p, Y < 6p, Z < 2p, all normalized; the constants of each f28_sub are chosen so
+// sum: X < 10p, Y < 2p, Z < 2p, all normalized; the constants of each f28_sub are chosen so
 // the subtrahend's top limb stays below the constant's (p256_fe28.h).
 struct jp28 {
   f28 x, y, z;
@@ -565,11 +573,12 @@ FGV_DEV void madd28(jp28 &a, const f28 &x2, const f28 &y2) {
   f28_sqr(x3, r);
   f28_sub(x3, x3, t, C8P28);
   f28_norm(x3);                 // < 10p
-  f28_sub(t, v, x3, C16P28);
-  f28_mul(y3, r, t);
-  f28_mul(t, a.y, hhh);
-  f28_sub(y3, y3, t, C4P28);
-  f28_norm(y3);                 // < 6p
+  f28_sub(t, v, x3, C16P28);    // < 18p
+  // y3 = r (v - x3) + (8p - y1) hhh: both products in one column sum, one reduction
+  f28 ny;
+#pragma unroll
+  for (int j = 0; j < 10; j++) ny.v[j] = C8P28[j] - a.y.v[j];  // < 8p, loose
+  f28_mul2(y3, r, t, ny, hhh);  // < 2p
   f28_mul(a.z, a.z, h);
   a.x = x3;
   a.y = y3;
@@ -598,10 +607,10 @@ FGV_DEV void add28(jp28 &a, const jp28 &b) {
   f28_sub(x3, x3, t, C8P28);
   f28_norm(x3);
   f28_sub(t, v, x3, C16P28);
-  f28_mul(y3, r, t);
-  f28_mul(t, s1, hhh);
-  f28_sub(y3, y3, t, C4P28);
-  f28_norm(y3);
+  f28 ns1;
+#pragma unroll
+  for (int j = 0; j < 10; j++) ns1.v[j] = C4P28[j] - s1.v[j];  // s1 < 2p: 4p - s1, loose
+  f28_mul2(y3, r, t, ns1, hhh);
   f28_mul(t, a.z, b.z);
   f28_mul(a.z, t, h);
   a.x = x3;
@@ -646,9 +655,9 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
     auto entry = [&](int t, int &d) -> const uint4 * {
       const int tt = (int)sub + t * (int)L;
       const bool isq = tt >= NGWIN;
-      d = (int)reinterpret_cast<const int16_t *>(dg + (isq ? DIG_Q_OFF : 0))[isq ? tt - NGWIN : tt];
+      d = isq ? (int)reinterpret_cast<const int16_t *>(dg + DIG_Q_OFF)[tt - NGWIN] : reinterpret_cast<const int32_t *>(dg)[tt];
       const int k = d == 0 ? 0 : (d < 0 ? -d : d) - 1;
-      return reinterpret_cast<const uint4 *>(isq ? qt + (tt - NGWIN) * TAB_K + k : gtab28 + (size_t)tt * GT_K + k);
+      return reinterpret_cast<const uint4 *>(isq ? qt + (size_t)(tt - NGWIN) * TAB_K + k : gtab28 + (size_t)tt * GT_K + k);
     };
     int dn;
     const uint4 *pn = entry(0, dn);

@@ -43,7 +43,8 @@ typedef struct fgv_ctx fgv_ctx;
 
 typedef struct fgv_config {
   int device;            /* HIP device ordinal (one process per GPU)                 */
-  uint32_t key_slots;    /* capacity of the device public-key table cache (0 = 4096) */
+  uint32_t key_slots;    /* capacity of the device public-key table cache (0 = 2048; 5.2 MB of HBM
+                            per slot: the key comb of one key, 13-bit windows)                  */
   uint32_t host_threads; /* host worker threads for parsing / policy fold (0 = min(24,
                             the process's CPU share: affinity mask, OMP_NUM_THREADS)) */
 } fgv_config;
@@ -318,7 +319,8 @@ int fgv_validate_shard_dev(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *b
  * like any other (channel model, identities, chaincodes, ledger txids: the same calls on every
  * context).  fgv_group_validate_blocks = fgv_validate_blocks over all devices: the blocks are
  * split into contiguous ranges of about equal bytes, one per device (each device stages, splits
- * and parses only its own), the devices validate in parallel (fgv_validate_shard_dev), their
+ * and parses only its own) -- or, with fewer blocks than devices (one block), the batch's
+ * transactions into contiguous index ranges -- the devices validate in parallel (fgv_validate_shard_dev), their
  * records are gathered onto the first device by peer copies (xGMI), and the first device runs
  * the batch's cross-transaction steps (fgv_finalize_flags_dev_plan).  Same flags as one GPU.
  * host_threads 0 in cfg: the process's CPU share divided among the devices. */
@@ -329,6 +331,14 @@ size_t fgv_group_size(const fgv_group *g);
 fgv_ctx *fgv_group_ctx(fgv_group *g, size_t i);
 int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                               uint8_t *flags, size_t flags_cap, size_t *ntx);
+/* fgv_p256_verify_msgs over all devices of the group (config C4 through the C ABI): items
+ * [n r / W, n (r+1) / W) on device r, each device verifying with its own key cache; same status
+ * bytes as one device.  The devices read only the message / signature byte spans their items
+ * reference. */
+int fgv_group_p256_verify_msgs(fgv_group *g, const uint8_t *keys, const uint8_t *msg_buf, size_t msg_buf_len,
+                               const uint64_t *msg_off, const uint32_t *msg_len, const uint8_t *sig_buf,
+                               size_t sig_buf_len, const uint64_t *sig_off, const uint32_t *sig_len, size_t n,
+                               uint8_t *status);
 
 /* Deliver-side pre-split (no reference counterpart: the Go committer re-walks each block
  * inside TxValidator.Validate, validator.go:180-265).  Starts walking the block data framing

@@ -74,3 +74,63 @@ def test_group_unsupported_propagates():
     with pytest.raises(_lib.Unsupported):
         g.validate_blocks(blks)
     g.close()
+
+
+@pytest.mark.parametrize("ndev", [2, 3, 4])
+def test_group_single_block_split_by_transaction(ndev):
+    """one block (fewer blocks than devices) is split by transaction index across
+    the devices; a txid repeated across the device ranges (tx 5 again at tx 170) is still caught
+    by markTXIdDuplicates in the finalize -- flags equal the single GPU's and the oracle's"""
+    net = network()
+    txs = []
+    b0 = blocks.make_block(net, 60, number=1, seed=961, faults=(), out_txs=txs)[0]
+    blk = blocks.make_block(net, 200, number=2, seed=962, reuse={170: (txs[5].creator, txs[5].nonce)})[0]
+    one = _lib.Engine(0)
+    _setup(one, net)
+    single = list(one.validate_blocks([blk])[0])
+    one.close()
+    exp = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), net.chaincodes), [blk])[0]
+    g = _lib.Group([0] * ndev)
+    for e in g.engines:
+        _setup(e, net)
+    got = list(g.validate_blocks([blk])[0])
+    assert got == single == list(exp)
+    # the same txid twice inside the split block: its second occurrence is 9
+    blk2 = blocks.make_block(net, 120, number=3, seed=963, faults=())[0]
+    from oracle.protowire import decode
+    envs = decode("Block", blk2)["data"]["data"]
+    from tests.blockfix import block_from_envs
+    dup = block_from_envs(envs[:100] + [envs[3]] + envs[100:], number=3)
+    got2 = list(g.validate_blocks([dup])[0])
+    exp2 = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), net.chaincodes), [dup])[0]
+    assert got2 == list(exp2) and got2[100] == 9
+    # two blocks over more devices: the ranges cross the block boundary
+    got3 = g.validate_blocks([b0, blk])
+    exp3 = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), net.chaincodes), [b0, blk])
+    assert [list(f) for f in got3] == [list(f) for f in exp3]
+    g.close()
+
+
+def test_group_verify_msgs_c4_share():
+    """fgv_group_p256_verify_msgs -- the C4 per-GPU share (131,072 identity.Verify
+    items, the fault mix) split over 2 device contexts through the C ABI equals one context"""
+    import numpy as np
+    from fabric_amd._lib import pack
+    from fabric_amd.synth.workloads import sig_pool
+    n, uniq = 131072, 16384
+    pool = sig_pool(uniq, seed=1001)
+    idx = np.arange(n) % uniq
+    keys = np.frombuffer(b"".join(pool["keys"][pool["key_index"][i]].pub for i in range(uniq)), np.uint8).reshape(-1, 64)[idx]
+    msgs = np.ascontiguousarray(pool["msgs"][idx])
+    mlen = np.full(n, msgs.shape[1], np.uint32)
+    moff = np.arange(n, dtype=np.uint64) * np.uint64(msgs.shape[1])
+    sa, so, sl = pack([pool["sigs"][i] for i in idx])
+    margs = (msgs.reshape(-1), moff, mlen)
+    g = _lib.Group([0, 0])
+    got = g.verify_msgs(keys, margs, (sa, so, sl))
+    g.close()
+    one = _lib.Engine(0)
+    single = one.verify_msgs(keys, margs, (sa, so, sl))
+    one.close()
+    assert (got == single).all()
+    assert ((got == 0) == pool["expect_valid"][idx]).all()

@@ -6,7 +6,7 @@
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
 P="rocprofv3 --output-format csv"
 timeout -k 10 300 $P --kernel-trace --stats -d $OUT/block -o run -- python bench.py --steps 10 --warmup 2 --cpu-threads 0 > $OUT/block.json 2> $OUT/block.err

@@ -124,15 +124,20 @@ def main(src, rnd):
                 fb, wb = F[kern]["FETCH_SIZE"] * 2 * 1024, W[kern]["WRITE_SIZE"] * 1024
                 traffic[wl] = dict(kernel=kern, fetch_bytes=round(fb), write_bytes=round(wb), hbm_bytes=round(fb + wb),
                                    avg_us=round(F[kern]["avg_s"] * 1e6, 1))
-        else:  # MVCC: all per-block kernels (the one-time k_mv_load excluded), per block
-            nblk = F.get("k_mv_lookup", {}).get("dispatches", 0)
+        else:  # MVCC: every per-block kernel (the one-time state load k_mv_tags excluded), per block
+            nblk = F.get("k_mvx_extract", {}).get("dispatches", 0)
+            per_block = [k for k in F if k.startswith("k_mv") and k != "k_mv_tags"]
             if nblk:
-                fb = sum(v["FETCH_SIZE"] * 2 * 1024 * v["dispatches"] for k, v in F.items()
-                         if k.startswith("k_mv") and k != "k_mv_load") / nblk
-                wb = sum(v["WRITE_SIZE"] * 1024 * v["dispatches"] for k, v in W.items()
-                         if k.startswith("k_mv") and k != "k_mv_load") / nblk
-                traffic[wl] = dict(kernel="k_mv_* per block", fetch_bytes=round(fb), write_bytes=round(wb),
-                                   hbm_bytes=round(fb + wb))
+                fb = sum(F[k]["FETCH_SIZE"] * 2 * 1024 * F[k]["dispatches"] for k in per_block) / nblk
+                wb = sum(W[k]["WRITE_SIZE"] * 1024 * W[k]["dispatches"] for k in per_block if k in W) / nblk
+                rounds = F.get("k_mvx_round", {}).get("dispatches", 0) / nblk
+                traffic[wl] = dict(kernels=sorted(per_block), fetch_bytes_per_block=round(fb),
+                                   write_bytes_per_block=round(wb), hbm_bytes_per_block=round(fb + wb),
+                                   blocks=nblk,
+                                   note=f"sum over one C3 block's MVCC kernels (k_mvx_round x{rounds:.1f}), "
+                                        "FETCH_SIZE x2 per MI355X_MICROARCH.md (small gathers uncalibrated: an "
+                                        "upper bound); the block's envelope bytes read by k_mvx_extract and the "
+                                        "1M-key table probes are included; k_mv_tags = the one-time state load")
     if traffic:
         json.dump(dict(round=rnd, source="rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, separate passes "
                                         "(tools/profile_round.sh)", workloads=traffic),
