@@ -195,6 +195,64 @@ def cpu_full_validator(net, blks, procs, target_s):
     return done / el, done, el, nblk
 
 
+def cpu_c_validator(net, blks, labels, threads, target_s, expected=None):
+    """The plain-C restatement of the committer for this workload's shapes (oracle/
+    cpu_validator.c: protobuf walk, registry lookup, SHA-256, Go-rule DER + low-S + OpenSSL 3
+    P-256 Verify, OutOf(n, member) fold, txid duplicates) on `threads` host threads, whole
+    blocks per thread, repeated until ~target_s of wall time.  Returns (tx/s, tx, seconds,
+    blocks, parity with the generator's labels)."""
+    import ctypes
+    import oracle
+    from fabric_amd.synth import blocks as B
+    L = oracle.lib()
+    ids = net.identities()
+    msp_ix = {m: i for i, m in enumerate(net.mspids)}
+    canon = {}
+    ser = [s for s, _ in ids]
+    soff = np.cumsum([0] + [len(x) for x in ser[:-1]]).astype(np.uint64)
+    slen = np.array([len(x) for x in ser], np.uint32)
+    sbuf = np.frombuffer(b"".join(ser), np.uint8)
+    keys = np.zeros((len(ids), 64), np.uint8)
+    msp = np.zeros(len(ids), np.int32)
+    cano = np.zeros(len(ids), np.int32)
+    ok = np.zeros(len(ids), np.uint8)
+    for i, (_, I) in enumerate(ids):
+        if I.pub is not None and I.key == "p256":
+            keys[i] = np.frombuffer(I.pub, np.uint8)
+            ok[i] = 1 if I.valid else 0
+        msp[i] = msp_ix.get(I.mspid, -1)
+        cano[i] = canon.setdefault((I.mspid, bytes(I.id_digest)), len(canon))
+    pol = np.array([msp_ix[m] for m in net.mspids], np.int32)
+    nb = len(blks)
+    bptr = (ctypes.c_void_p * nb)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value for b in blks])
+    lens = (ctypes.c_size_t * nb)(*[len(b) for b in blks])
+    exp = [c for f in expected for c in f] if expected is not None else \
+        [c for lab in labels for c in B.expected_codes(lab)]
+    flags = np.zeros(len(exp) + 16, np.uint8)
+    ntx = (ctypes.c_size_t * nb)()
+    fn = L.oracle_cpu_validate_blocks
+    fn.restype = ctypes.c_int
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    fn.argtypes = [vp, vp, sz, ctypes.c_char_p, ctypes.c_char_p, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp,
+                   vp, vp, sz, vp, sz, vp, ctypes.c_int]
+
+    def once():
+        rc = fn(ctypes.cast(bptr, vp), ctypes.cast(lens, vp), nb, net.channel.encode(), b"mycc", pol.ctypes.data,
+                len(pol), net.policy_n, sbuf.ctypes.data, soff.ctypes.data, slen.ctypes.data, keys.ctypes.data,
+                msp.ctypes.data, cano.ctypes.data, ok.ctypes.data, len(ids), flags.ctypes.data, len(flags),
+                ctypes.cast(ntx, vp), threads)
+        assert rc == 0, rc
+        return sum(ntx)
+    n0 = once()
+    parity = list(flags[:n0]) == exp
+    done, rounds, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < target_s:
+        done += once()
+        rounds += 1
+    el = time.perf_counter() - t0
+    return done / el, done, el, rounds * nb, parity
+
+
 def run_block(args, world, rank, local, dev_fn):
     import threading
 
@@ -235,9 +293,14 @@ def run_block(args, world, rank, local, dev_fn):
         # CPU baselines first: the full-validator workers are forked before any GPU use
         procs = args.cpu_threads if args.cpu_threads > 0 else _cpu_share()
         sample = my_blocks[0][:max(1, min(B, 2 * procs))]
-        full_n = cpu_full_validator(net, sample, procs, args.cpu_seconds)
-        full_1 = cpu_full_validator(net, sample[:2], 1, args.cpu_seconds / 2)
-        cpu = dict(procs=procs, full=full_n, full1=full_1)
+        labs = [m[1] for m in mine[0][:len(sample)]]
+        c_n = cpu_c_validator(net, sample, labs, procs, args.cpu_seconds)
+        c_1 = cpu_c_validator(net, sample[:2], labs[:2], 1, args.cpu_seconds / 2)
+        log(f"[bench] cpu C validator: {c_n[0]:,.0f} tx/s on {procs} threads, {c_1[0]:,.0f} tx/s on 1, "
+            f"parity {c_n[4] and c_1[4]}")
+        full_n = cpu_full_validator(net, sample, procs, args.cpu_seconds / 3)
+        full_1 = cpu_full_validator(net, sample[:1], 1, args.cpu_seconds / 4)
+        cpu = dict(procs=procs, full=full_n, full1=full_1, c=c_n, c1=c_1)
         log(f"[bench] cpu full validator: {full_n[0]:,.0f} tx/s on {procs} procs, {full_1[0]:,.0f} tx/s on 1")
     dev = dev_fn()
 
@@ -483,13 +546,20 @@ def run_block(args, world, rank, local, dev_fn):
     if cpu is not None:
         rate, n, cel, nb = cpu["full"]
         r1, n1, c1, nb1 = cpu["full1"]
+        crate, cn, ccel, cnb, cpar = cpu["c"]
+        cr1, cn1, cc1, _, cpar1 = cpu["c1"]
         out["cpu_baseline"] = dict(
-            value=round(rate, 1), unit="validated tx/s", cores=cpu["procs"], kind="port",
-            sample=f"{nb} blocks x {T} tx of this workload through the restated v20 committer (oracle/v20.py: "
-                   f"protobuf walk, MSP lookup, OpenSSL 3 P-256 Verify via oracle/liboracle.so, policy fold) on "
-                   f"{cpu['procs']} processes in {cel:.1f}s; 1 process: {r1:,.1f} tx/s ({n1} tx in {c1:.1f}s); "
-                   f"CPU {_cpu_model()}; Python restatement, not the Go peer (no Go toolchain on the box)",
-            one_thread=round(r1, 1), cpu_model=_cpu_model())
+            value=round(crate, 1), unit="validated tx/s", cores=cpu["procs"], kind="port",
+            sample=f"{cnb} blocks x {T} tx of this workload through the plain-C restated committer "
+                   f"(oracle/cpu_validator.c: protobuf walk, registry lookup, SHA-256, Go DER + low-S + OpenSSL 3 "
+                   f"P-256 Verify, OutOf fold, txid duplicates) on {cpu['procs']} threads in {ccel:.1f}s; 1 thread: "
+                   f"{cr1:,.1f} tx/s ({cn1} tx in {cc1:.1f}s); flags equal to the generator's labels: {cpar and cpar1}; "
+                   f"CPU {_cpu_model()}; a C restatement, not the Go peer (no Go toolchain on the box)",
+            one_thread=round(cr1, 1), parity_vs_labels=bool(cpar and cpar1), cpu_model=_cpu_model())
+        out["cpu_python_restatement"] = dict(
+            value=round(rate, 1), unit="validated tx/s", cores=cpu["procs"], one_thread=round(r1, 1),
+            sample=f"{nb} blocks through oracle/v20.py (the full restated v20 committer, the parity oracle) on "
+                   f"{cpu['procs']} processes in {cel:.1f}s; 1 process: {n1} tx in {c1:.1f}s")
         vpt = acc["verifies"] / (B * T * K)
         from fabric_amd.synth.workloads import sig_pool
         pool = sig_pool(4096, seed=99, msg_len=1850)

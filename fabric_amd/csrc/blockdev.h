@@ -56,9 +56,42 @@ struct DevTx {
   int32_t type;
   DSpan payload, env_sig, nonce, creator, chdr, act_hdr, ccpp, prop_hash, prp, txid;
   DSpan idx_nonce, idx_creator, index_txid;
-  uint8_t npol, nend, pad[2];
+  uint8_t npol, nend;
+  uint8_t nwr;  // vscc namespaces of Dispatch (written namespaces + the invoked chaincode)
+  uint8_t kln;  // k_bd_kl: earlier metadata writers of its written keys in its block (KlDev::dep)
   int16_t pol[BD_MAX_POL];
   DSpan end_ser[BD_MAX_END], end_sig[BD_MAX_END];
+  DSpan results;  // ChaincodeAction.results when the whole TxReadWriteSet decodes (else nil)
+};
+
+// ---------------------------------------------------------------- key-level endorsement
+// KeyLevelValidationParameterManagerImpl's per-block state (vpmanagerimpl.go:113-233) on the
+// device.  k_bd_parse records every metadata write of every transaction whose rwset decodes
+// (ExtractValidationParameterDependency, vpmanagerimpl.go:258-292) and every delete of a key that
+// holds a committed VALIDATION_PARAMETER (tx_ops.go:17-51: it clears the parameter) in a
+// chained hash table keyed by (namespace, collection, key); k_bd_kl then finds, per written key,
+// the earlier metadata writers of the same block (the txs whose vscc result a
+// GetValidationParameterForKey waits for) and the changes made by earlier blocks of the batch
+// (outside the model: the reference commits block k before block k+1 reads the parameter).
+// k_bd_fold folds every transaction against the committed parameters in parallel; the last
+// transaction of a block to finish then walks the block's dependent transactions in order.
+enum : uint32_t { KL_MD = 0, KL_DEL = 1 };
+struct KlRec {
+  uint64_t hash;
+  uint32_t tx, blk, kind, next;  // next: record index + 1 in the bucket's chain (0: end)
+  uint32_t ns_off, ns_len, coll_off, coll_len, key_off, key_len;  // spans of block `blk`
+};
+#define KL_DEPS 8      // earlier metadata writers of one transaction's keys
+#define KL_MAXDEP 64   // dependent transactions per block
+#define KL_BLK_WORDS 4 // per block: first tx, tx count, fold completions, dependents
+struct KlDev {
+  KlRec *rec;
+  unsigned long long *head;  // bucket -> (seq << 32) | (record index + 1); other seqs read as empty
+  uint32_t hmask, rcap, seq, on;  // on: whole batch (no shard ranges); the fold's walk needs the fused finalize
+  uint32_t *cnt;       // records (the batch counters' word 11)
+  uint32_t *blk;       // KL_BLK_WORDS per block (head region, reset per batch)
+  uint32_t *deplist;   // KL_MAXDEP per block
+  uint32_t *dep;       // KL_DEPS per transaction
 };
 
 // per-tx job bookkeeping written by k_bd_count / k_bd_emit
@@ -107,7 +140,7 @@ struct DevPolicy {
 };
 // chaincode table entry: namespace bytes, compiled EP, status (0 ok, 1 INVALID_CHAINCODE, 2
 // outside the model), collections known, its collections [coll0, coll0+ncoll) in the coll table,
-// key-level validation parameters in the state (writes to the namespace: host parser)
+// key-level validation parameters in the state (its keys are resolved one by one)
 #define BD_CC_WORDS 8
 // collection table entry: name bytes, EP (-1: the chaincode EP); implicit table: mspid bytes, EP
 #define BD_COLL_WORDS 3
@@ -135,6 +168,13 @@ struct DevChannel {  // device pointers + sizes (passed by value to the kernels)
   const uint32_t *subs;
   const DevPrin *prins;
   const int32_t *ident_ous;     // interned (OU, certifier) ids of the identities
+  // committed key-level validation parameters: open addressing, 8 words per slot (hash lo, hash
+  // hi, arena offset of ns || coll || key, the three lengths, policy index or -3, used); null when
+  // the state holds none
+  const uint32_t *kvp;
+  const uint8_t *kvp_bytes;
+  uint32_t kvp_mask;
+  uint32_t force_host;          // policy indices beyond int16 (DevTx::pol): the host parser
   const uint8_t *committed;     // committed ledger txids: open-addressing table of 32-byte keys
   uint32_t committed_mask;      // (all-zero key == empty; a zero txid is kept in committed_zero)
   uint32_t committed_zero;
@@ -165,6 +205,22 @@ BD_HD inline uint64_t bd_ident_hash_msp(const uint8_t *msp, uint32_t ml, uint32_
     if (k == 8) { h = bd_mix(h, w); w = 0; k = 0; }
   }
   return bd_mix(h, w ^ 0xA5);
+}
+// key-level state key (ns, coll, key): host form (byte loads); blockdev.hip kl_hash is the
+// word-load form of the same function
+inline uint64_t bd_kl_word(const uint8_t *p, uint32_t n, uint32_t j) {
+  uint32_t w = 0;
+  for (uint32_t b = 0; b < 4 && 4 * j + b < n; b++) w |= (uint32_t)p[4 * j + b] << (8 * b);
+  return w;
+}
+inline uint64_t bd_kl_hash(const uint8_t *ns, uint32_t nl, const uint8_t *coll, uint32_t cl, const uint8_t *key,
+                           uint32_t kl) {
+  uint64_t h = bd_mix(0x6A09E667F3BCC908ull, ((uint64_t)nl << 32) | cl);
+  h = bd_mix(h, kl);
+  for (uint32_t j = 0; 4 * j < nl; j++) h = bd_mix(h, bd_kl_word(ns, nl, j));
+  for (uint32_t j = 0; 4 * j < cl; j++) h = bd_mix(h, bd_kl_word(coll, cl, j));
+  for (uint32_t j = 0; 4 * j < kl; j++) h = bd_mix(h, bd_kl_word(key, kl, j));
+  return h;
 }
 // host form (byte loads); blockdev.hip has the word-load form of the same function
 inline uint64_t bd_ident_hash(const uint8_t *msp, uint32_t ml, const uint8_t *idb, uint32_t il) {

@@ -282,6 +282,162 @@ DEV bool msp_known(const DevChannel &ch, S mspid) {
   return false;
 }
 
+// ------------------------------------------------------------ key-level state keys
+// == bd_kl_hash (blockdev.h), word loads
+DEV uint64_t kl_hash(S ns, S coll, S key) {
+  uint64_t h = bd_mix(0x6A09E667F3BCC908ull, ((uint64_t)ns.n << 32) | coll.n);
+  h = bd_mix(h, key.n);
+  for (uint32_t j = 0; 4u * j < ns.n; j++) h = bd_mix(h, ld4(ns.p + 4u * j) & lo_mask(ns.n - 4u * j));
+  for (uint32_t j = 0; 4u * j < coll.n; j++) h = bd_mix(h, ld4(coll.p + 4u * j) & lo_mask(coll.n - 4u * j));
+  for (uint32_t j = 0; 4u * j < key.n; j++) h = bd_mix(h, ld4(key.p + 4u * j) & lo_mask(key.n - 4u * j));
+  return h;
+}
+// the committed VALIDATION_PARAMETER of (ns, coll, key): its policy, -3 (it does not unmarshal),
+// -1 none (Channel::kv_policy)
+DEV int32_t kvp_find(const DevChannel &ch, uint64_t h, S ns, S coll, S key) {
+  if (!ch.kvp) return -1;
+  for (uint32_t pos = (uint32_t)h & ch.kvp_mask;; pos = (pos + 1) & ch.kvp_mask) {
+    const uint32_t *e = ch.kvp + 8u * pos;
+    if (!e[7]) return -1;
+    if (e[0] == (uint32_t)h && e[1] == (uint32_t)(h >> 32) && e[3] == ns.n && e[4] == coll.n && e[5] == key.n) {
+      const uint8_t *a = ch.kvp_bytes + e[2];
+      if (s_eq(S{a, ns.n}, ns) && s_eq(S{a + ns.n, coll.n}, coll) && s_eq(S{a + ns.n + coll.n, key.n}, key))
+        return (int32_t)e[6];
+    }
+  }
+}
+
+// The written keys of a TxReadWriteSet that decoded in full (DevTx::results; every decode below
+// succeeds): f(ns, coll, key, kind, is_delete) for the public writes (kind 0) and metadata writes
+// (1) of each namespace, then each collection's hashed writes (0) and hashed metadata writes (1)
+// -- validator_keylevel.go:87-143's four lists (the order does not matter to the callers).
+struct KWrite {  // KVWrite / KVWriteHash: key (hash) = 1, is_delete = 2
+  S key{nullptr, 0};
+  bool del = false;
+  bool hashed = false;
+  DEV Kind kind(uint32_t n) {
+    return n == 1 ? (hashed ? K_BYTES : K_STRING) : (n == 2 || (hashed && n == 4)) ? K_VARINT : n == 3 ? K_BYTES : K_NONE;
+  }
+  DEV void on_varint(uint32_t n, uint64_t v) {
+    if (n == 2) del = v != 0;
+  }
+  DEV bool on_len(uint32_t n, S s, bool &) {
+    if (n == 1) key = s;
+    return true;
+  }
+};
+struct KMeta {  // KVMetadataWrite / KVMetadataWriteHash: key (hash) = 1, entries = 2
+  S key{nullptr, 0};
+  bool hashed = false;
+  DEV Kind kind(uint32_t n) { return n == 1 ? (hashed ? K_BYTES : K_STRING) : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &) {
+    if (n == 1) key = s;
+    return true;
+  }
+};
+template <class F>
+struct KKeys {  // KVRWSet (writes = 3, metadata_writes = 4) or HashedRWSet (2, 3)
+  F *f;
+  S ns, coll;
+  bool hashed;
+  DEV Kind kind(uint32_t n) { return (n >= 1 && n <= (hashed ? 3u : 4u)) ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &ovf) {
+    if (n == (hashed ? 2u : 3u)) {
+      KWrite w;
+      w.hashed = hashed;
+      if (!decode(s, w, ovf)) return false;
+      (*f)(ns, coll, w.key, 0, w.del);
+    } else if (n == (hashed ? 3u : 4u)) {
+      KMeta m;
+      m.hashed = hashed;
+      if (!decode(s, m, ovf)) return false;
+      (*f)(ns, coll, m.key, 1, false);
+    }
+    return true;
+  }
+};
+struct KColl {  // CollectionHashedReadWriteSet: collection_name = 1, hashed_rwset = 2
+  S name{nullptr, 0}, hashed{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : (n == 2 || n == 3) ? K_BYTES : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &) {
+    if (n == 1) name = s;
+    else if (n == 2) hashed = s;
+    return true;
+  }
+};
+template <class F>
+struct KColls {  // NsReadWriteSet.collection_hashed_rwset (3), in order
+  F *f;
+  S ns;
+  DEV Kind kind(uint32_t n) { return n == 3 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) {
+    KColl c;
+    if (!decode(s, c, ovf)) return false;
+    KKeys<F> k{f, ns, c.name, true};
+    return decode(c.hashed, k, ovf);
+  }
+};
+struct KNs {  // NsReadWriteSet: namespace = 1, rwset = 2 (collections: KColls)
+  S ns{nullptr, 0}, rwset{nullptr, 0};
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : n == 3 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t n, S s, bool &) {
+    if (n == 1) ns = s;
+    else if (n == 2) rwset = s;
+    return true;
+  }
+};
+// the keys of one NsReadWriteSet message `nsmsg` whose namespace is `ns` and KVRWSet `kv`
+template <class F>
+DEV bool ns_keys(S ns, S kv, S nsmsg, F &f, bool &ovf) {
+  KKeys<F> k{&f, ns, S{nullptr, 0}, false};
+  if (!decode(kv, k, ovf)) return false;
+  KColls<F> c{&f, ns};
+  return decode(nsmsg, c, ovf);
+}
+template <class F>
+struct KTx {  // TxReadWriteSet: ns_rwset = 2
+  F *f;
+  DEV Kind kind(uint32_t n) { return n == 1 ? K_VARINT : n == 2 ? K_REP_MSG : K_NONE; }
+  DEV void on_varint(uint32_t, uint64_t) {}
+  DEV bool on_len(uint32_t, S s, bool &ovf) {
+    KNs n;
+    if (!decode(s, n, ovf)) return false;
+    return ns_keys(n.ns, n.rwset, s, *f, ovf);
+  }
+};
+template <class F>
+DEV bool tx_keys(S results, F &f, bool &ovf) {
+  KTx<F> t{&f};
+  return decode(results, t, ovf);
+}
+
+// a chained record (k_bd_parse): false when the table is full (host parser)
+DEV bool kl_insert(const KlDev &kl, const uint8_t *base, uint32_t t, uint32_t blk, uint32_t kind, S ns, S coll, S key) {
+  const uint32_t r = atomicAdd(kl.cnt, 1u);
+  if (r >= kl.rcap) return false;
+  const uint64_t h = kl_hash(ns, coll, key);
+  KlRec &R = kl.rec[r];
+  R.hash = h;
+  R.tx = t;
+  R.blk = blk;
+  R.kind = kind;
+  R.ns_off = (uint32_t)(ns.p - base);
+  R.ns_len = ns.n;
+  R.coll_off = coll.n ? (uint32_t)(coll.p - base) : 0u;
+  R.coll_len = coll.n;
+  R.key_off = key.n ? (uint32_t)(key.p - base) : 0u;
+  R.key_len = key.n;
+  const unsigned long long old =
+      atomicExch(&kl.head[(uint32_t)h & kl.hmask], ((unsigned long long)kl.seq << 32) | (r + 1u));
+  R.next = (uint32_t)(old >> 32) == kl.seq ? (uint32_t)old : 0u;
+  return true;
+}
+
 }  // namespace
 
 // ============================================================ k_bd_parse
@@ -308,8 +464,10 @@ struct VCcActionPayloadChk {
   }
 };
 enum : uint8_t { X_OK = 0, X_FAIL = 1, X_PANIC = 2, X_UNKNOWN = 0xFF };
-// metadata writes of a TxReadWriteSet (rwset.FromProtoBytes: a decode error -> none)
-DEV bool rwset_md(S results, ParseLds &L, uint32_t lane, bool &ovf) {
+// metadata writes of a TxReadWriteSet (rwset.FromProtoBytes: a decode error -> none); rw_ok:
+// the whole rwset decodes
+DEV bool rwset_md(S results, ParseLds &L, uint32_t lane, bool &ovf, bool &rw_ok) {
+  rw_ok = false;
   VTxRwSet rw;
   rw.L = &L;
   rw.lane = lane;
@@ -320,12 +478,15 @@ DEV bool rwset_md(S results, ParseLds &L, uint32_t lane, bool &ovf) {
     if (!decode(L.rwset[k][lane], kv, ovf) || (L.cw[k][lane] & 2)) return false;
     md |= kv.nmeta != 0 || (L.cw[k][lane] & 4) != 0;
   }
+  rw_ok = true;
   return md;
 }
 // extractDependenciesForTx (validator_keylevel.go:184-222) for a tx whose validation walk
-// stopped before its ChaincodeAction (fgv_block.cpp extract_walk)
-DEV uint8_t extract_walk(S d, ParseLds &L, uint32_t lane, bool &md, bool &ovf) {
+// stopped before its ChaincodeAction (fgv_block.cpp extract_walk); `results`: the rwset bytes
+// when X_OK
+DEV uint8_t extract_walk(S d, ParseLds &L, uint32_t lane, bool &md, S &results, bool &rw_ok, bool &ovf) {
   md = false;
+  rw_ok = false;
   VTwoBytes env;
   if (!decode(d, env, ovf)) return X_FAIL;
   VPayload pl;
@@ -340,18 +501,23 @@ DEV uint8_t extract_walk(S d, ParseLds &L, uint32_t lane, bool &md, bool &ovf) {
   if (!decode(cap.action.prp, prp, ovf)) return X_FAIL;
   VCcAction cca;
   if (!decode(prp.b, cca, ovf)) return X_FAIL;
-  md = rwset_md(cca.results, L, lane, ovf);
+  results = cca.results;
+  md = rwset_md(cca.results, L, lane, ovf, rw_ok);
   return X_OK;
 }
 
 // fgv_block.cpp parse_tx, speculatively past the creator lookup (resolved by k_bd_ident;
 // k_bd_count applies the creator decision before anything downstream reads the rest).
-// Metadata writes and writes to namespaces with key-level parameters send the batch to the host
-// parser (flag 1); dependency-extraction failures and panics are recorded per block (xhaz).
+// Key-level endorsement (kl.on): a namespace with committed VALIDATION_PARAMETERs or with
+// metadata writes in this tx resolves its policies key by key (sbe_vscc's steps against the
+// committed state), and the tx's metadata writes / deletes of parameter-holding keys go to the
+// batch's record table (k_bd_kl).  Without kl.on (a shard of a batch) such a tx sends the batch
+// to the host parser (flag 1).  Dependency-extraction failures and panics are recorded per block
+// (xhaz).
 __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                  const uint64_t *__restrict__ bases, DevChannel ch,
                                                  DevTx *__restrict__ out, uint32_t *__restrict__ flags,
-                                                 uint32_t *__restrict__ xhaz) {
+                                                 uint32_t *__restrict__ xhaz, KlDev kl) {
   // front half: below the back half's verify chain (3), above k_bd_sha_payload (1)
   __builtin_amdgcn_s_setprio(2);
   __shared__ ParseLds L;
@@ -369,7 +535,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
     int32_t type;
     DSpan payload, env_sig, nonce, creator, chdr, act_hdr, ccpp, prop_hash, prp, txid;
     DSpan idx_nonce, idx_creator, index_txid;
-    uint8_t npol, nend;
+    uint8_t npol, nend, nwr;
   } R;
   R.blk = blk;
   R.pre = C_PENDING;
@@ -382,9 +548,11 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
   R.idx_nonce = R.idx_creator = R.index_txid = z;
   R.npol = 0;
   R.nend = 0;
+  R.nwr = 0;
   bool ovf = false;
   uint8_t xs = X_UNKNOWN;
-  bool md = false, vpns = false;
+  bool md = false, vpns = false, rw_ok = false;
+  S results{nullptr, 0};
   do {
     VTwoBytes env;
     if (!decode(d, env, ovf)) { R.pre = C_OTHER; break; }
@@ -456,6 +624,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
     VCcAction cca;
     if (!decode(prp.b, cca, ovf)) { R.disp = C_BAD_RESP; break; }
     xs = X_OK;  // (the dependency extraction decodes the same messages)
+    results = cca.results;
     VTxRwSet rw;
     rw.L = &L;
     rw.lane = lane;
@@ -471,6 +640,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
                             (kv.nwrites ? 4 : 0));
     }
     if (bad_rw) { R.disp = ovf ? C_UNSUPPORTED : C_BAD_RWSET; break; }
+    rw_ok = true;
     for (uint32_t k = 0; k < rw.nns; k++) md |= (wflags[k] & 2) != 0;
     if (!ext.has_ccid || !cca.has_ccid) { R.disp = C_OTHER; break; }
     const S ccid = ext.ccid.name;
@@ -496,6 +666,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
       }
     }
     if (ovf) break;
+    R.nwr = (uint8_t)nwr;
     for (uint32_t i = 1; i < nwr; i++)  // insertion sort
       for (uint32_t j = i; j > 0 && s_lt(L.wr[j][lane], L.wr[j - 1][lane]); j--) {
         const S tmp = L.wr[j][lane];
@@ -526,6 +697,46 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
         R.flags |= BDF_VW;
         vpns |= e[7] != 0;
       }
+      if (kl.on && k >= 0 && (e[7] != 0 || (wflags[k] & 2))) {
+        // key by key (fgv_block.cpp sbe_vscc against the committed state; an earlier metadata
+        // writer of the block is k_bd_kl's and the fold's): its parameter, else the collection
+        // EP once, else the chaincode EP once; no key -> the chaincode EP
+        bool some = false, cc_checked = false;
+        uint32_t ncc = 0;  // collections whose EP was pushed: L.coll[0 .. ncc)
+        auto step = [&](S ns, S coll, S key, int, bool) {
+          some = true;
+          const int32_t pi = kvp_find(ch, kl_hash(ns, coll, key), ns, coll, key);
+          if (pi == -3) { push(-2); return; }  // untranslatable: the reference halts
+          if (pi >= 0) { push(pi); return; }
+          if (coll.n) {
+            for (uint32_t c = 0; c < ncc; c++)
+              if (s_eq(L.coll[c][lane], coll)) return;
+            int32_t cp;
+            const uint32_t pl = 14;  // "_implicit_org_"
+            if (coll.n >= pl && ld4(coll.p) == 0x706d695fu && ld4(coll.p + 4) == 0x6963696cu &&
+                ld4(coll.p + 8) == 0x726f5f74u && (ld4(coll.p + 12) & 0xFFFFu) == 0x5f67u) {
+              cp = name_find(ch, ch.impl, ch.nimpl, S{coll.p + pl, coll.n - pl}, -2);
+              if (cp == -2) { push(-2); return; }
+            } else {
+              if (!e[4]) { push(-2); return; }
+              cp = name_find(ch, ch.colls + BD_COLL_WORDS * e[5], e[6], coll, -3);
+              if (cp == -3) { push(0); return; }  // no such collection -> policyErr
+            }
+            if (cp >= 0) {
+              push(cp);
+              if (ncc < BD_MAX_COLL) L.coll[ncc++][lane] = coll;
+              return;
+            }
+          }
+          if (!cc_checked) {
+            push(ep);
+            cc_checked = true;
+          }
+        };
+        if (!ns_keys(L.ns[k][lane], L.rwset[k][lane], L.msg[k][lane], step, ovf)) ovf = true;
+        if (!some) push(ep);
+        continue;
+      }
       bool any = false;
       if (k >= 0 && (wflags[k] & 4)) { push(ep); any = true; }
       if (k >= 0 && (L.cw[k][lane] & 1)) {
@@ -555,10 +766,22 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
     R.nend = (uint8_t)cap.action.nend;
     for (uint32_t q = 0; q < np; q++) O.pol[q] = L.pol[q][lane];
   } while (0);
-  if (xs == X_UNKNOWN && !ovf) xs = extract_walk(d, L, lane, md, ovf);
+  if (xs == X_UNKNOWN && !ovf) xs = extract_walk(d, L, lane, md, results, rw_ok, ovf);
   if (xs == X_FAIL) atomicMin(&xhaz[2 * blk], t + 1);
   if (xs == X_PANIC) atomicMin(&xhaz[2 * blk + 1], t + 1);
-  if (ovf || md || vpns) atomicOr(flags, 1u);  // capacity, or key-level endorsement: host parser
+  if (!rw_ok || xs != X_OK) results = S{nullptr, 0};
+  if (kl.on && !ovf && results.n && (md || ch.kvp)) {
+    // ExtractValidationParameterDependency's metadata writes, and the deletes that clear a
+    // committed parameter (oracle keylevel_writes: the key-level changes of the batch)
+    bool full = false;
+    auto rec = [&](S ns, S coll, S key, int kind, bool del) {
+      if (kind == 1) full |= !kl_insert(kl, base, t, blk, KL_MD, ns, coll, key);
+      else if (del && kvp_find(ch, kl_hash(ns, coll, key), ns, coll, key) != -1)
+        full |= !kl_insert(kl, base, t, blk, KL_DEL, ns, coll, key);
+    };
+    if (!tx_keys(results, rec, ovf) || full) ovf = true;
+  }
+  if (ovf || ch.force_host || (!kl.on && (md || vpns))) atomicOr(flags, 1u);  // capacity / a shard: host parser
   O.blk = R.blk;
   O.pre = R.pre;
   O.etx = R.etx;
@@ -580,6 +803,9 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
   O.index_txid = R.index_txid;
   O.npol = R.npol;
   O.nend = R.nend;
+  O.nwr = R.nwr;
+  O.kln = 0;
+  O.results = rel(base, results);
 }
 
 // ============================================================ k_bd_ident
@@ -1446,6 +1672,114 @@ DEV uint32_t hex_word(const uint32_t *dw, uint32_t j) {
 
 }  // namespace
 
+// ============================================================ k_bd_kl
+// Per transaction whose rwset decoded, every written key (oracle keylevel_writes' `touched`)
+// against the batch's key-level records (k_bd_parse): a change by an earlier block of the batch
+// -> unsupported (flag 2; oracle check_keylevel_batch); a metadata write by an earlier
+// transaction of its block -> a dependency (validation_parameter_updated): the writer goes to the
+// transaction's list and the transaction to its block's dependent list, which k_bd_fold walks in
+// block order.  Launched for the fused single-device call only; no records: nothing to do.
+__global__ __launch_bounds__(256) void k_bd_kl(uint32_t ntx, DevTx *__restrict__ txs,
+                                               const uint64_t *__restrict__ bases, KlDev kl,
+                                               uint32_t *__restrict__ flags) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx || *kl.cnt == 0) return;
+  DevTx &R = txs[t];
+  if (!R.results.len) return;
+  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
+  uint32_t deps[KL_DEPS];
+  uint32_t nd = 0;
+  bool over = false, unsup = false;
+  auto chk = [&](S ns, S coll, S key, int, bool) {
+    const uint64_t h = kl_hash(ns, coll, key);
+    const unsigned long long hv = kl.head[(uint32_t)h & kl.hmask];
+    if ((uint32_t)(hv >> 32) != kl.seq) return;
+    for (uint32_t r = (uint32_t)hv; r;) {
+      const KlRec &E = kl.rec[r - 1];
+      r = E.next;
+      if (E.hash != h || E.blk > R.blk || E.ns_len != ns.n || E.coll_len != coll.n || E.key_len != key.n) continue;
+      if (E.blk == R.blk && (E.kind != KL_MD || E.tx >= t)) continue;
+      const uint8_t *eb = reinterpret_cast<const uint8_t *>(bases[E.blk]);
+      if (!s_eq(S{eb + E.ns_off, ns.n}, ns) || !s_eq(S{eb + E.coll_off, coll.n}, coll) ||
+          !s_eq(S{eb + E.key_off, key.n}, key))
+        continue;
+      if (E.blk < R.blk) {
+        unsup = true;
+        continue;
+      }
+      bool seen = false;
+      for (uint32_t q = 0; q < nd; q++) seen |= deps[q] == E.tx;
+      if (seen) continue;
+      if (nd == KL_DEPS) over = true;
+      else deps[nd++] = E.tx;
+    }
+  };
+  bool ovf = false;
+  if (!tx_keys(absl(base, R.results), chk, ovf) || ovf) over = true;
+  if (unsup) atomicOr(flags, 2u);
+  if (over) atomicOr(flags, 1u);  // (capacity: host parser)
+  if (nd == 0) return;
+  for (uint32_t q = 0; q < nd; q++) kl.dep[(size_t)t * KL_DEPS + q] = deps[q];
+  R.kln = (uint8_t)nd;
+  const uint32_t slot = atomicAdd(&kl.blk[KL_BLK_WORDS * R.blk + 3], 1u);
+  if (slot >= KL_MAXDEP) {
+    atomicOr(flags, 1u);
+    return;
+  }
+  kl.deplist[(size_t)R.blk * KL_MAXDEP + slot] = t;
+}
+
+namespace {
+// The dependent transactions of block b in block order (BlockContext.validation_parameter_updated
+// restated): once every transaction of the block is folded, each dependent's vscc -- when it
+// ran -- fails if an earlier metadata writer's vscc for the namespace returned nil, and cannot be
+// decided (the reference waits forever, or Go map order decides) when a writer's never ran or
+// ran beside another failing namespace.  A dependent decided here is final before any later one
+// reads it.  Codes are the fused finalize's (ledger duplicates of earlier blocks included, before
+// markTXIdDuplicates).  Transactions with several vscc namespaces are decided only when the
+// answer needs no per-namespace result (a VALID writer); otherwise unsupported.
+// a byte another workgroup of this launch wrote (device-coherent load of its word)
+DEV uint8_t ld_code(const uint8_t *f, uint32_t i) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(f + (i & ~3u));
+  return (uint8_t)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8u * (i & 3u)));
+}
+__device__ __noinline__ void kl_walk_block(uint32_t b, const DevTx *txs, const KlDev &kl, const FinDev &fin,
+                                           fgv_tx_result *res, uint32_t *flags) {
+  const uint32_t nd = min(kl.blk[KL_BLK_WORDS * b + 3], (uint32_t)KL_MAXDEP);
+  uint32_t list[KL_MAXDEP];
+  for (uint32_t i = 0; i < nd; i++) {
+    const uint32_t v = kl.deplist[(size_t)b * KL_MAXDEP + i];
+    uint32_t j = i;
+    for (; j > 0 && list[j - 1] > v; j--) list[j] = list[j - 1];
+    list[j] = v;
+  }
+  for (uint32_t i = 0; i < nd; i++) {
+    const uint32_t t = list[i];
+    const DevTx &D = txs[t];
+    uint8_t code = ld_code(fin.flags, t);
+    const bool dfr = code == C_UNSUPPORTED && ld_code(reinterpret_cast<const uint8_t *>(res), (uint32_t)(t * sizeof(fgv_tx_result) + 2));
+    const bool ran = code == C_VALID || code == C_POLICY || (D.nwr > 1 && code == C_INVALID_CC) || dfr;
+    if (!ran) continue;
+    bool upd = false, bad = D.nwr != 1;
+    for (uint32_t q = 0; q < D.kln; q++) {
+      const uint32_t j = kl.dep[(size_t)t * KL_DEPS + q];
+      const uint8_t cj = ld_code(fin.flags, j);
+      if (cj == C_VALID) upd = true;              // its vscc of every namespace returned nil
+      else if (!(cj == C_POLICY && txs[j].nwr == 1)) bad = true;  // never ran / map order
+    }
+    if (bad || (dfr && !upd)) {
+      code = C_UNSUPPORTED;
+      atomicOr(flags, 2u);
+    } else if (upd) {
+      code = C_POLICY;  // ValidationParameterUpdatedError -> policyErr
+    }
+    fin.flags[t] = code;
+    res[t].code = code;
+    res[t].pad[0] = 0;
+  }
+}
+}  // namespace
+
 __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__restrict__ txs,
                                                  const uint64_t *__restrict__ bases, DevChannel ch,
                                                  const int32_t *__restrict__ ident,
@@ -1454,7 +1788,7 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
                                                  const uint8_t *__restrict__ digests,
                                                  const uint8_t *__restrict__ vstatus,
                                                  fgv_tx_result *__restrict__ res, uint32_t *__restrict__ flags,
-                                                 const uint32_t *__restrict__ xhaz, FinDev fin) {
+                                                 const uint32_t *__restrict__ xhaz, FinDev fin, KlDev kl) {
   __builtin_amdgcn_s_setprio(3);  // back half; a next batch's front half may run beside it
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
@@ -1465,7 +1799,7 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
   // digests: k_bd_sha's slots
   const size_t kT = (size_t)BD_DIG_T * ntx + t, kP = (size_t)BD_DIG_P * ntx + t, kI = (size_t)BD_DIG_I * ntx + t;
   uint8_t code;
-  bool reached = false;
+  bool reached = false, defer = false;
   const uint8_t *txd = nullptr;
   if (R.pre != C_PENDING) {
     code = R.pre;
@@ -1530,7 +1864,8 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
           seen[nids] = I.canon;
           ids[nids++] = e;
         }
-        bool has25 = false, has10 = false;
+        bool has25 = false, has10 = false, st = false;
+        for (uint32_t i = 0; i < R.npol; i++) st |= R.pol[i] == -2;
         code = C_VALID;
         for (uint32_t i = 0; i < R.npol && !unsup; i++) {
           const int pi = R.pol[i];
@@ -1541,6 +1876,10 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
           if (v == 2) { unsup = true; break; }
           if (v != 1) has10 = true;
         }
+        // a dependent transaction whose policies could not be evaluated (an identity or principal
+        // outside the model) is decided by the block walk: an updated key fails its vscc before
+        // any evaluation matters (validation_parameter_updated)
+        defer = unsup && !st && R.kln && kl.on && fin.owner;
         if (unsup) code = C_UNSUPPORTED;
         else if (has25 && has10) code = C_UNSUPPORTED;
         else if (has25) code = C_INVALID_CC;
@@ -1548,7 +1887,7 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
       }
     }
   }
-  if (code == C_UNSUPPORTED) atomicOr(flags, 2u);
+  if (code == C_UNSUPPORTED && !defer) atomicOr(flags, 2u);
   if (fin.owner) {  // k_fin_codes (finalize.hip) for the single-device fused call
     uint32_t slot = 0xFFFFFFFFu;
     uint8_t c2 = code;
@@ -1570,7 +1909,8 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
   fgv_tx_result o;
   o.code = code;
   o.flags = 0;
-  o.pad[0] = o.pad[1] = 0;
+  o.pad[0] = defer ? 1 : 0;  // (read by the block walk)
+  o.pad[1] = 0;
   for (int k = 0; k < 32; k++) o.txid[k] = o.index_txid[k] = 0;
   if (reached) {
     for (int k = 0; k < 32; k++) o.txid[k] = txd[k];
@@ -1586,4 +1926,16 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
     }
   }
   res[t] = o;
+  if (kl.on && *kl.cnt) {  // a batch with key-level changes
+    if (!fin.owner) {      // (the ordered walk reads the fused finalize's codes: host parser)
+      atomicOr(flags, 1u);
+      return;
+    }
+    __threadfence();
+    uint32_t *bw = kl.blk + KL_BLK_WORDS * R.blk;
+    if (atomicAdd(&bw[2], 1u) + 1u == bw[1]) {  // the block's last transaction to finish
+      __threadfence();
+      if (bw[3]) kl_walk_block(R.blk, txs, kl, fin, res, flags);
+    }
+  }
 }

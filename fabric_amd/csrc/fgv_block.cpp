@@ -44,6 +44,7 @@
 #include "fgv_channel.h"
 #include "blockdev.h"
 #include "fin_dev.h"
+#include "sha256_host.h"
 
 // ======================================================================= channel model
 // (fgv_channel.h)
@@ -107,11 +108,12 @@ using namespace fgvb;
 
 // channel model image in HBM for the device-resident path (blockdev.h DevChannel)
 struct DevImage {
-  DevBuf name, idents, ibytes, itable, ihash, cc, colls, impl, msps, ccb, pol, nodes, kids, subs, prins, iou, committed;
+  DevBuf name, idents, ibytes, itable, ihash, cc, colls, impl, msps, ccb, pol, nodes, kids, subs, prins, iou, committed,
+      kvp, kvpb;
   DevChannel ch{};
   void release() {
     for (DevBuf *b : {&name, &idents, &ibytes, &itable, &ihash, &cc, &colls, &impl, &msps, &ccb, &pol, &nodes, &kids,
-                      &subs, &prins, &iou, &committed})
+                      &subs, &prins, &iou, &committed, &kvp, &kvpb})
       b->release();
   }
 };
@@ -204,6 +206,9 @@ struct PreSplit {
 // batch k's back half (verify jobs, ECDSA, fold -- the main stream) runs.
 struct BdSet {
   DevBuf env, tx, ident, jobs, dig;  // env: envelope table | block bases | counters (the head)
+  DevBuf klrec, klhead, kldep, kllist;  // key-level records, their buckets, dependencies (blockdev.h KlDev)
+  uint32_t klseq = 0;                   // the bucket tag of the batch this set holds
+  KlDev kl{};
   HostBuf head, misc;                // pinned head staging / counters read back
   // 0 start, 1 payload hashes done (stream2), 2 k_bd_sha done (stream3), 3 head uploaded,
   // 4 parse done, 5 k_bd_sha start, 6 counts done, 7 k_bd_ident start (0, 5, 7: timing only),
@@ -231,7 +236,7 @@ struct BdSet {
     return true;
   }
   void release() {
-    for (DevBuf *b : {&env, &tx, &ident, &jobs, &dig}) b->release();
+    for (DevBuf *b : {&env, &tx, &ident, &jobs, &dig, &klrec, &klhead, &kldep, &kllist}) b->release();
     head.release();
     misc.release();
     for (auto &e : ev)
@@ -256,6 +261,7 @@ struct fgv_block_state {
   int last = 1;    // set of the last call
   int pending = -1;           // set enqueued by _enqueue and not yet finished
   double nv_per_tx = 0;       // verifies per tx of the last batch (lanes-per-verify estimate)
+  uint32_t klseq = 0;         // key-level bucket tags (blockdev.h KlDev::seq), one per front half
   std::chrono::steady_clock::time_point t_enq;
   explicit fgv_block_state(unsigned threads) : pool(threads) {}
   ~fgv_block_state() {
@@ -823,6 +829,33 @@ static void kl_keys(const Channel &ch, const Span &results, std::vector<std::str
   touched.insert(touched.end(), t.begin(), t.end());
 }
 
+// GetOrComputeTxIDFromEnvelope (protoutil/txutils.go:503-534): the txid index entry of one
+// envelope (chdr.TxId, or hex(SHA-256(nonce || creator)) when it is empty); false: none
+static bool index_entry(const Span &d, std::string &out) {
+  VEnvelope env;
+  VPayload pl;
+  VHeader hdr;
+  if (!pbw::decode(d.p, d.n, env) || !pbw::decode(env.payload.p, env.payload.n, pl) || !pl.header.decode_into(hdr) ||
+      !pl.header.present)
+    return false;
+  VChannelHeader c0;
+  if (!pbw::decode(hdr.channel_header.p, hdr.channel_header.n, c0)) return false;
+  if (c0.tx_id.n) {
+    out.assign(reinterpret_cast<const char *>(c0.tx_id.p), c0.tx_id.n);
+    return true;
+  }
+  VSignatureHeader s0;
+  if (!pbw::decode(hdr.signature_header.p, hdr.signature_header.n, s0)) return false;
+  std::string m(reinterpret_cast<const char *>(s0.nonce.p), s0.nonce.n);
+  m.append(reinterpret_cast<const char *>(s0.creator.p), s0.creator.n);
+  uint8_t dg[32];
+  fgvsha::sha256(reinterpret_cast<const uint8_t *>(m.data()), m.size(), dg);
+  static const char HX[] = "0123456789abcdef";
+  out.resize(64);
+  for (int k = 0; k < 32; k++) out[2 * k] = HX[dg[k] >> 4], out[2 * k + 1] = HX[dg[k] & 15];
+  return true;
+}
+
 static inline uint32_t sha_blocks(const ShaJob &j) { return (j.n[0] + j.n[1] + j.n[2] + 8) / 64 + 1; }
 
 int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
@@ -1034,6 +1067,39 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     }
     c->kl_changes = !changed.empty();
   }
+  // A metadata writer whose txid an earlier block of the batch indexes is a ledger duplicate in the
+  // reference (block k's txids are committed before block k+1 validates), so its vscc never runs
+  // and a later dependent waits forever.  The first block indexing each txid (every block the
+  // call has bytes for; a block before b without bytes: unknown -> its results are undecided).
+  std::unordered_map<std::string, uint32_t> first_index;
+  std::vector<uint8_t> index_unknown(nblocks, 0);
+  if (sequential && nblocks > 1) {
+    std::vector<std::vector<std::string>> keys(nblocks);
+    std::vector<uint8_t> nobytes(nblocks, 0);
+    S->pool.run(nblocks, [&](size_t b) {
+      if (tx_lo && tx_lo[b] == FGV_SHARD_SKIP) {
+        VBlock blk;
+        if (!lens[b] || !pbw::decode(h_blocks[b], lens[b], blk)) { nobytes[b] = 1; return; }
+        std::string k;
+        for (const Span &d : blk.data.data)
+          if (index_entry(d, k)) keys[b].push_back(k);
+        return;
+      }
+      std::string k;
+      for (const Span &d : envs[b])
+        if (index_entry(d, k)) keys[b].push_back(k);
+    });
+    bool unknown = false;
+    for (size_t b = 0; b < nblocks; b++) {
+      index_unknown[b] = unknown;
+      unknown |= nobytes[b] != 0;
+      for (std::string &k : keys[b]) first_index.emplace(std::move(k), (uint32_t)b);
+    }
+  }
+  auto batch_dup = [&](const Span &txid, size_t b) {
+    auto it = first_index.find(std::string(reinterpret_cast<const char *>(txid.p), txid.n));
+    return it != first_index.end() && it->second < b;
+  };
   static const char HEX[] = "0123456789abcdef";
   // pass 0: no key-level state (parallel); 1: key-level, every tx in parallel, a tx whose written
   // key has an earlier metadata writer only marked; 2: the marked txs again, in block order
@@ -1066,6 +1132,8 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         code = C_BAD_ETX;
       } else if ((reached = true, ch.is_committed(R.txid))) {
         code = C_DUP_TXID;  // checkTxIdDupsLedger (initial ledger; batch-earlier blocks: finalize)
+      } else if (pass != 0 && batch_dup(R.txid, b)) {
+        code = C_DUP_TXID;  // (the finalize marks it too; here its vscc must not run)
       } else if (R.disp != C_VALID) {
         code = R.disp;
       } else if ((R.vany && xpanic[b] < bi) || (R.vw && xfail[b] < bi)) {
@@ -1151,7 +1219,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
           }
           for (size_t q = 0; q < wr.size(); q++) {
             if (rs[q] != 0 && rs[q] != 1) continue;
-            bool others = false;
+            bool others = index_unknown[b] != 0;  // (it may be a ledger duplicate: undecided)
             for (size_t o = 0; o < wr.size(); o++) others |= o != q && (rs[o] == -1 || rs[o] == 0);
             sbe[b].res[bi].push_back({wr[q].str(), others ? VR_INDET : (int8_t)rs[q]});
           }
@@ -1552,9 +1620,50 @@ static int build_dev_image(fgv_block_state *S) {
       (rc = upload(D.nodes, nodes)) || (rc = upload(D.kids, kids)) || (rc = upload(D.subs, subs)) ||
       (rc = upload(D.prins, prins)))
     return rc;
+  // committed key-level validation parameters (Channel::kvmeta_pi): kvkey = u32 |ns| ns u32
+  // |coll| coll key -> slot (blockdev.h DevChannel::kvp)
+  std::vector<uint32_t> kvp;
+  std::vector<uint8_t> kvpb;
+  size_t kcap = 0;
+  if (!ch.kvmeta_pi.empty()) {
+    kcap = 16;
+    while (kcap < 2 * ch.kvmeta_pi.size()) kcap <<= 1;
+    kvp.assign(kcap * 8, 0);
+    for (const auto &kv : ch.kvmeta_pi) {
+      const std::string &k = kv.first;
+      uint32_t nl, cl;
+      memcpy(&nl, k.data(), 4);
+      memcpy(&cl, k.data() + 4 + nl, 4);
+      const uint8_t *ns = reinterpret_cast<const uint8_t *>(k.data()) + 4;
+      const uint8_t *coll = ns + nl + 4;
+      const uint8_t *key = coll + cl;
+      const uint32_t kl = (uint32_t)(k.size() - 8 - nl - cl);
+      const uint64_t h = bd_kl_hash(ns, nl, coll, cl, key, kl);
+      uint32_t pos = (uint32_t)h & (uint32_t)(kcap - 1);
+      while (kvp[8 * pos + 7]) pos = (pos + 1) & (uint32_t)(kcap - 1);
+      uint32_t *e = &kvp[8 * pos];
+      e[0] = (uint32_t)h;
+      e[1] = (uint32_t)(h >> 32);
+      e[2] = (uint32_t)kvpb.size();
+      e[3] = nl;
+      e[4] = cl;
+      e[5] = kl;
+      e[6] = (uint32_t)kv.second;
+      e[7] = 1;
+      kvpb.insert(kvpb.end(), ns, ns + nl);
+      kvpb.insert(kvpb.end(), coll, coll + cl);
+      kvpb.insert(kvpb.end(), key, key + kl);
+    }
+    kvpb.resize(kvpb.size() + 64, 0);
+    if ((rc = upload(D.kvp, kvp)) || (rc = upload(D.kvpb, kvpb))) return rc;
+  }
   int rc2 = build_committed(S);
   if (rc2) return rc2;
   DevChannel &d = D.ch;
+  d.kvp = kcap ? D.kvp.as<uint32_t>() : nullptr;
+  d.kvp_bytes = kcap ? D.kvpb.as<uint8_t>() : nullptr;
+  d.kvp_mask = kcap ? (uint32_t)(kcap - 1) : 0u;
+  d.force_host = ch.policies.size() > 32767 ? 1u : 0u;  // (DevTx::pol is int16)
   d.name = D.name.as<uint8_t>();
   d.name_len = (uint32_t)name.size();
   d.nident = (uint32_t)idents.size();
@@ -1627,7 +1736,8 @@ static int build_committed(fgv_block_state *S) {
 }
 
 __global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, DevChannel ch, DevTx *out,
-                           uint32_t *flags, uint32_t *xhaz);
+                           uint32_t *flags, uint32_t *xhaz, KlDev kl);
+__global__ void k_bd_kl(uint32_t ntx, DevTx *txs, const uint64_t *bases, KlDev kl, uint32_t *flags);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
@@ -1645,14 +1755,15 @@ __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases,
 __global__ void k_bd_fold(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
                           const DevJobIdx *jobs, const uint32_t *totals, const uint8_t *digests,
                           const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags, const uint32_t *xhaz,
-                          FinDev fin);
+                          FinDev fin, KlDev kl);
 
 // The batch head, one H2D copy: envelope table | block base addresses | 64 zero bytes (the
-// kernels' counters) | per-block dependency-extraction hazards (blockdev.h), each part 64-byte
-// aligned.
+// kernels' counters) | per-block dependency-extraction hazards (blockdev.h) | per-block
+// key-level words (KlDev::blk), each part 64-byte aligned.
 static size_t head_env_bytes(size_t total) { return (total * 4 * BD_ENV_WORDS + 63) & ~(size_t)63; }
+static size_t head_blk_bytes(size_t nblocks) { return (nblocks * 8 + 63) & ~(size_t)63; }
 static size_t head_bytes(size_t total, size_t nblocks) {
-  return head_env_bytes(total) + 2 * ((nblocks * 8 + 63) & ~(size_t)63) + 64;
+  return head_env_bytes(total) + 2 * head_blk_bytes(nblocks) + 64 + ((nblocks * 4 * KL_BLK_WORDS + 63) & ~(size_t)63);
 }
 
 // host: split each block into envelope spans (tag / length walk of the block data framing)
@@ -1806,6 +1917,25 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     if (panic) xh[2 * b + 1] = 0;
     B.force_host |= md;
   }
+  // key-level state of the batch (blockdev.h KlDev): per-block words, records chained in buckets
+  // tagged with this batch's sequence number (no reset between batches)
+  const size_t klb_off = B.moff + 64 + head_blk_bytes(nblocks);
+  uint32_t *klw = reinterpret_cast<uint32_t *>(head + klb_off);
+  for (size_t b = 0; b < nblocks; b++) {
+    klw[KL_BLK_WORDS * b] = (uint32_t)B.so.first[b];
+    klw[KL_BLK_WORDS * b + 1] = (uint32_t)(B.so.hi[b] - B.so.lo[b]);
+    klw[KL_BLK_WORDS * b + 2] = klw[KL_BLK_WORDS * b + 3] = 0;
+  }
+  const size_t rcap = 2 * total + 1024;
+  size_t hcap = 1024;
+  while (hcap < 2 * rcap) hcap <<= 1;
+  const size_t hbuf = B.klhead.cap;
+  if (!B.klrec.ensure(rcap * sizeof(KlRec)) || !B.klhead.ensure(hcap * 8) ||
+      !B.kldep.ensure(total * KL_DEPS * 4) || !B.kllist.ensure(nblocks * KL_MAXDEP * 4))
+    return FGV_ENOMEM;
+  if (B.klhead.cap != hbuf) HIP_TRY(hipMemsetAsync(B.klhead.p, 0, B.klhead.cap, sf));  // (new memory: no stale tag)
+  if (++S->klseq == 0) ++S->klseq;
+  B.klseq = S->klseq;
   const DevChannel ch = S->dimg.ch;
   B.stream = sf;
   if (wait) HIP_TRY(hipStreamWaitEvent(sf, wait, 0));
@@ -1827,7 +1957,18 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(128), 0, c->stream2, N, envtab, dbs,
                      B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
   HIP_TRY(hipEventRecord(B.ev[1], c->stream2));
-  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16);
+  B.kl = KlDev{B.klrec.as<KlRec>(),
+               B.klhead.as<unsigned long long>(),
+               (uint32_t)(hcap - 1),
+               (uint32_t)rcap,
+               B.klseq,
+               (!tx_lo && !tx_hi) ? 1u : 0u,
+               misc + 11,
+               reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + klb_off),
+               B.kllist.as<uint32_t>(),
+               B.kldep.as<uint32_t>()};
+  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16,
+                     B.kl);
   HIP_TRY(hipEventRecord(B.ev[4], sf));
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one
@@ -1917,6 +2058,10 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   // the fused single-device call: its finalize's txid index runs on stream3 right after the
   // batch's digests, beside the verify chain (fgv_finalize_early_index)
   if (c->want_early_fin && !tx_lo && !tx_hi && B.N) {
+    // the key-level dependencies (nothing to do without key-level records), ahead of the index
+    hipLaunchKernelGGL(k_bd_kl, dim3((B.N + 255) / 256), dim3(256), 0, c->stream3, B.N, B.tx.as<DevTx>(),
+                       reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff), B.kl,
+                       reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff) + 5);
     int rc = fgv_finalize_early_index(c, nblocks, B.so.ntx.data(), B.tx.as<DevTx>(),
                                       reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff),
                                       B.dig.as<uint8_t>(), c->stream3);
@@ -1976,9 +2121,10 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
                  c->fz_keys.as<uint8_t>(), c->fz_flags.as<uint8_t>(), c->fz_pslot.as<uint32_t>(),
                  (uint32_t)(cap - 1), c->fin_seed};
     c->fold_codes = true;
+    c->fold_unsup = misc + 5;  // (k_fin_dups: a first VALID position failed by the key-level walk)
   }
   hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
-                     B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5, misc + 16, fin);
+                     B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5, misc + 16, fin, B.kl);
   HIP_TRY(hipGetLastError());
   if (tim || c->ahead_mode == 3) HIP_TRY(hipEventRecord(c->kev[9], st));  // (ahead mode 3 waits on it)
   // (the counters' D2H is queued by fgv_block_validate_dev_finish, behind whatever the caller

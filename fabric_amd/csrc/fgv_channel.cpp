@@ -341,11 +341,20 @@ void Channel::compile() {
   // validation_logic.go:50-66) wraps the SignaturePolicyEnvelope as an ApplicationPolicy, which
   // the evaluator takes without the version check; an envelope that does not unmarshal fails
   // the translation
+  // (identical parameters share one compiled policy: a state typically holds few distinct ones)
   kvmeta_pi.clear();
+  std::unordered_map<std::string_view, int> by_bytes;
   for (const auto &kv : kvmeta) {
+    auto hit = by_bytes.find(kv.second);
+    if (hit != by_bytes.end()) {
+      kvmeta_pi[kv.first] = hit->second;
+      continue;
+    }
     std::vector<Span> one{Span{reinterpret_cast<const uint8_t *>(kv.second.data()), (uint32_t)kv.second.size()}};
     Policy P = compile_spe(*this, one, false);
-    kvmeta_pi[kv.first] = (P.kind == PK_SIG && !P.decode_ok) ? -3 : push_policy(*this, std::move(P));
+    const int pi = (P.kind == PK_SIG && !P.decode_ok) ? -3 : push_policy(*this, std::move(P));
+    by_bytes.emplace(kv.second, pi);
+    kvmeta_pi[kv.first] = pi;
   }
   dirty = false;
 }

@@ -1005,7 +1005,7 @@ static int fin_back(fgv_ctx *c, hipStream_t st, const FinPlan &F, const uint8_t 
                      c->fz_minvalid.as<uint32_t>(), mask, c->fin_seed, c->fz_flags.as<uint8_t>(),
                      c->fz_pslot.as<uint32_t>(), keys);
   hipLaunchKernelGGL(k_fin_dups, grid, blk, 0, st, n32, c->fz_pslot.as<uint32_t>(), c->fz_minvalid.as<uint32_t>(),
-                     c->fz_flags.as<uint8_t>());
+                     c->fz_flags.as<uint8_t>(), codes_done ? c->fold_unsup : nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->hb_fflags.p, c->fz_flags.p, F.P, hipMemcpyDeviceToHost, st));
   return FGV_OK;

@@ -129,6 +129,7 @@ struct fgv_ctx {
   // validate call before the device enqueue, consumed by its finalize
   bool want_early_fin = false, early_fin = false;
   bool fold_codes = false;  // k_bd_fold ran the finalize's codes step (the finalize runs the rest)
+  uint32_t *fold_unsup = nullptr;  // with fold_codes: the batch's flag word (k_fin_dups)
   bool early_fin_on = [] {  // A/B knob FGV_EARLY_FIN=0: the whole finalize after the fold
     const char *e = getenv("FGV_EARLY_FIN");
     return !(e && atoi(e) == 0);

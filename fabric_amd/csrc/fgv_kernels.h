@@ -162,4 +162,4 @@ __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *row
 struct DevTx;
 __global__ void k_fin_index_dev(uint32_t P, const DevTx *txs, const uint64_t *bases, const uint8_t *digests,
                                 uint8_t *keys, uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed);
-__global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags);
+__global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags, uint32_t *unsup);

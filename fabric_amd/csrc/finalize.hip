@@ -209,9 +209,16 @@ __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *row
   pslot[p] = slot;
 }
 
-__global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags) {
+// unsup (the fused single-device call: its batch counters' flag word): the first VALID position
+// of a txid was later failed by the key-level walk (blockdev.hip kl_walk_block), so the txid's
+// first VALID transaction is not known here -> the batch is unsupported (bit 2)
+__global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags,
+                           uint32_t *unsup) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   if (flags[p] != 0 || pslot[p] == 0xFFFFFFFFu) return;
-  if (minvalid[pslot[p]] < p) flags[p] = 9;  // markTXIdDuplicates: an earlier VALID tx of this block
+  const uint32_t m = minvalid[pslot[p]];
+  if (m >= p) return;
+  if (unsup && flags[m] != 0) atomicOr(unsup, 2u);
+  flags[p] = 9;  // markTXIdDuplicates: an earlier VALID tx of this block
 }

@@ -625,6 +625,40 @@ out:
   return ret;
 }
 
+/* the same with the key parsed once (EC_KEY made by oracle_p256_key_new, shared read-only by
+ * threads): what a long-running peer does with its deserialized identities */
+void *oracle_p256_key_new(const uint8_t qx[32], const uint8_t qy[32]) {
+  EC_KEY *key = EC_KEY_new_by_curve_name(NID_X9_62_prime256v1);
+  BIGNUM *bx = BN_bin2bn(qx, 32, NULL), *by = BN_bin2bn(qy, 32, NULL);
+  if (!key || !bx || !by || EC_KEY_set_public_key_affine_coordinates(key, bx, by) != 1) {
+    EC_KEY_free(key);
+    key = NULL;
+  }
+  BN_free(bx);
+  BN_free(by);
+  return key;
+}
+void oracle_p256_key_free(void *key) { EC_KEY_free((EC_KEY *)key); }
+int oracle_p256_verify_der_key(void *key, const uint8_t *sig, size_t sig_len, const uint8_t *digest,
+                               size_t digest_len) {
+  uint8_t r[32], s[32];
+  int big = 0;
+  int st = verify_front(sig, sig_len, digest_len, r, s, &big);
+  if (st) return st;
+  if (!key) return 5;
+  if (big) return 4;
+  const curve_t *C = curve();
+  u256 rv;
+  u256_from_be(&rv, r);
+  if (u256_cmp(&rv, &C->n) >= 0) return 4;
+  ECDSA_SIG *es = ECDSA_SIG_new();
+  BIGNUM *br = BN_bin2bn(r, 32, NULL), *bs = BN_bin2bn(s, 32, NULL);
+  ECDSA_SIG_set0(es, br, bs);
+  const int v = ECDSA_do_verify(digest, (int)digest_len, es, (EC_KEY *)key);
+  ECDSA_SIG_free(es);
+  return v == 1 ? 0 : 1;
+}
+
 /* ------------------------------------------------------- threaded batches */
 
 typedef struct {

@@ -60,6 +60,12 @@ void oracle_verify_msgs_batch(const uint8_t *keys /* n*64: qx||qy */, const uint
 /* Scalar mult helper for tests: out = k*G affine (32B BE x||y); returns 0 or 1 if inf. */
 int oracle_p256_base_mult(const uint8_t k[32], uint8_t out_x[32], uint8_t out_y[32]);
 
+/* key parsed once (oracle_p256_key_new), verified against many times (cpu_validator.c) */
+void *oracle_p256_key_new(const uint8_t qx[32], const uint8_t qy[32]);
+void oracle_p256_key_free(void *key);
+int oracle_p256_verify_der_key(void *key, const uint8_t *sig, size_t sig_len, const uint8_t *digest,
+                               size_t digest_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -284,3 +284,29 @@ def test_updated_key_skips_out_of_model_policy(mode):
     eng = _eng(net.channel, ids, net.chaincodes, None, mode)
     assert list(eng.validate_blocks([blk])[0]) == exp
     eng.close()
+
+
+@MODES
+def test_writer_duplicate_of_earlier_block(mode):
+    """a metadata writer whose txid an earlier block of the batch indexes is a ledger duplicate in
+    the reference (block k's txids are committed before block k+1 validates): its vscc never runs,
+    so a later writer of the same key waits forever -> Unsupported on both sides; the second block
+    alone validates as usual"""
+    net = network()
+    ccs = _net_ccs(net)
+    out = []
+    b1 = blocks.make_block(net, 20, number=1, seed=31, faults=(), out_txs=out)[0]
+    md = sbe_cases._entries({sbe_cases.VP: sbe_cases._spe_any([net.org_peers[0][0].mspid])})
+    rws = [blocks.tx_rwset([("mycc", blocks.f_msg(4, blocks.f_str(1, "dupk") + md), [])])]
+    rws += [blocks.tx_rwset([("mycc", blocks.kv_rwset([], [("dupk", b"v", False)]), [])])] * 5
+    b2 = blocks.make_block(net, 6, number=2, seed=32, faults=(), rwsets=rws,
+                           reuse={0: (out[3].creator, out[3].nonce)})[0]
+    model = lambda: v20.ChannelModel(net.channel, net.identities(), ccs)  # noqa: E731
+    with pytest.raises(v20.Unsupported):
+        v20.validate_blocks(model(), [b1, b2])
+    eng = _eng(net.channel, net.identities(), ccs, None, mode)
+    with pytest.raises(_lib.Unsupported):
+        eng.validate_blocks([b1, b2])
+    exp = _same(eng, model, [b2])
+    assert exp is not None and exp[0][0] == 0 and exp[0].count(10) == 5
+    eng.close()
