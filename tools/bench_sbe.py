@@ -1,8 +1,10 @@
 """Throughput of key-level-endorsement batches (profiling aid, not the bench contract): 32
 generated 500-tx blocks of namespace mycc with key-level parameters in state, metadata writes and
-in-block dependencies (tests/sbe_cases.py) -- the sequential host fold with GPU verification --
-against the same blocks with no key-level state, which the device fold takes.  Parity with the
-oracle is checked on the first batch of each; prints one JSON line."""
+in-block dependencies (tests/sbe_cases.py; each block over its own key space, as a batch whose
+blocks change each other's parameters is outside the model) -- on the device fold (DESIGN.md
+s6a) and, for comparison, on the host parser's sequential fold (parse mode 1) -- against the same
+blocks with no key-level state.  Blocks are host-resident (the call copies them H2D).  Parity with
+the oracle is checked on each configuration; prints one JSON line."""
 import json
 import os
 import sys
@@ -20,16 +22,21 @@ def main():
     net = network()
     ccs = {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
     nb, ntx, steps = 32, 500, 10
-    made = [sbe_cases.make_sbe_block(net, ntx, 5000 + k, number=1 + k, nkeys=2000, vp_keys=400) for k in range(nb)]
+    made = [sbe_cases.make_sbe_block(net, ntx, 5000 + k, number=1 + k, nkeys=2000, vp_keys=400, prefix="b%dk" % k)
+            for k in range(nb)]
     blks = [b for b, _ in made]
     kvmeta = {}
     for _, kv in made:
         kvmeta.update(kv)
-    out = {}
-    for name, kv in (("key_level", kvmeta), ("plain", {})):
+    out, exps = {}, {}
+    for name, kv, mode in (("key_level", kvmeta, 0), ("key_level_hostparse", kvmeta, 1), ("plain", {}, 0)):
         eng = _lib.Engine(0)
+        eng.set_parse_mode(mode)
         txvalidator.setup_channel(eng, net.channel, net.identities(), ccs, kvmeta=kv)
-        exp = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=kv), blks)
+        key = "kl" if kv else "plain"
+        if key not in exps:
+            exps[key] = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=kv), blks)
+        exp = exps[key]
         got = [list(f) for f in eng.validate_blocks(blks)]
         assert got == exp, name
         eng.validate_blocks(blks)
