@@ -83,24 +83,71 @@ def roofline(n_verifies, point_ms, workload):
                 work_unit="v_mad_u64_u32 (32x32->64 multiply-add) products of the comb algorithm")
 
 
-def block_roofline(kavg, pay_blocks, verifies, workload):
-    """roofline of the committer step's dominant kernel, k_point28 (the longest per-step kernel in
-    the rocprofv3 kernel trace of a 32-block-step run, profiles/round3_block_kernel_stats.csv):
-    v_mad_u64_u32 products of the comb (PRODUCTS_POINT per verify) / its per-step time (HIP
-    events on its own stream) vs the measured 31.06 T/s chip peak.  Second: k_bd_sha_payload,
-    SHA-256 compressions x 2.7e3 int32 ops vs the 78.6 T int32 lane-op peak."""
+def profiled_dominant(workload="block"):
+    """the top row of the latest committed per-step kernel stats (profiles/round*_<workload>_
+    kernel_stats.csv: rocprofv3 --kernel-trace --stats of 32-block steps, the one-time comb
+    table builds excluded) -> (kernel, avg us, file); (None, None, None) without one"""
+    import csv
+    import glob
+    import re
+    files = glob.glob(os.path.join(ROOT, "profiles", f"round*_{workload}_kernel_stats.csv"))
+    if not files:
+        return None, None, None
+    f = max(files, key=lambda p: int(re.search(r"round(\d+)", os.path.basename(p)).group(1)))
+    rows = [r for r in csv.DictReader(open(f)) if not r["Name"].startswith(("k_gtab", "k_keytab"))]
+    if not rows:
+        return None, None, None
+    top = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+    return top["Name"].split("(")[0], float(top["AverageNs"]) / 1e3, os.path.basename(f)
+
+
+def block_roofline(kavg, pay_blocks, verifies, batch_bytes, workload):
+    """roofline of the committer step's dominant kernel: the top row of the committed per-step
+    kernel stats (profiled_dominant), timed live (HIP events on its stream) in this run, with
+    frac_profiled = the same work / that row's average duration (recomputable from the file).
+    Work models:
+      k_point28         v_mad_u64_u32 products of the comb (PRODUCTS_POINT per verify) vs the
+                        measured 31.06 T/s chip peak;
+      k_bd_sha_payload  SHA-256 compressions x 2.7e3 int32 ops vs the 78.6 T
+                        int32 lane-op peak;
+      k_bd_parse        the batch's block bytes (each envelope's lines are requested once) vs
+                        8 TB/s HBM: a walk of dependent loads, so frac says how far from any
+                        throughput bound it runs.
+    The other two are `others`."""
     cands = {k: v for k, v in kavg.items() if k != "batch"}
-    r = roofline(verifies, kavg.get("k_point28", 0.0), workload + "_point")
-    r["dominant_kernel_live"] = max(cands, key=cands.get) if cands else None
-    r["per_launch_verifies"] = int(verifies)
+    dom, dom_us, dom_src = profiled_dominant("block" if workload == "block" else workload)
+    models = {}
+    pt = roofline(verifies, kavg.get("k_point28", 0.0), workload + "_point")
+    pt["per_launch_verifies"] = int(verifies)
+    if dom_us and dom == "k_point28":
+        pt["frac_profiled"] = round(verifies * PRODUCTS_POINT / (dom_us * 1e-6) / PEAK_MAD_PER_S, 4)
+    models["k_point28"] = pt
     t_pay = kavg.get("k_bd_sha_payload", 0.0) / 1e3
     ach = pay_blocks * SHA_OPS_PER_COMPRESSION / t_pay / 1e12 if t_pay > 0 else 0.0
     traffic, src = pmc_traffic(workload)
-    r["second"] = dict(bound="valu", achieved=round(ach, 3), peak=round(PEAK_INT32_OPS / 1e12, 1), unit="Tops/s",
-                       frac=round(ach * 1e12 / PEAK_INT32_OPS, 4), traffic=traffic, traffic_source=src,
-                       kernel="k_bd_sha_payload", kernel_avg_ms=round(t_pay * 1e3, 4),
-                       per_launch_compressions=int(pay_blocks),
-                       work_unit="SHA-256 compressions x 2.7e3 simple int32 ops (SURVEY.md s8(d))")
+    pay = dict(bound="valu", achieved=round(ach, 3), peak=round(PEAK_INT32_OPS / 1e12, 1), unit="Tops/s",
+               frac=round(ach * 1e12 / PEAK_INT32_OPS, 4), traffic=traffic, traffic_source=src,
+               kernel="k_bd_sha_payload", kernel_avg_ms=round(t_pay * 1e3, 4),
+               per_launch_compressions=int(pay_blocks),
+               work_unit="SHA-256 compressions x 2.7e3 simple int32 ops (SURVEY.md s8(d))")
+    if dom_us and dom == "k_bd_sha_payload":
+        pay["frac_profiled"] = round(pay_blocks * SHA_OPS_PER_COMPRESSION / (dom_us * 1e-6) / PEAK_INT32_OPS, 4)
+    models["k_bd_sha_payload"] = pay
+    t_parse = kavg.get("k_bd_parse", 0.0) / 1e3
+    gbs = batch_bytes / t_parse / 1e9 if t_parse > 0 else 0.0
+    ptr, psrc = pmc_traffic(workload + "_parse")
+    parse = dict(bound="hbm", achieved=round(gbs, 2), peak=8000.0, unit="GB/s", frac=round(gbs / 8000.0, 5),
+                 traffic=ptr, traffic_source=psrc, kernel="k_bd_parse", kernel_avg_ms=round(t_parse * 1e3, 4),
+                 per_launch_bytes=int(batch_bytes),
+                 work_unit="block bytes of the batch (every envelope line requested once, touch_lines)")
+    if dom_us and dom == "k_bd_parse":
+        parse["frac_profiled"] = round(batch_bytes / (dom_us * 1e-6) / 8e12, 5)
+    models["k_bd_parse"] = parse
+    key = dom if dom in models else "k_point28"
+    r = dict(models[key])
+    r["others"] = {k: v for k, v in models.items() if k != key}
+    r["dominant_kernel_profiled"] = dict(kernel=dom, avg_us=dom_us, source=dom_src)
+    r["dominant_kernel_live"] = max(cands, key=cands.get) if cands else None
     return r
 
 
@@ -541,7 +588,8 @@ def run_block(args, world, rank, local, dev_fn):
                sha256_compressions_per_step=int(acc["sha_blocks"] / K),
                host_ms=dict({k: round(v / K, 3) for k, v in host.items()},
                             **({"integrity_ms": round(integ["ms"] / K, 3)} if spec["integrity"] else {})),
-               roofline=block_roofline(kavg, acc["pay_blocks"] / K, acc["verifies"] / K, args.workload),
+               roofline=block_roofline(kavg, acc["pay_blocks"] / K, acc["verifies"] / K, batch_mb * 1e6,
+                                       args.workload),
                cpu_baseline=None)
     if cpu is not None:
         rate, n, cel, nb = cpu["full"]

@@ -517,7 +517,7 @@ DEV uint8_t extract_walk(S d, ParseLds &L, uint32_t lane, bool &md, S &results, 
 __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                  const uint64_t *__restrict__ bases, DevChannel ch,
                                                  DevTx *__restrict__ out, uint32_t *__restrict__ flags,
-                                                 uint32_t *__restrict__ xhaz, KlDev kl) {
+                                                 uint32_t *__restrict__ xhaz, KlDev kl, uint32_t touch) {
   // front half: below the back half's verify chain (3), above k_bd_sha_payload (1)
   __builtin_amdgcn_s_setprio(2);
   __shared__ ParseLds L;
@@ -528,6 +528,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
   const uint32_t blk = et[0];
   const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
   const S d{base + et[1], et[2]};
+  if (touch) touch_lines(d.p, d.n);  // (A/B: FGV_PARSE_TOUCH)
   DevTx &O = out[t];  // endorsements are written straight into it; the rest at the end
   struct {
     uint32_t blk;

@@ -1736,7 +1736,7 @@ static int build_committed(fgv_block_state *S) {
 }
 
 __global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, DevChannel ch, DevTx *out,
-                           uint32_t *flags, uint32_t *xhaz, KlDev kl);
+                           uint32_t *flags, uint32_t *xhaz, KlDev kl, uint32_t touch);
 __global__ void k_bd_kl(uint32_t ntx, DevTx *txs, const uint64_t *bases, KlDev kl, uint32_t *flags);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
@@ -1967,8 +1967,15 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
                reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + klb_off),
                B.kllist.as<uint32_t>(),
                B.kldep.as<uint32_t>()};
+  // every line of each envelope requested before the walk (touch_lines): measured on MI355X (C2,
+  // lean harness, one box) 0.665-0.667 ms per step against 0.702-0.724 without
+  // (profiles/round3_ab/parse_t*); FGV_PARSE_TOUCH=0 turns it off (A/B)
+  static const uint32_t parse_touch = [] {
+    const char *e = getenv("FGV_PARSE_TOUCH");
+    return e ? (uint32_t)atoi(e) : 1u;
+  }();
   hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16,
-                     B.kl);
+                     B.kl, parse_touch);
   HIP_TRY(hipEventRecord(B.ev[4], sf));
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one

@@ -42,6 +42,7 @@ struct fgv_mvcc_state {
   uint64_t nkeys = 0, arena_used = 0;  // read back from `top` after every commit / load
   DevBuf tbl, arena, top;              // top: [0] arena bytes used, [1] occupied slots
   DevBuf head, info, reads, writes, btbl, wslot, rslot, bad, st, pend, tail;
+  DevBuf xscr;  // k_mvx_extract's per-tx record scratch
   DevBuf lrecs, lbytes;                // load / apply staging
   DevBuf qver, qpres, qrange, qout;    // phantom path: lookups and range scans
   HostBuf hhead, htail;
@@ -54,7 +55,7 @@ struct fgv_mvcc_state {
 
 void fgv_mvcc_free(fgv_mvcc_state *M) {
   if (!M) return;
-  DevBuf *d[] = {&M->tbl, &M->arena, &M->top, &M->head, &M->info, &M->reads, &M->writes, &M->btbl, &M->wslot,
+  DevBuf *d[] = {&M->xscr, &M->tbl, &M->arena, &M->top, &M->head, &M->info, &M->reads, &M->writes, &M->btbl, &M->wslot,
                  &M->rslot, &M->bad, &M->st, &M->pend, &M->tail, &M->lrecs, &M->lbytes, &M->qver, &M->qpres,
                  &M->qrange, &M->qout};
   for (auto *b : d) b->release();
@@ -149,7 +150,7 @@ int fgv_statedb_init(fgv_ctx *c, uint64_t slots, uint64_t arena_bytes) {
   fgv_mvcc_state *M = c->mv;
   uint64_t cap = 1024;
   while (cap < (slots ? slots : (1ull << 22))) cap <<= 1;
-  if (!M->tbl.ensure(cap * sizeof(StateSlot)) || !M->arena.ensure(arena) || !M->top.ensure(64)) return FGV_ENOMEM;
+  if (!M->tbl.ensure(cap * sizeof(StateSlot)) || !M->arena.ensure(arena + 64) || !M->top.ensure(64)) return FGV_ENOMEM;
   M->cap = cap;
   M->mask = cap - 1;
   M->arena_cap = arena;
@@ -1063,7 +1064,18 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   HIP_TRY(hipMemcpyAsync(dh, h, hbytes, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(M->bad.p, 0, ntx, s));
   HIP_TRY(hipEventRecord(c->ev[0], s));
-  hipLaunchKernelGGL(k_mvx_extract, dim3((N + 63) / 64), dim3(64), 0, s, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c);
+  static const uint32_t touch = [] {
+    const char *e = getenv("FGV_MVX_TOUCH");
+    return e ? (uint32_t)atoi(e) : 1u;
+  }();
+  // FGV_MVX_ONEWALK=0: the second rwset walk for every tx (A/B of the scratch copy)
+  static const bool onewalk = [] {
+    const char *e = getenv("FGV_MVX_ONEWALK");
+    return !e || atoi(e) != 0;
+  }();
+  if (onewalk && !M->xscr.ensure(ntx * 2 * MVX_SCR * sizeof(MvRec))) return FGV_ENOMEM;
+  hipLaunchKernelGGL(k_mvx_extract, dim3((N + 63) / 64), dim3(64), 0, s, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c,
+                     touch, onewalk ? M->xscr.as<MvRec>() : nullptr);
   hipLaunchKernelGGL(k_mvx_prep, grid_stride(rcap), dim3(256), 0, s, dblk, d_r, d_w, d_b, epoch,
                      M->wslot.as<uint32_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
                      M->bad.as<uint8_t>(), d_c);
@@ -1101,7 +1113,16 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
     HIP_TRY(hipStreamSynchronize(s));
     return FGV_OK;
   };
-  int rc = enqueue(kRoundsPerEnqueue);
+  // rounds enqueued before the first host check: one more than the last block needed (a block
+  // needing more pays one extra synchronisation); FGV_MVX_ROUNDS fixes the count (A/B)
+  static const int fixed_rounds = [] {
+    const char *e = getenv("FGV_MVX_ROUNDS");
+    return e ? atoi(e) : 0;
+  }();
+  const uint32_t first = fixed_rounds > 0 ? (uint32_t)fixed_rounds
+                         : M->last_rounds ? std::min<uint32_t>(std::max<uint32_t>(M->last_rounds + 1, 2), kRoundsPerEnqueue)
+                                          : kRoundsPerEnqueue;
+  int rc = enqueue(first);
   if (rc) return rc;
   const MvCounters *hc = M->htail.as<MvCounters>();
   while (!hc->unsup && !hc->done) {  // a longer dependency chain: more rounds

@@ -50,8 +50,17 @@ using namespace pbd;
 // A key is (namespace, key bytes); a private-data key's namespace is ns + "$$h" + coll.  The
 // tag hashes the flattened namespace, a separator and the key (FNV-1a 64 + a finalizer); the
 // committed-state arena stores the flattened namespace followed by the key.
+// (bytes in order, read a word at a time: the loads are independent, the FNV chain is ALU)
 __device__ __forceinline__ uint64_t th(uint64_t h, const uint8_t *p, uint32_t n) {
-  for (uint32_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
+  uint32_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    const uint32_t w = ld4(p + i);
+    h = (h ^ (w & 0xFFu)) * 0x100000001b3ull;
+    h = (h ^ ((w >> 8) & 0xFFu)) * 0x100000001b3ull;
+    h = (h ^ ((w >> 16) & 0xFFu)) * 0x100000001b3ull;
+    h = (h ^ (w >> 24)) * 0x100000001b3ull;
+  }
+  for (; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
   return h;
 }
 __device__ __forceinline__ uint64_t th_fin(uint64_t h) {
@@ -73,10 +82,12 @@ __device__ __forceinline__ uint64_t rec_tag(const uint8_t *base, const MvRec &r)
 __device__ __forceinline__ uint32_t flat_ns_len(const MvRec &r) {
   return r.ns_len + ((r.flags & MVR_HASHED) ? 3u + r.coll_len : 0u);
 }
+// a word at a time (ld4: any alignment; block arenas, key staging and the state arena carry
+// >= 8 bytes of tail slack)
 __device__ __forceinline__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
-  for (uint32_t i = 0; i < n; i++)
-    if (a[i] != b[i]) return false;
-  return true;
+  uint32_t diff = 0;
+  for (uint32_t i = 0; i < n; i += 4) diff |= (ld4(a + i) ^ ld4(b + i)) & lo_mask(n - i);
+  return diff == 0;
 }
 // record == committed-state entry (flattened namespace + key at arena offset)
 __device__ __forceinline__ bool rec_eq_state(const uint8_t *base, const MvRec &r, const StateSlot &s,
@@ -121,14 +132,17 @@ namespace {
 // record sink: pass 1 counts, pass 2 writes records at the tx's claimed ranges
 struct Sink {
   const uint8_t *base;
-  MvRec *rout, *wout;  // null in the counting pass
+  MvRec *rout, *wout;  // null: count only
   uint32_t tx, nr, nw;
   uint64_t wbytes;     // arena bytes the writes could need (capacity check of the commit)
   bool big;            // a length exceeds the record fields
+  uint32_t kmax = 0xFFFFFFFFu;  // records per kind the outputs hold (the per-tx scratch)
+  bool spill = false;           // more than kmax of a kind: the scratch copy is incomplete
   __device__ void rec(MvRec *out, uint32_t k, S ns, bool hashed, S coll, S key, uint32_t flags, uint64_t b,
                       uint64_t t) {
     if (ns.n > 0xFFFF || key.n > 0xFFFF || coll.n > 0xFFFF || ns.n + 3u + coll.n > 0xFFFF) { big = true; return; }
     if (!out) return;
+    if (k >= kmax) { spill = true; return; }
     MvRec r;
     r.ns_off = (uint32_t)(ns.p - base);
     r.key_off = (uint32_t)(key.p - base);
@@ -385,6 +399,20 @@ DEV uint32_t wave_claim(uint32_t cnt, uint32_t *counter) {
   return b + v - cnt;
 }
 
+// the same for a 64-bit counter (every lane of the wave calls it)
+DEV uint64_t wave_claim64(uint32_t cnt, unsigned long long *counter) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t v = cnt;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(v, d);
+    if (lane >= d) v += o;
+  }
+  uint64_t b = 0;
+  if (lane == 63u && v) b = atomicAdd(counter, (unsigned long long)v);
+  b = __shfl(b, 63);
+  return b + v - cnt;
+}
+
 DEV uint32_t bmask_of(uint32_t nw) {
   uint32_t cap = 1024;
   while (cap < 2u * nw) cap <<= 1;
@@ -399,27 +427,36 @@ DEV uint32_t bmask_of(uint32_t nw) {
 // so the second walk finds the rwset bytes in the lane's caches: the block is read from HBM once.
 // Duplicate writes of one key in one tx (tx_ops.go:183-191 adds flags: undefined semantics)
 // -> unsupported.
+// touch: every line of the envelope is requested up front (touch_lines), so the walk's chain of
+// dependent loads hits the caches (FGV_MVX_TOUCH=0 turns it off, A/B)
+// scr (nullable): per-tx scratch of MVX_SCR reads + MVX_SCR writes; the counting walk writes
+// the records there too, so a tx within it is copied instead of walked a second time
 __global__ __launch_bounds__(64) void k_mvx_extract(uint32_t ntx, const uint8_t *__restrict__ base,
                                                     const uint32_t *__restrict__ envtab,
                                                     const uint8_t *__restrict__ in_flags, MvTxInfo *__restrict__ info,
                                                     MvRec *__restrict__ reads, MvRec *__restrict__ writes,
-                                                    MvCounters *__restrict__ c) {
+                                                    MvCounters *__restrict__ c, uint32_t touch, MvRec *__restrict__ scr) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t nr = 0, nw = 0;
   uint64_t wb = 0;
   MvTxInfo I{};
+  bool copied = false;
   if (t < ntx) {
     I.code = MV_SKIP;
+    if (touch && in_flags[t] == 0) touch_lines(base + envtab[2 * t], envtab[2 * t + 1]);
     if (in_flags[t] == 0) {
       S results{nullptr, 0};
       I.code = find_results(S{base + envtab[2 * t], envtab[2 * t + 1]}, results);
       if (I.code == 0) {
-        Sink sk{base, nullptr, nullptr, t, 0, 0, 0, false};
+        MvRec *sr = scr ? scr + (size_t)t * (2 * MVX_SCR) : nullptr;
+        Sink sk{base, sr, sr ? sr + MVX_SCR : nullptr, t, 0, 0, 0, false};
+        sk.kmax = MVX_SCR;
         bool host = false;
         I.code = walk_rwset(results, sk, host);
         I.rws_off = (uint32_t)(results.p - base);
         I.rws_len = results.n;
         if (I.code == 0) { nr = sk.nr; nw = sk.nw; wb = sk.wbytes; }
+        copied = sr && !sk.spill;
         // range queries / metadata writes: the block goes to the host path (fgv_mvcc.cpp),
         // which takes these codes and rwset spans (MV_HOSTPATH stops the device pipeline)
         if (I.code == 0 && host) atomicOr(&c->unsup, MV_HOSTPATH);
@@ -435,9 +472,15 @@ __global__ __launch_bounds__(64) void k_mvx_extract(uint32_t ntx, const uint8_t 
   if ((threadIdx.x & 63u) == 0 && wb) atomicAdd(&c->wbytes, (unsigned long long)wb);
   if (t >= ntx) return;
   if (I.code == 0) {
-    Sink sk{base, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
-    bool host = false;
-    walk_rwset(S{base + I.rws_off, I.rws_len}, sk, host);
+    if (copied) {  // (independent 16-byte copies instead of a second chain of dependent loads)
+      const MvRec *sr = scr + (size_t)t * (2 * MVX_SCR);
+      for (uint32_t k = 0; k < I.rcnt; k++) reads[I.rbeg + k] = sr[k];
+      for (uint32_t k = 0; k < I.wcnt; k++) writes[I.wbeg + k] = sr[MVX_SCR + k];
+    } else {
+      Sink sk{base, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
+      bool host = false;
+      walk_rwset(S{base + I.rws_off, I.rws_len}, sk, host);
+    }
     const MvRec *w = writes + I.wbeg;
     bool dup = false;
     for (uint32_t a = 0; a < I.wcnt && !dup; a++)
@@ -672,11 +715,24 @@ __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_
     if (!converged(c, rlast) || c->nomem) return;
     n = c->nw;
   }
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    if (!pend[i]) continue;
-    const MvRec w = recs[i];
-    const uint32_t fl = flat_ns_len(w);
-    const uint64_t off = atomicAdd(&top[0], (unsigned long long)((fl + w.key_len + 7u) & ~7u));
+  // every lane of a wave runs the same iterations, so the arena bytes and the slot count are
+  // claimed with one atomic per wave (a per-key atomicAdd on the two counters serialised the
+  // kernel on their cache line)
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+    const uint32_t i = i0 + threadIdx.x;
+    const bool mine = i < n && pend[i];
+    MvRec w{};
+    uint32_t fl = 0, need = 0;
+    if (mine) {
+      w = recs[i];
+      fl = flat_ns_len(w);
+      need = (fl + w.key_len + 7u) & ~7u;
+    }
+    const uint64_t off = wave_claim64(need, &top[0]);
+    const uint64_t nmine = __popcll(__ballot(mine));
+    if ((threadIdx.x & 63u) == 0 && nmine) atomicAdd(&top[1], (unsigned long long)nmine);
+    if (!mine) continue;
     uint8_t *a = arena + off;
     for (uint32_t q = 0; q < w.ns_len; q++) a[q] = base[w.ns_off + q];
     a += w.ns_len;
@@ -688,7 +744,6 @@ __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_
       a += 3 + w.coll_len;
     }
     for (uint32_t q = 0; q < w.key_len; q++) a[q] = base[w.key_off + q];
-    atomicAdd(&top[1], 1ull);
     const unsigned long long tag = (unsigned long long)(w.tag | MV_TAG_PRESENT);
     uint64_t idx = w.tag & mask;
     for (uint64_t probe = 0; probe <= mask; probe++, idx = (idx + 1) & mask) {

@@ -31,6 +31,26 @@ DEV uint32_t ld4(const uint8_t *p) {
 }
 DEV uint32_t lo_mask(uint32_t r) { return r >= 4u ? 0xFFFFFFFFu : ((1u << (8u * r)) - 1u); }
 
+// Issue one load per 128-byte line of [p, p + n) -- independent loads, all in flight at once --
+// so that a walk of the span that follows (one dependent load after another) finds its lines in
+// the caches instead of paying the HBM latency at every field.  The loaded words are consumed by
+// an empty asm (the loads are otherwise dead).
+DEV void touch_lines(const uint8_t *p, uint32_t n) {
+  const uintptr_t a0 = reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)127;
+  const uintptr_t a1 = reinterpret_cast<uintptr_t>(p) + n;
+  uint32_t acc = 0;
+  uintptr_t a = a0;
+  for (; a + 8 * 128 <= a1; a += 8 * 128) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = *reinterpret_cast<const uint32_t *>(a + 128 * k);
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc ^= v[k];
+  }
+  for (; a < a1; a += 128) acc ^= *reinterpret_cast<const uint32_t *>(a);
+  asm volatile("" ::"v"(acc));
+}
+
 DEV bool s_eq(S a, S b) {
   if (a.n != b.n) return false;
   for (uint32_t i = 0; i < a.n; i += 4)

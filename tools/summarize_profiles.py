@@ -57,7 +57,18 @@ def main(src, rnd):
         p = os.path.join(src, wl, "run_kernel_stats.csv")
         if not os.path.exists(p):
             continue
-        shutil.copy(p, f"profiles/{rnd}_{wl}_kernel_stats.csv")
+        # the per-step kernels only: the one-time comb-table builds (k_gtab per context, k_keytab
+        # per new key) are dropped, so the top row is the step's dominant kernel
+        with open(p) as fi, open(f"profiles/{rnd}_{wl}_kernel_stats.csv", "w", newline="") as fo:
+            rd = csv.DictReader(fi)
+            wr = csv.DictWriter(fo, fieldnames=rd.fieldnames)
+            wr.writeheader()
+            rows = [r for r in rd if not r["Name"].startswith(("k_gtab", "k_keytab"))]
+            tot = sum(float(r["TotalDurationNs"]) for r in rows) or 1.0
+            for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
+                r["Percentage"] = f"{100 * float(r['TotalDurationNs']) / tot:.2f}"
+                wr.writerow(r)
+        p = f"profiles/{rnd}_{wl}_kernel_stats.csv"
         js = os.path.join(src, wl + ".json")
         bench = json.load(open(js)) if os.path.exists(js) and os.path.getsize(js) else {}
         lines += [f"## {wl} workload", "", f"bench line (profiled run): value={bench.get('value')} {bench.get('unit')}, "
@@ -112,6 +123,7 @@ def main(src, rnd):
     traffic = {}
     for wl, fe, wr, kern in (("block", "pmc_blk_fetch", "pmc_blk_write", "k_bd_sha_payload"),
                              ("block_point", "pmc_blk_fetch", "pmc_blk_write", "k_point28"),
+                             ("block_parse", "pmc_blk_fetch", "pmc_blk_write", "k_bd_parse"),
                              ("sig", "pmc_sig_fetch", "pmc_sig_write", "k_point28"),
                              ("mvcc", "pmc_fetch", "pmc_write", None)):
         pf = os.path.join(src, fe, "run_counter_collection.csv")
