@@ -1789,16 +1789,27 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
                                                  const uint8_t *__restrict__ digests,
                                                  const uint8_t *__restrict__ vstatus,
                                                  fgv_tx_result *__restrict__ res, uint32_t *__restrict__ flags,
-                                                 const uint32_t *__restrict__ xhaz, FinDev fin, KlDev kl) {
+                                                 const uint32_t *__restrict__ xhaz, FinDev fin, KlDev kl,
+                                                 uint32_t touch) {
   __builtin_amdgcn_s_setprio(3);  // back half; a next batch's front half may run beside it
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
   const DevTx &R = txs[t];
   const DevJobIdx &J = jobs[t];
   const int32_t *id = ident + (size_t)t * BD_OCC;
-  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
   // digests: k_bd_sha's slots
   const size_t kT = (size_t)BD_DIG_T * ntx + t, kP = (size_t)BD_DIG_P * ntx + t, kI = (size_t)BD_DIG_I * ntx + t;
+  if (touch) {  // the lines the fold reads at fixed addresses, all requested at once (FGV_FOLD_TOUCH)
+    const uint8_t *dt = reinterpret_cast<const uint8_t *>(&R);
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t o = 0; o < sizeof(DevTx); o += 128) acc ^= *reinterpret_cast<const uint32_t *>(dt + o);
+    acc ^= *reinterpret_cast<const uint32_t *>(dt + sizeof(DevTx) - 4);
+    acc ^= J.cnt[0] ^ (uint32_t)id[0] ^ *reinterpret_cast<const uint32_t *>(digests + kT * 32) ^
+           *reinterpret_cast<const uint32_t *>(digests + kP * 32) ^ *reinterpret_cast<const uint32_t *>(digests + kI * 32);
+    asm volatile("" ::"v"(acc));
+  }
+  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
   uint8_t code;
   bool reached = false, defer = false;
   const uint8_t *txd = nullptr;

@@ -207,13 +207,18 @@ struct PreSplit {
 struct BdSet {
   DevBuf env, tx, ident, jobs, dig;  // env: envelope table | block bases | counters (the head)
   DevBuf klrec, klhead, kldep, kllist;  // key-level records, their buckets, dependencies (blockdev.h KlDev)
+  // the batch's verify jobs (k_bd_emit columns), status, r / s / w limbs, k_inv scratch: per set,
+  // so that k_bd_emit -> k_der -> k_inv of a batch can run ahead with its front half (vdone)
+  DevBuf vsig, vst, vr, vs, vw, vscr;
+  bool vdone = false;
   uint32_t klseq = 0;                   // the bucket tag of the batch this set holds
   KlDev kl{};
   HostBuf head, misc;                // pinned head staging / counters read back
   // 0 start, 1 payload hashes done (stream2), 2 k_bd_sha done (stream3), 3 head uploaded,
   // 4 parse done, 5 k_bd_sha start, 6 counts done, 7 k_bd_ident start (0, 5, 7: timing only),
-  // 8 every digest done (stream3, after joining stream2: the back half waits on this one only)
-  hipEvent_t ev[9] = {};
+  // 8 every digest done (stream3, after joining stream2: the back half waits on this one only),
+  // 9 the verify prefix done (k_bd_emit, k_der, k_inv)
+  hipEvent_t ev[10] = {};
   SplitOut so;
   bool presplit = false;
   bool force_host = false;  // a shard's block prefix writes metadata (host parser)
@@ -236,7 +241,9 @@ struct BdSet {
     return true;
   }
   void release() {
-    for (DevBuf *b : {&env, &tx, &ident, &jobs, &dig, &klrec, &klhead, &kldep, &kllist}) b->release();
+    for (DevBuf *b : {&env, &tx, &ident, &jobs, &dig, &klrec, &klhead, &kldep, &kllist, &vsig, &vst, &vr, &vs, &vw,
+                      &vscr})
+      b->release();
     head.release();
     misc.release();
     for (auto &e : ev)
@@ -1755,7 +1762,7 @@ __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases,
 __global__ void k_bd_fold(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
                           const DevJobIdx *jobs, const uint32_t *totals, const uint8_t *digests,
                           const uint8_t *vstatus, fgv_tx_result *res, uint32_t *flags, const uint32_t *xhaz,
-                          FinDev fin, KlDev kl);
+                          FinDev fin, KlDev kl, uint32_t touch);
 
 // The batch head, one H2D copy: envelope table | block base addresses | 64 zero bytes (the
 // kernels' counters) | per-block dependency-extraction hazards (blockdev.h) | per-block
@@ -1851,6 +1858,30 @@ static void prefix_hazards(const uint8_t *blk, size_t len, uint32_t lo, uint8_t 
   }
 }
 
+// k_bd_emit -> k_der -> k_inv of the batch in set B on stream `st` (its counts are done there):
+// the verify stages that need no digest, into the set's own buffers
+static int emit_prefix(fgv_ctx *c, fgv_block_state *S, BdSet &B, hipStream_t st) {
+  const uint32_t N = B.N;
+  const size_t cap = (size_t)N * (1 + BD_MAX_END);
+  if (!B.vsig.ensure(cap * 20 + 64) || !B.vst.ensure(cap + 64)) return FGV_ENOMEM;
+  uint32_t *misc = reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff);
+  const uint64_t *dbs = reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff);
+  uint8_t *sp = B.vsig.as<uint8_t>();
+  const bool tim = c->timing && B.timed;
+  if (tim) HIP_TRY(hipEventRecord(c->kev[6], st));
+  hipLaunchKernelGGL(k_bd_emit, dim3((N + 255) / 256), dim3(256), 0, st, N, B.tx.as<DevTx>(), dbs, S->dimg.ch,
+                     B.ident.as<int32_t>(), B.jobs.as<DevJobIdx>(), misc, reinterpret_cast<uint64_t *>(sp),
+                     reinterpret_cast<uint32_t *>(sp + cap * 8), reinterpret_cast<uint32_t *>(sp + cap * 12),
+                     reinterpret_cast<uint32_t *>(sp + cap * 16), misc + 10);
+  HIP_TRY(hipGetLastError());
+  if (tim) HIP_TRY(hipEventRecord(c->kev[7], st));
+  int rc = fgv_verify_prefix_dev(c, st, cap, misc + 10, sp, B.vst.as<uint8_t>(), B.vr, B.vs, B.vw, B.vscr);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(B.ev[9], st));
+  B.vdone = true;
+  return FGV_OK;
+}
+
 // Front half of a batch into set B, on the side streams: envelope spans (pre-split or walked
 // here), head upload, k_bd_sha_payload (stream2), k_bd_parse -> k_bd_ident -> k_bd_count ->
 // job counters in device memory (streamF), k_bd_sha (stream3).  `wait` (optional): an event the head
@@ -1861,7 +1892,9 @@ static void prefix_hazards(const uint8_t *blk, size_t len, uint32_t lo, uint8_t 
 // enqueued ahead beside the current batch's back half.
 static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks, const uint8_t *const *h_blocks,
                         const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
-                        const uint32_t *tx_hi, hipStream_t sf, hipEvent_t wait, hipEvent_t wait2 = nullptr) {
+                        const uint32_t *tx_hi, hipStream_t sf, hipEvent_t wait, hipEvent_t wait2 = nullptr,
+                        bool prefix = false) {
+  B.vdone = false;
   B.hb.assign(h_blocks, h_blocks + nblocks);
   B.db.assign(d_blocks, d_blocks + nblocks);
   B.lens.assign(lens, lens + nblocks);
@@ -2013,6 +2046,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(B.ev[6], sf));
   B.N = N;
+  if (prefix) return emit_prefix(c, S, B, sf);
   return FGV_OK;
 }
 
@@ -2062,18 +2096,6 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   S->last = cur;
   BdSet &B = S->set[cur];
   for (size_t b = 0; b < nblocks; b++) ntx_out[b] = B.so.ntx[b];
-  // the fused single-device call: its finalize's txid index runs on stream3 right after the
-  // batch's digests, beside the verify chain (fgv_finalize_early_index)
-  if (c->want_early_fin && !tx_lo && !tx_hi && B.N) {
-    // the key-level dependencies (nothing to do without key-level records), ahead of the index
-    hipLaunchKernelGGL(k_bd_kl, dim3((B.N + 255) / 256), dim3(256), 0, c->stream3, B.N, B.tx.as<DevTx>(),
-                       reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff), B.kl,
-                       reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff) + 5);
-    int rc = fgv_finalize_early_index(c, nblocks, B.so.ntx.data(), B.tx.as<DevTx>(),
-                                      reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff),
-                                      B.dig.as<uint8_t>(), c->stream3);
-    if (rc) return rc;
-  }
   c->n_sha_jobs = c->n_sha_blocks = c->n_verifies = 0;
   c->last_presplit = B.presplit;
   c->last_ahead = ahead_hit;
@@ -2099,24 +2121,36 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   DevTx *dtx = B.tx.as<DevTx>();
   int32_t *did = B.ident.as<int32_t>();
   DevJobIdx *dj = B.jobs.as<DevJobIdx>();
-  if (!c->bj_sigp.ensure(cap * 20 + 64) || !c->bj_vst.ensure(cap + 64)) return FGV_ENOMEM;
-  uint8_t *sp = c->bj_sigp.as<uint8_t>();
   const bool tim = c->timing && B.timed;
-  if (B.stream != st) HIP_TRY(hipStreamWaitEvent(st, B.ev[6], 0));  // (a front half enqueued ahead)
-  if (tim) HIP_TRY(hipEventRecord(c->kev[6], st));
-  hipLaunchKernelGGL(k_bd_emit, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
-                     reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + cap * 8),
-                     reinterpret_cast<uint32_t *>(sp + cap * 12), reinterpret_cast<uint32_t *>(sp + cap * 16),
-                     misc + 10);
-  HIP_TRY(hipGetLastError());
-  if (tim) HIP_TRY(hipEventRecord(c->kev[7], st));
+  if (B.vdone) {  // k_bd_emit, k_der, k_inv ran ahead with the front half (front_launch prefix)
+    HIP_TRY(hipStreamWaitEvent(st, B.ev[9], 0));
+  } else {
+    if (B.stream != st) HIP_TRY(hipStreamWaitEvent(st, B.ev[6], 0));  // (a front half enqueued ahead)
+    int rc = emit_prefix(c, S, B, st);
+    if (rc) return rc;
+  }
   c->digests_ready = B.ev[8];  // (payload and the other digests, joined on stream3)
   c->digests_ready2 = nullptr;
-  int rc = fgv_run_block_jobs_device(c, 0, cap, 0, 0, B.dig.as<uint8_t>(), misc + 10, n_est);
+  int rc = fgv_verify_main_dev(c, cap, misc + 10, n_est, B.vsig.as<uint8_t>(), B.vst.as<uint8_t>(),
+                               B.vr.as<uint32_t>(), B.vw.as<uint32_t>(), B.dig.as<uint8_t>());
   c->digests_ready = c->digests_ready2 = nullptr;
   if (rc) return rc;
   // (the digests were joined before k_prep: the verify stages always run, for the capacity)
   if (tim) HIP_TRY(hipEventRecord(c->kev[8], st));
+  // the fused single-device call: its finalize's txid index runs on stream3 after the batch's
+  // digests, beside the verify chain (fgv_finalize_early_index).  Enqueued after the verify
+  // chain, so the host's plan preparation overlaps the chain's first kernels instead of
+  // delaying them (the main stream is idle between two calls until k_bd_emit is queued)
+  if (c->want_early_fin && !tx_lo && !tx_hi && B.N) {
+    // the key-level dependencies (nothing to do without key-level records), ahead of the index
+    hipLaunchKernelGGL(k_bd_kl, dim3((B.N + 255) / 256), dim3(256), 0, c->stream3, B.N, B.tx.as<DevTx>(),
+                       reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff), B.kl,
+                       reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff) + 5);
+    int rc = fgv_finalize_early_index(c, nblocks, B.so.ntx.data(), B.tx.as<DevTx>(),
+                                      reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff),
+                                      B.dig.as<uint8_t>(), c->stream3);
+    if (rc) return rc;
+  }
   // the finalize's codes step inside the fold once the early index (stream3) is there
   FinDev fin{};
   c->fold_codes = false;
@@ -2130,8 +2164,13 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
     c->fold_codes = true;
     c->fold_unsup = misc + 5;  // (k_fin_dups: a first VALID position failed by the key-level walk)
   }
+  static const uint32_t fold_touch = [] {
+    const char *e = getenv("FGV_FOLD_TOUCH");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
   hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
-                     B.dig.as<uint8_t>(), c->bj_vst.as<uint8_t>(), d_res, misc + 5, misc + 16, fin, B.kl);
+                     B.dig.as<uint8_t>(), B.vst.as<uint8_t>(), d_res, misc + 5, misc + 16, fin, B.kl,
+                     fold_touch);
   HIP_TRY(hipGetLastError());
   if (tim || c->ahead_mode == 3) HIP_TRY(hipEventRecord(c->kev[9], st));  // (ahead mode 3 waits on it)
   // (the counters' D2H is queued by fgv_block_validate_dev_finish, behind whatever the caller
@@ -2154,8 +2193,13 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
                        : (ahead_mode == 4 && c->stage_ran) ? c->ev[5]
                        : ahead_mode == 3                   ? c->kev[9]
                                                            : nullptr;
-    if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after) ==
-        FGV_OK)
+    // FGV_PREFIX_AHEAD=0: the next batch's k_bd_emit / k_der / k_inv wait for its call (A/B)
+    static const bool prefix_ahead = [] {
+      const char *e = getenv("FGV_PREFIX_AHEAD");
+      return !e || atoi(e) != 0;
+    }();
+    if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after,
+                     prefix_ahead) == FGV_OK)
       S->ahead = cur ^ 1;
     else
       drain_ahead(c, S), S->ahead = -1;  // (the next call starts it again and reports any error)

@@ -225,24 +225,29 @@ int fgv_last_timing(fgv_ctx *c, double *sha_ms, double *prep_ms, double *point_m
 // k_inv on stream `st` (events ev[2]/ev[3]); the caller orders it after k_der.
 // N: capacity (column stride); dn: device-side item count (nullptr: N items)
 static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn, uint8_t *d_status,
-                      const uint32_t *d_slot, const uint32_t *d_r, const uint32_t *d_s) {
+                      const uint32_t *d_slot, const uint32_t *d_r, const uint32_t *d_s, DevBuf &w, DevBuf &wscr) {
   uint32_t nl = (N + PREP_B - 1) / PREP_B;
   nl = (nl + INV_THREADS - 1) / INV_THREADS * INV_THREADS;
-  if (!c->wscr.ensure((size_t)PREP_B * 8 * nl * 4) || !c->wv.ensure((size_t)N * 32)) return FGV_ENOMEM;
+  if (!wscr.ensure((size_t)PREP_B * 8 * nl * 4) || !w.ensure((size_t)N * 32)) return FGV_ENOMEM;
   const bool tim = c->timing || !dn;  // (host-count callers always time their stages)
   if (tim) HIP_TRY(hipEventRecord(c->ev[2], st));
   hipLaunchKernelGGL(k_inv, dim3(nl / INV_THREADS), dim3(INV_THREADS), 0, st, N, dn, d_status, d_slot,
-                     c->key_ok.as<uint8_t>(), d_r, d_s, c->wv.as<uint32_t>(), c->wscr.as<uint32_t>());
+                     c->key_ok.as<uint8_t>(), d_r, d_s, w.as<uint32_t>(), wscr.as<uint32_t>());
   HIP_TRY(hipGetLastError());
   if (tim) HIP_TRY(hipEventRecord(c->ev[3], st));
   return FGV_OK;
+}
+static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn, uint8_t *d_status,
+                      const uint32_t *d_slot, const uint32_t *d_r, const uint32_t *d_s) {
+  return launch_inv(c, st, N, dn, d_status, d_slot, d_r, d_s, c->wv, c->wscr);
 }
 
 // k_prep + k_point on the main stream, after k_inv (ev[3]) and the digests.  N: capacity;
 // dn: device-side item count (nullptr: N), n_est: the host's estimate of it (lanes per verify)
 static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_t n_est, uint8_t *d_status,
                              const uint32_t *d_slot, const uint32_t *d_r, const uint8_t *d_dig,
-                             const uint32_t *d_dig_idx) {
+                             const uint32_t *d_dig_idx, const uint32_t *d_w = nullptr) {
+  if (!d_w) d_w = c->wv.as<uint32_t>();
   if (!c->d1.ensure((size_t)DIG_STRIDE * N)) return FGV_ENOMEM;
   const bool tim = c->timing || !dn;
   if (tim) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev[3], 0));  // (k_inv may run on stream2)
@@ -259,7 +264,7 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
   }();
   uint32_t *redo = exact_only ? nullptr : c->redo.as<uint32_t>();
   hipLaunchKernelGGL(k_prep, dim3((N + 255) / 256), dim3(256), 0, c->stream, N, dn, d_status, d_r,
-                     c->wv.as<uint32_t>(), d_dig, d_dig_idx, c->d1.as<int8_t>(), redo);  // (k_prep zeroes *redo)
+                     d_w, d_dig, d_dig_idx, c->d1.as<int8_t>(), redo);  // (k_prep zeroes *redo)
   HIP_TRY(hipGetLastError());
   // (k_point28's bracket, always: its device time is read live; ahead mode 4 waits on it)
   HIP_TRY(hipEventRecord(c->ev[5], c->stream));
@@ -801,6 +806,35 @@ int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blo
   }
   c->stage_ran = ran;
   return FGV_OK;
+}
+
+// The device-parse committer's verify stages over one batch's own buffers (fgv_block.cpp
+// BdSet), split in two so that the prefix -- k_der, k_inv: they need only the batch's signature
+// list, not the digests -- can be enqueued ahead with the batch's front half, beside the
+// previous batch's back half.  sigblk: the k_bd_emit columns (ptr | len | key slot | digest
+// index, stride cap); dn: the verify count in device memory.
+int fgv_verify_prefix_dev(fgv_ctx *c, hipStream_t st, size_t cap, const uint32_t *dn, const uint8_t *sigblk,
+                          uint8_t *vst, DevBuf &r, DevBuf &s, DevBuf &w, DevBuf &wscr) {
+  const uint32_t N = (uint32_t)cap;
+  if (!r.ensure(cap * 32) || !s.ensure(cap * 32)) return FGV_ENOMEM;
+  hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, st, (const uint8_t *)nullptr,
+                     reinterpret_cast<const uint64_t *>(sigblk), reinterpret_cast<const uint32_t *>(sigblk + cap * 8), N,
+                     dn, vst, r.as<uint32_t>(), s.as<uint32_t>());
+  HIP_TRY(hipGetLastError());
+  return launch_inv(c, st, N, dn, vst, reinterpret_cast<const uint32_t *>(sigblk + cap * 12), r.as<uint32_t>(),
+                    s.as<uint32_t>(), w, wscr);
+}
+int fgv_verify_main_dev(fgv_ctx *c, size_t cap, const uint32_t *dn, size_t n_est, const uint8_t *sigblk, uint8_t *vst,
+                        const uint32_t *r, const uint32_t *w, const uint8_t *digests) {
+  c->n_sha_jobs = 0;
+  c->n_verifies = n_est;
+  c->n_sha_blocks = 0;
+  c->timing_ran = c->timing;
+  int rc = launch_prep_point(c, (uint32_t)cap, dn, (uint32_t)std::min(n_est, cap), vst,
+                             reinterpret_cast<const uint32_t *>(sigblk + cap * 12), r, digests,
+                             reinterpret_cast<const uint32_t *>(sigblk + cap * 16), w);
+  c->stage_ran = rc == FGV_OK;
+  return rc;
 }
 
 // stage times of the last fgv_run_block_jobs_device (after the stream has been synchronised)

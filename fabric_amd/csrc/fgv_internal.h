@@ -275,6 +275,10 @@ int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blo
 // wait for (and forget) a device-parse front half enqueued ahead of its call
 void fgv_block_drain(fgv_ctx *c);
 void fgv_read_block_job_times(fgv_ctx *c);
+int fgv_verify_prefix_dev(fgv_ctx *c, hipStream_t st, size_t cap, const uint32_t *dn, const uint8_t *sigblk,
+                          uint8_t *vst, DevBuf &r, DevBuf &s, DevBuf &w, DevBuf &wscr);
+int fgv_verify_main_dev(fgv_ctx *c, size_t cap, const uint32_t *dn, size_t n_est, const uint8_t *sigblk, uint8_t *vst,
+                        const uint32_t *r, const uint32_t *w, const uint8_t *digests);
 int fgv_block_set_parse_mode(fgv_block_state *S, int mode);
 int fgv_block_presplit(fgv_block_state *S, int device, size_t nblocks, const uint8_t *const *h_blocks,
                        const size_t *lens, const uint32_t *tx_lo, const uint32_t *tx_hi);

@@ -14,5 +14,11 @@ timeout -k 10 300 python -u bench.py --workload mvcc --steps 100 --warmup 5 > $O
 python3 -c "import json; d=json.load(open('$O/mvcc.json')); print('mvcc', d['value'], d['ms_per_step'], d['parity_vs_labels'], d['stage_ms'])"
 timeout -k 10 400 python -u tools/bench_sbe.py > $O/sbe.json 2> $O/sbe.err || { echo bench_sbe failed; tail -20 $O/sbe.err; exit 1; }
 cat $O/sbe.json
+for rep in 1 2; do
+  for tv in 1 0; do
+    FGV_FOLD_TOUCH=$tv timeout -k 10 300 python -u bench.py --steps 60 --warmup 5 --cpu-threads 0 --no-pcie --no-latency > $O/fold_t${tv}_$rep.json 2> $O/fold_t${tv}_$rep.err || { echo fold ab failed; tail -20 $O/fold_t${tv}_$rep.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/fold_t${tv}_$rep.json')); print('fold touch $tv rep $rep', d['value'], d['ms_per_step'], d['parity_vs_labels'], d['kernel_ms']['k_bd_fold'])"
+  done
+done
 PROF_OUT=$O/prof bash tools/profile_round.sh || { echo profile failed; exit 1; }
 echo done
