@@ -2193,10 +2193,13 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
                        : (ahead_mode == 4 && c->stage_ran) ? c->ev[5]
                        : ahead_mode == 3                   ? c->kev[9]
                                                            : nullptr;
-    // FGV_PREFIX_AHEAD=0: the next batch's k_bd_emit / k_der / k_inv wait for its call (A/B)
+    // FGV_PREFIX_AHEAD=1: the next batch's k_bd_emit / k_der / k_inv run ahead with its front
+    // half.  Measured on MI355X (C2 lean harness, alternating on one box, profiles/round3_ab/
+    // prefix_*): 0.748 / 0.753 ms per step ahead against 0.683 / 0.670 at the call -- beside the
+    // current back half they stretch k_point28 more than they shorten the chain -- so off.
     static const bool prefix_ahead = [] {
       const char *e = getenv("FGV_PREFIX_AHEAD");
-      return !e || atoi(e) != 0;
+      return e && atoi(e) != 0;
     }();
     if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after,
                      prefix_ahead) == FGV_OK)

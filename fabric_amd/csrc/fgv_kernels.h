@@ -119,7 +119,8 @@ struct BlkSlot {    // keys written in the block
   uint64_t last;    // (epoch << 32) | (tx + 1) of the last VALID writer
 };
 __global__ void k_mvx_extract(uint32_t ntx, const uint8_t *base, const uint32_t *envtab, const uint8_t *in_flags,
-                              MvTxInfo *info, MvRec *reads, MvRec *writes, MvCounters *c, uint32_t touch, MvRec *scr);
+                              MvTxInfo *info, MvRec *reads, MvRec *writes, MvCounters *c, uint32_t touch, MvRec *scr,
+                              uint8_t *bad);
 #define MVX_SCR 8  // k_mvx_extract scratch: records of each kind per tx
 __global__ void k_mvx_prep(const uint8_t *base, const MvRec *reads, const MvRec *writes, BlkSlot *btbl, uint32_t epoch,
                            uint32_t *wslot, const StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint8_t *bad,

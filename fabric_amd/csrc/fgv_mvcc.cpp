@@ -1062,7 +1062,6 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   const uint32_t N = (uint32_t)ntx;
   const size_t top_off = (kCounterBytes + ntx + 7) & ~(size_t)7;  // (in htail, behind the flags)
   HIP_TRY(hipMemcpyAsync(dh, h, hbytes, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemsetAsync(M->bad.p, 0, ntx, s));
   HIP_TRY(hipEventRecord(c->ev[0], s));
   static const uint32_t touch = [] {
     const char *e = getenv("FGV_MVX_TOUCH");
@@ -1075,7 +1074,7 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   }();
   if (onewalk && !M->xscr.ensure(ntx * 2 * MVX_SCR * sizeof(MvRec))) return FGV_ENOMEM;
   hipLaunchKernelGGL(k_mvx_extract, dim3((N + 63) / 64), dim3(64), 0, s, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c,
-                     touch, onewalk ? M->xscr.as<MvRec>() : nullptr);
+                     touch, onewalk ? M->xscr.as<MvRec>() : nullptr, M->bad.as<uint8_t>());
   hipLaunchKernelGGL(k_mvx_prep, grid_stride(rcap), dim3(256), 0, s, dblk, d_r, d_w, d_b, epoch,
                      M->wslot.as<uint32_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
                      M->bad.as<uint8_t>(), d_c);
@@ -1110,7 +1109,13 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
     // the arena top after the commit rides on the same synchronisation (no second one)
     if (commit) HIP_TRY(hipMemcpyAsync(M->htail.as<uint8_t>() + top_off, M->top.p, 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(c->ev[2], s));
-    HIP_TRY(hipStreamSynchronize(s));
+    // polled: a block's GPU work is ~0.2 ms, and a blocking synchronize's wake-up is a large
+    // share of that (FGV_MVCC_SPIN=0: blocking, A/B)
+    static const bool spin = [] {
+      const char *e = getenv("FGV_MVCC_SPIN");
+      return !e || atoi(e) != 0;
+    }();
+    HIP_TRY(fgv_stream_wait(s, spin));
     return FGV_OK;
   };
   // rounds enqueued before the first host check: one more than the last block needed (a block

@@ -435,13 +435,15 @@ __global__ __launch_bounds__(64) void k_mvx_extract(uint32_t ntx, const uint8_t 
                                                     const uint32_t *__restrict__ envtab,
                                                     const uint8_t *__restrict__ in_flags, MvTxInfo *__restrict__ info,
                                                     MvRec *__restrict__ reads, MvRec *__restrict__ writes,
-                                                    MvCounters *__restrict__ c, uint32_t touch, MvRec *__restrict__ scr) {
+                                                    MvCounters *__restrict__ c, uint32_t touch, MvRec *__restrict__ scr,
+                                                    uint8_t *__restrict__ bad) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t nr = 0, nw = 0;
   uint64_t wb = 0;
   MvTxInfo I{};
   bool copied = false;
   if (t < ntx) {
+    bad[t] = 0;  // (k_mvx_prep marks static conflicts after this kernel: no separate memset)
     I.code = MV_SKIP;
     if (touch && in_flags[t] == 0) touch_lines(base + envtab[2 * t], envtab[2 * t + 1]);
     if (in_flags[t] == 0) {

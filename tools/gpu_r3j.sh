@@ -19,5 +19,9 @@ for rep in 1 2; do
 done
 timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail -20 $O/bench.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['parity_vs_labels'], d['roofline']['kernel'], d['roofline']['frac'], d['pcie_inclusive']['ms_per_step'], d['cpu_baseline']['value'], d['kernel_ms'])"
+timeout -k 10 300 python -u bench.py --workload mvcc --steps 100 --warmup 5 > $O/mvcc.json 2> $O/mvcc.err || { echo mvcc failed; tail -20 $O/mvcc.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/mvcc.json')); print('mvcc', d['value'], d['ms_per_step'], d['parity_vs_labels'], d['stage_ms'])"
+timeout -k 10 400 python -u tools/bench_sbe.py > $O/sbe.json 2> $O/sbe.err || { echo bench_sbe failed; tail -20 $O/sbe.err; exit 1; }
+cat $O/sbe.json
 timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d $O/trace -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $O/trace.json 2> $O/trace.err || { echo trace failed; tail -20 $O/trace.err; exit 1; }
 echo done
