@@ -647,8 +647,10 @@ def run_mvcc(args, world, rank, local, dev):
     if args.mvcc_private_every > 0:  # private-data keys: hashed namespace mycc$$hpvt
         hk, hb, ht = st.items_hashed()
         eng.statedb_load(M.HASHED_NS, hk, hb, ht)
-    blocks = [M.make_block(st, T, number=1001 + i, seed=100 * rank + i) for i in range(W + K)]
-    log(f"[bench] rank {rank}: {args.state_keys} keys + {W + K} x {T}-tx blocks ready in {time.time() - t0:.1f}s")
+    C = max(1, args.mvcc_chain)
+    S = min(K, args.mvcc_single_steps) if C > 1 else 0  # the single-block pass after the chained one
+    blocks = [M.make_block(st, T, number=1001 + i, seed=100 * rank + i) for i in range(W + K + S)]
+    log(f"[bench] rank {rank}: {args.state_keys} keys + {W + K + S} x {T}-tx blocks ready in {time.time() - t0:.1f}s")
     sizes = [(len(b[0]) + 64 + 255) // 256 * 256 for b in blocks]
     arena = torch.zeros(sum(sizes), dtype=torch.uint8, device=dev)
     dptr, o = [], 0
@@ -668,23 +670,49 @@ def run_mvcc(args, world, rank, local, dev):
     lookup = total = 0.0
     rounds = []
     outs = []
-    # block i+1's framing is walked on the engine's host worker while block i validates
-    # (fgv_mvcc_validate_block_next; a peer has the next block in hand while it commits this one)
+    # C > 1: C consecutive blocks per fgv_mvcc_validate_blocks call (one device chain, block k+1's
+    # extraction beside block k's checks and commit; a peer catching up holds many blocks);
+    # C = 1: one fgv_mvcc_validate_block call per block, block i+1's framing walked on the engine's
+    # host worker while block i validates (fgv_mvcc_validate_block_next)
     t0 = time.perf_counter()
-    for i in range(W, W + K):
-        b, labels, flags = blocks[i]
-        nb = blocks[i + 1][0] if i + 1 < W + K and not args.no_presplit else None
-        outs.append(eng.mvcc_validate(b, 1001 + i, flags, commit=True, d_block=dptr[i], next_block=nb))
-        s = eng.mvcc_stats()
-        lookup += s["lookup_ms"]
-        total += s["total_ms"]
-        rounds.append(s["rounds"])
+    if C > 1:
+        for i0 in range(W, W + K, C):
+            i1 = min(i0 + C, W + K)
+            # the next call's blocks are walked on the engine's host worker while this chain runs
+            nxt = [blocks[i][0] for i in range(i1, min(i1 + C, W + K))] if not args.no_presplit else None
+            fl, rc, done = eng.mvcc_validate_blocks([blocks[i][0] for i in range(i0, i1)], range(1001 + i0, 1001 + i1),
+                                                    [blocks[i][2] for i in range(i0, i1)], commit=True,
+                                                    d_blocks=dptr[i0:i1], next_blocks=nxt)
+            _lib._check(rc)
+            outs += fl
+            s = eng.mvcc_stats()
+            total += s["total_ms"] * (i1 - i0)
+            rounds.append(s["rounds"])
+    else:
+        for i in range(W, W + K):
+            b, labels, flags = blocks[i]
+            nb = blocks[i + 1][0] if i + 1 < W + K and not args.no_presplit else None
+            outs.append(eng.mvcc_validate(b, 1001 + i, flags, commit=True, d_block=dptr[i], next_block=nb))
+            s = eng.mvcc_stats()
+            lookup += s["lookup_ms"]
+            total += s["total_ms"]
+            rounds.append(s["rounds"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     for i, f in zip(range(W, W + K), outs):
         ok &= bool((f == blocks[i][1]).all())
+    single = None
+    if S:  # per-block calls on the blocks that follow (latency of one block; untimed by the driver)
+        t1 = time.perf_counter()
+        for i in range(W + K, W + K + S):
+            b, labels, flags = blocks[i]
+            nb = blocks[i + 1][0] if i + 1 < W + K + S and not args.no_presplit else None
+            ok &= bool((eng.mvcc_validate(b, 1001 + i, flags, commit=True, d_block=dptr[i], next_block=nb)
+                        == labels).all())
+        el1 = time.perf_counter() - t1
+        single = dict(blocks=S, ms_per_block=round(el1 / S * 1e3, 3), tx_per_s=round(T * S / el1, 1))
     if world > 1:
         t = torch.tensor([el, 1.0 if ok else 0.0], dtype=torch.float64, device=dev)
         mx = t.clone()
@@ -701,15 +729,17 @@ def run_mvcc(args, world, rank, local, dev):
                 config=dict(workload=f"C3: {T}-tx blocks, {args.state_keys}-key state DB, 4R/4W, 5% intra-block "
                                      f"conflicts, 1% stale, 0.5% invalid-writer chains, commit per block"
                                      + (f", every {args.mvcc_private_every}th key private (hashed reads/writes)"
-                                        if args.mvcc_private_every > 0 else ""),
+                                        if args.mvcc_private_every > 0 else "")
+                                     + (f", {C} consecutive blocks per call (fgv_mvcc_validate_blocks)" if C > 1 else
+                                        ", one call per block"),
                             parallelism=f"replicas{world} (sequential per channel)"),
-                parity_vs_labels=ok, fixpoint_rounds=rounds,
+                parity_vs_labels=ok, fixpoint_rounds=rounds, blocks_per_call=C, single_block_calls=single,
                 stage_ms=dict(lookup=round(lookup / K, 4), gpu_total=round(per_block_ms, 4)),
                 roofline=dict(bound="hbm", achieved=round(achieved, 2), peak=8000.0, unit="GB/s",
                               frac=round(achieved / 8000.0, 5), traffic=mv_traffic, traffic_source=mv_src,
                               kernel="MVCC GPU stages (per block)",
                               per_launch_bytes=T * MVCC_BYTES_PER_TX,
-                              note="latency-bound: ~14 launches + 2 host syncs per 10k-tx block"),
+                              note="latency-bound: ~14 launches per 10k-tx block, one wait per call"),
                 cpu_baseline=None)
 
 
@@ -806,6 +836,10 @@ def main():
     ap.add_argument("--state-keys", type=int, default=1_000_000)
     ap.add_argument("--mvcc-private-every", type=int, default=0,
                     help="C3 variant: every Nth key is private data (collection hashed rwsets)")
+    ap.add_argument("--mvcc-chain", type=int, default=10,
+                    help="C3: consecutive blocks per fgv_mvcc_validate_blocks call (1: one call per block)")
+    ap.add_argument("--mvcc-single-steps", type=int, default=20,
+                    help="C3 with --mvcc-chain > 1: blocks validated one call each after the timed pass (latency)")
     ap.add_argument("--blocks-per-gpu", type=int, default=32)
     ap.add_argument("--tx-per-block", type=int, default=500)
     ap.add_argument("--per-gpu", type=int, default=131072)

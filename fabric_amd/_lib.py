@@ -24,7 +24,7 @@ EXPORTED = [
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
     "fgv_presplit", "fgv_last_presplit", "fgv_validate_shard_dev_next", "fgv_mvcc_validate_block_next",
-    "fgv_statedb_init", "fgv_statedb_load", "fgv_statedb_apply", "fgv_statedb_stats", "fgv_mvcc_validate_block", "fgv_mvcc_last_stats",
+    "fgv_statedb_init", "fgv_statedb_load", "fgv_statedb_apply", "fgv_statedb_stats", "fgv_mvcc_validate_block", "fgv_mvcc_validate_blocks", "fgv_mvcc_validate_blocks_next", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash",
     "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
     "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d",
@@ -161,6 +161,8 @@ def load():
         L.fgv_statedb_stats.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 4
         L.fgv_mvcc_validate_block.argtypes = [vp, vp, sz, vp, ctypes.c_uint64, vp, sz, ctypes.c_int]
         L.fgv_mvcc_validate_block_next.argtypes = [vp, vp, sz, vp, ctypes.c_uint64, vp, sz, ctypes.c_int, vp, sz]
+        L.fgv_mvcc_validate_blocks.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, ctypes.c_int, vp]
+        L.fgv_mvcc_validate_blocks_next.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, ctypes.c_int, vp, sz, vp, vp]
         L.fgv_mvcc_last_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.POINTER(ctypes.c_uint32)]
@@ -773,6 +775,32 @@ class Engine:
                                                         _ptr(f), len(f), 1 if commit else 0, nb.ctypes.data,
                                                         len(next_block)))
         return f
+
+    def mvcc_validate_blocks(self, blocks, block_nums, flags, commit=True, d_blocks=None, next_blocks=None):
+        """fgv_mvcc_validate_blocks: consecutive blocks validated (and committed) in order as one
+        device chain.  flags: one committer TxValidationFlags array per block.  next_blocks: the
+        blocks of the next call (their framing is walked meanwhile; keep the objects alive).
+        Returns (list of updated flag arrays, rc, n_done) -- rc != 0 is the error of block n_done."""
+        n = len(blocks)
+        bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+        fl = [np.array(f, dtype=np.uint8) for f in flags]
+        bp = (ctypes.c_void_p * max(n, 1))(*[b.ctypes.data for b in bufs])
+        ln = (ctypes.c_size_t * max(n, 1))(*[len(b) for b in blocks])
+        nums = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in block_nums])
+        fp = (ctypes.c_void_p * max(n, 1))(*[f.ctypes.data for f in fl])
+        nt = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in fl])
+        dp = None if d_blocks is None else (ctypes.c_void_p * max(n, 1))(*[d or None for d in d_blocks])
+        done = ctypes.c_size_t(0)
+        if next_blocks:
+            nbufs = [np.frombuffer(b, dtype=np.uint8) for b in next_blocks]
+            nbp = (ctypes.c_void_p * len(nbufs))(*[b.ctypes.data for b in nbufs])
+            nln = (ctypes.c_size_t * len(nbufs))(*[len(b) for b in next_blocks])
+            rc = self._L.fgv_mvcc_validate_blocks_next(self._h, n, bp, ln, dp, nums, fp, nt, 1 if commit else 0,
+                                                       ctypes.byref(done), len(nbufs), nbp, nln)
+        else:
+            rc = self._L.fgv_mvcc_validate_blocks(self._h, n, bp, ln, dp, nums, fp, nt, 1 if commit else 0,
+                                                  ctypes.byref(done))
+        return fl, rc, done.value
 
     def mvcc_stats(self):
         a, b = ctypes.c_double(), ctypes.c_double()

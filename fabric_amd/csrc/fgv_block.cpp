@@ -283,6 +283,7 @@ Channel &fgv_block_channel(fgv_block_state *S) { return S->ch; }
 void fgv_parallel_for(fgv_block_state *S, size_t n, const std::function<void(size_t)> &f) {
   S->pool.parallel_for(n, f);
 }
+void fgv_parallel_run(fgv_block_state *S, size_t n, const std::function<void(size_t)> &f) { S->pool.run(n, f); }
 void fgv_block_state_free(fgv_block_state *s) { delete s; }
 
 // ======================================================================= parsing
@@ -1842,6 +1843,21 @@ bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t le
   return true;
 }
 
+// The pre-split of exactly these whole blocks (fgv_mvcc_validate_blocks_next walked them while
+// the previous call ran): per block its envelope count, its first row in `et` (BD_ENV_WORDS per
+// envelope: block, offset, length).  Valid until the next pre-split.
+bool fgv_block_take_presplit_batch(fgv_block_state *S, size_t nb, const uint8_t *const *blocks, const size_t *lens,
+                                   const uint32_t **et, const size_t **ntx, const size_t **first) {
+  PreSplit &P = S->pre;
+  if (!P.active || !P.matches(nb, blocks, lens, nullptr, nullptr)) return false;
+  P.join();
+  if (P.rc != FGV_OK || P.out.ntx.size() != nb) return false;
+  *et = P.et.as<uint32_t>();
+  *ntx = P.out.ntx.data();
+  *first = P.out.first.data();
+  return true;
+}
+
 // The dependency-extraction hazards of transactions [0, lo) of a block (a shard starting inside
 // it): extraction failures, panics, metadata writes.
 static void prefix_hazards(const uint8_t *blk, size_t len, uint32_t lo, uint8_t &fail, uint8_t &panic, bool &md) {
@@ -2007,8 +2023,16 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     const char *e = getenv("FGV_PARSE_TOUCH");
     return e ? (uint32_t)atoi(e) : 1u;
   }();
-  hipLaunchKernelGGL(k_bd_parse, dim3((N + 63) / 64), dim3(64), 0, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16,
-                     B.kl, parse_touch);
+  // transactions (walking lanes) per workgroup: fewer lanes per wave = fewer distinct lines per
+  // load instruction in the walk's dependent chain, and more waves over the SIMDs (the LDS arrays
+  // stay sized for 64 lanes); FGV_PARSE_LANES = 16 / 32 / 64 (A/B)
+  static const uint32_t parse_lanes = [] {
+    const char *e = getenv("FGV_PARSE_LANES");
+    const uint32_t v = e ? (uint32_t)atoi(e) : 64u;
+    return (v == 16u || v == 32u) ? v : 64u;
+  }();
+  hipLaunchKernelGGL(k_bd_parse, dim3((N + parse_lanes - 1) / parse_lanes), dim3(parse_lanes), 0, sf, N, envtab, dbs,
+                     ch, dtx, misc + 5, misc + 16, B.kl, parse_touch);
   HIP_TRY(hipEventRecord(B.ev[4], sf));
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one

@@ -221,6 +221,8 @@ void fgv_block_state_free(fgv_block_state *s);
 
 #include <functional>
 void fgv_parallel_for(fgv_block_state *S, size_t n, const std::function<void(size_t)> &f);
+// one job per index on the pool (no chunking: for a few long jobs)
+void fgv_parallel_run(fgv_block_state *S, size_t n, const std::function<void(size_t)> &f);
 void fgv_mvcc_free(fgv_mvcc_state *M);
 
 int fgv_block_set_channel(fgv_block_state *S, const char *name);

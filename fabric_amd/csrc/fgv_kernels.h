@@ -83,6 +83,7 @@ __global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_
 #define MVR_DELETE 1u   // write: is a delete
 #define MVR_HASHED 2u   // private-data key: namespace = ns + "$$h" + coll
 #define MV_HOSTPATH 2u  // MvCounters.unsup bit: range queries / metadata writes -> the host path
+#define MV_HALT 4u      // MvCounters.unsup bit: an earlier block of the batch was not finished on the device
 #define MVRANGE_UNBOUNDED 1u  // MvRange.flags: end key "" (to the end of the namespace)
 #define MV_TAG_OCC 1ull      // tag bit 0: slot occupied (tags are never 0)
 #define MV_TAG_PRESENT 2ull  // committed-state tag bit 1: the key exists (clear = deleted)
@@ -118,13 +119,14 @@ struct BlkSlot {    // keys written in the block
   uint64_t fw_cand[2], fw_valid[2];
   uint64_t last;    // (epoch << 32) | (tx + 1) of the last VALID writer
 };
-__global__ void k_mvx_extract(uint32_t ntx, const uint8_t *base, const uint32_t *envtab, const uint8_t *in_flags,
-                              MvTxInfo *info, MvRec *reads, MvRec *writes, MvCounters *c, uint32_t touch, MvRec *scr,
-                              uint8_t *bad);
-#define MVX_SCR 8  // k_mvx_extract scratch: records of each kind per tx
+void mvx_extract_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint8_t *base, const uint32_t *envtab,
+                        const uint8_t *in_flags, MvTxInfo *info, MvRec *reads, MvRec *writes, MvCounters *c,
+                        uint32_t touch, MvRec *scr, uint8_t *bad);
+#define MVX_SCR 8    // k_mvx_extract scratch: records of each kind per tx
+
 __global__ void k_mvx_prep(const uint8_t *base, const MvRec *reads, const MvRec *writes, BlkSlot *btbl, uint32_t epoch,
                            uint32_t *wslot, const StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint8_t *bad,
-                           const MvCounters *c);
+                           MvCounters *c, const MvCounters *prev);
 __global__ void k_mvx_find(uint32_t ntx, const uint8_t *base, const MvRec *reads, const MvRec *writes,
                            const BlkSlot *btbl_r, BlkSlot *btbl, uint32_t epoch, const uint32_t *wslot, uint32_t *rslot,
                            const MvTxInfo *info, const uint8_t *bad, uint8_t *st, uint32_t rg1, const MvCounters *c);
@@ -143,6 +145,7 @@ __global__ void k_mv_upsert_insert(uint32_t mode, uint32_t rlast, uint32_t n_hos
                                    const MvRec *recs, const uint8_t *pend, StateSlot *tbl, uint64_t mask, uint8_t *arena,
                                    unsigned long long *top, uint64_t block_num, const MvCounters *c);
 __global__ void k_mv_tags(const uint8_t *base, MvRec *recs, uint32_t n);
+__global__ void k_mv_tail(const MvCounters *c, const unsigned long long *top, uint32_t *hc, unsigned long long *htop);
 struct MvRange {  // a range query's scan bounds (bytes in a host-built buffer)
   uint32_t ns_off, ns_len, s_off, s_len, e_off, e_len, flags, pad;
 };

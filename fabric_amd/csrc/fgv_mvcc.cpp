@@ -23,11 +23,14 @@
 #include <vector>
 
 #include "../../include/fgv.h"
+#include "blockdev.h"
 #include "fgv_internal.h"
 #include "fgv_visitors.h"
 #include "sha256_host.h"
 
 bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t len, std::vector<Span> &out);
+bool fgv_block_take_presplit_batch(fgv_block_state *S, size_t nb, const uint8_t *const *blocks, const size_t *lens,
+                                   const uint32_t **et, const size_t **ntx, const size_t **first);
 
 using namespace fgvb;
 
@@ -37,15 +40,36 @@ constexpr uint64_t kMaxArena = 32ull << 30;  // StateSlot.off8 addresses 8-byte 
 constexpr size_t kCounterBytes = 256;       // MvCounters, padded (head and tail)
 }  // namespace
 
+// per-block device buffers: the single-block path uses set 0, a batch of consecutive blocks
+// (fgv_mvcc_validate_blocks) rotates through kSets of them, so the extraction of the next blocks
+// runs ahead of the block being checked and committed
+constexpr int kSets = 3;
+struct MvSet {
+  DevBuf head, info, reads, writes, wslot, rslot, bad, st, pend, tail;
+  DevBuf xscr;  // k_mvx_extract's per-tx record scratch
+  DevBuf blk;   // the block's bytes when the caller gives no device copy (batch path)
+  hipEvent_t ev_x = nullptr;     // the block's extraction is done (stream2)
+  hipEvent_t ev_free = nullptr;  // the set's last reader on the main stream is done
+  void release() {
+    DevBuf *d[] = {&head, &info, &reads, &writes, &wslot, &rslot, &bad, &st, &pend, &tail, &xscr, &blk};
+    for (auto *b : d) b->release();
+    if (ev_x) hipEventDestroy(ev_x);
+    if (ev_free) hipEventDestroy(ev_free);
+    ev_x = ev_free = nullptr;
+  }
+};
+
 struct fgv_mvcc_state {
   uint64_t cap = 0, mask = 0, arena_cap = 0;
   uint64_t nkeys = 0, arena_used = 0;  // read back from `top` after every commit / load
   DevBuf tbl, arena, top;              // top: [0] arena bytes used, [1] occupied slots
-  DevBuf head, info, reads, writes, btbl, wslot, rslot, bad, st, pend, tail;
-  DevBuf xscr;  // k_mvx_extract's per-tx record scratch
+  DevBuf btbl;
+  DevBuf dheads;                       // batch path: every block's head (one copy per call)
+  MvSet set[kSets];
   DevBuf lrecs, lbytes;                // load / apply staging
   DevBuf qver, qpres, qrange, qout;    // phantom path: lookups and range scans
   HostBuf hhead, htail;
+  HostBuf bhead, btail;                // batch path: per-block head / tail regions
   std::vector<Span> pre_envs;          // envelope spans taken from a pre-split
   uint32_t epoch = 0;                  // block-table epoch (BlkSlot.owner)
   uint32_t rg = 0;                     // global fixpoint round tag (BlkSlot.fw_*)
@@ -55,12 +79,11 @@ struct fgv_mvcc_state {
 
 void fgv_mvcc_free(fgv_mvcc_state *M) {
   if (!M) return;
-  DevBuf *d[] = {&M->xscr, &M->tbl, &M->arena, &M->top, &M->head, &M->info, &M->reads, &M->writes, &M->btbl, &M->wslot,
-                 &M->rslot, &M->bad, &M->st, &M->pend, &M->tail, &M->lrecs, &M->lbytes, &M->qver, &M->qpres,
-                 &M->qrange, &M->qout};
+  DevBuf *d[] = {&M->tbl, &M->arena, &M->top, &M->btbl, &M->dheads, &M->lrecs, &M->lbytes, &M->qver, &M->qpres, &M->qrange, &M->qout};
   for (auto *b : d) b->release();
-  M->hhead.release();
-  M->htail.release();
+  for (auto &S : M->set) S.release();
+  HostBuf *h[] = {&M->hhead, &M->htail, &M->bhead, &M->btail};
+  for (auto *b : h) b->release();
   delete M;
 }
 
@@ -107,7 +130,7 @@ static int upsert_host(fgv_ctx *c, const char *ns, const uint8_t *key_buf, const
   if ((M->nkeys + n) * 10 > M->cap * 7 || M->arena_used + need > M->arena_cap) return FGV_ENOMEM;
   // staging: [ns | key bytes] in lbytes; one record per key (ns_off 0)
   const size_t kofs = (nsl + 7) & ~(size_t)7;
-  if (!M->lbytes.ensure(kofs + kb + 64) || !M->lrecs.ensure(n * sizeof(MvRec)) || !M->pend.ensure(n + 64))
+  if (!M->lbytes.ensure(kofs + kb + 64) || !M->lrecs.ensure(n * sizeof(MvRec)) || !M->set[0].pend.ensure(n + 64))
     return FGV_ENOMEM;
   if (kofs + kb > 0xFFFFFFFFull) return FGV_EINVAL;
   std::vector<MvRec> recs(n);
@@ -130,9 +153,9 @@ static int upsert_host(fgv_ctx *c, const char *ns, const uint8_t *key_buf, const
   hipLaunchKernelGGL(k_mv_tags, grid_for(n), dim3(256), 0, s, lb, M->lrecs.as<MvRec>(), (uint32_t)n);
   hipLaunchKernelGGL(k_mv_upsert_find, grid_stride(n), dim3(256), 0, s, 0u, 0u, (uint32_t)n, lb, M->lrecs.as<MvRec>(),
                      nullptr, nullptr, nullptr, 0u, M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(), 0ull,
-                     M->pend.as<uint8_t>(), nullptr);
+                     M->set[0].pend.as<uint8_t>(), nullptr);
   hipLaunchKernelGGL(k_mv_upsert_insert, grid_stride(n), dim3(256), 0, s, 0u, 0u, (uint32_t)n, lb,
-                     M->lrecs.as<MvRec>(), M->pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask,
+                     M->lrecs.as<MvRec>(), M->set[0].pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask,
                      M->arena.as<uint8_t>(), M->top.as<unsigned long long>(), 0ull, nullptr);
   HIP_TRY(hipGetLastError());
   return read_top(c, M);
@@ -615,7 +638,7 @@ static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, ui
                          const uint8_t *in_flags, uint8_t *flags, size_t ntx, int commit) {
   hipStream_t s = c->stream;
   std::vector<MvTxInfo> info(ntx);
-  HIP_TRY(hipMemcpyAsync(info.data(), M->info.p, ntx * sizeof(MvTxInfo), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(info.data(), M->set[0].info.p, ntx * sizeof(MvTxInfo), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   // 1. decode the participating transactions' rwsets
   std::vector<std::vector<TxNs>> txs(ntx);
@@ -966,7 +989,7 @@ static int phantom_block(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, ui
 // keys' validation parameters
 static int kvmeta_deletes(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, const uint8_t *flags, size_t ntx) {
   std::vector<MvTxInfo> info(ntx);
-  HIP_TRY(hipMemcpy(info.data(), M->info.p, ntx * sizeof(MvTxInfo), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(info.data(), M->set[0].info.p, ntx * sizeof(MvTxInfo), hipMemcpyDeviceToHost));
   for (size_t i = 0; i < ntx; i++) {
     if (flags[i] != 0 || info[i].code != 0) continue;
     HTxRW rw;
@@ -989,11 +1012,58 @@ static int kvmeta_deletes(fgv_ctx *c, fgv_mvcc_state *M, const uint8_t *block, c
   return FGV_OK;
 }
 
+// rounds enqueued before the first host check: one more than the last block needed (a block
+// needing more pays one extra synchronisation); FGV_MVX_ROUNDS fixes the count (A/B)
+static uint32_t first_rounds(const fgv_mvcc_state *M) {
+  static const int fixed_rounds = [] {
+    const char *e = getenv("FGV_MVX_ROUNDS");
+    return e ? atoi(e) : 0;
+  }();
+  if (fixed_rounds > 0) return (uint32_t)fixed_rounds;
+  return M->last_rounds ? std::min<uint32_t>(std::max<uint32_t>(M->last_rounds + 1, 2), kRoundsPerEnqueue)
+                        : kRoundsPerEnqueue;
+}
+static uint32_t mvx_touch() {
+  static const uint32_t touch = [] {
+    const char *e = getenv("FGV_MVX_TOUCH");
+    return e ? (uint32_t)atoi(e) : 1u;
+  }();
+  return touch;
+}
+// k_mvx_extract transactions per workgroup (16 / 32 / 64; FGV_MVX_TPW, A/B)
+static uint32_t mvx_tpw() {
+  static const uint32_t v = [] {
+    const char *e = getenv("FGV_MVX_TPW");
+    const uint32_t x = e ? (uint32_t)atoi(e) : 64u;
+    return (x == 16u || x == 32u) ? x : 64u;
+  }();
+  return v;
+}
+// FGV_MVCC_SPIN=0: blocking waits (A/B); polled by default -- a block's GPU work is ~0.2 ms, and a
+// blocking synchronize's wake-up is a large share of that
+static bool mvcc_spin() {
+  static const bool spin = [] {
+    const char *e = getenv("FGV_MVCC_SPIN");
+    return !e || atoi(e) != 0;
+  }();
+  return spin;
+}
+
+static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block,
+                                uint64_t block_num, uint8_t *flags, size_t ntx, int commit, const uint8_t *next,
+                                size_t next_len);
+
 static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block, uint64_t block_num,
                          uint8_t *flags, size_t ntx, int commit, const uint8_t *next, size_t next_len) {
   if (!c || !block || (ntx && !flags)) return FGV_EINVAL;
   if (len >= 0xFFFFFFFFull || ntx >= 0x7FFFFFFFull) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  return mvcc_validate_locked(c, block, len, d_block, block_num, flags, ntx, commit, next, next_len);
+}
+
+static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block,
+                                uint64_t block_num, uint8_t *flags, size_t ntx, int commit, const uint8_t *next,
+                                size_t next_len) {
   fgv_mvcc_state *M = c->mv;
   if (!M) return FGV_ESTATE;
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
@@ -1022,10 +1092,10 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   const size_t rcap = len / 2 + 64;
   uint64_t bcap = 1024;
   while (bcap < 2 * rcap) bcap <<= 1;  // >= 2 x the writes any block of this size can hold
-  if (!M->hhead.ensure(hbytes) || !M->head.ensure(hbytes) || !M->info.ensure(ntx * sizeof(MvTxInfo)) ||
-      !M->reads.ensure(rcap * sizeof(MvRec)) || !M->writes.ensure(rcap * sizeof(MvRec)) ||
-      !M->wslot.ensure(rcap * 4) || !M->rslot.ensure(rcap * 4) || !M->pend.ensure(rcap + 64) ||
-      !M->bad.ensure(ntx + 64) || !M->st.ensure(ntx + 64) || !M->tail.ensure(kCounterBytes + ntx + 64) ||
+  if (!M->hhead.ensure(hbytes) || !M->set[0].head.ensure(hbytes) || !M->set[0].info.ensure(ntx * sizeof(MvTxInfo)) ||
+      !M->set[0].reads.ensure(rcap * sizeof(MvRec)) || !M->set[0].writes.ensure(rcap * sizeof(MvRec)) ||
+      !M->set[0].wslot.ensure(rcap * 4) || !M->set[0].rslot.ensure(rcap * 4) || !M->set[0].pend.ensure(rcap + 64) ||
+      !M->set[0].bad.ensure(ntx + 64) || !M->set[0].st.ensure(ntx + 64) || !M->set[0].tail.ensure(kCounterBytes + ntx + 64) ||
       !M->htail.ensure(kCounterBytes + ntx + 64 + 16))
     return FGV_ENOMEM;
   if (bcap > M->btbl_cap) {  // (re)allocated tables start with epoch 0 everywhere
@@ -1051,83 +1121,65 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   }
   memcpy(h + et_bytes, flags, ntx);
   memset(h + et_bytes + fl_bytes, 0, kCounterBytes);
-  uint8_t *dh = M->head.as<uint8_t>();
+  uint8_t *dh = M->set[0].head.as<uint8_t>();
   const uint32_t *d_et = reinterpret_cast<const uint32_t *>(dh);
   const uint8_t *d_in = dh + et_bytes;
   MvCounters *d_c = reinterpret_cast<MvCounters *>(dh + et_bytes + fl_bytes);
-  MvTxInfo *d_info = M->info.as<MvTxInfo>();
-  MvRec *d_r = M->reads.as<MvRec>(), *d_w = M->writes.as<MvRec>();
+  MvTxInfo *d_info = M->set[0].info.as<MvTxInfo>();
+  MvRec *d_r = M->set[0].reads.as<MvRec>(), *d_w = M->set[0].writes.as<MvRec>();
   BlkSlot *d_b = M->btbl.as<BlkSlot>();
-  uint8_t *d_out = M->tail.as<uint8_t>() + kCounterBytes;
+  uint8_t *d_out = M->set[0].tail.as<uint8_t>() + kCounterBytes;
   const uint32_t N = (uint32_t)ntx;
   const size_t top_off = (kCounterBytes + ntx + 7) & ~(size_t)7;  // (in htail, behind the flags)
   HIP_TRY(hipMemcpyAsync(dh, h, hbytes, hipMemcpyHostToDevice, s));
   HIP_TRY(hipEventRecord(c->ev[0], s));
-  static const uint32_t touch = [] {
-    const char *e = getenv("FGV_MVX_TOUCH");
-    return e ? (uint32_t)atoi(e) : 1u;
-  }();
+  const uint32_t touch = mvx_touch();
   // FGV_MVX_ONEWALK=0: the second rwset walk for every tx (A/B of the scratch copy)
   static const bool onewalk = [] {
     const char *e = getenv("FGV_MVX_ONEWALK");
     return !e || atoi(e) != 0;
   }();
-  if (onewalk && !M->xscr.ensure(ntx * 2 * MVX_SCR * sizeof(MvRec))) return FGV_ENOMEM;
-  hipLaunchKernelGGL(k_mvx_extract, dim3((N + 63) / 64), dim3(64), 0, s, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c,
-                     touch, onewalk ? M->xscr.as<MvRec>() : nullptr, M->bad.as<uint8_t>());
+  if (onewalk && !M->set[0].xscr.ensure(ntx * 2 * MVX_SCR * sizeof(MvRec))) return FGV_ENOMEM;
+  mvx_extract_launch(mvx_tpw(), s, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c, touch,
+                     onewalk ? M->set[0].xscr.as<MvRec>() : nullptr, M->set[0].bad.as<uint8_t>());
   hipLaunchKernelGGL(k_mvx_prep, grid_stride(rcap), dim3(256), 0, s, dblk, d_r, d_w, d_b, epoch,
-                     M->wslot.as<uint32_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
-                     M->bad.as<uint8_t>(), d_c);
+                     M->set[0].wslot.as<uint32_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
+                     M->set[0].bad.as<uint8_t>(), d_c, nullptr);
   HIP_TRY(hipEventRecord(c->ev[1], s));
   const uint32_t rg0 = M->rg;
   hipLaunchKernelGGL(k_mvx_find, grid_stride(rcap + ntx), dim3(256), 0, s, N, dblk, d_r, d_w, d_b, d_b, epoch,
-                     M->wslot.as<uint32_t>(), M->rslot.as<uint32_t>(), d_info, M->bad.as<uint8_t>(),
-                     M->st.as<uint8_t>(), rg0 + 1, d_c);
+                     M->set[0].wslot.as<uint32_t>(), M->set[0].rslot.as<uint32_t>(), d_info, M->set[0].bad.as<uint8_t>(),
+                     M->set[0].st.as<uint8_t>(), rg0 + 1, d_c);
   // fixpoint rounds, enqueued ahead: a round after convergence exits at once
   uint32_t r = 0;
   auto enqueue = [&](uint32_t k) -> int {
     for (uint32_t q = 0; q < k; q++) {
       r++;
       hipLaunchKernelGGL(k_mvx_round, dim3((N + 63) / 64), dim3(64), 0, s, N, r, rg0 + r, d_info,
-                         M->rslot.as<uint32_t>(), M->wslot.as<uint32_t>(), d_b, M->st.as<uint8_t>(), d_c);
+                         M->set[0].rslot.as<uint32_t>(), M->set[0].wslot.as<uint32_t>(), d_b, M->set[0].st.as<uint8_t>(), d_c);
     }
-    hipLaunchKernelGGL(k_mvx_flags, grid_for(ntx), dim3(256), 0, s, N, r, d_in, d_info, M->st.as<uint8_t>(), d_out,
+    hipLaunchKernelGGL(k_mvx_flags, grid_for(ntx), dim3(256), 0, s, N, r, d_in, d_info, M->set[0].st.as<uint8_t>(), d_out,
                        d_c);
     if (commit) {
-      hipLaunchKernelGGL(k_mv_last, grid_stride(rcap), dim3(256), 0, s, r, d_w, M->wslot.as<uint32_t>(),
-                         M->st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
+      hipLaunchKernelGGL(k_mv_last, grid_stride(rcap), dim3(256), 0, s, r, d_w, M->set[0].wslot.as<uint32_t>(),
+                         M->set[0].st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
       hipLaunchKernelGGL(k_mv_upsert_find, grid_stride(rcap), dim3(256), 0, s, 1u, r, 0u, dblk, d_w,
-                         M->wslot.as<uint32_t>(), M->st.as<uint8_t>(), d_b, epoch, M->tbl.as<StateSlot>(), M->mask,
-                         M->arena.as<uint8_t>(), block_num, M->pend.as<uint8_t>(), d_c);
+                         M->set[0].wslot.as<uint32_t>(), M->set[0].st.as<uint8_t>(), d_b, epoch, M->tbl.as<StateSlot>(), M->mask,
+                         M->arena.as<uint8_t>(), block_num, M->set[0].pend.as<uint8_t>(), d_c);
       hipLaunchKernelGGL(k_mv_upsert_insert, grid_stride(rcap), dim3(256), 0, s, 1u, r, 0u, dblk, d_w,
-                         M->pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
+                         M->set[0].pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
                          M->top.as<unsigned long long>(), block_num, d_c);
     }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(M->tail.p, d_c, sizeof(MvCounters), hipMemcpyDeviceToDevice, s));
-    HIP_TRY(hipMemcpyAsync(M->htail.p, M->tail.p, kCounterBytes + ntx, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(M->set[0].tail.p, d_c, sizeof(MvCounters), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemcpyAsync(M->htail.p, M->set[0].tail.p, kCounterBytes + ntx, hipMemcpyDeviceToHost, s));
     // the arena top after the commit rides on the same synchronisation (no second one)
     if (commit) HIP_TRY(hipMemcpyAsync(M->htail.as<uint8_t>() + top_off, M->top.p, 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(c->ev[2], s));
-    // polled: a block's GPU work is ~0.2 ms, and a blocking synchronize's wake-up is a large
-    // share of that (FGV_MVCC_SPIN=0: blocking, A/B)
-    static const bool spin = [] {
-      const char *e = getenv("FGV_MVCC_SPIN");
-      return !e || atoi(e) != 0;
-    }();
-    HIP_TRY(fgv_stream_wait(s, spin));
+    HIP_TRY(fgv_stream_wait(s, mvcc_spin()));
     return FGV_OK;
   };
-  // rounds enqueued before the first host check: one more than the last block needed (a block
-  // needing more pays one extra synchronisation); FGV_MVX_ROUNDS fixes the count (A/B)
-  static const int fixed_rounds = [] {
-    const char *e = getenv("FGV_MVX_ROUNDS");
-    return e ? atoi(e) : 0;
-  }();
-  const uint32_t first = fixed_rounds > 0 ? (uint32_t)fixed_rounds
-                         : M->last_rounds ? std::min<uint32_t>(std::max<uint32_t>(M->last_rounds + 1, 2), kRoundsPerEnqueue)
-                                          : kRoundsPerEnqueue;
-  int rc = enqueue(first);
+  int rc = enqueue(first_rounds(M));
   if (rc) return rc;
   const MvCounters *hc = M->htail.as<MvCounters>();
   while (!hc->unsup && !hc->done) {  // a longer dependency chain: more rounds
@@ -1159,6 +1211,274 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   return FGV_OK;
 }
 
+// ======================================================================= consecutive blocks
+// fgv_mvcc_validate_blocks: blocks k = first..n-1, validated (and committed) in order exactly as
+// one fgv_mvcc_validate_block call per block, but enqueued as ONE device chain with one wait:
+//   host   : the framing walks (taken from a pre-split of this very batch -- walked while the
+//            previous call's chain ran -- else walked here on the host pool, one block per job)
+//            fill the pinned heads (envelope table | flags | zeroed counters) of every block;
+//   stream2: ONE copy of all heads, then k_mvx_extract of block after block -- extraction reads
+//            no state, so it runs ahead of the chain;
+//   stream : per block k_mvx_prep (block k proceeds only when block k-1 was decided and committed
+//            on the device, else nothing of it runs: MV_HALT), k_mvx_find, the fixpoint rounds,
+//            k_mvx_flags, the commit, and k_mv_tail: codes, counters and arena top land straight
+//            in the block's pinned tail region.
+// kSets buffer sets rotate; the extraction of block k+kSets waits for block k's chain.  After the
+// wait the host takes the blocks in order: the device result of every block before the first one
+// the device did not finish (range queries or metadata writes -> the phantom path, a longer
+// fixpoint, unsupported, table full) is final; *stop = that block (n when all finished).
+static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, const uint8_t *const *blocks,
+                      const size_t *lens, const uint8_t *const *d_blocks, const uint64_t *block_nums,
+                      uint8_t *const *flags, const size_t *ntx, int commit, size_t *stop, size_t n_next,
+                      const uint8_t *const *next_blocks, const size_t *next_lens) {
+  *stop = first;
+  const size_t nb = n - first;
+  // per-block sizes and the offsets of their head / tail regions
+  std::vector<size_t> hoff(nb + 1, 0), toff(nb + 1, 0);
+  size_t max_len = 0, max_ntx = 0;
+  for (size_t k = 0; k < nb; k++) {
+    const size_t T = ntx[first + k];
+    const size_t et_bytes = (T * 8 + 63) & ~(size_t)63, fl_bytes = (T + 63) & ~(size_t)63;
+    hoff[k + 1] = hoff[k] + et_bytes + fl_bytes + kCounterBytes;
+    toff[k + 1] = toff[k] + ((kCounterBytes + T + 7) & ~(size_t)7) + 64;
+    max_len = std::max(max_len, lens[first + k]);
+    max_ntx = std::max(max_ntx, T);
+  }
+  const size_t rcap = max_len / 2 + 64;
+  uint64_t bcap = 1024;
+  while (bcap < 2 * rcap) bcap <<= 1;
+  if (!M->bhead.ensure(hoff[nb]) || !M->btail.ensure(toff[nb]) || !M->dheads.ensure(hoff[nb])) return FGV_ENOMEM;
+  const int nsets = (int)std::min<size_t>(kSets, nb);
+  for (int q = 0; q < nsets; q++) {
+    MvSet &S = M->set[q];
+    if (!S.info.ensure(max_ntx * sizeof(MvTxInfo)) || !S.reads.ensure(rcap * sizeof(MvRec)) ||
+        !S.writes.ensure(rcap * sizeof(MvRec)) || !S.wslot.ensure(rcap * 4) || !S.rslot.ensure(rcap * 4) ||
+        !S.pend.ensure(rcap + 64) || !S.bad.ensure(max_ntx + 64) || !S.st.ensure(max_ntx + 64) ||
+        !S.tail.ensure(kCounterBytes + max_ntx + 64) || !S.xscr.ensure(max_ntx * 2 * MVX_SCR * sizeof(MvRec)))
+      return FGV_ENOMEM;
+    if (!S.ev_x) HIP_TRY(hipEventCreateWithFlags(&S.ev_x, hipEventDisableTiming));
+    if (!S.ev_free) HIP_TRY(hipEventCreateWithFlags(&S.ev_free, hipEventDisableTiming));
+  }
+  bool need_copy = false;
+  for (size_t k = 0; k < nb; k++) need_copy |= !d_blocks || !d_blocks[first + k];
+  if (need_copy)
+    for (int q = 0; q < nsets; q++)
+      if (!M->set[q].blk.ensure(max_len + 64)) return FGV_ENOMEM;
+  hipStream_t s = c->stream, sx = c->stream2;
+  if (bcap > M->btbl_cap) {  // (re)allocated tables start with epoch 0 everywhere
+    M->btbl.release();
+    if (!M->btbl.ensure(bcap * sizeof(BlkSlot))) return FGV_ENOMEM;
+    HIP_TRY(hipMemsetAsync(M->btbl.p, 0, bcap * sizeof(BlkSlot), s));
+    M->btbl_cap = bcap;
+    M->epoch = 0;
+    M->rg = 0;
+  }
+  const uint32_t R = first_rounds(M);
+  uint64_t rg_need = 1024;
+  for (size_t k = 0; k < nb; k++) rg_need += 4 * (uint64_t)ntx[first + k] + R + 2;
+  if ((uint64_t)M->epoch + nb >= 0xFFFFFFFFull || (uint64_t)M->rg + rg_need > 0xFFFFFFFFull) {
+    HIP_TRY(hipMemsetAsync(M->btbl.p, 0, M->btbl_cap * sizeof(BlkSlot), s));
+    M->epoch = 0;
+    M->rg = 0;
+  }
+  // FGV_MVCC_ZC=0: the tails come back by copies (A/B)
+  static const bool zc_on = [] {
+    const char *e = getenv("FGV_MVCC_ZC");
+    return !e || atoi(e) != 0;
+  }();
+  uint8_t *d_btail = nullptr;
+  if (zc_on && hipHostGetDevicePointer(reinterpret_cast<void **>(&d_btail), M->btail.p, 0) != hipSuccess) d_btail = nullptr;
+  const bool zc = d_btail != nullptr;
+  // the heads: envelope spans from the pre-split of this batch, else the framing walks here (one
+  // walk is 0.2-1 ms of dependent loads over a 4 MB block: longer than the block's device work)
+  std::vector<uint8_t> walked(nb, 0);
+  const uint32_t *pet = nullptr;
+  const size_t *pntx = nullptr, *pfirst = nullptr;
+  const bool pre = fgv_block_take_presplit_batch(c->blk, nb, blocks + first, lens + first, &pet, &pntx, &pfirst);
+  const bool pre0 = !pre && fgv_block_take_presplit(c->blk, blocks[first], lens[first], M->pre_envs);
+  fgv_parallel_run(c->blk, nb, [&](size_t k) {
+    const size_t b = first + k, T = ntx[b];
+    const size_t et_bytes = (T * 8 + 63) & ~(size_t)63, fl_bytes = (T + 63) & ~(size_t)63;
+    uint8_t *h = M->bhead.as<uint8_t>() + hoff[k];
+    uint32_t *et = reinterpret_cast<uint32_t *>(h);
+    if (pre) {
+      if (pntx[k] != T) return;
+      const uint32_t *e = pet + BD_ENV_WORDS * pfirst[k];
+      for (size_t i = 0; i < T; i++, e += BD_ENV_WORDS) {
+        et[2 * i] = e[1];
+        et[2 * i + 1] = e[2];
+      }
+    } else {
+      VBlock vb;
+      const std::vector<Span> *envs = nullptr;
+      if (k == 0 && pre0) envs = &M->pre_envs;
+      else if (pbw::decode(blocks[b], lens[b], vb)) envs = &vb.data.data;
+      if (!envs || envs->size() != T) return;
+      for (size_t i = 0; i < T; i++) {
+        et[2 * i] = (uint32_t)((*envs)[i].p - blocks[b]);
+        et[2 * i + 1] = (*envs)[i].n;
+      }
+    }
+    memcpy(h + et_bytes, flags[b], T);
+    memset(h + et_bytes + fl_bytes, 0, kCounterBytes);
+    walked[k] = 1;
+  });
+  size_t nq = 0;  // blocks enqueued: up to the first one that is not a block of ntx transactions
+  while (nq < nb && walked[nq]) nq++;
+  if (nq == 0) return FGV_OK;  // (the single-block path reports that block's error)
+  // (stream2 starts after whatever the main stream holds: the table reset above, earlier calls)
+  HIP_TRY(hipEventRecord(c->ev[0], s));
+  HIP_TRY(hipStreamWaitEvent(sx, c->ev[0], 0));
+  uint8_t *dheads = M->dheads.as<uint8_t>();
+  HIP_TRY(hipMemcpyAsync(dheads, M->bhead.p, hoff[nq], hipMemcpyHostToDevice, sx));
+  const uint32_t touch = mvx_touch();
+  BlkSlot *d_b = M->btbl.as<BlkSlot>();
+  const MvCounters *prev_c = nullptr;
+  for (size_t k = 0; k < nq; k++) {
+    const size_t b = first + k;
+    const uint8_t *block = blocks[b];
+    const size_t len = lens[b], T = ntx[b];
+    MvSet &S = M->set[k % kSets];
+    const size_t et_bytes = (T * 8 + 63) & ~(size_t)63, fl_bytes = (T + 63) & ~(size_t)63;
+    // stream2: the set is free once block k-kSets's chain is done
+    if (k >= (size_t)kSets) HIP_TRY(hipStreamWaitEvent(sx, S.ev_free, 0));
+    const uint8_t *dblk = d_blocks ? d_blocks[b] : nullptr;
+    if (!dblk) {
+      HIP_TRY(hipMemcpyAsync(S.blk.p, block, len, hipMemcpyHostToDevice, sx));
+      dblk = S.blk.as<uint8_t>();
+    }
+    uint8_t *dh = dheads + hoff[k];
+    const uint32_t *d_et = reinterpret_cast<const uint32_t *>(dh);
+    const uint8_t *d_in = dh + et_bytes;
+    MvCounters *d_c = reinterpret_cast<MvCounters *>(dh + et_bytes + fl_bytes);
+    MvTxInfo *d_info = S.info.as<MvTxInfo>();
+    MvRec *d_r = S.reads.as<MvRec>(), *d_w = S.writes.as<MvRec>();
+    const uint32_t N = (uint32_t)T;
+    mvx_extract_launch(mvx_tpw(), sx, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c, touch, S.xscr.as<MvRec>(),
+                       S.bad.as<uint8_t>());
+    HIP_TRY(hipEventRecord(S.ev_x, sx));
+    // main stream: block k's chain
+    HIP_TRY(hipStreamWaitEvent(s, S.ev_x, 0));
+    const uint32_t epoch = ++M->epoch;
+    const uint32_t rg0 = M->rg;
+    // k_mvx_prep gates the block on block k-1 (prev_c: decided and committed on the device)
+    hipLaunchKernelGGL(k_mvx_prep, grid_stride(rcap), dim3(256), 0, s, dblk, d_r, d_w, d_b, epoch,
+                       S.wslot.as<uint32_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
+                       S.bad.as<uint8_t>(), d_c, prev_c);
+    hipLaunchKernelGGL(k_mvx_find, grid_stride(rcap + T), dim3(256), 0, s, N, dblk, d_r, d_w, d_b, d_b, epoch,
+                       S.wslot.as<uint32_t>(), S.rslot.as<uint32_t>(), d_info, S.bad.as<uint8_t>(), S.st.as<uint8_t>(),
+                       rg0 + 1, d_c);
+    for (uint32_t r = 1; r <= R; r++)
+      hipLaunchKernelGGL(k_mvx_round, dim3((N + 63) / 64), dim3(64), 0, s, N, r, rg0 + r, d_info,
+                         S.rslot.as<uint32_t>(), S.wslot.as<uint32_t>(), d_b, S.st.as<uint8_t>(), d_c);
+    // zero-copy: the codes, counters and arena top go straight to the block's pinned tail region
+    uint8_t *d_out = zc ? d_btail + toff[k] + kCounterBytes : S.tail.as<uint8_t>() + kCounterBytes;
+    hipLaunchKernelGGL(k_mvx_flags, grid_for(T), dim3(256), 0, s, N, R, d_in, d_info, S.st.as<uint8_t>(), d_out, d_c);
+    if (commit) {
+      hipLaunchKernelGGL(k_mv_last, grid_stride(rcap), dim3(256), 0, s, R, d_w, S.wslot.as<uint32_t>(),
+                         S.st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
+      hipLaunchKernelGGL(k_mv_upsert_find, grid_stride(rcap), dim3(256), 0, s, 1u, R, 0u, dblk, d_w,
+                         S.wslot.as<uint32_t>(), S.st.as<uint8_t>(), d_b, epoch, M->tbl.as<StateSlot>(), M->mask,
+                         M->arena.as<uint8_t>(), block_nums[b], S.pend.as<uint8_t>(), d_c);
+      hipLaunchKernelGGL(k_mv_upsert_insert, grid_stride(rcap), dim3(256), 0, s, 1u, R, 0u, dblk, d_w,
+                         S.pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
+                         M->top.as<unsigned long long>(), block_nums[b], d_c);
+    }
+    HIP_TRY(hipGetLastError());
+    uint8_t *ht = M->btail.as<uint8_t>() + toff[k];
+    const size_t top_off = (kCounterBytes + T + 7) & ~(size_t)7;
+    if (zc) {
+      uint8_t *dt = d_btail + toff[k];
+      hipLaunchKernelGGL(k_mv_tail, dim3(1), dim3(64), 0, s, d_c, M->top.as<unsigned long long>(),
+                         reinterpret_cast<uint32_t *>(dt),
+                         commit ? reinterpret_cast<unsigned long long *>(dt + top_off) : nullptr);
+    } else {
+      HIP_TRY(hipMemcpyAsync(S.tail.p, d_c, sizeof(MvCounters), hipMemcpyDeviceToDevice, s));
+      HIP_TRY(hipMemcpyAsync(ht, S.tail.p, kCounterBytes + T, hipMemcpyDeviceToHost, s));
+      if (commit) HIP_TRY(hipMemcpyAsync(ht + top_off, M->top.p, 16, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipEventRecord(S.ev_free, s));  // the set's last reader of block k is done
+    M->rg = rg0 + R + 2;  // round tags of this block: rg0 + 1 .. rg0 + R + 1
+    prev_c = d_c;
+  }
+  HIP_TRY(hipEventRecord(c->ev[2], s));
+  // the next batch's framing walks run on the pre-split worker while this chain runs
+  if (n_next) fgv_block_presplit(c->blk, c->device, n_next, next_blocks, next_lens, nullptr, nullptr);
+  HIP_TRY(fgv_stream_wait(s, mvcc_spin()));
+  float ms = 0;
+  c->t_mvcc_lookup = 0;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[2]) == hipSuccess) c->t_mvcc_total = ms / (double)nq;
+  c->n_mvcc_reads = c->n_mvcc_writes = 0;
+  uint32_t rounds = 0;
+  size_t k = 0;
+  for (; k < nq; k++) {
+    const size_t b = first + k, T = ntx[b];
+    const uint8_t *ht = M->btail.as<uint8_t>() + toff[k];
+    const MvCounters *hc = reinterpret_cast<const MvCounters *>(ht);
+    if (hc->unsup || !hc->done || (commit && hc->nomem)) break;
+    memcpy(flags[b], ht + kCounterBytes, T);
+    if (commit) {
+      uint64_t t[2];
+      memcpy(t, ht + ((kCounterBytes + T + 7) & ~(size_t)7), 16);
+      M->arena_used = t[0];
+      M->nkeys = t[1];
+    }
+    c->n_mvcc_reads += hc->nr;
+    c->n_mvcc_writes += hc->nw;
+    rounds = std::max(rounds, hc->rounds);
+  }
+  if (rounds) M->last_rounds = rounds;
+  *stop = first + k;
+  return FGV_OK;
+}
+
+static int mvcc_blocks(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const size_t *lens,
+                       const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
+                       const size_t *ntx, int commit, size_t *n_done, size_t n_next,
+                       const uint8_t *const *next_blocks, const size_t *next_lens) {
+  size_t done = 0;
+  if (n_done) *n_done = 0;
+  if (!c || (n && (!blocks || !lens || !block_nums || !flags || !ntx))) return FGV_EINVAL;
+  for (size_t k = 0; k < n; k++)
+    if (!blocks[k] || (ntx[k] && !flags[k]) || lens[k] >= 0xFFFFFFFFull || ntx[k] >= 0x7FFFFFFFull) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  fgv_mvcc_state *M = c->mv;
+  if (!M) return FGV_ESTATE;
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  // FGV_MVCC_CHAIN=0: one single-block call per block (A/B)
+  static const bool chain = [] {
+    const char *e = getenv("FGV_MVCC_CHAIN");
+    return !e || atoi(e) != 0;
+  }();
+  while (done < n) {
+    // key-level state is kept current by the single-block path's host step (kvmeta_deletes); an
+    // empty block has no device work
+    size_t stop = done;
+    if (chain && ntx[done] > 0 && !(commit && fgv_block_kvmeta_count(c->blk) > 0)) {
+      size_t end = done;
+      while (end < n && ntx[end] > 0) end++;
+      const int rc = mvcc_chain(c, M, done, end, blocks, lens, d_blocks, block_nums, flags, ntx, commit, &stop,
+                                n_next, next_blocks, next_lens);
+      n_next = 0;  // (the next batch is being walked)
+      if (rc) {
+        if (n_done) *n_done = done;
+        return rc;
+      }
+      done = stop;
+      if (n_done) *n_done = done;
+      if (done == n) break;
+    }
+    // the first block the chain did not finish: the single-block path (phantom validators, more
+    // rounds, or the error it returns)
+    const int rc = mvcc_validate_locked(c, blocks[done], lens[done], d_blocks ? d_blocks[done] : nullptr,
+                                        block_nums[done], flags[done], ntx[done], commit, nullptr, 0);
+    if (rc) return rc;
+    done++;
+    if (n_done) *n_done = done;
+  }
+  return FGV_OK;
+}
+
 extern "C" {
 
 int fgv_mvcc_validate_block(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block,
@@ -1171,6 +1491,21 @@ int fgv_mvcc_validate_block_next(fgv_ctx *c, const uint8_t *block, size_t len, c
                                  size_t next_len) {
   if (next && !next_len) return FGV_EINVAL;
   return mvcc_validate(c, block, len, d_block, block_num, flags, ntx, commit, next, next_len);
+}
+
+int fgv_mvcc_validate_blocks(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const size_t *lens,
+                             const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
+                             const size_t *ntx, int commit, size_t *n_done) {
+  return mvcc_blocks(c, n, blocks, lens, d_blocks, block_nums, flags, ntx, commit, n_done, 0, nullptr, nullptr);
+}
+
+int fgv_mvcc_validate_blocks_next(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const size_t *lens,
+                                  const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
+                                  const size_t *ntx, int commit, size_t *n_done, size_t n_next,
+                                  const uint8_t *const *next_blocks, const size_t *next_lens) {
+  if (n_next && (!next_blocks || !next_lens)) return FGV_EINVAL;
+  return mvcc_blocks(c, n, blocks, lens, d_blocks, block_nums, flags, ntx, commit, n_done, n_next, next_blocks,
+                     next_lens);
 }
 
 int fgv_mvcc_last_stats(fgv_ctx *c, double *lookup_ms, double *total_ms, uint64_t *reads, uint64_t *writes,

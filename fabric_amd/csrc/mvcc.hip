@@ -422,40 +422,87 @@ DEV uint32_t bmask_of(uint32_t nw) {
 }  // namespace
 
 // ============================================================ rwset extraction
-// One lane per tx: the TxReadWriteSet walked twice by the same lane -- counting, then (its
-// record ranges claimed by wave-aggregated atomics) emitting 48-byte records + 64-bit tags --
-// so the second walk finds the rwset bytes in the lane's caches: the block is read from HBM once.
+// One workgroup (one wave) per TPW transactions.  The wave first copies the group's
+// envelopes into LDS -- coalesced dword loads, every envelope's lines in flight at once -- then
+// lane j walks transaction j's TxReadWriteSet from LDS (pbwire_dev.h rules) through a "virtual
+// base" (the LDS copy minus the envelope's block offset), so record offsets stay block-relative
+// while every dependent load of the walk is an LDS access instead of a cache / HBM round trip.
+// An envelope larger than CAP is walked from global memory (its lines requested up front).
+// The counting walk writes the records to the per-tx scratch too, so a tx within it is copied
+// instead of walked a second time; record ranges are claimed by wave-aggregated atomics.
 // Duplicate writes of one key in one tx (tx_ops.go:183-191 adds flags: undefined semantics)
 // -> unsupported.
-// touch: every line of the envelope is requested up front (touch_lines), so the walk's chain of
-// dependent loads hits the caches (FGV_MVX_TOUCH=0 turns it off, A/B)
-// scr (nullable): per-tx scratch of MVX_SCR reads + MVX_SCR writes; the counting walk writes
-// the records there too, so a tx within it is copied instead of walked a second time
-__global__ __launch_bounds__(64) void k_mvx_extract(uint32_t ntx, const uint8_t *__restrict__ base,
-                                                    const uint32_t *__restrict__ envtab,
-                                                    const uint8_t *__restrict__ in_flags, MvTxInfo *__restrict__ info,
-                                                    MvRec *__restrict__ reads, MvRec *__restrict__ writes,
-                                                    MvCounters *__restrict__ c, uint32_t touch, MvRec *__restrict__ scr,
-                                                    uint8_t *__restrict__ bad) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+// touch (global walks only): FGV_MVX_TOUCH=0 turns the up-front line requests off (A/B)
+// scr (nullable): per-tx scratch of MVX_SCR reads + MVX_SCR writes
+template <uint32_t TPW>
+__device__ __forceinline__ void mvx_extract(uint32_t ntx, const uint8_t *__restrict__ base,
+                                            const uint32_t *__restrict__ envtab, const uint8_t *__restrict__ in_flags,
+                                            MvTxInfo *__restrict__ info, MvRec *__restrict__ reads,
+                                            MvRec *__restrict__ writes, MvCounters *__restrict__ c, uint32_t touch,
+                                            MvRec *__restrict__ scr, uint8_t *__restrict__ bad) {
+  // LDS bytes per transaction (larger envelopes walk global memory): 48 KB per workgroup at 64
+  constexpr uint32_t CAP = TPW == 64 ? 768u : 1536u;
+  __shared__ uint32_t lds[TPW * (CAP / 4)];
+  __shared__ uint32_t pre[TPW + 1], src0[TPW];  // dword prefix of the staged envelopes, source dword
+  const uint32_t lane = threadIdx.x, t0 = blockIdx.x * TPW;
+  // stage: the dwords covering [off, off + len + 8) of each committer-valid envelope (the walk's
+  // over-read contract: up to 7 bytes past a span; block buffers carry >= 64 B of tail padding).
+  // Lane j reads transaction j's table entry; then every lane copies dwords of the concatenated
+  // envelopes (independent loads, all in flight).
+  uint32_t my_nw = 0;
+  if (lane < TPW && t0 + lane < ntx && in_flags[t0 + lane] == 0) {
+    const uint32_t off = envtab[2 * (t0 + lane)], len = envtab[2 * (t0 + lane) + 1];
+    const uint32_t a0 = off & ~3u, nwd = ((off + len + 8u + 3u) & ~3u) / 4u - a0 / 4u;
+    if (nwd <= CAP / 4) {
+      my_nw = nwd;
+      src0[lane] = a0 / 4u;
+    }
+  }
+  // inclusive prefix over the TPW lanes (wave scan)
+  uint32_t v = my_nw;
+  for (uint32_t d = 1; d < TPW; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)v, d);
+    if (lane >= d) v += o;
+  }
+  if (lane < TPW) pre[lane + 1] = v;
+  if (lane == 0) pre[0] = 0;
+  __syncthreads();
+  const uint32_t total = pre[TPW];
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(base);
+  for (uint32_t i = lane; i < total; i += 64) {
+    uint32_t j = 0;  // the envelope of dword i: pre[j] <= i < pre[j + 1]
+#pragma unroll
+    for (uint32_t b = TPW / 2; b > 0; b >>= 1)
+      if (pre[j + b] <= i) j += b;
+    const uint32_t k = i - pre[j];
+    lds[j * (CAP / 4) + k] = src[src0[j] + k];
+  }
+  __syncthreads();
+  const uint32_t t = lane < TPW ? t0 + lane : ntx;
   uint32_t nr = 0, nw = 0;
   uint64_t wb = 0;
   MvTxInfo I{};
   bool copied = false;
+  const uint8_t *vb = base;  // the walk's base: block offsets -> bytes (LDS copy or global)
   if (t < ntx) {
     bad[t] = 0;  // (k_mvx_prep marks static conflicts after this kernel: no separate memset)
     I.code = MV_SKIP;
-    if (touch && in_flags[t] == 0) touch_lines(base + envtab[2 * t], envtab[2 * t + 1]);
     if (in_flags[t] == 0) {
+      const uint32_t off = envtab[2 * t], len = envtab[2 * t + 1];
+      const uint32_t a0 = off & ~3u, nwd = ((off + len + 8u + 3u) & ~3u) / 4u - a0 / 4u;
+      if (nwd <= CAP / 4)
+        vb = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(lds + lane * (CAP / 4)) - a0);
+      else if (touch)
+        touch_lines(base + off, len);
       S results{nullptr, 0};
-      I.code = find_results(S{base + envtab[2 * t], envtab[2 * t + 1]}, results);
+      I.code = find_results(S{vb + off, len}, results);
       if (I.code == 0) {
         MvRec *sr = scr ? scr + (size_t)t * (2 * MVX_SCR) : nullptr;
-        Sink sk{base, sr, sr ? sr + MVX_SCR : nullptr, t, 0, 0, 0, false};
+        Sink sk{vb, sr, sr ? sr + MVX_SCR : nullptr, t, 0, 0, 0, false};
         sk.kmax = MVX_SCR;
         bool host = false;
         I.code = walk_rwset(results, sk, host);
-        I.rws_off = (uint32_t)(results.p - base);
+        I.rws_off = (uint32_t)(results.p - vb);
         I.rws_len = results.n;
         if (I.code == 0) { nr = sk.nr; nw = sk.nw; wb = sk.wbytes; }
         copied = sr && !sk.spill;
@@ -470,30 +517,53 @@ __global__ __launch_bounds__(64) void k_mvx_extract(uint32_t ntx, const uint8_t 
   I.wbeg = wave_claim(nw, &c->nw);
   I.rcnt = nr;
   I.wcnt = nw;
-  for (int off = 32; off > 0; off >>= 1) wb += __shfl_down(wb, off);
-  if ((threadIdx.x & 63u) == 0 && wb) atomicAdd(&c->wbytes, (unsigned long long)wb);
+  for (int o = 32; o > 0; o >>= 1) wb += __shfl_down(wb, o);
+  if (lane == 0 && wb) atomicAdd(&c->wbytes, (unsigned long long)wb);
   if (t >= ntx) return;
   if (I.code == 0) {
-    if (copied) {  // (independent 16-byte copies instead of a second chain of dependent loads)
+    if (copied) {  // (independent 16-byte copies instead of a second walk)
       const MvRec *sr = scr + (size_t)t * (2 * MVX_SCR);
       for (uint32_t k = 0; k < I.rcnt; k++) reads[I.rbeg + k] = sr[k];
       for (uint32_t k = 0; k < I.wcnt; k++) writes[I.wbeg + k] = sr[MVX_SCR + k];
     } else {
-      Sink sk{base, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
+      Sink sk{vb, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
       bool host = false;
-      walk_rwset(S{base + I.rws_off, I.rws_len}, sk, host);
+      walk_rwset(S{vb + I.rws_off, I.rws_len}, sk, host);
     }
-    const MvRec *w = writes + I.wbeg;
+    const MvRec *w = copied ? scr + (size_t)t * (2 * MVX_SCR) + MVX_SCR : writes + I.wbeg;
     bool dup = false;
     for (uint32_t a = 0; a < I.wcnt && !dup; a++)
       for (uint32_t b = a + 1; b < I.wcnt; b++)
-        if (rec_eq(base, w[a], w[b])) { dup = true; break; }
+        if (rec_eq(vb, w[a], w[b])) { dup = true; break; }
     if (dup) {
       I.code = MV_UNSUP;
       atomicOr(&c->unsup, 1u);
     }
   }
   info[t] = I;
+}
+template <uint32_t TPW>
+__global__ __launch_bounds__(64) void k_mvx_extract_t(uint32_t ntx, const uint8_t *__restrict__ base,
+                                                      const uint32_t *__restrict__ envtab,
+                                                      const uint8_t *__restrict__ in_flags, MvTxInfo *__restrict__ info,
+                                                      MvRec *__restrict__ reads, MvRec *__restrict__ writes,
+                                                      MvCounters *__restrict__ c, uint32_t touch, MvRec *__restrict__ scr,
+                                                      uint8_t *__restrict__ bad) {
+  mvx_extract<TPW>(ntx, base, envtab, in_flags, info, reads, writes, c, touch, scr, bad);
+}
+// transactions per workgroup (16 / 32 / 64): host picks (fgv_mvcc.cpp mvx_launch)
+void mvx_extract_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint8_t *base, const uint32_t *envtab,
+                        const uint8_t *in_flags, MvTxInfo *info, MvRec *reads, MvRec *writes, MvCounters *c,
+                        uint32_t touch, MvRec *scr, uint8_t *bad) {
+  if (tpw == 64)
+    hipLaunchKernelGGL(k_mvx_extract_t<64>, dim3((ntx + 63) / 64), dim3(64), 0, st, ntx, base, envtab, in_flags, info,
+                       reads, writes, c, touch, scr, bad);
+  else if (tpw == 32)
+    hipLaunchKernelGGL(k_mvx_extract_t<32>, dim3((ntx + 31) / 32), dim3(64), 0, st, ntx, base, envtab, in_flags, info,
+                       reads, writes, c, touch, scr, bad);
+  else
+    hipLaunchKernelGGL(k_mvx_extract_t<16>, dim3((ntx + 15) / 16), dim3(64), 0, st, ntx, base, envtab, in_flags, info,
+                       reads, writes, c, touch, scr, bad);
 }
 
 // ============================================================ lookups
@@ -504,7 +574,14 @@ __global__ __launch_bounds__(256) void k_mvx_prep(const uint8_t *__restrict__ ba
                                                   uint32_t epoch, uint32_t *__restrict__ wslot,
                                                   const StateSlot *__restrict__ tbl, uint64_t mask,
                                                   const uint8_t *__restrict__ arena, uint8_t *__restrict__ bad,
-                                                  const MvCounters *__restrict__ c) {
+                                                  MvCounters *__restrict__ c, const MvCounters *__restrict__ prev) {
+  // a chain of blocks (fgv_mvcc_validate_blocks): block k runs only when block k-1 was decided
+  // and committed on the device; else nothing of it runs (MV_HALT) and the host takes over from
+  // the first such block, in block order
+  if (prev && (prev->unsup || !prev->done || prev->nomem)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&c->unsup, MV_HALT);
+    return;
+  }
   const uint32_t nr = c->nr, nw = c->nw, bm = bmask_of(nw);
   if (c->unsup) return;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nr + nw; i += gridDim.x * blockDim.x) {
@@ -759,6 +836,17 @@ __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_
       }
     }
   }
+}
+
+// The tail of a block of a chain written straight into pinned host memory (no copy kernels):
+// its counters and, after a commit, the arena top (k_mvx_flags wrote the codes there already)
+__global__ __launch_bounds__(64) void k_mv_tail(const MvCounters *__restrict__ c, const unsigned long long *__restrict__ top,
+                                                uint32_t *__restrict__ hc, unsigned long long *__restrict__ htop) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(c);
+  if (t < sizeof(MvCounters) / 4) hc[t] = w[t];
+  if (htop && t < 2) htop[t] = top[t];
+  __threadfence_system();
 }
 
 // host-supplied key records (load / apply): tags

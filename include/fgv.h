@@ -471,6 +471,26 @@ int fgv_mvcc_validate_block(fgv_ctx *ctx, const uint8_t *block, size_t len, cons
 int fgv_mvcc_validate_block_next(fgv_ctx *ctx, const uint8_t *block, size_t len, const uint8_t *d_block,
                                  uint64_t block_num, uint8_t *flags, size_t ntx, int commit,
                                  const uint8_t *next, size_t next_len);
+/* n consecutive blocks of one channel, validated and (commit != 0) committed in order: the result
+ * is exactly that of one fgv_mvcc_validate_block call per block (each block reads the state the
+ * blocks before it committed, as the reference's committer does: kv_ledger.go CommitLegacy ->
+ * txmgr.ValidateAndPrepare -> Commit per block, one block at a time).  The engine enqueues the
+ * blocks as one device chain with one wait: block k+1's rwset extraction runs while block k is
+ * checked and committed.  A block the device cannot finish on its own (range queries, metadata
+ * writes, a long conflict chain) and the blocks after it continue through the single-block path.
+ * Stops at the first block whose call would fail and returns that error; *n_done (optional) =
+ * the blocks whose flags are final (and committed).  d_blocks may be NULL or hold NULLs. */
+int fgv_mvcc_validate_blocks(fgv_ctx *ctx, size_t n, const uint8_t *const *blocks, const size_t *lens,
+                             const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
+                             const size_t *ntx, int commit, size_t *n_done);
+/* fgv_mvcc_validate_blocks that also walks the NEXT batch's framing (next_blocks / next_lens,
+ * n_next blocks; the buffers must stay unchanged until that batch's call) on the engine's host
+ * worker while this batch's chain runs; that call then starts from the walked envelope spans.
+ * Results never depend on it. */
+int fgv_mvcc_validate_blocks_next(fgv_ctx *ctx, size_t n, const uint8_t *const *blocks, const size_t *lens,
+                                  const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
+                                  const size_t *ntx, int commit, size_t *n_done, size_t n_next,
+                                  const uint8_t *const *next_blocks, const size_t *next_lens);
 int fgv_mvcc_last_stats(fgv_ctx *ctx, double *lookup_ms, double *total_ms, uint64_t *reads,
                         uint64_t *writes, uint32_t *rounds);
 
