@@ -2023,9 +2023,10 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     const char *e = getenv("FGV_PARSE_TOUCH");
     return e ? (uint32_t)atoi(e) : 1u;
   }();
-  // transactions (walking lanes) per workgroup: fewer lanes per wave = fewer distinct lines per
-  // load instruction in the walk's dependent chain, and more waves over the SIMDs (the LDS arrays
-  // stay sized for 64 lanes); FGV_PARSE_LANES = 16 / 32 / 64 (A/B)
+  // transactions (walking lanes) per workgroup (the LDS arrays stay sized for 64 lanes);
+  // FGV_PARSE_LANES = 16 / 32 / 64 (A/B).  Measured on MI355X (C2 lean harness, two alternating
+  // rounds, profiles/round3_ab/parse_lanes_*): 64 -> 0.690 / 0.722 ms per step, 32 -> 0.706 /
+  // 0.720, 16 -> 0.794 / 0.811: fewer lanes per wave does not shorten the walk; 64 stays
   static const uint32_t parse_lanes = [] {
     const char *e = getenv("FGV_PARSE_LANES");
     const uint32_t v = e ? (uint32_t)atoi(e) : 64u;

@@ -1018,7 +1018,8 @@ static int fin_front(fgv_ctx *c, hipStream_t st, size_t nblocks, uint32_t W, siz
   hipLaunchKernelGGL(k_fin_rows, dim3((uint32_t)((std::max<size_t>(F.P, F.cap) + 255) / 256)), blk, 0, st, n32,
                      d_bstart, (uint32_t)nblocks, W, (uint32_t)rows, d_roff, d_roff + F.wn, d_roff + 2 * F.wn,
                      c->fz_rowmap.as<uint32_t>(), c->fz_blkof.as<uint32_t>(), (uint32_t)F.cap,
-                     c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), c->fz_minvalid.as<uint32_t>());
+                     c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), c->fz_minvalid.as<uint32_t>(), dtx,
+                     bases, digests, dtx ? c->fz_keys.as<uint8_t>() : nullptr);
   if (dtx)
     hipLaunchKernelGGL(k_fin_index_dev, grid, blk, 0, st, n32, dtx, bases, digests, c->fz_keys.as<uint8_t>(),
                        c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask, c->fin_seed);

@@ -1030,12 +1030,14 @@ static uint32_t mvx_touch() {
   }();
   return touch;
 }
-// k_mvx_extract transactions per workgroup (16 / 32 / 64; FGV_MVX_TPW, A/B)
+// k_mvx_extract transactions per workgroup (16 / 32 / 64; FGV_MVX_TPW, A/B).  Measured on MI355X
+// (chained C3, two alternating rounds, profiles/round3_ab/mvx_tpw*): 32 -> 60.0 / 63.6 M tx/s,
+// 64 -> 54.6 / 55.3, 16 -> 45.8 / 51.1
 static uint32_t mvx_tpw() {
   static const uint32_t v = [] {
     const char *e = getenv("FGV_MVX_TPW");
-    const uint32_t x = e ? (uint32_t)atoi(e) : 64u;
-    return (x == 16u || x == 32u) ? x : 64u;
+    const uint32_t x = e ? (uint32_t)atoi(e) : 32u;
+    return (x == 16u || x == 64u) ? x : 32u;
   }();
   return v;
 }

@@ -95,9 +95,14 @@ __device__ inline bool dev_index_key(const DevTx &R, const uint64_t *bases, cons
 // rank r holds transactions [rlo[r][b], rlo[r][b] + rcnt[r][b]) of block b, at its rows from
 // roff[r][b] (any shard plan whose ranges tile every block).  Also resets the txid table
 // (slots [0, cap)): the grid covers max(P, cap).
+// For a single-device batch (txs != null) it also writes every position's index key to `keys`:
+// k_fin_index_dev compares other owners' keys with plain loads -- written by this earlier kernel,
+// so no device-scope fence inside the insert (on MI355X an agent-scope release writes back the
+// whole L2 of the XCD: it made the insert 60-240 us beside the verify chain).
 __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, uint32_t W, uint32_t rows,
                            const uint32_t *roff, const uint32_t *rlo, const uint32_t *rcnt, uint32_t *rowmap,
-                           uint32_t *blkof, uint32_t cap, uint32_t *owner, int32_t *minblk, uint32_t *minvalid) {
+                           uint32_t *blkof, uint32_t cap, uint32_t *owner, int32_t *minblk, uint32_t *minvalid,
+                           const DevTx *txs, const uint64_t *bases, const uint8_t *digests, uint8_t *keys) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < cap) {
     owner[p] = 0u;
@@ -105,6 +110,14 @@ __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, u
     minvalid[p] = 0xFFFFFFFFu;
   }
   if (p >= P) return;
+  if (txs) {
+    uint32_t k[8];
+    if (dev_index_key(txs[p], bases, digests, P, p, k)) {
+      uint32_t *kd = reinterpret_cast<uint32_t *>(keys + (size_t)p * 32);
+#pragma unroll
+      for (int i = 0; i < 8; i++) kd[i] = k[i];
+    }
+  }
   uint32_t lo = 0, hi = nb;  // last b with blk_start[b] <= p
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -159,11 +172,7 @@ __global__ void k_fin_index_dev(uint32_t P, const DevTx *txs, const uint64_t *ba
   const DevTx &R = txs[p];
   uint32_t k[8];
   if (!dev_index_key(R, bases, digests, P, p, k)) return;
-  uint32_t *kd = reinterpret_cast<uint32_t *>(keys + (size_t)p * 32);
-#pragma unroll
-  for (int i = 0; i < 8; i++) kd[i] = k[i];
-  __threadfence();  // (the key is visible before the slot names its owner)
-  const uint64_t h = fin_hash(k, seed);
+  const uint64_t h = fin_hash(k, seed);  // (every key is in `keys` already: k_fin_rows)
   const int32_t b = (int32_t)R.blk;
   for (uint32_t probe = 0; probe <= mask; probe++) {
     const uint32_t s = (uint32_t)(h + probe) & mask;
@@ -178,7 +187,7 @@ __global__ void k_fin_index_dev(uint32_t P, const DevTx *txs, const uint64_t *ba
     const uint32_t *q = reinterpret_cast<const uint32_t *>(keys + (size_t)(o - 1) * 32);
     bool eq = true;
 #pragma unroll
-    for (int i = 0; i < 8; i++) eq &= __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k[i];
+    for (int i = 0; i < 8; i++) eq &= q[i] == k[i];
     if (eq) {
       atomicMin(&minblk[s], b);
       return;

@@ -1,0 +1,19 @@
+#!/bin/bash
+# round 3: txid-index keys written by k_fin_rows (no device-scope fence in k_fin_index_dev) and
+# the k_mvx_extract workgroup-width A/B: the full GPU suite, C2 lean x3, the default bench, a C2
+# trace, then tools/gpu_r3u.sh
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r3v
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { echo tests failed; tail -60 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for rep in 1 2 3; do
+  timeout -k 10 300 python -u bench.py --steps 60 --warmup 5 --cpu-threads 0 --no-pcie --no-latency > $O/lean_$rep.json 2> $O/lean_$rep.err || { echo lean failed; tail -20 $O/lean_$rep.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/lean_$rep.json')); print('lean rep $rep', d['value'], d['ms_per_step'], d['parity_vs_labels'], d['kernel_ms'])"
+done
+timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail -20 $O/bench.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench.json')); print('default', d['value'], d['ms_per_step'], d['parity_vs_labels'], d['roofline']['kernel'], d['roofline']['frac'], d['pcie_inclusive']['ms_per_step'])"
+timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace -d $O/tc2 -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $O/tc2.json 2> $O/tc2.err || { echo trace failed; tail -20 $O/tc2.err; exit 1; }
+bash tools/gpu_r3u.sh
