@@ -23,7 +23,7 @@ EXPORTED = [
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
-    "fgv_presplit", "fgv_last_presplit", "fgv_validate_shard_dev_next", "fgv_mvcc_validate_block_next",
+    "fgv_presplit", "fgv_prefetch", "fgv_last_presplit", "fgv_validate_shard_dev_next", "fgv_mvcc_validate_block_next",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_statedb_apply", "fgv_statedb_stats", "fgv_mvcc_validate_block", "fgv_mvcc_validate_blocks", "fgv_mvcc_validate_blocks_next", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash",
     "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
@@ -140,6 +140,7 @@ def load():
         L.fgv_validate_shard_dev.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
         L.fgv_finalize_flags_dev.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp]
         L.fgv_presplit.argtypes = [vp, sz, vp, vp, vp, vp]
+        L.fgv_prefetch.argtypes = [vp, sz, vp, vp]
         L.fgv_validate_shard_dev_next.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp, vp, vp, vp]
         L.fgv_last_presplit.argtypes = [vp]
         L.fgv_validate_shard_dev_pipelined.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, sz, vp, sz, vp, vp, vp, vp, vp]
@@ -653,6 +654,12 @@ class Engine:
         _check(self._L.fgv_validate_shard_dev(self._h, batch.nb, batch.ptrs, batch.lens, batch.dptr, _ptr(lo),
                                               _ptr(hi), ctypes.c_void_p(d_results), cap, batch.ntx))
         return np.ctypeslib.as_array(batch.ntx).astype(np.uint64)
+
+    def prefetch(self, batch):
+        """fgv_prefetch: queue the H2D copy of a later host-resident batch (block_batch(...) of
+        pinned blocks) on the engine's copy stream now; its validation call uses the staged copy."""
+        assert isinstance(batch, _BlockBatch)
+        _check(self._L.fgv_prefetch(self._h, batch.nb, batch.ptrs, batch.lens))
 
     def presplit(self, batch, tx_lo=None, tx_hi=None):
         """fgv_presplit: walk the batch's block framing on a background host thread for the

@@ -100,7 +100,8 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->streamF, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
   }
-  if (hipEventCreateWithFlags(&c->pf.ev, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
+  for (auto &e : c->stage_ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
   {
     std::random_device rd;  // per-context hash seed of the finalize txid table
     c->fin_seed = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)(uintptr_t)c;
@@ -143,7 +144,7 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   for (hipStream_t x : {c->stream2, c->stream3, c->streamF})  // (a front half enqueued ahead)
     if (x) hipStreamSynchronize(x);
-  DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
+  DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->stage[2], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
                  &c->bd_misc, &c->g_ok, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
                  &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
@@ -168,7 +169,8 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->stream3) hipStreamDestroy(c->stream3);
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   if (c->streamF) hipStreamDestroy(c->streamF);
-  if (c->pf.ev) hipEventDestroy(c->pf.ev);
+  for (auto e : c->stage_ev)
+    if (e) hipEventDestroy(e);
   delete c;
 }
 
@@ -1125,8 +1127,25 @@ static int copy_runs(size_t nblocks, const uint8_t *const *blocks, const size_t 
   return FGV_OK;
 }
 
-// Host-resident blocks -> device.  A batch that the previous _next call prefetched is already
-// on its way (copy stream): the compute stream waits for that copy instead of copying again.
+// A staging slot no staged batch holds and the current call's batch does not use (every earlier
+// call has completed: each validation call ends synchronised); with none free the oldest staged
+// batch is dropped (its front half, if enqueued ahead, is drained first).
+static int free_slot(fgv_ctx *c, int avoid) {
+  for (;;) {
+    for (int q = 0; q < fgv_ctx::kStage; q++) {
+      if (q == avoid) continue;
+      bool held = false;
+      for (const auto &e : c->pf) held |= e.slot == q;
+      if (!held) return q;
+    }
+    fgv_block_drain(c);  // (a front half enqueued ahead may read the arena about to be reused)
+    c->pf.erase(c->pf.begin());
+  }
+}
+
+// Host-resident blocks -> device.  A batch staged ahead (the previous _next / pipelined call's
+// NEXT batch, or fgv_prefetch) is already on its way (copy stream): the compute stream waits
+// for that copy instead of copying again.
 static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                         const uint8_t *const *d_blocks, std::vector<const uint8_t *> &dev) {
   dev.resize(nblocks);
@@ -1136,52 +1155,67 @@ static int stage_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks
     for (size_t b = 0; b < nblocks; b++) dev[b] = d_blocks[b];
     return FGV_OK;
   }
-  if (c->pf.on && c->pf.src.size() == nblocks) {
-    bool hit = true;
-    for (size_t b = 0; b < nblocks && hit; b++) hit = c->pf.src[b] == blocks[b] && c->pf.lens[b] == lens[b];
-    if (hit) {
-      c->pf.on = false;
-      c->stage_cur = c->pf.slot;
-      for (size_t b = 0; b < nblocks; b++) dev[b] = c->pf.dev[b];
-      c->n_prefetch_hits = nblocks;
-      HIP_TRY(hipStreamWaitEvent(c->stream, c->pf.ev, 0));
-      return FGV_OK;
-    }
+  for (size_t q = 0; q < c->pf.size(); q++) {
+    if (!c->pf[q].matches(nblocks, blocks, lens)) continue;
+    const fgv_ctx::Prefetch e = c->pf[q];
+    c->pf.erase(c->pf.begin() + (long)q);
+    c->stage_cur = e.slot;
+    for (size_t b = 0; b < nblocks; b++) dev[b] = e.dev[b];
+    c->n_prefetch_hits = nblocks;
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->stage_ev[e.slot], 0));
+    return FGV_OK;
   }
-  // copy now, into the arena no prefetch is writing (64 B padding after each block).  A front
-  // half enqueued ahead reads the prefetched arena, which this call's own prefetch may reuse.
-  if (c->pf.on) fgv_block_drain(c);
-  const int slot = c->pf.on ? 1 - c->pf.slot : c->stage_cur;
-  c->pf.on = false;
+  // copy now, into a slot no staged batch holds (64 B padding after each block)
+  const int slot = free_slot(c, -1);
   DevBuf &A = c->stage[slot];
   if (!A.ensure(stage_bytes(nblocks, lens))) return FGV_ENOMEM;
-  HIP_TRY(hipStreamWaitEvent(c->stream, c->pf.ev, 0));  // (an abandoned prefetch may still write the other arena)
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->stage_ev[slot], 0));  // (a dropped staging copy may still write it)
   size_t copied = 0;
   int rc = copy_runs(nblocks, blocks, lens, A.as<uint8_t>(), c->stream, dev.data(), &copied);
   if (rc) return rc;
+  HIP_TRY(hipEventRecord(c->stage_ev[slot], c->stream));
   c->stage_cur = slot;
   c->h2d_bytes = copied;
   return FGV_OK;
 }
 
-// Queue the next batch's H2D copy into the idle arena on the copy stream (it overlaps this
-// batch's kernels).  Called after stage_blocks of the current batch; every earlier user of the
-// idle arena has completed (each validation call ends synchronised).
-static int prefetch_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens) {
+// Stage a later batch's H2D copy into a free arena on the copy stream (it overlaps the kernels of
+// the batches before it).  Called after stage_blocks of the current batch, or from fgv_prefetch
+// between calls.  A batch already staged is not copied again.  -> the staged entry
+static int prefetch_blocks(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                           const fgv_ctx::Prefetch **out, bool in_call = true) {
+  *out = nullptr;
   if (!nblocks) return FGV_OK;
-  const int slot = 1 - c->stage_cur;
+  for (const auto &e : c->pf)
+    if (e.matches(nblocks, blocks, lens)) {
+      *out = &e;
+      return FGV_OK;
+    }
+  // (inside a call its own batch's slot is busy; between calls the last call's slot is free)
+  const int slot = free_slot(c, in_call ? c->stage_cur : -1);
   DevBuf &A = c->stage[slot];
   if (!A.ensure(stage_bytes(nblocks, lens))) return FGV_ENOMEM;
-  c->pf.src.assign(blocks, blocks + nblocks);
-  c->pf.lens.assign(lens, lens + nblocks);
-  c->pf.dev.resize(nblocks);
+  fgv_ctx::Prefetch e;
+  e.slot = slot;
+  e.src.assign(blocks, blocks + nblocks);
+  e.lens.assign(lens, lens + nblocks);
+  e.dev.resize(nblocks);
   size_t copied = 0;
-  int rc = copy_runs(nblocks, blocks, lens, A.as<uint8_t>(), c->copy_stream, c->pf.dev.data(), &copied);
+  int rc = copy_runs(nblocks, blocks, lens, A.as<uint8_t>(), c->copy_stream, e.dev.data(), &copied);
   if (rc) return rc;
-  HIP_TRY(hipEventRecord(c->pf.ev, c->copy_stream));
-  c->pf.slot = slot;
-  c->pf.on = true;
+  HIP_TRY(hipEventRecord(c->stage_ev[slot], c->copy_stream));
+  c->pf.push_back(std::move(e));
+  *out = &c->pf.back();
   return FGV_OK;
+}
+
+int fgv_prefetch(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens) {
+  if (!c || (nblocks && (!blocks || !lens))) return FGV_EINVAL;
+  if (nblocks == 0) return FGV_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  const fgv_ctx::Prefetch *e = nullptr;
+  return prefetch_blocks(c, nblocks, blocks, lens, &e, false);
 }
 
 static size_t shard_count(size_t nblocks, const size_t *ntx, const uint32_t *tx_lo, const uint32_t *tx_hi) {
@@ -1254,10 +1288,11 @@ static int shard_dev_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *bl
   int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
   if (rc) return rc;
   if (c->next.n && c->next.prefetch) {
-    rc = prefetch_blocks(c, c->next.n, c->next.blocks, c->next.lens);
+    const fgv_ctx::Prefetch *e = nullptr;
+    rc = prefetch_blocks(c, c->next.n, c->next.blocks, c->next.lens, &e);
     if (rc) return rc;
-    c->next.d_blocks = c->pf.dev.data();  // its front half can be enqueued ahead of its call
-    c->next.wait = c->pf.ev;
+    c->next.d_blocks = e->dev.data();  // its front half can be enqueued ahead of its call
+    c->next.wait = c->stage_ev[e->slot];
   }
   if (fgv_block_parse_mode(c->blk) == 0) {
     rc = fgv_block_validate_dev(c, c->blk, nblocks, blocks, lens, dev.data(), tx_lo, tx_hi,
@@ -1406,10 +1441,11 @@ static int validate_blocks_locked(fgv_ctx *c, size_t nblocks, const uint8_t *con
   int rc = stage_blocks(c, nblocks, blocks, lens, d_blocks, dev);
   if (rc) return rc;
   if (c->next.n && c->next.prefetch) {
-    rc = prefetch_blocks(c, c->next.n, c->next.blocks, c->next.lens);
+    const fgv_ctx::Prefetch *e = nullptr;
+    rc = prefetch_blocks(c, c->next.n, c->next.blocks, c->next.lens, &e);
     if (rc) return rc;
-    c->next.d_blocks = c->pf.dev.data();
-    c->next.wait = c->pf.ev;
+    c->next.d_blocks = e->dev.data();
+    c->next.wait = c->stage_ev[e->slot];
   }
   if (fgv_block_parse_mode(c->blk) == 0) {
     // records: at most one per 2 bytes of block data (an envelope's framing), and flags_cap

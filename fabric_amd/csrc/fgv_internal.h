@@ -178,18 +178,26 @@ struct fgv_ctx {
   bool timing = false;
   bool spin = false;  // FGV_SPIN=1: poll the committer's final wait (fgv_stream_wait; equal within noise on MI355X)
   bool timing_ran = true;  // the last verify stages recorded their events (read_stage_times)
-  // host-resident batches: two device staging arenas; fgv_validate_shard_dev_next copies the
-  // NEXT batch into the idle one on the copy stream while this batch's kernels run
-  DevBuf stage[2];
-  int stage_cur = 0;
+  // host-resident batches: a ring of device staging arenas.  The running call's batch holds one;
+  // batches staged ahead (the pipelined calls' NEXT batch, fgv_prefetch of later ones) hold the
+  // others, filled on the copy stream while earlier batches validate
+  static constexpr int kStage = 3;
+  DevBuf stage[kStage];
+  hipEvent_t stage_ev[kStage] = {};  // the slot's last staging copy
+  int stage_cur = 0;                 // the slot of the batch the current / last call validated
   hipStream_t copy_stream = nullptr;
   struct Prefetch {
-    bool on = false;
     int slot = 0;
     std::vector<const uint8_t *> src, dev;
     std::vector<size_t> lens;
-    hipEvent_t ev = nullptr;
-  } pf;
+    bool matches(size_t n, const uint8_t *const *b, const size_t *l) const {
+      if (n != src.size()) return false;
+      for (size_t i = 0; i < n; i++)
+        if (src[i] != b[i] || lens[i] != l[i]) return false;
+      return true;
+    }
+  };
+  std::vector<Prefetch> pf;  // staged batches, oldest first (at most kStage - 1)
   uint64_t n_prefetch_hits = 0, h2d_bytes = 0;  // last call: blocks found prefetched / bytes copied in the call
   DevBuf bd_env, bd_bases, bd_tx, bd_ident, bd_jobs, bd_misc;
   HostBuf hb_env, hb_bases, hb_misc;

@@ -352,6 +352,16 @@ int fgv_group_p256_verify_msgs(fgv_group *g, const uint8_t *keys, const uint8_t 
 int fgv_presplit(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                  const uint32_t *tx_lo, const uint32_t *tx_hi);
 int fgv_last_presplit(fgv_ctx *ctx);
+/* Queue the H2D copy of a LATER host-resident batch now, on the engine's copy stream (a peer
+ * calls it as soon as a batch of delivered blocks sits in its pinned receive buffer).  The
+ * validation call whose batch has the same block addresses and lengths -- or a pipelined call
+ * naming it as its next batch -- waits for that copy instead of copying.  The engine keeps three
+ * staging arenas: the running call's batch and two staged ones (a further fgv_prefetch drops the
+ * oldest staged batch, which its call then copies itself).  With the pipelined calls, staging
+ * batch k+2 during batch k keeps the PCIe link busy back to back.  The buffers must stay valid
+ * and unchanged until that call (or fgv_destroy); they should be pinned (fgv_host_alloc).  Results
+ * never depend on it. */
+int fgv_prefetch(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens);
 /* fgv_validate_shard_dev of the current batch that also pre-splits the NEXT batch (next_*,
  * same meaning as fgv_presplit's arguments) as soon as the current batch's GPU work is
  * queued, so the walk overlaps the current validation instead of following it.  When the

@@ -392,6 +392,32 @@ def test_single_gpu_pipelined_rotation(where):
     eng.validate_blocks_pipelined(batches[1], batches[0])
     assert list(eng.validate_blocks_pipelined(batches[2])) == exps[2] and not eng.last_presplit()
     assert [f for fl in eng.validate_blocks(sets[0]) for f in fl] == exps[0]
+    if where == "pinned":  # fgv_prefetch: batch k stages batch k+2 beside its pipelined next batch
+        order = [0, 1, 2, 1, 0, 2, 0, 1]
+        eng.prefetch(batches[order[0]])
+        eng.prefetch(batches[order[1]])
+        for i, k in enumerate(order):
+            if i + 2 < len(order):
+                eng.prefetch(batches[order[i + 2]])
+            nxt = batches[order[i + 1]] if i + 1 < len(order) else None
+            assert list(eng.validate_blocks_pipelined(batches[k], nxt)) == exps[k], (i, k)
+            assert eng.last_h2d()[1] == batches[k].nb, (i, eng.last_h2d())
+        # three staged batches fill the ring; a call of a fourth batch (batch 0's blocks in another
+        # pinned buffer) drops the oldest staged one, whose call then copies its blocks itself
+        pb = eng.host_alloc(sum(len(b) for b in sets[0]))
+        views, o = [], 0
+        for b in sets[0]:
+            pb.a[o:o + len(b)] = np.frombuffer(b, np.uint8)
+            views.append(pb.a[o:o + len(b)])
+            o += len(b)
+        bufs.append(pb)
+        extra = eng.block_batch(views)
+        for k in (1, 2, 0):
+            eng.prefetch(batches[k])
+        assert list(eng.validate_blocks_pipelined(extra)) == exps[0] and eng.last_h2d()[1] == 0
+        assert list(eng.validate_blocks_pipelined(batches[1])) == exps[1] and eng.last_h2d()[1] == 0
+        assert list(eng.validate_blocks_pipelined(batches[2])) == exps[2] and eng.last_h2d()[1] == batches[2].nb
+        assert list(eng.validate_blocks_pipelined(batches[0])) == exps[0] and eng.last_h2d()[1] == batches[0].nb
     for pb in bufs:
         pb.close()
     eng.close()
