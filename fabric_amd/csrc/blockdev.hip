@@ -891,28 +891,45 @@ __global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__r
 // ============================================================ k_bd_count
 // creator decision (msgvalidation.go:26-64: deserialize, Validate, then Verify) + count_jobs
 DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx &J);
-// Job slots are claimed with one atomicAdd per wave and kind (wave-inclusive scan by
-// shuffles): slots of a kind stay grouped, their order across waves is the atomics' order.
-__global__ __launch_bounds__(256) void k_bd_count(uint32_t ntx, DevTx *__restrict__ txs, DevChannel ch,
-                                                  const int32_t *__restrict__ ident, DevJobIdx *__restrict__ jobs,
-                                                  uint32_t *__restrict__ totals) {
+// Job slots are claimed with ONE atomicAdd per workgroup and kind: a wave-inclusive scan by
+// shuffles, the waves' totals scanned in LDS, lane q of the first wave adds kind q's workgroup
+// total (all kinds' atomics in flight at once).  Slots of a kind stay grouped; their order
+// across workgroups is the atomics' order.  (One atomic per wave and kind, issued one kind after
+// the other, made this kernel ~55 us of contended atomics on one cache line.)
+#define BC_THREADS 1024u
+__global__ __launch_bounds__(BC_THREADS) void k_bd_count(uint32_t ntx, DevTx *__restrict__ txs, DevChannel ch,
+                                                         const int32_t *__restrict__ ident,
+                                                         DevJobIdx *__restrict__ jobs, uint32_t *__restrict__ totals) {
   __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
+  __shared__ uint32_t wtot[BJ_KINDS][BC_THREADS / 64], wbase[BJ_KINDS][BC_THREADS / 64];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   DevJobIdx J;
   for (int q = 0; q < BJ_KINDS; q++) J.cnt[q] = J.base[q] = 0;
   if (t < ntx) count_jobs(txs[t], ch, ident + (size_t)t * BD_OCC, J);
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t incl[BJ_KINDS];
   for (int q = 0; q < BJ_KINDS; q++) {
     uint32_t v = J.cnt[q];
     for (uint32_t d = 1; d < 64; d <<= 1) {
       const uint32_t o = (uint32_t)__shfl_up((int)v, d);
       if (lane >= d) v += o;
     }
-    uint32_t b = 0;
-    if (lane == 63u && v) b = atomicAdd(&totals[q], v);
-    b = (uint32_t)__shfl((int)b, 63);
-    J.base[q] = b + v - J.cnt[q];
+    incl[q] = v;
+    if (lane == 63u) wtot[q][w] = v;
   }
+  __syncthreads();
+  if (w == 0 && lane < BJ_KINDS) {  // lane q: kind q over the workgroup's waves
+    const uint32_t q = lane;
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < BC_THREADS / 64; k++) {
+      const uint32_t x = wtot[q][k];
+      wtot[q][k] = run;
+      run += x;
+    }
+    wbase[q][0] = run ? atomicAdd(&totals[q], run) : 0u;
+  }
+  __syncthreads();
+  for (int q = 0; q < BJ_KINDS; q++) J.base[q] = wbase[q][0] + wtot[q][w] + incl[q] - J.cnt[q];
   if (t < ntx) jobs[t] = J;
 }
 DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx &J) {

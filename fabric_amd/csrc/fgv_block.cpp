@@ -2066,7 +2066,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 * BD_ID_PAR + 255) / 256)), dim3(256), 0, sf, N, dtx,
                      dbs, ch,
                      B.ident.as<int32_t>());
-  hipLaunchKernelGGL(k_bd_count, dim3((N + 255) / 256), dim3(256), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
+  hipLaunchKernelGGL(k_bd_count, dim3((N + 1023) / 1024), dim3(1024), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
                      B.jobs.as<DevJobIdx>(), misc);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(B.ev[6], sf));
