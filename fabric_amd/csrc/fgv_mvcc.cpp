@@ -1298,7 +1298,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   const size_t *pntx = nullptr, *pfirst = nullptr;
   const bool pre = fgv_block_take_presplit_batch(c->blk, nb, blocks + first, lens + first, &pet, &pntx, &pfirst);
   const bool pre0 = !pre && fgv_block_take_presplit(c->blk, blocks[first], lens[first], M->pre_envs);
-  fgv_parallel_run(c->blk, nb, [&](size_t k) {
+  auto fill = [&](size_t k) {
     const size_t b = first + k, T = ntx[b];
     const size_t et_bytes = (T * 8 + 63) & ~(size_t)63, fl_bytes = (T + 63) & ~(size_t)63;
     uint8_t *h = M->bhead.as<uint8_t>() + hoff[k];
@@ -1324,24 +1324,35 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
     memcpy(h + et_bytes, flags[b], T);
     memset(h + et_bytes + fl_bytes, 0, kCounterBytes);
     walked[k] = 1;
-  });
-  size_t nq = 0;  // blocks enqueued: up to the first one that is not a block of ntx transactions
-  while (nq < nb && walked[nq]) nq++;
-  if (nq == 0) return FGV_OK;  // (the single-block path reports that block's error)
+  };
+  // block 0's head first, on this thread: its copy and extraction start while the host pool
+  // fills the other blocks' heads
+  fill(0);
+  if (!walked[0]) return FGV_OK;  // (the single-block path reports that block's error)
   // (stream2 starts after whatever the main stream holds: the table reset above, earlier calls)
   HIP_TRY(hipEventRecord(c->ev[0], s));
   HIP_TRY(hipStreamWaitEvent(sx, c->ev[0], 0));
   uint8_t *dheads = M->dheads.as<uint8_t>();
-  HIP_TRY(hipMemcpyAsync(dheads, M->bhead.p, hoff[nq], hipMemcpyHostToDevice, sx));
+  HIP_TRY(hipMemcpyAsync(dheads, M->bhead.p, hoff[1], hipMemcpyHostToDevice, sx));
+  size_t nq = 1;  // blocks enqueued: up to the first one that is not a block of ntx transactions
+  bool rest_sent = nb == 1;
   const uint32_t touch = mvx_touch();
   BlkSlot *d_b = M->btbl.as<BlkSlot>();
   const MvCounters *prev_c = nullptr;
-  for (size_t k = 0; k < nq; k++) {
+  for (size_t k = 0; k < nb; k++) {
     const size_t b = first + k;
     const uint8_t *block = blocks[b];
     const size_t len = lens[b], T = ntx[b];
     MvSet &S = M->set[k % kSets];
     const size_t et_bytes = (T * 8 + 63) & ~(size_t)63, fl_bytes = (T + 63) & ~(size_t)63;
+    if (k == 1 && !rest_sent) {  // the other heads, once block 0 is on its way
+      fgv_parallel_run(c->blk, nb - 1, [&](size_t j) { fill(j + 1); });
+      while (nq < nb && walked[nq]) nq++;
+      if (nq > 1) HIP_TRY(hipMemcpyAsync(dheads + hoff[1], M->bhead.as<uint8_t>() + hoff[1], hoff[nq] - hoff[1],
+                                         hipMemcpyHostToDevice, sx));
+      rest_sent = true;
+    }
+    if (k >= nq) break;
     // stream2: the set is free once block k-kSets's chain is done
     if (k >= (size_t)kSets) HIP_TRY(hipStreamWaitEvent(sx, S.ev_free, 0));
     const uint8_t *dblk = d_blocks ? d_blocks[b] : nullptr;

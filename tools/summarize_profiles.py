@@ -17,10 +17,18 @@ PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 78.6 T full-rate 32-bit lane-ops/s
 HBM_PEAK = 8.0e12
 
 
+def norm(name):
+    """kernel name without arguments, a leading 'void ' or template arguments"""
+    k = name.split("(")[0]
+    if k.startswith("void "):
+        k = k[5:]
+    return k.split("<")[0]
+
+
 def kernel_stats(path):
     out = {}
     for r in csv.DictReader(open(path)):
-        out[r["Name"].split("(")[0]] = dict(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3,
+        out[norm(r["Name"])] = dict(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3,
                                             pct=float(r["Percentage"]))
     return out
 
@@ -32,7 +40,7 @@ def pmc(path):
     grid = {}
     seen = set()
     for r in csv.DictReader(open(path)):
-        k = r["Kernel_Name"].split("(")[0]
+        k = norm(r["Kernel_Name"])
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         n[(k, r["Counter_Name"])] += 1
         if (k, r["Dispatch_Id"]) not in seen:
@@ -137,7 +145,7 @@ def main(src, rnd):
                 traffic[wl] = dict(kernel=kern, fetch_bytes=round(fb), write_bytes=round(wb), hbm_bytes=round(fb + wb),
                                    avg_us=round(F[kern]["avg_s"] * 1e6, 1))
         else:  # MVCC: every per-block kernel (the one-time state load k_mv_tags excluded), per block
-            nblk = F.get("k_mvx_extract", {}).get("dispatches", 0)
+            nblk = F.get("k_mvx_extract", F.get("k_mvx_extract_t", {})).get("dispatches", 0)
             per_block = [k for k in F if k.startswith("k_mv") and k != "k_mv_tags"]
             if nblk:
                 fb = sum(F[k]["FETCH_SIZE"] * 2 * 1024 * F[k]["dispatches"] for k in per_block) / nblk
