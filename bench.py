@@ -424,7 +424,11 @@ def run_block(args, world, rank, local, dev_fn):
     def parity(k, flags):
         exp = np.array([e if e is not None else 255 for bl in labels[k] for e in blocks.expected_codes(bl)], np.int64)
         known = np.array([e is not None for bl in labels[k] for e in blocks.expected_codes(bl)])
-        return int(((flags.astype(np.int64) != exp) & known).sum())
+        bad = np.nonzero((flags.astype(np.int64) != exp) & known)[0]
+        if len(bad):  # (diagnostic: which transactions, which codes)
+            log(f"[bench] rank {rank}: batch {k}: {len(bad)} flags differ: "
+                + ", ".join(f"tx {int(i)} (block {int(i) // T}) got {int(flags[i])} want {int(exp[i])}" for i in bad[:8]))
+        return int(len(bad))
 
     def timed(steps_list, K, per_step=None, step_fn=None):
         fn = step_fn or step
