@@ -657,14 +657,36 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *c, const uint8_t *d_msg_buf, const uint64_
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
   const uint32_t N = (uint32_t)n;
-  if (!c->r.ensure(n * 32) || !c->s.ensure(n * 32)) return FGV_ENOMEM;
-  int rc = launch_sha(c, d_msg_buf, d_msg_off, d_msg_len, n);
-  if (rc) return rc;
+  if (!c->r.ensure(n * 32) || !c->s.ensure(n * 32) || !c->dig.ensure(n * 32)) return FGV_ENOMEM;
+  // k_sha256 on stream2 beside k_der + k_inv on the main stream (the inverse needs s, not the
+  // digest); k_prep waits for the digests.  FGV_SIG_FORK=0: all on one stream (A/B).  C4 on
+  // MI355X, alternating: 0.679 / 0.684 ms per 131k against 0.701 / 0.707 (profiles/round3_ab/sig_f*)
+  static const bool fork = [] {
+    const char *e = getenv("FGV_SIG_FORK");
+    return !e || atoi(e) != 0;
+  }();
+  int rc;
+  if (fork) {
+    HIP_TRY(hipEventRecord(c->ev[7], c->stream));  // (stream2 after the main stream's earlier work)
+    HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev[7], 0));
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream2));
+    hipLaunchKernelGGL(k_sha256, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, c->stream2, d_msg_buf, d_msg_off,
+                       d_msg_len, N, c->dig.as<uint8_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream2));
+  } else {
+    rc = launch_sha(c, d_msg_buf, d_msg_off, d_msg_len, n);
+    if (rc) return rc;
+  }
   hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, d_sig_buf, d_sig_off,
                      d_sig_len, N, (const uint32_t *)nullptr, d_status, c->r.as<uint32_t>(), c->s.as<uint32_t>());
   HIP_TRY(hipGetLastError());
-  rc = launch_verify_stages(c, N, d_status, d_key_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>(),
-                            c->dig.as<uint8_t>());
+  c->timing_ran = true;
+  rc = launch_inv(c, c->stream, N, nullptr, d_status, d_key_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>());
+  if (rc) return rc;
+  if (fork) c->digests_ready = c->ev[1];
+  rc = launch_prep_point(c, N, nullptr, N, d_status, d_key_slot, c->r.as<uint32_t>(), c->dig.as<uint8_t>(), nullptr);
+  c->digests_ready = nullptr;
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   float ms = 0;
