@@ -94,6 +94,7 @@ struct MvRec {  // one read or write: spans into the block (or a host-supplied k
   uint32_t key_off, ns_off, coll_off;
   uint16_t key_len, ns_len, coll_len, flags;
 };
+static_assert(sizeof(MvRec) == 48, "MvRec: 3 x 16 B (k_mvx_extract copies it as uint4)");
 struct MvTxInfo {  // per transaction
   uint32_t rbeg, rcnt, wbeg, wcnt;  // record ranges
   uint32_t rws_off, rws_len;        // TxReadWriteSet span in the block

@@ -434,6 +434,19 @@ DEV uint32_t bmask_of(uint32_t nw) {
 // -> unsupported.
 // touch (global walks only): FGV_MVX_TOUCH=0 turns the up-front line requests off (A/B)
 // scr (nullable): per-tx scratch of MVX_SCR reads + MVX_SCR writes
+// n 16-byte words, 8 loads issued before their stores (one round trip per pass)
+__device__ __forceinline__ void copy16(uint4 *__restrict__ d, const uint4 *__restrict__ s, uint32_t n) {
+  for (uint32_t q = 0; q < n; q += 8) {
+    uint4 v[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++)
+      if (q + u < n) v[u] = s[q + u];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++)
+      if (q + u < n) d[q + u] = v[u];
+  }
+}
+
 template <uint32_t TPW>
 __device__ __forceinline__ void mvx_extract(uint32_t ntx, const uint8_t *__restrict__ base,
                                             const uint32_t *__restrict__ envtab, const uint8_t *__restrict__ in_flags,
@@ -469,13 +482,28 @@ __device__ __forceinline__ void mvx_extract(uint32_t ntx, const uint8_t *__restr
   __syncthreads();
   const uint32_t total = pre[TPW];
   const uint32_t *src = reinterpret_cast<const uint32_t *>(base);
-  for (uint32_t i = lane; i < total; i += 64) {
-    uint32_t j = 0;  // the envelope of dword i: pre[j] <= i < pre[j + 1]
+  // 8 dwords per lane per pass: all 8 loads are issued before the first LDS store, so a pass
+  // costs one memory round trip (a plain loop waited for each load before its store)
+  constexpr uint32_t U = 8;
+  for (uint32_t i0 = lane; i0 < total; i0 += 64 * U) {
+    uint32_t v[U], dst[U];
 #pragma unroll
-    for (uint32_t b = TPW / 2; b > 0; b >>= 1)
-      if (pre[j + b] <= i) j += b;
-    const uint32_t k = i - pre[j];
-    lds[j * (CAP / 4) + k] = src[src0[j] + k];
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t i = i0 + 64 * u;
+      dst[u] = 0xFFFFFFFFu;
+      if (i < total) {
+        uint32_t j = 0;  // the envelope of dword i: pre[j] <= i < pre[j + 1]
+#pragma unroll
+        for (uint32_t b = TPW / 2; b > 0; b >>= 1)
+          if (pre[j + b] <= i) j += b;
+        const uint32_t k = i - pre[j];
+        v[u] = src[src0[j] + k];
+        dst[u] = j * (CAP / 4) + k;
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (dst[u] != 0xFFFFFFFFu) lds[dst[u]] = v[u];
   }
   __syncthreads();
   const uint32_t t = lane < TPW ? t0 + lane : ntx;
@@ -521,10 +549,10 @@ __device__ __forceinline__ void mvx_extract(uint32_t ntx, const uint8_t *__restr
   if (lane == 0 && wb) atomicAdd(&c->wbytes, (unsigned long long)wb);
   if (t >= ntx) return;
   if (I.code == 0) {
-    if (copied) {  // (independent 16-byte copies instead of a second walk)
+    if (copied) {  // (16-byte copies, 8 loads in flight per pass, instead of a second walk)
       const MvRec *sr = scr + (size_t)t * (2 * MVX_SCR);
-      for (uint32_t k = 0; k < I.rcnt; k++) reads[I.rbeg + k] = sr[k];
-      for (uint32_t k = 0; k < I.wcnt; k++) writes[I.wbeg + k] = sr[MVX_SCR + k];
+      copy16(reinterpret_cast<uint4 *>(reads + I.rbeg), reinterpret_cast<const uint4 *>(sr), I.rcnt * 3);
+      copy16(reinterpret_cast<uint4 *>(writes + I.wbeg), reinterpret_cast<const uint4 *>(sr + MVX_SCR), I.wcnt * 3);
     } else {
       Sink sk{vb, reads + I.rbeg, writes + I.wbeg, t, 0, 0, 0, false};
       bool host = false;
