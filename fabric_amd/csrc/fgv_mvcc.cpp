@@ -65,6 +65,7 @@ struct fgv_mvcc_state {
   DevBuf tbl, arena, top;              // top: [0] arena bytes used, [1] occupied slots
   DevBuf btbl;
   DevBuf dheads;                       // batch path: every block's head (one copy per call)
+  hipEvent_t ev_heads = nullptr;       // batch path: the heads' copy is done (second extraction stream)
   MvSet set[kSets];
   DevBuf lrecs, lbytes;                // load / apply staging
   DevBuf qver, qpres, qrange, qout;    // phantom path: lookups and range scans
@@ -82,6 +83,7 @@ void fgv_mvcc_free(fgv_mvcc_state *M) {
   DevBuf *d[] = {&M->tbl, &M->arena, &M->top, &M->btbl, &M->dheads, &M->lrecs, &M->lbytes, &M->qver, &M->qpres, &M->qrange, &M->qout};
   for (auto *b : d) b->release();
   for (auto &S : M->set) S.release();
+  if (M->ev_heads) hipEventDestroy(M->ev_heads);
   HostBuf *h[] = {&M->hhead, &M->htail, &M->bhead, &M->btail};
   for (auto *b : h) b->release();
   delete M;
@@ -1332,6 +1334,17 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   // (stream2 starts after whatever the main stream holds: the table reset above, earlier calls)
   HIP_TRY(hipEventRecord(c->ev[0], s));
   HIP_TRY(hipStreamWaitEvent(sx, c->ev[0], 0));
+  // FGV_MVX_STREAMS=2: extractions alternate over stream2 and stream3, two side by side (A/B).
+  // Measured on MI355X (chained C3, alternating): GPU 0.127 / 0.130 ms per block against 0.139 /
+  // 0.135 on one stream, but wall 46 / 63 M tx/s against 63 / 69 M (profiles/round3_ab/mvx_xs*):
+  // one stream stays the default
+  static const int nxs_env = [] {
+    const char *e = getenv("FGV_MVX_STREAMS");
+    return e ? atoi(e) : 1;
+  }();
+  const size_t nxs = nxs_env == 2 ? 2 : 1;
+  const hipStream_t xs[2] = {sx, c->stream3};
+  if (!M->ev_heads) HIP_TRY(hipEventCreateWithFlags(&M->ev_heads, hipEventDisableTiming));
   uint8_t *dheads = M->dheads.as<uint8_t>();
   HIP_TRY(hipMemcpyAsync(dheads, M->bhead.p, hoff[1], hipMemcpyHostToDevice, sx));
   size_t nq = 1;  // blocks enqueued: up to the first one that is not a block of ntx transactions
@@ -1350,14 +1363,19 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
       while (nq < nb && walked[nq]) nq++;
       if (nq > 1) HIP_TRY(hipMemcpyAsync(dheads + hoff[1], M->bhead.as<uint8_t>() + hoff[1], hoff[nq] - hoff[1],
                                          hipMemcpyHostToDevice, sx));
+      if (nxs > 1) {  // the second extraction stream starts after the heads' copy
+        HIP_TRY(hipEventRecord(M->ev_heads, sx));
+        HIP_TRY(hipStreamWaitEvent(xs[1], M->ev_heads, 0));
+      }
       rest_sent = true;
     }
     if (k >= nq) break;
-    // stream2: the set is free once block k-kSets's chain is done
-    if (k >= (size_t)kSets) HIP_TRY(hipStreamWaitEvent(sx, S.ev_free, 0));
+    // block k's extraction stream: the set is free once block k-kSets's chain is done
+    hipStream_t sxk = xs[k % nxs];
+    if (k >= (size_t)kSets) HIP_TRY(hipStreamWaitEvent(sxk, S.ev_free, 0));
     const uint8_t *dblk = d_blocks ? d_blocks[b] : nullptr;
     if (!dblk) {
-      HIP_TRY(hipMemcpyAsync(S.blk.p, block, len, hipMemcpyHostToDevice, sx));
+      HIP_TRY(hipMemcpyAsync(S.blk.p, block, len, hipMemcpyHostToDevice, sxk));
       dblk = S.blk.as<uint8_t>();
     }
     uint8_t *dh = dheads + hoff[k];
@@ -1367,9 +1385,9 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
     MvTxInfo *d_info = S.info.as<MvTxInfo>();
     MvRec *d_r = S.reads.as<MvRec>(), *d_w = S.writes.as<MvRec>();
     const uint32_t N = (uint32_t)T;
-    mvx_extract_launch(mvx_tpw(), sx, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c, touch, S.xscr.as<MvRec>(),
+    mvx_extract_launch(mvx_tpw(), sxk, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c, touch, S.xscr.as<MvRec>(),
                        S.bad.as<uint8_t>());
-    HIP_TRY(hipEventRecord(S.ev_x, sx));
+    HIP_TRY(hipEventRecord(S.ev_x, sxk));
     // main stream: block k's chain
     HIP_TRY(hipStreamWaitEvent(s, S.ev_x, 0));
     const uint32_t epoch = ++M->epoch;
