@@ -1029,6 +1029,17 @@ static int fin_prepare(fgv_ctx *c, size_t nblocks, const size_t *ntx, uint32_t W
   F.meta = meta;
   return FGV_OK;
 }
+// The finalize front (k_fin_rows, k_fin_index_dev) at wave priority 3, like the verify chain it
+// runs beside (the fold waits for it).  C2 lean harness on MI355X, alternating x3: 0.689 / 0.677 /
+// 0.655 ms per step against 0.679 / 0.696 / 0.681 at priority 0 (profiles/round3_ab/fp*): a
+// small gain at the noise level; FGV_FIN_PRIO=0 turns it off (A/B)
+static uint32_t fin_prio() {
+  static const uint32_t v = [] {
+    const char *e = getenv("FGV_FIN_PRIO");
+    return e ? (uint32_t)atoi(e) : 1u;
+  }();
+  return v;
+}
 // index from the gathered records (recs != null) or from a single-device batch's parse and
 // digests (dtx != null: the owners' keys go to c->fz_keys)
 static int fin_front(fgv_ctx *c, hipStream_t st, size_t nblocks, uint32_t W, size_t rows, const FinPlan &F,
@@ -1043,10 +1054,10 @@ static int fin_front(fgv_ctx *c, hipStream_t st, size_t nblocks, uint32_t W, siz
                      d_bstart, (uint32_t)nblocks, W, (uint32_t)rows, d_roff, d_roff + F.wn, d_roff + 2 * F.wn,
                      c->fz_rowmap.as<uint32_t>(), c->fz_blkof.as<uint32_t>(), (uint32_t)F.cap,
                      c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), c->fz_minvalid.as<uint32_t>(), dtx,
-                     bases, digests, dtx ? c->fz_keys.as<uint8_t>() : nullptr);
+                     bases, digests, dtx ? c->fz_keys.as<uint8_t>() : nullptr, fin_prio());
   if (dtx)
     hipLaunchKernelGGL(k_fin_index_dev, grid, blk, 0, st, n32, dtx, bases, digests, c->fz_keys.as<uint8_t>(),
-                       c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask, c->fin_seed);
+                       c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask, c->fin_seed, fin_prio());
   else
     hipLaunchKernelGGL(k_fin_index, grid, blk, 0, st, n32, d_recs, c->fz_rowmap.as<uint32_t>(),
                        c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(), mask,

@@ -161,12 +161,13 @@ struct DevTx;
 __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, uint32_t W, uint32_t rows,
                            const uint32_t *roff, const uint32_t *rlo, const uint32_t *rcnt, uint32_t *rowmap,
                            uint32_t *blkof, uint32_t cap, uint32_t *owner, int32_t *minblk, uint32_t *minvalid,
-                           const DevTx *txs, const uint64_t *bases, const uint8_t *digests, uint8_t *keys);
+                           const DevTx *txs, const uint64_t *bases, const uint8_t *digests, uint8_t *keys,
+                           uint32_t prio);
 __global__ void k_fin_index(uint32_t P, const uint8_t *recs, const uint32_t *rowmap, const uint32_t *blkof,
                             uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed);
 __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *rowmap, const uint32_t *blkof,
                             const uint32_t *owner, const int32_t *minblk, uint32_t *minvalid, uint32_t mask,
                             uint64_t seed, uint8_t *flags, uint32_t *pslot, const uint8_t *keys);
 __global__ void k_fin_index_dev(uint32_t P, const DevTx *txs, const uint64_t *bases, const uint8_t *digests,
-                                uint8_t *keys, uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed);
+                                uint8_t *keys, uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed, uint32_t prio);
 __global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags, uint32_t *unsup);

@@ -102,7 +102,9 @@ __device__ inline bool dev_index_key(const DevTx &R, const uint64_t *bases, cons
 __global__ void k_fin_rows(uint32_t P, const uint64_t *blk_start, uint32_t nb, uint32_t W, uint32_t rows,
                            const uint32_t *roff, const uint32_t *rlo, const uint32_t *rcnt, uint32_t *rowmap,
                            uint32_t *blkof, uint32_t cap, uint32_t *owner, int32_t *minblk, uint32_t *minvalid,
-                           const DevTx *txs, const uint64_t *bases, const uint8_t *digests, uint8_t *keys) {
+                           const DevTx *txs, const uint64_t *bases, const uint8_t *digests, uint8_t *keys,
+                           uint32_t prio) {
+  if (prio) __builtin_amdgcn_s_setprio(3);  // (beside k_point28: the fold waits for this index)
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < cap) {
     owner[p] = 0u;
@@ -166,7 +168,9 @@ __global__ void k_fin_index(uint32_t P, const uint8_t *recs, const uint32_t *row
 // position p == tx t), so it runs beside the verify chain instead of after the fold: the
 // owners' keys go to `keys` (32 B per position), which k_fin_codes then compares against
 __global__ void k_fin_index_dev(uint32_t P, const DevTx *txs, const uint64_t *bases, const uint8_t *digests,
-                                uint8_t *keys, uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed) {
+                                uint8_t *keys, uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed,
+                                uint32_t prio) {
+  if (prio) __builtin_amdgcn_s_setprio(3);
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   const DevTx &R = txs[p];
