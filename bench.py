@@ -844,8 +844,10 @@ def run_sig(args, world, rank, local, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # 40 timed steps: with 10 the pipeline's start-up was ~6 % of the C2 figure (MI355X, alternating:
+    # 0.748 / 0.724 ms per step at 10 steps, 0.701 / 0.676 at 40; profiles/round3_ab/steps*)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="block", choices=["block", "c5", "sig", "mvcc"])
     ap.add_argument("--c5-blocks-per-gpu", type=int, default=8)
     ap.add_argument("--c5-tx-per-block", type=int, default=20000)
