@@ -1652,6 +1652,12 @@ DEV int eval_policy(const DevChannel &ch, uint32_t pi, const int32_t *ids, uint3
 
 DEV bool hex32(S s, uint8_t out[32]) {
   if (s.n != 64) return false;
+  uint32_t w[8];
+  if (hex64_words(s.p, w)) {  // (all loads at once; fin_dev.h)
+    for (int k = 0; k < 32; k++) out[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    return true;
+  }
+  // not all lowercase hex: the byte loop, for the same partial output as the host parser
   for (int k = 0; k < 64; k++) {
     const uint8_t c = s.p[k];
     int v;

@@ -73,21 +73,8 @@ __device__ inline bool dev_index_key(const DevTx &R, const uint64_t *bases, cons
     return true;
   }
   if (R.index_txid.len != 64) return false;
-  const uint8_t *s = reinterpret_cast<const uint8_t *>(bases[R.blk]) + R.index_txid.off;
-  uint8_t o[32];
-  for (int i = 0; i < 64; i++) {
-    const uint8_t c = s[i];
-    int v;
-    if (c >= '0' && c <= '9') v = c - '0';
-    else if (c >= 'a' && c <= 'f') v = c - 'a' + 10;
-    else return false;  // only lowercase hex can equal a VALID txid
-    if (i & 1) o[i >> 1] |= (uint8_t)v;
-    else o[i >> 1] = (uint8_t)(v << 4);
-  }
-#pragma unroll
-  for (int i = 0; i < 8; i++) k[i] = (uint32_t)o[4 * i] | (uint32_t)o[4 * i + 1] << 8 | (uint32_t)o[4 * i + 2] << 16 |
-                                   (uint32_t)o[4 * i + 3] << 24;
-  return true;
+  // only lowercase hex can equal a VALID txid
+  return hex64_words(reinterpret_cast<const uint8_t *>(bases[R.blk]) + R.index_txid.off, k);
 }
 
 }  // namespace
