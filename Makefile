@@ -9,7 +9,7 @@ OBJDIR := build
 KOBJS := $(OBJDIR)/sha256.o $(OBJDIR)/p256_kernels.o $(OBJDIR)/der_kernel.o $(OBJDIR)/fgv_host.o $(OBJDIR)/fgv_block.o $(OBJDIR)/mvcc.o $(OBJDIR)/fgv_mvcc.o \
 	$(OBJDIR)/finalize.o $(OBJDIR)/fgv_integrity.o $(OBJDIR)/blockdev.o $(OBJDIR)/fgv_commit.o $(OBJDIR)/fgv_channel.o \
 	$(OBJDIR)/fgv_group.o $(OBJDIR)/fgv_msp.o $(OBJDIR)/fgv_x509.o
-HDRS := $(CSRC)/p256_field.h $(CSRC)/fgv_kernels.h $(CSRC)/fgv_der.h $(CSRC)/fgv_internal.h include/fgv.h $(CSRC)/blockdev.h $(CSRC)/pbwire_dev.h $(CSRC)/fin_dev.h
+HDRS := $(CSRC)/p256_field.h $(CSRC)/p256_fe28.h $(CSRC)/p256_modinv.h $(CSRC)/sha256_dev.h $(CSRC)/fgv_kernels.h $(CSRC)/fgv_der.h $(CSRC)/fgv_internal.h include/fgv.h $(CSRC)/blockdev.h $(CSRC)/pbwire_dev.h $(CSRC)/fin_dev.h
 
 all: fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so
 

@@ -306,7 +306,11 @@ def run_block(args, world, rank, local, dev_fn):
     from fabric_amd import _lib, shard, txvalidator
     from fabric_amd.synth import blocks
 
-    spec = BLOCK_SPECS[args.workload]
+    spec = dict(BLOCK_SPECS[args.workload])
+    if args.clients:  # identity churn: creators spread over this many client identities
+        spec["net"] = dict(spec["net"], clients=args.clients)
+        spec["desc"] = spec["desc"].replace("100 clients", f"{args.clients} clients (churn: client keys on the "
+                                            f"variable-base kernels)")
     t0 = time.time()
     pems = None
     if world > 1:
@@ -430,13 +434,15 @@ def run_block(args, world, rank, local, dev_fn):
                 + ", ".join(f"tx {int(i)} (block {int(i) // T}) got {int(flags[i])} want {int(exp[i])}" for i in bad[:8]))
         return int(len(bad))
 
-    def timed(steps_list, K, per_step=None, step_fn=None):
+    def timed(steps_list, K, per_step=None, step_fn=None, start=0):
+        # start: the rotation index the previous call announced as its next batch (its front
+        # half and pre-split are already queued), so timed call 0 continues the pipeline
         fn = step_fn or step
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for s in range(K):
+        for s in range(start, start + K):
             fn(steps_list[s % NB], s % NB)
             if per_step is not None:
                 per_step()
@@ -460,8 +466,10 @@ def run_block(args, world, rank, local, dev_fn):
 
     acc = dict(point=0.0, prep=0.0, sha=0.0, verifies=0, sha_blocks=0, pay_blocks=0)
     kern = {n: 0.0 for n in _lib.Engine.KERNELS}
-    host = dict(parse_ms=0.0, assemble_ms=0.0, device_ms=0.0, fold_ms=0.0)
-    cur = [0]
+    host = dict(parse_ms=0.0, assemble_ms=0.0, device_ms=0.0, fold_ms=0.0, front_ahead_ms=0.0)
+    # the last warmup call ran batch W-1 and announced batch W (mod NB): the timed loop starts there
+    start = args.warmup % NB
+    cur = [start]
 
     def collect():
         tm, cn = hsteps[cur[0] % NB].stats()
@@ -477,14 +485,16 @@ def run_block(args, world, rank, local, dev_fn):
         for key, v in kt.items():
             kern[key] += v
         acc["pay_blocks"] += npay
+        host["front_ahead_ms"] += eng.front_ahead_ms()
 
-    el = timed(hsteps, args.steps, collect)
+    el = timed(hsteps, args.steps, collect, start=start)
+    kstats = eng.key_stats()  # (vb_verifies_last: the last timed step's variable-base verifies)
     # per-kernel times of the back half need the timestamp events fgv_set_timing adds (each a
     # packet on the critical path): read them from an instrumented, untimed pass
     kdiag = {n: 0.0 for n in _lib.Engine.KERNELS}
     eng.set_timing(True)
-    for s in range(NB):
-        step(hsteps[s], s)
+    for s in range(start + args.steps, start + args.steps + NB):
+        step(hsteps[s % NB], s % NB)
         for key, v in eng.kernel_times()[0].items():
             kdiag[key] += v / NB
     eng.set_timing(False)
@@ -602,6 +612,8 @@ def run_block(args, world, rank, local, dev_fn):
                             **({"integrity_ms": round(integ["ms"] / K, 3)} if spec["integrity"] else {})),
                roofline=block_roofline(kavg, acc["pay_blocks"] / K, acc["verifies"] / K, batch_mb * 1e6,
                                        args.workload),
+               key_tiers=dict(ids=kstats["ids"], comb=kstats["comb"], vb=kstats["vb"], promoted=kstats["promoted"],
+                              vb_verifies_per_step=kstats["vb_verifies_last"]),
                cpu_baseline=None)
     if cpu is not None:
         rate, n, cel, nb = cpu["full"]
@@ -860,6 +872,9 @@ def main():
     ap.add_argument("--mvcc-single-steps", type=int, default=20,
                     help="C3 with --mvcc-chain > 1: blocks validated one call each after the timed pass (latency)")
     ap.add_argument("--blocks-per-gpu", type=int, default=32)
+    ap.add_argument("--clients", type=int, default=0,
+                    help="block workload: client identities (0: the workload's 100; e.g. 16000 = every creator "
+                         "of a 16k-tx step about once: identity churn, client keys on the variable-base kernels)")
     ap.add_argument("--tx-per-block", type=int, default=500)
     ap.add_argument("--per-gpu", type=int, default=131072)
     ap.add_argument("--batches", type=int, default=6,

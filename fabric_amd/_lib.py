@@ -19,7 +19,7 @@ EXPORTED = [
     "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_last_counts", "fgv_last_host_timing",
     "fgv_last_point_handovers", "fgv_last_kernel_times",
     "fgv_sha256_batch",
-    "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset",
+    "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset", "fgv_key_stats",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
@@ -79,7 +79,7 @@ class IdentityInfo(ctypes.Structure):
 
 class _Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("key_slots", ctypes.c_uint32),
-                ("host_threads", ctypes.c_uint32)]
+                ("host_threads", ctypes.c_uint32), ("key_ids", ctypes.c_uint32)]
 
 
 _L = None
@@ -116,6 +116,7 @@ def load():
         L.fgv_p256_verify_msgs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
         L.fgv_keys_register.argtypes = [vp, vp, sz, vp]
         L.fgv_keys_reset.argtypes = [vp]
+        L.fgv_key_stats.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 5
         L.fgv_p256_verify_msgs_dev.argtypes = [vp] * 8 + [sz, vp]
         L.fgv_channel_init.argtypes = [vp, ctypes.c_char_p]
         L.fgv_msp_add_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
@@ -346,10 +347,10 @@ class Group:
     """fgv_group: several GPUs driven from one process.  .engines[i] is device i's context
     (set each one up like an Engine: txvalidator.setup_channel(...) on every one)."""
 
-    def __init__(self, devices, key_slots: int = 0, host_threads: int = 0):
+    def __init__(self, devices, key_slots: int = 0, host_threads: int = 0, key_ids: int = 0):
         self._L = load()
         arr = (ctypes.c_int * len(devices))(*devices)
-        cfg = _Config(devices[0], key_slots, host_threads)
+        cfg = _Config(devices[0], key_slots, host_threads, key_ids)
         h = ctypes.c_void_p()
         _check(self._L.fgv_group_init(arr, len(devices), ctypes.byref(cfg), ctypes.byref(h)))
         self._g = h
@@ -400,12 +401,13 @@ class Group:
 class Engine:
     """One libfgv context = one GPU (one process per GPU)."""
 
-    def __init__(self, device: int = 0, key_slots: int = 0, host_threads: int = 0):
+    def __init__(self, device: int = 0, key_slots: int = 0, host_threads: int = 0, key_ids: int = 0):
         """host_threads: fgv_config.host_threads (0 = the library default, 24); the
-        FGV_HOST_THREADS environment variable sets it when the argument is 0"""
+        FGV_HOST_THREADS environment variable sets it when the argument is 0.  key_slots: comb
+        slots (0 = 2048); key_ids: distinct keys held at once (0 = 1M)"""
         self._L = load()
         host_threads = host_threads or int(os.environ.get("FGV_HOST_THREADS", "0"))
-        cfg = _Config(device, key_slots, host_threads)
+        cfg = _Config(device, key_slots, host_threads, key_ids)
         h = ctypes.c_void_p()
         _check(self._L.fgv_init(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
@@ -466,6 +468,12 @@ class Engine:
         _check(self._L.fgv_last_kernel_times(self._h, out, 11))
         return dict(zip(self.KERNELS, out[:10])), int(out[10])
 
+    def front_ahead_ms(self):
+        """fgv_last_kernel_times out[11]: host ms spent enqueueing the next batch's front half"""
+        out = (ctypes.c_double * 12)()
+        _check(self._L.fgv_last_kernel_times(self._h, out, 12))
+        return float(out[11])
+
     def point_handovers(self):
         v = ctypes.c_uint64()
         _check(self._L.fgv_last_point_handovers(self._h, ctypes.byref(v)))
@@ -513,6 +521,12 @@ class Engine:
 
     def keys_reset(self):
         _check(self._L.fgv_keys_reset(self._h))
+
+    def key_stats(self):
+        """fgv_key_stats: {ids, comb, vb, promoted, vb_verifies_last}"""
+        v = [ctypes.c_uint64() for _ in range(5)]
+        _check(self._L.fgv_key_stats(self._h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("ids", "comb", "vb", "promoted", "vb_verifies_last"), (x.value for x in v)))
 
     # --- HBM-resident batch: arguments are device pointers (ints), e.g. tensor.data_ptr()
     def verify_msgs_dev(self, msg_buf, msg_off, msg_len, sig_buf, sig_off, sig_len, key_slot, n, status):

@@ -2226,11 +2226,17 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
       const char *e = getenv("FGV_PREFIX_AHEAD");
       return e && atoi(e) != 0;
     }();
+    // (with keys on the variable-base kernels the prefix stays in the call: their list and
+    // counters belong to one batch at a time)
+    const auto tf = clk::now();
     if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after,
-                     prefix_ahead) == FGV_OK)
+                     prefix_ahead && c->n_vb == 0) == FGV_OK)
       S->ahead = cur ^ 1;
     else
       drain_ahead(c, S), S->ahead = -1;  // (the next call starts it again and reports any error)
+    c->t_kern[11] = ms_since(tf);  // host time to enqueue it (its pre-split join included)
+  } else {
+    c->t_kern[11] = 0;
   }
   S->pending = cur;
   return FGV_OK;

@@ -24,8 +24,25 @@
 #include "fgv_internal.h"
 #include "fgv_kernels.h"
 
-// Build tables for `nk` keys (qxy: nk*16 limbs) into `tables` at `slots`, KT_BUILD_KEYS keys
-// per k_keytab launch (its scratch is KT_ENTRIES Jacobian points per key).
+// ======================================================================= key tiers
+// DESIGN.md s4a.  Every P-256 key the engine verifies against has an id.  Registered keys
+// (fgv_keys_register, channel identities, MSP CA keys) hold ids [0, pinned) for good; ad-hoc
+// BCCSP keys (fgv_p256_verify_batch / _msgs) take ids after them until the id space is flushed.
+// Each id's verifies run on one of two kernel paths:
+//   comb -- kmap[id] = a slot of the comb-table cache (5.2 MB per key, built by k_keytab: ~80 us
+//           of whole-chip time per key, batched 32 keys per launch): k_point28, 32 mixed
+//           additions per verify;
+//   VB   -- kmap[id] = KEY_NONE: k_vb_mul / k_vb_fin from the key's coordinates alone (64 B,
+//           k_keyprep): 256 doublings + <= 64 additions for u2 * Q, ~9x a comb verify, no build.
+// Policy: a key expected to be hot -- fgv_keys_register, an identity with a PEER / ORDERER / ADMIN
+// role or unknown roles, an MSP CA key, an ad-hoc key used >= adhoc_comb_uses times in its call --
+// takes a comb slot while one is free.  Every other key (client identities, one-off ad-hoc keys)
+// starts on VB; k_vb_mul counts its verifies and queues it once they reach promote_uses, and the
+// next call builds its comb in a free slot (promote_consume).  A full comb cache never fails a
+// batch: the keys stay on VB.  Only the id space (fgv_config.key_ids) can run out.
+
+// Build comb tables for `nk` keys (h_qxy: nk*16 plain limbs) into `tables28` at `h_slots`,
+// KT_BUILD_KEYS keys per k_keytab launch (its scratch is KT_ENTRIES Jacobian points per key).
 static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slots, uint32_t nk,
                         apoint_raw *tables, apoint_raw *tables28, uint8_t *ok) {
   const uint32_t per = nk < KT_BUILD_KEYS ? nk : KT_BUILD_KEYS;
@@ -44,6 +61,117 @@ static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slo
   }
   HIP_TRY(hipEventRecord(c->ev[7], c->stream));
   return FGV_OK;
+}
+
+// comb tables for ids that have none (taken in order while comb slots are free; the rest stay on
+// VB).  Synchronises the stream (the staging buffers are reused by the next build).
+static int comb_build(fgv_ctx *c, const std::vector<uint32_t> &ids) {
+  std::vector<uint32_t> take;
+  for (uint32_t id : ids)
+    if (take.size() < c->comb_free.size() && id < c->n_ids && c->kmap_h[id] == KEY_NONE) take.push_back(id);
+  if (take.empty()) return FGV_OK;
+  const uint32_t nk = (uint32_t)take.size();
+  if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kslot.ensure((size_t)nk * 4) || !c->h_kid.ensure((size_t)nk * 4) ||
+      !c->kt_id.ensure((size_t)nk * 4))
+    return FGV_ENOMEM;
+  uint32_t *kq = c->h_kq.as<uint32_t>(), *ks = c->h_kslot.as<uint32_t>(), *ki = c->h_kid.as<uint32_t>();
+  for (uint32_t j = 0; j < nk; j++) {
+    const uint32_t id = take[j], slot = c->comb_free.back();
+    c->comb_free.pop_back();
+    c->comb_owner[slot] = id;
+    c->kmap_h[id] = slot;
+    c->n_vb--;
+    be32_to_limbs(c->id_key[id].data(), kq + 16 * j);
+    be32_to_limbs(c->id_key[id].data() + 32, kq + 16 * j + 8);
+    ks[j] = slot;
+    ki[j] = id;
+  }
+  int rc = build_tables(c, kq, ks, nk, nullptr, c->ktab28.as<apoint_raw>(), nullptr);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->kt_id.p, ki, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_kmap_set, dim3((nk + 63) / 64), dim3(64), 0, c->stream, c->kt_id.as<uint32_t>(),
+                     c->kt_slot.as<uint32_t>(), nk, c->kmap.as<uint32_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->ev[6], c->ev[7]) == hipSuccess) c->t_keytab += ms;
+  return FGV_OK;
+}
+
+// forget the ad-hoc ids [pinned, n_ids): their comb slots go back to the free list
+static int flush_adhoc(fgv_ctx *c) {
+  if (c->n_ids == c->pinned) return FGV_OK;
+  for (uint32_t id = c->pinned; id < c->n_ids; id++) {
+    c->key_map.erase(c->id_key[id]);
+    const uint32_t slot = c->kmap_h[id];
+    if (slot == KEY_NONE) {
+      c->n_vb--;
+    } else {
+      c->comb_owner[slot] = KEY_NONE;
+      c->comb_free.push_back(slot);
+      c->kmap_h[id] = KEY_NONE;
+    }
+  }
+  const size_t k = c->n_ids - c->pinned;
+  HIP_TRY(hipMemsetAsync(c->kmap.as<uint32_t>() + c->pinned, 0xFF, k * 4, c->stream));
+  HIP_TRY(hipMemsetAsync(c->vbuse.as<uint32_t>() + c->pinned, 0, k * 4, c->stream));
+  c->n_ids = c->pinned;
+  c->id_key.resize(c->n_ids);
+  return FGV_OK;
+}
+
+// ids for `keys` (distinct, none known yet): coordinates and on-curve bits on the device
+// (k_keyprep), then comb tables for those with want[i] (nullable: all) while slots are free.
+// Synchronises the stream.
+static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys, const std::vector<uint8_t> *want,
+                   uint32_t *ids_out) {
+  const uint32_t nk = (uint32_t)keys.size();
+  if (nk == 0) return FGV_OK;
+  if ((uint64_t)c->n_ids + nk > c->key_ids) return FGV_ENOMEM;
+  if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kid.ensure((size_t)nk * 4) || !c->kt_q.ensure((size_t)nk * 64) ||
+      !c->kt_id.ensure((size_t)nk * 4))
+    return FGV_ENOMEM;
+  uint32_t *kq = c->h_kq.as<uint32_t>(), *ki = c->h_kid.as<uint32_t>();
+  std::vector<uint32_t> comb;
+  for (uint32_t j = 0; j < nk; j++) {
+    const uint32_t id = c->n_ids++;
+    c->key_map.emplace(keys[j], id);
+    c->id_key.push_back(keys[j]);
+    c->kmap_h[id] = KEY_NONE;
+    c->n_vb++;
+    be32_to_limbs(keys[j].data(), kq + 16 * j);
+    be32_to_limbs(keys[j].data() + 32, kq + 16 * j + 8);
+    ki[j] = id;
+    ids_out[j] = id;
+    if (!want || (*want)[j]) comb.push_back(id);
+  }
+  HIP_TRY(hipMemcpyAsync(c->kt_q.p, kq, (size_t)nk * 64, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->kt_id.p, ki, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_keyprep, dim3((nk + 63) / 64), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
+                     c->kt_id.as<uint32_t>(), nk, c->vbq.as<uint32_t>(), c->key_ok.as<uint8_t>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));  // (the staging is reused by comb_build)
+  return comb_build(c, comb);
+}
+
+// The promotion queue k_vb_mul filled (copied back on streamV behind it): build combs for the
+// queued ids, then empty the queue on the device.  At the start of a call, under c->mu; a copy
+// still in flight is left for the next call.
+static int promote_consume(fgv_ctx *c) {
+  if (!c->vb_copied || hipEventQuery(c->vb_ev[2]) != hipSuccess) return FGV_OK;
+  c->vb_copied = false;
+  uint32_t *q = c->h_promo.as<uint32_t>();
+  const uint32_t np = std::min<uint32_t>(q[0], VB_PROMO_CAP);
+  if (np == 0) return FGV_OK;
+  std::vector<uint32_t> ids(q + 2, q + 2 + np);
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  q[0] = 0;
+  HIP_TRY(hipMemsetAsync(c->vbpromo.p, 0, 4, c->stream));
+  const uint32_t before = (uint32_t)c->comb_free.size();
+  int rc = comb_build(c, ids);
+  c->n_promoted += before - c->comb_free.size();
+  return rc;
 }
 
 extern "C" {
@@ -67,6 +195,9 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   if (!c) return FGV_ENOMEM;
   c->device = cfg ? cfg->device : 0;
   c->key_slots = (cfg && cfg->key_slots) ? cfg->key_slots : 2048;
+  c->key_ids = (cfg && cfg->key_ids) ? cfg->key_ids : (1u << 20);
+  if (const char *e = getenv("FGV_PROMOTE_USES")) c->promote_uses = (uint32_t)std::max(1, atoi(e));
+  if (const char *e = getenv("FGV_ADHOC_COMB")) c->adhoc_comb_uses = (uint32_t)std::max(1, atoi(e));
   // host workers: fgv_config.host_threads, else min(24, this process's CPU share) -- 24 measured
   // best on a whole machine (tools/sweep_threads.sh); eight ranks on one node each get their
   // affinity mask's share, not the whole machine
@@ -99,7 +230,10 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     if (hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->streamF, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+    if (hipStreamCreateWithPriority(&c->streamV, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
   }
+  for (auto &e : c->vb_ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
   for (auto &e : c->stage_ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
   {
@@ -117,9 +251,22 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     c->n_cu = (uint32_t)ncu;
   }
   if (!c->g_ok.ensure(16) || !c->gtab28.ensure(GT_BYTES) || !c->redo.ensure(64) ||
-      !c->ktab28.ensure((size_t)c->key_slots * KT_BYTES) ||
-      !c->key_ok.ensure(c->key_slots))
+      !c->ktab28.ensure((size_t)c->key_slots * KT_BYTES) || !c->key_ok.ensure(c->key_ids) ||
+      !c->kmap.ensure((size_t)c->key_ids * 4) || !c->vbq.ensure((size_t)c->key_ids * 64) ||
+      !c->vbuse.ensure((size_t)c->key_ids * 4) || !c->vbpromo.ensure((VB_PROMO_CAP + 2) * 4) ||
+      !c->h_promo.ensure((VB_PROMO_CAP + 2) * 4))
     return fail(FGV_ENOMEM);
+  // key tiers: every id starts without a comb; comb slots free, taken from slot 0 up
+  c->kmap_h.assign(c->key_ids, KEY_NONE);
+  c->comb_owner.assign(c->key_slots, KEY_NONE);
+  c->comb_free.resize(c->key_slots);
+  for (uint32_t k = 0; k < c->key_slots; k++) c->comb_free[k] = c->key_slots - 1 - k;
+  memset(c->h_promo.p, 0, (VB_PROMO_CAP + 2) * 4);
+  if (hipMemset(c->redo.p, 0, 64) != hipSuccess || hipMemset(c->kmap.p, 0xFF, (size_t)c->key_ids * 4) != hipSuccess ||
+      hipMemset(c->vbuse.p, 0, (size_t)c->key_ids * 4) != hipSuccess ||
+      hipMemset(c->vbpromo.p, 0, (VB_PROMO_CAP + 2) * 4) != hipSuccess ||
+      hipMemset(c->key_ok.p, 0, c->key_ids) != hipSuccess)
+    return fail(FGV_EDEVICE);
   // generator comb table (k_gtab), built once per context
   {
     DevBuf scr;
@@ -142,10 +289,11 @@ void fgv_destroy(fgv_ctx *c) {
   if (!c) return;
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
-  for (hipStream_t x : {c->stream2, c->stream3, c->streamF})  // (a front half enqueued ahead)
+  for (hipStream_t x : {c->stream2, c->stream3, c->streamF, c->streamV})  // (a front half enqueued ahead)
     if (x) hipStreamSynchronize(x);
   DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->stage[2], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
                  &c->bd_misc, &c->g_ok, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
+                 &c->kmap, &c->vbq, &c->vbuse, &c->vbpromo, &c->vblist, &c->vbacc, &c->vbscr, &c->kt_id,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
                  &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
                  &c->bj_dig, &c->bj_vst, &c->blk_arena, &c->fz_meta, &c->fz_rowmap, &c->fz_blkof,
@@ -158,7 +306,7 @@ void fgv_destroy(fgv_ctx *c) {
   HostBuf *h[] = {&c->h_status, &c->h_slot, &c->h_r, &c->h_s, &c->h_dig, &c->h_kq, &c->h_kslot,
                   &c->h_moff, &c->h_mlen, &c->hb_dig, &c->hb_vst, &c->hb_jobs, &c->hb_sigp,
                   &c->hb_sigl, &c->hb_slot, &c->hb_didx, &c->hb_fz, &c->hb_fflags, &c->hb_res,
-                  &c->hb_env, &c->hb_bases, &c->hb_misc};
+                  &c->hb_env, &c->hb_bases, &c->hb_misc, &c->h_promo, &c->h_kid};
   for (auto *b : h) b->release();
   for (auto &e : c->ev)
     if (e) hipEventDestroy(e);
@@ -169,6 +317,9 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->stream3) hipStreamDestroy(c->stream3);
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   if (c->streamF) hipStreamDestroy(c->streamF);
+  if (c->streamV) hipStreamDestroy(c->streamV);
+  for (auto &e : c->vb_ev)
+    if (e) hipEventDestroy(e);
   for (auto e : c->stage_ev)
     if (e) hipEventDestroy(e);
   delete c;
@@ -232,11 +383,42 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
   nl = (nl + INV_THREADS - 1) / INV_THREADS * INV_THREADS;
   if (!wscr.ensure((size_t)PREP_B * 8 * nl * 4) || !w.ensure((size_t)N * 32)) return FGV_ENOMEM;
   const bool tim = c->timing || !dn;  // (host-count callers always time their stages)
+  // keys whose variable-base verifies reached the promotion threshold in an earlier call get their
+  // comb tables now (stream-ordered before this batch's point kernels read kmap)
+  int prc = promote_consume(c);
+  if (prc) return prc;
+  // keys without a comb (c->n_vb): k_inv lists their items, k_vb_mul computes u2 * Q for them on
+  // streamV -- beside the hashes and k_prep: it needs s^-1, not the digest -- and
+  // launch_prep_point's k_vb_fin adds u1 * G once k_prep has run
+  const bool vb = c->n_vb > 0;
+  c->vb_launched = vb;
+  const size_t scr = (size_t)2 * c->n_cu * VB_THREADS * VB_TAB * VB_TAB_WORDS * 4;
+  if (vb && (!c->vblist.ensure((size_t)N * 4) || !c->vbacc.ensure((size_t)N * VB_TAB_WORDS * 4) ||
+             !c->vbscr.ensure(scr)))
+    return FGV_ENOMEM;
+  uint32_t *redo = c->redo.as<uint32_t>();
   if (tim) HIP_TRY(hipEventRecord(c->ev[2], st));
   hipLaunchKernelGGL(k_inv, dim3(nl / INV_THREADS), dim3(INV_THREADS), 0, st, N, dn, d_status, d_slot,
-                     c->key_ok.as<uint8_t>(), d_r, d_s, w.as<uint32_t>(), wscr.as<uint32_t>());
+                     c->key_ok.as<uint8_t>(), d_r, d_s, w.as<uint32_t>(), wscr.as<uint32_t>(),
+                     vb ? c->kmap.as<uint32_t>() : nullptr, vb ? c->vblist.as<uint32_t>() : nullptr,
+                     vb ? redo + RD_VB_CNT : nullptr);
   HIP_TRY(hipGetLastError());
   if (tim) HIP_TRY(hipEventRecord(c->ev[3], st));
+  if (vb) {
+    HIP_TRY(hipEventRecord(c->vb_ev[0], st));
+    HIP_TRY(hipStreamWaitEvent(c->streamV, c->vb_ev[0], 0));
+    hipLaunchKernelGGL(k_vb_mul, dim3(2 * c->n_cu), dim3(VB_THREADS), 0, c->streamV, N, d_slot,
+                       c->vbq.as<uint32_t>(), d_r, w.as<uint32_t>(), redo, redo + RD_VB_MUL,
+                       c->vblist.as<uint32_t>(), c->vbscr.as<uint32_t>(), c->vbacc.as<uint32_t>(),
+                       c->vbuse.as<uint32_t>(), c->promote_uses, c->vbpromo.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->vb_ev[1], c->streamV));
+    // the promotion queue back to the host behind it (read by the next call: promote_consume)
+    HIP_TRY(hipMemcpyAsync(c->h_promo.p, c->vbpromo.p, (VB_PROMO_CAP + 2) * 4, hipMemcpyDeviceToHost, c->streamV));
+    HIP_TRY(hipEventRecord(c->vb_ev[2], c->streamV));
+    c->vb_copied = true;
+    c->vb_pending = true;
+  }
   return FGV_OK;
 }
 static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn, uint8_t *d_status,
@@ -296,12 +478,22 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
 
   if (redo) {
     hipLaunchKernelGGL(k_point28, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, dn, L, d_status, d_slot,
-                       c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
+                       c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo,
+                       c->kmap.as<uint32_t>());
   }
   hipLaunchKernelGGL(k_point, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, dn, L, d_status, d_slot,
-                     c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo);
+                     c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo,
+                     c->kmap.as<uint32_t>());
   c->last_lanes = L;
   HIP_TRY(hipGetLastError());
+  if (c->vb_pending) {  // the variable-base items: + u1 * G and the x check, after k_vb_mul (streamV)
+    c->vb_pending = false;
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->vb_ev[1], 0));
+    hipLaunchKernelGGL(k_vb_fin, dim3(2 * c->n_cu), dim3(256), 0, c->stream, N, d_status, c->gtab28.as<apoint_raw>(),
+                       c->d1.as<int8_t>(), d_r, c->redo.as<uint32_t>(), c->vblist.as<uint32_t>(),
+                       c->vbacc.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipEventRecord(c->ev[6], c->stream));  // (ahead mode 1 waits on it)
   return FGV_OK;
 }
@@ -397,26 +589,27 @@ static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, 
   uint8_t *st = c->h_status.as<uint8_t>();
   uint32_t *slot = c->h_slot.as<uint32_t>(), *R = c->h_r.as<uint32_t>(), *S = c->h_s.as<uint32_t>();
 
-  // 1) host: Go-rule DER + low-S; key -> slot
-  std::vector<uint32_t> new_keys;  // item index of first occurrence
+  // 1) host: Go-rule DER + low-S; key -> id (new keys counted, assigned below)
+  std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> fresh;  // new key -> uses in this call
+  std::unordered_map<uint32_t, uint32_t> vb_uses;                        // known VB id -> uses in this call
   size_t pending = 0;
   for (size_t i = 0; i < n; i++) {
     uint32_t r[8], s[8];
     const int code = der_prepare(sig_buf, sig_buf_len, sig_off[i], sig_len[i], r, s);
     if (code < 0) return FGV_EINVAL;
     st[i] = (uint8_t)code;
-    if (code != ST_PENDING) {
-      slot[i] = 0;
-    } else {
+    slot[i] = 0;
+    if (code == ST_PENDING) {
       pending++;
       std::array<uint8_t, 64> k;
       memcpy(k.data(), keys + 64 * i, 64);
       auto it = c->key_map.find(k);
       if (it == c->key_map.end()) {
-        slot[i] = 0xFFFFFFFFu;  // assigned below
-        new_keys.push_back((uint32_t)i);
+        fresh[k]++;
+        slot[i] = KEY_NONE;  // assigned below
       } else {
         slot[i] = it->second;
+        if (c->kmap_h[it->second] == KEY_NONE) vb_uses[it->second]++;
       }
     }
     for (int k = 0; k < 8; k++) {
@@ -424,61 +617,54 @@ static int verify_core(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_buf, 
       S[(size_t)k * n + i] = s[k];
     }
   }
-  // 2) assign slots to new keys (dedup), evicting the whole cache if it would overflow
+  // 2) ids for new keys (the ad-hoc ids are flushed when the id space would overflow); a key
+  // used adhoc_comb_uses times in this call gets a comb table while slots are free (C4: 16 keys x
+  // 8192 uses), a one-off key runs on the variable-base kernels
   c->t_keytab = 0;
-  if (!new_keys.empty()) {
-    std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> fresh;
-    for (uint32_t i : new_keys) {
-      std::array<uint8_t, 64> k;
-      memcpy(k.data(), keys + 64 * (size_t)i, 64);
-      fresh.emplace(k, 0);
-    }
-    if (c->key_map.size() + fresh.size() > c->key_slots) {
-      // count distinct keys this batch needs; evict everything else
-      std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> needed;
-      for (size_t i = 0; i < n; i++)
-        if (st[i] == ST_PENDING) {
-          std::array<uint8_t, 64> k;
-          memcpy(k.data(), keys + 64 * i, 64);
-          needed.emplace(k, 0);
-        }
-      if (needed.size() + c->pinned > c->key_slots) return FGV_ENOMEM;
-      for (auto it = c->key_map.begin(); it != c->key_map.end();)
-        it = (it->second >= c->pinned) ? c->key_map.erase(it) : std::next(it);
-      for (auto it = needed.begin(); it != needed.end();)
-        it = c->key_map.count(it->first) ? needed.erase(it) : std::next(it);
-      fresh = std::move(needed);
-    }
-    uint32_t nk = (uint32_t)fresh.size();
-    if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kslot.ensure((size_t)nk * 4)) return FGV_ENOMEM;
-    uint32_t *kq = c->h_kq.as<uint32_t>(), *ks = c->h_kslot.as<uint32_t>();
-    uint32_t j = 0, next = (uint32_t)c->key_map.size();  // == pinned + live ad-hoc keys
-    for (auto &kv : fresh) {
-      be32_to_limbs(kv.first.data(), kq + 16 * j);
-      be32_to_limbs(kv.first.data() + 32, kq + 16 * j + 8);
-      ks[j] = next;
-      c->key_map.emplace(kv.first, next);
-      next++;
-      j++;
-    }
-    int rc = build_tables(c, kq, ks, nk, nullptr, c->ktab28.as<apoint_raw>(),
-                          c->key_ok.as<uint8_t>());
-    if (rc) return rc;
-    // re-resolve every pending slot (the cache may have been flushed)
-    for (size_t i = 0; i < n; i++)
-      if (st[i] == ST_PENDING) {
+  if (!fresh.empty() || !vb_uses.empty()) {
+    if ((uint64_t)c->n_ids + fresh.size() > c->key_ids) {
+      int rc = flush_adhoc(c);
+      if (rc) return rc;
+      fresh.clear();
+      vb_uses.clear();
+      for (size_t i = 0; i < n; i++) {
+        if (st[i] != ST_PENDING) continue;
         std::array<uint8_t, 64> k;
         memcpy(k.data(), keys + 64 * i, 64);
-        slot[i] = c->key_map[k];
+        auto it = c->key_map.find(k);
+        if (it == c->key_map.end()) {
+          fresh[k]++;
+          slot[i] = KEY_NONE;
+        } else if (c->kmap_h[it->second] == KEY_NONE) {
+          vb_uses[it->second]++;
+        }
       }
+      if ((uint64_t)c->n_ids + fresh.size() > c->key_ids) return FGV_ENOMEM;
+    }
+    std::vector<std::array<uint8_t, 64>> nk;
+    std::vector<uint8_t> want;
+    for (auto &kv : fresh) {
+      nk.push_back(kv.first);
+      want.push_back(kv.second >= c->adhoc_comb_uses);
+    }
+    std::vector<uint32_t> ids(nk.size());
+    int rc = ids_new(c, nk, &want, ids.data());
+    if (rc) return rc;
+    std::vector<uint32_t> hot;  // known VB keys this call uses often
+    for (auto &kv : vb_uses)
+      if (kv.second >= c->adhoc_comb_uses) hot.push_back(kv.first);
+    rc = comb_build(c, hot);
+    if (rc) return rc;
+    if (!nk.empty())
+      for (size_t i = 0; i < n; i++)
+        if (st[i] == ST_PENDING && slot[i] == KEY_NONE) {
+          std::array<uint8_t, 64> k;
+          memcpy(k.data(), keys + 64 * i, 64);
+          slot[i] = c->key_map[k];
+        }
   }
   // 3) upload + kernels
-  const int rc = verify_run(c, n, pending, h_digests, dev_digests, status_out);
-  if (rc) return rc;
-  float ms = 0;
-  if (!new_keys.empty() && hipEventElapsedTime(&ms, c->ev[6], c->ev[7]) == hipSuccess)
-    c->t_keytab = ms;
-  return FGV_OK;
+  return verify_run(c, n, pending, h_digests, dev_digests, status_out);
 }
 
 static int launch_sha(fgv_ctx *c, const uint8_t *d_buf, const uint64_t *d_off,
@@ -588,54 +774,82 @@ int fgv_p256_verify_msgs(fgv_ctx *c, const uint8_t *keys, const uint8_t *msg_buf
 int fgv_keys_reset(fgv_ctx *c) {
   if (!c) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->pinned) return FGV_ESTATE;  // identities of the channel model hold slots
-  c->key_map.clear();
+  if (c->pinned) return FGV_ESTATE;  // identities of the channel model hold ids
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  const int rc = flush_adhoc(c);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
   return FGV_OK;
 }
 
-static int keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots);
+int fgv_key_stats(fgv_ctx *c, uint64_t *ids, uint64_t *comb, uint64_t *vb, uint64_t *promoted,
+                  uint64_t *vb_verifies_last) {
+  if (!c) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (ids) *ids = c->n_ids;
+  if (comb) *comb = c->n_ids - c->n_vb;
+  if (vb) *vb = c->n_vb;
+  if (promoted) *promoted = c->n_promoted;
+  if (vb_verifies_last) {  // (k_vb_mul of the last verify stages wrote it; copied back behind it)
+    *vb_verifies_last = 0;
+    if (c->vb_launched) {
+      HIP_TRY(hipEventSynchronize(c->vb_ev[2]));
+      *vb_verifies_last = c->h_promo.as<uint32_t>()[1];
+    }
+  }
+  return FGV_OK;
+}
+
+static int keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots, const uint8_t *want_comb);
 
 int fgv_keys_register(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots) {
   if (!c || (n && (!keys || !slots))) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  return keys_register_locked(c, keys, n, slots);
+  return keys_register_locked(c, keys, n, slots, nullptr);
 }
 
-// registered keys are pinned: ad-hoc (BCCSP-path) keys are dropped first so the pinned range
-// stays contiguous
-static int keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots) {
+// registered keys are pinned: ad-hoc (BCCSP-path) ids are dropped first so the pinned range
+// stays contiguous.  A key registered before keeps its id and tier -- except that a key now
+// wanted hot gets a comb if it has none and a slot is free.
+static int keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots, const uint8_t *want_comb) {
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  c->t_keytab = 0;
   std::vector<std::array<uint8_t, 64>> fresh;
-  std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> seen;
+  std::vector<uint8_t> want;
+  std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> seen;  // fresh key -> index
+  std::vector<uint32_t> upgrade;
+  bool adhoc_hit = false;
   for (size_t i = 0; i < n; i++) {
     std::array<uint8_t, 64> k;
     memcpy(k.data(), keys + 64 * i, 64);
-    if (c->key_map.count(k) || seen.count(k)) continue;
-    seen.emplace(k, 0);
-    fresh.push_back(k);
-  }
-  if (c->pinned + fresh.size() > c->key_slots) return FGV_ENOMEM;
-  c->t_keytab = 0;
-  if (!fresh.empty()) {
-    for (auto it = c->key_map.begin(); it != c->key_map.end();)
-      it = (it->second >= c->pinned) ? c->key_map.erase(it) : std::next(it);
-    const uint32_t nk = (uint32_t)fresh.size();
-    if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kslot.ensure((size_t)nk * 4)) return FGV_ENOMEM;
-    uint32_t *kq = c->h_kq.as<uint32_t>(), *ks = c->h_kslot.as<uint32_t>();
-    uint32_t next = c->pinned;
-    for (uint32_t j = 0; j < nk; j++) {
-      be32_to_limbs(fresh[j].data(), kq + 16 * j);
-      be32_to_limbs(fresh[j].data() + 32, kq + 16 * j + 8);
-      ks[j] = next + j;
+    const bool w = !want_comb || want_comb[i];
+    auto it = c->key_map.find(k);
+    if (it != c->key_map.end() && it->second < c->pinned) {
+      if (w && c->kmap_h[it->second] == KEY_NONE) upgrade.push_back(it->second);
+      continue;
     }
-    int rc = build_tables(c, kq, ks, nk, nullptr, c->ktab28.as<apoint_raw>(),
-                          c->key_ok.as<uint8_t>());
+    adhoc_hit |= it != c->key_map.end();
+    auto sj = seen.find(k);
+    if (sj != seen.end()) {
+      want[sj->second] |= w;
+      continue;
+    }
+    seen.emplace(k, (uint32_t)fresh.size());
+    fresh.push_back(k);
+    want.push_back(w);
+  }
+  if (!fresh.empty() || adhoc_hit) {
+    int rc = flush_adhoc(c);
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    for (uint32_t j = 0; j < nk; j++) c->key_map.emplace(fresh[j], next + j);
-    c->pinned += nk;
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev[6], c->ev[7]) == hipSuccess) c->t_keytab = ms;
+    if ((uint64_t)c->pinned + fresh.size() > c->key_ids) return FGV_ENOMEM;
+    std::vector<uint32_t> ids(fresh.size());
+    rc = ids_new(c, fresh, &want, ids.data());
+    if (rc) return rc;
+    c->pinned = c->n_ids;
+  }
+  if (!upgrade.empty()) {
+    int rc = comb_build(c, upgrade);
+    if (rc) return rc;
   }
   for (size_t i = 0; i < n; i++) {
     std::array<uint8_t, 64> k;
@@ -698,8 +912,8 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *c, const uint8_t *d_msg_buf, const uint64_
 
 }  // extern "C"
 
-int fgv_keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots) {
-  return keys_register_locked(c, keys, n, slots);
+int fgv_keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots, const uint8_t *want_comb) {
+  return keys_register_locked(c, keys, n, slots, want_comb);
 }
 
 // ======================================================================= block engine glue
@@ -884,7 +1098,8 @@ int fgv_msp_register_identity(fgv_ctx *c, const uint8_t *serialized, size_t len,
   int32_t slot = -1;
   if (info->key_type == FGV_KEY_P256) {
     uint32_t s;
-    int rc = keys_register_locked(c, info->pubkey, 1, &s);
+    const uint8_t want = fgv_roles_want_comb(info->roles) ? 1 : 0;
+    int rc = keys_register_locked(c, info->pubkey, 1, &s, &want);
     if (rc) return rc;
     slot = (int32_t)s;
   }

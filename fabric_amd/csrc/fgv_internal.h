@@ -110,13 +110,31 @@ struct fgv_ctx {
   double t_kern[12] = {};
   uint64_t n_pay_blocks = 0;      // SHA-256 compressions of the payload hashes (last block call)
   std::mutex mu;
-  // generator table (88 KB) and the public-key table cache
+  // the generator comb, the key tiers (fgv_host.cpp): every key has an id;
+  // kmap[id] = its slot in the comb-table cache or KEY_NONE (variable-base kernels)
   DevBuf g_ok;
-  DevBuf key_ok;
-  DevBuf gtab28, ktab28, redo;  // Montgomery-280 copies of the comb tables (k_point28)
-  uint32_t key_slots = 0;
-  uint32_t pinned = 0;  // slots [0, pinned) hold registered keys and are never evicted
-  std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_map;
+  DevBuf key_ok;                // [id] the key is a P-256 point
+  DevBuf gtab28, ktab28, redo;  // Montgomery-280 comb tables (k_point28); redo: kernel counters
+  uint32_t key_slots = 0;       // comb slots (5.2 MB each)
+  uint32_t key_ids = 0;         // id capacity
+  uint32_t pinned = 0;          // ids [0, pinned): registered keys, for good; then ad-hoc ids up to n_ids
+  uint32_t n_ids = 0;
+  uint32_t n_vb = 0;            // ids without a comb (the variable-base kernels run when > 0)
+  std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_map;  // key -> id
+  std::vector<std::array<uint8_t, 64>> id_key;  // id -> key
+  std::vector<uint32_t> kmap_h;                 // host mirror of kmap
+  std::vector<uint32_t> comb_owner;             // comb slot -> id (KEY_NONE: free)
+  std::vector<uint32_t> comb_free;              // free comb slots (popped from the back)
+  DevBuf kmap, vbq, vbuse, vbpromo, vblist, vbacc, vbscr, kt_id;
+  HostBuf h_promo, h_kid;       // the promotion queue read back (k_vb_mul -> streamV copy)
+  hipStream_t streamV = nullptr;  // k_vb_mul: beside the hashes (u2 * Q needs no digest)
+  hipEvent_t vb_ev[3] = {};       // 0 the VB list is built (k_inv), 1 k_vb_mul done, 2 queue copied
+  bool vb_pending = false;        // k_vb_mul enqueued: launch_prep_point adds k_vb_fin
+  bool vb_copied = false;         // a promotion-queue copy was enqueued (vb_ev[2])
+  bool vb_launched = false;       // the last verify stages ran the variable-base kernels
+  uint32_t promote_uses = 64;     // variable-base verifies of one key before its comb is built
+  uint32_t adhoc_comb_uses = 32;  // uses of an ad-hoc key in one call for a comb
+  uint64_t n_promoted = 0;        // keys promoted to a comb since fgv_init
   fgv_block_state *blk = nullptr;
   DevBuf bj_jobs, bj_sigp, bj_sigl, bj_slot, bj_didx, bj_dig, bj_vst, blk_arena;
   HostBuf hb_dig, hb_vst;
@@ -333,8 +351,18 @@ struct fgv_sig_block {
 int fgv_block_sig_verdicts(fgv_ctx *c, size_t n, const fgv_sig_block *in, const char *policy, int bft,
                            uint8_t *verdict);
 
-// registered (pinned) P-256 keys -> key-table slots; c->mu held (fgv_host.cpp)
-int fgv_keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots);
+// registered (pinned) P-256 keys -> key ids; c->mu held (fgv_host.cpp).  want_comb[i] (nullable:
+// all): the key is expected to be hot (a comb slot while one is free), else it starts on the
+// variable-base kernels and is promoted by use
+int fgv_keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots,
+                             const uint8_t *want_comb = nullptr);
+// the comb policy of an identity by its role bits (fgv_identity_info.roles): keys of peers,
+// orderers, admins and identities whose roles are unknown are expected to sign often; keys of
+// identities with none of those roles (clients) start on the variable-base kernels
+inline bool fgv_roles_want_comb(uint32_t roles) {
+  if (roles & FGV_ROLES_UNKNOWN) return true;
+  return (roles & ((1u << 1) | (1u << 3) | (1u << 4))) != 0;  // ADMIN, PEER, ORDERER
+}
 // the channel model of a block state (fgv_block.cpp)
 fgvb::Channel &fgv_block_channel(fgv_block_state *S);
 // the identities a batch names (creators, endorsers) that the registry does not hold but a

@@ -49,16 +49,44 @@ struct jpoint_raw {  // key-table build scratch: Jacobian point + prefix product
 
 __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw *tables, apoint_raw *tables28,
                          jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys);
+// Key tiers.  Every key has an id; kmap[id] is its comb slot (the 5.2 MB table
+// above) or KEY_NONE: the variable-base kernel k_point_vb verifies it from its coordinates alone
+// (vbq[id]: Montgomery-256 x || y, 64 B).  k_keyprep checks new keys (on the curve) and writes
+// vbq / key_ok; k_kmap_set points ids at their freshly built comb tables (after k_keytab).
+#define KEY_NONE 0xFFFFFFFFu
+#define VB_THREADS 256      // k_vb_mul workgroup (grid 2 x n_cu: each lane owns a scratch table)
+#define VB_TAB 15           // per-lane table 1Q .. 15Q (4-bit fixed windows), Jacobian
+#define VB_TAB_WORDS 24     // x, y, z (Montgomery-256)
+// counters in the context's redo words: [0] k_point28 hand-overs, [1] k_point28 chunks, [2] k_point
+// chunks, [3] items k_inv listed for the variable-base kernels, [4] taken by k_vb_mul, [5] taken
+// by k_vb_fin, [6] finished k_vb_fin workgroups (the last one zeroes [3..6] for the next batch)
+#define RD_VB_CNT 3
+#define RD_VB_MUL 4
+#define RD_VB_FIN 5
+#define RD_VB_DONE 6
+#define VB_PROMO_CAP 1022   // promotion queue: [0] count, [1] the last batch's variable-base items,
+                            // then ids whose use count reached the threshold
+__global__ void k_keyprep(const uint32_t *qxy, const uint32_t *ids, uint32_t nkeys, uint32_t *vbq, uint8_t *key_ok);
+__global__ void k_kmap_set(const uint32_t *ids, const uint32_t *slots, uint32_t n, uint32_t *kmap);
+__global__ void k_vb_mul(uint32_t n, const uint32_t *key_slot, const uint32_t *vbq, const uint32_t *r_limbs,
+                         const uint32_t *w_in, const uint32_t *ctr, uint32_t *take, const uint32_t *list,
+                         uint32_t *scratch, uint32_t *acc, uint32_t *uses, uint32_t promote, uint32_t *promo);
+__global__ void k_vb_fin(uint32_t n, uint8_t *status, const apoint_raw *gtab28, const int8_t *digits,
+                         const uint32_t *r_limbs, uint32_t *ctr, const uint32_t *list, const uint32_t *acc);
 __global__ void k_gtab(apoint_raw *tables28, jpoint_raw *scratch, uint32_t w);
+// kmap (nullable: every key has a comb): items of keys without one go to vb_list (count at
+// vb_cnt, one atomic per wave) for k_vb_mul / k_vb_fin
 __global__ void k_inv(uint32_t n, const uint32_t *dn, uint8_t *status, const uint32_t *key_slot, const uint8_t *key_ok,
-                      const uint32_t *r_limbs, const uint32_t *s_limbs, uint32_t *w_out, uint32_t *w_scratch);
+                      const uint32_t *r_limbs, const uint32_t *s_limbs, uint32_t *w_out, uint32_t *w_scratch,
+                      const uint32_t *kmap, uint32_t *vb_list, uint32_t *vb_cnt);
 __global__ void k_prep(uint32_t n, const uint32_t *dn, const uint8_t *status, const uint32_t *r_limbs, const uint32_t *w_in,
                        const uint8_t *digests, const uint32_t *dig_idx, int8_t *digits, uint32_t *redo);
 __global__ void k_point(uint32_t n, const uint32_t *dn, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot, const apoint_raw *gtab,
-                        const apoint_raw *ktab, const int8_t *digits, const uint32_t *r_limbs, uint32_t *redo);
+                        const apoint_raw *ktab, const int8_t *digits, const uint32_t *r_limbs, uint32_t *redo,
+                        const uint32_t *kmap);
 __global__ void k_point28(uint32_t n, const uint32_t *dn, uint32_t lanes_per_item, uint8_t *status, const uint32_t *key_slot,
                           const apoint_raw *gtab28, const apoint_raw *ktab28, const int8_t *digits,
-                          const uint32_t *r_limbs, uint32_t *redo);
+                          const uint32_t *r_limbs, uint32_t *redo, const uint32_t *kmap);
 #define INV_THREADS 128
 struct ShaJob {  // message = span0 || span1 || span2 (absolute device addresses)
   uint64_t p[3];

@@ -498,12 +498,17 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
     if (g.info.key_type == FGV_KEY_P256) memcpy(g.info.pubkey, p.c.pub, 64);
     regs.push_back(g);
   }
-  // one key-table build for every new P-256 key
+  // every new P-256 key in one registration: comb tables for the roles that sign often (peers,
+  // orderers, admins), the variable-base kernels for the others until they are promoted by use
+  std::vector<uint8_t> want;
   for (const Reg &g : regs)
-    if (g.info.key_type == FGV_KEY_P256) keys.insert(keys.end(), g.info.pubkey, g.info.pubkey + 64);
+    if (g.info.key_type == FGV_KEY_P256) {
+      keys.insert(keys.end(), g.info.pubkey, g.info.pubkey + 64);
+      want.push_back(fgv_roles_want_comb(g.info.roles) ? 1 : 0);
+    }
   std::vector<uint32_t> kslots(keys.size() / 64);
   if (!kslots.empty()) {
-    const int rc = fgv_keys_register_locked(c, keys.data(), kslots.size(), kslots.data());
+    const int rc = fgv_keys_register_locked(c, keys.data(), kslots.size(), kslots.data(), want.data());
     if (rc) return rc;
   }
   size_t kq = 0, nreg = 0;

@@ -1,21 +1,26 @@
 // p256_kernels.hip -- ECDSA-P256 batch verification for gfx950.
 //
-// Pipeline per batch (one HIP stream, three launches):
-//   k_keytab  (per NEW public key, cached across batches) -- fixed-base comb table
-//             T_Q[w][k-1] = k * 2^(8w) * Q, w < 33, k = 1..128, affine Montgomery (270 KB/key),
-//             plus the same points in Montgomery-280 form for k_point28.
-//             The generator table T_G is the same kernel run once on G at init.
+// Per batch, on the context's streams (fgv_host.cpp launch_inv / launch_prep_point):
+//   k_keytab  (per NEW comb key, cached across batches) -- fixed-base comb table
+//             T_Q[w][k-1] = k * 2^(13w) * Q, 20 windows of 13 bits, k = 1..4096 (signed digits),
+//             affine Montgomery-280 (5.2 MB per key, fgv_kernels.h).  The generator comb T_G
+//             (12 windows of 22 bits, 1.61 GB) is built once per context by k_gtab.
+//   k_keyprep (per NEW key id) -- on-curve check, coordinates for the variable-base kernel.
 //   k_inv     (PREP_B items per lane) -- range checks, w = s^-1 mod n with a per-lane
 //             batched (Montgomery-trick) inversion; independent of the digests, so it runs
 //             concurrently with the SHA-256 jobs of a block batch (second stream).
-//   k_prep    (per item) -- u1 = e*w, u2 = r*w, signed 8-bit recoding into 33 digits each.
-//   k_point   (L lanes per item, L chosen per batch) -- R = sum_w T_G[w][d1_w] + T_Q[w][d2_w]: <= 66
-//             complete mixed additions and NO doublings, split over the lanes of a group
-//             (lane j sums windows j, j+L, ...), then a log2(L)-level butterfly of complete
-//             Jacobian additions across the group (cross-lane shuffles); T_G (L2-resident)
-//             and T_Q gathered from L2 / HBM; x_R mod n == r checked projectively
-//             (X == r*Z^2 or (r+n)*Z^2).  The split cuts the per-item latency ~L-fold, which
-//             is what bounds block-sized batches (tens of thousands of verifies).
+//   k_prep    (per item) -- u1 = e*w, u2 = r*w; signed recoding into 12 generator digits
+//             (22-bit) and 20 key digits (13-bit).
+//   k_point28 (L lanes per item, L chosen per batch) -- R = sum_w T_G[w][d1_w] + T_Q[w][d2_w]: 32
+//             mixed additions and NO doublings (radix 2^28, incomplete formulas), split over the
+//             lanes of a group, then a log2(L)-level butterfly across the group; x_R mod n == r
+//             checked projectively.  k_point (exact radix-2^32 arithmetic, complete formulas)
+//             finishes the items whose sum hit an exceptional addition.
+//   keys without a comb (kmap[id] == KEY_NONE; k_inv lists their items):
+//   k_vb_mul  (one lane per listed item, beside the hashes: u2 = r * s^-1 needs no digest) --
+//             u2 * Q by 4-bit fixed windows over a per-lane table 1Q..15Q: 256 doublings and <= 64
+//             additions, exact formulas;
+//   k_vb_fin  (after k_prep) -- + u1 * G from the generator comb (12 terms), x_R check.
 //
 // Semantics restated: Go 1.21.9 crypto/ecdsa verifyNISTEC (SEC 1 v2 s4.1.4) behind
 // fabric-lib-go bccsp/sw/ecdsa.go:41-57.  Exceptional additions (P == Q, P == -Q, inf)
@@ -95,10 +100,11 @@ FGV_DEV void load_fe(fe &a, const uint32_t *src) {
 }
 
 // ---------------------------------------------------------------- k_keytab
-// T_Q[w][k-1] = k * 2^(10w) * Q, w < 26, k = 1..512.  KT_THREADS_PER_KEY threads per key, thread
-// (w, chunk) builds entries k0..k0+31 of window w: B = 2^(10w) Q by doublings, P = k0 * B by
+// T_Q[w][k-1] = k * 2^(13w) * Q, w < NWIN, k = 1..TAB_K.  KT_THREADS_PER_KEY threads per key, thread
+// (w, chunk) builds entries k0..k0+31 of window w: B = 2^(13w) Q by doublings, P = k0 * B by
 // double-and-add, then P += B, one Montgomery-trick inversion per chunk (complete formulas:
-// pt_add routes P == B to a doubling).  Both Montgomery forms (k_point / k_point28).
+// pt_add routes P == B to a doubling).  Montgomery-280 form (k_point28; k_point converts an entry
+// when it reads it).  key_ok (nullable): the key's on-curve bit at its slot.
 // qxy: [nkeys][16] plain little-endian limbs (x then y); scratch: [nkeys][KT_ENTRIES] jpoint_raw.
 __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
                                                const uint32_t *__restrict__ slots,
@@ -120,7 +126,7 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
   }
   const bool ok = on_curve(x, y, xm, ym);
   const uint32_t slot = slots[kid];
-  if (r == 0) key_ok[slot] = ok ? 1 : 0;
+  if (r == 0 && key_ok) key_ok[slot] = ok ? 1 : 0;
   if (!ok) return;
   jpoint b;
   b.x = xm;
@@ -181,11 +187,11 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
 }
 
 // ---------------------------------------------------------------- k_gtab
-// Generator comb table T_G[w][k-1] = k * 2^(16w) * G, w < 16, k = 1..32768, plus T_G[16][0] =
-// 2^256 * G (the carry window).  Thread t builds GT_CHUNK consecutive entries k0..k0+31 of one
-// window: B = 2^(16w) G by doublings, P = k0 * B by double-and-add, then P += B, and one
-// Montgomery-trick inversion for the chunk's Z's (complete formulas throughout: pt_add routes
-// P == B to a doubling).  Both the Montgomery-2^256 (k_point) and 2^280 (k_point28) forms.
+// Generator comb table T_G[w][k-1] = k * 2^(22w) * G, w < NGWIN, k = 1..GT_K (signed digits).
+// Thread t builds GT_CHUNK consecutive entries k0..k0+31 of one window: B = 2^(22w) G by
+// doublings, P = k0 * B by double-and-add, then P += B, and one Montgomery-trick inversion for
+// the chunk's Z's (complete formulas throughout: pt_add routes P == B to a doubling).
+// Montgomery-280 form (k_point converts an entry when it reads it).
 __constant__ static const uint32_t G_PLAIN[16] = {
     0xD898C296u, 0xF4A13945u, 0x2DEB33A0u, 0x77037D81u, 0x63A440F2u, 0xF8BCE6E5u, 0xE12C4247u, 0x6B17D1F2u,
     0x37BF51F5u, 0xCBB64068u, 0x6B315ECEu, 0x2BCE3357u, 0x7C0F9E16u, 0x8EE7EB4Au, 0xFE1A7F9Bu, 0x4FE342E2u};
@@ -259,8 +265,8 @@ __global__ __launch_bounds__(64) void k_gtab(apoint_raw *__restrict__ tables28, 
 //           (status 4/5), s -> Montgomery, prefix products, ONE inversion per lane by
 //           Bernstein-Yang divsteps (p256_modinv.h; ~6x shorter critical path than the Fermat
 //           chain), walk back -> w = s^-1 (Montgomery form) [8][n].
-//   k_prep  one item per lane: e = digest mod n, u1 = e*w, u2 = r*w, signed 6-bit recoding
-//           into (d1, d2) digit pairs [n][DIG_STRIDE].
+//   k_prep  one item per lane: e = digest mod n, u1 = e*w, u2 = r*w, signed recoding into
+//           the comb digits [n][DIG_STRIDE] (u2 itself for a key without a comb).
 // R^3 mod n: maps the plain inverse of a Montgomery representative back to Montgomery form
 // (sn_mul(X^-1, R^3) = (A*R)^-1 * R^2 = A^-1 * R)
 __constant__ static const uint32_t R3N[8] = {0x0b65a624u, 0xac8ebec9u, 0x0c0555c9u, 0x111f28aeu,
@@ -273,7 +279,9 @@ __global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, const uint32_t 
                                                      const uint32_t *__restrict__ r_limbs,
                                                      const uint32_t *__restrict__ s_limbs,
                                                      uint32_t *__restrict__ w_out,
-                                                     uint32_t *__restrict__ w_scratch) {
+                                                     uint32_t *__restrict__ w_scratch,
+                                                     const uint32_t *__restrict__ kmap,
+                                                     uint32_t *__restrict__ vb_list, uint32_t *__restrict__ vb_cnt) {
   // latency-critical: it runs beside the SHA-256 jobs (second stream); win VALU arbitration
   __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
@@ -317,6 +325,17 @@ __global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, const uint32_t 
       live |= 1u << b;
       sn_mul(acc, acc, sm);
     }
+    if (kmap) {  // items of keys without a comb: the variable-base list (one atomic per wave)
+      const bool vb = use && kmap[key_slot[i]] == KEY_NONE;
+      const uint64_t m = __ballot(vb);
+      if (m) {
+        const uint32_t ln = __lane_id(), lead = (uint32_t)__builtin_ctzll(m);
+        uint32_t b0 = 0;
+        if (ln == lead) b0 = atomicAdd(vb_cnt, (uint32_t)__popcll(m));
+        b0 = (uint32_t)__shfl((int)b0, (int)lead);
+        if (vb) vb_list[b0 + (uint32_t)__popcll(m & ((1ull << ln) - 1ull))] = i;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 8; k++) w_scratch[((size_t)b * 8 + k) * nl + lane] = acc[k];
   }
@@ -352,7 +371,8 @@ __global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, const uint32_t 
 
 // in:  status, r limbs, w = s^-1 (Montgomery) from k_inv, digests [*][32] big-endian, item i
 //      using digest dig_idx[i] (or i when dig_idx is null).
-// out: digits [n][DIG_STRIDE]: u1 digits (int16 x NGWIN) at 0, u2 digits (int16 x NWIN) at DIG_Q_OFF.
+// out: digits [n][DIG_STRIDE]: u1 digits (int32 x NGWIN) at 0, u2 digits (int16 x NWIN) at DIG_Q_OFF
+//      (items of keys without a comb use the generator digits only: k_vb_fin).
 __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint32_t *__restrict__ dn,
                                               const uint8_t *__restrict__ status,
                                               const uint32_t *__restrict__ r_limbs,
@@ -421,7 +441,8 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint32_t *__rest
 }
 
 // ---------------------------------------------------------------- k_point
-// grid-stride over items; T_G (270 KB) and T_Q are gathered from L2 / HBM (64 B per term).
+// The exact fallback of k_point28: the same comb terms with complete formulas in radix-2^32
+// Montgomery arithmetic; T_G and T_Q entries gathered from HBM (64 B per term).
 
 FGV_DEV void shfl_fe(fe &r, const fe &a, int src_lane) {
 #pragma unroll
@@ -450,7 +471,8 @@ FGV_DEV bool next_chunk(uint32_t *counter, uint32_t &chunk, uint32_t waves, uint
 __global__ __launch_bounds__(POINT_THREADS, 2) void k_point(
     uint32_t n, const uint32_t *__restrict__ dn, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
     const apoint_raw *__restrict__ gtab, const apoint_raw *__restrict__ ktab,
-    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo) {
+    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo,
+    const uint32_t *__restrict__ kmap) {
   // after k_point28: only the items it left pending (exceptional additions) remain
   if (redo && *redo == 0u) return;
   __builtin_amdgcn_s_setprio(3);
@@ -468,7 +490,9 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point(
   while (next_chunk(ctr, chunk, waves, gpw, cnt)) {
     const uint32_t i = chunk * gpw + g;
     if (i >= cnt || status[i] != ST_PENDING) continue;
-    const apoint_raw *qt = ktab + (size_t)key_slot[i] * KT_ENTRIES;
+    const uint32_t cs = kmap[key_slot[i]];  // the key id's comb slot
+    if (cs == KEY_NONE) continue;  // (k_point_vb's item)
+    const apoint_raw *qt = ktab + (size_t)cs * KT_ENTRIES;
     const int8_t *dg = digits + (size_t)i * DIG_STRIDE;
     jpoint acc;
     fe_set_zero(acc.x);
@@ -632,7 +656,8 @@ FGV_DEV void f28_to_mont(f28 &r, const uint32_t w[8]) {
 __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
     uint32_t n, const uint32_t *__restrict__ dn, uint32_t L, uint8_t *__restrict__ status, const uint32_t *__restrict__ key_slot,
     const apoint_raw *__restrict__ gtab28, const apoint_raw *__restrict__ ktab28,
-    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo) {
+    const int8_t *__restrict__ digits, const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ redo,
+    const uint32_t *__restrict__ kmap) {
   __builtin_amdgcn_s_setprio(3);  // the verify chain; a next batch's front half may run beside it
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t gpw = 64u / L;
@@ -645,7 +670,9 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
   while (next_chunk(redo + 1, chunk, waves, gpw, cnt)) {
     const uint32_t i = chunk * gpw + g;
     if (i >= cnt || status[i] != ST_PENDING) continue;
-    const apoint_raw *qt = ktab28 + (size_t)key_slot[i] * KT_ENTRIES;
+    const uint32_t cs = kmap[key_slot[i]];  // the key id's comb slot
+    if (cs == KEY_NONE) continue;  // (k_point_vb's item)
+    const apoint_raw *qt = ktab28 + (size_t)cs * KT_ENTRIES;
     const int8_t *dg = digits + (size_t)i * DIG_STRIDE;
     jp28 acc;
     bool inf = true;
@@ -748,5 +775,210 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
       }
     }
     status[i] = st;
+  }
+}
+
+// ---------------------------------------------------------------- keys without a comb
+// k_keyprep: new key ids -> on-curve bit (k_inv reports 5 for a key off the curve, before the
+// range checks, as ecdsa.Verify does) and the Montgomery coordinates the variable-base kernel reads.
+// qxy: [nkeys][16] plain little-endian limbs (x then y).
+__global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy, const uint32_t *__restrict__ ids,
+                                                uint32_t nkeys, uint32_t *__restrict__ vbq,
+                                                uint8_t *__restrict__ key_ok) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nkeys) return;
+  fe x, y, xm, ym;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    x.v[i] = qxy[k * 16 + i];
+    y.v[i] = qxy[k * 16 + 8 + i];
+  }
+  const bool ok = on_curve(x, y, xm, ym);
+  const uint32_t id = ids[k];
+  key_ok[id] = ok ? 1 : 0;
+  if (!ok) fe_set_zero(xm), fe_set_zero(ym);
+  store_fe(vbq + (size_t)id * 16, xm);
+  store_fe(vbq + (size_t)id * 16 + 8, ym);
+}
+// ids whose comb tables k_keytab has just built (stream order) now take the comb path
+__global__ __launch_bounds__(64) void k_kmap_set(const uint32_t *__restrict__ ids, const uint32_t *__restrict__ slots,
+                                                 uint32_t n, uint32_t *__restrict__ kmap) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) kmap[ids[k]] = slots[k];
+}
+
+// one item per lane: a wave takes 64 consecutive list entries per atomic from `take`; every lane
+// of the wave runs the same number of rounds (the count is read once)
+FGV_DEV bool vb_next(uint32_t *take, uint32_t cnt, uint32_t &j) {
+  uint32_t b = 0;
+  if (__lane_id() == 0) b = atomicAdd(take, 64u);
+  b = __builtin_amdgcn_readfirstlane(b);
+  j = b + __lane_id();
+  return b < cnt;
+}
+FGV_DEV void store_jp(uint32_t *d, const jpoint &p) {
+  store_fe(d, p.x);
+  store_fe(d + 8, p.y);
+  store_fe(d + 16, p.z);
+}
+FGV_DEV void load_jp(jpoint &p, const uint32_t *s) {
+  load_fe(p.x, s);
+  load_fe(p.y, s + 8);
+  load_fe(p.z, s + 16);
+}
+
+// k_vb_mul: acc[j] = u2 * Q for list entry j (item i = list[j], key id key_slot[i]), u2 = r * s^-1
+// (plain; k_inv's w is s^-1 in Montgomery form) -- needs no digest, so it runs beside the hashes.
+// Left-to-right 4-bit fixed windows over the lane's table T[d-1] = d * Q (d = 1..15, Jacobian, in
+// the lane's scratch row; each entry of the next window is loaded one window ahead): 256
+// doublings, <= 64 additions, complete formulas (pt_dbl / pt_add_inl / pt_madd), so the result is
+// exact for every input.  Cost per verify ~ 256 x (3M + 5S) + 64 x (12M + 4S) + 14 x (8M + 3S):
+// ~9x a comb verify, one serial chain per item.  uses[id] counts the key's
+// variable-base verifies; the one that reaches `promote` queues the id (promo[0] count, ids from
+// promo[2]) for a comb build by the host; promo[1] = the batch's variable-base items.
+__global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_t *__restrict__ key_slot,
+                                                      const uint32_t *__restrict__ vbq,
+                                                      const uint32_t *__restrict__ r_limbs,
+                                                      const uint32_t *__restrict__ w_in,
+                                                      const uint32_t *__restrict__ ctr, uint32_t *__restrict__ take,
+                                                      const uint32_t *__restrict__ list,
+                                                      uint32_t *__restrict__ scratch, uint32_t *__restrict__ acc,
+                                                      uint32_t *__restrict__ uses, uint32_t promote,
+                                                      uint32_t *__restrict__ promo) {
+  __builtin_amdgcn_s_setprio(2);
+  const uint32_t cnt = ctr[RD_VB_CNT];
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&promo[1], cnt);  // (statistics: fgv_key_stats)
+  if (cnt == 0) return;
+  uint32_t *tab = scratch + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * (VB_TAB * VB_TAB_WORDS);
+  uint32_t j;
+  while (vb_next(take, cnt, j)) {
+    if (j >= cnt) continue;
+    const uint32_t i = list[j];
+    const uint32_t id = key_slot[i];
+    uint32_t r[8], w[8], u2[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      r[k] = r_limbs[(size_t)k * n + i];
+      w[k] = w_in[(size_t)k * n + i];
+    }
+    sn_mul(u2, r, w);
+    apoint q;
+    load_fe(q.x, vbq + (size_t)id * 16);
+    load_fe(q.y, vbq + (size_t)id * 16 + 8);
+    {  // T[0] = Q, T[d-1] = T[d-2] + Q (pt_madd routes 2Q to a doubling)
+      jpoint t;
+      t.x = q.x;
+      t.y = q.y;
+      fe_set_one(t.z);
+      store_jp(tab, t);
+#pragma unroll 1
+      for (int d = 2; d <= VB_TAB; d++) {
+        jpoint t2 = t;
+        pt_madd(t, t2, q);
+        store_jp(tab + (d - 1) * VB_TAB_WORDS, t);
+      }
+    }
+    jpoint a;
+    fe_set_zero(a.x);
+    fe_set_zero(a.y);
+    fe_set_zero(a.z);
+    // windows from the top: the top nibble of u2 is shifted out each round
+    uint32_t d = u2[7] >> 28;
+    jpoint e;
+    if (d) load_jp(e, tab + (d - 1) * VB_TAB_WORDS);
+#pragma unroll 1
+    for (int win = 63; win >= 0; win--) {
+#pragma unroll
+      for (int k = 7; k > 0; k--) u2[k] = (u2[k] << 4) | (u2[k - 1] >> 28);
+      u2[0] <<= 4;
+      const uint32_t dn = u2[7] >> 28;  // the next window's digit (0 after the last)
+      jpoint en;
+      if (win > 0 && dn) load_jp(en, tab + (dn - 1) * VB_TAB_WORDS);  // (in flight during the doublings)
+      if (win < 63) {
+#pragma unroll 1
+        for (int k = 0; k < 4; k++) {
+          jpoint t2 = a;
+          pt_dbl(a, t2);
+        }
+      }
+      if (d) {
+        jpoint t2 = a;
+        pt_add_inl(a, t2, e);
+      }
+      d = dn;
+      e = en;
+    }
+    store_jp(acc + (size_t)j * VB_TAB_WORDS, a);
+    const uint32_t u = atomicAdd(&uses[id], 1u);
+    if (u + 1u == promote) {
+      const uint32_t s = atomicAdd(&promo[0], 1u);
+      if (s < VB_PROMO_CAP) atomicExch(&promo[2 + s], id);
+    }
+  }
+}
+
+// k_vb_fin: after k_prep -- acc[j] + sum of the 12 generator comb terms of u1 (k_prep's digits),
+// then the projective x_R check of k_point -> status[list[j]].  The last workgroup to finish
+// zeroes the list counters for the next batch (atomics only: no fence, no extra launch).
+__global__ __launch_bounds__(256) void k_vb_fin(uint32_t n, uint8_t *__restrict__ status,
+                                                const apoint_raw *__restrict__ gtab28,
+                                                const int8_t *__restrict__ digits,
+                                                const uint32_t *__restrict__ r_limbs, uint32_t *__restrict__ ctr,
+                                                const uint32_t *__restrict__ list, const uint32_t *__restrict__ acc) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t cnt = ctr[RD_VB_CNT];
+  uint32_t j;
+  while (cnt && vb_next(ctr + RD_VB_FIN, cnt, j)) {
+    if (j >= cnt) continue;
+    const uint32_t i = list[j];
+    jpoint a;
+    load_jp(a, acc + (size_t)j * VB_TAB_WORDS);
+    const int32_t *g = reinterpret_cast<const int32_t *>(digits + (size_t)i * DIG_STRIDE);
+    fe c232;
+    fe_load_c(c232, C232_32);
+#pragma unroll 1
+    for (int win = 0; win < NGWIN; win++) {
+      const int dd = g[win];
+      if (dd == 0) continue;
+      const apoint_raw *e = gtab28 + (size_t)win * GT_K + ((dd < 0 ? -dd : dd) - 1);
+      apoint p;
+      load_fe(p.x, e->x);
+      load_fe(p.y, e->y);
+      fe_mul(p.x, p.x, c232);  // Montgomery-280 -> Montgomery-256 (as k_point)
+      fe_mul(p.y, p.y, c232);
+      if (dd < 0) fe_neg(p.y, p.y);
+      jpoint t2 = a;
+      pt_madd(a, t2, p);
+    }
+    uint8_t st = 1;
+    if (!fe_is_zero(a.z)) {
+      fe rr, rm, z2, lhs;
+#pragma unroll
+      for (int k = 0; k < 8; k++) rr.v[k] = r_limbs[(size_t)k * n + i];
+      fe_sqr(z2, a.z);
+      fe_to_mont(rm, rr);
+      fe_mul(lhs, rm, z2);
+      if (fe_eq(lhs, a.x)) {
+        st = 0;
+      } else {
+        uint32_t c = 0;
+        fe rn;
+#pragma unroll
+        for (int k = 0; k < 8; k++) rn.v[k] = addc(rr.v[k], N_LIMBS[k], c, &c);
+        if (c == 0u && lt_p(rn.v)) {
+          fe_to_mont(rm, rn);
+          fe_mul(lhs, rm, z2);
+          if (fe_eq(lhs, a.x)) st = 0;
+        }
+      }
+    }
+    status[i] = st;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(ctr + RD_VB_DONE, 1u) + 1u == gridDim.x) {
+    atomicExch(ctr + RD_VB_CNT, 0u);
+    atomicExch(ctr + RD_VB_MUL, 0u);
+    atomicExch(ctr + RD_VB_FIN, 0u);
+    atomicExch(ctr + RD_VB_DONE, 0u);
   }
 }

@@ -32,6 +32,11 @@ class Identity:
     ous: Optional[list] = None
 
 
+def roles_want_comb(roles):
+    """fgv_roles_want_comb (fgv_internal.h): unknown roles, or ADMIN / PEER / ORDERER"""
+    return roles is None or bool(roles & ((1 << 1) | (1 << 3) | (1 << 4)))
+
+
 def _as_identity(entry):
     """(serialized, Identity-like) or the round-1 (serialized, mspid, pub | None, valid, id_digest)"""
     if len(entry) == 2:
@@ -53,10 +58,11 @@ def setup_channel(engine: Engine, channel: str, identities, chaincodes, committe
     for m in msps:
         engine.msp_declare(m)
     identities = [_as_identity(e) for e in identities]
-    # all public keys first, in one fgv_keys_register call: their comb tables are then built by
-    # batched k_keytab launches (up to KT_BUILD_KEYS keys each) instead of one launch per key,
-    # and every registration below finds its key cached (same slots, first-seen order)
-    pubs = [i.pub for _s, i in identities if i.key == "p256" and i.pub is not None]
+    # the public keys that get comb tables (fgv_roles_want_comb: peers, orderers, admins, unknown
+    # roles) first, in one fgv_keys_register call: their tables are then built by batched k_keytab
+    # launches (up to KT_BUILD_KEYS keys each) instead of one launch per key.  Client keys start
+    # on the variable-base kernels and are promoted by use.
+    pubs = [i.pub for _s, i in identities if i.key == "p256" and i.pub is not None and roles_want_comb(i.roles)]
     if pubs:
         engine.keys_register(np.frombuffer(b"".join(bytes(p) for p in pubs), dtype=np.uint8))
     for ser, i in identities:

@@ -43,10 +43,16 @@ typedef struct fgv_ctx fgv_ctx;
 
 typedef struct fgv_config {
   int device;            /* HIP device ordinal (one process per GPU)                 */
-  uint32_t key_slots;    /* capacity of the device public-key table cache (0 = 2048; 5.2 MB of HBM
-                            per slot: the key comb of one key, 13-bit windows)                  */
+  uint32_t key_slots;    /* comb-table cache: keys verified by the fixed-base key comb (0 = 2048;
+                            5.2 MB of HBM per slot, 13-bit windows).  A key without a slot is
+                            verified by the variable-base kernels instead -- same results, ~9x
+                            the device work per verify -- so a full cache never fails a batch    */
   uint32_t host_threads; /* host worker threads for parsing / policy fold (0 = min(24,
                             the process's CPU share: affinity mask, OMP_NUM_THREADS)) */
+  uint32_t key_ids;      /* distinct P-256 keys the context holds at once (0 = 1M; 77 B of HBM
+                            each): registered keys for good, BCCSP-path keys until the id space is
+                            flushed; only a single call naming more distinct keys than that
+                            returns FGV_ENOMEM                                                    */
 } fgv_config;
 
 /* Replaces factory.GetDefault() / sw.NewDefaultSecurityLevel* for the verify + hash
@@ -68,7 +74,8 @@ int fgv_last_counts(fgv_ctx *ctx, uint64_t *sha_jobs, uint64_t *sha_blocks, uint
  * kernel's own stream): out[0] k_bd_sha_payload, [1] k_bd_parse, [2] k_bd_sha, [3] k_bd_ident +
  * k_bd_count, [4] k_bd_emit, [5] k_der + k_inv, [6] k_prep, [7] k_point28 (+ k_point hand-overs),
  * [8] k_bd_fold, [9] the batch (first kernel to last); out[10] = SHA-256 compressions of the
- * payload hashes (k_bd_sha_payload's work).  n entries are written. */
+ * payload hashes (k_bd_sha_payload's work); out[11] = host ms the pipelined call spent enqueueing
+ * the next batch's front half (its framing walk's join included).  n entries are written. */
 int fgv_last_kernel_times(fgv_ctx *ctx, double *out, size_t n);
 // Diagnostics: verifies of the last call that the fast point kernel (radix 2^28, incomplete
 // formulas) handed to the exact kernel because an exceptional addition occurred (P = +-Q).
@@ -100,12 +107,22 @@ int fgv_p256_verify_msgs(fgv_ctx *ctx, const uint8_t *keys, const uint8_t *msg_b
 
 /* ------------------------------------------- key registry + HBM-resident batches */
 
-/* Register public keys (n*64 bytes X||Y) in the device key-table cache and return their
- * slots.  The analogue of the MSP identity cache (msp/cache/cache.go:65-83): identities are
- * deserialized once, their key tables built once, and every later verify is a slot lookup.
- * Returns FGV_ENOMEM when the cache is full (call fgv_keys_reset and re-register). */
+/* Register public keys (n*64 bytes X||Y) with the context and return their key ids (the "slots"
+ * fgv_p256_verify_msgs_dev takes).  The analogue of the MSP identity cache (msp/cache/cache.go:
+ * 65-83): identities are deserialized once, and every later verify is an id lookup.
+ * Key tiers: a key registered here takes a comb-table slot (the fast fixed-base
+ * comb, built once per key) while one is free; otherwise -- and for identities registered with
+ * only a CLIENT role, whose keys sign rarely -- it is verified by the variable-base kernels from
+ * its coordinates alone, and promoted to a comb slot once it has signed FGV_PROMOTE_USES (64)
+ * verifies.  The comb cache filling up changes speed, never results; FGV_ENOMEM only when the
+ * id space (fgv_config.key_ids) is exhausted. */
 int fgv_keys_register(fgv_ctx *ctx, const uint8_t *keys, size_t n, uint32_t *slots);
 int fgv_keys_reset(fgv_ctx *ctx);
+/* Key-tier statistics: ids in use, ids with a comb table, ids on the variable-base kernels, keys
+ * promoted to a comb since fgv_init, and verifies of the last call that ran on the variable-base
+ * kernels (reads one counter back from the device). */
+int fgv_key_stats(fgv_ctx *ctx, uint64_t *ids, uint64_t *comb, uint64_t *vb, uint64_t *promoted,
+                  uint64_t *vb_verifies_last);
 
 /* identity.Verify over a batch already resident in device memory: every pointer below is a
  * DEVICE pointer (e.g. hipMalloc or a torch tensor's data_ptr on this device).  Message and

@@ -1,9 +1,84 @@
-set -e
-mkdir -p gpurun_out/r1s6
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r1s6/gpu_tests.log 2>&1
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r1s6/smoke.log 2>&1
-timeout -k 10 240 python bench.py > gpurun_out/r1s6/bench_block.json 2> gpurun_out/r1s6/bench_block.err
-timeout -k 10 240 python bench.py --workload sig > gpurun_out/r1s6/bench_sig.json 2> gpurun_out/r1s6/bench_sig.err
-timeout -k 10 240 python bench.py --workload mvcc > gpurun_out/r1s6/bench_mvcc.json 2> gpurun_out/r1s6/bench_mvcc.err
-timeout -k 10 300 python bench.py --workload c5 > gpurun_out/r1s6/bench_c5.json 2> gpurun_out/r1s6/bench_c5.err
-echo all-done
+#!/bin/bash
+# One GPU-box run (via gpurun) of named steps, each under its own time limit, stopping at the
+# first failure:
+#   bash tools/gpu_round.sh <out-name> <step> [<step> ...]
+# Steps:
+#   tests            the full GPU suite (pytest -m gpu)
+#   tests:<expr>     GPU tests matching a -k expression
+#   smoke            __graft_entry__.smoke()
+#   bench            the default bench (C2 headline line)
+#   lean<N>          N lean C2 runs (40 steps, no CPU baseline / PCIe / latency passes)
+#   churn            C2 with every creator a distinct identity (the cold-key path)
+#   mvcc | sig | c5 | sbe   the other workloads (tools/bench_sbe.py for sbe)
+#   trace            rocprofv3 --kernel-trace --stats of a C2 run
+#   profile          tools/profile_round.sh (stats + PMC passes of every workload)
+#   py:<file>        python <file> (a micro-benchmark or check under tools/)
+# Output: gpurun_out/<out-name>/.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+[ $# -ge 2 ] || { echo "usage: $0 <out-name> <step>..."; exit 2; }
+O=gpurun_out/$1
+shift
+mkdir -p "$O"
+show() { python3 -c "import json,sys; d=json.load(open('$1')); print('$2', *[d.get(k) for k in sys.argv[1:]])" "${@:3}"; }
+for step in "$@"; do
+  case "$step" in
+    tests)
+      timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 \
+        || { echo tests failed; tail -60 $O/tests.log; exit 1; }
+      tail -1 $O/tests.log ;;
+    tests:*)
+      k=${step#tests:}
+      timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests -k "$k" > $O/tests_k.log 2>&1 \
+        || { echo tests failed; tail -60 $O/tests_k.log; exit 1; }
+      tail -1 $O/tests_k.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 \
+        || { echo smoke failed; tail -30 $O/smoke.log; exit 1; }
+      tail -1 $O/smoke.log ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail -20 $O/bench.err; exit 1; }
+      show $O/bench.json bench value ms_per_step parity_vs_labels latency_1block_ms
+      python3 -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print('roofline', r['kernel'], r['frac'], r.get('frac_profiled'), 'pcie', d['pcie_inclusive']['ms_per_step'], 'cpu', d['cpu_baseline']['value'])" ;;
+    lean*)
+      n=${step#lean}; n=${n:-1}
+      for rep in $(seq 1 $n); do
+        timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --cpu-threads 0 --no-pcie --no-latency > $O/lean_$rep.json 2> $O/lean_$rep.err \
+          || { echo lean failed; tail -20 $O/lean_$rep.err; exit 1; }
+        show $O/lean_$rep.json "lean $rep" value ms_per_step parity_vs_labels
+      done ;;
+    churn)
+      timeout -k 10 400 python -u bench.py --clients 16000 --steps 20 --warmup 3 --cpu-threads 0 --no-pcie > $O/churn.json 2> $O/churn.err \
+        || { echo churn failed; tail -20 $O/churn.err; exit 1; }
+      show $O/churn.json churn value ms_per_step parity_vs_labels latency_1block_ms ;;
+    mvcc)
+      timeout -k 10 300 python -u bench.py --workload mvcc --steps 100 --warmup 5 > $O/mvcc.json 2> $O/mvcc.err \
+        || { echo mvcc failed; tail -20 $O/mvcc.err; exit 1; }
+      show $O/mvcc.json mvcc value ms_per_step parity_vs_labels stage_ms single_block_calls ;;
+    sig)
+      timeout -k 10 300 python -u bench.py --workload sig --steps 10 --warmup 2 > $O/sig.json 2> $O/sig.err \
+        || { echo sig failed; tail -20 $O/sig.err; exit 1; }
+      show $O/sig.json sig value ms_per_step parity_vs_labels ;;
+    c5)
+      timeout -k 10 400 python -u bench.py --workload c5 --steps 10 --warmup 2 > $O/c5.json 2> $O/c5.err \
+        || { echo c5 failed; tail -20 $O/c5.err; exit 1; }
+      show $O/c5.json c5 value ms_per_step parity_vs_labels host_ms ;;
+    sbe)
+      timeout -k 10 400 python -u tools/bench_sbe.py > $O/sbe.json 2> $O/sbe.err || { echo bench_sbe failed; tail -20 $O/sbe.err; exit 1; }
+      tail -c 400 $O/sbe.json; echo ;;
+    trace)
+      timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d $O/st -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $O/st.json 2> $O/st.err \
+        || { echo trace failed; tail -20 $O/st.err; exit 1; }
+      echo trace ok ;;
+    profile)
+      PROF_OUT=$O/prof bash tools/profile_round.sh || { echo profile failed; exit 1; } ;;
+    py:*)
+      f=${step#py:}
+      timeout -k 10 300 python -u $f > $O/$(basename $f).out 2>&1 || { echo "$f failed"; tail -30 $O/$(basename $f).out; exit 1; }
+      tail -20 $O/$(basename $f).out ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo done
