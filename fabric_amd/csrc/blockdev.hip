@@ -146,19 +146,21 @@ struct VCollHashed {
 // lane-minor): in private memory they were ~2 KB of scratch per lane -- HBM-backed reads in the
 // middle of a walk that is one long chain of dependent reads.
 #define BD_MAX_COLL 8
-#define PL 64u  // lanes per k_bd_parse workgroup
-struct ParseLds {
-  S ns[BD_MAX_NS][PL], rwset[BD_MAX_NS][PL], msg[BD_MAX_NS][PL];  // TxReadWriteSet namespaces
-  S wr[BD_MAX_POL][PL];   // written namespaces + the invoked chaincode, sorted
-  S coll[BD_MAX_COLL][PL];  // a namespace's collection hashed rwsets / collection names
-  uint8_t cw[BD_MAX_NS][PL];
-  int16_t pol[BD_MAX_POL][PL];
+#define PL 64u  // lanes per k_bd_parse workgroup (global walk)
+template <uint32_t W>  // W walking lanes per workgroup
+struct ParseLdsT {
+  S ns[BD_MAX_NS][W], rwset[BD_MAX_NS][W], msg[BD_MAX_NS][W];  // TxReadWriteSet namespaces
+  S wr[BD_MAX_POL][W];   // written namespaces + the invoked chaincode, sorted
+  S coll[BD_MAX_COLL][W];  // a namespace's collection hashed rwsets / collection names
+  uint8_t cw[BD_MAX_NS][W];
+  int16_t pol[BD_MAX_POL][W];
 };
 // NsReadWriteSet: namespace, rwset bytes, collection hashed rwsets (kept for the second pass)
 struct VNsRwSet {
   S ns{nullptr, 0}, rwset{nullptr, 0};
   uint32_t ncoll = 0;
-  S *coll_hashed;  // LDS, stride PL
+  S *coll_hashed;  // LDS, stride `stride`
+  uint32_t stride;
   DEV Kind kind(uint32_t n) { return n == 1 ? K_STRING : n == 2 ? K_BYTES : n == 3 ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
   DEV bool on_len(uint32_t n, S s, bool &ovf) {
@@ -167,13 +169,14 @@ struct VNsRwSet {
     VCollHashed c;
     if (!decode(s, c, ovf)) return false;
     if (ncoll == BD_MAX_COLL) { ovf = true; return false; }
-    coll_hashed[PL * ncoll++] = c.hashed;
+    coll_hashed[stride * ncoll++] = c.hashed;
     return true;
   }
 };
+template <uint32_t W>
 struct VTxRwSet {
   uint32_t nns = 0;
-  ParseLds *L;
+  ParseLdsT<W> *L;
   uint32_t lane;
   // L->ns / rwset / msg (msg: the NsReadWriteSet, collections re-walked); L->cw bit0: a
   // collection has hashed writes, bit1: a collection failed to decode, bit2: a collection has
@@ -183,6 +186,7 @@ struct VTxRwSet {
   DEV bool on_len(uint32_t, S s, bool &ovf) {
     VNsRwSet r;
     r.coll_hashed = &L->coll[0][lane];
+    r.stride = W;
     if (!decode(s, r, ovf)) return false;
     if (nns == BD_MAX_NS) { ovf = true; return false; }
     L->ns[nns][lane] = r.ns;
@@ -202,7 +206,8 @@ struct VTxRwSet {
 };
 // the collections of one NsReadWriteSet with hashed writes, in order (their EPs)
 struct VNsCollNames {
-  S *names;  // LDS, stride PL
+  S *names;  // LDS, stride `stride`
+  uint32_t stride;
   uint32_t n = 0;
   DEV Kind kind(uint32_t f) { return f == 3 ? K_REP_MSG : K_NONE; }
   DEV void on_varint(uint32_t, uint64_t) {}
@@ -213,7 +218,7 @@ struct VNsCollNames {
     if (!decode(c.hashed, h, ovf)) return false;
     if (!h.nwrites) return true;
     if (n == BD_MAX_COLL) { ovf = true; return false; }
-    names[PL * n++] = c.name;
+    names[stride * n++] = c.name;
     return true;
   }
 };
@@ -466,9 +471,10 @@ struct VCcActionPayloadChk {
 enum : uint8_t { X_OK = 0, X_FAIL = 1, X_PANIC = 2, X_UNKNOWN = 0xFF };
 // metadata writes of a TxReadWriteSet (rwset.FromProtoBytes: a decode error -> none); rw_ok:
 // the whole rwset decodes
-DEV bool rwset_md(S results, ParseLds &L, uint32_t lane, bool &ovf, bool &rw_ok) {
+template <uint32_t W>
+DEV bool rwset_md(S results, ParseLdsT<W> &L, uint32_t lane, bool &ovf, bool &rw_ok) {
   rw_ok = false;
-  VTxRwSet rw;
+  VTxRwSet<W> rw;
   rw.L = &L;
   rw.lane = lane;
   if (!decode(results, rw, ovf)) return false;
@@ -484,7 +490,8 @@ DEV bool rwset_md(S results, ParseLds &L, uint32_t lane, bool &ovf, bool &rw_ok)
 // extractDependenciesForTx (validator_keylevel.go:184-222) for a tx whose validation walk
 // stopped before its ChaincodeAction (fgv_block.cpp extract_walk); `results`: the rwset bytes
 // when X_OK
-DEV uint8_t extract_walk(S d, ParseLds &L, uint32_t lane, bool &md, S &results, bool &rw_ok, bool &ovf) {
+template <uint32_t W>
+DEV uint8_t extract_walk(S d, ParseLdsT<W> &L, uint32_t lane, bool &md, S &results, bool &rw_ok, bool &ovf) {
   md = false;
   rw_ok = false;
   VTwoBytes env;
@@ -514,21 +521,13 @@ DEV uint8_t extract_walk(S d, ParseLds &L, uint32_t lane, bool &md, S &results, 
 // batch's record table (k_bd_kl).  Without kl.on (a shard of a batch) such a tx sends the batch
 // to the host parser (flag 1).  Dependency-extraction failures and panics are recorded per block
 // (xhaz).
-__global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
-                                                 const uint64_t *__restrict__ bases, DevChannel ch,
-                                                 DevTx *__restrict__ out, uint32_t *__restrict__ flags,
-                                                 uint32_t *__restrict__ xhaz, KlDev kl, uint32_t touch) {
-  // front half: below the back half's verify chain (3), above k_bd_sha_payload (1)
-  __builtin_amdgcn_s_setprio(2);
-  __shared__ ParseLds L;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntx) return;  // (no barrier below: every lane works on its own LDS column)
-  const uint32_t *et = envtab + BD_ENV_WORDS * t;
-  const uint32_t blk = et[0];
-  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
-  const S d{base + et[1], et[2]};
-  if (touch) touch_lines(d.p, d.n);  // (A/B: FGV_PARSE_TOUCH)
+// One transaction t on lane `lane` (its LDS column of L): `base` maps block offsets to bytes --
+// the block in HBM, or a "virtual base" into the LDS copy of the envelope (k_bd_parse_lds), so the
+// recorded spans stay block-relative either way; d = the envelope.
+template <uint32_t W>
+DEV void parse_one(uint32_t t, uint32_t lane, uint32_t blk, ParseLdsT<W> &L, const uint8_t *base, S d,
+                   const DevChannel &ch, DevTx *__restrict__ out, uint32_t *__restrict__ flags,
+                   uint32_t *__restrict__ xhaz, const KlDev &kl) {
   DevTx &O = out[t];  // endorsements are written straight into it; the rest at the end
   struct {
     uint32_t blk;
@@ -626,7 +625,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
     if (!decode(prp.b, cca, ovf)) { R.disp = C_BAD_RESP; break; }
     xs = X_OK;  // (the dependency extraction decodes the same messages)
     results = cca.results;
-    VTxRwSet rw;
+    VTxRwSet<W> rw;
     rw.L = &L;
     rw.lane = lane;
     if (!decode(cca.results, rw, ovf)) { R.disp = C_BAD_RWSET; break; }
@@ -743,6 +742,7 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
       if (k >= 0 && (L.cw[k][lane] & 1)) {
         VNsCollNames cn;
         cn.names = &L.coll[0][lane];
+        cn.stride = W;
         if (!decode(L.msg[k][lane], cn, ovf)) break;
         for (uint32_t c = 0; c < cn.n; c++) {
           any = true;
@@ -807,6 +807,114 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
   O.nwr = R.nwr;
   O.kln = 0;
   O.results = rel(base, results);
+}
+
+// Global walk: one lane per transaction, the envelope's lines requested up front (touch).
+__global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *__restrict__ envtab,
+                                                 const uint64_t *__restrict__ bases, DevChannel ch,
+                                                 DevTx *__restrict__ out, uint32_t *__restrict__ flags,
+                                                 uint32_t *__restrict__ xhaz, KlDev kl, uint32_t touch) {
+  // front half: below the back half's verify chain (3), above k_bd_sha_payload (1)
+  __builtin_amdgcn_s_setprio(2);
+  __shared__ ParseLdsT<PL> L;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;  // (no barrier below: every lane works on its own LDS column)
+  const uint32_t *et = envtab + BD_ENV_WORDS * t;
+  const uint32_t blk = et[0];
+  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
+  const S d{base + et[1], et[2]};
+  if (touch) touch_lines(d.p, d.n);  // (A/B: FGV_PARSE_TOUCH)
+  parse_one<PL>(t, lane, blk, L, base, d, ch, out, flags, xhaz, kl);
+}
+
+// LDS-staged walk: one 64-lane workgroup per TPW transactions.  The wave first copies the
+// group's envelopes into LDS -- 16-byte loads of the aligned lines covering [off, off + len + 8)
+// (the walk's over-read contract), every line in flight at once -- then lane j walks transaction
+// j from LDS through a virtual base, so each of the walk's dependent loads is an LDS access
+// instead of a cache round trip (the global walk pays ~0.5-1 us per field).  An envelope larger
+// than CAP bytes is walked from global memory.
+template <uint32_t TPW, uint32_t CAP>
+__global__ __launch_bounds__(64) void k_bd_parse_lds(uint32_t ntx, const uint32_t *__restrict__ envtab,
+                                                     const uint64_t *__restrict__ bases, DevChannel ch,
+                                                     DevTx *__restrict__ out, uint32_t *__restrict__ flags,
+                                                     uint32_t *__restrict__ xhaz, KlDev kl) {
+  __builtin_amdgcn_s_setprio(2);
+  constexpr uint32_t C16 = CAP / 16;  // 16-byte lines per staged envelope
+  __shared__ ParseLdsT<TPW> L;
+  __shared__ uint4 env[TPW * C16];
+  __shared__ uint32_t pre[TPW + 1];
+  __shared__ uint64_t src[TPW];  // aligned source line of each staged envelope
+  const uint32_t lane = threadIdx.x, t0 = blockIdx.x * TPW;
+  uint32_t my = 0;
+  if (lane < TPW && t0 + lane < ntx) {
+    const uint32_t *et = envtab + BD_ENV_WORDS * (t0 + lane);
+    const uint64_t a = bases[et[0]] + et[1];
+    const uint64_t a0 = a & ~15ull, a1 = (a + et[2] + 8u + 15u) & ~15ull;
+    if (a1 - a0 <= CAP) {
+      my = (uint32_t)((a1 - a0) / 16u);
+      src[lane] = a0;
+    }
+  }
+  uint32_t v = my;  // inclusive prefix over the TPW lanes (wave scan)
+  for (uint32_t dd = 1; dd < TPW; dd <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)v, dd);
+    if (lane >= dd) v += o;
+  }
+  if (lane < TPW) pre[lane + 1] = v;
+  if (lane == 0) pre[0] = 0;
+  __syncthreads();
+  const uint32_t total = pre[TPW];
+  // 8 lines per lane per pass, all loads issued before the first LDS store
+  constexpr uint32_t U = 8;
+  for (uint32_t i0 = lane; i0 < total; i0 += 64 * U) {
+    uint4 val[U];
+    uint32_t dst[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t i = i0 + 64 * u;
+      dst[u] = 0xFFFFFFFFu;
+      if (i < total) {
+        uint32_t j = 0;  // the envelope of line i: pre[j] <= i < pre[j + 1]
+#pragma unroll
+        for (uint32_t b = TPW / 2; b > 0; b >>= 1)
+          if (pre[j + b] <= i) j += b;
+        const uint32_t k = i - pre[j];
+        val[u] = reinterpret_cast<const uint4 *>(src[j])[k];
+        dst[u] = j * C16 + k;
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (dst[u] != 0xFFFFFFFFu) env[dst[u]] = val[u];
+  }
+  __syncthreads();
+  const uint32_t t = t0 + lane;
+  if (lane >= TPW || t >= ntx) return;  // (no barrier below)
+  const uint32_t *et = envtab + BD_ENV_WORDS * t;
+  const uint32_t blk = et[0];
+  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
+  if (my) {  // the virtual base: block offset o -> env + (o - (a0 - block))
+    const uint64_t a0 = src[lane];
+    base = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(&env[lane * C16]) -
+                                             (uintptr_t)(a0 - bases[blk]));
+  } else {
+    touch_lines(base + et[1], et[2]);
+  }
+  parse_one<TPW>(t, lane, blk, L, base, S{base + et[1], et[2]}, ch, out, flags, xhaz, kl);
+}
+
+void bd_parse_lds_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint32_t *envtab, const uint64_t *bases,
+                         const DevChannel &ch, DevTx *out, uint32_t *flags, uint32_t *xhaz, const KlDev &kl) {
+  if (tpw == 16)
+    hipLaunchKernelGGL((k_bd_parse_lds<16, 4352>), dim3((ntx + 15) / 16), dim3(64), 0, st, ntx, envtab, bases, ch, out,
+                       flags, xhaz, kl);
+  else if (tpw == 4)
+    hipLaunchKernelGGL((k_bd_parse_lds<4, 4352>), dim3((ntx + 3) / 4), dim3(64), 0, st, ntx, envtab, bases, ch, out,
+                       flags, xhaz, kl);
+  else
+    hipLaunchKernelGGL((k_bd_parse_lds<8, 4352>), dim3((ntx + 7) / 8), dim3(64), 0, st, ntx, envtab, bases, ch, out,
+                       flags, xhaz, kl);
 }
 
 // ============================================================ k_bd_ident

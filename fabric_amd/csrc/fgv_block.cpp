@@ -1745,6 +1745,8 @@ static int build_committed(fgv_block_state *S) {
 
 __global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, DevChannel ch, DevTx *out,
                            uint32_t *flags, uint32_t *xhaz, KlDev kl, uint32_t touch);
+void bd_parse_lds_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint32_t *envtab, const uint64_t *bases,
+                         const DevChannel &ch, DevTx *out, uint32_t *flags, uint32_t *xhaz, const KlDev &kl);
 __global__ void k_bd_kl(uint32_t ntx, DevTx *txs, const uint64_t *bases, KlDev kl, uint32_t *flags);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
@@ -2032,8 +2034,18 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     const uint32_t v = e ? (uint32_t)atoi(e) : 64u;
     return (v == 16u || v == 32u) ? v : 64u;
   }();
-  hipLaunchKernelGGL(k_bd_parse, dim3((N + parse_lanes - 1) / parse_lanes), dim3(parse_lanes), 0, sf, N, envtab, dbs,
-                     ch, dtx, misc + 5, misc + 16, B.kl, parse_touch);
+  // FGV_PARSE_LDS = transactions per workgroup of the LDS-staged walk (k_bd_parse_lds: 4, 8 or 16,
+  // each envelope copied to LDS before the walk); 0 = the global walk above (A/B)
+  static const uint32_t parse_lds = [] {
+    const char *e = getenv("FGV_PARSE_LDS");
+    const uint32_t v = e ? (uint32_t)atoi(e) : 8u;
+    return (v == 4u || v == 8u || v == 16u) ? v : 0u;
+  }();
+  if (parse_lds)
+    bd_parse_lds_launch(parse_lds, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16, B.kl);
+  else
+    hipLaunchKernelGGL(k_bd_parse, dim3((N + parse_lanes - 1) / parse_lanes), dim3(parse_lanes), 0, sf, N, envtab,
+                       dbs, ch, dtx, misc + 5, misc + 16, B.kl, parse_touch);
   HIP_TRY(hipEventRecord(B.ev[4], sf));
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one

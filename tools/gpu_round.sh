@@ -8,6 +8,7 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench (C2 headline line)
 #   lean<N>          N lean C2 runs (40 steps, no CPU baseline / PCIe / latency passes)
+#   env:VAR=VAL:N    N lean C2 runs with an environment knob set (A/B)
 #   churn            C2 with every creator a distinct identity (the cold-key path)
 #   mvcc | sig | c5 | sbe   the other workloads (tools/bench_sbe.py for sbe)
 #   trace            rocprofv3 --kernel-trace --stats of a C2 run
@@ -47,6 +48,14 @@ for step in "$@"; do
         timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --cpu-threads 0 --no-pcie --no-latency > $O/lean_$rep.json 2> $O/lean_$rep.err \
           || { echo lean failed; tail -20 $O/lean_$rep.err; exit 1; }
         show $O/lean_$rep.json "lean $rep" value ms_per_step parity_vs_labels
+      done ;;
+    env:*)
+      # env:VAR=VAL:N -- N lean C2 runs with VAR=VAL (A/B against lean<N> on the same box)
+      spec=${step#env:}; n=${spec##*:}; kv=${spec%:*}; tag=$(echo $kv | tr '=' '_')
+      for rep in $(seq 1 $n); do
+        env $kv timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --cpu-threads 0 --no-pcie --no-latency > $O/lean_${tag}_$rep.json 2> $O/lean_${tag}_$rep.err \
+          || { echo lean $kv failed; tail -20 $O/lean_${tag}_$rep.err; exit 1; }
+        show $O/lean_${tag}_$rep.json "lean $kv $rep" value ms_per_step parity_vs_labels
       done ;;
     churn)
       timeout -k 10 400 python -u bench.py --clients 16000 --steps 20 --warmup 3 --cpu-threads 0 --no-pcie > $O/churn.json 2> $O/churn.err \
