@@ -20,6 +20,7 @@ EXPORTED = [
     "fgv_last_point_handovers", "fgv_last_kernel_times",
     "fgv_sha256_batch",
     "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset", "fgv_key_stats",
+    "fgv_set_block_outcomes", "fgv_last_block_status", "fgv_unsupported_stats",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
@@ -38,6 +39,7 @@ EXPORTED = [
 RESOLVE_KNOWN, RESOLVE_OK, RESOLVE_FAILED, RESOLVE_UNSUPPORTED, RESOLVE_REPEAT = range(5)
 TX_RESULT_BYTES = 68
 FGV_EUNSUPPORTED = -6
+BLOCK_LATER = 1  # fgv_last_block_status: wait for the commit of the earlier blocks
 
 
 class FgvError(RuntimeError):
@@ -117,6 +119,9 @@ def load():
         L.fgv_keys_register.argtypes = [vp, vp, sz, vp]
         L.fgv_keys_reset.argtypes = [vp]
         L.fgv_key_stats.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 5
+        L.fgv_set_block_outcomes.argtypes = [vp, ctypes.c_int]
+        L.fgv_last_block_status.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+        L.fgv_unsupported_stats.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 3
         L.fgv_p256_verify_msgs_dev.argtypes = [vp] * 8 + [sz, vp]
         L.fgv_channel_init.argtypes = [vp, ctypes.c_char_p]
         L.fgv_msp_add_identity.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
@@ -467,6 +472,22 @@ class Engine:
         out = (ctypes.c_double * 11)()
         _check(self._L.fgv_last_kernel_times(self._h, out, 11))
         return dict(zip(self.KERNELS, out[:10])), int(out[10])
+
+    def set_block_outcomes(self, on=True):
+        """fgv_set_block_outcomes: per-block results instead of a whole-batch Unsupported"""
+        _check(self._L.fgv_set_block_outcomes(self._h, 1 if on else 0))
+
+    def last_block_status(self, nblocks):
+        """fgv_last_block_status -> (per-block status list: 0 final, FGV_EUNSUPPORTED, BLOCK_LATER; n_final)"""
+        st = np.zeros(nblocks, np.int32)
+        nf = ctypes.c_size_t()
+        _check(self._L.fgv_last_block_status(self._h, _ptr(st), nblocks, ctypes.byref(nf)))
+        return st.tolist(), nf.value
+
+    def unsupported_stats(self):
+        v = [ctypes.c_uint64() for _ in range(3)]
+        _check(self._L.fgv_unsupported_stats(self._h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("batches", "blocks", "txs"), (x.value for x in v)))
 
     def front_ahead_ms(self):
         """fgv_last_kernel_times out[11]: host ms spent enqueueing the next batch's front half"""

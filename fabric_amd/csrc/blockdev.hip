@@ -1807,7 +1807,8 @@ DEV uint32_t hex_word(const uint32_t *dw, uint32_t j) {
 // ============================================================ k_bd_kl
 // Per transaction whose rwset decoded, every written key (oracle keylevel_writes' `touched`)
 // against the batch's key-level records (k_bd_parse): a change by an earlier block of the batch
-// -> unsupported (flag 2; oracle check_keylevel_batch); a metadata write by an earlier
+// -> unsupported (flag 2; oracle check_keylevel_batch), and flags[7] = ~(the lowest such block)
+// for the per-block outcomes (fgv_set_block_outcomes: blocks from there on are LATER); a metadata write by an earlier
 // transaction of its block -> a dependency (validation_parameter_updated): the writer goes to the
 // transaction's list and the transaction to its block's dependent list, which k_bd_fold walks in
 // block order.  Launched for the fused single-device call only; no records: nothing to do.
@@ -1837,6 +1838,7 @@ __global__ __launch_bounds__(256) void k_bd_kl(uint32_t ntx, DevTx *__restrict__
         continue;
       if (E.blk < R.blk) {
         unsup = true;
+        atomicMax(&flags[7], ~R.blk);  // the first block that must wait for an earlier one's commit
         continue;
       }
       bool seen = false;

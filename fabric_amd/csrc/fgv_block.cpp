@@ -268,6 +268,10 @@ struct fgv_block_state {
   int last = 1;    // set of the last call
   int pending = -1;           // set enqueued by _enqueue and not yet finished
   double nv_per_tx = 0;       // verifies per tx of the last batch (lanes-per-verify estimate)
+  // per-block outcomes (fgv_set_block_outcomes) of the running call: soft = report instead of
+  // failing the batch; split = the first block that must wait for an earlier block's commit
+  bool soft = false;
+  uint32_t split = UINT32_MAX;
   uint32_t klseq = 0;         // key-level bucket tags (blockdev.h KlDev::seq), one per front half
   std::chrono::steady_clock::time_point t_enq;
   explicit fgv_block_state(unsigned threads) : pool(threads) {}
@@ -279,6 +283,11 @@ struct fgv_block_state {
 };
 
 fgv_block_state *fgv_block_state_new(unsigned threads) { return new fgv_block_state(threads); }
+void fgv_block_set_soft(fgv_block_state *S, bool on) {
+  S->soft = on;
+  S->split = UINT32_MAX;
+}
+uint32_t fgv_block_split(fgv_block_state *S) { return S->split; }
 Channel &fgv_block_channel(fgv_block_state *S) { return S->ch; }
 void fgv_parallel_for(fgv_block_state *S, size_t n, const std::function<void(size_t)> &f) {
   S->pool.parallel_for(n, f);
@@ -1064,13 +1073,18 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     for (size_t t = 0; t < total; t++)
       if (recs[t].xstat == X_OK) kl_keys(ch, recs[t].results, chg[where[t].first], tch[where[t].first]);
     std::unordered_set<std::string> changed;
-    for (size_t b = 0; b < nblocks; b++) {
+    for (size_t b = 0; b < nblocks && b < S->split; b++) {
       if (unknown[b]) {
         if (!changed.empty()) return FGV_EUNSUPPORTED;
         continue;
       }
-      for (const std::string &k : tch[b])
-        if (changed.count(k)) return FGV_EUNSUPPORTED;
+      bool dep = false;
+      for (const std::string &k : tch[b]) dep |= changed.count(k) != 0;
+      if (dep) {
+        if (!S->soft) return FGV_EUNSUPPORTED;
+        S->split = (uint32_t)b;  // per-block outcomes: this block and the later ones wait
+        break;
+      }
       changed.insert(chg[b].begin(), chg[b].end());
     }
     c->kl_changes = !changed.empty();
@@ -1265,9 +1279,11 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     S->pool.parallel_for(total, [&](size_t t) { fold_one(t, 0); });
   }
   c->t_host_fold = ms_since(t_fold);
-  // (from the final codes: a pass-1 verdict of a tx folded again in pass 2 does not count)
-  for (size_t t = 0; t < total; t++)
-    if (res_out[t].code == C_UNSUPPORTED) return FGV_EUNSUPPORTED;
+  // (from the final codes: a pass-1 verdict of a tx folded again in pass 2 does not count;
+  // per-block outcomes: the codes stay, 0xFD marking the undecided transactions)
+  if (!S->soft)
+    for (size_t t = 0; t < total; t++)
+      if (res_out[t].code == C_UNSUPPORTED) return FGV_EUNSUPPORTED;
   return FGV_OK;
 }
 
@@ -2262,7 +2278,7 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   if (S->pending < 0) return FGV_OK;
   BdSet &B = S->set[S->pending];
   S->pending = -1;
-  if (B.misc_src) HIP_TRY(hipMemcpyAsync(B.misc.p, B.misc_src, 48, hipMemcpyDeviceToHost, c->stream));
+  if (B.misc_src) HIP_TRY(hipMemcpyAsync(B.misc.p, B.misc_src, 64, hipMemcpyDeviceToHost, c->stream));
   B.misc_src = nullptr;
   HIP_TRY(fgv_stream_wait(c->stream, c->spin));
   fgv_read_block_job_times(c);
@@ -2296,6 +2312,12 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   c->t_host_device = std::chrono::duration<double, std::milli>(clk::now() - S->t_enq).count();
   c->t_host_fold = 0;
   if ((hm[5] & 1u) || B.force_host) return 1;
+  // per-block outcomes: the undecided transactions carry 0xFD in the flags, the first block that
+  // must wait for an earlier one's commit comes back in word 12 (k_bd_kl)
+  if (S->soft) {
+    if (hm[12]) S->split = std::min<uint32_t>(S->split, ~hm[12]);
+    return FGV_OK;
+  }
   if (hm[5] & 2u) return FGV_EUNSUPPORTED;
   return FGV_OK;
 }

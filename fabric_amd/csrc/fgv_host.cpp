@@ -1680,6 +1680,27 @@ int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *r
   return fgv_finalize_impl(nblocks, ntx, results, flags);
 }
 
+// Per-block outcomes of a call validated with fgv_set_block_outcomes on: blocks from `split` on
+// wait for the commit of the earlier ones (LATER); a block with an undecided transaction (0xFD) is
+// unsupported, the others are final.
+static void block_outcomes(fgv_ctx *c, size_t nblocks, const size_t *ntx, const uint8_t *flags, uint32_t split) {
+  c->blk_status.assign(nblocks, FGV_OK);
+  c->n_final = std::min<size_t>(nblocks, split);
+  size_t o = 0;
+  for (size_t b = 0; b < nblocks; o += ntx[b], b++) {
+    if (b >= c->n_final) {
+      c->blk_status[b] = FGV_BLOCK_LATER;
+      continue;
+    }
+    size_t k = 0;
+    for (size_t t = 0; t < ntx[b]; t++) k += flags[o + t] == 0xFD;
+    if (k) {
+      c->blk_status[b] = FGV_EUNSUPPORTED;
+      c->unsup_txs += k;
+    }
+  }
+}
+
 // TxValidator.Validate of a batch on one GPU: the device-parse pass and the finalize kernels
 // (markTXIdDuplicates + the batch's txid index) are queued back to back and the call waits once.
 static int validate_blocks_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
@@ -1759,13 +1780,61 @@ int fgv_validate_blocks_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *con
   std::lock_guard<std::mutex> g(c->mu);
   c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks,   next_lens, nullptr, nullptr,
                                !next_d_blocks && !d_blocks, next_d_blocks, nullptr};
-  int rc = validate_blocks_locked(c, nblocks, blocks, lens, d_blocks, flags, flags_cap, ntx);
-  if (resolve_for_retry(c, rc, nblocks, blocks, lens))
-    rc = validate_blocks_locked(c, nblocks, blocks, lens, d_blocks, flags, flags_cap, ntx);
+  const bool soft = c->block_outcomes;
+  auto run = [&] {
+    fgv_block_set_soft(c->blk, soft);
+    const int r = validate_blocks_locked(c, nblocks, blocks, lens, d_blocks, flags, flags_cap, ntx);
+    if (soft && r == FGV_OK) block_outcomes(c, nblocks, ntx, flags, fgv_block_split(c->blk));
+    fgv_block_set_soft(c->blk, false);
+    return r;
+  };
+  int rc = run();
+  if (resolve_for_retry(c, rc, nblocks, blocks, lens)) {
+    rc = run();
+  } else if (soft && rc == FGV_OK && fgv_msp_auto(c)) {
+    // per-block outcomes: identities a channel MSP may hold, in the unsupported blocks only
+    std::vector<const uint8_t *> ub;
+    std::vector<size_t> ul;
+    for (size_t b = 0; b < nblocks; b++)
+      if (c->blk_status[b] == FGV_EUNSUPPORTED) ub.push_back(blocks[b]), ul.push_back(lens[b]);
+    size_t reg = 0;
+    if (!ub.empty() && fgv_msp_resolve_blocks_locked(c, ub.size(), ub.data(), ul.data(), &reg) == FGV_OK && reg > 0)
+      rc = run();
+  }
+  if (soft && rc == FGV_OK) {
+    for (size_t b = 0; b < nblocks; b++) c->unsup_blocks += c->blk_status[b] == FGV_EUNSUPPORTED;
+  } else if (rc == FGV_EUNSUPPORTED) {
+    c->unsup_batches++;
+    c->unsup_blocks += nblocks;
+  }
   if (c->next.n)  // not started inside (host-parse path, empty batch, early error): start it now
     fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, nullptr, nullptr);
   c->next = fgv_ctx::NextBatch{};
   return rc;
+}
+
+int fgv_set_block_outcomes(fgv_ctx *c, int on) {
+  if (!c) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->block_outcomes = on != 0;
+  return FGV_OK;
+}
+
+int fgv_last_block_status(fgv_ctx *c, int32_t *status, size_t n, size_t *n_final) {
+  if (!c || (n && !status)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (size_t b = 0; b < n; b++) status[b] = b < c->blk_status.size() ? c->blk_status[b] : FGV_OK;
+  if (n_final) *n_final = c->n_final;
+  return FGV_OK;
+}
+
+int fgv_unsupported_stats(fgv_ctx *c, uint64_t *batches, uint64_t *blocks, uint64_t *txs) {
+  if (!c) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (batches) *batches = c->unsup_batches;
+  if (blocks) *blocks = c->unsup_blocks;
+  if (txs) *txs = c->unsup_txs;
+  return FGV_OK;
 }
 
 }  // extern "C"

@@ -135,6 +135,11 @@ struct fgv_ctx {
   uint32_t promote_uses = 64;     // variable-base verifies of one key before its comb is built
   uint32_t adhoc_comb_uses = 32;  // uses of an ad-hoc key in one call for a comb
   uint64_t n_promoted = 0;        // keys promoted to a comb since fgv_init
+  // per-block outcomes (fgv_set_block_outcomes) and the fallback counters (fgv_unsupported_stats)
+  bool block_outcomes = false;
+  std::vector<int32_t> blk_status;
+  size_t n_final = 0;
+  uint64_t unsup_batches = 0, unsup_blocks = 0, unsup_txs = 0;
   fgv_block_state *blk = nullptr;
   DevBuf bj_jobs, bj_sigp, bj_sigl, bj_slot, bj_didx, bj_dig, bj_vst, blk_arena;
   HostBuf hb_dig, hb_vst;
@@ -243,6 +248,10 @@ inline hipError_t fgv_stream_wait(hipStream_t s, bool spin) {
 
 
 fgv_block_state *fgv_block_state_new(unsigned threads);
+// per-block outcomes of the next validation (fgv_set_block_outcomes): on = per-transaction 0xFD
+// codes and a split block instead of a whole-batch FGV_EUNSUPPORTED; split = UINT32_MAX: none
+void fgv_block_set_soft(fgv_block_state *S, bool on);
+uint32_t fgv_block_split(fgv_block_state *S);
 void fgv_block_state_free(fgv_block_state *s);
 
 #include <functional>

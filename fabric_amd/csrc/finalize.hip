@@ -219,6 +219,10 @@ __global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *mi
   if (flags[p] != 0 || pslot[p] == 0xFFFFFFFFu) return;
   const uint32_t m = minvalid[pslot[p]];
   if (m >= p) return;
-  if (unsup && flags[m] != 0) atomicOr(unsup, 2u);
+  if (unsup && flags[m] != 0) {  // the first VALID position was failed by the key-level walk
+    atomicOr(unsup, 2u);
+    flags[p] = 0xFD;  // (undecided: the per-block outcomes mark its block unsupported)
+    return;
+  }
   flags[p] = 9;  // markTXIdDuplicates: an earlier VALID tx of this block
 }

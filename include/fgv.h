@@ -284,6 +284,31 @@ int fgv_validate_blocks_pipelined(fgv_ctx *ctx, size_t nblocks, const uint8_t *c
                                   const uint8_t *const *next_blocks, const size_t *next_lens,
                                   const uint8_t *const *next_d_blocks);
 
+/* Per-block outcomes (off by default: a batch holding anything outside the engine's model returns
+ * FGV_EUNSUPPORTED as a whole, and the caller validates every block of it with the reference).
+ * On, fgv_validate_blocks[_pipelined] return FGV_OK for such a batch, and fgv_last_block_status
+ * reports for each block of the last call:
+ *   FGV_OK           -- its flags are final;
+ *   FGV_EUNSUPPORTED -- it holds something outside the model (a CONFIG transaction, a P-384 or
+ *                       SHA3 identity, a certificate no channel MSP can judge, ...): validate this
+ *                       block with the reference; its flag bytes are 0xFD where the engine could
+ *                       not decide a transaction;
+ *   FGV_BLOCK_LATER  -- not decided: an earlier block of the call may change the key-level
+ *                       VALIDATION_PARAMETER of a key this block writes, and the reference commits
+ *                       that block before this one reads it (statebased/vpmanagerimpl.go:296-355).
+ *                       Every block from the first such one (n_final) on is LATER: commit blocks
+ *                       [0, n_final) and call again with the rest.
+ * Blocks after an unsupported one stay final: a block reads the earlier blocks' txids (every one,
+ * whatever its code: checkTxIdDupsLedger, validator.go:460-481) and, through the rule above,
+ * never their codes.  Single-GPU calls; the shard and group calls keep the whole-batch
+ * FGV_EUNSUPPORTED.  fgv_unsupported_stats: fallback counters since fgv_init -- calls that
+ * returned FGV_EUNSUPPORTED, blocks handed to the reference (whole batches included), undecided
+ * transactions of per-block calls. */
+#define FGV_BLOCK_LATER 1
+int fgv_set_block_outcomes(fgv_ctx *ctx, int on);
+int fgv_last_block_status(fgv_ctx *ctx, int32_t *status, size_t n, size_t *n_final);
+int fgv_unsupported_stats(fgv_ctx *ctx, uint64_t *batches, uint64_t *blocks, uint64_t *txs);
+
 /* ----------------------------------------------- multi-GPU committer (one process per GPU)
  * fgv_validate_blocks = fgv_validate_shard over every transaction + fgv_finalize_flags.
  * With G GPUs each rank validates transactions [tx_lo[b], tx_hi[b]) of every block b (the

@@ -907,6 +907,43 @@ def validate_blocks(model, blocks):
     return out
 
 
+def validate_blocks_outcomes(model, blocks):
+    """The engine's per-block outcomes (fgv_set_block_outcomes, include/fgv.h) restated over the
+    reference's rules: n_final = the first block writing a key whose key-level parameter an earlier
+    block of the call may change (check_keylevel_batch's condition; the reference commits that
+    block first); each block before it is validated (None when Unsupported), and every block's
+    txids are indexed whatever its codes (blkstorage indexes every transaction,
+    block_serialization.go:95-115), so a block after an unsupported one is still decided.
+    -> (list of flags or None, n_final)"""
+    n_final = len(blocks)
+    seen_changed = set()
+    for b, blk in enumerate(blocks):
+        data = (decode("Block", blk).get("data") or {}).get("data", [])
+        ch_b, tc_b = set(), set()
+        for d in data:
+            c, t = keylevel_writes(model, d)
+            ch_b |= c
+            tc_b |= t
+        if seen_changed & tc_b:
+            n_final = b
+            break
+        seen_changed |= ch_b
+    out = []
+    for b, blk in enumerate(blocks):
+        if b >= n_final:
+            out.append(None)
+            continue
+        try:
+            out.append(validate_block(model, blk))
+        except Unsupported:
+            out.append(None)
+        for d in (decode("Block", blk).get("data") or {}).get("data", []):
+            t = index_txid(d)
+            if t:
+                model.committed.add(t)
+    return out, n_final
+
+
 def validate_block(model, block_bytes):
     """TxValidator.Validate -> list of validation codes (TxValidationFlags)."""
     blk = decode("Block", block_bytes)

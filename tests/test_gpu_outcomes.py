@@ -1,0 +1,113 @@
+"""GPU: per-block outcomes (fgv_set_block_outcomes, include/fgv.h).  A transaction outside the
+engine's model sends only its own block to the reference; a block whose keys' key-level
+parameters an earlier block of the call may change waits for that block's commit (n_final), and
+every other block's flags are final and equal the restated committer's
+(oracle.v20.validate_blocks_outcomes: validate_block per block, every earlier block's txids
+indexed -- validator.go:460-481 reads TxIDExists, whatever the earlier codes were)."""
+import pytest
+
+from fabric_amd import _lib, txvalidator
+from fabric_amd.synth import blocks
+from oracle import v20
+from tests import sbe_cases
+
+pytestmark = pytest.mark.gpu
+MODES = pytest.mark.parametrize("mode", [0, 1], ids=["devparse", "hostparse"])
+
+
+def _check(eng, model, blks):
+    got = eng.validate_blocks(blks)
+    st, n_final = eng.last_block_status(len(blks))
+    exp, exp_final = v20.validate_blocks_outcomes(model, blks)
+    assert n_final == exp_final
+    for b in range(len(blks)):
+        if b >= exp_final:
+            assert st[b] == _lib.BLOCK_LATER, b
+        elif exp[b] is None:
+            assert st[b] == _lib.FGV_EUNSUPPORTED, b
+            assert 0xFD in list(got[b])
+        else:
+            assert st[b] == 0, b
+            mism = [(i, int(got[b][i]), exp[b][i]) for i in range(len(exp[b])) if got[b][i] != exp[b][i]]
+            assert len(got[b]) == len(exp[b]) and not mism, (b, mism[:10])
+    return st, n_final
+
+
+@MODES
+def test_out_of_model_identity_confined_to_its_blocks(mode):
+    """one client registered as a P-384 identity (the engine does not verify P-384): only the blocks
+    where it creates or endorses a transaction are unsupported; the batch's other blocks are final"""
+    net = blocks.Network(seed=3, orgs=3, clients=3000)
+    blks, creators = [], []
+    for i in range(6):
+        txs = []
+        blks.append(blocks.make_block(net, 100, number=1 + i, seed=60 + i, out_txs=txs)[0])
+        creators.append({t.creator.serialized for t in txs})
+    # a creator that appears in blocks 1 and 4 only (or in one block): the P-384 identity
+    pick = None
+    for ser in creators[1]:
+        where = [b for b in range(6) if ser in creators[b]]
+        if where == [1]:
+            pick = ser
+            break
+    assert pick is not None
+    ids = []
+    for ser, ident in net.identities():
+        if ser == pick:
+            ident = txvalidator.Identity(ident.mspid, None, True, ident.id_digest, key="p384", roles=ident.roles)
+        ids.append((ser, ident))
+    eng = _lib.Engine(0)
+    try:
+        eng.set_parse_mode(mode)
+        txvalidator.setup_channel(eng, net.channel, ids, net.chaincodes)
+        with pytest.raises(_lib.Unsupported):  # (the whole-batch contract stays the default)
+            eng.validate_blocks(blks)
+        assert eng.unsupported_stats()["blocks"] == 6
+        eng.set_block_outcomes(True)
+        st, n_final = _check(eng, v20.ChannelModel(net.channel, ids, net.chaincodes), blks)
+        assert n_final == 6 and st == [0, _lib.FGV_EUNSUPPORTED, 0, 0, 0, 0], st
+        s = eng.unsupported_stats()
+        assert s["batches"] == 1 and s["blocks"] == 7 and s["txs"] >= 1, s
+    finally:
+        eng.close()
+
+
+@MODES
+def test_keylevel_split_at_block_boundary(mode):
+    """block 1 sets / clears key-level parameters that block 2 writes: blocks 0..1 are final, block 2
+    waits (n_final = 2); after block 1's MVCC commit, block 2 alone equals the oracle on the
+    committed state"""
+    from oracle import mvcc as OM
+    net = sbe_cases_network()
+    ccs = {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
+    b0 = blocks.make_block(net, 40, number=1, seed=17)[0]
+    (b1, kvmeta0), (b2, _) = [sbe_cases.make_sbe_block(net, 50, 948 + k, number=2 + k) for k in range(2)]
+    eng = _lib.Engine(0)
+    try:
+        eng.set_parse_mode(mode)
+        txvalidator.setup_channel(eng, net.channel, net.identities(), ccs, kvmeta=kvmeta0)
+        eng.set_block_outcomes(True)
+        model = lambda kv: v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=dict(kv))  # noqa: E731
+        st, n_final = _check(eng, model(kvmeta0), [b0, b1, b2])
+        assert n_final == 2 and st == [0, 0, _lib.BLOCK_LATER], st
+        eng.statedb_init(1 << 16, 8 << 20)
+        db = OM.StateDB({}, kvmeta=dict(kvmeta0))
+        for num, b in ((1, b0), (2, b1)):
+            f = v20.validate_block(model(db.kvmeta), b)
+            assert list(eng.mvcc_validate(b, num, f, commit=True)) == list(OM.validate_block(db, b, f, num, commit=True))
+        m2 = model(db.kvmeta)
+        for b in (b0, b1):
+            for d in (v20.decode("Block", b).get("data") or {}).get("data", []):
+                t = v20.index_txid(d)
+                if t:
+                    m2.committed.add(t)
+        eng.ledger_add_txids(sorted(m2.committed))
+        st, n_final = _check(eng, m2, [b2])
+        assert n_final == 1 and st == [0]
+    finally:
+        eng.close()
+
+
+def sbe_cases_network():
+    from tests.blockfix import network
+    return network()
