@@ -11,7 +11,7 @@ KOBJS := $(OBJDIR)/sha256.o $(OBJDIR)/p256_kernels.o $(OBJDIR)/der_kernel.o $(OB
 	$(OBJDIR)/fgv_group.o $(OBJDIR)/fgv_msp.o $(OBJDIR)/fgv_x509.o
 HDRS := $(CSRC)/p256_field.h $(CSRC)/p256_fe28.h $(CSRC)/p256_modinv.h $(CSRC)/sha256_dev.h $(CSRC)/fgv_kernels.h $(CSRC)/fgv_der.h $(CSRC)/fgv_internal.h include/fgv.h $(CSRC)/blockdev.h $(CSRC)/pbwire_dev.h $(CSRC)/fin_dev.h
 
-all: fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so
+all: fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so tests/gpu_helpers/libhexcheck.so
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
@@ -55,7 +55,11 @@ oracle/liboracle.so: oracle/fgv_oracle.c oracle/fgv_oracle.h
 fabric_amd/synth/libfgv_synth.so: fabric_amd/synth/fgv_synth.c
 	gcc -O2 -fPIC -shared -Wall -o $@ $< -lcrypto -lpthread
 
+# test helper (not part of the product): the device txid decoder on chosen offsets
+tests/gpu_helpers/libhexcheck.so: tests/gpu_helpers/hexcheck.hip $(CSRC)/fin_dev.h
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+
 clean:
-	rm -rf $(OBJDIR) fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so
+	rm -rf $(OBJDIR) fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so tests/gpu_helpers/libhexcheck.so
 
 .PHONY: all clean

@@ -328,7 +328,9 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
                 src = clean[rng.randrange(len(clean))]
                 t.creator, t.nonce = src.creator, src.nonce
             else:
-                t.label = "clean"
+                # relabelled clean: the creator-kind rule above applies again (an Ed25519 creator
+                # cannot be a clean transaction: DeserializeIdentity fails, code 4)
+                t.label = "clean" if t.creator.kind == "p256" else "ed25519_creator"
         r = rng.random()
         ne, accp = endorse_dist[-1][0], 0.0
         for e, p in endorse_dist:
