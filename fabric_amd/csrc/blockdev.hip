@@ -828,17 +828,98 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
   parse_one<PL>(t, lane, blk, L, base, d, ch, out, flags, xhaz, kl);
 }
 
+// ============================================================ k_bd_ident
+// ID_LANES lanes per (tx, occurrence): occurrence 0 = creator, 1..nend = endorsers.
+// Channel::lookup restated: decode SerializedIdentity (mspid UTF-8), hash, probe, exact compare.
+// The compare is split over the group's lanes a 32-bit word at a time (block bytes at any
+// alignment via v_alignbyte; registry fields are 4-byte aligned), then one ballot.
+#define ID_LANES 16u
+#define ID_PAR BD_ID_PAR
+DEV uint32_t ldu32(const uint8_t *p) {  // unaligned little-endian word (reads the next word too)
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
+}
+DEV uint32_t tail_mask(uint32_t n, uint32_t j) {  // bytes of word j inside [0, n)
+  const uint32_t r = n - 4u * j;
+  return r >= 4u ? 0xFFFFFFFFu : ((1u << (8u * r)) - 1u);
+}
+DEV uint64_t ident_hash_dev(S msp, S idb) {  // == bd_ident_hash (blockdev.h), word loads
+  uint64_t h = bd_ident_hash_msp(msp.p, msp.n, idb.n);
+  const uint32_t T = idb.n < BD_HASH_TAIL ? idb.n : BD_HASH_TAIL;
+  const uint8_t *s = idb.p + (idb.n - T);
+  for (uint32_t j = 0; 4u * j < T; j++) h = bd_mix(h, ldu32(s + 4u * j) & tail_mask(T, j));
+  return bd_mix(h, 0x5A);
+}
+// every lane of the group calls this with the same spans; `b` is 4-byte aligned
+DEV bool group_eq(S a, S b, uint32_t l) {
+  if (a.n != b.n) return false;
+  uint32_t diff = 0;
+  const uint32_t *bw = reinterpret_cast<const uint32_t *>(b.p);
+  for (uint32_t j = l; 4u * j < a.n; j += ID_LANES) diff |= (ldu32(a.p + 4u * j) ^ bw[j]) & tail_mask(a.n, j);
+  const uint64_t bal = __ballot(diff != 0u);
+  const uint32_t lane = threadIdx.x & 63u;
+  return ((bal >> (lane & ~(ID_LANES - 1u))) & ((1ull << ID_LANES) - 1ull)) == 0ull;
+}
+// Channel::lookup of one SerializedIdentity (every lane of a 16-lane group calls it with the same
+// span): the registry index, -1 (deserialize error / undeserializable key) or -2 (a certificate of
+// a channel MSP that was never registered: outside the engine)
+DEV int32_t ident_lookup(S ser, const DevChannel &ch, uint32_t l) {
+  VSerializedIdentity sid;
+  bool ovf = false;
+  if (!decode(ser, sid, ovf)) return -1;
+  const uint64_t h = ident_hash_dev(sid.mspid, sid.id_bytes);
+  // (an empty registry has no table: every identity of a channel MSP is a miss)
+  for (uint32_t pos = (uint32_t)h & ch.ident_mask; ch.nident; pos = (pos + 1) & ch.ident_mask) {
+    const uint32_t e = ch.ident_table[pos];
+    if (e == 0) break;
+    const uint32_t i = e - 1;
+    if (ch.ident_hash[i] != h) continue;
+    const DevIdent &I = ch.idents[i];
+    if (group_eq(sid.mspid, S{ch.ident_bytes + I.msp_off, I.msp_len}, l) &&
+        group_eq(sid.id_bytes, S{ch.ident_bytes + I.idb_off, I.idb_len}, l))
+      return I.vclass == 3 ? -1 : (int32_t)i;  // undeserializable key: deserialize error
+  }
+  return msp_known(ch, sid.mspid) ? -2 : -1;
+}
+__global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__restrict__ txs,
+                                                  const uint64_t *__restrict__ bases, DevChannel ch,
+                                                  int32_t *__restrict__ ident) {
+  __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
+  // ID_PAR groups per tx (one wave): group g resolves occurrences g, g + ID_PAR, ... -- a C2
+  // transaction's creator and endorsers in one pass instead of one after the other
+  const uint32_t grp = (blockIdx.x * blockDim.x + threadIdx.x) / ID_LANES;
+  const uint32_t t = grp / ID_PAR, g = grp % ID_PAR;
+  const uint32_t l = threadIdx.x % ID_LANES;
+  if (t >= ntx) return;  // whole groups exit together
+  const DevTx &R = txs[t];
+  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
+  const uint32_t nend = R.nend;
+  for (uint32_t k = g; k <= nend; k += ID_PAR) {
+    // the creator is needed when the parse got past the channel check (pre still pending)
+    const DSpan sp = k == 0 ? R.creator : R.end_ser[k - 1];
+    const bool want = k == 0 ? (R.pre == C_PENDING && sp.len != 0) : true;
+    const int32_t res = want ? ident_lookup(absl(base, sp), ch, l) : -1;
+    if (l == 0) ident[(size_t)t * BD_OCC + k] = res;
+  }
+}
+
 // LDS-staged walk: one 64-lane workgroup per TPW transactions.  The wave first copies the
 // group's envelopes into LDS -- 16-byte loads of the aligned lines covering [off, off + len + 8)
 // (the walk's over-read contract), every line in flight at once -- then lane j walks transaction
 // j from LDS through a virtual base, so each of the walk's dependent loads is an LDS access
 // instead of a cache round trip (the global walk pays ~0.5-1 us per field).  An envelope larger
 // than CAP bytes is walked from global memory.
+// ident (nullable): k_bd_ident's work in the same workgroup once the walks are done -- the
+// creator and endorser SerializedIdentities of the group's transactions (bytes in LDS when
+// staged) resolved against the HBM registry by four 16-lane groups at a time, the 56 lanes the
+// walk leaves idle -- so the front half has one kernel fewer on its chain.
 template <uint32_t TPW, uint32_t CAP>
 __global__ __launch_bounds__(64) void k_bd_parse_lds(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                      const uint64_t *__restrict__ bases, DevChannel ch,
                                                      DevTx *__restrict__ out, uint32_t *__restrict__ flags,
-                                                     uint32_t *__restrict__ xhaz, KlDev kl) {
+                                                     uint32_t *__restrict__ xhaz, KlDev kl,
+                                                     int32_t *__restrict__ ident) {
   __builtin_amdgcn_s_setprio(2);
   constexpr uint32_t C16 = CAP / 16;  // 16-byte lines per staged envelope
   __shared__ ParseLdsT<TPW> L;
@@ -889,111 +970,60 @@ __global__ __launch_bounds__(64) void k_bd_parse_lds(uint32_t ntx, const uint32_
       if (dst[u] != 0xFFFFFFFFu) env[dst[u]] = val[u];
   }
   __syncthreads();
+  __shared__ const uint8_t *vbase[TPW];  // each transaction's walk base (LDS virtual base or block)
+  __shared__ DSpan occ[TPW][BD_OCC];     // its creator and endorser SerializedIdentity spans
+  __shared__ uint32_t nocc[TPW];         // 1 + endorsements (0: no transaction)
+  __shared__ uint32_t want0[TPW];        // the creator is needed (the parse got past the channel check)
   const uint32_t t = t0 + lane;
-  if (lane >= TPW || t >= ntx) return;  // (no barrier below)
-  const uint32_t *et = envtab + BD_ENV_WORDS * t;
-  const uint32_t blk = et[0];
-  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
-  if (my) {  // the virtual base: block offset o -> env + (o - (a0 - block))
-    const uint64_t a0 = src[lane];
-    base = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(&env[lane * C16]) -
-                                             (uintptr_t)(a0 - bases[blk]));
-  } else {
-    touch_lines(base + et[1], et[2]);
+  if (lane < TPW && t < ntx) {
+    const uint32_t *et = envtab + BD_ENV_WORDS * t;
+    const uint32_t blk = et[0];
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[blk]);
+    if (my) {  // the virtual base: block offset o -> env + (o - (a0 - block))
+      const uint64_t a0 = src[lane];
+      base = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(&env[lane * C16]) -
+                                               (uintptr_t)(a0 - bases[blk]));
+    } else {
+      touch_lines(base + et[1], et[2]);
+    }
+    parse_one<TPW>(t, lane, blk, L, base, S{base + et[1], et[2]}, ch, out, flags, xhaz, kl);
+    if (ident) {
+      const DevTx &O = out[t];  // (written by this lane)
+      const uint32_t ne = O.nend;
+      vbase[lane] = base;
+      nocc[lane] = 1 + ne;
+      want0[lane] = O.pre == C_PENDING && O.creator.len != 0;
+      occ[lane][0] = O.creator;
+      for (uint32_t k = 0; k < ne; k++) occ[lane][1 + k] = O.end_ser[k];
+    }
+  } else if (ident && lane < TPW) {
+    nocc[lane] = 0;
   }
-  parse_one<TPW>(t, lane, blk, L, base, S{base + et[1], et[2]}, ch, out, flags, xhaz, kl);
+  if (!ident) return;
+  __syncthreads();
+  // k_bd_ident's lookups: group g of 16 lanes takes (transaction, occurrence) pairs g, g + 4, ...
+  const uint32_t g = lane / ID_LANES, l = lane % ID_LANES;
+  for (uint32_t p = g; p < TPW * BD_OCC; p += 64u / ID_LANES) {
+    const uint32_t j = p / BD_OCC, k = p % BD_OCC;
+    if (k >= nocc[j]) continue;  // (uniform within the group)
+    const bool want = k == 0 ? want0[j] != 0 : true;
+    const int32_t res = want ? ident_lookup(absl(vbase[j], occ[j][k]), ch, l) : -1;
+    if (l == 0) ident[(size_t)(t0 + j) * BD_OCC + k] = res;
+  }
 }
 
 void bd_parse_lds_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint32_t *envtab, const uint64_t *bases,
-                         const DevChannel &ch, DevTx *out, uint32_t *flags, uint32_t *xhaz, const KlDev &kl) {
+                         const DevChannel &ch, DevTx *out, uint32_t *flags, uint32_t *xhaz, const KlDev &kl,
+                         int32_t *ident) {
   if (tpw == 16)
     hipLaunchKernelGGL((k_bd_parse_lds<16, 4352>), dim3((ntx + 15) / 16), dim3(64), 0, st, ntx, envtab, bases, ch, out,
-                       flags, xhaz, kl);
+                       flags, xhaz, kl, ident);
   else if (tpw == 4)
     hipLaunchKernelGGL((k_bd_parse_lds<4, 4352>), dim3((ntx + 3) / 4), dim3(64), 0, st, ntx, envtab, bases, ch, out,
-                       flags, xhaz, kl);
+                       flags, xhaz, kl, ident);
   else
     hipLaunchKernelGGL((k_bd_parse_lds<8, 4352>), dim3((ntx + 7) / 8), dim3(64), 0, st, ntx, envtab, bases, ch, out,
-                       flags, xhaz, kl);
-}
-
-// ============================================================ k_bd_ident
-// ID_LANES lanes per (tx, occurrence): occurrence 0 = creator, 1..nend = endorsers.
-// Channel::lookup restated: decode SerializedIdentity (mspid UTF-8), hash, probe, exact compare.
-// The compare is split over the group's lanes a 32-bit word at a time (block bytes at any
-// alignment via v_alignbyte; registry fields are 4-byte aligned), then one ballot.
-#define ID_LANES 16u
-#define ID_PAR BD_ID_PAR
-DEV uint32_t ldu32(const uint8_t *p) {  // unaligned little-endian word (reads the next word too)
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
-}
-DEV uint32_t tail_mask(uint32_t n, uint32_t j) {  // bytes of word j inside [0, n)
-  const uint32_t r = n - 4u * j;
-  return r >= 4u ? 0xFFFFFFFFu : ((1u << (8u * r)) - 1u);
-}
-DEV uint64_t ident_hash_dev(S msp, S idb) {  // == bd_ident_hash (blockdev.h), word loads
-  uint64_t h = bd_ident_hash_msp(msp.p, msp.n, idb.n);
-  const uint32_t T = idb.n < BD_HASH_TAIL ? idb.n : BD_HASH_TAIL;
-  const uint8_t *s = idb.p + (idb.n - T);
-  for (uint32_t j = 0; 4u * j < T; j++) h = bd_mix(h, ldu32(s + 4u * j) & tail_mask(T, j));
-  return bd_mix(h, 0x5A);
-}
-// every lane of the group calls this with the same spans; `b` is 4-byte aligned
-DEV bool group_eq(S a, S b, uint32_t l) {
-  if (a.n != b.n) return false;
-  uint32_t diff = 0;
-  const uint32_t *bw = reinterpret_cast<const uint32_t *>(b.p);
-  for (uint32_t j = l; 4u * j < a.n; j += ID_LANES) diff |= (ldu32(a.p + 4u * j) ^ bw[j]) & tail_mask(a.n, j);
-  const uint64_t bal = __ballot(diff != 0u);
-  const uint32_t lane = threadIdx.x & 63u;
-  return ((bal >> (lane & ~(ID_LANES - 1u))) & ((1ull << ID_LANES) - 1ull)) == 0ull;
-}
-__global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__restrict__ txs,
-                                                  const uint64_t *__restrict__ bases, DevChannel ch,
-                                                  int32_t *__restrict__ ident) {
-  __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
-  // ID_PAR groups per tx (one wave): group g resolves occurrences g, g + ID_PAR, ... -- a C2
-  // transaction's creator and endorsers in one pass instead of one after the other
-  const uint32_t grp = (blockIdx.x * blockDim.x + threadIdx.x) / ID_LANES;
-  const uint32_t t = grp / ID_PAR, g = grp % ID_PAR;
-  const uint32_t l = threadIdx.x % ID_LANES;
-  if (t >= ntx) return;  // whole groups exit together
-  const DevTx &R = txs[t];
-  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
-  const uint32_t nend = R.nend;
-  for (uint32_t k = g; k <= nend; k += ID_PAR) {
-    int32_t res = -1;
-    // the creator is needed when the parse got past the channel check (pre still pending)
-    const DSpan sp = k == 0 ? R.creator : R.end_ser[k - 1];
-    const bool want = k == 0 ? (R.pre == C_PENDING && sp.len != 0) : true;
-    if (want) {
-      VSerializedIdentity sid;
-      bool ovf = false;
-      if (decode(absl(base, sp), sid, ovf)) {
-        const uint64_t h = ident_hash_dev(sid.mspid, sid.id_bytes);
-        bool found = false;
-        // (an empty registry has no table: every identity of a channel MSP is a miss)
-        for (uint32_t pos = (uint32_t)h & ch.ident_mask; ch.nident; pos = (pos + 1) & ch.ident_mask) {
-          const uint32_t e = ch.ident_table[pos];
-          if (e == 0) break;
-          const uint32_t i = e - 1;
-          if (ch.ident_hash[i] != h) continue;
-          const DevIdent &I = ch.idents[i];
-          if (group_eq(sid.mspid, S{ch.ident_bytes + I.msp_off, I.msp_len}, l) &&
-              group_eq(sid.id_bytes, S{ch.ident_bytes + I.idb_off, I.idb_len}, l)) {
-            found = true;
-            res = I.vclass == 3 ? -1 : (int32_t)i;  // undeserializable key: deserialize error
-            break;
-          }
-        }
-        // a certificate of a channel MSP that was never registered: outside the engine
-        if (!found && msp_known(ch, sid.mspid)) res = -2;
-      }
-    }
-    if (l == 0) ident[(size_t)t * BD_OCC + k] = res;
-  }
+                       flags, xhaz, kl, ident);
 }
 
 // ============================================================ k_bd_count

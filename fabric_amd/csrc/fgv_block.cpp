@@ -1762,7 +1762,8 @@ static int build_committed(fgv_block_state *S) {
 __global__ void k_bd_parse(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, DevChannel ch, DevTx *out,
                            uint32_t *flags, uint32_t *xhaz, KlDev kl, uint32_t touch);
 void bd_parse_lds_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint32_t *envtab, const uint64_t *bases,
-                         const DevChannel &ch, DevTx *out, uint32_t *flags, uint32_t *xhaz, const KlDev &kl);
+                         const DevChannel &ch, DevTx *out, uint32_t *flags, uint32_t *xhaz, const KlDev &kl,
+                         int32_t *ident);
 __global__ void k_bd_kl(uint32_t ntx, DevTx *txs, const uint64_t *bases, KlDev kl, uint32_t *flags);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
@@ -2057,8 +2058,16 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     const uint32_t v = e ? (uint32_t)atoi(e) : 8u;
     return (v == 4u || v == 8u || v == 16u) ? v : 0u;
   }();
+  // FGV_PARSE_IDENT=0: k_bd_ident as its own kernel after the LDS-staged parse (A/B); by default
+  // the parse workgroups resolve their transactions' identities themselves
+  static const bool parse_ident = [] {
+    const char *e = getenv("FGV_PARSE_IDENT");
+    return !e || atoi(e) != 0;
+  }();
+  const bool fused_ident = parse_lds && parse_ident;
   if (parse_lds)
-    bd_parse_lds_launch(parse_lds, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16, B.kl);
+    bd_parse_lds_launch(parse_lds, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16, B.kl,
+                        fused_ident ? B.ident.as<int32_t>() : nullptr);
   else
     hipLaunchKernelGGL(k_bd_parse, dim3((N + parse_lanes - 1) / parse_lanes), dim3(parse_lanes), 0, sf, N, envtab,
                        dbs, ch, dtx, misc + 5, misc + 16, B.kl, parse_touch);
@@ -2091,9 +2100,9 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[1], 0));
   HIP_TRY(hipEventRecord(B.ev[8], c->stream3));
   if (tim) HIP_TRY(hipEventRecord(B.ev[7], sf));
-  hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 * BD_ID_PAR + 255) / 256)), dim3(256), 0, sf, N, dtx,
-                     dbs, ch,
-                     B.ident.as<int32_t>());
+  if (!fused_ident)
+    hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 * BD_ID_PAR + 255) / 256)), dim3(256), 0, sf, N,
+                       dtx, dbs, ch, B.ident.as<int32_t>());
   hipLaunchKernelGGL(k_bd_count, dim3((N + 1023) / 1024), dim3(1024), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
                      B.jobs.as<DevJobIdx>(), misc);
   HIP_TRY(hipGetLastError());
