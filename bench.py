@@ -186,6 +186,14 @@ BLOCK_SPECS = {
 }
 
 
+def _dist_info(world):
+    """what the collective layer saw (the driver's scaling run checks that RCCL had N ranks)"""
+    if world > 1 and dist.is_initialized():
+        return dict(world_size=dist.get_world_size(), backend=str(dist.get_backend()),
+                    same_device=bool(os.environ.get("FGV_BENCH_SAME_DEVICE")))
+    return dict(world_size=1, backend=None)
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -301,7 +309,6 @@ def cpu_c_validator(net, blks, labels, threads, target_s, expected=None):
 
 
 def run_block(args, world, rank, local, dev_fn):
-    import threading
 
     from fabric_amd import _lib, shard, txvalidator
     from fabric_amd.synth import blocks
@@ -412,17 +419,30 @@ def run_block(args, world, rank, local, dev_fn):
         integ["ms"] += (time.perf_counter() - t) * 1e3
         integ["ok"] &= all(r[0] == _lib.BLK_OK for r in res) and chain.number == first - 1 + B
 
+    # C5: the deliver side verifies a batch (VerifyBlock: header chain, well-formedness, one
+    # sequential SHA-256 data hash per block -- SURVEY H6) ahead of its validation: while the
+    # committer validates batch k, VerifyBlock of batches k+1 .. k+INTEG_DEPTH runs on host threads
+    # (one engine pool of FGV_HASH_THREADS per concurrent call); a step ends when its own batch
+    # has been both verified and validated.  Consecutive calls take consecutive batches of the
+    # rotation in every loop below.
+    from concurrent.futures import ThreadPoolExecutor
+    integ_ex = ThreadPoolExecutor(max_workers=args.integ_depth) if spec["integrity"] else None
+    integ_fut, seq = {}, [0]
+
     def step(bs, k):
-        th = None
-        if spec["integrity"]:  # concurrent with the committer pass, as in a pipelined peer
-            th = threading.Thread(target=verify_mine, args=(k,))
-            th.start()
+        s = None
+        if spec["integrity"]:
+            s = seq[0]
+            seq[0] += 1
+            for d in range(args.integ_depth + 1):
+                if s + d not in integ_fut:
+                    integ_fut[s + d] = integ_ex.submit(verify_mine, (k + d) % NB)
         bs.validate()
         if world > 1:
             shard.allgather_device(send, recv)
         f = bs.finalize()
-        if th is not None:
-            th.join()
+        if s is not None:
+            integ_fut.pop(s).result()
         return f
 
     def parity(k, flags):
@@ -589,6 +609,7 @@ def run_block(args, world, rank, local, dev_fn):
     LIVE = ("k_bd_sha_payload", "k_bd_parse", "k_bd_sha", "k_bd_ident+count", "k_point28")
     kavg = {k: round(v / K, 4) if k in LIVE else round(kdiag[k], 4) for k, v in kern.items()}
     out = dict(metric=METRIC, value=round(total_tx / el, 1), unit="validated tx/s", n_gpus=world, steps=K,
+               dist=_dist_info(world),
                warmup=args.warmup, ms_per_step=round(el / K * 1e3, 3), higher_is_better=True, scaling="weak",
                vs_baseline=None, dtype="u32", data="synthetic",
                config=dict(workload=spec["desc"].format(T=T),
@@ -643,6 +664,13 @@ def run_block(args, world, rank, local, dev_fn):
             one_thread=round(vr1 / vpt, 1),
             sample=f"{vn} identity.Verify (SHA-256 1.85KB + Go DER/low-S + OpenSSL P-256) in {vel:.1f}s = "
                    f"{vr:,.0f}/s on {cpu['procs']} threads, {vr1:,.0f}/s on 1, / {vpt:.2f} verifies per tx")
+    if integ_ex is not None:
+        for f in integ_fut.values():
+            f.result()
+        integ_ex.shutdown()
+        out["integrity_pipeline"] = dict(depth=args.integ_depth, hash_threads_per_call=int(os.environ.get(
+            "FGV_HASH_THREADS", "8")), note="VerifyBlock of the next batches runs on host threads while the "
+                                             "committer validates this one; integrity_ms sums the calls' times")
     eng.close()
     return out
 
@@ -753,6 +781,7 @@ def run_mvcc(args, world, rank, local, dev):
     mv_traffic, mv_src = pmc_traffic("mvcc")
     achieved = T * MVCC_BYTES_PER_TX / (per_block_ms / 1e3) / 1e9
     return dict(metric=METRIC, value=round(T * K * world / el, 1), unit="MVCC-validated tx/s", n_gpus=world, steps=K,
+                dist=_dist_info(world),
                 warmup=W, ms_per_step=round(el / K * 1e3, 3), higher_is_better=True, scaling="weak",
                 vs_baseline=None, dtype="u64", data="synthetic",
                 config=dict(workload=f"C3: {T}-tx blocks, {args.state_keys}-key state DB, 4R/4W, 5% intra-block "
@@ -834,6 +863,7 @@ def run_sig(args, world, rank, local, dev):
         dist.all_reduce(mn, op=dist.ReduceOp.MIN)
         el, ok = float(mx[0]), bool(mn[1] > 0)
     out = dict(metric=METRIC, value=round(n * world * args.steps / el, 1), unit="verifies/s", n_gpus=world,
+               dist=_dist_info(world),
                steps=args.steps, warmup=args.warmup, ms_per_step=round(el / args.steps * 1e3, 3),
                higher_is_better=True, scaling="weak", vs_baseline=None, dtype="u32", data="synthetic",
                config=dict(workload="C4: P-256 SignedData batch, 131072/GPU, 1.85KB msgs, 16 keys, "
@@ -880,6 +910,8 @@ def main():
     ap.add_argument("--batches", type=int, default=6,
                     help="distinct blocks-per-gpu batches rotated through the timed loop (block workload)")
     ap.add_argument("--c5-batches", type=int, default=1)
+    ap.add_argument("--integ-depth", type=int, default=2,
+                    help="c5: batches whose VerifyBlock runs ahead of their validation (concurrent host calls)")
     ap.add_argument("--cpu-threads", type=int, default=-1,
                     help="CPU baseline processes/threads (-1: this rank's CPU share, 0: skip the baseline)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall time of each CPU baseline sample")

@@ -292,20 +292,29 @@ static int verify_impl(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *block
       s.final(o.data_hash);
     }
   };
-  std::unique_lock<std::mutex> lk;
   if (ctx) {
-    lk = std::unique_lock<std::mutex>(ctx->integ_mu);
-    if (!ctx->integ_pool) {
+    // one block per job (each hash chain is sequential) on a pool of its own: concurrent calls
+    // (a deliver service verifying the next batches while the committer validates this one) each
+    // take a free pool instead of queueing behind one another
+    ThreadPool *pool = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(ctx->integ_mu);
+      if (!ctx->integ_free.empty()) {
+        pool = ctx->integ_free.back();
+        ctx->integ_free.pop_back();
+      }
+    }
+    if (!pool) {
       const char *e = getenv("FGV_HASH_THREADS");
       const int n = e ? atoi(e) : 8;
-      ctx->integ_pool = new ThreadPool(n > 0 ? (unsigned)n : 1u);
+      pool = new ThreadPool(n > 0 ? (unsigned)n : 1u);
     }
-    ctx->integ_pool->run(nblocks, work);  // one block per job: each hash chain is sequential
+    pool->run(nblocks, work);
+    std::lock_guard<std::mutex> lk(ctx->integ_mu);
+    ctx->integ_free.push_back(pool);
   } else {
     for (size_t i = 0; i < nblocks; i++) work(i);
   }
-
-  if (lk.owns_lock()) lk.unlock();
 
   // orderer-signature verdicts of every block that can reach the signature check (speculative:
   // the chain checks come below; verdicts are pure functions of the block and the channel model)
@@ -379,8 +388,8 @@ extern "C" int fgv_blocks_verify_signed(fgv_ctx *ctx, size_t nblocks, const uint
 }
 
 void fgv_integrity_free(fgv_ctx *c) {
-  delete c->integ_pool;
-  c->integ_pool = nullptr;
+  for (ThreadPool *p : c->integ_free) delete p;
+  c->integ_free.clear();
 }
 
 extern "C" int fgv_sha256_host(const uint8_t *buf, size_t n, uint8_t out[32]) {

@@ -177,7 +177,7 @@ struct fgv_ctx {
   uint64_t n_mvcc_reads = 0, n_mvcc_writes = 0;
   // deliver-side integrity (fgv_integrity.cpp): own host pool, own lock -- runs concurrently
   // with committer calls on the same context
-  ThreadPool *integ_pool = nullptr;
+  std::vector<ThreadPool *> integ_free;  // idle host pools (one per concurrent call, created on demand)
   std::mutex integ_mu;
   // device-resident committer path (blockdev.hip)
   bool stage_ran = false;
