@@ -2052,10 +2052,13 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     return (v == 16u || v == 32u) ? v : 64u;
   }();
   // FGV_PARSE_LDS = transactions per workgroup of the LDS-staged walk (k_bd_parse_lds: 4, 8 or 16,
-  // each envelope copied to LDS before the walk); 0 = the global walk above (A/B)
+  // each envelope copied to LDS before the walk); 0 (default) = the global walk above.  Measured on
+  // MI355X (C2 lean harness, one box): 8 per workgroup 1.01 ms per step against 0.67-0.71 for the
+  // global walk -- the walk is bound by instruction issue per wave (8 walking lanes of 64), not
+  // by the latency of its loads (profiles/round4_ab)
   static const uint32_t parse_lds = [] {
     const char *e = getenv("FGV_PARSE_LDS");
-    const uint32_t v = e ? (uint32_t)atoi(e) : 8u;
+    const uint32_t v = e ? (uint32_t)atoi(e) : 0u;
     return (v == 4u || v == 8u || v == 16u) ? v : 0u;
   }();
   // FGV_PARSE_IDENT=0: k_bd_ident as its own kernel after the LDS-staged parse (A/B); by default
