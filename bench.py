@@ -484,30 +484,17 @@ def run_block(args, world, rank, local, dev_fn):
     if mism:
         log(f"[bench] rank {rank}: {mism} flags differ from generator labels")
 
-    acc = dict(point=0.0, prep=0.0, sha=0.0, verifies=0, sha_blocks=0, pay_blocks=0)
-    kern = {n: 0.0 for n in _lib.Engine.KERNELS}
-    host = dict(parse_ms=0.0, assemble_ms=0.0, device_ms=0.0, fold_ms=0.0, front_ahead_ms=0.0)
-    # the last warmup call ran batch W-1 and announced batch W (mod NB): the timed loop starts there
+    # the last warmup call ran batch W-1 and announced batch W (mod NB): the timed loop starts there.
+    # Per-call diagnostics are summed inside the library (fgv_stats_sums) and read once after the
+    # loop: no library call per step besides the validation itself.
     start = args.warmup % NB
-    cur = [start]
-
-    def collect():
-        tm, cn = hsteps[cur[0] % NB].stats()
-        cur[0] += 1
-        for key, v in zip(("parse_ms", "assemble_ms", "device_ms", "fold_ms"), tm[4:]):
-            host[key] += v
-        acc["sha"] += tm[0]
-        acc["prep"] += tm[1]
-        acc["point"] += tm[2]
-        acc["sha_blocks"] += cn[1]
-        acc["verifies"] += cn[2]
-        kt, npay = eng.kernel_times()
-        for key, v in kt.items():
-            kern[key] += v
-        acc["pay_blocks"] += npay
-        host["front_ahead_ms"] += eng.front_ahead_ms()
-
-    el = timed(hsteps, args.steps, collect, start=start)
+    eng.stats_sums(reset=True)
+    el = timed(hsteps, args.steps, start=start)
+    sums = eng.stats_sums()
+    acc = dict(point=sums["point_ms"], prep=sums["prep_ms"], sha=sums["sha_ms"], verifies=sums["verifies"],
+               sha_blocks=sums["sha_blocks"], pay_blocks=sums["pay_blocks"])
+    kern = dict(sums["kernel_ms"])
+    host = {k: sums[k] for k in ("parse_ms", "assemble_ms", "device_ms", "fold_ms", "front_ahead_ms")}
     kstats = eng.key_stats()  # (vb_verifies_last: the last timed step's variable-base verifies)
     # per-kernel times of the back half need the timestamp events fgv_set_timing adds (each a
     # packet on the critical path): read them from an instrumented, untimed pass

@@ -20,7 +20,7 @@ EXPORTED = [
     "fgv_last_point_handovers", "fgv_last_kernel_times",
     "fgv_sha256_batch",
     "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset", "fgv_key_stats",
-    "fgv_set_block_outcomes", "fgv_last_block_status", "fgv_unsupported_stats",
+    "fgv_set_block_outcomes", "fgv_last_block_status", "fgv_unsupported_stats", "fgv_stats_sums",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
@@ -120,6 +120,7 @@ def load():
         L.fgv_keys_reset.argtypes = [vp]
         L.fgv_key_stats.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 5
         L.fgv_set_block_outcomes.argtypes = [vp, ctypes.c_int]
+        L.fgv_stats_sums.argtypes = [vp, vp, sz, ctypes.c_int]
         L.fgv_last_block_status.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
         L.fgv_unsupported_stats.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 3
         L.fgv_p256_verify_msgs_dev.argtypes = [vp] * 8 + [sz, vp]
@@ -488,6 +489,15 @@ class Engine:
         v = [ctypes.c_uint64() for _ in range(3)]
         _check(self._L.fgv_unsupported_stats(self._h, *[ctypes.byref(x) for x in v]))
         return dict(zip(("batches", "blocks", "txs"), (x.value for x in v)))
+
+    def stats_sums(self, reset=False):
+        """fgv_stats_sums: running sums of the per-call diagnostics (include/fgv.h layout)"""
+        out = (ctypes.c_double * 23)()
+        _check(self._L.fgv_stats_sums(self._h, out, 23, 1 if reset else 0))
+        v = list(out)
+        return dict(calls=int(v[0]), kernel_ms=dict(zip(self.KERNELS, v[1:11])), front_ahead_ms=v[12],
+                    pay_blocks=v[13], sha_blocks=v[14], verifies=v[15], sha_ms=v[16], prep_ms=v[17], point_ms=v[18],
+                    parse_ms=v[19], assemble_ms=v[20], device_ms=v[21], fold_ms=v[22])
 
     def front_ahead_ms(self):
         """fgv_last_kernel_times out[11]: host ms spent enqueueing the next batch's front half"""

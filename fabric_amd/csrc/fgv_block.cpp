@@ -2169,11 +2169,6 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   if (N == 0) return FGV_OK;
   c->t_host_parse = ms_since(t0);
   auto t1 = clk::now();
-  // the next batch's framing walk, on the host worker while this batch's GPU work runs
-  if (nx.n) {
-    fgv_block_presplit(S, c->device, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi);
-    c->next.n = 0;
-  }
   // --- back half on the main stream, enqueued without reading the job counts back: the verify
   // columns are sized for the batch's capacity (a creator + BD_MAX_END endorsements per tx) and
   // k_bd_emit leaves the verify count in device memory (misc[10]) for k_der ... k_point
@@ -2193,6 +2188,12 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
     if (B.stream != st) HIP_TRY(hipStreamWaitEvent(st, B.ev[6], 0));  // (a front half enqueued ahead)
     int rc = emit_prefix(c, S, B, st);
     if (rc) return rc;
+  }
+  // the next batch's framing walk, on the host worker while this batch's GPU work runs (started
+  // once the first kernels of this back half are queued: the GPU gets them a few us sooner)
+  if (nx.n) {
+    fgv_block_presplit(S, c->device, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi);
+    c->next.n = 0;
   }
   c->digests_ready = B.ev[8];  // (payload and the other digests, joined on stream3)
   c->digests_ready2 = nullptr;

@@ -24,6 +24,8 @@
 #include "fgv_internal.h"
 #include "fgv_kernels.h"
 
+static void stats_accumulate(fgv_ctx *c);
+
 // ======================================================================= key tiers
 // DESIGN.md s4a.  Every P-256 key the engine verifies against has an id.  Registered keys
 // (fgv_keys_register, channel identities, MSP CA keys) hold ids [0, pinned) for good; ad-hoc
@@ -489,7 +491,9 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
   if (c->vb_pending) {  // the variable-base items: + u1 * G and the x check, after k_vb_mul (streamV)
     c->vb_pending = false;
     HIP_TRY(hipStreamWaitEvent(c->stream, c->vb_ev[1], 0));
-    hipLaunchKernelGGL(k_vb_fin, dim3(2 * c->n_cu), dim3(256), 0, c->stream, N, d_status, c->gtab28.as<apoint_raw>(),
+    // a small grid: its per-item work is 12 mixed additions, and every workgroup ends with an
+    // atomic on one counter word (a 2 x n_cu grid spent ~40 us on those alone with an empty list)
+    hipLaunchKernelGGL(k_vb_fin, dim3(VB_FIN_WGS), dim3(256), 0, c->stream, N, d_status, c->gtab28.as<apoint_raw>(),
                        c->d1.as<int8_t>(), d_r, c->redo.as<uint32_t>(), c->vblist.as<uint32_t>(),
                        c->vbacc.as<uint32_t>());
     HIP_TRY(hipGetLastError());
@@ -1588,6 +1592,7 @@ int fgv_validate_shard_dev_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *
   int rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
   if (resolve_for_retry(c, rc, nblocks, blocks, lens))
     rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  if (rc == FGV_OK) stats_accumulate(c);
   if (c->next.n) {  // not started inside (host-parse path, empty batch, early error): start it now
     fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, c->next.lo, c->next.hi);
   }
@@ -1678,6 +1683,23 @@ int fgv_finalize_flags_dev_plan(fgv_ctx *c, size_t nblocks, const size_t *ntx, u
 int fgv_finalize_flags(size_t nblocks, const size_t *ntx, const fgv_tx_result *results, uint8_t *flags) {
   if (nblocks && (!ntx || !flags)) return FGV_EINVAL;
   return fgv_finalize_impl(nblocks, ntx, results, flags);
+}
+
+// the running sums of fgv_stats_sums, after a validation call (layout in include/fgv.h)
+static void stats_accumulate(fgv_ctx *c) {
+  double *a = c->stat_sum;
+  a[0] += 1;
+  for (int i = 0; i < 12; i++) a[1 + i] += c->t_kern[i];
+  a[13] += (double)c->n_pay_blocks;
+  a[14] += (double)c->n_sha_blocks;
+  a[15] += (double)c->n_verifies;
+  a[16] += c->t_sha;
+  a[17] += c->t_prep;
+  a[18] += c->t_point;
+  a[19] += c->t_host_parse;
+  a[20] += c->t_host_assemble;
+  a[21] += c->t_host_device;
+  a[22] += c->t_host_fold;
 }
 
 // Per-block outcomes of a call validated with fgv_set_block_outcomes on: blocks from `split` on
@@ -1801,6 +1823,7 @@ int fgv_validate_blocks_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *con
     if (!ub.empty() && fgv_msp_resolve_blocks_locked(c, ub.size(), ub.data(), ul.data(), &reg) == FGV_OK && reg > 0)
       rc = run();
   }
+  if (rc == FGV_OK) stats_accumulate(c);
   if (soft && rc == FGV_OK) {
     for (size_t b = 0; b < nblocks; b++) c->unsup_blocks += c->blk_status[b] == FGV_EUNSUPPORTED;
   } else if (rc == FGV_EUNSUPPORTED) {
@@ -1811,6 +1834,15 @@ int fgv_validate_blocks_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *con
     fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, nullptr, nullptr);
   c->next = fgv_ctx::NextBatch{};
   return rc;
+}
+
+int fgv_stats_sums(fgv_ctx *c, double *out, size_t n, int reset) {
+  if (!c || (n && !out)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (size_t i = 0; i < n; i++) out[i] = i < FGV_STAT_SUMS ? c->stat_sum[i] : 0.0;
+  if (reset)
+    for (double &x : c->stat_sum) x = 0;
+  return FGV_OK;
 }
 
 int fgv_set_block_outcomes(fgv_ctx *c, int on) {

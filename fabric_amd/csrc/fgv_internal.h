@@ -17,6 +17,7 @@
 #include "../../include/fgv.h"
 #include "fgv_kernels.h"
 
+#define FGV_STAT_SUMS 23
 struct fgv_block_state;
 struct fgv_mvcc_state;
 struct fgv_msp_cache;
@@ -140,6 +141,9 @@ struct fgv_ctx {
   std::vector<int32_t> blk_status;
   size_t n_final = 0;
   uint64_t unsup_batches = 0, unsup_blocks = 0, unsup_txs = 0;
+  // running sums of the per-call diagnostics (fgv_stats_sums): a benchmark reads them once after
+  // its timed loop instead of one library call per step inside it
+  double stat_sum[FGV_STAT_SUMS] = {};
   fgv_block_state *blk = nullptr;
   DevBuf bj_jobs, bj_sigp, bj_sigl, bj_slot, bj_didx, bj_dig, bj_vst, blk_arena;
   HostBuf hb_dig, hb_vst;
@@ -365,12 +369,14 @@ int fgv_block_sig_verdicts(fgv_ctx *c, size_t n, const fgv_sig_block *in, const 
 // variable-base kernels and is promoted by use
 int fgv_keys_register_locked(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots,
                              const uint8_t *want_comb = nullptr);
-// the comb policy of an identity by its role bits (fgv_identity_info.roles): keys of peers,
-// orderers, admins and identities whose roles are unknown are expected to sign often; keys of
-// identities with none of those roles (clients) start on the variable-base kernels
+// the comb policy of an identity by its role bits (fgv_identity_info.roles): a definite client
+// (CLIENT, and none of ADMIN / PEER / ORDERER: a NodeOU classification) signs rarely and starts on
+// the variable-base kernels; every other identity (peers, orderers, admins, unknown roles, MSPs
+// without NodeOUs) is expected to sign often.  Either way use promotes a key.
 inline bool fgv_roles_want_comb(uint32_t roles) {
   if (roles & FGV_ROLES_UNKNOWN) return true;
-  return (roles & ((1u << 1) | (1u << 3) | (1u << 4))) != 0;  // ADMIN, PEER, ORDERER
+  const bool client = (roles & (1u << 2)) != 0;
+  return !client || (roles & ((1u << 1) | (1u << 3) | (1u << 4))) != 0;
 }
 // the channel model of a block state (fgv_block.cpp)
 fgvb::Channel &fgv_block_channel(fgv_block_state *S);

@@ -214,6 +214,7 @@ __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *row
 // first VALID transaction is not known here -> the batch is unsupported (bit 2)
 __global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags,
                            uint32_t *unsup) {
+  __builtin_amdgcn_s_setprio(3);  // the last kernel of the back half; the next front half runs beside it
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   if (flags[p] != 0 || pslot[p] == 0xFFFFFFFFu) return;

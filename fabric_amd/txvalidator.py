@@ -33,8 +33,9 @@ class Identity:
 
 
 def roles_want_comb(roles):
-    """fgv_roles_want_comb (fgv_internal.h): unknown roles, or ADMIN / PEER / ORDERER"""
-    return roles is None or bool(roles & ((1 << 1) | (1 << 3) | (1 << 4)))
+    """fgv_roles_want_comb (fgv_internal.h): anything but a definite client (CLIENT without
+    ADMIN / PEER / ORDERER)"""
+    return roles is None or not (roles & (1 << 2)) or bool(roles & ((1 << 1) | (1 << 3) | (1 << 4)))
 
 
 def _as_identity(entry):

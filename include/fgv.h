@@ -77,6 +77,13 @@ int fgv_last_counts(fgv_ctx *ctx, uint64_t *sha_jobs, uint64_t *sha_blocks, uint
  * payload hashes (k_bd_sha_payload's work); out[11] = host ms the pipelined call spent enqueueing
  * the next batch's front half (its framing walk's join included).  n entries are written. */
 int fgv_last_kernel_times(fgv_ctx *ctx, double *out, size_t n);
+/* Running sums over the block calls since the last reset (fgv_validate_blocks[_pipelined],
+ * fgv_validate_shard_dev[_pipelined]) of the per-call diagnostics above, so that a benchmark reads
+ * them once after its timed loop: out[0] calls, [1..12] fgv_last_kernel_times out[0..11] (ms; [10]
+ * the payload compressions), [13] payload compressions, [14] SHA-256 compressions, [15] verifies,
+ * [16..18] fgv_last_timing sha / prep / point ms, [19..22] fgv_last_host_timing parse / assemble /
+ * device / fold ms.  reset != 0 zeroes them after the read. */
+int fgv_stats_sums(fgv_ctx *ctx, double *out, size_t n, int reset);
 // Diagnostics: verifies of the last call that the fast point kernel (radix 2^28, incomplete
 // formulas) handed to the exact kernel because an exceptional addition occurred (P = +-Q).
 // Zero for honest inputs; reads one counter back from the device.

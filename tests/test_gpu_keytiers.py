@@ -231,7 +231,7 @@ def test_churn_blocks_all_creators_distinct(mode):
         eng.set_parse_mode(mode)
         txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes)
         ks = eng.key_stats()
-        assert ks["comb"] == 3 + 0 and ks["vb"] >= 3000, ks  # the 3 peers hot; clients + the forged one cold
+        assert ks["comb"] == 3 + 1 and ks["vb"] == 3000, ks  # the 3 peers and the forged identity hot, clients cold
         blks = [blocks.make_block(net, 500, number=1 + i, seed=40 + i)[0] for i in range(3)]
         got = eng.validate_blocks(blks)
         m = v20.ChannelModel(net.channel, net.identities(), net.chaincodes)
