@@ -494,7 +494,8 @@ def run_block(args, world, rank, local, dev_fn):
     acc = dict(point=sums["point_ms"], prep=sums["prep_ms"], sha=sums["sha_ms"], verifies=sums["verifies"],
                sha_blocks=sums["sha_blocks"], pay_blocks=sums["pay_blocks"])
     kern = dict(sums["kernel_ms"])
-    host = {k: sums[k] for k in ("parse_ms", "assemble_ms", "device_ms", "fold_ms", "front_ahead_ms")}
+    host = {k: sums[k] for k in ("parse_ms", "assemble_ms", "device_ms", "fold_ms", "front_ahead_ms", "gap_ms",
+                                 "finish_ms")}
     kstats = eng.key_stats()  # (vb_verifies_last: the last timed step's variable-base verifies)
     # per-kernel times of the back half need the timestamp events fgv_set_timing adds (each a
     # packet on the critical path): read them from an instrumented, untimed pass

@@ -492,12 +492,12 @@ class Engine:
 
     def stats_sums(self, reset=False):
         """fgv_stats_sums: running sums of the per-call diagnostics (include/fgv.h layout)"""
-        out = (ctypes.c_double * 23)()
-        _check(self._L.fgv_stats_sums(self._h, out, 23, 1 if reset else 0))
+        out = (ctypes.c_double * 25)()
+        _check(self._L.fgv_stats_sums(self._h, out, 25, 1 if reset else 0))
         v = list(out)
         return dict(calls=int(v[0]), kernel_ms=dict(zip(self.KERNELS, v[1:11])), front_ahead_ms=v[12],
                     pay_blocks=v[13], sha_blocks=v[14], verifies=v[15], sha_ms=v[16], prep_ms=v[17], point_ms=v[18],
-                    parse_ms=v[19], assemble_ms=v[20], device_ms=v[21], fold_ms=v[22])
+                    parse_ms=v[19], assemble_ms=v[20], device_ms=v[21], fold_ms=v[22], gap_ms=v[23], finish_ms=v[24])
 
     def front_ahead_ms(self):
         """fgv_last_kernel_times out[11]: host ms spent enqueueing the next batch's front half"""

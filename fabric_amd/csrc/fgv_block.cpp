@@ -2189,6 +2189,9 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
     int rc = emit_prefix(c, S, B, st);
     if (rc) return rc;
   }
+  // host time from the end of the previous validation call to this call's first back-half kernel
+  // (the caller's own work between calls included)
+  c->t_gap = c->t_call_end.time_since_epoch().count() ? ms_since(c->t_call_end) : 0.0;
   // the next batch's framing walk, on the host worker while this batch's GPU work runs (started
   // once the first kernels of this back half are queued: the GPU gets them a few us sooner)
   if (nx.n) {
@@ -2294,6 +2297,7 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   if (B.misc_src) HIP_TRY(hipMemcpyAsync(B.misc.p, B.misc_src, 64, hipMemcpyDeviceToHost, c->stream));
   B.misc_src = nullptr;
   HIP_TRY(fgv_stream_wait(c->stream, c->spin));
+  const auto t_woke = clk::now();
   fgv_read_block_job_times(c);
   {  // per-kernel device times (fgv_last_kernel_times)
     auto el = [&](hipEvent_t a, hipEvent_t b) {
@@ -2324,6 +2328,7 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   if (B.N) S->nv_per_tx = (double)hm[10] / B.N;  // the next batch's lanes-per-verify estimate
   c->t_host_device = std::chrono::duration<double, std::milli>(clk::now() - S->t_enq).count();
   c->t_host_fold = 0;
+  c->t_finish = std::chrono::duration<double, std::milli>(clk::now() - t_woke).count();
   if ((hm[5] & 1u) || B.force_host) return 1;
   // per-block outcomes: the undecided transactions carry 0xFD in the flags, the first block that
   // must wait for an earlier one's commit comes back in word 12 (k_bd_kl)

@@ -254,7 +254,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   }
   if (!c->g_ok.ensure(16) || !c->gtab28.ensure(GT_BYTES) || !c->redo.ensure(64) ||
       !c->ktab28.ensure((size_t)c->key_slots * KT_BYTES) || !c->key_ok.ensure(c->key_ids) ||
-      !c->kmap.ensure((size_t)c->key_ids * 4) || !c->vbq.ensure((size_t)c->key_ids * 64) ||
+      !c->kmap.ensure((size_t)c->key_ids * 4) || !c->vbq.ensure((size_t)c->key_ids * VBQ_WORDS * 4) ||
       !c->vbuse.ensure((size_t)c->key_ids * 4) || !c->vbpromo.ensure((VB_PROMO_CAP + 2) * 4) ||
       !c->h_promo.ensure((VB_PROMO_CAP + 2) * 4))
     return fail(FGV_ENOMEM);
@@ -483,7 +483,10 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
                        c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo,
                        c->kmap.as<uint32_t>());
   }
-  hipLaunchKernelGGL(k_point, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, dn, L, d_status, d_slot,
+  // (after k_point28 a small grid: honest batches hand nothing over, and an empty launch of 2 x n_cu
+  // workgroups waited ~50 us for CUs beside the next batch's front half)
+  hipLaunchKernelGGL(k_point, dim3(redo ? POINT_EXACT_WGS : 2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, dn, L,
+                     d_status, d_slot,
                      c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo,
                      c->kmap.as<uint32_t>());
   c->last_lanes = L;
@@ -1293,10 +1296,19 @@ static int fin_back(fgv_ctx *c, hipStream_t st, const FinPlan &F, const uint8_t 
                      c->fz_blkof.as<uint32_t>(), c->fz_owner.as<uint32_t>(), c->fz_minblk.as<int32_t>(),
                      c->fz_minvalid.as<uint32_t>(), mask, c->fin_seed, c->fz_flags.as<uint8_t>(),
                      c->fz_pslot.as<uint32_t>(), keys);
+  // the final flags go straight into the pinned host buffer (mapped): a 16 KB D2H copy behind the
+  // last kernel ran as a blit kernel that waited ~50 us for CUs held by the next batch's front
+  // half (MI355X C2 trace).  FGV_FLAGS_ZC=0: the copy (A/B)
+  static const bool zc_on = [] {
+    const char *e = getenv("FGV_FLAGS_ZC");
+    return !e || atoi(e) != 0;
+  }();
+  uint8_t *zc = nullptr;
+  if (zc_on && hipHostGetDevicePointer(reinterpret_cast<void **>(&zc), c->hb_fflags.p, 0) != hipSuccess) zc = nullptr;
   hipLaunchKernelGGL(k_fin_dups, grid, blk, 0, st, n32, c->fz_pslot.as<uint32_t>(), c->fz_minvalid.as<uint32_t>(),
-                     c->fz_flags.as<uint8_t>(), codes_done ? c->fold_unsup : nullptr);
+                     c->fz_flags.as<uint8_t>(), codes_done ? c->fold_unsup : nullptr, zc);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(c->hb_fflags.p, c->fz_flags.p, F.P, hipMemcpyDeviceToHost, st));
+  if (!zc) HIP_TRY(hipMemcpyAsync(c->hb_fflags.p, c->fz_flags.p, F.P, hipMemcpyDeviceToHost, st));
   return FGV_OK;
 }
 
@@ -1593,6 +1605,7 @@ int fgv_validate_shard_dev_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *
   if (resolve_for_retry(c, rc, nblocks, blocks, lens))
     rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
   if (rc == FGV_OK) stats_accumulate(c);
+  c->t_call_end = std::chrono::steady_clock::now();
   if (c->next.n) {  // not started inside (host-parse path, empty batch, early error): start it now
     fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, c->next.lo, c->next.hi);
   }
@@ -1700,6 +1713,8 @@ static void stats_accumulate(fgv_ctx *c) {
   a[20] += c->t_host_assemble;
   a[21] += c->t_host_device;
   a[22] += c->t_host_fold;
+  a[23] += c->t_gap;
+  a[24] += c->t_finish;
 }
 
 // Per-block outcomes of a call validated with fgv_set_block_outcomes on: blocks from `split` on
@@ -1824,6 +1839,7 @@ int fgv_validate_blocks_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *con
       rc = run();
   }
   if (rc == FGV_OK) stats_accumulate(c);
+  c->t_call_end = std::chrono::steady_clock::now();
   if (soft && rc == FGV_OK) {
     for (size_t b = 0; b < nblocks; b++) c->unsup_blocks += c->blk_status[b] == FGV_EUNSUPPORTED;
   } else if (rc == FGV_EUNSUPPORTED) {

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -17,7 +18,7 @@
 #include "../../include/fgv.h"
 #include "fgv_kernels.h"
 
-#define FGV_STAT_SUMS 23
+#define FGV_STAT_SUMS 25
 struct fgv_block_state;
 struct fgv_mvcc_state;
 struct fgv_msp_cache;
@@ -144,6 +145,8 @@ struct fgv_ctx {
   // running sums of the per-call diagnostics (fgv_stats_sums): a benchmark reads them once after
   // its timed loop instead of one library call per step inside it
   double stat_sum[FGV_STAT_SUMS] = {};
+  std::chrono::steady_clock::time_point t_call_end{};  // end of the last validation call
+  double t_gap = 0, t_finish = 0;  // host ms: previous call's end -> first kernel; the finish after its wait
   fgv_block_state *blk = nullptr;
   DevBuf bj_jobs, bj_sigp, bj_sigl, bj_slot, bj_didx, bj_dig, bj_vst, blk_arena;
   HostBuf hb_dig, hb_vst;

@@ -33,6 +33,7 @@
 #define PREP_B 2                            // items per lane in the batched inversion
 #define POINT_THREADS 256   // 4 waves per workgroup, 2 x n_cu workgroups: 2 waves per SIMD, <= 256 VGPRs
 #define POINT_LANES_MAX 8    // lanes cooperating on one verify in k_point (partial sums + tree)
+#define POINT_EXACT_WGS 64   // k_point's grid behind k_point28 (the hand-overs: exceptional additions only)
 #define DIG_STRIDE 96        // bytes per item of the digit array (G digits, then Q digits at DIG_Q_OFF)
 #define ST_PENDING 0xFF
 
@@ -51,10 +52,12 @@ __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw 
                          jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys);
 // Key tiers.  Every key has an id; kmap[id] is its comb slot (the 5.2 MB table
 // above) or KEY_NONE: the variable-base kernel k_point_vb verifies it from its coordinates alone
-// (vbq[id]: Montgomery-256 x || y, 64 B).  k_keyprep checks new keys (on the curve) and writes
-// vbq / key_ok; k_kmap_set points ids at their freshly built comb tables (after k_keytab).
+// (vbq[id]: the slice bases 2^(32 s) Q, s < 8, affine Montgomery-256, 512 B).  k_keyprep checks
+// new keys (on the curve) and writes vbq / key_ok; k_kmap_set points ids at their freshly built comb tables (after k_keytab).
 #define KEY_NONE 0xFFFFFFFFu
 #define VB_THREADS 256      // k_vb_mul workgroup (grid 2 x n_cu: each lane owns a scratch table)
+#define VB_LANES 8          // k_vb_mul lanes per item (32-bit slices of u2)
+#define VBQ_WORDS (VB_LANES * 16)  // per key id: the slice bases 2^(32 s) Q, affine Montgomery-256
 #define VB_TAB 15           // per-lane table 1Q .. 15Q (4-bit fixed windows), Jacobian
 #define VB_TAB_WORDS 24     // x, y, z (Montgomery-256)
 // counters in the context's redo words: [0] k_point28 hand-overs, [1] k_point28 chunks, [2] k_point
@@ -199,4 +202,5 @@ __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *row
                             uint64_t seed, uint8_t *flags, uint32_t *pslot, const uint8_t *keys);
 __global__ void k_fin_index_dev(uint32_t P, const DevTx *txs, const uint64_t *bases, const uint8_t *digests,
                                 uint8_t *keys, uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed, uint32_t prio);
-__global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags, uint32_t *unsup);
+__global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags, uint32_t *unsup,
+                           uint8_t *out);

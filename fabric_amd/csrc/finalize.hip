@@ -213,17 +213,23 @@ __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *row
 // of a txid was later failed by the key-level walk (blockdev.hip kl_walk_block), so the txid's
 // first VALID transaction is not known here -> the batch is unsupported (bit 2)
 __global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags,
-                           uint32_t *unsup) {
+                           uint32_t *unsup, uint8_t *out) {
   __builtin_amdgcn_s_setprio(3);  // the last kernel of the back half; the next front half runs beside it
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  if (flags[p] != 0 || pslot[p] == 0xFFFFFFFFu) return;
-  const uint32_t m = minvalid[pslot[p]];
-  if (m >= p) return;
-  if (unsup && flags[m] != 0) {  // the first VALID position was failed by the key-level walk
-    atomicOr(unsup, 2u);
-    flags[p] = 0xFD;  // (undecided: the per-block outcomes mark its block unsupported)
-    return;
+  uint8_t f = flags[p];
+  if (f == 0 && pslot[p] != 0xFFFFFFFFu) {
+    const uint32_t m = minvalid[pslot[p]];
+    if (m < p) {
+      if (unsup && flags[m] != 0) {  // the first VALID position was failed by the key-level walk
+        atomicOr(unsup, 2u);
+        f = 0xFD;  // (undecided: the per-block outcomes mark its block unsupported)
+      } else {
+        f = 9;  // markTXIdDuplicates: an earlier VALID tx of this block
+      }
+      flags[p] = f;
+    }
   }
-  flags[p] = 9;  // markTXIdDuplicates: an earlier VALID tx of this block
+  // (out: the caller's pinned flag buffer, mapped -- no copy kernel behind this one)
+  if (out) out[p] = f;
 }

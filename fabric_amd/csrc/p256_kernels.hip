@@ -17,9 +17,10 @@
 //             checked projectively.  k_point (exact radix-2^32 arithmetic, complete formulas)
 //             finishes the items whose sum hit an exceptional addition.
 //   keys without a comb (kmap[id] == KEY_NONE; k_inv lists their items):
-//   k_vb_mul  (one lane per listed item, beside the hashes: u2 = r * s^-1 needs no digest) --
-//             u2 * Q by 4-bit fixed windows over a per-lane table 1Q..15Q: 256 doublings and <= 64
-//             additions, exact formulas;
+//   k_vb_mul  (8 lanes per listed item, beside the hashes: u2 = r * s^-1 needs no digest) --
+//             u2 * Q as the sum over 32-bit slices of u2 against the key's slice bases 2^(32 s) Q
+//             (k_keyprep): per lane a 1Q..15Q table, 28 doublings and <= 8 additions, then a
+//             butterfly across the lanes; exact formulas;
 //   k_vb_fin  (after k_prep) -- + u1 * G from the generator comb (12 terms), x_R check.
 //
 // Semantics restated: Go 1.21.9 crypto/ecdsa verifyNISTEC (SEC 1 v2 s4.1.4) behind
@@ -780,8 +781,9 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
 
 // ---------------------------------------------------------------- keys without a comb
 // k_keyprep: new key ids -> on-curve bit (k_inv reports 5 for a key off the curve, before the
-// range checks, as ecdsa.Verify does) and the Montgomery coordinates the variable-base kernel reads.
-// qxy: [nkeys][16] plain little-endian limbs (x then y).
+// range checks, as ecdsa.Verify does) and the variable-base kernel's slice bases
+// Q_s = 2^(32 s) * Q, s = 0..VB_LANES-1 (affine Montgomery-256, vbq[id][s]: 32 doublings apart,
+// one inversion for all seven Z's).  qxy: [nkeys][16] plain little-endian limbs (x then y).
 __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy, const uint32_t *__restrict__ ids,
                                                 uint32_t nkeys, uint32_t *__restrict__ vbq,
                                                 uint8_t *__restrict__ key_ok) {
@@ -796,9 +798,44 @@ __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy
   const bool ok = on_curve(x, y, xm, ym);
   const uint32_t id = ids[k];
   key_ok[id] = ok ? 1 : 0;
-  if (!ok) fe_set_zero(xm), fe_set_zero(ym);
-  store_fe(vbq + (size_t)id * 16, xm);
-  store_fe(vbq + (size_t)id * 16 + 8, ym);
+  uint32_t *o = vbq + (size_t)id * VBQ_WORDS;
+  if (!ok) {
+    fe z;
+    fe_set_zero(z);
+    for (int s = 0; s < VB_LANES; s++) store_fe(o + 16 * s, z), store_fe(o + 16 * s + 8, z);
+    return;
+  }
+  store_fe(o, xm);
+  store_fe(o + 8, ym);
+  // Q_s in Jacobian (never infinity: 2^(32 s) < n), Z's multiplied up for one inversion
+  jpoint q[VB_LANES];
+  q[0].x = xm;
+  q[0].y = ym;
+  fe_set_one(q[0].z);
+  fe pref[VB_LANES];
+  pref[0] = q[0].z;
+  for (int s = 1; s < VB_LANES; s++) {
+    q[s] = q[s - 1];
+#pragma unroll 1
+    for (int d = 0; d < 32; d++) {
+      jpoint t2 = q[s];
+      pt_dbl(q[s], t2);
+    }
+    fe_mul(pref[s], pref[s - 1], q[s].z);
+  }
+  fe inv;
+  fe_inv(inv, pref[VB_LANES - 1]);
+  for (int s = VB_LANES - 1; s >= 1; s--) {
+    fe zinv, z2, z3, ax, ay;
+    fe_mul(zinv, inv, pref[s - 1]);  // Z_s^-1
+    fe_mul(inv, inv, q[s].z);
+    fe_sqr(z2, zinv);
+    fe_mul(z3, z2, zinv);
+    fe_mul(ax, q[s].x, z2);
+    fe_mul(ay, q[s].y, z3);
+    store_fe(o + 16 * s, ax);
+    store_fe(o + 16 * s + 8, ay);
+  }
 }
 // ids whose comb tables k_keytab has just built (stream order) now take the comb path
 __global__ __launch_bounds__(64) void k_kmap_set(const uint32_t *__restrict__ ids, const uint32_t *__restrict__ slots,
@@ -807,13 +844,13 @@ __global__ __launch_bounds__(64) void k_kmap_set(const uint32_t *__restrict__ id
   if (k < n) kmap[ids[k]] = slots[k];
 }
 
-// one item per lane: a wave takes 64 consecutive list entries per atomic from `take`; every lane
-// of the wave runs the same number of rounds (the count is read once)
-FGV_DEV bool vb_next(uint32_t *take, uint32_t cnt, uint32_t &j) {
+// `per` items per wave, taken per atomic from `take`; every lane of the wave runs the same
+// number of rounds (the count is read once).  j = the wave's first item of the round.
+FGV_DEV bool vb_next(uint32_t *take, uint32_t cnt, uint32_t per, uint32_t &j) {
   uint32_t b = 0;
-  if (__lane_id() == 0) b = atomicAdd(take, 64u);
+  if (__lane_id() == 0) b = atomicAdd(take, per);
   b = __builtin_amdgcn_readfirstlane(b);
-  j = b + __lane_id();
+  j = b;
   return b < cnt;
 }
 FGV_DEV void store_jp(uint32_t *d, const jpoint &p) {
@@ -829,13 +866,17 @@ FGV_DEV void load_jp(jpoint &p, const uint32_t *s) {
 
 // k_vb_mul: acc[j] = u2 * Q for list entry j (item i = list[j], key id key_slot[i]), u2 = r * s^-1
 // (plain; k_inv's w is s^-1 in Montgomery form) -- needs no digest, so it runs beside the hashes.
-// Left-to-right 4-bit fixed windows over the lane's table T[d-1] = d * Q (d = 1..15, Jacobian, in
-// the lane's scratch row; each entry of the next window is loaded one window ahead): 256
-// doublings, <= 64 additions, complete formulas (pt_dbl / pt_add_inl / pt_madd), so the result is
-// exact for every input.  Cost per verify ~ 256 x (3M + 5S) + 64 x (12M + 4S) + 14 x (8M + 3S):
-// ~9x a comb verify, one serial chain per item.  uses[id] counts the key's
-// variable-base verifies; the one that reaches `promote` queues the id (promo[0] count, ids from
-// promo[2]) for a comb build by the host; promo[1] = the batch's variable-base items.
+// VB_LANES lanes per item: lane s takes the 32 bits u2[s] of the scalar against its slice base
+// Q_s = 2^(32 s) Q (k_keyprep), so u2 * Q = sum_s u2[s] * Q_s:
+//   table T[d-1] = d * Q_s, d = 1..15 (Jacobian, the lane's scratch row; 14 mixed additions);
+//   8 windows of 4 bits, left to right: 28 doublings and <= 8 additions (each next entry loaded
+//   during the doublings);
+//   a 3-level butterfly of complete additions across the 8 lanes (cross-lane shuffles).
+// Complete formulas throughout (pt_madd / pt_dbl / pt_add_inl): exact for every input.  Per lane
+// ~560 field multiplications, the item's serial chain ~6x shorter than one lane doing all 256
+// doublings.  uses[id] counts the key's variable-base verifies; the one that
+// reaches `promote` queues the id (promo[0] count, ids from promo[2]) for a comb build by the host;
+// promo[1] = the batch's variable-base items.
 __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_t *__restrict__ key_slot,
                                                       const uint32_t *__restrict__ vbq,
                                                       const uint32_t *__restrict__ r_limbs,
@@ -849,10 +890,13 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_
   const uint32_t cnt = ctr[RD_VB_CNT];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&promo[1], cnt);  // (statistics: fgv_key_stats)
   if (cnt == 0) return;
+  const uint32_t lane = __lane_id(), sl = lane % VB_LANES, base = lane - sl;
+  constexpr uint32_t PER = 64u / VB_LANES;  // items per wave and round
   uint32_t *tab = scratch + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * (VB_TAB * VB_TAB_WORDS);
-  uint32_t j;
-  while (vb_next(take, cnt, j)) {
-    if (j >= cnt) continue;
+  uint32_t j0;
+  while (vb_next(take, cnt, PER, j0)) {
+    const uint32_t j = j0 + lane / VB_LANES;
+    if (j >= cnt) continue;  // (uniform within the lane group: its partners skip too)
     const uint32_t i = list[j];
     const uint32_t id = key_slot[i];
     uint32_t r[8], w[8], u2[8];
@@ -862,10 +906,13 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_
       w[k] = w_in[(size_t)k * n + i];
     }
     sn_mul(u2, r, w);
+    uint32_t dg = u2[0];  // this lane's 32 bits: u2[sl] (a select chain: no private array)
+#pragma unroll
+    for (int k = 1; k < 8; k++) dg = sl == (uint32_t)k ? u2[k] : dg;
     apoint q;
-    load_fe(q.x, vbq + (size_t)id * 16);
-    load_fe(q.y, vbq + (size_t)id * 16 + 8);
-    {  // T[0] = Q, T[d-1] = T[d-2] + Q (pt_madd routes 2Q to a doubling)
+    load_fe(q.x, vbq + (size_t)id * VBQ_WORDS + 16 * sl);
+    load_fe(q.y, vbq + (size_t)id * VBQ_WORDS + 16 * sl + 8);
+    {  // T[0] = Q_s, T[d-1] = T[d-2] + Q_s (pt_madd routes 2 Q_s to a doubling)
       jpoint t;
       t.x = q.x;
       t.y = q.y;
@@ -882,19 +929,16 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_
     fe_set_zero(a.x);
     fe_set_zero(a.y);
     fe_set_zero(a.z);
-    // windows from the top: the top nibble of u2 is shifted out each round
-    uint32_t d = u2[7] >> 28;
+    uint32_t d = dg >> 28;
     jpoint e;
     if (d) load_jp(e, tab + (d - 1) * VB_TAB_WORDS);
 #pragma unroll 1
-    for (int win = 63; win >= 0; win--) {
-#pragma unroll
-      for (int k = 7; k > 0; k--) u2[k] = (u2[k] << 4) | (u2[k - 1] >> 28);
-      u2[0] <<= 4;
-      const uint32_t dn = u2[7] >> 28;  // the next window's digit (0 after the last)
+    for (int win = 7; win >= 0; win--) {
+      dg <<= 4;
+      const uint32_t dn = dg >> 28;  // the next window's digit (0 after the last)
       jpoint en;
       if (win > 0 && dn) load_jp(en, tab + (dn - 1) * VB_TAB_WORDS);  // (in flight during the doublings)
-      if (win < 63) {
+      if (win < 7) {
 #pragma unroll 1
         for (int k = 0; k < 4; k++) {
           jpoint t2 = a;
@@ -908,6 +952,21 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_
       d = dn;
       e = en;
     }
+    // butterfly: at level m lane s adds lane s ^ m's partial sum; lane 0 of the group ends with all
+#pragma unroll 1
+    for (uint32_t m = 1; m < VB_LANES; m <<= 1) {
+      jpoint o;
+      const int src = (int)(base + (sl ^ m));
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        o.x.v[k] = (uint32_t)__shfl((int)a.x.v[k], src);
+        o.y.v[k] = (uint32_t)__shfl((int)a.y.v[k], src);
+        o.z.v[k] = (uint32_t)__shfl((int)a.z.v[k], src);
+      }
+      jpoint t2 = a;
+      pt_add_inl(a, t2, o);
+    }
+    if (sl != 0) continue;
     store_jp(acc + (size_t)j * VB_TAB_WORDS, a);
     const uint32_t u = atomicAdd(&uses[id], 1u);
     if (u + 1u == promote) {
@@ -927,8 +986,9 @@ __global__ __launch_bounds__(256) void k_vb_fin(uint32_t n, uint8_t *__restrict_
                                                 const uint32_t *__restrict__ list, const uint32_t *__restrict__ acc) {
   __builtin_amdgcn_s_setprio(3);
   const uint32_t cnt = ctr[RD_VB_CNT];
-  uint32_t j;
-  while (cnt && vb_next(ctr + RD_VB_FIN, cnt, j)) {
+  uint32_t j0;
+  while (cnt && vb_next(ctr + RD_VB_FIN, cnt, 64u, j0)) {
+    const uint32_t j = j0 + __lane_id();  // one item per lane
     if (j >= cnt) continue;
     const uint32_t i = list[j];
     jpoint a;

@@ -82,7 +82,9 @@ int fgv_last_kernel_times(fgv_ctx *ctx, double *out, size_t n);
  * them once after its timed loop: out[0] calls, [1..12] fgv_last_kernel_times out[0..11] (ms; [10]
  * the payload compressions), [13] payload compressions, [14] SHA-256 compressions, [15] verifies,
  * [16..18] fgv_last_timing sha / prep / point ms, [19..22] fgv_last_host_timing parse / assemble /
- * device / fold ms.  reset != 0 zeroes them after the read. */
+ * device / fold ms, [23] host ms from the end of the previous call to the call's first back-half
+ * kernel (the caller's work between calls included), [24] host ms of the call after its final
+ * wait.  reset != 0 zeroes them after the read. */
 int fgv_stats_sums(fgv_ctx *ctx, double *out, size_t n, int reset);
 // Diagnostics: verifies of the last call that the fast point kernel (radix 2^28, incomplete
 // formulas) handed to the exact kernel because an exceptional addition occurred (P = +-Q).
