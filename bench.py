@@ -41,6 +41,10 @@ METRIC = "ECDSA-P256 verifies/sec + validated tx/sec per block at 1/2/4/8 MI355X
 # 22-bit generator windows + 20 signed 13-bit key windows), the first one loaded, so 31 mixed
 # additions x (8 field mults x 64 + 3 squarings x 36 products) + the projective x-check (3 x 64)
 PRODUCTS_POINT = 31 * (8 * 64 + 3 * 36) + 3 * 64
+# the same for one variable-base verify in k_vb_mul: 8 lanes, each 14 mixed
+# additions (table d * Q_s), 28 doublings (3 mults + 5 squarings), 7.5 expected window additions
+# and 3 butterfly additions (12 mults + 4 squarings), + u2 = r * s^-1 (sn_mul, 128 products)
+VB_MUL_PRODUCTS = 8 * (14 * (8 * 64 + 3 * 36) + 28 * (3 * 64 + 5 * 36) + 10.5 * (12 * 64 + 4 * 36) + 128)
 # chip-wide v_mad_u64_u32 issue rate measured by tools/valu_peak.hip (profiles/round1_valu_peak.json)
 PEAK_MAD_PER_S = float(os.environ.get("FGV_PEAK_MAD", "3.106e13"))
 # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz simple int32 VALU lane-ops
@@ -81,6 +85,16 @@ def roofline(n_verifies, point_ms, workload):
                 kernel="k_point28 (+ k_point hand-overs)",
                 kernel_avg_ms=round(point_ms, 4), per_launch_products=int(n_verifies * PRODUCTS_POINT),
                 work_unit="v_mad_u64_u32 (32x32->64 multiply-add) products of the comb algorithm")
+
+
+def roofline_vb(n_items, vb_ms):
+    """k_vb_mul (the churn variants' dominant kernel) against the same v_mad_u64_u32 peak"""
+    t = vb_ms / 1e3
+    achieved = n_items * VB_MUL_PRODUCTS / t / 1e12 if t > 0 else 0.0
+    return dict(bound="valu", achieved=round(achieved, 3), peak=round(PEAK_MAD_PER_S / 1e12, 3), unit="Tops/s",
+                frac=round(achieved * 1e12 / PEAK_MAD_PER_S, 4), traffic=None, traffic_source=None,
+                kernel="k_vb_mul", kernel_avg_ms=round(vb_ms, 4), per_launch_products=int(n_items * VB_MUL_PRODUCTS),
+                work_unit="v_mad_u64_u32 products of the 8-lane variable-base multiplication u2 * Q")
 
 
 def profiled_dominant(workload="block"):
@@ -795,10 +809,17 @@ def run_sig(args, world, rank, local, dev):
     from fabric_amd.synth.workloads import sig_pool
 
     n = args.per_gpu
-    uniq = min(n, 16384)
-    pool = sig_pool(uniq, seed=1000 + rank)
+    nkeys = args.sig_keys
+    churn = nkeys > 16
+    # churn: as many distinct messages as keys (every item its own key when --sig-keys >= per-gpu)
+    uniq = min(n, max(16384, nkeys))
+    pool = sig_pool(uniq, seed=1000 + rank, nkeys=min(nkeys, uniq))
     eng = _lib.Engine(local)
-    slots_u = eng.keys_register(np.frombuffer(b"".join(k.pub for k in pool["keys"]), np.uint8).reshape(-1, 64))
+    # churn keys are registered cold (fgv_keys_register_tiered, hot=0): the variable-base kernels,
+    # no 5.2 MB comb per key -- a signer population that each signs about once per batch
+    slots_u = eng.keys_register(np.frombuffer(b"".join(k.pub for k in pool["keys"]), np.uint8).reshape(-1, 64),
+                                hot=False if churn else None)
+    kstats = eng.key_stats()
     idx = np.arange(n) % uniq
     msgs = np.ascontiguousarray(pool["msgs"][idx])
     msg_len = np.full(n, msgs.shape[1], np.uint32)
@@ -832,13 +853,14 @@ def run_sig(args, world, rank, local, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    acc = dict(point=0.0, prep=0.0, sha=0.0)
+    acc = dict(point=0.0, prep=0.0, sha=0.0, vb=0.0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tm = step()
         acc["point"] += tm["point_ms"]
         acc["prep"] += tm["prep_ms"]
         acc["sha"] += tm["sha_ms"]
+        acc["vb"] += tm["vb_mul_ms"]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -854,13 +876,16 @@ def run_sig(args, world, rank, local, dev):
                dist=_dist_info(world),
                steps=args.steps, warmup=args.warmup, ms_per_step=round(el / args.steps * 1e3, 3),
                higher_is_better=True, scaling="weak", vs_baseline=None, dtype="u32", data="synthetic",
-               config=dict(workload="C4: P-256 SignedData batch, 131072/GPU, 1.85KB msgs, 16 keys, "
-                                    "1% tamper/0.5% high-S/0.5% bad DER/0.1% trailing",
+               config=dict(workload=f"C4: P-256 SignedData batch, {n}/GPU, 1.85KB msgs, {min(nkeys, uniq)} keys"
+                                    + (" (churn: registered cold, variable-base kernels)" if churn else "")
+                                    + ", 1% tamper/0.5% high-S/0.5% bad DER/0.1% trailing",
                            global_batch=n * world, parallelism=f"shard{world}+allgather(1B/item)"),
                parity_vs_labels=ok,
+               key_tiers=dict(comb=kstats["comb"], vb=kstats["vb"], promoted=eng.key_stats()["promoted"]),
                stage_ms=dict(sha=round(acc["sha"] / args.steps, 4), prep=round(acc["prep"] / args.steps, 4),
-                             point=round(acc["point"] / args.steps, 4)),
-               roofline=roofline(n, acc["point"] / args.steps, "sig"), cpu_baseline=None)
+                             point=round(acc["point"] / args.steps, 4), vb_mul=round(acc["vb"] / args.steps, 4)),
+               roofline=(roofline_vb(n, acc["vb"] / args.steps) if churn
+                         else roofline(n, acc["point"] / args.steps, "sig")), cpu_baseline=None)
     if rank == 0 and world == 1 and args.cpu_threads > 0:
         rate, done, cel = cpu_verify_rate(pool["keymat"], [m.tobytes() for m in pool["msgs"]], pool["sigs"],
                                           args.cpu_threads)
@@ -895,6 +920,8 @@ def main():
                          "of a 16k-tx step about once: identity churn, client keys on the variable-base kernels)")
     ap.add_argument("--tx-per-block", type=int, default=500)
     ap.add_argument("--per-gpu", type=int, default=131072)
+    ap.add_argument("--sig-keys", type=int, default=16,
+                    help="C4: distinct signing keys (>16: churn, keys registered cold on the variable-base kernels)")
     ap.add_argument("--batches", type=int, default=6,
                     help="distinct blocks-per-gpu batches rotated through the timed loop (block workload)")
     ap.add_argument("--c5-batches", type=int, default=1)

@@ -17,9 +17,9 @@ SIG_VALID, SIG_FALSE, SIG_DER, SIG_HIGH_S, SIG_RANGE, SIG_BADKEY, SIG_EMPTY = ra
 
 EXPORTED = [
     "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_last_counts", "fgv_last_host_timing",
-    "fgv_last_point_handovers", "fgv_last_kernel_times",
+    "fgv_last_point_handovers", "fgv_last_kernel_times", "fgv_last_vb_timing",
     "fgv_sha256_batch",
-    "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_reset", "fgv_key_stats",
+    "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_register_tiered", "fgv_keys_reset", "fgv_key_stats",
     "fgv_set_block_outcomes", "fgv_last_block_status", "fgv_unsupported_stats", "fgv_stats_sums",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
@@ -109,6 +109,7 @@ def load():
         L.fgv_strerror.argtypes = [ctypes.c_int]
         L.fgv_strerror.restype = ctypes.c_char_p
         L.fgv_last_timing.argtypes = [vp] + [ctypes.POINTER(ctypes.c_double)] * 4
+        L.fgv_last_vb_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         L.fgv_last_counts.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 3
         L.fgv_last_point_handovers.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
         L.fgv_last_kernel_times.argtypes = [vp, vp, sz]
@@ -117,6 +118,7 @@ def load():
         L.fgv_p256_verify_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp]
         L.fgv_p256_verify_msgs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
         L.fgv_keys_register.argtypes = [vp, vp, sz, vp]
+        L.fgv_keys_register_tiered.argtypes = [vp, vp, sz, vp, vp]
         L.fgv_keys_reset.argtypes = [vp]
         L.fgv_key_stats.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 5
         L.fgv_set_block_outcomes.argtypes = [vp, ctypes.c_int]
@@ -443,7 +445,9 @@ class Engine:
     def timing(self):
         v = [ctypes.c_double() for _ in range(4)]
         _check(self._L.fgv_last_timing(self._h, *[ctypes.byref(x) for x in v]))
-        return dict(zip(("sha_ms", "prep_ms", "point_ms", "keytab_ms"), (x.value for x in v)))
+        vb = ctypes.c_double()
+        _check(self._L.fgv_last_vb_timing(self._h, ctypes.byref(vb)))
+        return dict(zip(("sha_ms", "prep_ms", "point_ms", "keytab_ms", "vb_mul_ms"), [x.value for x in v] + [vb.value]))
 
     def host_timing(self):
         v = [ctypes.c_double() for _ in range(4)]
@@ -544,10 +548,16 @@ class Engine:
         return st
 
     # --- key registry (MSP identity cache analogue)
-    def keys_register(self, keys):
+    def keys_register(self, keys, hot=None):
+        """hot: None (every key asks for a comb slot) or a per-key bool array (False: start on the
+        variable-base kernels, fgv_keys_register_tiered)"""
         keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 64)
         slots = np.zeros(len(keys), dtype=np.uint32)
-        _check(self._L.fgv_keys_register(self._h, _ptr(keys), len(keys), _ptr(slots)))
+        if hot is None:
+            _check(self._L.fgv_keys_register(self._h, _ptr(keys), len(keys), _ptr(slots)))
+        else:
+            h = np.ascontiguousarray(np.broadcast_to(np.asarray(hot, dtype=np.uint8), (len(keys),)))
+            _check(self._L.fgv_keys_register_tiered(self._h, _ptr(keys), len(keys), _ptr(h), _ptr(slots)))
         return slots
 
     def keys_reset(self):

@@ -115,6 +115,9 @@ static int flush_adhoc(fgv_ctx *c) {
     }
   }
   const size_t k = c->n_ids - c->pinned;
+  c->promo_backlog.erase(std::remove_if(c->promo_backlog.begin(), c->promo_backlog.end(),
+                                        [c](uint32_t id) { return id >= c->pinned; }),
+                         c->promo_backlog.end());
   HIP_TRY(hipMemsetAsync(c->kmap.as<uint32_t>() + c->pinned, 0xFF, k * 4, c->stream));
   HIP_TRY(hipMemsetAsync(c->vbuse.as<uint32_t>() + c->pinned, 0, k * 4, c->stream));
   c->n_ids = c->pinned;
@@ -160,16 +163,25 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
 // queued ids, then empty the queue on the device.  At the start of a call, under c->mu; a copy
 // still in flight is left for the next call.
 static int promote_consume(fgv_ctx *c) {
-  if (!c->vb_copied || hipEventQuery(c->vb_ev[2]) != hipSuccess) return FGV_OK;
-  c->vb_copied = false;
-  uint32_t *q = c->h_promo.as<uint32_t>();
-  const uint32_t np = std::min<uint32_t>(q[0], VB_PROMO_CAP);
-  if (np == 0) return FGV_OK;
-  std::vector<uint32_t> ids(q + 2, q + 2 + np);
+  if (c->vb_copied && hipEventQuery(c->vb_ev[2]) == hipSuccess) {  // (a copy in flight: a later call)
+    c->vb_copied = false;
+    uint32_t *q = c->h_promo.as<uint32_t>();
+    const uint32_t np = std::min<uint32_t>(q[0], VB_PROMO_CAP);
+    if (np) {
+      c->promo_backlog.insert(c->promo_backlog.end(), q + 2, q + 2 + np);
+      q[0] = 0;
+      HIP_TRY(hipMemsetAsync(c->vbpromo.p, 0, 4, c->stream));
+    }
+  }
+  if (c->comb_free.empty()) c->promo_backlog.clear();  // (nothing more can be promoted)
+  if (c->promo_backlog.empty()) return FGV_OK;
+  // at most promote_per_call builds per call (~80 us of the whole chip each), so a burst of keys
+  // reaching the threshold together spreads over calls instead of stalling one
+  const size_t take = std::min<size_t>(c->promo_backlog.size(), c->promote_per_call);
+  std::vector<uint32_t> ids(c->promo_backlog.begin(), c->promo_backlog.begin() + take);
+  c->promo_backlog.erase(c->promo_backlog.begin(), c->promo_backlog.begin() + take);
   std::sort(ids.begin(), ids.end());
   ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-  q[0] = 0;
-  HIP_TRY(hipMemsetAsync(c->vbpromo.p, 0, 4, c->stream));
   const uint32_t before = (uint32_t)c->comb_free.size();
   int rc = comb_build(c, ids);
   c->n_promoted += before - c->comb_free.size();
@@ -200,6 +212,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   c->key_ids = (cfg && cfg->key_ids) ? cfg->key_ids : (1u << 20);
   if (const char *e = getenv("FGV_PROMOTE_USES")) c->promote_uses = (uint32_t)std::max(1, atoi(e));
   if (const char *e = getenv("FGV_ADHOC_COMB")) c->adhoc_comb_uses = (uint32_t)std::max(1, atoi(e));
+  if (const char *e = getenv("FGV_PROMOTE_PER_CALL")) c->promote_per_call = (uint32_t)std::max(1, atoi(e));
   // host workers: fgv_config.host_threads, else min(24, this process's CPU share) -- 24 measured
   // best on a whole machine (tools/sweep_threads.sh); eight ranks on one node each get their
   // affinity mask's share, not the whole machine
@@ -236,6 +249,8 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   }
   for (auto &e : c->vb_ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
+  for (auto &e : c->vb_t)
+    if (hipEventCreate(&e) != hipSuccess) return fail(FGV_EDEVICE);
   for (auto &e : c->stage_ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
   {
@@ -322,6 +337,8 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->streamV) hipStreamDestroy(c->streamV);
   for (auto &e : c->vb_ev)
     if (e) hipEventDestroy(e);
+  for (auto &e : c->vb_t)
+    if (e) hipEventDestroy(e);
   for (auto e : c->stage_ev)
     if (e) hipEventDestroy(e);
   delete c;
@@ -361,6 +378,12 @@ int fgv_last_point_handovers(fgv_ctx *c, uint64_t *handovers) {
       hipStreamSynchronize(c->stream) != hipSuccess)
     return FGV_EDEVICE;
   *handovers = n;
+  return FGV_OK;
+}
+
+int fgv_last_vb_timing(fgv_ctx *c, double *vb_mul_ms) {
+  if (!c || !vb_mul_ms) return FGV_EINVAL;
+  *vb_mul_ms = c->t_vb;
   return FGV_OK;
 }
 
@@ -409,11 +432,14 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
   if (vb) {
     HIP_TRY(hipEventRecord(c->vb_ev[0], st));
     HIP_TRY(hipStreamWaitEvent(c->streamV, c->vb_ev[0], 0));
+    c->vb_timed = tim;
+    if (tim) HIP_TRY(hipEventRecord(c->vb_t[0], c->streamV));
     hipLaunchKernelGGL(k_vb_mul, dim3(2 * c->n_cu), dim3(VB_THREADS), 0, c->streamV, N, d_slot,
                        c->vbq.as<uint32_t>(), d_r, w.as<uint32_t>(), redo, redo + RD_VB_MUL,
                        c->vblist.as<uint32_t>(), c->vbscr.as<uint32_t>(), c->vbacc.as<uint32_t>(),
                        c->vbuse.as<uint32_t>(), c->promote_uses, c->vbpromo.as<uint32_t>());
     HIP_TRY(hipGetLastError());
+    if (tim) HIP_TRY(hipEventRecord(c->vb_t[1], c->streamV));
     HIP_TRY(hipEventRecord(c->vb_ev[1], c->streamV));
     // the promotion queue back to the host behind it (read by the next call: promote_consume)
     HIP_TRY(hipMemcpyAsync(c->h_promo.p, c->vbpromo.p, (VB_PROMO_CAP + 2) * 4, hipMemcpyDeviceToHost, c->streamV));
@@ -516,8 +542,9 @@ static int launch_verify_stages(fgv_ctx *c, uint32_t N, uint8_t *d_status, const
 
 static void read_stage_times(fgv_ctx *c, bool ran) {
   float ms = 0;
-  c->t_prep = c->t_point = 0;
+  c->t_prep = c->t_point = c->t_vb = 0;
   if (!ran || !c->timing_ran) return;
+  if (c->vb_launched && c->vb_timed && hipEventElapsedTime(&ms, c->vb_t[0], c->vb_t[1]) == hipSuccess) c->t_vb = ms;
   if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->t_prep = ms;
   if (hipEventElapsedTime(&ms, c->ev[4], c->ev[5]) == hipSuccess) c->t_prep += ms;
   if (hipEventElapsedTime(&ms, c->ev[5], c->ev[6]) == hipSuccess) c->t_point = ms;
@@ -813,6 +840,12 @@ int fgv_keys_register(fgv_ctx *c, const uint8_t *keys, size_t n, uint32_t *slots
   if (!c || (n && (!keys || !slots))) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   return keys_register_locked(c, keys, n, slots, nullptr);
+}
+
+int fgv_keys_register_tiered(fgv_ctx *c, const uint8_t *keys, size_t n, const uint8_t *hot, uint32_t *slots) {
+  if (!c || (n && (!keys || !slots))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return keys_register_locked(c, keys, n, slots, hot);
 }
 
 // registered keys are pinned: ad-hoc (BCCSP-path) ids are dropped first so the pinned range

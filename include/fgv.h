@@ -64,6 +64,9 @@ const char *fgv_strerror(int code);
 /* kernel-time accounting of the last call (ms, HIP events around each kernel) */
 int fgv_last_timing(fgv_ctx *ctx, double *sha_ms, double *prep_ms, double *point_ms,
                     double *keytab_ms);
+/* k_vb_mul's device time in the last timed verify call (0 when no item ran on the variable-base
+ * kernels): it runs on its own stream beside the hashes, so point_ms above does not hold it. */
+int fgv_last_vb_timing(fgv_ctx *ctx, double *vb_mul_ms);
 /* host-side wall time of the last block call: parse, job assembly, device pass (incl.
  * transfers), fold (ms) */
 int fgv_last_host_timing(fgv_ctx *ctx, double *parse_ms, double *assemble_ms, double *device_ms,
@@ -126,6 +129,11 @@ int fgv_p256_verify_msgs(fgv_ctx *ctx, const uint8_t *keys, const uint8_t *msg_b
  * verifies.  The comb cache filling up changes speed, never results; FGV_ENOMEM only when the
  * id space (fgv_config.key_ids) is exhausted. */
 int fgv_keys_register(fgv_ctx *ctx, const uint8_t *keys, size_t n, uint32_t *slots);
+/* The same with a per-key tier hint: hot[i] != 0 asks for a comb slot now (as fgv_keys_register),
+ * 0 starts the key on the variable-base kernels until it has signed FGV_PROMOTE_USES verifies --
+ * for keys that will sign rarely (a client population, a churn of one-off signers).  hot may be
+ * NULL (all hot).  Results never depend on the tier. */
+int fgv_keys_register_tiered(fgv_ctx *ctx, const uint8_t *keys, size_t n, const uint8_t *hot, uint32_t *slots);
 int fgv_keys_reset(fgv_ctx *ctx);
 /* Key-tier statistics: ids in use, ids with a comb table, ids on the variable-base kernels, keys
  * promoted to a comb since fgv_init, and verifies of the last call that ran on the variable-base

@@ -242,3 +242,45 @@ def test_churn_blocks_all_creators_distinct(mode):
         assert eng.key_stats()["vb_verifies_last"] > 1000
     finally:
         eng.close()
+
+
+def test_c4_churn_every_item_its_own_key():
+    """C4-shaped batch (1.85 KB messages, the injected tamper / high-S / bad-DER / trailing mix) where
+    every item has its own key, registered cold (fgv_keys_register_tiered, hot = 0): all on the
+    variable-base kernels, HBM-resident, statuses equal the oracle's"""
+    import torch
+    from fabric_amd.synth.workloads import sig_pool
+    n = 6000
+    pool = sig_pool(n, seed=77, nkeys=n)
+    eng = _lib.Engine(0)
+    try:
+        slots = eng.keys_register(np.frombuffer(b"".join(k.pub for k in pool["keys"]), np.uint8).reshape(-1, 64),
+                                  hot=False)
+        ks = eng.key_stats()
+        assert ks["comb"] == 0 and ks["vb"] == n, ks
+        msgs = pool["msgs"]
+        dev = torch.device("cuda", 0)
+        d_m = torch.zeros(msgs.size + 64, dtype=torch.uint8, device=dev)
+        d_m[:msgs.size] = torch.from_numpy(msgs.reshape(-1).copy()).to(dev)
+        sa, so, sl = _lib.pack(pool["sigs"])
+        d_s = torch.zeros(sa.size + 64, dtype=torch.uint8, device=dev)
+        d_s[:sa.size] = torch.from_numpy(sa.copy()).to(dev)
+
+        def t(a, dt):
+            return torch.from_numpy(np.ascontiguousarray(a).view(dt).copy()).to(dev)
+        hold = [t(np.arange(n, dtype=np.uint64) * np.uint64(msgs.shape[1]), np.int64),
+                t(np.full(n, msgs.shape[1], np.uint32), np.int32), t(so, np.int64), t(sl, np.int32),
+                t(slots[pool["key_index"]].astype(np.uint32), np.int32)]
+        d_st = torch.zeros(n, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        eng.verify_msgs_dev(d_m.data_ptr(), hold[0].data_ptr(), hold[1].data_ptr(), d_s.data_ptr(),
+                            hold[2].data_ptr(), hold[3].data_ptr(), hold[4].data_ptr(), n, d_st.data_ptr())
+        st = d_st.cpu().numpy()
+        exp = [oracle.identity_verify(pool["keys"][i].qx, pool["keys"][i].qy, msgs[i].tobytes(), pool["sigs"][i],
+                                      ossl=True) for i in range(n)]
+        assert st.tolist() == exp
+        assert ((st == 0) == pool["expect_valid"]).all()
+        assert eng.key_stats()["vb_verifies_last"] >= int((st == 0).sum())
+        assert eng.timing()["vb_mul_ms"] > 0
+    finally:
+        eng.close()

@@ -10,6 +10,8 @@
 #   lean<N>          N lean C2 runs (40 steps, no CPU baseline / PCIe / latency passes)
 #   env:VAR=VAL:N    N lean C2 runs with an environment knob set (A/B)
 #   churn            C2 with every creator a distinct identity (the cold-key path)
+#   sigchurn         C4 with every item its own key (registered cold)
+#   churntrace       rocprofv3 kernel + HIP API trace of a short churn run
 #   mvcc | sig | c5 | sbe   the other workloads (tools/bench_sbe.py for sbe)
 #   trace            rocprofv3 --kernel-trace --stats of a C2 run
 #   lattrace         the same of tools/latency_probe.py (single-block calls)
@@ -62,6 +64,14 @@ for step in "$@"; do
       timeout -k 10 400 python -u bench.py --clients 16000 --steps 20 --warmup 3 --cpu-threads 0 --no-pcie > $O/churn.json 2> $O/churn.err \
         || { echo churn failed; tail -20 $O/churn.err; exit 1; }
       show $O/churn.json churn value ms_per_step parity_vs_labels latency_1block_ms ;;
+    sigchurn)
+      timeout -k 10 400 python -u bench.py --workload sig --sig-keys 131072 --steps 10 --warmup 2 --cpu-threads 0 > $O/sigchurn.json 2> $O/sigchurn.err \
+        || { echo sigchurn failed; tail -20 $O/sigchurn.err; exit 1; }
+      show $O/sigchurn.json sigchurn value ms_per_step parity_vs_labels stage_ms key_tiers ;;
+    churntrace)
+      timeout -k 10 400 rocprofv3 --output-format csv --kernel-trace --hip-trace --stats -d $O/ct -o run -- python bench.py --clients 16000 --steps 8 --warmup 3 --cpu-threads 0 --no-pcie --no-latency > $O/ct.json 2> $O/ct.err \
+        || { echo churntrace failed; tail -20 $O/ct.err; exit 1; }
+      echo churntrace ok ;;
     mvcc)
       timeout -k 10 300 python -u bench.py --workload mvcc --steps 100 --warmup 5 > $O/mvcc.json 2> $O/mvcc.err \
         || { echo mvcc failed; tail -20 $O/mvcc.err; exit 1; }
