@@ -1842,6 +1842,15 @@ DEV uint32_t hex_word(const uint32_t *dw, uint32_t j) {
 // transaction of its block -> a dependency (validation_parameter_updated): the writer goes to the
 // transaction's list and the transaction to its block's dependent list, which k_bd_fold walks in
 // block order.  Launched for the fused single-device call only; no records: nothing to do.
+// The batch head (envelope table, block bases, counters, key-level words) pulled from the
+// host's pinned copy by the GPU itself: 16 B per lane over PCIe, a few microseconds for a
+// C2 head, and no copy-engine round trip ahead of the parse (FGV_HEAD_PULL, A/B against the
+// hipMemcpyAsync it replaces).
+__global__ __launch_bounds__(256) void k_head_pull(const uint4 *__restrict__ src, uint4 *__restrict__ dst, uint32_t n16) {
+  __builtin_amdgcn_s_setprio(3);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
 __global__ __launch_bounds__(256) void k_bd_kl(uint32_t ntx, DevTx *__restrict__ txs,
                                                const uint64_t *__restrict__ bases, KlDev kl,
                                                uint32_t *__restrict__ flags) {

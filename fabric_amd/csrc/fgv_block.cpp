@@ -1765,6 +1765,7 @@ void bd_parse_lds_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint3
                          const DevChannel &ch, DevTx *out, uint32_t *flags, uint32_t *xhaz, const KlDev &kl,
                          int32_t *ident);
 __global__ void k_bd_kl(uint32_t ntx, DevTx *txs, const uint64_t *bases, KlDev kl, uint32_t *flags);
+__global__ void k_head_pull(const uint4 *src, uint4 *dst, uint32_t n16);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals);
@@ -2013,7 +2014,24 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   const bool tim = c->timing;
   B.timed = tim;
   if (tim) HIP_TRY(hipEventRecord(B.ev[0], sf));
-  HIP_TRY(hipMemcpyAsync(B.env.p, head, hbytes, hipMemcpyHostToDevice, sf));
+  // FGV_HEAD_PULL=1: the GPU reads the head from the pinned host copy (k_head_pull) instead of a
+  // copy-engine transfer (A/B)
+  static const bool head_pull = [] {
+    const char *e = getenv("FGV_HEAD_PULL");
+    return e && atoi(e) != 0;
+  }();
+  const uint4 *hsrc = nullptr;
+  if (head_pull && (hbytes & 15) == 0 &&
+      hipHostGetDevicePointer(reinterpret_cast<void **>(const_cast<uint4 **>(&hsrc)), head, 0) != hipSuccess)
+    hsrc = nullptr;
+  if (hsrc) {
+    const uint32_t n16 = (uint32_t)(hbytes / 16);
+    hipLaunchKernelGGL(k_head_pull, dim3(std::min<uint32_t>((n16 + 255) / 256, 128)), dim3(256), 0, sf, hsrc,
+                       B.env.as<uint4>(), n16);
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(hipMemcpyAsync(B.env.p, head, hbytes, hipMemcpyHostToDevice, sf));
+  }
   HIP_TRY(hipEventRecord(B.ev[3], sf));
   // [0..5) totals, [5] flags, bytes 24..32 k_bd_sha compressions, 32..40 payload compressions
   uint32_t *misc = reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff);
@@ -2135,6 +2153,16 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   auto t0 = clk::now();
   fgv_ctx::NextBatch nx = c->next;  // the batch whose front half this call enqueues ahead
+  // FGV_PRESPLIT_EARLY=1: the next batch's framing walk starts at the top of the call (A/B against
+  // starting it once the first back-half kernels are queued)
+  static const bool presplit_early = [] {
+    const char *e = getenv("FGV_PRESPLIT_EARLY");
+    return e && atoi(e) != 0;
+  }();
+  if (presplit_early && nx.n) {
+    fgv_block_presplit(S, c->device, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi);
+    c->next.n = 0;
+  }
   if (S->ch.dirty || S->dev_dirty) {
     drain_ahead(c, S);  // (its kernels read the image about to be rebuilt; its results are stale)
     if (S->ch.dirty) S->ch.compile();
@@ -2194,7 +2222,7 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   c->t_gap = c->t_call_end.time_since_epoch().count() ? ms_since(c->t_call_end) : 0.0;
   // the next batch's framing walk, on the host worker while this batch's GPU work runs (started
   // once the first kernels of this back half are queued: the GPU gets them a few us sooner)
-  if (nx.n) {
+  if (nx.n && !presplit_early) {
     fgv_block_presplit(S, c->device, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi);
     c->next.n = 0;
   }

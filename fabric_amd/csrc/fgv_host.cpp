@@ -136,6 +136,19 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
   if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kid.ensure((size_t)nk * 4) || !c->kt_q.ensure((size_t)nk * 64) ||
       !c->kt_id.ensure((size_t)nk * 4))
     return FGV_ENOMEM;
+  // the variable-base tables (7.5 KB per id) grow by doubling; kernels in flight read the old rows
+  if (c->n_ids + nk > c->vbt_keys) {
+    const uint32_t want = std::min<uint32_t>(c->key_ids, std::max<uint32_t>({c->n_ids + nk, 2 * c->vbt_keys, 4096u}));
+    DevBuf nb;
+    if (!nb.ensure((size_t)want * VBT_WORDS * 4)) return FGV_ENOMEM;
+    HIP_TRY(hipStreamSynchronize(c->streamV));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->vbt_keys) HIP_TRY(hipMemcpy(nb.p, c->vbt.p, (size_t)c->vbt_keys * VBT_WORDS * 4, hipMemcpyDeviceToDevice));
+    c->vbt.release();
+    c->vbt = nb;
+    nb.p = nullptr;
+    c->vbt_keys = want;
+  }
   uint32_t *kq = c->h_kq.as<uint32_t>(), *ki = c->h_kid.as<uint32_t>();
   std::vector<uint32_t> comb;
   for (uint32_t j = 0; j < nk; j++) {
@@ -152,8 +165,8 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
   }
   HIP_TRY(hipMemcpyAsync(c->kt_q.p, kq, (size_t)nk * 64, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->kt_id.p, ki, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_keyprep, dim3((nk + 63) / 64), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
-                     c->kt_id.as<uint32_t>(), nk, c->vbq.as<uint32_t>(), c->key_ok.as<uint8_t>());
+  hipLaunchKernelGGL(k_keyprep, dim3((nk * VB_LANES + 63) / 64), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
+                     c->kt_id.as<uint32_t>(), nk, c->vbt.as<uint32_t>(), c->key_ok.as<uint8_t>());
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));  // (the staging is reused by comb_build)
   return comb_build(c, comb);
@@ -166,6 +179,7 @@ static int promote_consume(fgv_ctx *c) {
   if (c->vb_copied && hipEventQuery(c->vb_ev[2]) == hipSuccess) {  // (a copy in flight: a later call)
     c->vb_copied = false;
     uint32_t *q = c->h_promo.as<uint32_t>();
+    c->vb_last_items = q[1];
     const uint32_t np = std::min<uint32_t>(q[0], VB_PROMO_CAP);
     if (np) {
       c->promo_backlog.insert(c->promo_backlog.end(), q + 2, q + 2 + np);
@@ -269,7 +283,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   }
   if (!c->g_ok.ensure(16) || !c->gtab28.ensure(GT_BYTES) || !c->redo.ensure(64) ||
       !c->ktab28.ensure((size_t)c->key_slots * KT_BYTES) || !c->key_ok.ensure(c->key_ids) ||
-      !c->kmap.ensure((size_t)c->key_ids * 4) || !c->vbq.ensure((size_t)c->key_ids * VBQ_WORDS * 4) ||
+      !c->kmap.ensure((size_t)c->key_ids * 4) ||
       !c->vbuse.ensure((size_t)c->key_ids * 4) || !c->vbpromo.ensure((VB_PROMO_CAP + 2) * 4) ||
       !c->h_promo.ensure((VB_PROMO_CAP + 2) * 4))
     return fail(FGV_ENOMEM);
@@ -310,7 +324,7 @@ void fgv_destroy(fgv_ctx *c) {
     if (x) hipStreamSynchronize(x);
   DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->stage[2], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
                  &c->bd_misc, &c->g_ok, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
-                 &c->kmap, &c->vbq, &c->vbuse, &c->vbpromo, &c->vblist, &c->vbacc, &c->vbscr, &c->kt_id,
+                 &c->kmap, &c->vbt, &c->vbuse, &c->vbpromo, &c->vblist, &c->vbacc, &c->kt_id,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
                  &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
                  &c->bj_dig, &c->bj_vst, &c->blk_arena, &c->fz_meta, &c->fz_rowmap, &c->fz_blkof,
@@ -417,9 +431,7 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
   // launch_prep_point's k_vb_fin adds u1 * G once k_prep has run
   const bool vb = c->n_vb > 0;
   c->vb_launched = vb;
-  const size_t scr = (size_t)2 * c->n_cu * VB_THREADS * VB_TAB * VB_TAB_WORDS * 4;
-  if (vb && (!c->vblist.ensure((size_t)N * 4) || !c->vbacc.ensure((size_t)N * VB_TAB_WORDS * 4) ||
-             !c->vbscr.ensure(scr)))
+  if (vb && (!c->vblist.ensure((size_t)N * 4) || !c->vbacc.ensure((size_t)N * VB_ACC_WORDS * 4)))
     return FGV_ENOMEM;
   uint32_t *redo = c->redo.as<uint32_t>();
   if (tim) HIP_TRY(hipEventRecord(c->ev[2], st));
@@ -434,9 +446,15 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
     HIP_TRY(hipStreamWaitEvent(c->streamV, c->vb_ev[0], 0));
     c->vb_timed = tim;
     if (tim) HIP_TRY(hipEventRecord(c->vb_t[0], c->streamV));
-    hipLaunchKernelGGL(k_vb_mul, dim3(2 * c->n_cu), dim3(VB_THREADS), 0, c->streamV, N, d_slot,
-                       c->vbq.as<uint32_t>(), d_r, w.as<uint32_t>(), redo, redo + RD_VB_MUL,
-                       c->vblist.as<uint32_t>(), c->vbscr.as<uint32_t>(), c->vbacc.as<uint32_t>(),
+    // FGV_VB_WGS = workgroups per CU (k_vb_mul fits 3 waves per SIMD; default 2: beside k_point28)
+    static const uint32_t vb_wgs = [] {
+      const char *e = getenv("FGV_VB_WGS");
+      const int v = e ? atoi(e) : 2;
+      return (uint32_t)(v >= 1 && v <= 3 ? v : 2);
+    }();
+    hipLaunchKernelGGL(k_vb_mul, dim3(vb_wgs * c->n_cu), dim3(VB_THREADS), 0, c->streamV, N, d_slot,
+                       c->vbt.as<uint32_t>(), d_r, w.as<uint32_t>(), redo, redo + RD_VB_MUL,
+                       c->vblist.as<uint32_t>(), c->vbacc.as<uint32_t>(),
                        c->vbuse.as<uint32_t>(), c->promote_uses, c->vbpromo.as<uint32_t>());
     HIP_TRY(hipGetLastError());
     if (tim) HIP_TRY(hipEventRecord(c->vb_t[1], c->streamV));
@@ -520,9 +538,12 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
   if (c->vb_pending) {  // the variable-base items: + u1 * G and the x check, after k_vb_mul (streamV)
     c->vb_pending = false;
     HIP_TRY(hipStreamWaitEvent(c->stream, c->vb_ev[1], 0));
-    // a small grid: its per-item work is 12 mixed additions, and every workgroup ends with an
-    // atomic on one counter word (a 2 x n_cu grid spent ~40 us on those alone with an empty list)
-    hipLaunchKernelGGL(k_vb_fin, dim3(VB_FIN_WGS), dim3(256), 0, c->stream, N, d_status, c->gtab28.as<apoint_raw>(),
+    // the grid follows the last read-back batch's variable-base item count (one item per lane):
+    // at least VB_FIN_WGS -- every workgroup ends with an atomic on one counter word, and a 2 x n_cu
+    // grid spent ~40 us on those alone with an empty list -- at most 2 x n_cu
+    const uint32_t fin_wgs = std::min<uint32_t>(std::max<uint32_t>((c->vb_last_items + 255) / 256, VB_FIN_WGS),
+                                                2 * c->n_cu);
+    hipLaunchKernelGGL(k_vb_fin, dim3(fin_wgs), dim3(256), 0, c->stream, N, d_status, c->gtab28.as<apoint_raw>(),
                        c->d1.as<int8_t>(), d_r, c->redo.as<uint32_t>(), c->vblist.as<uint32_t>(),
                        c->vbacc.as<uint32_t>());
     HIP_TRY(hipGetLastError());

@@ -51,15 +51,16 @@ struct jpoint_raw {  // key-table build scratch: Jacobian point + prefix product
 __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw *tables, apoint_raw *tables28,
                          jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys);
 // Key tiers.  Every key has an id; kmap[id] is its comb slot (the 5.2 MB table
-// above) or KEY_NONE: the variable-base kernel k_point_vb verifies it from its coordinates alone
-// (vbq[id]: the slice bases 2^(32 s) Q, s < 8, affine Montgomery-256, 512 B).  k_keyprep checks
-// new keys (on the curve) and writes vbq / key_ok; k_kmap_set points ids at their freshly built comb tables (after k_keytab).
+// above) or KEY_NONE: the variable-base kernels verify it from a 7.5 KB per-key table
+// (vbt[id][s][d-1] = d * 2^(32 s) Q, s < 8, d = 1..15, affine Montgomery-256).  k_keyprep checks
+// new keys (on the curve) and writes vbt / key_ok; k_kmap_set points ids at their freshly built
+// comb tables (after k_keytab).
 #define KEY_NONE 0xFFFFFFFFu
-#define VB_THREADS 256      // k_vb_mul workgroup (grid 2 x n_cu: each lane owns a scratch table)
+#define VB_THREADS 256      // k_vb_mul workgroup (grid 2 x n_cu)
 #define VB_LANES 8          // k_vb_mul lanes per item (32-bit slices of u2)
-#define VBQ_WORDS (VB_LANES * 16)  // per key id: the slice bases 2^(32 s) Q, affine Montgomery-256
-#define VB_TAB 15           // per-lane table 1Q .. 15Q (4-bit fixed windows), Jacobian
-#define VB_TAB_WORDS 24     // x, y, z (Montgomery-256)
+#define VB_TAB 15           // per slice: 1 .. 15 times the slice base (4-bit fixed windows)
+#define VBT_WORDS (VB_LANES * VB_TAB * 16)  // per key id: 120 affine points, 7,680 B
+#define VB_ACC_WORDS 24     // k_vb_mul -> k_vb_fin partial result: x, y, z (Montgomery-256)
 // counters in the context's redo words: [0] k_point28 hand-overs, [1] k_point28 chunks, [2] k_point
 // chunks, [3] items k_inv listed for the variable-base kernels, [4] taken by k_vb_mul, [5] taken
 // by k_vb_fin, [6] finished k_vb_fin workgroups (the last one zeroes [3..6] for the next batch)
@@ -70,11 +71,11 @@ __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw 
 #define VB_FIN_WGS 32        // k_vb_fin workgroups (256 threads)
 #define VB_PROMO_CAP 1022   // promotion queue: [0] count, [1] the last batch's variable-base items,
                             // then ids whose use count reached the threshold
-__global__ void k_keyprep(const uint32_t *qxy, const uint32_t *ids, uint32_t nkeys, uint32_t *vbq, uint8_t *key_ok);
+__global__ void k_keyprep(const uint32_t *qxy, const uint32_t *ids, uint32_t nkeys, uint32_t *vbt, uint8_t *key_ok);
 __global__ void k_kmap_set(const uint32_t *ids, const uint32_t *slots, uint32_t n, uint32_t *kmap);
-__global__ void k_vb_mul(uint32_t n, const uint32_t *key_slot, const uint32_t *vbq, const uint32_t *r_limbs,
+__global__ void k_vb_mul(uint32_t n, const uint32_t *key_slot, const uint32_t *vbt, const uint32_t *r_limbs,
                          const uint32_t *w_in, const uint32_t *ctr, uint32_t *take, const uint32_t *list,
-                         uint32_t *scratch, uint32_t *acc, uint32_t *uses, uint32_t promote, uint32_t *promo);
+                         uint32_t *acc, uint32_t *uses, uint32_t promote, uint32_t *promo);
 __global__ void k_vb_fin(uint32_t n, uint8_t *status, const apoint_raw *gtab28, const int8_t *digits,
                          const uint32_t *r_limbs, uint32_t *ctr, const uint32_t *list, const uint32_t *acc);
 __global__ void k_gtab(apoint_raw *tables28, jpoint_raw *scratch, uint32_t w);

@@ -781,13 +781,16 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
 
 // ---------------------------------------------------------------- keys without a comb
 // k_keyprep: new key ids -> on-curve bit (k_inv reports 5 for a key off the curve, before the
-// range checks, as ecdsa.Verify does) and the variable-base kernel's slice bases
-// Q_s = 2^(32 s) * Q, s = 0..VB_LANES-1 (affine Montgomery-256, vbq[id][s]: 32 doublings apart,
-// one inversion for all seven Z's).  qxy: [nkeys][16] plain little-endian limbs (x then y).
+// range checks, as ecdsa.Verify does) and the variable-base kernel's per-key table
+// vbt[id][s][d-1] = d * Q_s, Q_s = 2^(32 s) * Q, s < VB_LANES, d = 1..VB_TAB (affine Montgomery-256,
+// 7.5 KB per key).  One thread per (key, slice): 32 s doublings to Q_s, 14 complete additions,
+// one inversion for the slice's 15 Z's (prefix products).  qxy: [nkeys][16] plain little-endian
+// limbs (x then y).
 __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy, const uint32_t *__restrict__ ids,
-                                                uint32_t nkeys, uint32_t *__restrict__ vbq,
+                                                uint32_t nkeys, uint32_t *__restrict__ vbt,
                                                 uint8_t *__restrict__ key_ok) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = t / VB_LANES, sl = t % VB_LANES;
   if (k >= nkeys) return;
   fe x, y, xm, ym;
 #pragma unroll
@@ -797,44 +800,47 @@ __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy
   }
   const bool ok = on_curve(x, y, xm, ym);
   const uint32_t id = ids[k];
-  key_ok[id] = ok ? 1 : 0;
-  uint32_t *o = vbq + (size_t)id * VBQ_WORDS;
-  if (!ok) {
+  if (sl == 0) key_ok[id] = ok ? 1 : 0;
+  uint32_t *o = vbt + (size_t)id * VBT_WORDS + sl * (VB_TAB * 16);
+  if (!ok) {  // (never read: k_inv fails the key's items first)
     fe z;
     fe_set_zero(z);
-    for (int s = 0; s < VB_LANES; s++) store_fe(o + 16 * s, z), store_fe(o + 16 * s + 8, z);
+    for (int d = 0; d < VB_TAB; d++) store_fe(o + 16 * d, z), store_fe(o + 16 * d + 8, z);
     return;
   }
-  store_fe(o, xm);
-  store_fe(o + 8, ym);
-  // Q_s in Jacobian (never infinity: 2^(32 s) < n), Z's multiplied up for one inversion
-  jpoint q[VB_LANES];
-  q[0].x = xm;
-  q[0].y = ym;
-  fe_set_one(q[0].z);
-  fe pref[VB_LANES];
-  pref[0] = q[0].z;
-  for (int s = 1; s < VB_LANES; s++) {
-    q[s] = q[s - 1];
+  jpoint q;  // Q_s (never infinity: 2^(32 s) < n)
+  q.x = xm;
+  q.y = ym;
+  fe_set_one(q.z);
 #pragma unroll 1
-    for (int d = 0; d < 32; d++) {
-      jpoint t2 = q[s];
-      pt_dbl(q[s], t2);
-    }
-    fe_mul(pref[s], pref[s - 1], q[s].z);
+  for (uint32_t d = 0; d < 32 * sl; d++) {
+    jpoint t2 = q;
+    pt_dbl(q, t2);
+  }
+  jpoint T[VB_TAB];  // d * Q_s (d < n: never infinity)
+  fe pref[VB_TAB];
+  T[0] = q;
+  pref[0] = q.z;
+  for (int d = 1; d < VB_TAB; d++) {
+    pt_add_inl(T[d], T[d - 1], q);  // (d = 1: T[0] == q, routed to the doubling)
+    fe_mul(pref[d], pref[d - 1], T[d].z);
   }
   fe inv;
-  fe_inv(inv, pref[VB_LANES - 1]);
-  for (int s = VB_LANES - 1; s >= 1; s--) {
+  fe_inv(inv, pref[VB_TAB - 1]);
+  for (int d = VB_TAB - 1; d >= 0; d--) {
     fe zinv, z2, z3, ax, ay;
-    fe_mul(zinv, inv, pref[s - 1]);  // Z_s^-1
-    fe_mul(inv, inv, q[s].z);
+    if (d > 0) {
+      fe_mul(zinv, inv, pref[d - 1]);  // Z_d^-1
+      fe_mul(inv, inv, T[d].z);
+    } else {
+      zinv = inv;
+    }
     fe_sqr(z2, zinv);
     fe_mul(z3, z2, zinv);
-    fe_mul(ax, q[s].x, z2);
-    fe_mul(ay, q[s].y, z3);
-    store_fe(o + 16 * s, ax);
-    store_fe(o + 16 * s + 8, ay);
+    fe_mul(ax, T[d].x, z2);
+    fe_mul(ay, T[d].y, z3);
+    store_fe(o + 16 * d, ax);
+    store_fe(o + 16 * d + 8, ay);
   }
 }
 // ids whose comb tables k_keytab has just built (stream order) now take the comb path
@@ -866,24 +872,21 @@ FGV_DEV void load_jp(jpoint &p, const uint32_t *s) {
 
 // k_vb_mul: acc[j] = u2 * Q for list entry j (item i = list[j], key id key_slot[i]), u2 = r * s^-1
 // (plain; k_inv's w is s^-1 in Montgomery form) -- needs no digest, so it runs beside the hashes.
-// VB_LANES lanes per item: lane s takes the 32 bits u2[s] of the scalar against its slice base
-// Q_s = 2^(32 s) Q (k_keyprep), so u2 * Q = sum_s u2[s] * Q_s:
-//   table T[d-1] = d * Q_s, d = 1..15 (Jacobian, the lane's scratch row; 14 mixed additions);
-//   8 windows of 4 bits, left to right: 28 doublings and <= 8 additions (each next entry loaded
-//   during the doublings);
+// VB_LANES lanes per item: lane s takes the 32 bits u2[s] of the scalar against the key's slice
+// table d * Q_s, Q_s = 2^(32 s) Q (k_keyprep, affine), so u2 * Q = sum_s u2[s] * Q_s:
+//   8 windows of 4 bits, left to right: 28 doublings and <= 8 mixed additions (each next entry
+//   loaded during the doublings);
 //   a 3-level butterfly of complete additions across the 8 lanes (cross-lane shuffles).
 // Complete formulas throughout (pt_madd / pt_dbl / pt_add_inl): exact for every input.  Per lane
-// ~560 field multiplications, the item's serial chain ~6x shorter than one lane doing all 256
-// doublings.  uses[id] counts the key's variable-base verifies; the one that
-// reaches `promote` queues the id (promo[0] count, ids from promo[2]) for a comb build by the host;
-// promo[1] = the batch's variable-base items.
+// ~330 field multiplications.  uses[id] counts the key's variable-base verifies;
+// the one that reaches `promote` queues the id (promo[0] count, ids from promo[2]) for a comb build
+// by the host; promo[1] = the batch's variable-base items.
 __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_t *__restrict__ key_slot,
-                                                      const uint32_t *__restrict__ vbq,
+                                                      const uint32_t *__restrict__ vbt,
                                                       const uint32_t *__restrict__ r_limbs,
                                                       const uint32_t *__restrict__ w_in,
                                                       const uint32_t *__restrict__ ctr, uint32_t *__restrict__ take,
-                                                      const uint32_t *__restrict__ list,
-                                                      uint32_t *__restrict__ scratch, uint32_t *__restrict__ acc,
+                                                      const uint32_t *__restrict__ list, uint32_t *__restrict__ acc,
                                                       uint32_t *__restrict__ uses, uint32_t promote,
                                                       uint32_t *__restrict__ promo) {
   __builtin_amdgcn_s_setprio(2);
@@ -892,7 +895,6 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_
   if (cnt == 0) return;
   const uint32_t lane = __lane_id(), sl = lane % VB_LANES, base = lane - sl;
   constexpr uint32_t PER = 64u / VB_LANES;  // items per wave and round
-  uint32_t *tab = scratch + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * (VB_TAB * VB_TAB_WORDS);
   uint32_t j0;
   while (vb_next(take, cnt, PER, j0)) {
     const uint32_t j = j0 + lane / VB_LANES;
@@ -909,35 +911,20 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_
     uint32_t dg = u2[0];  // this lane's 32 bits: u2[sl] (a select chain: no private array)
 #pragma unroll
     for (int k = 1; k < 8; k++) dg = sl == (uint32_t)k ? u2[k] : dg;
-    apoint q;
-    load_fe(q.x, vbq + (size_t)id * VBQ_WORDS + 16 * sl);
-    load_fe(q.y, vbq + (size_t)id * VBQ_WORDS + 16 * sl + 8);
-    {  // T[0] = Q_s, T[d-1] = T[d-2] + Q_s (pt_madd routes 2 Q_s to a doubling)
-      jpoint t;
-      t.x = q.x;
-      t.y = q.y;
-      fe_set_one(t.z);
-      store_jp(tab, t);
-#pragma unroll 1
-      for (int d = 2; d <= VB_TAB; d++) {
-        jpoint t2 = t;
-        pt_madd(t, t2, q);
-        store_jp(tab + (d - 1) * VB_TAB_WORDS, t);
-      }
-    }
+    const uint32_t *qt = vbt + (size_t)id * VBT_WORDS + sl * (VB_TAB * 16);
     jpoint a;
     fe_set_zero(a.x);
     fe_set_zero(a.y);
     fe_set_zero(a.z);
     uint32_t d = dg >> 28;
-    jpoint e;
-    if (d) load_jp(e, tab + (d - 1) * VB_TAB_WORDS);
+    apoint e;
+    if (d) load_fe(e.x, qt + 16 * (d - 1)), load_fe(e.y, qt + 16 * (d - 1) + 8);
 #pragma unroll 1
     for (int win = 7; win >= 0; win--) {
       dg <<= 4;
       const uint32_t dn = dg >> 28;  // the next window's digit (0 after the last)
-      jpoint en;
-      if (win > 0 && dn) load_jp(en, tab + (dn - 1) * VB_TAB_WORDS);  // (in flight during the doublings)
+      apoint en;
+      if (win > 0 && dn) load_fe(en.x, qt + 16 * (dn - 1)), load_fe(en.y, qt + 16 * (dn - 1) + 8);
       if (win < 7) {
 #pragma unroll 1
         for (int k = 0; k < 4; k++) {
@@ -947,7 +934,7 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_
       }
       if (d) {
         jpoint t2 = a;
-        pt_add_inl(a, t2, e);
+        pt_madd(a, t2, e);  // (a = infinity: e itself)
       }
       d = dn;
       e = en;
@@ -967,7 +954,7 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_
       pt_add_inl(a, t2, o);
     }
     if (sl != 0) continue;
-    store_jp(acc + (size_t)j * VB_TAB_WORDS, a);
+    store_jp(acc + (size_t)j * VB_ACC_WORDS, a);
     const uint32_t u = atomicAdd(&uses[id], 1u);
     if (u + 1u == promote) {
       const uint32_t s = atomicAdd(&promo[0], 1u);
@@ -992,7 +979,7 @@ __global__ __launch_bounds__(256) void k_vb_fin(uint32_t n, uint8_t *__restrict_
     if (j >= cnt) continue;
     const uint32_t i = list[j];
     jpoint a;
-    load_jp(a, acc + (size_t)j * VB_TAB_WORDS);
+    load_jp(a, acc + (size_t)j * VB_ACC_WORDS);
     const int32_t *g = reinterpret_cast<const int32_t *>(digits + (size_t)i * DIG_STRIDE);
     fe c232;
     fe_load_c(c232, C232_32);

@@ -54,7 +54,7 @@ for step in "$@"; do
       done ;;
     env:*)
       # env:VAR=VAL:N -- N lean C2 runs with VAR=VAL (A/B against lean<N> on the same box)
-      spec=${step#env:}; n=${spec##*:}; kv=${spec%:*}; tag=$(echo $kv | tr '=' '_')
+      spec=${step#env:}; n=${spec##*:}; kv=${spec%:*}; tag=$(echo $kv | tr '= ' '__')
       for rep in $(seq 1 $n); do
         env $kv timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --cpu-threads 0 --no-pcie --no-latency > $O/lean_${tag}_$rep.json 2> $O/lean_${tag}_$rep.err \
           || { echo lean $kv failed; tail -20 $O/lean_${tag}_$rep.err; exit 1; }
