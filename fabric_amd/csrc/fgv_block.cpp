@@ -2302,7 +2302,7 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
     // counters belong to one batch at a time)
     const auto tf = clk::now();
     if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after,
-                     prefix_ahead && c->n_vb == 0) == FGV_OK)
+                     prefix_ahead && c->n_vb == 0 && !c->kt_busy) == FGV_OK)
       S->ahead = cur ^ 1;
     else
       drain_ahead(c, S), S->ahead = -1;  // (the next call starts it again and reports any error)

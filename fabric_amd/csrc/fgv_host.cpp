@@ -46,28 +46,40 @@ static void stats_accumulate(fgv_ctx *c);
 // Build comb tables for `nk` keys (h_qxy: nk*16 plain limbs) into `tables28` at `h_slots`,
 // KT_BUILD_KEYS keys per k_keytab launch (its scratch is KT_ENTRIES Jacobian points per key).
 static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slots, uint32_t nk,
-                        apoint_raw *tables, apoint_raw *tables28, uint8_t *ok) {
+                        apoint_raw *tables, apoint_raw *tables28, uint8_t *ok, hipStream_t st = nullptr) {
+  const bool timed = st == nullptr;
+  if (!st) st = c->stream;
   const uint32_t per = nk < KT_BUILD_KEYS ? nk : KT_BUILD_KEYS;
   if (!c->kt_q.ensure((size_t)nk * 64) || !c->kt_slot.ensure((size_t)nk * 4) ||
       !c->kt_scratch.ensure((size_t)per * KT_ENTRIES * sizeof(jpoint_raw)))
     return FGV_ENOMEM;
-  HIP_TRY(hipMemcpyAsync(c->kt_q.p, h_qxy, (size_t)nk * 64, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->kt_slot.p, h_slots, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipEventRecord(c->ev[6], c->stream));
+  HIP_TRY(hipMemcpyAsync(c->kt_q.p, h_qxy, (size_t)nk * 64, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(c->kt_slot.p, h_slots, (size_t)nk * 4, hipMemcpyHostToDevice, st));
+  if (timed) HIP_TRY(hipEventRecord(c->ev[6], st));
   for (uint32_t k = 0; k < nk; k += per) {
     const uint32_t m = nk - k < per ? nk - k : per;
     const uint32_t threads = m * KT_THREADS_PER_KEY;
-    hipLaunchKernelGGL(k_keytab, dim3((threads + 63) / 64), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>() + 16 * k,
+    hipLaunchKernelGGL(k_keytab, dim3((threads + 63) / 64), dim3(64), 0, st, c->kt_q.as<uint32_t>() + 16 * k,
                        c->kt_slot.as<uint32_t>() + k, tables, tables28, c->kt_scratch.as<jpoint_raw>(), ok, m);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(c->ev[7], c->stream));
+  if (timed) HIP_TRY(hipEventRecord(c->ev[7], st));
   return FGV_OK;
 }
 
 // comb tables for ids that have none (taken in order while comb slots are free; the rest stay on
 // VB).  Synchronises the stream (the staging buffers are reused by the next build).
-static int comb_build(fgv_ctx *c, const std::vector<uint32_t> &ids) {
+// The staging buffers of an asynchronous build (streamK) are free again.
+static int kt_wait(fgv_ctx *c) {
+  if (!c->kt_busy) return FGV_OK;
+  HIP_TRY(hipEventSynchronize(c->kt_ev));
+  c->kt_busy = false;
+  return FGV_OK;
+}
+
+static int comb_build(fgv_ctx *c, const std::vector<uint32_t> &ids, bool async = false) {
+  int wrc = kt_wait(c);
+  if (wrc) return wrc;
   std::vector<uint32_t> take;
   for (uint32_t id : ids)
     if (take.size() < c->comb_free.size() && id < c->n_ids && c->kmap_h[id] == KEY_NONE) take.push_back(id);
@@ -88,12 +100,22 @@ static int comb_build(fgv_ctx *c, const std::vector<uint32_t> &ids) {
     ks[j] = slot;
     ki[j] = id;
   }
-  int rc = build_tables(c, kq, ks, nk, nullptr, c->ktab28.as<apoint_raw>(), nullptr);
+  // async (promotions): on streamK, nobody waits.  A kernel that reads kmap while the build is in
+  // flight sees KEY_NONE (variable-base path) or the slot once the table is complete (k_kmap_set
+  // runs after k_keytab): kmap only goes from KEY_NONE to a slot outside a flush, and both paths
+  // give the same status, so a batch may even see the change between k_inv and k_point28
+  hipStream_t st = async ? c->streamK : c->stream;
+  int rc = build_tables(c, kq, ks, nk, nullptr, c->ktab28.as<apoint_raw>(), nullptr, async ? st : nullptr);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(c->kt_id.p, ki, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_kmap_set, dim3((nk + 63) / 64), dim3(64), 0, c->stream, c->kt_id.as<uint32_t>(),
+  HIP_TRY(hipMemcpyAsync(c->kt_id.p, ki, (size_t)nk * 4, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_kmap_set, dim3((nk + 63) / 64), dim3(64), 0, st, c->kt_id.as<uint32_t>(),
                      c->kt_slot.as<uint32_t>(), nk, c->kmap.as<uint32_t>());
   HIP_TRY(hipGetLastError());
+  if (async) {
+    HIP_TRY(hipEventRecord(c->kt_ev, st));
+    c->kt_busy = true;
+    return FGV_OK;
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
   float ms = 0;
   if (hipEventElapsedTime(&ms, c->ev[6], c->ev[7]) == hipSuccess) c->t_keytab += ms;
@@ -103,6 +125,8 @@ static int comb_build(fgv_ctx *c, const std::vector<uint32_t> &ids) {
 // forget the ad-hoc ids [pinned, n_ids): their comb slots go back to the free list
 static int flush_adhoc(fgv_ctx *c) {
   if (c->n_ids == c->pinned) return FGV_OK;
+  int wrc = kt_wait(c);  // (a promotion's k_kmap_set must land before the reset below)
+  if (wrc) return wrc;
   for (uint32_t id = c->pinned; id < c->n_ids; id++) {
     c->key_map.erase(c->id_key[id]);
     const uint32_t slot = c->kmap_h[id];
@@ -130,6 +154,8 @@ static int flush_adhoc(fgv_ctx *c) {
 // Synchronises the stream.
 static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys, const std::vector<uint8_t> *want,
                    uint32_t *ids_out) {
+  int wrc = kt_wait(c);  // (the staging buffers below)
+  if (wrc) return wrc;
   const uint32_t nk = (uint32_t)keys.size();
   if (nk == 0) return FGV_OK;
   if ((uint64_t)c->n_ids + nk > c->key_ids) return FGV_ENOMEM;
@@ -197,7 +223,7 @@ static int promote_consume(fgv_ctx *c) {
   std::sort(ids.begin(), ids.end());
   ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
   const uint32_t before = (uint32_t)c->comb_free.size();
-  int rc = comb_build(c, ids);
+  int rc = comb_build(c, ids, true);
   c->n_promoted += before - c->comb_free.size();
   return rc;
 }
@@ -260,6 +286,8 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->streamF, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->streamV, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+    if (hipStreamCreateWithPriority(&c->streamK, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+    if (hipEventCreateWithFlags(&c->kt_ev, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
   }
   for (auto &e : c->vb_ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
@@ -320,7 +348,7 @@ void fgv_destroy(fgv_ctx *c) {
   if (!c) return;
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
-  for (hipStream_t x : {c->stream2, c->stream3, c->streamF, c->streamV})  // (a front half enqueued ahead)
+  for (hipStream_t x : {c->stream2, c->stream3, c->streamF, c->streamV, c->streamK})  // (a front half enqueued ahead)
     if (x) hipStreamSynchronize(x);
   DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->stage[2], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
                  &c->bd_misc, &c->g_ok, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
@@ -348,6 +376,8 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->stream3) hipStreamDestroy(c->stream3);
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   if (c->streamF) hipStreamDestroy(c->streamF);
+  if (c->streamK) hipStreamSynchronize(c->streamK), hipStreamDestroy(c->streamK);
+  if (c->kt_ev) hipEventDestroy(c->kt_ev);
   if (c->streamV) hipStreamDestroy(c->streamV);
   for (auto &e : c->vb_ev)
     if (e) hipEventDestroy(e);
@@ -429,7 +459,10 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
   // keys without a comb (c->n_vb): k_inv lists their items, k_vb_mul computes u2 * Q for them on
   // streamV -- beside the hashes and k_prep: it needs s^-1, not the digest -- and
   // launch_prep_point's k_vb_fin adds u1 * G once k_prep has run
-  const bool vb = c->n_vb > 0;
+  // (a promotion still building on streamK: its keys count as comb keys on the host but may read
+  // KEY_NONE on the device, so their items still need the variable-base kernels)
+  if (c->kt_busy && hipEventQuery(c->kt_ev) == hipSuccess) c->kt_busy = false;
+  const bool vb = c->n_vb > 0 || c->kt_busy;
   c->vb_launched = vb;
   if (vb && (!c->vblist.ensure((size_t)N * 4) || !c->vbacc.ensure((size_t)N * VB_ACC_WORDS * 4)))
     return FGV_ENOMEM;
@@ -841,6 +874,8 @@ int fgv_key_stats(fgv_ctx *c, uint64_t *ids, uint64_t *comb, uint64_t *vb, uint6
                   uint64_t *vb_verifies_last) {
   if (!c) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  int wrc = kt_wait(c);  // (promotions still building count as promoted; their kmap lands first)
+  if (wrc) return wrc;
   if (ids) *ids = c->n_ids;
   if (comb) *comb = c->n_ids - c->n_vb;
   if (vb) *vb = c->n_vb;

@@ -132,6 +132,9 @@ struct fgv_ctx {
   uint32_t vb_last_items = 0;      // the last read-back batch's variable-base items (k_vb_fin's grid)
   HostBuf h_promo, h_kid;       // the promotion queue read back (k_vb_mul -> streamV copy)
   hipStream_t streamV = nullptr;  // k_vb_mul: beside the hashes (u2 * Q needs no digest)
+  hipStream_t streamK = nullptr;  // promotion comb builds (k_keytab + k_kmap_set), not waited on
+  hipEvent_t kt_ev = nullptr;     // the last build on streamK (its staging buffers are reused)
+  bool kt_busy = false;
   hipEvent_t vb_ev[3] = {};       // 0 the VB list is built (k_inv), 1 k_vb_mul done, 2 queue copied
   hipEvent_t vb_t[2] = {};        // k_vb_mul's bracket on streamV (timed calls)
   double t_vb = 0;                // k_vb_mul ms of the last timed call
@@ -142,7 +145,7 @@ struct fgv_ctx {
   uint32_t promote_uses = 64;     // variable-base verifies of one key before its comb is built
   uint32_t adhoc_comb_uses = 32;  // uses of an ad-hoc key in one call for a comb
   uint64_t n_promoted = 0;        // keys promoted to a comb since fgv_init
-  uint32_t promote_per_call = 32; // comb builds from the promotion queue per call (FGV_PROMOTE_PER_CALL)
+  uint32_t promote_per_call = 8;  // comb builds from the promotion queue per call (FGV_PROMOTE_PER_CALL)
   std::vector<uint32_t> promo_backlog;  // queued ids not built yet
   // per-block outcomes (fgv_set_block_outcomes) and the fallback counters (fgv_unsupported_stats)
   bool block_outcomes = false;

@@ -36,6 +36,7 @@
 #define POINT_EXACT_WGS 64   // k_point's grid behind k_point28 (the hand-overs: exceptional additions only)
 #define DIG_STRIDE 96        // bytes per item of the digit array (G digits, then Q digits at DIG_Q_OFF)
 #define ST_PENDING 0xFF
+#define ST_VB 0xFE       // k_inv: pending on the variable-base kernels (k_vb_mul / k_vb_fin finish it)
 
 struct apoint_raw {  // affine point, Montgomery limbs (64 B, 16-B aligned)
   uint32_t x[8];

@@ -334,7 +334,10 @@ __global__ __launch_bounds__(INV_THREADS) void k_inv(uint32_t n, const uint32_t 
         uint32_t b0 = 0;
         if (ln == lead) b0 = atomicAdd(vb_cnt, (uint32_t)__popcll(m));
         b0 = (uint32_t)__shfl((int)b0, (int)lead);
-        if (vb) vb_list[b0 + (uint32_t)__popcll(m & ((1ull << ln) - 1ull))] = i;
+        if (vb) {
+          vb_list[b0 + (uint32_t)__popcll(m & ((1ull << ln) - 1ull))] = i;
+          status[i] = ST_VB;  // (the path is decided here, once: kmap may change under a batch)
+        }
       }
     }
 #pragma unroll
@@ -388,7 +391,7 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint32_t *__rest
     redo[1] = 0u;
     redo[2] = 0u;
   }
-  if (i >= (dn ? min(n, *dn) : n) || status[i] != ST_PENDING) return;
+  if (i >= (dn ? min(n, *dn) : n) || (status[i] != ST_PENDING && status[i] != ST_VB)) return;
   uint32_t w[8], r[8], e[8], u1[8], u2[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
