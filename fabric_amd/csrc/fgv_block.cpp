@@ -2273,6 +2273,9 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   // (the counters' D2H is queued by fgv_block_validate_dev_finish, behind whatever the caller
   // queues after the fold -- the finalize -- so it never sits between the fold and the finalize)
   B.misc_src = misc;
+  c->fin_misc_src = c->fold_codes ? misc : nullptr;  // (k_fin_dups copies them out: fin_back)
+  c->fin_misc_dst = B.misc.as<uint32_t>();
+  c->fin_misc_done = false;
   c->t_bd_pre = ms_since(t1);
   c->t_host_assemble = c->t_bd_pre;
   S->t_enq = clk::now();
@@ -2322,8 +2325,10 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   if (S->pending < 0) return FGV_OK;
   BdSet &B = S->set[S->pending];
   S->pending = -1;
-  if (B.misc_src) HIP_TRY(hipMemcpyAsync(B.misc.p, B.misc_src, 64, hipMemcpyDeviceToHost, c->stream));
+  if (B.misc_src && !c->fin_misc_done) HIP_TRY(hipMemcpyAsync(B.misc.p, B.misc_src, 64, hipMemcpyDeviceToHost, c->stream));
   B.misc_src = nullptr;
+  c->fin_misc_done = false;
+  c->fin_misc_src = nullptr;
   HIP_TRY(fgv_stream_wait(c->stream, c->spin));
   const auto t_woke = clk::now();
   fgv_read_block_job_times(c);

@@ -1394,8 +1394,16 @@ static int fin_back(fgv_ctx *c, hipStream_t st, const FinPlan &F, const uint8_t 
   }();
   uint8_t *zc = nullptr;
   if (zc_on && hipHostGetDevicePointer(reinterpret_cast<void **>(&zc), c->hb_fflags.p, 0) != hipSuccess) zc = nullptr;
+  // (the fused call: the batch counters ride along, written by the last workgroup)
+  uint32_t *mz = nullptr;
+  if (zc && codes_done && c->fin_misc_src && c->fin_misc_dst &&
+      hipHostGetDevicePointer(reinterpret_cast<void **>(&mz), c->fin_misc_dst, 0) != hipSuccess)
+    mz = nullptr;
   hipLaunchKernelGGL(k_fin_dups, grid, blk, 0, st, n32, c->fz_pslot.as<uint32_t>(), c->fz_minvalid.as<uint32_t>(),
-                     c->fz_flags.as<uint8_t>(), codes_done ? c->fold_unsup : nullptr, zc);
+                     c->fz_flags.as<uint8_t>(), codes_done ? c->fold_unsup : nullptr, zc,
+                     mz ? c->fin_misc_src : nullptr, mz, c->redo.as<uint32_t>() + RD_FIN_DONE);
+  c->fin_misc_done = mz != nullptr;
+  c->fin_misc_src = nullptr;
   HIP_TRY(hipGetLastError());
   if (!zc) HIP_TRY(hipMemcpyAsync(c->hb_fflags.p, c->fz_flags.p, F.P, hipMemcpyDeviceToHost, st));
   return FGV_OK;

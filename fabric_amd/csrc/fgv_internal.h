@@ -170,6 +170,11 @@ struct fgv_ctx {
   bool want_early_fin = false, early_fin = false;
   bool fold_codes = false;  // k_bd_fold ran the finalize's codes step (the finalize runs the rest)
   uint32_t *fold_unsup = nullptr;  // with fold_codes: the batch's flag word (k_fin_dups)
+  // with fold_codes: the batch's 64 B of counters in HBM and its pinned host copy; k_fin_dups's last
+  // workgroup writes them straight into the mapped host copy (fin_misc_done), no copy kernel
+  const uint32_t *fin_misc_src = nullptr;
+  uint32_t *fin_misc_dst = nullptr;
+  bool fin_misc_done = false;
   bool early_fin_on = [] {  // A/B knob FGV_EARLY_FIN=0: the whole finalize after the fold
     const char *e = getenv("FGV_EARLY_FIN");
     return !(e && atoi(e) == 0);

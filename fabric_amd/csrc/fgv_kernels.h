@@ -69,6 +69,7 @@ __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw 
 #define RD_VB_MUL 4
 #define RD_VB_FIN 5
 #define RD_VB_DONE 6
+#define RD_FIN_DONE 8     // finished k_fin_dups workgroups (the last one copies the counters out)
 #define VB_FIN_WGS 32        // k_vb_fin workgroups (256 threads)
 #define VB_PROMO_CAP 1022   // promotion queue: [0] count, [1] the last batch's variable-base items,
                             // then ids whose use count reached the threshold
@@ -205,4 +206,4 @@ __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *row
 __global__ void k_fin_index_dev(uint32_t P, const DevTx *txs, const uint64_t *bases, const uint8_t *digests,
                                 uint8_t *keys, uint32_t *owner, int32_t *minblk, uint32_t mask, uint64_t seed, uint32_t prio);
 __global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags, uint32_t *unsup,
-                           uint8_t *out);
+                           uint8_t *out, const uint32_t *misc_src, uint32_t *misc_out, uint32_t *done);

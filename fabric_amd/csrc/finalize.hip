@@ -213,23 +213,39 @@ __global__ void k_fin_codes(uint32_t P, const uint8_t *recs, const uint32_t *row
 // of a txid was later failed by the key-level walk (blockdev.hip kl_walk_block), so the txid's
 // first VALID transaction is not known here -> the batch is unsupported (bit 2)
 __global__ void k_fin_dups(uint32_t P, const uint32_t *pslot, const uint32_t *minvalid, uint8_t *flags,
-                           uint32_t *unsup, uint8_t *out) {
+                           uint32_t *unsup, uint8_t *out, const uint32_t *misc_src, uint32_t *misc_out,
+                           uint32_t *done) {
   __builtin_amdgcn_s_setprio(3);  // the last kernel of the back half; the next front half runs beside it
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  uint8_t f = flags[p];
-  if (f == 0 && pslot[p] != 0xFFFFFFFFu) {
-    const uint32_t m = minvalid[pslot[p]];
-    if (m < p) {
-      if (unsup && flags[m] != 0) {  // the first VALID position was failed by the key-level walk
-        atomicOr(unsup, 2u);
-        f = 0xFD;  // (undecided: the per-block outcomes mark its block unsupported)
-      } else {
-        f = 9;  // markTXIdDuplicates: an earlier VALID tx of this block
+  if (p < P) {
+    uint8_t f = flags[p];
+    if (f == 0 && pslot[p] != 0xFFFFFFFFu) {
+      const uint32_t m = minvalid[pslot[p]];
+      if (m < p) {
+        if (unsup && flags[m] != 0) {  // the first VALID position was failed by the key-level walk
+          atomicOr(unsup, 2u);
+          f = 0xFD;  // (undecided: the per-block outcomes mark its block unsupported)
+        } else {
+          f = 9;  // markTXIdDuplicates: an earlier VALID tx of this block
+        }
+        flags[p] = f;
       }
-      flags[p] = f;
+    }
+    // (out: the caller's pinned flag buffer, mapped -- no copy kernel behind this one)
+    if (out) out[p] = f;
+  }
+  if (!misc_out) return;
+  // the batch counters (misc_src[5] may have just been set above) to the mapped host copy by the
+  // last workgroup to finish
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t t = atomicAdd(done, 1u);
+    if (t == gridDim.x - 1) {
+      __threadfence();
+      for (int k = 0; k < 16; k++) misc_out[k] = __atomic_load_n(misc_src + k, __ATOMIC_RELAXED);
+      __threadfence_system();
+      atomicExch(done, 0u);
     }
   }
-  // (out: the caller's pinned flag buffer, mapped -- no copy kernel behind this one)
-  if (out) out[p] = f;
 }
