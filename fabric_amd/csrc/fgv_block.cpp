@@ -265,6 +265,9 @@ struct fgv_block_state {
   int parse_mode = 0;  // 0: device parse (host parser for capacity overflows), 1: host parse
   BdSet set[2];
   int ahead = -1;  // set holding a front half enqueued ahead of its call (-1: none)
+  bool ahead_deferred = false;  // a front half to launch once the caller's finalize is queued
+  fgv_ctx::NextBatch ahead_nx{};
+  int ahead_cur = 0;
   int last = 1;    // set of the last call
   int pending = -1;           // set enqueued by _enqueue and not yet finished
   double nv_per_tx = 0;       // verifies per tx of the last batch (lanes-per-verify estimate)
@@ -2145,6 +2148,56 @@ static void drain_ahead(fgv_ctx *c, fgv_block_state *S) {
 
 void fgv_block_drain(fgv_ctx *c) { drain_ahead(c, c->blk); }
 
+// The next batch's front half, ahead of its call, while this back half runs: its device copy is
+// known (caller-resident, or being prefetched by the copy stream).
+static void launch_ahead(fgv_ctx *c, fgv_block_state *S, const fgv_ctx::NextBatch &nx, int cur) {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+  // Measured on MI355X (C2, 32 x 500-tx batches, fused single-GPU call; DESIGN.md s5,
+  // profiles/round3_ab): enqueued at once (2, the default) 0.715-0.724 ms per step against 0.773-
+  // 0.799 not ahead (0), in the full default bench and in the lean A/B harness alike; after this
+  // batch's ECDSA (1) or after its fold (3) it collides with k_point28 or with the next call's own
+  // kernels.  fgv_set_ahead / FGV_AHEAD select a placement (A/B).
+  const int ahead_mode = c->ahead_mode;
+  if (nx.n && nx.d_blocks && ahead_mode) {
+    BdSet &A = S->set[cur ^ 1];
+    hipEvent_t after = (ahead_mode == 1 && c->stage_ran)   ? c->ev[6]
+                       : (ahead_mode == 4 && c->stage_ran) ? c->ev[5]
+                       : ahead_mode == 3                   ? c->kev[9]
+                                                           : nullptr;
+    // FGV_PREFIX_AHEAD=1: the next batch's k_bd_emit / k_der / k_inv run ahead with its front
+    // half.  Measured on MI355X (C2 lean harness, alternating on one box, profiles/round3_ab/
+    // prefix_*): 0.748 / 0.753 ms per step ahead against 0.683 / 0.670 at the call -- beside the
+    // current back half they stretch k_point28 more than they shorten the chain -- so off.
+    static const bool prefix_ahead = [] {
+      const char *e = getenv("FGV_PREFIX_AHEAD");
+      return e && atoi(e) != 0;
+    }();
+    // (with keys on the variable-base kernels the prefix stays in the call: their list and
+    // counters belong to one batch at a time)
+    const auto tf = clk::now();
+    if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after,
+                     prefix_ahead && c->n_vb == 0 && !c->kt_busy) == FGV_OK)
+      S->ahead = cur ^ 1;
+    else
+      drain_ahead(c, S), S->ahead = -1;  // (the next call starts it again and reports any error)
+    c->t_kern[11] = ms_since(tf);  // host time to enqueue it (its pre-split join included)
+  } else {
+    c->t_kern[11] = 0;
+  }
+}
+
+void fgv_block_launch_deferred_ahead(fgv_ctx *c, bool launch) {
+  fgv_block_state *S = c->blk;
+  if (!S || !S->ahead_deferred) return;
+  S->ahead_deferred = false;
+  if (launch) {
+    launch_ahead(c, S, S->ahead_nx, S->ahead_cur);
+  } else {
+    c->t_kern[11] = 0;
+  }
+}
+
 int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblocks, const uint8_t *const *h_blocks,
                                    const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
                                    const uint32_t *tx_hi, fgv_tx_result *d_res, size_t res_cap, size_t *ntx_out) {
@@ -2279,39 +2332,16 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   c->t_bd_pre = ms_since(t1);
   c->t_host_assemble = c->t_bd_pre;
   S->t_enq = clk::now();
-  // --- the next batch's front half, ahead of its call, while this back half runs: its
-  // device copy is known (caller-resident, or being prefetched by the copy stream)
-  // Measured on MI355X (C2, 32 x 500-tx batches, fused single-GPU call; DESIGN.md s5,
-  // profiles/round3_ab): enqueued at once (2, the default) 0.715-0.724 ms per step against 0.773-
-  // 0.799 not ahead (0), in the full default bench and in the lean A/B harness alike; after this
-  // batch's ECDSA (1) or after its fold (3) it collides with k_point28 or with the next call's own
-  // kernels.  fgv_set_ahead / FGV_AHEAD select a placement (A/B).
-  const int ahead_mode = c->ahead_mode;
-  if (nx.n && nx.d_blocks && ahead_mode) {
-    BdSet &A = S->set[cur ^ 1];
-    hipEvent_t after = (ahead_mode == 1 && c->stage_ran)   ? c->ev[6]
-                       : (ahead_mode == 4 && c->stage_ran) ? c->ev[5]
-                       : ahead_mode == 3                   ? c->kev[9]
-                                                           : nullptr;
-    // FGV_PREFIX_AHEAD=1: the next batch's k_bd_emit / k_der / k_inv run ahead with its front
-    // half.  Measured on MI355X (C2 lean harness, alternating on one box, profiles/round3_ab/
-    // prefix_*): 0.748 / 0.753 ms per step ahead against 0.683 / 0.670 at the call -- beside the
-    // current back half they stretch k_point28 more than they shorten the chain -- so off.
-    static const bool prefix_ahead = [] {
-      const char *e = getenv("FGV_PREFIX_AHEAD");
-      return e && atoi(e) != 0;
-    }();
-    // (with keys on the variable-base kernels the prefix stays in the call: their list and
-    // counters belong to one batch at a time)
-    const auto tf = clk::now();
-    if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after,
-                     prefix_ahead && c->n_vb == 0 && !c->kt_busy) == FGV_OK)
-      S->ahead = cur ^ 1;
-    else
-      drain_ahead(c, S), S->ahead = -1;  // (the next call starts it again and reports any error)
-    c->t_kern[11] = ms_since(tf);  // host time to enqueue it (its pre-split join included)
+  // --- the next batch's front half, ahead of its call (launch_ahead).  The fused single-GPU
+  // call defers it until its finalize kernels are queued: the host spends ~0.1 ms enqueuing a
+  // front half (its pre-split join included), and k_fin_dups queued behind that started ~65 us
+  // after the fold it follows (MI355X C2 trace, r4e)
+  if (c->defer_ahead) {
+    S->ahead_nx = nx;
+    S->ahead_cur = cur;
+    S->ahead_deferred = true;
   } else {
-    c->t_kern[11] = 0;
+    launch_ahead(c, S, nx, cur);
   }
   S->pending = cur;
   return FGV_OK;

@@ -1857,10 +1857,18 @@ static int validate_blocks_locked(fgv_ctx *c, size_t nblocks, const uint8_t *con
     const size_t bound = std::min(flags_cap, bytes / 2 + nblocks);
     if (!c->fz_res.ensure(bound * sizeof(fgv_tx_result) + 64)) return FGV_ENOMEM;
     c->want_early_fin = c->early_fin_on;
+    // (the next batch's front half is queued after this batch's finalize: defer_ahead)
+    static const bool defer = [] {
+      const char *e = getenv("FGV_DEFER_AHEAD");
+      return !e || atoi(e) != 0;
+    }();
+    c->defer_ahead = defer;
     rc = fgv_block_validate_dev_enqueue(c, c->blk, nblocks, blocks, lens, dev.data(), nullptr, nullptr,
                                         c->fz_res.as<fgv_tx_result>(), bound, ntx);
     c->want_early_fin = false;
+    c->defer_ahead = false;
     if (rc) {
+      fgv_block_launch_deferred_ahead(c, false);
       fgv_block_validate_dev_finish(c, c->blk);  // (waits for anything already queued)
       c->early_fin = c->fold_codes = false;
       return rc;
@@ -1868,6 +1876,7 @@ static int validate_blocks_locked(fgv_ctx *c, size_t nblocks, const uint8_t *con
     size_t total = 0;
     for (size_t b = 0; b < nblocks; b++) total += ntx[b];
     if (total) rc = finalize_dev_core(c, nblocks, ntx, 1, total, c->fz_res.as<uint8_t>(), flags, nullptr, nullptr, true);
+    fgv_block_launch_deferred_ahead(c, rc == FGV_OK);
     const int rv = fgv_block_validate_dev_finish(c, c->blk);
     if (rc) return rc;
     if (rv == FGV_OK) {

@@ -175,6 +175,7 @@ struct fgv_ctx {
   const uint32_t *fin_misc_src = nullptr;
   uint32_t *fin_misc_dst = nullptr;
   bool fin_misc_done = false;
+  bool defer_ahead = false;  // the fused call: the next front half after the finalize is queued
   bool early_fin_on = [] {  // A/B knob FGV_EARLY_FIN=0: the whole finalize after the fold
     const char *e = getenv("FGV_EARLY_FIN");
     return !(e && atoi(e) == 0);
@@ -333,6 +334,8 @@ int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blo
                               const uint8_t *dig = nullptr, const uint32_t *dn = nullptr, size_t n_est = 0);
 // wait for (and forget) a device-parse front half enqueued ahead of its call
 void fgv_block_drain(fgv_ctx *c);
+// the front half fgv_block_validate_dev_enqueue deferred (c->defer_ahead): launch it, or drop it
+void fgv_block_launch_deferred_ahead(fgv_ctx *c, bool launch = true);
 void fgv_read_block_job_times(fgv_ctx *c);
 int fgv_verify_prefix_dev(fgv_ctx *c, hipStream_t st, size_t cap, const uint32_t *dn, const uint8_t *sigblk,
                           uint8_t *vst, DevBuf &r, DevBuf &s, DevBuf &w, DevBuf &wscr);
