@@ -215,6 +215,11 @@ static int promote_consume(fgv_ctx *c) {
   }
   if (c->comb_free.empty()) c->promo_backlog.clear();  // (nothing more can be promoted)
   if (c->promo_backlog.empty()) return FGV_OK;
+  // the previous builds still running: leave the queue for a later call (never block the host)
+  if (c->kt_busy) {
+    if (hipEventQuery(c->kt_ev) != hipSuccess) return FGV_OK;
+    c->kt_busy = false;
+  }
   // at most promote_per_call builds per call (~80 us of the whole chip each), so a burst of keys
   // reaching the threshold together spreads over calls instead of stalling one
   const size_t take = std::min<size_t>(c->promo_backlog.size(), c->promote_per_call);

@@ -145,7 +145,7 @@ struct fgv_ctx {
   uint32_t promote_uses = 64;     // variable-base verifies of one key before its comb is built
   uint32_t adhoc_comb_uses = 32;  // uses of an ad-hoc key in one call for a comb
   uint64_t n_promoted = 0;        // keys promoted to a comb since fgv_init
-  uint32_t promote_per_call = 8;  // comb builds from the promotion queue per call (FGV_PROMOTE_PER_CALL)
+  uint32_t promote_per_call = 32; // comb builds from the promotion queue per call (FGV_PROMOTE_PER_CALL)
   std::vector<uint32_t> promo_backlog;  // queued ids not built yet
   // per-block outcomes (fgv_set_block_outcomes) and the fallback counters (fgv_unsupported_stats)
   bool block_outcomes = false;

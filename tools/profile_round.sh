@@ -21,4 +21,7 @@ timeout -k 10 300 $P --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d $OUT/pmc
 timeout -k 10 300 $P --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc_blk_write -o run -- python bench.py --steps 5 --warmup 1 --cpu-threads 0 --no-pcie --no-latency > $OUT/pmc_blk_write.json 2> $OUT/pmc_blk_write.err
 timeout -k 10 300 $P --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d $OUT/pmc_sig_fetch -o run -- python bench.py --workload sig --steps 3 --warmup 1 --cpu-threads 0 > $OUT/pmc_sig_fetch.json 2> $OUT/pmc_sig_fetch.err
 timeout -k 10 300 $P --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc_sig_write -o run -- python bench.py --workload sig --steps 3 --warmup 1 --cpu-threads 0 > $OUT/pmc_sig_write.json 2> $OUT/pmc_sig_write.err
+# the cold-key path: C4 with every item its own key (k_vb_mul dominant)
+timeout -k 10 300 $P --kernel-trace --stats -d $OUT/sigchurn -o run -- python bench.py --workload sig --sig-keys 131072 --steps 5 --warmup 1 --cpu-threads 0 > $OUT/sigchurn.json 2> $OUT/sigchurn.err
+timeout -k 10 300 $P --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d $OUT/pmc_sigchurn_valu -o run -- python bench.py --workload sig --sig-keys 131072 --steps 3 --warmup 1 --cpu-threads 0 > $OUT/pmc_sigchurn_valu.json 2> $OUT/pmc_sigchurn_valu.err
 echo profile-done

@@ -61,7 +61,7 @@ def main(src, rnd):
              "Collected by `tools/profile_round.sh` (kernel-trace/stats runs and separate `--pmc` runs, "
              "as MI355X_MICROARCH.md prescribes).  Profiled runs clock lower than un-profiled ones "
              "(DVFS), so durations here read a few % above the bench's live HIP-event numbers.", ""]
-    for wl in ("block", "sig", "mvcc"):
+    for wl in ("block", "sig", "mvcc", "sigchurn"):
         p = os.path.join(src, wl, "run_kernel_stats.csv")
         if not os.path.exists(p):
             continue
@@ -85,7 +85,8 @@ def main(src, rnd):
             lines.append(f"| {k[:60]} | {v['calls']} | {v['avg_us']:.1f} | {v['pct']:.1f} |")
         lines.append("")
     for vname, title in (("pmc_valu", "sig workload: 131,072 verifies per dispatch"),
-                         ("pmc_blk_valu", "block workload: one C2 step of 16k transactions")):
+                         ("pmc_blk_valu", "block workload: one C2 step of 16k transactions"),
+                         ("pmc_sigchurn_valu", "sig churn: 131,072 verifies, every item its own key")):
       p = os.path.join(src, vname, "run_counter_collection.csv")
       if os.path.exists(p):
         lines += [f"## VALU counters ({title})", "",
