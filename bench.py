@@ -41,10 +41,10 @@ METRIC = "ECDSA-P256 verifies/sec + validated tx/sec per block at 1/2/4/8 MI355X
 # 22-bit generator windows + 20 signed 13-bit key windows), the first one loaded, so 31 mixed
 # additions x (8 field mults x 64 + 3 squarings x 36 products) + the projective x-check (3 x 64)
 PRODUCTS_POINT = 31 * (8 * 64 + 3 * 36) + 3 * 64
-# the same for one variable-base verify in k_vb_mul: 8 lanes, each 14 mixed
-# additions (table d * Q_s), 28 doublings (3 mults + 5 squarings), 7.5 expected window additions
-# and 3 butterfly additions (12 mults + 4 squarings), + u2 = r * s^-1 (sn_mul, 128 products)
-VB_MUL_PRODUCTS = 8 * (14 * (8 * 64 + 3 * 36) + 28 * (3 * 64 + 5 * 36) + 10.5 * (12 * 64 + 4 * 36) + 128)
+# the same for one variable-base verify in k_vb_mul: 8 lanes, each 28 doublings
+# (3 mults + 5 squarings), 7.5 expected mixed additions from the key's table (8 mults + 3
+# squarings) and 3 butterfly additions (12 mults + 4 squarings), + u2 = r * s^-1 (sn_mul, 128)
+VB_MUL_PRODUCTS = 8 * (28 * (3 * 64 + 5 * 36) + 7.5 * (8 * 64 + 3 * 36) + 3 * (12 * 64 + 4 * 36) + 128)
 # chip-wide v_mad_u64_u32 issue rate measured by tools/valu_peak.hip (profiles/round1_valu_peak.json)
 PEAK_MAD_PER_S = float(os.environ.get("FGV_PEAK_MAD", "3.106e13"))
 # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz simple int32 VALU lane-ops

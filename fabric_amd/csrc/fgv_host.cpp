@@ -286,10 +286,33 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
     if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi) != hipSuccess) return fail(FGV_EDEVICE);
-    if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
-    if (hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+    // FGV_FRONT_RESERVE=k (A/B): the front-half streams (payload, k_bd_sha, parse / identities)
+    // leave k CUs per XCD to the main stream, so the back half's short kernels (k_point, fold,
+    // dups, emit ...) find CUs while the next batch's front half holds the rest.  CUs 33 x + 8 j
+    // (x < 8, j < k): k per XCD whether CU ids run XCD-major or round-robin over the XCDs.
+    static const int reserve = [] {
+      const char *e = getenv("FGV_FRONT_RESERVE");
+      const int v = e ? atoi(e) : 0;
+      return v >= 0 && v <= 3 ? v : 0;
+    }();
+    int ncu0 = 0;
+    if (reserve && hipDeviceGetAttribute(&ncu0, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess &&
+        ncu0 == 256) {
+      uint32_t mask[8];
+      for (auto &m : mask) m = 0xFFFFFFFFu;
+      for (int x = 0; x < 8; x++)
+        for (int j = 0; j < reserve; j++) {
+          const int cu = 33 * x + 8 * j;
+          mask[cu / 32] &= ~(1u << (cu % 32));
+        }
+      for (hipStream_t *sp : {&c->stream2, &c->stream3, &c->streamF})
+        if (hipExtStreamCreateWithCUMask(sp, 8, mask) != hipSuccess) return fail(FGV_EDEVICE);
+    } else {
+      if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+      if (hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+      if (hipStreamCreateWithPriority(&c->streamF, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+    }
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
-    if (hipStreamCreateWithPriority(&c->streamF, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->streamV, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->streamK, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipEventCreateWithFlags(&c->kt_ev, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
@@ -484,13 +507,14 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
     HIP_TRY(hipStreamWaitEvent(c->streamV, c->vb_ev[0], 0));
     c->vb_timed = tim;
     if (tim) HIP_TRY(hipEventRecord(c->vb_t[0], c->streamV));
-    // FGV_VB_WGS = workgroups per CU (k_vb_mul fits 3 waves per SIMD; default 2: beside k_point28)
+    // FGV_VB_WGS = workgroups per CU (k_vb_mul fits 3 waves per SIMD, k_vb_mul_o4 4; default 2:
+    // beside k_point28)
     static const uint32_t vb_wgs = [] {
       const char *e = getenv("FGV_VB_WGS");
       const int v = e ? atoi(e) : 2;
-      return (uint32_t)(v >= 1 && v <= 3 ? v : 2);
+      return (uint32_t)(v >= 1 && v <= 4 ? v : 2);
     }();
-    hipLaunchKernelGGL(k_vb_mul, dim3(vb_wgs * c->n_cu), dim3(VB_THREADS), 0, c->streamV, N, d_slot,
+    hipLaunchKernelGGL(vb_wgs == 4 ? k_vb_mul_o4 : k_vb_mul, dim3(vb_wgs * c->n_cu), dim3(VB_THREADS), 0, c->streamV, N, d_slot,
                        c->vbt.as<uint32_t>(), d_r, w.as<uint32_t>(), redo, redo + RD_VB_MUL,
                        c->vblist.as<uint32_t>(), c->vbacc.as<uint32_t>(),
                        c->vbuse.as<uint32_t>(), c->promote_uses, c->vbpromo.as<uint32_t>());

@@ -78,6 +78,9 @@ __global__ void k_kmap_set(const uint32_t *ids, const uint32_t *slots, uint32_t 
 __global__ void k_vb_mul(uint32_t n, const uint32_t *key_slot, const uint32_t *vbt, const uint32_t *r_limbs,
                          const uint32_t *w_in, const uint32_t *ctr, uint32_t *take, const uint32_t *list,
                          uint32_t *acc, uint32_t *uses, uint32_t promote, uint32_t *promo);
+__global__ void k_vb_mul_o4(uint32_t n, const uint32_t *key_slot, const uint32_t *vbt, const uint32_t *r_limbs,
+                            const uint32_t *w_in, const uint32_t *ctr, uint32_t *take, const uint32_t *list,
+                            uint32_t *acc, uint32_t *uses, uint32_t promote, uint32_t *promo);
 __global__ void k_vb_fin(uint32_t n, uint8_t *status, const apoint_raw *gtab28, const int8_t *digits,
                          const uint32_t *r_limbs, uint32_t *ctr, const uint32_t *list, const uint32_t *acc);
 __global__ void k_gtab(apoint_raw *tables28, jpoint_raw *scratch, uint32_t w);

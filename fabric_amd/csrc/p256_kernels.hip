@@ -884,14 +884,11 @@ FGV_DEV void load_jp(jpoint &p, const uint32_t *s) {
 // ~330 field multiplications.  uses[id] counts the key's variable-base verifies;
 // the one that reaches `promote` queues the id (promo[0] count, ids from promo[2]) for a comb build
 // by the host; promo[1] = the batch's variable-base items.
-__global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_t *__restrict__ key_slot,
-                                                      const uint32_t *__restrict__ vbt,
-                                                      const uint32_t *__restrict__ r_limbs,
-                                                      const uint32_t *__restrict__ w_in,
-                                                      const uint32_t *__restrict__ ctr, uint32_t *__restrict__ take,
-                                                      const uint32_t *__restrict__ list, uint32_t *__restrict__ acc,
-                                                      uint32_t *__restrict__ uses, uint32_t promote,
-                                                      uint32_t *__restrict__ promo) {
+FGV_DEV void vb_mul_body(uint32_t n, const uint32_t *__restrict__ key_slot, const uint32_t *__restrict__ vbt,
+                         const uint32_t *__restrict__ r_limbs, const uint32_t *__restrict__ w_in,
+                         const uint32_t *__restrict__ ctr, uint32_t *__restrict__ take,
+                         const uint32_t *__restrict__ list, uint32_t *__restrict__ acc, uint32_t *__restrict__ uses,
+                         uint32_t promote, uint32_t *__restrict__ promo) {
   __builtin_amdgcn_s_setprio(2);
   const uint32_t cnt = ctr[RD_VB_CNT];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&promo[1], cnt);  // (statistics: fgv_key_stats)
@@ -964,6 +961,19 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(uint32_t n, const uint32_
       if (s < VB_PROMO_CAP) atomicExch(&promo[2 + s], id);
     }
   }
+}
+
+#define VB_MUL_ARGS                                                                                               \
+  uint32_t n, const uint32_t *__restrict__ key_slot, const uint32_t *__restrict__ vbt,                            \
+      const uint32_t *__restrict__ r_limbs, const uint32_t *__restrict__ w_in, const uint32_t *__restrict__ ctr, \
+      uint32_t *__restrict__ take, const uint32_t *__restrict__ list, uint32_t *__restrict__ acc,                 \
+      uint32_t *__restrict__ uses, uint32_t promote, uint32_t *__restrict__ promo
+__global__ __launch_bounds__(VB_THREADS) void k_vb_mul(VB_MUL_ARGS) {
+  vb_mul_body(n, key_slot, vbt, r_limbs, w_in, ctr, take, list, acc, uses, promote, promo);
+}
+// the same held to 128 VGPRs (4 waves per SIMD, a few more spills): FGV_VB_WGS=4 (A/B)
+__global__ __launch_bounds__(VB_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_vb_mul_o4(VB_MUL_ARGS) {
+  vb_mul_body(n, key_slot, vbt, r_limbs, w_in, ctr, take, list, acc, uses, promote, promo);
 }
 
 // k_vb_fin: after k_prep -- acc[j] + sum of the 12 generator comb terms of u1 (k_prep's digits),

@@ -17,6 +17,7 @@
 #   lattrace         the same of tools/latency_probe.py (single-block calls)
 #   profile          tools/profile_round.sh (stats + PMC passes of every workload)
 #   py:<file>        python <file> (a micro-benchmark or check under tools/)
+#   with:VAR=VAL:<step>  <step> with VAR=VAL in its environment
 # Output: gpurun_out/<out-name>/.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -97,6 +98,10 @@ for step in "$@"; do
       tail -1 $O/lat.out ;;
     profile)
       PROF_OUT=$O/prof bash tools/profile_round.sh || { echo profile failed; exit 1; } ;;
+    with:*)
+      # with:VAR=VAL:<step> -- any other step with VAR=VAL set (its output under <out>/<VAR_VAL>/)
+      spec=${step#with:}; kv=${spec%%:*}; sub=${spec#*:}; tag=$(echo $kv | tr '=' '_')
+      env $kv bash "$0" "${O#gpurun_out/}/$tag" "$sub" || exit 1 ;;
     py:*)
       f=${step#py:}
       timeout -k 10 300 python -u $f > $O/$(basename $f).out 2>&1 || { echo "$f failed"; tail -30 $O/$(basename $f).out; exit 1; }
