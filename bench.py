@@ -418,10 +418,13 @@ def run_block(args, world, rank, local, dev_fn):
         # batch k's call pre-splits (and, host-resident, pre-copies) batch k+1 of the rotation
         # one GPU: validation + finalize in one call (fgv_validate_blocks_pipelined); N > 1: each rank
         # validates its shard, the ranks all-gather the records, every rank finalizes
-        return [_lib.BlockStep(eng, batches[k], lo, hi, send.data_ptr(), rows, ntx, world, recv.data_ptr(), flags_out,
-                               plan=plan, presplit=not args.no_presplit, next_batch=batches[(k + 1) % NB],
-                               fused=world == 1 and not args.shard_protocol)
-                for k in range(NB)]
+        st = [_lib.BlockStep(eng, batches[k], lo, hi, send.data_ptr(), rows, ntx, world, recv.data_ptr(), flags_out,
+                             plan=plan, presplit=not args.no_presplit, next_batch=batches[(k + 1) % NB],
+                             fused=world == 1 and not args.shard_protocol)
+              for k in range(NB)]
+        for k, s in enumerate(st):
+            s.after_next = batches[(k + 2) % NB]
+        return st
 
     integ = dict(ms=0.0, ok=True)
 
@@ -455,6 +458,10 @@ def run_block(args, world, rank, local, dev_fn):
         if world > 1:
             shard.allgather_device(send, recv)
         f = bs.finalize()
+        if args.presplit_early and world == 1 and not args.no_presplit:
+            # a peer walks a batch's framing once its blocks are delivered, ahead of the call
+            # before it (fgv_presplit): that call's ahead front half then skips the wait for it
+            eng.presplit(bs.after_next)
         if s is not None:
             integ_fut.pop(s).result()
         return f
@@ -936,6 +943,8 @@ def main():
     ap.add_argument("--latency-reps", type=int, default=20)
     ap.add_argument("--host-parse", action="store_true", help="parse transactions on host threads (A/B)")
     ap.add_argument("--no-presplit", action="store_true", help="walk each batch's framing inside its validation call (A/B)")
+    ap.add_argument("--presplit-early", action="store_true",
+                    help="start batch k+2's framing walk (fgv_presplit) when call k returns (A/B)")
     ap.add_argument("--shard-protocol", action="store_true",
                     help="N=1 through the multi-GPU protocol (shard_dev + finalize_flags_dev) instead of the fused call")
     args = ap.parse_args()

@@ -1841,6 +1841,9 @@ static int split_batch(ThreadPool &pool, size_t nblocks, const uint8_t *const *h
 int fgv_block_presplit(fgv_block_state *S, int device, size_t nblocks, const uint8_t *const *h_blocks,
                        const size_t *lens, const uint32_t *tx_lo, const uint32_t *tx_hi) {
   PreSplit &P = S->pre;
+  // the same batch requested again (the caller's own fgv_presplit earlier, then the call that
+  // announces it as its next): the walk already running or done stands
+  if (P.active && P.matches(nblocks, h_blocks, lens, tx_lo, tx_hi)) return FGV_OK;
   P.join();  // an earlier pre-split nobody used
   P.device = device;
   P.blocks.assign(h_blocks, h_blocks + nblocks);
