@@ -48,6 +48,14 @@ for step in "$@"; do
       timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail -20 $O/bench.err; exit 1; }
       show $O/bench.json bench value ms_per_step parity_vs_labels latency_1block_ms
       python3 -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print('roofline', r['kernel'], r['frac'], r.get('frac_profiled'), 'pcie', d['pcie_inclusive']['ms_per_step'], 'cpu', d['cpu_baseline']['value'])" ;;
+    leanx:*)
+      # leanx:<bench args, commas for spaces>:N -- N lean C2 runs with extra bench arguments (A/B)
+      spec=${step#leanx:}; n=${spec##*:}; xa=$(echo ${spec%:*} | tr ',' ' '); tag=$(echo ${spec%:*} | tr -c 'a-zA-Z0-9\n' '_')
+      for rep in $(seq 1 $n); do
+        timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --cpu-threads 0 --no-pcie --no-latency $xa > $O/leanx_${tag}_$rep.json 2> $O/leanx_${tag}_$rep.err \
+          || { echo leanx $xa failed; tail -20 $O/leanx_${tag}_$rep.err; exit 1; }
+        show $O/leanx_${tag}_$rep.json "lean $xa $rep" value ms_per_step parity_vs_labels
+      done ;;
     lean*)
       n=${step#lean}; n=${n:-1}
       for rep in $(seq 1 $n); do
@@ -67,14 +75,6 @@ for step in "$@"; do
       timeout -k 10 300 python -u bench.py --shard-protocol --steps 40 --warmup 5 --cpu-threads 0 --no-pcie --no-latency > $O/shardp.json 2> $O/shardp.err \
         || { echo shardp failed; tail -20 $O/shardp.err; exit 1; }
       show $O/shardp.json shardp value ms_per_step parity_vs_labels ;;
-    leanx:*)
-      # leanx:<bench args, commas for spaces>:N -- N lean C2 runs with extra bench arguments (A/B)
-      spec=${step#leanx:}; n=${spec##*:}; xa=$(echo ${spec%:*} | tr ',' ' '); tag=$(echo ${spec%:*} | tr -c 'a-zA-Z0-9\n' '_')
-      for rep in $(seq 1 $n); do
-        timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --cpu-threads 0 --no-pcie --no-latency $xa > $O/leanx_${tag}_$rep.json 2> $O/leanx_${tag}_$rep.err \
-          || { echo leanx $xa failed; tail -20 $O/leanx_${tag}_$rep.err; exit 1; }
-        show $O/leanx_${tag}_$rep.json "lean $xa $rep" value ms_per_step parity_vs_labels
-      done ;;
     churn)
       timeout -k 10 400 python -u bench.py --clients 16000 --steps 20 --warmup 3 --cpu-threads 0 --no-pcie > $O/churn.json 2> $O/churn.err \
         || { echo churn failed; tail -20 $O/churn.err; exit 1; }
