@@ -100,7 +100,7 @@ def roofline_vb(n_items, vb_ms):
 def profiled_dominant(workload="block"):
     """the top row of the latest committed per-step kernel stats (profiles/round*_<workload>_
     kernel_stats.csv: rocprofv3 --kernel-trace --stats of 32-block steps, the one-time comb
-    table builds excluded) -> (kernel, avg us, file); (None, None, None) without one"""
+    table builds and key preparations excluded) -> (kernel, avg us, file); (None, None, None) without one"""
     import csv
     import glob
     import re
@@ -108,7 +108,7 @@ def profiled_dominant(workload="block"):
     if not files:
         return None, None, None
     f = max(files, key=lambda p: int(re.search(r"round(\d+)", os.path.basename(p)).group(1)))
-    rows = [r for r in csv.DictReader(open(f)) if not r["Name"].startswith(("k_gtab", "k_keytab"))]
+    rows = [r for r in csv.DictReader(open(f)) if not r["Name"].startswith(("k_gtab", "k_keytab", "k_keyprep", "k_kmap_set"))]
     if not rows:
         return None, None, None
     top = max(rows, key=lambda r: float(r["TotalDurationNs"]))

@@ -814,8 +814,11 @@ __global__ __launch_bounds__(PL) void k_bd_parse(uint32_t ntx, const uint32_t *_
                                                  const uint64_t *__restrict__ bases, DevChannel ch,
                                                  DevTx *__restrict__ out, uint32_t *__restrict__ flags,
                                                  uint32_t *__restrict__ xhaz, KlDev kl, uint32_t touch) {
-  // front half: below the back half's verify chain (3), above k_bd_sha_payload (1)
-  __builtin_amdgcn_s_setprio(2);
+  // front half: below the back half's verify chain (3), above k_bd_sha (1); touch bit 8: at 3
+  // (FGV_FRONT_PRIO, A/B)
+  if (touch & 0x100u) __builtin_amdgcn_s_setprio(3);
+  else __builtin_amdgcn_s_setprio(2);
+  touch &= 0xFFu;
   __shared__ ParseLdsT<PL> L;
   const uint32_t lane = threadIdx.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -884,8 +887,9 @@ DEV int32_t ident_lookup(S ser, const DevChannel &ch, uint32_t l) {
 }
 __global__ __launch_bounds__(256) void k_bd_ident(uint32_t ntx, const DevTx *__restrict__ txs,
                                                   const uint64_t *__restrict__ bases, DevChannel ch,
-                                                  int32_t *__restrict__ ident) {
-  __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
+                                                  int32_t *__restrict__ ident, uint32_t prio) {
+  if (prio == 3) __builtin_amdgcn_s_setprio(3);  // (FGV_FRONT_PRIO, A/B)
+  else __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
   // ID_PAR groups per tx (one wave): group g resolves occurrences g, g + ID_PAR, ... -- a C2
   // transaction's creator and endorsers in one pass instead of one after the other
   const uint32_t grp = (blockIdx.x * blockDim.x + threadIdx.x) / ID_LANES;
@@ -1037,8 +1041,10 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
 #define BC_THREADS 1024u
 __global__ __launch_bounds__(BC_THREADS) void k_bd_count(uint32_t ntx, DevTx *__restrict__ txs, DevChannel ch,
                                                          const int32_t *__restrict__ ident,
-                                                         DevJobIdx *__restrict__ jobs, uint32_t *__restrict__ totals) {
-  __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
+                                                         DevJobIdx *__restrict__ jobs, uint32_t *__restrict__ totals,
+                                                         uint32_t prio) {
+  if (prio == 3) __builtin_amdgcn_s_setprio(3);  // (FGV_FRONT_PRIO, A/B)
+  else __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
   __shared__ uint32_t wtot[BJ_KINDS][BC_THREADS / 64], wbase[BJ_KINDS][BC_THREADS / 64];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   DevJobIdx J;

@@ -1769,9 +1769,10 @@ void bd_parse_lds_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint3
                          int32_t *ident);
 __global__ void k_bd_kl(uint32_t ntx, DevTx *txs, const uint64_t *bases, KlDev kl, uint32_t *flags);
 __global__ void k_head_pull(const uint4 *src, uint4 *dst, uint32_t n16);
-__global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident);
+__global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident,
+                           uint32_t prio);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
-                           uint32_t *totals);
+                           uint32_t *totals, uint32_t prio);
 __global__ void k_bd_sha(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
 __global__ void k_bd_sha2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
 __global__ void k_bd_sha_p2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig,
@@ -2062,6 +2063,12 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   // every line of each envelope requested before the walk (touch_lines): measured on MI355X (C2,
   // lean harness, one box) 0.665-0.667 ms per step against 0.702-0.724 without
   // (profiles/round3_ab/parse_t*); FGV_PARSE_TOUCH=0 turns it off (A/B)
+  // FGV_FRONT_PRIO=3: the front-half chain (parse, identities, counts) at the verify chain's wave
+  // priority instead of 2 (A/B: since round 4 it is the step's critical path)
+  static const uint32_t front_prio = [] {
+    const char *e = getenv("FGV_FRONT_PRIO");
+    return e && atoi(e) == 3 ? 3u : 2u;
+  }();
   static const uint32_t parse_touch = [] {
     const char *e = getenv("FGV_PARSE_TOUCH");
     return e ? (uint32_t)atoi(e) : 1u;
@@ -2097,7 +2104,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
                         fused_ident ? B.ident.as<int32_t>() : nullptr);
   else
     hipLaunchKernelGGL(k_bd_parse, dim3((N + parse_lanes - 1) / parse_lanes), dim3(parse_lanes), 0, sf, N, envtab,
-                       dbs, ch, dtx, misc + 5, misc + 16, B.kl, parse_touch);
+                       dbs, ch, dtx, misc + 5, misc + 16, B.kl, parse_touch | (front_prio == 3 ? 0x100u : 0u));
   HIP_TRY(hipEventRecord(B.ev[4], sf));
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one
@@ -2129,9 +2136,9 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   if (tim) HIP_TRY(hipEventRecord(B.ev[7], sf));
   if (!fused_ident)
     hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 * BD_ID_PAR + 255) / 256)), dim3(256), 0, sf, N,
-                       dtx, dbs, ch, B.ident.as<int32_t>());
+                       dtx, dbs, ch, B.ident.as<int32_t>(), front_prio);
   hipLaunchKernelGGL(k_bd_count, dim3((N + 1023) / 1024), dim3(1024), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
-                     B.jobs.as<DevJobIdx>(), misc);
+                     B.jobs.as<DevJobIdx>(), misc, front_prio);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(B.ev[6], sf));
   B.N = N;

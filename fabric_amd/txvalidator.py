@@ -59,13 +59,15 @@ def setup_channel(engine: Engine, channel: str, identities, chaincodes, committe
     for m in msps:
         engine.msp_declare(m)
     identities = [_as_identity(e) for e in identities]
-    # the public keys that get comb tables (fgv_roles_want_comb: peers, orderers, admins, unknown
-    # roles) first, in one fgv_keys_register call: their tables are then built by batched k_keytab
-    # launches (up to KT_BUILD_KEYS keys each) instead of one launch per key.  Client keys start
-    # on the variable-base kernels and are promoted by use.
-    pubs = [i.pub for _s, i in identities if i.key == "p256" and i.pub is not None and roles_want_comb(i.roles)]
-    if pubs:
-        engine.keys_register(np.frombuffer(b"".join(bytes(p) for p in pubs), dtype=np.uint8))
+    # every P-256 public key first, in one fgv_keys_register_tiered call: the keys that get comb
+    # tables (fgv_roles_want_comb: peers, orderers, admins, unknown roles) are built by batched
+    # k_keytab launches (up to KT_BUILD_KEYS keys each), the variable-base tables of the client
+    # keys by one k_keyprep launch -- instead of one launch and one synchronisation per identity
+    # below.  Client keys start on the variable-base kernels and are promoted by use.
+    keyed = [i for _s, i in identities if i.key == "p256" and i.pub is not None]
+    if keyed:
+        engine.keys_register(np.frombuffer(b"".join(bytes(i.pub) for i in keyed), dtype=np.uint8),
+                             hot=[roles_want_comb(i.roles) for i in keyed])
     for ser, i in identities:
         engine.msp_register_identity(ser, i.key, i.pub, i.valid, i.id_digest, roles=i.roles,
                                      hash_family=i.hash_family)

@@ -66,12 +66,12 @@ def main(src, rnd):
         if not os.path.exists(p):
             continue
         # the per-step kernels only: the one-time comb-table builds (k_gtab per context, k_keytab
-        # per new key) are dropped, so the top row is the step's dominant kernel
+        # per new key) and key preparations (k_keyprep, k_kmap_set) are dropped, so the top row is the step's dominant kernel
         with open(p) as fi, open(f"profiles/{rnd}_{wl}_kernel_stats.csv", "w", newline="") as fo:
             rd = csv.DictReader(fi)
             wr = csv.DictWriter(fo, fieldnames=rd.fieldnames)
             wr.writeheader()
-            rows = [r for r in rd if not r["Name"].startswith(("k_gtab", "k_keytab"))]
+            rows = [r for r in rd if not r["Name"].startswith(("k_gtab", "k_keytab", "k_keyprep", "k_kmap_set"))]
             tot = sum(float(r["TotalDurationNs"]) for r in rows) or 1.0
             for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
                 r["Percentage"] = f"{100 * float(r['TotalDurationNs']) / tot:.2f}"
