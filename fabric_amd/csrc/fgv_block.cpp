@@ -2045,11 +2045,21 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   const uint32_t *envtab = B.env.as<uint32_t>();
   const uint64_t *dbs = reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff);
   DevTx *dtx = B.tx.as<DevTx>();
-  // the payload hashes (the longest serial chains) start with the parse, on the second stream
-  HIP_TRY(hipStreamWaitEvent(c->stream2, B.ev[3], 0));
-  hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(128), 0, c->stream2, N, envtab, dbs,
-                     B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
-  HIP_TRY(hipEventRecord(B.ev[1], c->stream2));
+  // the payload hashes (the longest serial chains) beside the parse, on the second stream.  Queued
+  // after the parse (the front half's critical chain since round 4: its launch is ~15 us earlier);
+  // FGV_PAYLOAD_FIRST=1 queues them before it (A/B)
+  static const bool payload_first = [] {
+    const char *e = getenv("FGV_PAYLOAD_FIRST");
+    return e && atoi(e) != 0;
+  }();
+  auto launch_payload = [&]() -> hipError_t {
+    hipError_t e = hipStreamWaitEvent(c->stream2, B.ev[3], 0);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(128), 0, c->stream2, N, envtab, dbs,
+                       B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
+    return hipEventRecord(B.ev[1], c->stream2);
+  };
+  if (payload_first) HIP_TRY(launch_payload());
   B.kl = KlDev{B.klrec.as<KlRec>(),
                B.klhead.as<unsigned long long>(),
                (uint32_t)(hcap - 1),
@@ -2060,15 +2070,16 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
                reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + klb_off),
                B.kllist.as<uint32_t>(),
                B.kldep.as<uint32_t>()};
-  // every line of each envelope requested before the walk (touch_lines): measured on MI355X (C2,
-  // lean harness, one box) 0.665-0.667 ms per step against 0.702-0.724 without
-  // (profiles/round3_ab/parse_t*); FGV_PARSE_TOUCH=0 turns it off (A/B)
   // FGV_FRONT_PRIO=3: the front-half chain (parse, identities, counts) at the verify chain's wave
-  // priority instead of 2 (A/B: since round 4 it is the step's critical path)
+  // priority instead of 2 (A/B: measured 0.572-0.575 ms per C2 step
+  // against 0.559-0.561 at 2, alternating on one box, r4o)
   static const uint32_t front_prio = [] {
     const char *e = getenv("FGV_FRONT_PRIO");
     return e && atoi(e) == 3 ? 3u : 2u;
   }();
+  // every line of each envelope requested before the walk (touch_lines): measured on MI355X (C2,
+  // lean harness, one box) 0.665-0.667 ms per step against 0.702-0.724 without
+  // (profiles/round3_ab/parse_t*); FGV_PARSE_TOUCH=0 turns it off (A/B)
   static const uint32_t parse_touch = [] {
     const char *e = getenv("FGV_PARSE_TOUCH");
     return e ? (uint32_t)atoi(e) : 1u;
@@ -2106,6 +2117,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     hipLaunchKernelGGL(k_bd_parse, dim3((N + parse_lanes - 1) / parse_lanes), dim3(parse_lanes), 0, sf, N, envtab,
                        dbs, ch, dtx, misc + 5, misc + 16, B.kl, parse_touch | (front_prio == 3 ? 0x100u : 0u));
   HIP_TRY(hipEventRecord(B.ev[4], sf));
+  if (!payload_first) HIP_TRY(launch_payload());
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one
   HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[4], 0));

@@ -16,6 +16,7 @@
 #   churntrace       rocprofv3 kernel + HIP API trace of a short churn run
 #   mvcc | sig | c5 | sbe   the other workloads (tools/bench_sbe.py for sbe)
 #   trace            rocprofv3 --kernel-trace --stats of a C2 run
+#   apitrace         kernel + HIP API trace of a C2 run (host enqueue costs)
 #   lattrace         the same of tools/latency_probe.py (single-block calls)
 #   profile          tools/profile_round.sh (stats + PMC passes of every workload)
 #   py:<file>        python <file> (a micro-benchmark or check under tools/)
@@ -106,6 +107,10 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d $O/st -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $O/st.json 2> $O/st.err \
         || { echo trace failed; tail -20 $O/st.err; exit 1; }
       echo trace ok ;;
+    apitrace)
+      timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --hip-trace -d $O/at -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $O/at.json 2> $O/at.err \
+        || { echo apitrace failed; tail -20 $O/at.err; exit 1; }
+      echo apitrace ok ;;
     lattrace)
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d $O/lat -o run -- python tools/latency_probe.py > $O/lat.out 2> $O/lat.err \
         || { echo lattrace failed; tail -20 $O/lat.err; exit 1; }
