@@ -145,12 +145,15 @@ struct MvCounters {  // device-side counters of one block (zeroed by the head co
   uint32_t undec[4];          // undecided txs after round r (slot r & 3)
   uint32_t pad[2];
 };
-struct StateSlot {  // committed state: open addressing; arena holds flattened ns || key
-  uint64_t tag;     // 0 = empty; bit 1 = present
-  uint64_t blk, txn;
-  uint32_t off8;    // arena offset / 8 (arena up to 32 GiB)
-  uint16_t ns_len, key_len;
+#define MV_INLINE 32  // flattened ns || key bytes a committed-state slot holds inline
+struct __attribute__((aligned(64))) StateSlot {  // committed state: open addressing, one 64 B line;
+  uint64_t tag;     // 0 = empty; bit 1 = present        the arena holds every flattened ns || key,
+  uint64_t blk, txn;                                  // the slot a copy of a short one (ns_len +
+  uint32_t off8;    // arena offset / 8 (arena up to 32 GiB)   key_len <= MV_INLINE), so a probe of
+  uint16_t ns_len, key_len;                           // a short key reads this line only
+  uint8_t ik[MV_INLINE];
 };
+static_assert(sizeof(StateSlot) == 64, "StateSlot: one 64 B line");
 struct BlkSlot {    // keys written in the block
   uint64_t owner;   // (block epoch << 32) | (write index + 1); an older epoch = free
   // fixpoint first writers, double buffered by round parity: (global round << 32) |

@@ -175,7 +175,8 @@ int fgv_statedb_init(fgv_ctx *c, uint64_t slots, uint64_t arena_bytes) {
   fgv_mvcc_state *M = c->mv;
   uint64_t cap = 1024;
   while (cap < (slots ? slots : (1ull << 22))) cap <<= 1;
-  if (!M->tbl.ensure(cap * sizeof(StateSlot)) || !M->arena.ensure(arena + 64) || !M->top.ensure(64)) return FGV_ENOMEM;
+  if (!M->tbl.ensure(cap * sizeof(StateSlot) + 64) ||  // (+64: word loads past the last slot's inline key)
+      !M->arena.ensure(arena + 64) || !M->top.ensure(64)) return FGV_ENOMEM;
   M->cap = cap;
   M->mask = cap - 1;
   M->arena_cap = arena;

@@ -93,7 +93,8 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uin
 __device__ __forceinline__ bool rec_eq_state(const uint8_t *base, const MvRec &r, const StateSlot &s,
                                              const uint8_t *arena) {
   if (s.ns_len != flat_ns_len(r) || s.key_len != r.key_len) return false;
-  const uint8_t *a = arena + ((uint64_t)s.off8 << 3);
+  // a short key from the slot's own line (MV_INLINE), a longer one from the arena
+  const uint8_t *a = (uint32_t)s.ns_len + s.key_len <= MV_INLINE ? s.ik : arena + ((uint64_t)s.off8 << 3);
   if (!bytes_eq(a, base + r.ns_off, r.ns_len)) return false;
   a += r.ns_len;
   if (r.flags & MVR_HASHED) {
@@ -860,6 +861,10 @@ __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_
         tbl[idx].key_len = w.key_len;
         tbl[idx].blk = mode == 1 ? block_num : w.blk;
         tbl[idx].txn = mode == 1 ? (uint64_t)w.tx : w.txn;
+        if (fl + w.key_len <= MV_INLINE) {  // the inline copy (the arena bytes written above)
+          const uint8_t *src = arena + off;
+          for (uint32_t q = 0; q < fl + w.key_len; q++) tbl[idx].ik[q] = src[q];
+        }
         break;
       }
     }

@@ -15,6 +15,7 @@
 #   sigchurn         C4 with every item its own key (registered cold)
 #   churntrace       rocprofv3 kernel + HIP API trace of a short churn run
 #   mvcc | sig | c5 | sbe   the other workloads (tools/bench_sbe.py for sbe)
+#   mvccpmc          FETCH_SIZE / WRITE_SIZE passes of the mvcc workload
 #   trace            rocprofv3 --kernel-trace --stats of a C2 run
 #   apitrace         kernel + HIP API trace of a C2 run (host enqueue costs)
 #   lattrace         the same of tools/latency_probe.py (single-block calls)
@@ -88,6 +89,11 @@ for step in "$@"; do
       timeout -k 10 400 rocprofv3 --output-format csv --kernel-trace --hip-trace --stats -d $O/ct -o run -- python bench.py --clients 16000 --steps 8 --warmup 3 --cpu-threads 0 --no-pcie --no-latency > $O/ct.json 2> $O/ct.err \
         || { echo churntrace failed; tail -20 $O/ct.err; exit 1; }
       echo churntrace ok ;;
+    mvccpmc)
+      timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d $O/pmc_fetch -o run -- python bench.py --workload mvcc --steps 10 --warmup 2 > $O/pmc_fetch.json 2> $O/pmc_fetch.err \
+        && timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o run -- python bench.py --workload mvcc --steps 10 --warmup 2 > $O/pmc_write.json 2> $O/pmc_write.err \
+        || { echo mvccpmc failed; exit 1; }
+      echo mvccpmc ok ;;
     mvcc)
       timeout -k 10 300 python -u bench.py --workload mvcc --steps 100 --warmup 5 > $O/mvcc.json 2> $O/mvcc.err \
         || { echo mvcc failed; tail -20 $O/mvcc.err; exit 1; }
