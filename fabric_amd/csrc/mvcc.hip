@@ -861,9 +861,11 @@ __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_
         tbl[idx].key_len = w.key_len;
         tbl[idx].blk = mode == 1 ? block_num : w.blk;
         tbl[idx].txn = mode == 1 ? (uint64_t)w.tx : w.txn;
-        if (fl + w.key_len <= MV_INLINE) {  // the inline copy (the arena bytes written above)
-          const uint8_t *src = arena + off;
-          for (uint32_t q = 0; q < fl + w.key_len; q++) tbl[idx].ik[q] = src[q];
+        if (fl + w.key_len <= MV_INLINE) {  // the inline copy (the arena bytes written above; off
+          // is 8-byte aligned), 8-byte words: bytes past the key are never compared
+          const uint2 *src = reinterpret_cast<const uint2 *>(arena + off);
+          uint2 *dst = reinterpret_cast<uint2 *>(tbl[idx].ik);
+          for (uint32_t q = 0; 8 * q < fl + w.key_len; q++) dst[q] = src[q];
         }
         break;
       }
