@@ -841,17 +841,22 @@ __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_
     const uint64_t nmine = __popcll(__ballot(mine));
     if ((threadIdx.x & 63u) == 0 && nmine) atomicAdd(&top[1], (unsigned long long)nmine);
     if (!mine) continue;
-    uint8_t *a = arena + off;
-    for (uint32_t q = 0; q < w.ns_len; q++) a[q] = base[w.ns_off + q];
-    a += w.ns_len;
-    if (w.flags & MVR_HASHED) {
-      a[0] = '$';
-      a[1] = '$';
-      a[2] = 'h';
-      for (uint32_t q = 0; q < w.coll_len; q++) a[3 + q] = base[w.coll_off + q];
-      a += 3 + w.coll_len;
-    }
-    for (uint32_t q = 0; q < w.key_len; q++) a[q] = base[w.key_off + q];
+    // the flattened ns [|| "$$h" || coll] || key, zero-padded to `need`, written a 32-bit word at a
+    // time (byte stores cost a memory write each: ~0.7 KB of WRITE_SIZE per key, r4r)
+    auto flat_byte = [&](uint32_t j) -> uint32_t {
+      if (j < w.ns_len) return base[w.ns_off + j];
+      j -= w.ns_len;
+      if (w.flags & MVR_HASHED) {
+        if (j < 3) return j < 2 ? (uint32_t)'$' : (uint32_t)'h';
+        j -= 3;
+        if (j < w.coll_len) return base[w.coll_off + j];
+        j -= w.coll_len;
+      }
+      return j < w.key_len ? base[w.key_off + j] : 0u;
+    };
+    uint32_t *aw = reinterpret_cast<uint32_t *>(arena + off);  // (off: 8-byte aligned)
+    for (uint32_t o = 0; o < need; o += 4)
+      aw[o / 4] = flat_byte(o) | (flat_byte(o + 1) << 8) | (flat_byte(o + 2) << 16) | (flat_byte(o + 3) << 24);
     const unsigned long long tag = (unsigned long long)(w.tag | MV_TAG_PRESENT);
     uint64_t idx = w.tag & mask;
     for (uint64_t probe = 0; probe <= mask; probe++, idx = (idx + 1) & mask) {
