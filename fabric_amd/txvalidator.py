@@ -47,12 +47,14 @@ def _as_identity(entry):
 
 
 def setup_channel(engine: Engine, channel: str, identities, chaincodes, committed_txids=(), config=None, msps=(),
-                  kvmeta=None):
+                  kvmeta=None, hot_clients=False):
     """identities: iterable of (serialized, Identity) or (serialized, mspid, pubkey64 | None,
     valid, id_digest).  chaincodes: ns -> ApplicationPolicy bytes, or a dict {policy,
     plugin="vscc", collections=None | {name: EP bytes | None}, sbe=False}.  config: the channel's
     common.Config bytes (channel policies, MSPs, application orgs); msps: further MSP ids.
-    kvmeta: {(ns, coll, key bytes): VALIDATION_PARAMETER bytes} of the committed state."""
+    kvmeta: {(ns, coll, key bytes): VALIDATION_PARAMETER bytes} of the committed state.
+    hot_clients: register client keys with comb tables too (a peer whose clients are known to sign
+    often: the steady state promotion by use reaches anyway)."""
     engine.channel_init(channel)
     if config is not None:
         engine.channel_config(config)
@@ -67,7 +69,7 @@ def setup_channel(engine: Engine, channel: str, identities, chaincodes, committe
     keyed = [i for _s, i in identities if i.key == "p256" and i.pub is not None]
     if keyed:
         engine.keys_register(np.frombuffer(b"".join(bytes(i.pub) for i in keyed), dtype=np.uint8),
-                             hot=[roles_want_comb(i.roles) for i in keyed])
+                             hot=[hot_clients or roles_want_comb(i.roles) for i in keyed])
     for ser, i in identities:
         engine.msp_register_identity(ser, i.key, i.pub, i.valid, i.id_digest, roles=i.roles,
                                      hash_family=i.hash_family)
