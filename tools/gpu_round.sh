@@ -19,6 +19,7 @@
 #   trace            rocprofv3 --kernel-trace --stats of a C2 run
 #   apitrace         kernel + HIP API trace of a C2 run (host enqueue costs)
 #   lattrace         the same of tools/latency_probe.py (single-block calls)
+#   profileblock     the block workload's part of it only
 #   profile          tools/profile_round.sh (stats + PMC passes of every workload)
 #   py:<file>        python <file> (a micro-benchmark or check under tools/)
 #   with:VAR=VAL:<step>  <step> with VAR=VAL in its environment
@@ -121,6 +122,15 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d $O/lat -o run -- python tools/latency_probe.py > $O/lat.out 2> $O/lat.err \
         || { echo lattrace failed; tail -20 $O/lat.err; exit 1; }
       tail -1 $O/lat.out ;;
+    profileblock)
+      # the block workload's stats + PMC passes only (tools/profile_round.sh's block lines)
+      P="rocprofv3 --output-format csv"; D=$O/prof; mkdir -p $D
+      timeout -k 10 300 $P --kernel-trace --stats -d $D/block -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $D/block.json 2> $D/block.err \
+        && timeout -k 10 300 $P --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d $D/pmc_blk_valu -o run -- python bench.py --steps 5 --warmup 1 --cpu-threads 0 --no-pcie --no-latency > $D/pmc_blk_valu.json 2> $D/pmc_blk_valu.err \
+        && timeout -k 10 300 $P --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d $D/pmc_blk_fetch -o run -- python bench.py --steps 5 --warmup 1 --cpu-threads 0 --no-pcie --no-latency > $D/pmc_blk_fetch.json 2> $D/pmc_blk_fetch.err \
+        && timeout -k 10 300 $P --kernel-trace --pmc WRITE_SIZE -d $D/pmc_blk_write -o run -- python bench.py --steps 5 --warmup 1 --cpu-threads 0 --no-pcie --no-latency > $D/pmc_blk_write.json 2> $D/pmc_blk_write.err \
+        || { echo profileblock failed; exit 1; }
+      echo profileblock ok ;;
     profile)
       PROF_OUT=$O/prof bash tools/profile_round.sh || { echo profile failed; exit 1; } ;;
     with:*)
