@@ -201,7 +201,7 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
 // The promotion queue k_vb_mul filled (copied back on streamV behind it): build combs for the
 // queued ids, then empty the queue on the device.  At the start of a call, under c->mu; a copy
 // still in flight is left for the next call.
-static int promote_consume(fgv_ctx *c) {
+static int promote_consume(fgv_ctx *c, uint32_t items) {
   if (c->vb_copied && hipEventQuery(c->vb_ev[2]) == hipSuccess) {  // (a copy in flight: a later call)
     c->vb_copied = false;
     uint32_t *q = c->h_promo.as<uint32_t>();
@@ -220,9 +220,13 @@ static int promote_consume(fgv_ctx *c) {
     if (hipEventQuery(c->kt_ev) != hipSuccess) return FGV_OK;
     c->kt_busy = false;
   }
-  // at most promote_per_call builds per call (~80 us of the whole chip each), so a burst of keys
-  // reaching the threshold together spreads over calls instead of stalling one
-  const size_t take = std::min<size_t>(c->promo_backlog.size(), c->promote_per_call);
+  // at most promote_per_call builds per call (~80 us of the whole chip each), and about one per
+  // 3,000 verify slots of this call, so a burst of keys reaching the threshold together spreads
+  // over calls, and a small call (one block) is not swamped by builds running beside it
+  // (FGV_PROMOTE_PER_CALL set: exactly that many, whatever the call's size)
+  const size_t per = c->promote_fixed ? c->promote_per_call
+                                      : std::max<size_t>(1, std::min<size_t>(c->promote_per_call, items / 3000));
+  const size_t take = std::min<size_t>(c->promo_backlog.size(), per);
   std::vector<uint32_t> ids(c->promo_backlog.begin(), c->promo_backlog.begin() + take);
   c->promo_backlog.erase(c->promo_backlog.begin(), c->promo_backlog.begin() + take);
   std::sort(ids.begin(), ids.end());
@@ -257,7 +261,10 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   c->key_ids = (cfg && cfg->key_ids) ? cfg->key_ids : (1u << 20);
   if (const char *e = getenv("FGV_PROMOTE_USES")) c->promote_uses = (uint32_t)std::max(1, atoi(e));
   if (const char *e = getenv("FGV_ADHOC_COMB")) c->adhoc_comb_uses = (uint32_t)std::max(1, atoi(e));
-  if (const char *e = getenv("FGV_PROMOTE_PER_CALL")) c->promote_per_call = (uint32_t)std::max(1, atoi(e));
+  if (const char *e = getenv("FGV_PROMOTE_PER_CALL")) {
+    c->promote_per_call = (uint32_t)std::max(1, atoi(e));
+    c->promote_fixed = true;
+  }
   // host workers: fgv_config.host_threads, else min(24, this process's CPU share) -- 24 measured
   // best on a whole machine (tools/sweep_threads.sh); eight ranks on one node each get their
   // affinity mask's share, not the whole machine
@@ -488,7 +495,7 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
   const bool tim = c->timing || !dn;  // (host-count callers always time their stages)
   // keys whose variable-base verifies reached the promotion threshold in an earlier call get their
   // comb tables now (stream-ordered before this batch's point kernels read kmap)
-  int prc = promote_consume(c);
+  int prc = promote_consume(c, N);
   if (prc) return prc;
   // keys without a comb (c->n_vb): k_inv lists their items, k_vb_mul computes u2 * Q for them on
   // streamV -- beside the hashes and k_prep: it needs s^-1, not the digest -- and

@@ -147,6 +147,7 @@ struct fgv_ctx {
   uint64_t n_promoted = 0;        // keys promoted to a comb since fgv_init
   uint32_t promote_per_call = 32; // comb builds from the promotion queue per call (FGV_PROMOTE_PER_CALL)
   std::vector<uint32_t> promo_backlog;  // queued ids not built yet
+  bool promote_fixed = false;  // FGV_PROMOTE_PER_CALL given: no scaling by call size
   // per-block outcomes (fgv_set_block_outcomes) and the fallback counters (fgv_unsupported_stats)
   bool block_outcomes = false;
   std::vector<int32_t> blk_status;

@@ -197,7 +197,7 @@ def test_register_past_comb_capacity():
 def test_promotion_by_use():
     """variable-base keys whose verifies reach FGV_PROMOTE_USES get a comb table from the next call
     on (k_vb_mul queues them; built asynchronously); results are the same before, during and after"""
-    with _env(FGV_ADHOC_COMB=10**9, FGV_PROMOTE_USES=8):
+    with _env(FGV_ADHOC_COMB=10**9, FGV_PROMOTE_USES=8, FGV_PROMOTE_PER_CALL=8):
         eng = _lib.Engine(0, key_slots=16)
     try:
         keys = [synth.Key(95, i) for i in range(6)]
