@@ -330,7 +330,24 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
     }
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(FGV_EDEVICE);
     if (hipStreamCreateWithPriority(&c->streamV, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
-    if (hipStreamCreateWithPriority(&c->streamK, hipStreamNonBlocking, lo) != hipSuccess) return fail(FGV_EDEVICE);
+    // streamK (promotion comb builds: one k_keytab launch runs ~2-3 ms whatever its key count)
+    // on a CU-masked queue of its own -- CUs i with i % 8 == 7 by default (FGV_KT_CUS=0: an
+    // ordinary stream): on a shared hardware queue a build held up every kernel queued behind it
+    // (C2 churn 1.90 ms per step with promotions against 0.97 without, r4y)
+    static const int kt_cus = [] {
+      const char *e = getenv("FGV_KT_CUS");
+      return e ? atoi(e) : 1;
+    }();
+    int ncu_k = 0;
+    if (kt_cus && hipDeviceGetAttribute(&ncu_k, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess &&
+        ncu_k > 0 && ncu_k % 32 == 0) {
+      std::vector<uint32_t> mask((size_t)ncu_k / 32, 0u);
+      for (int i = 7; i < ncu_k; i += 8) mask[(size_t)i / 32] |= 1u << (i % 32);
+      if (hipExtStreamCreateWithCUMask(&c->streamK, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+        return fail(FGV_EDEVICE);
+    } else if (hipStreamCreateWithPriority(&c->streamK, hipStreamNonBlocking, lo) != hipSuccess) {
+      return fail(FGV_EDEVICE);
+    }
     if (hipEventCreateWithFlags(&c->kt_ev, hipEventDisableTiming) != hipSuccess) return fail(FGV_EDEVICE);
   }
   for (auto &e : c->vb_ev)
