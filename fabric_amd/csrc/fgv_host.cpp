@@ -296,8 +296,8 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   // queues of a priority exist, and (as we read the traces) the process's first stream holds one.  streamF (the
   // next batch's parse / identities / counts) comes before the copy stream so that it gets a queue
   // of its own: created after it, it shared the first stream's queue and the C2 step measured
-  // 0.63-0.65 ms instead of 0.55-0.58 (MI355X).  streamV / streamK share with
-  // stream2 / stream3.
+  // 0.63-0.65 ms instead of 0.55-0.58 (MI355X).  streamK (comb builds) is
+  // CU-masked: a queue of its own.
   {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
