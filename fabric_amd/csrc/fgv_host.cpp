@@ -51,8 +51,7 @@ static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slo
   if (!st) st = c->stream;
   const uint32_t per = nk < KT_BUILD_KEYS ? nk : KT_BUILD_KEYS;
   // the scratch at its full size on first use (335 MB): grown build by build, every larger
-  // promotion batch paid a hipFree -- a device-wide synchronisation -- inside a call (the C2 churn
-  // run measured 1.97 ms per step with promotions, 1.01 with them off, r4x)
+  // promotion batch would pay a hipFree -- a device-wide synchronisation -- inside a call
   if (!c->kt_q.ensure((size_t)nk * 64) || !c->kt_slot.ensure((size_t)nk * 4) ||
       !c->kt_scratch.ensure((size_t)KT_BUILD_KEYS * KT_ENTRIES * sizeof(jpoint_raw)))
     return FGV_ENOMEM;
