@@ -22,6 +22,9 @@ c5 (configs[4]): 20k-tx blocks, 5-of-8 policy, P-256 + Ed25519, + deliver-side i
 sig (configs[3], C4 shape): 131,072 P-256 identity.Verify calls per GPU on 1.85 KB
   messages, inputs resident in HBM; value = verifies/s.
 mvcc (configs[2], C3): 10k-tx blocks against a 1M-key state DB, validated and committed.
+pipeline: the end-to-end commit path on the same C2-shaped blocks (committer -> MVCC with
+  commit -> commit hash); value = committed tx/s; run with e.g. --steps 12 --warmup 2 (every
+  batch is distinct and generated up front).
 """
 import argparse
 import json
@@ -907,6 +910,144 @@ def run_sig(args, world, rank, local, dev):
     return out
 
 
+# ------------------------------------------------------------------ end-to-end pipeline
+def run_pipeline(args, world, rank, local, dev):
+    """A peer's commit path on the same blocks, one step = one batch of B consecutive C2-shaped
+    blocks (fabric_amd/synth/pipeline.py): committer validation (fgv_validate_blocks_pipelined,
+    HBM-resident, the next batch pre-split) -> MVCC validation and commit of the B blocks in one
+    device chain (fgv_mvcc_validate_blocks, the committer's flags in) -> the chained commit hashes
+    (fgv_commit_hashes, host), the hashes of batch k computed on a host thread while batch k+1 is
+    validated (they gate nothing: kv_ledger.go:806-817 chains them after the commit).  Reference:
+    gossip/privdata/coordinator.go:152-184, core/ledger/kvledger/kv_ledger.go:612-652.  Every
+    batch is distinct and processed once, in order, so each block reads the state the previous
+    blocks committed.  Replicas for N > 1 (MVCC and the commit hash are sequential per channel)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from fabric_amd import _lib, shard, txvalidator
+    from fabric_amd.synth import blocks, pipeline
+    from fabric_amd.synth.mvcc import MvccState
+
+    B, T, W, K, L = args.blocks_per_gpu, args.tx_per_block, args.warmup, args.steps, args.pipeline_latency_blocks
+    t0 = time.time()
+    net = blocks.Network(seed=3, orgs=3, clients=100)
+    st = MvccState(args.state_keys, seed=4 + rank)
+    keys, kb, kt = st.items()
+    batches, cexp, fexp, prev = [], [], [], b"\x00" * 32
+    first = 1001
+    for k in range(W + K):
+        bl, c, f, prev = pipeline.make_blocks(net, st, B, T, first + k * B, seed=17 + k + 1000 * rank, prev_hash=prev)
+        batches.append(bl), cexp.append(c), fexp.append(f)
+    lat_blocks, lat_c, lat_f, _ = pipeline.make_blocks(net, st, L, T, first + (W + K) * B, seed=9999 + rank,
+                                                       prev_hash=prev)
+    log(f"[bench] rank {rank}: {args.state_keys} keys + {W + K} x {B} blocks x {T} tx (+{L} latency blocks) ready "
+        f"in {time.time() - t0:.1f}s")
+    eng = _lib.Engine(local, host_threads=args.host_threads or min(24, _cpu_share()))
+    txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes, hot_clients=True)
+    eng.statedb_init(4 * args.state_keys, 256 << 20)
+    eng.statedb_load("mycc", keys, kb, kt)
+    allb = [bl for bl in batches] + [[b] for b in lat_blocks]
+    sizes = [(len(b) + 64 + 255) // 256 * 256 for bl in allb for b in bl]
+    arena = torch.zeros(sum(sizes), dtype=torch.uint8, device=dev)
+    dptrs, o = [], 0
+    for bl in allb:
+        cur = []
+        for b in bl:
+            arena[o:o + len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+            cur.append(arena.data_ptr() + o)
+            o += (len(b) + 64 + 255) // 256 * 256
+        dptrs.append(cur)
+    torch.cuda.synchronize()
+    NBT = W + K
+    hb = [eng.block_batch(batches[k], dptrs[k]) for k in range(NBT)]
+    ntx = np.array([T] * B, dtype=np.int64)
+    plan = shard.plan(ntx, 1, "block")
+    rows = shard.plan_rows(*plan)
+    send = torch.zeros((rows, shard.REC), dtype=torch.uint8, device=dev)
+    flags_out = np.empty(B * T, dtype=np.uint8)
+    nums = [list(range(first + k * B, first + (k + 1) * B)) for k in range(NBT)]
+    csteps = [_lib.BlockStep(eng, hb[k], plan[0][0], plan[1][0], send.data_ptr(), rows, ntx, 1, send.data_ptr(),
+                             flags_out, plan=plan, presplit=True, next_batch=hb[(k + 1) % NBT], fused=True)
+              for k in range(NBT)]
+    msteps = [_lib.MvccChainStep(eng, batches[k], nums[k], [np.zeros(T, np.uint8)] * B, commit=True, d_blocks=dptrs[k],
+                                 next_blocks=batches[k + 1] if k + 1 < NBT else None) for k in range(NBT)]
+    hsteps = [_lib.CommitHashes(batches[k], nums[k]) for k in range(NBT)]
+    hash_ex = ThreadPoolExecutor(max_workers=1)
+    state = dict(prev=b"", fut=None, mism=0, stage=np.zeros(3))
+
+    def step(k, check):
+        t = time.perf_counter()
+        cf = csteps[k].validate() or csteps[k].finalize()
+        t1 = time.perf_counter()
+        msteps[k].set_flags([cf[b * T:(b + 1) * T] for b in range(B)])
+        fl, rc, done = msteps[k].run()
+        _lib._check(rc)
+        t2 = time.perf_counter()
+        if state["fut"] is not None:
+            state["prev"] = state["fut"].result()[-1]
+        t3 = time.perf_counter()
+        flc = [f.copy() for f in fl]
+        state["fut"] = hash_ex.submit(hsteps[k].run, flc, state["prev"])
+        state["stage"] += (t1 - t, t2 - t1, t3 - t2)
+        if check:
+            for b in range(B):
+                state["mism"] += int((cf[b * T:(b + 1) * T] != cexp[k][b]).sum()) + int((fl[b] != fexp[k][b]).sum())
+
+    for k in range(W):
+        step(k, True)
+    torch.cuda.synchronize()
+    state["stage"][:] = 0
+    t0 = time.perf_counter()
+    for k in range(W, W + K):
+        step(k, False)
+    state["prev"] = state["fut"].result()[-1]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    for k in range(W, W + K):  # parity of the timed batches after the clock: the final flags
+        for b in range(B):     # (committer code, else MVCC code) of every block
+            state["mism"] += int((msteps[k].flags[b] != fexp[k][b]).sum())
+    stage = state["stage"] / K * 1e3
+    # per-block latency: one block through all three stages, one call each (block in hand ->
+    # final flags and commit hash), the state continuing from the timed batches
+    lats = []
+    prev = state["prev"]
+    for i, b in enumerate(lat_blocks):
+        num = first + NBT * B + i
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        cf = eng.validate_blocks([b], d_blocks=[dptrs[NBT + i][0]])[0]
+        mf = eng.mvcc_validate(b, num, cf, commit=True, d_block=dptrs[NBT + i][0])
+        prev = _lib.commit_hash(b, mf, num, prev)
+        lats.append((time.perf_counter() - t) * 1e3)
+        state["mism"] += int((cf != lat_c[i]).sum()) + int((mf != lat_f[i]).sum())
+    hash_ex.shutdown()
+    eng.close()
+    ok = state["mism"] == 0
+    if world > 1:
+        tt = torch.tensor([el, 1.0 if ok else 0.0], dtype=torch.float64, device=dev)
+        mx = tt.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        mn = tt.clone()
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        el, ok = float(mx[0]), bool(mn[1] > 0)
+    return dict(metric=METRIC, value=round(world * B * T * K / el, 1), unit="committed tx/s (end to end)",
+                n_gpus=world, steps=K, dist=_dist_info(world), warmup=W, ms_per_step=round(el / K * 1e3, 3),
+                higher_is_better=True, scaling="weak", vs_baseline=None, dtype="u32", data="synthetic",
+                config=dict(workload=f"commit pipeline: {B} x {T}-tx C2 blocks per step (OutOf(2,[Org1..3.member]), "
+                                     f"C2 faults) -> MVCC of the same blocks against a {args.state_keys}-key state DB "
+                                     f"(4R/4W x 200B read-modify-write, 1% stale, 5% conflicts, 2% reads of "
+                                     f"committer-invalid writes) with commit -> chained commit hashes",
+                            blocks_per_step=B, tx_per_block=T, global_batch=world * B * T,
+                            parallelism=f"replicas{world} (one channel per GPU)"),
+                parity_vs_labels=ok,
+                stage_ms_per_step=dict(committer=round(stage[0], 3), mvcc_chain=round(stage[1], 3),
+                                       commit_hash_wait=round(stage[2], 3)),
+                latency_1block_ms=dict(median=round(float(np.median(lats[2:])), 4) if len(lats) > 2 else None,
+                                       p90=round(float(np.percentile(lats[2:], 90)), 4) if len(lats) > 2 else None,
+                                       blocks=len(lats), note="one block in hand -> committer flags -> MVCC flags "
+                                                              "and commit -> commit hash, one call each"),
+                cpu_baseline=None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -914,7 +1055,9 @@ def main():
     # 0.748 / 0.724 ms per step at 10 steps, 0.701 / 0.676 at 40; profiles/round3_ab/steps*)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="block", choices=["block", "c5", "sig", "mvcc"])
+    ap.add_argument("--workload", default="block", choices=["block", "c5", "sig", "mvcc", "pipeline"])
+    ap.add_argument("--pipeline-latency-blocks", type=int, default=12,
+                    help="pipeline: blocks taken one call per stage after the timed batches (latency)")
     ap.add_argument("--c5-blocks-per-gpu", type=int, default=8)
     ap.add_argument("--c5-tx-per-block", type=int, default=20000)
     ap.add_argument("--tx-per-mvcc-block", type=int, default=10000)
@@ -977,7 +1120,7 @@ def main():
     else:
         if args.cpu_threads < 0:
             args.cpu_threads = _cpu_share()
-        out = dict(sig=run_sig, mvcc=run_mvcc)[args.workload](args, world, rank, local, dev_fn())
+        out = dict(sig=run_sig, mvcc=run_mvcc, pipeline=run_pipeline)[args.workload](args, world, rank, local, dev_fn())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -26,7 +26,7 @@ EXPORTED = [
     "fgv_validate_shard_dev", "fgv_finalize_flags_dev", "fgv_finalize_flags_dev_plan",
     "fgv_presplit", "fgv_prefetch", "fgv_last_presplit", "fgv_validate_shard_dev_next", "fgv_mvcc_validate_block_next",
     "fgv_statedb_init", "fgv_statedb_load", "fgv_statedb_apply", "fgv_statedb_stats", "fgv_mvcc_validate_block", "fgv_mvcc_validate_blocks", "fgv_mvcc_validate_blocks_next", "fgv_mvcc_last_stats",
-    "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash",
+    "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash", "fgv_commit_hashes",
     "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
     "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d",
     "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead", "fgv_blocks_verify_signed",
@@ -181,6 +181,7 @@ def load():
         L.fgv_set_parse_mode.argtypes = [vp, ctypes.c_int]
         L.fgv_sha256_host.argtypes = [vp, sz, vp]
         L.fgv_commit_hash.argtypes = [vp, sz, vp, sz, ctypes.c_uint64, vp, sz, vp]
+        L.fgv_commit_hashes.argtypes = [sz, vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint]
         L.fgv_host_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
         L.fgv_host_free.argtypes = [vp, vp]
         L.fgv_last_h2d.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
@@ -250,6 +251,11 @@ class MvccChainStep:
             self._nbufs = [np.frombuffer(b, dtype=np.uint8) for b in next_blocks]
             self._next = (len(next_blocks), (ctypes.c_void_p * len(next_blocks))(*[b.ctypes.data for b in self._nbufs]),
                           (ctypes.c_size_t * len(next_blocks))(*[len(b) for b in next_blocks]))
+
+    def set_flags(self, flags):
+        """the committer flags the next run() starts from (one array per block)"""
+        for f0, f in zip(self._flags0, flags):
+            np.copyto(f0, f)
 
     def run(self):
         for f, f0 in zip(self.flags, self._flags0):
@@ -960,6 +966,35 @@ def commit_hash(block: bytes, flags, block_num: int, prev: bytes = b""):
     _check(L.fgv_commit_hash(b.ctypes.data, len(block), _ptr(f), len(f), block_num,
                              pv.ctypes.data if pv is not None else None, len(prev), out))
     return out.raw
+
+
+class CommitHashes:
+    """fgv_commit_hashes over a fixed list of consecutive blocks with the ctypes arguments bound
+    once (the pipeline bench): run(flags, prev) -> n x 32-byte commit hashes (bytes)."""
+
+    def __init__(self, blocks, block_nums, threads=0):
+        self._L = load()
+        n = self.n = len(blocks)
+        self._bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+        self._bp = (ctypes.c_void_p * max(n, 1))(*[b.ctypes.data for b in self._bufs])
+        self._ln = (ctypes.c_size_t * max(n, 1))(*[len(b) for b in blocks])
+        self._nums = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in block_nums])
+        self._threads = threads
+        self.out = ctypes.create_string_buffer(32 * max(n, 1))
+
+    def run(self, flags, prev=b""):
+        fl = [np.ascontiguousarray(f, dtype=np.uint8) for f in flags]
+        fp = (ctypes.c_void_p * max(self.n, 1))(*[f.ctypes.data for f in fl])
+        nt = (ctypes.c_size_t * max(self.n, 1))(*[len(f) for f in fl])
+        pv = ctypes.create_string_buffer(prev, len(prev)) if prev else None
+        _check(self._L.fgv_commit_hashes(self.n, self._bp, self._ln, fp, nt, self._nums, pv, len(prev), self.out,
+                                         self._threads))
+        return [self.out.raw[32 * b:32 * b + 32] for b in range(self.n)]
+
+
+def commit_hashes(blocks, flags, block_nums, prev: bytes = b"", threads=0):
+    """fgv_commit_hashes: the chained commit hashes of consecutive blocks (kv_ledger.go:806-817)."""
+    return CommitHashes(blocks, block_nums, threads).run(flags, prev)
 
 
 def x509_probe(pem: bytes):

@@ -10,7 +10,10 @@
 // collections sorted, as txmgr.Updates{KVWrite{namespace, collection, key, isDelete, value,
 // version_bytes}} (txmgr/updates.proto).  A serial SHA-256 over one short message per block: host
 // code (SHA extensions when present), like the block data hash in fgv_integrity.cpp.
+#include <algorithm>
+#include <atomic>
 #include <map>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -144,9 +147,10 @@ int add_tx(Span d, uint64_t blk, uint64_t txi, std::map<std::string, KeyMap> &pu
 
 }  // namespace
 
-extern "C" int fgv_commit_hash(const uint8_t *block, size_t len, const uint8_t *flags, size_t ntx,
-                               uint64_t block_num, const uint8_t *prev, size_t prev_len, uint8_t out[32]) {
-  if (!block || !out || (ntx && !flags) || (prev_len && !prev)) return FGV_EINVAL;
+// SHA-256 stream over len(flags) || flags || update batch bytes of one block: everything of
+// the commit hash but the previous hash, which comes last (kv_ledger.go:806-817)
+static int commit_prefix(const uint8_t *block, size_t len, const uint8_t *flags, size_t ntx, uint64_t block_num,
+                         fgvsha::Stream &s) {
   VBlock b;
   if (!pbw::decode(block, len, b) || b.data.data.size() != ntx) return FGV_EINVAL;
   std::map<std::string, KeyMap> pub;
@@ -190,11 +194,55 @@ extern "C" int fgv_commit_hash(const uint8_t *block, size_t len, const uint8_t *
   }
   std::string pre;
   put_varint(pre, ntx);
-  fgvsha::Stream s;
   s.update(reinterpret_cast<const uint8_t *>(pre.data()), pre.size());
   if (ntx) s.update(flags, ntx);
   s.update(reinterpret_cast<const uint8_t *>(batch.data()), batch.size());
+  return FGV_OK;
+}
+
+extern "C" int fgv_commit_hash(const uint8_t *block, size_t len, const uint8_t *flags, size_t ntx,
+                               uint64_t block_num, const uint8_t *prev, size_t prev_len, uint8_t out[32]) {
+  if (!block || !out || (ntx && !flags) || (prev_len && !prev)) return FGV_EINVAL;
+  fgvsha::Stream s;
+  const int rc = commit_prefix(block, len, flags, ntx, block_num, s);
+  if (rc) return rc;
   if (prev_len) s.update(prev, prev_len);
   s.final(out);
+  return FGV_OK;
+}
+
+// Consecutive blocks: every block's update batch and the SHA-256 of everything before the
+// previous hash on host workers in parallel, then the chain -- one last update and the final
+// padding per block -- in block order.
+extern "C" int fgv_commit_hashes(size_t n, const uint8_t *const *blocks, const size_t *lens,
+                                 const uint8_t *const *flags, const size_t *ntx, const uint64_t *block_nums,
+                                 const uint8_t *prev, size_t prev_len, uint8_t *out, unsigned threads) {
+  if (n && (!blocks || !lens || !flags || !ntx || !block_nums || !out)) return FGV_EINVAL;
+  if (prev_len && !prev) return FGV_EINVAL;
+  for (size_t b = 0; b < n; b++)
+    if (!blocks[b] || (ntx[b] && !flags[b])) return FGV_EINVAL;
+  std::vector<fgvsha::Stream> st(n);
+  std::vector<int> rc(n, FGV_OK);
+  auto one = [&](size_t b) { rc[b] = commit_prefix(blocks[b], lens[b], flags[b], ntx[b], block_nums[b], st[b]); };
+  const unsigned nt = std::min<size_t>(n, threads ? threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+  if (nt <= 1) {
+    for (size_t b = 0; b < n; b++) one(b);
+  } else {
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++)
+      th.emplace_back([&] {
+        for (size_t b; (b = next.fetch_add(1)) < n;) one(b);
+      });
+    for (size_t b; (b = next.fetch_add(1)) < n;) one(b);
+    for (auto &t : th) t.join();
+  }
+  for (size_t b = 0; b < n; b++)
+    if (rc[b]) return rc[b];
+  for (size_t b = 0; b < n; b++) {
+    if (b) st[b].update(out + 32 * (b - 1), 32);
+    else if (prev_len) st[b].update(prev, prev_len);
+    st[b].final(out + 32 * b);
+  }
   return FGV_OK;
 }

@@ -82,8 +82,12 @@ static int kt_wait(fgv_ctx *c) {
 static int comb_build(fgv_ctx *c, const std::vector<uint32_t> &ids, bool async = false) {
   int wrc = kt_wait(c);
   if (wrc) return wrc;
+  // (distinct ids: a key named twice must not take two slots nor count twice against n_vb)
+  std::vector<uint32_t> uniq(ids);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
   std::vector<uint32_t> take;
-  for (uint32_t id : ids)
+  for (uint32_t id : uniq)
     if (take.size() < c->comb_free.size() && id < c->n_ids && c->kmap_h[id] == KEY_NONE) take.push_back(id);
   if (take.empty()) return FGV_OK;
   const uint32_t nk = (uint32_t)take.size();
@@ -101,6 +105,14 @@ static int comb_build(fgv_ctx *c, const std::vector<uint32_t> &ids, bool async =
     be32_to_limbs(c->id_key[id].data() + 32, kq + 16 * j + 8);
     ks[j] = slot;
     ki[j] = id;
+  }
+  if (async && c->promote_at) {  // (test knob: the table now, k_kmap_set at a chosen point later)
+    int rc = build_tables(c, kq, ks, nk, nullptr, c->ktab28.as<apoint_raw>(), nullptr, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->kt_id.p, ki, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->kmap_defer = nk;
+    return FGV_OK;
   }
   // async (promotions): on streamK, nobody waits.  A kernel that reads kmap while the build is in
   // flight sees KEY_NONE (variable-base path) or the slot once the table is complete (k_kmap_set
@@ -124,10 +136,23 @@ static int comb_build(fgv_ctx *c, const std::vector<uint32_t> &ids, bool async =
   return FGV_OK;
 }
 
+// FGV_PROMOTE_AT: the deferred k_kmap_set of a promotion, enqueued on `st` at chain point
+// `point` (1 after k_inv, 2 before k_point28, 3 before k_vb_fin; 0 whatever the point)
+static int kmap_defer_flush(fgv_ctx *c, hipStream_t st, uint32_t point) {
+  if (!c->kmap_defer || (point && point != c->promote_at)) return FGV_OK;
+  hipLaunchKernelGGL(k_kmap_set, dim3((c->kmap_defer + 63) / 64), dim3(64), 0, st, c->kt_id.as<uint32_t>(),
+                     c->kt_slot.as<uint32_t>(), c->kmap_defer, c->kmap.as<uint32_t>());
+  c->kmap_defer = 0;
+  HIP_TRY(hipGetLastError());
+  return FGV_OK;
+}
+
 // forget the ad-hoc ids [pinned, n_ids): their comb slots go back to the free list
 static int flush_adhoc(fgv_ctx *c) {
   if (c->n_ids == c->pinned) return FGV_OK;
   int wrc = kt_wait(c);  // (a promotion's k_kmap_set must land before the reset below)
+  if (wrc) return wrc;
+  wrc = kmap_defer_flush(c, c->stream, 0);
   if (wrc) return wrc;
   for (uint32_t id = c->pinned; id < c->n_ids; id++) {
     c->key_map.erase(c->id_key[id]);
@@ -167,15 +192,19 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
   // the variable-base tables (7.5 KB per id) grow by doubling; kernels in flight read the old rows
   if (c->n_ids + nk > c->vbt_keys) {
     const uint32_t want = std::min<uint32_t>(c->key_ids, std::max<uint32_t>({c->n_ids + nk, 2 * c->vbt_keys, 4096u}));
+    uint32_t grow = want;
     DevBuf nb;
-    if (!nb.ensure((size_t)want * VBT_WORDS * 4)) return FGV_ENOMEM;
+    if (!nb.ensure((size_t)grow * VBT_WORDS * 4)) {  // (no room to double: exactly what is needed)
+      grow = c->n_ids + nk;
+      if (!nb.ensure((size_t)grow * VBT_WORDS * 4)) return FGV_ENOMEM;
+    }
     HIP_TRY(hipStreamSynchronize(c->streamV));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->vbt_keys) HIP_TRY(hipMemcpy(nb.p, c->vbt.p, (size_t)c->vbt_keys * VBT_WORDS * 4, hipMemcpyDeviceToDevice));
     c->vbt.release();
     c->vbt = nb;
     nb.p = nullptr;
-    c->vbt_keys = want;
+    c->vbt_keys = grow;
   }
   uint32_t *kq = c->h_kq.as<uint32_t>(), *ki = c->h_kid.as<uint32_t>();
   std::vector<uint32_t> comb;
@@ -203,7 +232,9 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
 // The promotion queue k_vb_mul filled (copied back on streamV behind it): build combs for the
 // queued ids, then empty the queue on the device.  At the start of a call, under c->mu; a copy
 // still in flight is left for the next call.
-static int promote_consume(fgv_ctx *c, uint32_t items) {
+// `st`: the stream this call's k_inv runs on -- the queue's reset is ordered before the k_vb_mul
+// that follows it (that kernel waits for an event recorded on `st` after k_inv)
+static int promote_consume(fgv_ctx *c, uint32_t items, hipStream_t st) {
   if (c->vb_copied && hipEventQuery(c->vb_ev[2]) == hipSuccess) {  // (a copy in flight: a later call)
     c->vb_copied = false;
     uint32_t *q = c->h_promo.as<uint32_t>();
@@ -212,10 +243,19 @@ static int promote_consume(fgv_ctx *c, uint32_t items) {
     if (np) {
       c->promo_backlog.insert(c->promo_backlog.end(), q + 2, q + 2 + np);
       q[0] = 0;
-      HIP_TRY(hipMemsetAsync(c->vbpromo.p, 0, 4, c->stream));
+      HIP_TRY(hipMemsetAsync(c->vbpromo.p, 0, 4, st));
     }
   }
-  if (c->comb_free.empty()) c->promo_backlog.clear();  // (nothing more can be promoted)
+  // a full comb cache keeps the queue (bounded, distinct ids) for slots a flush frees later:
+  // k_vb_mul queues a key once, when its count reaches the threshold
+  if (c->comb_free.empty()) {
+    if (c->promo_backlog.size() > VB_BACKLOG_CAP) {
+      std::sort(c->promo_backlog.begin(), c->promo_backlog.end());
+      c->promo_backlog.erase(std::unique(c->promo_backlog.begin(), c->promo_backlog.end()), c->promo_backlog.end());
+      if (c->promo_backlog.size() > VB_BACKLOG_CAP) c->promo_backlog.resize(VB_BACKLOG_CAP);
+    }
+    return FGV_OK;
+  }
   if (c->promo_backlog.empty()) return FGV_OK;
   // the previous builds still running: leave the queue for a later call (never block the host)
   if (c->kt_busy) {
@@ -263,6 +303,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   c->key_ids = (cfg && cfg->key_ids) ? cfg->key_ids : (1u << 20);
   if (const char *e = getenv("FGV_PROMOTE_USES")) c->promote_uses = (uint32_t)std::max(1, atoi(e));
   if (const char *e = getenv("FGV_ADHOC_COMB")) c->adhoc_comb_uses = (uint32_t)std::max(1, atoi(e));
+  if (const char *e = getenv("FGV_PROMOTE_AT")) c->promote_at = (uint32_t)std::max(0, std::min(3, atoi(e)));
   if (const char *e = getenv("FGV_PROMOTE_PER_CALL")) {
     c->promote_per_call = (uint32_t)std::max(1, atoi(e));
     c->promote_fixed = true;
@@ -514,7 +555,7 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
   const bool tim = c->timing || !dn;  // (host-count callers always time their stages)
   // keys whose variable-base verifies reached the promotion threshold in an earlier call get their
   // comb tables now (stream-ordered before this batch's point kernels read kmap)
-  int prc = promote_consume(c, N);
+  int prc = promote_consume(c, N, st);
   if (prc) return prc;
   // keys without a comb (c->n_vb): k_inv lists their items, k_vb_mul computes u2 * Q for them on
   // streamV -- beside the hashes and k_prep: it needs s^-1, not the digest -- and
@@ -522,17 +563,26 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
   // (a promotion still building on streamK: its keys count as comb keys on the host but may read
   // KEY_NONE on the device, so their items still need the variable-base kernels)
   if (c->kt_busy && hipEventQuery(c->kt_ev) == hipSuccess) c->kt_busy = false;
-  const bool vb = c->n_vb > 0 || c->kt_busy;
+  const bool vb = c->n_vb > 0 || c->kt_busy || c->kmap_defer;
+  uint32_t *redo = c->redo.as<uint32_t>();
+  if (c->vb_pending) {
+    // an earlier call queued k_inv / k_vb_mul but failed before its k_vb_fin (which resets the
+    // list counters): wait for that k_vb_mul, then reset them here
+    c->vb_pending = false;
+    HIP_TRY(hipStreamWaitEvent(st, c->vb_ev[1], 0));
+    HIP_TRY(hipMemsetAsync(redo + RD_VB_CNT, 0, 4 * (RD_VB_DONE - RD_VB_CNT + 1), st));
+  }
   c->vb_launched = vb;
   if (vb && (!c->vblist.ensure((size_t)N * 4) || !c->vbacc.ensure((size_t)N * VB_ACC_WORDS * 4)))
     return FGV_ENOMEM;
-  uint32_t *redo = c->redo.as<uint32_t>();
   if (tim) HIP_TRY(hipEventRecord(c->ev[2], st));
   hipLaunchKernelGGL(k_inv, dim3(nl / INV_THREADS), dim3(INV_THREADS), 0, st, N, dn, d_status, d_slot,
                      c->key_ok.as<uint8_t>(), d_r, d_s, w.as<uint32_t>(), wscr.as<uint32_t>(),
                      vb ? c->kmap.as<uint32_t>() : nullptr, vb ? c->vblist.as<uint32_t>() : nullptr,
                      vb ? redo + RD_VB_CNT : nullptr);
   HIP_TRY(hipGetLastError());
+  prc = kmap_defer_flush(c, st, 1);
+  if (prc) return prc;
   if (tim) HIP_TRY(hipEventRecord(c->ev[3], st));
   if (vb) {
     HIP_TRY(hipEventRecord(c->vb_ev[0], st));
@@ -616,6 +666,8 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
   }
   if (forced >= 1 && forced <= POINT_LANES_MAX) L = (uint32_t)forced;
 
+  int frc = kmap_defer_flush(c, c->stream, 2);
+  if (frc) return frc;
   if (redo) {
     hipLaunchKernelGGL(k_point28, dim3(2 * c->n_cu), dim3(POINT_THREADS), 0, c->stream, N, dn, L, d_status, d_slot,
                        c->gtab28.as<apoint_raw>(), c->ktab28.as<apoint_raw>(), c->d1.as<int8_t>(), d_r, redo,
@@ -632,6 +684,8 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
   if (c->vb_pending) {  // the variable-base items: + u1 * G and the x check, after k_vb_mul (streamV)
     c->vb_pending = false;
     HIP_TRY(hipStreamWaitEvent(c->stream, c->vb_ev[1], 0));
+    frc = kmap_defer_flush(c, c->stream, 3);
+    if (frc) return frc;
     // the grid follows the last read-back batch's variable-base item count (one item per lane):
     // at least VB_FIN_WGS -- every workgroup ends with an atomic on one counter word, and a 2 x n_cu
     // grid spent ~40 us on those alone with an empty list -- at most 2 x n_cu
@@ -642,6 +696,8 @@ static int launch_prep_point(fgv_ctx *c, uint32_t N, const uint32_t *dn, uint32_
                        c->vbacc.as<uint32_t>());
     HIP_TRY(hipGetLastError());
   }
+  frc = kmap_defer_flush(c, c->stream, 0);  // (a point this call did not reach)
+  if (frc) return frc;
   HIP_TRY(hipEventRecord(c->ev[6], c->stream));  // (ahead mode 1 waits on it)
   return FGV_OK;
 }
@@ -1889,11 +1945,16 @@ static void block_outcomes(fgv_ctx *c, size_t nblocks, const size_t *ntx, const 
     }
     size_t k = 0;
     for (size_t t = 0; t < ntx[b]; t++) k += flags[o + t] == 0xFD;
-    if (k) {
-      c->blk_status[b] = FGV_EUNSUPPORTED;
-      c->unsup_txs += k;
-    }
+    if (k) c->blk_status[b] = FGV_EUNSUPPORTED;
   }
+}
+
+// undecided transactions of the call's final outcomes (counted once, after any rerun)
+static void count_unsup_txs(fgv_ctx *c, size_t nblocks, const size_t *ntx, const uint8_t *flags) {
+  size_t o = 0;
+  for (size_t b = 0; b < nblocks && b < c->blk_status.size(); o += ntx[b], b++)
+    if (c->blk_status[b] == FGV_EUNSUPPORTED)
+      for (size_t t = 0; t < ntx[b]; t++) c->unsup_txs += flags[o + t] == 0xFD;
 }
 
 // TxValidator.Validate of a batch on one GPU: the device-parse pass and the finalize kernels
@@ -1985,7 +2046,12 @@ int fgv_validate_blocks_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *con
   c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks,   next_lens, nullptr, nullptr,
                                !next_d_blocks && !d_blocks, next_d_blocks, nullptr};
   const bool soft = c->block_outcomes;
+  // (a failed call leaves no per-block outcomes of an earlier call behind)
+  c->blk_status.clear();
+  c->n_final = 0;
   auto run = [&] {
+    c->blk_status.clear();
+    c->n_final = 0;
     fgv_block_set_soft(c->blk, soft);
     const int r = validate_blocks_locked(c, nblocks, blocks, lens, d_blocks, flags, flags_cap, ntx);
     if (soft && r == FGV_OK) block_outcomes(c, nblocks, ntx, flags, fgv_block_split(c->blk));
@@ -2009,6 +2075,7 @@ int fgv_validate_blocks_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *con
   c->t_call_end = std::chrono::steady_clock::now();
   if (soft && rc == FGV_OK) {
     for (size_t b = 0; b < nblocks; b++) c->unsup_blocks += c->blk_status[b] == FGV_EUNSUPPORTED;
+    count_unsup_txs(c, nblocks, ntx, flags);
   } else if (rc == FGV_EUNSUPPORTED) {
     c->unsup_batches++;
     c->unsup_blocks += nblocks;

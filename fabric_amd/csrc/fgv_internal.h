@@ -144,9 +144,14 @@ struct fgv_ctx {
   bool vb_launched = false;       // the last verify stages ran the variable-base kernels
   uint32_t promote_uses = 64;     // variable-base verifies of one key before its comb is built
   uint32_t adhoc_comb_uses = 32;  // uses of an ad-hoc key in one call for a comb
+  // FGV_PROMOTE_AT = 1 / 2 / 3 (test knob, tests/test_gpu_concurrency.py): promotions build their
+  // tables on the main stream and enqueue k_kmap_set after k_inv / before k_point28 / before
+  // k_vb_fin of the consuming batch; kmap_defer = ids whose k_kmap_set is still to be enqueued
+  uint32_t promote_at = 0;
+  uint32_t kmap_defer = 0;
   uint64_t n_promoted = 0;        // keys promoted to a comb since fgv_init
   uint32_t promote_per_call = 32; // comb builds from the promotion queue per call (FGV_PROMOTE_PER_CALL)
-  std::vector<uint32_t> promo_backlog;  // queued ids not built yet
+  std::vector<uint32_t> promo_backlog;  // queued ids not built yet (<= VB_BACKLOG_CAP while no comb slot is free)
   bool promote_fixed = false;  // FGV_PROMOTE_PER_CALL given: no scaling by call size
   // per-block outcomes (fgv_set_block_outcomes) and the fallback counters (fgv_unsupported_stats)
   bool block_outcomes = false;

@@ -71,6 +71,7 @@ __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw 
 #define RD_VB_DONE 6
 #define RD_FIN_DONE 8     // finished k_fin_dups workgroups (the last one copies the counters out)
 #define VB_FIN_WGS 32        // k_vb_fin workgroups (256 threads)
+#define VB_BACKLOG_CAP 65536u  // host: promotion ids kept while the comb cache is full
 #define VB_PROMO_CAP 1022   // promotion queue: [0] count, [1] the last batch's variable-base items,
                             // then ids whose use count reached the threshold
 __global__ void k_keyprep(const uint32_t *qxy, const uint32_t *ids, uint32_t nkeys, uint32_t *vbt, uint8_t *key_ok);

@@ -292,7 +292,8 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
     of private-data collections -- every tx then also writes one key hash into one of them
     (chosen per tx), so its namespace checks that collection's endorsement policy (the codes
     are then the oracle's to decide, labels stay as generated); rwsets: the TxReadWriteSet bytes
-    of each tx instead of the generated ones (codes then the oracle's to decide)."""
+    of each tx instead of the generated ones (codes then the oracle's to decide), or a function
+    of the drawn labels returning them."""
     rng = random.Random((net.seed << 20) ^ (number << 4) ^ seed)
     txs = []
     fault_names = [f for f, _ in faults]
@@ -370,6 +371,10 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         t.ts = (1_700_000_000 + number * 1000 + i, rng.randrange(10 ** 9))
         txs.append(t)
 
+    # rwsets may be a function of the labels just drawn (the end-to-end pipeline generator
+    # derives each transaction's MVCC reads from which earlier transactions will be valid)
+    if callable(rwsets):
+        rwsets = rwsets([t.label for t in txs])
     # pass 1: headers, proposal response payloads, endorsement digests
     e_privs, e_digests, e_refs = [], [], []
     ed_privs, ed_msgs, ed_refs = [], [], []

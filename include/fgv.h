@@ -49,10 +49,13 @@ typedef struct fgv_config {
                             the device work per verify -- so a full cache never fails a batch    */
   uint32_t host_threads; /* host worker threads for parsing / policy fold (0 = min(24,
                             the process's CPU share: affinity mask, OMP_NUM_THREADS)) */
-  uint32_t key_ids;      /* distinct P-256 keys the context holds at once (0 = 1M; 77 B of HBM
-                            each): registered keys for good, BCCSP-path keys until the id space is
-                            flushed; only a single call naming more distinct keys than that
-                            returns FGV_ENOMEM                                                    */
+  uint32_t key_ids;      /* distinct P-256 keys the context holds at once (0 = 1M): registered
+                            keys for good, BCCSP-path keys until the id space is flushed.  HBM:
+                            9 B per id up front (key map, use count, on-curve bit) plus 7,680 B
+                            per id in use (the variable-base multiples 1..15 * 2^(32 s) Q), grown
+                            by doubling as ids are taken -- 1M ids in use is ~7.7 GB.  FGV_ENOMEM:
+                            a single call naming more distinct keys than key_ids, or a device
+                            that cannot hold the multiples of the ids in use                      */
 } fgv_config;
 
 /* Replaces factory.GetDefault() / sw.NewDefaultSecurityLevel* for the verify + hash
@@ -627,6 +630,14 @@ int fgv_blocks_verify_signed(fgv_ctx *ctx, size_t nblocks, const uint8_t *const 
  * written twice by one transaction; FGV_EINVAL if a VALID transaction does not parse. */
 int fgv_commit_hash(const uint8_t *block, size_t len, const uint8_t *flags, size_t ntx, uint64_t block_num,
                     const uint8_t *prev, size_t prev_len, uint8_t out[32]);
+
+/* fgv_commit_hash of n consecutive blocks (block b chained to block b-1's hash, block 0 to
+ * prev): the update batches and everything before the previous hash are hashed on up to
+ * `threads` host threads in parallel (0 = min(16, hardware threads)), then the chain.
+ * out: n x 32 bytes.  Same per-block result as fgv_commit_hash (kv_ledger.go:806-817). */
+int fgv_commit_hashes(size_t n, const uint8_t *const *blocks, const size_t *lens, const uint8_t *const *flags,
+                      const size_t *ntx, const uint64_t *block_nums, const uint8_t *prev, size_t prev_len,
+                      uint8_t *out, unsigned threads);
 
 /* host SHA-256 of one buffer (the data-hash primitive); returns 1 when the SHA extensions
  * were used, 0 for the portable path */

@@ -1,0 +1,37 @@
+"""CPU (host code of libfgv.so): fgv_commit_hashes -- the update batches of consecutive blocks
+hashed on host threads in parallel, then chained in block order -- reproduces every commit hash
+stored in the reference's sample ledgers (kv_ledger.go:806-817; tests/golden/sample_ledgers.*),
+and equals block-by-block fgv_commit_hash on the end-to-end pipeline generator's blocks."""
+import numpy as np
+import pytest
+
+from fabric_amd import _lib
+from tests.test_oracle_ledgers import ledgers
+
+
+@pytest.mark.parametrize("name", ["v20_testchannel", "v11_ledger1", "v11_ledger2"])
+@pytest.mark.parametrize("threads", [0, 1, 3])
+def test_commit_hashes_reference_ledgers(name, threads):
+    bl = [b for b in ledgers()[name] if b["commit_hash"] is not None]
+    assert bl[0]["number"] == 1
+    got = _lib.commit_hashes([b["block"] for b in bl], [np.array(b["flags"], np.uint8) for b in bl],
+                             [b["number"] for b in bl], b"", threads=threads)
+    assert [h.hex() for h in got] == [b["commit_hash"] for b in bl]
+    # a chain resumed in the middle: the previous block's hash as `prev`
+    k = len(bl) // 2
+    tail = _lib.commit_hashes([b["block"] for b in bl[k:]], [np.array(b["flags"], np.uint8) for b in bl[k:]],
+                              [b["number"] for b in bl[k:]], bytes.fromhex(bl[k - 1]["commit_hash"]), threads=threads)
+    assert [h.hex() for h in tail] == [b["commit_hash"] for b in bl[k:]]
+
+
+def test_commit_hashes_pipeline_blocks():
+    from fabric_amd.synth import blocks, pipeline
+    from fabric_amd.synth.mvcc import MvccState
+    net = blocks.Network(seed=3, orgs=3, clients=10)
+    st = MvccState(5000, seed=2)
+    blks, _, fexp, _ = pipeline.make_blocks(net, st, 4, 40, 3001, seed=1)
+    got = _lib.commit_hashes(blks, fexp, range(3001, 3005), b"\x07" * 32)
+    prev = b"\x07" * 32
+    for b in range(4):
+        prev = _lib.commit_hash(blks[b], fexp[b], 3001 + b, prev)
+        assert got[b] == prev, b
