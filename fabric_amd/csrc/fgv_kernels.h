@@ -123,6 +123,7 @@ __global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_
 #define MVR_HASHED 2u   // private-data key: namespace = ns + "$$h" + coll
 #define MV_HOSTPATH 2u  // MvCounters.unsup bit: range queries / metadata writes -> the host path
 #define MV_HALT 4u      // MvCounters.unsup bit: an earlier block of the batch was not finished on the device
+#define MV_OVF 8u       // MvCounters.unsup bit: batch pass, a key with more than MB_WR writers (per-block chain)
 #define MVRANGE_UNBOUNDED 1u  // MvRange.flags: end key "" (to the end of the namespace)
 #define MV_TAG_OCC 1ull      // tag bit 0: slot occupied (tags are never 0)
 #define MV_TAG_PRESENT 2ull  // committed-state tag bit 1: the key exists (clear = deleted)
@@ -162,6 +163,29 @@ struct BlkSlot {    // keys written in the block
   uint64_t fw_cand[2], fw_valid[2];
   uint64_t last;    // (epoch << 32) | (tx + 1) of the last VALID writer
 };
+#define MB_WR 8  // batch pass: writers of one key a slot lists
+struct __attribute__((aligned(64))) MbSlot {  // keys written in a batch of consecutive blocks
+  uint64_t owner;   // (batch epoch << 32) | (write index + 1); an older epoch = free
+  uint64_t last;    // (epoch << 32) | (global tx + 1) of the last VALID writer
+  uint32_t nwr;     // writers listed (reset by the slot's claimer)
+  uint32_t wr[MB_WR];  // their write-record indices, in no particular order
+};
+__global__ void k_mvb_prep(const uint8_t *base, const MvRec *reads, const MvRec *writes, MbSlot *btbl, uint32_t epoch,
+                           uint32_t *wslot, const StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint8_t *rstat,
+                           MvCounters *c);
+__global__ void k_mvb_find(uint32_t ntx, const uint8_t *base, const MvRec *reads, const MvRec *writes, MbSlot *btbl,
+                           uint32_t epoch, const uint32_t *wslot, uint32_t *rslot, const MvTxInfo *info, uint8_t *st,
+                           MvCounters *c);
+__global__ void k_mvb_round(uint32_t ntx, uint32_t r, const MvTxInfo *info, const MvRec *reads, const MvRec *writes,
+                            const uint32_t *rslot, const uint8_t *rstat, const MbSlot *btbl, uint8_t *st,
+                            const uint32_t *bfirst, const uint64_t *bnums, uint32_t nb, MvCounters *c);
+__global__ void k_mvb_last(uint32_t rlast, const MvRec *writes, const uint32_t *wslot, const uint8_t *st, MbSlot *btbl,
+                           uint32_t epoch, MvCounters *c, const unsigned long long *top, uint64_t slots_cap,
+                           uint64_t arena_cap);
+__global__ void k_mvb_upsert_find(uint32_t rlast, const uint8_t *base, MvRec *recs, const uint32_t *wslot,
+                                  const uint8_t *st, const MbSlot *btbl, uint32_t epoch, StateSlot *tbl, uint64_t mask,
+                                  const uint8_t *arena, const uint32_t *bfirst, const uint64_t *bnums, uint32_t nb,
+                                  uint8_t *pend, const MvCounters *c);
 void mvx_extract_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint8_t *base, const uint32_t *envtab,
                         const uint8_t *in_flags, MvTxInfo *info, MvRec *reads, MvRec *writes, MvCounters *c,
                         uint32_t touch, MvRec *scr, uint8_t *bad);

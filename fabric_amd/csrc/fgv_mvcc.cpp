@@ -76,15 +76,22 @@ struct fgv_mvcc_state {
   uint32_t rg = 0;                     // global fixpoint round tag (BlkSlot.fw_*)
   uint64_t btbl_cap = 0;
   uint32_t last_rounds = 0;
+  // batch pass (mvcc_batch): one head / tail per call, the batch write table, blocks staged
+  // contiguously when the caller gives no device copies
+  DevBuf mbdhead, mbtbl, mbblk, mbrstat;
+  HostBuf mbhead, mbtail;
+  uint64_t mbtbl_cap = 0;
+  uint32_t mb_epoch = 0, mb_rounds = 0;
 };
 
 void fgv_mvcc_free(fgv_mvcc_state *M) {
   if (!M) return;
-  DevBuf *d[] = {&M->tbl, &M->arena, &M->top, &M->btbl, &M->dheads, &M->lrecs, &M->lbytes, &M->qver, &M->qpres, &M->qrange, &M->qout};
+  DevBuf *d[] = {&M->tbl, &M->arena, &M->top, &M->btbl, &M->dheads, &M->lrecs, &M->lbytes, &M->qver, &M->qpres, &M->qrange, &M->qout,
+                 &M->mbdhead, &M->mbtbl, &M->mbblk, &M->mbrstat};
   for (auto *b : d) b->release();
   for (auto &S : M->set) S.release();
   if (M->ev_heads) hipEventDestroy(M->ev_heads);
-  HostBuf *h[] = {&M->hhead, &M->htail, &M->bhead, &M->btail};
+  HostBuf *h[] = {&M->hhead, &M->htail, &M->bhead, &M->btail, &M->mbhead, &M->mbtail};
   for (auto *b : h) b->release();
   delete M;
 }
@@ -1464,6 +1471,201 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   return FGV_OK;
 }
 
+// ======================================================================= batch pass
+// Consecutive blocks [first, n) validated as ONE device pass (mvcc.hip "batch pass"): one
+// extraction over every transaction of the batch in block order, the write table of the whole
+// batch, the fixpoint under the sequential rule restated there (a read checks the last valid
+// earlier writer of its key: same block -> conflict, an earlier block -> that writer's height,
+// none -> the state before the batch), one commit of each key's last valid writer at its own
+// block's height.  Results equal one fgv_mvcc_validate_block call per block.  The blocks' bytes
+// must lie within 4 GB of one base (the records' 32-bit offsets): caller device copies that do,
+// or host blocks staged here back to back.  Anything the pass does not finish -- unsupported or
+// host-path transactions (range queries, metadata writes), a key with more than MB_WR writers, a
+// longer fixpoint, a full table -- commits nothing and leaves *stop at `first`: the per-block
+// chain then takes the blocks.
+static int mvcc_batch(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, const uint8_t *const *blocks,
+                      const size_t *lens, const uint8_t *const *d_blocks, const uint64_t *block_nums,
+                      uint8_t *const *flags, const size_t *ntx, int commit, size_t *stop, size_t n_next,
+                      const uint8_t *const *next_blocks, const size_t *next_lens) {
+  *stop = first;
+  const size_t nb = n - first;
+  size_t total = 0, bytes = 0;
+  for (size_t k = 0; k < nb; k++) total += ntx[first + k], bytes += lens[first + k];
+  if (total >= 0x7FFFFFFFull) return FGV_OK;
+  // the common base: the caller's device copies when they span < 4 GB, else a staging copy
+  const uint8_t *base = nullptr;
+  std::vector<uint64_t> boff(nb);
+  bool have_dev = d_blocks != nullptr;
+  for (size_t k = 0; have_dev && k < nb; k++) have_dev = d_blocks[first + k] != nullptr;
+  if (have_dev) {
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    for (size_t k = 0; k < nb; k++) {
+      const uintptr_t a = (uintptr_t)d_blocks[first + k];
+      lo = std::min(lo, a);
+      hi = std::max(hi, a + lens[first + k] + 64);
+    }
+    if (hi - lo >= (1ull << 32)) return FGV_OK;  // (the per-block chain)
+    base = reinterpret_cast<const uint8_t *>(lo);
+    for (size_t k = 0; k < nb; k++) boff[k] = (uintptr_t)d_blocks[first + k] - lo;
+  } else {
+    uint64_t o = 0;
+    for (size_t k = 0; k < nb; k++) {
+      boff[k] = o;
+      o += (lens[first + k] + 64 + 255) & ~(size_t)255;
+    }
+    if (o >= (1ull << 32) || !M->mbblk.ensure(o)) return o >= (1ull << 32) ? FGV_OK : FGV_ENOMEM;
+    base = M->mbblk.as<uint8_t>();
+  }
+  // head: envelope table (8 B/tx) | committer flags | counters | block firsts (nb + 1) | numbers
+  const size_t et_bytes = (total * 8 + 63) & ~(size_t)63, fl_bytes = (total + 63) & ~(size_t)63;
+  const size_t bf_off = et_bytes + fl_bytes + kCounterBytes, bn_off = bf_off + (((nb + 1) * 4 + 63) & ~(size_t)63);
+  const size_t hbytes = bn_off + ((nb * 8 + 63) & ~(size_t)63);
+  const size_t tbytes = kCounterBytes + ((total + 63) & ~(size_t)63) + 64;
+  const size_t rcap = bytes / 2 + 64;
+  uint64_t bcap = 1024;
+  while (bcap < 2 * rcap) bcap <<= 1;
+  MvSet &S = M->set[0];
+  if (!M->mbhead.ensure(hbytes) || !M->mbdhead.ensure(hbytes) || !M->mbtail.ensure(tbytes) ||
+      !S.info.ensure(total * sizeof(MvTxInfo)) || !S.reads.ensure(rcap * sizeof(MvRec)) ||
+      !S.writes.ensure(rcap * sizeof(MvRec)) || !S.wslot.ensure(rcap * 4) || !S.rslot.ensure(rcap * 4) ||
+      !S.pend.ensure(rcap + 64) || !S.bad.ensure(total + 64) || !S.st.ensure(total + 64) ||
+      !S.xscr.ensure(total * 2 * MVX_SCR * sizeof(MvRec)) || !M->mbrstat.ensure(rcap + 64))
+    return FGV_ENOMEM;
+  hipStream_t s = c->stream;
+  if (bcap > M->mbtbl_cap) {  // (re)allocated: epoch 0 everywhere
+    M->mbtbl.release();
+    if (!M->mbtbl.ensure(bcap * sizeof(MbSlot))) return FGV_ENOMEM;
+    HIP_TRY(hipMemsetAsync(M->mbtbl.p, 0, bcap * sizeof(MbSlot), s));
+    M->mbtbl_cap = bcap;
+    M->mb_epoch = 0;
+  }
+  if (M->mb_epoch + 1 >= 0xFFFFFFFFu) {
+    HIP_TRY(hipMemsetAsync(M->mbtbl.p, 0, M->mbtbl_cap * sizeof(MbSlot), s));
+    M->mb_epoch = 0;
+  }
+  uint8_t *d_tail = nullptr;
+  if (hipHostGetDevicePointer(reinterpret_cast<void **>(&d_tail), M->mbtail.p, 0) != hipSuccess) return FGV_OK;
+  // envelope spans: the pre-split of this batch, else the framing walks on the host pool
+  uint8_t *h = M->mbhead.as<uint8_t>();
+  uint32_t *et = reinterpret_cast<uint32_t *>(h);
+  uint32_t *bfirst = reinterpret_cast<uint32_t *>(h + bf_off);
+  uint64_t *bnums = reinterpret_cast<uint64_t *>(h + bn_off);
+  bfirst[0] = 0;
+  for (size_t k = 0; k < nb; k++) {
+    bfirst[k + 1] = bfirst[k] + (uint32_t)ntx[first + k];
+    bnums[k] = block_nums[first + k];
+  }
+  const uint32_t *pet = nullptr;
+  const size_t *pntx = nullptr, *pfirst = nullptr;
+  const bool pre = fgv_block_take_presplit_batch(c->blk, nb, blocks + first, lens + first, &pet, &pntx, &pfirst);
+  std::vector<uint8_t> ok(nb, 0);
+  auto fill = [&](size_t k) {
+    const size_t b = first + k, T = ntx[b];
+    uint32_t *e_out = et + 2 * (size_t)bfirst[k];
+    if (pre) {
+      if (pntx[k] != T) return;
+      const uint32_t *e = pet + BD_ENV_WORDS * pfirst[k];
+      for (size_t i = 0; i < T; i++, e += BD_ENV_WORDS) {
+        e_out[2 * i] = (uint32_t)(boff[k] + e[1]);
+        e_out[2 * i + 1] = e[2];
+      }
+    } else {
+      VBlock vb;
+      if (!pbw::decode(blocks[b], lens[b], vb) || vb.data.data.size() != T) return;
+      for (size_t i = 0; i < T; i++) {
+        e_out[2 * i] = (uint32_t)(boff[k] + (uint64_t)(vb.data.data[i].p - blocks[b]));
+        e_out[2 * i + 1] = vb.data.data[i].n;
+      }
+    }
+    memcpy(h + et_bytes + bfirst[k], flags[b], T);
+    ok[k] = 1;
+  };
+  if (pre) {
+    for (size_t k = 0; k < nb; k++) fill(k);
+  } else {
+    fgv_parallel_run(c->blk, nb, fill);
+  }
+  for (size_t k = 0; k < nb; k++)
+    if (!ok[k]) return FGV_OK;  // (the per-block path reports the block's error)
+  memset(h + et_bytes + fl_bytes, 0, kCounterBytes);
+  HIP_TRY(hipEventRecord(c->ev[0], s));
+  if (!have_dev)
+    for (size_t k = 0; k < nb; k++)
+      HIP_TRY(hipMemcpyAsync(M->mbblk.as<uint8_t>() + boff[k], blocks[first + k], lens[first + k],
+                             hipMemcpyHostToDevice, s));
+  uint8_t *dh = M->mbdhead.as<uint8_t>();
+  HIP_TRY(hipMemcpyAsync(dh, h, hbytes, hipMemcpyHostToDevice, s));
+  const uint32_t *d_et = reinterpret_cast<const uint32_t *>(dh);
+  const uint8_t *d_in = dh + et_bytes;
+  MvCounters *d_c = reinterpret_cast<MvCounters *>(dh + et_bytes + fl_bytes);
+  const uint32_t *d_bf = reinterpret_cast<const uint32_t *>(dh + bf_off);
+  const uint64_t *d_bn = reinterpret_cast<const uint64_t *>(dh + bn_off);
+  MvTxInfo *d_info = S.info.as<MvTxInfo>();
+  MvRec *d_r = S.reads.as<MvRec>(), *d_w = S.writes.as<MvRec>();
+  MbSlot *d_b = M->mbtbl.as<MbSlot>();
+  const uint32_t N = (uint32_t)total, NB = (uint32_t)nb;
+  const uint32_t epoch = ++M->mb_epoch;
+  mvx_extract_launch(mvx_tpw(), s, N, base, d_et, d_in, d_info, d_r, d_w, d_c, mvx_touch(), S.xscr.as<MvRec>(),
+                     S.bad.as<uint8_t>());
+  hipLaunchKernelGGL(k_mvb_prep, grid_stride(2 * rcap), dim3(256), 0, s, base, d_r, d_w, d_b, epoch,
+                     S.wslot.as<uint32_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
+                     M->mbrstat.as<uint8_t>(), d_c);
+  hipLaunchKernelGGL(k_mvb_find, grid_stride(2 * rcap + total), dim3(256), 0, s, N, base, d_r, d_w, d_b, epoch,
+                     S.wslot.as<uint32_t>(), S.rslot.as<uint32_t>(), d_info, S.st.as<uint8_t>(), d_c);
+  // rounds: one more than the last batch needed, at least 4 (FGV_MVB_ROUNDS fixes the count)
+  static const uint32_t fixed_rounds = [] {
+    const char *e = getenv("FGV_MVB_ROUNDS");
+    return e ? (uint32_t)std::max(1, std::min(64, atoi(e))) : 0u;
+  }();
+  const uint32_t R = fixed_rounds ? fixed_rounds : std::min<uint32_t>(16, std::max<uint32_t>(4, M->mb_rounds + 1));
+  for (uint32_t r = 1; r <= R; r++)
+    hipLaunchKernelGGL(k_mvb_round, dim3((N + 63) / 64), dim3(64), 0, s, N, r, d_info, d_r, d_w,
+                       S.rslot.as<uint32_t>(), M->mbrstat.as<uint8_t>(), d_b, S.st.as<uint8_t>(), d_bf, d_bn, NB, d_c);
+  hipLaunchKernelGGL(k_mvx_flags, grid_for(total), dim3(256), 0, s, N, R, d_in, d_info, S.st.as<uint8_t>(),
+                     d_tail + kCounterBytes, d_c);
+  if (commit) {
+    hipLaunchKernelGGL(k_mvb_last, grid_stride(rcap), dim3(256), 0, s, R, d_w, S.wslot.as<uint32_t>(),
+                       S.st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
+    hipLaunchKernelGGL(k_mvb_upsert_find, grid_stride(rcap), dim3(256), 0, s, R, base, d_w, S.wslot.as<uint32_t>(),
+                       S.st.as<uint8_t>(), d_b, epoch, M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(), d_bf,
+                       d_bn, NB, S.pend.as<uint8_t>(), d_c);
+    hipLaunchKernelGGL(k_mv_upsert_insert, grid_stride(rcap), dim3(256), 0, s, 2u, R, 0u, base, d_w,
+                       S.pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
+                       M->top.as<unsigned long long>(), 0ull, d_c);
+  }
+  const size_t top_off = kCounterBytes + ((total + 63) & ~(size_t)63);
+  hipLaunchKernelGGL(k_mv_tail, dim3(1), dim3(64), 0, s, d_c, M->top.as<unsigned long long>(),
+                     reinterpret_cast<uint32_t *>(d_tail),
+                     commit ? reinterpret_cast<unsigned long long *>(d_tail + top_off) : nullptr);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[2], s));
+  // the next batch's framing walks run on the pre-split worker meanwhile
+  if (n_next) fgv_block_presplit(c->blk, c->device, n_next, next_blocks, next_lens, nullptr, nullptr);
+  HIP_TRY(fgv_stream_wait(s, mvcc_spin()));
+  const uint8_t *ht = M->mbtail.as<uint8_t>();
+  const MvCounters *hc = reinterpret_cast<const MvCounters *>(ht);
+  if (hc->unsup || !hc->done || (commit && hc->nomem)) {
+    if (!hc->unsup && !hc->done) M->mb_rounds = R;  // (the fixpoint needed more: one more next time)
+    return FGV_OK;  // nothing committed: the per-block chain takes the blocks
+  }
+  for (size_t k = 0; k < nb; k++) memcpy(flags[first + k], ht + kCounterBytes + bfirst[k], ntx[first + k]);
+  if (commit) {
+    uint64_t t[2];
+    memcpy(t, ht + top_off, 16);
+    M->arena_used = t[0];
+    M->nkeys = t[1];
+  }
+  float ms = 0;
+  c->t_mvcc_lookup = 0;
+  if (hipEventElapsedTime(&ms, c->ev[0], c->ev[2]) == hipSuccess) c->t_mvcc_total = ms / (double)nb;
+  c->n_mvcc_reads = hc->nr;
+  c->n_mvcc_writes = hc->nw;
+  M->mb_rounds = hc->rounds;
+  M->last_rounds = hc->rounds;
+  *stop = n;
+  return FGV_OK;
+}
+
 static int mvcc_blocks(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const size_t *lens,
                        const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
                        const size_t *ntx, int commit, size_t *n_done, size_t n_next,
@@ -1489,6 +1691,23 @@ static int mvcc_blocks(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const
     if (chain && ntx[done] > 0 && !(commit && fgv_block_kvmeta_count(c->blk) > 0)) {
       size_t end = done;
       while (end < n && ntx[end] > 0) end++;
+      // FGV_MVCC_BATCH=0: the per-block chain only (A/B)
+      static const bool batch = [] {
+        const char *e = getenv("FGV_MVCC_BATCH");
+        return !e || atoi(e) != 0;
+      }();
+      if (batch && end - done >= 2) {
+        const int rc = mvcc_batch(c, M, done, end, blocks, lens, d_blocks, block_nums, flags, ntx, commit, &stop,
+                                  n_next, next_blocks, next_lens);
+        n_next = 0;  // (the next batch is being walked)
+        if (rc) return rc;
+        if (stop == end) {
+          done = end;
+          if (n_done) *n_done = done;
+          if (done == n) break;
+          continue;
+        }
+      }
       const int rc = mvcc_chain(c, M, done, end, blocks, lens, d_blocks, block_nums, flags, ntx, commit, &stop,
                                 n_next, next_blocks, next_lens);
       n_next = 0;  // (the next batch is being walked)

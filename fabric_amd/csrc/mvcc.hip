@@ -819,7 +819,7 @@ __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_
                                                           unsigned long long *__restrict__ top, uint64_t block_num,
                                                           const MvCounters *__restrict__ c) {
   uint32_t n = n_host;
-  if (mode == 1) {
+  if (mode >= 1) {  // (mode 2: the batch pass -- its versions are in the records)
     if (!converged(c, rlast) || c->nomem) return;
     n = c->nw;
   }
@@ -946,6 +946,222 @@ __global__ __launch_bounds__(256) void k_mv_range_scan(uint64_t cap, const State
       v[0] = sl.blk;
       v[1] = sl.txn;
       for (uint32_t k = 0; k < sl.key_len; k++) out[o + 24 + k] = key[k];
+    }
+  }
+}
+
+// ============================================================ batch pass (consecutive blocks as one)
+// fgv_mvcc_validate_blocks over B consecutive blocks whose bytes lie within 4 GB of one base
+// (their records then share the block code's 32-bit offsets): ONE extraction, lookup and
+// fixpoint over every transaction of the batch in block order (global index g), one commit of
+// the batch's last valid writers -- a fixed ~10 launches per call instead of ~14 per block.
+//
+// The sequential reference rule, restated over the batch (validator.go:81-200, run block after
+// block with each block's updates committed before the next -- kv_ledger.go:612-652): a read of
+// key K with version V by transaction g is valid iff, with W = the LAST valid writer of K among
+// the batch's transactions before g,
+//   W in g's own block              -> conflict (updates.Exists);
+//   W in an earlier block           -> V == Height{block of W, tx of W} (nil if W deleted K): the
+//                                      committed state g's block reads was written by W;
+//   no such W                       -> V == the committed version before the batch (nil if absent).
+// Fixpoint: a read is decided once no UNDECIDED writer of K sits after the last VALID one before
+// g; a transaction is INVALID as soon as one decided read conflicts, VALID once all its reads
+// are decided and clear.  The lowest undecided transaction always decides, so rounds <= the
+// longest chain of dependent outcomes; the host enqueues a few and falls back to the per-block
+// chain when they do not suffice (nothing is committed then).
+// The batch's writers of one key are listed in its write-table slot (MB_WR at most; more -> the
+// per-block chain, MV_OVF).
+__device__ __forceinline__ uint32_t blk_of(const uint32_t *__restrict__ bfirst, uint32_t nb, uint32_t g) {
+  uint32_t lo = 0, hi = nb;  // bfirst[lo] <= g < bfirst[hi]
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (bfirst[m] <= g) lo = m;
+    else hi = m;
+  }
+  return lo;
+}
+
+// writes: claim the key's batch slot (epoch-tagged owner; the claimer empties its writer list);
+// reads: committed-state probe, static version check against the state before the batch
+__global__ __launch_bounds__(256) void k_mvb_prep(const uint8_t *__restrict__ base, const MvRec *__restrict__ reads,
+                                                  const MvRec *__restrict__ writes, MbSlot *__restrict__ btbl,
+                                                  uint32_t epoch, uint32_t *__restrict__ wslot,
+                                                  const StateSlot *__restrict__ tbl, uint64_t mask,
+                                                  const uint8_t *__restrict__ arena, uint8_t *__restrict__ rstat,
+                                                  MvCounters *__restrict__ c) {
+  const uint32_t nr = c->nr, nw = c->nw, bm = bmask_of(nw);
+  if (c->unsup) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nr + nw; i += gridDim.x * blockDim.x) {
+    if (i < nw) {
+      const MvRec w = writes[i];
+      const uint64_t mine = ((uint64_t)epoch << 32) | (i + 1);
+      uint32_t idx = (uint32_t)w.tag & bm, out = FW_INF;
+      for (uint32_t probe = 0; probe <= bm && out == FW_INF; probe++, idx = (idx + 1) & bm) {
+        unsigned long long *o = reinterpret_cast<unsigned long long *>(&btbl[idx].owner);
+        unsigned long long cur = *reinterpret_cast<volatile unsigned long long *>(o);
+        while ((uint32_t)(cur >> 32) != epoch) {
+          const unsigned long long prev = atomicCAS(o, cur, (unsigned long long)mine);
+          if (prev == cur) {
+            cur = mine;
+            btbl[idx].nwr = 0u;  // (the list fills in k_mvb_find, after every claim)
+            break;
+          }
+          cur = prev;
+        }
+        if (cur == mine || rec_eq(base, writes[(uint32_t)cur - 1], w)) out = idx;
+      }
+      wslot[i] = out;
+    } else {
+      const MvRec r = reads[i - nw];
+      const int64_t s = state_find(tbl, mask, arena, base, r);
+      const bool committed = s >= 0 && (tbl[s].tag & MV_TAG_PRESENT);
+      const bool has_ver = (r.flags & MVR_HASVER) != 0;
+      bool same;
+      if (!committed || !has_ver) same = committed == has_ver;
+      else same = tbl[s].blk == r.blk && tbl[s].txn == r.txn;
+      rstat[i - nw] = same ? 0 : 1;
+    }
+  }
+}
+
+// writes -> their slot's writer list; reads -> the key's slot (FW_INF: no batch writer);
+// transactions -> initial state
+__global__ __launch_bounds__(256) void k_mvb_find(uint32_t ntx, const uint8_t *__restrict__ base,
+                                                  const MvRec *__restrict__ reads, const MvRec *__restrict__ writes,
+                                                  MbSlot *__restrict__ btbl, uint32_t epoch,
+                                                  const uint32_t *__restrict__ wslot, uint32_t *__restrict__ rslot,
+                                                  const MvTxInfo *__restrict__ info, uint8_t *__restrict__ st,
+                                                  MvCounters *__restrict__ c) {
+  const uint32_t nr = c->nr, nw = c->nw, bm = bmask_of(nw);
+  if (c->unsup) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nw + nr + ntx; i += gridDim.x * blockDim.x) {
+    if (i < nw) {
+      const uint32_t s = wslot[i];
+      const uint32_t k = s == FW_INF ? MB_WR : atomicAdd(&btbl[s].nwr, 1u);
+      if (k < MB_WR) btbl[s].wr[k] = i;
+      else atomicOr(&c->unsup, MV_OVF);  // (a hot key: the per-block chain)
+    } else if (i < nw + nr) {
+      const MvRec r = reads[i - nw];
+      uint32_t idx = (uint32_t)r.tag & bm, out = FW_INF;
+      for (uint32_t probe = 0; probe <= bm; probe++, idx = (idx + 1) & bm) {
+        const uint64_t own = btbl[idx].owner;
+        if ((uint32_t)(own >> 32) != epoch) break;
+        const MvRec &o = writes[(uint32_t)own - 1];
+        if (o.tag == r.tag && rec_eq(base, o, r)) { out = idx; break; }
+      }
+      rslot[i - nw] = out;
+    } else {
+      const uint32_t t = i - nw - nr;
+      st[t] = info[t].code == 0 ? ST_UNDEC : ST_INVALID;
+    }
+  }
+}
+
+// fixpoint round r (1-based)
+__global__ __launch_bounds__(64) void k_mvb_round(uint32_t ntx, uint32_t r, const MvTxInfo *__restrict__ info,
+                                                  const MvRec *__restrict__ reads, const MvRec *__restrict__ writes,
+                                                  const uint32_t *__restrict__ rslot, const uint8_t *__restrict__ rstat,
+                                                  const MbSlot *__restrict__ btbl, uint8_t *__restrict__ st,
+                                                  const uint32_t *__restrict__ bfirst, const uint64_t *__restrict__ bnums,
+                                                  uint32_t nb, MvCounters *__restrict__ c) {
+  if (c->done || c->unsup) return;
+  if (r > 1 && c->undec[(r - 1) & 3] == 0) {  // round r-1 decided everything
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      c->done = 1;
+      c->rounds = r - 1;
+    }
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) c->undec[(r + 1) & 3] = 0;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t und = 0;
+  if (g < ntx && st[g] == ST_UNDEC) {
+    const MvTxInfo I = info[g];
+    const uint32_t gb = blk_of(bfirst, nb, g);
+    bool conflict = false, open = false;
+    for (uint32_t j = I.rbeg; j < I.rbeg + I.rcnt && !conflict; j++) {
+      const uint32_t s = rslot[j];
+      int64_t vmax = -1, umax = -1;
+      uint32_t vw = 0;
+      if (s != FW_INF) {
+        const uint32_t n = min(btbl[s].nwr, (uint32_t)MB_WR);
+        for (uint32_t q = 0; q < n; q++) {
+          const uint32_t w = btbl[s].wr[q];
+          const uint32_t gw = writes[w].tx;
+          if (gw >= g) continue;
+          const uint8_t sw = st[gw];
+          if (sw == ST_VALID && (int64_t)gw > vmax) { vmax = gw; vw = w; }
+          else if (sw == ST_UNDEC && (int64_t)gw > umax) umax = gw;
+        }
+      }
+      if (umax > vmax) { open = true; continue; }  // an undecided later writer decides this read
+      if (vmax < 0) {
+        conflict = rstat[j] != 0;
+        continue;
+      }
+      const uint32_t wb = blk_of(bfirst, nb, (uint32_t)vmax);
+      if (wb == gb) { conflict = true; continue; }  // written earlier in the same block
+      const MvRec rd = reads[j];
+      const bool has_ver = (rd.flags & MVR_HASVER) != 0;
+      if (writes[vw].flags & MVR_DELETE) conflict = has_ver;
+      else conflict = !has_ver || rd.blk != bnums[wb] || rd.txn != (uint64_t)((uint32_t)vmax - bfirst[wb]);
+    }
+    const uint8_t s = conflict ? ST_INVALID : open ? ST_UNDEC : ST_VALID;
+    if (s != ST_UNDEC) st[g] = s;
+    und = s == ST_UNDEC;
+  }
+  for (int off = 32; off > 0; off >>= 1) und += __shfl_down(und, off);
+  if ((threadIdx.x & 63u) == 0 && und) atomicAdd(&c->undec[r & 3], und);
+}
+
+// commit, part 1: the last VALID writer of each key over the whole batch; capacity check
+__global__ __launch_bounds__(256) void k_mvb_last(uint32_t rlast, const MvRec *__restrict__ writes,
+                                                  const uint32_t *__restrict__ wslot, const uint8_t *__restrict__ st,
+                                                  MbSlot *__restrict__ btbl, uint32_t epoch, MvCounters *__restrict__ c,
+                                                  const unsigned long long *__restrict__ top, uint64_t slots_cap,
+                                                  uint64_t arena_cap) {
+  if (!converged(c, rlast)) return;
+  const uint32_t nw = c->nw;
+  if ((top[1] + nw) * 10 > slots_cap * 7 || top[0] + c->wbytes > arena_cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) c->nomem = 1;
+    return;
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += gridDim.x * blockDim.x) {
+    const uint32_t tx = writes[i].tx;
+    if (st[tx] == ST_VALID)
+      atomicMax(reinterpret_cast<unsigned long long *>(&btbl[wslot[i]].last), ((unsigned long long)epoch << 32) | (tx + 1));
+  }
+}
+
+// commit, part 2: the last valid writer of each key updates the committed entry in place at
+// Height{its block's number, its index in the block}, or is marked for insertion (then
+// k_mv_upsert_insert, mode 2, takes the version from the record written here)
+__global__ __launch_bounds__(256) void k_mvb_upsert_find(uint32_t rlast, const uint8_t *__restrict__ base,
+                                                         MvRec *__restrict__ recs, const uint32_t *__restrict__ wslot,
+                                                         const uint8_t *__restrict__ st, const MbSlot *__restrict__ btbl,
+                                                         uint32_t epoch, StateSlot *__restrict__ tbl, uint64_t mask,
+                                                         const uint8_t *__restrict__ arena,
+                                                         const uint32_t *__restrict__ bfirst,
+                                                         const uint64_t *__restrict__ bnums, uint32_t nb,
+                                                         uint8_t *__restrict__ pend, const MvCounters *__restrict__ c) {
+  if (!converged(c, rlast) || c->nomem) return;
+  const uint32_t n = c->nw;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    MvRec w = recs[i];
+    pend[i] = 0;
+    if (st[w.tx] != ST_VALID || btbl[wslot[i]].last != (((uint64_t)epoch << 32) | (w.tx + 1))) continue;
+    const uint32_t b = blk_of(bfirst, nb, w.tx);
+    const uint64_t vb = bnums[b], vt = w.tx - bfirst[b];
+    const bool del = (w.flags & MVR_DELETE) != 0;
+    const int64_t s = state_find(tbl, mask, arena, base, w);
+    if (s >= 0) {
+      tbl[s].blk = vb;
+      tbl[s].txn = vt;
+      tbl[s].tag = del ? (tbl[s].tag & ~MV_TAG_PRESENT) : (tbl[s].tag | MV_TAG_PRESENT);
+    } else if (!del) {
+      recs[i].blk = vb;
+      recs[i].txn = vt;
+      pend[i] = 1;
     }
   }
 }

@@ -194,3 +194,73 @@ def test_chain_empty_call():
     out, rc, done = eng.mvcc_validate_blocks([], [], [], commit=True)
     assert rc == 0 and done == 0 and out == []
     eng.close()
+
+
+def _random_batch(seed, nblocks, ntx, nkeys, committed, base_num, dels=0.15, hot=None):
+    """blocks over a small key space: reads at the committed version, at an earlier block's
+    height (right or wrong), nil, or a stale version; writes and deletes of few keys, so keys
+    have several writers across and inside blocks.  `committed`: the version map a correct
+    endorser would have seen before each block -- updated here by the ORACLE's own commit
+    (reads are drawn from the true state half of the time)."""
+    import random
+    rng = random.Random(seed)
+    out = []
+    keys = ["k%03d" % i for i in range(nkeys)]
+    for b in range(nblocks):
+        envs = []
+        for t in range(ntx):
+            reads = []
+            for _ in range(rng.randrange(0, 4)):
+                k = hot if hot and rng.random() < 0.3 else rng.choice(keys)
+                u = rng.random()
+                if u < 0.5:
+                    v = committed.get(k)
+                elif u < 0.7:
+                    v = (base_num + rng.randrange(max(1, b)), rng.randrange(ntx))
+                elif u < 0.85:
+                    v = None
+                else:
+                    v = (rng.randrange(1, 50), rng.randrange(20))
+                reads.append((k, v))
+            writes = []
+            for k in rng.sample(keys, rng.randrange(0, 3)):
+                writes.append((k, b"v%d" % t, rng.random() < dels))
+            if hot and rng.random() < 0.5 and hot not in [w[0] for w in writes]:
+                writes.append((hot, b"h", False))
+            envs.append(_tx(reads, writes))
+        out.append(_blk(envs))
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_batch_pass_cross_block_rules(seed):
+    """fgv_mvcc_validate_blocks over blocks whose transactions read keys the batch's earlier
+    blocks wrote or deleted (at those blocks' heights, stale heights, nil), with several writers
+    of a key across and inside blocks: every block's flags and the committed state equal the
+    oracle committing block after block"""
+    import random
+    rng = random.Random(seed)
+    init = {("ns1", "k%03d" % i): (rng.randrange(1, 40), rng.randrange(10)) for i in range(40) if rng.random() < 0.7}
+    db = OM.StateDB(dict(init))
+    eng = _lib.Engine(0)
+    eng.statedb_init(1 << 12, 1 << 20)
+    ks = [k for (_, k) in init]
+    eng.statedb_load("ns1", ks, np.array([init[("ns1", k)][0] for k in ks]), np.array([init[("ns1", k)][1] for k in ks]))
+    base_num = 100
+    for call in range(3):
+        nb = 4
+        # blocks drawn against the oracle's state as it evolves (half the reads current)
+        committed = {k: v for (_, k), v in db.v.items()}
+        blks = _random_batch(seed * 10 + call, nb, 30, 40, committed, base_num, hot=None if call < 2 else "k007")
+        exp = [list(OM.validate_block(db, blk, [0] * 30, base_num + i, commit=True)) for i, blk in enumerate(blks)]
+        fl, rc, done = eng.mvcc_validate_blocks(blks, range(base_num, base_num + nb), [[0] * 30] * nb, commit=True)
+        assert rc == 0 and done == nb
+        for i in range(nb):
+            assert list(fl[i]) == exp[i], (call, i, [(t, int(fl[i][t]), exp[i][t]) for t in range(30) if fl[i][t] != exp[i][t]][:8])
+        base_num += nb
+    # the committed state: every key probed at the oracle's version
+    keys = sorted({k for (_, k) in db.v} | set(ks))
+    vers = [db.v.get(("ns1", k)) for k in keys]
+    envs = [_tx([(k, v)], []) for k, v in zip(keys, vers)]
+    assert list(eng.mvcc_validate(_blk(envs), base_num, [0] * len(envs), commit=False)) == [0] * len(envs)
+    eng.close()

@@ -14,6 +14,7 @@
 #   churn            C2 with every creator a distinct identity (the cold-key path)
 #   sigchurn         C4 with every item its own key (registered cold)
 #   churntrace       rocprofv3 kernel + HIP API trace of a short churn run
+#   pipeline         the end-to-end commit pipeline (committer -> MVCC -> commit hash)
 #   mvcc | sig | c5 | sbe   the other workloads (tools/bench_sbe.py for sbe)
 #   mvccpmc          FETCH_SIZE / WRITE_SIZE passes of the mvcc workload
 #   trace            rocprofv3 --kernel-trace --stats of a C2 run
@@ -95,6 +96,10 @@ for step in "$@"; do
         && timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o run -- python bench.py --workload mvcc --steps 10 --warmup 2 > $O/pmc_write.json 2> $O/pmc_write.err \
         || { echo mvccpmc failed; exit 1; }
       echo mvccpmc ok ;;
+    pipeline)
+      timeout -k 10 400 python -u bench.py --workload pipeline --steps 12 --warmup 2 > $O/pipeline.json 2> $O/pipeline.err \
+        || { echo pipeline failed; tail -20 $O/pipeline.err; exit 1; }
+      show $O/pipeline.json pipeline value ms_per_step parity_vs_labels stage_ms_per_step latency_1block_ms ;;
     mvcc)
       timeout -k 10 300 python -u bench.py --workload mvcc --steps 100 --warmup 5 > $O/mvcc.json 2> $O/mvcc.err \
         || { echo mvcc failed; tail -20 $O/mvcc.err; exit 1; }
