@@ -259,8 +259,8 @@ def test_batch_pass_cross_block_rules(seed):
             assert list(fl[i]) == exp[i], (call, i, [(t, int(fl[i][t]), exp[i][t]) for t in range(30) if fl[i][t] != exp[i][t]][:8])
         base_num += nb
     # the committed state: every key probed at the oracle's version
-    keys = sorted({k for (_, k) in db.v} | set(ks))
-    vers = [db.v.get(("ns1", k)) for k in keys]
+    keys = sorted({k.decode() for (_, k) in db.v} | set(ks))
+    vers = [db.get_version("ns1", k) for k in keys]
     envs = [_tx([(k, v)], []) for k, v in zip(keys, vers)]
     assert list(eng.mvcc_validate(_blk(envs), base_num, [0] * len(envs), commit=False)) == [0] * len(envs)
     eng.close()
