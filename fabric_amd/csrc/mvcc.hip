@@ -1057,7 +1057,24 @@ __global__ __launch_bounds__(256) void k_mvb_find(uint32_t ntx, const uint8_t *_
   }
 }
 
-// fixpoint round r (1-based)
+// Transaction states shared across the launch's workgroups (and XCDs): device-scope atomics on
+// the 32-bit word holding the byte (a state goes from UNDEC = 0 to VALID or INVALID once)
+__device__ __forceinline__ uint8_t st_ld(const uint8_t *st, uint32_t g) {
+  const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t *>(st) + (g >> 2), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return (uint8_t)(w >> (8 * (g & 3u)));
+}
+__device__ __forceinline__ void st_set(uint8_t *st, uint32_t g, uint8_t s) {
+  __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(st) + (g >> 2), (uint32_t)s << (8 * (g & 3u)), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// fixpoint round r (1-based).  Within a round an undecided transaction re-evaluates up to
+// MVB_SPIN times, reading the other transactions' states as they are published, so a chain of
+// dependent outcomes (a read of a key an earlier block's transaction wrote, whose own validity
+// waits on an earlier one ...) resolves inside one launch instead of one launch per link.  The
+// loop is bounded: whatever is still undecided is counted and the next round continues it.
+#define MVB_SPIN 96u
 __global__ __launch_bounds__(64) void k_mvb_round(uint32_t ntx, uint32_t r, const MvTxInfo *__restrict__ info,
                                                   const MvRec *__restrict__ reads, const MvRec *__restrict__ writes,
                                                   const uint32_t *__restrict__ rslot, const uint8_t *__restrict__ rstat,
@@ -1075,39 +1092,44 @@ __global__ __launch_bounds__(64) void k_mvb_round(uint32_t ntx, uint32_t r, cons
   if (blockIdx.x == 0 && threadIdx.x == 0) c->undec[(r + 1) & 3] = 0;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t und = 0;
-  if (g < ntx && st[g] == ST_UNDEC) {
+  if (g < ntx && st_ld(st, g) == ST_UNDEC) {
     const MvTxInfo I = info[g];
     const uint32_t gb = blk_of(bfirst, nb, g);
-    bool conflict = false, open = false;
-    for (uint32_t j = I.rbeg; j < I.rbeg + I.rcnt && !conflict; j++) {
-      const uint32_t s = rslot[j];
-      int64_t vmax = -1, umax = -1;
-      uint32_t vw = 0;
-      if (s != FW_INF) {
-        const uint32_t n = min(btbl[s].nwr, (uint32_t)MB_WR);
-        for (uint32_t q = 0; q < n; q++) {
-          const uint32_t w = btbl[s].wr[q];
-          const uint32_t gw = writes[w].tx;
-          if (gw >= g) continue;
-          const uint8_t sw = st[gw];
-          if (sw == ST_VALID && (int64_t)gw > vmax) { vmax = gw; vw = w; }
-          else if (sw == ST_UNDEC && (int64_t)gw > umax) umax = gw;
+    uint8_t s = ST_UNDEC;
+    for (uint32_t pass = 0;; pass++) {
+      bool conflict = false, open = false;
+      for (uint32_t j = I.rbeg; j < I.rbeg + I.rcnt && !conflict; j++) {
+        const uint32_t sl = rslot[j];
+        int64_t vmax = -1, umax = -1;
+        uint32_t vw = 0;
+        if (sl != FW_INF) {
+          const uint32_t n = min(btbl[sl].nwr, (uint32_t)MB_WR);
+          for (uint32_t q = 0; q < n; q++) {
+            const uint32_t w = btbl[sl].wr[q];
+            const uint32_t gw = writes[w].tx;
+            if (gw >= g) continue;
+            const uint8_t sw = st_ld(st, gw);
+            if (sw == ST_VALID && (int64_t)gw > vmax) { vmax = gw; vw = w; }
+            else if (sw == ST_UNDEC && (int64_t)gw > umax) umax = gw;
+          }
         }
+        if (umax > vmax) { open = true; continue; }  // an undecided later writer decides this read
+        if (vmax < 0) {
+          conflict = rstat[j] != 0;
+          continue;
+        }
+        const uint32_t wb = blk_of(bfirst, nb, (uint32_t)vmax);
+        if (wb == gb) { conflict = true; continue; }  // written earlier in the same block
+        const MvRec rd = reads[j];
+        const bool has_ver = (rd.flags & MVR_HASVER) != 0;
+        if (writes[vw].flags & MVR_DELETE) conflict = has_ver;
+        else conflict = !has_ver || rd.blk != bnums[wb] || rd.txn != (uint64_t)((uint32_t)vmax - bfirst[wb]);
       }
-      if (umax > vmax) { open = true; continue; }  // an undecided later writer decides this read
-      if (vmax < 0) {
-        conflict = rstat[j] != 0;
-        continue;
-      }
-      const uint32_t wb = blk_of(bfirst, nb, (uint32_t)vmax);
-      if (wb == gb) { conflict = true; continue; }  // written earlier in the same block
-      const MvRec rd = reads[j];
-      const bool has_ver = (rd.flags & MVR_HASVER) != 0;
-      if (writes[vw].flags & MVR_DELETE) conflict = has_ver;
-      else conflict = !has_ver || rd.blk != bnums[wb] || rd.txn != (uint64_t)((uint32_t)vmax - bfirst[wb]);
+      s = conflict ? ST_INVALID : open ? ST_UNDEC : ST_VALID;
+      if (s != ST_UNDEC || pass + 1 >= MVB_SPIN) break;
+      __builtin_amdgcn_s_sleep(4);
     }
-    const uint8_t s = conflict ? ST_INVALID : open ? ST_UNDEC : ST_VALID;
-    if (s != ST_UNDEC) st[g] = s;
+    if (s != ST_UNDEC) st_set(st, g, s);
     und = s == ST_UNDEC;
   }
   for (int off = 32; off > 0; off >>= 1) und += __shfl_down(und, off);

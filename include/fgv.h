@@ -632,8 +632,9 @@ int fgv_commit_hash(const uint8_t *block, size_t len, const uint8_t *flags, size
                     const uint8_t *prev, size_t prev_len, uint8_t out[32]);
 
 /* fgv_commit_hash of n consecutive blocks (block b chained to block b-1's hash, block 0 to
- * prev): the update batches and everything before the previous hash are hashed on up to
- * `threads` host threads in parallel (0 = min(16, hardware threads)), then the chain.
+ * prev): the update batches and everything before the previous hash are hashed on a
+ * persistent pool of min(16, hardware threads) host threads in parallel (threads = 1: on the
+ * caller's thread only; other values: the pool), then the chain.
  * out: n x 32 bytes.  Same per-block result as fgv_commit_hash (kv_ledger.go:806-817). */
 int fgv_commit_hashes(size_t n, const uint8_t *const *blocks, const size_t *lens, const uint8_t *const *flags,
                       const size_t *ntx, const uint64_t *block_nums, const uint8_t *prev, size_t prev_len,

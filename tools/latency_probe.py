@@ -21,13 +21,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--tx", type=int, default=500)
+    ap.add_argument("--churn", action="store_true", help="client keys on the variable-base kernels (no combs)")
     a = ap.parse_args()
     net = blocks.Network(seed=3, orgs=3, clients=100)
     blk, lab, _ = blocks.make_block(net, a.tx, number=1, seed=7)
     exp = np.array([e if e is not None else 255 for e in blocks.expected_codes(lab)])
     known = np.array([e is not None for e in blocks.expected_codes(lab)])
     eng = _lib.Engine(0)
-    txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes)
+    # the bench's headline setup: the 100 clients hold comb tables (--churn: variable-base)
+    txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes, hot_clients=not a.churn)
     dev = torch.device("cuda", 0)
     d = torch.zeros(len(blk) + 256, dtype=torch.uint8, device=dev)
     d[:len(blk)].copy_(torch.frombuffer(bytearray(blk), dtype=torch.uint8))
