@@ -100,6 +100,12 @@ struct DevJobIdx {
   uint32_t cnt[BJ_KINDS];  // jobs of each kind (creator-payload, txid, proposal, endorsement, index)
   uint32_t base[BJ_KINDS]; // first job of each kind (slot within the kind's group)
 };
+// the verify job columns (fgv_block_jobs_reserve layout, stride = the batch's capacity):
+// k_bd_count writes them when given (sig_ptr != null), else k_bd_emit
+struct BdVerifyCols {
+  uint64_t *sig_ptr;
+  uint32_t *sig_len, *key_slot, *dig_idx;
+};
 
 // identity registry in HBM (built on the host from the channel model)
 struct DevIdent {

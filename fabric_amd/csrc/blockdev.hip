@@ -72,22 +72,31 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
 // total (all kinds' atomics in flight at once).  Slots of a kind stay grouped; their order
 // across workgroups is the atomics' order.  (One atomic per wave and kind, issued one kind after
 // the other, made this kernel ~55 us of contended atomics on one cache line.)
+// With the verify columns given (vc.sig_ptr != null, the default device path) the kernel also
+// does k_bd_emit's work: a transaction's creator and endorsement verifies take ONE contiguous
+// range of the BJ_C counter (J.base[BJ_C] = the creator's slot, J.base[BJ_E] = the first
+// endorsement's, absolute; totals[BJ_E] stays 0, so totals[BJ_C] is the verify count the
+// stages behind read), and the thread writes its verify jobs at once -- one launch fewer on the
+// committer's chain.
 #define BC_THREADS 1024u
 __global__ __launch_bounds__(BC_THREADS) void k_bd_count(uint32_t ntx, DevTx *__restrict__ txs, DevChannel ch,
                                                          const int32_t *__restrict__ ident,
                                                          DevJobIdx *__restrict__ jobs, uint32_t *__restrict__ totals,
-                                                         uint32_t prio) {
+                                                         uint32_t prio, const uint64_t *__restrict__ bases,
+                                                         BdVerifyCols vc) {
   if (prio == 3) __builtin_amdgcn_s_setprio(3);  // (FGV_FRONT_PRIO, A/B)
   else __builtin_amdgcn_s_setprio(2);  // front-half chain; k_bd_sha fills the SIMDs beside it
   __shared__ uint32_t wtot[BJ_KINDS][BC_THREADS / 64], wbase[BJ_KINDS][BC_THREADS / 64];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool fused = vc.sig_ptr != nullptr;
   DevJobIdx J;
   for (int q = 0; q < BJ_KINDS; q++) J.cnt[q] = J.base[q] = 0;
   if (t < ntx) count_jobs(txs[t], ch, ident + (size_t)t * BD_OCC, J);
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   uint32_t incl[BJ_KINDS];
   for (int q = 0; q < BJ_KINDS; q++) {
-    uint32_t v = J.cnt[q];
+    // (fused: the endorsements claim inside the creator kind's range)
+    uint32_t v = fused ? (q == BJ_C ? J.cnt[BJ_C] + J.cnt[BJ_E] : q == BJ_E ? 0u : J.cnt[q]) : J.cnt[q];
     for (uint32_t d = 1; d < 64; d <<= 1) {
       const uint32_t o = (uint32_t)__shfl_up((int)v, d);
       if (lane >= d) v += o;
@@ -108,7 +117,34 @@ __global__ __launch_bounds__(BC_THREADS) void k_bd_count(uint32_t ntx, DevTx *__
   }
   __syncthreads();
   for (int q = 0; q < BJ_KINDS; q++) J.base[q] = wbase[q][0] + wtot[q][w] + incl[q] - J.cnt[q];
-  if (t < ntx) jobs[t] = J;
+  if (fused) {
+    const uint32_t v0 = wbase[BJ_C][0] + wtot[BJ_C][w] + incl[BJ_C] - (J.cnt[BJ_C] + J.cnt[BJ_E]);
+    J.base[BJ_C] = v0;
+    J.base[BJ_E] = v0 + J.cnt[BJ_C];
+  }
+  if (t >= ntx) return;
+  jobs[t] = J;
+  if (!fused) return;
+  // k_bd_emit's assembly: verify jobs [creator | its endorsements]; digests are k_bd_sha's slots
+  const DevTx &R = txs[t];
+  const int32_t *id = ident + (size_t)t * BD_OCC;
+  const uint64_t base = bases[R.blk];
+  auto verify = [&](uint32_t vi, DSpan sig, int32_t slot, uint32_t dig) {
+    vc.sig_ptr[vi] = sig.len ? base + sig.off : 0ull;
+    vc.sig_len[vi] = sig.len;
+    vc.key_slot[vi] = (uint32_t)slot;
+    vc.dig_idx[vi] = dig;
+  };
+  if (J.cnt[BJ_C]) verify(J.base[BJ_C], R.env_sig, ch.idents[id[0]].key_slot, t);
+  if (J.cnt[BJ_E]) {
+    uint32_t r = 0;
+    for (uint32_t k = 0; k < R.nend && r < J.cnt[BJ_E]; k++) {
+      const int32_t e = id[1 + k];
+      if (e < 0 || ch.idents[e].vclass != 0) continue;
+      verify(J.base[BJ_E] + r, R.end_sig[k], ch.idents[e].key_slot, (1 + k) * ntx + t);
+      r++;
+    }
+  }
 }
 DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx &J) {
   if (R.pre == C_PENDING) {  // DeserializeIdentity -> Validate -> Verify (msgvalidation.go:26-64)

@@ -405,7 +405,9 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
           if (e < 0) continue;
           const DevIdent &I = ch.idents[e];
           const bool has_job = I.vclass == 0;
-          const uint32_t vj = has_job ? totals[0] + J.base[BJ_E] + r : 0u;
+          // (k_bd_count's fused emission leaves totals[BJ_E] at 0 and J.base[BJ_E] absolute; k_bd_emit
+          // numbers endorsements after all creators)
+          const uint32_t vj = has_job ? (totals[BJ_E] ? totals[0] : 0u) + J.base[BJ_E] + r : 0u;
           if (has_job) r++;
           bool dup = false;
           for (uint32_t q = 0; q < nids; q++) dup |= seen[q] == I.canon;

@@ -211,6 +211,7 @@ struct BdSet {
   // so that k_bd_emit -> k_der -> k_inv of a batch can run ahead with its front half (vdone)
   DevBuf vsig, vst, vr, vs, vw, vscr;
   bool vdone = false;
+  bool emitted = false;  // k_bd_count wrote the verify jobs (FGV_FUSE_EMIT, default): no k_bd_emit
   uint32_t klseq = 0;                   // the bucket tag of the batch this set holds
   KlDev kl{};
   HostBuf head, misc;                // pinned head staging / counters read back
@@ -1772,7 +1773,7 @@ __global__ void k_head_pull(const uint4 *src, uint4 *dst, uint32_t n16);
 __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, int32_t *ident,
                            uint32_t prio);
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
-                           uint32_t *totals, uint32_t prio);
+                           uint32_t *totals, uint32_t prio, const uint64_t *bases, BdVerifyCols vc);
 __global__ void k_bd_sha(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
 __global__ void k_bd_sha2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
 __global__ void k_bd_sha_p2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig,
@@ -1911,14 +1912,20 @@ static int emit_prefix(fgv_ctx *c, fgv_block_state *S, BdSet &B, hipStream_t st)
   const uint64_t *dbs = reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff);
   uint8_t *sp = B.vsig.as<uint8_t>();
   const bool tim = c->timing && B.timed;
-  if (tim) HIP_TRY(hipEventRecord(c->kev[6], st));
-  hipLaunchKernelGGL(k_bd_emit, dim3((N + 255) / 256), dim3(256), 0, st, N, B.tx.as<DevTx>(), dbs, S->dimg.ch,
-                     B.ident.as<int32_t>(), B.jobs.as<DevJobIdx>(), misc, reinterpret_cast<uint64_t *>(sp),
-                     reinterpret_cast<uint32_t *>(sp + cap * 8), reinterpret_cast<uint32_t *>(sp + cap * 12),
-                     reinterpret_cast<uint32_t *>(sp + cap * 16), misc + 10);
-  HIP_TRY(hipGetLastError());
-  if (tim) HIP_TRY(hipEventRecord(c->kev[7], st));
-  int rc = fgv_verify_prefix_dev(c, st, cap, misc + 10, sp, B.vst.as<uint8_t>(), B.vr, B.vs, B.vw, B.vscr);
+  // the verify count the stages read: k_bd_count's creator-kind total when it emitted the jobs
+  // (endorsements inside the same range), else k_bd_emit's sum
+  const uint32_t *dn = misc + BJ_C;
+  if (!B.emitted) {
+    if (tim) HIP_TRY(hipEventRecord(c->kev[6], st));
+    hipLaunchKernelGGL(k_bd_emit, dim3((N + 255) / 256), dim3(256), 0, st, N, B.tx.as<DevTx>(), dbs, S->dimg.ch,
+                       B.ident.as<int32_t>(), B.jobs.as<DevJobIdx>(), misc, reinterpret_cast<uint64_t *>(sp),
+                       reinterpret_cast<uint32_t *>(sp + cap * 8), reinterpret_cast<uint32_t *>(sp + cap * 12),
+                       reinterpret_cast<uint32_t *>(sp + cap * 16), misc + 10);
+    HIP_TRY(hipGetLastError());
+    if (tim) HIP_TRY(hipEventRecord(c->kev[7], st));
+    dn = misc + 10;
+  }
+  int rc = fgv_verify_prefix_dev(c, st, cap, dn, sp, B.vst.as<uint8_t>(), B.vr, B.vs, B.vw, B.vscr);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(B.ev[9], st));
   B.vdone = true;
@@ -2149,8 +2156,24 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   if (!fused_ident)
     hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 * BD_ID_PAR + 255) / 256)), dim3(256), 0, sf, N,
                        dtx, dbs, ch, B.ident.as<int32_t>(), front_prio);
+  // FGV_FUSE_EMIT=0: k_bd_emit as its own kernel at the head of the back half (A/B); by default
+  // k_bd_count writes the verify jobs itself
+  static const bool fuse_emit = [] {
+    const char *e = getenv("FGV_FUSE_EMIT");
+    return !e || atoi(e) != 0;
+  }();
+  BdVerifyCols vc{nullptr, nullptr, nullptr, nullptr};
+  B.emitted = false;
+  if (fuse_emit) {
+    const size_t cap = (size_t)N * (1 + BD_MAX_END);
+    if (!B.vsig.ensure(cap * 20 + 64) || !B.vst.ensure(cap + 64)) return FGV_ENOMEM;
+    uint8_t *sp = B.vsig.as<uint8_t>();
+    vc = BdVerifyCols{reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + cap * 8),
+                      reinterpret_cast<uint32_t *>(sp + cap * 12), reinterpret_cast<uint32_t *>(sp + cap * 16)};
+    B.emitted = true;
+  }
   hipLaunchKernelGGL(k_bd_count, dim3((N + 1023) / 1024), dim3(1024), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
-                     B.jobs.as<DevJobIdx>(), misc, front_prio);
+                     B.jobs.as<DevJobIdx>(), misc, front_prio, dbs, vc);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(B.ev[6], sf));
   B.N = N;
@@ -2303,7 +2326,7 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   }
   c->digests_ready = B.ev[8];  // (payload and the other digests, joined on stream3)
   c->digests_ready2 = nullptr;
-  int rc = fgv_verify_main_dev(c, cap, misc + 10, n_est, B.vsig.as<uint8_t>(), B.vst.as<uint8_t>(),
+  int rc = fgv_verify_main_dev(c, cap, B.emitted ? misc + BJ_C : misc + 10, n_est, B.vsig.as<uint8_t>(), B.vst.as<uint8_t>(),
                                B.vr.as<uint32_t>(), B.vw.as<uint32_t>(), B.dig.as<uint8_t>());
   c->digests_ready = c->digests_ready2 = nullptr;
   if (rc) return rc;
@@ -2409,8 +2432,9 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   memcpy(&np, hm + 8, 8);
   c->n_sha_blocks = nb + np;
   c->n_pay_blocks = np;
-  c->n_verifies = hm[10];
-  if (B.N) S->nv_per_tx = (double)hm[10] / B.N;  // the next batch's lanes-per-verify estimate
+  const uint32_t nv = B.emitted ? hm[BJ_C] : hm[10];  // (the fused count: endorsements inside BJ_C)
+  c->n_verifies = nv;
+  if (B.N) S->nv_per_tx = (double)nv / B.N;  // the next batch's lanes-per-verify estimate
   c->t_host_device = std::chrono::duration<double, std::milli>(clk::now() - S->t_enq).count();
   c->t_host_fold = 0;
   c->t_finish = std::chrono::duration<double, std::milli>(clk::now() - t_woke).count();

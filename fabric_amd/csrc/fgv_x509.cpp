@@ -60,6 +60,7 @@ bool eq(const uint8_t *b, const T &t, const char *hex_bytes, size_t n) {
 OIDV(OID_EC_KEY, '\x2a', '\x86', '\x48', '\xce', '\x3d', '\x02', '\x01');
 OIDV(OID_P256, '\x2a', '\x86', '\x48', '\xce', '\x3d', '\x03', '\x01', '\x07');
 OIDV(OID_ED25519, '\x2b', '\x65', '\x70');
+OIDV(OID_RSA, '\x2a', '\x86', '\x48', '\x86', '\xf7', '\x0d', '\x01', '\x01', '\x01');
 OIDV(OID_OU, '\x55', '\x04', '\x0b');
 #undef OIDV
 // AlgorithmIdentifier{ecdsa-with-SHA256} with no parameters
@@ -298,7 +299,13 @@ void parse(Cert &c) {
     }
   } else if (eq(b, koid, OID_ED25519, sizeof OID_ED25519)) {
     c.key = XK_UNDESERIALIZABLE;  // (a parse error or a KeyImport error: undeserializable either way)
-  } else {  // (RSA: Go's PKCS#1 key checks are not restated)
+  } else if (eq(b, koid, OID_RSA, sizeof OID_RSA)) {
+    // RSA never passes identity.Verify (msp/identities.go:190 passes nil opts, rejected by
+    // bccsp/sw/rsa.go:48-61): key accepted or not by Go's PKCS#1 checks, every path
+    // treats the identity alike (creator: BAD_CREATOR_SIGNATURE; endorsement, orderer signature:
+    // skipped) -- FGV_KEY_OTHER, whose Verify always fails
+    c.key = XK_OTHER;
+  } else {
     unsup();
   }
   // issuerUniqueID / subjectUniqueID: not restated

@@ -342,7 +342,15 @@ def parse_certificate(der):
             raise Unsupported("EC curve")
     elif koid == OID_ED25519:
         key = "undeserializable"  # (a parse or a KeyImport error: undeserializable either way)
-    else:  # (RSA: Go's PKCS#1 key checks are not restated)
+    elif koid == OID_RSA:
+        # RSA can never pass identity.Verify: msp/identities.go:190 passes nil opts and the RSA
+        # verifiers reject them (fabric-lib-go bccsp/sw/rsa.go:48-61).  Whether Go's
+        # PKCS#1 key checks accept the key (a deserialized identity that never verifies) or not
+        # (DeserializeIdentity fails) the outcome is the same on every path that uses it --
+        # creator: BAD_CREATOR_SIGNATURE; endorsement / orderer signature: skipped, before any
+        # de-duplication (common/policies/policy.go:363-395) -- so those checks are not restated.
+        key = "other"
+    else:
         raise Unsupported("public key algorithm")
     if t.peek(0x81) or t.peek(0x82):
         raise Unsupported("issuer/subject unique id")

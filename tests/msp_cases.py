@@ -65,6 +65,14 @@ def fork_hazard_variants(pem):
     ]
 
 
+def rsa_spki(n, e):
+    """SubjectPublicKeyInfo{rsaEncryption, NULL, BIT STRING RSAPublicKey{modulus, exponent}}"""
+    def sint(v):
+        b = v.to_bytes((v.bit_length() + 8) // 8 or 1, "big", signed=True)
+        return G.tlv(0x02, b)
+    return G.seq(G.seq(G.oid("2a864886f70d010101"), G.tlv(0x05, b"")), G.tlv(0x03, b"\x00" + G.seq(sint(n), sint(e))))
+
+
 def synthetic():
     """-> (config bytes, [(label, serialized, status, valid, roles)]) -- valid / roles only for OK"""
     ca1, ca2, ca3, ca4, ca5 = Key(77, 1), Key(77, 2), Key(77, 3), Key(77, 4), Key(77, 5)
@@ -78,7 +86,7 @@ def synthetic():
     i1 = G.ca_cert(int1, "int1.org1", issuer_key=ca4, issuer_cn="ca4.org1", serial=11)
     i2 = G.ca_cert(int2, "int2.org1", issuer_key=ca5, issuer_cn="ca5.org1", serial=12)
     r2 = G.ca_cert(ca2, "ca2.org2", org="Org2", with_ski=False)  # Org2MSP: a root without SKI
-    k = [Key(77, 100 + i) for i in range(40)]
+    k = [Key(77, 100 + i) for i in range(42)]
 
     def leaf(i, ous, issuer_key=ca1, issuer=n1, **kw):
         return G.cert(k[i], issuer_key, G.name("leaf%d" % i, ous=ous), issuer, serial=1000 + i, **kw)
@@ -132,6 +140,11 @@ def synthetic():
     add("basic_constraints_trailing_element",
         leaf(38, ["peer"], extensions=[G.ext("551d13", G.seq(G.tlv(0x01, b"\x00"), G.tlv(0x04, b"x")))]), UNSUP)
     add("no_begin_anywhere", b"-----END CERTIFICATE-----\n", FAILED)
+    # RSA leaves (never pass identity.Verify): registered as keys that never verify,
+    # with their validity and roles -- a 2048-bit modulus, and a key Go's PKCS#1 checks would
+    # reject (negative modulus): the same verdict on every path
+    add("rsa_leaf", leaf(39, ["peer"], spki=rsa_spki((1 << 2047) + 12345, 65537)), OK, True, _roles(MEMBER, PEER))
+    add("rsa_leaf_bad_modulus", leaf(40, ["client"], spki=rsa_spki(-5, 3)), OK, True, _roles(MEMBER, CLIENT))
     out.append(("repeat", out[0][1], REPEAT, None, None))  # the same bytes again in one call
     out.append(("msp_root_without_ski", serialized_identity("Org2MSP", leaf(24, ["peer"], issuer_key=ca2,
                                                                            issuer=G.name("ca2.org2", "Org2"))),
