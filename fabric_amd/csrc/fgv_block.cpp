@@ -1924,6 +1924,9 @@ static int emit_prefix(fgv_ctx *c, fgv_block_state *S, BdSet &B, hipStream_t st)
     HIP_TRY(hipGetLastError());
     if (tim) HIP_TRY(hipEventRecord(c->kev[7], st));
     dn = misc + 10;
+  } else if (tim) {  // (no k_bd_emit: an empty interval, so fgv_last_kernel_times reads recorded events)
+    HIP_TRY(hipEventRecord(c->kev[6], st));
+    HIP_TRY(hipEventRecord(c->kev[7], st));
   }
   int rc = fgv_verify_prefix_dev(c, st, cap, dn, sp, B.vst.as<uint8_t>(), B.vr, B.vs, B.vw, B.vscr);
   if (rc) return rc;
@@ -2425,6 +2428,7 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
     c->t_kern[8] = tim ? el(c->kev[8], c->kev[9]) : 0.0;               // k_bd_fold
     c->t_kern[9] = tim ? el(B.ev[0], c->kev[9]) : 0.0;                 // the batch, head upload to fold
     c->t_sha = std::max(c->t_kern[0], el(B.ev[3], B.ev[2]));
+    (void)hipGetLastError();  // (an interval whose events this call did not record is 0, not a sticky error)
   }
   const uint32_t *hm = B.misc.as<uint32_t>();
   uint64_t nb, np;

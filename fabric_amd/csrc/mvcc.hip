@@ -1074,7 +1074,7 @@ __device__ __forceinline__ void st_set(uint8_t *st, uint32_t g, uint8_t s) {
 // dependent outcomes (a read of a key an earlier block's transaction wrote, whose own validity
 // waits on an earlier one ...) resolves inside one launch instead of one launch per link.  The
 // loop is bounded: whatever is still undecided is counted and the next round continues it.
-#define MVB_SPIN 96u
+#define MVB_SPIN 1u
 __global__ __launch_bounds__(64) void k_mvb_round(uint32_t ntx, uint32_t r, const MvTxInfo *__restrict__ info,
                                                   const MvRec *__restrict__ reads, const MvRec *__restrict__ writes,
                                                   const uint32_t *__restrict__ rslot, const uint8_t *__restrict__ rstat,

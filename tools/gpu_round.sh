@@ -119,6 +119,14 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d $O/st -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $O/st.json 2> $O/st.err \
         || { echo trace failed; tail -20 $O/st.err; exit 1; }
       echo trace ok ;;
+    mvcctrace)
+      timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --hip-trace --stats -d $O/mt -o run -- python bench.py --workload mvcc --steps 40 --warmup 2 --mvcc-single-steps 0 > $O/mt.json 2> $O/mt.err \
+        || { echo mvcctrace failed; tail -20 $O/mt.err; exit 1; }
+      echo mvcctrace ok ;;
+    pipetrace)
+      timeout -k 10 400 rocprofv3 --output-format csv --kernel-trace --hip-trace --stats -d $O/pt -o run -- python bench.py --workload pipeline --steps 6 --warmup 2 --pipeline-latency-blocks 4 > $O/pt.json 2> $O/pt.err \
+        || { echo pipetrace failed; tail -20 $O/pt.err; exit 1; }
+      echo pipetrace ok ;;
     apitrace)
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --hip-trace -d $O/at -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $O/at.json 2> $O/at.err \
         || { echo apitrace failed; tail -20 $O/at.err; exit 1; }
