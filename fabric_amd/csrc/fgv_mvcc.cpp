@@ -1612,12 +1612,12 @@ static int mvcc_batch(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
                      M->mbrstat.as<uint8_t>(), d_c);
   hipLaunchKernelGGL(k_mvb_find, grid_stride(2 * rcap + total), dim3(256), 0, s, N, base, d_r, d_w, d_b, epoch,
                      S.wslot.as<uint32_t>(), S.rslot.as<uint32_t>(), d_info, S.st.as<uint8_t>(), d_c);
-  // rounds: one more than the last batch needed, at least 4 (FGV_MVB_ROUNDS fixes the count)
+  // rounds: two more than the last batch needed, at least 6 (FGV_MVB_ROUNDS fixes the count)
   static const uint32_t fixed_rounds = [] {
     const char *e = getenv("FGV_MVB_ROUNDS");
     return e ? (uint32_t)std::max(1, std::min(64, atoi(e))) : 0u;
   }();
-  const uint32_t R = fixed_rounds ? fixed_rounds : std::min<uint32_t>(16, std::max<uint32_t>(4, M->mb_rounds + 1));
+  const uint32_t R = fixed_rounds ? fixed_rounds : std::min<uint32_t>(32, std::max<uint32_t>(6, M->mb_rounds + 2));
   for (uint32_t r = 1; r <= R; r++)
     hipLaunchKernelGGL(k_mvb_round, dim3((N + 63) / 64), dim3(64), 0, s, N, r, d_info, d_r, d_w,
                        S.rslot.as<uint32_t>(), M->mbrstat.as<uint8_t>(), d_b, S.st.as<uint8_t>(), d_bf, d_bn, NB, d_c);
@@ -1696,7 +1696,18 @@ static int mvcc_blocks(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const
         const char *e = getenv("FGV_MVCC_BATCH");
         return !e || atoi(e) != 0;
       }();
-      if (batch && end - done >= 2) {
+      // the batch pass for runs of small blocks, where the per-block chain is launch-bound: its
+      // fixpoint rounds grow with the batch's longest chain of dependent outcomes, which large
+      // blocks over a dense key space make long (C3, 10 x 10k-tx blocks: 20+ rounds, measured
+      // 47 M tx/s through the pass against 63 M chained) -- FGV_MVCC_BATCH_TX = the largest
+      // block the pass takes (default 4096 transactions)
+      static const size_t batch_tx = [] {
+        const char *e = getenv("FGV_MVCC_BATCH_TX");
+        return e ? (size_t)atol(e) : (size_t)4096;
+      }();
+      size_t big = 0;
+      for (size_t k = done; k < end; k++) big = std::max(big, ntx[k]);
+      if (batch && end - done >= 2 && big <= batch_tx) {
         const int rc = mvcc_batch(c, M, done, end, blocks, lens, d_blocks, block_nums, flags, ntx, commit, &stop,
                                   n_next, next_blocks, next_lens);
         n_next = 0;  // (the next batch is being walked)

@@ -1057,23 +1057,19 @@ __global__ __launch_bounds__(256) void k_mvb_find(uint32_t ntx, const uint8_t *_
   }
 }
 
-// Transaction states shared across the launch's workgroups (and XCDs): device-scope atomics on
-// the 32-bit word holding the byte (a state goes from UNDEC = 0 to VALID or INVALID once)
-__device__ __forceinline__ uint8_t st_ld(const uint8_t *st, uint32_t g) {
-  const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t *>(st) + (g >> 2), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-  return (uint8_t)(w >> (8 * (g & 3u)));
-}
-__device__ __forceinline__ void st_set(uint8_t *st, uint32_t g, uint8_t s) {
-  __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(st) + (g >> 2), (uint32_t)s << (8 * (g & 3u)), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_AGENT);
-}
+// Transaction states read by other transactions of the same launch: a plain load may see a state
+// decided in this round or not yet (other workgroups, other XCDs' L2s) -- either is correct, the
+// rule only ever acts on decided states; an undecided view waits for the next round
+__device__ __forceinline__ uint8_t st_ld(const uint8_t *st, uint32_t g) { return st[g]; }
+__device__ __forceinline__ void st_set(uint8_t *st, uint32_t g, uint8_t s) { st[g] = s; }
 
-// fixpoint round r (1-based).  Within a round an undecided transaction re-evaluates up to
-// MVB_SPIN times, reading the other transactions' states as they are published, so a chain of
-// dependent outcomes (a read of a key an earlier block's transaction wrote, whose own validity
-// waits on an earlier one ...) resolves inside one launch instead of one launch per link.  The
-// loop is bounded: whatever is still undecided is counted and the next round continues it.
+// fixpoint round r (1-based): every undecided transaction evaluates its reads once.  Rounds grow
+// with the longest chain of dependent outcomes in the batch -- a read of a key an earlier
+// transaction of the batch wrote, whose own validity waits on an earlier one ... -- which is
+// short for batches of small blocks (the pass's purpose) and long for a few large blocks over a
+// dense key space (C3: ~20 links); the host chooses the per-block chain for those.
+// (Re-evaluating inside one launch while other workgroups publish -- device-scope atomic state
+// loads, up to 96 passes -- measured slower on MI355X: C3 30.5 M tx/s against 47.3 M, r5e/r5f.)
 #define MVB_SPIN 1u
 __global__ __launch_bounds__(64) void k_mvb_round(uint32_t ntx, uint32_t r, const MvTxInfo *__restrict__ info,
                                                   const MvRec *__restrict__ reads, const MvRec *__restrict__ writes,
