@@ -28,7 +28,8 @@ EXPORTED = [
     "fgv_statedb_init", "fgv_statedb_load", "fgv_statedb_apply", "fgv_statedb_stats", "fgv_mvcc_validate_block", "fgv_mvcc_validate_blocks", "fgv_mvcc_validate_blocks_next", "fgv_mvcc_last_stats",
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash", "fgv_commit_hashes",
     "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
-    "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d",
+    "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d", "fgv_dev_alloc", "fgv_dev_upload",
+    "fgv_dev_free",
     "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead", "fgv_blocks_verify_signed",
     "fgv_validate_blocks_pipelined", "fgv_set_timing",
     "fgv_group_init", "fgv_group_destroy", "fgv_group_size", "fgv_group_ctx", "fgv_group_validate_blocks",
@@ -95,10 +96,11 @@ def load():
     touches first (a second copy makes torch report "No HIP GPUs are available")."""
     global _L
     if _L is None:
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        if not os.environ.get("FGV_NO_TORCH"):  # (the torch-free harness: tools/bench_notorch.py)
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         if not os.path.exists(LIB_PATH):
             raise FgvError(f"{LIB_PATH} not built -- run `make` (or __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)
@@ -184,6 +186,9 @@ def load():
         L.fgv_commit_hashes.argtypes = [sz, vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint]
         L.fgv_host_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
         L.fgv_host_free.argtypes = [vp, vp]
+        L.fgv_dev_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
+        L.fgv_dev_upload.argtypes = [vp, vp, vp, sz]
+        L.fgv_dev_free.argtypes = [vp, vp]
         L.fgv_last_h2d.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.fgv_msp_resolve.argtypes = [vp, sz, vp, vp, vp]
         L.fgv_msp_resolve_blocks.argtypes = [vp, sz, vp, vp, ctypes.POINTER(sz)]
@@ -468,6 +473,20 @@ class Engine:
     def host_alloc(self, nbytes):
         """fgv_host_alloc: page-locked host memory as a PinnedBuffer (uint8 array in .a)"""
         return PinnedBuffer(self, nbytes)
+
+    def dev_alloc(self, nbytes):
+        """fgv_dev_alloc: HBM of the context's device (an int address); free with dev_free"""
+        p = ctypes.c_void_p()
+        _check(self._L.fgv_dev_alloc(self._h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def dev_upload(self, dst, data: bytes, offset=0):
+        """fgv_dev_upload: host bytes -> HBM at dst + offset (synchronous)"""
+        buf = np.frombuffer(data, dtype=np.uint8)
+        _check(self._L.fgv_dev_upload(self._h, dst + offset, buf.ctypes.data, buf.size))
+
+    def dev_free(self, p):
+        _check(self._L.fgv_dev_free(self._h, p))
 
     def last_h2d(self):
         """fgv_last_h2d: (bytes the last call copied itself, blocks found prefetched)"""

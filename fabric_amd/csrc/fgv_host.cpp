@@ -1868,6 +1868,31 @@ int fgv_host_alloc(fgv_ctx *c, size_t bytes, void **out) {
   return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? FGV_OK : FGV_ENOMEM;
 }
 
+int fgv_dev_alloc(fgv_ctx *c, size_t bytes, void **out) {
+  if (!c || !out) return FGV_EINVAL;
+  *out = nullptr;
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  return hipMalloc(out, bytes ? bytes : 1) == hipSuccess ? FGV_OK : FGV_ENOMEM;
+}
+
+int fgv_dev_upload(fgv_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c || (bytes && (!dst || !src))) return FGV_EINVAL;
+  if (!bytes) return FGV_OK;
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? FGV_OK : FGV_EDEVICE;
+}
+
+int fgv_dev_free(fgv_ctx *c, void *p) {
+  if (!c) return FGV_EINVAL;
+  if (!p) return FGV_OK;
+  {  // (kernels of this context may still read it)
+    std::lock_guard<std::mutex> g(c->mu);
+    for (hipStream_t x : {c->stream, c->stream2, c->stream3, c->streamF, c->copy_stream, c->streamV})
+      if (x) hipStreamSynchronize(x);
+  }
+  return hipFree(p) == hipSuccess ? FGV_OK : FGV_EINVAL;
+}
+
 int fgv_host_free(fgv_ctx *c, void *p) {
   if (!c) return FGV_EINVAL;
   if (!p) return FGV_OK;

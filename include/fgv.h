@@ -477,6 +477,13 @@ int fgv_set_timing(fgv_ctx *ctx, int on);
  * itself, and blocks it found already copied by the previous call's prefetch. */
 int fgv_host_alloc(fgv_ctx *ctx, size_t bytes, void **out);
 int fgv_host_free(fgv_ctx *ctx, void *p);
+/* HBM of the context's device for blocks a caller keeps resident (the d_blocks of the validation
+ * calls) -- a peer without another GPU runtime (a Go peer through cgo) allocates and fills it
+ * through the engine: fgv_dev_alloc (hipMalloc), fgv_dev_upload (a synchronous copy from host
+ * memory at `dst`), fgv_dev_free (waits for the context's streams first). */
+int fgv_dev_alloc(fgv_ctx *ctx, size_t bytes, void **out);
+int fgv_dev_upload(fgv_ctx *ctx, void *dst, const void *src, size_t bytes);
+int fgv_dev_free(fgv_ctx *ctx, void *p);
 int fgv_last_h2d(fgv_ctx *ctx, uint64_t *copied_bytes, uint64_t *prefetched_blocks);
 int fgv_finalize_flags_dev(fgv_ctx *ctx, size_t nblocks, const size_t *ntx, uint32_t world,
                            size_t rows_per_rank, const void *d_gathered, uint8_t *flags);

@@ -14,6 +14,7 @@
 #   churn            C2 with every creator a distinct identity (the cold-key path)
 #   sigchurn         C4 with every item its own key (registered cold)
 #   churntrace       rocprofv3 kernel + HIP API trace of a short churn run
+#   notorch | notorch2   the C2 line through the C ABI alone (no torch), one / two contexts
 #   pipeline         the end-to-end commit pipeline (committer -> MVCC -> commit hash)
 #   mvcc | sig | c5 | sbe   the other workloads (tools/bench_sbe.py for sbe)
 #   mvccpmc          FETCH_SIZE / WRITE_SIZE passes of the mvcc workload
@@ -119,6 +120,14 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d $O/st -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $O/st.json 2> $O/st.err \
         || { echo trace failed; tail -20 $O/st.err; exit 1; }
       echo trace ok ;;
+    notorch)
+      timeout -k 10 400 python -u tools/bench_notorch.py > $O/notorch.json 2> $O/notorch.err \
+        || { echo notorch failed; tail -20 $O/notorch.err; exit 1; }
+      show $O/notorch.json notorch value ms_per_step parity_vs_labels torch_loaded ;;
+    notorch2)
+      timeout -k 10 400 python -u tools/bench_notorch.py --contexts 2 > $O/notorch2.json 2> $O/notorch2.err \
+        || { echo notorch2 failed; tail -20 $O/notorch2.err; exit 1; }
+      show $O/notorch2.json notorch2 value ms_per_step per_context_ms_per_step parity_vs_labels ;;
     mvcctrace)
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --hip-trace --stats -d $O/mt -o run -- python bench.py --workload mvcc --steps 40 --warmup 2 --mvcc-single-steps 0 > $O/mt.json 2> $O/mt.err \
         || { echo mvcctrace failed; tail -20 $O/mt.err; exit 1; }
