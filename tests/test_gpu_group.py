@@ -134,3 +134,31 @@ def test_group_verify_msgs_c4_share():
     one.close()
     assert (got == single).all()
     assert ((got == 0) == pool["expect_valid"][idx]).all()
+
+
+def test_group_verify_msgs_c4_whole_batch():
+    """the whole C4 batch -- 1,048,576 identity.Verify items of 1.85 KB messages
+    (a 16,384-item pool with the injected tamper / high-S / bad-DER / trailing-bytes mix, repeated)
+    -- through fgv_group_p256_verify_msgs over 8 device contexts on the box's one GPU: every
+    status is the generator's expectation (the size-independent property at full size; the
+    131,072-item share above equals one context bit for bit)"""
+    import numpy as np
+    from fabric_amd._lib import pack
+    from fabric_amd.synth.workloads import sig_pool
+    n, uniq = 1 << 20, 16384
+    pool = sig_pool(uniq, seed=1002)
+    idx = np.arange(n) % uniq
+    keys = np.frombuffer(b"".join(pool["keys"][pool["key_index"][i]].pub for i in range(uniq)), np.uint8).reshape(-1, 64)[idx]
+    msgs = np.ascontiguousarray(pool["msgs"][idx])
+    mlen = np.full(n, msgs.shape[1], np.uint32)
+    moff = np.arange(n, dtype=np.uint64) * np.uint64(msgs.shape[1])
+    sa, so, sl = pack([pool["sigs"][i] for i in range(uniq)])
+    so = so[idx]
+    sl = sl[idx]
+    g = _lib.Group([0] * 8, key_slots=64)
+    got = g.verify_msgs(keys, (msgs.reshape(-1), moff, mlen), (sa, so, sl))
+    g.close()
+    exp = pool["expect_valid"][idx]
+    assert got.shape == (n,)
+    bad = np.nonzero((got == 0) != exp)[0]
+    assert len(bad) == 0, (len(bad), bad[:8], got[bad[:8]])
