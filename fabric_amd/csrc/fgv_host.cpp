@@ -453,7 +453,7 @@ void fgv_destroy(fgv_ctx *c) {
     if (x) hipStreamSynchronize(x);
   DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->stage[2], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
                  &c->bd_misc, &c->g_ok, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
-                 &c->kmap, &c->vbt, &c->vbuse, &c->vbpromo, &c->vblist, &c->vbacc, &c->kt_id,
+                 &c->kmap, &c->vbt, &c->vbuse, &c->vbpromo, &c->vblist, &c->vbhand, &c->vbacc, &c->kt_id,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
                  &c->moff, &c->mlen, &c->bj_jobs, &c->bj_sigp, &c->bj_sigl, &c->bj_slot, &c->bj_didx,
                  &c->bj_dig, &c->bj_vst, &c->blk_arena, &c->fz_meta, &c->fz_rowmap, &c->fz_blkof,
@@ -571,9 +571,11 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
     c->vb_pending = false;
     HIP_TRY(hipStreamWaitEvent(st, c->vb_ev[1], 0));
     HIP_TRY(hipMemsetAsync(redo + RD_VB_CNT, 0, 4 * (RD_VB_DONE - RD_VB_CNT + 1), st));
+    HIP_TRY(hipMemsetAsync(redo + RD_VB2_CNT, 0, 4 * (RD_VB2_MUL - RD_VB2_CNT + 1), st));
   }
   c->vb_launched = vb;
-  if (vb && (!c->vblist.ensure((size_t)N * 4) || !c->vbacc.ensure((size_t)N * VB_ACC_WORDS * 4)))
+  if (vb && (!c->vblist.ensure((size_t)N * 4) || !c->vbhand.ensure((size_t)N * 4) ||
+             !c->vbacc.ensure((size_t)N * VB_ACC_WORDS * 4)))
     return FGV_ENOMEM;
   if (tim) HIP_TRY(hipEventRecord(c->ev[2], st));
   hipLaunchKernelGGL(k_inv, dim3(nl / INV_THREADS), dim3(INV_THREADS), 0, st, N, dn, d_status, d_slot,
@@ -596,10 +598,28 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
       const int v = e ? atoi(e) : 2;
       return (uint32_t)(v >= 1 && v <= 4 ? v : 2);
     }();
-    hipLaunchKernelGGL(vb_wgs == 4 ? k_vb_mul_o4 : k_vb_mul, dim3(vb_wgs * c->n_cu), dim3(VB_THREADS), 0, c->streamV, N, d_slot,
-                       c->vbt.as<uint32_t>(), d_r, w.as<uint32_t>(), redo, redo + RD_VB_MUL,
-                       c->vblist.as<uint32_t>(), c->vbacc.as<uint32_t>(),
-                       c->vbuse.as<uint32_t>(), c->promote_uses, c->vbpromo.as<uint32_t>());
+    // FGV_VB28=0: the exact radix-2^32 kernel alone (A/B); by default k_vb_mul28 (radix 2^28,
+    // incomplete formulas) and the exact kernel over its hand-over list only (empty for honest
+    // inputs: it returns at once)
+    static const bool vb28 = [] {
+      const char *e = getenv("FGV_VB28");
+      return !e || atoi(e) != 0;
+    }();
+    if (vb28) {
+      hipLaunchKernelGGL(k_vb_mul28, dim3(vb_wgs * c->n_cu), dim3(VB_THREADS), 0, c->streamV, N, d_slot,
+                         c->vbt.as<uint32_t>(), d_r, w.as<uint32_t>(), redo, c->vblist.as<uint32_t>(),
+                         c->vbacc.as<uint32_t>(), c->vbuse.as<uint32_t>(), c->promote_uses,
+                         c->vbpromo.as<uint32_t>(), c->vbhand.as<uint32_t>());
+      hipLaunchKernelGGL(k_vb_mul, dim3(VB_HAND_WGS), dim3(VB_THREADS), 0, c->streamV, N, d_slot, c->vbt.as<uint32_t>(),
+                         d_r, w.as<uint32_t>(), redo + (RD_VB2_CNT - RD_VB_CNT), redo + RD_VB2_MUL,
+                         c->vblist.as<uint32_t>(), c->vbacc.as<uint32_t>(), (uint32_t *)nullptr, 0u,
+                         c->vbpromo.as<uint32_t>(), c->vbhand.as<uint32_t>());
+    } else {
+      hipLaunchKernelGGL(vb_wgs == 4 ? k_vb_mul_o4 : k_vb_mul, dim3(vb_wgs * c->n_cu), dim3(VB_THREADS), 0, c->streamV,
+                         N, d_slot, c->vbt.as<uint32_t>(), d_r, w.as<uint32_t>(), redo, redo + RD_VB_MUL,
+                         c->vblist.as<uint32_t>(), c->vbacc.as<uint32_t>(), c->vbuse.as<uint32_t>(),
+                         c->promote_uses, c->vbpromo.as<uint32_t>(), (const uint32_t *)nullptr);
+    }
     HIP_TRY(hipGetLastError());
     if (tim) HIP_TRY(hipEventRecord(c->vb_t[1], c->streamV));
     HIP_TRY(hipEventRecord(c->vb_ev[1], c->streamV));

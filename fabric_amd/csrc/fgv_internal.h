@@ -127,7 +127,7 @@ struct fgv_ctx {
   std::vector<uint32_t> kmap_h;                 // host mirror of kmap
   std::vector<uint32_t> comb_owner;             // comb slot -> id (KEY_NONE: free)
   std::vector<uint32_t> comb_free;              // free comb slots (popped from the back)
-  DevBuf kmap, vbt, vbuse, vbpromo, vblist, vbacc, kt_id;
+  DevBuf kmap, vbt, vbuse, vbpromo, vblist, vbhand, vbacc, kt_id;
   uint32_t vbt_keys = 0;           // key ids vbt holds rows for (grown by doubling, up to key_ids)
   uint32_t vb_last_items = 0;      // the last read-back batch's variable-base items (k_vb_fin's grid)
   HostBuf h_promo, h_kid;       // the promotion queue read back (k_vb_mul -> streamV copy)

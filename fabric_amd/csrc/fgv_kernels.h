@@ -69,6 +69,9 @@ __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw 
 #define RD_VB_MUL 4
 #define RD_VB_FIN 5
 #define RD_VB_DONE 6
+#define RD_VB2_CNT 9    // k_vb_mul28's hand-over list: items for the exact k_vb_mul
+#define RD_VB2_MUL 10   // the exact hand-over pass's work counter
+#define VB_HAND_WGS 16  // the exact hand-over pass's grid (empty for honest inputs)
 #define RD_FIN_DONE 8     // finished k_fin_dups workgroups (the last one copies the counters out)
 #define VB_FIN_WGS 32        // k_vb_fin workgroups (256 threads)
 #define VB_BACKLOG_CAP 65536u  // host: promotion ids kept while the comb cache is full
@@ -77,11 +80,14 @@ __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw 
 __global__ void k_keyprep(const uint32_t *qxy, const uint32_t *ids, uint32_t nkeys, uint32_t *vbt, uint8_t *key_ok);
 __global__ void k_kmap_set(const uint32_t *ids, const uint32_t *slots, uint32_t n, uint32_t *kmap);
 __global__ void k_vb_mul(uint32_t n, const uint32_t *key_slot, const uint32_t *vbt, const uint32_t *r_limbs,
-                         const uint32_t *w_in, const uint32_t *ctr, uint32_t *take, const uint32_t *list,
-                         uint32_t *acc, uint32_t *uses, uint32_t promote, uint32_t *promo);
+                         const uint32_t *w_in, const uint32_t *ctr, uint32_t *take, const uint32_t *list, uint32_t *acc,
+                         uint32_t *uses, uint32_t promote, uint32_t *promo, const uint32_t *remap);
 __global__ void k_vb_mul_o4(uint32_t n, const uint32_t *key_slot, const uint32_t *vbt, const uint32_t *r_limbs,
                             const uint32_t *w_in, const uint32_t *ctr, uint32_t *take, const uint32_t *list,
-                            uint32_t *acc, uint32_t *uses, uint32_t promote, uint32_t *promo);
+                            uint32_t *acc, uint32_t *uses, uint32_t promote, uint32_t *promo, const uint32_t *remap);
+__global__ void k_vb_mul28(uint32_t n, const uint32_t *key_slot, const uint32_t *vbt, const uint32_t *r_limbs,
+                           const uint32_t *w_in, uint32_t *ctr, const uint32_t *list, uint32_t *acc, uint32_t *uses,
+                           uint32_t promote, uint32_t *promo, uint32_t *hand);
 __global__ void k_vb_fin(uint32_t n, uint8_t *status, const apoint_raw *gtab28, const int8_t *digits,
                          const uint32_t *r_limbs, uint32_t *ctr, const uint32_t *list, const uint32_t *acc);
 __global__ void k_gtab(apoint_raw *tables28, jpoint_raw *scratch, uint32_t w);

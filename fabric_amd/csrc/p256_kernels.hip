@@ -785,8 +785,8 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
 // ---------------------------------------------------------------- keys without a comb
 // k_keyprep: new key ids -> on-curve bit (k_inv reports 5 for a key off the curve, before the
 // range checks, as ecdsa.Verify does) and the variable-base kernel's per-key table
-// vbt[id][s][d-1] = d * Q_s, Q_s = 2^(32 s) * Q, s < VB_LANES, d = 1..VB_TAB (affine Montgomery-256,
-// 7.5 KB per key).  One thread per (key, slice): 32 s doublings to Q_s, 14 complete additions,
+// vbt[id][s][d-1] = d * Q_s, Q_s = 2^(32 s) * Q, s < VB_LANES, d = 1..VB_TAB (affine, Montgomery-280
+// form as the comb tables, 7.5 KB per key).  One thread per (key, slice): 32 s doublings to Q_s, 14 complete additions,
 // one inversion for the slice's 15 Z's (prefix products).  qxy: [nkeys][16] plain little-endian
 // limbs (x then y).
 __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy, const uint32_t *__restrict__ ids,
@@ -842,6 +842,10 @@ __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy
     fe_mul(z3, z2, zinv);
     fe_mul(ax, T[d].x, z2);
     fe_mul(ay, T[d].y, z3);
+    fe c280;  // (stored in the Montgomery-280 form k_vb_mul28 reads, like the comb tables)
+    fe_load_c(c280, C280_32);
+    fe_mul(ax, ax, c280);
+    fe_mul(ay, ay, c280);
     store_fe(o + 16 * d, ax);
     store_fe(o + 16 * d + 8, ay);
   }
@@ -884,21 +888,26 @@ FGV_DEV void load_jp(jpoint &p, const uint32_t *s) {
 // ~330 field multiplications.  uses[id] counts the key's variable-base verifies;
 // the one that reaches `promote` queues the id (promo[0] count, ids from promo[2]) for a comb build
 // by the host; promo[1] = the batch's variable-base items.
+// remap (the exact hand-over of k_vb_mul28): ctr[RD_VB_CNT] counts the remap entries, each the
+// list index of an item k_vb_mul28 could not finish; no use counting then (uses == nullptr)
 FGV_DEV void vb_mul_body(uint32_t n, const uint32_t *__restrict__ key_slot, const uint32_t *__restrict__ vbt,
                          const uint32_t *__restrict__ r_limbs, const uint32_t *__restrict__ w_in,
                          const uint32_t *__restrict__ ctr, uint32_t *__restrict__ take,
                          const uint32_t *__restrict__ list, uint32_t *__restrict__ acc, uint32_t *__restrict__ uses,
-                         uint32_t promote, uint32_t *__restrict__ promo) {
+                         uint32_t promote, uint32_t *__restrict__ promo, const uint32_t *__restrict__ remap) {
   __builtin_amdgcn_s_setprio(2);
   const uint32_t cnt = ctr[RD_VB_CNT];
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&promo[1], cnt);  // (statistics: fgv_key_stats)
+  if (!remap && blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&promo[1], cnt);  // (statistics: fgv_key_stats)
   if (cnt == 0) return;
   const uint32_t lane = __lane_id(), sl = lane % VB_LANES, base = lane - sl;
   constexpr uint32_t PER = 64u / VB_LANES;  // items per wave and round
+  fe c232;  // (the table is Montgomery-280: x 2^280 * 2^232 / 2^256 = x 2^256)
+  fe_load_c(c232, C232_32);
   uint32_t j0;
   while (vb_next(take, cnt, PER, j0)) {
-    const uint32_t j = j0 + lane / VB_LANES;
-    if (j >= cnt) continue;  // (uniform within the lane group: its partners skip too)
+    const uint32_t jr = j0 + lane / VB_LANES;
+    if (jr >= cnt) continue;  // (uniform within the lane group: its partners skip too)
+    const uint32_t j = remap ? remap[jr] : jr;
     const uint32_t i = list[j];
     const uint32_t id = key_slot[i];
     uint32_t r[8], w[8], u2[8];
@@ -925,6 +934,10 @@ FGV_DEV void vb_mul_body(uint32_t n, const uint32_t *__restrict__ key_slot, cons
       const uint32_t dn = dg >> 28;  // the next window's digit (0 after the last)
       apoint en;
       if (win > 0 && dn) load_fe(en.x, qt + 16 * (dn - 1)), load_fe(en.y, qt + 16 * (dn - 1) + 8);
+      if (d) {
+        fe_mul(e.x, e.x, c232);
+        fe_mul(e.y, e.y, c232);
+      }
       if (win < 7) {
 #pragma unroll 1
         for (int k = 0; k < 4; k++) {
@@ -955,6 +968,7 @@ FGV_DEV void vb_mul_body(uint32_t n, const uint32_t *__restrict__ key_slot, cons
     }
     if (sl != 0) continue;
     store_jp(acc + (size_t)j * VB_ACC_WORDS, a);
+    if (!uses) continue;
     const uint32_t u = atomicAdd(&uses[id], 1u);
     if (u + 1u == promote) {
       const uint32_t s = atomicAdd(&promo[0], 1u);
@@ -967,13 +981,205 @@ FGV_DEV void vb_mul_body(uint32_t n, const uint32_t *__restrict__ key_slot, cons
   uint32_t n, const uint32_t *__restrict__ key_slot, const uint32_t *__restrict__ vbt,                            \
       const uint32_t *__restrict__ r_limbs, const uint32_t *__restrict__ w_in, const uint32_t *__restrict__ ctr, \
       uint32_t *__restrict__ take, const uint32_t *__restrict__ list, uint32_t *__restrict__ acc,                 \
-      uint32_t *__restrict__ uses, uint32_t promote, uint32_t *__restrict__ promo
+      uint32_t *__restrict__ uses, uint32_t promote, uint32_t *__restrict__ promo, const uint32_t *__restrict__ remap
 __global__ __launch_bounds__(VB_THREADS) void k_vb_mul(VB_MUL_ARGS) {
-  vb_mul_body(n, key_slot, vbt, r_limbs, w_in, ctr, take, list, acc, uses, promote, promo);
+  vb_mul_body(n, key_slot, vbt, r_limbs, w_in, ctr, take, list, acc, uses, promote, promo, remap);
 }
 // the same held to 128 VGPRs (4 waves per SIMD, a few more spills): FGV_VB_WGS=4 (A/B)
 __global__ __launch_bounds__(VB_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_vb_mul_o4(VB_MUL_ARGS) {
-  vb_mul_body(n, key_slot, vbt, r_limbs, w_in, ctr, take, list, acc, uses, promote, promo);
+  vb_mul_body(n, key_slot, vbt, r_limbs, w_in, ctr, take, list, acc, uses, promote, promo, remap);
+}
+
+// ---------------------------------------------------------------- k_vb_mul28 (fast path)
+// The variable-base product u2 * Q in radix-2^28 Montgomery-280 arithmetic (p256_fe28.h), the
+// structure of vb_mul_body: VB_LANES lanes per item, lane s sums u2[s] * Q_s over 8 windows of
+// 4 bits (28 doublings, <= 8 mixed additions from the key's Montgomery-280 slice table), then a
+// 3-level butterfly.  Incomplete formulas, as k_point28: an exceptional addition (a partial sum
+// equal to +-the added point) leaves Z = 0, which stays 0; such an item goes to the hand-over list
+// (redo[RD_VB2_CNT], its list index in `hand`) and the exact k_vb_mul finishes it.  The result is
+// converted to the Montgomery-256 Jacobian form k_vb_fin reads.
+// 8 R mod p and 2^256 mod p (radix 2^28): doubling's 8 beta; Montgomery-280 -> -256
+__constant__ static const uint32_t C8R28[10] = {0x8000000u, 0x0u, 0x0u, 0x0u, 0xffff800u,
+                                                0xfffffffu, 0xfffffffu, 0xf7fffffu, 0x7ffffffu, 0x0u};
+__constant__ static const uint32_t C256_28[10] = {0x1u, 0x0u, 0x0u, 0xffff000u, 0xfffffffu,
+                                                  0xfffffffu, 0xeffffffu, 0xfffffffu, 0x0u, 0x0u};
+
+// a = 2a, dbl-2001-b (a = -3): delta = Z^2, gamma = Y^2, beta = X gamma, alpha = 3 (X - delta)(X + delta),
+// X3 = alpha^2 - 8 beta, Y3 = alpha (4 beta - X3) - 8 gamma^2, Z3 = 2 Y Z.  In: X < 10p, Y, Z < 2p,
+// normalized (madd28's running sum); out: X3 < 6p, Y3 < 2p, Z3 < 2p, normalized.  Z = 0 stays 0.
+FGV_DEV void dbl28(jp28 &a) {
+  f28 delta, gamma, beta, t1, t2, al, a3, x3, b8, b4, t, ng, g8, y2, c;
+  f28_sqr(delta, a.z);              // < 2p
+  f28_sqr(gamma, a.y);              // < 2p
+  f28_mul(beta, a.x, gamma);        // < 2p
+  f28_sub(t1, a.x, delta, C4P28);   // X - delta + 4p < 14p, loose
+  f28_add(t2, a.x, delta);          // < 12p, limbs < 2^29
+  f28_mul(al, t1, t2);              // < 2p
+  f28_add(a3, al, al);
+  f28_add(a3, a3, al);              // 3 alpha < 6p, limbs < 3 * 2^28
+  f28_sqr(x3, a3);                  // < 2p
+  f28_load_c(c, C8R28);
+  f28_mul(b8, beta, c);             // 8 beta mod p, < 2p
+  f28_sub(x3, x3, b8, C4P28);       // < 6p, loose
+  f28_norm(x3);
+  f28_add(b4, beta, beta);
+  f28_add(b4, b4, b4);
+  f28_norm(b4);                     // 4 beta < 8p
+  f28_sub(t, b4, x3, C8P28);        // 4 beta - X3 + 8p < 16p, loose (x3 top limb <= 90 < 125)
+  f28 zero;
+#pragma unroll
+  for (int j = 0; j < 10; j++) zero.v[j] = 0u;
+  f28_sub(ng, zero, gamma, C4P28);  // 4p - gamma, loose
+  f28_add(g8, gamma, gamma);
+  f28_add(g8, g8, g8);
+  f28_norm(g8);                     // 4 gamma < 8p
+  f28_add(g8, g8, g8);
+  f28_norm(g8);                     // 8 gamma < 16p, normalized
+  f28_add(y2, a.y, a.y);            // 2Y, limbs < 2^29
+  f28_mul(a.z, y2, a.z);            // Z3 = 2 Y Z < 2p
+  f28_mul2(a.y, a3, t, ng, g8);     // alpha (4 beta - X3) + (4p - gamma) 8 gamma < 2p
+  a.x = x3;
+}
+
+// normalized value < 2p -> canonical (< p), packed into 8 x 32-bit limbs
+FGV_DEV void f28_to32(uint32_t w[8], const f28 &a) {
+  f28 r;
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {  // r = a - p (with borrow)
+    const int32_t d = (int32_t)a.v[i] - (int32_t)P28[i] + br;
+    br = d >> 28;  // (arithmetic: -1 on borrow)
+    r.v[i] = (uint32_t)d & F28_MASK;
+  }
+  const bool ge = br >= 0;  // a >= p: take a - p
+  uint32_t v[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) v[i] = ge ? r.v[i] : a.v[i];
+  // 10 x 28 bits -> 8 x 32 bits
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int bit = 32 * k, li = bit / 28, sh = bit % 28;
+    uint32_t x = v[li] >> sh;
+    if (li + 1 < 10) x |= v[li + 1] << (28 - sh);
+    if (sh > 24 && li + 2 < 10) x |= v[li + 2] << (56 - sh);
+    w[k] = x;
+  }
+}
+
+__global__ __launch_bounds__(VB_THREADS) void k_vb_mul28(uint32_t n, const uint32_t *__restrict__ key_slot,
+                                                          const uint32_t *__restrict__ vbt,
+                                                          const uint32_t *__restrict__ r_limbs,
+                                                          const uint32_t *__restrict__ w_in,
+                                                          uint32_t *__restrict__ ctr, const uint32_t *__restrict__ list,
+                                                          uint32_t *__restrict__ acc, uint32_t *__restrict__ uses,
+                                                          uint32_t promote, uint32_t *__restrict__ promo,
+                                                          uint32_t *__restrict__ hand) {
+  __builtin_amdgcn_s_setprio(2);
+  const uint32_t cnt = ctr[RD_VB_CNT];
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&promo[1], cnt);  // (statistics: fgv_key_stats)
+  if (cnt == 0) return;
+  const uint32_t lane = __lane_id(), sl = lane % VB_LANES, base = lane - sl;
+  constexpr uint32_t PER = 64u / VB_LANES;
+  uint32_t j0;
+  while (vb_next(ctr + RD_VB_MUL, cnt, PER, j0)) {
+    const uint32_t j = j0 + lane / VB_LANES;
+    if (j >= cnt) continue;  // (uniform within the lane group)
+    const uint32_t i = list[j];
+    const uint32_t id = key_slot[i];
+    uint32_t r[8], w[8], u2[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      r[k] = r_limbs[(size_t)k * n + i];
+      w[k] = w_in[(size_t)k * n + i];
+    }
+    sn_mul(u2, r, w);
+    uint32_t dg = u2[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) dg = sl == (uint32_t)k ? u2[k] : dg;
+    const uint4 *qt = reinterpret_cast<const uint4 *>(vbt + (size_t)id * VBT_WORDS + sl * (VB_TAB * 16));
+    jp28 a;
+    bool inf = true;
+    // the entry of window win-1 is loaded while window win is worked (one gather in flight)
+    uint32_t d = dg >> 28;
+    uint4 n0, n1, n2, n3;
+    if (d) n0 = qt[4 * (d - 1)], n1 = qt[4 * (d - 1) + 1], n2 = qt[4 * (d - 1) + 2], n3 = qt[4 * (d - 1) + 3];
+#pragma unroll 1
+    for (int win = 7; win >= 0; win--) {
+      const uint32_t wx[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+      const uint32_t wy[8] = {n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
+      dg <<= 4;
+      const uint32_t dn = dg >> 28;  // the next window's digit (0 after the last)
+      if (win > 0 && dn) {
+        const uint4 *e = qt + 4 * (dn - 1);
+        n0 = e[0], n1 = e[1], n2 = e[2], n3 = e[3];
+      }
+      if (!inf) {
+        dbl28(a);
+        dbl28(a);
+        dbl28(a);
+        dbl28(a);
+      }
+      if (d) {
+        f28 px, py;
+        f28_from32(px, wx);
+        f28_from32(py, wy);
+        if (inf) {
+          a.x = px;
+          a.y = py;
+          f28_load_c(a.z, ONE28);
+          inf = false;
+        } else {
+          madd28(a, px, py);
+        }
+      }
+      d = dn;
+    }
+    // butterfly over the item's lanes (infinite partial sums skipped)
+#pragma unroll 1
+    for (uint32_t m = 1; m < VB_LANES; m <<= 1) {
+      const int src = (int)(base + (sl ^ m));
+      jp28 o;
+      shfl_f28(o.x, a.x, src);
+      shfl_f28(o.y, a.y, src);
+      shfl_f28(o.z, a.z, src);
+      const bool oinf = __shfl((int)inf, src) != 0;
+      if (!oinf) {
+        if (inf) {
+          a = o;
+          inf = false;
+        } else {
+          add28(a, o);
+        }
+      }
+    }
+    if (sl != 0) continue;
+    const uint32_t u = atomicAdd(&uses[id], 1u);
+    if (u + 1u == promote) {
+      const uint32_t s = atomicAdd(&promo[0], 1u);
+      if (s < VB_PROMO_CAP) atomicExch(&promo[2 + s], id);
+    }
+    if (inf || f28_is_zero(a.z)) {  // an exceptional addition (u2 * Q is never infinity): exact kernel
+      hand[atomicAdd(ctr + RD_VB2_CNT, 1u)] = j;
+      continue;
+    }
+    // Montgomery-280 -> Montgomery-256 Jacobian (k_vb_fin's form), canonical limbs
+    f28 c, x, y, z;
+    f28_load_c(c, C256_28);
+    f28_mul(x, a.x, c);
+    f28_mul(y, a.y, c);
+    f28_mul(z, a.z, c);
+    uint32_t *o = acc + (size_t)j * VB_ACC_WORDS;
+    uint32_t t[8];
+    f28_to32(t, x);
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[k] = t[k];
+    f28_to32(t, y);
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[8 + k] = t[k];
+    f28_to32(t, z);
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[16 + k] = t[k];
+  }
 }
 
 // k_vb_fin: after k_prep -- acc[j] + sum of the 12 generator comb terms of u1 (k_prep's digits),
@@ -1040,5 +1246,7 @@ __global__ __launch_bounds__(256) void k_vb_fin(uint32_t n, uint8_t *__restrict_
     atomicExch(ctr + RD_VB_MUL, 0u);
     atomicExch(ctr + RD_VB_FIN, 0u);
     atomicExch(ctr + RD_VB_DONE, 0u);
+    atomicExch(ctr + RD_VB2_CNT, 0u);
+    atomicExch(ctr + RD_VB2_MUL, 0u);
   }
 }
