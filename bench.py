@@ -474,7 +474,7 @@ def run_block(args, world, rank, local, dev_fn):
                     integ_fut[s + d] = integ_ex.submit(verify_mine, (k + d) % NB)
         bs.validate()
         if world > 1:
-            shard.allgather_device(send, recv)
+            shard.allgather_device(send, recv, eng=eng)
         f = bs.finalize()
         if args.presplit_early and world == 1 and not args.no_presplit:
             # a peer walks a batch's framing once its blocks are delivered, ahead of the call

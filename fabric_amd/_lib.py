@@ -29,7 +29,7 @@ EXPORTED = [
     "fgv_blocks_verify", "fgv_sha256_host", "fgv_set_parse_mode", "fgv_commit_hash", "fgv_commit_hashes",
     "fgv_channel_config", "fgv_msp_declare", "fgv_msp_register_identity", "fgv_chaincode_define2",
     "fgv_collection_define", "fgv_host_alloc", "fgv_host_free", "fgv_last_h2d", "fgv_dev_alloc", "fgv_dev_upload",
-    "fgv_dev_free",
+    "fgv_dev_free", "fgv_stream_wait_external",
     "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead", "fgv_blocks_verify_signed",
     "fgv_validate_blocks_pipelined", "fgv_set_timing",
     "fgv_group_init", "fgv_group_destroy", "fgv_group_size", "fgv_group_ctx", "fgv_group_validate_blocks",
@@ -189,6 +189,7 @@ def load():
         L.fgv_dev_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
         L.fgv_dev_upload.argtypes = [vp, vp, vp, sz]
         L.fgv_dev_free.argtypes = [vp, vp]
+        L.fgv_stream_wait_external.argtypes = [vp, vp]
         L.fgv_last_h2d.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.fgv_msp_resolve.argtypes = [vp, sz, vp, vp, vp]
         L.fgv_msp_resolve_blocks.argtypes = [vp, sz, vp, vp, ctypes.POINTER(sz)]
@@ -484,6 +485,11 @@ class Engine:
         """fgv_dev_upload: host bytes -> HBM at dst + offset (synchronous)"""
         buf = np.frombuffer(data, dtype=np.uint8)
         _check(self._L.fgv_dev_upload(self._h, dst + offset, buf.ctypes.data, buf.size))
+
+    def wait_stream(self, stream_handle):
+        """fgv_stream_wait_external: the engine's next work waits for `stream_handle` (a raw HIP
+        stream, e.g. torch.cuda.current_stream().cuda_stream) -- no host synchronisation"""
+        _check(self._L.fgv_stream_wait_external(self._h, ctypes.c_void_p(stream_handle)))
 
     def dev_free(self, p):
         _check(self._L.fgv_dev_free(self._h, p))

@@ -479,6 +479,7 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->streamF) hipStreamDestroy(c->streamF);
   if (c->streamK) hipStreamSynchronize(c->streamK), hipStreamDestroy(c->streamK);
   if (c->kt_ev) hipEventDestroy(c->kt_ev);
+  if (c->ext_ev) hipEventDestroy(c->ext_ev);
   if (c->streamV) hipStreamDestroy(c->streamV);
   for (auto &e : c->vb_ev)
     if (e) hipEventDestroy(e);
@@ -1886,6 +1887,16 @@ int fgv_host_alloc(fgv_ctx *c, size_t bytes, void **out) {
   *out = nullptr;
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
   return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? FGV_OK : FGV_ENOMEM;
+}
+
+int fgv_stream_wait_external(fgv_ctx *c, void *stream) {
+  if (!c || !stream) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  if (!c->ext_ev) HIP_TRY(hipEventCreateWithFlags(&c->ext_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(c->ext_ev, static_cast<hipStream_t>(stream)));
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->ext_ev, 0));
+  return FGV_OK;
 }
 
 int fgv_dev_alloc(fgv_ctx *c, size_t bytes, void **out) {

@@ -147,6 +147,7 @@ struct fgv_ctx {
   // FGV_PROMOTE_AT = 1 / 2 / 3 (test knob, tests/test_gpu_concurrency.py): promotions build their
   // tables on the main stream and enqueue k_kmap_set after k_inv / before k_point28 / before
   // k_vb_fin of the consuming batch; kmap_defer = ids whose k_kmap_set is still to be enqueued
+  hipEvent_t ext_ev = nullptr;  // fgv_stream_wait_external
   uint32_t promote_at = 0;
   uint32_t kmap_defer = 0;
   uint64_t n_promoted = 0;        // keys promoted to a comb since fgv_init

@@ -81,18 +81,22 @@ def allgather_results(local, ntx, world, device=None, group=None, out=None, plan
     return reorder(g, ntx, world, rows, plan_)
 
 
-def allgather_device(send, recv, group=None):
+def allgather_device(send, recv, group=None, eng=None):
     """All-gather the per-rank device record buffers (rows x 68 each) into `recv`
-    (world*rows x 68, rank-major -- the layout fgv_finalize_flags_dev reads), and wait for it
-    so the engine's own stream may read `recv`.  gloo (CPU rehearsal) gathers through host
-    memory."""
+    (world*rows x 68, rank-major -- the layout fgv_finalize_flags_dev reads).  With `eng` the
+    engine's stream waits for the collective's stream by an event (fgv_stream_wait_external: no
+    host synchronisation; the finalize kernels queue behind it), else the host waits for it.
+    gloo (CPU rehearsal) gathers through host memory."""
     if dist.get_backend(group) == "gloo":
         tmp = torch.empty(recv.shape, dtype=recv.dtype)
         dist.all_gather_into_tensor(tmp, send.cpu(), group=group)
         recv.copy_(tmp)
     else:
         dist.all_gather_into_tensor(recv, send, group=group)
-    torch.cuda.current_stream(recv.device).synchronize()
+    if eng is not None:
+        eng.wait_stream(torch.cuda.current_stream(recv.device).cuda_stream)
+    else:
+        torch.cuda.current_stream(recv.device).synchronize()
 
 
 def reorder(gathered, ntx, world, rows, plan_=None):
