@@ -1890,7 +1890,7 @@ int fgv_host_alloc(fgv_ctx *c, size_t bytes, void **out) {
 }
 
 int fgv_stream_wait_external(fgv_ctx *c, void *stream) {
-  if (!c || !stream) return FGV_EINVAL;
+  if (!c) return FGV_EINVAL;  // (stream == NULL: the device's null stream)
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
   if (!c->ext_ev) HIP_TRY(hipEventCreateWithFlags(&c->ext_ev, hipEventDisableTiming));

@@ -483,7 +483,8 @@ int fgv_host_free(fgv_ctx *ctx, void *p);
  * memory at `dst`), fgv_dev_free (waits for the context's streams first). */
 /* The context's next device work waits for everything queued so far on `stream` (a HIP stream
  * of the context's device, e.g. the caller's RCCL stream after the all-gather of the shard
- * records that fgv_finalize_flags_dev reads) -- an event, no host synchronisation. */
+ * records that fgv_finalize_flags_dev reads; NULL = the null stream) -- an event, no host
+ * synchronisation. */
 int fgv_stream_wait_external(fgv_ctx *ctx, void *stream);
 int fgv_dev_alloc(fgv_ctx *ctx, size_t bytes, void **out);
 int fgv_dev_upload(fgv_ctx *ctx, void *dst, const void *src, size_t bytes);
