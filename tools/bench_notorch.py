@@ -62,8 +62,8 @@ class Channel:
         NB = len(self.blks)
         self.NB = NB
         self.hb = [self.eng.block_batch(self.blks[k], dptrs[k]) for k in range(NB)]
-        self.flags = np.empty(sum(len(bl) for bl in self.labels[0]) * T, dtype=np.uint8)
         B = len(self.blks[0])
+        self.flags = np.empty(B * T, dtype=np.uint8)
         ntx = np.array([T] * B, dtype=np.int64)
         self.steps = [_lib.BlockStep(self.eng, self.hb[k], [0] * B, [T] * B, 0, B * T, ntx, 1, 0, self.flags,
                                      presplit=True, next_batch=self.hb[(k + 1) % NB], fused=True) for k in range(NB)]
