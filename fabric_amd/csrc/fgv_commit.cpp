@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -33,6 +34,8 @@ namespace {
 struct WEnt {
   Span ns, coll, key, value;  // value: the put's value (public) or value hash (hashed)
   uint32_t tx;
+  uint32_t grp;               // (namespace, hashed, collection) group: its rank after sort_groups
+  uint64_t kp;                // the key's first 8 bytes, big-endian, zero-padded (sort prefix)
   bool hashed, del;
 };
 
@@ -42,9 +45,6 @@ inline int span_cmp(const Span &a, const Span &b) {  // std::string / Go sort.St
   return c ? c : (a.n < b.n ? -1 : a.n > b.n ? 1 : 0);
 }
 inline bool span_eq(const Span &a, const Span &b) { return a.n == b.n && (a.n == 0 || memcmp(a.p, b.p, a.n) == 0); }
-inline bool same_key(const WEnt &a, const WEnt &b) {
-  return a.hashed == b.hashed && span_eq(a.key, b.key) && span_eq(a.ns, b.ns) && span_eq(a.coll, b.coll);
-}
 
 inline size_t varint_len(uint64_t v) {
   size_t n = 1;
@@ -78,7 +78,7 @@ inline size_t opv(uint8_t *o, uint64_t n) {
 
 // txmgr.Updates.KVWrite{namespace 1 (on the first write of a namespace), collection 2 (on the
 // first write of a collection), key 3, is_delete 4, value 5, version_bytes 6}, as repeated field 1
-void kvwrite(std::vector<uint8_t> &out, const Span &ns, const Span &coll, const WEnt &w, uint64_t blk) {
+uint8_t *kvwrite(uint8_t *o, const Span &ns, const Span &coll, const WEnt &w, uint64_t blk) {
   uint8_t ver[18];
   size_t vl = opv(ver, blk);
   vl += opv(ver + vl, w.tx);
@@ -89,9 +89,6 @@ void kvwrite(std::vector<uint8_t> &out, const Span &ns, const Span &coll, const 
   if (w.del) m += 2;
   else if (w.value.n) m += field_len(w.value.n);
   m += field_len(vl);
-  const size_t at = out.size();
-  out.resize(at + field_len(m));
-  uint8_t *o = out.data() + at;
   *o++ = (uint8_t)(1 << 3 | 2);
   o = put_varint(o, m);
   if (ns.n) o = put_bytes(o, 1, ns.p, ns.n);
@@ -103,18 +100,105 @@ void kvwrite(std::vector<uint8_t> &out, const Span &ns, const Span &coll, const 
   } else if (w.value.n) {
     o = put_bytes(o, 5, w.value.p, w.value.n);
   }
-  put_bytes(o, 6, ver, vl);
+  return put_bytes(o, 6, ver, vl);
 }
 
 constexpr uint8_t kEmptySha256[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
                                       0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
                                       0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
 
+// KVRWSet / HashedRWSet with the writes captured and the reads and range queries skipped at
+// the wire level: a VALID transaction's read set was decoded by the validation that flagged
+// it, and the update batch holds writes only
+struct VKVWritesOnly {
+  uint32_t nmeta = 0;
+  std::vector<VKVWrite> *writes = nullptr;
+  pbw::Kind kind(uint32_t n) { return (n == 3 || n == 4) ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 4) {
+      nmeta++;
+      return true;
+    }
+    VKVWrite w;
+    if (!pbw::decode(s.p, s.n, w)) return false;
+    writes->push_back(w);
+    return true;
+  }
+};
+struct VHashedWritesOnly {
+  uint32_t nmeta = 0;
+  std::vector<VHashWrite> *writes = nullptr;
+  pbw::Kind kind(uint32_t n) { return (n == 2 || n == 3) ? pbw::K_REP_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t n, Span s) {
+    if (n == 3) {
+      nmeta++;
+      return true;
+    }
+    VHashWrite w;
+    if (!pbw::decode(s.p, s.n, w)) return false;
+    writes->push_back(w);
+    return true;
+  }
+};
+
+// ChaincodeActionPayload.action.proposal_response_payload alone (the endorsements were
+// verified by the validation that flagged the transaction VALID); every occurrence of the
+// action merged in order, the last payload winning, as VCcActionPayload
+struct VEaPrp {
+  Span prp;
+  pbw::Kind kind(uint32_t n) { return n == 1 ? pbw::K_BYTES : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    prp = s;
+    return true;
+  }
+};
+struct VCapPrp {
+  bool has_action = false;
+  VEaPrp action;
+  pbw::Kind kind(uint32_t n) { return n == 2 ? pbw::K_MSG : pbw::K_NONE; }
+  void on_varint(uint32_t, uint64_t) {}
+  bool on_len(uint32_t, Span s) {
+    has_action = true;
+    return pbw::decode(s.p, s.n, action);
+  }
+};
+
+inline uint64_t key_prefix(const Span &k) {
+  uint64_t v = 0;
+  const size_t m = k.n < 8 ? k.n : 8;
+  for (size_t i = 0; i < m; i++) v |= (uint64_t)k.p[i] << (56 - 8 * i);
+  return v;
+}
+
+struct SortRec {
+  uint64_t kp;
+  uint32_t grp, i;
+};
+
+// per-thread scratch reused across blocks (a fresh ~0.5 MB batch buffer per block cost its
+// page faults every call)
 struct TxScratch {
-  std::vector<VKVRead> reads;
   std::vector<VKVWrite> writes;
-  std::vector<VHashRead> hreads;
   std::vector<VHashWrite> hwrites;
+  std::vector<WEnt> w;
+  std::vector<WEnt> grp;  // one representative entry per (namespace, hashed, collection) group
+  std::vector<uint32_t> rank;
+  std::vector<SortRec> ix;
+  std::unique_ptr<uint8_t[]> batch;
+  size_t cap = 0;
+  uint32_t last = UINT32_MAX;
+  uint32_t group_of(const WEnt &e) {
+    if (last < grp.size() && grp[last].hashed == e.hashed && span_eq(grp[last].ns, e.ns) &&
+        span_eq(grp[last].coll, e.coll))
+      return last;
+    for (uint32_t g = 0; g < grp.size(); g++)
+      if (grp[g].hashed == e.hashed && span_eq(grp[g].ns, e.ns) && span_eq(grp[g].coll, e.coll)) return last = g;
+    grp.push_back(e);
+    return last = (uint32_t)(grp.size() - 1);
+  }
 };
 
 // the writes of one VALID transaction (FGV_OK / FGV_EINVAL / FGV_EUNSUPPORTED)
@@ -129,7 +213,7 @@ int add_tx(Span d, uint32_t txi, std::vector<WEnt> &out, TxScratch &x) {
   if (chdr.type == 1) return FGV_OK;  // CONFIG: namespace "" only (core/peer/configtx_processor.go:19-39)
   if (chdr.type != 3) return FGV_EUNSUPPORTED;
   VTransaction tx;
-  VCcActionPayload cap;
+  VCapPrp cap;
   VPrp prp;
   VCcAction cca;
   VTxRwSet rw;
@@ -140,36 +224,37 @@ int add_tx(Span d, uint32_t txi, std::vector<WEnt> &out, TxScratch &x) {
     return FGV_EINVAL;
   const size_t mine = out.size();
   for (const VNsRwSet &ns : rw.ns) {
-    x.reads.clear();
     x.writes.clear();
-    VKVRWSet kv;
-    kv.reads = &x.reads;
+    VKVWritesOnly kv;
     kv.writes = &x.writes;
     if (!pbw::decode(ns.rwset.p, ns.rwset.n, kv)) return FGV_EINVAL;
     if (kv.nmeta) return FGV_EUNSUPPORTED;  // metadata: merged values come from the state DB
     for (const VKVWrite &w : x.writes) {
       const bool del = w.is_delete || w.value.n == 0;  // IsKVWriteDelete (rwset_proto_util.go:366-368)
-      out.push_back(WEnt{ns.ns, Span(), w.key, del ? Span() : w.value, txi, false, del});
+      WEnt e{ns.ns, Span(), w.key, del ? Span() : w.value, txi, 0, key_prefix(w.key), false, del};
+      e.grp = x.group_of(e);
+      out.push_back(e);
     }
     for (const VCollHashed &c : ns.coll) {
-      x.hreads.clear();
       x.hwrites.clear();
-      VHashedRWSet h;
-      h.reads = &x.hreads;
+      VHashedWritesOnly h;
       h.writes = &x.hwrites;
       if (!pbw::decode(c.hashed.p, c.hashed.n, h)) return FGV_EINVAL;
       if (h.nmeta) return FGV_EUNSUPPORTED;
       for (const VHashWrite &w : x.hwrites) {  // IsKVWriteHashDelete (rwset_proto_util.go:370-375)
         const bool del = w.is_delete || w.value_hash.n == 0 ||
                          (w.value_hash.n == 32 && memcmp(w.value_hash.p, kEmptySha256, 32) == 0);
-        out.push_back(WEnt{ns.ns, c.name, w.key, del ? Span() : w.value_hash, txi, true, del});
+        WEnt e{ns.ns, c.name, w.key, del ? Span() : w.value_hash, txi, 0, key_prefix(w.key), true, del};
+        e.grp = x.group_of(e);
+        out.push_back(e);
       }
     }
   }
   // a key written twice by one transaction: txOps flag arithmetic (tx_ops.go:183-191)
   for (size_t a = mine; a < out.size(); a++)
     for (size_t b = a + 1; b < out.size(); b++)
-      if (same_key(out[a], out[b])) return FGV_EUNSUPPORTED;
+      if (out[a].grp == out[b].grp && out[a].kp == out[b].kp && span_eq(out[a].key, out[b].key))
+        return FGV_EUNSUPPORTED;
   return FGV_OK;
 }
 
@@ -181,42 +266,65 @@ static int commit_prefix(const uint8_t *block, size_t len, const uint8_t *flags,
                          fgvsha::Stream &s) {
   VBlock b;
   if (!pbw::decode(block, len, b) || b.data.data.size() != ntx) return FGV_EINVAL;
-  std::vector<WEnt> w;
-  w.reserve(ntx * 4 + 16);
-  TxScratch x;
+  thread_local TxScratch x;
+  std::vector<WEnt> &w = x.w;
+  w.clear();
+  x.grp.clear();
+  x.last = UINT32_MAX;
   for (size_t i = 0; i < ntx; i++) {
     if (flags[i] != 0) continue;
     const int rc = add_tx(b.data.data[i], (uint32_t)i, w, x);
     if (rc) return rc;
   }
-  // (namespace, public < hashed, collection, key, tx): the last of each key's run is its update
-  std::sort(w.begin(), w.end(), [](const WEnt &p, const WEnt &q) {
-    int c = span_cmp(p.ns, q.ns);
-    if (c) return c < 0;
+  // groups in (namespace, public < hashed, collection) order, then each group's keys: the entry
+  // order is (group, key, tx) and the last of each key's run is its update
+  const size_t ng = x.grp.size();
+  std::vector<uint32_t> ord(ng);
+  for (uint32_t g = 0; g < ng; g++) ord[g] = g;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t c) {
+    const WEnt &p = x.grp[a], &q = x.grp[c];
+    int r = span_cmp(p.ns, q.ns);
+    if (r) return r < 0;
     if (p.hashed != q.hashed) return !p.hashed;
-    if ((c = span_cmp(p.coll, q.coll))) return c < 0;
-    if ((c = span_cmp(p.key, q.key))) return c < 0;
-    return p.tx < q.tx;
+    return span_cmp(p.coll, q.coll) < 0;
   });
-  std::vector<uint8_t> batch;
-  size_t est = 0;
+  x.rank.resize(ng);
+  for (uint32_t g = 0; g < ng; g++) x.rank[ord[g]] = g;
+  // sorted as 16-byte (group rank, key prefix, entry) records -- entries are in transaction
+  // order, so the entry index breaks ties as the transaction number would
+  std::vector<SortRec> &ix = x.ix;
+  ix.resize(w.size());
+  for (uint32_t i = 0; i < w.size(); i++) ix[i] = SortRec{w[i].kp, x.rank[w[i].grp], i};
+  std::sort(ix.begin(), ix.end(), [&w](const SortRec &p, const SortRec &q) {
+    if (p.grp != q.grp) return p.grp < q.grp;
+    if (p.kp != q.kp) return p.kp < q.kp;
+    const int c = span_cmp(w[p.i].key, w[q.i].key);
+    return c ? c < 0 : p.i < q.i;
+  });
+  size_t est = 0;  // bound: every entry with its namespace and collection, 48 B of tags and lengths
   for (const WEnt &e : w) est += e.ns.n + e.coll.n + e.key.n + e.value.n + 48;
-  batch.reserve(est + 256);
+  if (est > x.cap) {
+    x.cap = est + est / 4 + 4096;
+    x.batch.reset(new uint8_t[x.cap]);
+  }
+  uint8_t *const b0 = x.batch.get();
+  uint8_t *o = b0;
   const WEnt *prev = nullptr;  // the last update written
-  for (size_t i = 0; i < w.size(); i++) {
-    const WEnt &e = w[i];
-    if (i + 1 < w.size() && same_key(w[i + 1], e)) continue;  // a later transaction writes this key too
+  for (size_t i = 0; i < ix.size(); i++) {
+    const WEnt &e = w[ix[i].i];
+    if (i + 1 < ix.size() && ix[i + 1].grp == ix[i].grp && ix[i + 1].kp == ix[i].kp && span_eq(w[ix[i + 1].i].key, e.key))
+      continue;  // a later transaction writes this key too
     if (e.ns.n == 0) continue;  // channel config: not part of the hash (update_batch_bytes.go:39-44)
     const bool new_ns = !prev || !span_eq(prev->ns, e.ns);
     const bool new_coll = e.hashed && (new_ns || !prev->hashed || !span_eq(prev->coll, e.coll));
-    kvwrite(batch, new_ns ? e.ns : Span(), new_coll ? e.coll : Span(), e, block_num);
+    o = kvwrite(o, new_ns ? e.ns : Span(), new_coll ? e.coll : Span(), e, block_num);
     prev = &e;
   }
   uint8_t pre[10];
   const size_t pl = (size_t)(put_varint(pre, ntx) - pre);
   s.update(pre, pl);
   if (ntx) s.update(flags, ntx);
-  if (!batch.empty()) s.update(batch.data(), batch.size());
+  if (o != b0) s.update(b0, (size_t)(o - b0));
   return FGV_OK;
 }
 
