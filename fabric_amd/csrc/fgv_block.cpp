@@ -174,7 +174,7 @@ struct PreSplit {
   }
   void start() {
     if (!th.joinable()) {
-      pool.reset(new ThreadPool(8));
+      pool.reset(new ThreadPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency()))));
       th = std::thread([this] { worker(); });
     }
     std::lock_guard<std::mutex> lk(mu);

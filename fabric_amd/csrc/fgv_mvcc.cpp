@@ -25,6 +25,7 @@
 #include "../../include/fgv.h"
 #include "blockdev.h"
 #include "fgv_internal.h"
+#include "mvcc_multi.h"
 #include "fgv_visitors.h"
 #include "sha256_host.h"
 
@@ -42,8 +43,9 @@ constexpr size_t kCounterBytes = 256;       // MvCounters, padded (head and tail
 
 // per-block device buffers: the single-block path uses set 0, a batch of consecutive blocks
 // (fgv_mvcc_validate_blocks) rotates through kSets of them, so the extraction of the next blocks
-// runs ahead of the block being checked and committed
-constexpr int kSets = 3;
+// runs ahead of the block being checked and committed (blocks 1 .. kSets-1 of a call in one
+// launch: mvcc_multi.h)
+constexpr int kSets = MVX_MULTI_MAX;
 struct MvSet {
   DevBuf head, info, reads, writes, wslot, rslot, bad, st, pend, tail;
   DevBuf xscr;  // k_mvx_extract's per-tx record scratch
@@ -66,6 +68,7 @@ struct fgv_mvcc_state {
   DevBuf btbl;
   DevBuf dheads;                       // batch path: every block's head (one copy per call)
   hipEvent_t ev_heads = nullptr;       // batch path: the heads' copy is done (second extraction stream)
+  hipEvent_t ev_multi[5] = {};         // batch path: the multi-block extraction groups are done
   MvSet set[kSets];
   DevBuf lrecs, lbytes;                // load / apply staging
   DevBuf qver, qpres, qrange, qout;    // phantom path: lookups and range scans
@@ -91,6 +94,8 @@ void fgv_mvcc_free(fgv_mvcc_state *M) {
   for (auto *b : d) b->release();
   for (auto &S : M->set) S.release();
   if (M->ev_heads) hipEventDestroy(M->ev_heads);
+  for (hipEvent_t &e : M->ev_multi)
+    if (e) hipEventDestroy(e);
   HostBuf *h[] = {&M->hhead, &M->htail, &M->bhead, &M->btail, &M->mbhead, &M->mbtail};
   for (auto *b : h) b->release();
   delete M;
@@ -1353,6 +1358,20 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   const size_t nxs = nxs_env == 2 ? 2 : 1;
   const hipStream_t xs[2] = {sx, c->stream3};
   if (!M->ev_heads) HIP_TRY(hipEventCreateWithFlags(&M->ev_heads, hipEventDisableTiming));
+  for (hipEvent_t &e : M->ev_multi)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // FGV_MVX_MULTI=0: one extraction launch per block (A/B).  Else blocks 1 .. m_end-1 are walked
+  // on stream3, beside block 0's extraction and chain, in groups of 1, 2, 4, 8 blocks per launch:
+  // a lone block's walk (~0.11 ms for 10k tx, one lane per tx) leaves most of the chip idle, a
+  // group of n walks in ~0.045 n ms, and the doubling groups finish about when the chain reaches
+  // them (MI355X, chained C3, profiles/round5_mvcc_*)
+  static const bool multi_on = [] {
+    const char *e = getenv("FGV_MVX_MULTI");
+    return !e || atoi(e) != 0;
+  }();
+  size_t m_end = 1;        // blocks [1, m_end) extracted by the group launches
+  size_t grp_end[5] = {};  // group g: blocks [grp_end[g-1] or 1, grp_end[g])
+  int ngrp = 0;
   uint8_t *dheads = M->dheads.as<uint8_t>();
   HIP_TRY(hipMemcpyAsync(dheads, M->bhead.p, hoff[1], hipMemcpyHostToDevice, sx));
   size_t nq = 1;  // blocks enqueued: up to the first one that is not a block of ntx transactions
@@ -1366,38 +1385,94 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
     const size_t len = lens[b], T = ntx[b];
     MvSet &S = M->set[k % kSets];
     const size_t et_bytes = (T * 8 + 63) & ~(size_t)63, fl_bytes = (T + 63) & ~(size_t)63;
-    if (k == 1 && !rest_sent) {  // the other heads, once block 0 is on its way
+    if (k >= nq) break;
+    if (k >= 1 && k < m_end) {  // extracted by a group launch: wait for it at its first block
+      for (int g = 0; g < ngrp; g++)
+        if (k == (g ? grp_end[g - 1] : 1)) HIP_TRY(hipStreamWaitEvent(s, M->ev_multi[g], 0));
+    } else {
+    // block k's extraction stream: the set is free once block k-kSets's chain is done
+      hipStream_t sxk = xs[k % nxs];
+      if (k >= (size_t)kSets) HIP_TRY(hipStreamWaitEvent(sxk, S.ev_free, 0));
+      const uint8_t *db = d_blocks ? d_blocks[b] : nullptr;
+      if (!db) HIP_TRY(hipMemcpyAsync(S.blk.p, block, len, hipMemcpyHostToDevice, sxk));
+      uint8_t *dh = dheads + hoff[k];
+      mvx_extract_launch(mvx_tpw(), sxk, (uint32_t)T, db ? db : S.blk.as<uint8_t>(),
+                         reinterpret_cast<const uint32_t *>(dh), dh + et_bytes, S.info.as<MvTxInfo>(),
+                         S.reads.as<MvRec>(), S.writes.as<MvRec>(),
+                         reinterpret_cast<MvCounters *>(dh + et_bytes + fl_bytes), touch, S.xscr.as<MvRec>(),
+                         S.bad.as<uint8_t>());
+      HIP_TRY(hipEventRecord(S.ev_x, sxk));
+      // main stream: block k's chain
+      HIP_TRY(hipStreamWaitEvent(s, S.ev_x, 0));
+    }
+    if (k == 0 && !rest_sent) {  // the other heads, once block 0's extraction is on its way
       fgv_parallel_run(c->blk, nb - 1, [&](size_t j) { fill(j + 1); });
       while (nq < nb && walked[nq]) nq++;
-      if (nq > 1) HIP_TRY(hipMemcpyAsync(dheads + hoff[1], M->bhead.as<uint8_t>() + hoff[1], hoff[nq] - hoff[1],
-                                         hipMemcpyHostToDevice, sx));
-      if (nxs > 1) {  // the second extraction stream starts after the heads' copy
-        HIP_TRY(hipEventRecord(M->ev_heads, sx));
-        HIP_TRY(hipStreamWaitEvent(xs[1], M->ev_heads, 0));
+      const bool multi = multi_on && nq > 2;
+      if (nq > 1) {  // the other heads: on stream3 when the groups start there, else behind block 0
+        hipStream_t hs = multi ? xs[1] : sx;
+        if (multi) HIP_TRY(hipStreamWaitEvent(hs, c->ev[0], 0));
+        HIP_TRY(hipMemcpyAsync(dheads + hoff[1], M->bhead.as<uint8_t>() + hoff[1], hoff[nq] - hoff[1],
+                               hipMemcpyHostToDevice, hs));
+        if (nxs > 1 || multi) {  // the other extraction stream starts after the heads' copy
+          HIP_TRY(hipEventRecord(M->ev_heads, hs));
+          HIP_TRY(hipStreamWaitEvent(multi ? sx : xs[1], M->ev_heads, 0));
+        }
+      }
+      if (multi) {
+        m_end = std::min(nq, (size_t)kSets);
+        const uint32_t tpw = mvx_tpw();
+        for (size_t g0 = 1, gs = 1; g0 < m_end && ngrp < 5; g0 += gs, gs *= 2) {
+          const size_t g1 = (ngrp == 4) ? m_end : std::min(m_end, g0 + gs);
+          MvxJobs J{};
+          J.touch = touch;
+          uint32_t wgs = 0;
+          for (size_t q = g0; q < g1; q++) {
+            const size_t bq = first + q, Tq = ntx[bq];
+            MvSet &Sq = M->set[q];
+            const uint8_t *db = d_blocks ? d_blocks[bq] : nullptr;
+            if (!db) {
+              HIP_TRY(hipMemcpyAsync(Sq.blk.p, blocks[bq], lens[bq], hipMemcpyHostToDevice, xs[1]));
+              db = Sq.blk.as<uint8_t>();
+            }
+            const size_t etq = (Tq * 8 + 63) & ~(size_t)63, flq = (Tq + 63) & ~(size_t)63;
+            uint8_t *dh = dheads + hoff[q];
+            MvxJob &j = J.j[J.n++];
+            j.base = db;
+            j.envtab = reinterpret_cast<const uint32_t *>(dh);
+            j.in_flags = dh + etq;
+            j.info = Sq.info.as<MvTxInfo>();
+            j.reads = Sq.reads.as<MvRec>();
+            j.writes = Sq.writes.as<MvRec>();
+            j.c = reinterpret_cast<MvCounters *>(dh + etq + flq);
+            j.scr = Sq.xscr.as<MvRec>();
+            j.bad = Sq.bad.as<uint8_t>();
+            j.ntx = (uint32_t)Tq;
+            j.wg0 = wgs;
+            wgs += (uint32_t)((Tq + tpw - 1) / tpw);
+          }
+          if (wgs) mvx_extract_multi_launch(tpw, xs[1], J, wgs);
+          HIP_TRY(hipGetLastError());
+          HIP_TRY(hipEventRecord(M->ev_multi[ngrp], xs[1]));
+          grp_end[ngrp++] = g1;
+          if (g1 == m_end) break;
+        }
       }
       rest_sent = true;
     }
-    if (k >= nq) break;
-    // block k's extraction stream: the set is free once block k-kSets's chain is done
-    hipStream_t sxk = xs[k % nxs];
-    if (k >= (size_t)kSets) HIP_TRY(hipStreamWaitEvent(sxk, S.ev_free, 0));
-    const uint8_t *dblk = d_blocks ? d_blocks[b] : nullptr;
-    if (!dblk) {
-      HIP_TRY(hipMemcpyAsync(S.blk.p, block, len, hipMemcpyHostToDevice, sxk));
-      dblk = S.blk.as<uint8_t>();
+    // the next call's framing walks start on the pre-split worker as soon as every head of this
+    // call is filled (they overwrite the pre-split table the heads were filled from)
+    if (k == 0 && n_next) {
+      fgv_block_presplit(c->blk, c->device, n_next, next_blocks, next_lens, nullptr, nullptr);
+      n_next = 0;
     }
+    const uint8_t *dblk = d_blocks && d_blocks[b] ? d_blocks[b] : S.blk.as<uint8_t>();
     uint8_t *dh = dheads + hoff[k];
-    const uint32_t *d_et = reinterpret_cast<const uint32_t *>(dh);
     const uint8_t *d_in = dh + et_bytes;
     MvCounters *d_c = reinterpret_cast<MvCounters *>(dh + et_bytes + fl_bytes);
     MvTxInfo *d_info = S.info.as<MvTxInfo>();
     MvRec *d_r = S.reads.as<MvRec>(), *d_w = S.writes.as<MvRec>();
     const uint32_t N = (uint32_t)T;
-    mvx_extract_launch(mvx_tpw(), sxk, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c, touch, S.xscr.as<MvRec>(),
-                       S.bad.as<uint8_t>());
-    HIP_TRY(hipEventRecord(S.ev_x, sxk));
-    // main stream: block k's chain
-    HIP_TRY(hipStreamWaitEvent(s, S.ev_x, 0));
     const uint32_t epoch = ++M->epoch;
     const uint32_t rg0 = M->rg;
     // k_mvx_prep gates the block on block k-1 (prev_c: decided and committed on the device)

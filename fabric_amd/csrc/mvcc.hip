@@ -37,6 +37,7 @@
 //                        -> VALID   if every read key k has fw_cand(k) >= i.
 //   The lowest undecided tx is always decided, so rounds <= longest alternating chain.
 #include "fgv_kernels.h"
+#include "mvcc_multi.h"
 #include "pbwire_dev.h"
 
 using namespace pbd;
@@ -453,12 +454,12 @@ __device__ __forceinline__ void mvx_extract(uint32_t ntx, const uint8_t *__restr
                                             const uint32_t *__restrict__ envtab, const uint8_t *__restrict__ in_flags,
                                             MvTxInfo *__restrict__ info, MvRec *__restrict__ reads,
                                             MvRec *__restrict__ writes, MvCounters *__restrict__ c, uint32_t touch,
-                                            MvRec *__restrict__ scr, uint8_t *__restrict__ bad) {
+                                            MvRec *__restrict__ scr, uint8_t *__restrict__ bad, uint32_t wg) {
   // LDS bytes per transaction (larger envelopes walk global memory): 48 KB per workgroup at 64
   constexpr uint32_t CAP = TPW == 64 ? 768u : 1536u;
   __shared__ uint32_t lds[TPW * (CAP / 4)];
   __shared__ uint32_t pre[TPW + 1], src0[TPW];  // dword prefix of the staged envelopes, source dword
-  const uint32_t lane = threadIdx.x, t0 = blockIdx.x * TPW;
+  const uint32_t lane = threadIdx.x, t0 = wg * TPW;
   // stage: the dwords covering [off, off + len + 8) of each committer-valid envelope (the walk's
   // over-read contract: up to 7 bytes past a span; block buffers carry >= 64 B of tail padding).
   // Lane j reads transaction j's table entry; then every lane copies dwords of the concatenated
@@ -578,7 +579,21 @@ __global__ __launch_bounds__(64) void k_mvx_extract_t(uint32_t ntx, const uint8_
                                                       MvRec *__restrict__ reads, MvRec *__restrict__ writes,
                                                       MvCounters *__restrict__ c, uint32_t touch, MvRec *__restrict__ scr,
                                                       uint8_t *__restrict__ bad) {
-  mvx_extract<TPW>(ntx, base, envtab, in_flags, info, reads, writes, c, touch, scr, bad);
+  mvx_extract<TPW>(ntx, base, envtab, in_flags, info, reads, writes, c, touch, scr, bad, blockIdx.x);
+}
+// several blocks in one launch (mvcc_multi.h): workgroup -> its block by the jobs' wg0
+template <uint32_t TPW>
+__global__ __launch_bounds__(64) void k_mvx_extract_multi(const MvxJobs J) {
+  uint32_t q = 0;
+  while (q + 1 < J.n && blockIdx.x >= J.j[q + 1].wg0) q++;
+  const MvxJob &b = J.j[q];
+  mvx_extract<TPW>(b.ntx, b.base, b.envtab, b.in_flags, b.info, b.reads, b.writes, b.c, J.touch, b.scr, b.bad,
+                   blockIdx.x - b.wg0);
+}
+void mvx_extract_multi_launch(uint32_t tpw, hipStream_t st, const MvxJobs &J, uint32_t wgs) {
+  if (tpw == 64) hipLaunchKernelGGL(k_mvx_extract_multi<64>, dim3(wgs), dim3(64), 0, st, J);
+  else if (tpw == 32) hipLaunchKernelGGL(k_mvx_extract_multi<32>, dim3(wgs), dim3(64), 0, st, J);
+  else hipLaunchKernelGGL(k_mvx_extract_multi<16>, dim3(wgs), dim3(64), 0, st, J);
 }
 // transactions per workgroup (16 / 32 / 64): host picks (fgv_mvcc.cpp mvx_launch)
 void mvx_extract_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint8_t *base, const uint32_t *envtab,
