@@ -717,6 +717,9 @@ def run_mvcc(args, world, rank, local, dev):
     from fabric_amd.synth import mvcc as M
 
     T, K, W = args.tx_per_mvcc_block, args.steps, args.warmup
+    C = max(1, args.mvcc_chain)
+    if C > 1:  # warm up with chain calls of the timed size (buffer sets of a C-block call allocated)
+        W = max(W, C)
     t0 = time.time()
     st = M.MvccState(args.state_keys, seed=4 + rank, private_every=args.mvcc_private_every)
     keys, blk, txn = st.items()
@@ -726,7 +729,6 @@ def run_mvcc(args, world, rank, local, dev):
     if args.mvcc_private_every > 0:  # private-data keys: hashed namespace mycc$$hpvt
         hk, hb, ht = st.items_hashed()
         eng.statedb_load(M.HASHED_NS, hk, hb, ht)
-    C = max(1, args.mvcc_chain)
     S = min(K, args.mvcc_single_steps) if C > 1 else 0  # the single-block pass after the chained one
     blocks = [M.make_block(st, T, number=1001 + i, seed=100 * rank + i) for i in range(W + K + S)]
     log(f"[bench] rank {rank}: {args.state_keys} keys + {W + K + S} x {T}-tx blocks ready in {time.time() - t0:.1f}s")
@@ -739,10 +741,21 @@ def run_mvcc(args, world, rank, local, dev):
         o += sz
     torch.cuda.synchronize()
     ok = True
-    for i in range(W):
-        b, labels, flags = blocks[i]
-        nb = blocks[i + 1][0] if not args.no_presplit else None
-        ok &= bool((eng.mvcc_validate(b, 1001 + i, flags, commit=True, d_block=dptr[i], next_block=nb) == labels).all())
+    if C > 1:  # chain calls (the last one announces the first timed call's blocks for its pre-split)
+        for i0 in range(0, W, C):
+            i1 = min(i0 + C, W)
+            nxt = [blocks[i][0] for i in range(i1, min(i1 + C, W + K))] if not args.no_presplit else None
+            ws = _lib.MvccChainStep(eng, [blocks[i][0] for i in range(i0, i1)], range(1001 + i0, 1001 + i1),
+                                    [blocks[i][2] for i in range(i0, i1)], commit=True, d_blocks=dptr[i0:i1],
+                                    next_blocks=nxt)
+            fl, rc, done = ws.run()
+            _lib._check(rc)
+            ok &= all(bool((f == blocks[i][1]).all()) for f, i in zip(fl, range(i0, i1)))
+    else:
+        for i in range(W):
+            b, labels, flags = blocks[i]
+            nb = blocks[i + 1][0] if not args.no_presplit else None
+            ok &= bool((eng.mvcc_validate(b, 1001 + i, flags, commit=True, d_block=dptr[i], next_block=nb) == labels).all())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

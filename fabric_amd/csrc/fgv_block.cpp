@@ -24,6 +24,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -132,6 +133,12 @@ struct SplitOut {
 // thread (a thread start would cost more than the overlap gains).
 static int split_batch(ThreadPool &pool, size_t nblocks, const uint8_t *const *h_blocks, const size_t *lens,
                        const uint32_t *tx_lo, const uint32_t *tx_hi, SplitOut &o, HostBuf &et);
+// FGV_PRESPLIT_LOG=1: each pre-split walk's duration and each wait for one on stderr (profiling aid)
+static bool presplit_log() {
+  static const bool on = getenv("FGV_PRESPLIT_LOG") && atoi(getenv("FGV_PRESPLIT_LOG"));
+  return on;
+}
+
 struct PreSplit {
   std::thread th;
   std::mutex mu;
@@ -163,9 +170,14 @@ struct PreSplit {
       int r = FGV_OK;
       if (!dev_set) r = hipSetDevice(device) == hipSuccess ? FGV_OK : FGV_EDEVICE;  // (pinned staging)
       dev_set = r == FGV_OK;
+      const bool log = presplit_log();
+      const auto t0 = std::chrono::steady_clock::now();
       if (r == FGV_OK)
         r = split_batch(*pool, blocks.size(), blocks.data(), lens.data(), lo_in.empty() ? nullptr : lo_in.data(),
                         hi_in.empty() ? nullptr : hi_in.data(), out, et);
+      if (log)
+        fprintf(stderr, "[fgv] pre-split of %zu blocks: %.3f ms\n", blocks.size(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
       lk.lock();
       rc = r;
       done = true;
@@ -1878,7 +1890,11 @@ bool fgv_block_take_presplit_batch(fgv_block_state *S, size_t nb, const uint8_t 
                                    const uint32_t **et, const size_t **ntx, const size_t **first) {
   PreSplit &P = S->pre;
   if (!P.active || !P.matches(nb, blocks, lens, nullptr, nullptr)) return false;
+  const auto t0 = std::chrono::steady_clock::now();
   P.join();
+  if (presplit_log())
+    fprintf(stderr, "[fgv] waited %.3f ms for the pre-split of %zu blocks\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), nb);
   if (P.rc != FGV_OK || P.out.ntx.size() != nb) return false;
   *et = P.et.as<uint32_t>();
   *ntx = P.out.ntx.data();

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <string>
@@ -1056,6 +1058,16 @@ static uint32_t mvx_tpw() {
   }();
   return v;
 }
+// the first block of a chain is extracted alone on an idle chip (FGV_MVX_TPW0, A/B; default as
+// FGV_MVX_TPW)
+static uint32_t mvx_tpw0() {
+  static const uint32_t v = [] {
+    const char *e = getenv("FGV_MVX_TPW0");
+    const uint32_t x = e ? (uint32_t)atoi(e) : mvx_tpw();
+    return (x == 16u || x == 64u || x == 32u) ? x : mvx_tpw();
+  }();
+  return v;
+}
 // FGV_MVCC_SPIN=0: blocking waits (A/B); polled by default -- a block's GPU work is ~0.2 ms, and a
 // blocking synchronize's wake-up is a large share of that
 static bool mvcc_spin() {
@@ -1244,12 +1256,25 @@ static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, co
 // wait the host takes the blocks in order: the device result of every block before the first one
 // the device did not finish (range queries or metadata writes -> the phantom path, a longer
 // fixpoint, unsupported, table full) is final; *stop = that block (n when all finished).
+// FGV_MVCC_LOG=1: each chain call's host timeline on stderr (profiling aid): microseconds from
+// entry to the first record, block 0's launch, the other heads' launches, the end of the
+// enqueue, the end of the wait and the return, and since the previous call's return
+static bool mvcc_log() {
+  static const bool on = getenv("FGV_MVCC_LOG") && atoi(getenv("FGV_MVCC_LOG"));
+  return on;
+}
+static double mvcc_now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, const uint8_t *const *blocks,
                       const size_t *lens, const uint8_t *const *d_blocks, const uint64_t *block_nums,
                       uint8_t *const *flags, const size_t *ntx, int commit, size_t *stop, size_t n_next,
                       const uint8_t *const *next_blocks, const size_t *next_lens) {
   *stop = first;
   const size_t nb = n - first;
+  static double last_exit = 0;
+  double tl[6] = {mvcc_now_us(), 0, 0, 0, 0, 0};
   // per-block sizes and the offsets of their head / tail regions
   std::vector<size_t> hoff(nb + 1, 0), toff(nb + 1, 0);
   size_t max_len = 0, max_ntx = 0;
@@ -1345,6 +1370,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   fill(0);
   if (!walked[0]) return FGV_OK;  // (the single-block path reports that block's error)
   // (stream2 starts after whatever the main stream holds: the table reset above, earlier calls)
+  tl[1] = mvcc_now_us();
   HIP_TRY(hipEventRecord(c->ev[0], s));
   HIP_TRY(hipStreamWaitEvent(sx, c->ev[0], 0));
   // FGV_MVX_STREAMS=2: extractions alternate over stream2 and stream3, two side by side (A/B).
@@ -1379,6 +1405,14 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   const uint32_t touch = mvx_touch();
   BlkSlot *d_b = M->btbl.as<BlkSlot>();
   const MvCounters *prev_c = nullptr;
+  // FGV_MVCC_FUSE=0: k_mvx_flags + k_mv_last and one k_mv_tail per block (A/B); else the fused
+  // k_mvx_flags_last and the tails of the call at its end (mvcc_multi.h)
+  static const bool fuse = [] {
+    const char *e = getenv("FGV_MVCC_FUSE");
+    return !e || atoi(e) != 0;
+  }();
+  std::vector<const MvCounters *> tails_c;
+  std::vector<uint32_t *> tails_h;
   for (size_t k = 0; k < nb; k++) {
     const size_t b = first + k;
     const uint8_t *block = blocks[b];
@@ -1396,7 +1430,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
       const uint8_t *db = d_blocks ? d_blocks[b] : nullptr;
       if (!db) HIP_TRY(hipMemcpyAsync(S.blk.p, block, len, hipMemcpyHostToDevice, sxk));
       uint8_t *dh = dheads + hoff[k];
-      mvx_extract_launch(mvx_tpw(), sxk, (uint32_t)T, db ? db : S.blk.as<uint8_t>(),
+      mvx_extract_launch(k == 0 ? mvx_tpw0() : mvx_tpw(), sxk, (uint32_t)T, db ? db : S.blk.as<uint8_t>(),
                          reinterpret_cast<const uint32_t *>(dh), dh + et_bytes, S.info.as<MvTxInfo>(),
                          S.reads.as<MvRec>(), S.writes.as<MvRec>(),
                          reinterpret_cast<MvCounters *>(dh + et_bytes + fl_bytes), touch, S.xscr.as<MvRec>(),
@@ -1405,6 +1439,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
       // main stream: block k's chain
       HIP_TRY(hipStreamWaitEvent(s, S.ev_x, 0));
     }
+    if (k == 0) tl[2] = mvcc_now_us();
     if (k == 0 && !rest_sent) {  // the other heads, once block 0's extraction is on its way
       fgv_parallel_run(c->blk, nb - 1, [&](size_t j) { fill(j + 1); });
       while (nq < nb && walked[nq]) nq++;
@@ -1460,6 +1495,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
       }
       rest_sent = true;
     }
+    if (k == 0) tl[3] = mvcc_now_us();
     // the next call's framing walks start on the pre-split worker as soon as every head of this
     // call is filled (they overwrite the pre-split table the heads were filled from)
     if (k == 0 && n_next) {
@@ -1487,10 +1523,17 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
                          S.rslot.as<uint32_t>(), S.wslot.as<uint32_t>(), d_b, S.st.as<uint8_t>(), d_c);
     // zero-copy: the codes, counters and arena top go straight to the block's pinned tail region
     uint8_t *d_out = zc ? d_btail + toff[k] + kCounterBytes : S.tail.as<uint8_t>() + kCounterBytes;
-    hipLaunchKernelGGL(k_mvx_flags, grid_for(T), dim3(256), 0, s, N, R, d_in, d_info, S.st.as<uint8_t>(), d_out, d_c);
+    if (fuse) {
+      hipLaunchKernelGGL(k_mvx_flags_last, grid_stride(std::max(rcap, T)), dim3(256), 0, s, N, R, d_in, d_info,
+                         S.st.as<uint8_t>(), d_out, d_c, commit ? 1u : 0u, d_w, S.wslot.as<uint32_t>(), d_b, epoch,
+                         M->top.as<unsigned long long>(), M->cap, M->arena_cap);
+    } else {
+      hipLaunchKernelGGL(k_mvx_flags, grid_for(T), dim3(256), 0, s, N, R, d_in, d_info, S.st.as<uint8_t>(), d_out, d_c);
+      if (commit)
+        hipLaunchKernelGGL(k_mv_last, grid_stride(rcap), dim3(256), 0, s, R, d_w, S.wslot.as<uint32_t>(),
+                           S.st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
+    }
     if (commit) {
-      hipLaunchKernelGGL(k_mv_last, grid_stride(rcap), dim3(256), 0, s, R, d_w, S.wslot.as<uint32_t>(),
-                         S.st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
       hipLaunchKernelGGL(k_mv_upsert_find, grid_stride(rcap), dim3(256), 0, s, 1u, R, 0u, dblk, d_w,
                          S.wslot.as<uint32_t>(), S.st.as<uint8_t>(), d_b, epoch, M->tbl.as<StateSlot>(), M->mask,
                          M->arena.as<uint8_t>(), block_nums[b], S.pend.as<uint8_t>(), d_c);
@@ -1501,7 +1544,10 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
     HIP_TRY(hipGetLastError());
     uint8_t *ht = M->btail.as<uint8_t>() + toff[k];
     const size_t top_off = (kCounterBytes + T + 7) & ~(size_t)7;
-    if (zc) {
+    if (zc && fuse) {
+      tails_c.push_back(d_c);
+      tails_h.push_back(reinterpret_cast<uint32_t *>(d_btail + toff[k]));
+    } else if (zc) {
       uint8_t *dt = d_btail + toff[k];
       hipLaunchKernelGGL(k_mv_tail, dim3(1), dim3(64), 0, s, d_c, M->top.as<unsigned long long>(),
                          reinterpret_cast<uint32_t *>(dt),
@@ -1515,10 +1561,29 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
     M->rg = rg0 + R + 2;  // round tags of this block: rg0 + 1 .. rg0 + R + 1
     prev_c = d_c;
   }
+  // fused mode: every block's counters in one launch per MVX_MULTI_MAX blocks, and the arena top
+  // after the last commit once, into the last block's tail (a later block commits nothing after a
+  // block the device did not finish, so the final top is the last finished block's)
+  const size_t last_top = tails_c.empty() ? 0 : toff[tails_c.size() - 1] +
+                                                     ((kCounterBytes + ntx[first + tails_c.size() - 1] + 7) & ~(size_t)7);
+  for (size_t q0 = 0; q0 < tails_c.size(); q0 += MVX_MULTI_MAX) {
+    MvTails Tl{};
+    const size_t q1 = std::min(tails_c.size(), q0 + MVX_MULTI_MAX);
+    for (size_t q = q0; q < q1; q++) {
+      Tl.c[Tl.n] = tails_c[q];
+      Tl.hc[Tl.n++] = tails_h[q];
+    }
+    hipLaunchKernelGGL(k_mv_tails, dim3(Tl.n), dim3(64), 0, s, Tl, M->top.as<unsigned long long>(),
+                       (commit && q1 == tails_c.size()) ? reinterpret_cast<unsigned long long *>(d_btail + last_top)
+                                                        : nullptr);
+  }
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[2], s));
   // the next batch's framing walks run on the pre-split worker while this chain runs
   if (n_next) fgv_block_presplit(c->blk, c->device, n_next, next_blocks, next_lens, nullptr, nullptr);
+  tl[4] = mvcc_now_us();
   HIP_TRY(fgv_stream_wait(s, mvcc_spin()));
+  tl[5] = mvcc_now_us();
   float ms = 0;
   c->t_mvcc_lookup = 0;
   if (hipEventElapsedTime(&ms, c->ev[0], c->ev[2]) == hipSuccess) c->t_mvcc_total = ms / (double)nq;
@@ -1533,7 +1598,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
     memcpy(flags[b], ht + kCounterBytes, T);
     if (commit) {
       uint64_t t[2];
-      memcpy(t, ht + ((kCounterBytes + T + 7) & ~(size_t)7), 16);
+      memcpy(t, tails_c.empty() ? ht + ((kCounterBytes + T + 7) & ~(size_t)7) : M->btail.as<uint8_t>() + last_top, 16);
       M->arena_used = t[0];
       M->nkeys = t[1];
     }
@@ -1543,6 +1608,13 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   }
   if (rounds) M->last_rounds = rounds;
   *stop = first + k;
+  if (mvcc_log()) {
+    const double t = mvcc_now_us();
+    fprintf(stderr, "[fgv] mvcc chain %zu blocks: since last %.0f | ev0 %.0f b0 %.0f rest %.0f enq %.0f wait %.0f ret %.0f us\n",
+            nq, last_exit ? tl[0] - last_exit : 0.0, tl[1] - tl[0], tl[2] - tl[0], tl[3] - tl[0], tl[4] - tl[0],
+            tl[5] - tl[0], t - tl[0]);
+    last_exit = t;
+  }
   return FGV_OK;
 }
 

@@ -766,6 +766,42 @@ __global__ __launch_bounds__(256) void k_mvx_flags(uint32_t ntx, uint32_t rlast,
   out[t] = f;
 }
 
+// the fused flags + last step of a chain block (mvcc_multi.h): k_mvx_flags over ntx, then (commit)
+// k_mv_last's capacity check and last-valid-writer election over the block's writes
+__global__ __launch_bounds__(256) void k_mvx_flags_last(uint32_t ntx, uint32_t rlast, const uint8_t *__restrict__ in_flags,
+                                                        const MvTxInfo *__restrict__ info, const uint8_t *__restrict__ st,
+                                                        uint8_t *__restrict__ out, MvCounters *__restrict__ c,
+                                                        uint32_t commit, const MvRec *__restrict__ writes,
+                                                        const uint32_t *__restrict__ wslot, BlkSlot *__restrict__ btbl,
+                                                        uint32_t epoch, const unsigned long long *__restrict__ top,
+                                                        uint64_t slots_cap, uint64_t arena_cap) {
+  if (!converged(c, rlast)) return;
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  if (gid == 0 && !c->done) {
+    c->done = 1;
+    c->rounds = rlast;
+  }
+  for (uint32_t t = gid; t < ntx; t += stride) {
+    const uint8_t code = info[t].code;
+    uint8_t f;
+    if (code == MV_SKIP) f = in_flags[t];
+    else if (code != 0) f = code;
+    else f = st[t] == ST_INVALID ? 11 : 0;
+    out[t] = f;
+  }
+  if (!commit) return;
+  const uint32_t nw = c->nw;
+  if ((top[1] + nw) * 10 > slots_cap * 7 || top[0] + c->wbytes > arena_cap) {
+    if (gid == 0) c->nomem = 1;
+    return;
+  }
+  for (uint32_t i = gid; i < nw; i += stride) {
+    const uint32_t tx = writes[i].tx;
+    if (st[tx] == ST_VALID)
+      atomicMax(reinterpret_cast<unsigned long long *>(&btbl[wslot[i]].last), ((unsigned long long)epoch << 32) | (tx + 1));
+  }
+}
+
 // ============================================================ commit
 // last VALID writer of each key (a key is written at most once per tx: duplicates are
 // unsupported), and the capacity check of the whole commit
@@ -901,6 +937,18 @@ __global__ __launch_bounds__(64) void k_mv_tail(const MvCounters *__restrict__ c
   const uint32_t *w = reinterpret_cast<const uint32_t *>(c);
   if (t < sizeof(MvCounters) / 4) hc[t] = w[t];
   if (htop && t < 2) htop[t] = top[t];
+  __threadfence_system();
+}
+
+// k_mv_tail for several chain blocks (mvcc_multi.h): workgroup q copies block q's counters
+__global__ __launch_bounds__(64) void k_mv_tails(const MvTails T, const unsigned long long *__restrict__ top,
+                                                 unsigned long long *__restrict__ htop) {
+  const uint32_t t = threadIdx.x, q = blockIdx.x;
+  if (q < T.n) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(T.c[q]);
+    if (t < sizeof(MvCounters) / 4) T.hc[q][t] = w[t];
+  }
+  if (q == 0 && htop && t < 2) htop[t] = top[t];
   __threadfence_system();
 }
 

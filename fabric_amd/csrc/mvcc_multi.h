@@ -26,3 +26,18 @@ struct MvxJobs {
 };
 // grid = the workgroups of every block (wg0 of block q = sum of the earlier blocks')
 void mvx_extract_multi_launch(uint32_t tpw, hipStream_t st, const MvxJobs &J, uint32_t wgs);
+
+// k_mvx_flags and k_mv_last of one chain block in one launch (independent steps after the
+// fixpoint; commit = 0: the codes only)
+__global__ void k_mvx_flags_last(uint32_t ntx, uint32_t rlast, const uint8_t *in_flags, const MvTxInfo *info,
+                                 const uint8_t *st, uint8_t *out, MvCounters *c, uint32_t commit, const MvRec *writes,
+                                 const uint32_t *wslot, BlkSlot *btbl, uint32_t epoch, const unsigned long long *top,
+                                 uint64_t slots_cap, uint64_t arena_cap);
+// the tails of up to MVX_MULTI_MAX chain blocks at once (k_mv_tail's work; workgroup q = block q):
+// their counters, and the arena top once, after the last block's commit
+struct MvTails {
+  uint32_t n;
+  const MvCounters *c[MVX_MULTI_MAX];
+  uint32_t *hc[MVX_MULTI_MAX];
+};
+__global__ void k_mv_tails(const MvTails T, const unsigned long long *top, unsigned long long *htop);
