@@ -146,7 +146,9 @@ def main(src, rnd):
                 traffic[wl] = dict(kernel=kern, fetch_bytes=round(fb), write_bytes=round(wb), hbm_bytes=round(fb + wb),
                                    avg_us=round(F[kern]["avg_s"] * 1e6, 1))
         else:  # MVCC: every per-block kernel (the one-time state load k_mv_tags excluded), per block
-            nblk = F.get("k_mvx_extract", F.get("k_mvx_extract_t", {})).get("dispatches", 0)
+            # blocks: one k_mvx_prep per block on every path (the chain's extractions are grouped
+            # since round 5, k_mvx_extract_multi walking several blocks per launch)
+            nblk = F.get("k_mvx_prep", {}).get("dispatches", 0)
             per_block = [k for k in F if k.startswith("k_mv") and k != "k_mv_tags"]
             if nblk:
                 fb = sum(F[k]["FETCH_SIZE"] * 2 * 1024 * F[k]["dispatches"] for k in per_block) / nblk
