@@ -1182,9 +1182,16 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul28(uint32_t n, const uint3
   }
 }
 
+// 2^304 mod p, radix 2^28: f28_mul(x * 2^256, K304) = x * 2^280 (Montgomery-256 -> Montgomery-280)
+__constant__ static const uint32_t K304_28[10] = {0xffffu,    0x100000u, 0x0u,      0x1000u,    0xfffffffu,
+                                                  0xfffffefu, 0xffffffu, 0xffff000u, 0xffffffeu, 0xfu};
+
 // k_vb_fin: after k_prep -- acc[j] + sum of the 12 generator comb terms of u1 (k_prep's digits),
 // then the projective x_R check of k_point -> status[list[j]].  The last workgroup to finish
 // zeroes the list counters for the next batch (atomics only: no fence, no extra launch).
+// The sum runs in radix 2^28 (k_point28's incomplete mixed addition on the Montgomery-280 comb
+// entries as stored); an item whose sum met an exceptional case (Z = 0 at the end) is summed
+// again with the complete radix-2^32 addition, as every item was before round 5.
 __global__ __launch_bounds__(256) void k_vb_fin(uint32_t n, uint8_t *__restrict__ status,
                                                 const apoint_raw *__restrict__ gtab28,
                                                 const int8_t *__restrict__ digits,
@@ -1200,41 +1207,105 @@ __global__ __launch_bounds__(256) void k_vb_fin(uint32_t n, uint8_t *__restrict_
     jpoint a;
     load_jp(a, acc + (size_t)j * VB_ACC_WORDS);
     const int32_t *g = reinterpret_cast<const int32_t *>(digits + (size_t)i * DIG_STRIDE);
-    fe c232;
-    fe_load_c(c232, C232_32);
-#pragma unroll 1
-    for (int win = 0; win < NGWIN; win++) {
-      const int dd = g[win];
-      if (dd == 0) continue;
-      const apoint_raw *e = gtab28 + (size_t)win * GT_K + ((dd < 0 ? -dd : dd) - 1);
-      apoint p;
-      load_fe(p.x, e->x);
-      load_fe(p.y, e->y);
-      fe_mul(p.x, p.x, c232);  // Montgomery-280 -> Montgomery-256 (as k_point)
-      fe_mul(p.y, p.y, c232);
-      if (dd < 0) fe_neg(p.y, p.y);
-      jpoint t2 = a;
-      pt_madd(a, t2, p);
-    }
+    uint32_t r[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) r[k] = r_limbs[(size_t)k * n + i];
     uint8_t st = 1;
-    if (!fe_is_zero(a.z)) {
-      fe rr, rm, z2, lhs;
+    bool exact = fe_is_zero(a.z);
+    if (!exact) {
+      jp28 b;
+      f28 t, k304;
+      f28_load_c(k304, K304_28);
+      f28_from32(t, a.x.v);
+      f28_mul(b.x, t, k304);
+      f28_from32(t, a.y.v);
+      f28_mul(b.y, t, k304);
+      f28_from32(t, a.z.v);
+      f28_mul(b.z, t, k304);
+#pragma unroll 1
+      for (int win = 0; win < NGWIN; win++) {
+        const int dd = g[win];
+        if (dd == 0) continue;
+        const uint4 *e = reinterpret_cast<const uint4 *>(gtab28 + (size_t)win * GT_K + ((dd < 0 ? -dd : dd) - 1));
+        const uint4 n0 = e[0], n1 = e[1], n2 = e[2], n3 = e[3];
+        const uint32_t wx[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+        const uint32_t wy[8] = {n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
+        f28 px, py;
+        f28_from32(px, wx);
+        f28_from32(py, wy);
+        if (dd < 0) {
+          f28 z;
 #pragma unroll
-      for (int k = 0; k < 8; k++) rr.v[k] = r_limbs[(size_t)k * n + i];
-      fe_sqr(z2, a.z);
-      fe_to_mont(rm, rr);
-      fe_mul(lhs, rm, z2);
-      if (fe_eq(lhs, a.x)) {
-        st = 0;
+          for (int q = 0; q < 10; q++) z.v[q] = 0u;
+          f28_sub(py, z, py, C4P28);
+          f28_norm(py);
+        }
+        madd28(b, px, py);
+      }
+      if (f28_is_zero(b.z)) {
+        exact = true;  // an exceptional addition: the complete sum below decides
       } else {
-        uint32_t c = 0;
-        fe rn;
+        f28 z2, rm, lhs, d, one;
+        f28_sqr(z2, b.z);
+        f28_load_c(one, ONE28);
+        f28_to_mont(rm, r);
+        f28_mul(lhs, rm, z2);
+        f28_sub(d, b.x, lhs, C4P28);
+        f28_mul(d, d, one);
+        if (f28_is_zero(d)) {
+          st = 0;
+        } else {
+          // x_R in [n, p): x_R mod n == r  <=>  x_R == r + n  (only if r + n < p)
+          uint32_t c = 0, rn[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) rn.v[k] = addc(rr.v[k], N_LIMBS[k], c, &c);
-        if (c == 0u && lt_p(rn.v)) {
-          fe_to_mont(rm, rn);
-          fe_mul(lhs, rm, z2);
-          if (fe_eq(lhs, a.x)) st = 0;
+          for (int k = 0; k < 8; k++) rn[k] = addc(r[k], N_LIMBS[k], c, &c);
+          if (c == 0u && lt_p(rn)) {
+            f28_to_mont(rm, rn);
+            f28_mul(lhs, rm, z2);
+            f28_sub(d, b.x, lhs, C4P28);
+            f28_mul(d, d, one);
+            if (f28_is_zero(d)) st = 0;
+          }
+        }
+      }
+    }
+    if (exact) {
+      fe c232;
+      fe_load_c(c232, C232_32);
+#pragma unroll 1
+      for (int win = 0; win < NGWIN; win++) {
+        const int dd = g[win];
+        if (dd == 0) continue;
+        const apoint_raw *e = gtab28 + (size_t)win * GT_K + ((dd < 0 ? -dd : dd) - 1);
+        apoint p;
+        load_fe(p.x, e->x);
+        load_fe(p.y, e->y);
+        fe_mul(p.x, p.x, c232);  // Montgomery-280 -> Montgomery-256 (as k_point)
+        fe_mul(p.y, p.y, c232);
+        if (dd < 0) fe_neg(p.y, p.y);
+        jpoint t2 = a;
+        pt_madd(a, t2, p);
+      }
+      st = 1;
+      if (!fe_is_zero(a.z)) {
+        fe rr, rm, z2, lhs;
+#pragma unroll
+        for (int k = 0; k < 8; k++) rr.v[k] = r[k];
+        fe_sqr(z2, a.z);
+        fe_to_mont(rm, rr);
+        fe_mul(lhs, rm, z2);
+        if (fe_eq(lhs, a.x)) {
+          st = 0;
+        } else {
+          uint32_t c = 0;
+          fe rn;
+#pragma unroll
+          for (int k = 0; k < 8; k++) rn.v[k] = addc(rr.v[k], N_LIMBS[k], c, &c);
+          if (c == 0u && lt_p(rn.v)) {
+            fe_to_mont(rm, rn);
+            fe_mul(lhs, rm, z2);
+            if (fe_eq(lhs, a.x)) st = 0;
+          }
         }
       }
     }
