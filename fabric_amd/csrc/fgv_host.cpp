@@ -189,7 +189,7 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
   if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kid.ensure((size_t)nk * 4) || !c->kt_q.ensure((size_t)nk * 64) ||
       !c->kt_id.ensure((size_t)nk * 4))
     return FGV_ENOMEM;
-  // the variable-base tables (7.5 KB per id) grow by doubling; kernels in flight read the old rows
+  // the variable-base tables (15 KB per id) grow by doubling; kernels in flight read the old rows
   if (c->n_ids + nk > c->vbt_keys) {
     const uint32_t want = std::min<uint32_t>(c->key_ids, std::max<uint32_t>({c->n_ids + nk, 2 * c->vbt_keys, 4096u}));
     uint32_t grow = want;
@@ -222,7 +222,7 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
   }
   HIP_TRY(hipMemcpyAsync(c->kt_q.p, kq, (size_t)nk * 64, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->kt_id.p, ki, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_keyprep, dim3((nk * VB_LANES + 63) / 64), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
+  hipLaunchKernelGGL(k_keyprep, dim3((nk * VB_SLICES + 63) / 64), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
                      c->kt_id.as<uint32_t>(), nk, c->vbt.as<uint32_t>(), c->key_ok.as<uint8_t>());
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));  // (the staging is reused by comb_build)
@@ -606,8 +606,23 @@ static int launch_inv(fgv_ctx *c, hipStream_t st, uint32_t N, const uint32_t *dn
       const char *e = getenv("FGV_VB28");
       return !e || atoi(e) != 0;
     }();
+    // lanes per item: 16 for a small batch (the previous batch's count up to 8 items per CU: a
+    // single block's cold creators are one serial chain per lane, and 16 lanes halve it), else 8
+    // (a full batch shares the chip with the hashes and the comb verifies, and 16 lanes add
+    // butterfly work).  Measured on MI355X (r5v): C2 churn single-block latency 0.63-0.64 ms
+    // with 16 against 0.68 with 8; a C2 churn step (~16k cold items) 1.07 ms with 16 against
+    // 1.01-1.03 with 8.  FGV_VB_LANES=8 / 16 fixes it (A/B).
+    static const int vb_lanes_env = [] {
+      const char *e = getenv("FGV_VB_LANES");
+      return e ? atoi(e) : 0;
+    }();
+    // The 16-lane grid is 4 workgroups per CU (not all resident at once: the items are taken from
+    // a work queue, so a late workgroup only finds fewer left).
+    const uint32_t wgs16 = 4;
+    const bool lanes16 = vb_lanes_env == 16 || (vb_lanes_env != 8 && c->vb_last_items <= 8u * c->n_cu);
     if (vb28) {
-      hipLaunchKernelGGL(k_vb_mul28, dim3(vb_wgs * c->n_cu), dim3(VB_THREADS), 0, c->streamV, N, d_slot,
+      hipLaunchKernelGGL(lanes16 ? k_vb_mul28_16 : k_vb_mul28, dim3((lanes16 ? wgs16 : vb_wgs) * c->n_cu), dim3(VB_THREADS),
+                         0, c->streamV, N, d_slot,
                          c->vbt.as<uint32_t>(), d_r, w.as<uint32_t>(), redo, c->vblist.as<uint32_t>(),
                          c->vbacc.as<uint32_t>(), c->vbuse.as<uint32_t>(), c->promote_uses,
                          c->vbpromo.as<uint32_t>(), c->vbhand.as<uint32_t>());

@@ -785,15 +785,15 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
 // ---------------------------------------------------------------- keys without a comb
 // k_keyprep: new key ids -> on-curve bit (k_inv reports 5 for a key off the curve, before the
 // range checks, as ecdsa.Verify does) and the variable-base kernel's per-key table
-// vbt[id][s][d-1] = d * Q_s, Q_s = 2^(32 s) * Q, s < VB_LANES, d = 1..VB_TAB (affine, Montgomery-280
-// form as the comb tables, 7.5 KB per key).  One thread per (key, slice): 32 s doublings to Q_s, 14 complete additions,
-// one inversion for the slice's 15 Z's (prefix products).  qxy: [nkeys][16] plain little-endian
-// limbs (x then y).
+// vbt[id][s][d-1] = d * Q_s, Q_s = 2^(16 s) * Q, s < VB_SLICES, d = 1..VB_TAB (affine, Montgomery-280
+// form as the comb tables, 15 KB per key; the 8-lane kernels read the even slices).  One thread per
+// (key, slice): 16 s doublings to Q_s, 14 complete additions, one inversion for the slice's 15 Z's
+// (prefix products).  qxy: [nkeys][16] plain little-endian limbs (x then y).
 __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy, const uint32_t *__restrict__ ids,
                                                 uint32_t nkeys, uint32_t *__restrict__ vbt,
                                                 uint8_t *__restrict__ key_ok) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t k = t / VB_LANES, sl = t % VB_LANES;
+  const uint32_t k = t / VB_SLICES, sl = t % VB_SLICES;
   if (k >= nkeys) return;
   fe x, y, xm, ym;
 #pragma unroll
@@ -811,12 +811,12 @@ __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy
     for (int d = 0; d < VB_TAB; d++) store_fe(o + 16 * d, z), store_fe(o + 16 * d + 8, z);
     return;
   }
-  jpoint q;  // Q_s (never infinity: 2^(32 s) < n)
+  jpoint q;  // Q_s (never infinity: 2^(16 s) < n)
   q.x = xm;
   q.y = ym;
   fe_set_one(q.z);
 #pragma unroll 1
-  for (uint32_t d = 0; d < 32 * sl; d++) {
+  for (uint32_t d = 0; d < 16 * sl; d++) {
     jpoint t2 = q;
     pt_dbl(q, t2);
   }
@@ -880,7 +880,7 @@ FGV_DEV void load_jp(jpoint &p, const uint32_t *s) {
 // k_vb_mul: acc[j] = u2 * Q for list entry j (item i = list[j], key id key_slot[i]), u2 = r * s^-1
 // (plain; k_inv's w is s^-1 in Montgomery form) -- needs no digest, so it runs beside the hashes.
 // VB_LANES lanes per item: lane s takes the 32 bits u2[s] of the scalar against the key's slice
-// table d * Q_s, Q_s = 2^(32 s) Q (k_keyprep, affine), so u2 * Q = sum_s u2[s] * Q_s:
+// table d * 2^(32 s) Q (k_keyprep's slice 2s, affine), so u2 * Q = sum_s u2[s] * 2^(32 s) Q:
 //   8 windows of 4 bits, left to right: 28 doublings and <= 8 mixed additions (each next entry
 //   loaded during the doublings);
 //   a 3-level butterfly of complete additions across the 8 lanes (cross-lane shuffles).
@@ -920,7 +920,7 @@ FGV_DEV void vb_mul_body(uint32_t n, const uint32_t *__restrict__ key_slot, cons
     uint32_t dg = u2[0];  // this lane's 32 bits: u2[sl] (a select chain: no private array)
 #pragma unroll
     for (int k = 1; k < 8; k++) dg = sl == (uint32_t)k ? u2[k] : dg;
-    const uint32_t *qt = vbt + (size_t)id * VBT_WORDS + sl * (VB_TAB * 16);
+    const uint32_t *qt = vbt + (size_t)id * VBT_WORDS + (2 * sl) * (VB_TAB * 16);  // Q_{2 sl} = 2^(32 sl) Q
     jpoint a;
     fe_set_zero(a.x);
     fe_set_zero(a.y);
@@ -992,9 +992,10 @@ __global__ __launch_bounds__(VB_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
 
 // ---------------------------------------------------------------- k_vb_mul28 (fast path)
 // The variable-base product u2 * Q in radix-2^28 Montgomery-280 arithmetic (p256_fe28.h), the
-// structure of vb_mul_body: VB_LANES lanes per item, lane s sums u2[s] * Q_s over 8 windows of
-// 4 bits (28 doublings, <= 8 mixed additions from the key's Montgomery-280 slice table), then a
-// 3-level butterfly.  Incomplete formulas, as k_point28: an exceptional addition (a partial sum
+// structure of vb_mul_body: LANES (8 or 16) lanes per item, lane s sums its 32 (16) bits of u2
+// times 2^(32 s) Q (2^(16 s) Q) over 8 (4) windows of 4 bits -- 28 (12) doublings, <= 8 (4) mixed
+// additions from the key's Montgomery-280 slice table -- then a 3- (4-) level butterfly.  16 lanes
+// halve the serial chain of a lane for the same doublings in total (small batches: latency).  Incomplete formulas, as k_point28: an exceptional addition (a partial sum
 // equal to +-the added point) leaves Z = 0, which stays 0; such an item goes to the hand-over list
 // (redo[RD_VB2_CNT], its list index in `hand`) and the exact k_vb_mul finishes it.  The result is
 // converted to the Montgomery-256 Jacobian form k_vb_fin reads.
@@ -1066,7 +1067,8 @@ FGV_DEV void f28_to32(uint32_t w[8], const f28 &a) {
   }
 }
 
-__global__ __launch_bounds__(VB_THREADS) void k_vb_mul28(uint32_t n, const uint32_t *__restrict__ key_slot,
+template <uint32_t LANES>
+FGV_DEV void vb_mul28_body(uint32_t n, const uint32_t *__restrict__ key_slot,
                                                           const uint32_t *__restrict__ vbt,
                                                           const uint32_t *__restrict__ r_limbs,
                                                           const uint32_t *__restrict__ w_in,
@@ -1078,11 +1080,13 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul28(uint32_t n, const uint3
   const uint32_t cnt = ctr[RD_VB_CNT];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&promo[1], cnt);  // (statistics: fgv_key_stats)
   if (cnt == 0) return;
-  const uint32_t lane = __lane_id(), sl = lane % VB_LANES, base = lane - sl;
-  constexpr uint32_t PER = 64u / VB_LANES;
+  // LANES lanes per item, lane sl taking BITS bits of u2 against slice sl * (VB_SLICES / LANES)
+  constexpr uint32_t BITS = 256u / LANES, WINS = BITS / 4u;
+  const uint32_t lane = __lane_id(), sl = lane % LANES, base = lane - sl;
+  constexpr uint32_t PER = 64u / LANES;
   uint32_t j0;
   while (vb_next(ctr + RD_VB_MUL, cnt, PER, j0)) {
-    const uint32_t j = j0 + lane / VB_LANES;
+    const uint32_t j = j0 + lane / LANES;
     if (j >= cnt) continue;  // (uniform within the lane group)
     const uint32_t i = list[j];
     const uint32_t id = key_slot[i];
@@ -1093,10 +1097,14 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul28(uint32_t n, const uint3
       w[k] = w_in[(size_t)k * n + i];
     }
     sn_mul(u2, r, w);
+    // this lane's BITS bits of u2, top-aligned (a select chain: no private array)
+    const uint32_t li = sl * BITS / 32u;
     uint32_t dg = u2[0];
 #pragma unroll
-    for (int k = 1; k < 8; k++) dg = sl == (uint32_t)k ? u2[k] : dg;
-    const uint4 *qt = reinterpret_cast<const uint4 *>(vbt + (size_t)id * VBT_WORDS + sl * (VB_TAB * 16));
+    for (int k = 1; k < 8; k++) dg = li == (uint32_t)k ? u2[k] : dg;
+    if (BITS == 16u) dg = (sl & 1u) ? (dg & 0xFFFF0000u) : (dg << 16);
+    const uint4 *qt = reinterpret_cast<const uint4 *>(vbt + (size_t)id * VBT_WORDS +
+                                                      sl * (VB_SLICES / LANES) * (VB_TAB * 16));
     jp28 a;
     bool inf = true;
     // the entry of window win-1 is loaded while window win is worked (one gather in flight)
@@ -1104,7 +1112,7 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul28(uint32_t n, const uint3
     uint4 n0, n1, n2, n3;
     if (d) n0 = qt[4 * (d - 1)], n1 = qt[4 * (d - 1) + 1], n2 = qt[4 * (d - 1) + 2], n3 = qt[4 * (d - 1) + 3];
 #pragma unroll 1
-    for (int win = 7; win >= 0; win--) {
+    for (int win = (int)WINS - 1; win >= 0; win--) {
       const uint32_t wx[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
       const uint32_t wy[8] = {n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
       dg <<= 4;
@@ -1136,7 +1144,7 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul28(uint32_t n, const uint3
     }
     // butterfly over the item's lanes (infinite partial sums skipped)
 #pragma unroll 1
-    for (uint32_t m = 1; m < VB_LANES; m <<= 1) {
+    for (uint32_t m = 1; m < LANES; m <<= 1) {
       const int src = (int)(base + (sl ^ m));
       jp28 o;
       shfl_f28(o.x, a.x, src);
@@ -1180,6 +1188,18 @@ __global__ __launch_bounds__(VB_THREADS) void k_vb_mul28(uint32_t n, const uint3
 #pragma unroll
     for (int k = 0; k < 8; k++) o[16 + k] = t[k];
   }
+}
+
+#define VB_MUL28_ARGS                                                                                              \
+  uint32_t n, const uint32_t *__restrict__ key_slot, const uint32_t *__restrict__ vbt,                           \
+      const uint32_t *__restrict__ r_limbs, const uint32_t *__restrict__ w_in, uint32_t *__restrict__ ctr,      \
+      const uint32_t *__restrict__ list, uint32_t *__restrict__ acc, uint32_t *__restrict__ uses, uint32_t promote, \
+      uint32_t *__restrict__ promo, uint32_t *__restrict__ hand
+__global__ __launch_bounds__(VB_THREADS) void k_vb_mul28(VB_MUL28_ARGS) {
+  vb_mul28_body<8>(n, key_slot, vbt, r_limbs, w_in, ctr, list, acc, uses, promote, promo, hand);
+}
+__global__ __launch_bounds__(VB_THREADS) void k_vb_mul28_16(VB_MUL28_ARGS) {
+  vb_mul28_body<16>(n, key_slot, vbt, r_limbs, w_in, ctr, list, acc, uses, promote, promo, hand);
 }
 
 // 2^304 mod p, radix 2^28: f28_mul(x * 2^256, K304) = x * 2^280 (Montgomery-256 -> Montgomery-280)
