@@ -114,12 +114,13 @@ struct DevIdent {
   int32_t msp;        // interned Mspid
   uint32_t canon;     // dedup id (Mspid + Id)
   uint32_t valid;
-  uint32_t vclass;    // Verify: 0 on the GPU, 1 always fails, 2 outside the engine; 3 undeserializable
+  uint32_t vclass;    // Verify: 0 on the GPU (SHA-256 or, hash3, SHA3-256 digests), 1 always fails, 2 outside
+                      // the engine (P-384); 3 undeserializable
   uint32_t roles;     // SatisfiesPrincipal(ROLE r) bits
   uint32_t roles_known;
   uint32_t ous_known;        // GetOrganizationalUnits known: ident_ous[ou_off .. ou_off + ou_n)
   uint32_t ou_off, ou_n;
-  uint32_t pad;
+  uint32_t hash3;     // SHA3 MSP (vclass 0): its Verify digests are SHA3-256 (k_bd_sha3)
 };
 // one leaf principal (fgv_channel.h Prin; kinds DPR_* = PR_*)
 enum : int32_t { DPR_ROLE = 0, DPR_IDENTITY = 1, DPR_OU = 2, DPR_NOMINAL = 3, DPR_NEVER = 4, DPR_UNRESOLVED = 5 };

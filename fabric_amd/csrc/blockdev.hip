@@ -151,7 +151,7 @@ DEV void count_jobs(DevTx &R, const DevChannel &ch, const int32_t *id, DevJobIdx
     const int32_t ci = id[0];
     if (ci == -2) R.pre = C_UNSUPPORTED;
     else if (ci < 0 || !ch.idents[ci].valid || ch.idents[ci].vclass == 1) R.pre = C_BAD_CREATOR;
-    else if (ch.idents[ci].vclass != 0) R.pre = C_UNSUPPORTED;  // P-384 key / SHA3 MSP
+    else if (ch.idents[ci].vclass != 0) R.pre = C_UNSUPPORTED;  // P-384 key
   }
   if ((R.flags & BDF_INDEX_OK) && !(R.flags & BDF_INDEX_FROM_TXID)) J.cnt[BJ_I] = 1;
   if (R.pre == C_PENDING) {

@@ -2,6 +2,7 @@
 // the creator signature's digest) and k_bd_sha (every other message of a transaction).  Shared
 // helpers: blockdev_dev.h.  Reference: core/common/validation/msgvalidation.go:26-64, 248-320,
 // msp/identities.go:179-199 (identity.Verify hashes the message), protoutil/txutils.go:503-534.
+#include "sha3_dev.h"
 #include "blockdev_dev.h"
 
 // ============================================================ k_bd_sha_payload
@@ -543,4 +544,31 @@ __global__ __launch_bounds__(64) void k_bd_sha_p3(uint32_t ntx, const DevTx *__r
                                                   unsigned long long *__restrict__ nblk_out) {
   __builtin_amdgcn_s_setprio(3);
   bd_sha_body(ntx, txs, bases, dig, nblk_out);
+}
+
+// SHA3 MSPs (identities.go:170-199, getHashOpt :219-227): once the identities are resolved
+// (after k_bd_count), the creator digest (slot 0) and each endorsement digest (slot 1 + k) of an
+// identity whose MSP hashes with SHA3 are replaced by SHA3-256 of the same message.  One lane
+// per transaction; launched only for a channel that has such identities.
+__global__ __launch_bounds__(64) void k_bd_sha3(uint32_t ntx, const DevTx *__restrict__ txs,
+                                                const uint64_t *__restrict__ bases, DevChannel ch,
+                                                const int32_t *__restrict__ ident, uint8_t *__restrict__ dig) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  const DevTx &R = txs[t];
+  const int32_t *id = ident + (size_t)t * BD_OCC;
+  const uint8_t *base = reinterpret_cast<const uint8_t *>(bases[R.blk]);
+  const int32_t ci = id[0];
+  if (ci >= 0 && ch.idents[ci].hash3) {  // Envelope.payload
+    const uint8_t *const p[3] = {base + R.payload.off, base, base};
+    const uint32_t n[3] = {R.payload.len, 0u, 0u};
+    fgvsha3::sha3_256_spans(p, n, dig + (size_t)t * 32);
+  }
+  for (uint32_t k = 0; k < R.nend && k < BD_MAX_END; k++) {  // prp || endorser
+    const int32_t e = id[1 + k];
+    if (e < 0 || !ch.idents[e].hash3) continue;
+    const uint8_t *const p[3] = {base + R.prp.off, base + R.end_ser[k].off, base};
+    const uint32_t n[3] = {R.prp.len, R.end_ser[k].len, 0u};
+    fgvsha3::sha3_256_spans(p, n, dig + ((size_t)(1 + k) * ntx + t) * 32);
+  }
 }

@@ -112,6 +112,7 @@ struct DevImage {
   DevBuf name, idents, ibytes, itable, ihash, cc, colls, impl, msps, ccb, pol, nodes, kids, subs, prins, iou, committed,
       kvp, kvpb;
   DevChannel ch{};
+  bool has_sha3 = false;  // an identity of a SHA3 MSP: the batch runs k_bd_sha3 (fgv_front_launch)
   void release() {
     for (DevBuf *b : {&name, &idents, &ibytes, &itable, &ihash, &cc, &colls, &impl, &msps, &ccb, &pol, &nodes, &kids,
                       &subs, &prins, &iou, &committed, &kvp, &kvpb})
@@ -413,8 +414,8 @@ static void parse_tx_flow(const Channel &ch, Span d, TxRec &R) {
   if (R.creator_ident == -2) { R.pre = C_UNSUPPORTED; return; }  // unregistered certificate of a channel MSP
   if (R.creator_ident < 0) { R.pre = C_BAD_CREATOR; return; }
   const Ident &ci = ch.idents[R.creator_ident];
-  if (!ci.valid || ci.verify_class() == 1) { R.pre = C_BAD_CREATOR; return; }
-  if (ci.verify_class() == 2) { R.pre = C_UNSUPPORTED; return; }  // P-384 key / SHA3 MSP
+  if (!ci.valid || ci.verify_class_tx() == 1) { R.pre = C_BAD_CREATOR; return; }
+  if (ci.verify_class_tx() == 2) { R.pre = C_UNSUPPORTED; return; }  // P-384 key
   if (chdr.type != 3) return;  // CONFIG (unsupported) / CONFIG_UPDATE (7) decided in the fold
 
   // validateEndorserTransaction (msgvalidation.go:165-245)
@@ -679,7 +680,7 @@ static void count_jobs(const Channel &ch, TxRec &R) {
   if (R.disp != C_VALID) return;
   uint32_t ne = 0;
   for (const EndRec &e : R.ends)
-    if (e.ident >= 0 && ch.idents[e.ident].verify_class() == 0) ne++;
+    if (e.ident >= 0 && ch.idents[e.ident].verify_class_tx() == 0) ne++;
   R.n_ej = (uint16_t)std::min<uint32_t>(ne, 0xFFFF);
 }
 
@@ -988,6 +989,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
       if (R.n_cj) {
         R.cjob = o[0]++;
         job(R.cjob, b, R.payload);
+        if (ch.idents[R.creator_ident].hash3) J.jobs[R.cjob].pad = SHAJOB_SHA3;  // SHA3 MSP
         R.cvjob = ov0++;
         verify(R.cvjob, b, R.env_sig, ch.idents[R.creator_ident].key_slot, R.cjob);
       }
@@ -997,9 +999,10 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         uint32_t left = R.n_ej;
         for (EndRec &e2 : R.ends) {
           if (!left) break;
-          if (e2.ident < 0 || ch.idents[e2.ident].verify_class() != 0) continue;
+          if (e2.ident < 0 || ch.idents[e2.ident].verify_class_tx() != 0) continue;
           const uint32_t hj = o[3]++;
           job(hj, b, R.prp, e2.endorser);
+          if (ch.idents[e2.ident].hash3) J.jobs[hj].pad = SHAJOB_SHA3;
           e2.vjob = ov3++;
           verify(e2.vjob, b, e2.sig, ch.idents[e2.ident].key_slot, hj);
           left--;
@@ -1190,7 +1193,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
             if (e.ident < 0) continue;
             const Ident &I = ch.idents[e.ident];
             if (std::find(seen.begin(), seen.end(), I.canon) != seen.end()) continue;
-            const int vc = I.verify_class();
+            const int vc = I.verify_class_tx();
             if (vc == 2) { ids_unsup = true; return; }
             if (vc == 1 || e.vjob == UINT32_MAX || vstatus[e.vjob] != 0) continue;
             seen.push_back(I.canon);
@@ -1556,6 +1559,7 @@ static int build_dev_image(fgv_block_state *S) {
   std::vector<int32_t> iou;
   std::vector<uint8_t> ib;
   std::vector<uint64_t> ih(ch.idents.size());
+  D.has_sha3 = false;
   for (size_t i = 0; i < ch.idents.size(); i++) {
     const Ident &I = ch.idents[i];
     DevIdent &d = idents[i];
@@ -1572,14 +1576,15 @@ static int build_dev_image(fgv_block_state *S) {
     d.msp = I.msp;
     d.canon = I.canon;
     d.valid = I.valid ? 1u : 0u;
-    d.vclass = I.kind == FGV_KEY_UNDESERIALIZABLE ? 3u : (uint32_t)I.verify_class();
+    d.vclass = I.kind == FGV_KEY_UNDESERIALIZABLE ? 3u : (uint32_t)I.verify_class_tx();
+    d.hash3 = (I.hash3 && d.vclass == 0) ? 1u : 0u;
+    D.has_sha3 |= d.hash3 != 0;
     d.roles = I.roles;
     d.roles_known = I.roles_known ? 1u : 0u;
     d.ous_known = I.ous_known ? 1u : 0u;
     d.ou_off = (uint32_t)iou.size();
     d.ou_n = (uint32_t)I.ous.size();
     iou.insert(iou.end(), I.ous.begin(), I.ous.end());
-    d.pad = 0;
     ih[i] = bd_ident_hash(reinterpret_cast<const uint8_t *>(I.mspid.data()), d.msp_len,
                           reinterpret_cast<const uint8_t *>(I.id_bytes.data()), d.idb_len);
   }
@@ -1787,6 +1792,8 @@ __global__ void k_bd_ident(uint32_t ntx, const DevTx *txs, const uint64_t *bases
 __global__ void k_bd_count(uint32_t ntx, DevTx *txs, DevChannel ch, const int32_t *ident, DevJobIdx *jobs,
                            uint32_t *totals, uint32_t prio, const uint64_t *bases, BdVerifyCols vc);
 __global__ void k_bd_sha(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
+__global__ void k_bd_sha3(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
+                          uint8_t *dig);
 __global__ void k_bd_sha2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig, unsigned long long *nblk);
 __global__ void k_bd_sha_p2(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig,
                             unsigned long long *nblk);
@@ -2170,7 +2177,10 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
                        c->stream3, N, dtx, dbs, B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 6));
   HIP_TRY(hipEventRecord(B.ev[2], c->stream3));
   HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[1], 0));
-  HIP_TRY(hipEventRecord(B.ev[8], c->stream3));
+  // a channel with SHA3 MSP identities: their digests are replaced once the identities are known
+  // (after k_bd_count, below), and the digests join there instead
+  const bool sha3 = S->dimg.has_sha3;
+  if (!sha3) HIP_TRY(hipEventRecord(B.ev[8], c->stream3));
   if (tim) HIP_TRY(hipEventRecord(B.ev[7], sf));
   if (!fused_ident)
     hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 * BD_ID_PAR + 255) / 256)), dim3(256), 0, sf, N,
@@ -2195,6 +2205,13 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
                      B.jobs.as<DevJobIdx>(), misc, front_prio, dbs, vc);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(B.ev[6], sf));
+  if (sha3) {
+    HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[6], 0));
+    hipLaunchKernelGGL(k_bd_sha3, dim3((N + 63) / 64), dim3(64), 0, c->stream3, N, dtx, dbs, ch,
+                       (const int32_t *)B.ident.as<int32_t>(), B.dig.as<uint8_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(B.ev[8], c->stream3));
+  }
   B.N = N;
   if (prefix) return emit_prefix(c, S, B, sf);
   return FGV_OK;

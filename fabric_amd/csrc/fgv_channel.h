@@ -53,6 +53,14 @@ struct Ident {
     if (kind != FGV_KEY_P256 || hash3 || key_slot < 0) return 2;
     return 0;
   }
+  // the same for the committer's creator and endorsement signatures, whose digests follow the
+  // identity's hash family (SHA3 MSPs included since round 5: the SHA3-256 digest pass); the
+  // other Verify callers (orderer signatures) keep SHA3 identities outside the engine
+  int verify_class_tx() const {
+    if (kind == FGV_KEY_OTHER) return 1;
+    if (kind != FGV_KEY_P256 || key_slot < 0) return 2;
+    return 0;
+  }
 };
 
 struct PNode {

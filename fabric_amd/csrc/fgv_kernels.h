@@ -113,8 +113,9 @@ __global__ void k_point28(uint32_t n, const uint32_t *dn, uint32_t lanes_per_ite
 struct ShaJob {  // message = span0 || span1 || span2 (absolute device addresses)
   uint64_t p[3];
   uint32_t n[3];
-  uint32_t pad;
+  uint32_t pad;   // SHAJOB_SHA3: SHA3-256 instead (an identity of a SHA3 MSP, identities.go:219-227)
 };
+#define SHAJOB_SHA3 1u
 __global__ void k_sha256_jobs(const ShaJob *jobs, uint32_t n, uint8_t *out);
 __global__ void k_sha256(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint32_t n,
                          uint8_t *out);

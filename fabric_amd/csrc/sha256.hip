@@ -6,12 +6,19 @@
 #include "fgv_kernels.h"
 
 #include "sha256_dev.h"
+#include "sha3_dev.h"
 
 __global__ __launch_bounds__(256) void k_sha256_jobs(const ShaJob *__restrict__ jobs, uint32_t n,
                                                      uint8_t *__restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const ShaJob j = jobs[i];
+  if (j.pad == SHAJOB_SHA3) {  // a SHA3 MSP's identity.Verify digest (sha3_dev.h)
+    const uint8_t *const p3[3] = {reinterpret_cast<const uint8_t *>(j.p[0]), reinterpret_cast<const uint8_t *>(j.p[1]),
+                                  reinterpret_cast<const uint8_t *>(j.p[2])};
+    fgvsha3::sha3_256_spans(p3, j.n, out + (size_t)i * 32);
+    return;
+  }
   JobView v;
   v.p[0] = reinterpret_cast<const uint8_t *>(j.p[0]);
   v.p[1] = reinterpret_cast<const uint8_t *>(j.p[1]);

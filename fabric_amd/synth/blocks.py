@@ -154,12 +154,18 @@ def chaincode_id(name: str, version: str = "") -> bytes:
 class Identity:
     """key: synth.Key (P-256) or synth.EdKey (Ed25519, config C5)."""
 
-    def __init__(self, key, mspid: str, pem: bytes, role: str):
+    def __init__(self, key, mspid: str, pem: bytes, role: str, hash_family: str = "SHA2"):
         self.key, self.mspid, self.pem, self.role = key, mspid, pem, role
+        self.hash_family = hash_family  # the MSP's SignatureHashFamily (identities.go:219-227)
         self.kind = getattr(key, "kind", "p256")
         self.serialized = serialized_identity(mspid, pem)
         der = _pem_to_der(pem)
         self.id_digest = hashlib.sha256(der).digest()  # identity Id = hex(SHA-256(cert.Raw))
+
+
+def verify_digest(ident, msg: bytes) -> bytes:
+    """what identity.Verify hashes msg to: SHA3-256 for an MSP whose hash family is SHA3"""
+    return hashlib.sha3_256(msg).digest() if ident.hash_family == "SHA3" else hashlib.sha256(msg).digest()
 
 
 def _pem_to_der(pem: bytes) -> bytes:
@@ -174,10 +180,13 @@ class Network:
     and number of the peers that hold Ed25519 keys (config C5, "Fabric v3" identities)."""
 
     def __init__(self, seed=3, orgs=3, clients=100, channel="testchannel", policy_n=2, pems=None,
-                 peers_per_org=1, ed25519_frac=0.0, ed25519_peers=0):
+                 peers_per_org=1, ed25519_frac=0.0, ed25519_peers=0, hash_families=None):
         """pems: certificates exported by another process (Network.export_pems()) -- X.509
-        signatures are randomised, so multi-process users share one set of certificates."""
+        signatures are randomised, so multi-process users share one set of certificates.
+        hash_families: {mspid: "SHA3"} -- that MSP's identities sign SHA3-256 digests (its
+        channel config must say so: chanconfig.make_config(hash_families=...))."""
         self.seed, self.channel, self.policy_n = seed, channel, policy_n
+        self.hash_families = dict(hash_families or {})
         _pem_iter = iter(pems) if pems is not None else None
         sel = random.Random(seed * 7919 + 17)
 
@@ -230,6 +239,8 @@ class Network:
         fk = Key(seed, 40_002)
         self.forged = Identity(fk, self.mspids[0], cert(fk, rogue_ca, "forged", self.mspids[0], "ca.rogue",
                                                              False, 8), "peer")
+        for ident in self.peers + self.clients + [self.forged]:
+            ident.hash_family = self.hash_families.get(ident.mspid, "SHA2")
         self.chaincodes = {"mycc": out_of_policy(policy_n, self.mspids)}
 
     def export_pems(self):
@@ -251,9 +262,11 @@ class Network:
             if ident.kind != "p256":
                 out.append((ident.serialized, Identity(ident.mspid, None, True, ident.id_digest, key="undeserializable")))
                 continue
-            out.append((ident.serialized, Identity(ident.mspid, ident.key.pub, True, ident.id_digest, roles=1 | role_bit)))
+            out.append((ident.serialized, Identity(ident.mspid, ident.key.pub, True, ident.id_digest, roles=1 | role_bit,
+                                                   hash_family=ident.hash_family)))
         out.append((self.forged.serialized, Identity(self.forged.mspid, self.forged.key.pub, False,
-                                                     self.forged.id_digest, roles=0)))
+                                                     self.forged.id_digest, roles=0,
+                                                     hash_family=self.forged.hash_family)))
         return out
 
     def identities_legacy(self):
@@ -412,7 +425,7 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
                 ed_refs.append((t, j))
                 continue
             e_privs.append(e.key.priv)
-            e_digests.append(hashlib.sha256(t.prp + e.serialized).digest())
+            e_digests.append(verify_digest(e, t.prp + e.serialized))
             e_refs.append((t, j))
     esigs = sign_batch(b"".join(e_privs), b"".join(e_digests), len(e_privs), threads=threads) if e_privs else []
     for t in txs:
@@ -437,7 +450,7 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
             t.payload = t.payload[:-3]  # truncated -> Payload unmarshal error
         if t.creator.kind == "p256":
             c_privs.append(t.creator.key.priv)
-            c_digests.append(hashlib.sha256(t.payload).digest())
+            c_digests.append(verify_digest(t.creator, t.payload))
     csigs = sign_batch(b"".join(c_privs), b"".join(c_digests), len(c_privs), threads=threads,
                        high_s=False) if c_privs else []
     ed_tx = [t for t in txs if t.creator.kind != "p256"]

@@ -55,7 +55,7 @@ class Ident:
     key: KEY_P256 (verified on the GPU), KEY_P384 (bccsp verifies it: outside the engine ->
     Unsupported when a verify is needed), KEY_OTHER (RSA...: Verify fails),
     KEY_UNDESERIALIZABLE (e.g. Ed25519 under Fabric 2.x: DeserializeIdentity fails, F4).
-    hash: the MSP's SignatureHashFamily (identities.go:219-227); SHA3 -> Unsupported.
+    hash: the MSP's SignatureHashFamily (identities.go:219-227): SHA2 -> SHA-256, SHA3 -> SHA3-256.
     roles: bit r <=> msp.SatisfiesPrincipal(id, ROLE{mspid, r}) (MEMBER 0, ADMIN 1, CLIENT 2,
     PEER 3, ORDERER 4; msp/mspimpl.go:331-376, 477-660); None = unknown (legacy registration)."""
 
@@ -191,16 +191,27 @@ class ChannelModel:
             self._msp_models = msps_of_config(self.config_msps) if self.policies is not None else {}
         return self._msp_models
 
+    # the engine digests SHA3 identities' messages for the committer's creator and endorsement
+    # signatures only (its orderer-signature path keeps them outside the model):
+    # blockverify.block_signatures_ok clears this while it evaluates
+    sha3_verify = True
+
     def verify(self, ident, msg, sig):
-        """identity.Verify: 0 iff valid (msp/identities.go:170-199)."""
+        """identity.Verify: 0 iff valid (msp/identities.go:170-199): the digest follows the
+        MSP's SignatureHashFamily (getHashOpt :219-227: SHA2 -> SHA-256, SHA3 -> SHA3-256)."""
         self.verify_calls += 1
         if ident.key == KEY_OTHER:
             return 5
-        if ident.key != KEY_P256 or ident.hash_family != "SHA2":
-            raise Unsupported("P-384 key or SHA3 hash family")
+        if ident.key != KEY_P256:
+            raise Unsupported("P-384 key")
+        if ident.hash_family == "SHA3" and not self.sha3_verify:
+            raise Unsupported("SHA3 identity outside the committer's signatures")
+        if ident.hash_family not in ("SHA2", "SHA3"):
+            raise Unsupported("hash family %r" % ident.hash_family)
         if not sig:
             return 6
-        return verify_der(ident.pub[:32], ident.pub[32:], sig, sha256(msg))
+        digest = hashlib.sha3_256(msg).digest() if ident.hash_family == "SHA3" else sha256(msg)
+        return verify_der(ident.pub[:32], ident.pub[32:], sig, digest)
 
     def channel_policy(self, ref):
         """ChannelPolicyReferenceProviderImpl -> ManagerImpl.GetPolicy (policy.go:330-358)"""
