@@ -174,6 +174,8 @@ struct MspModel {
   bool node_ous = false;
   RoleOU role_ou[5];
   std::vector<std::vector<uint8_t>> admins;  // sanitized admin certificates
+  std::vector<fgvx::Crl> crls;               // the MSP's revocation lists
+  std::vector<std::vector<uint8_t>> crl_ok;  // [crl][ca]: the CA signed the CRL (its SKI = the AKI)
 
   // the CA whose subject is x's issuer: index, -1 none, -2 several (x509 could build several
   // chains: outside the model)
@@ -192,7 +194,13 @@ struct MspModel {
   void build(fgv_ctx *c, const std::string &conf) {
     VMspCfg fc;
     if (!pbw::decode(reinterpret_cast<const uint8_t *>(conf.data()), conf.size(), fc)) return fail();
-    if (!fc.crls.empty()) return fail();
+    // setupCRLs (mspimplsetup.go:215-245): a CRL x509.ParseCRL rejects fails the setup; shapes
+    // outside oracle/crl.py's model leave the MSP to the reference
+    for (const Span &x : fc.crls) {
+      fgvx::Crl crl;
+      if (fgvx::parse_crl(x.p, x.n, crl) != fgvx::X_OK) return fail();
+      crls.push_back(std::move(crl));
+    }
     VCryptoCfg cc;
     if (!decode_all(fc.crypto, cc)) return fail();
     if (!cc.idhash.eq("SHA256", 6) && cc.idhash.n) return fail();
@@ -250,6 +258,45 @@ struct MspModel {
       for (uint8_t v : st)
         if (v != 0) return fail();
     }
+    // CheckCRLSignature of every CRL by each CA whose SubjectKeyIdentifier is the CRL's
+    // AuthorityKeyIdentifier (validateCertAgainstChain consults only those): ECDSA over SHA-256 of
+    // the TBSCertList with the re-marshalled (r, s), high S accepted -- one GPU pass
+    crl_ok.assign(crls.size(), std::vector<uint8_t>(cas.size(), 0));
+    {
+      std::vector<uint8_t> cm, cs;
+      std::vector<uint64_t> cmo, cso;
+      std::vector<uint32_t> cml, csl, csl_slots;
+      std::vector<std::pair<size_t, size_t>> who;
+      for (size_t i = 0; i < crls.size(); i++)
+        for (size_t j = 0; j < cas.size(); j++) {
+          const fgvx::Cert &ca = cas[j].c;
+          const fgvx::Crl &x = crls[i];
+          if (!ca.has_ski || ca.ski_len != x.aki.size() ||
+              !std::equal(x.aki.begin(), x.aki.end(), ca.der.begin() + ca.ski_off) || !x.rs_ok)
+            continue;
+          uint8_t s2[32];
+          memcpy(s2, x.s, 32);
+          fgvx::to_low_s(s2);
+          const std::vector<uint8_t> low = fgvx::der_sig(x.r, s2);
+          cmo.push_back(cm.size());
+          cm.insert(cm.end(), x.der.begin() + x.tbs_off, x.der.begin() + x.tbs_off + x.tbs_len);
+          cml.push_back((uint32_t)x.tbs_len);
+          cso.push_back(cs.size());
+          cs.insert(cs.end(), low.begin(), low.end());
+          csl.push_back((uint32_t)low.size());
+          csl_slots.push_back(cas[j].slot);
+          who.push_back({i, j});
+        }
+      std::vector<uint8_t> cst(who.size(), 0);  // (c NULL, the sanitizer probe: taken as verified)
+      if (c && !who.empty() &&
+          fgv_verify_msgs_slots_locked(c, cm.data(), cm.size(), cmo.data(), cml.data(), cs.data(), cs.size(), cso.data(),
+                                       csl.data(), csl_slots.data(), who.size(), cst.data()) != FGV_OK)
+        return fail();
+      for (size_t q = 0; q < who.size(); q++) crl_ok[who[q].first][who[q].second] = cst[q] == 0;
+    }
+    // finalizeSetupCAs -> validateCAIdentity: a revoked intermediate CA fails the setup
+    for (size_t i = 0; i < cas.size(); i++)
+      if (!cas[i].root && revoked(cas[i].c, cas[i].chain[1])) return fail();
     for (CA &a : cas) {
       if (!a.root)
         for (size_t k = 1; k < a.chain.size(); k++) cas[a.chain[k]].internal = true;
@@ -301,6 +348,13 @@ struct MspModel {
     }
   }
   void fail() { unsup = true; }
+  // validateCertAgainstChain's CRL loop (mspimplvalidate.go:94-140): c's serial revoked by a CRL
+  // that its issuing CA (cas[issuer]) signed
+  bool revoked(const fgvx::Cert &c, int issuer) const {
+    for (size_t i = 0; i < crls.size(); i++)
+      if (crl_ok[i][issuer] && crls[i].revokes(c)) return true;
+    return false;
+  }
   bool has(int role, const fgvx::Cert &c) const {
     const RoleOU &ro = role_ou[role];
     return ro.present && std::find(c.ous.begin(), c.ous.end(), ro.name) != c.ous.end();
@@ -461,6 +515,7 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
     // then the OUs (validateIdentityOUsV142) with the chain above the identity as certifier
     const CA &issuer = m.cas[p.p1];
     bool valid = !issuer.internal && issuer.c.has_ski;
+    if (valid && !m.crls.empty() && m.revoked(p.c, p.p1)) valid = false;  // revoked (CRLs)
     const Dig &cid = issuer.chain_id;
     if (valid && !m.ou_ids.empty()) {
       bool any = false;

@@ -253,6 +253,8 @@ void parse(Cert &c) {
   c.version = 3;
   const T serial = t.elem(0x02);  // ReadASN1Integer(*big.Int)
   if (!int_minimal(b, serial.cs, serial.ce)) perr();
+  c.serial_off = serial.cs;
+  c.serial_len = serial.ce - serial.cs;
   const T alg = t.elem(0x30);
   const T oalg = input.elem(0x30);
   if (alg.ce - alg.cs != oalg.ce - oalg.cs || memcmp(b + alg.cs, b + oalg.cs, alg.ce - alg.cs)) perr();
@@ -358,9 +360,11 @@ void parse(Cert &c) {
       k.rest_unread();
       c.bc_valid = true;
     } else if (x.id == 14) {  // subjectKeyIdentifier
-      v.elem(0x04);
+      const T k = v.elem(0x04);
       v.rest_unread();
       c.has_ski = true;
+      c.ski_off = k.cs;
+      c.ski_len = k.ce - k.cs;
     } else if (x.id == 15) {  // parseKeyUsageExtension: ReadASN1BitString, its first 9 bits
       const T bs = v.elem(0x03);
       bitstring_ok(b, bs);
@@ -540,6 +544,159 @@ int pem_decode(const uint8_t *p, size_t n, std::vector<uint8_t> &der) {
     der.push_back((uint8_t)(w >> 16));
     if (pad < 2) der.push_back((uint8_t)(w >> 8));
     if (pad < 1) der.push_back((uint8_t)w);
+  }
+  return X_OK;
+}
+
+namespace {
+const uint8_t OID_AKI[3] = {0x55, 0x1d, 0x23};
+const uint8_t OID_ECDSA_SHA256_B[8] = {0x2a, 0x86, 0x48, 0xce, 0x3d, 0x04, 0x03, 0x02};
+
+// AlgorithmIdentifier {OID, [NULL]} -> the OID element
+T crl_alg(const uint8_t *b, size_t s, size_t e) {
+  const std::vector<T> k = children(b, s, e);
+  if (k.empty() || !valid_oid(b, k[0])) unsup();
+  if (k.size() > 2 || (k.size() == 2 && (k[1].tag != 0x05 || k[1].ce != k[1].cs))) unsup();
+  return k[0];
+}
+void crl_time(const uint8_t *b, const T &t) {
+  if (t.tag != 0x17 && t.tag != 0x18) unsup();
+  parse_time(b, t);
+}
+// Extensions: (OID element, value element) of each {OID, [BOOLEAN], OCTET STRING}
+std::vector<std::pair<T, T>> crl_exts(const uint8_t *b, size_t s, size_t e) {
+  std::vector<std::pair<T, T>> out;
+  for (const T &x : children(b, s, e)) {
+    if (x.tag != 0x30) unsup();
+    std::vector<T> k = children(b, x.cs, x.ce);
+    if (k.size() == 3 && k[1].tag == 0x01) {
+      if (k[1].ce - k[1].cs != 1 || (b[k[1].cs] != 0x00 && b[k[1].cs] != 0xFF)) perr();  // asn1 parseBool
+      k.erase(k.begin() + 1);
+    }
+    if (k.size() != 2 || !valid_oid(b, k[0]) || k[1].tag != 0x04) unsup();
+    out.push_back({k[0], k[1]});
+  }
+  return out;
+}
+void parse_crl_der(Crl &c) {
+  const uint8_t *b = c.der.data();
+  const size_t n = c.der.size();
+  const T top = tlv(b, 0, n);
+  if (top.tag != 0x30 || top.ce != n) perr();  // "x509: trailing data after CRL"
+  const std::vector<T> t3 = children(b, top.cs, top.ce);
+  if (t3.size() != 3 || t3[0].tag != 0x30 || t3[1].tag != 0x30 || t3[2].tag != 0x03) unsup();
+  c.tbs_off = t3[0].hs;
+  c.tbs_len = t3[0].ce - t3[0].hs;
+  const std::vector<T> k = children(b, t3[0].cs, t3[0].ce);
+  size_t i = 0;
+  if (i < k.size() && k[i].tag == 0x02) {  // version (optional, default 0): 0 or 1
+    if (!int_minimal(b, k[i].cs, k[i].ce)) perr();
+    if (k[i].ce - k[i].cs != 1 || b[k[i].cs] > 1) unsup();
+    i++;
+  }
+  if (i >= k.size() || k[i].tag != 0x30) unsup();
+  crl_alg(b, k[i].cs, k[i].ce);
+  i++;
+  if (i >= k.size() || k[i].tag != 0x30) unsup();
+  for (const T &rdn : children(b, k[i].cs, k[i].ce)) {  // issuer RDNSequence
+    if (rdn.tag != 0x31) unsup();
+    for (const T &atv : children(b, rdn.cs, rdn.ce)) {
+      if (atv.tag != 0x30) unsup();
+      const std::vector<T> a = children(b, atv.cs, atv.ce);
+      if (a.size() != 2 || !valid_oid(b, a[0])) unsup();
+      if (a[1].tag != 0x13 && a[1].tag != 0x0C && a[1].tag != 0x16) unsup();
+      name_string(b, a[1]);
+    }
+  }
+  i++;
+  if (i >= k.size()) unsup();
+  crl_time(b, k[i++]);  // thisUpdate
+  if (i < k.size() && (k[i].tag == 0x17 || k[i].tag == 0x18)) crl_time(b, k[i++]);  // nextUpdate
+  if (i < k.size() && k[i].tag == 0x30) {  // revokedCertificates
+    for (const T &rc : children(b, k[i].cs, k[i].ce)) {
+      if (rc.tag != 0x30) unsup();
+      const std::vector<T> r = children(b, rc.cs, rc.ce);
+      if ((r.size() != 2 && r.size() != 3) || r[0].tag != 0x02) unsup();
+      if (!int_minimal(b, r[0].cs, r[0].ce)) perr();
+      c.serials.emplace_back(b + r[0].cs, b + r[0].ce);
+      crl_time(b, r[1]);
+      if (r.size() == 3) {
+        if (r[2].tag != 0x30) unsup();
+        crl_exts(b, r[2].cs, r[2].ce);
+      }
+    }
+    i++;
+  }
+  std::vector<std::pair<T, T>> exts;
+  if (i < k.size() && k[i].tag == 0xA0) {  // crlExtensions [0] EXPLICIT
+    const std::vector<T> in = children(b, k[i].cs, k[i].ce);
+    if (in.size() != 1 || in[0].tag != 0x30) unsup();
+    exts = crl_exts(b, in[0].cs, in[0].ce);
+    i++;
+  }
+  if (i != k.size()) unsup();
+  // exactly one AuthorityKeyIdentifier, holding only a [0] keyIdentifier
+  int naki = 0;
+  for (const auto &x : exts) {
+    if (x.first.ce - x.first.cs != 3 || memcmp(b + x.first.cs, OID_AKI, 3) != 0) continue;
+    naki++;
+    const T a = tlv(b, x.second.cs, x.second.ce);
+    if (a.tag != 0x30 || a.ce != x.second.ce) unsup();
+    const std::vector<T> ak = children(b, a.cs, a.ce);
+    if (ak.size() != 1 || ak[0].tag != 0x80) unsup();
+    c.aki.assign(b + ak[0].cs, b + ak[0].ce);
+  }
+  if (naki != 1) unsup();
+  const T alg = crl_alg(b, t3[1].cs, t3[1].ce);
+  if (alg.ce - alg.cs != 8 || memcmp(b + alg.cs, OID_ECDSA_SHA256_B, 8) != 0) unsup();
+  // signatureValue BIT STRING, no padding bits; utils.UnmarshalECDSASignature reads the first two
+  // INTEGERs of the SEQUENCE (R, S > 0, else setup fails)
+  if (t3[2].ce == t3[2].cs || b[t3[2].cs] != 0) unsup();
+  const size_t ss = t3[2].cs + 1, se = t3[2].ce;
+  T sq;
+  try {
+    sq = tlv(b, ss, se);
+  } catch (const XErr &) {
+    perr();
+  }
+  if (sq.tag != 0x30) perr();
+  const std::vector<T> rs = children(b, sq.cs, sq.ce);
+  if (rs.size() < 2 || rs[0].tag != 0x02 || rs[1].tag != 0x02) unsup();
+  bool ok = true;
+  uint8_t *out[2] = {c.r, c.s};
+  for (int q = 0; q < 2; q++) {
+    size_t a = rs[q].cs;
+    const size_t e = rs[q].ce;
+    if (!int_minimal(b, a, e)) perr();
+    if (b[a] & 0x80) perr();  // negative: "R/S must be larger than zero"
+    if (e - a == 1 && b[a] == 0) perr();  // zero
+    if (b[a] == 0) a++;
+    if (e - a > 32) {
+      ok = false;  // >= 2^256 > n: CheckCRLSignature fails
+      continue;
+    }
+    memset(out[q], 0, 32);
+    memcpy(out[q] + 32 - (e - a), b + a, e - a);
+  }
+  c.rs_ok = ok && lt_n(c.r) && lt_n(c.s);
+}
+}  // namespace
+
+int parse_crl(const uint8_t *p, size_t n, Crl &out) {
+  out = Crl();
+  static const char PFX[] = "-----BEGIN X509 CRL";
+  static const char FULL[] = "-----BEGIN X509 CRL-----";
+  if (n >= sizeof PFX - 1 && memcmp(p, PFX, sizeof PFX - 1) == 0) {
+    if (n < sizeof FULL - 1 || memcmp(p, FULL, sizeof FULL - 1) != 0) return X_UNSUP;
+    const int rc = pem_decode(p, n, out.der);
+    if (rc != X_OK) return rc == X_PARSE ? X_UNSUP : rc;
+  } else {
+    out.der.assign(p, p + n);
+  }
+  try {
+    parse_crl_der(out);
+  } catch (const XErr &e) {
+    return e.code;
   }
   return X_OK;
 }

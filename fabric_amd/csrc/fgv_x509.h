@@ -8,6 +8,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -30,6 +31,8 @@ struct Cert {
   int64_t path_len = -1;                    // basicConstraints MaxPathLen (-1: none)
   uint32_t key_usage = 0;                   // Go KeyUsage bits
   int version = 0;                          // 1..3
+  size_t serial_off = 0, serial_len = 0;    // serialNumber INTEGER content (minimal)
+  size_t ski_off = 0, ski_len = 0;          // subjectKeyIdentifier OCTET STRING content (has_ski)
   const uint8_t *tbs() const { return der.data() + tbs_off; }
   const uint8_t *sig() const { return der.data() + sig_off; }
   bool same_issuer_as_subject_of(const Cert &ca) const {
@@ -55,6 +58,25 @@ bool is_zero(const uint8_t v[32]);
 // sanitizeECDSASignedCert: the certificate re-marshalled with a low-S signature (X_UNSUP when the
 // signature is not strict DER: Go's re-marshal would differ from what this restates)
 int sanitized_raw(const Cert &c, std::vector<uint8_t> &out);
+// A certificate revocation list of an MSP (setupCRLs, mspimplsetup.go:215-245; the modelled
+// shape of oracle/crl.py): the TBSCertList bytes, its AuthorityKeyIdentifier keyIdentifier, the
+// revoked serial numbers (minimal INTEGER contents), the re-marshalled ECDSA (r, s)
+struct Crl {
+  std::vector<uint8_t> der;
+  size_t tbs_off = 0, tbs_len = 0;
+  std::vector<uint8_t> aki;
+  std::vector<std::vector<uint8_t>> serials;
+  uint8_t r[32] = {}, s[32] = {};
+  bool rs_ok = false;  // 0 < r, s < n (else CheckCRLSignature fails)
+  bool revokes(const Cert &c) const {
+    for (const auto &v : serials)
+      if (v.size() == c.serial_len && std::equal(v.begin(), v.end(), c.der.begin() + c.serial_off)) return true;
+    return false;
+  }
+};
+// x509.ParseCRL (+ setupCRLs' signature re-marshal): X_OK, X_PARSE (Go fails: the MSP does not
+// set up), X_UNSUP (outside the modelled shape)
+int parse_crl(const uint8_t *p, size_t n, Crl &out);
 // P-256 affine point on the curve (x, y < p and y^2 = x^3 - 3x + b)
 bool p256_on_curve(const uint8_t x[32], const uint8_t y[32]);
 

@@ -48,7 +48,7 @@ def msp_value(mspid, hash_family="SHA2"):
 
 
 def fabric_msp_config(mspid, root_certs=(), admins=(), ou_ids=(), node_ous=("client", "peer", "admin", "orderer"),
-                      node_ou_certs=None, hash_family="SHA2", intermediate_certs=()):
+                      node_ou_certs=None, hash_family="SHA2", intermediate_certs=(), crls=()):
     """FabricMSPConfig bytes: root CA PEMs, admin PEMs, OrganizationalUnitIdentifiers [(cert PEM,
     ou)], NodeOUs (client, peer, admin, orderer identifiers; None entries are left out; node_ous
     None = disabled; node_ou_certs: role index -> certificate PEM)"""
@@ -59,6 +59,8 @@ def fabric_msp_config(mspid, root_certs=(), admins=(), ou_ids=(), node_ous=("cli
         out += f_bytes(3, c)
     for c in admins:
         out += f_bytes(4, c)
+    for c in crls:  # revocation_list
+        out += f_bytes(5, c)
     for cert, ou in ou_ids:
         out += f_msg(7, f_bytes(1, cert) + f_str(2, ou))
     out += f_msg(8, f_str(1, hash_family) + f_str(2, "SHA256"))

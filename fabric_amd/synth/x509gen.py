@@ -90,3 +90,15 @@ def ca_cert(key: Key, cn="ca.org1", org="Org1", with_ski=True, usage=(0, 5, 6), 
     nm = name(cn, org)
     exts = [key_usage(usage), basic_constraints(True, path_len=path_len)] + ([ski(key)] if with_ski else [])
     return cert(key, issuer_key or key, nm, name(issuer_cn, org) if issuer_cn else nm, serial=serial, extensions=exts)
+
+
+def crl(signer_key: Key, issuer_cn, aki_key: Key, serials, org="Org1", high_s=False, this_update="240601000000Z"):
+    """-> PEM "X509 CRL": v2 CertificateList revoking `serials`, signed (ecdsa-with-SHA256) by
+    signer_key, its AuthorityKeyIdentifier the SKI x509gen gives aki_key's certificate"""
+    revoked = seq(*[seq(integer(v), tlv(0x17, this_update.encode())) for v in serials]) if serials else b""
+    aki = ext("551d23", seq(tlv(0x80, hashlib.sha256(aki_key.pub).digest()[:20])))
+    tbs = seq(integer(1), ALG, name(issuer_cn, org), tlv(0x17, this_update.encode()),
+              tlv(0x17, b"340101000000Z"), revoked, tlv(0xA0, seq(aki)))
+    r, s = sign_rs(signer_key, hashlib.sha256(tbs).digest(), high_s)
+    der = seq(tbs, ALG, tlv(0x03, b"\x00" + der_encode(r, s)))
+    return b"-----BEGIN X509 CRL-----\n" + base64.encodebytes(der) + b"-----END X509 CRL-----\n"

@@ -10,7 +10,8 @@ validated by the channel's MSP (bccspmsp, MSP version 1.4.3 -- Fabric v2 channel
                        KeyUsages Any; exactly one chain) -- else DeserializeIdentity fails --
                        and is re-marshalled with a low-S signature
   mspimplvalidate.go   validateIdentity: the chain again, the signing CA's SubjectKeyIdentifier
-                       must exist (validateCertAgainstChain), CRLs, validateIdentityOUsV142
+                       must exist (validateCertAgainstChain), CRLs (oracle/crl.py),
+                       validateIdentityOUsV142
                        (OrganizationalUnitIdentifiers intersection; NodeOU: exactly one of the
                        client / peer / admin / orderer OUs)
   mspimpl.go:607-680   satisfiesPrincipalInternalV142 / PreV13 for ROLE principals: MEMBER =
@@ -22,12 +23,13 @@ intermediates are internal nodes of the certification tree, and an identity whos
 internal node is invalid; the certifier identifier of a chain is SHA-256 over its certificates
 (getCertificationChainIdentifierFromChain).  x509 Verify (Go 1.21) per hop: CheckSignatureFrom,
 validity at the leaf's NotBefore + 1 s, an intermediate needs basicConstraints CA, MaxPathLen.
-Modelled MSP shapes: no CRLs, P-256 CAs, at most one candidate parent per hop, OU certificates
-that are CAs of the MSP; anything else raises Unsupported.
+Modelled MSP shapes: CRLs of the shape oracle/crl.py models, P-256 CAs, at most one candidate
+parent per hop, OU certificates that are CAs of the MSP; anything else raises Unsupported.
 """
 import hashlib
 
 from . import verify_der
+from . import crl as CRL
 from . import x509 as X
 from .protowire import decode
 from .v20 import KEY_OTHER, KEY_P256, KEY_P384, Ident, Unsupported
@@ -56,8 +58,13 @@ class MSP:
     def __init__(self, fc):
         """fc: decoded FabricMSPConfig"""
         self.name = fc.get("name", "")
-        if fc.get("revocation_list"):
-            raise Unsupported("CRLs")
+        # setupCRLs (mspimplsetup.go:215-245): a CRL x509.ParseCRL rejects fails the setup
+        self.crls = []
+        for raw in fc.get("revocation_list", []):
+            try:
+                self.crls.append(CRL.parse_crl(raw))
+            except X.ParseError:
+                raise Unsupported("a CRL the MSP does not set up with")
         cc = fc.get("crypto_config") or {}
         if cc.get("identity_identifier_hash_function", "SHA256") not in ("SHA256", ""):
             raise Unsupported("identity identifier hash")
@@ -79,6 +86,9 @@ class MSP:
             self.inter_chain[c["raw2"]] = ch
             for p in ch[1:]:
                 self.internal.add(p["raw2"])
+            # finalizeSetupCAs -> validateCAIdentity: a revoked intermediate fails the setup
+            if CRL.revoked(c, ch, self.crls, verify_der):
+                raise Unsupported("revoked intermediate CA: the MSP does not set up")
 
         # certifier identifiers: SHA-256 over the chain of the OU's certificate (a root: itself)
         def certifier(pem):
@@ -183,6 +193,9 @@ class MSP:
         # Validate: the issuer must be a leaf of the certification tree, its SKI must exist
         # (setup guarantees it), then the OUs; the certifier is the chain above the identity
         valid = chain[1]["raw2"] not in self.internal and chain[1]["ski"] is not None
+        # validateCertAgainstChain: revoked by a CRL its issuing CA signed (mspimplvalidate.go:94-140)
+        if valid and self.crls and CRL.revoked(c, chain, self.crls, verify_der):
+            valid = False
         certifier = hashlib.sha256(b"".join(x["raw2"] for x in chain[1:])).digest()
         ous = [(o, certifier) for o in c["ous"]]
         if valid and self.ou_ids:

@@ -26,7 +26,8 @@ DIRS = ["msp/testdata/" + d for d in (
     "nodeous1", "nodeous2", "nodeous3", "nodeous4", "nodeous5", "nodeous6", "nodeous7", "nodeous8",
     "nodeouadmin", "nodeouadmin2", "nodeouadmin3", "nodeouadminclient", "nodeouadminclient2",
     "nodeouorderer", "nodeouorderer2", "nodeouorderer3", "nodeousbadconf2", "mspid", "expired",
-    "badadmin", "badconfigou", "badconfigoucert", "intermediate", "intermediate2", "external", "revocation")] + \
+    "badadmin", "badconfigou", "badconfigoucert", "intermediate", "intermediate2", "external", "revocation",
+    "revocation2", "revokedica")] + \
     ["sampleconfig/msp"]
 IDENTITY_FOLDERS = ("signcerts", "admincerts", "adm", "cacerts", "intermediatecerts", "users")
 

@@ -8,7 +8,8 @@ SubjectKeyIdentifier (the MSP would not set up: outside the model).  Leaves cove
 the miss path: role OUs, two role OUs, no OU, a listed admin, a high-S CA signature, unknown
 issuer, wrong CA key, an unhandled critical extension, a CA as an identity, SAN (DNS / URI), an
 empty validity window, Ed25519, a malformed IA5 OU, not PEM, a chain through an intermediate, an
-issuer that is an internal node, a path length exceeded.  Shapes Go's pem / x509 parsers may accept
+issuer that is an internal node, a path length exceeded, CRLs (a revoked leaf, a list signed by another key, a serial revoked
+under another issuer).  Shapes Go's pem / x509 parsers may accept
 and the restatement does not model (fork_hazard_variants) must come out Unsupported, never a code."""
 import base64
 
@@ -86,7 +87,7 @@ def synthetic():
     i1 = G.ca_cert(int1, "int1.org1", issuer_key=ca4, issuer_cn="ca4.org1", serial=11)
     i2 = G.ca_cert(int2, "int2.org1", issuer_key=ca5, issuer_cn="ca5.org1", serial=12)
     r2 = G.ca_cert(ca2, "ca2.org2", org="Org2", with_ski=False)  # Org2MSP: a root without SKI
-    k = [Key(77, 100 + i) for i in range(42)]
+    k = [Key(77, 100 + i) for i in range(46)]
 
     def leaf(i, ous, issuer_key=ca1, issuer=n1, **kw):
         return G.cert(k[i], issuer_key, G.name("leaf%d" % i, ous=ous), issuer, serial=1000 + i, **kw)
@@ -145,11 +146,22 @@ def synthetic():
     # reject (negative modulus): the same verdict on every path
     add("rsa_leaf", leaf(39, ["peer"], spki=rsa_spki((1 << 2047) + 12345, 65537)), OK, True, _roles(MEMBER, PEER))
     add("rsa_leaf_bad_modulus", leaf(40, ["client"], spki=rsa_spki(-5, 3)), OK, True, _roles(MEMBER, CLIENT))
+    # CRLs (mspimplvalidate.go:94-140): CA1's list revokes leaf 41 and leaf 43 under INT1 (another
+    # issuer: its CRL would need INT1's SKI as AKI -- not revoked); a list carrying CA1's AKI but
+    # signed with CA2's key (CheckCRLSignature fails: ignored) names leaf 42; CA1 signs its list
+    # with a high-S signature, which Go's ecdsa accepts
+    add("revoked_by_crl", leaf(41, ["peer"]), OK, False, 0)
+    add("crl_signed_by_another_key", leaf(42, ["client"]), OK, True, _roles(MEMBER, CLIENT))
+    add("serial_revoked_under_another_ca", leaf(43, ["peer"], issuer_key=int1, issuer=nI1), OK, True,
+        _roles(MEMBER, PEER))
+    crls = [G.crl(ca1, "ca1.org1", ca1, [1041, 1043, 99], high_s=True),
+            G.crl(ca2, "ca1.org1", ca1, [1042])]
     out.append(("repeat", out[0][1], REPEAT, None, None))  # the same bytes again in one call
     out.append(("msp_root_without_ski", serialized_identity("Org2MSP", leaf(24, ["peer"], issuer_key=ca2,
                                                                            issuer=G.name("ca2.org2", "Org2"))),
                 UNSUP, None, None))
-    fabric = fabric_msp_config(MSPID, root_certs=[r1, r3, r4, r5], intermediate_certs=[i1, i2], admins=[listed_admin])
+    fabric = fabric_msp_config(MSPID, root_certs=[r1, r3, r4, r5], intermediate_certs=[i1, i2], admins=[listed_admin],
+                               crls=crls)
     fabric2 = fabric_msp_config("Org2MSP", root_certs=[r2])
     cfg = make_config([MSPID, "Org2MSP"], msp_configs={MSPID: fabric, "Org2MSP": fabric2})
     return cfg, out

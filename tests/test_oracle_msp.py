@@ -101,9 +101,53 @@ def test_ca_certificate_as_identity_is_outside_the_model():
 
 
 def test_msps_outside_the_model():
-    for rel in ("msp/testdata/external", "msp/testdata/revocation"):  # CRL distribution points, CRLs
+    for rel in ("msp/testdata/external",):  # CRL distribution points
         with pytest.raises(Unsupported):
             _msp(rel)
+
+
+# ---- msp/revocation_test.go (CRLs: oracle/crl.py)
+def test_revoked_identity_is_invalid():  # TestRevocation/ValidCRLSignature
+    i = _one("revocation", "signcerts")
+    assert i is not None and not i.valid and not has(i, 0)
+
+
+def test_revoked_identity_fails_an_identity_principal():  # TestIdentityPolicyPrincipalAgainstRevokedIdentity
+    assert not _one("revocation", "signcerts").valid  # (an IDENTITY principal validates first)
+
+
+def test_crl_with_a_bad_signature_revokes_nothing():  # TestRevocation/InvalidCRLSignature
+    i = _one("revocation2", "signcerts")
+    assert i is not None and i.valid
+
+
+def test_revoked_intermediate_ca_fails_setup():  # TestRevokedIntermediateCA: "CA Certificate is not valid"
+    with pytest.raises(Unsupported):
+        _msp("msp/testdata/revokedica")
+
+
+def _der_tlv(tag, body):
+    return bytes([tag]) + X._der_len(len(body)) + body
+
+
+def test_crl_signature_with_a_trailing_integer_still_revokes():  # TestRevocation/MalformedCRLSignature
+    """setupCRLs re-marshals (R, S): a signature SEQUENCE{R, S, T} still revokes"""
+    import base64
+    from oracle import crl as CRL
+    conf = decode("FabricMSPConfig", bytes.fromhex(FX["msps"]["msp/testdata/revocation"]["config"]))
+    raw = conf["revocation_list"][0]
+    der = X.pem_decode(raw)
+    t, s, e = X.tlv(der, 0)
+    top = X.children(der, s, e)
+    c = CRL.parse_crl(raw)
+    sig = _der_tlv(0x30, X._der_intb(c["r"]) + X._der_intb(c["s"]) + X._der_intb(100))
+    new = _der_tlv(0x30, der[top[0][3]:top[0][2]] + der[top[1][3]:top[1][2]] + _der_tlv(0x03, b"\x00" + sig))
+    pem = b"-----BEGIN X509 CRL-----\n" + b"\n".join(
+        base64.b64encode(new)[i:i + 64] for i in range(0, len(base64.b64encode(new)), 64)) + b"\n-----END X509 CRL-----\n"
+    conf["revocation_list"] = [pem]
+    m = MSP(conf)
+    pem_id = FX["msps"]["msp/testdata/revocation"]["identities"]["signcerts/signcert-revoked.pem"].encode()
+    assert not m.resolve(pem_id).valid
 
 
 # ---- msp/mspwithintermediatecas_test.go
