@@ -442,6 +442,7 @@ def run_block(args, world, rank, local, dev_fn):
               for k in range(NB)]
         for k, s in enumerate(st):
             s.after_next = batches[(k + 2) % NB]
+            s.after_next2 = batches[(k + 3) % NB]
         return st
 
     integ = dict(ms=0.0, ok=True)
@@ -477,9 +478,11 @@ def run_block(args, world, rank, local, dev_fn):
             shard.allgather_device(send, recv, eng=eng)
         f = bs.finalize()
         if args.presplit_early and world == 1 and not args.no_presplit:
-            # a peer walks a batch's framing once its blocks are delivered, ahead of the call
-            # before it (fgv_presplit): that call's ahead front half then skips the wait for it
+            # a peer walks a batch's framing once its blocks are delivered (fgv_presplit keeps the
+            # two latest requests): batches k+2 and k+3 after call k, so the call before each
+            # batch finds its walk done at its top and queues the batch's parse there (front_early)
             eng.presplit(bs.after_next)
+            eng.presplit(bs.after_next2)
         if s is not None:
             integ_fut.pop(s).result()
         return f
@@ -1114,8 +1117,10 @@ def main():
     ap.add_argument("--latency-reps", type=int, default=20)
     ap.add_argument("--host-parse", action="store_true", help="parse transactions on host threads (A/B)")
     ap.add_argument("--no-presplit", action="store_true", help="walk each batch's framing inside its validation call (A/B)")
-    ap.add_argument("--presplit-early", action="store_true",
-                    help="start batch k+2's framing walk (fgv_presplit) when call k returns (A/B)")
+    ap.add_argument("--presplit-early", dest="presplit_early", action="store_true", default=True,
+                    help="pre-split batches k+2 and k+3 (fgv_presplit) when call k returns (default)")
+    ap.add_argument("--no-presplit-early", dest="presplit_early", action="store_false",
+                    help="only the pipelined call's own pre-split of its next batch (A/B)")
     ap.add_argument("--shard-protocol", action="store_true",
                     help="N=1 through the multi-GPU protocol (shard_dev + finalize_flags_dev) instead of the fused call")
     args = ap.parse_args()

@@ -196,6 +196,10 @@ struct PreSplit {
     active = true;
     cv.notify_all();
   }
+  bool ready() {  // the requested split is done (no wait)
+    std::lock_guard<std::mutex> lk(mu);
+    return done;
+  }
   void join() {  // wait for the requested split (if any); the result stays readable
     if (!active) return;
     std::unique_lock<std::mutex> lk(mu);
@@ -268,7 +272,12 @@ struct BdSet {
 struct fgv_block_state {
   Channel ch;
   ThreadPool pool;
-  PreSplit pre;
+  // the two most recent pre-split requests (fgv_presplit): a call uses the one of its batch and
+  // discards those requested before it, so a caller may walk batch k+2 while batch k+1's walk
+  // waits for its call (FIFO of requests: pre_ord)
+  PreSplit pre[2];
+  uint64_t pre_ord[2] = {0, 0};
+  uint64_t pre_next = 1;
   // per-call scratch
   std::vector<TxRec> recs;
   // device image of `ch`, rebuilt when the channel model changes (the committed txid table
@@ -279,6 +288,8 @@ struct fgv_block_state {
   int parse_mode = 0;  // 0: device parse (host parser for capacity overflows), 1: host parse
   BdSet set[2];
   int ahead = -1;  // set holding a front half enqueued ahead of its call (-1: none)
+  int early = -1;  // set holding phase a of the next batch's front half, queued at the call's top
+  double early_ms = 0;  // host time of that phase a
   bool ahead_deferred = false;  // a front half to launch once the caller's finalize is queued
   fgv_ctx::NextBatch ahead_nx{};
   int ahead_cur = 0;
@@ -1859,13 +1870,31 @@ static int split_batch(ThreadPool &pool, size_t nblocks, const uint8_t *const *h
   return FGV_OK;
 }
 
+// the pending pre-split of exactly this batch, or null
+static PreSplit *pre_find(fgv_block_state *S, size_t nb, const uint8_t *const *b, const size_t *l, const uint32_t *lo,
+                          const uint32_t *hi) {
+  for (PreSplit &P : S->pre)
+    if (P.active && P.matches(nb, b, l, lo, hi)) return &P;
+  return nullptr;
+}
+
+// discard the pending pre-splits requested before P (every one: P null)
+static void pre_discard_older(fgv_block_state *S, const PreSplit *P) {
+  const uint64_t ord = P ? S->pre_ord[P - S->pre] : UINT64_MAX;
+  for (int i = 0; i < 2; i++)
+    if (&S->pre[i] != P && S->pre[i].active && S->pre_ord[i] < ord) S->pre[i].join();
+}
+
 int fgv_block_presplit(fgv_block_state *S, int device, size_t nblocks, const uint8_t *const *h_blocks,
                        const size_t *lens, const uint32_t *tx_lo, const uint32_t *tx_hi) {
-  PreSplit &P = S->pre;
   // the same batch requested again (the caller's own fgv_presplit earlier, then the call that
   // announces it as its next): the walk already running or done stands
-  if (P.active && P.matches(nblocks, h_blocks, lens, tx_lo, tx_hi)) return FGV_OK;
-  P.join();  // an earlier pre-split nobody used
+  if (pre_find(S, nblocks, h_blocks, lens, tx_lo, tx_hi)) return FGV_OK;
+  // a free slot, else the older request (discarded: nobody used it)
+  int i = !S->pre[0].active ? 0 : !S->pre[1].active ? 1 : (S->pre_ord[0] < S->pre_ord[1] ? 0 : 1);
+  PreSplit &P = S->pre[i];
+  P.join();
+  S->pre_ord[i] = S->pre_next++;
   P.device = device;
   P.blocks.assign(h_blocks, h_blocks + nblocks);
   P.lens.assign(lens, lens + nblocks);
@@ -1880,8 +1909,10 @@ int fgv_block_presplit(fgv_block_state *S, int device, size_t nblocks, const uin
 // MVCC (fgv_mvcc_validate_block): the envelope spans of `block` from a pre-split of exactly
 // this one block, if one was requested; a pre-split of another batch is left pending.
 bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t len, std::vector<Span> &out) {
-  PreSplit &P = S->pre;
-  if (!P.active || !P.matches(1, &block, &len, nullptr, nullptr)) return false;
+  PreSplit *Q = pre_find(S, 1, &block, &len, nullptr, nullptr);
+  if (!Q) return false;
+  pre_discard_older(S, Q);
+  PreSplit &P = *Q;
   P.join();
   if (P.rc != FGV_OK || P.out.ntx.size() != 1) return false;
   const uint32_t *e = P.et.as<uint32_t>();
@@ -1895,8 +1926,10 @@ bool fgv_block_take_presplit(fgv_block_state *S, const uint8_t *block, size_t le
 // envelope: block, offset, length).  Valid until the next pre-split.
 bool fgv_block_take_presplit_batch(fgv_block_state *S, size_t nb, const uint8_t *const *blocks, const size_t *lens,
                                    const uint32_t **et, const size_t **ntx, const size_t **first) {
-  PreSplit &P = S->pre;
-  if (!P.active || !P.matches(nb, blocks, lens, nullptr, nullptr)) return false;
+  PreSplit *Q = pre_find(S, nb, blocks, lens, nullptr, nullptr);
+  if (!Q) return false;
+  pre_discard_older(S, Q);
+  PreSplit &P = *Q;
   const auto t0 = std::chrono::steady_clock::now();
   P.join();
   if (presplit_log())
@@ -1958,6 +1991,37 @@ static int emit_prefix(fgv_ctx *c, fgv_block_state *S, BdSet &B, hipStream_t st)
   return FGV_OK;
 }
 
+// The front-half chain (parse, identities, counts) at wave priority 3, the verify chain's
+// (FGV_FRONT_PRIO=2: one below it).  With the front half queued behind the back half (round 4) 3
+// measured 0.572-0.575 ms per C2 step against 0.559-0.561 at 2 (r4o), 0.560-0.564 against
+// 0.557-0.562 in round 5 (r5fp); with its parse queued at the call's top (front_early, round 5)
+// 0.516-0.521 against 0.522-0.541, alternating on one box (r5f3, r5f4): 3 is the default
+static uint32_t front_prio_knob() {
+  static const uint32_t v = [] {
+    const char *e = getenv("FGV_FRONT_PRIO");
+    return e && atoi(e) == 2 ? 2u : 3u;
+  }();
+  return v;
+}
+// FGV_PARSE_LDS = transactions per workgroup of the LDS-staged walk (see front_launch_a)
+static uint32_t parse_lds_knob() {
+  static const uint32_t v = [] {
+    const char *e = getenv("FGV_PARSE_LDS");
+    const uint32_t x = e ? (uint32_t)atoi(e) : 0u;
+    return (x == 4u || x == 8u || x == 16u) ? x : 0u;
+  }();
+  return v;
+}
+// FGV_PARSE_IDENT=0: k_bd_ident as its own kernel after the LDS-staged parse (A/B); by default
+// the parse workgroups resolve their transactions' identities themselves
+static bool parse_ident_knob() {
+  static const bool v = [] {
+    const char *e = getenv("FGV_PARSE_IDENT");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 // Front half of a batch into set B, on the side streams: envelope spans (pre-split or walked
 // here), head upload, k_bd_sha_payload (stream2), k_bd_parse -> k_bd_ident -> k_bd_count ->
 // job counters in device memory (streamF), k_bd_sha (stream3).  `wait` (optional): an event the head
@@ -1966,10 +2030,69 @@ static int emit_prefix(fgv_ctx *c, fgv_block_state *S, BdSet &B, hipStream_t st)
 // `sf` carries the parse -> identities -> counts chain: the main stream for the call's own batch
 // (its back half then follows in order, with no cross-stream hop), c->streamF for a front half
 // enqueued ahead beside the current batch's back half.
-static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks, const uint8_t *const *h_blocks,
-                        const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
-                        const uint32_t *tx_hi, hipStream_t sf, hipEvent_t wait, hipEvent_t wait2 = nullptr,
-                        bool prefix = false) {
+// k_bd_ident -> k_bd_count of the batch in set B on its parse stream (front_launch_a, or _b with
+// FGV_FRONT_COUNTS_B=1)
+static int front_counts(fgv_block_state *S, BdSet &B) {
+  const uint32_t N = B.N;
+  const DevChannel ch = S->dimg.ch;
+  hipStream_t sf = B.stream;
+  const bool tim = B.timed;
+  uint32_t *misc = reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff);
+  const uint64_t *dbs = reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff);
+  DevTx *dtx = B.tx.as<DevTx>();
+  const uint32_t front_prio = front_prio_knob();
+  const bool fused_ident = parse_lds_knob() && parse_ident_knob();
+  if (tim) HIP_TRY(hipEventRecord(B.ev[7], sf));
+  if (!fused_ident)
+    hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 * BD_ID_PAR + 255) / 256)), dim3(256), 0, sf, N,
+                       dtx, dbs, ch, B.ident.as<int32_t>(), front_prio);
+  // FGV_FUSE_EMIT=0: k_bd_emit as its own kernel at the head of the back half (A/B); by default
+  // k_bd_count writes the verify jobs itself
+  static const bool fuse_emit = [] {
+    const char *e = getenv("FGV_FUSE_EMIT");
+    return !e || atoi(e) != 0;
+  }();
+  BdVerifyCols vc{nullptr, nullptr, nullptr, nullptr};
+  B.emitted = false;
+  if (fuse_emit) {
+    const size_t cap = (size_t)N * (1 + BD_MAX_END);
+    if (!B.vsig.ensure(cap * 20 + 64) || !B.vst.ensure(cap + 64)) return FGV_ENOMEM;
+    uint8_t *sp = B.vsig.as<uint8_t>();
+    vc = BdVerifyCols{reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + cap * 8),
+                      reinterpret_cast<uint32_t *>(sp + cap * 12), reinterpret_cast<uint32_t *>(sp + cap * 16)};
+    B.emitted = true;
+  }
+  hipLaunchKernelGGL(k_bd_count, dim3((N + 1023) / 1024), dim3(1024), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
+                     B.jobs.as<DevJobIdx>(), misc, front_prio, dbs, vc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(B.ev[6], sf));
+  return FGV_OK;
+}
+
+// FGV_FRONT_COUNTS_B=1: identities and counts queued with phase b (behind the call's back half)
+// instead of right after the parse (A/B)
+static bool counts_in_b() {
+  static const bool v = [] {
+    const char *e = getenv("FGV_FRONT_COUNTS_B");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
+// Two phases (front_launch = both): front_launch_a -- the host part, head upload, k_bd_parse and
+// the payload hashes; front_launch_b -- k_bd_sha (stream3), identities and counts.  A call may
+// queue phase a of the next batch at its top and phase b behind its own back half (front_early).
+static int front_launch_a(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks, const uint8_t *const *h_blocks,
+                          const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                          const uint32_t *tx_hi, hipStream_t sf, hipEvent_t wait, hipEvent_t wait2) {
+  // FGV_FRONT_LOG=1: host time of each phase of the enqueue, one stderr line per call (profiling aid)
+  static const bool flog = getenv("FGV_FRONT_LOG") && atoi(getenv("FGV_FRONT_LOG"));
+  using fclk = std::chrono::steady_clock;
+  const auto ft0 = fclk::now();
+  double fts[6] = {};
+  auto fmark = [&](int i) {
+    if (flog) fts[i] = std::chrono::duration<double, std::micro>(fclk::now() - ft0).count();
+  };
   B.vdone = false;
   B.hb.assign(h_blocks, h_blocks + nblocks);
   B.db.assign(d_blocks, d_blocks + nblocks);
@@ -1985,18 +2108,23 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   for (auto &e : B.ev)
     if (!e) HIP_TRY(hipEventCreate(&e));
   // --- host: the batch's envelope spans, split ahead by fgv_presplit or here
-  if (S->pre.active) {
-    S->pre.join();  // (the worker is idle from here on)
-    if (S->pre.rc == FGV_OK && S->pre.matches(nblocks, h_blocks, lens, tx_lo, tx_hi)) {
-      B.so = std::move(S->pre.out);
-      std::swap(B.head, S->pre.et);  // (B's old head: no copy from it is pending)
-      B.presplit = true;
+  {
+    PreSplit *P = pre_find(S, nblocks, h_blocks, lens, tx_lo, tx_hi);
+    pre_discard_older(S, P);  // (requests before this batch's: nobody will use them)
+    if (P) {
+      P->join();  // (its worker is idle from here on)
+      if (P->rc == FGV_OK) {
+        B.so = std::move(P->out);
+        std::swap(B.head, P->et);  // (B's old head: no copy from it is pending)
+        B.presplit = true;
+      }
     }
   }
   if (!B.presplit) {
     int rc = split_batch(S->pool, nblocks, h_blocks, lens, tx_lo, tx_hi, B.so, B.head);
     if (rc) return rc;
   }
+  fmark(0);
   const size_t total = B.so.total;
   if (total == 0) return FGV_OK;
   const uint32_t N = (uint32_t)total;
@@ -2045,6 +2173,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   if (B.klhead.cap != hbuf) HIP_TRY(hipMemsetAsync(B.klhead.p, 0, B.klhead.cap, sf));  // (new memory: no stale tag)
   if (++S->klseq == 0) ++S->klseq;
   B.klseq = S->klseq;
+  fmark(1);
   const DevChannel ch = S->dimg.ch;
   B.stream = sf;
   if (wait) HIP_TRY(hipStreamWaitEvent(sf, wait, 0));
@@ -2073,6 +2202,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     HIP_TRY(hipMemcpyAsync(B.env.p, head, hbytes, hipMemcpyHostToDevice, sf));
   }
   HIP_TRY(hipEventRecord(B.ev[3], sf));
+  fmark(2);
   // [0..5) totals, [5] flags, bytes 24..32 k_bd_sha compressions, 32..40 payload compressions
   uint32_t *misc = reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff);
   const uint32_t *envtab = B.env.as<uint32_t>();
@@ -2103,13 +2233,7 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
                reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + klb_off),
                B.kllist.as<uint32_t>(),
                B.kldep.as<uint32_t>()};
-  // FGV_FRONT_PRIO=3: the front-half chain (parse, identities, counts) at the verify chain's wave
-  // priority instead of 2 (A/B: measured 0.572-0.575 ms per C2 step
-  // against 0.559-0.561 at 2, alternating on one box, r4o)
-  static const uint32_t front_prio = [] {
-    const char *e = getenv("FGV_FRONT_PRIO");
-    return e && atoi(e) == 3 ? 3u : 2u;
-  }();
+  const uint32_t front_prio = front_prio_knob();
   // every line of each envelope requested before the walk (touch_lines): measured on MI355X (C2,
   // lean harness, one box) 0.665-0.667 ms per step against 0.702-0.724 without
   // (profiles/round3_ab/parse_t*); FGV_PARSE_TOUCH=0 turns it off (A/B)
@@ -2131,18 +2255,8 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   // MI355X (C2 lean harness, one box): 8 per workgroup 1.01 ms per step against 0.67-0.71 for the
   // global walk -- the walk is bound by instruction issue per wave (8 walking lanes of 64), not
   // by the latency of its loads (profiles/round4_ab)
-  static const uint32_t parse_lds = [] {
-    const char *e = getenv("FGV_PARSE_LDS");
-    const uint32_t v = e ? (uint32_t)atoi(e) : 0u;
-    return (v == 4u || v == 8u || v == 16u) ? v : 0u;
-  }();
-  // FGV_PARSE_IDENT=0: k_bd_ident as its own kernel after the LDS-staged parse (A/B); by default
-  // the parse workgroups resolve their transactions' identities themselves
-  static const bool parse_ident = [] {
-    const char *e = getenv("FGV_PARSE_IDENT");
-    return !e || atoi(e) != 0;
-  }();
-  const bool fused_ident = parse_lds && parse_ident;
+  const uint32_t parse_lds = parse_lds_knob();
+  const bool fused_ident = parse_lds && parse_ident_knob();
   if (parse_lds)
     bd_parse_lds_launch(parse_lds, sf, N, envtab, dbs, ch, dtx, misc + 5, misc + 16, B.kl,
                         fused_ident ? B.ident.as<int32_t>() : nullptr);
@@ -2151,6 +2265,29 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
                        dbs, ch, dtx, misc + 5, misc + 16, B.kl, parse_touch | (front_prio == 3 ? 0x100u : 0u));
   HIP_TRY(hipEventRecord(B.ev[4], sf));
   if (!payload_first) HIP_TRY(launch_payload());
+  B.N = N;
+  if (!counts_in_b()) {
+    int rc = front_counts(S, B);
+    if (rc) return rc;
+  }
+  fmark(3);
+  if (flog)
+    fprintf(stderr, "[fgv] front_launch_a us: split %.1f head %.1f upload %.1f parse+payload(+counts) %.1f (N %u, %s)\n",
+            fts[0], fts[1] - fts[0], fts[2] - fts[1], fts[3] - fts[2], N, B.presplit ? "presplit" : "walked");
+  return FGV_OK;
+}
+
+static int front_launch_b(fgv_ctx *c, fgv_block_state *S, BdSet &B, bool prefix) {
+  if (B.N == 0) return FGV_OK;
+  static const bool flog = getenv("FGV_FRONT_LOG") && atoi(getenv("FGV_FRONT_LOG"));
+  const auto ft0 = std::chrono::steady_clock::now();
+  const uint32_t N = B.N;
+  const DevChannel ch = S->dimg.ch;
+  hipStream_t sf = B.stream;
+  const bool tim = B.timed;
+  uint32_t *misc = reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff);
+  const uint64_t *dbs = reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff);
+  DevTx *dtx = B.tx.as<DevTx>();
   // every other SHA-256 message is known after the parse: hashed on the third stream while
   // identities and job counts are worked out on this one
   HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[4], 0));
@@ -2181,30 +2318,10 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
   // (after k_bd_count, below), and the digests join there instead
   const bool sha3 = S->dimg.has_sha3;
   if (!sha3) HIP_TRY(hipEventRecord(B.ev[8], c->stream3));
-  if (tim) HIP_TRY(hipEventRecord(B.ev[7], sf));
-  if (!fused_ident)
-    hipLaunchKernelGGL(k_bd_ident, dim3((uint32_t)(((uint64_t)N * 16 * BD_ID_PAR + 255) / 256)), dim3(256), 0, sf, N,
-                       dtx, dbs, ch, B.ident.as<int32_t>(), front_prio);
-  // FGV_FUSE_EMIT=0: k_bd_emit as its own kernel at the head of the back half (A/B); by default
-  // k_bd_count writes the verify jobs itself
-  static const bool fuse_emit = [] {
-    const char *e = getenv("FGV_FUSE_EMIT");
-    return !e || atoi(e) != 0;
-  }();
-  BdVerifyCols vc{nullptr, nullptr, nullptr, nullptr};
-  B.emitted = false;
-  if (fuse_emit) {
-    const size_t cap = (size_t)N * (1 + BD_MAX_END);
-    if (!B.vsig.ensure(cap * 20 + 64) || !B.vst.ensure(cap + 64)) return FGV_ENOMEM;
-    uint8_t *sp = B.vsig.as<uint8_t>();
-    vc = BdVerifyCols{reinterpret_cast<uint64_t *>(sp), reinterpret_cast<uint32_t *>(sp + cap * 8),
-                      reinterpret_cast<uint32_t *>(sp + cap * 12), reinterpret_cast<uint32_t *>(sp + cap * 16)};
-    B.emitted = true;
+  if (counts_in_b()) {
+    int rc = front_counts(S, B);
+    if (rc) return rc;
   }
-  hipLaunchKernelGGL(k_bd_count, dim3((N + 1023) / 1024), dim3(1024), 0, sf, N, dtx, ch, B.ident.as<int32_t>(),
-                     B.jobs.as<DevJobIdx>(), misc, front_prio, dbs, vc);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(B.ev[6], sf));
   if (sha3) {
     HIP_TRY(hipStreamWaitEvent(c->stream3, B.ev[6], 0));
     hipLaunchKernelGGL(k_bd_sha3, dim3((N + 63) / 64), dim3(64), 0, c->stream3, N, dtx, dbs, ch,
@@ -2212,14 +2329,26 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(B.ev[8], c->stream3));
   }
-  B.N = N;
+  if (flog)
+    fprintf(stderr, "[fgv] front_launch_b us: %.1f\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - ft0).count());
   if (prefix) return emit_prefix(c, S, B, sf);
   return FGV_OK;
+}
+
+static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks, const uint8_t *const *h_blocks,
+                        const size_t *lens, const uint8_t *const *d_blocks, const uint32_t *tx_lo,
+                        const uint32_t *tx_hi, hipStream_t sf, hipEvent_t wait, hipEvent_t wait2 = nullptr,
+                        bool prefix = false) {
+  int rc = front_launch_a(c, S, B, nblocks, h_blocks, lens, d_blocks, tx_lo, tx_hi, sf, wait, wait2);
+  if (rc) return rc;
+  return front_launch_b(c, S, B, prefix);
 }
 
 // Wait for a front half enqueued ahead and forget it (its batch was not the next call's, or
 // the channel model is about to change under it).
 static void drain_ahead(fgv_ctx *c, fgv_block_state *S) {
+  if (S->early >= 0) S->ahead = S->early, S->early = -1;  // (a phase a without its phase b)
   if (S->ahead < 0) return;
   hipStreamSynchronize(c->streamF);
   hipStreamSynchronize(c->stream2);
@@ -2240,6 +2369,10 @@ static void launch_ahead(fgv_ctx *c, fgv_block_state *S, const fgv_ctx::NextBatc
   // batch's ECDSA (1) or after its fold (3) it collides with k_point28 or with the next call's own
   // kernels.  fgv_set_ahead / FGV_AHEAD select a placement (A/B).
   const int ahead_mode = c->ahead_mode;
+  if (S->early >= 0 && !(nx.n && nx.d_blocks && ahead_mode)) {
+    S->ahead = S->early, S->early = -1;
+    drain_ahead(c, S);
+  }
   if (nx.n && nx.d_blocks && ahead_mode) {
     BdSet &A = S->set[cur ^ 1];
     hipEvent_t after = (ahead_mode == 1 && c->stage_ran)   ? c->ev[6]
@@ -2257,12 +2390,16 @@ static void launch_ahead(fgv_ctx *c, fgv_block_state *S, const fgv_ctx::NextBatc
     // (with keys on the variable-base kernels the prefix stays in the call: their list and
     // counters belong to one batch at a time)
     const auto tf = clk::now();
-    if (front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait, after,
-                     prefix_ahead && c->n_vb == 0 && !c->kt_busy) == FGV_OK)
+    const bool pre = prefix_ahead && c->n_vb == 0 && !c->kt_busy;
+    const bool early = S->early == (cur ^ 1);
+    S->early = -1;
+    if ((early ? front_launch_b(c, S, A, pre)
+               : front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait,
+                              after, pre)) == FGV_OK)
       S->ahead = cur ^ 1;
     else
       drain_ahead(c, S), S->ahead = -1;  // (the next call starts it again and reports any error)
-    c->t_kern[11] = ms_since(tf);  // host time to enqueue it (its pre-split join included)
+    c->t_kern[11] = ms_since(tf) + (early ? S->early_ms : 0.0);  // host time to enqueue it (its pre-split join included)
   } else {
     c->t_kern[11] = 0;
   }
@@ -2275,6 +2412,7 @@ void fgv_block_launch_deferred_ahead(fgv_ctx *c, bool launch) {
   if (launch) {
     launch_ahead(c, S, S->ahead_nx, S->ahead_cur);
   } else {
+    if (S->early >= 0) drain_ahead(c, S);  // (phase a queued at the call's top: forgotten)
     c->t_kern[11] = 0;
   }
 }
@@ -2354,9 +2492,33 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   // host time from the end of the previous validation call to this call's first back-half kernel
   // (the caller's own work between calls included)
   c->t_gap = c->t_call_end.time_since_epoch().count() ? ms_since(c->t_call_end) : 0.0;
+  // FGV_FRONT_EARLY (default 1): when the next batch's framing walk is already done (the caller
+  // pre-split it with fgv_presplit after the previous call), its head upload, k_bd_parse and
+  // payload hashes are queued here, beside this batch's first back-half kernels, instead of behind
+  // the whole back half and finalize (~0.1 ms of host enqueue later); the rest of its front half
+  // follows where it always did (launch_ahead: front_launch_b)
+  static const bool front_early = [] {
+    const char *e = getenv("FGV_FRONT_EARLY");
+    return !e || atoi(e) != 0;
+  }();
+  S->early = -1;
+  S->early_ms = 0;
+  const auto te = clk::now();
+  const PreSplit *nxp = nx.n ? pre_find(S, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi) : nullptr;
+  if (front_early && nx.n && nx.d_blocks && c->ahead_mode == 2 && nxp && const_cast<PreSplit *>(nxp)->ready()) {
+    if (front_launch_a(c, S, S->set[cur ^ 1], nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF,
+                       nx.wait, nullptr) == FGV_OK) {
+      S->early = cur ^ 1;
+      S->early_ms = ms_since(te);
+    } else {
+      S->ahead = cur ^ 1;  // (the next call starts it again and reports any error)
+      drain_ahead(c, S);
+    }
+    c->next.n = 0;  // (its pre-split is used)
+  }
   // the next batch's framing walk, on the host worker while this batch's GPU work runs (started
   // once the first kernels of this back half are queued: the GPU gets them a few us sooner)
-  if (nx.n && !presplit_early) {
+  if (nx.n && !presplit_early && S->early < 0) {
     fgv_block_presplit(S, c->device, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi);
     c->next.n = 0;
   }

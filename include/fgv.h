@@ -407,9 +407,12 @@ int fgv_group_p256_verify_msgs(fgv_group *g, const uint8_t *keys, const uint8_t 
  * (the envelope spans) of a batch on a background host thread and returns at once; the next
  * fgv_validate_shard_dev whose batch has the same block addresses, lengths and tx_lo/tx_hi
  * uses that split instead of walking the blocks itself -- a peer splits block k+1 while
- * block k validates.  The block buffers must stay unchanged until that call.  A pre-split
- * that no call matches is discarded by the next fgv_presplit or validation call; results
- * never depend on whether a pre-split was used.  fgv_last_presplit: 1 if the last
+ * block k validates.  The block buffers must stay unchanged until that call.  The two most
+ * recent requests are kept (a peer walks batches k+2 and k+3 while batch k validates: the
+ * pipelined call before batch k+2 then finds its walk done and queues that batch's parse at
+ * its own top); a validation call uses the request of its batch and discards the requests made
+ * before it (all pending ones when none matches), and a third request discards the oldest.
+ * Results never depend on whether a pre-split was used.  fgv_last_presplit: 1 if the last
  * device-parse validation used one (diagnostic). */
 int fgv_presplit(fgv_ctx *ctx, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                  const uint32_t *tx_lo, const uint32_t *tx_hi);

@@ -423,6 +423,69 @@ def test_single_gpu_pipelined_rotation(where):
     eng.close()
 
 
+@pytest.mark.parametrize("where", ["hbm", "pinned"])
+def test_pipelined_rotation_presplit_after_next(where):
+    """The caller pre-splits the batch after next once a call returns (fgv_presplit, the
+    deliver-side walk): the following call finds that walk done and queues the next batch's head
+    upload, parse and payload hashes at its top (front_launch_a, FGV_FRONT_EARLY), the rest behind
+    its back half.  Flags equal the oracle's on every call of a rotation that also announces
+    batches it then does not call (the early half is drained and forgotten) and pre-splits batches
+    that are never announced."""
+    import time
+    import torch
+    net = network()
+    sizes = [[23, 5], [31], [9, 17, 3]]
+    sets, exps = [], []
+    for k, sz in enumerate(sizes):
+        blks = [blocks.make_block(net, n, number=1 + i, seed=900 + 10 * k + i)[0] for i, n in enumerate(sz)]
+        sets.append(blks)
+        exps.append([f for fl in _oracle(net, blks) for f in fl])
+    eng = _engine_for(net)
+    bufs, batches, keep = [], [], []
+    for blks in sets:
+        if where == "hbm":
+            arena = torch.zeros(sum((len(b) + 64 + 255) // 256 * 256 for b in blks), dtype=torch.uint8, device="cuda")
+            dp, o = [], 0
+            for b in blks:
+                arena[o:o + len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+                dp.append(arena.data_ptr() + o)
+                o += (len(b) + 64 + 255) // 256 * 256
+            keep.append(arena)
+            batches.append(eng.block_batch(blks, dp))
+        else:
+            pb = eng.host_alloc(sum(len(b) for b in blks))
+            views, o = [], 0
+            for b in blks:
+                pb.a[o:o + len(b)] = np.frombuffer(b, np.uint8)
+                views.append(pb.a[o:o + len(b)])
+                o += len(b)
+            bufs.append(pb)
+            batches.append(eng.block_batch(views))
+    torch.cuda.synchronize()
+    # (called, announced next, pre-split after the call); the announced batch is called next
+    # except at steps 5 (announced 0, calls 1) and 8 (announced 2, calls 0)
+    script = [(0, 1, 2), (1, 2, 0), (2, 0, 1), (0, 1, 2), (1, 0, 2), (1, 2, 0), (2, 0, 0), (0, 2, 1),
+              (0, 1, 1), (1, None, None)]
+    for i, (k, nx, after) in enumerate(script):
+        flags = eng.validate_blocks_pipelined(batches[k], None if nx is None else batches[nx])
+        assert list(flags) == exps[k], (i, k)
+        if after is not None:
+            eng.presplit(batches[after])
+            time.sleep(0.05)  # (the walk is done when the next call starts: the early path runs)
+    # the bench's pattern: after call k, pre-split k+2 and k+3 (both slots), no waiting
+    rot = [0, 1, 2, 0, 1, 2, 0, 1, 2, 0]
+    for i, k in enumerate(rot):
+        nx = batches[rot[i + 1]] if i + 1 < len(rot) else None
+        assert list(eng.validate_blocks_pipelined(batches[k], nx)) == exps[k], (i, k)
+        for d in (2, 3):
+            if i + d < len(rot):
+                eng.presplit(batches[rot[i + d]])
+    assert [f for fl in eng.validate_blocks(sets[2]) for f in fl] == exps[2]
+    for pb in bufs:
+        pb.close()
+    eng.close()
+
+
 def _random_records(rng, ntx, pool):
     """fgv_tx_result records honouring the engine's invariants: VALID => REACHED;
     REACHED => INDEXED with index_txid == txid."""

@@ -71,6 +71,9 @@ class Channel:
     def step(self, s):
         st = self.steps[s % self.NB]
         st.validate()
+        # as bench.py: batches k+2 and k+3 pre-split once call k returns (fgv_presplit)
+        self.eng.presplit(self.hb[(s + 2) % self.NB])
+        self.eng.presplit(self.hb[(s + 3) % self.NB])
         return st.flags
 
     def parity(self, k, flags):
