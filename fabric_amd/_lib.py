@@ -33,6 +33,7 @@ EXPORTED = [
     "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead", "fgv_blocks_verify_signed",
     "fgv_validate_blocks_pipelined", "fgv_set_timing",
     "fgv_group_init", "fgv_group_destroy", "fgv_group_size", "fgv_group_ctx", "fgv_group_validate_blocks",
+    "fgv_group_set_block_outcomes", "fgv_group_last_block_status",
     "fgv_msp_resolve", "fgv_msp_resolve_blocks", "fgv_set_auto_resolve", "fgv_msp_identity",
     "fgv_kvmeta_set", "fgv_kvmeta_count", "fgv_kvmeta_get", "fgv_msp_identity_ous", "fgv_group_p256_verify_msgs",
 ]
@@ -166,6 +167,8 @@ def load():
         L.fgv_group_ctx.argtypes = [vp, sz]
         L.fgv_group_ctx.restype = vp
         L.fgv_group_validate_blocks.argtypes = [vp, sz, vp, vp, vp, sz, vp]
+        L.fgv_group_set_block_outcomes.argtypes = [vp, ctypes.c_int]
+        L.fgv_group_last_block_status.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
         L.fgv_finalize_flags_dev_plan.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.fgv_statedb_load.argtypes = [vp, ctypes.c_char_p, vp, vp, vp, vp, vp, sz]
@@ -391,6 +394,17 @@ class Group:
             out.append(flags[o:o + ntx[i]].copy())
             o += ntx[i]
         return out
+
+    def set_block_outcomes(self, on=True):
+        """fgv_group_set_block_outcomes: per-block results instead of a whole-batch Unsupported"""
+        _check(self._L.fgv_group_set_block_outcomes(self._g, 1 if on else 0))
+
+    def last_block_status(self, nblocks):
+        """fgv_group_last_block_status -> (per-block status list, n_final), as Engine.last_block_status"""
+        st = np.zeros(nblocks, np.int32)
+        nf = ctypes.c_size_t()
+        _check(self._L.fgv_group_last_block_status(self._g, _ptr(st), nblocks, ctypes.byref(nf)))
+        return st.tolist(), nf.value
 
     def verify_msgs(self, keys, msgs, sigs):
         """fgv_group_p256_verify_msgs: Engine.verify_msgs over the group's devices"""

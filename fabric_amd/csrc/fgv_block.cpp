@@ -290,6 +290,8 @@ struct fgv_block_state {
   int ahead = -1;  // set holding a front half enqueued ahead of its call (-1: none)
   int early = -1;  // set holding phase a of the next batch's front half, queued at the call's top
   double early_ms = 0;  // host time of that phase a
+  int prefix_next = -1;  // set whose verify prefix the finish queues on the main stream (prefix_main)
+  hipEvent_t done_ev = nullptr;  // the call's own work on the main stream (the finish waits on it)
   bool ahead_deferred = false;  // a front half to launch once the caller's finalize is queued
   fgv_ctx::NextBatch ahead_nx{};
   int ahead_cur = 0;
@@ -299,11 +301,13 @@ struct fgv_block_state {
   // per-block outcomes (fgv_set_block_outcomes) of the running call: soft = report instead of
   // failing the batch; split = the first block that must wait for an earlier block's commit
   bool soft = false;
+  bool soft_unsup = false;  // the soft call marked some transaction undecided (0xFD)
   uint32_t split = UINT32_MAX;
   uint32_t klseq = 0;         // key-level bucket tags (blockdev.h KlDev::seq), one per front half
   std::chrono::steady_clock::time_point t_enq;
   explicit fgv_block_state(unsigned threads) : pool(threads) {}
   ~fgv_block_state() {
+    if (done_ev) hipEventDestroy(done_ev);
     dimg.release();
     set[0].release();
     set[1].release();
@@ -313,8 +317,10 @@ struct fgv_block_state {
 fgv_block_state *fgv_block_state_new(unsigned threads) { return new fgv_block_state(threads); }
 void fgv_block_set_soft(fgv_block_state *S, bool on) {
   S->soft = on;
+  S->soft_unsup = false;
   S->split = UINT32_MAX;
 }
+bool fgv_block_soft_unsup(fgv_block_state *S) { return S->soft_unsup; }
 uint32_t fgv_block_split(fgv_block_state *S) { return S->split; }
 Channel &fgv_block_channel(fgv_block_state *S) { return S->ch; }
 void fgv_parallel_for(fgv_block_state *S, size_t n, const std::function<void(size_t)> &f) {
@@ -1311,13 +1317,18 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   c->t_host_fold = ms_since(t_fold);
   // (from the final codes: a pass-1 verdict of a tx folded again in pass 2 does not count;
   // per-block outcomes: the codes stay, 0xFD marking the undecided transactions)
-  if (!S->soft)
-    for (size_t t = 0; t < total; t++)
-      if (res_out[t].code == C_UNSUPPORTED) return FGV_EUNSUPPORTED;
+  for (size_t t = 0; t < total; t++)
+    if (res_out[t].code == C_UNSUPPORTED) {
+      if (!S->soft) return FGV_EUNSUPPORTED;
+      S->soft_unsup = true;
+      break;
+    }
   return FGV_OK;
 }
 
-int fgv_block_kl_check(fgv_block_state *S, size_t nblocks, const uint8_t *const *blocks, const size_t *lens) {
+int fgv_block_kl_check(fgv_block_state *S, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                       uint32_t *split) {
+  if (split) *split = UINT32_MAX;
   Channel &ch = S->ch;
   if (ch.dirty) ch.compile();
   std::vector<std::vector<std::string>> chg(nblocks), tch(nblocks);
@@ -1335,7 +1346,11 @@ int fgv_block_kl_check(fgv_block_state *S, size_t nblocks, const uint8_t *const 
   for (size_t b = 0; b < nblocks; b++) {
     if (bad[b]) return FGV_EINVAL;
     for (const std::string &k : tch[b])
-      if (changed.count(k)) return FGV_EUNSUPPORTED;
+      if (changed.count(k)) {
+        if (!split) return FGV_EUNSUPPORTED;
+        *split = (uint32_t)b;  // per-block outcomes: this block and the later ones wait
+        return FGV_OK;
+      }
     changed.insert(chg[b].begin(), chg[b].end());
   }
   return FGV_OK;
@@ -2349,7 +2364,9 @@ static int front_launch(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nblocks
 // the channel model is about to change under it).
 static void drain_ahead(fgv_ctx *c, fgv_block_state *S) {
   if (S->early >= 0) S->ahead = S->early, S->early = -1;  // (a phase a without its phase b)
+  S->prefix_next = -1;
   if (S->ahead < 0) return;
+  hipStreamSynchronize(c->stream);  // (a verify prefix queued there by the last finish)
   hipStreamSynchronize(c->streamF);
   hipStreamSynchronize(c->stream2);
   hipStreamSynchronize(c->stream3);
@@ -2360,7 +2377,7 @@ void fgv_block_drain(fgv_ctx *c) { drain_ahead(c, c->blk); }
 
 // The next batch's front half, ahead of its call, while this back half runs: its device copy is
 // known (caller-resident, or being prefetched by the copy stream).
-static void launch_ahead(fgv_ctx *c, fgv_block_state *S, const fgv_ctx::NextBatch &nx, int cur) {
+static void launch_ahead(fgv_ctx *c, fgv_block_state *S, const fgv_ctx::NextBatch &nx, int cur, bool fused = false) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   // Measured on MI355X (C2, 32 x 500-tx batches, fused single-GPU call; DESIGN.md s5,
@@ -2390,13 +2407,26 @@ static void launch_ahead(fgv_ctx *c, fgv_block_state *S, const fgv_ctx::NextBatc
     // (with keys on the variable-base kernels the prefix stays in the call: their list and
     // counters belong to one batch at a time)
     const auto tf = clk::now();
-    const bool pre = prefix_ahead && c->n_vb == 0 && !c->kt_busy;
+    // FGV_PREFIX_MAIN=1 (the fused single-GPU call, without fgv_set_timing): the next batch's
+    // k_bd_emit / k_der / k_inv queued on the main stream behind this call's finalize
+    // (fgv_block_validate_dev_finish), so they start as soon as its k_fin_dups ends instead of
+    // after the host's turnaround to the next call; the finish waits on an event recorded before
+    // them.  Measured on MI355X (C2 lean harness, one box, r5pm): 0.546-0.554 ms per step against
+    // 0.516-0.522 without -- off (A/B)
+    static const bool prefix_main = [] {
+      const char *e = getenv("FGV_PREFIX_MAIN");
+      return e && atoi(e) != 0;
+    }();
+    const bool vb_free = c->n_vb == 0 && !c->kt_busy;
+    const bool pre = prefix_ahead && vb_free;
+    S->prefix_next = -1;
+    const bool pmain = !pre && prefix_main && fused && vb_free && !c->timing;
     const bool early = S->early == (cur ^ 1);
     S->early = -1;
     if ((early ? front_launch_b(c, S, A, pre)
                : front_launch(c, S, A, nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF, nx.wait,
                               after, pre)) == FGV_OK)
-      S->ahead = cur ^ 1;
+      S->ahead = cur ^ 1, S->prefix_next = pmain ? cur ^ 1 : -1;
     else
       drain_ahead(c, S), S->ahead = -1;  // (the next call starts it again and reports any error)
     c->t_kern[11] = ms_since(tf) + (early ? S->early_ms : 0.0);  // host time to enqueue it (its pre-split join included)
@@ -2410,7 +2440,7 @@ void fgv_block_launch_deferred_ahead(fgv_ctx *c, bool launch) {
   if (!S || !S->ahead_deferred) return;
   S->ahead_deferred = false;
   if (launch) {
-    launch_ahead(c, S, S->ahead_nx, S->ahead_cur);
+    launch_ahead(c, S, S->ahead_nx, S->ahead_cur, true);
   } else {
     if (S->early >= 0) drain_ahead(c, S);  // (phase a queued at the call's top: forgotten)
     c->t_kern[11] = 0;
@@ -2602,7 +2632,28 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   B.misc_src = nullptr;
   c->fin_misc_done = false;
   c->fin_misc_src = nullptr;
-  HIP_TRY(fgv_stream_wait(c->stream, c->spin));
+  const int pp = S->prefix_next;
+  S->prefix_next = -1;
+  if (pp >= 0 && S->ahead == pp && S->set[pp].N && !S->set[pp].vdone) {
+    // the next batch's verify prefix behind this call's work (prefix_main, launch_ahead)
+    if (!S->done_ev) HIP_TRY(hipEventCreateWithFlags(&S->done_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(S->done_ev, c->stream));
+    BdSet &A = S->set[pp];
+    HIP_TRY(hipStreamWaitEvent(c->stream, A.ev[6], 0));
+    if (emit_prefix(c, S, A, c->stream) != FGV_OK) {
+      drain_ahead(c, S);  // (the next call starts its batch again)
+      A.vdone = false;
+    }
+    if (c->spin) {
+      hipError_t e;
+      while ((e = hipEventQuery(S->done_ev)) == hipErrorNotReady) __builtin_ia32_pause();
+      HIP_TRY(e);
+    } else {
+      HIP_TRY(hipEventSynchronize(S->done_ev));
+    }
+  } else {
+    HIP_TRY(fgv_stream_wait(c->stream, c->spin));
+  }
   const auto t_woke = clk::now();
   fgv_read_block_job_times(c);
   {  // per-kernel device times (fgv_last_kernel_times)
@@ -2641,6 +2692,7 @@ int fgv_block_validate_dev_finish(fgv_ctx *c, fgv_block_state *S) {
   // per-block outcomes: the undecided transactions carry 0xFD in the flags, the first block that
   // must wait for an earlier one's commit comes back in word 12 (k_bd_kl)
   if (S->soft) {
+    if (hm[5] & 2u) S->soft_unsup = true;
     if (hm[12]) S->split = std::min<uint32_t>(S->split, ~hm[12]);
     return FGV_OK;
   }

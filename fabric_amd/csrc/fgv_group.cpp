@@ -28,6 +28,10 @@ struct fgv_group {
   hipStream_t s0 = nullptr; // device 0: the gather copies
   ThreadPool *pool = nullptr;
   std::mutex mu;
+  // per-block outcomes (fgv_group_set_block_outcomes) and those of the last call
+  bool soft = false;
+  std::vector<int32_t> blk_status;
+  size_t n_final = 0;
 };
 
 extern "C" {
@@ -96,6 +100,9 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
   if (!g || (nblocks && (!blocks || !lens || !flags || !ntx))) return FGV_EINVAL;
   if (nblocks == 0) return FGV_OK;
   std::lock_guard<std::mutex> lk(g->mu);
+  g->blk_status.clear();
+  g->n_final = 0;
+  const bool soft = g->soft;
   const size_t W = g->ctx.size();
   // The plan.  At least as many blocks as devices: contiguous block ranges of about total/W
   // bytes (a device stages, splits and parses only its own).  Fewer (one block, a short batch):
@@ -146,6 +153,7 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
     }
   }
   std::vector<int> rcs(W, FGV_OK);
+  std::vector<uint32_t> split(W, UINT32_MAX);  // per-block outcomes: each device's first waiting block
   std::vector<std::vector<size_t>> ntx_dev(W, std::vector<size_t>(nblocks, 0));
   g->pool->run(W, [&](size_t r) {
     if (by_tx ? nrec[r] == 0 : b0[r + 1] == b0[r]) return;
@@ -158,13 +166,23 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
       return;
     }
     // (an identity this device's registry has not seen is resolved inside, MSP cache miss)
-    if (by_tx)
+    if (soft && by_tx)
+      rcs[r] = fgv_validate_shard_dev_soft(g->ctx[r], nblocks, blocks, lens, &lo[r * nblocks], &hi[r * nblocks],
+                                           g->res[r].p, cap[r], ntx_dev[r].data(), &split[r]);
+    else if (soft)
+      rcs[r] = fgv_validate_shard_dev_soft(g->ctx[r], b0[r + 1] - b0[r], blocks + b0[r], lens + b0[r], nullptr,
+                                           nullptr, g->res[r].p, cap[r], ntx + b0[r], &split[r]);
+    else if (by_tx)
       rcs[r] = fgv_validate_shard_dev(g->ctx[r], nblocks, blocks, lens, nullptr, &lo[r * nblocks], &hi[r * nblocks],
                                       g->res[r].p, cap[r], ntx_dev[r].data());
     else
       rcs[r] = fgv_validate_shard_dev(g->ctx[r], b0[r + 1] - b0[r], blocks + b0[r], lens + b0[r], nullptr, nullptr,
                                       nullptr, g->res[r].p, cap[r], ntx + b0[r]);
   });
+  // the first block that waits for an earlier block's commit (per-block outcomes; global index)
+  size_t n_final = nblocks;
+  for (size_t r = 0; r < W; r++)
+    if (split[r] != UINT32_MAX) n_final = std::min(n_final, (by_tx ? 0 : b0[r]) + (size_t)split[r]);
   int unsup = 0;
   for (int rc : rcs) {
     if (rc == FGV_EUNSUPPORTED) unsup = 1;
@@ -181,8 +199,10 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
     // validated against the state before them (fgv_block_validate_impl's batch rule across devices)
     for (size_t r = 0; r + 1 < W; r++)
       if (b0[r + 1] > b0[r] && b0[r + 1] < nblocks && g->ctx[r]->kl_changes) {
-        const int rc = fgv_block_kl_check(g->ctx[0]->blk, nblocks, blocks, lens);  // (the whole batch, host)
+        uint32_t ks = UINT32_MAX;  // (the whole batch, host; soft: the first waiting block)
+        const int rc = fgv_block_kl_check(g->ctx[0]->blk, nblocks, blocks, lens, soft ? &ks : nullptr);
         if (rc) return rc;
+        if (ks != UINT32_MAX) n_final = std::min(n_final, (size_t)ks);
         break;
       }
     for (size_t r = 0; r < W; r++)
@@ -198,7 +218,14 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
     all += nrec[r];
   }
   if (all > flags_cap) return FGV_EINVAL;
-  if (all == 0) return FGV_OK;
+  if (all == 0) {
+    if (soft) {
+      g->blk_status.assign(nblocks, FGV_OK);
+      g->n_final = n_final;
+      for (size_t b = n_final; b < nblocks; b++) g->blk_status[b] = FGV_BLOCK_LATER;
+    }
+    return FGV_OK;
+  }
   // gather onto device 0 (rank r's rows at r x rows), then the finalize there
   if (hipSetDevice(g->dev[0]) != hipSuccess) return FGV_EDEVICE;
   if (!g->gath.ensure(W * rows * sizeof(fgv_tx_result) + 64)) return FGV_ENOMEM;
@@ -209,7 +236,41 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
                                nrec[r] * sizeof(fgv_tx_result), g->s0));
   }
   HIP_TRY(hipStreamSynchronize(g->s0));
-  return fgv_finalize_flags_dev_plan(g->ctx[0], nblocks, ntx, (uint32_t)W, rows, lo.data(), hi.data(), dst, flags);
+  const int rc = fgv_finalize_flags_dev_plan(g->ctx[0], nblocks, ntx, (uint32_t)W, rows, lo.data(), hi.data(), dst,
+                                             flags);
+  if (rc || !soft) return rc;
+  // per-block outcomes (fgv_last_block_status's rules): blocks from n_final on wait; a block with
+  // an undecided transaction (0xFD) goes to the reference; the others are final
+  g->blk_status.assign(nblocks, FGV_OK);
+  g->n_final = n_final;
+  size_t o = 0;
+  for (size_t b = 0; b < nblocks; o += ntx[b], b++) {
+    if (b >= n_final) {
+      g->blk_status[b] = FGV_BLOCK_LATER;
+      continue;
+    }
+    for (size_t t = 0; t < ntx[b]; t++)
+      if (flags[o + t] == 0xFD) {
+        g->blk_status[b] = FGV_EUNSUPPORTED;
+        break;
+      }
+  }
+  return FGV_OK;
+}
+
+int fgv_group_set_block_outcomes(fgv_group *g, int on) {
+  if (!g) return FGV_EINVAL;
+  std::lock_guard<std::mutex> lk(g->mu);
+  g->soft = on != 0;
+  return FGV_OK;
+}
+
+int fgv_group_last_block_status(fgv_group *g, int32_t *status, size_t n, size_t *n_final) {
+  if (!g || (n && !status)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> lk(g->mu);
+  for (size_t b = 0; b < n; b++) status[b] = b < g->blk_status.size() ? g->blk_status[b] : FGV_OK;
+  if (n_final) *n_final = g->n_final;
+  return FGV_OK;
 }
 
 int fgv_group_p256_verify_msgs(fgv_group *g, const uint8_t *keys, const uint8_t *msg_buf, size_t msg_buf_len,

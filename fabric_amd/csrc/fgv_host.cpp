@@ -1837,6 +1837,32 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   return rc;
 }
 
+int fgv_validate_shard_dev_soft(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                const uint32_t *tx_lo, const uint32_t *tx_hi, void *d_results, size_t results_cap,
+                                size_t *ntx, uint32_t *split) {
+  if (!c || !split || (nblocks && (!blocks || !lens || !ntx || (results_cap && !d_results)))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->next = fgv_ctx::NextBatch{};
+  bool unsup = false;
+  auto run = [&] {
+    fgv_block_set_soft(c->blk, true);
+    const int r = shard_dev_locked(c, nblocks, blocks, lens, nullptr, tx_lo, tx_hi, d_results, results_cap, ntx);
+    *split = fgv_block_split(c->blk);
+    unsup = fgv_block_soft_unsup(c->blk);
+    fgv_block_set_soft(c->blk, false);
+    return r;
+  };
+  int rc = run();
+  if (resolve_for_retry(c, rc, nblocks, blocks, lens)) {
+    rc = run();
+  } else if (rc == FGV_OK && unsup && fgv_msp_auto(c)) {
+    // identities a channel MSP may hold (the records do not say which blocks: the shard's blocks)
+    size_t reg = 0;
+    if (fgv_msp_resolve_blocks_locked(c, nblocks, blocks, lens, &reg) == FGV_OK && reg > 0) rc = run();
+  }
+  return rc;
+}
+
 int fgv_validate_shard_dev_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                                      const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
                                      void *d_results, size_t results_cap, size_t *ntx, size_t next_nblocks,

@@ -282,6 +282,13 @@ fgv_block_state *fgv_block_state_new(unsigned threads);
 // codes and a split block instead of a whole-batch FGV_EUNSUPPORTED; split = UINT32_MAX: none
 void fgv_block_set_soft(fgv_block_state *S, bool on);
 uint32_t fgv_block_split(fgv_block_state *S);
+bool fgv_block_soft_unsup(fgv_block_state *S);  // the last soft validation left a transaction undecided
+// fgv_validate_shard_dev with per-block outcomes (fgv_group's soft calls): undecided transactions
+// carry 0xFD in their records instead of failing the shard; *split = the first block of this
+// call's list that must wait for an earlier block's commit (UINT32_MAX: none)
+extern "C" int fgv_validate_shard_dev_soft(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                const uint32_t *tx_lo, const uint32_t *tx_hi, void *d_results, size_t results_cap,
+                                size_t *ntx, uint32_t *split);
 void fgv_block_state_free(fgv_block_state *s);
 
 #include <functional>
@@ -319,7 +326,10 @@ int fgv_block_identity_ous(fgv_block_state *S, const uint8_t *ser, size_t len, s
                            const size_t *ou_lens, const uint8_t *const *certifiers, const size_t *cert_lens);
 // the key-level batch rule of fgv_block_validate_impl over whole blocks (a group's device ranges
 // together): FGV_EUNSUPPORTED when a block may change the parameter of a key a later block writes
-int fgv_block_kl_check(fgv_block_state *S, size_t nblocks, const uint8_t *const *blocks, const size_t *lens);
+// split (per-block outcomes): instead of FGV_EUNSUPPORTED, the first block that must wait for an
+// earlier block's commit (UINT32_MAX: none)
+int fgv_block_kl_check(fgv_block_state *S, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                       uint32_t *split = nullptr);
 int fgv_finalize_impl(size_t nblocks, const size_t *ntx, const fgv_tx_result *res, uint8_t *flags);
 
 // Pinned host staging for one block batch's device jobs (valid until the next reserve).

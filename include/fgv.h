@@ -393,6 +393,15 @@ size_t fgv_group_size(const fgv_group *g);
 fgv_ctx *fgv_group_ctx(fgv_group *g, size_t i);
 int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                               uint8_t *flags, size_t flags_cap, size_t *ntx);
+/* Per-block outcomes of the group call (fgv_set_block_outcomes / fgv_last_block_status for one
+ * context, same statuses and rules): on, fgv_group_validate_blocks returns FGV_OK for a batch
+ * holding transactions outside the model -- each device marks them 0xFD in its records instead of
+ * failing its range, and their blocks come back FGV_EUNSUPPORTED -- and a block whose keys'
+ * key-level parameters an earlier block may change comes back FGV_BLOCK_LATER with every block
+ * after it (n_final), whether the earlier block is on the same device or on another one (a device
+ * whose blocks change key-level state: the whole batch is checked on the host). */
+int fgv_group_set_block_outcomes(fgv_group *g, int on);
+int fgv_group_last_block_status(fgv_group *g, int32_t *status, size_t n, size_t *n_final);
 /* fgv_p256_verify_msgs over all devices of the group (config C4 through the C ABI): items
  * [n r / W, n (r+1) / W) on device r, each device verifying with its own key cache; same status
  * bytes as one device.  The devices read only the message / signature byte spans their items

@@ -111,3 +111,72 @@ def test_keylevel_split_at_block_boundary(mode):
 def sbe_cases_network():
     from tests.blockfix import network
     return network()
+
+
+def _check_group(g, model, blks):
+    """_check through fgv_group_validate_blocks / fgv_group_last_block_status"""
+    got = g.validate_blocks(blks)
+    st, n_final = g.last_block_status(len(blks))
+    exp, exp_final = v20.validate_blocks_outcomes(model, blks)
+    assert n_final == exp_final
+    for b in range(len(blks)):
+        if b >= exp_final:
+            assert st[b] == _lib.BLOCK_LATER, b
+        elif exp[b] is None:
+            assert st[b] == _lib.FGV_EUNSUPPORTED, b
+            assert 0xFD in list(got[b])
+        else:
+            assert st[b] == 0, b
+            mism = [(i, int(got[b][i]), exp[b][i]) for i in range(len(exp[b])) if got[b][i] != exp[b][i]]
+            assert len(got[b]) == len(exp[b]) and not mism, (b, mism[:10])
+    return st, n_final
+
+
+@pytest.mark.parametrize("ndev", [2, 3, 7])
+def test_group_out_of_model_identity_confined_to_its_blocks(ndev):
+    """the P-384 case through fgv_group (block plan with 2 and 3 devices; 7 devices > 6 blocks:
+    the transaction-index plan): only the blocks holding the identity's transactions are
+    unsupported, on whichever device validated them; the other blocks' flags are final"""
+    net = blocks.Network(seed=3, orgs=3, clients=3000)
+    blks, creators = [], []
+    for i in range(6):
+        txs = []
+        blks.append(blocks.make_block(net, 100, number=1 + i, seed=60 + i, out_txs=txs)[0])
+        creators.append({t.creator.serialized for t in txs})
+    pick = next(ser for ser in creators[4] if [b for b in range(6) if ser in creators[b]] == [4])
+    ids = []
+    for ser, ident in net.identities():
+        if ser == pick:
+            ident = txvalidator.Identity(ident.mspid, None, True, ident.id_digest, key="p384", roles=ident.roles)
+        ids.append((ser, ident))
+    g = _lib.Group([0] * ndev)
+    try:
+        for e in g.engines:
+            txvalidator.setup_channel(e, net.channel, ids, net.chaincodes)
+        with pytest.raises(_lib.Unsupported):  # (the whole-batch contract stays the default)
+            g.validate_blocks(blks)
+        g.set_block_outcomes(True)
+        st, n_final = _check_group(g, v20.ChannelModel(net.channel, ids, net.chaincodes), blks)
+        assert n_final == 6 and st == [0, 0, 0, 0, _lib.FGV_EUNSUPPORTED, 0], st
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("ndev", [1, 2, 3])
+def test_group_keylevel_split_across_devices(ndev):
+    """block 1 sets / clears key-level parameters that block 2 writes; with 2 or 3 devices the
+    two blocks sit on different devices (block plan by bytes): blocks 0..1 final, block 2 LATER"""
+    net = sbe_cases_network()
+    ccs = {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
+    b0 = blocks.make_block(net, 40, number=1, seed=17)[0]
+    (b1, kvmeta0), (b2, _) = [sbe_cases.make_sbe_block(net, 50, 948 + k, number=2 + k) for k in range(2)]
+    g = _lib.Group([0] * ndev)
+    try:
+        for e in g.engines:
+            txvalidator.setup_channel(e, net.channel, net.identities(), ccs, kvmeta=kvmeta0)
+        g.set_block_outcomes(True)
+        model = v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=dict(kvmeta0))
+        st, n_final = _check_group(g, model, [b0, b1, b2])
+        assert n_final == 2 and st == [0, 0, _lib.BLOCK_LATER], st
+    finally:
+        g.close()
