@@ -36,9 +36,11 @@ __device__ __forceinline__ void pay_view(uint32_t ntx, uint32_t t, const uint32_
 
 __global__ __launch_bounds__(128) void k_bd_sha_payload(uint32_t ntx, const uint32_t *__restrict__ envtab,
                                                         const uint64_t *__restrict__ bases, uint8_t *__restrict__ dig,
-                                                        unsigned long long *__restrict__ nblk_total) {
-  // the longest serial chains of the batch: first in issue order
-  __builtin_amdgcn_s_setprio(2);
+                                                        unsigned long long *__restrict__ nblk_total,
+                                                        uint32_t prio) {
+  // the longest serial chains of the batch: first in issue order (FGV_PAYLOAD_PRIO)
+  if (prio == 3) __builtin_amdgcn_s_setprio(3);
+  else __builtin_amdgcn_s_setprio(2);
   __shared__ uint4 KW[2][16][64];  // [buffer][t / 4][lane]: KW[t] = W[t] + K[t] of one block
   const uint32_t lane = threadIdx.x & 63u;
   const bool sched = threadIdx.x >= 64;  // wave-uniform

@@ -1826,7 +1826,7 @@ __global__ void k_bd_sha_p2(uint32_t ntx, const DevTx *txs, const uint64_t *base
 __global__ void k_bd_sha_p3(uint32_t ntx, const DevTx *txs, const uint64_t *bases, uint8_t *dig,
                             unsigned long long *nblk);
 __global__ void k_bd_sha_payload(uint32_t ntx, const uint32_t *envtab, const uint64_t *bases, uint8_t *dig,
-                                 unsigned long long *nblk);
+                                 unsigned long long *nblk, uint32_t prio);
 __global__ void k_bd_emit(uint32_t ntx, const DevTx *txs, const uint64_t *bases, DevChannel ch, const int32_t *ident,
                           const DevJobIdx *jobs, const uint32_t *totals, uint64_t *sig_ptr, uint32_t *sig_len,
                           uint32_t *key_slot, uint32_t *dig_idx, uint32_t *nv_out);
@@ -2233,8 +2233,13 @@ static int front_launch_a(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nbloc
   auto launch_payload = [&]() -> hipError_t {
     hipError_t e = hipStreamWaitEvent(c->stream2, B.ev[3], 0);
     if (e != hipSuccess) return e;
+    // FGV_PAYLOAD_PRIO=3: the payload hashes at the front chain's wave priority (A/B; default 2)
+    static const uint32_t pay_prio = [] {
+      const char *e = getenv("FGV_PAYLOAD_PRIO");
+      return e && atoi(e) == 3 ? 3u : 2u;
+    }();
     hipLaunchKernelGGL(k_bd_sha_payload, dim3((N + 63) / 64), dim3(128), 0, c->stream2, N, envtab, dbs,
-                       B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8));
+                       B.dig.as<uint8_t>(), reinterpret_cast<unsigned long long *>(misc + 8), pay_prio);
     return hipEventRecord(B.ev[1], c->stream2);
   };
   if (payload_first) HIP_TRY(launch_payload());
@@ -2392,10 +2397,14 @@ static void launch_ahead(fgv_ctx *c, fgv_block_state *S, const fgv_ctx::NextBatc
   }
   if (nx.n && nx.d_blocks && ahead_mode) {
     BdSet &A = S->set[cur ^ 1];
-    hipEvent_t after = (ahead_mode == 1 && c->stage_ran)   ? c->ev[6]
-                       : (ahead_mode == 4 && c->stage_ran) ? c->ev[5]
-                       : ahead_mode == 3                   ? c->kev[9]
-                                                           : nullptr;
+    // (mode 2 with this batch's verifies on the variable-base kernels: after its k_prep, as mode 4 --
+    // C2 churn with the next batch pre-split ahead, lean harness: 1.239 ms per step against 1.377
+    // at once, 1.577 after the ECDSA, 1.664 after the fold; r5pe2)
+    const bool vb_now = ahead_mode == 2 && c->n_vb > 0 && c->stage_ran;
+    hipEvent_t after = (ahead_mode == 1 && c->stage_ran)               ? c->ev[6]
+                       : ((ahead_mode == 4 || vb_now) && c->stage_ran) ? c->ev[5]
+                       : ahead_mode == 3                               ? c->kev[9]
+                                                                       : nullptr;
     // FGV_PREFIX_AHEAD=1: the next batch's k_bd_emit / k_der / k_inv run ahead with its front
     // half.  Measured on MI355X (C2 lean harness, alternating on one box, profiles/round3_ab/
     // prefix_*): 0.748 / 0.753 ms per step ahead against 0.683 / 0.670 at the call -- beside the
@@ -2535,7 +2544,10 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   S->early_ms = 0;
   const auto te = clk::now();
   const PreSplit *nxp = nx.n ? pre_find(S, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi) : nullptr;
-  if (front_early && nx.n && nx.d_blocks && c->ahead_mode == 2 && nxp && const_cast<PreSplit *>(nxp)->ready()) {
+  // (not while the verifies use the variable-base kernels -- the last call's n_vb: beside them the
+  // early parse measured 1.36 ms per C2 churn step against 1.30 without, r5pc)
+  if (front_early && nx.n && nx.d_blocks && c->ahead_mode == 2 && c->n_vb == 0 && nxp &&
+      const_cast<PreSplit *>(nxp)->ready()) {
     if (front_launch_a(c, S, S->set[cur ^ 1], nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF,
                        nx.wait, nullptr) == FGV_OK) {
       S->early = cur ^ 1;
