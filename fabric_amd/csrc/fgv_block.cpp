@@ -1111,7 +1111,11 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     std::unordered_set<std::string> changed;
     for (size_t b = 0; b < nblocks && b < S->split; b++) {
       if (unknown[b]) {
-        if (!changed.empty()) return FGV_EUNSUPPORTED;
+        if (!changed.empty()) {
+          if (!S->soft) return FGV_EUNSUPPORTED;
+          S->split = (uint32_t)b;  // (another rank's block whose bytes are not here: it waits)
+          break;
+        }
         continue;
       }
       bool dep = false;

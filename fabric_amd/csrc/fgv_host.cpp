@@ -1825,28 +1825,35 @@ static int shard_dev_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *bl
   return FGV_OK;
 }
 
+static int shard_dev_outcomes(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                              const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                              void *d_results, size_t results_cap, size_t *ntx);
+
 int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                            const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
                            void *d_results, size_t results_cap, size_t *ntx) {
   if (!c || (nblocks && (!blocks || !lens || !ntx || (results_cap && !d_results)))) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   c->next = fgv_ctx::NextBatch{};
+  if (c->block_outcomes)
+    return shard_dev_outcomes(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
   int rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
   if (resolve_for_retry(c, rc, nblocks, blocks, lens))
     rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
   return rc;
 }
 
-int fgv_validate_shard_dev_soft(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
-                                const uint32_t *tx_lo, const uint32_t *tx_hi, void *d_results, size_t results_cap,
-                                size_t *ntx, uint32_t *split) {
-  if (!c || !split || (nblocks && (!blocks || !lens || !ntx || (results_cap && !d_results)))) return FGV_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  c->next = fgv_ctx::NextBatch{};
+// shard_dev_locked with per-block outcomes on (the caller holds c->mu): undecided transactions keep
+// 0xFD in their records; *split = the first block of the call's list that must wait for an earlier
+// block's commit (UINT32_MAX: none).  A soft pass that left transactions undecided resolves the
+// blocks' identities through the MSP cache-miss path and runs again, as fgv_validate_blocks does.
+static int shard_dev_soft_locked(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                 const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                                 void *d_results, size_t results_cap, size_t *ntx, uint32_t *split) {
   bool unsup = false;
   auto run = [&] {
     fgv_block_set_soft(c->blk, true);
-    const int r = shard_dev_locked(c, nblocks, blocks, lens, nullptr, tx_lo, tx_hi, d_results, results_cap, ntx);
+    const int r = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
     *split = fgv_block_split(c->blk);
     unsup = fgv_block_soft_unsup(c->blk);
     fgv_block_set_soft(c->blk, false);
@@ -1856,11 +1863,37 @@ int fgv_validate_shard_dev_soft(fgv_ctx *c, size_t nblocks, const uint8_t *const
   if (resolve_for_retry(c, rc, nblocks, blocks, lens)) {
     rc = run();
   } else if (rc == FGV_OK && unsup && fgv_msp_auto(c)) {
-    // identities a channel MSP may hold (the records do not say which blocks: the shard's blocks)
+    // identities a channel MSP may hold (the records stay on the device: the call's blocks)
     size_t reg = 0;
     if (fgv_msp_resolve_blocks_locked(c, nblocks, blocks, lens, &reg) == FGV_OK && reg > 0) rc = run();
   }
   return rc;
+}
+
+// the shard calls with fgv_set_block_outcomes on: this rank's statuses (LATER from its split on;
+// the caller marks unsupported blocks from the final flags and takes n_final's minimum over ranks)
+static int shard_dev_outcomes(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                              const uint8_t *const *d_blocks, const uint32_t *tx_lo, const uint32_t *tx_hi,
+                              void *d_results, size_t results_cap, size_t *ntx) {
+  c->blk_status.clear();
+  c->n_final = 0;
+  uint32_t sp = UINT32_MAX;
+  const int rc = shard_dev_soft_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap,
+                                       ntx, &sp);
+  if (rc) return rc;
+  c->n_final = std::min<size_t>(nblocks, sp);
+  c->blk_status.assign(nblocks, FGV_OK);
+  for (size_t b = c->n_final; b < nblocks; b++) c->blk_status[b] = FGV_BLOCK_LATER;
+  return FGV_OK;
+}
+
+int fgv_validate_shard_dev_soft(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                const uint32_t *tx_lo, const uint32_t *tx_hi, void *d_results, size_t results_cap,
+                                size_t *ntx, uint32_t *split) {
+  if (!c || !split || (nblocks && (!blocks || !lens || !ntx || (results_cap && !d_results)))) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->next = fgv_ctx::NextBatch{};
+  return shard_dev_soft_locked(c, nblocks, blocks, lens, nullptr, tx_lo, tx_hi, d_results, results_cap, ntx, split);
 }
 
 int fgv_validate_shard_dev_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
@@ -1877,9 +1910,14 @@ int fgv_validate_shard_dev_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *
   // too; a device-resident one (next_d_blocks) is read in place
   c->next = fgv_ctx::NextBatch{next_nblocks, next_blocks,   next_lens, next_lo, next_hi,
                                !next_d_blocks && !d_blocks, next_d_blocks, nullptr};
-  int rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
-  if (resolve_for_retry(c, rc, nblocks, blocks, lens))
+  int rc;
+  if (c->block_outcomes) {
+    rc = shard_dev_outcomes(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  } else {
     rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+    if (resolve_for_retry(c, rc, nblocks, blocks, lens))
+      rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  }
   if (rc == FGV_OK) stats_accumulate(c);
   c->t_call_end = std::chrono::steady_clock::now();
   if (c->next.n) {  // not started inside (host-parse path, empty batch, early error): start it now

@@ -110,3 +110,35 @@ def reorder(gathered, ntx, world, rows, plan_=None):
             off = int(cnt[r, :b].sum())
             parts.append(gathered[r * rows + off: r * rows + off + int(cnt[r, b])])
     return np.concatenate(parts) if parts else np.zeros((0, REC), np.uint8)
+
+
+UNSUPPORTED = -6  # FGV_EUNSUPPORTED
+LATER = 1  # FGV_BLOCK_LATER
+
+
+def block_outcomes(flags, ntx, n_final_local, group=None):
+    """Per-block outcomes of the shard protocol (each rank's engine with fgv_set_block_outcomes
+    on; include/fgv.h): n_final = the minimum over ranks of each rank's fgv_last_block_status
+    n_final (an all-reduce when torch.distributed is initialised; a rank's key-level walk sees only
+    its own transactions of a block), then per block of the final flags: LATER from n_final on,
+    FGV_EUNSUPPORTED where an undecided transaction (0xFD) remains, else 0 (final).  The same
+    rules as the single-GPU call (oracle/v20.py validate_blocks_outcomes)."""
+    n_final = int(n_final_local)
+    if dist.is_available() and dist.is_initialized():
+        t = torch.tensor([n_final], dtype=torch.int64)
+        if dist.get_backend(group) != "gloo":
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        n_final = int(t.item())
+    flags = np.asarray(flags, dtype=np.uint8)
+    st, o = [], 0
+    for b, n in enumerate(np.asarray(ntx, dtype=np.int64)):
+        n = int(n)
+        if b >= n_final:
+            st.append(LATER)
+        elif n and (flags[o:o + n] == 0xFD).any():
+            st.append(UNSUPPORTED)
+        else:
+            st.append(0)
+        o += n
+    return st, n_final

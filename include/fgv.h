@@ -320,8 +320,13 @@ int fgv_validate_blocks_pipelined(fgv_ctx *ctx, size_t nblocks, const uint8_t *c
  *                       [0, n_final) and call again with the rest.
  * Blocks after an unsupported one stay final: a block reads the earlier blocks' txids (every one,
  * whatever its code: checkTxIdDupsLedger, validator.go:460-481) and, through the rule above,
- * never their codes.  Single-GPU calls (the group call: fgv_group_set_block_outcomes); the shard
- * calls keep the whole-batch FGV_EUNSUPPORTED.  fgv_unsupported_stats: fallback counters since fgv_init -- calls that
+ * never their codes.  Single-GPU calls; the group call with fgv_group_set_block_outcomes; the
+ * shard calls (fgv_validate_shard_dev[_pipelined]) of the one-process-per-GPU protocol: the
+ * rank's records keep 0xFD for undecided transactions and fgv_last_block_status reports this
+ * rank's n_final (its key-level walk sees its own transactions; another rank's block whose bytes
+ * are not in the call waits behind a change) with LATER from there on -- the caller takes the
+ * minimum n_final over the ranks and marks the blocks whose final flags hold 0xFD unsupported
+ * (fabric_amd/shard.py block_outcomes).  fgv_unsupported_stats: fallback counters since fgv_init -- calls that
  * returned FGV_EUNSUPPORTED, blocks handed to the reference (whole batches included), undecided
  * transactions of per-block calls. */
 #define FGV_BLOCK_LATER 1

@@ -180,3 +180,96 @@ def test_group_keylevel_split_across_devices(ndev):
         assert n_final == 2 and st == [0, 0, _lib.BLOCK_LATER], st
     finally:
         g.close()
+
+
+def _shard_protocol_outcomes(eng, blks, shards, mode):
+    """fgv_validate_shard_dev per rank (one engine, ranks in turn) into the rank-major gathered
+    buffer, fgv_finalize_flags_dev, then shard.block_outcomes over the ranks' n_final"""
+    import numpy as np
+    import torch
+    from fabric_amd import shard
+    ntx = np.array([len((v20.decode("Block", b).get("data") or {}).get("data", [])) for b in blks], dtype=np.int64)
+    plan = shard.plan(ntx, shards, mode)
+    rows = shard.plan_rows(*plan)
+    recv = torch.zeros((shards * rows, shard.REC), dtype=torch.uint8, device="cuda")
+    batch = eng.block_batch(blks)
+    n_final = len(blks)
+    for r in range(shards):
+        eng.validate_shard_dev(batch, plan[0][r], plan[1][r], recv[r * rows:].data_ptr(), rows)
+        n_final = min(n_final, eng.last_block_status(len(blks))[1])
+    flags = eng.finalize_flags_dev(ntx, shards, rows, recv.data_ptr(), plan=None if mode == "tx" else plan)
+    st, nf = shard.block_outcomes(flags, ntx, n_final)
+    out, o = [], 0
+    for n in ntx:
+        out.append(flags[o:o + int(n)])
+        o += int(n)
+    return out, st, nf
+
+
+def _expect(model, blks, got, st, n_final, may_defer=()):
+    """may_defer: blocks the protocol may hand to the reference although the oracle decides them
+    (a dependent transaction whose metadata writer another rank validated)"""
+    exp, exp_final = v20.validate_blocks_outcomes(model, blks)
+    assert n_final == exp_final
+    for b in range(len(blks)):
+        if b >= exp_final:
+            assert st[b] == _lib.BLOCK_LATER, b
+        elif b in may_defer and st[b] == _lib.FGV_EUNSUPPORTED:
+            assert 0xFD in list(got[b])
+        elif exp[b] is None:
+            assert st[b] == _lib.FGV_EUNSUPPORTED, b
+            assert 0xFD in list(got[b])
+        else:
+            assert st[b] == 0, b
+            mism = [(i, int(got[b][i]), exp[b][i]) for i in range(len(exp[b])) if got[b][i] != exp[b][i]]
+            assert len(got[b]) == len(exp[b]) and not mism, (b, mism[:10])
+
+
+@pytest.mark.parametrize("shards,mode", [(2, "tx"), (3, "tx"), (2, "block"), (3, "block")])
+def test_shard_protocol_out_of_model_identity(shards, mode):
+    """the P-384 case through the one-process-per-GPU protocol (fgv_set_block_outcomes on the
+    ranks' engines): only the identity's block is unsupported, the others equal the oracle"""
+    net = blocks.Network(seed=3, orgs=3, clients=3000)
+    blks, creators = [], []
+    for i in range(6):
+        txs = []
+        blks.append(blocks.make_block(net, 100, number=1 + i, seed=60 + i, out_txs=txs)[0])
+        creators.append({t.creator.serialized for t in txs})
+    pick = next(ser for ser in creators[2] if [b for b in range(6) if ser in creators[b]] == [2])
+    ids = []
+    for ser, ident in net.identities():
+        if ser == pick:
+            ident = txvalidator.Identity(ident.mspid, None, True, ident.id_digest, key="p384", roles=ident.roles)
+        ids.append((ser, ident))
+    eng = _lib.Engine(0)
+    try:
+        txvalidator.setup_channel(eng, net.channel, ids, net.chaincodes)
+        eng.set_block_outcomes(True)
+        got, st, n_final = _shard_protocol_outcomes(eng, blks, shards, mode)
+        _expect(v20.ChannelModel(net.channel, ids, net.chaincodes), blks, got, st, n_final)
+        assert n_final == 6 and st == [0, 0, _lib.FGV_EUNSUPPORTED, 0, 0, 0], st
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("shards,mode", [(2, "tx"), (2, "block"), (3, "block")])
+def test_shard_protocol_keylevel_split(shards, mode):
+    """the key-level split through the shard protocol: block 0 final, block 2 LATER; block 1 final
+    with whole blocks per rank -- split by transaction index, its dependents whose metadata writer
+    is on the other rank are undecided, so it may go to the reference instead"""
+    net = sbe_cases_network()
+    ccs = {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
+    b0 = blocks.make_block(net, 40, number=1, seed=17)[0]
+    (b1, kvmeta0), (b2, _) = [sbe_cases.make_sbe_block(net, 50, 948 + k, number=2 + k) for k in range(2)]
+    eng = _lib.Engine(0)
+    try:
+        txvalidator.setup_channel(eng, net.channel, net.identities(), ccs, kvmeta=kvmeta0)
+        eng.set_block_outcomes(True)
+        got, st, n_final = _shard_protocol_outcomes(eng, [b0, b1, b2], shards, mode)
+        _expect(v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=dict(kvmeta0)), [b0, b1, b2], got, st,
+                n_final, may_defer={1} if mode == "tx" else ())
+        assert n_final == 2 and st[0] == 0 and st[2] == _lib.BLOCK_LATER, st
+        if mode == "block":
+            assert st[1] == 0, st
+    finally:
+        eng.close()

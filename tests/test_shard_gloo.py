@@ -82,3 +82,33 @@ def test_finalize_semantics_cpu():
     b2 = [rec(10, True, 1, 1), rec(0, True, 2, 2), rec(0, True, 3, 3), rec(0, True, 3, 3), rec(5, False, 3, 3)]
     flags = _lib.finalize_flags([2, 5], np.stack(b1 + b2))
     assert flags.tolist() == [0, 4, 9, 9, 0, 9, 5]
+
+
+def _outcome_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ntx = [3, 2, 4, 1]
+    flags = np.array([0, 0, 10, 0xFD, 0, 0, 0, 0, 0, 0xFD], np.uint8)  # undecided: blocks 1 and 3
+    # rank 0's key-level walk found no wait; rank 1's makes block 3 wait (its n_final = 3)
+    q.put((rank, shard.block_outcomes(flags, ntx, 4 if rank == 0 else 3)))
+    dist.destroy_process_group()
+
+
+def test_block_outcomes_world2():
+    """shard.block_outcomes: n_final is the minimum over the ranks (all-reduce), the statuses come
+    from the final flags (0xFD -> unsupported) and are the same on every rank"""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_outcome_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, (st, n_final) in out:
+        assert n_final == 3, rank
+        assert st == [0, shard.UNSUPPORTED, 0, shard.LATER], (rank, st)
+    # one process: no all-reduce
+    assert shard.block_outcomes(np.zeros(3, np.uint8), [1, 1, 1], 3) == ([0, 0, 0], 3)
