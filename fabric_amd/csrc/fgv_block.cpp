@@ -2607,7 +2607,14 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
     const char *e = getenv("FGV_FOLD_TOUCH");
     return e ? (uint32_t)atoi(e) : 0u;
   }();
-  hipLaunchKernelGGL(k_bd_fold, dim3((N + 255) / 256), dim3(256), 0, st, N, dtx, dbs, ch, did, dj, misc,
+  // FGV_FOLD_WG = threads per workgroup of the fold (64 / 128 / 256, default 256; A/B: a lane per
+  // transaction, latency-bound, so smaller workgroups spread the same waves over more CUs)
+  static const uint32_t fold_wg = [] {
+    const char *e = getenv("FGV_FOLD_WG");
+    const uint32_t v = e ? (uint32_t)atoi(e) : 256u;
+    return (v == 64u || v == 128u) ? v : 256u;
+  }();
+  hipLaunchKernelGGL(k_bd_fold, dim3((N + fold_wg - 1) / fold_wg), dim3(fold_wg), 0, st, N, dtx, dbs, ch, did, dj, misc,
                      B.dig.as<uint8_t>(), B.vst.as<uint8_t>(), d_res, misc + 5, misc + 16, fin, B.kl,
                      fold_touch);
   HIP_TRY(hipGetLastError());
