@@ -228,6 +228,7 @@ struct BdSet {
   // so that k_bd_emit -> k_der -> k_inv of a batch can run ahead with its front half (vdone)
   DevBuf vsig, vst, vr, vs, vw, vscr;
   bool vdone = false;
+  uint32_t prio = 2;  // the front chain's wave priority for this batch (front_launch_a)
   bool emitted = false;  // k_bd_count wrote the verify jobs (FGV_FUSE_EMIT, default): no k_bd_emit
   uint32_t klseq = 0;                   // the bucket tag of the batch this set holds
   KlDev kl{};
@@ -2059,7 +2060,7 @@ static int front_counts(fgv_block_state *S, BdSet &B) {
   uint32_t *misc = reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + B.moff);
   const uint64_t *dbs = reinterpret_cast<const uint64_t *>(B.env.as<uint8_t>() + B.eoff);
   DevTx *dtx = B.tx.as<DevTx>();
-  const uint32_t front_prio = front_prio_knob();
+  const uint32_t front_prio = B.prio;
   const bool fused_ident = parse_lds_knob() && parse_ident_knob();
   if (tim) HIP_TRY(hipEventRecord(B.ev[7], sf));
   if (!fused_ident)
@@ -2257,7 +2258,8 @@ static int front_launch_a(fgv_ctx *c, fgv_block_state *S, BdSet &B, size_t nbloc
                reinterpret_cast<uint32_t *>(B.env.as<uint8_t>() + klb_off),
                B.kllist.as<uint32_t>(),
                B.kldep.as<uint32_t>()};
-  const uint32_t front_prio = front_prio_knob();
+  B.prio = front_prio_knob();
+  const uint32_t front_prio = B.prio;
   // every line of each envelope requested before the walk (touch_lines): measured on MI355X (C2,
   // lean harness, one box) 0.665-0.667 ms per step against 0.702-0.724 without
   // (profiles/round3_ab/parse_t*); FGV_PARSE_TOUCH=0 turns it off (A/B)
@@ -2401,10 +2403,15 @@ static void launch_ahead(fgv_ctx *c, fgv_block_state *S, const fgv_ctx::NextBatc
   }
   if (nx.n && nx.d_blocks && ahead_mode) {
     BdSet &A = S->set[cur ^ 1];
-    // (mode 2 with this batch's verifies on the variable-base kernels: after its k_prep, as mode 4 --
-    // C2 churn with the next batch pre-split ahead, lean harness: 1.239 ms per step against 1.377
-    // at once, 1.577 after the ECDSA, 1.664 after the fold; r5pe2)
-    const bool vb_now = ahead_mode == 2 && c->n_vb > 0 && c->stage_ran;
+    // (mode 2 with this batch's verifies on the variable-base kernels, or with the next batch's H2D
+    // copy still in flight: after this batch's k_prep, as mode 4 -- C2 churn with the next batch
+    // pre-split ahead, lean harness: 1.239 ms per step against 1.377 at once, 1.577 after the
+    // ECDSA, 1.664 after the fold, r5pe2; C2 PCIe-inclusive: 1.123 ms against 1.251 at once, r5pcie5)
+    static const bool copy_after = [] {  // FGV_COPY_AFTER=0: a copy-pending batch's front half at once (A/B)
+      const char *e = getenv("FGV_COPY_AFTER");
+      return !e || atoi(e) != 0;
+    }();
+    const bool vb_now = ahead_mode == 2 && (c->n_vb > 0 || (copy_after && nx.wait)) && c->stage_ran;
     hipEvent_t after = (ahead_mode == 1 && c->stage_ran)               ? c->ev[6]
                        : ((ahead_mode == 4 || vb_now) && c->stage_ran) ? c->ev[5]
                        : ahead_mode == 3                               ? c->kev[9]
@@ -2550,7 +2557,7 @@ int fgv_block_validate_dev_enqueue(fgv_ctx *c, fgv_block_state *S, size_t nblock
   const PreSplit *nxp = nx.n ? pre_find(S, nx.n, nx.blocks, nx.lens, nx.lo, nx.hi) : nullptr;
   // (not while the verifies use the variable-base kernels -- the last call's n_vb: beside them the
   // early parse measured 1.36 ms per C2 churn step against 1.30 without, r5pc)
-  if (front_early && nx.n && nx.d_blocks && c->ahead_mode == 2 && c->n_vb == 0 && nxp &&
+  if (front_early && nx.n && nx.d_blocks && !nx.wait && c->ahead_mode == 2 && c->n_vb == 0 && nxp &&
       const_cast<PreSplit *>(nxp)->ready()) {
     if (front_launch_a(c, S, S->set[cur ^ 1], nx.n, nx.blocks, nx.lens, nx.d_blocks, nx.lo, nx.hi, c->streamF,
                        nx.wait, nullptr) == FGV_OK) {
