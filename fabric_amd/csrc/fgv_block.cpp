@@ -938,14 +938,46 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     total += hi[b] - lo[b];
   }
   if (total > res_cap) return FGV_EINVAL;
+  // Blocks the reference cannot validate (key-level dependency tracking, validator_keylevel.go:
+  // 184-241): a tx whose dependency extraction failed before a later tx's vscc reads a written
+  // key, or panicked before a later tx's vscc runs.  Per block, the first such tx index; a shard
+  // starting inside a block walks the block's earlier transactions too.
+  std::vector<uint32_t> xfail(nblocks, UINT32_MAX), xpanic(nblocks, UINT32_MAX);
+  bool sequential = false;
+  std::vector<std::vector<std::pair<uint32_t, Span>>> pre_md(nblocks);  // prefix metadata writers
+  for (size_t b = 0; b < nblocks; b++)
+    for (uint32_t i = 0; i < lo[b]; i++) {
+      TxRec tmp;
+      extract_walk(envs[b][i], tmp);
+      if (tmp.xstat == X_FAIL) xfail[b] = std::min(xfail[b], i);
+      if (tmp.xstat == X_PANIC) xpanic[b] = std::min(xpanic[b], i);
+      if (tmp.has_md) pre_md[b].push_back({i, tmp.results}), sequential = true;
+    }
+  // Shadow transactions (a shard split inside a block): the metadata writers before
+  // this rank's range are validated here too -- parsed, verified and folded in block order like the
+  // rank's own, their records dropped -- so a dependent whose writer another rank holds reads that
+  // writer's vscc result per namespace (vpmanagerimpl.go:296-355 SetTxValidationResult /
+  // GetValidationParameterForKey) instead of staying undecided.  Every writer a shadow depends on
+  // is an earlier metadata writer, so the set is closed.  Metadata writers are rare: the extra
+  // work is a handful of transactions per split block.
+  size_t nshadow = 0;
+  for (size_t b = 0; b < nblocks; b++)
+    if (hi[b] > lo[b]) nshadow += pre_md[b].size();
+  const size_t total_all = total + nshadow;
   std::vector<TxRec> &recs = S->recs;
-  if (recs.size() < total) recs.resize(total);
-  std::vector<std::pair<uint32_t, uint32_t>> where(total);
-  for (size_t b = 0, t = 0; b < nblocks; b++)
-    for (size_t i = lo[b]; i < hi[b]; i++) where[t++] = {(uint32_t)b, (uint32_t)i};
+  if (recs.size() < total_all) recs.resize(total_all);
+  std::vector<std::pair<uint32_t, uint32_t>> where(total_all);
+  std::vector<uint32_t> outpos(total_all, UINT32_MAX);  // the record's row in res_out (shadows: none)
+  for (size_t b = 0, t = 0, r = 0; b < nblocks; b++) {
+    if (hi[b] > lo[b])
+      for (const auto &pm : pre_md[b]) where[t++] = {(uint32_t)b, pm.first};
+    for (size_t i = lo[b]; i < hi[b]; i++) outpos[t] = (uint32_t)r++, where[t++] = {(uint32_t)b, (uint32_t)i};
+  }
+  std::vector<fgv_tx_result> shadow_res(nshadow ? total_all : 0);
+  auto res_at = [&](size_t t) -> fgv_tx_result & { return outpos[t] != UINT32_MAX ? res_out[outpos[t]] : shadow_res[t]; };
 
   // --- A. parse (every check that needs no crypto) + per-tx device job counts
-  S->pool.parallel_for(total, [&](size_t t) {
+  S->pool.parallel_for(total_all, [&](size_t t) {
     TxRec &R = recs[t];
     parse_tx(ch, envs[where[t].first][where[t].second], R);
     count_jobs(ch, R);
@@ -958,11 +990,11 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   //     ecdsa [creator signatures | endorsement signatures]
   // chunked exclusive scan over the per-tx counts, then a parallel fill of pinned buffers
   constexpr size_t CH = 256;
-  const size_t nch = (total + CH - 1) / CH;
+  const size_t nch = (total_all + CH - 1) / CH;
   std::vector<std::array<uint32_t, 5>> cbase(nch + 1);
   S->pool.run(nch, [&](size_t k) {
     std::array<uint32_t, 5> a{};
-    for (size_t t = k * CH, e = std::min(total, t + CH); t < e; t++) {
+    for (size_t t = k * CH, e = std::min(total_all, t + CH); t < e; t++) {
       const TxRec &R = recs[t];
       a[0] += R.n_cj; a[1] += R.n_tj; a[2] += R.n_pj; a[3] += R.n_ej; a[4] += R.n_ij;
     }
@@ -1001,7 +1033,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
       J.key_slot[vi] = (uint32_t)slot;
       J.dig_idx[vi] = dig;
     };
-    for (size_t t = k * CH, e = std::min(total, t + CH); t < e; t++) {
+    for (size_t t = k * CH, e = std::min(total_all, t + CH); t < e; t++) {
       TxRec &R = recs[t];
       const size_t b = where[t].first;
       if (R.n_cj) {
@@ -1043,22 +1075,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   auto t_fold = clk::now();
 
   // --- C. fold (code precedence, validator.go:297-453) + result records
-  // Blocks the reference cannot validate (key-level dependency tracking, validator_keylevel.go:
-  // 184-241): a tx whose dependency extraction failed before a later tx's vscc reads a written
-  // key, or panicked before a later tx's vscc runs.  Per block, the first such tx index; a shard
-  // starting inside a block walks the block's earlier transactions too.
-  std::vector<uint32_t> xfail(nblocks, UINT32_MAX), xpanic(nblocks, UINT32_MAX);
-  bool sequential = false;
-  std::vector<std::vector<std::pair<uint32_t, Span>>> pre_md(nblocks);  // prefix metadata writers
-  for (size_t b = 0; b < nblocks; b++)
-    for (uint32_t i = 0; i < lo[b]; i++) {
-      TxRec tmp;
-      extract_walk(envs[b][i], tmp);
-      if (tmp.xstat == X_FAIL) xfail[b] = std::min(xfail[b], i);
-      if (tmp.xstat == X_PANIC) xpanic[b] = std::min(xpanic[b], i);
-      if (tmp.has_md) pre_md[b].push_back({i, tmp.results}), sequential = true;
-    }
-  for (size_t t = 0; t < total; t++) {
+  for (size_t t = 0; t < total_all; t++) {
     const TxRec &R = recs[t];
     const size_t b = where[t].first;
     const uint32_t i = where[t].second;
@@ -1073,8 +1090,9 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
       sbe[b].res.resize(hi[b]);
       for (const auto &pm : pre_md[b]) add_deps(pm.second, pm.first, sbe[b]);
     }
-    for (size_t t = 0; t < total; t++)
-      if (recs[t].has_md && recs[t].xstat == X_OK) add_deps(recs[t].results, where[t].second, sbe[where[t].first]);
+    for (size_t t = 0; t < total_all; t++)  // (the shadows were added as prefix writers)
+      if (outpos[t] != UINT32_MAX && recs[t].has_md && recs[t].xstat == X_OK)
+        add_deps(recs[t].results, where[t].second, sbe[where[t].first]);
   }
   // The batch validates every block against the key-level state committed before it, but the
   // reference commits block k before block k+1's vscc reads GetStateMetadata.  A key whose
@@ -1107,8 +1125,8 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         if (tmp.xstat == X_OK) kl_keys(ch, tmp.results, chg[b], tch[b]);
       }
     }
-    for (size_t t = 0; t < total; t++)
-      if (recs[t].xstat == X_OK) kl_keys(ch, recs[t].results, chg[where[t].first], tch[where[t].first]);
+    for (size_t t = 0; t < total_all; t++)  // (shadows: walked above as other ranks' transactions)
+      if (outpos[t] != UINT32_MAX && recs[t].xstat == X_OK) kl_keys(ch, recs[t].results, chg[where[t].first], tch[where[t].first]);
     std::unordered_set<std::string> changed;
     for (size_t b = 0; b < nblocks && b < S->split; b++) {
       if (unknown[b]) {
@@ -1166,7 +1184,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   static const char HEX[] = "0123456789abcdef";
   // pass 0: no key-level state (parallel); 1: key-level, every tx in parallel, a tx whose written
   // key has an earlier metadata writer only marked; 2: the marked txs again, in block order
-  std::vector<uint8_t> touched(sequential ? total : 0, 0);
+  std::vector<uint8_t> touched(sequential ? total_all : 0, 0);
   auto fold_one = [&](size_t t, int pass) {
     const TxRec &R = recs[t];
     const size_t b = where[t].first;
@@ -1294,7 +1312,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
         else if (has10) code = C_POLICY;
       }
     }
-    fgv_tx_result &o = res_out[t];
+    fgv_tx_result &o = res_at(t);
     memset(&o, 0, sizeof o);
     o.code = code;
     if (reached) {  // chdr.TxId == hex(digest): the record carries the digest bytes
@@ -1313,11 +1331,11 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     }
   };
   if (sequential) {  // block order for the txs that read the vscc results of earlier ones
-    S->pool.parallel_for(total, [&](size_t t) { fold_one(t, 1); });
-    for (size_t t = 0; t < total; t++)
+    S->pool.parallel_for(total_all, [&](size_t t) { fold_one(t, 1); });
+    for (size_t t = 0; t < total_all; t++)
       if (touched[t]) fold_one(t, 2);
   } else {
-    S->pool.parallel_for(total, [&](size_t t) { fold_one(t, 0); });
+    S->pool.parallel_for(total_all, [&](size_t t) { fold_one(t, 0); });
   }
   c->t_host_fold = ms_since(t_fold);
   // (from the final codes: a pass-1 verdict of a tx folded again in pass 2 does not count;

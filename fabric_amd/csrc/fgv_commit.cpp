@@ -187,6 +187,7 @@ struct TxScratch {
   std::vector<WEnt> grp;  // one representative entry per (namespace, hashed, collection) group
   std::vector<uint32_t> rank;
   std::vector<SortRec> ix;
+  std::vector<uint32_t> dup;  // one transaction's write indices (the twice-written-key check)
   std::unique_ptr<uint8_t[]> batch;
   size_t cap = 0;
   uint32_t last = UINT32_MAX;
@@ -250,11 +251,29 @@ int add_tx(Span d, uint32_t txi, std::vector<WEnt> &out, TxScratch &x) {
       }
     }
   }
-  // a key written twice by one transaction: txOps flag arithmetic (tx_ops.go:183-191)
-  for (size_t a = mine; a < out.size(); a++)
-    for (size_t b = a + 1; b < out.size(); b++)
-      if (out[a].grp == out[b].grp && out[a].kp == out[b].kp && span_eq(out[a].key, out[b].key))
-        return FGV_EUNSUPPORTED;
+  // a key written twice by one transaction: txOps flag arithmetic (tx_ops.go:183-191).  Pairwise
+  // for a handful of writes; otherwise the transaction's writes sorted by (group, prefix, key) and
+  // neighbours compared, so a bulk-load transaction stays O(w log w)
+  const size_t nw = out.size() - mine;
+  if (nw <= 16) {
+    for (size_t a = mine; a < out.size(); a++)
+      for (size_t b = a + 1; b < out.size(); b++)
+        if (out[a].grp == out[b].grp && out[a].kp == out[b].kp && span_eq(out[a].key, out[b].key))
+          return FGV_EUNSUPPORTED;
+    return FGV_OK;
+  }
+  std::vector<uint32_t> &o = x.dup;
+  o.resize(nw);
+  for (uint32_t i = 0; i < nw; i++) o[i] = (uint32_t)(mine + i);
+  std::sort(o.begin(), o.end(), [&out](uint32_t a, uint32_t b) {
+    if (out[a].grp != out[b].grp) return out[a].grp < out[b].grp;
+    if (out[a].kp != out[b].kp) return out[a].kp < out[b].kp;
+    return span_cmp(out[a].key, out[b].key) < 0;
+  });
+  for (size_t i = 1; i < nw; i++) {
+    const WEnt &a = out[o[i - 1]], &b = out[o[i]];
+    if (a.grp == b.grp && a.kp == b.kp && span_eq(a.key, b.key)) return FGV_EUNSUPPORTED;
+  }
   return FGV_OK;
 }
 

@@ -32,6 +32,7 @@ struct fgv_group {
   bool soft = false;
   std::vector<int32_t> blk_status;
   size_t n_final = 0;
+  int last_rc = FGV_OK;  // the last call's return code
 };
 
 extern "C" {
@@ -95,6 +96,9 @@ size_t fgv_group_size(const fgv_group *g) { return g ? g->ctx.size() : 0; }
 
 fgv_ctx *fgv_group_ctx(fgv_group *g, size_t i) { return g && i < g->ctx.size() ? g->ctx[i] : nullptr; }
 
+static int group_validate_locked(fgv_group *g, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                 uint8_t *flags, size_t flags_cap, size_t *ntx);
+
 int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                               uint8_t *flags, size_t flags_cap, size_t *ntx) {
   if (!g || (nblocks && (!blocks || !lens || !flags || !ntx))) return FGV_EINVAL;
@@ -102,6 +106,11 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
   std::lock_guard<std::mutex> lk(g->mu);
   g->blk_status.clear();
   g->n_final = 0;
+  return g->last_rc = group_validate_locked(g, nblocks, blocks, lens, flags, flags_cap, ntx);
+}
+
+static int group_validate_locked(fgv_group *g, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
+                                 uint8_t *flags, size_t flags_cap, size_t *ntx) {
   const bool soft = g->soft;
   const size_t W = g->ctx.size();
   // The plan.  At least as many blocks as devices: contiguous block ranges of about total/W
@@ -268,6 +277,11 @@ int fgv_group_set_block_outcomes(fgv_group *g, int on) {
 int fgv_group_last_block_status(fgv_group *g, int32_t *status, size_t n, size_t *n_final) {
   if (!g || (n && !status)) return FGV_EINVAL;
   std::lock_guard<std::mutex> lk(g->mu);
+  if (g->last_rc != FGV_OK) {  // a failed call decided nothing
+    for (size_t b = 0; b < n; b++) status[b] = g->last_rc;
+    if (n_final) *n_final = 0;
+    return g->last_rc;
+  }
   for (size_t b = 0; b < n; b++) status[b] = b < g->blk_status.size() ? g->blk_status[b] : FGV_OK;
   if (n_final) *n_final = g->n_final;
   return FGV_OK;

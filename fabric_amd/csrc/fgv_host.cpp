@@ -1837,10 +1837,11 @@ int fgv_validate_shard_dev(fgv_ctx *c, size_t nblocks, const uint8_t *const *blo
   c->next = fgv_ctx::NextBatch{};
   if (c->block_outcomes)
     return shard_dev_outcomes(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+  c->blk_status.clear();
   int rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
   if (resolve_for_retry(c, rc, nblocks, blocks, lens))
     rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
-  return rc;
+  return c->last_rc = rc;
 }
 
 // shard_dev_locked with per-block outcomes on (the caller holds c->mu): undecided transactions keep
@@ -1880,6 +1881,7 @@ static int shard_dev_outcomes(fgv_ctx *c, size_t nblocks, const uint8_t *const *
   uint32_t sp = UINT32_MAX;
   const int rc = shard_dev_soft_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap,
                                        ntx, &sp);
+  c->last_rc = rc;
   if (rc) return rc;
   c->n_final = std::min<size_t>(nblocks, sp);
   c->blk_status.assign(nblocks, FGV_OK);
@@ -1914,9 +1916,11 @@ int fgv_validate_shard_dev_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *
   if (c->block_outcomes) {
     rc = shard_dev_outcomes(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
   } else {
+    c->blk_status.clear();
     rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
     if (resolve_for_retry(c, rc, nblocks, blocks, lens))
       rc = shard_dev_locked(c, nblocks, blocks, lens, d_blocks, tx_lo, tx_hi, d_results, results_cap, ntx);
+    c->last_rc = rc;
   }
   if (rc == FGV_OK) stats_accumulate(c);
   c->t_call_end = std::chrono::steady_clock::now();
@@ -2218,6 +2222,7 @@ int fgv_validate_blocks_pipelined(fgv_ctx *c, size_t nblocks, const uint8_t *con
   if (c->next.n)  // not started inside (host-parse path, empty batch, early error): start it now
     fgv_block_presplit(c->blk, c->device, c->next.n, c->next.blocks, c->next.lens, nullptr, nullptr);
   c->next = fgv_ctx::NextBatch{};
+  c->last_rc = rc;
   return rc;
 }
 
@@ -2240,6 +2245,13 @@ int fgv_set_block_outcomes(fgv_ctx *c, int on) {
 int fgv_last_block_status(fgv_ctx *c, int32_t *status, size_t n, size_t *n_final) {
   if (!c || (n && !status)) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  // a call that failed decided nothing: every status is its return code, and so is ours (ADVICE r5:
+  // a caller reading the statuses without the call's code must not see final blocks)
+  if (c->last_rc != FGV_OK) {
+    for (size_t b = 0; b < n; b++) status[b] = c->last_rc;
+    if (n_final) *n_final = 0;
+    return c->last_rc;
+  }
   for (size_t b = 0; b < n; b++) status[b] = b < c->blk_status.size() ? c->blk_status[b] : FGV_OK;
   if (n_final) *n_final = c->n_final;
   return FGV_OK;

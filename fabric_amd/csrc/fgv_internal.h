@@ -157,6 +157,7 @@ struct fgv_ctx {
   // per-block outcomes (fgv_set_block_outcomes) and the fallback counters (fgv_unsupported_stats)
   bool block_outcomes = false;
   std::vector<int32_t> blk_status;
+  int last_rc = FGV_OK;  // the last validate call's return code (fgv_last_block_status)
   size_t n_final = 0;
   uint64_t unsup_batches = 0, unsup_blocks = 0, unsup_txs = 0;
   // running sums of the per-call diagnostics (fgv_stats_sums): a benchmark reads them once after

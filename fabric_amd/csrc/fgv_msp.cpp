@@ -338,6 +338,7 @@ struct MspModel {
         ro.has_cert = true;
       }
     }
+    std::vector<fgvx::Cert> acs;
     for (const Span &pem : fc.admins) {
       std::vector<uint8_t> der, raw2;
       fgvx::Cert ac;
@@ -345,6 +346,54 @@ struct MspModel {
       if (fgvx::parse_certificate(std::move(der), ac) != fgvx::X_OK) return fail();
       if (fgvx::sanitized_raw(ac, raw2) != fgvx::X_OK) return fail();
       admins.push_back(std::move(raw2));
+      acs.push_back(std::move(ac));
+    }
+    // postSetupV142 (mspimplsetup.go:684-702; without NodeOUs postSetupV1, :612-624): every admin
+    // must Validate -- chain, CRLs, OU identifiers -- or, with NodeOUs, carry the client or the
+    // admin OU (hasOURole over GetOrganizationalUnits, empty without a certification chain).
+    // Else the MSP does not set up (oracle/msp.py MSP.__init__): outside the model.
+    if (!acs.empty()) {
+      std::vector<uint8_t> am, as;
+      std::vector<uint64_t> amo, aso;
+      std::vector<uint32_t> aml, asl, aslots;
+      std::vector<int> p1(acs.size());
+      for (size_t k = 0; k < acs.size(); k++) {
+        const fgvx::Cert &x = acs[k];
+        const int64_t now = x.not_before + 1;  // (getUniqueValidationChain, as for any identity)
+        if (x.is_ca || x.unhandled_critical || !(x.not_before <= now && now <= x.not_after)) return fail();
+        p1[k] = unique_parent(x, -1);
+        if (p1[k] < 0) return fail();
+        const std::vector<int> &up = cas[p1[k]].chain;
+        for (size_t q = 0; q < up.size(); q++)
+          if (!parent_ok(cas[up[q]].c, now, q)) return fail();
+        if (!ca_job(x, cas[p1[k]].slot, am, amo, aml, as, aso, asl, aslots)) return fail();
+      }
+      if (c) {  // (c NULL, the sanitizer probe: taken as verified)
+        std::vector<uint8_t> st(amo.size(), 1);
+        if (fgv_verify_msgs_slots_locked(c, am.data(), am.size(), amo.data(), aml.data(), as.data(), as.size(),
+                                         aso.data(), asl.data(), aslots.data(), amo.size(), st.data()) != FGV_OK)
+          return fail();
+        for (uint8_t v : st)
+          if (v != 0) return fail();
+      }
+      for (size_t k = 0; k < acs.size(); k++) {
+        const fgvx::Cert &x = acs[k];
+        if (node_ous) {
+          if (!has(R_CLIENT, x) && !has(R_ADMIN, x)) return fail();
+          continue;
+        }
+        const CA &issuer = cas[p1[k]];
+        if (issuer.internal || !issuer.c.has_ski || revoked(x, p1[k])) return fail();
+        if (!ou_ids.empty()) {
+          bool any = false;
+          for (const std::string &o : x.ous) {
+            auto it = ou_ids.find(o);
+            if (it != ou_ids.end() && std::find(it->second.begin(), it->second.end(), issuer.chain_id) != it->second.end())
+              any = true;
+          }
+          if (!any) return fail();
+        }
+      }
     }
   }
   void fail() { unsup = true; }

@@ -326,7 +326,9 @@ int fgv_validate_blocks_pipelined(fgv_ctx *ctx, size_t nblocks, const uint8_t *c
  * rank's n_final (its key-level walk sees its own transactions; another rank's block whose bytes
  * are not in the call waits behind a change) with LATER from there on -- the caller takes the
  * minimum n_final over the ranks and marks the blocks whose final flags hold 0xFD unsupported
- * (fabric_amd/shard.py block_outcomes).  fgv_unsupported_stats: fallback counters since fgv_init -- calls that
+ * (fabric_amd/shard.py block_outcomes).  After a call that failed (returned anything but FGV_OK),
+ * fgv_last_block_status fills every status with that return code, sets n_final = 0 and returns
+ * the code: a failed call decided no block.  fgv_unsupported_stats: fallback counters since fgv_init -- calls that
  * returned FGV_EUNSUPPORTED, blocks handed to the reference (whole batches included), undecided
  * transactions of per-block calls. */
 #define FGV_BLOCK_LATER 1
@@ -406,6 +408,7 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
  * after it (n_final), whether the earlier block is on the same device or on another one (a device
  * whose blocks change key-level state: the whole batch is checked on the host). */
 int fgv_group_set_block_outcomes(fgv_group *g, int on);
+/* (after a failed group call: every status = its return code, n_final = 0, returns the code) */
 int fgv_group_last_block_status(fgv_group *g, int32_t *status, size_t n, size_t *n_final);
 /* fgv_p256_verify_msgs over all devices of the group (config C4 through the C ABI): items
  * [n r / W, n (r+1) / W) on device r, each device verifying with its own key cache; same status

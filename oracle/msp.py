@@ -119,6 +119,7 @@ class MSP:
             if o is not None and self.node_ous:
                 self.role_ou[role] = (o.get("organizational_unit_identifier", ""), certifier(o.get("certificate")))
         self.admins = []
+        admin_certs = []
         for pem in fc.get("admins", []):
             der = X.pem_decode(pem)
             try:
@@ -126,6 +127,20 @@ class MSP:
                 self.admins.append(X.sanitized_raw(c))
             except (X.ParseError, TypeError):
                 raise Unsupported("admin certificate")
+            admin_certs.append(c)
+        # postSetupV142 (mspimplsetup.go:684-702): without NodeOUs, postSetupV1 (:612-624) -- every
+        # admin must Validate (its chain, the CRLs, the OU identifiers); with NodeOUs every admin
+        # must carry the client or the admin OU (hasOURole over GetOrganizationalUnits, which is
+        # empty when the admin has no certification chain).  Otherwise the MSP does not set up.
+        for c in admin_certs:
+            chain = self._chain(c)
+            if chain is None:
+                raise Unsupported("admin without a validation chain: the MSP does not set up")
+            if not self.node_ous:
+                if not self._valid(c, chain)[0]:
+                    raise Unsupported("admin that does not validate: the MSP does not set up")
+            elif not (self._has(ROLE_CLIENT, c) or self._has(ROLE_ADMIN, c)):
+                raise Unsupported("admin without the client or admin OU: the MSP does not set up")
 
     def _parent_ok(self, parent, now, below):
         """x509 isValid for a CA at `below` intermediates under it + CheckSignatureFrom's rules"""
@@ -190,6 +205,18 @@ class MSP:
             return None  # sanitizeCert: no validation chain -> newIdentity fails
         raw2 = X.sanitized_raw(c)
         digest = hashlib.sha256(raw2).digest()
+        valid, ous = self._valid(c, chain)
+        roles = 1 if valid else 0
+        if raw2 in self.admins or (valid and self.node_ous and self._has(ROLE_ADMIN, c)):
+            roles |= 1 << ROLE_ADMIN
+        for role in (ROLE_CLIENT, ROLE_PEER, ROLE_ORDERER):
+            if valid and self.node_ous and self._has(role, c):
+                roles |= 1 << role
+        key = {"p256": KEY_P256, "p384": KEY_P384}.get(c["key"], KEY_OTHER)
+        return Ident(self.name, c["pub"] if key == KEY_P256 else None, valid, digest, key=key, roles=roles, ous=ous)
+
+    def _valid(self, c, chain):
+        """validateIdentity of a leaf with its validation chain -> (valid, its OUs with certifier)"""
         # Validate: the issuer must be a leaf of the certification tree, its SKI must exist
         # (setup guarantees it), then the OUs; the certifier is the chain above the identity
         valid = chain[1]["raw2"] not in self.internal and chain[1]["ski"] is not None
@@ -215,14 +242,7 @@ class MSP:
                     break
             if cnt != 1:
                 valid = False
-        roles = 1 if valid else 0
-        if raw2 in self.admins or (valid and self.node_ous and self._has(ROLE_ADMIN, c)):
-            roles |= 1 << ROLE_ADMIN
-        for role in (ROLE_CLIENT, ROLE_PEER, ROLE_ORDERER):
-            if valid and self.node_ous and self._has(role, c):
-                roles |= 1 << role
-        key = {"p256": KEY_P256, "p384": KEY_P384}.get(c["key"], KEY_OTHER)
-        return Ident(self.name, c["pub"] if key == KEY_P256 else None, valid, digest, key=key, roles=roles, ous=ous)
+        return valid, ous
 
     def _has(self, role, c):
         ou = self.role_ou.get(role)

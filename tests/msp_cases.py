@@ -165,3 +165,38 @@ def synthetic():
     fabric2 = fabric_msp_config("Org2MSP", root_certs=[r2])
     cfg = make_config([MSPID, "Org2MSP"], msp_configs={MSPID: fabric, "Org2MSP": fabric2})
     return cfg, out
+
+
+def admin_setup_cases():
+    """the MSP's post-setup admin checks (mspimplsetup.go:612-624 postSetupV1 without
+    NodeOUs -- every admin must Validate, CRLs included; :684-702 postSetupV142 with NodeOUs -- every
+    admin carries the client or the admin OU).  -> [(label, config bytes, probe serialized identity,
+    sets_up)]: when the MSP does not set up, the probe (an ordinary peer leaf) is Unsupported."""
+    ca1, ca2 = Key(78, 1), Key(78, 2)
+    n1 = G.name("ca1.org1")
+    r1 = G.ca_cert(ca1, "ca1.org1")
+    k = [Key(78, 100 + i) for i in range(12)]
+
+    def leaf(i, ous, issuer_key=ca1, issuer=n1):
+        return G.cert(k[i], issuer_key, G.name("adm%d" % i, ous=ous), issuer, serial=2000 + i)
+
+    probe = serialized_identity(MSPID, leaf(0, ["peer", "dept1"]))
+    out = []
+
+    def case(label, admin, sets_up, node_ous=True, crls=(), ou_ids=()):
+        fabric = fabric_msp_config(MSPID, root_certs=[r1], admins=[admin], crls=crls, ou_ids=ou_ids,
+                                   node_ous=("client", "peer", "admin", "orderer") if node_ous else None)
+        out.append((label, make_config([MSPID], msp_configs={MSPID: fabric}), probe, sets_up))
+
+    case("admin_valid_no_nodeous", leaf(1, ["client"]), True, node_ous=False)
+    case("admin_revoked_no_nodeous", leaf(2, ["client"]), False, node_ous=False,
+         crls=[G.crl(ca1, "ca1.org1", ca1, [2002])])
+    case("admin_revoked_with_nodeous", leaf(3, ["client"]), True, crls=[G.crl(ca1, "ca1.org1", ca1, [2003])])
+    case("admin_ou_ids_mismatch_no_nodeous", leaf(4, ["dept2"]), False, node_ous=False, ou_ids=[(r1, "dept1")])
+    case("admin_ou_ids_match_no_nodeous", leaf(5, ["dept1"]), True, node_ous=False, ou_ids=[(r1, "dept1")])
+    case("admin_peer_ou_with_nodeous", leaf(6, ["peer"]), False)
+    case("admin_admin_ou_with_nodeous", leaf(7, ["admin"]), True)
+    case("admin_unknown_issuer", leaf(8, ["client"], issuer=G.name("ca.other")), False)
+    case("admin_wrong_ca_key_no_nodeous", leaf(9, ["client"], issuer_key=ca2), False, node_ous=False)
+    case("admin_wrong_ca_key_with_nodeous", leaf(10, ["client"], issuer_key=ca2), False)
+    return out

@@ -35,3 +35,43 @@ def test_commit_hashes_pipeline_blocks():
     for b in range(4):
         prev = _lib.commit_hash(blks[b], fexp[b], 3001 + b, prev)
         assert got[b] == prev, b
+
+
+def _bulk_block(nwrites, dup_at=None):
+    """Two transactions: a bulk load of `nwrites` keys (one key written twice when dup_at is
+    set) and an ordinary one; flags all VALID (the commit hash does not validate)."""
+    from fabric_amd.synth import blocks
+    net = blocks.Network(seed=5, orgs=3, clients=4)
+    keys = ["bulk%06d" % i for i in range(nwrites)]
+    if dup_at is not None:
+        keys[dup_at] = keys[dup_at // 2]
+    bulk = blocks.tx_rwset([("mycc", blocks.kv_rwset([], [(k, b"v%d" % i, False) for i, k in enumerate(keys)]))])
+    other = blocks.tx_rwset([("mycc", blocks.kv_rwset([], [("bulk000001", b"later", False), ("z", b"", True)]))])
+    blk, _, _ = blocks.make_block(net, 2, number=9, seed=1, faults=(("clean", 1.0),), rwsets=[bulk, other])
+    return blk
+
+
+def test_commit_hash_bulk_transaction():
+    """one VALID transaction writing 50k keys -- the twice-written-key check
+    is O(w log w), not pairwise; the hash equals the oracle's."""
+    import time
+
+    import oracle.commithash as och
+    blk = _bulk_block(50_000)
+    flags = np.zeros(2, np.uint8)
+    t0 = time.perf_counter()
+    got = _lib.commit_hash(blk, flags, 9, b"\x01" * 32)
+    dt = time.perf_counter() - t0
+    assert dt < 1.0, dt  # pairwise: ~1.25e9 comparisons, several seconds
+    assert got == och.block_commit_hash(blk, [0, 0], 9, b"\x01" * 32)
+
+
+def test_commit_hash_bulk_transaction_dup_key():
+    """A key written twice inside one bulk transaction stays outside the model (tx_ops.go:183-191
+    flag arithmetic), as in the oracle."""
+    import oracle.commithash as och
+    blk = _bulk_block(5_000, dup_at=4_321)
+    with pytest.raises(Exception):
+        och.block_commit_hash(blk, [0, 0], 9, b"")
+    with pytest.raises(_lib.FgvError):
+        _lib.commit_hash(blk, np.zeros(2, np.uint8), 9, b"")

@@ -209,3 +209,18 @@ def test_fork_hazard_reframings_are_unsupported():
         with pytest.raises(v20.Unsupported):
             v20.validate_block(v20.ChannelModel("testchannel", unreg, defs[13], config=config), blk)
         eng.close()
+
+
+def test_admin_setup_cases():
+    """an MSP whose admins fail the post-setup checks (a revoked admin without NodeOUs,
+    an admin without the client / admin OU, an admin with no chain) does not set up in the
+    reference: the engine leaves it to the reference (Unsupported), as the oracle does"""
+    for label, cfg, probe, sets_up in MC.admin_setup_cases():
+        eng = _lib.Engine(0)
+        try:
+            eng.channel_init("ch")
+            eng.channel_config(cfg)
+            st = eng.msp_resolve([probe])
+            assert st == ([MC.OK] if sets_up else [MC.UNSUP]), (label, st)
+        finally:
+            eng.close()

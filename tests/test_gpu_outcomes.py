@@ -62,6 +62,8 @@ def test_out_of_model_identity_confined_to_its_blocks(mode):
         txvalidator.setup_channel(eng, net.channel, ids, net.chaincodes)
         with pytest.raises(_lib.Unsupported):  # (the whole-batch contract stays the default)
             eng.validate_blocks(blks)
+        with pytest.raises(_lib.Unsupported):  # a failed call decided nothing
+            eng.last_block_status(6)
         assert eng.unsupported_stats()["blocks"] == 6
         eng.set_block_outcomes(True)
         st, n_final = _check(eng, v20.ChannelModel(net.channel, ids, net.chaincodes), blks)
@@ -155,6 +157,8 @@ def test_group_out_of_model_identity_confined_to_its_blocks(ndev):
             txvalidator.setup_channel(e, net.channel, ids, net.chaincodes)
         with pytest.raises(_lib.Unsupported):  # (the whole-batch contract stays the default)
             g.validate_blocks(blks)
+        with pytest.raises(_lib.Unsupported):  # a failed call decided nothing
+            g.last_block_status(6)
         g.set_block_outcomes(True)
         st, n_final = _check_group(g, v20.ChannelModel(net.channel, ids, net.chaincodes), blks)
         assert n_final == 6 and st == [0, 0, 0, 0, _lib.FGV_EUNSUPPORTED, 0], st
@@ -162,10 +166,12 @@ def test_group_out_of_model_identity_confined_to_its_blocks(ndev):
         g.close()
 
 
-@pytest.mark.parametrize("ndev", [1, 2, 3])
+@pytest.mark.parametrize("ndev", [1, 2, 3, 4, 7])
 def test_group_keylevel_split_across_devices(ndev):
     """block 1 sets / clears key-level parameters that block 2 writes; with 2 or 3 devices the
-    two blocks sit on different devices (block plan by bytes): blocks 0..1 final, block 2 LATER"""
+    two blocks sit on different devices (block plan by bytes): blocks 0..1 final, block 2 LATER.
+    4 and 7 devices > 3 blocks: the transaction-index plan splits block 1 between devices, and a
+    dependent whose metadata writer another device holds is decided there (shadow writers)"""
     net = sbe_cases_network()
     ccs = {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
     b0 = blocks.make_block(net, 40, number=1, seed=17)[0]
@@ -206,16 +212,12 @@ def _shard_protocol_outcomes(eng, blks, shards, mode):
     return out, st, nf
 
 
-def _expect(model, blks, got, st, n_final, may_defer=()):
-    """may_defer: blocks the protocol may hand to the reference although the oracle decides them
-    (a dependent transaction whose metadata writer another rank validated)"""
+def _expect(model, blks, got, st, n_final):
     exp, exp_final = v20.validate_blocks_outcomes(model, blks)
     assert n_final == exp_final
     for b in range(len(blks)):
         if b >= exp_final:
             assert st[b] == _lib.BLOCK_LATER, b
-        elif b in may_defer and st[b] == _lib.FGV_EUNSUPPORTED:
-            assert 0xFD in list(got[b])
         elif exp[b] is None:
             assert st[b] == _lib.FGV_EUNSUPPORTED, b
             assert 0xFD in list(got[b])
@@ -252,11 +254,12 @@ def test_shard_protocol_out_of_model_identity(shards, mode):
         eng.close()
 
 
-@pytest.mark.parametrize("shards,mode", [(2, "tx"), (2, "block"), (3, "block")])
+@pytest.mark.parametrize("shards,mode", [(2, "tx"), (3, "tx"), (5, "tx"), (2, "block"), (3, "block")])
 def test_shard_protocol_keylevel_split(shards, mode):
-    """the key-level split through the shard protocol: block 0 final, block 2 LATER; block 1 final
-    with whole blocks per rank -- split by transaction index, its dependents whose metadata writer
-    is on the other rank are undecided, so it may go to the reference instead"""
+    """the key-level split through the shard protocol: block 0 final, block 2 LATER, block 1 final
+    and equal to the oracle in every plan -- split by transaction index, a dependent whose metadata
+    writer another rank holds reads that writer's vscc result from the rank's shadow validation of
+    the block's earlier metadata writers (vpmanagerimpl.go:296-355)"""
     net = sbe_cases_network()
     ccs = {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
     b0 = blocks.make_block(net, 40, number=1, seed=17)[0]
@@ -267,9 +270,32 @@ def test_shard_protocol_keylevel_split(shards, mode):
         eng.set_block_outcomes(True)
         got, st, n_final = _shard_protocol_outcomes(eng, [b0, b1, b2], shards, mode)
         _expect(v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=dict(kvmeta0)), [b0, b1, b2], got, st,
-                n_final, may_defer={1} if mode == "tx" else ())
-        assert n_final == 2 and st[0] == 0 and st[2] == _lib.BLOCK_LATER, st
-        if mode == "block":
-            assert st[1] == 0, st
+                n_final)
+        assert n_final == 2 and st == [0, 0, _lib.BLOCK_LATER], st
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("seed", [948, 3, 77])
+@MODES
+def test_shard_protocol_keylevel_tx_split_seeds(seed, mode):
+    """one key-level block split by transaction index at every shard count 2..6: dependents whose
+    metadata writers sit on other ranks, chains of writers across ranks; every plan's flags equal
+    the oracle's and the block is final (no deferral to the reference)"""
+    net = sbe_cases_network()
+    ccs = {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
+    b1, kvmeta0 = sbe_cases.make_sbe_block(net, 60, seed, number=2)
+    model = v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=dict(kvmeta0))
+    exp, _ = v20.validate_blocks_outcomes(model, [b1])
+    eng = _lib.Engine(0)
+    try:
+        eng.set_parse_mode(mode)
+        txvalidator.setup_channel(eng, net.channel, net.identities(), ccs, kvmeta=kvmeta0)
+        eng.set_block_outcomes(True)
+        for shards in range(2, 7):
+            got, st, n_final = _shard_protocol_outcomes(eng, [b1], shards, "tx")
+            _expect(model, [b1], got, st, n_final)
+            if exp[0] is not None:
+                assert st == [0], (shards, st)
     finally:
         eng.close()

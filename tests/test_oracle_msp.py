@@ -355,3 +355,22 @@ def test_engine_parser_matches_on_mutated_pem_text():
                 assert a["status"] == 2 or b"-----BEGIN " not in m
                 n_unsup += a["status"] == 2
     assert n_unsup > 100
+
+
+# ---- the MSP's post-setup admin checks (mspimplsetup.go:612-624, 684-702)
+@pytest.mark.parametrize("rel", ["nodeous1", "nodeous8", "badadmin"])
+def test_msp_with_invalid_admin_does_not_set_up(rel):
+    """TestInvalidAdminNodeOU (nodeous1, nodeous8: NodeOUs on, the admin carries no client / admin
+    OU) and TestBadAdminIdentity (badadmin): Setup fails in the reference -> outside the model"""
+    with pytest.raises(Unsupported):
+        _msp("msp/testdata/" + rel)
+
+
+def test_admin_setup_cases_oracle():
+    from oracle import v20
+    from tests.msp_cases import MSPID, admin_setup_cases
+    for label, cfg, probe, sets_up in admin_setup_cases():
+        m = v20.ChannelModel("ch", [], {}, config=cfg).msp_models()[MSPID]
+        assert isinstance(m, Exception) != sets_up, (label, m)
+        if sets_up:
+            assert m.resolve(decode("SerializedIdentity", probe).get("id_bytes")) is not None, label
