@@ -357,7 +357,10 @@ __global__ __launch_bounds__(256) void k_bd_fold(uint32_t ntx, const DevTx *__re
   } else if (vstatus[J.base[BJ_C]] != 0) {
     code = C_BAD_CREATOR;
   } else if (R.type == 1) {
+    // CONFIG reaching ChannelResources.Apply (validator.go:397-420): the configuration the later
+    // blocks validate under changes -- per-block outcomes: they wait (LATER from R.blk + 1)
     code = C_UNSUPPORTED;
+    atomicMax(&flags[7], ~(R.blk + 1u));
   } else if (R.type == 2) {
     code = C_UNSUP_PAYLOAD;
   } else {

@@ -1185,6 +1185,7 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
   // pass 0: no key-level state (parallel); 1: key-level, every tx in parallel, a tx whose written
   // key has an earlier metadata writer only marked; 2: the marked txs again, in block order
   std::vector<uint8_t> touched(sequential ? total_all : 0, 0);
+  std::vector<uint8_t> cfg_blk(nblocks, 0);  // blocks with a CONFIG transaction reaching Apply
   auto fold_one = [&](size_t t, int pass) {
     const TxRec &R = recs[t];
     const size_t b = where[t].first;
@@ -1196,7 +1197,8 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     } else if (vstatus[R.cvjob] != 0) {
       code = C_BAD_CREATOR;
     } else if (R.type == 1) {
-      code = C_UNSUPPORTED;  // CONFIG transaction
+      code = C_UNSUPPORTED;  // CONFIG transaction (validator.go:397-420: ChannelResources.Apply)
+      cfg_blk[b] = 1;        // per-block outcomes: the later blocks wait for its commit
     } else if (R.type == 2) {
       code = C_UNSUP_PAYLOAD;
     } else {
@@ -1338,6 +1340,11 @@ int fgv_block_validate_impl(fgv_ctx *c, fgv_block_state *S, size_t nblocks, cons
     S->pool.parallel_for(total_all, [&](size_t t) { fold_one(t, 0); });
   }
   c->t_host_fold = ms_since(t_fold);
+  for (size_t b = 0; b < nblocks; b++)
+    if (cfg_blk[b]) {
+      S->split = std::min<uint32_t>(S->split, (uint32_t)b + 1);
+      break;
+    }
   // (from the final codes: a pass-1 verdict of a tx folded again in pass 2 does not count;
   // per-block outcomes: the codes stay, 0xFD marking the undecided transactions)
   for (size_t t = 0; t < total; t++)

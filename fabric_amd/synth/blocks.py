@@ -486,6 +486,28 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
     return block, labels, envs
 
 
+def config_block(net: Network, number: int, seed: int = 0, bad_sig=False, prev_hash=b"\x00" * 32):
+    """A block holding one CONFIG transaction (HeaderType_CONFIG = 1), signed by a client of the
+    network (orderers cut config transactions into blocks of their own): the envelope passes
+    ValidateTransaction and reaches ChannelResources.Apply (validator.go:397-420) unless bad_sig.
+    Payload.data is a stand-in ConfigEnvelope (the engine never decodes it)."""
+    rng = random.Random((net.seed << 20) ^ (number << 4) ^ seed ^ 0xC0F)
+    creator = next(c for c in net.clients if c.kind == "p256")
+    nonce = bytes(rng.getrandbits(8) for _ in range(24))
+    txid = hashlib.sha256(nonce + creator.serialized).hexdigest()
+    chdr = f_varint(1, 1) + f_msg(3, f_varint(1, 1_700_000_000 + number)) + f_str(4, net.channel) + f_str(5, txid)
+    shdr = f_bytes(1, creator.serialized) + f_bytes(2, nonce)
+    payload = f_msg(1, f_bytes(1, chdr) + f_bytes(2, shdr)) + f_bytes(2, f_msg(1, f_msg(1, f_varint(1, number))))
+    sig = sign_batch(creator.key.priv, verify_digest(creator, payload), 1, threads=1, high_s=False)[0]
+    if bad_sig:
+        sig = sig[:12] + bytes([sig[12] ^ 0x21]) + sig[13:]
+    env = f_bytes(1, payload) + f_bytes(2, sig)
+    data_hash = hashlib.sha256(env).digest()
+    header = f_varint(1, number) + f_bytes(2, prev_hash) + f_bytes(3, data_hash)
+    metadata = b"".join(f_msg(1, b"") for _ in range(5))
+    return f_msg(1, header) + f_msg(2, f_msg(1, env)) + f_msg(3, metadata)
+
+
 def header_hash(number: int, prev_hash: bytes, envs) -> bytes:
     """BlockHeaderHash of a generated block (protoutil/blockutils.go:48-67: SHA-256 of the DER
     SEQUENCE{INTEGER number, OCTET STRING previous_hash, OCTET STRING data_hash}), used to

@@ -46,6 +46,11 @@ class Unsupported(Exception):
     """Input outside the modelled environment (config tx, channel-reference policy, ...)."""
 
 
+class ConfigTransaction(Unsupported):
+    """A CONFIG transaction that reaches ChannelResources.Apply (validator.go:397-420): the
+    channel's configuration (MSPs, policies) changes for every later block."""
+
+
 KEY_P256, KEY_P384, KEY_OTHER, KEY_UNDESERIALIZABLE = "p256", "p384", "other", "undeserializable"
 IMPLICIT_PREFIX = "_implicit_org_"  # core/chaincode/implicitcollection/name.go:24-29
 
@@ -538,7 +543,7 @@ def validate_transaction(model, env):
             return payload, (chdr, shdr), INVALID_ENDORSER_TRANSACTION
         return payload, (chdr, shdr), VALID
     if t == CONFIG:
-        raise Unsupported("CONFIG transaction")
+        raise ConfigTransaction("CONFIG transaction")
     return None, None, UNSUPPORTED_TX_PAYLOAD
 
 
@@ -948,11 +953,26 @@ def validate_blocks_outcomes(model, blocks):
             out.append(validate_block(model, blk))
         except Unsupported:
             out.append(None)
+        # a CONFIG transaction that reaches ChannelResources.Apply changes the configuration the
+        # later blocks validate under: they wait for this block's commit (the caller re-applies
+        # the channel config and calls again)
+        if any(_reaches_config_apply(model, d) for d in (decode("Block", blk).get("data") or {}).get("data", [])):
+            n_final = min(n_final, b + 1)
         for d in (decode("Block", blk).get("data") or {}).get("data", []):
             t = index_txid(d)
             if t:
                 model.committed.add(t)
     return out, n_final
+
+
+def _reaches_config_apply(model, d):
+    try:
+        validate_transaction(model, decode("Envelope", d))
+    except ConfigTransaction:
+        return True
+    except (Unsupported, DecodeError):
+        return False
+    return False
 
 
 def validate_block(model, block_bytes):

@@ -299,3 +299,57 @@ def test_shard_protocol_keylevel_tx_split_seeds(seed, mode):
                 assert st == [0], (shards, st)
     finally:
         eng.close()
+
+
+@MODES
+def test_config_block_confined(mode):
+    """a CONFIG block in the middle of a call: its block goes to the reference and every later
+    block waits (LATER: the configuration it applies governs them); with a bad creator signature
+    it never reaches ChannelResources.Apply -- code 4, every block final"""
+    net = blocks.Network(seed=3, orgs=3, clients=50)
+    bl = [blocks.make_block(net, 60, number=n, seed=n)[0] for n in (1, 3, 4)]
+    model = lambda: v20.ChannelModel(net.channel, net.identities(), net.chaincodes)  # noqa: E731
+    eng = _lib.Engine(0)
+    try:
+        eng.set_parse_mode(mode)
+        txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes)
+        eng.set_block_outcomes(True)
+        st, n_final = _check(eng, model(), [bl[0], blocks.config_block(net, 2), bl[1], bl[2]])
+        assert n_final == 2 and st == [0, _lib.FGV_EUNSUPPORTED, _lib.BLOCK_LATER, _lib.BLOCK_LATER], st
+        st, n_final = _check(eng, model(), [bl[0], blocks.config_block(net, 2, bad_sig=True), bl[1], bl[2]])
+        assert n_final == 4 and st == [0, 0, 0, 0], st
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("ndev", [2, 5])
+def test_group_config_block_confined(ndev):
+    """the same through fgv_group (block plan with 2 devices, transaction plan with 5 > 4 blocks)"""
+    net = blocks.Network(seed=3, orgs=3, clients=50)
+    bl = [blocks.make_block(net, 60, number=n, seed=n)[0] for n in (1, 3, 4)]
+    g = _lib.Group([0] * ndev)
+    try:
+        for e in g.engines:
+            txvalidator.setup_channel(e, net.channel, net.identities(), net.chaincodes)
+        g.set_block_outcomes(True)
+        st, n_final = _check_group(g, v20.ChannelModel(net.channel, net.identities(), net.chaincodes),
+                                   [bl[0], blocks.config_block(net, 2), bl[1], bl[2]])
+        assert n_final == 2 and st == [0, _lib.FGV_EUNSUPPORTED, _lib.BLOCK_LATER, _lib.BLOCK_LATER], st
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("shards,mode", [(2, "tx"), (2, "block"), (3, "block")])
+def test_shard_protocol_config_block_confined(shards, mode):
+    net = blocks.Network(seed=3, orgs=3, clients=50)
+    bl = [blocks.make_block(net, 60, number=n, seed=n)[0] for n in (1, 3, 4)]
+    blks = [bl[0], blocks.config_block(net, 2), bl[1], bl[2]]
+    eng = _lib.Engine(0)
+    try:
+        txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes)
+        eng.set_block_outcomes(True)
+        got, st, n_final = _shard_protocol_outcomes(eng, blks, shards, mode)
+        _expect(v20.ChannelModel(net.channel, net.identities(), net.chaincodes), blks, got, st, n_final)
+        assert n_final == 2 and st[:2] == [0, _lib.FGV_EUNSUPPORTED], st
+    finally:
+        eng.close()

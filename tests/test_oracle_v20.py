@@ -94,3 +94,17 @@ def test_c5_ed25519_block_matches_generator_labels():
     exp = blocks.expected_codes(labels)
     assert [f for f, e in zip(flags, exp) if e is not None] == [e for e in exp if e is not None]
     assert {"ed25519_creator", "endorse_short", "clean"} <= set(labels)
+
+
+def test_config_block_outcomes():
+    """a CONFIG transaction that reaches ChannelResources.Apply (validator.go:397-420) changes the
+    configuration later blocks validate under: per-block outcomes send its block to the reference
+    and make every later block wait (n_final = its index + 1); one whose creator signature fails
+    never reaches Apply -- code 4, nothing waits"""
+    net = network()
+    m = lambda: v20.ChannelModel(net.channel, net.identities(), net.chaincodes)  # noqa: E731
+    b0, b2 = [blocks.make_block(net, 12, number=n, seed=n)[0] for n in (1, 3)]
+    out, nf = v20.validate_blocks_outcomes(m(), [b0, blocks.config_block(net, 2), b2])
+    assert nf == 2 and out[0] is not None and out[1] is None
+    out, nf = v20.validate_blocks_outcomes(m(), [b0, blocks.config_block(net, 2, bad_sig=True), b2])
+    assert nf == 3 and out[1] == [4] and out[2] is not None
