@@ -33,7 +33,7 @@ EXPORTED = [
     "fgv_validate_shard_dev_pipelined", "fgv_last_ahead", "fgv_set_ahead", "fgv_blocks_verify_signed",
     "fgv_validate_blocks_pipelined", "fgv_set_timing",
     "fgv_group_init", "fgv_group_destroy", "fgv_group_size", "fgv_group_ctx", "fgv_group_validate_blocks",
-    "fgv_group_set_block_outcomes", "fgv_group_last_block_status",
+    "fgv_group_set_block_outcomes", "fgv_group_last_block_status", "fgv_group_set_collective",
     "fgv_msp_resolve", "fgv_msp_resolve_blocks", "fgv_set_auto_resolve", "fgv_msp_identity",
     "fgv_kvmeta_set", "fgv_kvmeta_count", "fgv_kvmeta_get", "fgv_msp_identity_ous", "fgv_group_p256_verify_msgs",
 ]
@@ -168,6 +168,7 @@ def load():
         L.fgv_group_ctx.restype = vp
         L.fgv_group_validate_blocks.argtypes = [vp, sz, vp, vp, vp, sz, vp]
         L.fgv_group_set_block_outcomes.argtypes = [vp, ctypes.c_int]
+        L.fgv_group_set_collective.argtypes = [vp, ctypes.c_int]
         L.fgv_group_last_block_status.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
         L.fgv_finalize_flags_dev_plan.argtypes = [vp, sz, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         L.fgv_statedb_init.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
@@ -398,6 +399,13 @@ class Group:
     def set_block_outcomes(self, on=True):
         """fgv_group_set_block_outcomes: per-block results instead of a whole-batch Unsupported"""
         _check(self._L.fgv_group_set_block_outcomes(self._g, 1 if on else 0))
+
+    COLL_PEER, COLL_RCCL = 0, 1
+
+    def set_collective(self, mode):
+        """fgv_group_set_collective: COLL_PEER (peer copies onto device 0) or COLL_RCCL (ncclAllGather
+        of the records into every device + a finalize on each)"""
+        _check(self._L.fgv_group_set_collective(self._g, mode))
 
     def last_block_status(self, nblocks):
         """fgv_group_last_block_status -> (per-block status list, n_final), as Engine.last_block_status"""

@@ -11,14 +11,50 @@
 // markTXIdDuplicates (validator.go:279-295) -- as the finalize kernels.  Only the records cross
 // the fabric (a gather to one device, not an all-gather: the flags leave from there), and the
 // per-device work is TxValidator.Validate's, so results equal fgv_validate_blocks on one GPU.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <sched.h>
 
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "fgv_internal.h"
 #include "thread_pool.h"
+
+// RCCL, loaded on first use (fgv_group_set_collective): the library is resolved at run time with
+// RTLD_LOCAL so a host process that carries its own RCCL copy (a torch peer, say) keeps it apart
+// from ours, and a peer that never asks for the collective never loads it.
+namespace {
+struct Rccl {
+  void *h = nullptr;
+  decltype(&ncclCommInitAll) comm_init_all = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  bool load() {
+    if (h) return true;
+    for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+      h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (h) break;
+    }
+    if (!h) return false;
+    comm_init_all = reinterpret_cast<decltype(comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+    comm_destroy = reinterpret_cast<decltype(comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    all_gather = reinterpret_cast<decltype(all_gather)>(dlsym(h, "ncclAllGather"));
+    group_start = reinterpret_cast<decltype(group_start)>(dlsym(h, "ncclGroupStart"));
+    group_end = reinterpret_cast<decltype(group_end)>(dlsym(h, "ncclGroupEnd"));
+    return comm_init_all && comm_destroy && all_gather && group_start && group_end;
+  }
+};
+Rccl &rccl() {
+  static Rccl r;
+  return r;
+}
+std::mutex rccl_mu;  // (one-time load)
+}  // namespace
 
 struct fgv_group {
   std::vector<fgv_ctx *> ctx;
@@ -33,6 +69,13 @@ struct fgv_group {
   std::vector<int32_t> blk_status;
   size_t n_final = 0;
   int last_rc = FGV_OK;  // the last call's return code
+  // FGV_GROUP_COLL_RCCL: one RCCL communicator over the devices, the records all-gathered into
+  // every device's HBM on its own stream, the finalize on every device
+  int coll = FGV_GROUP_COLL_PEER;
+  std::vector<ncclComm_t> comms;
+  std::vector<hipStream_t> cs;   // per device: the collective's stream
+  std::vector<DevBuf> gathr;     // per device: world x rows records
+  std::vector<std::vector<uint8_t>> dflags;  // devices 1..: their finalized flags (checked equal)
 };
 
 extern "C" {
@@ -78,8 +121,54 @@ int fgv_group_init(const int *devices, size_t ndev, const fgv_config *cfg, fgv_g
   return FGV_OK;
 }
 
+static void coll_release(fgv_group *g) {
+  for (size_t i = 0; i < g->comms.size(); i++)
+    if (g->comms[i]) rccl().comm_destroy(g->comms[i]);
+  g->comms.clear();
+  for (size_t i = 0; i < g->cs.size(); i++)
+    if (hipSetDevice(g->dev[i]) == hipSuccess) {
+      if (g->cs[i]) hipStreamDestroy(g->cs[i]);
+      if (i < g->gathr.size()) g->gathr[i].release();
+    }
+  g->cs.clear();
+  g->gathr.clear();
+  g->dflags.clear();
+  g->coll = FGV_GROUP_COLL_PEER;
+}
+
+int fgv_group_set_collective(fgv_group *g, int mode) {
+  if (!g || (mode != FGV_GROUP_COLL_PEER && mode != FGV_GROUP_COLL_RCCL)) return FGV_EINVAL;
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (mode == g->coll) return FGV_OK;
+  coll_release(g);
+  if (mode == FGV_GROUP_COLL_PEER) return FGV_OK;
+  const size_t W = g->ctx.size();
+  for (size_t i = 0; i < W; i++)  // (a communicator has one rank per device)
+    for (size_t j = i + 1; j < W; j++)
+      if (g->dev[i] == g->dev[j]) return FGV_EINVAL;
+  {
+    std::lock_guard<std::mutex> l2(rccl_mu);
+    if (!rccl().load()) return FGV_EDEVICE;
+  }
+  g->comms.assign(W, nullptr);
+  if (rccl().comm_init_all(g->comms.data(), (int)W, g->dev.data()) != ncclSuccess) {
+    g->comms.clear();
+    return FGV_EDEVICE;
+  }
+  g->cs.assign(W, nullptr);
+  g->gathr.resize(W);
+  for (size_t i = 0; i < W; i++)
+    if (hipSetDevice(g->dev[i]) != hipSuccess || hipStreamCreateWithFlags(&g->cs[i], hipStreamNonBlocking) != hipSuccess) {
+      coll_release(g);
+      return FGV_EDEVICE;
+    }
+  g->coll = FGV_GROUP_COLL_RCCL;
+  return FGV_OK;
+}
+
 void fgv_group_destroy(fgv_group *g) {
   if (!g) return;
+  coll_release(g);
   delete g->pool;
   for (size_t i = 0; i < g->ctx.size(); i++) {
     if (hipSetDevice(g->dev[i]) == hipSuccess) g->res[i].release();
@@ -98,6 +187,8 @@ fgv_ctx *fgv_group_ctx(fgv_group *g, size_t i) { return g && i < g->ctx.size() ?
 
 static int group_validate_locked(fgv_group *g, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                                  uint8_t *flags, size_t flags_cap, size_t *ntx);
+static int group_outcomes(fgv_group *g, size_t nblocks, const size_t *ntx, const uint8_t *flags, bool soft,
+                          size_t n_final);
 
 int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const *blocks, const size_t *lens,
                               uint8_t *flags, size_t flags_cap, size_t *ntx) {
@@ -161,6 +252,7 @@ static int group_validate_locked(fgv_group *g, size_t nblocks, const uint8_t *co
       cap[q] = std::min(flags_cap, bytes / 2 + (b0[q + 1] - b0[q]));
     }
   }
+  const size_t capmax = *std::max_element(cap.begin(), cap.end());
   std::vector<int> rcs(W, FGV_OK);
   std::vector<uint32_t> split(W, UINT32_MAX);  // per-block outcomes: each device's first waiting block
   std::vector<std::vector<size_t>> ntx_dev(W, std::vector<size_t>(nblocks, 0));
@@ -170,7 +262,8 @@ static int group_validate_locked(fgv_group *g, size_t nblocks, const uint8_t *co
       rcs[r] = FGV_EDEVICE;
       return;
     }
-    if (!g->res[r].ensure(cap[r] * sizeof(fgv_tx_result) + 64)) {
+    // (the RCCL all-gather sends the same row count from every device: room for the largest share)
+    if (!g->res[r].ensure((g->coll == FGV_GROUP_COLL_RCCL ? capmax : cap[r]) * sizeof(fgv_tx_result) + 64)) {
       rcs[r] = FGV_ENOMEM;
       return;
     }
@@ -235,6 +328,42 @@ static int group_validate_locked(fgv_group *g, size_t nblocks, const uint8_t *co
     }
     return FGV_OK;
   }
+  if (g->coll == FGV_GROUP_COLL_RCCL) {
+    // ncclAllGather of every device's rows (68 B records, rank r's at r x rows, the
+    // layout fabric_amd/shard.py's all-gather makes) into every device's HBM over xGMI, then the
+    // finalize on every device -- each holds the batch's final flags; device 0's go to the caller
+    // and the others' are checked equal to them
+    std::vector<int> grc(W, FGV_OK);
+    g->pool->run(W, [&](size_t r) {
+      if (hipSetDevice(g->dev[r]) != hipSuccess) { grc[r] = FGV_EDEVICE; return; }
+      if (g->res[r].cap < rows * sizeof(fgv_tx_result) || !g->gathr[r].ensure(W * rows * sizeof(fgv_tx_result) + 64))
+        grc[r] = FGV_ENOMEM;
+    });
+    for (int rc : grc)
+      if (rc) return rc;
+    if (rccl().group_start() != ncclSuccess) return FGV_EDEVICE;
+    ncclResult_t nr = ncclSuccess;
+    for (size_t r = 0; r < W && nr == ncclSuccess; r++) {
+      if (hipSetDevice(g->dev[r]) != hipSuccess) { nr = ncclInvalidUsage; break; }
+      nr = rccl().all_gather(g->res[r].p, g->gathr[r].p, rows * sizeof(fgv_tx_result), ncclUint8, g->comms[r], g->cs[r]);
+    }
+    if (rccl().group_end() != ncclSuccess || nr != ncclSuccess) return FGV_EDEVICE;
+    g->dflags.resize(W);
+    for (size_t r = 1; r < W; r++) g->dflags[r].resize(all);
+    g->pool->run(W, [&](size_t r) {
+      if (hipSetDevice(g->dev[r]) != hipSuccess || hipStreamSynchronize(g->cs[r]) != hipSuccess) {
+        grc[r] = FGV_EDEVICE;
+        return;
+      }
+      grc[r] = fgv_finalize_flags_dev_plan(g->ctx[r], nblocks, ntx, (uint32_t)W, rows, lo.data(), hi.data(),
+                                           g->gathr[r].p, r == 0 ? flags : g->dflags[r].data());
+    });
+    for (int rc : grc)
+      if (rc) return rc;
+    for (size_t r = 1; r < W; r++)
+      if (memcmp(g->dflags[r].data(), flags, all) != 0) return FGV_EDEVICE;  // (devices disagree)
+    return group_outcomes(g, nblocks, ntx, flags, soft, n_final);
+  }
   // gather onto device 0 (rank r's rows at r x rows), then the finalize there
   if (hipSetDevice(g->dev[0]) != hipSuccess) return FGV_EDEVICE;
   if (!g->gath.ensure(W * rows * sizeof(fgv_tx_result) + 64)) return FGV_ENOMEM;
@@ -247,7 +376,13 @@ static int group_validate_locked(fgv_group *g, size_t nblocks, const uint8_t *co
   HIP_TRY(hipStreamSynchronize(g->s0));
   const int rc = fgv_finalize_flags_dev_plan(g->ctx[0], nblocks, ntx, (uint32_t)W, rows, lo.data(), hi.data(), dst,
                                              flags);
-  if (rc || !soft) return rc;
+  if (rc) return rc;
+  return group_outcomes(g, nblocks, ntx, flags, soft, n_final);
+}
+
+static int group_outcomes(fgv_group *g, size_t nblocks, const size_t *ntx, const uint8_t *flags, bool soft,
+                          size_t n_final) {
+  if (!soft) return FGV_OK;
   // per-block outcomes (fgv_last_block_status's rules): blocks from n_final on wait; a block with
   // an undecided transaction (0xFD) goes to the reference; the others are final
   g->blk_status.assign(nblocks, FGV_OK);

@@ -408,6 +408,18 @@ int fgv_group_validate_blocks(fgv_group *g, size_t nblocks, const uint8_t *const
  * after it (n_final), whether the earlier block is on the same device or on another one (a device
  * whose blocks change key-level state: the whole batch is checked on the host). */
 int fgv_group_set_block_outcomes(fgv_group *g, int on);
+/* How the group's records meet:
+ *   FGV_GROUP_COLL_PEER (default) -- gathered onto the first device with peer copies over xGMI,
+ *     finalized there (works with a device listed twice);
+ *   FGV_GROUP_COLL_RCCL -- one RCCL communicator over the group's devices (ncclCommInitAll; the
+ *     devices must be distinct): ncclAllGather of the 68 B records into every device's HBM, each
+ *     on its own stream, then the finalize on every device (the north star's collective; every
+ *     device holds the final flags, the caller gets the first device's and the others are checked
+ *     equal).  RCCL is loaded at run time (dlopen, RTLD_LOCAL).  FGV_EDEVICE when it is absent or
+ *     the communicator cannot be created; FGV_EINVAL for repeated devices. */
+#define FGV_GROUP_COLL_PEER 0
+#define FGV_GROUP_COLL_RCCL 1
+int fgv_group_set_collective(fgv_group *g, int mode);
 /* (after a failed group call: every status = its return code, n_final = 0, returns the code) */
 int fgv_group_last_block_status(fgv_group *g, int32_t *status, size_t n, size_t *n_final);
 /* fgv_p256_verify_msgs over all devices of the group (config C4 through the C ABI): items

@@ -162,3 +162,42 @@ def test_group_verify_msgs_c4_whole_batch():
     assert got.shape == (n,)
     bad = np.nonzero((got == 0) != exp)[0]
     assert len(bad) == 0, (len(bad), bad[:8], got[bad[:8]])
+
+
+def test_group_rccl_collective_world1():
+    """fgv_group_set_collective(RCCL) through the C ABI: an RCCL communicator over
+    the group's devices (world 1 on the box's one GPU), ncclAllGather of the records on the
+    engine's own stream, the finalize on every device; flags equal the peer-copy path's and the
+    oracle's, across duplicate txids of earlier blocks and per-block outcomes.  Repeated devices
+    cannot form a communicator: FGV_EINVAL, and the group keeps working on peer copies."""
+    net = network()
+    txs1 = []
+    blks = [blocks.make_block(net, 40, number=1, seed=901, faults=(), out_txs=txs1)[0]]
+    for i in range(2, 5):
+        reuse = {2: (txs1[i].creator, txs1[i].nonce)} if i == 3 else None
+        blks.append(blocks.make_block(net, 30 + 7 * i, number=i, seed=900 + i, reuse=reuse)[0])
+    exp = v20.validate_blocks(v20.ChannelModel(net.channel, net.identities(), net.chaincodes), blks)
+    g = _lib.Group([0])
+    try:
+        _setup(g.engines[0], net)
+        g.set_collective(_lib.Group.COLL_RCCL)
+        for rep in range(2):  # (the second call reuses the communicator and buffers)
+            got = g.validate_blocks(blks)
+            assert [list(f) for f in got] == [list(f) for f in exp], rep
+        g.set_block_outcomes(True)
+        got = g.validate_blocks(blks)
+        assert [list(f) for f in got] == [list(f) for f in exp]
+        assert g.last_block_status(len(blks)) == ([0] * len(blks), len(blks))
+        g.set_collective(_lib.Group.COLL_PEER)
+        assert [list(f) for f in g.validate_blocks(blks)] == [list(f) for f in exp]
+    finally:
+        g.close()
+    g2 = _lib.Group([0, 0])
+    try:
+        with pytest.raises(_lib.FgvError):
+            g2.set_collective(_lib.Group.COLL_RCCL)
+        for e in g2.engines:
+            _setup(e, net)
+        assert [list(f) for f in g2.validate_blocks(blks)] == [list(f) for f in exp]
+    finally:
+        g2.close()
