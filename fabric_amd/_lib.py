@@ -19,7 +19,7 @@ EXPORTED = [
     "fgv_init", "fgv_destroy", "fgv_strerror", "fgv_last_timing", "fgv_last_counts", "fgv_last_host_timing",
     "fgv_last_point_handovers", "fgv_last_kernel_times", "fgv_last_vb_timing",
     "fgv_sha256_batch",
-    "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_keys_register", "fgv_keys_register_tiered", "fgv_keys_reset", "fgv_key_stats",
+    "fgv_p256_verify_batch", "fgv_p256_verify_msgs", "fgv_p384_verify_msgs", "fgv_keys_register", "fgv_keys_register_tiered", "fgv_keys_reset", "fgv_key_stats",
     "fgv_set_block_outcomes", "fgv_last_block_status", "fgv_unsupported_stats", "fgv_stats_sums",
     "fgv_p256_verify_msgs_dev", "fgv_channel_init", "fgv_msp_add_identity", "fgv_chaincode_define",
     "fgv_ledger_add_txids", "fgv_validate_blocks", "fgv_validate_shard", "fgv_finalize_flags",
@@ -78,7 +78,8 @@ CC_COLLECTIONS_KNOWN, CC_KEY_LEVEL_EP = 1, 2
 class IdentityInfo(ctypes.Structure):
     """fgv_identity_info (include/fgv.h)"""
     _fields_ = [("key_type", ctypes.c_uint32), ("hash_family", ctypes.c_uint32), ("valid", ctypes.c_uint32),
-                ("roles", ctypes.c_uint32), ("pubkey", ctypes.c_uint8 * 64), ("id_digest", ctypes.c_uint8 * 32)]
+                ("roles", ctypes.c_uint32), ("pubkey", ctypes.c_uint8 * 64), ("id_digest", ctypes.c_uint8 * 32),
+                ("pubkey_p384", ctypes.c_uint8 * 96)]
 
 
 class _Config(ctypes.Structure):
@@ -120,6 +121,7 @@ def load():
         L.fgv_sha256_batch.argtypes = [vp, vp, sz, vp, vp, sz, vp]
         L.fgv_p256_verify_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp]
         L.fgv_p256_verify_msgs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
+        L.fgv_p384_verify_msgs.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
         L.fgv_keys_register.argtypes = [vp, vp, sz, vp]
         L.fgv_keys_register_tiered.argtypes = [vp, vp, sz, vp, vp]
         L.fgv_keys_reset.argtypes = [vp]
@@ -600,6 +602,18 @@ class Engine:
                                             n, _ptr(st)))
         return st
 
+    def verify_msgs_p384(self, keys, msgs, sigs):
+        """fgv_p384_verify_msgs: identity.Verify for P-384 keys (keys: n x 96 bytes X || Y)"""
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        marena, moffs, mlens = pack(msgs) if isinstance(msgs, list) else msgs
+        sarena, soffs, slens = pack(sigs) if isinstance(sigs, list) else sigs
+        n = len(soffs)
+        st = np.zeros(n, dtype=np.uint8)
+        _check(self._L.fgv_p384_verify_msgs(self._h, _ptr(keys), _ptr(marena), marena.size, _ptr(moffs),
+                                            _ptr(mlens), _ptr(sarena), sarena.size, _ptr(soffs), _ptr(slens),
+                                            n, _ptr(st)))
+        return st
+
     # --- key registry (MSP identity cache analogue)
     def keys_register(self, keys, hot=None):
         """hot: None (every key asks for a comb slot) or a per-key bool array (False: start on the
@@ -686,7 +700,9 @@ class Engine:
         info.hash_family = 1 if hash_family == "SHA3" else 0
         info.valid = 1 if valid else 0
         info.roles = ROLES_UNKNOWN if roles is None else int(roles)
-        if pub is not None:
+        if pub is not None and key == "p384":
+            ctypes.memmove(info.pubkey_p384, bytes(pub)[:96], min(96, len(pub)))
+        elif pub is not None:
             ctypes.memmove(info.pubkey, bytes(pub)[:64], min(64, len(pub)))
         ctypes.memmove(info.id_digest, bytes(id_digest), 32)
         _check(self._L.fgv_msp_register_identity(self._h, serialized, len(serialized), ctypes.byref(info)))
@@ -734,7 +750,8 @@ class Engine:
         if rc != 0:
             return None
         return dict(key=info.key_type, hash_family=info.hash_family, valid=bool(info.valid), roles=info.roles,
-                    pub=bytes(info.pubkey), id_digest=bytes(info.id_digest))
+                    pub=bytes(info.pubkey_p384) if info.key_type == KEY_TYPES["p384"] else bytes(info.pubkey),
+                    id_digest=bytes(info.id_digest))
 
     def ledger_add_txids(self, txids):
         arena, offs, lens = pack([t.encode() for t in txids])

@@ -17,12 +17,19 @@ __global__ __launch_bounds__(256) void k_der(const uint8_t *__restrict__ sig_buf
                                              const uint32_t *__restrict__ dn,
                                              uint8_t *__restrict__ status,
                                              uint32_t *__restrict__ r_limbs,
-                                             uint32_t *__restrict__ s_limbs) {
+                                             uint32_t *__restrict__ s_limbs,
+                                             const uint32_t *__restrict__ key_slot) {
   __builtin_amdgcn_s_setprio(3);  // on the verify chain; SHA-256 may be running beside it
   __shared__ uint32_t stage[256 * DER_STAGE_DW];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   // n: capacity (the r / s column stride); dn: the item count in device memory (or n)
   if (i >= (dn ? min(n, *dn) : n)) return;
+  if (key_slot && (key_slot[i] & KEY_P384_FLAG)) {  // a P-384 identity's signature: k_p384_verify
+    status[i] = ST_P384;
+#pragma unroll
+    for (int k = 0; k < 8; k++) r_limbs[(size_t)k * n + i] = s_limbs[(size_t)k * n + i] = 0;
+    return;
+  }
   uint32_t r[8], s[8];
   uint8_t code = ST_PENDING;
   const uint32_t L = len[i];

@@ -1455,13 +1455,14 @@ int fgv_block_add_identity(fgv_block_state *S, const uint8_t *ser, size_t len, i
   I.mspid = sid.mspid.str();
   I.id_bytes = sid.id_bytes.str();
   I.kind = (uint8_t)info->key_type;
-  I.key_slot = info->key_type == FGV_KEY_P256 ? key_slot : -1;
+  I.key_slot = (info->key_type == FGV_KEY_P256 || info->key_type == FGV_KEY_P384) ? key_slot : -1;
   I.hash3 = info->hash_family == FGV_HASH_SHA3;
   I.valid = info->valid != 0;
   I.roles_known = (info->roles & FGV_ROLES_UNKNOWN) == 0;
   I.roles = I.roles_known ? info->roles : 0;
   memcpy(I.digest, info->id_digest, 32);
   if (I.kind == FGV_KEY_P256) memcpy(I.pub, info->pubkey, 64);
+  if (I.kind == FGV_KEY_P384) memcpy(I.pub384, info->pubkey_p384, 96);
   std::string canon = I.mspid + std::string(reinterpret_cast<const char *>(info->id_digest), 32);
   auto it = ch.canon_ids.find(canon);
   if (it == ch.canon_ids.end()) it = ch.canon_ids.emplace(canon, (uint32_t)ch.canon_ids.size()).first;

@@ -41,6 +41,7 @@ struct Ident {
   int32_t msp = -1;             // interned Mspid
   uint8_t digest[32] = {};      // identity Id (SHA-256 of the certificate)
   uint8_t pub[64] = {};         // P-256 X || Y (FGV_KEY_P256)
+  uint8_t pub384[96] = {};      // P-384 X || Y (FGV_KEY_P384; key_slot = KEY_P384_FLAG | its table index)
   // GetOrganizationalUnits (msp/identities.go): (OU identifier, certifiers identifier) pairs,
   // interned by Channel::ou_intern; unknown unless the MSP cache miss or fgv_msp_identity_ous
   // gave them
@@ -54,11 +55,12 @@ struct Ident {
     return 0;
   }
   // the same for the committer's creator and endorsement signatures, whose digests follow the
-  // identity's hash family (SHA3 MSPs included since round 5: the SHA3-256 digest pass); the
-  // other Verify callers (orderer signatures) keep SHA3 identities outside the engine
+  // identity's hash family (SHA3 MSPs included since round 5: the SHA3-256 digest pass) and whose
+  // P-384 keys are verified per item (round 6, p384.hip); the other Verify callers (orderer
+  // signatures) keep SHA3 and P-384 identities outside the engine
   int verify_class_tx() const {
     if (kind == FGV_KEY_OTHER) return 1;
-    if (kind != FGV_KEY_P256 || key_slot < 0) return 2;
+    if ((kind != FGV_KEY_P256 && kind != FGV_KEY_P384) || key_slot < 0) return 2;
     return 0;
   }
 };

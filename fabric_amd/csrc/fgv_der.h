@@ -62,8 +62,10 @@ __host__ __device__ inline bool der_read_tl(const uint8_t *b, size_t n, size_t &
   return true;
 }
 
-// One INTEGER.  Writes the magnitude as 8 little-endian u32 limbs; big=true if >= 2^256.
-__host__ __device__ inline bool der_read_int(const uint8_t *b, size_t n, size_t &o, uint32_t limbs[8], bool &big,
+// One INTEGER.  Writes the magnitude as NLIMB little-endian u32 limbs (8: P-256, 12: P-384);
+// big=true if >= 2^(32 NLIMB).
+template <int NLIMB = 8>
+__host__ __device__ inline bool der_read_int(const uint8_t *b, size_t n, size_t &o, uint32_t limbs[NLIMB], bool &big,
                          bool &positive) {
   if (o == n) return false;  // "sequence truncated"
   DerTL t;
@@ -81,8 +83,8 @@ __host__ __device__ inline bool der_read_int(const uint8_t *b, size_t n, size_t 
     len--;
   }
   positive = !neg && len > 0;
-  big = len > 32;
-  for (int k = 0; k < 8; k++) limbs[k] = 0;
+  big = len > 4u * NLIMB;
+  for (int k = 0; k < NLIMB; k++) limbs[k] = 0;
   if (!big) {
     for (size_t i = 0; i < len; i++) {
       const size_t bytepos = len - 1 - i;  // little-endian byte index
@@ -93,8 +95,9 @@ __host__ __device__ inline bool der_read_int(const uint8_t *b, size_t n, size_t 
 }
 
 // Returns 0 on success (r, s written), 2 (FGV_SIG_DER) on any error.
-__host__ __device__ inline int der_decode_sig(const uint8_t *sig, size_t n, uint32_t r[8], uint32_t s[8], bool &r_big,
-                          bool &s_big) {
+template <int NLIMB = 8>
+__host__ __device__ inline int der_decode_sig(const uint8_t *sig, size_t n, uint32_t r[NLIMB], uint32_t s[NLIMB],
+                                              bool &r_big, bool &s_big) {
   size_t o = 0;
   DerTL t;
   if (n == 0 || !der_read_tl(sig, n, o, t)) return 2;
@@ -104,8 +107,8 @@ __host__ __device__ inline int der_decode_sig(const uint8_t *sig, size_t n, uint
   const size_t in_n = t.len;
   size_t io = 0;
   bool rp, sp;
-  if (!der_read_int(in, in_n, io, r, r_big, rp)) return 2;
-  if (!der_read_int(in, in_n, io, s, s_big, sp)) return 2;
+  if (!der_read_int<NLIMB>(in, in_n, io, r, r_big, rp)) return 2;
+  if (!der_read_int<NLIMB>(in, in_n, io, s, s_big, sp)) return 2;
   if (!rp || !sp) return 2;
   return 0;
 }

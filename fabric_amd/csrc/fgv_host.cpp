@@ -451,7 +451,7 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   for (hipStream_t x : {c->stream2, c->stream3, c->streamF, c->streamV, c->streamK})  // (a front half enqueued ahead)
     if (x) hipStreamSynchronize(x);
-  DevBuf *d[] = {&c->stage[0], &c->stage[1], &c->stage[2], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
+  DevBuf *d[] = {&c->p384_items, &c->stage[0], &c->stage[1], &c->stage[2], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
                  &c->bd_misc, &c->g_ok, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
                  &c->kmap, &c->vbt, &c->vbuse, &c->vbpromo, &c->vblist, &c->vbhand, &c->vbacc, &c->kt_id,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,
@@ -462,6 +462,7 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->mv) fgv_mvcc_free(c->mv);
   fgv_integrity_free(c);
   fgv_msp_cache_free(c);
+  fgv_p384_free(c);
   for (auto *b : d) b->release();
   HostBuf *h[] = {&c->h_status, &c->h_slot, &c->h_r, &c->h_s, &c->h_dig, &c->h_kq, &c->h_kslot,
                   &c->h_moff, &c->h_mlen, &c->hb_dig, &c->hb_vst, &c->hb_jobs, &c->hb_sigp,
@@ -995,6 +996,54 @@ int fgv_p256_verify_batch(fgv_ctx *c, const uint8_t *keys, const uint8_t *sig_bu
   return verify_core(c, keys, sig_buf, sig_buf_len, sig_off, sig_len, digests, n, status, false);
 }
 
+// identity.Verify for P-384 keys (bccsp sw ecdsaPublicKeyKeyVerifier over any NIST curve,
+// sw/ecdsa.go:41-75): SHA-256 of the messages (k_sha256), the keys registered in the context's
+// P-384 table (comb built once per key), then k_p384_verify -- one status byte per item.
+int fgv_p384_verify_msgs(fgv_ctx *c, const uint8_t *keys, const uint8_t *msg_buf, size_t msg_buf_len,
+                         const uint64_t *msg_off, const uint32_t *msg_len, const uint8_t *sig_buf, size_t sig_buf_len,
+                         const uint64_t *sig_off, const uint32_t *sig_len, size_t n, uint8_t *status) {
+  if (!c || (n && (!keys || !msg_off || !msg_len || !sig_off || !sig_len || !status))) return FGV_EINVAL;
+  if (n == 0) return FGV_OK;
+  if (n > 0x3fffffffu) return FGV_EINVAL;
+  for (size_t i = 0; i < n; i++)
+    if (sig_off[i] > sig_buf_len || sig_len[i] > sig_buf_len - sig_off[i]) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  // the columns k_p384_verify reads: absolute signature addresses, lengths, flagged key slots;
+  // digests at index i; status ST_P384 for every item
+  std::vector<uint32_t> slots(n);
+  for (size_t i = 0; i < n; i++) {
+    uint32_t k;
+    const int rc = fgv_p384_key_locked(c, keys + 96 * i, &k);
+    if (rc) return rc;
+    slots[i] = KEY_P384_FLAG | k;
+  }
+  int rc = sha_core(c, msg_buf, msg_buf_len, msg_off, msg_len, n);
+  if (rc) return rc;
+  const size_t col = n * 8 + n * 4 + n * 4;
+  if (!c->p384_items.ensure(col + sig_buf_len + 64) || !c->status.ensure(n)) return FGV_ENOMEM;
+  uint8_t *d = c->p384_items.as<uint8_t>();
+  uint8_t *dsig = d + col;
+  std::vector<uint64_t> ptr(n);
+  std::vector<uint32_t> len(n);
+  for (size_t i = 0; i < n; i++) {
+    ptr[i] = (uint64_t)(uintptr_t)(dsig + sig_off[i]);
+    len[i] = sig_len[i];
+  }
+  if (sig_buf_len) HIP_TRY(hipMemcpyAsync(dsig, sig_buf, sig_buf_len, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d, ptr.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d + n * 8, len.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d + n * 12, slots.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemsetAsync(c->status.p, ST_P384, n, c->stream));
+  rc = fgv_p384_launch(c, c->stream, (uint32_t)n, nullptr, c->status.as<uint8_t>(), reinterpret_cast<const uint64_t *>(d),
+                       reinterpret_cast<const uint32_t *>(d + n * 8), reinterpret_cast<const uint32_t *>(d + n * 12),
+                       nullptr, c->dig.as<uint8_t>());
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return FGV_OK;
+}
+
 int fgv_p256_verify_msgs(fgv_ctx *c, const uint8_t *keys, const uint8_t *msg_buf,
                          size_t msg_buf_len, const uint64_t *msg_off, const uint32_t *msg_len,
                          const uint8_t *sig_buf, size_t sig_buf_len, const uint64_t *sig_off,
@@ -1142,7 +1191,8 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *c, const uint8_t *d_msg_buf, const uint64_
     if (rc) return rc;
   }
   hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, d_sig_buf, d_sig_off,
-                     d_sig_len, N, (const uint32_t *)nullptr, d_status, c->r.as<uint32_t>(), c->s.as<uint32_t>());
+                     d_sig_len, N, (const uint32_t *)nullptr, d_status, c->r.as<uint32_t>(), c->s.as<uint32_t>(),
+                     (const uint32_t *)nullptr);
   HIP_TRY(hipGetLastError());
   c->timing_ran = true;
   rc = launch_inv(c, c->stream, N, nullptr, d_status, d_key_slot, c->r.as<uint32_t>(), c->s.as<uint32_t>());
@@ -1208,7 +1258,7 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
     // main stream (launched together, the SHA workgroups would occupy the CUs first)
     hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr, d_sigp,
                        d_sigl, N, (const uint32_t *)nullptr, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(),
-                       c->s.as<uint32_t>());
+                       c->s.as<uint32_t>(), d_slot);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[7], c->stream));
     HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev[7], 0));
@@ -1228,6 +1278,10 @@ int fgv_run_block_jobs(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blocks, co
     int rc = launch_prep_point(c, N, nullptr, N, c->bj_vst.as<uint8_t>(),
                                reinterpret_cast<const uint32_t *>(dsig + nv * 12), c->r.as<uint32_t>(),
                                c->bj_dig.as<uint8_t>(), reinterpret_cast<const uint32_t *>(dsig + nv * 16));
+    if (rc) return rc;
+    rc = fgv_p384_launch(c, c->stream, N, nullptr, c->bj_vst.as<uint8_t>(), reinterpret_cast<const uint64_t *>(dsig),
+                         reinterpret_cast<const uint32_t *>(dsig + nv * 8), reinterpret_cast<const uint32_t *>(dsig + nv * 12),
+                         reinterpret_cast<const uint32_t *>(dsig + nv * 16), c->bj_dig.as<uint8_t>());
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->hb_vst.p, c->bj_vst.p, nv, hipMemcpyDeviceToHost, c->stream));
     ran = true;
@@ -1262,7 +1316,7 @@ int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blo
     const uint32_t *d_sigl = reinterpret_cast<const uint32_t *>(dsig + nv * 8);
     const uint32_t *d_slot = reinterpret_cast<const uint32_t *>(dsig + nv * 12);
     hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, c->stream, (const uint8_t *)nullptr, d_sigp,
-                       d_sigl, N, dn, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(), c->s.as<uint32_t>());
+                       d_sigl, N, dn, c->bj_vst.as<uint8_t>(), c->r.as<uint32_t>(), c->s.as<uint32_t>(), d_slot);
     HIP_TRY(hipGetLastError());
     // k_inv beside the SHA-256 jobs when this call hashes (second stream); the device-parse
     // committer's hashes already run on the second stream (k_bd_sha), so k_inv follows k_der
@@ -1289,6 +1343,10 @@ int fgv_run_block_jobs_device(fgv_ctx *c, size_t nj, size_t nv, uint64_t sha_blo
                                reinterpret_cast<const uint32_t *>(dsig + nv * 12), c->r.as<uint32_t>(), digs,
                                reinterpret_cast<const uint32_t *>(dsig + nv * 16));
     if (rc) return rc;
+    rc = fgv_p384_launch(c, c->stream, N, dn, c->bj_vst.as<uint8_t>(), reinterpret_cast<const uint64_t *>(dsig),
+                         reinterpret_cast<const uint32_t *>(dsig + nv * 8), reinterpret_cast<const uint32_t *>(dsig + nv * 12),
+                         reinterpret_cast<const uint32_t *>(dsig + nv * 16), digs);
+    if (rc) return rc;
     ran = true;
   }
   c->stage_ran = ran;
@@ -1306,7 +1364,7 @@ int fgv_verify_prefix_dev(fgv_ctx *c, hipStream_t st, size_t cap, const uint32_t
   if (!r.ensure(cap * 32) || !s.ensure(cap * 32)) return FGV_ENOMEM;
   hipLaunchKernelGGL(k_der, dim3((N + 255) / 256), dim3(256), 0, st, (const uint8_t *)nullptr,
                      reinterpret_cast<const uint64_t *>(sigblk), reinterpret_cast<const uint32_t *>(sigblk + cap * 8), N,
-                     dn, vst, r.as<uint32_t>(), s.as<uint32_t>());
+                     dn, vst, r.as<uint32_t>(), s.as<uint32_t>(), reinterpret_cast<const uint32_t *>(sigblk + cap * 12));
   HIP_TRY(hipGetLastError());
   return launch_inv(c, st, N, dn, vst, reinterpret_cast<const uint32_t *>(sigblk + cap * 12), r.as<uint32_t>(),
                     s.as<uint32_t>(), w, wscr);
@@ -1320,6 +1378,12 @@ int fgv_verify_main_dev(fgv_ctx *c, size_t cap, const uint32_t *dn, size_t n_est
   int rc = launch_prep_point(c, (uint32_t)cap, dn, (uint32_t)std::min(n_est, cap), vst,
                              reinterpret_cast<const uint32_t *>(sigblk + cap * 12), r, digests,
                              reinterpret_cast<const uint32_t *>(sigblk + cap * 16), w);
+  // (P-384 identities' signatures: their own kernel, same stream, before the fold reads vst)
+  if (rc == FGV_OK)
+    rc = fgv_p384_launch(c, c->stream, (uint32_t)cap, dn, vst, reinterpret_cast<const uint64_t *>(sigblk),
+                         reinterpret_cast<const uint32_t *>(sigblk + cap * 8),
+                         reinterpret_cast<const uint32_t *>(sigblk + cap * 12),
+                         reinterpret_cast<const uint32_t *>(sigblk + cap * 16), digests);
   c->stage_ran = rc == FGV_OK;
   return rc;
 }
@@ -1351,6 +1415,17 @@ int fgv_msp_register_identity(fgv_ctx *c, const uint8_t *serialized, size_t len,
     int rc = keys_register_locked(c, info->pubkey, 1, &s, &want);
     if (rc) return rc;
     slot = (int32_t)s;
+  } else if (info->key_type == FGV_KEY_P384) {
+    // verified per item on the GPU (p384.hip) when the key is given; an all-zero key is "not
+    // known": the identity stays outside the engine, as before round 6
+    bool given = false;
+    for (int i = 0; i < 96; i++) given |= info->pubkey_p384[i] != 0;
+    if (given) {
+      uint32_t k;
+      int rc = fgv_p384_key_locked(c, info->pubkey_p384, &k);
+      if (rc) return rc;
+      slot = (int32_t)(KEY_P384_FLAG | k);
+    }
   }
   return fgv_block_add_identity(c->blk, serialized, len, slot, info);
 }

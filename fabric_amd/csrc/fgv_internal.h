@@ -100,8 +100,11 @@ struct FinPlan {
   size_t cap = 0, wn = 0, meta = 0;
 };
 
+struct fgv_p384_state;  // p384.hip: the context's P-384 keys and comb tables
 struct fgv_ctx {
   fgv_mvcc_state *mv = nullptr;
+  fgv_p384_state *p384 = nullptr;
+  DevBuf p384_items;  // fgv_p384_verify_msgs: item columns + signature bytes
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // k_der + k_inv of a block batch, concurrent with SHA-256
@@ -259,6 +262,13 @@ struct fgv_ctx {
   fgv_msp_cache *msp = nullptr;  // MSP models of the cache-miss path (fgv_msp.cpp)
 };
 void fgv_integrity_free(fgv_ctx *c);
+// P-384 identities (p384.hip): register a key (X || Y big-endian, 96 B) -> its table index, the
+// per-item verify launch over a verify list, teardown
+int fgv_p384_key_locked(fgv_ctx *c, const uint8_t pub[96], uint32_t *idx);
+uint32_t fgv_p384_nkeys(const fgv_ctx *c);
+int fgv_p384_launch(fgv_ctx *c, hipStream_t st, uint32_t n, const uint32_t *dn, uint8_t *status, const uint64_t *sigp,
+                    const uint32_t *sigl, const uint32_t *slot, const uint32_t *dig_idx, const uint8_t *digests);
+void fgv_p384_free(fgv_ctx *c);
 
 // Wait for a stream: polled (hipStreamQuery) when `spin`, else a blocking synchronize.  The
 // committer's calls wait ~0.8 ms for their batch; polling returns as soon as the last copy lands

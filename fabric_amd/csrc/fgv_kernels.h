@@ -37,6 +37,8 @@
 #define DIG_STRIDE 96        // bytes per item of the digit array (G digits, then Q digits at DIG_Q_OFF)
 #define ST_PENDING 0xFF
 #define ST_VB 0xFE       // k_inv: pending on the variable-base kernels (k_vb_mul / k_vb_fin finish it)
+#define ST_P384 0xFD     // k_der: a P-384 key (KEY_P384_FLAG in its key slot): k_p384_verify finishes it
+#define KEY_P384_FLAG 0x40000000u  // key slot of a P-384 identity: the flag | its index in the P-384 key table
 
 struct apoint_raw {  // affine point, Montgomery limbs (64 B, 16-B aligned)
   uint32_t x[8];
@@ -122,8 +124,20 @@ __global__ void k_sha256(const uint8_t *buf, const uint64_t *off, const uint32_t
 // Verify stages: n is the batch capacity (the column stride of r / s / w); dn (optional) points
 // to the item count in device memory, written by an earlier kernel on the stream (the block
 // committer's job counts), so the stages are enqueued without the host knowing it.
+// key_slot (optional): a slot with KEY_P384_FLAG marks a P-384 identity's signature -> ST_P384
 __global__ void k_der(const uint8_t *sig_buf, const uint64_t *off, const uint32_t *len, uint32_t n,
-                      const uint32_t *dn, uint8_t *status, uint32_t *r_limbs, uint32_t *s_limbs);
+                      const uint32_t *dn, uint8_t *status, uint32_t *r_limbs, uint32_t *s_limbs,
+                      const uint32_t *key_slot);
+// P-384 (p384.hip): the committer's P-384 identities, verified per item beside the P-256 chain
+#define P384_WIN 48                                   // 8-bit windows of a scalar < 2^384
+#define P384_TK 255                                   // entries d = 1..255 per window
+#define P384_ENTRIES ((size_t)P384_WIN * P384_TK)     // 12,240 affine points per comb table
+#define P384_ENTRY_WORDS 24                           // x || y, Montgomery, 12 limbs each
+#define P384_LANES 4                                  // lanes per verify (windows split across them)
+__global__ void k_p384_verify(uint32_t n, const uint32_t *dn, uint8_t *status, const uint64_t *sigp,
+                              const uint32_t *sigl, const uint32_t *slot, const uint32_t *dig_idx,
+                              const uint8_t *digests, const uint32_t *gtab, const uint32_t *ktab,
+                              const uint8_t *key_ok, uint32_t nkeys);
 
 // ---- MVCC (mvcc.hip)
 #define MV_NIL 16       // NIL_TXACTION

@@ -706,6 +706,7 @@ int fgv_msp_identity(fgv_ctx *c, const uint8_t *serialized, size_t len, fgv_iden
     out->valid = I.valid;
     out->roles = I.roles_known ? I.roles : FGV_ROLES_UNKNOWN;
     memcpy(out->pubkey, I.pub, 64);
+    memcpy(out->pubkey_p384, I.pub384, 96);
     memcpy(out->id_digest, I.digest, 32);
     return FGV_OK;
   }

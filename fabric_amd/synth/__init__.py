@@ -33,6 +33,13 @@ def lib():
                                                ctypes.c_size_t, ctypes.c_void_p]
         L.synth_make_cert_ed25519.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                               ctypes.c_char_p, ctypes.c_long, ctypes.c_char_p, ctypes.c_size_t]
+        L.synth_p384_keygen.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p,
+                                        ctypes.c_char_p]
+        L.synth_p384_sign_rs.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                                         ctypes.c_char_p, ctypes.c_char_p]
+        L.synth_make_cert_p384.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                           ctypes.c_char_p, ctypes.c_char_p, ctypes.c_long, ctypes.c_char_p,
+                                           ctypes.c_size_t]
         _LIB = L
     return _LIB
 
@@ -124,6 +131,57 @@ def make_cert_ed25519(subject: EdKey, issuer: Key, cn: str, org: str, issuer_cn:
     out = ctypes.create_string_buffer(4096)
     n = lib().synth_make_cert_ed25519(subject.priv, issuer.priv, cn.encode(), org.encode(), issuer_cn.encode(),
                                       serial, out, 4096)
+    if n < 0:
+        raise RuntimeError("certificate generation failed")
+    return out.raw[:n]
+
+
+# ---------------------------------------------------------------- P-384 identities
+N384 = int("ffffffffffffffffffffffffffffffffffffffffffffffffc7634d81f4372ddf581a0db248b0a77aecec196accc52973", 16)
+
+
+class Key384:
+    """A P-384 key pair derived deterministically from (seed, idx); pub = X || Y (96 bytes)."""
+
+    kind = "p384"
+
+    def __init__(self, seed: int, idx: int):
+        priv = ctypes.create_string_buffer(48)
+        qx = ctypes.create_string_buffer(48)
+        qy = ctypes.create_string_buffer(48)
+        lib().synth_p384_keygen(seed, idx, priv, qx, qy)
+        self.priv, self.qx, self.qy = priv.raw, qx.raw, qy.raw
+
+    @property
+    def pub(self) -> bytes:
+        return self.qx + self.qy
+
+
+def der_encode_int(r: int, s: int) -> bytes:
+    """DER ECDSASignature of arbitrary-size non-negative r, s (minimal INTEGERs)"""
+    def i(v):
+        b = v.to_bytes(v.bit_length() // 8 + 1, "big")
+        return b"\x02" + bytes([len(b)]) + b
+    body = i(r) + i(s)
+    return b"\x30" + bytes([len(body)]) + body
+
+
+def sign384_rs(key: Key384, digest: bytes, high_s: bool = False):
+    r = ctypes.create_string_buffer(48)
+    s = ctypes.create_string_buffer(48)
+    lib().synth_p384_sign_rs(key.priv, digest, len(digest), 1 if high_s else 0, r, s)
+    return int.from_bytes(r.raw, "big"), int.from_bytes(s.raw, "big")
+
+
+def sign384(key: Key384, digest: bytes, high_s: bool = False) -> bytes:
+    return der_encode_int(*sign384_rs(key, digest, high_s))
+
+
+def make_cert_p384(subject: Key384, issuer: Key, cn: str, org: str, issuer_cn: str, serial: int, ou: str = "") -> bytes:
+    """X.509 certificate of a P-384 key issued by a P-256 CA (ecdsa-with-SHA256)"""
+    out = ctypes.create_string_buffer(4096)
+    n = lib().synth_make_cert_p384(subject.priv, issuer.priv, cn.encode(), org.encode(), ou.encode(),
+                                   issuer_cn.encode(), serial, out, 4096)
     if n < 0:
         raise RuntimeError("certificate generation failed")
     return out.raw[:n]

@@ -19,7 +19,7 @@ vendor/github.com/hyperledger/fabric-protos-go).
 import hashlib
 import random
 
-from . import EdKey, Key, ed25519_sign_batch, make_cert, make_cert_ed25519, sign_batch
+from . import EdKey, Key, Key384, ed25519_sign_batch, make_cert, make_cert_ed25519, make_cert_p384, sign384, sign_batch
 
 # ------------------------------------------------------------------ proto3 encoding
 
@@ -180,7 +180,8 @@ class Network:
     and number of the peers that hold Ed25519 keys (config C5, "Fabric v3" identities)."""
 
     def __init__(self, seed=3, orgs=3, clients=100, channel="testchannel", policy_n=2, pems=None,
-                 peers_per_org=1, ed25519_frac=0.0, ed25519_peers=0, hash_families=None):
+                 peers_per_org=1, ed25519_frac=0.0, ed25519_peers=0, hash_families=None, p384_clients=0,
+                 p384_peers=0):
         """pems: certificates exported by another process (Network.export_pems()) -- X.509
         signatures are randomised, so multi-process users share one set of certificates.
         hash_families: {mspid: "SHA3"} -- that MSP's identities sign SHA3-256 digests (its
@@ -195,6 +196,9 @@ class Network:
         kc = int(round(ed25519_frac * clients))
         ed_clients = set(sel.sample(range(clients), kc)) if kc else set()
         ed_peers = set(sel.sample(range(npeer), min(ed25519_peers, npeer))) if ed25519_peers else set()
+        # P-384 identities (round 6): the first p384_clients clients and p384_peers peers not drawn above
+        p384_c = set([c for c in range(clients) if c not in ed_clients][:p384_clients])
+        p384_p = set([q for q in range(npeer) if q not in ed_peers][:p384_peers])
 
         def cert(*a):  # reuse exported certificates in order
             return next(_pem_iter) if _pem_iter is not None else make_cert(*a)
@@ -213,6 +217,10 @@ class Network:
                 if idx in ed_peers:
                     pk = EdKey(seed, 20_000 + idx)
                     pem = ed_cert(pk, self.cas[o], name, m, f"ca.org{o + 1}", 100 + idx)
+                elif idx in p384_p:
+                    pk = Key384(seed, 20_000 + idx)
+                    pem = next(_pem_iter) if _pem_iter is not None else make_cert_p384(
+                        pk, self.cas[o], name, m, f"ca.org{o + 1}", 100 + idx)
                 else:
                     pk = Key(seed, 20_000 + idx)
                     pem = cert(pk, self.cas[o], name, m, f"ca.org{o + 1}", False, 100 + idx)
@@ -225,6 +233,10 @@ class Network:
             if c in ed_clients:
                 ck = EdKey(seed, 30_000 + c)
                 pem = ed_cert(ck, self.cas[o], name, self.mspids[o], f"ca.org{o + 1}", 1000 + c)
+            elif c in p384_c:
+                ck = Key384(seed, 30_000 + c)
+                pem = next(_pem_iter) if _pem_iter is not None else make_cert_p384(
+                    ck, self.cas[o], name, self.mspids[o], f"ca.org{o + 1}", 1000 + c)
             else:
                 ck = Key(seed, 30_000 + c)
                 pem = cert(ck, self.cas[o], name, self.mspids[o], f"ca.org{o + 1}", False, 1000 + c)
@@ -259,6 +271,10 @@ class Network:
         out = []
         for ident in self.peers + self.clients:
             role_bit = 1 << (3 if ident.role == "peer" else 2)
+            if ident.kind == "p384":  # (round 6: verified per item on the GPU)
+                out.append((ident.serialized, Identity(ident.mspid, ident.key.pub, True, ident.id_digest, key="p384",
+                                                       roles=1 | role_bit, hash_family=ident.hash_family)))
+                continue
             if ident.kind != "p256":
                 out.append((ident.serialized, Identity(ident.mspid, None, True, ident.id_digest, key="undeserializable")))
                 continue
@@ -327,8 +343,8 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         if force is not None and force[i] is not None:
             t.label = force[i]
         t.creator = net.rogue if t.label == "rogue_creator" else rng.choice(net.clients)
-        if t.creator.kind != "p256" and t.label in ("clean", "one_bad_endorsement", "policy_unsatisfied",
-                                                     "bad_creator_sig", "high_s_creator"):
+        if t.creator.kind not in ("p256", "p384") and t.label in ("clean", "one_bad_endorsement", "policy_unsatisfied",
+                                                                   "bad_creator_sig", "high_s_creator"):
             t.label = "ed25519_creator"  # DeserializeIdentity fails
         t.nonce = bytes(rng.getrandbits(8) for _ in range(24))
         if reuse and i in reuse:
@@ -344,7 +360,7 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
             else:
                 # relabelled clean: the creator-kind rule above applies again (an Ed25519 creator
                 # cannot be a clean transaction: DeserializeIdentity fails, code 4)
-                t.label = "clean" if t.creator.kind == "p256" else "ed25519_creator"
+                t.label = "clean" if t.creator.kind in ("p256", "p384") else "ed25519_creator"
         r = rng.random()
         ne, accp = endorse_dist[-1][0], 0.0
         for e, p in endorse_dist:
@@ -373,7 +389,7 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         if t.label in _ENDORSE_LABELS:
             # distinct orgs among the P-256 endorsers with a good signature (Ed25519 endorsers
             # fail DeserializeIdentity and are skipped) must satisfy OutOf(policy_n, orgs)
-            good = {e.mspid for j, e in enumerate(t.endorsers) if e.kind == "p256" and j != t.bad_endorsement}
+            good = {e.mspid for j, e in enumerate(t.endorsers) if e.kind in ("p256", "p384") and j != t.bad_endorsement}
             if len(good) < getattr(net, "policy_n", 2):
                 t.label = "endorse_short"
         t.reads = [(f"k{rng.randrange(key_space):07d}", (rng.randrange(1, 1000), rng.randrange(500)))
@@ -390,6 +406,7 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         rwsets = rwsets([t.label for t in txs])
     # pass 1: headers, proposal response payloads, endorsement digests
     e_privs, e_digests, e_refs = [], [], []
+    p384_refs = []  # (tx, endorsement index, DER signature) of P-384 endorsers
     ed_privs, ed_msgs, ed_refs = [], [], []
     for t in txs:
         txid = hashlib.sha256(t.nonce + t.creator.serialized).hexdigest()
@@ -419,6 +436,9 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
         cca = f_bytes(1, rw) + f_bytes(2, events) + f_msg(3, f_varint(1, 200)) + f_msg(4, chaincode_id(ccname, "1.0"))
         t.prp = f_bytes(1, ph) + f_bytes(2, cca)
         for j, e in enumerate(t.endorsers):
+            if e.kind == "p384":
+                p384_refs.append((t, j, sign384(e.key, verify_digest(e, t.prp + e.serialized))))
+                continue
             if e.kind != "p256":
                 ed_privs.append(e.key.priv)
                 ed_msgs.append(t.prp + e.serialized)
@@ -430,7 +450,8 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
     esigs = sign_batch(b"".join(e_privs), b"".join(e_digests), len(e_privs), threads=threads) if e_privs else []
     for t in txs:
         t.esigs = [None] * len(t.endorsers)
-    for (t, j), s in list(zip(e_refs, esigs)) + list(zip(ed_refs, ed25519_sign_batch(b"".join(ed_privs), ed_msgs))):
+    for (t, j), s in list(zip(e_refs, esigs)) + list(zip(ed_refs, ed25519_sign_batch(b"".join(ed_privs), ed_msgs))) + \
+            [((t, j), s) for t, j, s in p384_refs]:
         if j == t.bad_endorsement:
             s = s[:10] + bytes([s[10] ^ 0x55]) + s[11:]
         t.esigs[j] = s
@@ -453,19 +474,25 @@ def make_block(net: Network, ntx: int, number: int = 1, seed: int = 0, faults=FA
             c_digests.append(verify_digest(t.creator, t.payload))
     csigs = sign_batch(b"".join(c_privs), b"".join(c_digests), len(c_privs), threads=threads,
                        high_s=False) if c_privs else []
-    ed_tx = [t for t in txs if t.creator.kind != "p256"]
+    ed_tx = [t for t in txs if t.creator.kind == "ed25519"]
     ed_sigs = iter(ed25519_sign_batch(b"".join(t.creator.key.priv for t in ed_tx), [t.payload for t in ed_tx]))
     p_sigs = iter(csigs)
-    csigs = [next(p_sigs) if t.creator.kind == "p256" else next(ed_sigs) for t in txs]
+    csigs = [next(p_sigs) if t.creator.kind == "p256" else
+             sign384(t.creator.key, verify_digest(t.creator, t.payload)) if t.creator.kind == "p384" else next(ed_sigs)
+             for t in txs]
     envs = []
     for t, s in zip(txs, csigs):
         if t.label == "bad_creator_sig":
             s = s[:12] + bytes([s[12] ^ 0x21]) + s[13:]
         if t.label == "high_s_creator":
             from .workloads import _der_int, _der_rs, N
+            from . import N384, der_encode_int
             r_, s_ = _der_rs(s)
-            body = _der_int(r_) + _der_int(N - s_)
-            s = b"\x30" + bytes([len(body)]) + body
+            if t.creator.kind == "p384":
+                s = der_encode_int(r_, N384 - s_)
+            else:
+                body = _der_int(r_) + _der_int(N - s_)
+                s = b"\x30" + bytes([len(body)]) + body
         if t.label == "no_sig":
             s = b""
         env = f_bytes(1, t.payload) + f_bytes(2, s)

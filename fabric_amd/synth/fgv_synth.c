@@ -274,3 +274,110 @@ int synth_make_cert_ed25519(const uint8_t subj_ed_priv[32], const uint8_t issuer
   EVP_PKEY_free(ipk);
   return ret;
 }
+
+/* ---------------------------------------------------------------- P-384 identities
+ * Keys, signatures (over a 32-byte SHA-256 / SHA3-256 digest, as identity.Verify hashes with the
+ * MSP's family; Fabric signers emit low-S) and certificates issued by a P-256 CA. */
+static EC_GROUP *G384;
+static pthread_once_t G384_ONCE = PTHREAD_ONCE_INIT;
+static void g384_init(void) { G384 = EC_GROUP_new_by_curve_name(NID_secp384r1); }
+static EC_GROUP *g384(void) {
+  pthread_once(&G384_ONCE, g384_init);
+  return G384;
+}
+static EC_KEY *key384_from_priv(const uint8_t priv[48]) {
+  EC_KEY *k = EC_KEY_new_by_curve_name(NID_secp384r1);
+  BIGNUM *d = BN_bin2bn(priv, 48, NULL);
+  EC_POINT *pub = EC_POINT_new(g384());
+  EC_POINT_mul(g384(), pub, d, NULL, NULL, NULL);
+  EC_KEY_set_private_key(k, d);
+  EC_KEY_set_public_key(k, pub);
+  EC_POINT_free(pub);
+  BN_free(d);
+  return k;
+}
+/* priv = SHA-384("fgv-p384" || seed || idx || ctr) in [1, n-1] */
+int synth_p384_keygen(uint64_t seed, uint32_t idx, uint8_t priv[48], uint8_t qx[48], uint8_t qy[48]) {
+  const BIGNUM *n = EC_GROUP_get0_order(g384());
+  for (uint32_t ctr = 0;; ctr++) {
+    uint8_t buf[8 + 8 + 4 + 4];
+    memcpy(buf, "fgv-p384", 8);
+    memcpy(buf + 8, &seed, 8);
+    memcpy(buf + 16, &idx, 4);
+    memcpy(buf + 20, &ctr, 4);
+    SHA384(buf, sizeof buf, priv);
+    BIGNUM *d = BN_bin2bn(priv, 48, NULL);
+    int ok = !BN_is_zero(d) && BN_cmp(d, n) < 0;
+    BN_free(d);
+    if (ok) break;
+  }
+  EC_KEY *k = key384_from_priv(priv);
+  BIGNUM *x = BN_new(), *y = BN_new();
+  EC_POINT_get_affine_coordinates(g384(), EC_KEY_get0_public_key(k), x, y, NULL);
+  BN_bn2binpad(x, qx, 48);
+  BN_bn2binpad(y, qy, 48);
+  BN_free(x);
+  BN_free(y);
+  EC_KEY_free(k);
+  return 0;
+}
+/* raw (r, s), 48 bytes each; mode 0 low-S, 1 the high-S twin */
+int synth_p384_sign_rs(const uint8_t priv[48], const uint8_t *digest, size_t dlen, int mode, uint8_t r[48], uint8_t s[48]) {
+  EC_KEY *k = key384_from_priv(priv);
+  ECDSA_SIG *sig = ECDSA_do_sign(digest, (int)dlen, k);
+  const BIGNUM *br, *bs;
+  ECDSA_SIG_get0(sig, &br, &bs);
+  const BIGNUM *n = EC_GROUP_get0_order(g384());
+  BIGNUM *half = BN_dup(n);
+  BN_rshift1(half, half);
+  BIGNUM *ss = BN_dup(bs);
+  int high = BN_cmp(ss, half) > 0;
+  if ((mode == 0 && high) || (mode == 1 && !high)) BN_sub(ss, n, ss);
+  BN_bn2binpad(br, r, 48);
+  BN_bn2binpad(ss, s, 48);
+  BN_free(ss);
+  BN_free(half);
+  ECDSA_SIG_free(sig);
+  EC_KEY_free(k);
+  return 0;
+}
+/* X.509 v3 certificate for a P-384 subject key, signed by a P-256 issuer key (ecdsa-with-SHA256) */
+int synth_make_cert_p384(const uint8_t subj_priv[48], const uint8_t issuer_priv[32], const char *cn, const char *org,
+                         const char *ou, const char *issuer_cn, long serial, char *pem_out, size_t cap) {
+  EC_KEY *sk = key384_from_priv(subj_priv), *ik = key_from_priv(issuer_priv);
+  EVP_PKEY *spk = EVP_PKEY_new(), *ipk = EVP_PKEY_new();
+  EVP_PKEY_assign_EC_KEY(spk, sk);
+  EVP_PKEY_assign_EC_KEY(ipk, ik);
+  X509 *x = X509_new();
+  X509_set_version(x, 2);
+  ASN1_INTEGER_set(X509_get_serialNumber(x), serial);
+  ASN1_TIME_set_string(X509_getm_notBefore(x), "20240101000000Z");
+  ASN1_TIME_set_string(X509_getm_notAfter(x), "20340101000000Z");
+  X509_NAME *sn = X509_NAME_new(), *in = X509_NAME_new();
+  X509_NAME_add_entry_by_txt(sn, "O", MBSTRING_ASC, (const unsigned char *)org, -1, -1, 0);
+  if (ou && *ou) X509_NAME_add_entry_by_txt(sn, "OU", MBSTRING_ASC, (const unsigned char *)ou, -1, -1, 0);
+  X509_NAME_add_entry_by_txt(sn, "CN", MBSTRING_ASC, (const unsigned char *)cn, -1, -1, 0);
+  X509_NAME_add_entry_by_txt(in, "O", MBSTRING_ASC, (const unsigned char *)org, -1, -1, 0);
+  X509_NAME_add_entry_by_txt(in, "CN", MBSTRING_ASC, (const unsigned char *)issuer_cn, -1, -1, 0);
+  X509_set_subject_name(x, sn);
+  X509_set_issuer_name(x, in);
+  X509_set_pubkey(x, spk);
+  X509_sign(x, ipk, EVP_sha256());
+  BIO *b = BIO_new(BIO_s_mem());
+  PEM_write_bio_X509(b, x);
+  char *data;
+  long len = BIO_get_mem_data(b, &data);
+  int ret = -1;
+  if (len >= 0 && (size_t)len < cap) {
+    memcpy(pem_out, data, len);
+    pem_out[len] = 0;
+    ret = (int)len;
+  }
+  BIO_free(b);
+  X509_NAME_free(sn);
+  X509_NAME_free(in);
+  X509_free(x);
+  EVP_PKEY_free(spk);
+  EVP_PKEY_free(ipk);
+  return ret;
+}

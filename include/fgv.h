@@ -115,6 +115,15 @@ int fgv_p256_verify_batch(fgv_ctx *ctx, const uint8_t *keys, const uint8_t *sig_
 
 /* Fused identity.Verify(msg, sig): digest = SHA-256(msg) on the device, then verify.
  * Replaces msp/identities.go:170-199 (getHashOpt SHA2 + bccsp.Hash + bccsp.Verify). */
+/* identity.Verify(msg, sig) for P-384 keys (replaces bccsp sw verifyECDSA for the P-384 curve,
+ * fabric-lib-go bccsp/sw/ecdsa.go:41-57 with the P-384 half order of bccsp/utils/ecdsa.go:26-31):
+ * keys n x 96 bytes (X || Y big-endian), digest = SHA-256(msg), Go-rule DER, low S, then the
+ * equation on the GPU (per-key comb tables built once per context).  Same status bytes as P-256
+ * (5: the key is not a P-384 point).  The committer verifies P-384 creators and endorsers the same
+ * way when their identities are registered with pubkey_p384. */
+int fgv_p384_verify_msgs(fgv_ctx *ctx, const uint8_t *keys, const uint8_t *msg_buf, size_t msg_buf_len,
+                         const uint64_t *msg_off, const uint32_t *msg_len, const uint8_t *sig_buf, size_t sig_buf_len,
+                         const uint64_t *sig_off, const uint32_t *sig_len, size_t n, uint8_t *status);
 int fgv_p256_verify_msgs(fgv_ctx *ctx, const uint8_t *keys, const uint8_t *msg_buf,
                          size_t msg_buf_len, const uint64_t *msg_off, const uint32_t *msg_len,
                          const uint8_t *sig_buf, size_t sig_buf_len, const uint64_t *sig_off,
@@ -205,7 +214,8 @@ int fgv_p256_verify_msgs_dev(fgv_ctx *ctx, const uint8_t *d_msg_buf, const uint6
  * (same MSP, valid, an (OU, certifier) pair of the identity), ANONYMITY (NOMINAL: any identity)
  * and COMBINED (every principal it collects, in order). */
 #define FGV_KEY_P256 1             /* verified on the GPU                                      */
-#define FGV_KEY_P384 2             /* bccsp verifies it: outside the engine                    */
+#define FGV_KEY_P384 2             /* P-384: verified per item on the GPU when pubkey_p384 is given
+                                      (committer signatures; all zero: outside the engine)      */
 #define FGV_KEY_OTHER 3            /* RSA etc.: Verify fails                        */
 #define FGV_KEY_UNDESERIALIZABLE 4 /* DeserializeIdentity fails (Ed25519 under Fabric 2.x, F4)  */
 #define FGV_HASH_SHA2 0
@@ -221,6 +231,7 @@ typedef struct fgv_identity_info {
                              477-660); or FGV_ROLES_UNKNOWN                                    */
   uint8_t pubkey[64];     /* P-256 X || Y (FGV_KEY_P256)                                      */
   uint8_t id_digest[32];  /* identity Id: SHA-256 of the certificate (common/policies/policy.go:375) */
+  uint8_t pubkey_p384[96]; /* P-384 X || Y big-endian (FGV_KEY_P384); all zero: key not given  */
 } fgv_identity_info;
 #define FGV_CC_COLLECTIONS_KNOWN 1u /* the definition's collections are all declared           */
 #define FGV_CC_KEY_LEVEL_EP 2u      /* the state holds key-level endorsement (SBE) metadata for

@@ -35,6 +35,7 @@ def lib():
         L.oracle_verify_msgs_batch.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_size_t, ctypes.c_void_p,
                                                                        ctypes.c_int, ctypes.c_int]
         L.oracle_verify_msgs_batch.restype = None
+        L.oracle_p384_verify_der.argtypes = [c_u8p, c_u8p, c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_size_t]
         _LIB = L
     return _LIB
 
@@ -61,6 +62,12 @@ def verify_der(qx: bytes, qy: bytes, sig: bytes, digest: bytes, ossl: bool = Fal
     """bccsp Verify(pk, sig, digest) status byte (0 = valid)."""
     f = lib().oracle_p256_verify_der_ossl if ossl else lib().oracle_p256_verify_der
     return f(qx, qy, sig, len(sig), digest, len(digest))
+
+
+def verify_der_p384(pub96: bytes, sig: bytes, digest: bytes) -> int:
+    """bccsp Verify for a P-384 key (X || Y, 96 bytes): Go-rule DER, the P-384 half order, then
+    the equation (OpenSSL arithmetic) -- status byte, 0 = valid."""
+    return lib().oracle_p384_verify_der(pub96[:48], pub96[48:96], sig, len(sig), digest, len(digest))
 
 
 def identity_verify(qx: bytes, qy: bytes, msg: bytes, sig: bytes, ossl: bool = False) -> int:

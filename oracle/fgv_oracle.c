@@ -700,3 +700,54 @@ void oracle_verify_msgs_batch(const uint8_t *keys, const uint8_t *msg_buf, const
   }
   for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
 }
+
+/* ------------------------------------------------------- P-384 (OpenSSL back-end)
+ * bccsp sw verifyECDSA for a P-384 key (fabric-lib-go bccsp/sw/ecdsa.go:41-57): the same Go-rule
+ * DER decode (48-byte integers), the low-S rule with the P-384 half order (bccsp/utils/
+ * ecdsa.go:26-31), then Go ecdsa.Verify's rules with OpenSSL's group arithmetic (r, s in [1, n),
+ * the 32-byte digest as e -- no truncation against a 384-bit order --, R != inf, x_R mod n == r).
+ * Status bytes as for P-256. */
+int oracle_p384_verify_der(const uint8_t qx[48], const uint8_t qy[48], const uint8_t *sig, size_t sig_len,
+                           const uint8_t *digest, size_t digest_len) {
+  if (sig_len == 0 || digest_len == 0) return 6;
+  size_t off = 0, len;
+  int cls, compound, tag;
+  if (der_tag_len(sig, sig_len, &off, &cls, &compound, &tag, &len)) return 2;
+  if (cls != 0 || tag != 16 || !compound) return 2;
+  if (off + len < off || off + len > sig_len) return 2;
+  const uint8_t *inner = sig + off, *rv, *sv;
+  size_t io = 0, rl, sl;
+  int rneg, sneg;
+  if (der_integer(inner, len, &io, &rv, &rl, &rneg)) return 2;
+  if (der_integer(inner, len, &io, &sv, &sl, &sneg)) return 2;
+  int rz = 1, sz = 1;
+  for (size_t i = 0; i < rl; i++) if (rv[i]) rz = 0;
+  for (size_t i = 0; i < sl; i++) if (sv[i]) sz = 0;
+  if (rneg || rz || sneg || sz) return 2;
+  int ret = 1;
+  EC_KEY *key = EC_KEY_new_by_curve_name(NID_secp384r1);
+  const EC_GROUP *grp = EC_KEY_get0_group(key);
+  BIGNUM *br = BN_bin2bn(rv, (int)rl, NULL), *bs = BN_bin2bn(sv, (int)sl, NULL);
+  BIGNUM *half = BN_dup(EC_GROUP_get0_order(grp));
+  BIGNUM *bx = BN_bin2bn(qx, 48, NULL), *by = BN_bin2bn(qy, 48, NULL);
+  BN_rshift1(half, half);
+  if (BN_cmp(bs, half) > 0) { ret = 3; goto out; }
+  if (EC_KEY_set_public_key_affine_coordinates(key, bx, by) != 1) { ret = 5; goto out; }
+  if (BN_cmp(br, EC_GROUP_get0_order(grp)) >= 0) { ret = 4; goto out; }
+  {
+    ECDSA_SIG *es = ECDSA_SIG_new();
+    ECDSA_SIG_set0(es, br, bs);
+    br = bs = NULL;
+    const int v = ECDSA_do_verify(digest, (int)digest_len, es, key);
+    ECDSA_SIG_free(es);
+    ret = v == 1 ? 0 : 1;
+  }
+out:
+  BN_free(br);
+  BN_free(bs);
+  BN_free(half);
+  BN_free(bx);
+  BN_free(by);
+  EC_KEY_free(key);
+  return ret;
+}

@@ -61,6 +61,10 @@ void oracle_verify_msgs_batch(const uint8_t *keys /* n*64: qx||qy */, const uint
 int oracle_p256_base_mult(const uint8_t k[32], uint8_t out_x[32], uint8_t out_y[32]);
 
 /* key parsed once (oracle_p256_key_new), verified against many times (cpu_validator.c) */
+/* bccsp Verify for a P-384 key: Go-rule DER (48-byte integers), the P-384 half order, then
+ * Go ecdsa.Verify's rules over OpenSSL's secp384r1 arithmetic; the same status bytes. */
+int oracle_p384_verify_der(const uint8_t qx[48], const uint8_t qy[48], const uint8_t *sig, size_t sig_len,
+                           const uint8_t *digest, size_t digest_len);
 void *oracle_p256_key_new(const uint8_t qx[32], const uint8_t qy[32]);
 void oracle_p256_key_free(void *key);
 int oracle_p256_verify_der_key(void *key, const uint8_t *sig, size_t sig_len, const uint8_t *digest,

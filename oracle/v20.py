@@ -30,7 +30,7 @@ Anything outside that model raises Unsupported (the engine returns an error for 
 """
 import hashlib
 
-from . import sha256, verify_der
+from . import sha256, verify_der, verify_der_p384
 from .protowire import DecodeError, decode
 
 VALID, NIL_ENVELOPE, BAD_PAYLOAD, BAD_COMMON_HEADER, BAD_CREATOR_SIGNATURE = 0, 1, 2, 3, 4
@@ -57,8 +57,8 @@ IMPLICIT_PREFIX = "_implicit_org_"  # core/chaincode/implicitcollection/name.go:
 
 class Ident:
     """An MSP identity as the peer's MSP layer knows it.
-    key: KEY_P256 (verified on the GPU), KEY_P384 (bccsp verifies it: outside the engine ->
-    Unsupported when a verify is needed), KEY_OTHER (RSA...: Verify fails),
+    key: KEY_P256 (verified on the GPU), KEY_P384 (pub = X || Y, 96 bytes: verified like P-256 with
+    the P-384 constants; without pub, outside the engine -> Unsupported when a verify is needed), KEY_OTHER (RSA...: Verify fails),
     KEY_UNDESERIALIZABLE (e.g. Ed25519 under Fabric 2.x: DeserializeIdentity fails, F4).
     hash: the MSP's SignatureHashFamily (identities.go:219-227): SHA2 -> SHA-256, SHA3 -> SHA3-256.
     roles: bit r <=> msp.SatisfiesPrincipal(id, ROLE{mspid, r}) (MEMBER 0, ADMIN 1, CLIENT 2,
@@ -207,8 +207,12 @@ class ChannelModel:
         self.verify_calls += 1
         if ident.key == KEY_OTHER:
             return 5
-        if ident.key != KEY_P256:
-            raise Unsupported("P-384 key")
+        if ident.key == KEY_P384 and (ident.pub is None or len(ident.pub) != 96):
+            raise Unsupported("P-384 key not known")  # (the engine: registered without pubkey_p384)
+        if ident.key not in (KEY_P256, KEY_P384):
+            raise Unsupported("key type %r" % ident.key)
+        if ident.key == KEY_P384 and not self.sha3_verify:
+            raise Unsupported("P-384 identity outside the committer's signatures")  # (the orderer path)
         if ident.hash_family == "SHA3" and not self.sha3_verify:
             raise Unsupported("SHA3 identity outside the committer's signatures")
         if ident.hash_family not in ("SHA2", "SHA3"):
@@ -216,6 +220,8 @@ class ChannelModel:
         if not sig:
             return 6
         digest = hashlib.sha3_256(msg).digest() if ident.hash_family == "SHA3" else sha256(msg)
+        if ident.key == KEY_P384:
+            return verify_der_p384(ident.pub, sig, digest)
         return verify_der(ident.pub[:32], ident.pub[32:], sig, digest)
 
     def channel_policy(self, ref):

@@ -285,8 +285,8 @@ def test_shard_protocol_keylevel_tx_split_seeds(seed, mode):
     net = sbe_cases_network()
     ccs = {ns: dict(policy=p, collections={"pvt1": None}) for ns, p in net.chaincodes.items()}
     b1, kvmeta0 = sbe_cases.make_sbe_block(net, 60, seed, number=2)
-    model = v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=dict(kvmeta0))
-    exp, _ = v20.validate_blocks_outcomes(model, [b1])
+    model = lambda: v20.ChannelModel(net.channel, net.identities(), ccs, kvmeta=dict(kvmeta0))  # noqa: E731
+    exp, _ = v20.validate_blocks_outcomes(model(), [b1])  # (it indexes the block's txids: a fresh model each time)
     eng = _lib.Engine(0)
     try:
         eng.set_parse_mode(mode)
@@ -294,7 +294,7 @@ def test_shard_protocol_keylevel_tx_split_seeds(seed, mode):
         eng.set_block_outcomes(True)
         for shards in range(2, 7):
             got, st, n_final = _shard_protocol_outcomes(eng, [b1], shards, "tx")
-            _expect(model, [b1], got, st, n_final)
+            _expect(model(), [b1], got, st, n_final)
             if exp[0] is not None:
                 assert st == [0], (shards, st)
     finally:
