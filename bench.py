@@ -40,10 +40,11 @@ import torch
 import torch.distributed as dist
 
 METRIC = "ECDSA-P256 verifies/sec + validated tx/sec per block at 1/2/4/8 MI355X"
-# 32x32->64 multiply-add products per verify in the comb: 32 terms (12 signed
-# 22-bit generator windows + 20 signed 13-bit key windows), the first one loaded, so 31 mixed
-# additions x (8 field mults x 64 + 3 squarings x 36 products) + the projective x-check (3 x 64)
-PRODUCTS_POINT = 31 * (8 * 64 + 3 * 36) + 3 * 64
+# 32x32->64 multiply-add products per verify in the comb: 28 terms (12 signed
+# 22-bit generator windows + 16 signed 17-bit key windows; round 5: 20 13-bit windows, 32 terms),
+# the first one loaded, so 27 mixed additions x (8 field mults x 64 + 3 squarings x 36 products)
+# + the projective x-check (3 x 64)
+PRODUCTS_POINT = 27 * (8 * 64 + 3 * 36) + 3 * 64
 # the same for one variable-base verify in k_vb_mul: 8 lanes, each 28 doublings
 # (3 mults + 5 squarings), 7.5 expected mixed additions from the key's table (8 mults + 3
 # squarings) and 3 butterfly additions (12 mults + 4 squarings), + u2 = r * s^-1 (sn_mul, 128)

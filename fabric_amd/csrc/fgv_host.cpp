@@ -299,7 +299,7 @@ int fgv_init(const fgv_config *cfg, fgv_ctx **out) {
   fgv_ctx *c = new (std::nothrow) fgv_ctx();
   if (!c) return FGV_ENOMEM;
   c->device = cfg ? cfg->device : 0;
-  c->key_slots = (cfg && cfg->key_slots) ? cfg->key_slots : 2048;
+  c->key_slots = (cfg && cfg->key_slots) ? cfg->key_slots : 256;  // x 64 MiB (KT_BYTES): 16 GiB of comb tables
   c->key_ids = (cfg && cfg->key_ids) ? cfg->key_ids : (1u << 20);
   if (const char *e = getenv("FGV_PROMOTE_USES")) c->promote_uses = (uint32_t)std::max(1, atoi(e));
   if (const char *e = getenv("FGV_ADHOC_COMB")) c->adhoc_comb_uses = (uint32_t)std::max(1, atoi(e));

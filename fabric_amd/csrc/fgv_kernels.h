@@ -3,19 +3,20 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Key comb (u2 * Q): 20 windows of 13 bits with signed digits in [-4096, 4095] (20 x 13 = 260 bits:
-// the top window, bits 247..259 of a scalar < 2^256, absorbs the final carry); 4096 entries
-// (|d| = 1..4096) per window, 5.2 MB per key, one copy in Montgomery-280 form (k_point28; the exact
+// Key comb (u2 * Q): 16 windows of 17 bits with signed digits in [-65536, 65535] (16 x 17 = 272 bits:
+// the top window, bits 255..271 of a scalar < 2^256, absorbs the final carry); 65536 entries
+// (|d| = 1..65536) per window, 64 MiB per key, one copy in Montgomery-280 form (k_point28; the exact
 // k_point converts an entry with one multiplication), built by k_keytab (KT_CHUNK entries per thread).
-// 13-bit windows: 37 comb terms per verify instead of 43 with 10-bit windows.
-#define WBITS 13
-#define NWIN 20
-#define TAB_K 4096
+// 17-bit windows (round 6): 28 comb terms per verify instead of 32 with 13-bit windows (5.2 MB per
+// key), -12.5 % of k_point28's additions for 12.8x the table (HBM holds 256 hot keys in 16 GiB).
+#define WBITS 17
+#define NWIN 16
+#define TAB_K 65536
 #define KT_CHUNK 32
-#define KT_THREADS_PER_KEY (NWIN * (TAB_K / KT_CHUNK))  // 2,560
-#define KT_BUILD_KEYS 32                                 // keys per k_keytab launch (scratch bound)
-#define KT_ENTRIES (NWIN * TAB_K)           // 81,920 affine points per table
-#define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 5,242,880 bytes per table
+#define KT_THREADS_PER_KEY (NWIN * (TAB_K / KT_CHUNK))  // 32,768
+#define KT_BUILD_KEYS 2                                  // keys per k_keytab launch (scratch bound: 256 MiB)
+#define KT_ENTRIES (NWIN * TAB_K)           // 1,048,576 affine points per table
+#define KT_BYTES ((size_t)KT_ENTRIES * 64)  // 67,108,864 bytes per table
 // Generator comb (u1 * G): 12 windows of 22 bits with signed digits in [-2^21, 2^21 - 1] (12 x 22
 // = 264 bits: the top window, bits 242..263 of a scalar < 2^256, absorbs the final carry);
 // 2^21 entries per window, 1.61 GB, one copy in Montgomery-280 form (the exact k_point converts
@@ -29,12 +30,12 @@
 #define GT_CHUNK 32                            // consecutive entries per k_gtab thread
 #define GT_THREADS_PER_WIN (GT_K / GT_CHUNK)   // 65,536 threads per k_gtab launch (one window)
 #define NTERMS (NGWIN + NWIN)         // comb terms per verify: 12 G + 20 Q
-#define DIG_Q_OFF 48                  // digit array item: G digits int32 x 12 at 0, Q digits int16 x 20 here
+#define DIG_Q_OFF 48                  // digit array item: G digits int32 x 12 at 0, Q digits int32 x 16 here
 #define PREP_B 2                            // items per lane in the batched inversion
 #define POINT_THREADS 256   // 4 waves per workgroup, 2 x n_cu workgroups: 2 waves per SIMD, <= 256 VGPRs
 #define POINT_LANES_MAX 8    // lanes cooperating on one verify in k_point (partial sums + tree)
 #define POINT_EXACT_WGS 64   // k_point's grid behind k_point28 (the hand-overs: exceptional additions only)
-#define DIG_STRIDE 96        // bytes per item of the digit array (G digits, then Q digits at DIG_Q_OFF)
+#define DIG_STRIDE 112       // bytes per item of the digit array (G digits, then Q digits at DIG_Q_OFF)
 #define ST_PENDING 0xFF
 #define ST_VB 0xFE       // k_inv: pending on the variable-base kernels (k_vb_mul / k_vb_fin finish it)
 #define ST_P384 0xFD     // k_der: a P-384 key (KEY_P384_FLAG in its key slot): k_p384_verify finishes it

@@ -101,8 +101,8 @@ FGV_DEV void load_fe(fe &a, const uint32_t *src) {
 }
 
 // ---------------------------------------------------------------- k_keytab
-// T_Q[w][k-1] = k * 2^(13w) * Q, w < NWIN, k = 1..TAB_K.  KT_THREADS_PER_KEY threads per key, thread
-// (w, chunk) builds entries k0..k0+31 of window w: B = 2^(13w) Q by doublings, P = k0 * B by
+// T_Q[w][k-1] = k * 2^(17w) * Q, w < NWIN, k = 1..TAB_K.  KT_THREADS_PER_KEY threads per key, thread
+// (w, chunk) builds entries k0..k0+31 of window w: B = 2^(17w) Q by doublings, P = k0 * B by
 // double-and-add, then P += B, one Montgomery-trick inversion per chunk (complete formulas:
 // pt_add routes P == B to a doubling).  Montgomery-280 form (k_point28; k_point converts an entry
 // when it reads it).  key_ok (nullable): the key's on-curve bit at its slot.
@@ -411,8 +411,8 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint32_t *__rest
   sn_mul(u1, e, w);  // e * s^-1 (plain)
   sn_mul(u2, r, w);  // r * s^-1 (plain)
   // signed recoding, digits in [-2^(W-1), 2^(W-1) - 1]: u1 in base 2^22 (12 int32 digits,
-  // generator comb), u2 in base 2^13 (20 int16 digits); the top window of a scalar < 2^256
-  // (bits 242.. / 247..) is far below half its range, so the final carry never leaves it
+  // generator comb), u2 in base 2^17 (16 int32 digits); the top window of a scalar < 2^256
+  // (bits 242.. / 255..) is far below half its range, so the final carry never leaves it
   int8_t *dp = digits + (size_t)i * DIG_STRIDE;
   {
     constexpr int GMASK = (1 << GWBITS) - 1, GHALF = 1 << (GWBITS - 1);
@@ -431,7 +431,7 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint32_t *__rest
   }
   constexpr int WMASK = (1 << WBITS) - 1, WHALF = 1 << (WBITS - 1);
   int c2 = 0;
-  uint16_t *q = reinterpret_cast<uint16_t *>(dp + DIG_Q_OFF);
+  int32_t *q = reinterpret_cast<int32_t *>(dp + DIG_Q_OFF);
 #pragma unroll
   for (int win = 0; win < NWIN; win++) {
     const int bit = WBITS * win, li = bit >> 5, sh = bit & 31;
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(256) void k_prep(uint32_t n, const uint32_t *__rest
     int a2 = (int)(v2 & WMASK) + c2;
     c2 = a2 >= WHALF;
     a2 -= c2 << WBITS;
-    q[win] = (uint16_t)(int16_t)a2;
+    q[win] = a2;
   }
 }
 
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point(
     for (int t = 0; t < nterms; t++) {
       const int tt = (int)sub + t * (int)L;
       const bool isq = tt >= NGWIN;
-      const int d = isq ? (int)reinterpret_cast<const int16_t *>(dg + DIG_Q_OFF)[tt - NGWIN]
+      const int d = isq ? reinterpret_cast<const int32_t *>(dg + DIG_Q_OFF)[tt - NGWIN]
                         : reinterpret_cast<const int32_t *>(dg)[tt];
       if (d == 0) continue;
       const int k = (d < 0 ? -d : d) - 1;
@@ -686,7 +686,7 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
     auto entry = [&](int t, int &d) -> const uint4 * {
       const int tt = (int)sub + t * (int)L;
       const bool isq = tt >= NGWIN;
-      d = isq ? (int)reinterpret_cast<const int16_t *>(dg + DIG_Q_OFF)[tt - NGWIN] : reinterpret_cast<const int32_t *>(dg)[tt];
+      d = isq ? reinterpret_cast<const int32_t *>(dg + DIG_Q_OFF)[tt - NGWIN] : reinterpret_cast<const int32_t *>(dg)[tt];
       const int k = d == 0 ? 0 : (d < 0 ? -d : d) - 1;
       return reinterpret_cast<const uint4 *>(isq ? qt + (size_t)(tt - NGWIN) * TAB_K + k : gtab28 + (size_t)tt * GT_K + k);
     };

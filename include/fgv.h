@@ -43,8 +43,8 @@ typedef struct fgv_ctx fgv_ctx;
 
 typedef struct fgv_config {
   int device;            /* HIP device ordinal (one process per GPU)                 */
-  uint32_t key_slots;    /* comb-table cache: keys verified by the fixed-base key comb (0 = 2048;
-                            5.2 MB of HBM per slot, 13-bit windows).  A key without a slot is
+  uint32_t key_slots;    /* comb-table cache: keys verified by the fixed-base key comb (0 = 256;
+                            64 MiB of HBM per slot, 17-bit windows).  A key without a slot is
                             verified by the variable-base kernels instead -- same results, ~9x
                             the device work per verify -- so a full cache never fails a batch    */
   uint32_t host_threads; /* host worker threads for parsing / policy fold (0 = min(24,

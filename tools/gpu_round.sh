@@ -140,6 +140,19 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --hip-trace -d $O/at -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie > $O/at.json 2> $O/at.err \
         || { echo apitrace failed; tail -20 $O/at.err; exit 1; }
       echo apitrace ok ;;
+    pcietrace)
+      # the PCIe-inclusive rotation's copies and kernels (tools/copy_trace.py reads the CSVs)
+      timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --memory-copy-trace -d $O/pcie -o run -- python bench.py --steps 12 --warmup 3 --cpu-threads 0 --no-latency > $O/pcie.json 2> $O/pcie.err \
+        || { echo pcietrace failed; tail -20 $O/pcie.err; exit 1; }
+      python3 tools/copy_trace.py $O/pcie > $O/pcie_summary.txt 2>&1; tail -25 $O/pcie_summary.txt ;;
+    pcie*)
+      # pcie<N>: N runs of the default bench's PCIe-inclusive pass (lean: no CPU baseline / latency)
+      n=${step#pcie}; n=${n:-1}
+      for rep in $(seq 1 $n); do
+        timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency > $O/pcie_$rep.json 2> $O/pcie_$rep.err \
+          || { echo pcie failed; tail -20 $O/pcie_$rep.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/pcie_$rep.json')); p=d['pcie_inclusive']; print('pcie $rep', d['ms_per_step'], p['ms_per_step'], p['h2d_GBps'], p['parity_vs_labels'])"
+      done ;;
     lattrace)
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d $O/lat -o run -- python tools/latency_probe.py > $O/lat.out 2> $O/lat.err \
         || { echo lattrace failed; tail -20 $O/lat.err; exit 1; }
