@@ -53,7 +53,8 @@ static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slo
   // the scratch at its full size on first use (335 MB): grown build by build, every larger
   // promotion batch would pay a hipFree -- a device-wide synchronisation -- inside a call
   if (!c->kt_q.ensure((size_t)nk * 64) || !c->kt_slot.ensure((size_t)nk * 4) ||
-      !c->kt_scratch.ensure((size_t)KT_BUILD_KEYS * KT_ENTRIES * sizeof(jpoint_raw)))
+      !c->kt_scratch.ensure((size_t)KT_BUILD_KEYS * KT_ENTRIES * sizeof(jpoint_raw)) ||
+      !c->kt_base.ensure((size_t)KT_BUILD_KEYS * NWIN * sizeof(jpoint_raw)))
     return FGV_ENOMEM;
   HIP_TRY(hipMemcpyAsync(c->kt_q.p, h_qxy, (size_t)nk * 64, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(c->kt_slot.p, h_slots, (size_t)nk * 4, hipMemcpyHostToDevice, st));
@@ -61,8 +62,11 @@ static int build_tables(fgv_ctx *c, const uint32_t *h_qxy, const uint32_t *h_slo
   for (uint32_t k = 0; k < nk; k += per) {
     const uint32_t m = nk - k < per ? nk - k : per;
     const uint32_t threads = m * KT_THREADS_PER_KEY;
+    hipLaunchKernelGGL(k_keybase, dim3((m * NWIN + 63) / 64), dim3(64), 0, st, c->kt_q.as<uint32_t>() + 16 * k, m,
+                       c->kt_base.as<jpoint_raw>());
     hipLaunchKernelGGL(k_keytab, dim3((threads + 63) / 64), dim3(64), 0, st, c->kt_q.as<uint32_t>() + 16 * k,
-                       c->kt_slot.as<uint32_t>() + k, tables, tables28, c->kt_scratch.as<jpoint_raw>(), ok, m);
+                       c->kt_slot.as<uint32_t>() + k, tables, tables28, c->kt_scratch.as<jpoint_raw>(), ok, m,
+                       c->kt_base.as<const jpoint_raw>());
     HIP_TRY(hipGetLastError());
   }
   if (timed) HIP_TRY(hipEventRecord(c->ev[7], st));
@@ -262,12 +266,12 @@ static int promote_consume(fgv_ctx *c, uint32_t items, hipStream_t st) {
     if (hipEventQuery(c->kt_ev) != hipSuccess) return FGV_OK;
     c->kt_busy = false;
   }
-  // at most promote_per_call builds per call (~80 us of the whole chip each), and about one per
-  // 3,000 verify slots of this call, so a burst of keys reaching the threshold together spreads
-  // over calls, and a small call (one block) is not swamped by builds running beside it
-  // (FGV_PROMOTE_PER_CALL set: exactly that many, whatever the call's size)
+  // at most promote_per_call builds per call, and about one per 24,000 verify slots of this call (a
+  // 17-bit comb is 64 MiB: ~8x a 13-bit one's build, round 6), so a burst of keys reaching the
+  // threshold together spreads over calls, and a small call (one block) is not swamped by builds
+  // running beside it (FGV_PROMOTE_PER_CALL set: exactly that many, whatever the call's size)
   const size_t per = c->promote_fixed ? c->promote_per_call
-                                      : std::max<size_t>(1, std::min<size_t>(c->promote_per_call, items / 3000));
+                                      : std::max<size_t>(1, std::min<size_t>(c->promote_per_call, items / 24000));
   const size_t take = std::min<size_t>(c->promo_backlog.size(), per);
   std::vector<uint32_t> ids(c->promo_backlog.begin(), c->promo_backlog.begin() + take);
   c->promo_backlog.erase(c->promo_backlog.begin(), c->promo_backlog.begin() + take);
@@ -451,7 +455,7 @@ void fgv_destroy(fgv_ctx *c) {
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   for (hipStream_t x : {c->stream2, c->stream3, c->streamF, c->streamV, c->streamK})  // (a front half enqueued ahead)
     if (x) hipStreamSynchronize(x);
-  DevBuf *d[] = {&c->p384_items, &c->stage[0], &c->stage[1], &c->stage[2], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
+  DevBuf *d[] = {&c->p384_items, &c->kt_base, &c->stage[0], &c->stage[1], &c->stage[2], &c->bd_env, &c->bd_bases, &c->bd_tx, &c->bd_ident, &c->bd_jobs,
                  &c->bd_misc, &c->g_ok, &c->key_ok, &c->gtab28, &c->ktab28, &c->redo, &c->kt_q, &c->kt_slot, &c->kt_scratch,
                  &c->kmap, &c->vbt, &c->vbuse, &c->vbpromo, &c->vblist, &c->vbhand, &c->vbacc, &c->kt_id,
                  &c->status, &c->slot, &c->r, &c->s, &c->dig, &c->d1, &c->wv, &c->wscr, &c->msg,

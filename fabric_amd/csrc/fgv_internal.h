@@ -104,6 +104,7 @@ struct fgv_p384_state;  // p384.hip: the context's P-384 keys and comb tables
 struct fgv_ctx {
   fgv_mvcc_state *mv = nullptr;
   fgv_p384_state *p384 = nullptr;
+  DevBuf kt_base;     // k_keybase: the window bases of the keys of one k_keytab launch
   DevBuf p384_items;  // fgv_p384_verify_msgs: item columns + signature bytes
   int device = 0;
   hipStream_t stream = nullptr;
@@ -145,7 +146,8 @@ struct fgv_ctx {
   bool vb_pending = false;        // k_vb_mul enqueued: launch_prep_point adds k_vb_fin
   bool vb_copied = false;         // a promotion-queue copy was enqueued (vb_ev[2])
   bool vb_launched = false;       // the last verify stages ran the variable-base kernels
-  uint32_t promote_uses = 64;     // variable-base verifies of one key before its comb is built
+  uint32_t promote_uses = 256;    // variable-base verifies of one key before its comb is built (a 64 MiB
+                                  // 17-bit comb repays its build over ~30k verifies: round 6, 64 -> 256)
   uint32_t adhoc_comb_uses = 32;  // uses of an ad-hoc key in one call for a comb
   // FGV_PROMOTE_AT = 1 / 2 / 3 (test knob, tests/test_gpu_concurrency.py): promotions build their
   // tables on the main stream and enqueue k_kmap_set after k_inv / before k_point28 / before

@@ -52,8 +52,9 @@ struct jpoint_raw {  // key-table build scratch: Jacobian point + prefix product
   uint32_t pref[8];
 };
 
+__global__ void k_keybase(const uint32_t *qxy, uint32_t nkeys, jpoint_raw *bases);
 __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw *tables, apoint_raw *tables28,
-                         jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys);
+                         jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys, const jpoint_raw *bases);
 // Key tiers.  Every key has an id; kmap[id] is its comb slot (the 5.2 MB table
 // above) or KEY_NONE: the variable-base kernels verify it from a 15 KB per-key table
 // (vbt[id][s][d-1] = d * 2^(32 s) Q, s < 8, d = 1..15, affine Montgomery-256).  k_keyprep checks

@@ -107,12 +107,39 @@ FGV_DEV void load_fe(fe &a, const uint32_t *src) {
 // pt_add routes P == B to a doubling).  Montgomery-280 form (k_point28; k_point converts an entry
 // when it reads it).  key_ok (nullable): the key's on-curve bit at its slot.
 // qxy: [nkeys][16] plain little-endian limbs (x then y); scratch: [nkeys][KT_ENTRIES] jpoint_raw.
+// k_keybase: the window bases B_w = 2^(17w) Q of each key (one thread per (key, w): 17 w doublings),
+// so that k_keytab's 32,768 threads per key start from their base instead of each redoing up to
+// 255 doublings (half of a 17-bit table's build).  Off-curve keys: nothing (k_keytab skips them).
+__global__ __launch_bounds__(64) void k_keybase(const uint32_t *__restrict__ qxy, uint32_t nkeys,
+                                                jpoint_raw *__restrict__ bases) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t kid = t / NWIN, w = t % NWIN;
+  if (kid >= nkeys) return;
+  fe x, y, xm, ym;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    x.v[i] = qxy[kid * 16 + i];
+    y.v[i] = qxy[kid * 16 + 8 + i];
+  }
+  if (!on_curve(x, y, xm, ym)) return;
+  jpoint b;
+  b.x = xm;
+  b.y = ym;
+  fe_set_one(b.z);
+  for (uint32_t i = 0; i < WBITS * w; i++) pt_dbl(b, b);
+  jpoint_raw &o = bases[(size_t)kid * NWIN + w];
+  store_fe(o.x, b.x);
+  store_fe(o.y, b.y);
+  store_fe(o.z, b.z);
+}
+
 __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
                                                const uint32_t *__restrict__ slots,
                                                apoint_raw *__restrict__ tables,
                                                apoint_raw *__restrict__ tables28,
                                                jpoint_raw *__restrict__ scratch,
-                                               uint8_t *__restrict__ key_ok, uint32_t nkeys) {
+                                               uint8_t *__restrict__ key_ok, uint32_t nkeys,
+                                               const jpoint_raw *__restrict__ bases) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t kid = t / KT_THREADS_PER_KEY, r = t % KT_THREADS_PER_KEY;
   if (kid >= nkeys) return;
@@ -130,10 +157,17 @@ __global__ __launch_bounds__(64) void k_keytab(const uint32_t *__restrict__ qxy,
   if (r == 0 && key_ok) key_ok[slot] = ok ? 1 : 0;
   if (!ok) return;
   jpoint b;
-  b.x = xm;
-  b.y = ym;
-  fe_set_one(b.z);
-  for (uint32_t i = 0; i < WBITS * w; i++) pt_dbl(b, b);
+  if (bases) {  // (k_keybase)
+    const jpoint_raw &o = bases[(size_t)kid * NWIN + w];
+    load_fe(b.x, o.x);
+    load_fe(b.y, o.y);
+    load_fe(b.z, o.z);
+  } else {
+    b.x = xm;
+    b.y = ym;
+    fe_set_one(b.z);
+    for (uint32_t i = 0; i < WBITS * w; i++) pt_dbl(b, b);
+  }
   jpoint pk = b;
   for (int bit = 30 - __builtin_clz(k0 | 1u); bit >= 0; bit--) {
     jpoint t2 = pk;

@@ -1,6 +1,9 @@
 """PCIe-inclusive rotation from a rocprofv3 --memory-copy-trace --kernel-trace run of bench.py
-(profiling aid): the batch-sized host-to-device copies in time order -- duration,
-GB/s, the idle link between consecutive copies -- and what the GPU ran during each idle gap.
+(profiling aid).  The trace holds no byte counts, so batch copies are the
+host-to-device copies longer than 300 us; bench.py's raw-rate probe (5+1 torch copies, stream 0)
+separates the untimed parity pass from the timed pass.  Printed: each timed batch copy (start, end,
+idle link before it), the per-step completion times (k_fin_dups ends) and the largest idle gaps with
+the kernels that started inside them.
 
 usage: python tools/copy_trace.py <rocprofv3 output dir>
 """
@@ -17,38 +20,31 @@ if not mc:
     sys.exit("no memory_copy_trace.csv under %s" % d)
 rows = list(csv.DictReader(open(mc[0])))
 kern = list(csv.DictReader(open(kt[0]))) if kt else []
-kern.sort(key=lambda r: int(r["Start_Timestamp"]))
-
-
-def size(r):
-    for k in ("Bytes", "Size", "Copy_Bytes"):
-        if k in r and r[k]:
-            return int(r[k])
-    return 0
-
-
-h2d = [r for r in rows if "HOST_TO_DEVICE" in (r.get("Direction", "") + r.get("Kind", "") + r.get("Operation", "")).upper()]
-big = [r for r in h2d if size(r) >= 16 << 20]
-big.sort(key=lambda r: int(r["Start_Timestamp"]))
-print("columns:", list(rows[0].keys()) if rows else None)
-print("H2D copies: %d, batch-sized (>= 16 MiB): %d" % (len(h2d), len(big)))
-gaps, durs, rates = [], [], []
-prev = None
-for r in big:
-    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+T = lambda r, k: int(r[k])  # noqa: E731
+t0 = min(T(r, "Start_Timestamp") for r in rows)
+big = [r for r in rows if T(r, "End_Timestamp") - T(r, "Start_Timestamp") > 300_000]
+probe = [r for r in big if r["Stream_Id"] == "0"]
+cut = max(T(r, "End_Timestamp") for r in probe) if probe else t0
+timed = sorted((r for r in big if r["Stream_Id"] != "0" and T(r, "Start_Timestamp") >= cut),
+               key=lambda r: T(r, "Start_Timestamp"))
+print("batch copies in the timed pass: %d" % len(timed))
+prev, gaps, durs = None, [], []
+for r in timed:
+    s, e = T(r, "Start_Timestamp"), T(r, "End_Timestamp")
+    g = (s - prev) / 1e3 if prev is not None else 0.0
     durs.append((e - s) / 1e3)
-    rates.append(size(r) / max(e - s, 1))  # bytes/ns = GB/s
     if prev is not None:
-        gaps.append(((s - prev) / 1e3, prev, s))
+        gaps.append((g, prev, s))
+    print("copy %9.3f - %9.3f ms  idle before %7.1f us" % ((s - t0) / 1e6, (e - t0) / 1e6, g))
     prev = e
+fd = sorted(T(k, "End_Timestamp") for k in kern if k["Kernel_Name"].startswith("k_fin_dups") and T(k, "End_Timestamp") > cut)
+if len(fd) > 1:
+    steps = [(b - a) / 1e3 for a, b in zip(fd, fd[1:])]
+    print("steps (k_fin_dups to k_fin_dups) us: med %.1f min %.1f max %.1f, n=%d" % (S.median(steps), min(steps), max(steps), len(steps)))
+    print("  per step:", " ".join("%.0f" % x for x in steps))
 if durs:
-    print("copy duration us: med %.1f min %.1f max %.1f; GB/s med %.1f" % (S.median(durs), min(durs), max(durs), S.median(rates)))
-if gaps:
-    g = [x[0] for x in gaps]
-    print("idle link between batch copies us: med %.1f p90 %.1f max %.1f (n=%d)" % (S.median(g), sorted(g)[len(g) * 9 // 10], max(g), len(g)))
-    span = (int(big[-1]["End_Timestamp"]) - int(big[0]["Start_Timestamp"])) / 1e3
-    print("link busy over the pass: %.1f %% of %.1f us" % (100 * sum(durs[1:]) / span if span else 0, span))
-    print("--- the largest gaps: kernels that started inside them")
-    for gap, a, b in sorted(gaps, reverse=True)[:5]:
-        ks = [x["Kernel_Name"].split("(")[0] for x in kern if a <= int(x["Start_Timestamp"]) < b]
-        print("%8.1f us: %s" % (gap, ", ".join(ks[:12])))
+    print("batch copy us: med %.1f; idle link med %.1f max %.1f" % (S.median(durs), S.median(g for g, _, _ in gaps) if gaps else 0,
+                                                                 max((g for g, _, _ in gaps), default=0)))
+for g, a, b in sorted(gaps, reverse=True)[:4]:
+    ks = [x["Kernel_Name"].split("(")[0] for x in kern if a <= T(x, "Start_Timestamp") < b]
+    print("idle %8.1f us at %.3f ms: %s" % (g, (a - t0) / 1e6, ", ".join(ks[:10])))

@@ -142,7 +142,7 @@ for step in "$@"; do
       echo apitrace ok ;;
     pcietrace)
       # the PCIe-inclusive rotation's copies and kernels (tools/copy_trace.py reads the CSVs)
-      timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --memory-copy-trace -d $O/pcie -o run -- python bench.py --steps 12 --warmup 3 --cpu-threads 0 --no-latency > $O/pcie.json 2> $O/pcie.err \
+      timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --memory-copy-trace -d $O/pcie -o run -- python bench.py --steps ${PCIE_STEPS:-20} --warmup 3 --cpu-threads 0 --no-latency > $O/pcie.json 2> $O/pcie.err \
         || { echo pcietrace failed; tail -20 $O/pcie.err; exit 1; }
       python3 tools/copy_trace.py $O/pcie > $O/pcie_summary.txt 2>&1; tail -25 $O/pcie_summary.txt ;;
     pcie*)
