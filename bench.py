@@ -27,6 +27,7 @@ pipeline: the end-to-end commit path on the same C2-shaped blocks (committer -> 
   batch is distinct and generated up front).
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -40,6 +41,7 @@ import torch
 import torch.distributed as dist
 
 METRIC = "ECDSA-P256 verifies/sec + validated tx/sec per block at 1/2/4/8 MI355X"
+STEPLOG = os.environ.get("BENCH_STEPLOG") == "1"  # per-step host timings of the timed loops (stderr)
 # 32x32->64 multiply-add products per verify in the comb: 28 terms (12 signed
 # 22-bit generator windows + 16 signed 17-bit key windows; round 5: 20 13-bit windows, 32 terms),
 # the first one loaded, so 27 mixed additions x (8 field mults x 64 + 3 squarings x 36 products)
@@ -475,16 +477,23 @@ def run_block(args, world, rank, local, dev_fn):
             for d in range(args.integ_depth + 1):
                 if s + d not in integ_fut:
                     integ_fut[s + d] = integ_ex.submit(verify_mine, (k + d) % NB)
+        t_a = time.perf_counter() if STEPLOG else 0.0
         bs.validate()
         if world > 1:
             shard.allgather_device(send, recv, eng=eng)
+        t_b = time.perf_counter() if STEPLOG else 0.0
         f = bs.finalize()
+        t_c = time.perf_counter() if STEPLOG else 0.0
         if args.presplit_early and world == 1 and not args.no_presplit:
             # a peer walks a batch's framing once its blocks are delivered (fgv_presplit keeps the
             # two latest requests): batches k+2 and k+3 after call k, so the call before each
             # batch finds its walk done at its top and queues the batch's parse there (front_early)
             eng.presplit(bs.after_next)
             eng.presplit(bs.after_next2)
+        if STEPLOG:
+            ht = eng.host_timing()
+            steplog.append(dict(validate=(t_b - t_a) * 1e3, finalize=(t_c - t_b) * 1e3,
+                                presplit=(time.perf_counter() - t_c) * 1e3, **{"lib_" + k: v for k, v in ht.items()}))
         if s is not None:
             integ_fut.pop(s).result()
         return f
@@ -498,19 +507,38 @@ def run_block(args, world, rank, local, dev_fn):
                 + ", ".join(f"tx {int(i)} (block {int(i) // T}) got {int(flags[i])} want {int(exp[i])}" for i in bad[:8]))
         return int(len(bad))
 
+    steplog = []  # (BENCH_STEPLOG) per-step host phases
+
     def timed(steps_list, K, per_step=None, step_fn=None, start=0):
         # start: the rotation index the previous call announced as its next batch (its front
         # half and pre-split are already queued), so timed call 0 continues the pipeline
         fn = step_fn or step
         if world > 1:
             dist.barrier()
+        # the interpreter's cyclic GC stays out of the timed loop (a generation-2 pass over the
+        # bench's millions of label / block objects took ~6 ms inside one step of the PCIe pass)
+        gc.collect()
+        gc.disable()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        marks = []
         for s in range(start, start + K):
             fn(steps_list[s % NB], s % NB)
             if per_step is not None:
                 per_step()
+            if STEPLOG:
+                marks.append(time.perf_counter())
         torch.cuda.synchronize()
+        gc.enable()
+        if STEPLOG and marks:  # (diagnostic: host-side per-step durations, BENCH_STEPLOG=1)
+            d = [(b - a) * 1e3 for a, b in zip([t0] + marks[:-1], marks)]
+            log("[bench] steps ms: " + " ".join("%.3f" % x for x in d))
+            if len(steplog) >= K:
+                j = max(range(K), key=lambda q: d[q])
+                med = sorted(range(K), key=lambda q: d[q])[K // 2]
+                log("[bench] slowest step %d: %s" % (j, {k: round(v, 3) for k, v in steplog[-K + j].items()}))
+                log("[bench] median step %d: %s" % (med, {k: round(v, 3) for k, v in steplog[-K + med].items()}))
+            steplog.clear()
         if world > 1:
             dist.barrier()
         return time.perf_counter() - t0
@@ -584,13 +612,26 @@ def run_block(args, world, rank, local, dev_fn):
         # batch k stages batch k+2 (fgv_prefetch) besides its pipelined NEXT batch k+1: the copy
         # stream always holds the next copy, so the link runs back to back
         def pin_step(bs, k):
+            t_p = time.perf_counter() if STEPLOG else 0.0
             eng.prefetch(pin_batches[(k + 2) % NB])
-            return step(bs, k)
+            f = step(bs, k)
+            if STEPLOG and steplog:
+                steplog[-1]["prefetch"] = (time.perf_counter() - t_p) * 1e3 - sum(
+                    steplog[-1][q] for q in ("validate", "finalize", "presplit"))
+            return f
 
         pm = 0
-        for k in range(NB):  # parity of every batch (untimed), leaving batches 0 and 1 staged
+        for k in range(NB):  # parity of every batch (untimed)
             pm += parity(k, pin_step(psteps[k], k).copy())
-        # raw H2D rate of one batch from pinned memory (the PCIe link's share of the step)
+        # warmup as the HBM pass has (untimed), continuing the rotation: the timed loop starts at
+        # the batch the last call announced
+        for s in range(NB, NB + args.warmup):
+            pin_step(psteps[s % NB], s % NB)
+        Kp = max(K, 2 * NB)
+        pel = timed(psteps, Kp, step_fn=pin_step, start=(NB + args.warmup) % NB)
+        # raw H2D rate of one batch from pinned memory (the PCIe link's share of the step), after
+        # the timed pass (torch's copies beside the engine's staged ones would skew neither)
+        torch.cuda.synchronize()  # (device-wide: the engine's queued next-batch work too)
         hb = torch.from_numpy(pins[0].a)
         dbuf = torch.empty(hb.numel(), dtype=torch.uint8, device=dev)
         dbuf.copy_(hb, non_blocking=True)
@@ -601,8 +642,6 @@ def run_block(args, world, rank, local, dev_fn):
         torch.cuda.synchronize()
         h2d = hb.numel() * 5 / (time.perf_counter() - t) / 1e9
         del dbuf
-        Kp = max(K, 2 * NB)
-        pel = timed(psteps, Kp, step_fn=pin_step)
         if world > 1:
             t2 = torch.tensor([pel, float(pm)], dtype=torch.float64, device=dev)
             dist.all_reduce(t2, op=dist.ReduceOp.MAX)

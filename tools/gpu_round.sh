@@ -145,6 +145,20 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --memory-copy-trace -d $O/pcie -o run -- python bench.py --steps ${PCIE_STEPS:-20} --warmup 3 --cpu-threads 0 --no-latency > $O/pcie.json 2> $O/pcie.err \
         || { echo pcietrace failed; tail -20 $O/pcie.err; exit 1; }
       python3 tools/copy_trace.py $O/pcie > $O/pcie_summary.txt 2>&1; tail -25 $O/pcie_summary.txt ;;
+    pcietrace2)
+      # copies only (no kernel trace): the unprofiled kernels' timing, the copies' timeline
+      BENCH_STEPLOG=1 timeout -k 10 300 rocprofv3 --output-format csv --memory-copy-trace -d $O/pcie2 -o run -- python bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency > $O/pcie2.json 2> $O/pcie2.err \
+        || { echo pcietrace2 failed; tail -20 $O/pcie2.err; exit 1; }
+      grep "steps ms\|slowest" $O/pcie2.err | tail -2
+      python3 tools/copy_trace.py $O/pcie2 > $O/pcie2_summary.txt 2>&1; tail -28 $O/pcie2_summary.txt ;;
+    pciesteps)
+      # unprofiled PCIe passes at 12 / 20 / 40 timed steps with per-step host timings (BENCH_STEPLOG)
+      for k in 12 20 40; do
+        BENCH_STEPLOG=1 timeout -k 10 300 python -u bench.py --steps $k --warmup 3 --cpu-threads 0 --no-latency > $O/pcies_$k.json 2> $O/pcies_$k.err \
+          || { echo pciesteps failed; tail -20 $O/pcies_$k.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/pcies_$k.json')); p=d['pcie_inclusive']; print('pcie steps $k', d['ms_per_step'], p['ms_per_step'])"
+        grep "steps ms\|slowest\|median step" $O/pcies_$k.err | tail -3
+      done ;;
     pcie*)
       # pcie<N>: N runs of the default bench's PCIe-inclusive pass (lean: no CPU baseline / latency)
       n=${step#pcie}; n=${n:-1}
