@@ -10,7 +10,7 @@ CSRC := fabric_amd/csrc
 OBJDIR := build
 KOBJS := $(OBJDIR)/sha256.o $(OBJDIR)/p256_kernels.o $(OBJDIR)/der_kernel.o $(OBJDIR)/fgv_host.o $(OBJDIR)/fgv_block.o $(OBJDIR)/mvcc.o $(OBJDIR)/fgv_mvcc.o \
 	$(OBJDIR)/finalize.o $(OBJDIR)/fgv_integrity.o $(OBJDIR)/blockdev.o $(OBJDIR)/blockdev_lds.o $(OBJDIR)/blockdev_sha.o $(OBJDIR)/blockdev_fold.o $(OBJDIR)/fgv_commit.o $(OBJDIR)/fgv_channel.o \
-	$(OBJDIR)/fgv_group.o $(OBJDIR)/fgv_msp.o $(OBJDIR)/fgv_x509.o $(OBJDIR)/p384.o
+	$(OBJDIR)/fgv_group.o $(OBJDIR)/fgv_msp.o $(OBJDIR)/fgv_x509.o $(OBJDIR)/p384.o $(OBJDIR)/mvcc_ub.o
 
 all: fabric_amd/libfgv.so oracle/liboracle.so fabric_amd/synth/libfgv_synth.so tests/gpu_helpers/libhexcheck.so
 

@@ -1013,6 +1013,8 @@ def run_pipeline(args, world, rank, local, dev):
     txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes, hot_clients=True)
     eng.statedb_init(4 * args.state_keys, 256 << 20)
     eng.statedb_load("mycc", keys, kb, kt)
+    dev_ub = not args.pipeline_host_hash
+    eng.mvcc_set_update_bytes(dev_ub)
     allb = [bl for bl in batches] + [[b] for b in lat_blocks]
     sizes = [(len(b) + 64 + 255) // 256 * 256 for bl in allb for b in bl]
     arena = torch.zeros(sum(sizes), dtype=torch.uint8, device=dev)
@@ -1038,9 +1040,9 @@ def run_pipeline(args, world, rank, local, dev):
               for k in range(NBT)]
     msteps = [_lib.MvccChainStep(eng, batches[k], nums[k], [np.zeros(T, np.uint8)] * B, commit=True, d_blocks=dptrs[k],
                                  next_blocks=batches[k + 1] if k + 1 < NBT else None) for k in range(NBT)]
-    hsteps = [_lib.CommitHashes(batches[k], nums[k]) for k in range(NBT)]
+    hsteps = [_lib.CommitHashesDev(eng, batches[k], nums[k]) for k in range(NBT)]
     hash_ex = ThreadPoolExecutor(max_workers=1)
-    state = dict(prev=b"", fut=None, mism=0, stage=np.zeros(3))
+    state = dict(prev=b"", fut=None, mism=0, stage=np.zeros(3), futs={}, prevs={})
 
     def step(k, check):
         t = time.perf_counter()
@@ -1049,12 +1051,14 @@ def run_pipeline(args, world, rank, local, dev):
         msteps[k].set_flags([cf[b * T:(b + 1) * T] for b in range(B)])
         fl, rc, done = msteps[k].run()
         _lib._check(rc)
+        ticket = eng.mvcc_last_ticket() if dev_ub else 0
         t2 = time.perf_counter()
         if state["fut"] is not None:
             state["prev"] = state["fut"].result()[-1]
         t3 = time.perf_counter()
         flc = [f.copy() for f in fl]
-        state["fut"] = hash_ex.submit(hsteps[k].run, flc, state["prev"])
+        state["fut"] = hash_ex.submit(hsteps[k].run, flc, state["prev"], ticket)
+        state["futs"][k], state["prevs"][k] = state["fut"], state["prev"]
         state["stage"] += (t1 - t, t2 - t1, t3 - t2)
         if check:
             for b in range(B):
@@ -1073,18 +1077,22 @@ def run_pipeline(args, world, rank, local, dev):
     for k in range(W, W + K):  # parity of the timed batches after the clock: the final flags
         for b in range(B):     # (committer code, else MVCC code) of every block
             state["mism"] += int((msteps[k].flags[b] != fexp[k][b]).sum())
+        # and the commit hashes against the host decode of the same blocks (fgv_commit_hashes)
+        hh = _lib.commit_hashes(batches[k], fexp[k], nums[k], state["prevs"][k])
+        state["mism"] += int(hh != state["futs"][k].result())
     stage = state["stage"] / K * 1e3
     # per-block latency: one block through all three stages, one call each (block in hand ->
     # final flags and commit hash), the state continuing from the timed batches
     lats = []
     prev = state["prev"]
+    lat_h = [_lib.CommitHashesDev(eng, [b], [first + NBT * B + i], threads=1) for i, b in enumerate(lat_blocks)]
     for i, b in enumerate(lat_blocks):
         num = first + NBT * B + i
         torch.cuda.synchronize()
         t = time.perf_counter()
         cf = eng.validate_blocks([b], d_blocks=[dptrs[NBT + i][0]])[0]
         mf = eng.mvcc_validate(b, num, cf, commit=True, d_block=dptrs[NBT + i][0])
-        prev = _lib.commit_hash(b, mf, num, prev)
+        prev = lat_h[i].run([mf], prev, eng.mvcc_last_ticket() if dev_ub else 0)[0]
         lats.append((time.perf_counter() - t) * 1e3)
         state["mism"] += int((cf != lat_c[i]).sum()) + int((mf != lat_f[i]).sum())
     hash_ex.shutdown()
@@ -1103,7 +1111,8 @@ def run_pipeline(args, world, rank, local, dev):
                 config=dict(workload=f"commit pipeline: {B} x {T}-tx C2 blocks per step (OutOf(2,[Org1..3.member]), "
                                      f"C2 faults) -> MVCC of the same blocks against a {args.state_keys}-key state DB "
                                      f"(4R/4W x 200B read-modify-write, 1% stale, 5% conflicts, 2% reads of "
-                                     f"committer-invalid writes) with commit -> chained commit hashes",
+                                     f"committer-invalid writes) with commit -> chained commit hashes "
+                                     f"({'host-built' if args.pipeline_host_hash else 'device-built'} update batches)",
                             blocks_per_step=B, tx_per_block=T, global_batch=world * B * T,
                             parallelism=f"replicas{world} (one channel per GPU)"),
                 parity_vs_labels=ok,
@@ -1126,6 +1135,9 @@ def main():
     ap.add_argument("--workload", default="block", choices=["block", "c5", "sig", "mvcc", "pipeline"])
     ap.add_argument("--pipeline-latency-blocks", type=int, default=12,
                     help="pipeline: blocks taken one call per stage after the timed batches (latency)")
+    ap.add_argument("--pipeline-host-hash", action="store_true",
+                    help="pipeline: build the update batches on the host from the blocks (round 5) instead of "
+                         "on the device (fgv_mvcc_set_update_bytes)")
     ap.add_argument("--c5-blocks-per-gpu", type=int, default=8)
     ap.add_argument("--c5-tx-per-block", type=int, default=20000)
     ap.add_argument("--tx-per-mvcc-block", type=int, default=10000)

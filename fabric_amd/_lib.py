@@ -36,6 +36,8 @@ EXPORTED = [
     "fgv_group_set_block_outcomes", "fgv_group_last_block_status", "fgv_group_set_collective",
     "fgv_msp_resolve", "fgv_msp_resolve_blocks", "fgv_set_auto_resolve", "fgv_msp_identity",
     "fgv_kvmeta_set", "fgv_kvmeta_count", "fgv_kvmeta_get", "fgv_msp_identity_ous", "fgv_group_p256_verify_msgs",
+    "fgv_mvcc_set_update_bytes", "fgv_mvcc_last_ticket", "fgv_mvcc_update_bytes_acquire",
+    "fgv_mvcc_update_bytes_release", "fgv_commit_hashes_ub",
 ]
 # fgv_msp_resolve status (include/fgv.h)
 RESOLVE_KNOWN, RESOLVE_OK, RESOLVE_FAILED, RESOLVE_UNSUPPORTED, RESOLVE_REPEAT = range(5)
@@ -190,6 +192,11 @@ def load():
         L.fgv_sha256_host.argtypes = [vp, sz, vp]
         L.fgv_commit_hash.argtypes = [vp, sz, vp, sz, ctypes.c_uint64, vp, sz, vp]
         L.fgv_commit_hashes.argtypes = [sz, vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint]
+        L.fgv_commit_hashes_ub.argtypes = [sz, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint]
+        L.fgv_mvcc_set_update_bytes.argtypes = [vp, ctypes.c_int]
+        L.fgv_mvcc_last_ticket.argtypes = [vp, vp]
+        L.fgv_mvcc_update_bytes_acquire.argtypes = [vp, ctypes.c_uint64, sz, vp, vp]
+        L.fgv_mvcc_update_bytes_release.argtypes = [vp, ctypes.c_uint64]
         L.fgv_host_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
         L.fgv_host_free.argtypes = [vp, vp]
         L.fgv_dev_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
@@ -947,6 +954,27 @@ class Engine:
                                                         len(next_block)))
         return f
 
+    def mvcc_set_update_bytes(self, on=True):
+        """fgv_mvcc_set_update_bytes: committing MVCC calls also build each block's update-batch
+        bytes on the device (mvcc_ub.hip); fetch them with mvcc_update_bytes / commit_hashes_dev."""
+        _check(self._L.fgv_mvcc_set_update_bytes(self._h, 1 if on else 0))
+
+    def mvcc_last_ticket(self):
+        t = ctypes.c_uint64(0)
+        _check(self._L.fgv_mvcc_last_ticket(self._h, ctypes.byref(t)))
+        return t.value
+
+    def mvcc_update_bytes(self, ticket, n):
+        """copies of the device-built update-batch bytes of the call `ticket` (None where a block's
+        were not produced on the device)"""
+        ptrs = (ctypes.c_void_p * max(n, 1))()
+        lens = (ctypes.c_size_t * max(n, 1))()
+        _check(self._L.fgv_mvcc_update_bytes_acquire(self._h, ticket, n, ptrs, lens))
+        try:
+            return [ctypes.string_at(ptrs[b], lens[b]) if ptrs[b] else None for b in range(n)]
+        finally:
+            self._L.fgv_mvcc_update_bytes_release(self._h, ticket)
+
     def mvcc_validate_blocks(self, blocks, block_nums, flags, commit=True, d_blocks=None, next_blocks=None):
         """fgv_mvcc_validate_blocks: consecutive blocks validated (and committed) in order as one
         device chain.  flags: one committer TxValidationFlags array per block.  next_blocks: the
@@ -1054,6 +1082,53 @@ class CommitHashes:
         _check(self._L.fgv_commit_hashes(self.n, self._bp, self._ln, fp, nt, self._nums, pv, len(prev), self.out,
                                          self._threads))
         return [self.out.raw[32 * b:32 * b + 32] for b in range(self.n)]
+
+
+class CommitHashesDev(CommitHashes):
+    """fgv_commit_hashes_ub with the device-built update-batch bytes of an MVCC call (its ticket):
+    acquire -> hash -> release; a block without device bytes is decoded on the host."""
+
+    def __init__(self, eng, blocks, block_nums, threads=0):
+        super().__init__(blocks, block_nums, threads)
+        self._eng = eng
+        self._ub = (ctypes.c_void_p * max(self.n, 1))()
+        self._ubl = (ctypes.c_size_t * max(self.n, 1))()
+
+    def run(self, flags, prev=b"", ticket=0):
+        fl = [np.ascontiguousarray(f, dtype=np.uint8) for f in flags]
+        fp = (ctypes.c_void_p * max(self.n, 1))(*[f.ctypes.data for f in fl])
+        nt = (ctypes.c_size_t * max(self.n, 1))(*[len(f) for f in fl])
+        pv = ctypes.create_string_buffer(prev, len(prev)) if prev else None
+        h = self._eng._h
+        got = ticket and self._L.fgv_mvcc_update_bytes_acquire(h, ticket, self.n, self._ub, self._ubl) == 0
+        try:
+            _check(self._L.fgv_commit_hashes_ub(self.n, self._ub if got else None, self._ubl if got else None,
+                                                self._bp, self._ln, fp, nt, self._nums, pv, len(prev), self.out,
+                                                self._threads))
+        finally:
+            if got:
+                self._L.fgv_mvcc_update_bytes_release(h, ticket)
+        return [self.out.raw[32 * b:32 * b + 32] for b in range(self.n)]
+
+
+def commit_hashes_ub(ub, blocks, flags, block_nums, prev: bytes = b"", threads=0):
+    """fgv_commit_hashes_ub with the update-batch bytes given per block (None: decode the block)"""
+    L = load()
+    n = len(flags)
+    ubb = [None if u is None else np.frombuffer(u, dtype=np.uint8) if len(u) else np.zeros(1, np.uint8) for u in ub]
+    up = (ctypes.c_void_p * max(n, 1))(*[None if u is None else u.ctypes.data for u in ubb])
+    ul = (ctypes.c_size_t * max(n, 1))(*[0 if u is None else len(u) for u in ub])
+    bufs = [np.frombuffer(b, dtype=np.uint8) for b in blocks]
+    bp = (ctypes.c_void_p * max(n, 1))(*[b.ctypes.data for b in bufs])
+    ln = (ctypes.c_size_t * max(n, 1))(*[len(b) for b in blocks])
+    nums = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in block_nums])
+    fl = [np.ascontiguousarray(f, dtype=np.uint8) for f in flags]
+    fp = (ctypes.c_void_p * max(n, 1))(*[f.ctypes.data for f in fl])
+    nt = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in fl])
+    pv = ctypes.create_string_buffer(prev, len(prev)) if prev else None
+    out = ctypes.create_string_buffer(32 * max(n, 1))
+    _check(L.fgv_commit_hashes_ub(n, up, ul, bp, ln, fp, nt, nums, pv, len(prev), out, threads))
+    return [out.raw[32 * b:32 * b + 32] for b in range(n)]
 
 
 def commit_hashes(blocks, flags, block_nums, prev: bytes = b"", threads=0):

@@ -364,13 +364,35 @@ extern "C" int fgv_commit_hash(const uint8_t *block, size_t len, const uint8_t *
 extern "C" int fgv_commit_hashes(size_t n, const uint8_t *const *blocks, const size_t *lens,
                                  const uint8_t *const *flags, const size_t *ntx, const uint64_t *block_nums,
                                  const uint8_t *prev, size_t prev_len, uint8_t *out, unsigned threads) {
-  if (n && (!blocks || !lens || !flags || !ntx || !block_nums || !out)) return FGV_EINVAL;
+  return fgv_commit_hashes_ub(n, nullptr, nullptr, blocks, lens, flags, ntx, block_nums, prev, prev_len, out, threads);
+}
+
+// The same chain with the update-batch bytes given where the device serialised them
+// (fgv_mvcc_update_bytes_acquire): such a block's prefix is varint(len(flags)) || flags || bytes,
+// one SHA-256 stream; a block without them is decoded as above.
+extern "C" int fgv_commit_hashes_ub(size_t n, const uint8_t *const *ub, const size_t *ub_lens,
+                                    const uint8_t *const *blocks, const size_t *lens, const uint8_t *const *flags,
+                                    const size_t *ntx, const uint64_t *block_nums, const uint8_t *prev,
+                                    size_t prev_len, uint8_t *out, unsigned threads) {
+  if (n && (!flags || !ntx || !out)) return FGV_EINVAL;
   if (prev_len && !prev) return FGV_EINVAL;
-  for (size_t b = 0; b < n; b++)
-    if (!blocks[b] || (ntx[b] && !flags[b])) return FGV_EINVAL;
+  if (ub && !ub_lens) return FGV_EINVAL;
+  for (size_t b = 0; b < n; b++) {
+    if (ntx[b] && !flags[b]) return FGV_EINVAL;
+    if (!(ub && ub[b]) && (!blocks || !lens || !block_nums || !blocks[b])) return FGV_EINVAL;
+  }
   std::vector<fgvsha::Stream> st(n);
   std::vector<int> rc(n, FGV_OK);
-  auto one = [&](size_t b) { rc[b] = commit_prefix(blocks[b], lens[b], flags[b], ntx[b], block_nums[b], st[b]); };
+  auto one = [&](size_t b) {
+    if (ub && ub[b]) {
+      uint8_t pre[10];
+      st[b].update(pre, (size_t)(put_varint(pre, ntx[b]) - pre));
+      if (ntx[b]) st[b].update(flags[b], ntx[b]);
+      if (ub_lens[b]) st[b].update(ub[b], ub_lens[b]);
+      return;
+    }
+    rc[b] = commit_prefix(blocks[b], lens[b], flags[b], ntx[b], block_nums[b], st[b]);
+  };
   // a persistent pool of min(16, hardware threads) workers, one caller at a time (a pool per call
   // spent ~20 us per thread creation); `threads` = 1 runs on the caller only
   static std::mutex pool_mu;

@@ -241,6 +241,19 @@ __global__ void k_mv_upsert_insert(uint32_t mode, uint32_t rlast, uint32_t n_hos
                                    unsigned long long *top, uint64_t block_num, const MvCounters *c);
 __global__ void k_mv_tags(const uint8_t *base, MvRec *recs, uint32_t n);
 __global__ void k_mv_tail(const MvCounters *c, const unsigned long long *top, uint32_t *hc, unsigned long long *htop);
+// mvcc_ub.hip -- a committed block's update-batch bytes (the commit hash's input) on the device.
+// Block write records carry their value span in blk (offset from the base) and txn (length)
+// until the batch pass's commit stores versions there (k_mvb_upsert_find runs after k_ub_block).
+#define UB_OK 0u
+#define UB_NONE 1u  // not produced on the device (too many writes / groups, arena full, not decided)
+struct UbMeta {
+  uint64_t off;  // in the call's arena
+  uint32_t len, status;
+};
+void ub_block_launch(hipStream_t s, uint32_t nb, const uint8_t *base, const MvRec *writes, const MvTxInfo *info,
+                     const uint8_t *st, const MvCounters *c, uint32_t rlast, const uint32_t *bfirst,
+                     const uint64_t *bnums, uint32_t ntx0, uint64_t num0, uint8_t *out, uint64_t out_cap,
+                     unsigned long long *used, UbMeta *meta);
 struct MvRange {  // a range query's scan bounds (bytes in a host-built buffer)
   uint32_t ns_off, ns_len, s_off, s_len, e_off, e_len, flags, pad;
 };

@@ -15,9 +15,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -87,6 +89,27 @@ struct fgv_mvcc_state {
   HostBuf mbhead, mbtail;
   uint64_t mbtbl_cap = 0;
   uint32_t mb_epoch = 0, mb_rounds = 0;
+  // update-batch bytes (fgv_mvcc_set_update_bytes, mvcc_ub.hip): one generation per committing
+  // call, two alternating, so a host thread hashes call k's bytes while call k+1 runs
+  struct UbGen {
+    DevBuf arena, used;      // the serialisation arena and its claim counter
+    HostBuf meta;            // UbMeta per block of the call (pinned, written by k_ub_block)
+    HostBuf host;            // the bytes, copied back after the call
+    hipEvent_t ev = nullptr; // that copy is done
+    uint64_t ticket = 0;     // the call (0: none)
+    uint64_t cap = 0;
+    size_t nb = 0;
+    int readers = 0;         // fgv_mvcc_update_bytes_acquire holders
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    std::vector<uint8_t> ok;
+  } ub[2];
+  bool ub_on = false;
+  int ub_cur = -1;           // generation of the call in progress (-1: none)
+  uint64_t ub_calls = 0, ub_last = 0;
+  std::mutex ub_mu;
+  std::condition_variable ub_cv;
+  hipStream_t ub_stream = nullptr;
 };
 
 void fgv_mvcc_free(fgv_mvcc_state *M) {
@@ -100,6 +123,14 @@ void fgv_mvcc_free(fgv_mvcc_state *M) {
     if (e) hipEventDestroy(e);
   HostBuf *h[] = {&M->hhead, &M->htail, &M->bhead, &M->btail, &M->mbhead, &M->mbtail};
   for (auto *b : h) b->release();
+  for (auto &G : M->ub) {
+    G.arena.release();
+    G.used.release();
+    G.meta.release();
+    G.host.release();
+    if (G.ev) hipEventDestroy(G.ev);
+  }
+  if (M->ub_stream) hipStreamDestroy(M->ub_stream);
   delete M;
 }
 
@@ -1078,21 +1109,108 @@ static bool mvcc_spin() {
   return spin;
 }
 
+// ----------------------------------------------------------------- update-batch bytes
+// A committing call with fgv_mvcc_set_update_bytes on takes generation (calls + 1) & 1: it waits
+// for that generation's readers (fgv_mvcc_update_bytes_acquire of the call two back) and for its
+// previous copy back, then every device path of the call launches k_ub_block behind its flags
+// (meta entry = the block's index in the call).  After the call the produced bytes come back in
+// one copy on their own stream; the ticket names the call.
+static int ub_begin(fgv_ctx *c, fgv_mvcc_state *M, size_t nb, const size_t *lens) {
+  M->ub_cur = -1;
+  if (!M->ub_on || nb == 0) return FGV_OK;
+  const int gi = (int)((M->ub_calls + 1) & 1);
+  auto &G = M->ub[gi];
+  {
+    std::unique_lock<std::mutex> lk(M->ub_mu);
+    M->ub_cv.wait(lk, [&] { return G.readers == 0; });
+    G.ticket = 0;
+  }
+  // arena: 5/4 of the blocks' bytes (an update batch holds the valid writes' keys and values, once
+  // each, plus ~30 B of framing per write); a block that does not fit is decoded on the host
+  uint64_t cap = 1 << 20;
+  for (size_t k = 0; k < nb; k++) cap += lens[k] + lens[k] / 4;
+  if (!G.arena.ensure(cap) || !G.used.ensure(64) || !G.meta.ensure(nb * sizeof(UbMeta))) return FGV_ENOMEM;
+  G.cap = cap;
+  UbMeta *m = G.meta.as<UbMeta>();
+  for (size_t k = 0; k < nb; k++) m[k] = UbMeta{0, 0, UB_NONE};
+  if (!G.ev) HIP_TRY(hipEventCreateWithFlags(&G.ev, hipEventDisableTiming));
+  else HIP_TRY(hipStreamWaitEvent(c->stream, G.ev, 0));  // the copy back of two calls ago
+  HIP_TRY(hipMemsetAsync(G.used.p, 0, 8, c->stream));
+  G.nb = nb;
+  M->ub_cur = gi;
+  return FGV_OK;
+}
+// the device view of meta entry `idx` of the call in progress (null: no update bytes this call)
+static UbMeta *ub_meta_dev(fgv_mvcc_state *M, size_t idx) {
+  if (M->ub_cur < 0) return nullptr;
+  auto &G = M->ub[M->ub_cur];
+  UbMeta *d = nullptr;
+  if (idx >= G.nb || hipHostGetDevicePointer(reinterpret_cast<void **>(&d), G.meta.p, 0) != hipSuccess) return nullptr;
+  return d + idx;
+}
+static void ub_launch(hipStream_t s, fgv_mvcc_state *M, size_t idx, uint32_t nb, const uint8_t *base,
+                      const MvRec *writes, const MvTxInfo *info, const uint8_t *st, const MvCounters *c, uint32_t rlast,
+                      const uint32_t *bfirst, const uint64_t *bnums, uint32_t ntx0, uint64_t num0) {
+  UbMeta *m = ub_meta_dev(M, idx);
+  if (!m) return;
+  auto &G = M->ub[M->ub_cur];
+  ub_block_launch(s, nb, base, writes, info, st, c, rlast, bfirst, bnums, ntx0, num0, G.arena.as<uint8_t>(), G.cap,
+                  G.used.as<unsigned long long>(), m);
+}
+// after the call's last synchronisation: the produced blocks' bytes back to the host, one copy
+static void ub_end(fgv_ctx *c, fgv_mvcc_state *M, bool ok) {
+  const int gi = M->ub_cur;
+  M->ub_cur = -1;
+  if (gi < 0) return;
+  auto &G = M->ub[gi];
+  const UbMeta *m = G.meta.as<UbMeta>();
+  uint64_t total = 0;
+  std::vector<uint64_t> off(G.nb);
+  std::vector<uint32_t> len(G.nb);
+  std::vector<uint8_t> good(G.nb);
+  for (size_t k = 0; k < G.nb; k++) {
+    good[k] = ok && m[k].status == UB_OK;
+    off[k] = m[k].off;
+    len[k] = m[k].len;
+    if (good[k]) total = std::max<uint64_t>(total, m[k].off + m[k].len);
+  }
+  if (ok && !M->ub_stream && hipStreamCreateWithFlags(&M->ub_stream, hipStreamNonBlocking) != hipSuccess) ok = false;
+  if (ok && total && (!G.host.ensure(total) ||
+                      hipMemcpyAsync(G.host.p, G.arena.p, total, hipMemcpyDeviceToHost, M->ub_stream) != hipSuccess))
+    ok = false;
+  if (ok && hipEventRecord(G.ev, M->ub_stream) != hipSuccess) ok = false;
+  (void)c;
+  std::lock_guard<std::mutex> lk(M->ub_mu);
+  if (!ok) return;  // (ticket stays 0: the caller decodes every block on the host)
+  G.off.swap(off);
+  G.len.swap(len);
+  G.ok.swap(good);
+  G.ticket = ++M->ub_calls;
+  M->ub_last = G.ticket;
+}
+
 static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block,
                                 uint64_t block_num, uint8_t *flags, size_t ntx, int commit, const uint8_t *next,
-                                size_t next_len);
+                                size_t next_len, size_t ub_idx = 0);
 
 static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block, uint64_t block_num,
                          uint8_t *flags, size_t ntx, int commit, const uint8_t *next, size_t next_len) {
   if (!c || !block || (ntx && !flags)) return FGV_EINVAL;
   if (len >= 0xFFFFFFFFull || ntx >= 0x7FFFFFFFull) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  return mvcc_validate_locked(c, block, len, d_block, block_num, flags, ntx, commit, next, next_len);
+  fgv_mvcc_state *M = c->mv;
+  if (M && commit) {
+    const int rc = ub_begin(c, M, 1, &len);
+    if (rc) return rc;
+  }
+  const int rc = mvcc_validate_locked(c, block, len, d_block, block_num, flags, ntx, commit, next, next_len, 0);
+  if (M) ub_end(c, M, rc == FGV_OK);
+  return rc;
 }
 
 static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block,
                                 uint64_t block_num, uint8_t *flags, size_t ntx, int commit, const uint8_t *next,
-                                size_t next_len) {
+                                size_t next_len, size_t ub_idx) {
   fgv_mvcc_state *M = c->mv;
   if (!M) return FGV_ESTATE;
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
@@ -1189,6 +1307,8 @@ static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, co
     }
     hipLaunchKernelGGL(k_mvx_flags, grid_for(ntx), dim3(256), 0, s, N, r, d_in, d_info, M->set[0].st.as<uint8_t>(), d_out,
                        d_c);
+    if (commit)  // (self-gated: a launch before convergence reports "not produced", the next decides)
+      ub_launch(s, M, ub_idx, 1, dblk, d_w, d_info, M->set[0].st.as<uint8_t>(), d_c, r, nullptr, nullptr, N, block_num);
     if (commit) {
       hipLaunchKernelGGL(k_mv_last, grid_stride(rcap), dim3(256), 0, s, r, d_w, M->set[0].wslot.as<uint32_t>(),
                          M->set[0].st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
@@ -1534,6 +1654,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
                            S.st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
     }
     if (commit) {
+      ub_launch(s, M, b, 1, dblk, d_w, d_info, S.st.as<uint8_t>(), d_c, R, nullptr, nullptr, N, block_nums[b]);
       hipLaunchKernelGGL(k_mv_upsert_find, grid_stride(rcap), dim3(256), 0, s, 1u, R, 0u, dblk, d_w,
                          S.wslot.as<uint32_t>(), S.st.as<uint8_t>(), d_b, epoch, M->tbl.as<StateSlot>(), M->mask,
                          M->arena.as<uint8_t>(), block_nums[b], S.pend.as<uint8_t>(), d_c);
@@ -1770,6 +1891,8 @@ static int mvcc_batch(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
                        S.rslot.as<uint32_t>(), M->mbrstat.as<uint8_t>(), d_b, S.st.as<uint8_t>(), d_bf, d_bn, NB, d_c);
   hipLaunchKernelGGL(k_mvx_flags, grid_for(total), dim3(256), 0, s, N, R, d_in, d_info, S.st.as<uint8_t>(),
                      d_tail + kCounterBytes, d_c);
+  if (commit)  // (before k_mvb_upsert_find, which stores versions in the write records' value fields)
+    ub_launch(s, M, first, NB, base, d_w, d_info, S.st.as<uint8_t>(), d_c, R, d_bf, d_bn, 0u, 0ull);
   if (commit) {
     hipLaunchKernelGGL(k_mvb_last, grid_stride(rcap), dim3(256), 0, s, R, d_w, S.wslot.as<uint32_t>(),
                        S.st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
@@ -1813,11 +1936,14 @@ static int mvcc_batch(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   return FGV_OK;
 }
 
+static int mvcc_blocks_run(fgv_ctx *c, fgv_mvcc_state *M, size_t n, const uint8_t *const *blocks, const size_t *lens,
+                           const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
+                           const size_t *ntx, int commit, size_t *n_done, size_t n_next,
+                           const uint8_t *const *next_blocks, const size_t *next_lens);
 static int mvcc_blocks(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const size_t *lens,
                        const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
                        const size_t *ntx, int commit, size_t *n_done, size_t n_next,
                        const uint8_t *const *next_blocks, const size_t *next_lens) {
-  size_t done = 0;
   if (n_done) *n_done = 0;
   if (!c || (n && (!blocks || !lens || !block_nums || !flags || !ntx))) return FGV_EINVAL;
   for (size_t k = 0; k < n; k++)
@@ -1826,6 +1952,21 @@ static int mvcc_blocks(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const
   fgv_mvcc_state *M = c->mv;
   if (!M) return FGV_ESTATE;
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
+  if (commit) {
+    const int rc = ub_begin(c, M, n, lens);
+    if (rc) return rc;
+  }
+  const int rc = mvcc_blocks_run(c, M, n, blocks, lens, d_blocks, block_nums, flags, ntx, commit, n_done, n_next,
+                                 next_blocks, next_lens);
+  ub_end(c, M, rc == FGV_OK || (n_done && *n_done > 0));
+  return rc;
+}
+
+static int mvcc_blocks_run(fgv_ctx *c, fgv_mvcc_state *M, size_t n, const uint8_t *const *blocks, const size_t *lens,
+                           const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
+                           const size_t *ntx, int commit, size_t *n_done, size_t n_next,
+                           const uint8_t *const *next_blocks, const size_t *next_lens) {
+  size_t done = 0;
   // FGV_MVCC_CHAIN=0: one single-block call per block (A/B)
   static const bool chain = [] {
     const char *e = getenv("FGV_MVCC_CHAIN");
@@ -1880,7 +2021,7 @@ static int mvcc_blocks(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const
     // the first block the chain did not finish: the single-block path (phantom validators, more
     // rounds, or the error it returns)
     const int rc = mvcc_validate_locked(c, blocks[done], lens[done], d_blocks ? d_blocks[done] : nullptr,
-                                        block_nums[done], flags[done], ntx[done], commit, nullptr, 0);
+                                        block_nums[done], flags[done], ntx[done], commit, nullptr, 0, done);
     if (rc) return rc;
     done++;
     if (n_done) *n_done = done;
@@ -1915,6 +2056,62 @@ int fgv_mvcc_validate_blocks_next(fgv_ctx *c, size_t n, const uint8_t *const *bl
   if (n_next && (!next_blocks || !next_lens)) return FGV_EINVAL;
   return mvcc_blocks(c, n, blocks, lens, d_blocks, block_nums, flags, ntx, commit, n_done, n_next, next_blocks,
                      next_lens);
+}
+
+int fgv_mvcc_set_update_bytes(fgv_ctx *c, int on) {
+  if (!c) return FGV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->mv) return FGV_ESTATE;
+  c->mv->ub_on = on != 0;
+  return FGV_OK;
+}
+
+int fgv_mvcc_last_ticket(fgv_ctx *c, uint64_t *ticket) {
+  if (!c || !ticket) return FGV_EINVAL;
+  fgv_mvcc_state *M = c->mv;
+  if (!M) return FGV_ESTATE;
+  std::lock_guard<std::mutex> lk(M->ub_mu);
+  *ticket = M->ub_last;
+  return FGV_OK;
+}
+
+int fgv_mvcc_update_bytes_acquire(fgv_ctx *c, uint64_t ticket, size_t n, const uint8_t **bytes, size_t *lens) {
+  if (!c || (n && (!bytes || !lens))) return FGV_EINVAL;
+  fgv_mvcc_state *M = c->mv;
+  if (!M) return FGV_ESTATE;
+  fgv_mvcc_state::UbGen *G = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(M->ub_mu);
+    for (auto &g : M->ub)
+      if (ticket && g.ticket == ticket) G = &g;
+    if (!G) return FGV_ESTATE;  // not a call of the last two with update bytes
+    if (n > G->nb) return FGV_EINVAL;
+    G->readers++;
+  }
+  hipSetDevice(c->device);
+  if (hipEventSynchronize(G->ev) != hipSuccess) {
+    fgv_mvcc_update_bytes_release(c, ticket);
+    return FGV_EDEVICE;
+  }
+  for (size_t b = 0; b < n; b++) {
+    bytes[b] = G->ok[b] ? G->host.as<uint8_t>() + G->off[b] : nullptr;
+    lens[b] = G->ok[b] ? G->len[b] : 0;
+  }
+  return FGV_OK;
+}
+
+int fgv_mvcc_update_bytes_release(fgv_ctx *c, uint64_t ticket) {
+  if (!c) return FGV_EINVAL;
+  fgv_mvcc_state *M = c->mv;
+  if (!M) return FGV_ESTATE;
+  std::lock_guard<std::mutex> lk(M->ub_mu);
+  for (auto &g : M->ub)
+    if (ticket && g.ticket == ticket && g.readers > 0) {
+      g.readers--;
+      M->ub_cv.notify_all();
+      return FGV_OK;
+    }
+  return FGV_ESTATE;
 }
 
 int fgv_mvcc_last_stats(fgv_ctx *c, double *lookup_ms, double *total_ms, uint64_t *reads, uint64_t *writes,

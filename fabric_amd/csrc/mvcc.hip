@@ -162,8 +162,10 @@ struct Sink {
   __device__ void read(S ns, bool hashed, S coll, S key, bool has_ver, uint64_t b, uint64_t t) {
     rec(rout, nr++, ns, hashed, coll, key, has_ver ? MVR_HASVER : 0u, b, t);
   }
-  __device__ void write(S ns, bool hashed, S coll, S key, bool del) {
-    rec(wout, nw++, ns, hashed, coll, key, del ? MVR_DELETE : 0u, 0, 0);
+  // (a write's blk / txn: its value span -- offset from base, length -- for k_ub_block)
+  __device__ void write(S ns, bool hashed, S coll, S key, bool del, S val) {
+    rec(wout, nw++, ns, hashed, coll, key, del ? MVR_DELETE : 0u, del ? 0ull : (uint64_t)(val.p - base),
+        del ? 0ull : val.n);
     wbytes += ((uint64_t)ns.n + (hashed ? 3u + coll.n : 0u) + key.n + 7u) & ~7ull;
   }
 };
@@ -260,7 +262,7 @@ struct VRW {
                                0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
         del = bytes_eq(w.val.p, e, 32);
       }
-      sk->write(ns, hashed, coll, w.key, del);
+      sk->write(ns, hashed, coll, w.key, del, w.val);
       return true;
     }
     host = true;  // metadata write (conditional on the key existing: the host path)

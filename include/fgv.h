@@ -320,15 +320,17 @@ int fgv_validate_blocks_pipelined(fgv_ctx *ctx, size_t nblocks, const uint8_t *c
  * On, fgv_validate_blocks[_pipelined] return FGV_OK for such a batch, and fgv_last_block_status
  * reports for each block of the last call:
  *   FGV_OK           -- its flags are final;
- *   FGV_EUNSUPPORTED -- it holds something outside the model (a CONFIG transaction, a P-384 or
- *                       SHA3 identity, a certificate no channel MSP can judge, ...): validate this
- *                       block with the reference; its flag bytes are 0xFD where the engine could
- *                       not decide a transaction;
+ *   FGV_EUNSUPPORTED -- it holds something outside the model (a CONFIG transaction, a P-384
+ *                       identity registered without its key, a SHA3 identity, a certificate no
+ *                       channel MSP can judge, ...): validate this block with the reference; its
+ *                       flag bytes are 0xFD where the engine could not decide a transaction;
  *   FGV_BLOCK_LATER  -- not decided: an earlier block of the call may change the key-level
  *                       VALIDATION_PARAMETER of a key this block writes, and the reference commits
- *                       that block before this one reads it (statebased/vpmanagerimpl.go:296-355).
- *                       Every block from the first such one (n_final) on is LATER: commit blocks
- *                       [0, n_final) and call again with the rest.
+ *                       that block before this one reads it (statebased/vpmanagerimpl.go:296-355);
+ *                       or an earlier block holds a CONFIG transaction that reaches its apply step
+ *                       (a config update changes the channel's MSPs and policies for every later
+ *                       block).  Every block from the first such one (n_final) on is LATER: commit
+ *                       blocks [0, n_final) and call again with the rest.
  * Blocks after an unsupported one stay final: a block reads the earlier blocks' txids (every one,
  * whatever its code: checkTxIdDupsLedger, validator.go:460-481) and, through the rule above,
  * never their codes.  Single-GPU calls; the group call with fgv_group_set_block_outcomes; the
@@ -694,6 +696,28 @@ int fgv_commit_hash(const uint8_t *block, size_t len, const uint8_t *flags, size
 int fgv_commit_hashes(size_t n, const uint8_t *const *blocks, const size_t *lens, const uint8_t *const *flags,
                       const size_t *ntx, const uint64_t *block_nums, const uint8_t *prev, size_t prev_len,
                       uint8_t *out, unsigned threads);
+
+/* The update-batch bytes on the device (round 6).  With fgv_mvcc_set_update_bytes(ctx, 1), every
+ * committing fgv_mvcc_validate_block[s][_next] call also serialises each committed block's
+ * updateBatchBytes on the GPU from its MVCC write records (fabric_amd/csrc/mvcc_ub.hip: the valid
+ * writes gathered, grouped, sorted and framed as txmgr.Updates, update_batch_bytes.go:29-105) and
+ * copies them back on a stream of their own after the call, so only the serial SHA-256 stays on
+ * the host.  fgv_mvcc_last_ticket names the last such call; fgv_mvcc_update_bytes_acquire(ticket)
+ * waits for its copy and gives block b's bytes (bytes[b] = NULL: not produced on the device -- a
+ * block on the host phantom path, more than 8,192 valid writes, ...); they stay valid until
+ * fgv_mvcc_update_bytes_release(ticket).  Two calls are kept: the second committing call after
+ * `ticket` waits for its release.  Only blocks [0, n_done) of a call are committed.
+ * fgv_commit_hashes_ub: fgv_commit_hashes with ub[b] (ub_lens[b] bytes) used as block b's update
+ * batch where given (ub NULL or ub[b] NULL: block b is decoded from blocks[b] as before) -- the
+ * same 32 bytes per block. */
+int fgv_mvcc_set_update_bytes(fgv_ctx *ctx, int on);
+int fgv_mvcc_last_ticket(fgv_ctx *ctx, uint64_t *ticket);
+int fgv_mvcc_update_bytes_acquire(fgv_ctx *ctx, uint64_t ticket, size_t n, const uint8_t **bytes, size_t *lens);
+int fgv_mvcc_update_bytes_release(fgv_ctx *ctx, uint64_t ticket);
+int fgv_commit_hashes_ub(size_t n, const uint8_t *const *ub, const size_t *ub_lens, const uint8_t *const *blocks,
+                         const size_t *lens, const uint8_t *const *flags, const size_t *ntx,
+                         const uint64_t *block_nums, const uint8_t *prev, size_t prev_len, uint8_t *out,
+                         unsigned threads);
 
 /* host SHA-256 of one buffer (the data-hash primitive); returns 1 when the SHA extensions
  * were used, 0 for the portable path */

@@ -37,6 +37,27 @@ def test_commit_hashes_pipeline_blocks():
         assert got[b] == prev, b
 
 
+def test_commit_hashes_ub_given_bytes():
+    """fgv_commit_hashes_ub (the device update-batch path's host half): blocks whose update bytes
+    are given hash them as they are (here the oracle's deterministicBytesForPubAndHashUpdates),
+    the others are decoded -- the same chain as fgv_commit_hashes and the reference ledgers"""
+    from oracle import commithash
+    bl = [b for b in ledgers()["v20_testchannel"] if b["commit_hash"] is not None]
+    blks = [b["block"] for b in bl]
+    fl = [np.array(b["flags"], np.uint8) for b in bl]
+    nums = [b["number"] for b in bl]
+    ub = [commithash.update_batch_bytes(*commithash.update_batch(b, list(f), n)) if i % 2 == 0 else None
+          for i, (b, f, n) in enumerate(zip(blks, fl, nums))]
+    got = _lib.commit_hashes_ub(ub, blks, fl, nums)
+    assert [h.hex() for h in got] == [b["commit_hash"] for b in bl]
+    # bytes that differ from the block's update batch change the hash (they are what is hashed)
+    if any(u for u in ub if u):
+        k = next(i for i, u in enumerate(ub) if u)
+        bad = list(ub)
+        bad[k] = ub[k] + b"\x00"
+        assert _lib.commit_hashes_ub(bad, blks, fl, nums)[k] != got[k]
+
+
 def _bulk_block(nwrites, dup_at=None):
     """Two transactions: a bulk load of `nwrites` keys (one key written twice when dup_at is
     set) and an ordinary one; flags all VALID (the commit hash does not validate)."""
