@@ -210,7 +210,7 @@ __global__ void k_mvb_round(uint32_t ntx, uint32_t r, const MvTxInfo *info, cons
 __global__ void k_mvb_last(uint32_t rlast, const MvRec *writes, const uint32_t *wslot, const uint8_t *st, MbSlot *btbl,
                            uint32_t epoch, MvCounters *c, const unsigned long long *top, uint64_t slots_cap,
                            uint64_t arena_cap);
-__global__ void k_mvb_upsert_find(uint32_t rlast, const uint8_t *base, MvRec *recs, const uint32_t *wslot,
+__global__ void k_mvb_upsert_find(uint32_t rlast, const uint8_t *base, const MvRec *recs, const uint32_t *wslot,
                                   const uint8_t *st, const MbSlot *btbl, uint32_t epoch, StateSlot *tbl, uint64_t mask,
                                   const uint8_t *arena, const uint32_t *bfirst, const uint64_t *bnums, uint32_t nb,
                                   uint8_t *pend, const MvCounters *c);
@@ -238,7 +238,8 @@ __global__ void k_mv_upsert_find(uint32_t mode, uint32_t rlast, uint32_t n_host,
                                  const MvCounters *c);
 __global__ void k_mv_upsert_insert(uint32_t mode, uint32_t rlast, uint32_t n_host, const uint8_t *base,
                                    const MvRec *recs, const uint8_t *pend, StateSlot *tbl, uint64_t mask, uint8_t *arena,
-                                   unsigned long long *top, uint64_t block_num, const MvCounters *c);
+                                   unsigned long long *top, uint64_t block_num, const MvCounters *c,
+                                   const uint32_t *bfirst, const uint64_t *bnums, uint32_t nb);
 __global__ void k_mv_tags(const uint8_t *base, MvRec *recs, uint32_t n);
 __global__ void k_mv_tail(const MvCounters *c, const unsigned long long *top, uint32_t *hc, unsigned long long *htop);
 // mvcc_ub.hip -- a committed block's update-batch bytes (the commit hash's input) on the device.
@@ -246,14 +247,28 @@ __global__ void k_mv_tail(const MvCounters *c, const unsigned long long *top, ui
 // until the batch pass's commit stores versions there (k_mvb_upsert_find runs after k_ub_block).
 #define UB_OK 0u
 #define UB_NONE 1u  // not produced on the device (too many writes / groups, arena full, not decided)
-struct UbMeta {
+#define UB_MAX 8192u  // valid writes of one block the device serialisation sorts (LDS)
+struct UbMeta {  // per block of the call, pinned host memory (written by k_ub_sort)
   uint64_t off;  // in the call's arena
   uint32_t len, status;
+};
+struct UbBlk {  // per block of one launch, device memory: k_ub_sort -> k_ub_write
+  uint64_t off;
+  uint32_t len, nent, t0;
+  uint64_t num;
+};
+#define UBE_LIVE 1u  // UbEnt.flags: a surviving write (the last of its key)
+#define UBE_NS 2u    // carries the namespace field (first write of a namespace)
+#define UBE_COLL 4u  // carries the collection field (first write of a collection)
+struct UbEnt {   // one sorted position of a block: the record, its offset in the block's bytes
+  uint32_t rec, off, flags;
 };
 void ub_block_launch(hipStream_t s, uint32_t nb, const uint8_t *base, const MvRec *writes, const MvTxInfo *info,
                      const uint8_t *st, const MvCounters *c, uint32_t rlast, const uint32_t *bfirst,
                      const uint64_t *bnums, uint32_t ntx0, uint64_t num0, uint8_t *out, uint64_t out_cap,
-                     unsigned long long *used, UbMeta *meta);
+                     unsigned long long *used, UbMeta *meta, UbBlk *dmeta, UbEnt *ents);
+void ub_copy_launch(hipStream_t s, const uint8_t *arena, uint8_t *host_dev, const unsigned long long *used,
+                    uint64_t cap);
 struct MvRange {  // a range query's scan bounds (bytes in a host-built buffer)
   uint32_t ns_off, ns_len, s_off, s_len, e_off, e_len, flags, pad;
 };

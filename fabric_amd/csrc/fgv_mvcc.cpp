@@ -93,23 +93,23 @@ struct fgv_mvcc_state {
   // call, two alternating, so a host thread hashes call k's bytes while call k+1 runs
   struct UbGen {
     DevBuf arena, used;      // the serialisation arena and its claim counter
-    HostBuf meta;            // UbMeta per block of the call (pinned, written by k_ub_block)
-    HostBuf host;            // the bytes, copied back after the call
+    HostBuf meta;            // UbMeta per block of the call (pinned, written by k_ub_sort)
+    HostBuf host;            // the arena, copied back by k_ub_copy after the call
     hipEvent_t ev = nullptr; // that copy is done
     uint64_t ticket = 0;     // the call (0: none)
     uint64_t cap = 0;
     size_t nb = 0;
     int readers = 0;         // fgv_mvcc_update_bytes_acquire holders
-    std::vector<uint64_t> off;
-    std::vector<uint32_t> len;
-    std::vector<uint8_t> ok;
   } ub[2];
+  DevBuf ub_dmeta, ub_ents;  // one launch's per-block results and sorted entries (k_ub_sort -> k_ub_write)
   bool ub_on = false;
   int ub_cur = -1;           // generation of the call in progress (-1: none)
   uint64_t ub_calls = 0, ub_last = 0;
   std::mutex ub_mu;
   std::condition_variable ub_cv;
-  hipStream_t ub_stream = nullptr;
+  hipStream_t ub_stream = nullptr;    // the batch pass's serialisation and every call's copy back
+  hipEvent_t ub_in = nullptr, ub_tail = nullptr;  // (into / the last work queued on ub_stream)
+  bool ub_tail_set = false, ub_side = false;
 };
 
 void fgv_mvcc_free(fgv_mvcc_state *M) {
@@ -123,6 +123,7 @@ void fgv_mvcc_free(fgv_mvcc_state *M) {
     if (e) hipEventDestroy(e);
   HostBuf *h[] = {&M->hhead, &M->htail, &M->bhead, &M->btail, &M->mbhead, &M->mbtail};
   for (auto *b : h) b->release();
+  if (M->ub_stream) hipStreamSynchronize(M->ub_stream);
   for (auto &G : M->ub) {
     G.arena.release();
     G.used.release();
@@ -130,6 +131,10 @@ void fgv_mvcc_free(fgv_mvcc_state *M) {
     G.host.release();
     if (G.ev) hipEventDestroy(G.ev);
   }
+  M->ub_dmeta.release();
+  M->ub_ents.release();
+  if (M->ub_in) hipEventDestroy(M->ub_in);
+  if (M->ub_tail) hipEventDestroy(M->ub_tail);
   if (M->ub_stream) hipStreamDestroy(M->ub_stream);
   delete M;
 }
@@ -203,7 +208,7 @@ static int upsert_host(fgv_ctx *c, const char *ns, const uint8_t *key_buf, const
                      M->set[0].pend.as<uint8_t>(), nullptr);
   hipLaunchKernelGGL(k_mv_upsert_insert, grid_stride(n), dim3(256), 0, s, 0u, 0u, (uint32_t)n, lb,
                      M->lrecs.as<MvRec>(), M->set[0].pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask,
-                     M->arena.as<uint8_t>(), M->top.as<unsigned long long>(), 0ull, nullptr);
+                     M->arena.as<uint8_t>(), M->top.as<unsigned long long>(), 0ull, nullptr, nullptr, nullptr, 0u);
   HIP_TRY(hipGetLastError());
   return read_top(c, M);
 }
@@ -1111,12 +1116,20 @@ static bool mvcc_spin() {
 
 // ----------------------------------------------------------------- update-batch bytes
 // A committing call with fgv_mvcc_set_update_bytes on takes generation (calls + 1) & 1: it waits
-// for that generation's readers (fgv_mvcc_update_bytes_acquire of the call two back) and for its
-// previous copy back, then every device path of the call launches k_ub_block behind its flags
-// (meta entry = the block's index in the call).  After the call the produced bytes come back in
-// one copy on their own stream; the ticket names the call.
+// for that generation's readers (fgv_mvcc_update_bytes_acquire of the call two back).  Every
+// device path of the call launches k_ub_sort + k_ub_write behind its flags (meta entry = the
+// block's index in the call): the batch pass on ub_stream, beside its commit kernels (the call
+// does not wait for them), the chain and the single-block path in line.  After the call k_ub_copy
+// brings the arena back on ub_stream; the ticket names the call, and acquire waits for the copy.
+// Every MVCC call first fences its stream behind ub_stream (the serialisation reads the records,
+// codes and counters the next call overwrites).
+static int ub_fence(fgv_ctx *c, fgv_mvcc_state *M) {
+  if (M->ub_tail_set) HIP_TRY(hipStreamWaitEvent(c->stream, M->ub_tail, 0));
+  return FGV_OK;
+}
 static int ub_begin(fgv_ctx *c, fgv_mvcc_state *M, size_t nb, const size_t *lens) {
   M->ub_cur = -1;
+  M->ub_side = false;
   if (!M->ub_on || nb == 0) return FGV_OK;
   const int gi = (int)((M->ub_calls + 1) & 1);
   auto &G = M->ub[gi];
@@ -1129,62 +1142,64 @@ static int ub_begin(fgv_ctx *c, fgv_mvcc_state *M, size_t nb, const size_t *lens
   // each, plus ~30 B of framing per write); a block that does not fit is decoded on the host
   uint64_t cap = 1 << 20;
   for (size_t k = 0; k < nb; k++) cap += lens[k] + lens[k] / 4;
-  if (!G.arena.ensure(cap) || !G.used.ensure(64) || !G.meta.ensure(nb * sizeof(UbMeta))) return FGV_ENOMEM;
+  cap = (cap + 15) & ~(uint64_t)15;
+  if (!G.arena.ensure(cap) || !G.used.ensure(64) || !G.meta.ensure(nb * sizeof(UbMeta)) || !G.host.ensure(cap) ||
+      !M->ub_dmeta.ensure(nb * sizeof(UbBlk)) || !M->ub_ents.ensure(nb * (size_t)UB_MAX * sizeof(UbEnt)))
+    return FGV_ENOMEM;
   G.cap = cap;
   UbMeta *m = G.meta.as<UbMeta>();
   for (size_t k = 0; k < nb; k++) m[k] = UbMeta{0, 0, UB_NONE};
   if (!G.ev) HIP_TRY(hipEventCreateWithFlags(&G.ev, hipEventDisableTiming));
-  else HIP_TRY(hipStreamWaitEvent(c->stream, G.ev, 0));  // the copy back of two calls ago
+  if (!M->ub_in) HIP_TRY(hipEventCreateWithFlags(&M->ub_in, hipEventDisableTiming));
+  if (!M->ub_tail) HIP_TRY(hipEventCreateWithFlags(&M->ub_tail, hipEventDisableTiming));
+  if (!M->ub_stream) HIP_TRY(hipStreamCreateWithFlags(&M->ub_stream, hipStreamNonBlocking));
   HIP_TRY(hipMemsetAsync(G.used.p, 0, 8, c->stream));
   G.nb = nb;
   M->ub_cur = gi;
   return FGV_OK;
 }
-// the device view of meta entry `idx` of the call in progress (null: no update bytes this call)
-static UbMeta *ub_meta_dev(fgv_mvcc_state *M, size_t idx) {
-  if (M->ub_cur < 0) return nullptr;
+// k_ub_sort + k_ub_write for `nb` blocks whose call-level indices start at idx: on stream s (in
+// line), or beside it on ub_stream once s's work so far is done (side)
+static void ub_launch(hipStream_t s, bool side, fgv_mvcc_state *M, size_t idx, uint32_t nb, const uint8_t *base,
+                      const MvRec *writes, const MvTxInfo *info, const uint8_t *st, const MvCounters *c,
+                      uint32_t rlast, const uint32_t *bfirst, const uint64_t *bnums, uint32_t ntx0, uint64_t num0) {
+  if (M->ub_cur < 0) return;
   auto &G = M->ub[M->ub_cur];
-  UbMeta *d = nullptr;
-  if (idx >= G.nb || hipHostGetDevicePointer(reinterpret_cast<void **>(&d), G.meta.p, 0) != hipSuccess) return nullptr;
-  return d + idx;
+  UbMeta *m = nullptr;
+  if (idx + nb > G.nb || hipHostGetDevicePointer(reinterpret_cast<void **>(&m), G.meta.p, 0) != hipSuccess) return;
+  hipStream_t q = s;
+  if (side) {
+    if (hipEventRecord(M->ub_in, s) != hipSuccess || hipStreamWaitEvent(M->ub_stream, M->ub_in, 0) != hipSuccess) return;
+    q = M->ub_stream;
+  } else if (M->ub_side) {  // (the shared launch scratch: behind the side launch of this call)
+    if (hipStreamWaitEvent(s, M->ub_tail, 0) != hipSuccess) return;
+  }
+  ub_block_launch(q, nb, base, writes, info, st, c, rlast, bfirst, bnums, ntx0, num0, G.arena.as<uint8_t>(), G.cap,
+                  G.used.as<unsigned long long>(), m + idx, M->ub_dmeta.as<UbBlk>(), M->ub_ents.as<UbEnt>());
+  if (side && hipEventRecord(M->ub_tail, M->ub_stream) == hipSuccess) {
+    M->ub_side = true;
+    M->ub_tail_set = true;
+  }
 }
-static void ub_launch(hipStream_t s, fgv_mvcc_state *M, size_t idx, uint32_t nb, const uint8_t *base,
-                      const MvRec *writes, const MvTxInfo *info, const uint8_t *st, const MvCounters *c, uint32_t rlast,
-                      const uint32_t *bfirst, const uint64_t *bnums, uint32_t ntx0, uint64_t num0) {
-  UbMeta *m = ub_meta_dev(M, idx);
-  if (!m) return;
-  auto &G = M->ub[M->ub_cur];
-  ub_block_launch(s, nb, base, writes, info, st, c, rlast, bfirst, bnums, ntx0, num0, G.arena.as<uint8_t>(), G.cap,
-                  G.used.as<unsigned long long>(), m);
-}
-// after the call's last synchronisation: the produced blocks' bytes back to the host, one copy
+// after the call's last synchronisation: the arena back to the host on ub_stream (no host wait)
 static void ub_end(fgv_ctx *c, fgv_mvcc_state *M, bool ok) {
   const int gi = M->ub_cur;
   M->ub_cur = -1;
   if (gi < 0) return;
   auto &G = M->ub[gi];
-  const UbMeta *m = G.meta.as<UbMeta>();
-  uint64_t total = 0;
-  std::vector<uint64_t> off(G.nb);
-  std::vector<uint32_t> len(G.nb);
-  std::vector<uint8_t> good(G.nb);
-  for (size_t k = 0; k < G.nb; k++) {
-    good[k] = ok && m[k].status == UB_OK;
-    off[k] = m[k].off;
-    len[k] = m[k].len;
-    if (good[k]) total = std::max<uint64_t>(total, m[k].off + m[k].len);
+  uint8_t *hd = nullptr;
+  if (ok && hipHostGetDevicePointer(reinterpret_cast<void **>(&hd), G.host.p, 0) != hipSuccess) ok = false;
+  // (the in-line launches finished with the call's own synchronisation; the side ones are ahead
+  // on ub_stream)
+  if (ok) {
+    ub_copy_launch(M->ub_stream, G.arena.as<uint8_t>(), hd, G.used.as<unsigned long long>(), G.cap);
+    ok = hipGetLastError() == hipSuccess && hipEventRecord(G.ev, M->ub_stream) == hipSuccess &&
+         hipEventRecord(M->ub_tail, M->ub_stream) == hipSuccess;
+    if (ok) M->ub_tail_set = true;
   }
-  if (ok && !M->ub_stream && hipStreamCreateWithFlags(&M->ub_stream, hipStreamNonBlocking) != hipSuccess) ok = false;
-  if (ok && total && (!G.host.ensure(total) ||
-                      hipMemcpyAsync(G.host.p, G.arena.p, total, hipMemcpyDeviceToHost, M->ub_stream) != hipSuccess))
-    ok = false;
-  if (ok && hipEventRecord(G.ev, M->ub_stream) != hipSuccess) ok = false;
   (void)c;
   std::lock_guard<std::mutex> lk(M->ub_mu);
   if (!ok) return;  // (ticket stays 0: the caller decodes every block on the host)
-  G.off.swap(off);
-  G.len.swap(len);
-  G.ok.swap(good);
   G.ticket = ++M->ub_calls;
   M->ub_last = G.ticket;
 }
@@ -1199,8 +1214,9 @@ static int mvcc_validate(fgv_ctx *c, const uint8_t *block, size_t len, const uin
   if (len >= 0xFFFFFFFFull || ntx >= 0x7FFFFFFFull) return FGV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   fgv_mvcc_state *M = c->mv;
-  if (M && commit) {
-    const int rc = ub_begin(c, M, 1, &len);
+  if (M && hipSetDevice(c->device) == hipSuccess) {
+    int rc = ub_fence(c, M);
+    if (!rc && commit) rc = ub_begin(c, M, 1, &len);
     if (rc) return rc;
   }
   const int rc = mvcc_validate_locked(c, block, len, d_block, block_num, flags, ntx, commit, next, next_len, 0);
@@ -1308,7 +1324,7 @@ static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, co
     hipLaunchKernelGGL(k_mvx_flags, grid_for(ntx), dim3(256), 0, s, N, r, d_in, d_info, M->set[0].st.as<uint8_t>(), d_out,
                        d_c);
     if (commit)  // (self-gated: a launch before convergence reports "not produced", the next decides)
-      ub_launch(s, M, ub_idx, 1, dblk, d_w, d_info, M->set[0].st.as<uint8_t>(), d_c, r, nullptr, nullptr, N, block_num);
+      ub_launch(s, false, M, ub_idx, 1, dblk, d_w, d_info, M->set[0].st.as<uint8_t>(), d_c, r, nullptr, nullptr, N, block_num);
     if (commit) {
       hipLaunchKernelGGL(k_mv_last, grid_stride(rcap), dim3(256), 0, s, r, d_w, M->set[0].wslot.as<uint32_t>(),
                          M->set[0].st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
@@ -1317,7 +1333,7 @@ static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, co
                          M->arena.as<uint8_t>(), block_num, M->set[0].pend.as<uint8_t>(), d_c);
       hipLaunchKernelGGL(k_mv_upsert_insert, grid_stride(rcap), dim3(256), 0, s, 1u, r, 0u, dblk, d_w,
                          M->set[0].pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
-                         M->top.as<unsigned long long>(), block_num, d_c);
+                         M->top.as<unsigned long long>(), block_num, d_c, nullptr, nullptr, 0u);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(M->set[0].tail.p, d_c, sizeof(MvCounters), hipMemcpyDeviceToDevice, s));
@@ -1654,13 +1670,13 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
                            S.st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
     }
     if (commit) {
-      ub_launch(s, M, b, 1, dblk, d_w, d_info, S.st.as<uint8_t>(), d_c, R, nullptr, nullptr, N, block_nums[b]);
+      ub_launch(s, false, M, b, 1, dblk, d_w, d_info, S.st.as<uint8_t>(), d_c, R, nullptr, nullptr, N, block_nums[b]);
       hipLaunchKernelGGL(k_mv_upsert_find, grid_stride(rcap), dim3(256), 0, s, 1u, R, 0u, dblk, d_w,
                          S.wslot.as<uint32_t>(), S.st.as<uint8_t>(), d_b, epoch, M->tbl.as<StateSlot>(), M->mask,
                          M->arena.as<uint8_t>(), block_nums[b], S.pend.as<uint8_t>(), d_c);
       hipLaunchKernelGGL(k_mv_upsert_insert, grid_stride(rcap), dim3(256), 0, s, 1u, R, 0u, dblk, d_w,
                          S.pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
-                         M->top.as<unsigned long long>(), block_nums[b], d_c);
+                         M->top.as<unsigned long long>(), block_nums[b], d_c, nullptr, nullptr, 0u);
     }
     HIP_TRY(hipGetLastError());
     uint8_t *ht = M->btail.as<uint8_t>() + toff[k];
@@ -1892,7 +1908,7 @@ static int mvcc_batch(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   hipLaunchKernelGGL(k_mvx_flags, grid_for(total), dim3(256), 0, s, N, R, d_in, d_info, S.st.as<uint8_t>(),
                      d_tail + kCounterBytes, d_c);
   if (commit)  // (before k_mvb_upsert_find, which stores versions in the write records' value fields)
-    ub_launch(s, M, first, NB, base, d_w, d_info, S.st.as<uint8_t>(), d_c, R, d_bf, d_bn, 0u, 0ull);
+    ub_launch(s, true, M, first, NB, base, d_w, d_info, S.st.as<uint8_t>(), d_c, R, d_bf, d_bn, 0u, 0ull);
   if (commit) {
     hipLaunchKernelGGL(k_mvb_last, grid_stride(rcap), dim3(256), 0, s, R, d_w, S.wslot.as<uint32_t>(),
                        S.st.as<uint8_t>(), d_b, epoch, d_c, M->top.as<unsigned long long>(), M->cap, M->arena_cap);
@@ -1901,7 +1917,7 @@ static int mvcc_batch(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
                        d_bn, NB, S.pend.as<uint8_t>(), d_c);
     hipLaunchKernelGGL(k_mv_upsert_insert, grid_stride(rcap), dim3(256), 0, s, 2u, R, 0u, base, d_w,
                        S.pend.as<uint8_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
-                       M->top.as<unsigned long long>(), 0ull, d_c);
+                       M->top.as<unsigned long long>(), 0ull, d_c, d_bf, d_bn, NB);
   }
   const size_t top_off = kCounterBytes + ((total + 63) & ~(size_t)63);
   hipLaunchKernelGGL(k_mv_tail, dim3(1), dim3(64), 0, s, d_c, M->top.as<unsigned long long>(),
@@ -1952,8 +1968,9 @@ static int mvcc_blocks(fgv_ctx *c, size_t n, const uint8_t *const *blocks, const
   fgv_mvcc_state *M = c->mv;
   if (!M) return FGV_ESTATE;
   if (hipSetDevice(c->device) != hipSuccess) return FGV_EDEVICE;
-  if (commit) {
-    const int rc = ub_begin(c, M, n, lens);
+  {
+    int rc = ub_fence(c, M);
+    if (!rc && commit) rc = ub_begin(c, M, n, lens);
     if (rc) return rc;
   }
   const int rc = mvcc_blocks_run(c, M, n, blocks, lens, d_blocks, block_nums, flags, ntx, commit, n_done, n_next,
@@ -2000,6 +2017,10 @@ static int mvcc_blocks_run(fgv_ctx *c, fgv_mvcc_state *M, size_t n, const uint8_
                                   n_next, next_blocks, next_lens);
         n_next = 0;  // (the next batch is being walked)
         if (rc) return rc;
+        if (stop != end) {  // (the blocks again below: behind the pass's serialisation on ub_stream)
+          const int rf = ub_fence(c, M);
+          if (rf) return rf;
+        }
         if (stop == end) {
           done = end;
           if (n_done) *n_done = done;
@@ -2093,9 +2114,11 @@ int fgv_mvcc_update_bytes_acquire(fgv_ctx *c, uint64_t ticket, size_t n, const u
     fgv_mvcc_update_bytes_release(c, ticket);
     return FGV_EDEVICE;
   }
+  const UbMeta *m = G->meta.as<UbMeta>();
   for (size_t b = 0; b < n; b++) {
-    bytes[b] = G->ok[b] ? G->host.as<uint8_t>() + G->off[b] : nullptr;
-    lens[b] = G->ok[b] ? G->len[b] : 0;
+    const bool ok = m[b].status == UB_OK && m[b].off + m[b].len <= G->cap;
+    bytes[b] = ok ? G->host.as<uint8_t>() + m[b].off : nullptr;
+    lens[b] = ok ? m[b].len : 0;
   }
   return FGV_OK;
 }

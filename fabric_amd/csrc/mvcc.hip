@@ -865,12 +865,14 @@ __global__ __launch_bounds__(256) void k_mv_upsert_find(uint32_t mode, uint32_t 
 
 // Upsert phase 2: claim empty slots for keys known to be absent and distinct (no compares).
 // top[0] = arena bytes used, top[1] = occupied slots.
+__device__ __forceinline__ uint32_t blk_of(const uint32_t *__restrict__ bfirst, uint32_t nb, uint32_t g);
 __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_t rlast, uint32_t n_host,
                                                           const uint8_t *__restrict__ base, const MvRec *__restrict__ recs,
                                                           const uint8_t *__restrict__ pend, StateSlot *__restrict__ tbl,
                                                           uint64_t mask, uint8_t *__restrict__ arena,
                                                           unsigned long long *__restrict__ top, uint64_t block_num,
-                                                          const MvCounters *__restrict__ c) {
+                                                          const MvCounters *__restrict__ c, const uint32_t *__restrict__ bfirst,
+                                                          const uint64_t *__restrict__ bnums, uint32_t nb) {
   uint32_t n = n_host;
   if (mode >= 1) {  // (mode 2: the batch pass -- its versions are in the records)
     if (!converged(c, rlast) || c->nomem) return;
@@ -917,8 +919,14 @@ __global__ __launch_bounds__(256) void k_mv_upsert_insert(uint32_t mode, uint32_
         tbl[idx].off8 = (uint32_t)(off >> 3);
         tbl[idx].ns_len = (uint16_t)fl;
         tbl[idx].key_len = w.key_len;
-        tbl[idx].blk = mode == 1 ? block_num : w.blk;
-        tbl[idx].txn = mode == 1 ? (uint64_t)w.tx : w.txn;
+        if (mode == 2) {  // the batch pass: Height{the record's block, its index there}
+          const uint32_t b = blk_of(bfirst, nb, w.tx);
+          tbl[idx].blk = bnums[b];
+          tbl[idx].txn = w.tx - bfirst[b];
+        } else {
+          tbl[idx].blk = mode == 1 ? block_num : w.blk;
+          tbl[idx].txn = mode == 1 ? (uint64_t)w.tx : w.txn;
+        }
         if (fl + w.key_len <= MV_INLINE) {  // the inline copy (the arena bytes written above; off
           // is 8-byte aligned), 8-byte words: bytes past the key are never compared
           const uint2 *src = reinterpret_cast<const uint2 *>(arena + off);
@@ -1218,9 +1226,10 @@ __global__ __launch_bounds__(256) void k_mvb_last(uint32_t rlast, const MvRec *_
 
 // commit, part 2: the last valid writer of each key updates the committed entry in place at
 // Height{its block's number, its index in the block}, or is marked for insertion (then
-// k_mv_upsert_insert, mode 2, takes the version from the record written here)
+// k_mv_upsert_insert, mode 2, derives the same version from the record's transaction; the records
+// stay unchanged -- k_ub_block may be reading their value spans beside these kernels)
 __global__ __launch_bounds__(256) void k_mvb_upsert_find(uint32_t rlast, const uint8_t *__restrict__ base,
-                                                         MvRec *__restrict__ recs, const uint32_t *__restrict__ wslot,
+                                                         const MvRec *__restrict__ recs, const uint32_t *__restrict__ wslot,
                                                          const uint8_t *__restrict__ st, const MbSlot *__restrict__ btbl,
                                                          uint32_t epoch, StateSlot *__restrict__ tbl, uint64_t mask,
                                                          const uint8_t *__restrict__ arena,
@@ -1242,8 +1251,6 @@ __global__ __launch_bounds__(256) void k_mvb_upsert_find(uint32_t rlast, const u
       tbl[s].txn = vt;
       tbl[s].tag = del ? (tbl[s].tag & ~MV_TAG_PRESENT) : (tbl[s].tag | MV_TAG_PRESENT);
     } else if (!del) {
-      recs[i].blk = vb;
-      recs[i].txn = vt;
       pend[i] = 1;
     }
   }

@@ -12,15 +12,19 @@
 // a collection), key 3, is_delete 4, value 5, version_bytes 6} as repeated field 1 of
 // txmgr.Updates.  Host restatement: fgv_commit.cpp commit_prefix (and oracle/commithash.py).
 //
-// One workgroup (1,024 lanes) per block, everything in LDS:
+// k_ub_sort: one workgroup (1,024 lanes) per block, everything in LDS:
 //   1. gather: the write records of the block's VALID transactions (MvTxInfo.code 0 and the
 //      fixpoint's ST_VALID), a block-wide scan of the per-transaction counts;
 //   2. groups: (namespace, hashed, collection) found by leader election (the first unassigned
 //      entry's group, compared by every lane; a block has a handful), ranked by one lane;
 //   3. sort: 64-bit keys (group rank | 7 key bytes after the prefix every key of the block shares)
 //      by a bitonic network over up to UB_MAX entries, ties by the full key, then by transaction;
-//   4. the last entry of each key's run survives; sizes, a block-wide scan, one arena claim;
-//   5. every lane serialises its survivors.
+//   4. the last entry of each key's run survives; sizes, a block-wide scan, one arena claim; the
+//      survivors' (record, offset, fields) go to the entry list.
+// k_ub_write: one lane per listed entry over the whole chip (the byte framing of ~30 B plus the
+// key and value per write: the serialisation's bulk, spread over every CU instead of one per block).
+// k_ub_copy: the call's arena to pinned host memory, 16-byte stores (sizes read on the device, so
+// the host never waits for them).
 // A block that does not fit (more than UB_MAX valid writes, more than UB_GROUPS groups, the arena
 // full) reports status UB_NONE: the host decodes that block instead (fgv_commit.cpp).
 #include "fgv_kernels.h"
@@ -29,7 +33,6 @@
 using namespace pbd;
 
 #define UB_T 1024u
-#define UB_MAX 8192u    // valid writes one block's LDS sort holds (96 KB of keys and indices)
 #define UB_GROUPS 64u   // (namespace, hashed, collection) groups of one block
 #define UB_ST_VALID 1   // mvcc.hip ST_VALID: the fixpoint's verdict for a VALID transaction
 
@@ -119,15 +122,15 @@ DEV uint32_t kvwrite_len(const uint8_t *base, const MvRec &r, bool with_ns, bool
 
 }  // namespace
 
-__global__ __launch_bounds__(UB_T) void k_ub_block(const uint8_t *__restrict__ base, const MvRec *__restrict__ writes,
-                                                   const MvTxInfo *__restrict__ info, const uint8_t *__restrict__ st,
-                                                   const MvCounters *__restrict__ c, uint32_t rlast,
-                                                   const uint32_t *__restrict__ bfirst, const uint64_t *__restrict__ bnums,
-                                                   uint32_t ntx0, uint64_t num0, uint8_t *__restrict__ out,
-                                                   uint64_t out_cap, unsigned long long *__restrict__ used,
-                                                   UbMeta *__restrict__ meta) {
+__global__ __launch_bounds__(UB_T) void k_ub_sort(const uint8_t *__restrict__ base, const MvRec *__restrict__ writes,
+                                                  const MvTxInfo *__restrict__ info, const uint8_t *__restrict__ st,
+                                                  const MvCounters *__restrict__ c, uint32_t rlast,
+                                                  const uint32_t *__restrict__ bfirst, const uint64_t *__restrict__ bnums,
+                                                  uint32_t ntx0, uint64_t num0, uint64_t out_cap,
+                                                  unsigned long long *__restrict__ used, UbMeta *__restrict__ meta,
+                                                  UbBlk *__restrict__ dmeta, UbEnt *__restrict__ ents) {
   __shared__ uint64_t skey[UB_MAX];
-  __shared__ uint32_t sidx[UB_MAX];  // record index; after the sort's use: the entry's output offset
+  __shared__ uint32_t sidx[UB_MAX];  // record index (skey: the sort key, then the entry's output offset)
   __shared__ uint8_t sgrp[UB_MAX];
   __shared__ uint32_t wsum[UB_T / 64], grep[UB_GROUPS], gfirst[UB_GROUPS];
   __shared__ uint8_t grank[UB_GROUPS], gnewns[UB_GROUPS], gskip[UB_GROUPS];
@@ -136,6 +139,9 @@ __global__ __launch_bounds__(UB_T) void k_ub_block(const uint8_t *__restrict__ b
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t b = blockIdx.x;
   UbMeta *mo = meta + b;
+  UbBlk *dm = dmeta + b;
+  UbEnt *ent = ents + (size_t)b * UB_MAX;
+  if (tid == 0) dm->nent = 0;  // (k_ub_write: nothing of this block unless it finishes below)
   // the fixpoint converged (mvcc.hip converged()): otherwise a later launch of this block decides
   if (c->unsup || !(c->done || c->undec[rlast & 3] == 0)) {
     if (tid == 0) mo->status = UB_NONE;
@@ -352,46 +358,80 @@ __global__ __launch_bounds__(UB_T) void k_ub_block(const uint8_t *__restrict__ b
     if (tid == 0) mo->status = UB_NONE;
     return;
   }
-  // 5. serialise
-  uint8_t *ob = out + sh_off;
+  // the survivors' entries (sorted order) for k_ub_write
+  const uint64_t boff = sh_off;
   for (uint32_t i = tid; i < M; i += UB_T) {
-    if (sgrp[i] == 0xFF) continue;
-    const MvRec &R = writes[sidx[i]];
     const uint32_t g = sgrp[i];
-    const bool first = gfirst[g] == i;
-    const bool wns = first && gnewns[g], wcoll = first && (R.flags & MVR_HASHED);
-    const uint32_t txn = R.tx - t0;
-    const uint32_t vl = opv_len(num) + opv_len(txn);
-    const uint32_t m = kvwrite_len(base, R, wns, wcoll, vl);
-    uint8_t *o = ob + (uint32_t)skey[i];
-    *o++ = (uint8_t)(1 << 3 | 2);
-    o = put_varint(o, m);
-    if (wns && R.ns_len) o = put_span(o, 1, ns_of(base, R));
-    if (wcoll && R.coll_len) o = put_span(o, 2, coll_of(base, R));
-    if (R.key_len) o = put_span(o, 3, key_of(base, R));
-    if (R.flags & MVR_DELETE) {
-      *o++ = 0x20;  // isDelete = true
-      *o++ = 0x01;
-    } else if (R.txn) {
-      o = put_span(o, 5, value_of(base, R));
+    if (g == 0xFF) {
+      ent[i] = UbEnt{0, 0, 0};
+      continue;
     }
-    *o++ = (uint8_t)(6 << 3 | 2);
-    o = put_varint(o, vl);
-    o = put_opv(o, num);
-    put_opv(o, txn);
+    const bool first = gfirst[g] == i;
+    const bool hashed = writes[sidx[i]].flags & MVR_HASHED;
+    ent[i] = UbEnt{sidx[i], (uint32_t)skey[i],
+                   (first && gnewns[g] ? UBE_NS : 0u) | (first && hashed ? UBE_COLL : 0u) | UBE_LIVE};
   }
   if (tid == 0) {
-    mo->off = sh_off;
+    *dm = UbBlk{boff, sh_total, M, t0, num};
+    mo->off = boff;
     mo->len = sh_total;
     mo->status = UB_OK;
-    __threadfence_system();
   }
+}
+
+// one lane per entry: block q of the launch = blockIdx.x / (UB_MAX / 256)
+__global__ __launch_bounds__(256) void k_ub_write(const uint8_t *__restrict__ base, const MvRec *__restrict__ writes,
+                                                  const UbBlk *__restrict__ dmeta, const UbEnt *__restrict__ ents,
+                                                  uint8_t *__restrict__ out) {
+  constexpr uint32_t WPB = UB_MAX / 256;
+  const uint32_t q = blockIdx.x / WPB, i = (blockIdx.x % WPB) * 256 + threadIdx.x;
+  const UbBlk B = dmeta[q];
+  if (i >= B.nent) return;
+  const UbEnt E = ents[(size_t)q * UB_MAX + i];
+  if (!(E.flags & UBE_LIVE)) return;
+  const MvRec &R = writes[E.rec];
+  const bool wns = E.flags & UBE_NS, wcoll = E.flags & UBE_COLL;
+  const uint32_t txn = R.tx - B.t0;
+  const uint32_t vl = opv_len(B.num) + opv_len(txn);
+  const uint32_t m = kvwrite_len(base, R, wns, wcoll, vl);
+  uint8_t *o = out + B.off + E.off;
+  *o++ = (uint8_t)(1 << 3 | 2);
+  o = put_varint(o, m);
+  if (wns && R.ns_len) o = put_span(o, 1, ns_of(base, R));
+  if (wcoll && R.coll_len) o = put_span(o, 2, coll_of(base, R));
+  if (R.key_len) o = put_span(o, 3, key_of(base, R));
+  if (R.flags & MVR_DELETE) {
+    *o++ = 0x20;  // isDelete = true
+    *o++ = 0x01;
+  } else if (R.txn) {
+    o = put_span(o, 5, value_of(base, R));
+  }
+  *o++ = (uint8_t)(6 << 3 | 2);
+  o = put_varint(o, vl);
+  o = put_opv(o, B.num);
+  put_opv(o, txn);
+}
+
+// the arena [0, used) to pinned host memory (16-byte loads and stores; the arena and the host
+// buffer are 16-byte aligned, the tail rounded up inside their capacity)
+__global__ __launch_bounds__(256) void k_ub_copy(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                 const unsigned long long *__restrict__ used, uint64_t cap) {
+  const uint64_t u = *used;  // (claims past the capacity failed their blocks: never copied)
+  const uint64_t n16 = ((u < cap ? u : cap) + 15) / 16;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) dst[i] = src[i];
+  __threadfence_system();
 }
 
 void ub_block_launch(hipStream_t s, uint32_t nb, const uint8_t *base, const MvRec *writes, const MvTxInfo *info,
                      const uint8_t *st, const MvCounters *c, uint32_t rlast, const uint32_t *bfirst,
                      const uint64_t *bnums, uint32_t ntx0, uint64_t num0, uint8_t *out, uint64_t out_cap,
-                     unsigned long long *used, UbMeta *meta) {
-  hipLaunchKernelGGL(k_ub_block, dim3(nb), dim3(UB_T), 0, s, base, writes, info, st, c, rlast, bfirst, bnums, ntx0,
-                     num0, out, out_cap, used, meta);
+                     unsigned long long *used, UbMeta *meta, UbBlk *dmeta, UbEnt *ents) {
+  hipLaunchKernelGGL(k_ub_sort, dim3(nb), dim3(UB_T), 0, s, base, writes, info, st, c, rlast, bfirst, bnums, ntx0,
+                     num0, out_cap, used, meta, dmeta, ents);
+  hipLaunchKernelGGL(k_ub_write, dim3(nb * (UB_MAX / 256)), dim3(256), 0, s, base, writes, dmeta, ents, out);
+}
+void ub_copy_launch(hipStream_t s, const uint8_t *arena, uint8_t *host_dev, const unsigned long long *used,
+                    uint64_t cap) {
+  hipLaunchKernelGGL(k_ub_copy, dim3(512), dim3(256), 0, s, reinterpret_cast<const uint4 *>(arena),
+                     reinterpret_cast<uint4 *>(host_dev), used, cap);
 }

@@ -151,10 +151,12 @@ for step in "$@"; do
         || { echo pcietrace2 failed; tail -20 $O/pcie2.err; exit 1; }
       grep "steps ms\|slowest" $O/pcie2.err | tail -2
       python3 tools/copy_trace.py $O/pcie2 > $O/pcie2_summary.txt 2>&1; tail -28 $O/pcie2_summary.txt ;;
-    pciesteps)
-      # unprofiled PCIe passes at 12 / 20 / 40 timed steps with per-step host timings (BENCH_STEPLOG)
+    pciesteps*)
+      # unprofiled PCIe passes at 12 / 20 / 40 timed steps with per-step host timings (BENCH_STEPLOG);
+      # pciesteps<W>: W warmup steps (default 3)
+      w=${step#pciesteps}; w=${w:-3}
       for k in 12 20 40; do
-        BENCH_STEPLOG=1 timeout -k 10 300 python -u bench.py --steps $k --warmup 3 --cpu-threads 0 --no-latency > $O/pcies_$k.json 2> $O/pcies_$k.err \
+        BENCH_STEPLOG=1 timeout -k 10 300 python -u bench.py --steps $k --warmup $w --cpu-threads 0 --no-latency > $O/pcies_$k.json 2> $O/pcies_$k.err \
           || { echo pciesteps failed; tail -20 $O/pcies_$k.err; exit 1; }
         python3 -c "import json; d=json.load(open('$O/pcies_$k.json')); p=d['pcie_inclusive']; print('pcie steps $k', d['ms_per_step'], p['ms_per_step'])"
         grep "steps ms\|slowest\|median step" $O/pcies_$k.err | tail -3
