@@ -267,8 +267,6 @@ void ub_block_launch(hipStream_t s, uint32_t nb, const uint8_t *base, const MvRe
                      const uint8_t *st, const MvCounters *c, uint32_t rlast, const uint32_t *bfirst,
                      const uint64_t *bnums, uint32_t ntx0, uint64_t num0, uint8_t *out, uint64_t out_cap,
                      unsigned long long *used, UbMeta *meta, UbBlk *dmeta, UbEnt *ents);
-void ub_copy_launch(hipStream_t s, const uint8_t *arena, uint8_t *host_dev, const unsigned long long *used,
-                    uint64_t cap);
 struct MvRange {  // a range query's scan bounds (bytes in a host-built buffer)
   uint32_t ns_off, ns_len, s_off, s_len, e_off, e_len, flags, pad;
 };

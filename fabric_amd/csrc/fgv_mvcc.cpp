@@ -94,7 +94,8 @@ struct fgv_mvcc_state {
   struct UbGen {
     DevBuf arena, used;      // the serialisation arena and its claim counter
     HostBuf meta;            // UbMeta per block of the call (pinned, written by k_ub_sort)
-    HostBuf host;            // the arena, copied back by k_ub_copy after the call
+    HostBuf host;            // the arena, copied back after the call
+    HostBuf usedh;           // the claim counter, read back at the call's end
     hipEvent_t ev = nullptr; // that copy is done
     uint64_t ticket = 0;     // the call (0: none)
     uint64_t cap = 0;
@@ -129,6 +130,7 @@ void fgv_mvcc_free(fgv_mvcc_state *M) {
     G.used.release();
     G.meta.release();
     G.host.release();
+    G.usedh.release();
     if (G.ev) hipEventDestroy(G.ev);
   }
   M->ub_dmeta.release();
@@ -1119,7 +1121,7 @@ static bool mvcc_spin() {
 // for that generation's readers (fgv_mvcc_update_bytes_acquire of the call two back).  Every
 // device path of the call launches k_ub_sort + k_ub_write behind its flags (meta entry = the
 // block's index in the call): the batch pass on ub_stream, beside its commit kernels (the call
-// does not wait for them), the chain and the single-block path in line.  After the call k_ub_copy
+// does not wait for them), the chain and the single-block path in line.  After the call one copy
 // brings the arena back on ub_stream; the ticket names the call, and acquire waits for the copy.
 // Every MVCC call first fences its stream behind ub_stream (the serialisation reads the records,
 // codes and counters the next call overwrites).
@@ -1143,7 +1145,8 @@ static int ub_begin(fgv_ctx *c, fgv_mvcc_state *M, size_t nb, const size_t *lens
   uint64_t cap = 1 << 20;
   for (size_t k = 0; k < nb; k++) cap += lens[k] + lens[k] / 4;
   cap = (cap + 15) & ~(uint64_t)15;
-  if (!G.arena.ensure(cap) || !G.used.ensure(64) || !G.meta.ensure(nb * sizeof(UbMeta)) || !G.host.ensure(cap) ||
+  if (!G.arena.ensure(cap) || !G.used.ensure(64) || !G.usedh.ensure(64) || !G.meta.ensure(nb * sizeof(UbMeta)) ||
+      !G.host.ensure(cap) ||
       !M->ub_dmeta.ensure(nb * sizeof(UbBlk)) || !M->ub_ents.ensure(nb * (size_t)UB_MAX * sizeof(UbEnt)))
     return FGV_ENOMEM;
   G.cap = cap;
@@ -1153,6 +1156,7 @@ static int ub_begin(fgv_ctx *c, fgv_mvcc_state *M, size_t nb, const size_t *lens
   if (!M->ub_in) HIP_TRY(hipEventCreateWithFlags(&M->ub_in, hipEventDisableTiming));
   if (!M->ub_tail) HIP_TRY(hipEventCreateWithFlags(&M->ub_tail, hipEventDisableTiming));
   if (!M->ub_stream) HIP_TRY(hipStreamCreateWithFlags(&M->ub_stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamWaitEvent(c->stream, G.ev, 0));  // (the copy back of two calls ago read this arena)
   HIP_TRY(hipMemsetAsync(G.used.p, 0, 8, c->stream));
   G.nb = nb;
   M->ub_cur = gi;
@@ -1181,22 +1185,24 @@ static void ub_launch(hipStream_t s, bool side, fgv_mvcc_state *M, size_t idx, u
     M->ub_tail_set = true;
   }
 }
-// after the call's last synchronisation: the arena back to the host on ub_stream (no host wait)
+// after the call's last synchronisation: the bytes back to the host on ub_stream, one copy of
+// exactly the claimed arena (the copy engine: no CU time beside the next call's kernels)
 static void ub_end(fgv_ctx *c, fgv_mvcc_state *M, bool ok) {
   const int gi = M->ub_cur;
   M->ub_cur = -1;
   if (gi < 0) return;
   auto &G = M->ub[gi];
-  uint8_t *hd = nullptr;
-  if (ok && hipHostGetDevicePointer(reinterpret_cast<void **>(&hd), G.host.p, 0) != hipSuccess) ok = false;
   // (the in-line launches finished with the call's own synchronisation; the side ones are ahead
-  // on ub_stream)
+  // on ub_stream and, started at the batch's flags, usually done by now)
+  uint64_t total = 0;
   if (ok) {
-    ub_copy_launch(M->ub_stream, G.arena.as<uint8_t>(), hd, G.used.as<unsigned long long>(), G.cap);
-    ok = hipGetLastError() == hipSuccess && hipEventRecord(G.ev, M->ub_stream) == hipSuccess &&
-         hipEventRecord(M->ub_tail, M->ub_stream) == hipSuccess;
-    if (ok) M->ub_tail_set = true;
+    ok = hipMemcpyAsync(G.usedh.p, G.used.p, 8, hipMemcpyDeviceToHost, M->ub_stream) == hipSuccess &&
+         hipStreamSynchronize(M->ub_stream) == hipSuccess;
+    if (ok) total = std::min<uint64_t>(*G.usedh.as<uint64_t>(), G.cap);
   }
+  if (ok && total)
+    ok = hipMemcpyAsync(G.host.p, G.arena.p, total, hipMemcpyDeviceToHost, M->ub_stream) == hipSuccess;
+  if (ok) ok = hipEventRecord(G.ev, M->ub_stream) == hipSuccess;
   (void)c;
   std::lock_guard<std::mutex> lk(M->ub_mu);
   if (!ok) return;  // (ticket stays 0: the caller decodes every block on the host)

@@ -23,8 +23,6 @@
 //      survivors' (record, offset, fields) go to the entry list.
 // k_ub_write: one lane per listed entry over the whole chip (the byte framing of ~30 B plus the
 // key and value per write: the serialisation's bulk, spread over every CU instead of one per block).
-// k_ub_copy: the call's arena to pinned host memory, 16-byte stores (sizes read on the device, so
-// the host never waits for them).
 // A block that does not fit (more than UB_MAX valid writes, more than UB_GROUPS groups, the arena
 // full) reports status UB_NONE: the host decodes that block instead (fgv_commit.cpp).
 #include "fgv_kernels.h"
@@ -136,6 +134,7 @@ __global__ __launch_bounds__(UB_T) void k_ub_sort(const uint8_t *__restrict__ ba
   __shared__ uint8_t grank[UB_GROUPS], gnewns[UB_GROUPS], gskip[UB_GROUPS];
   __shared__ uint32_t sh_m, sh_lead, sh_ng, sh_bad, sh_lcp, sh_total;
   __shared__ unsigned long long sh_off;
+  __builtin_amdgcn_s_setprio(0);  // (beside the commit and the next call's kernels: off their chains)
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t b = blockIdx.x;
   UbMeta *mo = meta + b;
@@ -383,6 +382,7 @@ __global__ __launch_bounds__(UB_T) void k_ub_sort(const uint8_t *__restrict__ ba
 __global__ __launch_bounds__(256) void k_ub_write(const uint8_t *__restrict__ base, const MvRec *__restrict__ writes,
                                                   const UbBlk *__restrict__ dmeta, const UbEnt *__restrict__ ents,
                                                   uint8_t *__restrict__ out) {
+  __builtin_amdgcn_s_setprio(0);
   constexpr uint32_t WPB = UB_MAX / 256;
   const uint32_t q = blockIdx.x / WPB, i = (blockIdx.x % WPB) * 256 + threadIdx.x;
   const UbBlk B = dmeta[q];
@@ -412,16 +412,6 @@ __global__ __launch_bounds__(256) void k_ub_write(const uint8_t *__restrict__ ba
   put_opv(o, txn);
 }
 
-// the arena [0, used) to pinned host memory (16-byte loads and stores; the arena and the host
-// buffer are 16-byte aligned, the tail rounded up inside their capacity)
-__global__ __launch_bounds__(256) void k_ub_copy(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
-                                                 const unsigned long long *__restrict__ used, uint64_t cap) {
-  const uint64_t u = *used;  // (claims past the capacity failed their blocks: never copied)
-  const uint64_t n16 = ((u < cap ? u : cap) + 15) / 16;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) dst[i] = src[i];
-  __threadfence_system();
-}
-
 void ub_block_launch(hipStream_t s, uint32_t nb, const uint8_t *base, const MvRec *writes, const MvTxInfo *info,
                      const uint8_t *st, const MvCounters *c, uint32_t rlast, const uint32_t *bfirst,
                      const uint64_t *bnums, uint32_t ntx0, uint64_t num0, uint8_t *out, uint64_t out_cap,
@@ -429,9 +419,4 @@ void ub_block_launch(hipStream_t s, uint32_t nb, const uint8_t *base, const MvRe
   hipLaunchKernelGGL(k_ub_sort, dim3(nb), dim3(UB_T), 0, s, base, writes, info, st, c, rlast, bfirst, bnums, ntx0,
                      num0, out_cap, used, meta, dmeta, ents);
   hipLaunchKernelGGL(k_ub_write, dim3(nb * (UB_MAX / 256)), dim3(256), 0, s, base, writes, dmeta, ents, out);
-}
-void ub_copy_launch(hipStream_t s, const uint8_t *arena, uint8_t *host_dev, const unsigned long long *used,
-                    uint64_t cap) {
-  hipLaunchKernelGGL(k_ub_copy, dim3(512), dim3(256), 0, s, reinterpret_cast<const uint4 *>(arena),
-                     reinterpret_cast<uint4 *>(host_dev), used, cap);
 }
