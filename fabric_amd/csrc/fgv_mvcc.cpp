@@ -94,9 +94,10 @@ struct fgv_mvcc_state {
   struct UbGen {
     DevBuf arena, used;      // the serialisation arena and its claim counter
     HostBuf meta;            // UbMeta per block of the call (pinned, written by k_ub_sort)
-    HostBuf host;            // the arena, copied back after the call
-    HostBuf usedh;           // the claim counter, read back at the call's end
-    hipEvent_t ev = nullptr; // that copy is done
+    HostBuf host;            // the arena, copied back by the first acquire
+    HostBuf usedh;           // the claim counter, read back with it
+    hipEvent_t kev = nullptr, cev = nullptr;  // the call's serialisation / a copy back is done
+    bool copied = false;
     uint64_t ticket = 0;     // the call (0: none)
     uint64_t cap = 0;
     size_t nb = 0;
@@ -108,7 +109,9 @@ struct fgv_mvcc_state {
   uint64_t ub_calls = 0, ub_last = 0;
   std::mutex ub_mu;
   std::condition_variable ub_cv;
-  hipStream_t ub_stream = nullptr;    // the batch pass's serialisation and every call's copy back
+  hipStream_t ub_stream = nullptr;    // the batch pass's serialisation
+  hipStream_t ub_cp = nullptr;        // the copies back (fgv_mvcc_update_bytes_acquire)
+  std::mutex ub_cp_mu;
   hipEvent_t ub_in = nullptr, ub_tail = nullptr;  // (into / the last work queued on ub_stream)
   bool ub_tail_set = false, ub_side = false;
 };
@@ -125,19 +128,22 @@ void fgv_mvcc_free(fgv_mvcc_state *M) {
   HostBuf *h[] = {&M->hhead, &M->htail, &M->bhead, &M->btail, &M->mbhead, &M->mbtail};
   for (auto *b : h) b->release();
   if (M->ub_stream) hipStreamSynchronize(M->ub_stream);
+  if (M->ub_cp) hipStreamSynchronize(M->ub_cp);
   for (auto &G : M->ub) {
     G.arena.release();
     G.used.release();
     G.meta.release();
     G.host.release();
     G.usedh.release();
-    if (G.ev) hipEventDestroy(G.ev);
+    if (G.kev) hipEventDestroy(G.kev);
+    if (G.cev) hipEventDestroy(G.cev);
   }
   M->ub_dmeta.release();
   M->ub_ents.release();
   if (M->ub_in) hipEventDestroy(M->ub_in);
   if (M->ub_tail) hipEventDestroy(M->ub_tail);
   if (M->ub_stream) hipStreamDestroy(M->ub_stream);
+  if (M->ub_cp) hipStreamDestroy(M->ub_cp);
   delete M;
 }
 
@@ -1152,12 +1158,15 @@ static int ub_begin(fgv_ctx *c, fgv_mvcc_state *M, size_t nb, const size_t *lens
   G.cap = cap;
   UbMeta *m = G.meta.as<UbMeta>();
   for (size_t k = 0; k < nb; k++) m[k] = UbMeta{0, 0, UB_NONE};
-  if (!G.ev) HIP_TRY(hipEventCreateWithFlags(&G.ev, hipEventDisableTiming));
+  if (!G.kev) HIP_TRY(hipEventCreateWithFlags(&G.kev, hipEventDisableTiming));
+  if (!G.cev) HIP_TRY(hipEventCreateWithFlags(&G.cev, hipEventDisableTiming));
   if (!M->ub_in) HIP_TRY(hipEventCreateWithFlags(&M->ub_in, hipEventDisableTiming));
   if (!M->ub_tail) HIP_TRY(hipEventCreateWithFlags(&M->ub_tail, hipEventDisableTiming));
   if (!M->ub_stream) HIP_TRY(hipStreamCreateWithFlags(&M->ub_stream, hipStreamNonBlocking));
-  HIP_TRY(hipStreamWaitEvent(c->stream, G.ev, 0));  // (the copy back of two calls ago read this arena)
+  if (!M->ub_cp) HIP_TRY(hipStreamCreateWithFlags(&M->ub_cp, hipStreamNonBlocking));
+  // (a copy back of this generation's arena ran inside an acquire that has been released)
   HIP_TRY(hipMemsetAsync(G.used.p, 0, 8, c->stream));
+  G.copied = false;
   G.nb = nb;
   M->ub_cur = gi;
   return FGV_OK;
@@ -1185,29 +1194,37 @@ static void ub_launch(hipStream_t s, bool side, fgv_mvcc_state *M, size_t idx, u
     M->ub_tail_set = true;
   }
 }
-// after the call's last synchronisation: the bytes back to the host on ub_stream, one copy of
-// exactly the claimed arena (the copy engine: no CU time beside the next call's kernels)
+// after the call's last synchronisation: the call's serialisation is named by an event (the side
+// launch on ub_stream may still run; the in-line ones are done) and a ticket.  Nothing waits here:
+// the first fgv_mvcc_update_bytes_acquire of the ticket copies the claimed arena back (the copy
+// engine, exactly the claimed bytes), so the host thread that hashes pays for it, not this call.
 static void ub_end(fgv_ctx *c, fgv_mvcc_state *M, bool ok) {
   const int gi = M->ub_cur;
   M->ub_cur = -1;
   if (gi < 0) return;
   auto &G = M->ub[gi];
-  // (the in-line launches finished with the call's own synchronisation; the side ones are ahead
-  // on ub_stream and, started at the batch's flags, usually done by now)
-  uint64_t total = 0;
-  if (ok) {
-    ok = hipMemcpyAsync(G.usedh.p, G.used.p, 8, hipMemcpyDeviceToHost, M->ub_stream) == hipSuccess &&
-         hipStreamSynchronize(M->ub_stream) == hipSuccess;
-    if (ok) total = std::min<uint64_t>(*G.usedh.as<uint64_t>(), G.cap);
-  }
-  if (ok && total)
-    ok = hipMemcpyAsync(G.host.p, G.arena.p, total, hipMemcpyDeviceToHost, M->ub_stream) == hipSuccess;
-  if (ok) ok = hipEventRecord(G.ev, M->ub_stream) == hipSuccess;
-  (void)c;
+  if (ok) ok = hipEventRecord(G.kev, M->ub_side ? M->ub_stream : c->stream) == hipSuccess;
   std::lock_guard<std::mutex> lk(M->ub_mu);
   if (!ok) return;  // (ticket stays 0: the caller decodes every block on the host)
   G.ticket = ++M->ub_calls;
   M->ub_last = G.ticket;
+}
+// the claimed arena of generation G back to its host buffer (once per call)
+static int ub_copy_back(fgv_mvcc_state *M, fgv_mvcc_state::UbGen &G) {
+  std::lock_guard<std::mutex> lk(M->ub_cp_mu);
+  if (G.copied) return FGV_OK;
+  HIP_TRY(hipStreamWaitEvent(M->ub_cp, G.kev, 0));
+  HIP_TRY(hipMemcpyAsync(G.usedh.p, G.used.p, 8, hipMemcpyDeviceToHost, M->ub_cp));
+  HIP_TRY(hipEventRecord(G.cev, M->ub_cp));
+  HIP_TRY(hipEventSynchronize(G.cev));
+  const uint64_t total = std::min<uint64_t>(*G.usedh.as<uint64_t>(), G.cap);
+  if (total) {
+    HIP_TRY(hipMemcpyAsync(G.host.p, G.arena.p, total, hipMemcpyDeviceToHost, M->ub_cp));
+    HIP_TRY(hipEventRecord(G.cev, M->ub_cp));
+    HIP_TRY(hipEventSynchronize(G.cev));
+  }
+  G.copied = true;
+  return FGV_OK;
 }
 
 static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, const uint8_t *d_block,
@@ -2116,9 +2133,10 @@ int fgv_mvcc_update_bytes_acquire(fgv_ctx *c, uint64_t ticket, size_t n, const u
     G->readers++;
   }
   hipSetDevice(c->device);
-  if (hipEventSynchronize(G->ev) != hipSuccess) {
+  const int rc = ub_copy_back(M, *G);
+  if (rc) {
     fgv_mvcc_update_bytes_release(c, ticket);
-    return FGV_EDEVICE;
+    return rc;
   }
   const UbMeta *m = G->meta.as<UbMeta>();
   for (size_t b = 0; b < n; b++) {

@@ -21,7 +21,7 @@
 //      by a bitonic network over up to UB_MAX entries, ties by the full key, then by transaction;
 //   4. the last entry of each key's run survives; sizes, a block-wide scan, one arena claim; the
 //      survivors' (record, offset, fields) go to the entry list.
-// k_ub_write: one lane per listed entry over the whole chip (the byte framing of ~30 B plus the
+// k_ub_write: one wave per listed entry over the whole chip (the byte framing of ~30 B plus the
 // key and value per write: the serialisation's bulk, spread over every CU instead of one per block).
 // A block that does not fit (more than UB_MAX valid writes, more than UB_GROUPS groups, the arena
 // full) reports status UB_NONE: the host decodes that block instead (fgv_commit.cpp).
@@ -71,40 +71,6 @@ DEV uint32_t opv_len(uint64_t n) {  // EncodeOrderPreservingVarUint64 (common/le
   uint32_t k = 0;
   while (k < 8 && (n >> (56 - 8 * k) & 0xFF) == 0) k++;
   return 1u + (8u - k);
-}
-DEV uint8_t *put_varint(uint8_t *o, uint64_t v) {
-  while (v >= 0x80) {
-    *o++ = (uint8_t)(v | 0x80);
-    v >>= 7;
-  }
-  *o++ = (uint8_t)v;
-  return o;
-}
-DEV uint8_t *put_span(uint8_t *o, uint32_t field, S s) {
-  *o++ = (uint8_t)(field << 3 | 2);
-  o = put_varint(o, s.n);
-  uint32_t i = 0;
-  for (; i + 4 <= s.n; i += 4) {
-    const uint32_t w = ld4(s.p + i);
-    o[0] = (uint8_t)w;
-    o[1] = (uint8_t)(w >> 8);
-    o[2] = (uint8_t)(w >> 16);
-    o[3] = (uint8_t)(w >> 24);
-    o += 4;
-  }
-  for (; i < s.n; i++) *o++ = s.p[i];
-  return o;
-}
-DEV uint8_t *put_opv(uint8_t *o, uint64_t n) {
-  uint32_t k = 0;
-  while (k < 8 && (n >> (56 - 8 * k) & 0xFF) == 0) k++;
-  *o++ = (uint8_t)(8 - k);
-  for (; k < 8; k++) *o++ = (uint8_t)(n >> (56 - 8 * k));
-  return o;
-}
-// the value a write records: a put's value (public) or value hash (hashed); deletes carry none
-DEV S value_of(const uint8_t *base, const MvRec &r) {
-  return (r.flags & MVR_DELETE) ? S{base, 0} : S{base + r.blk, (uint32_t)r.txn};
 }
 // KVWrite message length (field 1's payload) of entry r with the namespace / collection fields
 // present or not
@@ -378,38 +344,79 @@ __global__ __launch_bounds__(UB_T) void k_ub_sort(const uint8_t *__restrict__ ba
   }
 }
 
-// one lane per entry: block q of the launch = blockIdx.x / (UB_MAX / 256)
+// One wave per entry: its ~230 bytes written 64 contiguous bytes per store instruction (a lane per
+// byte position), the key and value read the same way -- one cache line per wave-wide access
+// instead of 64 scattered ones.  The entry's bytes are segments: literal tag / length bytes (at
+// most 6 each), the namespace, collection, key and value copied from the block, and the version
+// field (tag, length, EncodeOrderPreservingVarUint64 of the block number and of the tx index).
+DEV uint32_t lit_put(uint64_t &w, uint32_t tag, uint32_t n) {  // tag || varint(n) into w -> length
+  w = tag;
+  uint32_t k = 1;
+  while (n >= 0x80) {
+    w |= (uint64_t)((n & 0x7F) | 0x80) << (8 * k++);
+    n >>= 7;
+  }
+  w |= (uint64_t)n << (8 * k++);
+  return k;
+}
+DEV uint32_t opv_byte(uint64_t n, uint32_t len, uint32_t q) {  // byte q of opv(n) (len = opv_len(n))
+  return q == 0 ? len - 1 : (uint32_t)(n >> (8 * (len - 1 - q))) & 0xFF;
+}
+// waves of the launch: block q of the launch takes UB_WAVES waves, wave j of them entries j, j + UB_WAVES, ...
+#define UB_WAVES 256u
 __global__ __launch_bounds__(256) void k_ub_write(const uint8_t *__restrict__ base, const MvRec *__restrict__ writes,
                                                   const UbBlk *__restrict__ dmeta, const UbEnt *__restrict__ ents,
                                                   uint8_t *__restrict__ out) {
   __builtin_amdgcn_s_setprio(0);
-  constexpr uint32_t WPB = UB_MAX / 256;
-  const uint32_t q = blockIdx.x / WPB, i = (blockIdx.x % WPB) * 256 + threadIdx.x;
+  constexpr uint32_t WG_PER_BLOCK = UB_WAVES / 4;
+  const uint32_t q = blockIdx.x / WG_PER_BLOCK;
+  const uint32_t w0 = (blockIdx.x % WG_PER_BLOCK) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   const UbBlk B = dmeta[q];
-  if (i >= B.nent) return;
-  const UbEnt E = ents[(size_t)q * UB_MAX + i];
-  if (!(E.flags & UBE_LIVE)) return;
-  const MvRec &R = writes[E.rec];
-  const bool wns = E.flags & UBE_NS, wcoll = E.flags & UBE_COLL;
-  const uint32_t txn = R.tx - B.t0;
-  const uint32_t vl = opv_len(B.num) + opv_len(txn);
-  const uint32_t m = kvwrite_len(base, R, wns, wcoll, vl);
-  uint8_t *o = out + B.off + E.off;
-  *o++ = (uint8_t)(1 << 3 | 2);
-  o = put_varint(o, m);
-  if (wns && R.ns_len) o = put_span(o, 1, ns_of(base, R));
-  if (wcoll && R.coll_len) o = put_span(o, 2, coll_of(base, R));
-  if (R.key_len) o = put_span(o, 3, key_of(base, R));
-  if (R.flags & MVR_DELETE) {
-    *o++ = 0x20;  // isDelete = true
-    *o++ = 0x01;
-  } else if (R.txn) {
-    o = put_span(o, 5, value_of(base, R));
+  const uint32_t lnum = opv_len(B.num);
+  for (uint32_t i = w0; i < B.nent; i += UB_WAVES) {
+    const UbEnt E = ents[(size_t)q * UB_MAX + i];
+    if (!(E.flags & UBE_LIVE)) continue;
+    const MvRec R = writes[E.rec];
+    const bool wns = (E.flags & UBE_NS) && R.ns_len, wcoll = (E.flags & UBE_COLL) && R.coll_len;
+    const uint32_t txn = R.tx - B.t0, ltx = opv_len(txn), vl = lnum + ltx;
+    const bool del = R.flags & MVR_DELETE, val = !del && R.txn;
+    const uint32_t m = kvwrite_len(base, R, wns, wcoll, vl);
+    // segments in order: L0 [L1 C1] [L2 C2] [L3 C3] (L4 | L4 C4) V
+    uint64_t l0, l1 = 0, l2 = 0, l3 = 0, l4 = 0;
+    const uint32_t n0 = lit_put(l0, 0x0A, m);
+    const uint32_t n1 = wns ? lit_put(l1, 0x0A, R.ns_len) : 0, c1 = wns ? R.ns_len : 0;
+    const uint32_t n2 = wcoll ? lit_put(l2, 0x12, R.coll_len) : 0, c2 = wcoll ? R.coll_len : 0;
+    const uint32_t n3 = R.key_len ? lit_put(l3, 0x1A, R.key_len) : 0, c3 = R.key_len;
+    uint32_t n4 = 0, c4 = 0;
+    if (del) {
+      l4 = 0x0120;  // is_delete = true
+      n4 = 2;
+    } else if (val) {
+      n4 = lit_put(l4, 0x2A, (uint32_t)R.txn);
+      c4 = (uint32_t)R.txn;
+    }
+    const uint32_t s1 = n0, s1c = s1 + n1, s2 = s1c + c1, s2c = s2 + n2, s3 = s2c + c2, s3c = s3 + n3;
+    const uint32_t s4 = s3c + c3, s4c = s4 + n4, s5 = s4c + c4, sz = s5 + 2 + vl;
+    const uint8_t *pns = base + R.ns_off, *pcoll = base + R.coll_off, *pkey = base + R.key_off, *pval = base + R.blk;
+    uint8_t *o = out + B.off + E.off;
+    for (uint32_t p = lane; p < sz; p += 64) {
+      uint32_t v;
+      if (p < s1) v = (uint32_t)(l0 >> (8 * p));
+      else if (p < s1c) v = (uint32_t)(l1 >> (8 * (p - s1)));
+      else if (p < s2) v = pns[p - s1c];
+      else if (p < s2c) v = (uint32_t)(l2 >> (8 * (p - s2)));
+      else if (p < s3) v = pcoll[p - s2c];
+      else if (p < s3c) v = (uint32_t)(l3 >> (8 * (p - s3)));
+      else if (p < s4) v = pkey[p - s3c];
+      else if (p < s4c) v = (uint32_t)(l4 >> (8 * (p - s4)));
+      else if (p < s5) v = pval[p - s4c];
+      else {
+        const uint32_t r = p - s5;  // version field: 0x32, vl, opv(num), opv(txn)
+        v = r == 0 ? 0x32u : r == 1 ? vl : r - 2 < lnum ? opv_byte(B.num, lnum, r - 2) : opv_byte(txn, ltx, r - 2 - lnum);
+      }
+      o[p] = (uint8_t)v;
+    }
   }
-  *o++ = (uint8_t)(6 << 3 | 2);
-  o = put_varint(o, vl);
-  o = put_opv(o, B.num);
-  put_opv(o, txn);
 }
 
 void ub_block_launch(hipStream_t s, uint32_t nb, const uint8_t *base, const MvRec *writes, const MvTxInfo *info,
@@ -418,5 +425,5 @@ void ub_block_launch(hipStream_t s, uint32_t nb, const uint8_t *base, const MvRe
                      unsigned long long *used, UbMeta *meta, UbBlk *dmeta, UbEnt *ents) {
   hipLaunchKernelGGL(k_ub_sort, dim3(nb), dim3(UB_T), 0, s, base, writes, info, st, c, rlast, bfirst, bnums, ntx0,
                      num0, out_cap, used, meta, dmeta, ents);
-  hipLaunchKernelGGL(k_ub_write, dim3(nb * (UB_MAX / 256)), dim3(256), 0, s, base, writes, dmeta, ents, out);
+  hipLaunchKernelGGL(k_ub_write, dim3(nb * (UB_WAVES / 4)), dim3(256), 0, s, base, writes, dmeta, ents, out);
 }

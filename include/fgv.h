@@ -700,10 +700,11 @@ int fgv_commit_hashes(size_t n, const uint8_t *const *blocks, const size_t *lens
 /* The update-batch bytes on the device (round 6).  With fgv_mvcc_set_update_bytes(ctx, 1), every
  * committing fgv_mvcc_validate_block[s][_next] call also serialises each committed block's
  * updateBatchBytes on the GPU from its MVCC write records (fabric_amd/csrc/mvcc_ub.hip: the valid
- * writes gathered, grouped, sorted and framed as txmgr.Updates, update_batch_bytes.go:29-105) and
- * copies them back on a stream of their own after the call, so only the serial SHA-256 stays on
- * the host.  fgv_mvcc_last_ticket names the last such call; fgv_mvcc_update_bytes_acquire(ticket)
- * waits for its copy and gives block b's bytes (bytes[b] = NULL: not produced on the device -- a
+ * writes gathered, grouped, sorted and framed as txmgr.Updates, update_batch_bytes.go:29-105), so
+ * only the serial SHA-256 stays on the host; the MVCC call itself does not wait for them.
+ * fgv_mvcc_last_ticket names the last such call; fgv_mvcc_update_bytes_acquire(ticket) (from any
+ * thread: the peer's hashing goroutine) waits for them, copies them back on the first acquire of
+ * the ticket, and gives block b's bytes (bytes[b] = NULL: not produced on the device -- a
  * block on the host phantom path, more than 8,192 valid writes, ...); they stay valid until
  * fgv_mvcc_update_bytes_release(ticket).  Two calls are kept: the second committing call after
  * `ticket` waits for its release.  Only blocks [0, n_done) of a call are committed.
