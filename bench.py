@@ -578,6 +578,10 @@ def run_block(args, world, rank, local, dev_fn):
         for key, v in eng.kernel_times()[0].items():
             kdiag[key] += v / NB
     eng.set_timing(False)
+    # per-rank timing (the multi-rank rehearsal compares each rank's own device time with N=1's)
+    log(f"[bench] rank {rank}/{world}: {el / args.steps * 1e3:.3f} ms per step, device batch "
+        f"{kern.get('batch', 0.0) / max(1, args.steps):.3f} ms (first kernel to last), "
+        f"{B * T} tx per rank-step")
     tot = torch.tensor([el, acc["verifies"], 1.0 if mism == 0 else 0.0], dtype=torch.float64, device=dev)
     if world > 1:
         mx = tot.clone()

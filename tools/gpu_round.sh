@@ -151,6 +151,17 @@ for step in "$@"; do
         || { echo pcietrace2 failed; tail -20 $O/pcie2.err; exit 1; }
       grep "steps ms\|slowest" $O/pcie2.err | tail -2
       python3 tools/copy_trace.py $O/pcie2 > $O/pcie2_summary.txt 2>&1; tail -28 $O/pcie2_summary.txt ;;
+    rehearse2)
+      # two ranks of the shard protocol on the one GPU (gloo between them; the driver runs the real
+      # N=2..8 over RCCL): per-rank step and device time against N=1 through the same protocol
+      timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --cpu-threads 0 --no-latency --no-pcie --shard-protocol \
+        > $O/n1_shard.json 2> $O/n1_shard.err || { echo rehearse2 n1 failed; tail -20 $O/n1_shard.err; exit 1; }
+      FGV_BENCH_SAME_DEVICE=1 FGV_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 \
+        --cpu-threads 0 --no-latency --no-pcie > $O/n2_same.json 2> $O/n2_same.err \
+        || { echo rehearse2 n2 failed; tail -20 $O/n2_same.err; exit 1; }
+      grep "ms per step, device batch" $O/n1_shard.err $O/n2_same.err
+      show $O/n2_same.json n2 value ms_per_step parity_vs_labels ;;
     pciesteps*)
       # unprofiled PCIe passes at 12 / 20 / 40 timed steps with per-step host timings (BENCH_STEPLOG);
       # pciesteps<W>: W warmup steps (default 3)
