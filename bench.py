@@ -579,9 +579,10 @@ def run_block(args, world, rank, local, dev_fn):
             kdiag[key] += v / NB
     eng.set_timing(False)
     # per-rank timing (the multi-rank rehearsal compares each rank's own device time with N=1's)
-    log(f"[bench] rank {rank}/{world}: {el / args.steps * 1e3:.3f} ms per step, device batch "
-        f"{kern.get('batch', 0.0) / max(1, args.steps):.3f} ms (first kernel to last), "
-        f"{B * T} tx per rank-step")
+    print(f"[bench] rank {rank}/{world}: {el / args.steps * 1e3:.3f} ms per step, device batch "
+          f"{kern.get('batch', 0.0) / max(1, args.steps):.3f} ms (first kernel to last), device pass "
+          f"{host['device_ms'] / max(1, args.steps):.3f} ms (host wall of the device work), "
+          f"{B * T} tx per rank-step", file=sys.stderr, flush=True)
     tot = torch.tensor([el, acc["verifies"], 1.0 if mism == 0 else 0.0], dtype=torch.float64, device=dev)
     if world > 1:
         mx = tot.clone()
