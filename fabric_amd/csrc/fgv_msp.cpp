@@ -600,6 +600,7 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
     g.info.hash_family = m.sha3 ? FGV_HASH_SHA3 : FGV_HASH_SHA2;
     g.info.key_type = p.c.key == fgvx::XK_P256 ? FGV_KEY_P256 : p.c.key == fgvx::XK_P384 ? FGV_KEY_P384 : FGV_KEY_OTHER;
     if (g.info.key_type == FGV_KEY_P256) memcpy(g.info.pubkey, p.c.pub, 64);
+    if (g.info.key_type == FGV_KEY_P384) memcpy(g.info.pubkey_p384, p.c.pub384, 96);  // (round 6)
     regs.push_back(g);
   }
   // every new P-256 key in one registration: comb tables for the roles that sign often (peers,
@@ -617,7 +618,13 @@ int fgv_msp_resolve_locked(fgv_ctx *c, size_t n, const uint8_t *const *ser, cons
   }
   size_t kq = 0, nreg = 0;
   for (const Reg &g : regs) {
-    const int32_t slot = g.info.key_type == FGV_KEY_P256 ? (int32_t)kslots[kq++] : -1;
+    int32_t slot = g.info.key_type == FGV_KEY_P256 ? (int32_t)kslots[kq++] : -1;
+    if (g.info.key_type == FGV_KEY_P384) {  // a P-384 leaf: its comb in the P-384 key table (p384.hip)
+      uint32_t k;
+      const int rc = fgv_p384_key_locked(c, g.info.pubkey_p384, &k);
+      if (rc) return rc;
+      slot = (int32_t)(KEY_P384_FLAG | k);
+    }
     if (fgv_block_add_identity(c->blk, ser[g.i], lens[g.i], slot, &g.info) == FGV_OK) {
       nreg++;
       std::vector<const char *> op;

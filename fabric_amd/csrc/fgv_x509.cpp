@@ -8,6 +8,7 @@
 
 #include <algorithm>
 
+#include "p384_field.h"
 #include "pbwire.h"
 
 namespace fgvx {
@@ -59,6 +60,7 @@ bool eq(const uint8_t *b, const T &t, const char *hex_bytes, size_t n) {
 #define OIDV(name, ...) const char name[] = {__VA_ARGS__}
 OIDV(OID_EC_KEY, '\x2a', '\x86', '\x48', '\xce', '\x3d', '\x02', '\x01');
 OIDV(OID_P256, '\x2a', '\x86', '\x48', '\xce', '\x3d', '\x03', '\x01', '\x07');
+OIDV(OID_P384, '\x2b', '\x81', '\x04', '\x00', '\x22');  // secp384r1
 OIDV(OID_ED25519, '\x2b', '\x65', '\x70');
 OIDV(OID_RSA, '\x2a', '\x86', '\x48', '\x86', '\xf7', '\x0d', '\x01', '\x01', '\x01');
 OIDV(OID_OU, '\x55', '\x04', '\x0b');
@@ -296,7 +298,16 @@ void parse(Cert &c) {
       if (!p256_on_curve(bits + 2, bits + 34)) perr();  // elliptic.Unmarshal fails
       memcpy(c.pub, bits + 2, 64);
       c.key = XK_P256;
-    } else {  // (P-384 and other curves: not restated; no GPU verify either)
+    } else if (khas && kpar.tag == 0x06 && eq(b, kpar, OID_P384, sizeof OID_P384)) {
+      // P-384 leaves (round 6): elliptic.Unmarshal of the uncompressed point, verified per item
+      // on the GPU (p384.hip) like the registered P-384 identities
+      const uint8_t *bits = b + spk.cs;
+      const size_t bl = spk.ce - spk.cs;
+      if (bl != 98 || bits[0] != 0 || bits[1] != 4) unsup();
+      if (!p384_on_curve(bits + 2, bits + 50)) perr();
+      memcpy(c.pub384, bits + 2, 96);
+      c.key = XK_P384;
+    } else {  // (other curves: not restated; no GPU verify either)
       unsup();
     }
   } else if (eq(b, koid, OID_ED25519, sizeof OID_ED25519)) {
@@ -811,6 +822,16 @@ int sanitized_raw(const Cert &c, std::vector<uint8_t> &out) {
   return X_OK;
 }
 
+bool p384_on_curve(const uint8_t xb[48], const uint8_t yb[48]) {  // both < p, y^2 = x^3 - 3x + b
+  uint32_t x[p384::NL], y[p384::NL];
+  for (int k = 0; k < p384::NL; k++) {
+    const uint8_t *q = xb + 4 * (p384::NL - 1 - k), *r = yb + 4 * (p384::NL - 1 - k);
+    x[k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+    y[k] = ((uint32_t)r[0] << 24) | ((uint32_t)r[1] << 16) | ((uint32_t)r[2] << 8) | (uint32_t)r[3];
+  }
+  return p384::on_curve(x, y);
+}
+
 bool p256_on_curve(const uint8_t xb[32], const uint8_t yb[32]) {
   const U256 x = from_be(xb), y = from_be(yb);
   if (cmp(x, P) >= 0 || cmp(y, P) >= 0) return false;
@@ -858,7 +879,7 @@ extern "C" int fgv_x509_probe(const uint8_t *pem, size_t n, char *out, size_t ca
           std::to_string(c.bc_valid) + ",\"path_len\":" + std::to_string(c.path_len) + ",\"has_ski\":" + std::to_string(c.has_ski) + ",\"key_usage\":" +
           std::to_string(c.key_usage) + ",\"unhandled_critical\":" + std::to_string(c.unhandled_critical) +
           ",\"not_before\":" + std::to_string(c.not_before) + ",\"not_after\":" + std::to_string(c.not_after) +
-          ",\"pub\":\"" + (c.key == XK_P256 ? hex(c.pub, 64) : std::string()) + "\"";
+          ",\"pub\":\"" + (c.key == XK_P256 ? hex(c.pub, 64) : c.key == XK_P384 ? hex(c.pub384, 96) : std::string()) + "\"";
       fgvsha::sha256(c.tbs(), c.tbs_len, h);
       j += ",\"tbs\":\"" + hex(h, 32) + "\"";
       fgvsha::sha256(c.der.data() + c.issuer_off, c.issuer_len, h);

@@ -27,6 +27,7 @@ struct Cert {
   std::vector<std::string> ous;             // subject OrganizationalUnit values, in order
   int key = XK_OTHER;                       // subject public key class
   uint8_t pub[64] = {};                     // P-256 X || Y
+  uint8_t pub384[96] = {};                  // P-384 X || Y (XK_P384, round 6)
   bool is_ca = false, bc_valid = false, has_ski = false, unhandled_critical = false;
   int64_t path_len = -1;                    // basicConstraints MaxPathLen (-1: none)
   uint32_t key_usage = 0;                   // Go KeyUsage bits
@@ -79,5 +80,6 @@ struct Crl {
 int parse_crl(const uint8_t *p, size_t n, Crl &out);
 // P-256 affine point on the curve (x, y < p and y^2 = x^3 - 3x + b)
 bool p256_on_curve(const uint8_t x[32], const uint8_t y[32]);
+bool p384_on_curve(const uint8_t x[48], const uint8_t y[48]);
 
 }  // namespace fgvx

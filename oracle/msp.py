@@ -213,7 +213,8 @@ class MSP:
             if valid and self.node_ous and self._has(role, c):
                 roles |= 1 << role
         key = {"p256": KEY_P256, "p384": KEY_P384}.get(c["key"], KEY_OTHER)
-        return Ident(self.name, c["pub"] if key == KEY_P256 else None, valid, digest, key=key, roles=roles, ous=ous)
+        return Ident(self.name, c["pub"] if key in (KEY_P256, KEY_P384) else None, valid, digest, key=key, roles=roles,
+                     ous=ous)
 
     def _valid(self, c, chain):
         """validateIdentity of a leaf with its validation chain -> (valid, its OUs with certifier)"""

@@ -35,6 +35,8 @@ EXT_GO_PARSED = {bytes.fromhex(h) for h in ("551d1e", "551d1f", "551d20", "2b060
 P256_N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
 P256_P = 0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF
 P256_B = 0x5AC635D8AA3A93E7B3EBBD55769886BC651D06B0CC53B0F63BCE3C3E27D2604B
+P384_P = 2 ** 384 - 2 ** 128 - 2 ** 96 + 2 ** 32 - 1
+P384_B = 0xB3312FA7E23EE7E4988E056BE3F82D19181D9C6EFE8141120314088F5013875AC656398D8A2ED19D2A85C8EDD3EC2AEF
 
 
 def tlv(b, i, end=None):
@@ -338,7 +340,16 @@ def parse_certificate(der):
             if x >= P256_P or y >= P256_P or (y * y - (x * x * x - 3 * x + P256_B)) % P256_P:
                 raise ParseError("point not on curve")
             key, pub = "p256", pt[1:]
-        else:  # (P-384 and other curves: not restated; the engine cannot verify them either)
+        elif kpar is not None and kpar[0] == 0x06 and der[kpar[1]:kpar[2]] == OID_P384:
+            # P-384 leaves (round 6): crypto/elliptic Unmarshal of the uncompressed point
+            pt = bits[1:] if bits[:1] == b"\x00" else b""
+            if len(pt) != 97 or pt[0] != 4:
+                raise Unsupported("P-384 point encoding")
+            x, y = int.from_bytes(pt[1:49], "big"), int.from_bytes(pt[49:], "big")
+            if x >= P384_P or y >= P384_P or (y * y - (x * x * x - 3 * x + P384_B)) % P384_P:
+                raise ParseError("point not on curve")
+            key, pub = "p384", pt[1:]
+        else:  # (other curves: not restated; the engine cannot verify them either)
             raise Unsupported("EC curve")
     elif koid == OID_ED25519:
         key = "undeserializable"  # (a parse or a KeyImport error: undeserializable either way)

@@ -13,7 +13,7 @@ under another issuer).  Shapes Go's pem / x509 parsers may accept
 and the restatement does not model (fork_hazard_variants) must come out Unsupported, never a code."""
 import base64
 
-from fabric_amd.synth import EdKey, Key, make_cert_ed25519
+from fabric_amd.synth import EdKey, Key, Key384, make_cert_ed25519
 from fabric_amd.synth import x509gen as G
 from fabric_amd.synth.blocks import serialized_identity
 from fabric_amd.synth.chanconfig import fabric_msp_config, make_config
@@ -127,6 +127,19 @@ def synthetic():
     add("not_pem", b"definitely not a certificate", FAILED)
     add("key_usage_critical_ok", leaf(21, ["client"], extensions=[G.key_usage((0,))]), OK, True,
         _roles(MEMBER, CLIENT))
+    # P-384 leaves under a P-256 CA (round 6): resolved on a cache miss, verified on the GPU
+    k384 = [Key384(77, 200 + i) for i in range(3)]
+
+    def spki384(x, y):
+        return G.seq(G.seq(G.oid(G.OID_EC), G.oid("2b81040022")), G.tlv(0x03, b"\x00\x04" + x + y))
+
+    def leaf384(i, ous, x=None, y=None):
+        kk = k384[i]
+        return G.cert(k[0], ca1, G.name("p384leaf%d" % i, ous=ous), n1, serial=2000 + i,
+                      spki=spki384(x or kk.qx, y or kk.qy))
+    add("p384_peer", leaf384(0, ["peer"]), OK, True, _roles(MEMBER, PEER))
+    add("p384_client", leaf384(1, ["client"]), OK, True, _roles(MEMBER, CLIENT))
+    add("p384_off_curve", leaf384(2, ["peer"], y=bytes(47) + b"\x05"), FAILED)
     # re-framings of a valid peer certificate: Go's parsers may accept each (extra outer element,
     # PEM framing) -> Unsupported; a canonical CRLF / 64-column framing -> the same identity
     for j in range(9):

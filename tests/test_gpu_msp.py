@@ -45,7 +45,7 @@ def _check(eng, ser, st, exp_st, ident, label):
     elif exp_st == MC.OK:
         assert rec["key"] == _lib.KEY_TYPES[ident.key] and rec["valid"] == ident.valid and rec["roles"] == ident.roles, label
         assert rec["id_digest"] == ident.id_digest, label
-        if ident.key == v20.KEY_P256:
+        if ident.key in (v20.KEY_P256, v20.KEY_P384):
             assert rec["pub"] == ident.pub, label
 
 

@@ -182,7 +182,7 @@ def _oracle_view(pem):
     except Unsupported:
         return {"stage": "parse", "status": 2}
     h = lambda b: hashlib.sha256(b).hexdigest()
-    v = {"stage": "ok", "status": 0, "key": {"p256": 1, "other": 3, "undeserializable": 4}[c["key"]], "version": c["version"],
+    v = {"stage": "ok", "status": 0, "key": {"p256": 1, "p384": 2, "other": 3, "undeserializable": 4}[c["key"]], "version": c["version"],
          "is_ca": int(c["is_ca"]), "bc_valid": int(c["bc_valid"]), "path_len": c["path_len"], "has_ski": int(c["ski"] is not None),
          "key_usage": c["key_usage"], "unhandled_critical": int(c["unhandled_critical"]),
          "not_before": c["not_before"], "not_after": c["not_after"],
