@@ -193,7 +193,7 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
   if (!c->h_kq.ensure((size_t)nk * 64) || !c->h_kid.ensure((size_t)nk * 4) || !c->kt_q.ensure((size_t)nk * 64) ||
       !c->kt_id.ensure((size_t)nk * 4))
     return FGV_ENOMEM;
-  // the variable-base tables (15 KB per id) grow by doubling; kernels in flight read the old rows
+  // the variable-base tables (60 KB per id) grow by doubling; kernels in flight read the old rows
   if (c->n_ids + nk > c->vbt_keys) {
     const uint32_t want = std::min<uint32_t>(c->key_ids, std::max<uint32_t>({c->n_ids + nk, 2 * c->vbt_keys, 4096u}));
     uint32_t grow = want;
@@ -226,7 +226,7 @@ static int ids_new(fgv_ctx *c, const std::vector<std::array<uint8_t, 64>> &keys,
   }
   HIP_TRY(hipMemcpyAsync(c->kt_q.p, kq, (size_t)nk * 64, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->kt_id.p, ki, (size_t)nk * 4, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_keyprep, dim3((nk * VB_SLICES + 63) / 64), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
+  hipLaunchKernelGGL(k_keyprep, dim3((nk * VB_WINS + 63) / 64), dim3(64), 0, c->stream, c->kt_q.as<uint32_t>(),
                      c->kt_id.as<uint32_t>(), nk, c->vbt.as<uint32_t>(), c->key_ok.as<uint8_t>());
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));  // (the staging is reused by comb_build)

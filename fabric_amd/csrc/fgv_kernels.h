@@ -55,17 +55,18 @@ struct jpoint_raw {  // key-table build scratch: Jacobian point + prefix product
 __global__ void k_keybase(const uint32_t *qxy, uint32_t nkeys, jpoint_raw *bases);
 __global__ void k_keytab(const uint32_t *qxy, const uint32_t *slots, apoint_raw *tables, apoint_raw *tables28,
                          jpoint_raw *scratch, uint8_t *key_ok, uint32_t nkeys, const jpoint_raw *bases);
-// Key tiers.  Every key has an id; kmap[id] is its comb slot (the 5.2 MB table
-// above) or KEY_NONE: the variable-base kernels verify it from a 15 KB per-key table
-// (vbt[id][s][d-1] = d * 2^(32 s) Q, s < 8, d = 1..15, affine Montgomery-256).  k_keyprep checks
+// Key tiers.  Every key has an id; kmap[id] is its comb slot (the 64 MiB table
+// above) or KEY_NONE: the variable-base kernels verify it from a 60 KB per-key table
+// (vbt[id][w][d-1] = d * 2^(4 w) Q, w < 64, d = 1..15, affine Montgomery-280: every 4-bit window
+// of u2 has its own base, so u2 * Q is additions only -- no doublings).  k_keyprep checks
 // new keys (on the curve) and writes vbt / key_ok; k_kmap_set points ids at their freshly built
 // comb tables (after k_keytab).
 #define KEY_NONE 0xFFFFFFFFu
 #define VB_THREADS 256      // k_vb_mul workgroup (grid 2 x n_cu)
 #define VB_LANES 8          // k_vb_mul lanes per item (32-bit slices of u2)
-#define VB_SLICES 16        // per-key table slices: Q_s = 2^(16 s) Q (lane s of 16 / lane s/2 of 8)
-#define VB_TAB 15           // per slice: 1 .. 15 times the slice base (4-bit fixed windows)
-#define VBT_WORDS (VB_SLICES * VB_TAB * 16)  // per key id: 240 affine points, 15,360 B
+#define VB_WINS 64          // per-key table windows: W_w = 2^(4 w) Q, one per 4-bit window of u2 (round 6)
+#define VB_TAB 15           // per window: 1 .. 15 times its base
+#define VBT_WORDS (VB_WINS * VB_TAB * 16)  // per key id: 960 affine points, 61,440 B
 #define VB_ACC_WORDS 24     // k_vb_mul -> k_vb_fin partial result: x, y, z (Montgomery-256)
 // counters in the context's redo words: [0] k_point28 hand-overs, [1] k_point28 chunks, [2] k_point
 // chunks, [3] items k_inv listed for the variable-base kernels, [4] taken by k_vb_mul, [5] taken

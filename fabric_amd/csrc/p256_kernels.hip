@@ -819,15 +819,16 @@ __global__ __launch_bounds__(POINT_THREADS, 2) void k_point28(
 // ---------------------------------------------------------------- keys without a comb
 // k_keyprep: new key ids -> on-curve bit (k_inv reports 5 for a key off the curve, before the
 // range checks, as ecdsa.Verify does) and the variable-base kernel's per-key table
-// vbt[id][s][d-1] = d * Q_s, Q_s = 2^(16 s) * Q, s < VB_SLICES, d = 1..VB_TAB (affine, Montgomery-280
-// form as the comb tables, 15 KB per key; the 8-lane kernels read the even slices).  One thread per
-// (key, slice): 16 s doublings to Q_s, 14 complete additions, one inversion for the slice's 15 Z's
-// (prefix products).  qxy: [nkeys][16] plain little-endian limbs (x then y).
+// vbt[id][w][d-1] = d * W_w, W_w = 2^(4 w) * Q, w < VB_WINS, d = 1..VB_TAB (affine, Montgomery-280
+// form as the comb tables, 60 KB per key: one base per 4-bit window of the scalar, so the verify's
+// u2 * Q is a sum of table entries).  One thread per (key, window): 4 w doublings to W_w, 14
+// complete additions, one inversion for the window's 15 Z's (prefix products).  qxy: [nkeys][16]
+// plain little-endian limbs (x then y).
 __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy, const uint32_t *__restrict__ ids,
                                                 uint32_t nkeys, uint32_t *__restrict__ vbt,
                                                 uint8_t *__restrict__ key_ok) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t k = t / VB_SLICES, sl = t % VB_SLICES;
+  const uint32_t k = t / VB_WINS, sl = t % VB_WINS;
   if (k >= nkeys) return;
   fe x, y, xm, ym;
 #pragma unroll
@@ -845,16 +846,16 @@ __global__ __launch_bounds__(64) void k_keyprep(const uint32_t *__restrict__ qxy
     for (int d = 0; d < VB_TAB; d++) store_fe(o + 16 * d, z), store_fe(o + 16 * d + 8, z);
     return;
   }
-  jpoint q;  // Q_s (never infinity: 2^(16 s) < n)
+  jpoint q;  // W_w (never infinity: 2^(4 w) < n)
   q.x = xm;
   q.y = ym;
   fe_set_one(q.z);
 #pragma unroll 1
-  for (uint32_t d = 0; d < 16 * sl; d++) {
+  for (uint32_t d = 0; d < 4 * sl; d++) {
     jpoint t2 = q;
     pt_dbl(q, t2);
   }
-  jpoint T[VB_TAB];  // d * Q_s (d < n: never infinity)
+  jpoint T[VB_TAB];  // d * W_w (d * 2^(4 w) < n: never infinity)
   fe pref[VB_TAB];
   T[0] = q;
   pref[0] = q.z;
@@ -913,13 +914,12 @@ FGV_DEV void load_jp(jpoint &p, const uint32_t *s) {
 
 // k_vb_mul: acc[j] = u2 * Q for list entry j (item i = list[j], key id key_slot[i]), u2 = r * s^-1
 // (plain; k_inv's w is s^-1 in Montgomery form) -- needs no digest, so it runs beside the hashes.
-// VB_LANES lanes per item: lane s takes the 32 bits u2[s] of the scalar against the key's slice
-// table d * 2^(32 s) Q (k_keyprep's slice 2s, affine), so u2 * Q = sum_s u2[s] * 2^(32 s) Q:
-//   8 windows of 4 bits, left to right: 28 doublings and <= 8 mixed additions (each next entry
-//   loaded during the doublings);
+// VB_LANES lanes per item: lane s takes the 32 bits u2[s] of the scalar -- windows 8 s .. 8 s + 7
+// -- against the key's window tables d * 2^(4 w) Q (k_keyprep, affine), so u2 * Q = sum_w
+// digit_w * 2^(4 w) Q:
+//   <= 8 mixed additions, no doublings (each next entry loaded during the addition);
 //   a 3-level butterfly of complete additions across the 8 lanes (cross-lane shuffles).
-// Complete formulas throughout (pt_madd / pt_dbl / pt_add_inl): exact for every input.  Per lane
-// ~330 field multiplications.  uses[id] counts the key's variable-base verifies;
+// Complete formulas throughout (pt_madd / pt_add_inl): exact for every input.  uses[id] counts the key's variable-base verifies;
 // the one that reaches `promote` queues the id (promo[0] count, ids from promo[2]) for a comb build
 // by the host; promo[1] = the batch's variable-base items.
 // remap (the exact hand-over of k_vb_mul28): ctr[RD_VB_CNT] counts the remap entries, each the
@@ -954,37 +954,24 @@ FGV_DEV void vb_mul_body(uint32_t n, const uint32_t *__restrict__ key_slot, cons
     uint32_t dg = u2[0];  // this lane's 32 bits: u2[sl] (a select chain: no private array)
 #pragma unroll
     for (int k = 1; k < 8; k++) dg = sl == (uint32_t)k ? u2[k] : dg;
-    const uint32_t *qt = vbt + (size_t)id * VBT_WORDS + (2 * sl) * (VB_TAB * 16);  // Q_{2 sl} = 2^(32 sl) Q
+    // window w = 8 sl + k of this lane: table rows (8 sl + k), digit (dg >> 4 k) & 15
+    const uint32_t *qt = vbt + (size_t)id * VBT_WORDS + (8 * sl) * (VB_TAB * 16);
     jpoint a;
     fe_set_zero(a.x);
     fe_set_zero(a.y);
     fe_set_zero(a.z);
-    uint32_t d = dg >> 28;
-    apoint e;
-    if (d) load_fe(e.x, qt + 16 * (d - 1)), load_fe(e.y, qt + 16 * (d - 1) + 8);
 #pragma unroll 1
-    for (int win = 7; win >= 0; win--) {
-      dg <<= 4;
-      const uint32_t dn = dg >> 28;  // the next window's digit (0 after the last)
-      apoint en;
-      if (win > 0 && dn) load_fe(en.x, qt + 16 * (dn - 1)), load_fe(en.y, qt + 16 * (dn - 1) + 8);
-      if (d) {
-        fe_mul(e.x, e.x, c232);
-        fe_mul(e.y, e.y, c232);
-      }
-      if (win < 7) {
-#pragma unroll 1
-        for (int k = 0; k < 4; k++) {
-          jpoint t2 = a;
-          pt_dbl(a, t2);
-        }
-      }
-      if (d) {
-        jpoint t2 = a;
-        pt_madd(a, t2, e);  // (a = infinity: e itself)
-      }
-      d = dn;
-      e = en;
+    for (int k = 0; k < 8; k++) {
+      const uint32_t d = (dg >> (4 * k)) & 15u;
+      if (!d) continue;
+      const uint32_t *row = qt + k * (VB_TAB * 16) + 16 * (d - 1);
+      apoint e;
+      load_fe(e.x, row);
+      load_fe(e.y, row + 8);
+      fe_mul(e.x, e.x, c232);
+      fe_mul(e.y, e.y, c232);
+      jpoint t2 = a;
+      pt_madd(a, t2, e);  // (a = infinity: e itself)
     }
     // butterfly: at level m lane s adds lane s ^ m's partial sum; lane 0 of the group ends with all
 #pragma unroll 1
@@ -1026,55 +1013,17 @@ __global__ __launch_bounds__(VB_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
 
 // ---------------------------------------------------------------- k_vb_mul28 (fast path)
 // The variable-base product u2 * Q in radix-2^28 Montgomery-280 arithmetic (p256_fe28.h), the
-// structure of vb_mul_body: LANES (8 or 16) lanes per item, lane s sums its 32 (16) bits of u2
-// times 2^(32 s) Q (2^(16 s) Q) over 8 (4) windows of 4 bits -- 28 (12) doublings, <= 8 (4) mixed
-// additions from the key's Montgomery-280 slice table -- then a 3- (4-) level butterfly.  16 lanes
-// halve the serial chain of a lane for the same doublings in total (small batches: latency).  Incomplete formulas, as k_point28: an exceptional addition (a partial sum
+// structure of vb_mul_body: LANES (8 or 16) lanes per item, lane s sums its 8 (4) windows of 4
+// bits of u2 against the key's window tables d * 2^(4 w) Q -- <= 8 (4) mixed additions and no
+// doublings (round 6: the 28 (12) doublings per lane of the 15 KB slice tables were ~70 % of the
+// kernel's multiplications) -- then a 3- (4-) level butterfly.  16 lanes halve the serial chain of
+// a lane (small batches: latency).  Incomplete formulas, as k_point28: an exceptional addition (a partial sum
 // equal to +-the added point) leaves Z = 0, which stays 0; such an item goes to the hand-over list
 // (redo[RD_VB2_CNT], its list index in `hand`) and the exact k_vb_mul finishes it.  The result is
 // converted to the Montgomery-256 Jacobian form k_vb_fin reads.
-// 8 R mod p and 2^256 mod p (radix 2^28): doubling's 8 beta; Montgomery-280 -> -256
-__constant__ static const uint32_t C8R28[10] = {0x8000000u, 0x0u, 0x0u, 0x0u, 0xffff800u,
-                                                0xfffffffu, 0xfffffffu, 0xf7fffffu, 0x7ffffffu, 0x0u};
+// 2^256 mod p (radix 2^28): Montgomery-280 -> -256
 __constant__ static const uint32_t C256_28[10] = {0x1u, 0x0u, 0x0u, 0xffff000u, 0xfffffffu,
                                                   0xfffffffu, 0xeffffffu, 0xfffffffu, 0x0u, 0x0u};
-
-// a = 2a, dbl-2001-b (a = -3): delta = Z^2, gamma = Y^2, beta = X gamma, alpha = 3 (X - delta)(X + delta),
-// X3 = alpha^2 - 8 beta, Y3 = alpha (4 beta - X3) - 8 gamma^2, Z3 = 2 Y Z.  In: X < 10p, Y, Z < 2p,
-// normalized (madd28's running sum); out: X3 < 6p, Y3 < 2p, Z3 < 2p, normalized.  Z = 0 stays 0.
-FGV_DEV void dbl28(jp28 &a) {
-  f28 delta, gamma, beta, t1, t2, al, a3, x3, b8, b4, t, ng, g8, y2, c;
-  f28_sqr(delta, a.z);              // < 2p
-  f28_sqr(gamma, a.y);              // < 2p
-  f28_mul(beta, a.x, gamma);        // < 2p
-  f28_sub(t1, a.x, delta, C4P28);   // X - delta + 4p < 14p, loose
-  f28_add(t2, a.x, delta);          // < 12p, limbs < 2^29
-  f28_mul(al, t1, t2);              // < 2p
-  f28_add(a3, al, al);
-  f28_add(a3, a3, al);              // 3 alpha < 6p, limbs < 3 * 2^28
-  f28_sqr(x3, a3);                  // < 2p
-  f28_load_c(c, C8R28);
-  f28_mul(b8, beta, c);             // 8 beta mod p, < 2p
-  f28_sub(x3, x3, b8, C4P28);       // < 6p, loose
-  f28_norm(x3);
-  f28_add(b4, beta, beta);
-  f28_add(b4, b4, b4);
-  f28_norm(b4);                     // 4 beta < 8p
-  f28_sub(t, b4, x3, C8P28);        // 4 beta - X3 + 8p < 16p, loose (x3 top limb <= 90 < 125)
-  f28 zero;
-#pragma unroll
-  for (int j = 0; j < 10; j++) zero.v[j] = 0u;
-  f28_sub(ng, zero, gamma, C4P28);  // 4p - gamma, loose
-  f28_add(g8, gamma, gamma);
-  f28_add(g8, g8, g8);
-  f28_norm(g8);                     // 4 gamma < 8p
-  f28_add(g8, g8, g8);
-  f28_norm(g8);                     // 8 gamma < 16p, normalized
-  f28_add(y2, a.y, a.y);            // 2Y, limbs < 2^29
-  f28_mul(a.z, y2, a.z);            // Z3 = 2 Y Z < 2p
-  f28_mul2(a.y, a3, t, ng, g8);     // alpha (4 beta - X3) + (4p - gamma) 8 gamma < 2p
-  a.x = x3;
-}
 
 // normalized value < 2p -> canonical (< p), packed into 8 x 32-bit limbs
 FGV_DEV void f28_to32(uint32_t w[8], const f28 &a) {
@@ -1114,7 +1063,7 @@ FGV_DEV void vb_mul28_body(uint32_t n, const uint32_t *__restrict__ key_slot,
   const uint32_t cnt = ctr[RD_VB_CNT];
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&promo[1], cnt);  // (statistics: fgv_key_stats)
   if (cnt == 0) return;
-  // LANES lanes per item, lane sl taking BITS bits of u2 against slice sl * (VB_SLICES / LANES)
+  // LANES lanes per item, lane sl taking BITS bits of u2: windows sl * WINS .. sl * WINS + WINS - 1
   constexpr uint32_t BITS = 256u / LANES, WINS = BITS / 4u;
   const uint32_t lane = __lane_id(), sl = lane % LANES, base = lane - sl;
   constexpr uint32_t PER = 64u / LANES;
@@ -1131,35 +1080,28 @@ FGV_DEV void vb_mul28_body(uint32_t n, const uint32_t *__restrict__ key_slot,
       w[k] = w_in[(size_t)k * n + i];
     }
     sn_mul(u2, r, w);
-    // this lane's BITS bits of u2, top-aligned (a select chain: no private array)
+    // this lane's BITS bits of u2, low-aligned (a select chain: no private array)
     const uint32_t li = sl * BITS / 32u;
     uint32_t dg = u2[0];
 #pragma unroll
     for (int k = 1; k < 8; k++) dg = li == (uint32_t)k ? u2[k] : dg;
-    if (BITS == 16u) dg = (sl & 1u) ? (dg & 0xFFFF0000u) : (dg << 16);
-    const uint4 *qt = reinterpret_cast<const uint4 *>(vbt + (size_t)id * VBT_WORDS +
-                                                      sl * (VB_SLICES / LANES) * (VB_TAB * 16));
+    if (BITS == 16u) dg = (sl & 1u) ? (dg >> 16) : (dg & 0xFFFFu);
+    // window sl * WINS + k: digit (dg >> 4 k) & 15, row block k of this lane's tables
+    const uint4 *qt = reinterpret_cast<const uint4 *>(vbt + (size_t)id * VBT_WORDS + sl * WINS * (VB_TAB * 16));
     jp28 a;
     bool inf = true;
-    // the entry of window win-1 is loaded while window win is worked (one gather in flight)
-    uint32_t d = dg >> 28;
+    // the entry of window k+1 is loaded while window k is added (one gather in flight)
+    uint32_t d = dg & 15u;
     uint4 n0, n1, n2, n3;
     if (d) n0 = qt[4 * (d - 1)], n1 = qt[4 * (d - 1) + 1], n2 = qt[4 * (d - 1) + 2], n3 = qt[4 * (d - 1) + 3];
 #pragma unroll 1
-    for (int win = (int)WINS - 1; win >= 0; win--) {
+    for (uint32_t k = 0; k < WINS; k++) {
       const uint32_t wx[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
       const uint32_t wy[8] = {n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
-      dg <<= 4;
-      const uint32_t dn = dg >> 28;  // the next window's digit (0 after the last)
-      if (win > 0 && dn) {
-        const uint4 *e = qt + 4 * (dn - 1);
+      const uint32_t dn = k + 1 < WINS ? (dg >> (4 * (k + 1))) & 15u : 0u;  // the next window's digit
+      if (dn) {
+        const uint4 *e = qt + (k + 1) * (VB_TAB * 4) + 4 * (dn - 1);
         n0 = e[0], n1 = e[1], n2 = e[2], n3 = e[3];
-      }
-      if (!inf) {
-        dbl28(a);
-        dbl28(a);
-        dbl28(a);
-        dbl28(a);
       }
       if (d) {
         f28 px, py;

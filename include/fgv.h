@@ -51,9 +51,10 @@ typedef struct fgv_config {
                             the process's CPU share: affinity mask, OMP_NUM_THREADS)) */
   uint32_t key_ids;      /* distinct P-256 keys the context holds at once (0 = 1M): registered
                             keys for good, BCCSP-path keys until the id space is flushed.  HBM:
-                            9 B per id up front (key map, use count, on-curve bit) plus 15,360 B
-                            per id in use (the variable-base multiples 1..15 * 2^(16 s) Q), grown
-                            by doubling as ids are taken -- 1M ids in use is ~15.4 GB.  FGV_ENOMEM:
+                            9 B per id up front (key map, use count, on-curve bit) plus 61,440 B
+                            per id in use (the variable-base multiples 1..15 * 2^(4 w) Q of every
+                            4-bit window w), grown by doubling as ids are taken -- 1M ids in use is
+                            ~61.5 GB of the 288 GB.  FGV_ENOMEM:
                             a single call naming more distinct keys than key_ids, or a device
                             that cannot hold the multiples of the ids in use                      */
 } fgv_config;
