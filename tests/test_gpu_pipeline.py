@@ -53,3 +53,37 @@ def test_pipeline_blocks_match_oracles(nblocks, ntx):
         assert eng.statedb_stats()["keys"] >= len(keys)
     finally:
         eng.close()
+
+
+def test_pipeline_32x500_device_update_batches():
+    """the bench's step shape -- 32 x 500-tx blocks through the committer and one
+    MVCC chain call with the update batches built on the device (mvcc_ub.hip) -- every block's
+    bytes equal oracle.commithash's update batch and the chained hashes equal the oracle's."""
+    net = blocks.Network(seed=3, orgs=3, clients=40)
+    st = MvccState(200_000, seed=12)
+    keys, kb, kt = st.items()
+    blks, cexp, fexp, _ = pipeline.make_blocks(net, st, 32, 500, 4001, seed=21)
+    nums = list(range(4001, 4033))
+    eng = _lib.Engine(0)
+    try:
+        txvalidator.setup_channel(eng, net.channel, net.identities(), net.chaincodes)
+        eng.statedb_init(1 << 20, 64 << 20)
+        eng.statedb_load("mycc", keys, kb, kt)
+        eng.mvcc_set_update_bytes(True)
+        cf = eng.validate_blocks(blks)
+        for b in range(32):
+            assert list(cf[b]) == list(cexp[b]), b
+        fl, rc, done = eng.mvcc_validate_blocks(blks, nums, cf, commit=True)
+        assert rc == 0 and done == 32
+        ticket = eng.mvcc_last_ticket()
+        ub = eng.mvcc_update_bytes(ticket, 32)
+        prev, want = b"\x05" * 32, []
+        for b in range(32):
+            assert list(fl[b]) == list(fexp[b]), b
+            want_ub = commithash.update_batch_bytes(*commithash.update_batch(blks[b], list(fl[b]), nums[b]))
+            assert ub[b] == want_ub, b
+            prev = commithash.commit_hash(list(fl[b]), want_ub, prev)
+            want.append(prev)
+        assert _lib.CommitHashesDev(eng, blks, nums).run(fl, b"\x05" * 32, ticket=ticket) == want
+    finally:
+        eng.close()
