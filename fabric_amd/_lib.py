@@ -708,7 +708,8 @@ class Engine:
         info.valid = 1 if valid else 0
         info.roles = ROLES_UNKNOWN if roles is None else int(roles)
         if pub is not None and key == "p384":
-            ctypes.memmove(info.pubkey_p384, bytes(pub)[:96], min(96, len(pub)))
+            if len(pub) == 96:  # (X || Y; anything else leaves the key unknown: outside the engine)
+                ctypes.memmove(info.pubkey_p384, bytes(pub), 96)
         elif pub is not None:
             ctypes.memmove(info.pubkey, bytes(pub)[:64], min(64, len(pub)))
         ctypes.memmove(info.id_digest, bytes(id_digest), 32)
