@@ -114,7 +114,7 @@ def profiled_dominant(workload="block"):
     if not files:
         return None, None, None
     f = max(files, key=lambda p: int(re.search(r"round(\d+)", os.path.basename(p)).group(1)))
-    rows = [r for r in csv.DictReader(open(f)) if not r["Name"].startswith(("k_gtab", "k_keytab", "k_keyprep", "k_kmap_set"))]
+    rows = [r for r in csv.DictReader(open(f)) if not r["Name"].startswith(("k_gtab", "k_keytab", "k_keybase", "k_keyprep", "k_kmap_set", "k_p384_tab", "k_p384_norm"))]
     if not rows:
         return None, None, None
     top = max(rows, key=lambda r: float(r["TotalDurationNs"]))

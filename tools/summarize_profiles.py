@@ -71,7 +71,7 @@ def main(src, rnd):
             rd = csv.DictReader(fi)
             wr = csv.DictWriter(fo, fieldnames=rd.fieldnames)
             wr.writeheader()
-            rows = [r for r in rd if not r["Name"].startswith(("k_gtab", "k_keytab", "k_keyprep", "k_kmap_set"))]
+            rows = [r for r in rd if not r["Name"].startswith(("k_gtab", "k_keytab", "k_keybase", "k_keyprep", "k_kmap_set", "k_p384_tab", "k_p384_norm"))]
             tot = sum(float(r["TotalDurationNs"]) for r in rows) or 1.0
             for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
                 r["Percentage"] = f"{100 * float(r['TotalDurationNs']) / tot:.2f}"
