@@ -1436,26 +1436,33 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   double tl[6] = {mvcc_now_us(), 0, 0, 0, 0, 0};
   // per-block sizes and the offsets of their head / tail regions
   std::vector<size_t> hoff(nb + 1, 0), toff(nb + 1, 0);
-  size_t max_len = 0, max_ntx = 0;
+  size_t max_len = 0;
   for (size_t k = 0; k < nb; k++) {
     const size_t T = ntx[first + k];
     const size_t et_bytes = (T * 8 + 63) & ~(size_t)63, fl_bytes = (T + 63) & ~(size_t)63;
     hoff[k + 1] = hoff[k] + et_bytes + fl_bytes + kCounterBytes;
     toff[k + 1] = toff[k] + ((kCounterBytes + T + 7) & ~(size_t)7) + 64;
     max_len = std::max(max_len, lens[first + k]);
-    max_ntx = std::max(max_ntx, T);
   }
   const size_t rcap = max_len / 2 + 64;
   uint64_t bcap = 1024;
   while (bcap < 2 * rcap) bcap <<= 1;
   if (!M->bhead.ensure(hoff[nb]) || !M->btail.ensure(toff[nb]) || !M->dheads.ensure(hoff[nb])) return FGV_ENOMEM;
+  // each buffer set is sized for the blocks that use it (k % kSets == q), not for the call's
+  // largest block: a call of many blocks holds up to kSets sets
   const int nsets = (int)std::min<size_t>(kSets, nb);
+  std::vector<size_t> qlen(nsets, 0), qntx(nsets, 0);
+  for (size_t k = 0; k < nb; k++) {
+    qlen[k % kSets] = std::max(qlen[k % kSets], lens[first + k]);
+    qntx[k % kSets] = std::max(qntx[k % kSets], ntx[first + k]);
+  }
   for (int q = 0; q < nsets; q++) {
     MvSet &S = M->set[q];
-    if (!S.info.ensure(max_ntx * sizeof(MvTxInfo)) || !S.reads.ensure(rcap * sizeof(MvRec)) ||
-        !S.writes.ensure(rcap * sizeof(MvRec)) || !S.wslot.ensure(rcap * 4) || !S.rslot.ensure(rcap * 4) ||
-        !S.pend.ensure(rcap + 64) || !S.bad.ensure(max_ntx + 64) || !S.st.ensure(max_ntx + 64) ||
-        !S.tail.ensure(kCounterBytes + max_ntx + 64) || !S.xscr.ensure(max_ntx * 2 * MVX_SCR * sizeof(MvRec)))
+    const size_t rq = qlen[q] / 2 + 64, tq = qntx[q];  // (a KVRead / KVWrite takes >= 2 block bytes)
+    if (!S.info.ensure(tq * sizeof(MvTxInfo)) || !S.reads.ensure(rq * sizeof(MvRec)) ||
+        !S.writes.ensure(rq * sizeof(MvRec)) || !S.wslot.ensure(rq * 4) || !S.rslot.ensure(rq * 4) ||
+        !S.pend.ensure(rq + 64) || !S.bad.ensure(tq + 64) || !S.st.ensure(tq + 64) ||
+        !S.tail.ensure(kCounterBytes + tq + 64) || !S.xscr.ensure(tq * 2 * MVX_SCR * sizeof(MvRec)))
       return FGV_ENOMEM;
     if (!S.ev_x) HIP_TRY(hipEventCreateWithFlags(&S.ev_x, hipEventDisableTiming));
     if (!S.ev_free) HIP_TRY(hipEventCreateWithFlags(&S.ev_free, hipEventDisableTiming));
@@ -1464,7 +1471,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   for (size_t k = 0; k < nb; k++) need_copy |= !d_blocks || !d_blocks[first + k];
   if (need_copy)
     for (int q = 0; q < nsets; q++)
-      if (!M->set[q].blk.ensure(max_len + 64)) return FGV_ENOMEM;
+      if (!M->set[q].blk.ensure(qlen[q] + 64)) return FGV_ENOMEM;
   hipStream_t s = c->stream, sx = c->stream2;
   if (bcap > M->btbl_cap) {  // (re)allocated tables start with epoch 0 everywhere
     M->btbl.release();

@@ -609,7 +609,13 @@ int fgv_mvcc_validate_block_next(fgv_ctx *ctx, const uint8_t *block, size_t len,
  * checked and committed.  A block the device cannot finish on its own (range queries, metadata
  * writes, a long conflict chain) and the blocks after it continue through the single-block path.
  * Stops at the first block whose call would fail and returns that error; *n_done (optional) =
- * the blocks whose flags are final (and committed).  d_blocks may be NULL or hold NULLs. */
+ * the blocks whose flags are final (and committed).  d_blocks may be NULL or hold NULLs.
+ * HBM held by the context after such calls (kept for the next ones): up to 16 buffer sets (block k
+ * of a call uses set k % 16), each sized for the largest block that used it -- per block byte
+ * ~55 B of records and slots, plus ~0.8 KB per transaction of extraction scratch and a staging
+ * copy of the block when it is host-resident; the batch pass (runs of blocks <= 4,096 tx) holds
+ * the same for a whole run; the update-batch arenas (fgv_mvcc_set_update_bytes) 2 x 1.25 x the
+ * call's block bytes in HBM and in pinned host memory. */
 int fgv_mvcc_validate_blocks(fgv_ctx *ctx, size_t n, const uint8_t *const *blocks, const size_t *lens,
                              const uint8_t *const *d_blocks, const uint64_t *block_nums, uint8_t *const *flags,
                              const size_t *ntx, int commit, size_t *n_done);
