@@ -1114,6 +1114,20 @@ static uint32_t mvx_tpw0() {
 }
 // FGV_MVCC_SPIN=0: blocking waits (A/B); polled by default -- a block's GPU work is ~0.2 ms, and a
 // blocking synchronize's wake-up is a large share of that
+// FGV_MVX_ONEWALK=1: k_mvx_extract's counting walk also writes every transaction's records to a
+// per-tx scratch in global memory and copies them to the claimed ranges, instead of walking the
+// (LDS-staged) rwset a second time.  Measured on MI355X (C3, r6z / r6za): the same rate either way
+// (92.5-93.9 M against 90.6-92.6 M tx/s) and the scratch costs its own write and read back
+// (k_mvx_extract_t: 9.7 MB written per block against 6.2 MB with two walks): off by default.
+static bool mvx_onewalk() {
+  static const bool on = [] {
+    const char *e = getenv("FGV_MVX_ONEWALK");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+static MvRec *mvx_scr(MvSet &S) { return mvx_onewalk() ? S.xscr.as<MvRec>() : nullptr; }
+
 static bool mvcc_spin() {
   static const bool spin = [] {
     const char *e = getenv("FGV_MVCC_SPIN");
@@ -1320,14 +1334,9 @@ static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, co
   HIP_TRY(hipMemcpyAsync(dh, h, hbytes, hipMemcpyHostToDevice, s));
   HIP_TRY(hipEventRecord(c->ev[0], s));
   const uint32_t touch = mvx_touch();
-  // FGV_MVX_ONEWALK=0: the second rwset walk for every tx (A/B of the scratch copy)
-  static const bool onewalk = [] {
-    const char *e = getenv("FGV_MVX_ONEWALK");
-    return !e || atoi(e) != 0;
-  }();
-  if (onewalk && !M->set[0].xscr.ensure(ntx * 2 * MVX_SCR * sizeof(MvRec))) return FGV_ENOMEM;
-  mvx_extract_launch(mvx_tpw(), s, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c, touch,
-                     onewalk ? M->set[0].xscr.as<MvRec>() : nullptr, M->set[0].bad.as<uint8_t>());
+  if (mvx_onewalk() && !M->set[0].xscr.ensure(ntx * 2 * MVX_SCR * sizeof(MvRec))) return FGV_ENOMEM;
+  mvx_extract_launch(mvx_tpw(), s, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c, touch, mvx_scr(M->set[0]),
+                     M->set[0].bad.as<uint8_t>());
   hipLaunchKernelGGL(k_mvx_prep, grid_stride(rcap), dim3(256), 0, s, dblk, d_r, d_w, d_b, epoch,
                      M->set[0].wslot.as<uint32_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
                      M->set[0].bad.as<uint8_t>(), d_c, nullptr);
@@ -1462,7 +1471,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
     if (!S.info.ensure(tq * sizeof(MvTxInfo)) || !S.reads.ensure(rq * sizeof(MvRec)) ||
         !S.writes.ensure(rq * sizeof(MvRec)) || !S.wslot.ensure(rq * 4) || !S.rslot.ensure(rq * 4) ||
         !S.pend.ensure(rq + 64) || !S.bad.ensure(tq + 64) || !S.st.ensure(tq + 64) ||
-        !S.tail.ensure(kCounterBytes + tq + 64) || !S.xscr.ensure(tq * 2 * MVX_SCR * sizeof(MvRec)))
+        !S.tail.ensure(kCounterBytes + tq + 64) || (mvx_onewalk() && !S.xscr.ensure(tq * 2 * MVX_SCR * sizeof(MvRec))))
       return FGV_ENOMEM;
     if (!S.ev_x) HIP_TRY(hipEventCreateWithFlags(&S.ev_x, hipEventDisableTiming));
     if (!S.ev_free) HIP_TRY(hipEventCreateWithFlags(&S.ev_free, hipEventDisableTiming));
@@ -1599,7 +1608,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
       mvx_extract_launch(k == 0 ? mvx_tpw0() : mvx_tpw(), sxk, (uint32_t)T, db ? db : S.blk.as<uint8_t>(),
                          reinterpret_cast<const uint32_t *>(dh), dh + et_bytes, S.info.as<MvTxInfo>(),
                          S.reads.as<MvRec>(), S.writes.as<MvRec>(),
-                         reinterpret_cast<MvCounters *>(dh + et_bytes + fl_bytes), touch, S.xscr.as<MvRec>(),
+                         reinterpret_cast<MvCounters *>(dh + et_bytes + fl_bytes), touch, mvx_scr(S),
                          S.bad.as<uint8_t>());
       HIP_TRY(hipEventRecord(S.ev_x, sxk));
       // main stream: block k's chain
@@ -1646,7 +1655,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
             j.reads = Sq.reads.as<MvRec>();
             j.writes = Sq.writes.as<MvRec>();
             j.c = reinterpret_cast<MvCounters *>(dh + etq + flq);
-            j.scr = Sq.xscr.as<MvRec>();
+            j.scr = mvx_scr(Sq);
             j.bad = Sq.bad.as<uint8_t>();
             j.ntx = (uint32_t)Tq;
             j.wg0 = wgs;
@@ -1843,7 +1852,7 @@ static int mvcc_batch(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
       !S.info.ensure(total * sizeof(MvTxInfo)) || !S.reads.ensure(rcap * sizeof(MvRec)) ||
       !S.writes.ensure(rcap * sizeof(MvRec)) || !S.wslot.ensure(rcap * 4) || !S.rslot.ensure(rcap * 4) ||
       !S.pend.ensure(rcap + 64) || !S.bad.ensure(total + 64) || !S.st.ensure(total + 64) ||
-      !S.xscr.ensure(total * 2 * MVX_SCR * sizeof(MvRec)) || !M->mbrstat.ensure(rcap + 64))
+      (mvx_onewalk() && !S.xscr.ensure(total * 2 * MVX_SCR * sizeof(MvRec))) || !M->mbrstat.ensure(rcap + 64))
     return FGV_ENOMEM;
   hipStream_t s = c->stream;
   if (bcap > M->mbtbl_cap) {  // (re)allocated: epoch 0 everywhere
@@ -1919,7 +1928,7 @@ static int mvcc_batch(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
   MbSlot *d_b = M->mbtbl.as<MbSlot>();
   const uint32_t N = (uint32_t)total, NB = (uint32_t)nb;
   const uint32_t epoch = ++M->mb_epoch;
-  mvx_extract_launch(mvx_tpw(), s, N, base, d_et, d_in, d_info, d_r, d_w, d_c, mvx_touch(), S.xscr.as<MvRec>(),
+  mvx_extract_launch(mvx_tpw(), s, N, base, d_et, d_in, d_info, d_r, d_w, d_c, mvx_touch(), mvx_scr(S),
                      S.bad.as<uint8_t>());
   hipLaunchKernelGGL(k_mvb_prep, grid_stride(2 * rcap), dim3(256), 0, s, base, d_r, d_w, d_b, epoch,
                      S.wslot.as<uint32_t>(), M->tbl.as<StateSlot>(), M->mask, M->arena.as<uint8_t>(),
