@@ -1114,15 +1114,15 @@ static uint32_t mvx_tpw0() {
 }
 // FGV_MVCC_SPIN=0: blocking waits (A/B); polled by default -- a block's GPU work is ~0.2 ms, and a
 // blocking synchronize's wake-up is a large share of that
-// FGV_MVX_ONEWALK=1: k_mvx_extract's counting walk also writes every transaction's records to a
-// per-tx scratch in global memory and copies them to the claimed ranges, instead of walking the
-// (LDS-staged) rwset a second time.  Measured on MI355X (C3, r6z / r6za): the same rate either way
-// (92.5-93.9 M against 90.6-92.6 M tx/s) and the scratch costs its own write and read back
-// (k_mvx_extract_t: 9.7 MB written per block against 6.2 MB with two walks): off by default.
+// FGV_MVX_ONEWALK (default 1): k_mvx_extract's counting walk also writes every transaction's
+// records to a per-tx scratch in global memory and copies them to the claimed ranges, instead of
+// walking the (LDS-staged) rwset a second time.  The scratch costs its own write and read back
+// (k_mvx_extract_t: 9.7 MB written per C3 block against 6.2 MB with two walks, r6za), but two walks
+// measured slower on MI355X (C3, every path, r6zb): 84.4-85.1 M tx/s against 91.2-92.6 M -- on.
 static bool mvx_onewalk() {
   static const bool on = [] {
     const char *e = getenv("FGV_MVX_ONEWALK");
-    return e && atoi(e) != 0;
+    return !e || atoi(e) != 0;
   }();
   return on;
 }
