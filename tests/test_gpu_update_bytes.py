@@ -170,3 +170,48 @@ def test_update_bytes_tickets_two_generations():
         eng.mvcc_set_update_bytes(False)
     finally:
         eng.close()
+
+
+def test_update_bytes_phantom_path_block_falls_back():
+    """a block with range queries goes through the host phantom path (fgv_mvcc.cpp): its update
+    bytes are not produced on the device (NULL), the device-path blocks' are, and the chained
+    hashes equal the host decode and the oracle either way"""
+    from fabric_amd.synth import mvcc as M
+    from tests import rq_cases as RQ
+    from tests.blockfix import block_from_envs
+    st = M.MvccState(2000, seed=7)
+    db = {("mycc", k): (int(b), int(t)) for k, b, t in zip(*st.items())}
+    ost = mvcc.StateDB(db)
+    eng = _lib.Engine(0)
+    try:
+        eng.statedb_init(1 << 13, 8 << 20)
+        keys0 = [k for (ns, k) in db]
+        eng.statedb_load("mycc", keys0, [db[("mycc", k)][0] for k in keys0], [db[("mycc", k)][1] for k in keys0])
+        eng.mvcc_set_update_bytes(True)
+        prev = b""
+        for b in range(4):
+            number = 2001 + b
+            if b % 2 == 0:
+                blk, _, flags = M.make_block(st, 300, number=number, seed=30 + b)
+            else:
+                keys = sorted(k for (ns, k) in db if ns == "mycc")[:40]
+                cur = {k.decode() if isinstance(k, bytes) else k: v for (ns, k), v in ost.v.items() if ns == "mycc"}
+                res = sorted((k, v) for k, v in cur.items() if keys[0] <= k < keys[-1])
+                envs = [RQ.env([("mycc", RQ.B.kv_rwset([], [(keys[3], b"new", False)], []))], 0, number),
+                        RQ.env([("mycc", RQ.B.kv_rwset([], [], [RQ.rqi(keys[0], keys[-1], True, raw=res)]))], 1, number)]
+                blk, flags = block_from_envs(envs, number=number), [0, 0]
+            exp = mvcc.validate_block(ost, blk, list(flags), number, commit=True)
+            got = eng.mvcc_validate(blk, number, flags, commit=True)
+            assert list(got) == list(exp), b
+            t = eng.mvcc_last_ticket()
+            ub = eng.mvcc_update_bytes(t, 1)[0]
+            want = commithash.update_batch_bytes(*commithash.update_batch(blk, list(got), number))
+            if b % 2 == 0:
+                assert ub == want, b  # the device path
+            else:
+                assert ub is None, b  # the phantom path: decoded on the host
+            h = _lib.CommitHashesDev(eng, [blk], [number]).run([got], prev, ticket=t)[0]
+            assert h == _lib.commit_hash(blk, got, number, prev) == commithash.commit_hash(list(got), want, prev)
+            prev = h
+    finally:
+        eng.close()
