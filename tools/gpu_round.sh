@@ -180,6 +180,11 @@ for step in "$@"; do
           || { echo pcie failed; tail -20 $O/pcie_$rep.err; exit 1; }
         python3 -c "import json; d=json.load(open('$O/pcie_$rep.json')); p=d['pcie_inclusive']; print('pcie $rep', d['ms_per_step'], p['ms_per_step'], p['h2d_GBps'], p['parity_vs_labels'])"
       done ;;
+    latapi)
+      # the single-block chain with the HIP API trace: when the host enqueued each kernel
+      timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --hip-trace -d $O/latapi -o run -- python tools/latency_probe.py > $O/latapi.out 2> $O/latapi.err \
+        || { echo latapi failed; tail -20 $O/latapi.err; exit 1; }
+      tail -1 $O/latapi.out ;;
     lattrace)
       timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d $O/lat -o run -- python tools/latency_probe.py > $O/lat.out 2> $O/lat.err \
         || { echo lattrace failed; tail -20 $O/lat.err; exit 1; }
