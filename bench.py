@@ -76,8 +76,11 @@ def pmc_traffic(workload):
         if "hbm_bytes" in t:
             return t["hbm_bytes"], (f"{os.path.basename(files[-1])}: {t['kernel']} fetch {t['fetch_bytes']} B + "
                                     f"write {t['write_bytes']} B")
+        low = (f"; lower bound {t['hbm_bytes_per_block_low']} B with the gathers' FETCH_SIZE unscaled"
+               if "hbm_bytes_per_block_low" in t else "")
         return t["hbm_bytes_per_block"], (f"{os.path.basename(files[-1])}: per block, {len(t['kernels'])} kernels, "
-                                          f"fetch {t['fetch_bytes_per_block']} B + write {t['write_bytes_per_block']} B")
+                                          f"fetch {t['fetch_bytes_per_block']} B + write {t['write_bytes_per_block']} B"
+                                          + low)
     except (KeyError, ValueError, OSError):
         return None, None
 

@@ -1119,6 +1119,7 @@ static uint32_t mvx_tpw0() {
 // walking the (LDS-staged) rwset a second time.  The scratch costs its own write and read back
 // (k_mvx_extract_t: 9.7 MB written per C3 block against 6.2 MB with two walks, r6za), but two walks
 // measured slower on MI355X (C3, every path, r6zb): 84.4-85.1 M tx/s against 91.2-92.6 M -- on.
+// Since r6zk the scratch is in LDS (mvcc.hip FGV_MVX_LDSSCR): one global write per record.
 static bool mvx_onewalk() {
   static const bool on = [] {
     const char *e = getenv("FGV_MVX_ONEWALK");

@@ -18,6 +18,7 @@
 #   pipeline         the end-to-end commit pipeline (committer -> MVCC -> commit hash)
 #   mvcc | sig | c5 | sbe   the other workloads (tools/bench_sbe.py for sbe)
 #   mvccpmc          FETCH_SIZE / WRITE_SIZE passes of the mvcc workload
+#   fetchcalib       FETCH_SIZE against known bytes (streaming read, random 64 B gathers)
 #   trace            rocprofv3 --kernel-trace --stats of a C2 run
 #   apitrace         kernel + HIP API trace of a C2 run (host enqueue costs)
 #   lattrace         the same of tools/latency_probe.py (single-block calls)
@@ -97,6 +98,11 @@ for step in "$@"; do
         && timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o run -- python bench.py --workload mvcc --steps 10 --warmup 2 > $O/pmc_write.json 2> $O/pmc_write.err \
         || { echo mvccpmc failed; exit 1; }
       echo mvccpmc ok ;;
+    fetchcalib)
+      # FETCH_SIZE against known bytes: a streaming read and random 64 B gathers (tools/fetch_calib.py)
+      timeout -s KILL 120 rocprofv3 --output-format csv --kernel-trace --pmc FETCH_SIZE -d $O/fcal -o run -- python tools/fetch_calib.py > $O/fcal.out 2>&1 \
+        || { echo fetchcalib failed; tail -20 $O/fcal.out; exit 1; }
+      python3 tools/fetch_calib_report.py $O/fcal/run_counter_collection.csv | tee $O/fcal_report.txt ;;
     pipeline)
       timeout -k 10 400 python -u bench.py --workload pipeline --steps 12 --warmup 2 > $O/pipeline.json 2> $O/pipeline.err \
         || { echo pipeline failed; tail -20 $O/pipeline.err; exit 1; }

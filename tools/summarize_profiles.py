@@ -156,11 +156,16 @@ def main(src, rnd):
                 rounds = F.get("k_mvx_round", {}).get("dispatches", 0) / nblk
                 traffic[wl] = dict(kernels=sorted(per_block), fetch_bytes_per_block=round(fb),
                                    write_bytes_per_block=round(wb), hbm_bytes_per_block=round(fb + wb),
+                                   hbm_bytes_per_block_low=round(fb / 2 + wb),
                                    blocks=nblk,
-                                   note=f"sum over one C3 block's MVCC kernels (k_mvx_round x{rounds:.1f}), "
-                                        "FETCH_SIZE x2 per MI355X_MICROARCH.md (small gathers uncalibrated: an "
-                                        "upper bound); the block's envelope bytes read by k_mvx_extract and the "
-                                        "1M-key table probes are included; k_mv_tags = the one-time state load")
+                                   note=f"sum over one C3 block's MVCC kernels (k_mvx_round x{rounds:.1f}); "
+                                        "FETCH_SIZE x2 per MI355X_MICROARCH.md (exact for streaming reads) gives "
+                                        "hbm_bytes_per_block, an upper bound: random row gathers read 128 B per "
+                                        "row at a counter ratio of 1.0 (tools/fetch_calib.py, "
+                                        "profiles/round6_fetch_calibration.md), so the counter unscaled "
+                                        "(hbm_bytes_per_block_low) is the lower bound; the block's envelope bytes "
+                                        "read by k_mvx_extract and the 1M-key table probes are included; "
+                                        "k_mv_tags = the one-time state load")
     if traffic:
         json.dump(dict(round=rnd, source="rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, separate passes "
                                         "(tools/profile_round.sh)", workloads=traffic),
