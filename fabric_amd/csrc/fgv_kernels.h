@@ -219,6 +219,7 @@ void mvx_extract_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint8_
                         const uint8_t *in_flags, MvTxInfo *info, MvRec *reads, MvRec *writes, MvCounters *c,
                         uint32_t touch, MvRec *scr, uint8_t *bad);
 #define MVX_SCR 8    // k_mvx_extract scratch: records of each kind per tx
+bool mvx_lds_scratch();  // the scratch is in LDS (FGV_MVX_LDSSCR=1, default): no global scratch bytes
 
 __global__ void k_mvx_prep(const uint8_t *base, const MvRec *reads, const MvRec *writes, BlkSlot *btbl, uint32_t epoch,
                            uint32_t *wslot, const StateSlot *tbl, uint64_t mask, const uint8_t *arena, uint8_t *bad,

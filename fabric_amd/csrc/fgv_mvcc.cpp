@@ -1128,6 +1128,9 @@ static bool mvx_onewalk() {
   return on;
 }
 static MvRec *mvx_scr(MvSet &S) { return mvx_onewalk() ? S.xscr.as<MvRec>() : nullptr; }
+// bytes of the global per-tx scratch for `ntx` transactions: a token buffer when the scratch is in
+// LDS (mvcc.hip FGV_MVX_LDSSCR=1: the kernel only needs to know that a scratch is wanted)
+static size_t mvx_scr_bytes(size_t ntx) { return mvx_lds_scratch() ? 64 : ntx * 2 * MVX_SCR * sizeof(MvRec); }
 
 static bool mvcc_spin() {
   static const bool spin = [] {
@@ -1335,7 +1338,7 @@ static int mvcc_validate_locked(fgv_ctx *c, const uint8_t *block, size_t len, co
   HIP_TRY(hipMemcpyAsync(dh, h, hbytes, hipMemcpyHostToDevice, s));
   HIP_TRY(hipEventRecord(c->ev[0], s));
   const uint32_t touch = mvx_touch();
-  if (mvx_onewalk() && !M->set[0].xscr.ensure(ntx * 2 * MVX_SCR * sizeof(MvRec))) return FGV_ENOMEM;
+  if (mvx_onewalk() && !M->set[0].xscr.ensure(mvx_scr_bytes(ntx))) return FGV_ENOMEM;
   mvx_extract_launch(mvx_tpw(), s, N, dblk, d_et, d_in, d_info, d_r, d_w, d_c, touch, mvx_scr(M->set[0]),
                      M->set[0].bad.as<uint8_t>());
   hipLaunchKernelGGL(k_mvx_prep, grid_stride(rcap), dim3(256), 0, s, dblk, d_r, d_w, d_b, epoch,
@@ -1472,7 +1475,7 @@ static int mvcc_chain(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
     if (!S.info.ensure(tq * sizeof(MvTxInfo)) || !S.reads.ensure(rq * sizeof(MvRec)) ||
         !S.writes.ensure(rq * sizeof(MvRec)) || !S.wslot.ensure(rq * 4) || !S.rslot.ensure(rq * 4) ||
         !S.pend.ensure(rq + 64) || !S.bad.ensure(tq + 64) || !S.st.ensure(tq + 64) ||
-        !S.tail.ensure(kCounterBytes + tq + 64) || (mvx_onewalk() && !S.xscr.ensure(tq * 2 * MVX_SCR * sizeof(MvRec))))
+        !S.tail.ensure(kCounterBytes + tq + 64) || (mvx_onewalk() && !S.xscr.ensure(mvx_scr_bytes(tq))))
       return FGV_ENOMEM;
     if (!S.ev_x) HIP_TRY(hipEventCreateWithFlags(&S.ev_x, hipEventDisableTiming));
     if (!S.ev_free) HIP_TRY(hipEventCreateWithFlags(&S.ev_free, hipEventDisableTiming));
@@ -1853,7 +1856,7 @@ static int mvcc_batch(fgv_ctx *c, fgv_mvcc_state *M, size_t first, size_t n, con
       !S.info.ensure(total * sizeof(MvTxInfo)) || !S.reads.ensure(rcap * sizeof(MvRec)) ||
       !S.writes.ensure(rcap * sizeof(MvRec)) || !S.wslot.ensure(rcap * 4) || !S.rslot.ensure(rcap * 4) ||
       !S.pend.ensure(rcap + 64) || !S.bad.ensure(total + 64) || !S.st.ensure(total + 64) ||
-      (mvx_onewalk() && !S.xscr.ensure(total * 2 * MVX_SCR * sizeof(MvRec))) || !M->mbrstat.ensure(rcap + 64))
+      (mvx_onewalk() && !S.xscr.ensure(mvx_scr_bytes(total))) || !M->mbrstat.ensure(rcap + 64))
     return FGV_ENOMEM;
   hipStream_t s = c->stream;
   if (bcap > M->mbtbl_cap) {  // (re)allocated: epoch 0 everywhere

@@ -642,6 +642,7 @@ static uint32_t mvx_ldsscr() {
   }();
   return on;
 }
+bool mvx_lds_scratch() { return mvx_ldsscr() == 1u; }
 template <uint32_t TPW, uint32_t XM>
 static void mvx_multi_go(hipStream_t st, const MvxJobs &J, uint32_t wgs) {
   hipLaunchKernelGGL((k_mvx_extract_multi<TPW, XM>), dim3(wgs), dim3(64), 0, st, J);
