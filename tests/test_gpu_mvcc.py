@@ -271,3 +271,43 @@ def test_load_semantics():
     envs = [_tx([("b", None)], []), _tx([("b", (1, 1))], [])]
     assert list(eng.mvcc_validate(_blk(envs), 9, [0, 0], commit=False)) == [0, 11]
     eng.close()
+
+
+def test_extraction_scratch_spill_and_envelope_sizes():
+    """k_mvx_extract's record scratch (LDS by default, 8 records of each kind per transaction) and
+    its staging cap (768 B per transaction with the LDS scratch): transactions with more than 8
+    reads or writes take the second walk, envelopes past the cap are walked from global memory,
+    beside ordinary small ones in the same workgroups -- flags and the committed state over two
+    blocks match the oracle."""
+    import random
+    rng = random.Random(7)
+    keys = ["k%d" % i for i in range(200)]
+    db = OM.StateDB({("ns1", k): (1, i) for i, k in enumerate(keys)})
+    eng = _lib.Engine(0)
+    eng.statedb_init(1 << 12, 4 << 20)
+    eng.statedb_load("ns1", keys, [1] * len(keys), list(range(len(keys))))
+    envs = [
+        _tx([(keys[i], (1, i)) for i in range(12)], [("w%d" % i, b"x" * 5, False) for i in range(10)]),  # spill both
+        _tx([("w3", None)], []),                                      # written by tx 0 -> 11
+        _tx([(keys[20], (1, 20))], [("big1", b"y" * 1000, False)]),   # envelope past 768 B
+        _tx([(keys[21], (1, 21))], [("big2", b"z" * 2000, False)]),   # past 1,536 B
+        _tx([], [("m%d" % i, b"v", i % 3 == 0) for i in range(9)]),   # 9 writes, some deletes
+        _tx([("m4", None)], []),                                      # written by tx 4 -> 11
+        _tx([(keys[i], (1, i)) for i in range(30, 39)], []),          # 9 reads
+        _tx([(keys[40], (7, 7))], [("big3", b"q" * 900, False)]),     # stale read, big envelope -> 11
+    ]
+    for i in range(56):  # small transactions around them
+        k = rng.randrange(50, 200)
+        envs.append(_tx([(keys[k], (1, k))], [(keys[k], b"s", False)] if i % 2 else []))
+    blk = _blk(envs)
+    n = len(envs)
+    want = OM.validate_block(db, blk, [0] * n, 2, commit=True)
+    got = eng.mvcc_validate(blk, 2, [0] * n, commit=True)
+    assert list(got) == want
+    assert want[1] == 11 and want[5] == 11 and want[7] == 11 and want[0] == 0
+    # the next block reads what block 2 committed (versions Height{2, tx})
+    envs2 = [_tx([("w%d" % i, (2, 0)) for i in range(10)], []), _tx([("big2", (2, 3)), ("m1", (2, 4))], []),
+             _tx([("m0", None), ("big3", None)], []), _tx([("big1", (1, 0))], [])]
+    blk2 = _blk(envs2)
+    assert list(eng.mvcc_validate(blk2, 3, [0] * 4)) == OM.validate_block(db, blk2, [0] * 4, 3, commit=True)
+    eng.close()
