@@ -462,8 +462,8 @@ __device__ __forceinline__ void mvx_extract(uint32_t ntx, const uint8_t *__restr
                                             MvRec *__restrict__ writes, MvCounters *__restrict__ c, uint32_t touch,
                                             MvRec *__restrict__ scr, uint8_t *__restrict__ bad, uint32_t wg) {
   // LDS bytes per transaction (larger envelopes walk global memory): 48 KB per workgroup at 64;
-  // with the LDS record scratch (24 KB at 32 per workgroup) half of that, so a workgroup still
-  // takes 48 KB at 32 (three per CU)
+  // halved in modes 1 and 2 -- with the LDS record scratch (mode 1, 24 KB at 32 per workgroup) a
+  // workgroup still takes 48 KB at 32 (three per CU)
   constexpr bool LS = XM == 1;
   constexpr uint32_t CAP = (TPW == 64 ? 768u : 1536u) / (XM ? 2u : 1u);
   __shared__ uint32_t lds[TPW * (CAP / 4)];
