@@ -453,8 +453,8 @@ __device__ __forceinline__ void copy16(uint4 *__restrict__ d, const uint4 *__res
 
 // XM (FGV_MVX_LDSSCR, with a scratch requested): 1 = LS, the counting walk's records go to an LDS
 // scratch (MVX_SCR of each kind per transaction) and the wave copies them to the claimed ranges
-// with coalesced 16-byte stores -- each record is written to global memory once; 0 / 2 = the
-// per-tx scratch in global memory (`scr`) with the full / halved staging cap (A/B)
+// with coalesced 16-byte stores -- each record is written to global memory once; 0 = the per-tx
+// scratch in global memory (`scr`) with the full staging cap (A/B)
 template <uint32_t TPW, uint32_t XM>
 __device__ __forceinline__ void mvx_extract(uint32_t ntx, const uint8_t *__restrict__ base,
                                             const uint32_t *__restrict__ envtab, const uint8_t *__restrict__ in_flags,
@@ -462,10 +462,10 @@ __device__ __forceinline__ void mvx_extract(uint32_t ntx, const uint8_t *__restr
                                             MvRec *__restrict__ writes, MvCounters *__restrict__ c, uint32_t touch,
                                             MvRec *__restrict__ scr, uint8_t *__restrict__ bad, uint32_t wg) {
   // LDS bytes per transaction (larger envelopes walk global memory): 48 KB per workgroup at 64;
-  // halved in modes 1 and 2 -- with the LDS record scratch (mode 1, 24 KB at 32 per workgroup) a
-  // workgroup still takes 48 KB at 32 (three per CU)
+  // halved with the LDS record scratch (24 KB at 32 per workgroup), so that a workgroup still
+  // takes 48 KB at 32 (three per CU)
   constexpr bool LS = XM == 1;
-  constexpr uint32_t CAP = (TPW == 64 ? 768u : 1536u) / (XM ? 2u : 1u);
+  constexpr uint32_t CAP = (TPW == 64 ? 768u : 1536u) / (LS ? 2u : 1u);
   __shared__ uint32_t lds[TPW * (CAP / 4)];
   __shared__ uint32_t pre[TPW + 1], src0[TPW];  // dword prefix of the staged envelopes, source dword
   __shared__ uint4 lscr[LS ? TPW * 2 * MVX_SCR * 3 : 1];  // (LS) per-tx records: MVX_SCR reads, MVX_SCR writes
@@ -630,15 +630,16 @@ __global__ __launch_bounds__(64) void k_mvx_extract_multi(const MvxJobs J) {
 // transactions per workgroup (16 / 32 / 64): host picks (fgv_mvcc.cpp mvx_launch).
 // FGV_MVX_LDSSCR (with a scratch requested, FGV_MVX_ONEWALK): 1 (default) the records' scratch
 // in LDS, each record written to global memory once (mvx_extract); 0 the per-tx scratch in global
-// memory with the full staging cap, 2 the same with the halved cap (A/B).  Measured on MI355X (C3
-// chained, 10 blocks per call, alternating on one box, r6zk): 0 -> 93.2 / 93.4 M tx/s, 1 -> 97.0 /
-// 96.1, 2 -> 97.6 / 97.4 -- the gain is the workgroups' smaller LDS footprint (C3 envelopes are
-// ~430 B), and 1 also drops the scratch's global write and read back
+// memory with the full staging cap, at 32 per workgroup whatever FGV_MVX_TPW says (A/B; each
+// instantiation of the walk costs minutes of compile).  Measured on MI355X (C3 chained, 10 blocks
+// per call, alternating on one box, r6zk): 0 -> 93.2 / 93.4 M tx/s, 1 -> 97.0 / 96.1, and a
+// temporary mode with the global scratch and the halved cap 97.6 / 97.4 -- the gain is the
+// workgroups' smaller LDS footprint (C3 envelopes are ~430 B), and 1 also drops the scratch's
+// global write and read back
 static uint32_t mvx_ldsscr() {
   static const uint32_t on = [] {
     const char *e = getenv("FGV_MVX_LDSSCR");
-    const uint32_t v = e ? (uint32_t)atoi(e) : 1u;
-    return v <= 2u ? v : 1u;
+    return e && atoi(e) == 0 ? 0u : 1u;
   }();
   return on;
 }
@@ -649,9 +650,10 @@ static void mvx_multi_go(hipStream_t st, const MvxJobs &J, uint32_t wgs) {
 }
 void mvx_extract_multi_launch(uint32_t tpw, hipStream_t st, const MvxJobs &J, uint32_t wgs) {
   const uint32_t ls = J.n && J.j[0].scr ? mvx_ldsscr() : 0u;
-  if (tpw == 64) (ls == 1 ? mvx_multi_go<64, 1> : ls == 2 ? mvx_multi_go<64, 2> : mvx_multi_go<64, 0>)(st, J, wgs);
-  else if (tpw == 32) (ls == 1 ? mvx_multi_go<32, 1> : ls == 2 ? mvx_multi_go<32, 2> : mvx_multi_go<32, 0>)(st, J, wgs);
-  else (ls == 1 ? mvx_multi_go<16, 1> : ls == 2 ? mvx_multi_go<16, 2> : mvx_multi_go<16, 0>)(st, J, wgs);
+  if (ls != 1) mvx_multi_go<32, 0>(st, J, wgs);  // (the A/B mode: 32 per workgroup)
+  else if (tpw == 64) mvx_multi_go<64, 1>(st, J, wgs);
+  else if (tpw == 32) mvx_multi_go<32, 1>(st, J, wgs);
+  else mvx_multi_go<16, 1>(st, J, wgs);
 }
 template <uint32_t TPW, uint32_t XM>
 static void mvx_extract_go(hipStream_t st, uint32_t ntx, const uint8_t *base, const uint32_t *envtab,
@@ -664,15 +666,10 @@ void mvx_extract_launch(uint32_t tpw, hipStream_t st, uint32_t ntx, const uint8_
                         const uint8_t *in_flags, MvTxInfo *info, MvRec *reads, MvRec *writes, MvCounters *c,
                         uint32_t touch, MvRec *scr, uint8_t *bad) {
   const uint32_t ls = scr ? mvx_ldsscr() : 0u;
-  if (tpw == 64)
-    (ls == 1 ? mvx_extract_go<64, 1> : ls == 2 ? mvx_extract_go<64, 2> : mvx_extract_go<64, 0>)(st, ntx, base, envtab, in_flags, info, reads, writes,
-                                                                c, touch, scr, bad);
-  else if (tpw == 32)
-    (ls == 1 ? mvx_extract_go<32, 1> : ls == 2 ? mvx_extract_go<32, 2> : mvx_extract_go<32, 0>)(st, ntx, base, envtab, in_flags, info, reads, writes,
-                                                                c, touch, scr, bad);
-  else
-    (ls == 1 ? mvx_extract_go<16, 1> : ls == 2 ? mvx_extract_go<16, 2> : mvx_extract_go<16, 0>)(st, ntx, base, envtab, in_flags, info, reads, writes,
-                                                                c, touch, scr, bad);
+  if (ls != 1) mvx_extract_go<32, 0>(st, ntx, base, envtab, in_flags, info, reads, writes, c, touch, scr, bad);
+  else if (tpw == 64) mvx_extract_go<64, 1>(st, ntx, base, envtab, in_flags, info, reads, writes, c, touch, scr, bad);
+  else if (tpw == 32) mvx_extract_go<32, 1>(st, ntx, base, envtab, in_flags, info, reads, writes, c, touch, scr, bad);
+  else mvx_extract_go<16, 1>(st, ntx, base, envtab, in_flags, info, reads, writes, c, touch, scr, bad);
 }
 
 // ============================================================ lookups
